@@ -1,0 +1,228 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE.json's metric on MI355X:
+"filterbank GB/s reduced (node) + % HBM roofline, 8-bank 0000 band".
+
+Default workload (configs[2], the north-star band): 8 banks of 0000-product
+data, each (2^26 channels x 1 IF x 16 spectra) Float32 = 4 GiB, frequency
+decimated by 1024 and time integrated by 16, stitched into one
+(524288, 1, 1) band product.  The band is one fixed job (strong scaling):
+with N GPUs each rank owns 8/N contiguous banks (one launch reduces them all
+into its stitched slice), RCCL gathers the slices to rank 0 over xGMI and rank
+0 stitches.  At N=1 one GPU holds all 32 GiB and does the whole band in a
+single launch.
+
+A step = one pass of the hot path over the band, inputs resident in HBM.
+Algorithmic bytes per step = 4*nchan*nif*ntime read + 4*(nchan/F)*nif*(ntime/T)
+written, summed over banks.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg3]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (N > 1)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "filterbank GB/s reduced (node) + % HBM roofline, 8-bank 0000 band"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+CONFIGS = {
+    # BASELINE.json configs[0]: 0002 single bank (the reference's CPU case)
+    "cfg1": dict(workload="0002 single bank (65536 ch x 1 IF x 279 spectra), window t=1:272, "
+                 "F=64 T=16", nbank=1, nchan=65536, nif=1, ntime=279, tw=272, F=64, T=16,
+                 nfpc=1024, product=2),
+    # configs[1]: 8 banks of 0002 stitched on one GPU
+    "cfg2": dict(workload="0002 band: 8 banks (65536 ch x 1 IF x 279), window t=1:272, F=64 "
+                 "T=16, stitched to 524288 ch", nbank=8, nchan=65536, nif=1, ntime=279, tw=272,
+                 F=64, T=16, nfpc=1024, product=2),
+    # configs[2]: the north star
+    "cfg3": dict(workload="0000 band: 8 banks x (2^26 ch x 1 IF x 16 spectra) = 32 GiB, F=1024 "
+                 "T=16, stitched to 524288 ch (RCCL gather when N>1)", nbank=8, nchan=1 << 26,
+                 nif=1, ntime=16, tw=16, F=1024, T=16, nfpc=1 << 20, product=0),
+    # gather-stress variant of configs[2]: time integration only
+    "cfg3f1": dict(workload="0000 band, F=1 T=16 (256 MiB/bank output, gather-stress)",
+                   nbank=8, nchan=1 << 26, nif=1, ntime=16, tw=16, F=1, T=16, nfpc=1 << 20,
+                   product=0),
+    # configs[3]: 0001 high-time-resolution banks
+    "cfg4": dict(workload="0001 band: 8 banks (512 ch x 1 IF x 880000 spectra), window "
+                 "t=1:879616, F=8 T=1024", nbank=8, nchan=512, nif=1, ntime=880000, tw=879616,
+                 F=8, T=1024, nfpc=8, product=1),
+}
+
+
+def log(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def traffic_from_profile(cfg_name, n_local_banks):
+    """HBM bytes per launch from the committed PMC profile (profiles/), or None."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    e = d.get(cfg_name)
+    if not e or e.get("banks_per_launch") != n_local_banks:
+        return None
+    return e.get("hbm_bytes_per_launch")
+
+
+def cpu_baseline(cfg, seconds, eng, torch):
+    """The oracle (C restatement, one thread per bank like one Distributed
+    worker per bank) on a bounded sample of the same workload."""
+    import __graft_entry__ as entry
+
+    orc = entry.load_oracle()
+    nb = cfg["nbank"]
+    nch = min(cfg["nchan"], 1 << 22) if cfg["nchan"] >= 1 << 22 else cfg["nchan"]
+    nt = min(cfg["tw"], 16 * 1024) if cfg["T"] <= 16 * 1024 else cfg["tw"]
+    nt -= nt % cfg["T"]
+    banks = []
+    for b in range(nb):
+        t = eng.synth(nch, cfg["nif"], nt, cfg["nfpc"], seed=10 * b + cfg["product"], kind=0)
+        banks.append(eng.fb_to_numpy(t))
+        del t
+    torch.cuda.empty_cache()
+    per_rep = sum(4 * (nch * cfg["nif"] * nt + (nch // cfg["F"]) * cfg["nif"] * (nt // cfg["T"]))
+                  for _ in range(nb))
+    orc.reduce_banks_mt(banks, cfg["F"], cfg["T"])  # warm
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        orc.reduce_banks_mt(banks, cfg["F"], cfg["T"])
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds and reps >= 3:
+            break
+    return {"value": round(per_rep * reps / el / 1e9, 3), "unit": "GB/s", "cores": nb,
+            "kind": "port",
+            "sample": f"{nb} banks x ({nch} ch x {cfg['nif']} IF x {nt} spectra), F={cfg['F']} "
+                      f"T={cfg['T']}, {reps} reps in {el:.1f} s, oracle/bldp_oracle.c "
+                      f"(float64 accumulate), one pthread per bank"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import __graft_entry__ as entry
+
+    pkg = entry.load_package()
+    eng = pkg.engine
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    cfg = CONFIGS[args.config]
+    nb = cfg["nbank"]
+    if nb % world:
+        raise SystemExit(f"{nb} banks do not shard over {world} GPUs")
+    mine = list(pkg.band.banks_for_rank(nb, rank, world)) if nb >= world else [0]
+    win = None
+    if cfg["tw"] != cfg["ntime"]:
+        win = [0, cfg["nchan"], 1, 0, cfg["nif"], 1, 0, cfg["tw"], 1]  # idxs=(:, :, 1:tw)
+
+    log(f"rank {rank}/{world}: generating banks {mine} of {args.config} on device")
+    banks = [eng.synth(cfg["nchan"], cfg["nif"], cfg["ntime"], cfg["nfpc"],
+                       seed=10 * b + cfg["product"], kind=0) for b in mine]
+    torch.cuda.synchronize()
+    nco, ni, nto = cfg["nchan"] // cfg["F"], cfg["nif"], cfg["tw"] // cfg["T"]
+    read_b = 4 * cfg["nchan"] * cfg["nif"] * cfg["tw"]
+    write_b = 4 * nco * ni * nto
+    bytes_step = nb * (read_b + write_b)          # whole band (all ranks)
+    bytes_launch = len(mine) * (read_b + write_b)  # this rank's single reduce launch
+    out = eng.fb_empty(len(mine) * nco, ni, nto)
+    stream = torch.cuda.current_stream()
+
+    def step(ev0=None, ev1=None):
+        if ev0 is not None:
+            ev0.record(stream)
+        eng.band_reduce(banks, cfg["F"], cfg["T"], "sum", win, out=out)
+        if ev1 is not None:
+            ev1.record(stream)
+        if world > 1:
+            return pkg.band.band_reduce_dist(
+                banks, cfg["F"], cfg["T"], "sum", win,
+                reduce_fn=lambda *a: out)  # exchange + stitch of this step's slice
+        return out
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(*evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    if world > 1:
+        t = torch.tensor([el, kern_ms], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el, kern_ms = float(t[0]), float(t[1])
+    ms_step = el * 1e3 / args.steps
+    value = bytes_step / (ms_step * 1e-3) / 1e9
+    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
+    traffic = traffic_from_profile(args.config, len(mine))
+
+    result = None
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            del banks
+            torch.cuda.empty_cache()
+            log("cpu baseline (oracle port) ...")
+            cpu = cpu_baseline(cfg, args.cpu_seconds, eng, torch)
+        result = {
+            "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic: gamma(2, 5e8) x per-coarse-channel bandpass x DC spike, "
+                    "generated on device (bldp_synth_f32); no published reference number",
+            "config": {"workload": cfg["workload"], "name": args.config, "nbank": nb,
+                       "nchan": cfg["nchan"], "nif": cfg["nif"], "ntime": cfg["tw"],
+                       "fqavby": cfg["F"], "tavby": cfg["T"],
+                       "parallelism": f"{len(mine)} bank(s)/GPU x {world} GPU(s)"
+                                      + (", RCCL gather + stitch" if world > 1 else
+                                         ", single-launch band reduce+stitch"),
+                       "bytes_per_step": bytes_step},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic, "kernel": "bldp k_reduce_vec (band launch)",
+                         "kernel_ms": round(kern_ms, 4), "bytes_per_launch": bytes_launch},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return result
+
+
+if __name__ == "__main__":
+    main()

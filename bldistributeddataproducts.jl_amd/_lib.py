@@ -1,0 +1,128 @@
+"""ctypes boundary to libbldp_hip.so (include/bldp.h).
+
+This is the same binding a Julia ``ccall`` shim makes; the
+Python host mirror calls the HIP library through it and through nothing else.
+There is no CPU fallback: if the library is missing the first call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libbldp_hip.so")
+CSRC = os.path.join(PKG_DIR, "csrc")
+
+OPS = {"sum": 0, "mean": 1, "max": 2, "min": 3}
+PATHS = {0: "vector", 1: "narrow", 2: "scalar"}
+
+BLDP_OK, BLDP_EINVAL, BLDP_EDIM, BLDP_EHIP, BLDP_ENOMEM, BLDP_EBOUNDS = 0, -1, -2, -3, -5, -6
+
+
+class BLDPError(RuntimeError):
+    """Any libbldp_hip failure (ErrorException on the Julia side)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+class DimensionMismatch(BLDPError, ValueError):
+    """fqavby/tavby does not divide the selected axis
+    (Julia reshape in fqav, src/gbtworkerfunctions.jl:18-19)."""
+
+
+class BoundsError(BLDPError, IndexError):
+    """Window outside the array (h5["data"][idxs...], :185)."""
+
+
+class ArgumentError(BLDPError, ValueError):
+    """Invalid argument (Julia AssertionError / ArgumentError analogues)."""
+
+
+# every symbol include/bldp.h declares, with its ctypes signature
+P, I64, I, D, SZ, U64 = (ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_double,
+                         ctypes.c_size_t, ctypes.c_uint64)
+SIGNATURES = {
+    "bldp_abi_version": ([], I),
+    "bldp_last_error": ([ctypes.c_char_p, SZ], I),
+    "bldp_device_count": ([P], I),
+    "bldp_reduce_shape": ([I64, I64, I64, P, I64, I64, P], I),
+    "bldp_reduce_plan_f32": ([P, I64, I64, I64, P, I64, I64, I, P, P], I),
+    "bldp_reduce_f32": ([P, I64, I64, I64, P, I64, I64, I, P, P], I),
+    "bldp_reduce_strided_f32": ([P, I64, I64, I64, P, I64, I64, I, P, I64, I64, P], I),
+    "bldp_reduce_host_f32": ([I, P, I64, I64, I64, P, I64, I64, I, P], I),
+    "bldp_band_reduce_f32": ([I, P, I64, I64, I64, P, I64, I64, I, P, P], I),
+    "bldp_stitch_f32": ([I, P, I64, I64, I64, P, P], I),
+    "bldp_despike_f32": ([P, I64, I64, I64, I64, P], I),
+    "bldp_kurtosis_workspace_size": ([I64, I64, I64, P], SZ),
+    "bldp_kurtosis_f32": ([P, I64, I64, I64, P, P, P, P], I),
+    "bldp_fqav_range": ([D, D, I64, I64, P, P, P], I),
+    "bldp_synth_f32": ([P, I64, I64, I64, I64, U64, I, P], I),
+}
+
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    """Compile libbldp_hip.so in-tree for gfx950 (hipcc, see csrc/Makefile)."""
+    if force and os.path.exists(LIB_PATH):
+        os.remove(LIB_PATH)
+    subprocess.run(["make", "-s", "-C", CSRC], check=True)
+    return LIB_PATH
+
+
+def lib():
+    """The loaded library.  torch is imported first so that the process has a
+    single HIP runtime (libamdhip64.so.7) shared by torch and libbldp_hip."""
+    global _lib
+    if _lib is None:
+        import torch  # noqa: F401  (HIP runtime load order, see docstring)
+
+        if not os.path.exists(LIB_PATH):
+            raise BLDPError(BLDP_EINVAL, f"{LIB_PATH} is not built; run __graft_entry__.build()")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (args, res) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        if L.bldp_abi_version() != 1:
+            raise BLDPError(BLDP_EINVAL, "libbldp_hip ABI version mismatch")
+        _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    buf = ctypes.create_string_buffer(1024)
+    lib().bldp_last_error(buf, len(buf))
+    return buf.value.decode(errors="replace")
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc == BLDP_OK:
+        return
+    msg = last_error() or what
+    if rc == BLDP_EDIM:
+        raise DimensionMismatch(rc, msg)
+    if rc == BLDP_EBOUNDS:
+        raise BoundsError(rc, msg)
+    if rc == BLDP_EINVAL:
+        raise ArgumentError(rc, msg)
+    raise BLDPError(rc, msg)
+
+
+def win_arg(win):
+    """9-int64 window -> (keepalive, pointer) or (None, None) for (:,:,:)."""
+    if win is None:
+        return None, None
+    w = (ctypes.c_int64 * 9)(*[int(x) for x in win])
+    return w, ctypes.cast(w, ctypes.c_void_p)
+
+
+def stream_ptr(stream=None) -> int:
+    """hipStream_t of a torch stream (default: torch's current stream)."""
+    import torch
+
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)

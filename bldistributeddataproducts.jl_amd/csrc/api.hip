@@ -1,0 +1,409 @@
+// api.hip — the extern "C" boundary of libbldp_hip (declared in include/bldp.h).
+//
+// Argument validation mirrors the reference's error behaviour:
+//   * fqavby must divide the selected channel count (Julia reshape in
+//     fqav, src/gbtworkerfunctions.jl:18-19 -> DimensionMismatch) => BLDP_EDIM;
+//     the same rule is applied to tavby on the time axis;
+//   * a window outside the array (h5["data"][idxs...] / dmmap[idxs...],
+//     :174,:185 -> BoundsError) => BLDP_EBOUNDS;
+//   * everything else that Julia would reject by type or @assert => BLDP_EINVAL.
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "bldp_impl.h"
+
+using namespace bldp;
+
+namespace {
+
+thread_local std::string g_err;
+
+}  // namespace
+
+int bldp::set_error(int code, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+namespace {
+
+#define fail bldp::set_error
+
+#define HIPCHK(x)                                                                      \
+  do {                                                                                 \
+    hipError_t e_ = (x);                                                               \
+    if (e_ != hipSuccess) return fail(BLDP_EHIP, "%s: %s", #x, hipGetErrorString(e_)); \
+  } while (0)
+
+// Resolved window: element (c, i, t) at base[off + c*cs + i*ld_i + t*ld_t].
+struct Geo {
+  int64_t nc, ni, nt;
+  int64_t off, cs, ld_i, ld_t;
+};
+
+int resolve_window(int64_t nchan, int64_t nif, int64_t ntime, const int64_t *win, Geo *g) {
+  if (nchan < 0 || nif < 0 || ntime < 0)
+    return fail(BLDP_EINVAL, "negative array dimension (%lld, %lld, %lld)", (long long)nchan,
+                (long long)nif, (long long)ntime);
+  const int64_t dims[3] = {nchan, nif, ntime};
+  int64_t start[3], count[3], step[3];
+  for (int ax = 0; ax < 3; ++ax) {
+    if (win) {
+      start[ax] = win[3 * ax];
+      count[ax] = win[3 * ax + 1];
+      step[ax] = win[3 * ax + 2];
+    } else {
+      start[ax] = 0;
+      count[ax] = dims[ax];
+      step[ax] = 1;
+    }
+    if (count[ax] < 0) return fail(BLDP_EINVAL, "negative window count on axis %d", ax + 1);
+    if (count[ax] > 0) {
+      if (step[ax] == 0) return fail(BLDP_EINVAL, "zero window step on axis %d", ax + 1);
+      const int64_t last = start[ax] + (count[ax] - 1) * step[ax];
+      if (start[ax] < 0 || start[ax] >= dims[ax] || last < 0 || last >= dims[ax])
+        return fail(BLDP_EBOUNDS,
+                    "BoundsError: window %lld:%lld:%lld (1-based) outside axis %d of size %lld",
+                    (long long)(start[ax] + 1), (long long)step[ax], (long long)(last + 1),
+                    ax + 1, (long long)dims[ax]);
+    }
+  }
+  g->nc = count[0];
+  g->ni = count[1];
+  g->nt = count[2];
+  const bool empty = g->nc == 0 || g->ni == 0 || g->nt == 0;
+  g->off = empty ? 0 : start[0] + nchan * (start[1] + nif * start[2]);
+  g->cs = step[0];
+  g->ld_i = nchan * step[1];
+  g->ld_t = nchan * nif * step[2];
+  return BLDP_OK;
+}
+
+int resolve_factors(const Geo &g, int64_t fqavby, int64_t tavby, int64_t *F, int64_t *T) {
+  *F = fqavby <= 1 ? 1 : fqavby;  // fqav: n <= 1 returns A (src/gbtworkerfunctions.jl:17)
+  *T = tavby <= 1 ? 1 : tavby;
+  if (g.nc % *F != 0)
+    return fail(BLDP_EDIM, "DimensionMismatch: fqavby=%lld does not divide nchan=%lld",
+                (long long)*F, (long long)g.nc);
+  if (g.nt % *T != 0)
+    return fail(BLDP_EDIM, "DimensionMismatch: tavby=%lld does not divide ntime=%lld",
+                (long long)*T, (long long)g.nt);
+  return BLDP_OK;
+}
+
+int num_cus_current() {
+  static std::mutex mu;
+  static std::map<int, int> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(dev);
+  if (it != cache.end()) return it->second;
+  int n = 256;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    n = 256;
+  cache[dev] = n;
+  return n;
+}
+
+// Library-owned scratch, cached per (device, stream) so that concurrent
+// streams never share a buffer.  Growing synchronizes that stream first.
+struct Scratch {
+  void *ptr = nullptr;
+  size_t bytes = 0;
+};
+std::mutex g_ws_mu;
+std::map<std::pair<int, void *>, Scratch> g_ws;
+
+int scratch(hipStream_t s, size_t bytes, void **out) {
+  int dev = 0;
+  HIPCHK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  Scratch &w = g_ws[{dev, (void *)s}];
+  if (w.bytes < bytes) {
+    if (w.ptr) {
+      HIPCHK(hipStreamSynchronize(s));
+      HIPCHK(hipFree(w.ptr));
+      w.ptr = nullptr;
+      w.bytes = 0;
+    }
+    size_t want = std::max<size_t>(bytes, 1 << 20);
+    if (hipMalloc(&w.ptr, want) != hipSuccess) {
+      w.ptr = nullptr;
+      return fail(BLDP_ENOMEM, "hipMalloc of %zu bytes of scratch failed", want);
+    }
+    w.bytes = want;
+  }
+  *out = w.ptr;
+  return BLDP_OK;
+}
+
+bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
+
+bool vec_ok(const Geo &g) {
+  return g.cs == 1 && g.off % 4 == 0 && (g.ni <= 1 || g.ld_i % 4 == 0) &&
+         (g.nt <= 1 || g.ld_t % 4 == 0);
+}
+
+int valid_op(int op) { return op >= BLDP_OP_SUM && op <= BLDP_OP_MIN; }
+
+// Shared by every reduce entry point.
+int reduce_impl(int nbank, const float *const *in, int64_t nchan, int64_t nif, int64_t ntime,
+                const int64_t *win, int64_t fqavby, int64_t tavby, int op, float *out,
+                int64_t out_bank, int64_t out_ld_i, int64_t out_ld_t, bool stitched,
+                hipStream_t s, int64_t *info) {
+  if (nbank < 1 || nbank > BLDP_MAX_BANKS)
+    return fail(BLDP_EINVAL, "nbank=%d outside 1..%d", nbank, BLDP_MAX_BANKS);
+  if (!valid_op(op)) return fail(BLDP_EINVAL, "unknown op %d (0=sum 1=mean 2=max 3=min)", op);
+  Geo g;
+  int rc = resolve_window(nchan, nif, ntime, win, &g);
+  if (rc) return rc;
+  int64_t F, T;
+  rc = resolve_factors(g, fqavby, tavby, &F, &T);
+  if (rc) return rc;
+  RedArgs a{};
+  a.nco = g.nc / F;
+  a.ni = g.ni;
+  a.nto = g.nt / T;
+  a.F = F;
+  a.T = T;
+  a.nbank = nbank;
+  if (stitched) {
+    a.out_bank = a.nco;
+    a.out_ld_i = nbank * a.nco;
+    a.out_ld_t = nbank * a.nco * a.ni;
+  } else {
+    a.out_bank = out_bank;
+    a.out_ld_i = out_ld_i;
+    a.out_ld_t = out_ld_t;
+  }
+  a.in_off = g.off;
+  a.in_cs = g.cs;
+  a.in_ld_i = g.ld_i;
+  a.in_ld_t = g.ld_t;
+  a.out = out;
+  const bool empty = a.nco == 0 || a.ni == 0 || a.nto == 0;
+  bool aligned = vec_ok(g);
+  if (!in) return fail(BLDP_EINVAL, "null input pointer array");
+  for (int b = 0; b < nbank; ++b) {
+    a.in[b] = in[b];
+    aligned = aligned && aligned16(a.in[b]);
+  }
+  Plan p = plan_reduce(a, aligned, num_cus_current());
+  if (!info) {
+    for (int b = 0; b < nbank; ++b)
+      if (!in[b] && !empty) return fail(BLDP_EINVAL, "null input pointer (bank %d)", b);
+    if (!out && !empty) return fail(BLDP_EINVAL, "null output pointer");
+  }
+  if (info) {
+    info[0] = p.path;
+    info[1] = p.lpg;
+    info[2] = a.ts;
+    info[3] = a.k4;
+    info[4] = a.nchunk;
+    info[5] = p.grid;
+    info[6] = (int64_t)p.ws_bytes;
+    info[7] = a.vec_out;
+    return BLDP_OK;  // plan query only
+  }
+  if (empty) return BLDP_OK;
+  if (p.ws_bytes) {
+    void *ws = nullptr;
+    rc = scratch(s, p.ws_bytes, &ws);
+    if (rc) return rc;
+    a.ws = (float *)ws;
+  }
+  hipError_t e = launch_reduce(a, p, op, s);
+  if (e != hipSuccess) return fail(BLDP_EHIP, "reduce launch: %s", hipGetErrorString(e));
+  return BLDP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bldp_abi_version(void) { return BLDP_ABI_VERSION; }
+
+int bldp_last_error(char *buf, size_t len) {
+  if (!buf || len == 0) return BLDP_EINVAL;
+  std::snprintf(buf, len, "%s", g_err.c_str());
+  return BLDP_OK;
+}
+
+int bldp_device_count(int *n) {
+  if (!n) return fail(BLDP_EINVAL, "null pointer");
+  HIPCHK(hipGetDeviceCount(n));
+  return BLDP_OK;
+}
+
+int bldp_reduce_shape(int64_t nchan, int64_t nif, int64_t ntime, const int64_t *win,
+                      int64_t fqavby, int64_t tavby, int64_t out_shape[3]) {
+  if (!out_shape) return fail(BLDP_EINVAL, "null out_shape");
+  Geo g;
+  int rc = resolve_window(nchan, nif, ntime, win, &g);
+  if (rc) return rc;
+  int64_t F, T;
+  rc = resolve_factors(g, fqavby, tavby, &F, &T);
+  if (rc) return rc;
+  out_shape[0] = g.nc / F;
+  out_shape[1] = g.ni;
+  out_shape[2] = g.nt / T;
+  return BLDP_OK;
+}
+
+int bldp_reduce_plan_f32(const float *in, int64_t nchan, int64_t nif, int64_t ntime,
+                         const int64_t *win, int64_t fqavby, int64_t tavby, int op,
+                         const float *out, int64_t info[8]) {
+  if (!info) return fail(BLDP_EINVAL, "null info");
+  int64_t sh[3];
+  int rc = bldp_reduce_shape(nchan, nif, ntime, win, fqavby, tavby, sh);
+  if (rc) return rc;
+  const float *ins[1] = {in};
+  return reduce_impl(1, ins, nchan, nif, ntime, win, fqavby, tavby, op, (float *)out,
+                     sh[0] * sh[1] * sh[2], sh[0], sh[0] * sh[1], false, nullptr, info);
+}
+
+int bldp_reduce_f32(const float *in, int64_t nchan, int64_t nif, int64_t ntime,
+                    const int64_t *win, int64_t fqavby, int64_t tavby, int op, float *out,
+                    void *stream) {
+  int64_t sh[3];
+  int rc = bldp_reduce_shape(nchan, nif, ntime, win, fqavby, tavby, sh);
+  if (rc) return rc;
+  const float *ins[1] = {in};
+  return reduce_impl(1, ins, nchan, nif, ntime, win, fqavby, tavby, op, out,
+                     sh[0] * sh[1] * sh[2], sh[0], sh[0] * sh[1], false, (hipStream_t)stream,
+                     nullptr);
+}
+
+int bldp_reduce_strided_f32(const float *in, int64_t nchan, int64_t nif, int64_t ntime,
+                            const int64_t *win, int64_t fqavby, int64_t tavby, int op,
+                            float *out, int64_t out_ld_i, int64_t out_ld_t, void *stream) {
+  const float *ins[1] = {in};
+  return reduce_impl(1, ins, nchan, nif, ntime, win, fqavby, tavby, op, out, 0, out_ld_i,
+                     out_ld_t, false, (hipStream_t)stream, nullptr);
+}
+
+int bldp_band_reduce_f32(int nbank, const float *const *in, int64_t nchan, int64_t nif,
+                         int64_t ntime, const int64_t *win, int64_t fqavby, int64_t tavby,
+                         int op, float *out, void *stream) {
+  return reduce_impl(nbank, in, nchan, nif, ntime, win, fqavby, tavby, op, out, 0, 0, 0, true,
+                     (hipStream_t)stream, nullptr);
+}
+
+int bldp_stitch_f32(int nbank, const float *gathered, int64_t nc, int64_t nif, int64_t ntime,
+                    float *out, void *stream) {
+  if (nbank < 1 || nbank > BLDP_MAX_BANKS)
+    return fail(BLDP_EINVAL, "nbank=%d outside 1..%d", nbank, BLDP_MAX_BANKS);
+  if (nc < 0 || nif < 0 || ntime < 0) return fail(BLDP_EINVAL, "negative dimension");
+  const int64_t n = nc * nif * ntime;
+  if (n > 0 && (!gathered || !out)) return fail(BLDP_EINVAL, "null pointer");
+  if (n > 0 && gathered == out) return fail(BLDP_EINVAL, "stitch cannot run in place");
+  hipError_t e = launch_stitch(nbank, gathered, nc, nif * ntime, out, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(BLDP_EHIP, "stitch launch: %s", hipGetErrorString(e));
+  return BLDP_OK;
+}
+
+int bldp_despike_f32(float *data, int64_t nchan, int64_t nif, int64_t ntime, int64_t nfpc,
+                     void *stream) {
+  if (nchan < 0 || nif < 0 || ntime < 0) return fail(BLDP_EINVAL, "negative dimension");
+  // spike = nfpc÷2 + 1 (1-based, src/gbt.jl:102); spike-1 must be a valid index
+  if (nfpc < 2) return fail(BLDP_EBOUNDS, "BoundsError: nfpc=%lld < 2", (long long)nfpc);
+  const int64_t sp = nfpc / 2;  // 0-based spike bin
+  const int64_t nspike = nchan > sp ? (nchan - sp + nfpc - 1) / nfpc : 0;
+  const int64_t nsrc = nchan > sp - 1 ? (nchan - (sp - 1) + nfpc - 1) / nfpc : 0;
+  if (nspike != nsrc)  // d[spike:nfpc:end] .= d[spike-1:nfpc:end] length mismatch
+    return fail(BLDP_EDIM,
+                "DimensionMismatch: %lld spike bins vs %lld source bins (nchan=%lld, nfpc=%lld)",
+                (long long)nspike, (long long)nsrc, (long long)nchan, (long long)nfpc);
+  if (nspike * nif * ntime > 0 && !data) return fail(BLDP_EINVAL, "null pointer");
+  hipError_t e = launch_despike(data, nchan, nif * ntime, nfpc, nspike, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(BLDP_EHIP, "despike launch: %s", hipGetErrorString(e));
+  return BLDP_OK;
+}
+
+static int kurt_setup(const float *in, int64_t nchan, int64_t nif, int64_t ntime,
+                      const int64_t *win, KurtArgs *k) {
+  Geo g;
+  int rc = resolve_window(nchan, nif, ntime, win, &g);
+  if (rc) return rc;
+  *k = KurtArgs{};
+  k->in = in;
+  k->in_off = g.off;
+  k->in_cs = g.cs;
+  k->in_ld_i = g.ld_i;
+  k->in_ld_t = g.ld_t;
+  k->nc = g.nc;
+  k->ni = g.ni;
+  k->nt = g.nt;
+  k->vec = vec_ok(g) && g.nc % 4 == 0 && aligned16(in);
+  plan_kurtosis(*k, num_cus_current());
+  return BLDP_OK;
+}
+
+size_t bldp_kurtosis_workspace_size(int64_t nchan, int64_t nif, int64_t ntime,
+                                    const int64_t *win) {
+  KurtArgs k;
+  if (kurt_setup(nullptr, nchan, nif, ntime, win, &k)) return 0;
+  k.vec = 1;  // the plan does not depend on alignment
+  return kurtosis_ws_bytes(k);
+}
+
+int bldp_kurtosis_f32(const float *in, int64_t nchan, int64_t nif, int64_t ntime,
+                      const int64_t *win, double *out, void *workspace, void *stream) {
+  KurtArgs k;
+  int rc = kurt_setup(in, nchan, nif, ntime, win, &k);
+  if (rc) return rc;
+  if (k.nc * k.ni == 0) return BLDP_OK;
+  if (!out || (!in && k.nt > 0)) return fail(BLDP_EINVAL, "null pointer");
+  k.out = out;
+  hipStream_t s = (hipStream_t)stream;
+  void *ws = workspace;
+  if (!ws) {
+    rc = scratch(s, kurtosis_ws_bytes(k), &ws);
+    if (rc) return rc;
+  }
+  hipError_t e = launch_kurtosis(k, (char *)ws, s);
+  if (e != hipSuccess) return fail(BLDP_EHIP, "kurtosis launch: %s", hipGetErrorString(e));
+  return BLDP_OK;
+}
+
+int bldp_fqav_range(double first, double step, int64_t len, int64_t n, double *out_first,
+                    double *out_step, int64_t *out_len) {
+  if (!out_first || !out_step || !out_len) return fail(BLDP_EINVAL, "null pointer");
+  if (len < 0) return fail(BLDP_EINVAL, "negative range length");
+  if (n <= 1) {  // src/gbtworkerfunctions.jl:28
+    *out_first = first;
+    *out_step = step;
+    *out_len = len;
+    return BLDP_OK;
+  }
+  *out_first = first + (double)(n - 1) * step / 2.0;  // :29
+  *out_step = (double)n * step;                        // :30
+  *out_len = len / n;                                  // :31 (floor)
+  return BLDP_OK;
+}
+
+int bldp_synth_f32(float *out, int64_t nchan, int64_t nif, int64_t ntime, int64_t nfpc,
+                   uint64_t seed, int kind, void *stream) {
+  if (nchan < 0 || nif < 0 || ntime < 0) return fail(BLDP_EINVAL, "negative dimension");
+  if (kind != 0 && kind != 1) return fail(BLDP_EINVAL, "unknown synth kind %d", kind);
+  if (nfpc < 1) return fail(BLDP_EINVAL, "nfpc must be >= 1");
+  if (nchan * nif * ntime > 0 && !out) return fail(BLDP_EINVAL, "null pointer");
+  hipError_t e = launch_synth(out, nchan, nif, ntime, nfpc, seed, kind, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(BLDP_EHIP, "synth launch: %s", hipGetErrorString(e));
+  return BLDP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,75 @@
+// Internal launch interface shared by kernels.hip and api.hip (not part of the ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bldp.h"
+
+namespace bldp {
+
+// Record the thread-local error message returned by bldp_last_error; returns code.
+int set_error(int code, const char *fmt, ...);
+
+// One reduction launch: nbank banks with identical geometry.
+// Window element (c, i, t) of bank b sits at
+//   in[b][in_off + c*in_cs + i*in_ld_i + t*in_ld_t]
+// and output element (c', i, t') of bank b is written at
+//   out[b*out_bank + c' + i*out_ld_i + t'*out_ld_t].
+struct RedArgs {
+  const float *in[BLDP_MAX_BANKS];
+  float *out;
+  float *ws;  // partials [nchunk][nbank][nto][ni][nco] when nchunk > 1
+  int64_t out_bank, out_ld_i, out_ld_t;
+  int64_t in_off, in_cs, in_ld_i, in_ld_t;
+  int64_t nco, ni, nto, F, T;
+  int64_t rows_per_chunk;  // time rows of one T-block handled by one block
+  int64_t blocks_c;        // blocks along the output-channel axis
+  int32_t nchunk, nbank;
+  int32_t ts;              // waves of a tile that split the T rows (1, 2, 4)
+  int32_t k4;              // float4 loads per lane per row (vector path)
+  int32_t vec_out;         // narrow path: 16/8-byte output stores are legal
+  float div;               // F*T, the mean divisor
+};
+
+enum Path { PATH_VEC = 0, PATH_NARROW = 1, PATH_SCALAR = 2 };
+
+struct Plan {
+  int path;
+  int lpg;                   // lanes per output group (vector path)
+  int64_t grid;              // blocks of 256 threads
+  int64_t nout;              // outputs per bank
+  size_t ws_bytes;           // partial workspace required (0 if nchunk == 1)
+};
+
+// Fill the launch geometry (path, lpg, ts, k4, nchunk, rows_per_chunk,
+// blocks_c, grid) for an args struct whose shape/stride fields are set.
+// `aligned` says whether 16-byte vector loads are legal.
+Plan plan_reduce(RedArgs &a, bool aligned, int num_cus);
+
+hipError_t launch_reduce(const RedArgs &a, const Plan &p, int op, hipStream_t s);
+
+hipError_t launch_stitch(int nbank, const float *g, int64_t nc, int64_t nrows, float *out,
+                         hipStream_t s);
+hipError_t launch_despike(float *d, int64_t nchan, int64_t nrows, int64_t nfpc, int64_t nspike,
+                          hipStream_t s);
+
+struct KurtArgs {
+  const float *in;
+  int64_t in_off, in_cs, in_ld_i, in_ld_t;
+  int64_t nc, ni, nt;
+  int64_t rows_per_chunk;
+  int32_t nchunk;
+  int32_t vec;  // float4 along channels legal
+  double *ws_sum;   // [nchunk][ni][nc]
+  float *mean;      // [ni][nc]
+  double *ws_mom;   // [nchunk][2][ni][nc]
+  double *out;      // [ni][nc]
+};
+void plan_kurtosis(KurtArgs &k, int num_cus);
+size_t kurtosis_ws_bytes(const KurtArgs &k);
+hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s);
+
+hipError_t launch_synth(float *out, int64_t nchan, int64_t nif, int64_t ntime, int64_t nfpc,
+                        uint64_t seed, int kind, hipStream_t s);
+
+}  // namespace bldp

@@ -1,0 +1,690 @@
+// kernels.hip — CDNA4 (gfx950) kernels of libbldp_hip.
+//
+// The hot path is fqav (src/gbtworkerfunctions.jl:16-20) fused with the
+// additive time integration (fqav on axis 3) over a window of a
+// (nchan, nif, ntime) Float32 filterbank, channel fastest.  It is a pure HBM
+// stream (<= 0.25 flop/byte), so the kernels are built around:
+//   * 16-byte (global_load_dwordx4) loads along the channel axis, one 1 KiB
+//     contiguous segment per wave-instruction;
+//   * batches of 8 independent loads per lane before any use, with 8
+//     independent accumulators (latency hiding + shorter FP32 add chains);
+//   * wavefront xor-shuffles to combine the lanes of one decimation group;
+//   * an LDS combine of the waves that split the time rows of one tile, and
+//     a deterministic two-stage (partials + finalize) split of very long time
+//     blocks across workgroups;
+//   * IEEE-754-2019 maximum/minimum (v_maximum3_f32 / v_minimum3_f32 on
+//     gfx950) for max/min, which is exactly Julia's max/min: NaN propagates
+//     and -0.0 < +0.0.
+// No MFMA: nothing here is matmul shaped.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "bldp_impl.h"
+
+namespace bldp {
+namespace {
+
+constexpr int kBlock = 256;  // 4 waves of 64
+
+template <int OP>
+struct R {
+  // sum and mean: Julia's reducedim init is zero(T) (+0.0f)
+  __device__ static constexpr float id() { return 0.0f; }
+  __device__ static float f(float x, float y) { return x + y; }
+};
+template <>
+struct R<BLDP_OP_MAX> {
+  __device__ static constexpr float id() { return -INFINITY; }
+  __device__ static float f(float x, float y) { return __builtin_elementwise_maximum(x, y); }
+};
+template <>
+struct R<BLDP_OP_MIN> {
+  __device__ static constexpr float id() { return INFINITY; }
+  __device__ static float f(float x, float y) { return __builtin_elementwise_minimum(x, y); }
+};
+
+template <int OP>
+__device__ __forceinline__ float4 f4(float4 a, float4 b) {
+  return make_float4(R<OP>::f(a.x, b.x), R<OP>::f(a.y, b.y), R<OP>::f(a.z, b.z),
+                     R<OP>::f(a.w, b.w));
+}
+template <int OP>
+__device__ __forceinline__ float fold4(float4 v) {
+  return R<OP>::f(R<OP>::f(v.x, v.y), R<OP>::f(v.z, v.w));
+}
+__device__ __forceinline__ float4 ld4(const float *p) {
+  return *reinterpret_cast<const float4 *>(p);
+}
+
+// blockIdx.x -> (bc, i, chunk, to, bank); bc fastest so that consecutive
+// workgroups stream consecutive channel segments of one row.
+struct Coord {
+  int64_t bc, i, chunk, to;
+  int bank;
+};
+__device__ __forceinline__ Coord decompose(const RedArgs &a) {
+  Coord c;
+  int64_t b = blockIdx.x;
+  c.bc = b % a.blocks_c;
+  b /= a.blocks_c;
+  c.i = b % a.ni;
+  b /= a.ni;
+  c.chunk = b % a.nchunk;
+  b /= a.nchunk;
+  c.to = b % a.nto;
+  c.bank = (int)(b / a.nto);
+  return c;
+}
+
+template <int OP>
+__device__ __forceinline__ float finish(float s, const RedArgs &a) {
+  if (OP == BLDP_OP_MEAN) return s / a.div;
+  return s;
+}
+
+// ---------------------------------------------------------------------------
+// Vector path, F % 4 == 0.  A group of F channels (G4 = F/4 float4 per row)
+// is owned by LPG lanes (largest power of two dividing G4, <= 64); each lane
+// reads K4 = G4/LPG float4 per row.  A wave therefore owns 64/LPG consecutive
+// outputs and every load instruction covers LPG*16 contiguous bytes per group
+// (1 KiB per wave when K4 == 1 or LPG == 64).  `ts` waves split the T rows of
+// a tile; 4/ts tiles per workgroup.
+template <int OP, int LPG, int K4C>
+__global__ __launch_bounds__(kBlock) void k_reduce_vec(const RedArgs a) {
+  constexpr int OPW = 64 / LPG;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int ts = a.ts;
+  const int wt = wave / ts;
+  const int tsi = wave - wt * ts;
+  const Coord c = decompose(a);
+  const int g = lane / LPG, j = lane % LPG;
+  const int64_t co = (c.bc * (4 / ts) + wt) * OPW + g;
+  const bool valid = co < a.nco;
+  const int64_t r0 = c.chunk * a.rows_per_chunk;
+  const int64_t r1 = min(a.T, r0 + a.rows_per_chunk);
+  const float id = R<OP>::id();
+
+  float4 acc[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) acc[q] = make_float4(id, id, id, id);
+
+  if (valid) {
+    const float *p = a.in[c.bank] + a.in_off + c.i * a.in_ld_i +
+                     (c.to * a.T + r0 + tsi) * a.in_ld_t + co * a.F + 4 * j;
+    int64_t nrows = r1 - r0 - tsi;
+    nrows = nrows > 0 ? (nrows + ts - 1) / ts : 0;
+    const int64_t rstep = (int64_t)ts * a.in_ld_t;
+    if constexpr (K4C > 0) {
+      constexpr int RB = (K4C >= 8) ? 1 : 8 / K4C;
+      constexpr int NV = RB * K4C;
+      for (; nrows >= RB; nrows -= RB) {
+        float4 v[NV];
+#pragma unroll
+        for (int u = 0; u < RB; ++u)
+#pragma unroll
+          for (int k = 0; k < K4C; ++k) v[u * K4C + k] = ld4(p + u * rstep + 4 * k * LPG);
+        p += RB * rstep;
+#pragma unroll
+        for (int q = 0; q < NV; ++q) acc[q % 8] = f4<OP>(acc[q % 8], v[q]);
+      }
+      for (; nrows > 0; --nrows) {
+#pragma unroll
+        for (int k = 0; k < K4C; ++k) acc[k % 8] = f4<OP>(acc[k % 8], ld4(p + 4 * k * LPG));
+        p += rstep;
+      }
+    } else {
+      const int K4 = a.k4;
+      for (; nrows > 0; --nrows) {
+        int k = 0;
+        for (; k + 8 <= K4; k += 8) {
+          float4 v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = ld4(p + 4 * (k + u) * LPG);
+#pragma unroll
+          for (int u = 0; u < 8; ++u) acc[u] = f4<OP>(acc[u], v[u]);
+        }
+        for (; k < K4; ++k) acc[0] = f4<OP>(acc[0], ld4(p + 4 * k * LPG));
+        p += rstep;
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q] = f4<OP>(acc[q], acc[q + 4]);
+  acc[0] = f4<OP>(acc[0], acc[2]);
+  acc[1] = f4<OP>(acc[1], acc[3]);
+  float s = fold4<OP>(f4<OP>(acc[0], acc[1]));
+
+  // combine the LPG lanes of a group (xor butterfly inside aligned segments)
+#pragma unroll
+  for (int off = LPG / 2; off > 0; off >>= 1) s = R<OP>::f(s, __shfl_xor(s, off, 64));
+
+  if (ts > 1) {  // combine the waves that split the time rows, through LDS
+    __shared__ float red[4][64];
+    red[wave][lane] = s;
+    __syncthreads();
+    if (tsi == 0)
+      for (int q = 1; q < ts; ++q) s = R<OP>::f(s, red[wave + q][lane]);
+  }
+  if (tsi == 0 && j == 0 && valid) {
+    if (a.nchunk == 1) {
+      a.out[c.bank * a.out_bank + c.i * a.out_ld_i + c.to * a.out_ld_t + co] = finish<OP>(s, a);
+    } else {
+      a.ws[(((c.chunk * a.nbank + c.bank) * a.nto + c.to) * a.ni + c.i) * a.nco + co] = s;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Narrow path, F in {1, 2}: one float4 (4 channels) per lane per row; no
+// cross-lane work.  F == 1 is pure time integration (gather-stress variant).
+template <int OP, int F>
+__global__ __launch_bounds__(kBlock) void k_reduce_narrow(const RedArgs a) {
+  const Coord c = decompose(a);
+  const int64_t q4 = c.bc * kBlock + threadIdx.x;  // float4 column
+  const int64_t nc4 = a.nco * F / 4;
+  if (q4 >= nc4) return;
+  const int64_t r0 = c.chunk * a.rows_per_chunk;
+  const int64_t r1 = min(a.T, r0 + a.rows_per_chunk);
+  const float id = R<OP>::id();
+  float4 acc[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) acc[q] = make_float4(id, id, id, id);
+  const float *p =
+      a.in[c.bank] + a.in_off + c.i * a.in_ld_i + (c.to * a.T + r0) * a.in_ld_t + 4 * q4;
+  const int64_t st = a.in_ld_t;
+  int64_t nrows = r1 - r0;
+  for (; nrows >= 8; nrows -= 8) {
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = ld4(p + u * st);
+    p += 8 * st;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc[u] = f4<OP>(acc[u], v[u]);
+  }
+  for (; nrows > 0; --nrows) {
+    acc[0] = f4<OP>(acc[0], ld4(p));
+    p += st;
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q] = f4<OP>(acc[q], acc[q + 4]);
+  acc[0] = f4<OP>(acc[0], acc[2]);
+  acc[1] = f4<OP>(acc[1], acc[3]);
+  float4 r = f4<OP>(acc[0], acc[1]);
+  const int64_t co = q4 * (4 / F);
+  if (a.nchunk == 1) {
+    float *o = a.out + c.bank * a.out_bank + c.i * a.out_ld_i + c.to * a.out_ld_t + co;
+    if (F == 1) {
+      r = make_float4(finish<OP>(r.x, a), finish<OP>(r.y, a), finish<OP>(r.z, a),
+                      finish<OP>(r.w, a));
+      if (a.vec_out) {
+        *reinterpret_cast<float4 *>(o) = r;
+      } else {
+        o[0] = r.x; o[1] = r.y; o[2] = r.z; o[3] = r.w;
+      }
+    } else {
+      const float x = finish<OP>(R<OP>::f(r.x, r.y), a), y = finish<OP>(R<OP>::f(r.z, r.w), a);
+      if (a.vec_out) {
+        *reinterpret_cast<float2 *>(o) = make_float2(x, y);
+      } else {
+        o[0] = x; o[1] = y;
+      }
+    }
+  } else {
+    float *o = a.ws + (((c.chunk * a.nbank + c.bank) * a.nto + c.to) * a.ni + c.i) * a.nco + co;
+    if (F == 1) {
+      *reinterpret_cast<float4 *>(o) = r;
+    } else {
+      *reinterpret_cast<float2 *>(o) = make_float2(R<OP>::f(r.x, r.y), R<OP>::f(r.z, r.w));
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Scalar path: any F, any channel step, any alignment.  One lane per output.
+template <int OP>
+__global__ __launch_bounds__(kBlock) void k_reduce_scalar(const RedArgs a) {
+  const Coord c = decompose(a);
+  const int64_t co = c.bc * kBlock + threadIdx.x;
+  if (co >= a.nco) return;
+  const int64_t r0 = c.chunk * a.rows_per_chunk;
+  const int64_t r1 = min(a.T, r0 + a.rows_per_chunk);
+  float acc[4] = {R<OP>::id(), R<OP>::id(), R<OP>::id(), R<OP>::id()};
+  const float *p = a.in[c.bank] + a.in_off + c.i * a.in_ld_i + (c.to * a.T + r0) * a.in_ld_t +
+                   co * a.F * a.in_cs;
+  const int64_t cs = a.in_cs;
+  for (int64_t r = r0; r < r1; ++r) {
+    int64_t k = 0;
+    for (; k + 4 <= a.F; k += 4) {
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = p[(k + u) * cs];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] = R<OP>::f(acc[u], v[u]);
+    }
+    for (; k < a.F; ++k) acc[0] = R<OP>::f(acc[0], p[k * cs]);
+    p += a.in_ld_t;
+  }
+  const float s = R<OP>::f(R<OP>::f(acc[0], acc[1]), R<OP>::f(acc[2], acc[3]));
+  if (a.nchunk == 1)
+    a.out[c.bank * a.out_bank + c.i * a.out_ld_i + c.to * a.out_ld_t + co] = finish<OP>(s, a);
+  else
+    a.ws[(((c.chunk * a.nbank + c.bank) * a.nto + c.to) * a.ni + c.i) * a.nco + co] = s;
+}
+
+// Second stage of a time-chunked reduction: fold the nchunk partials of every
+// output in chunk order (deterministic), apply the mean divisor, scatter into
+// the (possibly stitched) output layout.
+template <int OP>
+__global__ __launch_bounds__(kBlock) void k_reduce_finalize(const RedArgs a) {
+  const int64_t per_chunk = (int64_t)a.nbank * a.nto * a.ni * a.nco;
+  for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < per_chunk;
+       e += (int64_t)gridDim.x * kBlock) {
+    float s = a.ws[e];
+    for (int ch = 1; ch < a.nchunk; ++ch) s = R<OP>::f(s, a.ws[ch * per_chunk + e]);
+    int64_t r = e;
+    const int64_t co = r % a.nco;
+    r /= a.nco;
+    const int64_t i = r % a.ni;
+    r /= a.ni;
+    const int64_t to = r % a.nto;
+    const int64_t bank = r / a.nto;
+    a.out[bank * a.out_bank + i * a.out_ld_i + to * a.out_ld_t + co] = finish<OP>(s, a);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Band stitch: bank-major gathered blocks -> vcat along channels.
+__global__ __launch_bounds__(kBlock) void k_stitch4(int nbank, const float *__restrict__ g,
+                                                    int64_t nc, int64_t nrows,
+                                                    float *__restrict__ out) {
+  const int64_t nc4 = nc / 4, wide4 = nc4 * nbank, n4 = wide4 * nrows;
+  for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < n4;
+       e += (int64_t)gridDim.x * kBlock) {
+    const int64_t row = e / wide4, cw = e - row * wide4;
+    const int64_t b = cw / nc4, c4 = cw - b * nc4;
+    reinterpret_cast<float4 *>(out)[e] =
+        reinterpret_cast<const float4 *>(g)[(b * nrows + row) * nc4 + c4];
+  }
+}
+__global__ __launch_bounds__(kBlock) void k_stitch1(int nbank, const float *__restrict__ g,
+                                                    int64_t nc, int64_t nrows,
+                                                    float *__restrict__ out) {
+  const int64_t wide = nc * nbank, n = wide * nrows;
+  for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * kBlock) {
+    const int64_t row = e / wide, cw = e - row * wide;
+    const int64_t b = cw / nc, c = cw - b * nc;
+    out[e] = g[(b * nrows + row) * nc + c];
+  }
+}
+
+// DC-spike patch: d[spike + k*nfpc] = d[spike - 1 + k*nfpc] per row.
+__global__ __launch_bounds__(kBlock) void k_despike(float *d, int64_t nchan, int64_t nrows,
+                                                    int64_t nfpc, int64_t nspike) {
+  const int64_t n = nrows * nspike;
+  const int64_t spike = nfpc / 2;
+  for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * kBlock) {
+    const int64_t row = e / nspike, k = e - row * nspike;
+    float *r = d + row * nchan + k * nfpc + spike;
+    r[0] = r[-1];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Kurtosis (StatsBase two-pass recipe).  Lanes map to channels (coalesced),
+// workgroups split time into chunks; FP64 partial moments.
+struct KCoord {
+  int64_t col, i, chunk;
+};
+__device__ __forceinline__ KCoord kdecompose(const KurtArgs &k, int64_t ncols) {
+  const int64_t bcs = (ncols + kBlock - 1) / kBlock;
+  int64_t b = blockIdx.x;
+  KCoord c;
+  const int64_t bc = b % bcs;
+  b /= bcs;
+  c.i = b % k.ni;
+  c.chunk = b / k.ni;
+  c.col = bc * kBlock + threadIdx.x;
+  return c;
+}
+
+template <int VEC>
+__global__ __launch_bounds__(kBlock) void k_kurt_sum(const KurtArgs k) {
+  const int64_t ncols = VEC ? k.nc / 4 : k.nc;
+  const KCoord c = kdecompose(k, ncols);
+  if (c.col >= ncols) return;
+  const int64_t r0 = c.chunk * k.rows_per_chunk, r1 = min(k.nt, r0 + k.rows_per_chunk);
+  const float *p = k.in + k.in_off + c.i * k.in_ld_i + r0 * k.in_ld_t +
+                   (VEC ? 4 * c.col : c.col * k.in_cs);
+  double s[4] = {0.0, 0.0, 0.0, 0.0};
+  int64_t n = r1 - r0;
+  if (VEC) {
+    for (; n >= 4; n -= 4) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = ld4(p + u * k.in_ld_t);
+      p += 4 * k.in_ld_t;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        s[0] += (double)v[u].x; s[1] += (double)v[u].y;
+        s[2] += (double)v[u].z; s[3] += (double)v[u].w;
+      }
+    }
+    for (; n > 0; --n, p += k.in_ld_t) {
+      const float4 v = ld4(p);
+      s[0] += (double)v.x; s[1] += (double)v.y; s[2] += (double)v.z; s[3] += (double)v.w;
+    }
+    double *o = k.ws_sum + (c.chunk * k.ni + c.i) * k.nc + 4 * c.col;
+    o[0] = s[0]; o[1] = s[1]; o[2] = s[2]; o[3] = s[3];
+  } else {
+    for (; n >= 4; n -= 4) {
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = p[u * k.in_ld_t];
+      p += 4 * k.in_ld_t;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s[u] += (double)v[u];
+    }
+    for (; n > 0; --n, p += k.in_ld_t) s[0] += (double)p[0];
+    k.ws_sum[(c.chunk * k.ni + c.i) * k.nc + c.col] = (s[0] + s[1]) + (s[2] + s[3]);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_kurt_mean(const KurtArgs k) {
+  const int64_t n = k.ni * k.nc;
+  for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * kBlock) {
+    double s = 0.0;
+    for (int ch = 0; ch < k.nchunk; ++ch) s += k.ws_sum[ch * n + e];
+    // Statistics.mean on Float32: Float32 sum / length, in Float32
+    k.mean[e] = (float)s / (float)k.nt;
+  }
+}
+
+template <int VEC>
+__global__ __launch_bounds__(kBlock) void k_kurt_mom(const KurtArgs k) {
+  const int64_t ncols = VEC ? k.nc / 4 : k.nc;
+  const KCoord c = kdecompose(k, ncols);
+  if (c.col >= ncols) return;
+  const int64_t r0 = c.chunk * k.rows_per_chunk, r1 = min(k.nt, r0 + k.rows_per_chunk);
+  const float *p = k.in + k.in_off + c.i * k.in_ld_i + r0 * k.in_ld_t +
+                   (VEC ? 4 * c.col : c.col * k.in_cs);
+  const int64_t mo = c.i * k.nc + (VEC ? 4 * c.col : c.col);
+  const int64_t n = k.ni * k.nc;
+  double *o2 = k.ws_mom + (c.chunk * 2) * n + mo;
+  double *o4 = o2 + n;
+  if (VEC) {
+    const float4 m = ld4(k.mean + mo);
+    double c2[4] = {0, 0, 0, 0}, c4[4] = {0, 0, 0, 0};
+    for (int64_t r = r0; r < r1; ++r, p += k.in_ld_t) {
+      const float4 v = ld4(p);
+      // StatsBase: z = v[i] - m (Float32); z2 = z*z (Float32);
+      // cm2 += z2; cm4 += z2*z2 (Float64 accumulators)
+      const float zx = v.x - m.x, zy = v.y - m.y, zz = v.z - m.z, zw = v.w - m.w;
+      const float qx = zx * zx, qy = zy * zy, qz = zz * zz, qw = zw * zw;
+      c2[0] += (double)qx; c2[1] += (double)qy; c2[2] += (double)qz; c2[3] += (double)qw;
+      c4[0] += (double)(qx * qx); c4[1] += (double)(qy * qy);
+      c4[2] += (double)(qz * qz); c4[3] += (double)(qw * qw);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { o2[u] = c2[u]; o4[u] = c4[u]; }
+  } else {
+    const float m = k.mean[mo];
+    double c2 = 0.0, c4 = 0.0;
+    for (int64_t r = r0; r < r1; ++r, p += k.in_ld_t) {
+      const float z = p[0] - m;
+      const float z2 = z * z;
+      c2 += (double)z2;
+      c4 += (double)(z2 * z2);
+    }
+    o2[0] = c2;
+    o4[0] = c4;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_kurt_final(const KurtArgs k) {
+  const int64_t n = k.ni * k.nc;
+  for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * kBlock) {
+    double cm2 = 0.0, cm4 = 0.0;
+    for (int ch = 0; ch < k.nchunk; ++ch) {
+      cm2 += k.ws_mom[(ch * 2) * n + e];
+      cm4 += k.ws_mom[(ch * 2 + 1) * n + e];
+    }
+    cm4 /= (double)k.nt;
+    cm2 /= (double)k.nt;
+    k.out[e] = (cm4 / (cm2 * cm2)) - 3.0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic filterbank generator (counter-based, so any element is
+// reproducible from (seed, index) alone).
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+__device__ __forceinline__ float synth_val(uint64_t e, int64_t nchan, int64_t nfpc,
+                                           uint64_t seed, int kind) {
+  const uint64_t h = splitmix64(e + seed * 0xD1B54A32D192ED03ull);
+  if (kind == 1) return (float)(h >> 56);
+  const float u1 = (float)((h >> 41) + 1) * (1.0f / 8388608.0f);
+  const float u2 = (float)(((h >> 17) & 0x7FFFFF) + 1) * (1.0f / 8388608.0f);
+  const float gam = -(logf(u1) + logf(u2)) * 5.0e8f;  // gamma(k=2, theta=5e8)
+  const int64_t x = (int64_t)(e % (uint64_t)nchan) % nfpc;
+  const float s = sinf(3.14159265f * ((float)x + 0.5f) / (float)nfpc);
+  float bp = 0.2f + 0.8f * s * s;  // per-coarse-channel scallop
+  if (x == nfpc / 2) bp *= 10.0f;  // DC spike (src/gbt.jl:102 position)
+  return gam * bp;
+}
+__global__ __launch_bounds__(kBlock) void k_synth(float *out, int64_t n, int64_t nchan,
+                                                  int64_t nfpc, uint64_t seed, int kind,
+                                                  int vec) {
+  const int64_t n4 = (n + 3) / 4;
+  for (int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x; q < n4;
+       q += (int64_t)gridDim.x * kBlock) {
+    const int64_t e = 4 * q;
+    if (vec && e + 3 < n) {
+      float4 v = make_float4(synth_val(e, nchan, nfpc, seed, kind),
+                             synth_val(e + 1, nchan, nfpc, seed, kind),
+                             synth_val(e + 2, nchan, nfpc, seed, kind),
+                             synth_val(e + 3, nchan, nfpc, seed, kind));
+      *reinterpret_cast<float4 *>(out + e) = v;
+    } else {
+      for (int64_t x = e; x < n && x < e + 4; ++x) out[x] = synth_val(x, nchan, nfpc, seed, kind);
+    }
+  }
+}
+
+int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+template <int OP>
+hipError_t launch_vec(const RedArgs &a, const Plan &p, hipStream_t s) {
+  const dim3 grid((unsigned)p.grid), block(kBlock);
+  const int k4c = (a.k4 == 1 || a.k4 == 2 || a.k4 == 4) ? a.k4 : 0;
+#define BLDP_VEC(L, K)                                                 \
+  if (p.lpg == L && k4c == K) {                                        \
+    hipLaunchKernelGGL((k_reduce_vec<OP, L, K>), grid, block, 0, s, a); \
+    return hipGetLastError();                                          \
+  }
+  BLDP_VEC(64, 1) BLDP_VEC(64, 2) BLDP_VEC(64, 4) BLDP_VEC(64, 0)
+  BLDP_VEC(32, 1) BLDP_VEC(32, 0) BLDP_VEC(16, 1) BLDP_VEC(16, 0)
+  BLDP_VEC(8, 1) BLDP_VEC(8, 0) BLDP_VEC(4, 1) BLDP_VEC(4, 0)
+  BLDP_VEC(2, 1) BLDP_VEC(2, 0) BLDP_VEC(1, 1) BLDP_VEC(1, 0)
+#undef BLDP_VEC
+  return hipErrorInvalidValue;
+}
+
+template <int OP>
+hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
+  hipError_t e = hipSuccess;
+  const dim3 grid((unsigned)p.grid), block(kBlock);
+  if (p.path == PATH_VEC) {
+    e = launch_vec<OP>(a, p, s);
+  } else if (p.path == PATH_NARROW) {
+    if (a.F == 1)
+      hipLaunchKernelGGL((k_reduce_narrow<OP, 1>), grid, block, 0, s, a);
+    else
+      hipLaunchKernelGGL((k_reduce_narrow<OP, 2>), grid, block, 0, s, a);
+    e = hipGetLastError();
+  } else {
+    hipLaunchKernelGGL((k_reduce_scalar<OP>), grid, block, 0, s, a);
+    e = hipGetLastError();
+  }
+  if (e != hipSuccess || a.nchunk == 1) return e;
+  const int64_t nout = (int64_t)a.nbank * a.nto * a.ni * a.nco;
+  const unsigned fg = (unsigned)std::min<int64_t>(cdiv(nout, kBlock), 8192);
+  hipLaunchKernelGGL((k_reduce_finalize<OP>), dim3(fg), block, 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+Plan plan_reduce(RedArgs &a, bool aligned, int num_cus) {
+  Plan p{};
+  const int64_t F = a.F, T = a.T;
+  p.nout = a.nco * a.ni * a.nto;
+  const int64_t target_waves = (int64_t)num_cus * 16;  // ~4 waves per SIMD
+  int64_t tiles;  // independent wave/thread tiles before any time split
+  a.ts = 1;
+  a.k4 = 1;
+  if (aligned && F % 4 == 0) {
+    p.path = PATH_VEC;
+    const int64_t g4 = F / 4;
+    int lpg = 1;
+    while (lpg < 64 && g4 % (2 * lpg) == 0) lpg *= 2;
+    p.lpg = lpg;
+    a.k4 = (int32_t)(g4 / lpg);
+    const int64_t ctiles = cdiv(a.nco, 64 / lpg);
+    tiles = ctiles * a.ni * a.nto * a.nbank;
+    while (a.ts < 4 && tiles * a.ts < target_waves && T >= 2 * a.ts * 8) a.ts *= 2;
+    a.blocks_c = cdiv(ctiles, 4 / a.ts);
+    tiles *= a.ts;
+  } else if (aligned && (F == 1 || F == 2) && (a.nco * F) % 4 == 0) {
+    p.path = PATH_NARROW;
+    const int64_t nc4 = a.nco * F / 4;
+    a.blocks_c = cdiv(nc4, kBlock);
+    tiles = cdiv(nc4, 64) * a.ni * a.nto * a.nbank;
+  } else {
+    p.path = PATH_SCALAR;
+    a.blocks_c = cdiv(a.nco, kBlock);
+    tiles = cdiv(a.nco, 64) * a.ni * a.nto * a.nbank;
+  }
+  // Long time blocks with too few tiles: split the T rows across workgroups.
+  const int64_t rows_per_wave = cdiv(T, a.ts);
+  int64_t nchunk = 1;
+  if (tiles < target_waves && rows_per_wave >= 128) {
+    nchunk = std::min<int64_t>(cdiv(target_waves, tiles), rows_per_wave / 64);
+    nchunk = std::max<int64_t>(nchunk, 1);
+  }
+  a.rows_per_chunk = cdiv(T, nchunk);
+  if (a.rows_per_chunk < 1) a.rows_per_chunk = 1;
+  a.nchunk = (int32_t)std::max<int64_t>(1, cdiv(T, a.rows_per_chunk));
+  p.ws_bytes = a.nchunk > 1 ? (size_t)a.nchunk * a.nbank * p.nout * sizeof(float) : 0;
+  p.grid = a.blocks_c * a.ni * a.nchunk * a.nto * a.nbank;
+  // narrow-path vector stores
+  a.vec_out = 0;
+  if (p.path == PATH_NARROW) {
+    const int64_t w = 4 / F;  // outputs per lane
+    const uintptr_t op = (uintptr_t)a.out;
+    a.vec_out = (op % (4 * w) == 0) && a.out_bank % w == 0 && a.out_ld_i % w == 0 &&
+                a.out_ld_t % w == 0;
+  }
+  a.div = (float)(F * T);
+  return p;
+}
+
+hipError_t launch_reduce(const RedArgs &a, const Plan &p, int op, hipStream_t s) {
+  if (p.grid <= 0) return hipSuccess;
+  switch (op) {
+    case BLDP_OP_SUM: return launch_op<BLDP_OP_SUM>(a, p, s);
+    case BLDP_OP_MEAN: return launch_op<BLDP_OP_MEAN>(a, p, s);
+    case BLDP_OP_MAX: return launch_op<BLDP_OP_MAX>(a, p, s);
+    case BLDP_OP_MIN: return launch_op<BLDP_OP_MIN>(a, p, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_stitch(int nbank, const float *g, int64_t nc, int64_t nrows, float *out,
+                         hipStream_t s) {
+  const int64_t n = (int64_t)nbank * nc * nrows;
+  if (n == 0) return hipSuccess;
+  const bool v = nc % 4 == 0 && (uintptr_t)g % 16 == 0 && (uintptr_t)out % 16 == 0;
+  const int64_t work = v ? n / 4 : n;
+  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(work, kBlock), 16384);
+  if (v)
+    hipLaunchKernelGGL(k_stitch4, dim3(grid), dim3(kBlock), 0, s, nbank, g, nc, nrows, out);
+  else
+    hipLaunchKernelGGL(k_stitch1, dim3(grid), dim3(kBlock), 0, s, nbank, g, nc, nrows, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_despike(float *d, int64_t nchan, int64_t nrows, int64_t nfpc, int64_t nspike,
+                          hipStream_t s) {
+  const int64_t n = nrows * nspike;
+  if (n == 0) return hipSuccess;
+  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(n, kBlock), 16384);
+  hipLaunchKernelGGL(k_despike, dim3(grid), dim3(kBlock), 0, s, d, nchan, nrows, nfpc, nspike);
+  return hipGetLastError();
+}
+
+void plan_kurtosis(KurtArgs &k, int num_cus) {
+  const int64_t ncols = k.vec ? k.nc / 4 : k.nc;
+  const int64_t tiles = cdiv(ncols, 64) * k.ni;
+  const int64_t target = (int64_t)num_cus * 16;
+  int64_t nchunk = 1;
+  if (tiles < target && k.nt >= 128) nchunk = std::min<int64_t>(cdiv(target, tiles), k.nt / 64);
+  nchunk = std::max<int64_t>(nchunk, 1);
+  k.rows_per_chunk = std::max<int64_t>(1, cdiv(k.nt, nchunk));
+  k.nchunk = (int32_t)std::max<int64_t>(1, cdiv(k.nt, k.rows_per_chunk));
+}
+
+size_t kurtosis_ws_bytes(const KurtArgs &k) {
+  const size_t n = (size_t)k.ni * k.nc;
+  auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  return up(n * k.nchunk * sizeof(double)) + up(n * sizeof(float)) +
+         up(2 * n * k.nchunk * sizeof(double));
+}
+
+hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s) {
+  const size_t n = (size_t)k.ni * k.nc;
+  if (n == 0) return hipSuccess;
+  auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  k.ws_sum = reinterpret_cast<double *>(ws);
+  k.mean = reinterpret_cast<float *>(ws + up(n * k.nchunk * sizeof(double)));
+  k.ws_mom = reinterpret_cast<double *>(ws + up(n * k.nchunk * sizeof(double)) +
+                                        up(n * sizeof(float)));
+  const int64_t ncols = k.vec ? k.nc / 4 : k.nc;
+  const dim3 grid((unsigned)(cdiv(ncols, kBlock) * k.ni * k.nchunk)), block(kBlock);
+  const unsigned eg = (unsigned)std::min<int64_t>(cdiv((int64_t)n, kBlock), 8192);
+  if (k.vec)
+    hipLaunchKernelGGL(k_kurt_sum<1>, grid, block, 0, s, k);
+  else
+    hipLaunchKernelGGL(k_kurt_sum<0>, grid, block, 0, s, k);
+  hipLaunchKernelGGL(k_kurt_mean, dim3(eg), block, 0, s, k);
+  if (k.vec)
+    hipLaunchKernelGGL(k_kurt_mom<1>, grid, block, 0, s, k);
+  else
+    hipLaunchKernelGGL(k_kurt_mom<0>, grid, block, 0, s, k);
+  hipLaunchKernelGGL(k_kurt_final, dim3(eg), block, 0, s, k);
+  return hipGetLastError();
+}
+
+hipError_t launch_synth(float *out, int64_t nchan, int64_t nif, int64_t ntime, int64_t nfpc,
+                        uint64_t seed, int kind, hipStream_t s) {
+  const int64_t n = nchan * nif * ntime;
+  if (n == 0) return hipSuccess;
+  const int vec = ((uintptr_t)out % 16) == 0;
+  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(cdiv(n, 4), kBlock), 65536);
+  hipLaunchKernelGGL(k_synth, dim3(grid), dim3(kBlock), 0, s, out, n, nchan, nfpc, seed, kind,
+                     vec);
+  return hipGetLastError();
+}
+
+}  // namespace bldp

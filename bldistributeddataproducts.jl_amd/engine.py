@@ -1,0 +1,270 @@
+"""Device-side operations on filterbank tensors, all through libbldp_hip.
+
+Layout: a filterbank is a torch tensor whose LOGICAL shape is Julia's
+``(nchan, nif, ntime)`` and whose memory is channel-fastest, i.e. strides
+``(1, nchan, nchan*nif)`` — a ``permute(2, 1, 0)`` view of a contiguous
+``[ntime][nif][nchan]`` buffer, the on-disk FBH5 order (SURVEY.md §8 notation).
+Views with larger pitches (sub-windows of a bigger array) are accepted as-is;
+anything else is rejected rather than silently copied.
+
+torch supplies device memory and streams only; every byte of arithmetic runs
+in the HIP kernels of libbldp_hip.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .idxs import window_shape
+
+__all__ = [
+    "fb_empty", "fb_from_numpy", "fb_to_numpy", "reduce", "band_reduce", "stitch",
+    "despike", "kurtosis", "synth", "plan", "reduce_host",
+]
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+def fb_empty(nchan, nif, ntime, device=None, dtype=None):
+    """Uninitialised Julia-order (nchan, nif, ntime) Float32 tensor on the GPU."""
+    torch = _torch()
+    dtype = dtype or torch.float32
+    return torch.empty((int(ntime), int(nif), int(nchan)), dtype=dtype,
+                       device=device or "cuda").permute(2, 1, 0)
+
+
+def fb_from_numpy(a: np.ndarray, device=None):
+    """Host (nchan, nif, ntime) array -> device tensor with the same layout."""
+    torch = _torch()
+    a = np.asfortranarray(np.asarray(a, dtype=np.float32))
+    if a.ndim != 3:
+        raise ValueError("filterbank arrays are 3-D (nchan, nif, ntime)")
+    t = torch.from_numpy(np.ascontiguousarray(a.transpose(2, 1, 0)))
+    return t.to(device or "cuda").permute(2, 1, 0)
+
+
+def fb_to_numpy(t) -> np.ndarray:
+    """Device tensor (Julia order) -> Fortran-ordered numpy array."""
+    if t.dim() == 3:
+        return np.asfortranarray(t.permute(2, 1, 0).contiguous().cpu().numpy().transpose(2, 1, 0))
+    return np.asfortranarray(t.t().contiguous().cpu().numpy().T)
+
+
+def _abi_dims(t):
+    """Map a channel-fastest tensor to (ptr, nchan, nif, ntime) of an array
+    that contains it, so that its logical index (c, i, t) is element
+    c + nchan*(i + nif*t) of the ABI array."""
+    torch = _torch()
+    if t.dtype != torch.float32:
+        raise TypeError("filterbank tensors are Float32")
+    if not t.is_cuda:
+        raise TypeError("device tensor expected (use getdata/reduce_host for host arrays)")
+    if t.dim() != 3:
+        raise ValueError("filterbank tensors are 3-D (nchan, nif, ntime)")
+    n0, n1, n2 = t.shape
+    s0, s1, s2 = t.stride()
+    if n0 > 1 and s0 != 1:
+        raise ValueError("channel axis must be the fastest (stride 1); use fb_empty layout")
+    if n1 > 1 and n2 > 1:
+        if s1 < n0 or s2 % s1 or s2 // s1 < n1:
+            raise ValueError(f"unsupported strides {t.stride()} for shape {tuple(t.shape)}")
+        nchan, nif = s1, s2 // s1
+    elif n1 > 1:
+        if s1 < n0:
+            raise ValueError(f"unsupported strides {t.stride()}")
+        nchan, nif = s1, n1
+    else:
+        nchan = s2 if (n2 > 1 and s2 >= n0) else n0
+        if n2 > 1 and s2 < n0:
+            raise ValueError(f"unsupported strides {t.stride()}")
+        nif = 1
+    return t.data_ptr(), int(nchan), int(nif), int(n2)
+
+
+def _check_bounds(win, shape):
+    if win is None:
+        return
+    for ax in range(3):
+        st, ct, sp = win[3 * ax: 3 * ax + 3]
+        if ct > 0:
+            last = st + (ct - 1) * sp
+            if min(st, last) < 0 or max(st, last) >= shape[ax]:
+                raise _lib.BoundsError(
+                    _lib.BLDP_EBOUNDS,
+                    f"BoundsError: window {st + 1}:{sp}:{last + 1} outside axis {ax + 1} of "
+                    f"size {shape[ax]}")
+
+
+def _full_win(win, shape):
+    return list(win) if win is not None else [0, shape[0], 1, 0, shape[1], 1, 0, shape[2], 1]
+
+
+def out_shape(shape, win, fqavby, tavby):
+    nc, ni, nt = window_shape(win, shape)
+    F, T = max(int(fqavby), 1), max(int(tavby), 1)
+    if nc % F:
+        raise _lib.DimensionMismatch(_lib.BLDP_EDIM,
+                                     f"DimensionMismatch: fqavby={F} does not divide nchan={nc}")
+    if nt % T:
+        raise _lib.DimensionMismatch(_lib.BLDP_EDIM,
+                                     f"DimensionMismatch: tavby={T} does not divide ntime={nt}")
+    return nc // F, ni, nt // T
+
+
+def reduce(x, fqavby=1, tavby=1, op="sum", win=None, out=None, stream=None):
+    """fqav on the channel axis fused with time integration, on the GPU.
+
+    x: device filterbank tensor; win: 9-int window (see idxs.to_window) or
+    None; returns a Julia-order (nc/F, ni, nt/T) device tensor."""
+    L = _lib.lib()
+    shape = tuple(x.shape)
+    _check_bounds(win, shape)
+    nco, ni, nto = out_shape(shape, win, fqavby, tavby)
+    if out is None:
+        out = fb_empty(nco, ni, nto, device=x.device)
+    elif tuple(out.shape) != (nco, ni, nto):
+        raise ValueError(f"out has shape {tuple(out.shape)}, expected {(nco, ni, nto)}")
+    optr, onc, oni, _ = _abi_dims(out) if out.numel() else (0, nco, ni, nto)
+    ptr, nchan, nif, ntime = _abi_dims(x)
+    keep, wp = _lib.win_arg(_full_win(win, shape))
+    rc = L.bldp_reduce_strided_f32(ptr, nchan, nif, ntime, wp, int(fqavby), int(tavby),
+                                   _lib.OPS[op], optr, onc, onc * oni, _lib.stream_ptr(stream))
+    _lib.check(rc, "bldp_reduce_strided_f32")
+    return out
+
+
+def plan(x, fqavby=1, tavby=1, op="sum", win=None) -> dict:
+    """Launch plan the library picks for this call (path, lanes/group, ...)."""
+    L = _lib.lib()
+    shape = tuple(x.shape)
+    _check_bounds(win, shape)
+    ptr, nchan, nif, ntime = _abi_dims(x)
+    info = (ctypes.c_int64 * 8)()
+    keep, wp = _lib.win_arg(_full_win(win, shape))
+    rc = L.bldp_reduce_plan_f32(ptr, nchan, nif, ntime, wp, int(fqavby), int(tavby),
+                                _lib.OPS[op], None, info)
+    _lib.check(rc, "bldp_reduce_plan_f32")
+    keys = ["path", "lanes_per_group", "time_split_waves", "float4_per_lane", "time_chunks",
+            "workgroups", "workspace_bytes", "vec_out"]
+    d = dict(zip(keys, list(info)))
+    d["path"] = _lib.PATHS[d["path"]]
+    return d
+
+
+def band_reduce(banks, fqavby=1, tavby=1, op="sum", win=None, out=None, stream=None):
+    """Reduce every bank of a band resident on ONE GPU and stitch them in bank
+    order (reduce(vcat, ...), src/gbt.jl:103) in a single launch."""
+    L = _lib.lib()
+    banks = list(banks)
+    if not banks:
+        raise ValueError("no banks")
+    shape = tuple(banks[0].shape)
+    geo = None
+    for b in banks:
+        if tuple(b.shape) != shape:
+            raise ValueError("all banks of a band must have the same shape")
+        g = _abi_dims(b)[1:]
+        if geo is None:
+            geo = g
+        elif g != geo:
+            raise ValueError("all banks of a band must have the same layout")
+    _check_bounds(win, shape)
+    nco, ni, nto = out_shape(shape, win, fqavby, tavby)
+    nb = len(banks)
+    if out is None:
+        out = fb_empty(nb * nco, ni, nto, device=banks[0].device)
+    if tuple(out.shape) != (nb * nco, ni, nto) or (
+            out.numel() and out.stride() != (1, nb * nco, nb * nco * ni) and ni * nto > 1):
+        raise ValueError("out must be a dense Julia-order (nbank*nco, ni, nto) tensor")
+    ptrs = (ctypes.c_void_p * nb)(*[b.data_ptr() for b in banks])
+    keep, wp = _lib.win_arg(_full_win(win, shape))
+    nchan, nif, ntime = geo
+    rc = L.bldp_band_reduce_f32(nb, ctypes.cast(ptrs, ctypes.c_void_p), nchan, nif, ntime, wp,
+                                int(fqavby), int(tavby), _lib.OPS[op],
+                                out.data_ptr() if out.numel() else None,
+                                _lib.stream_ptr(stream))
+    _lib.check(rc, "bldp_band_reduce_f32")
+    return out
+
+
+def stitch(gathered, nbank, out=None, stream=None):
+    """gathered: nbank dense (nc, ni, nt) blocks back to back (1-D or a
+    [nbank, nt, ni, nc] contiguous tensor); returns vcat (nbank*nc, ni, nt)."""
+    L = _lib.lib()
+    g = gathered
+    if g.dim() == 4:
+        nb, nt, ni, nc = g.shape
+    else:
+        raise ValueError("gathered must be a contiguous [nbank, ntime, nif, nc] tensor")
+    if nb != nbank or not g.is_contiguous():
+        raise ValueError("gathered must be a contiguous [nbank, ntime, nif, nc] tensor")
+    if out is None:
+        out = fb_empty(nbank * nc, ni, nt, device=g.device)
+    rc = L.bldp_stitch_f32(nbank, g.data_ptr(), nc, ni, nt, out.data_ptr(),
+                           _lib.stream_ptr(stream))
+    _lib.check(rc, "bldp_stitch_f32")
+    return out
+
+
+def despike(x, nfpc, stream=None):
+    """In place: every coarse channel's DC bin takes its left neighbour's
+    value (src/gbt.jl:101-102,111).  Returns x."""
+    L = _lib.lib()
+    ptr, nchan, nif, ntime = _abi_dims(x)
+    if nchan != x.shape[0] or (x.shape[1] > 1 and nif != x.shape[1]):
+        raise ValueError("despike needs a dense Julia-order tensor")
+    rc = L.bldp_despike_f32(ptr, x.shape[0], x.shape[1], x.shape[2], int(nfpc),
+                            _lib.stream_ptr(stream))
+    _lib.check(rc, "bldp_despike_f32")
+    return x
+
+
+def kurtosis(x, win=None, stream=None):
+    """Excess kurtosis over time per (channel, IF): (nc, ni) float64 tensor."""
+    torch = _torch()
+    L = _lib.lib()
+    shape = tuple(x.shape)
+    _check_bounds(win, shape)
+    nc, ni, _ = window_shape(win, shape)
+    out = torch.empty((ni, nc), dtype=torch.float64, device=x.device).t()
+    ptr, nchan, nif, ntime = _abi_dims(x)
+    keep, wp = _lib.win_arg(_full_win(win, shape))
+    rc = L.bldp_kurtosis_f32(ptr, nchan, nif, ntime, wp, out.data_ptr() if out.numel() else None,
+                             None, _lib.stream_ptr(stream))
+    _lib.check(rc, "bldp_kurtosis_f32")
+    return out
+
+
+def synth(nchan, nif, ntime, nfpc=1024, seed=0, kind=0, device=None, stream=None):
+    """Synthetic BL-like filterbank generated on the GPU (bldp_synth_f32)."""
+    L = _lib.lib()
+    out = fb_empty(nchan, nif, ntime, device=device)
+    rc = L.bldp_synth_f32(out.data_ptr() if out.numel() else None, nchan, nif, ntime, nfpc,
+                          seed, kind, _lib.stream_ptr(stream))
+    _lib.check(rc, "bldp_synth_f32")
+    return out
+
+
+def reduce_host(a: np.ndarray, fqavby=1, tavby=1, op="sum", win=None, device=0) -> np.ndarray:
+    """Host array in, host array out (bldp_reduce_host_f32): the window is
+    streamed through the GPU and reduced there."""
+    L = _lib.lib()
+    a = np.asarray(a)
+    if a.dtype != np.float32 or not a.flags.f_contiguous or a.ndim != 3:
+        raise TypeError("host filterbank must be a Fortran-ordered float32 (nchan, nif, ntime)")
+    shape = a.shape
+    _check_bounds(win, shape)
+    nco, ni, nto = out_shape(shape, win, fqavby, tavby)
+    out = np.empty((nco, ni, nto), dtype=np.float32, order="F")
+    keep, wp = _lib.win_arg(_full_win(win, shape))
+    rc = L.bldp_reduce_host_f32(int(device), a.ctypes.data if a.size else None, shape[0],
+                                shape[1], shape[2], wp, int(fqavby), int(tavby), _lib.OPS[op],
+                                out.ctypes.data if out.size else None)
+    _lib.check(rc, "bldp_reduce_host_f32")
+    return out

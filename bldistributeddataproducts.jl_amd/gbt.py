@@ -1,0 +1,99 @@
+"""Mirror of module ``GBT`` (src/gbt.jl) on one MI355X node.
+
+In the reference a *worker* is a Julia process on a ``blcXY`` host reached
+over ssh (src/gbt.jl:12-46).  Here a worker is a GPU of this node: worker
+``w`` runs its bank's read + reduce on device ``w``.  The fan-out/gather shape
+of every call is unchanged: one call per ``(worker, fname)`` pair, results in
+an array of the same size (src/gbt.jl:73-78).  ``getband`` is the additive
+stitched-product call.
+"""
+from __future__ import annotations
+
+import warnings
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+from . import readers, worker as W
+from .idxs import COLON
+
+__all__ = ["datahosts", "setupworkers", "getinventories", "getheaders", "getdata",
+           "getkurtosis", "getband", "fqav"]
+
+fqav = W.fqav  # `using .WorkerFunctions` re-exports fqav (src/gbt.jl:6)
+
+_workers: list[int] = []
+
+
+def datahosts(prefix: str = "") -> list[str]:
+    """["blc00", ..., "blc77"] (src/gbt.jl:8-10)."""
+    return [f"{prefix}blc{i}{j}" for i in range(8) for j in range(8)]
+
+
+def setupworkers(hosts=(), **kwargs) -> list[int]:
+    """Bind one worker per host to the GPUs of this node, round-robin
+    (src/gbt.jl:12-46).  Warns and returns [] when workers already exist
+    (:20-23)."""
+    global _workers
+    if _workers:
+        warnings.warn("workers already added, not adding more")
+        return []
+    import torch
+
+    ndev = torch.cuda.device_count()
+    if ndev == 0:
+        raise RuntimeError("no GPU visible: workers run on MI355X devices")
+    hosts = list(hosts) or datahosts(kwargs.get("prefix", ""))
+    _workers = [k % ndev for k in range(len(hosts))]
+    return list(_workers)
+
+
+def _fanout(workers, fnames, fn):
+    workers, fnames = np.asarray(workers, dtype=object), np.asarray(fnames, dtype=object)
+    assert workers.shape == fnames.shape, "workers and fnames must have the same size"
+    flat = list(zip(workers.ravel(), fnames.ravel()))
+    with ThreadPoolExecutor(max_workers=max(1, len(flat))) as ex:  # @spawnat per pair
+        res = list(ex.map(lambda wf: fn(*wf), flat))  # fetch.(futures)
+    out = np.empty(len(res), dtype=object)
+    out[:] = res
+    return out.reshape(workers.shape)
+
+
+def getinventories(workers, filere=r"0002.h5$", root="/datax/dibas",
+                   sessionre=readers.DEFAULT_SESSIONRE, extra="GUPPI",
+                   playerre=readers.DEFAULT_PLAYERRE):
+    """src/gbt.jl:48-58."""
+    return [readers.getinventory(filere, root=root, sessionre=sessionre, extra=extra,
+                                 playerre=playerre, worker=w) for w in workers]
+
+
+def getheaders(workers, fnames):
+    """src/gbt.jl:60-67."""
+    return _fanout(workers, fnames, lambda w, f: readers.getheader(f))
+
+
+def getdata(workers, fnames, idxs=(COLON, COLON, COLON), fqavby=1, fqavfunc="sum", tavby=1):
+    """src/gbt.jl:69-79 (+ tavby): an array of per-bank (nchan/fqavby, nif,
+    ntime/tavby) Float32 arrays, the same size as workers/fnames."""
+    return _fanout(workers, fnames,
+                   lambda w, f: W.getdata(f, idxs, fqavby, fqavfunc, tavby, device=int(w)))
+
+
+def getkurtosis(workers, fnames, idxs=(COLON, COLON, COLON)):
+    """src/gbt.jl:81-88."""
+    return _fanout(workers, fnames, lambda w, f: W.getkurtosis(f, idxs, device=int(w)))
+
+
+def getband(workers, fnames, idxs=(COLON, COLON, COLON), fqavby=1, fqavfunc="sum", tavby=1,
+            despike_nfpc=None):
+    """The stitched band product: reduce(vcat, getdata(...)) in the given
+    bank order (src/gbt.jl:103).  With ``despike_nfpc`` the DC bin of every
+    coarse channel is patched as in loadscan (src/gbt.jl:101-102,111)."""
+    parts = list(getdata(workers, fnames, idxs, fqavby, fqavfunc, tavby).ravel())
+    band = np.asfortranarray(np.concatenate(parts, axis=0))
+    if despike_nfpc:
+        from . import engine
+
+        x = engine.fb_from_numpy(band, device=f"cuda:{int(np.asarray(workers).ravel()[0])}")
+        band = engine.fb_to_numpy(engine.despike(x, despike_nfpc))
+    return band

@@ -1,0 +1,196 @@
+"""Mirror of ``GBT.WorkerFunctions`` (src/gbtworkerfunctions.jl) — the
+worker-side read + reduce, with the reduction moved onto the MI355X.
+
+Same names, argument meanings and error behaviour as the reference:
+
+* ``fqav(A, n, f="sum")``  — :16-20 (array) and :27-33 (range);
+* ``sanitizeidxs``          — :167-169 (re-exported from .idxs);
+* ``getdata(fname, idxs, fqavby=1, fqavfunc="sum")`` — :191-195, plus the
+  additive ``tavby`` time integration;
+* ``getfbdata`` / ``getfbh5data`` — :171-177 / :179-189;
+* ``getkurtosis``            — :197-202;
+* ``getinventory`` / headers — :35-159 (host metadata, see .readers).
+
+``fqavfunc`` is one of ``"sum" | "mean" | "max" | "min"`` (or the Python
+builtins ``sum``/``max``/``min``, ``numpy.sum``/``mean``/``max``/``min``).
+Any other callable is applied on the host exactly like the reference's
+generic ``f(reshape(A, ...); dims=1)`` path (README.md:192-195) — that is the
+reference behaviour for functions the GPU does not implement, not a fallback
+of the GPU path.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib, engine, readers
+from .idxs import COLON, JRange, sanitizeidxs, to_window  # noqa: F401  (re-exports)
+
+__all__ = [
+    "fqav", "FRange", "sanitizeidxs", "getdata", "getfbdata", "getfbh5data", "getkurtosis",
+    "getinventory", "getfbheader", "getfbh5header", "getheader",
+]
+
+
+@dataclass(frozen=True)
+class FRange:
+    """Julia ``range(first; step, length)`` (a StepRangeLen) — the type
+    ``fqav(r::AbstractRange, n)`` returns (src/gbtworkerfunctions.jl:32)."""
+
+    first: float
+    step: float
+    length: int
+
+    def __len__(self):
+        return self.length
+
+    @property
+    def last(self) -> float:
+        return self.first + (self.length - 1) * self.step
+
+    def values(self) -> np.ndarray:
+        return self.first + self.step * np.arange(self.length, dtype=np.float64)
+
+
+def _opname(f) -> str | None:
+    if isinstance(f, str):
+        if f not in _lib.OPS:
+            raise ValueError(f"fqavfunc {f!r} not one of {sorted(_lib.OPS)}")
+        return f
+    names = {sum: "sum", max: "max", min: "min", np.sum: "sum", np.mean: "mean",
+             np.max: "max", np.min: "min", np.amax: "max", np.amin: "min"}
+    return names.get(f)
+
+
+def _is_tensor(x) -> bool:
+    try:
+        import torch
+    except ImportError:  # pragma: no cover
+        return False
+    return isinstance(x, torch.Tensor)
+
+
+def fqav_range(r, n: int):
+    """fqav(r::AbstractRange, n) (src/gbtworkerfunctions.jl:27-33)."""
+    if isinstance(r, JRange):
+        first, step, length = float(r.first), float(r.step), len(r)
+    elif isinstance(r, FRange):
+        first, step, length = r.first, r.step, r.length
+    else:
+        raise TypeError("range expected")
+    if n <= 1:  # :28
+        return r
+    import ctypes
+
+    f, s, l = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
+    _lib.check(_lib.lib().bldp_fqav_range(first, step, length, int(n), ctypes.byref(f),
+                                          ctypes.byref(s), ctypes.byref(l)), "bldp_fqav_range")
+    return FRange(f.value, s.value, l.value)
+
+
+def _host_generic(A: np.ndarray, n: int, f) -> np.ndarray:
+    """Reference semantics for an arbitrary Julia-style f(X; dims=1)."""
+    if A.shape[0] % n:
+        raise _lib.DimensionMismatch(_lib.BLDP_EDIM,
+                                     f"DimensionMismatch: fqavby={n} does not divide {A.shape[0]}")
+    R = np.asarray(A).reshape((n, A.shape[0] // n) + A.shape[1:], order="F")
+    return np.asfortranarray(np.asarray(f(R, axis=0), dtype=A.dtype))
+
+
+def fqav(A, n: int, f="sum"):
+    """Reduce every ``n`` elements of the first dimension of ``A`` with ``f``
+    (src/gbtworkerfunctions.jl:16-20).  ``n <= 1`` returns ``A`` itself (:17).
+    Device tensors stay on the device; host arrays go through the GPU and
+    come back as host arrays."""
+    if isinstance(A, (JRange, FRange)):
+        return fqav_range(A, n)
+    if n <= 1:
+        return A
+    op = _opname(f)
+    if _is_tensor(A):
+        if op is None:
+            raise TypeError("only sum/mean/max/min run on device tensors")
+        return engine.reduce(A, n, 1, op)
+    A = np.asarray(A)
+    if op is None:
+        return _host_generic(A, n, f)
+    a3 = A.reshape(A.shape + (1,) * (3 - A.ndim)) if A.ndim < 3 else A
+    if a3.ndim != 3:
+        raise ValueError("fqav arrays are at most 3-D (nchan, nif, ntime)")
+    out = engine.reduce_host(np.asfortranarray(a3, dtype=np.float32), n, 1, op)
+    return out.reshape((out.shape[0],) + A.shape[1:])
+
+
+def _reduce_array(x, idxs, fqavby, fqavfunc, tavby, device):
+    idxs = sanitizeidxs(idxs)
+    win = to_window(idxs, x.shape)
+    op = _opname(fqavfunc)
+    if op is None:
+        if tavby > 1:
+            raise TypeError("tavby needs fqavfunc in sum/mean/max/min")
+        a = np.asarray(x)
+        if win is not None:
+            ax = [win[3 * k] + win[3 * k + 2] * np.arange(win[3 * k + 1]) for k in range(3)]
+            a = a[np.ix_(*ax)]
+        return fqav(a, fqavby, fqavfunc)
+    if _is_tensor(x):
+        return engine.reduce(x, fqavby, tavby, op, win)
+    a = np.asarray(x)
+    if a.dtype != np.float32 or not a.flags.f_contiguous:
+        a = np.asfortranarray(a, dtype=np.float32)
+    return engine.reduce_host(a, fqavby, tavby, op, win, device=device)
+
+
+def getfbdata(fbname, idxs=(COLON, COLON, COLON), fqavby=1, fqavfunc="sum", tavby=1,
+              device=0):
+    """SIGPROC filterbank: mmap, window, reduce (src/gbtworkerfunctions.jl:171-177)."""
+    assert len(idxs) == 3, "idxs must have exactly three indices"  # :172
+    _, data = readers.fil_mmap(fbname)
+    try:
+        return _reduce_array(data, idxs, fqavby, fqavfunc, tavby, device)
+    finally:
+        del data  # finalize(parent(dmmap)) (:175)
+
+
+def getfbh5data(fbh5name, idxs=(COLON, COLON, COLON), fqavby=1, fqavfunc="sum", tavby=1,
+                device=0):
+    """FBH5: read the window (whole dataset for (:,:,:)), then reduce
+    (src/gbtworkerfunctions.jl:179-189)."""
+    assert len(idxs) == 3, "idxs must have exactly three indices"  # :180
+    data = readers.fbh5_read(fbh5name, sanitizeidxs(idxs))
+    return _reduce_array(data, (COLON, COLON, COLON), fqavby, fqavfunc, tavby, device)
+
+
+def getdata(fname, idxs=(COLON, COLON, COLON), fqavby=1, fqavfunc="sum", tavby=1, device=0):
+    """WorkerFunctions.getdata (src/gbtworkerfunctions.jl:191-195).
+
+    ``fname`` may also be an in-memory filterbank: a Fortran-ordered
+    (nchan, nif, ntime) float32 array (result on the host) or a Julia-order
+    device tensor (result stays on the device)."""
+    if not isinstance(fname, (str, bytes)) and not hasattr(fname, "__fspath__"):
+        return _reduce_array(fname, idxs, fqavby, fqavfunc, tavby, device)
+    idxs = sanitizeidxs(idxs)  # :192
+    if readers.ishdf5(fname):  # :193
+        return getfbh5data(fname, idxs, fqavby, fqavfunc, tavby, device)
+    return getfbdata(fname, idxs, fqavby, fqavfunc, tavby, device)
+
+
+def getkurtosis(fname, idxs=(COLON, COLON, COLON), device=0):
+    """Excess kurtosis of every (channel, IF) row over time, Float64 (nc, ni)
+    (src/gbtworkerfunctions.jl:197-202)."""
+    idxs = sanitizeidxs(idxs)
+    if _is_tensor(fname):
+        return engine.kurtosis(fname, to_window(idxs, fname.shape))
+    data = getdata(fname, idxs, device=device)  # :198 (window read, no fqav)
+    import torch
+
+    with torch.cuda.device(device):
+        x = engine.fb_from_numpy(data, device=f"cuda:{device}")
+        return engine.fb_to_numpy(engine.kurtosis(x))
+
+
+getinventory = readers.getinventory
+getfbheader = readers.getfbheader
+getfbh5header = readers.getfbh5header
+getheader = readers.getheader

@@ -1,0 +1,147 @@
+/*
+ * bldp.h — C ABI of libbldp_hip, the MI355X engine for the worker-side
+ * reduction of BLDistributedDataProducts.jl (reference v0.3.2).
+ *
+ * Every entry point here replaces one piece of the reference's Julia hot path
+ * (paths are relative to the reference repo root):
+ *
+ *   bldp_reduce_f32        fqav(A, n; f) src/gbtworkerfunctions.jl:16-20, applied
+ *                          to the window read at :182-186 / :173-174, plus the
+ *                          additive time integration (fqav on axis 3).
+ *   bldp_reduce_host_f32   same, for a host array (what WorkerFunctions.getdata
+ *                          holds after the HDF5/mmap read, :174 / :188).
+ *   bldp_band_reduce_f32   GBT.getdata fan-out (src/gbt.jl:69-79) + the band
+ *                          stitch reduce(vcat, ...) (src/gbt.jl:103) for banks
+ *                          resident on one GPU.
+ *   bldp_stitch_f32        reduce(vcat, banks) (src/gbt.jl:103) of bank-major
+ *                          gathered blocks.
+ *   bldp_despike_f32       d[spike:nfpc:end,:,:] .= d[spike-1:nfpc:end,:,:]
+ *                          (src/gbt.jl:101-102,111).
+ *   bldp_kurtosis_f32      getkurtosis (src/gbtworkerfunctions.jl:197-202) with
+ *                          StatsBase.kurtosis' two-pass recipe.
+ *   bldp_fqav_range        fqav(r::AbstractRange, n) src/gbtworkerfunctions.jl:27-33.
+ *
+ * Conventions
+ *   - Arrays are Julia column-major (nchan, nif, ntime), channel fastest
+ *     (README.md:165-168); in C terms data[t][i][c].
+ *   - A window is 9 int64: {c0, nc, cs, i0, ni, is, t0, nt, ts} = 0-based
+ *     start, count and step per axis (a Julia range a:s:b becomes start=a-1,
+ *     count=length, step=s).  NULL means the whole array, i.e. idxs=(:,:,:).
+ *   - fqavby <= 1 / tavby <= 1 disable that axis (fqav returns A, :17).
+ *     fqavby must divide nc (Julia reshape -> DimensionMismatch, :18-19);
+ *     tavby must divide nt (same rule on axis 3).  Both give BLDP_EDIM.
+ *   - "_f32" device entry points take DEVICE pointers and a hipStream_t passed
+ *     as void* (NULL = the null stream).  They are asynchronous on that stream
+ *     and never synchronize; buffers are owned by the caller.
+ *   - Return value 0 = ok, negative = error; bldp_last_error() returns the
+ *     thread-local message of the last failing call.
+ */
+#ifndef BLDP_H
+#define BLDP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BLDP_ABI_VERSION 1
+
+#if defined(BLDP_BUILD)
+#define BLDP_API __attribute__((visibility("default")))
+#else
+#define BLDP_API
+#endif
+
+/* fqavfunc values named by README.md:192-195 */
+enum bldp_op { BLDP_OP_SUM = 0, BLDP_OP_MEAN = 1, BLDP_OP_MAX = 2, BLDP_OP_MIN = 3 };
+
+/* error codes */
+#define BLDP_OK 0
+#define BLDP_EINVAL (-1)  /* bad argument / AssertionError analogue            */
+#define BLDP_EDIM (-2)    /* DimensionMismatch: fqavby/tavby does not divide     */
+#define BLDP_EHIP (-3)    /* HIP runtime error                                   */
+#define BLDP_ENOMEM (-5)  /* device or pinned allocation failed                  */
+#define BLDP_EBOUNDS (-6) /* window outside the array (BoundsError analogue)     */
+
+#define BLDP_MAX_BANKS 64
+
+BLDP_API int bldp_abi_version(void);
+/* Copy the last error message of this thread into buf (NUL-terminated). */
+BLDP_API int bldp_last_error(char *buf, size_t len);
+/* Number of visible GPUs. */
+BLDP_API int bldp_device_count(int *n);
+
+/* Output shape of a reduction: nco = nc/F, nto = nt/T (after the divisibility
+ * checks), ni = window IF count.  Pure host function. */
+BLDP_API int bldp_reduce_shape(int64_t nchan, int64_t nif, int64_t ntime, const int64_t *win,
+                      int64_t fqavby, int64_t tavby, int64_t out_shape[3]);
+
+/* Introspection (tests/bench): the launch plan bldp_reduce_f32 would use for
+ * these pointers.  info = {path (0 vector, 1 narrow, 2 scalar), lanes per
+ * group, waves splitting T, float4 per lane per row, time chunks, workgroups,
+ * workspace bytes, vector output stores}.  Launches nothing. */
+BLDP_API int bldp_reduce_plan_f32(const float *in, int64_t nchan, int64_t nif, int64_t ntime,
+                         const int64_t *win, int64_t fqavby, int64_t tavby, int op,
+                         const float *out, int64_t info[8]);
+
+/* out[c', i, t'] = op over the F x T block of the window (device pointers).
+ * out is dense (nco, ni, nto). */
+BLDP_API int bldp_reduce_f32(const float *in, int64_t nchan, int64_t nif, int64_t ntime,
+                    const int64_t *win, int64_t fqavby, int64_t tavby, int op, float *out,
+                    void *stream);
+
+/* Same with an explicit output layout: element (c', i, t') is written at
+ * out[c' + out_ld_i * i + out_ld_t * t'] (lets a bank write straight into
+ * its slot of a stitched band product). */
+BLDP_API int bldp_reduce_strided_f32(const float *in, int64_t nchan, int64_t nif, int64_t ntime,
+                            const int64_t *win, int64_t fqavby, int64_t tavby, int op,
+                            float *out, int64_t out_ld_i, int64_t out_ld_t, void *stream);
+
+/* Host-pointer form: in and out are host memory; the window is streamed to
+ * device `dev` through double-buffered staging and reduced there.
+ * Synchronous (returns when out is filled). */
+BLDP_API int bldp_reduce_host_f32(int dev, const float *in, int64_t nchan, int64_t nif, int64_t ntime,
+                         const int64_t *win, int64_t fqavby, int64_t tavby, int op, float *out);
+
+/* Band of nbank banks on ONE device, all with the same (nchan, nif, ntime)
+ * and window: reduces every bank and writes the stitched product
+ * out (nbank*nco, ni, nto) in bank order, i.e. reduce(vcat, ...) of the
+ * per-bank results (src/gbt.jl:103).  in[] is a HOST array of device
+ * pointers.  One launch covers every bank. */
+BLDP_API int bldp_band_reduce_f32(int nbank, const float *const *in, int64_t nchan, int64_t nif,
+                         int64_t ntime, const int64_t *win, int64_t fqavby, int64_t tavby,
+                         int op, float *out, void *stream);
+
+/* gathered: nbank dense blocks (nc, nif, ntime) back to back (bank-major,
+ * what a gather to the root leaves); out: (nbank*nc, nif, ntime) = vcat. */
+BLDP_API int bldp_stitch_f32(int nbank, const float *gathered, int64_t nc, int64_t nif, int64_t ntime,
+                    float *out, void *stream);
+
+/* In place on data (nchan, nif, ntime): for every coarse channel the DC bin
+ * (0-based nfpc/2) takes the value of its left neighbour. nfpc >= 2. */
+BLDP_API int bldp_despike_f32(float *data, int64_t nchan, int64_t nif, int64_t ntime, int64_t nfpc,
+                     void *stream);
+
+/* Excess kurtosis over time of every (channel, if) row of the window.
+ * out is (nc, ni) float64 on the device. workspace: device scratch of
+ * bldp_kurtosis_workspace_size() bytes, or NULL for a library-cached one. */
+BLDP_API size_t bldp_kurtosis_workspace_size(int64_t nchan, int64_t nif, int64_t ntime, const int64_t *win);
+BLDP_API int bldp_kurtosis_f32(const float *in, int64_t nchan, int64_t nif, int64_t ntime,
+                      const int64_t *win, double *out, void *workspace, void *stream);
+
+/* fqav(r::AbstractRange, n): first/step/length of the averaged axis. */
+BLDP_API int bldp_fqav_range(double first, double step, int64_t len, int64_t n, double *out_first,
+                    double *out_step, int64_t *out_len);
+
+/* Synthetic BL-like filterbank (nchan, nif, ntime) on the device:
+ * kind 0 = gamma(2, 5e8) x bandpass scallop x DC spike (nfpc bins per coarse
+ * channel); kind 1 = integer-valued 0..255 (order-independent exact sums). */
+BLDP_API int bldp_synth_f32(float *out, int64_t nchan, int64_t nif, int64_t ntime, int64_t nfpc,
+                   uint64_t seed, int kind, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BLDP_H */

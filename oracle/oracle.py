@@ -1,0 +1,302 @@
+"""TEST INFRASTRUCTURE ONLY — the parity oracle for libbldp_hip.
+
+Two independent CPU restatements of the reference's worker-side reduction
+(BLDistributedDataProducts.jl v0.3.2, src/gbtworkerfunctions.jl):
+
+* ``C``: ctypes binding to ``oracle/liboracle.so`` (bldp_oracle.c), the
+  authoritative checker and the ``cpu_baseline`` of bench.py;
+* ``np_*``: a NumPy restatement written directly from the Julia source, used
+  to cross-check the C restatement and to generate tests/golden fixtures.
+
+Only tests/, ``__graft_entry__.smoke()`` and bench.py's cpu_baseline leg may
+import this module.  The product path never does.
+
+Parity status: pinned against the reference's own
+known-answer tests only for ``fqav(::AbstractRange, n)`` (test/runtests.jl:5-6).
+The array reductions are *parity unpinned* — Julia is absent here and the
+reference ships no array fixtures — and are held instead to (a) agreement of
+the two restatements, (b) integer-valued fixtures whose float32 sums are exact
+in every summation order.
+
+Array convention: Julia order.  A filterbank is a numpy array of logical shape
+(nchan, nif, ntime), Fortran-contiguous (channel fastest), exactly the bytes
+HDF5.jl / Blio hand to WorkerFunctions.getdata (README.md:165-168).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+OPS = {"sum": 0, "mean": 1, "max": 2, "min": 3}
+
+
+class DimensionMismatch(ValueError):
+    """Julia's DimensionMismatch (fqav reshape, src/gbtworkerfunctions.jl:18)."""
+
+
+class BoundsErr(IndexError):
+    """Julia's BoundsError (window outside the array)."""
+
+
+# --------------------------------------------------------------------------
+# C restatement (ctypes)
+# --------------------------------------------------------------------------
+_lib = None
+
+
+def build() -> str:
+    """Compile liboracle.so with the committed Makefile (gcc)."""
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        P, I64, I = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+        L.oracle_reduce.argtypes = [P, I64, I64, I64, P, I64, I64, I, P]
+        L.oracle_reduce.restype = I
+        L.oracle_kurtosis.argtypes = [P, I64, I64, I64, P, P]
+        L.oracle_kurtosis.restype = I
+        L.oracle_stitch.argtypes = [I, P, I64, I64, I64, P]
+        L.oracle_stitch.restype = I
+        L.oracle_despike.argtypes = [P, I64, I64, I64, I64]
+        L.oracle_despike.restype = I
+        D = ctypes.c_double
+        L.oracle_fqav_range.argtypes = [D, D, I64, I64, P, P, P]
+        L.oracle_fqav_range.restype = None
+        L.oracle_synth.argtypes = [P, I64, I64, I64, I64, ctypes.c_uint64, I]
+        L.oracle_synth.restype = None
+        L.oracle_reduce_banks_mt.argtypes = [I, P, I64, I64, I64, I64, I64, I, P]
+        L.oracle_reduce_banks_mt.restype = I
+        _lib = L
+    return _lib
+
+
+def _fa(a: np.ndarray) -> np.ndarray:
+    a = np.asarray(a, dtype=np.float32)
+    if a.ndim != 3:
+        raise ValueError("filterbank arrays are 3-D (nchan, nif, ntime)")
+    return np.asfortranarray(a)
+
+
+def _win(win):
+    if win is None:
+        return None, None
+    w = (ctypes.c_int64 * 9)(*[int(x) for x in win])
+    return w, ctypes.cast(w, ctypes.c_void_p)
+
+
+def _check(rc: int, what: str):
+    if rc == -2:
+        raise DimensionMismatch(what)
+    if rc == -6:
+        raise BoundsErr(what)
+    if rc != 0:
+        raise ValueError(f"{what}: oracle error {rc}")
+
+
+def window_shape(shape, win):
+    if win is None:
+        return tuple(shape)
+    return (int(win[1]), int(win[4]), int(win[7]))
+
+
+def reduce(a, fqavby=1, tavby=1, op="sum", win=None) -> np.ndarray:
+    """C restatement of fqav on axis 1 fused with fqav on axis 3."""
+    a = _fa(a)
+    nc, ni, nt = window_shape(a.shape, win)
+    F, T = max(int(fqavby), 1), max(int(tavby), 1)
+    if nc % F or nt % T:
+        raise DimensionMismatch(f"fqavby={F} / tavby={T} vs window {nc}x{nt}")
+    out = np.empty((nc // F, ni, nt // T), dtype=np.float32, order="F")
+    keep, wp = _win(win)
+    rc = lib().oracle_reduce(a.ctypes.data, a.shape[0], a.shape[1], a.shape[2], wp, F, T,
+                             OPS[op], out.ctypes.data)
+    _check(rc, "oracle_reduce")
+    return out
+
+
+def kurtosis(a, win=None) -> np.ndarray:
+    a = _fa(a)
+    nc, ni, nt = window_shape(a.shape, win)
+    out = np.empty((nc, ni), dtype=np.float64, order="F")
+    keep, wp = _win(win)
+    rc = lib().oracle_kurtosis(a.ctypes.data, a.shape[0], a.shape[1], a.shape[2], wp,
+                               out.ctypes.data)
+    _check(rc, "oracle_kurtosis")
+    return out
+
+
+def stitch(banks) -> np.ndarray:
+    banks = [_fa(b) for b in banks]
+    nc, ni, nt = banks[0].shape
+    ptrs = (ctypes.c_void_p * len(banks))(*[b.ctypes.data for b in banks])
+    out = np.empty((nc * len(banks), ni, nt), dtype=np.float32, order="F")
+    rc = lib().oracle_stitch(len(banks), ctypes.cast(ptrs, ctypes.c_void_p), nc, ni, nt,
+                             out.ctypes.data)
+    _check(rc, "oracle_stitch")
+    return out
+
+
+def despike(d, nfpc) -> np.ndarray:
+    d = _fa(d).copy(order="F")
+    rc = lib().oracle_despike(d.ctypes.data, d.shape[0], d.shape[1], d.shape[2], int(nfpc))
+    _check(rc, "oracle_despike")
+    return d
+
+
+def fqav_range(first, step, length, n):
+    f, s, l = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
+    lib().oracle_fqav_range(float(first), float(step), int(length), int(n), ctypes.byref(f),
+                            ctypes.byref(s), ctypes.byref(l))
+    return f.value, s.value, l.value
+
+
+def synth(nchan, nif, ntime, nfpc, seed, kind=0) -> np.ndarray:
+    out = np.empty((nchan, nif, ntime), dtype=np.float32, order="F")
+    lib().oracle_synth(out.ctypes.data, nchan, nif, ntime, nfpc, seed, kind)
+    return out
+
+
+def reduce_banks_mt(banks, fqavby, tavby, op="sum"):
+    """CPU baseline: one thread per bank (one Distributed worker per bank)."""
+    banks = [_fa(b) for b in banks]
+    nchan, nif, ntime = banks[0].shape
+    F, T = max(int(fqavby), 1), max(int(tavby), 1)
+    outs = [np.empty((nchan // F, nif, ntime // T), np.float32, order="F") for _ in banks]
+    ip = (ctypes.c_void_p * len(banks))(*[b.ctypes.data for b in banks])
+    op_ = (ctypes.c_void_p * len(banks))(*[o.ctypes.data for o in outs])
+    rc = lib().oracle_reduce_banks_mt(len(banks), ctypes.cast(ip, ctypes.c_void_p), nchan, nif,
+                                      ntime, F, T, OPS[op], ctypes.cast(op_, ctypes.c_void_p))
+    _check(rc, "oracle_reduce_banks_mt")
+    return outs
+
+
+# --------------------------------------------------------------------------
+# NumPy restatement (independent of the C code)
+# --------------------------------------------------------------------------
+def np_window(a: np.ndarray, win) -> np.ndarray:
+    """h5["data"][idxs...] with idxs given as 9 ints (0-based start, count, step)."""
+    if win is None:
+        return a
+    ax = [win[3 * k] + win[3 * k + 2] * np.arange(win[3 * k + 1]) for k in range(3)]
+    for k in range(3):
+        if len(ax[k]) and (ax[k].min() < 0 or ax[k].max() >= a.shape[k]):
+            raise BoundsErr(f"axis {k + 1}")
+    return np.asfortranarray(a[np.ix_(*ax)])
+
+
+def _fix_zero(m, R, axis, op):
+    """numpy's max/min keep whichever signed zero came first; Julia orders
+    -0.0 < +0.0.  Repair the all-zero-extremum groups."""
+    zero = m == 0
+    if not zero.any():
+        return m
+    if op == "max":
+        pos = np.any((R == 0) & ~np.signbit(R), axis=axis)
+        return np.where(zero, np.where(pos, np.float32(0.0), np.float32(-0.0)), m)
+    neg = np.any((R == 0) & np.signbit(R), axis=axis)
+    return np.where(zero, np.where(neg, np.float32(-0.0), np.float32(0.0)), m)
+
+
+def np_fqav(a: np.ndarray, n: int, f: str = "sum") -> np.ndarray:
+    """fqav(A, n; f) (src/gbtworkerfunctions.jl:16-20) on the first axis."""
+    if n <= 1:  # :17 — returns A itself
+        return a
+    if a.shape[0] % n:  # :18 reshape -> DimensionMismatch
+        raise DimensionMismatch(f"fqavby={n} does not divide {a.shape[0]}")
+    R = a.reshape((n, a.shape[0] // n) + a.shape[1:], order="F")  # :18 (column-major)
+    if f in ("sum", "mean"):  # :19 f(...; dims=1), Float64 accumulation here
+        s = R.astype(np.float64).sum(axis=0)
+        if f == "mean":
+            s = s / n
+        return np.asfortranarray((s + 0.0).astype(np.float32))
+    m = R.max(axis=0) if f == "max" else R.min(axis=0)
+    return np.asfortranarray(_fix_zero(m, R, 0, f))
+
+
+def np_tavby(a: np.ndarray, n: int, f: str = "sum") -> np.ndarray:
+    """Time integration: fqav applied to axis 3,
+    permutedims(fqav(permutedims(A, (3,2,1)), n), (3,2,1))."""
+    if n <= 1:
+        return a
+    return np.asfortranarray(np.transpose(np_fqav(np.transpose(a, (2, 1, 0)), n, f), (2, 1, 0)))
+
+
+def np_reduce(a, fqavby=1, tavby=1, op="sum", win=None) -> np.ndarray:
+    """Channel decimation then time integration, float64 throughout for
+    sum/mean (the composition is computed in float64 before rounding)."""
+    w = np_window(np.asarray(a, dtype=np.float32), win)
+    if op in ("sum", "mean"):
+        w64 = w.astype(np.float64)
+        F, T = max(int(fqavby), 1), max(int(tavby), 1)
+        if w64.shape[0] % F or w64.shape[2] % T:
+            raise DimensionMismatch("factor does not divide window")
+        R = w64.reshape((F, w64.shape[0] // F, w64.shape[1], T, w64.shape[2] // T), order="F")
+        s = R.sum(axis=(0, 3))
+        if op == "mean":
+            s = s / (F * T)
+        return np.asfortranarray((s + 0.0).astype(np.float32))
+    return np_tavby(np_fqav(w, int(fqavby), op), int(tavby), op)
+
+
+def np_kurtosis(a, win=None) -> np.ndarray:
+    """getkurtosis (src/gbtworkerfunctions.jl:197-202), StatsBase recipe."""
+    w = np_window(np.asarray(a, dtype=np.float32), win)
+    nc, ni, nt = w.shape
+    rows = w.reshape((nc * ni, nt), order="F")  # :199-200
+    m = (rows.astype(np.float64).sum(axis=1).astype(np.float32) / np.float32(nt))[:, None]
+    z = (rows - m).astype(np.float32)
+    z2 = (z * z).astype(np.float32)
+    cm2 = z2.astype(np.float64).sum(axis=1) / nt
+    cm4 = (z2 * z2).astype(np.float64).sum(axis=1) / nt
+    with np.errstate(divide="ignore", invalid="ignore"):
+        k = cm4 / (cm2 * cm2) - 3.0
+    return np.asfortranarray(k.reshape((nc, ni), order="F"))  # :201
+
+
+def np_stitch(banks) -> np.ndarray:
+    """reduce(vcat, banks) (src/gbt.jl:103)."""
+    return np.asfortranarray(np.concatenate([np.asarray(b) for b in banks], axis=0))
+
+
+def np_despike(d, nfpc) -> np.ndarray:
+    """d[spike:nfpc:end,:,:] .= d[spike-1:nfpc:end,:,:] (src/gbt.jl:101-102,111)."""
+    d = np.array(d, dtype=np.float32, order="F", copy=True)
+    spike = nfpc // 2 + 1
+    if spike - 1 < 1:
+        raise BoundsErr("spike-1 == 0")
+    dst = np.arange(spike - 1, d.shape[0], nfpc)
+    src = np.arange(spike - 2, d.shape[0], nfpc)
+    if len(dst) != len(src):
+        raise DimensionMismatch("spike/source lengths differ")
+    d[dst] = d[src]
+    return d
+
+
+def np_fqav_range(first, step, length, n):
+    """fqav(r::AbstractRange, n) (src/gbtworkerfunctions.jl:27-33)."""
+    if n <= 1:
+        return float(first), float(step), int(length)
+    return first + (n - 1) * step / 2, float(n * step), length // n
+
+
+def gamma_bandpass(nchan, nif, ntime, nfpc, seed):
+    """NumPy synthetic BL-like power: gamma(2, 5e8) x per-coarse-channel
+    scallop x DC spike at bin nfpc/2."""
+    rng = np.random.default_rng(seed)
+    g = rng.gamma(2.0, 5e8, size=(ntime, nif, nchan)).astype(np.float32)
+    x = np.arange(nchan) % nfpc
+    bp = (0.2 + 0.8 * np.sin(np.pi * (x + 0.5) / nfpc) ** 2).astype(np.float32)
+    bp[x == nfpc // 2] *= 10.0
+    return np.asfortranarray(np.transpose(g * bp, (2, 1, 0)))

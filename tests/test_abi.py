@@ -1,0 +1,135 @@
+"""CPU: the C-ABI library loads, exports every symbol include/bldp.h declares,
+and its host-only entry points (shape, plan, range, argument checks) behave
+like the reference without a GPU."""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+
+def declared_symbols():
+    src = open(os.path.join(REPO, "include", "bldp.h")).read()
+    return sorted(set(re.findall(r"BLDP_API\s+\w+\s+(bldp_\w+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def L(pkg):
+    return pkg._lib.lib()
+
+
+def test_header_and_binding_agree(pkg):
+    decl = declared_symbols()
+    assert len(decl) >= 15
+    assert sorted(pkg._lib.SIGNATURES) == decl
+
+
+def test_library_exports_every_declared_symbol(pkg, L):
+    out = subprocess.run(["nm", "-D", "--defined-only", pkg._lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r" T (bldp_\w+)", out))
+    missing = set(declared_symbols()) - exported
+    assert not missing, missing
+    for s in declared_symbols():
+        assert getattr(L, s) is not None
+    assert L.bldp_abi_version() == 1
+
+
+def test_library_is_gfx950_code(pkg):
+    blob = open(pkg._lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_no_gpu_error_path(pkg, L):
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    n = ctypes.c_int(-1)
+    rc = L.bldp_device_count(ctypes.byref(n))
+    assert rc == pkg._lib.BLDP_EHIP
+    assert "device" in pkg._lib.last_error().lower()
+
+
+def test_reduce_shape_and_errors(pkg, L):
+    sh = (ctypes.c_int64 * 3)()
+    assert L.bldp_reduce_shape(65536, 1, 279, None, 64, 1, sh) == 0
+    assert list(sh) == [1024, 1, 279]
+    keep, wp = pkg._lib.win_arg([0, 65536, 1, 0, 1, 1, 0, 272, 1])  # idxs=(:, :, 1:272)
+    assert L.bldp_reduce_shape(65536, 1, 279, wp, 64, 16, sh) == 0
+    assert list(sh) == [1024, 1, 17]
+    assert L.bldp_reduce_shape(65536, 1, 279, None, 64, 16, sh) == pkg._lib.BLDP_EDIM
+    assert "tavby=16" in pkg._lib.last_error()
+    assert L.bldp_reduce_shape(100, 1, 10, None, 3, 1, sh) == pkg._lib.BLDP_EDIM
+    assert "DimensionMismatch" in pkg._lib.last_error()
+    keep, wp = pkg._lib.win_arg([90, 20, 1, 0, 1, 1, 0, 10, 1])
+    assert L.bldp_reduce_shape(100, 1, 10, wp, 1, 1, sh) == pkg._lib.BLDP_EBOUNDS
+    keep, wp = pkg._lib.win_arg([0, 10, 0, 0, 1, 1, 0, 10, 1])
+    assert L.bldp_reduce_shape(100, 1, 10, wp, 1, 1, sh) == pkg._lib.BLDP_EINVAL
+    # n <= 1 disables an axis (fqav returns A, src/gbtworkerfunctions.jl:17)
+    assert L.bldp_reduce_shape(7, 3, 5, None, 0, -2, sh) == 0 and list(sh) == [7, 3, 5]
+
+
+def test_fqav_range_kats_through_abi(L):
+    f, s, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
+    assert L.bldp_fqav_range(1.0, 1.0, 4, 4, ctypes.byref(f), ctypes.byref(s), ctypes.byref(n)) == 0
+    assert (f.value, s.value, n.value) == (2.5, 4.0, 1)  # test/runtests.jl:5
+    assert L.bldp_fqav_range(1.0, 2.0, 8, 4, ctypes.byref(f), ctypes.byref(s), ctypes.byref(n)) == 0
+    assert (f.value, s.value, n.value) == (4.0, 8.0, 2)  # test/runtests.jl:6
+
+
+def plan(pkg, L, ptr, nchan, nif, ntime, F, T, win=None):
+    info = (ctypes.c_int64 * 8)()
+    keep, wp = pkg._lib.win_arg(win)
+    rc = L.bldp_reduce_plan_f32(ptr, nchan, nif, ntime, wp, F, T, 0, None, info)
+    assert rc == 0, pkg._lib.last_error()
+    return list(info)
+
+
+def test_launch_plans_host_only(pkg, L):
+    A = 1 << 20  # any 16-byte aligned address
+    # cfg3 bank: vector path, one wave per group (64 lanes x 4 float4 per row)
+    p = plan(pkg, L, A, 1 << 26, 1, 16, 1024, 16)
+    assert p[0] == 0 and p[1] == 64 and p[3] == 4 and p[4] == 1
+    assert p[5] == 65536 // 4
+    # cfg1: F=64 -> 16 lanes per group
+    p = plan(pkg, L, A, 65536, 1, 279, 64, 16, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
+    assert p[0] == 0 and p[1] == 16 and p[3] == 1
+    # cfg4: narrow channel, long time -> time split waves and/or chunks
+    p = plan(pkg, L, A, 512, 1, 879616, 8, 1024)
+    assert p[0] == 0 and p[1] == 2 and (p[2] > 1 or p[4] > 1)
+    # F=1 time-only: narrow path; odd F: scalar path; misaligned pointer: scalar
+    assert plan(pkg, L, A, 4096, 1, 16, 1, 16)[0] == 1
+    assert plan(pkg, L, A, 4095, 1, 16, 3, 1)[0] == 2
+    assert plan(pkg, L, A + 4, 4096, 1, 16, 64, 1)[0] == 2
+    # one long time block with few outputs -> chunked across workgroups
+    p = plan(pkg, L, A, 64, 1, 100000, 8, 100000)
+    assert p[4] > 1 and p[6] > 0
+
+
+def test_null_pointer_rejected(pkg, L):
+    assert L.bldp_reduce_f32(None, 64, 1, 4, None, 4, 1, 0, None, None) == pkg._lib.BLDP_EINVAL
+    assert L.bldp_reduce_f32(None, 64, 1, 4, None, 4, 1, 9, None, None) == pkg._lib.BLDP_EINVAL
+    assert "op" in pkg._lib.last_error()
+
+
+def test_empty_calls_are_noops(pkg, L):
+    assert L.bldp_reduce_f32(None, 64, 1, 0, None, 4, 1, 0, None, None) == 0
+    assert L.bldp_despike_f32(None, 0, 1, 1, 16, None) == 0
+    sz = L.bldp_kurtosis_workspace_size(512, 1, 880000, None)
+    assert sz > 512 * 8
+
+
+def test_despike_and_stitch_argument_checks(pkg, L):
+    assert L.bldp_despike_f32(None, 10, 1, 1, 4, None) == pkg._lib.BLDP_EDIM
+    assert L.bldp_despike_f32(None, 10, 1, 1, 1, None) == pkg._lib.BLDP_EBOUNDS
+    assert L.bldp_stitch_f32(0, None, 4, 1, 1, None, None) == pkg._lib.BLDP_EINVAL
+    buf = np.zeros(16, np.float32)
+    assert L.bldp_stitch_f32(2, buf.ctypes.data, 4, 2, 1, buf.ctypes.data, None) == \
+        pkg._lib.BLDP_EINVAL

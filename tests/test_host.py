@@ -1,0 +1,167 @@
+"""CPU: host-side logic — Julia index handling (sanitizeidxs, ranges), the
+SIGPROC reader, the inventory walk, the GBT fan-out shape, and the sharded
+band exchange (world_size 2, gloo)."""
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+
+
+def test_sanitizeidxs_and_window(pkg):
+    J, C = pkg.JRange, pkg.COLON
+    # Integers become i:i so results stay 3-D (src/gbtworkerfunctions.jl:167-169)
+    assert pkg.sanitizeidxs((C, 2, J(5, 10))) == (C, J(2, 2), J(5, 10))
+    to_window = pkg.idxs.to_window
+    assert to_window((C, C, C), (10, 2, 7)) is None
+    assert to_window((J(3, 8), 1, C), (10, 2, 7)) == [2, 6, 1, 0, 1, 1, 0, 7, 1]
+    assert to_window((J(9, -2, 1), C, J(1, 3, 7)), (10, 2, 7)) == [8, 5, -2, 0, 2, 1, 0, 3, 3]
+    assert len(J(1, 2, 15)) == 8 and len(J(5, 4)) == 0 and list(J(1, 3, 7)) == [1, 4, 7]
+    with pytest.raises(AssertionError):
+        to_window((C, C), (1, 1, 1))  # @assert length(idxs) == 3
+    with pytest.raises(TypeError):
+        to_window((range(3), C, C), (10, 1, 1))
+
+
+def test_fqav_range_mirror(pkg):
+    # GBT.fqav(1:4, 4) === 2.5:4.0:2.5 ; GBT.fqav(1:2:15, 4) === 4.0:8.0:12.0
+    r = pkg.GBT.fqav(pkg.JRange(1, 4), 4)
+    assert (r.first, r.step, len(r), r.last) == (2.5, 4.0, 1, 2.5)
+    r = pkg.GBT.fqav(pkg.JRange(1, 2, 15), 4)
+    assert (r.first, r.step, len(r), r.last) == (4.0, 8.0, 2, 12.0)
+    rr = pkg.JRange(1, 9)
+    assert pkg.fqav(rr, 1) is rr
+
+
+def test_fqav_passthrough_and_generic_host(pkg):
+    a = np.arange(24, dtype=np.float32).reshape((4, 2, 3), order="F")
+    assert pkg.fqav(a, 1) is a  # n <= 1 returns A itself (:17)
+    med = pkg.fqav(a, 2, np.median)  # any f(X; dims) runs as the reference does
+    np.testing.assert_array_equal(med, np.median(a.reshape((2, 2, 2, 3), order="F"), axis=0))
+    with pytest.raises(pkg.DimensionMismatch):
+        pkg.fqav(a, 3, np.median)
+
+
+def test_sigproc_roundtrip_and_header(pkg, tmp_path):
+    rd = pkg.readers
+    data = np.asfortranarray(np.random.default_rng(0).random((64, 2, 5)).astype(np.float32))
+    hdr = dict(telescope_id=6, machine_id=10, data_type=1, source_name="VOYAGER1",
+               tstart=59000.5, tsamp=18.253611, fch1=8438.96484375, foff=-2.7939677238464355e-06,
+               nchans=64, nifs=2, nbits=32)
+    f = tmp_path / "guppi_59000_00001_VOYAGER1_0001.rawspec.0000.fil"
+    rd.write_fil(f, hdr, data)
+    assert not rd.ishdf5(f)
+    h, mm = rd.fil_mmap(f)
+    assert h["nsamps"] == 5 and mm.shape == (64, 2, 5)
+    np.testing.assert_array_equal(np.asarray(mm), data)
+    gh = rd.getfbheader(f)
+    assert gh["nfpc"] == 1048576  # round(Int32, 187.5/64/abs(foff)) (:134)
+    assert "header_size" not in gh and "sample_size" not in gh
+
+
+def test_ishdf5_signature(pkg, tmp_path):
+    p = tmp_path / "x.h5"
+    p.write_bytes(b"\x89HDF\r\n\x1a\n" + b"\0" * 100)
+    assert pkg.readers.ishdf5(p)
+    q = tmp_path / "y.h5"
+    q.write_bytes(b"\0" * 512 + b"\x89HDF\r\n\x1a\n" + b"\0" * 100)
+    assert pkg.readers.ishdf5(q)
+
+
+def test_inventory_walk(pkg, tmp_path):
+    root = tmp_path / "datax"
+    good = root / "AGBT22B_999_01" / "GUPPI" / "BLP42"
+    good.mkdir(parents=True)
+    (good / "blc42_guppi_59000_12345_HIP1234_0011.rawspec.0002.h5").write_bytes(b"")
+    (good / "blc42_guppi_59000_12345_HIP1234_0011.rawspec.0000.h5").write_bytes(b"")
+    (good / "junk.0002.h5").write_bytes(b"")  # does not match the guppi regex -> warn
+    (root / "AGBT22B_999_01" / "GUPPI" / "XYZ").mkdir()  # player regex filters it out
+    (root / "notasession").mkdir()
+    warns = []
+    inv = pkg.readers.getinventory(root=str(root), worker=3, warn=warns.append)
+    assert len(inv) == 1 and len(warns) == 1
+    e = inv[0]
+    assert (e["imjd"], e["smjd"], e["session"], e["scan"], e["src_name"], e["band"], e["bank"],
+            e["worker"]) == (59000, 12345, "AGBT22B_999_01", "0011", "HIP1234", 4, 2, 3)
+    assert e["host"] == socket.gethostname() and e["file"].endswith("0002.h5")
+    assert tuple(e) == pkg.readers.INVENTORY_FIELDS
+    assert pkg.readers.getinventory(root=str(tmp_path / "missing")) == []
+    invs = pkg.GBT.getinventories([1, 2], root=str(root))
+    assert [len(i) for i in invs] == [1, 1] and invs[1][0]["worker"] == 2
+
+
+def test_datahosts(pkg):
+    h = pkg.GBT.datahosts()
+    assert len(h) == 64 and h[0] == "blc00" and h[-1] == "blc77"
+    assert pkg.GBT.datahosts("x")[9] == "xblc11"
+
+
+def test_getdata_size_assert(pkg):
+    with pytest.raises(AssertionError):
+        pkg.GBT.getdata([0, 1], ["a"])
+
+
+def test_banks_for_rank(pkg):
+    b = pkg.band.banks_for_rank
+    assert [list(b(8, r, 4)) for r in range(4)] == [[0, 1], [2, 3], [4, 5], [6, 7]]
+    assert list(b(8, 0, 1)) == list(range(8))
+    with pytest.raises(ValueError):
+        b(8, 0, 3)
+
+
+def _band_worker(rank, world, port, F, T, ni, nt, q):
+    import sys
+
+    import torch
+    import torch.distributed as dist
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import __graft_entry__ as entry
+
+    pkg, orc = entry.load_package(), entry.load_oracle()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(42)
+    banks = [np.asfortranarray(rng.integers(0, 256, (256, ni, nt)).astype(np.float32))
+             for _ in range(8)]
+    mine = [banks[b] for b in pkg.band.banks_for_rank(8, rank, world)]
+
+    def to_t(a):  # Julia-order CPU tensor with channel-fastest strides
+        return torch.from_numpy(np.ascontiguousarray(a.transpose(2, 1, 0))).permute(2, 1, 0)
+
+    def reduce_fn(bs, F_, T_, op, win):  # CPU stand-in for engine.band_reduce
+        return to_t(orc.stitch([orc.reduce(b, F_, T_, op, win) for b in bs]))
+
+    def stitch_fn(g, n):  # CPU stand-in for engine.stitch: [n, nto, ni, nc] -> vcat
+        parts = [np.asfortranarray(g[k].numpy().transpose(2, 1, 0)) for k in range(n)]
+        return to_t(orc.stitch(parts))
+
+    res = pkg.band.band_reduce_dist(mine, F, T, "sum", None, reduce_fn=reduce_fn,
+                                    stitch_fn=stitch_fn)
+    if rank == 0:
+        want = orc.stitch([orc.reduce(b, F, T) for b in banks])
+        got = res.permute(2, 1, 0).contiguous().numpy().transpose(2, 1, 0)
+        q.put(bool(np.array_equal(got, want)) and got.shape == want.shape)
+    else:
+        q.put(res is None)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("F,T,ni,nt", [(16, 4, 2, 8), (256, 8, 1, 8)])
+def test_band_exchange_gloo_world2(F, T, ni, nt):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + (os.getpid() % 1000) + F
+    procs = [ctx.Process(target=_band_worker, args=(r, 2, port, F, T, ni, nt, q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=180)
+    results = [q.get(timeout=5) for _ in procs]
+    assert all(p.exitcode == 0 for p in procs)
+    assert all(results)

@@ -1,0 +1,127 @@
+"""CPU: pin the oracle.  The reference's own KATs (test/runtests.jl:5-6), the
+committed golden fixtures, and agreement of the C and NumPy restatements."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from conftest import same_bits
+
+
+def test_reference_range_kats(orc, golden):
+    # GBT.fqav(1:4, 4) === 2.5:4.0:2.5 ; GBT.fqav(1:2:15, 4) === 4.0:8.0:12.0
+    assert orc.fqav_range(1, 1, 4, 4) == (2.5, 4.0, 1)
+    assert orc.fqav_range(1, 2, 8, 4) == (4.0, 8.0, 2)
+    for k in golden.manifest["kat_range"]:
+        assert list(orc.fqav_range(k["first"], k["step"], k["length"], k["n"])) == k["expect"]
+        assert list(orc.np_fqav_range(k["first"], k["step"], k["length"], k["n"])) == k["expect"]
+
+
+def test_range_passthrough_and_floor(orc):
+    assert orc.fqav_range(10.0, 0.5, 7, 1) == (10.0, 0.5, 7)  # n <= 1 returns r (:28)
+    assert orc.fqav_range(10.0, 0.5, 7, 0) == (10.0, 0.5, 7)
+    f, s, n = orc.fqav_range(0.0, 1.0, 10, 4)  # length ÷ n floors (:31)
+    assert (f, s, n) == (1.5, 4.0, 2)
+
+
+@pytest.mark.parametrize("kind", ["reduce"])
+def test_c_oracle_matches_golden(orc, golden, kind):
+    for c in golden.cases(kind):
+        a = golden.input(c["input"])
+        got = orc.reduce(a, c["fqavby"], c["tavby"], c["op"], c["win"])
+        want = golden.output(c)
+        if c["exact"]:
+            assert same_bits(got, want), c
+        else:
+            np.testing.assert_allclose(got, want, rtol=1e-6, err_msg=str(c))
+
+
+def test_kurtosis_golden(orc, golden):
+    for c in golden.cases("kurtosis"):
+        got = orc.kurtosis(golden.input(c["input"]), c["win"])
+        want = golden.output(c)
+        assert np.array_equal(np.isnan(got), np.isnan(want))
+        np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-5)
+    full = golden.output(golden.cases("kurtosis")[0])
+    assert np.isnan(full[5, 1])  # constant row -> NaN
+
+
+def test_stitch_band_despike_golden(orc, golden):
+    st = golden.cases("stitch")[0]
+    banks = [golden.input(n) for n in st["input"]]
+    assert same_bits(orc.stitch(banks), golden.output(st))
+    bd = golden.cases("band")[0]
+    got = orc.stitch([orc.reduce(b, bd["fqavby"], bd["tavby"], bd["op"]) for b in banks])
+    assert same_bits(got, golden.output(bd))
+    ds = golden.cases("despike")[0]
+    a = golden.input(ds["input"])[:, :, : ds["ntime"]]
+    assert same_bits(orc.despike(a, ds["nfpc"]), golden.output(ds))
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_c_and_numpy_restatements_agree(orc, seed):
+    rng = np.random.default_rng(seed)
+    nc = int(rng.choice([12, 48, 96, 256]))
+    ni, nt = int(rng.integers(1, 4)), int(rng.integers(1, 40))
+    a = np.asfortranarray(rng.gamma(2.0, 1e3, (nc, ni, nt)).astype(np.float32))
+    Fs = [f for f in (1, 2, 3, 4, 6, 12) if nc % f == 0]
+    Ts = [t for t in (1, 2, 3, 5) if nt % t == 0]
+    for op in ("sum", "mean", "max", "min"):
+        F, T = int(rng.choice(Fs)), int(rng.choice(Ts))
+        c, n = orc.reduce(a, F, T, op), orc.np_reduce(a, F, T, op)
+        if op in ("max", "min"):
+            assert same_bits(c, n)
+        else:
+            np.testing.assert_allclose(c, n, rtol=1e-6)
+    np.testing.assert_allclose(orc.kurtosis(a), orc.np_kurtosis(a), rtol=1e-4, atol=1e-5)
+
+
+def test_errors(orc):
+    a = np.zeros((12, 1, 6), np.float32, order="F")
+    with pytest.raises(orc.DimensionMismatch):  # reshape in fqav (:18-19)
+        orc.reduce(a, 5, 1)
+    with pytest.raises(orc.DimensionMismatch):
+        orc.reduce(a, 1, 4)
+    with pytest.raises(orc.BoundsErr):
+        orc.reduce(a, 1, 1, "sum", [10, 4, 1, 0, 1, 1, 0, 6, 1])
+    with pytest.raises(orc.DimensionMismatch):  # spike/source lengths differ
+        orc.despike(np.zeros((10, 1, 1), np.float32), 4)
+    with pytest.raises(orc.BoundsErr):
+        orc.despike(np.zeros((10, 1, 1), np.float32), 1)
+
+
+def test_empty_and_passthrough(orc):
+    a = np.zeros((8, 2, 0), np.float32, order="F")
+    assert orc.reduce(a, 4, 1).shape == (2, 2, 0)
+    b = np.arange(24, dtype=np.float32).reshape((4, 2, 3), order="F")
+    assert same_bits(orc.reduce(b, 1, 1), b)  # n <= 1 returns the data unchanged
+    assert same_bits(orc.reduce(b, 0, -3), b)
+
+
+def test_julia_zero_and_nan_semantics(orc):
+    a = np.array([-0.0, -0.0, -0.0, 0.0, 1.0, np.nan], np.float32).reshape((6, 1, 1), order="F")
+    s = orc.reduce(a[:2], 2, 1, "sum")
+    assert s[0, 0, 0] == 0 and not np.signbit(s[0, 0, 0])  # reducedim init +0.0
+    pair = np.asfortranarray(a[2:4])  # (-0.0, +0.0): Julia orders -0.0 < +0.0
+    assert not np.signbit(orc.reduce(pair, 2, 1, "max")[0, 0, 0])
+    assert np.signbit(orc.reduce(pair, 2, 1, "min")[0, 0, 0])
+    assert np.signbit(orc.reduce(np.asfortranarray(a[:2]), 2, 1, "max")[0, 0, 0])
+    assert np.isnan(orc.reduce(a[4:6], 2, 1, "max")[0, 0, 0])
+    assert np.isnan(orc.reduce(a[4:6], 2, 1, "min")[0, 0, 0])
+
+
+def test_synth_generator_integer_kind(orc):
+    a = orc.synth(64, 2, 5, 16, 3, kind=1)
+    assert a.dtype == np.float32 and a.min() >= 0 and a.max() <= 255
+    assert np.array_equal(a, np.round(a))
+    b = orc.synth(64, 2, 5, 16, 3, kind=0)
+    assert np.all(b > 0)
+
+
+def test_baseline_threads_match_single(orc):
+    rng = np.random.default_rng(3)
+    banks = [np.asfortranarray(rng.integers(0, 256, (256, 1, 8)).astype(np.float32))
+             for _ in range(4)]
+    outs = orc.reduce_banks_mt(banks, 16, 4)
+    for b, o in zip(banks, outs):
+        assert same_bits(o, orc.reduce(b, 16, 4))
