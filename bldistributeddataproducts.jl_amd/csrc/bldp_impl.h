@@ -24,6 +24,7 @@ struct RedArgs {
   int64_t nco, ni, nto, F, T;
   int64_t rows_per_chunk;  // time rows of one T-block handled by one block
   int64_t blocks_c;        // blocks along the output-channel axis
+  int64_t ntiles;          // workgroup tiles (grid may be smaller: grid-stride)
   int32_t nchunk, nbank;
   int32_t ts;              // waves of a tile that split the T rows (1, 2, 4)
   int32_t k4;              // float4 loads per lane per row (vector path)

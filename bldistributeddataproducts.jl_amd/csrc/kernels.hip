@@ -53,8 +53,29 @@ template <int OP>
 __device__ __forceinline__ float fold4(float4 v) {
   return R<OP>::f(R<OP>::f(v.x, v.y), R<OP>::f(v.z, v.w));
 }
+// Build-time variants (A/B tested with tools/ab_variants.py):
+//   BLDP_NT_LOADS  1 (default) = streaming loads carry the non-temporal hint:
+//                  the window is read once; measured +10% on cfg3 (6.35 -> 6.98 TB/s)
+//   BLDP_BATCH     independent 16-byte loads a lane issues before the first use
+#ifndef BLDP_NT_LOADS
+#define BLDP_NT_LOADS 1
+#endif
+#ifndef BLDP_BATCH
+#define BLDP_BATCH 8
+#endif
+//   BLDP_MAX_WG_PER_CU  0 (default) = one workgroup per tile; N = grid capped
+//                  at N workgroups per CU, each looping over tiles
+#ifndef BLDP_MAX_WG_PER_CU
+#define BLDP_MAX_WG_PER_CU 0
+#endif
+typedef float f4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float4 ld4(const float *p) {
-  return *reinterpret_cast<const float4 *>(p);
+#if BLDP_NT_LOADS
+  const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(p));
+#else
+  const f4v v = *reinterpret_cast<const f4v *>(p);
+#endif
+  return make_float4(v.x, v.y, v.z, v.w);
 }
 
 // blockIdx.x -> (bc, i, chunk, to, bank); bc fastest so that consecutive
@@ -63,9 +84,9 @@ struct Coord {
   int64_t bc, i, chunk, to;
   int bank;
 };
-__device__ __forceinline__ Coord decompose(const RedArgs &a) {
+__device__ __forceinline__ Coord decompose(const RedArgs &a, int64_t tile) {
   Coord c;
-  int64_t b = blockIdx.x;
+  int64_t b = tile;
   c.bc = b % a.blocks_c;
   b /= a.blocks_c;
   c.i = b % a.ni;
@@ -91,14 +112,14 @@ __device__ __forceinline__ float finish(float s, const RedArgs &a) {
 // (1 KiB per wave when K4 == 1 or LPG == 64).  `ts` waves split the T rows of
 // a tile; 4/ts tiles per workgroup.
 template <int OP, int LPG, int K4C>
-__global__ __launch_bounds__(kBlock) void k_reduce_vec(const RedArgs a) {
+__device__ __forceinline__ void vec_tile(const RedArgs &a, int64_t tile) {
   constexpr int OPW = 64 / LPG;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int ts = a.ts;
   const int wt = wave / ts;
   const int tsi = wave - wt * ts;
-  const Coord c = decompose(a);
+  const Coord c = decompose(a, tile);
   const int g = lane / LPG, j = lane % LPG;
   const int64_t co = (c.bc * (4 / ts) + wt) * OPW + g;
   const bool valid = co < a.nco;
@@ -117,7 +138,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce_vec(const RedArgs a) {
     nrows = nrows > 0 ? (nrows + ts - 1) / ts : 0;
     const int64_t rstep = (int64_t)ts * a.in_ld_t;
     if constexpr (K4C > 0) {
-      constexpr int RB = (K4C >= 8) ? 1 : 8 / K4C;
+      constexpr int RB = (K4C >= BLDP_BATCH) ? 1 : BLDP_BATCH / K4C;
       constexpr int NV = RB * K4C;
       for (; nrows >= RB; nrows -= RB) {
         float4 v[NV];
@@ -166,6 +187,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce_vec(const RedArgs a) {
     __syncthreads();
     if (tsi == 0)
       for (int q = 1; q < ts; ++q) s = R<OP>::f(s, red[wave + q][lane]);
+    __syncthreads();  // red[] is reused by the next tile of a grid-stride loop
   }
   if (tsi == 0 && j == 0 && valid) {
     if (a.nchunk == 1) {
@@ -180,8 +202,8 @@ __global__ __launch_bounds__(kBlock) void k_reduce_vec(const RedArgs a) {
 // Narrow path, F in {1, 2}: one float4 (4 channels) per lane per row; no
 // cross-lane work.  F == 1 is pure time integration (gather-stress variant).
 template <int OP, int F>
-__global__ __launch_bounds__(kBlock) void k_reduce_narrow(const RedArgs a) {
-  const Coord c = decompose(a);
+__device__ __forceinline__ void narrow_tile(const RedArgs &a, int64_t tile) {
+  const Coord c = decompose(a, tile);
   const int64_t q4 = c.bc * kBlock + threadIdx.x;  // float4 column
   const int64_t nc4 = a.nco * F / 4;
   if (q4 >= nc4) return;
@@ -195,13 +217,13 @@ __global__ __launch_bounds__(kBlock) void k_reduce_narrow(const RedArgs a) {
       a.in[c.bank] + a.in_off + c.i * a.in_ld_i + (c.to * a.T + r0) * a.in_ld_t + 4 * q4;
   const int64_t st = a.in_ld_t;
   int64_t nrows = r1 - r0;
-  for (; nrows >= 8; nrows -= 8) {
-    float4 v[8];
+  for (; nrows >= BLDP_BATCH; nrows -= BLDP_BATCH) {
+    float4 v[BLDP_BATCH];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = ld4(p + u * st);
-    p += 8 * st;
+    for (int u = 0; u < BLDP_BATCH; ++u) v[u] = ld4(p + u * st);
+    p += BLDP_BATCH * st;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) acc[u] = f4<OP>(acc[u], v[u]);
+    for (int u = 0; u < BLDP_BATCH; ++u) acc[u % 8] = f4<OP>(acc[u % 8], v[u]);
   }
   for (; nrows > 0; --nrows) {
     acc[0] = f4<OP>(acc[0], ld4(p));
@@ -244,8 +266,8 @@ __global__ __launch_bounds__(kBlock) void k_reduce_narrow(const RedArgs a) {
 // ---------------------------------------------------------------------------
 // Scalar path: any F, any channel step, any alignment.  One lane per output.
 template <int OP>
-__global__ __launch_bounds__(kBlock) void k_reduce_scalar(const RedArgs a) {
-  const Coord c = decompose(a);
+__device__ __forceinline__ void scalar_tile(const RedArgs &a, int64_t tile) {
+  const Coord c = decompose(a, tile);
   const int64_t co = c.bc * kBlock + threadIdx.x;
   if (co >= a.nco) return;
   const int64_t r0 = c.chunk * a.rows_per_chunk;
@@ -271,6 +293,21 @@ __global__ __launch_bounds__(kBlock) void k_reduce_scalar(const RedArgs a) {
     a.out[c.bank * a.out_bank + c.i * a.out_ld_i + c.to * a.out_ld_t + co] = finish<OP>(s, a);
   else
     a.ws[(((c.chunk * a.nbank + c.bank) * a.nto + c.to) * a.ni + c.i) * a.nco + co] = s;
+}
+
+// Grid-stride wrappers: one tile per workgroup when the grid covers every
+// tile (the default), several when plan_reduce caps the grid (BLDP_MAX_WG_PER_CU).
+template <int OP, int LPG, int K4C>
+__global__ __launch_bounds__(kBlock) void k_reduce_vec(const RedArgs a) {
+  for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) vec_tile<OP, LPG, K4C>(a, t);
+}
+template <int OP, int F>
+__global__ __launch_bounds__(kBlock) void k_reduce_narrow(const RedArgs a) {
+  for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) narrow_tile<OP, F>(a, t);
+}
+template <int OP>
+__global__ __launch_bounds__(kBlock) void k_reduce_scalar(const RedArgs a) {
+  for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) scalar_tile<OP>(a, t);
 }
 
 // Second stage of a time-chunked reduction: fold the nchunk partials of every
@@ -587,7 +624,9 @@ Plan plan_reduce(RedArgs &a, bool aligned, int num_cus) {
   if (a.rows_per_chunk < 1) a.rows_per_chunk = 1;
   a.nchunk = (int32_t)std::max<int64_t>(1, cdiv(T, a.rows_per_chunk));
   p.ws_bytes = a.nchunk > 1 ? (size_t)a.nchunk * a.nbank * p.nout * sizeof(float) : 0;
-  p.grid = a.blocks_c * a.ni * a.nchunk * a.nto * a.nbank;
+  a.ntiles = a.blocks_c * a.ni * a.nchunk * a.nto * a.nbank;
+  p.grid = a.ntiles;
+  if (BLDP_MAX_WG_PER_CU > 0) p.grid = std::min<int64_t>(p.grid, (int64_t)BLDP_MAX_WG_PER_CU * num_cus);
   // narrow-path vector stores
   a.vec_out = 0;
   if (p.path == PATH_NARROW) {

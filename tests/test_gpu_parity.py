@@ -81,7 +81,7 @@ SHAPES = [
     (16384, 1, 16, 1024, 16), (65536, 1, 4, 16384, 4), (6144, 1, 8, 12, 2),
     (6144, 1, 8, 384, 8), (4096, 1, 32, 1, 16), (4096, 3, 10, 2, 5), (4096, 1, 8, 1, 1),
     (96, 3, 10, 3, 5), (300, 2, 7, 5, 7), (512, 1, 8192, 8, 1024), (64, 1, 20000, 8, 20000),
-    (512, 2, 4096, 1, 4096), (1024, 1, 2000, 6, 1000),
+    (512, 2, 4096, 1, 4096), (1020, 1, 2000, 6, 1000),
 ]
 
 
@@ -133,7 +133,7 @@ WINDOWS = [
     [33, 512, 1, 0, 2, 1, 0, 48, 1],        # misaligned channel start -> scalar path
     [1020, 96, -3, 0, 2, 1, 44, 12, -3],    # reversed strided channels and times
     [5, 120, 8, 0, 2, 1, 0, 48, 1],         # strided channels
-    [0, 1024, 1, 1, 1, 1, 0, 48, 2],        # every other spectrum
+    [0, 1024, 1, 1, 1, 1, 0, 24, 2],        # every other spectrum
     [0, 1024, 1, 0, 2, 1, 7, 1, 1],         # an Integer time index (i:i)
 ]
 

@@ -1,0 +1,147 @@
+#!/usr/bin/env python3
+"""A/B kernel build variants in ONE process (interleaved rounds).
+
+Each variant is libbldp_hip compiled with different -D knobs into
+build/variants/libbldp_<name>.so; all copies are loaded side by side with
+ctypes (separate handles, separate code objects) and timed on the same device
+buffers with HIP events, round-robin, so clock/thermal drift hits every
+variant alike (cdna_hip_programming.md §5.4 rule 24).
+
+    python tools/ab_variants.py --build            # here (hipcc cross-compiles)
+    python tools/ab_variants.py --run [--rounds 7] # on the GPU box
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+VDIR = os.path.join(REPO, "build", "variants")
+CSRC = os.path.join(REPO, "bldistributeddataproducts.jl_amd", "csrc")
+
+VARIANTS = {
+    "base": "",                                # nt loads, batch 8, one WG per tile
+    "plain": "-DBLDP_NT_LOADS=0",
+    "b4": "-DBLDP_BATCH=4",
+    "cap4": "-DBLDP_MAX_WG_PER_CU=4",
+    "cap8": "-DBLDP_MAX_WG_PER_CU=8",
+    "cap16": "-DBLDP_MAX_WG_PER_CU=16",
+}
+
+
+def build(names):
+    os.makedirs(VDIR, exist_ok=True)
+    for n in names:
+        out = os.path.join(VDIR, f"libbldp_{n}.so")
+        subprocess.run(["make", "-s", "-B", "-C", CSRC, f"OUT={out}", f"EXTRA={VARIANTS[n]}"],
+                       check=True)
+        print("built", out)
+
+
+def load(path):
+    import __graft_entry__ as entry
+
+    pkg = entry.load_package()
+    L = ctypes.CDLL(path)
+    for name, (args, res) in pkg._lib.SIGNATURES.items():
+        getattr(L, name).argtypes = args
+        getattr(L, name).restype = res
+    return L
+
+
+def run(names, rounds, iters):
+    import torch
+
+    import __graft_entry__ as entry
+
+    pkg = entry.load_package()
+    eng = pkg.engine
+    libs = {n: load(os.path.join(VDIR, f"libbldp_{n}.so")) for n in names}
+    stream = torch.cuda.current_stream()
+    sp = int(stream.cuda_stream)
+    cases = []
+
+    def band_case(label, banks, F, T, win=None):
+        nchan, nif, ntime = banks[0].shape[0], banks[0].shape[1], banks[0].shape[2]
+        nc = win[1] if win else nchan
+        nt = win[7] if win else ntime
+        out = eng.fb_empty(len(banks) * (nc // F), nif, nt // T)
+        ptrs = (ctypes.c_void_p * len(banks))(*[b.data_ptr() for b in banks])
+        keep, wp = pkg._lib.win_arg(win)
+        nbytes = len(banks) * 4 * (nc * nif * nt + (nc // F) * nif * (nt // T))
+
+        def go(L):
+            rc = L.bldp_band_reduce_f32(len(banks), ctypes.cast(ptrs, ctypes.c_void_p), nchan,
+                                        nif, ntime, wp, F, T, 0, out.data_ptr(), sp)
+            assert rc == 0
+        cases.append((label, go, nbytes, out, keep))
+
+    b3 = [eng.synth(1 << 26, 1, 16, 1 << 20, seed=10 * b, kind=0) for b in range(8)]
+    band_case("cfg3 F1024 T16", b3, 1024, 16)
+    band_case("cfg3 F1 T16", b3, 1, 16)
+    band_case("cfg3 F64 T16", b3, 64, 16)
+    b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
+    band_case("cfg2 F64 T16", b2, 64, 16, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
+    b4 = [eng.synth(512, 1, 880000, 8, seed=10 * b + 1, kind=0) for b in range(8)]
+    band_case("cfg4 F8 T1024", b4, 8, 1024, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
+    torch.cuda.synchronize()
+
+    res = {c[0]: {n: [] for n in names} for c in cases}
+    ref = {}
+    for r in range(rounds):
+        for label, go, nbytes, out, _ in cases:
+            for n in names:
+                L = libs[n]
+                go(L)  # warm
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(iters):
+                    go(L)
+                e1.record(stream)
+                e1.synchronize()
+                ms = e0.elapsed_time(e1) / iters
+                res[label][n].append(ms)
+                if r == 0:
+                    o = out.float().sum().item()
+                    ref.setdefault(label, o)
+                    if abs(o - ref[label]) > 1e-4 * abs(ref[label]):
+                        print(f"WARNING {label} {n}: checksum {o} vs {ref[label]}")
+        print(f"round {r} done", file=sys.stderr, flush=True)
+    summary = {}
+    for label, go, nbytes, out, _ in cases:
+        summary[label] = {}
+        for n in names:
+            ts = sorted(res[label][n])
+            med = ts[len(ts) // 2]
+            summary[label][n] = {"median_ms": round(med, 4), "min_ms": round(ts[0], 4),
+                                 "GBps_median": round(nbytes / med / 1e6, 1)}
+        print(label, json.dumps(summary[label]))
+    return summary
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build", action="store_true")
+    ap.add_argument("--run", action="store_true")
+    ap.add_argument("--variants", default=",".join(VARIANTS))
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    names = a.variants.split(",")
+    if a.build:
+        build(names)
+    if a.run:
+        s = run(names, a.rounds, a.iters)
+        if a.json:
+            with open(a.json, "w") as f:
+                json.dump(s, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

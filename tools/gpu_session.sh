@@ -1,0 +1,44 @@
+#!/bin/bash
+# One GPU session on the MI355X box: probe, smoke, GPU parity tests, bench,
+# rocprofv3 kernel stats.  Every GPU step has its own time limit; after a
+# crash/abort/timeout nothing further touches the GPU.
+#   usage: tools/gpu_session.sh TAG [steps...]   steps: smoke tests bench prof pmc
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=${1:-r01}; shift || true
+STEPS=${*:-"smoke tests bench prof"}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+
+run() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -n 12 "$OUT/$name.log"
+  case $rc in
+    0|1) return 0 ;;   # 1 = test/assert failures: the GPU is fine
+    *) echo "== $name ended with rc=$rc: stopping GPU work"; exit $rc ;;
+  esac
+}
+
+{ which julia || echo "julia: absent"; rocm-smi --showproductname 2>/dev/null | head -8; nproc; } \
+  > "$OUT/probe.log" 2>&1
+for s in $STEPS; do
+  case $s in
+    smoke) run smoke 300 python -c "import __graft_entry__ as e; e.smoke()" ;;
+    tests) run tests 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    bench) run bench 600 python bench.py ;;
+    prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv \
+             -d "$OUT/prof" -o run -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv \
+             -d "$OUT/pmc_fetch" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline
+           run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv \
+             -d "$OUT/pmc_write" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+    bench_*) run "$s" 600 python bench.py --config "${s#bench_}" ;;
+    ab)    run ab 900 python tools/ab_variants.py --run --json "$OUT/ab.json" ;;
+  esac
+done
+echo "== session done"

@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""Turn two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE; separate runs as
+MI355X_MICROARCH.md §rocprofv3 PMC slots requires) into per-launch HBM bytes
+of the reduce kernel, and record them in profiles/pmc_traffic.json for bench.py.
+
+gfx950 corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE (KiB) reports half
+the bytes of a wide (16 B/lane) coalesced streaming read -> x2; WRITE_SIZE is
+exact for 16 B/lane stores (the reduce kernel's output writes are 4 B and tiny;
+taken as reported).
+
+    python tools/pmc_traffic.py CONFIG BANKS_PER_LAUNCH FETCH.csv WRITE.csv
+"""
+from __future__ import annotations
+
+import csv
+import json
+import os
+import statistics
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def per_dispatch(path, counter, kernel_substr="k_reduce"):
+    vals = []
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if kernel_substr in row["Kernel_Name"] and row["Counter_Name"] == counter:
+                vals.append(float(row["Counter_Value"]))
+    if not vals:
+        raise SystemExit(f"no {counter} rows for {kernel_substr} in {path}")
+    return vals
+
+
+def main():
+    cfg, nbank, fpath, wpath = sys.argv[1], int(sys.argv[2]), sys.argv[3], sys.argv[4]
+    fetch = per_dispatch(fpath, "FETCH_SIZE")
+    write = per_dispatch(wpath, "WRITE_SIZE")
+    f_kib, w_kib = statistics.median(fetch), statistics.median(write)
+    hbm = 2 * f_kib * 1024 + w_kib * 1024
+    out = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(out) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        d = {}
+    d[cfg] = {"banks_per_launch": nbank, "hbm_bytes_per_launch": int(hbm),
+              "fetch_size_kib_median": f_kib, "write_size_kib_median": w_kib,
+              "dispatches": [len(fetch), len(write)],
+              "correction": "hbm = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 half-count "
+                            "of 16B/lane streaming reads)",
+              "source": [os.path.relpath(fpath, REPO), os.path.relpath(wpath, REPO)]}
+    with open(out, "w") as f:
+        json.dump(d, f, indent=1)
+    print(json.dumps(d[cfg]))
+
+
+if __name__ == "__main__":
+    main()
