@@ -58,6 +58,7 @@ SIGNATURES = {
     "bldp_despike_f32": ([P, I64, I64, I64, I64, P], I),
     "bldp_kurtosis_workspace_size": ([I64, I64, I64, P], SZ),
     "bldp_kurtosis_f32": ([P, I64, I64, I64, P, P, P, P], I),
+    "bldp_kurtosis_host_f32": ([I, P, I64, I64, I64, P, P], I),
     "bldp_fqav_range": ([D, D, I64, I64, P, P, P], I),
     "bldp_synth_f32": ([P, I64, I64, I64, I64, U64, I, P], I),
 }

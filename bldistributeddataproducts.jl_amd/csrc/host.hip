@@ -14,6 +14,8 @@
 
 extern "C" int bldp_reduce_shape(int64_t, int64_t, int64_t, const int64_t *, int64_t, int64_t,
                                  int64_t *);
+extern "C" int bldp_kurtosis_f32(const float *, int64_t, int64_t, int64_t, const int64_t *,
+                                 double *, void *, void *);
 extern "C" int bldp_reduce_strided_f32(const float *, int64_t, int64_t, int64_t,
                                        const int64_t *, int64_t, int64_t, int, float *, int64_t,
                                        int64_t, void *);
@@ -112,5 +114,60 @@ done:
     if (dout[b]) (void)hipFree(dout[b]);
     if (st[b]) (void)hipStreamDestroy(st[b]);
   }
+  return rc;
+}
+
+// Stage the window rows ([t][i][span] dense) on the device with the same copy
+// rules as bldp_reduce_host_f32, then run the two-pass kurtosis there.
+extern "C" int bldp_kurtosis_host_f32(int dev, const float *in, int64_t nchan, int64_t nif,
+                                      int64_t ntime, const int64_t *win, double *out) {
+  int64_t sh[3];
+  int rc = bldp_reduce_shape(nchan, nif, ntime, win, 1, 1, sh);
+  if (rc) return rc;
+  const int64_t nc = sh[0], ni = sh[1], nt = sh[2];
+  if (nc * ni == 0) return BLDP_OK;
+  if (!out || (!in && nt > 0)) return bldp::set_error(BLDP_EINVAL, "null pointer");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || dev < 0 || dev >= ndev)
+    return bldp::set_error(BLDP_EINVAL, "device %d not available", dev);
+  DevGuard guard(dev);
+  const int64_t c0 = win ? win[0] : 0, cs = win ? win[2] : 1;
+  const int64_t i0 = win ? win[3] : 0, is = win ? win[5] : 1;
+  const int64_t t0 = win ? win[6] : 0, ts = win ? win[8] : 1;
+  const int64_t acs = cs < 0 ? -cs : cs;
+  const int64_t span = (nc - 1) * acs + 1;
+  const int64_t c_lo = cs < 0 ? c0 + (nc - 1) * cs : c0;
+  const int64_t ld_i = nchan * is, ld_t = nchan * nif * ts;
+  const float *row0 = in + c_lo + nchan * (i0 + nif * t0);
+  float *dbuf = nullptr;
+  double *dout = nullptr;
+  hipStream_t st = nullptr;
+  const int64_t dwin[9] = {cs < 0 ? (nc - 1) * acs : 0, nc, cs, 0, ni, 1, 0, nt, 1};
+  HCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  HCHK(hipMalloc(&dbuf, (size_t)std::max<int64_t>(1, span * ni * nt) * sizeof(float)));
+  HCHK(hipMalloc(&dout, (size_t)(nc * ni) * sizeof(double)));
+  if (nt > 0) {
+    const bool uniform = (ni == 1 && ld_t > 0 && ld_t >= span) ||
+                         (ld_i > 0 && ld_i >= span && ld_t == ni * ld_i);
+    if (uniform) {
+      const int64_t pitch = ni == 1 ? ld_t : ld_i;
+      HCHK(hipMemcpy2DAsync(dbuf, span * sizeof(float), row0, pitch * sizeof(float),
+                            span * sizeof(float), (size_t)(nt * ni), hipMemcpyHostToDevice, st));
+    } else {
+      for (int64_t r = 0; r < nt; ++r)
+        for (int64_t i = 0; i < ni; ++i)
+          HCHK(hipMemcpyAsync(dbuf + (r * ni + i) * span, row0 + r * ld_t + i * ld_i,
+                              span * sizeof(float), hipMemcpyHostToDevice, st));
+    }
+  }
+  rc = bldp_kurtosis_f32(dbuf, span, ni, nt, dwin, dout, nullptr, st);
+  if (rc) goto done;
+  HCHK(hipMemcpyAsync(out, dout, (size_t)(nc * ni) * sizeof(double), hipMemcpyDeviceToHost, st));
+  HCHK(hipStreamSynchronize(st));
+done:
+  if (st) (void)hipStreamSynchronize(st);
+  if (dbuf) (void)hipFree(dbuf);
+  if (dout) (void)hipFree(dout);
+  if (st) (void)hipStreamDestroy(st);
   return rc;
 }

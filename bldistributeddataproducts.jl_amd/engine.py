@@ -21,7 +21,7 @@ from .idxs import window_shape
 
 __all__ = [
     "fb_empty", "fb_from_numpy", "fb_to_numpy", "reduce", "band_reduce", "stitch",
-    "despike", "kurtosis", "synth", "plan", "reduce_host",
+    "despike", "kurtosis", "synth", "plan", "reduce_host", "kurtosis_host",
 ]
 
 
@@ -267,4 +267,20 @@ def reduce_host(a: np.ndarray, fqavby=1, tavby=1, op="sum", win=None, device=0) 
                                 shape[1], shape[2], wp, int(fqavby), int(tavby), _lib.OPS[op],
                                 out.ctypes.data if out.size else None)
     _lib.check(rc, "bldp_reduce_host_f32")
+    return out
+
+
+def kurtosis_host(a: np.ndarray, win=None, device=0) -> np.ndarray:
+    """Host array in, (nc, ni) float64 host array out (bldp_kurtosis_host_f32)."""
+    L = _lib.lib()
+    a = np.asarray(a)
+    if a.dtype != np.float32 or not a.flags.f_contiguous or a.ndim != 3:
+        raise TypeError("host filterbank must be a Fortran-ordered float32 (nchan, nif, ntime)")
+    _check_bounds(win, a.shape)
+    nc, ni, _ = window_shape(win, a.shape)
+    out = np.empty((nc, ni), dtype=np.float64, order="F")
+    keep, wp = _lib.win_arg(_full_win(win, a.shape))
+    rc = L.bldp_kurtosis_host_f32(int(device), a.ctypes.data if a.size else None, a.shape[0],
+                                  a.shape[1], a.shape[2], wp, out.ctypes.data if out.size else None)
+    _lib.check(rc, "bldp_kurtosis_host_f32")
     return out

@@ -1,0 +1,94 @@
+#=
+BLDPHip.jl — the Julia side of the drop-in: `ccall` bindings to libbldp_hip
+(include/bldp.h) for BLDistributedDataProducts.jl's WorkerFunctions.
+
+UNTESTED HERE: Julia is absent from both the build container and the MI355X
+box (probed), so this file is the binding a maintainer adds, exercised in this
+repo only through the identical Python ctypes binding (_lib.py / tests/).
+See INTEGRATION.md for the two-line patch to src/gbtworkerfunctions.jl.
+=#
+module BLDPHip
+
+using Statistics: mean
+
+export gpu_fqav, gpu_reduce, gpu_kurtosis, gpu_band
+
+const libbldp = get(ENV, "BLDP_LIB", joinpath(@__DIR__, "..", "libbldp_hip.so"))
+
+# fqavfunc values with a GPU implementation (README.md:192-195); anything
+# else keeps the reference's host fqav.
+opcode(f) = f === sum ? Cint(0) : f === mean ? Cint(1) : f === maximum ? Cint(2) :
+            f === minimum ? Cint(3) : nothing
+
+function lasterror()
+    buf = Vector{UInt8}(undef, 1024)
+    ccall((:bldp_last_error, libbldp), Cint, (Ptr{UInt8}, Csize_t), buf, length(buf))
+    unsafe_string(pointer(buf))
+end
+
+function check(rc::Integer)
+    rc == 0 && return nothing
+    msg = lasterror()
+    rc == -2 && throw(DimensionMismatch(msg))   # fqavby/tavby does not divide
+    rc == -6 && throw(BoundsError(msg))         # window outside the array
+    rc == -1 && throw(ArgumentError(msg))
+    error("libbldp_hip error $rc: $msg")
+end
+
+# Julia index -> (0-based start, count, step) on an axis of length n
+axiswin(::Colon, n) = (0, n, 1)
+axiswin(i::Integer, n) = (i - 1, 1, 1)                      # sanitizeidxs: i -> i:i
+axiswin(r::AbstractRange{<:Integer}, n) = (first(r) - 1, length(r), step(r))
+
+function window(idxs::Tuple, sz)
+    @assert length(idxs) == 3 "idxs must have exactly three indices"
+    all(i -> i isa Colon, idxs) && return C_NULL
+    Int64[x for ax in 1:3 for x in axiswin(idxs[ax], sz[ax])]
+end
+
+"""
+    gpu_reduce(A::Array{Float32,3}, fqavby, tavby=1; f=sum, idxs=(:,:,:), dev=0)
+
+`fqav(A[idxs...], fqavby; f)` fused with the same reduction over `tavby`
+spectra, computed on GPU `dev` (bldp_reduce_host_f32)."""
+function gpu_reduce(A::Array{Float32,3}, fqavby::Integer, tavby::Integer=1;
+                    f=sum, idxs::Tuple=(:, :, :), dev::Integer=0)
+    op = opcode(f)
+    op === nothing && throw(ArgumentError("no GPU kernel for $f"))
+    win = window(idxs, size(A))
+    shp = zeros(Int64, 3)
+    GC.@preserve win check(ccall((:bldp_reduce_shape, libbldp), Cint,
+        (Int64, Int64, Int64, Ptr{Int64}, Int64, Int64, Ptr{Int64}),
+        size(A, 1), size(A, 2), size(A, 3), win, fqavby, tavby, shp))
+    out = Array{Float32,3}(undef, shp...)
+    GC.@preserve A win out check(ccall((:bldp_reduce_host_f32, libbldp), Cint,
+        (Cint, Ptr{Float32}, Int64, Int64, Int64, Ptr{Int64}, Int64, Int64, Cint, Ptr{Float32}),
+        dev, A, size(A, 1), size(A, 2), size(A, 3), win, fqavby, tavby, op, out))
+    out
+end
+
+"""
+    gpu_fqav(A, n; f=sum, tavby=1)
+
+Drop-in for `fqav(A, n; f)` (src/gbtworkerfunctions.jl:16-20): same
+pass-through for `n <= 1`, same DimensionMismatch, GPU for sum/mean/maximum/
+minimum, the reference's host code for any other `f`."""
+function gpu_fqav(A, n::Integer; f=sum, tavby::Integer=1, dev::Integer=0)
+    (n <= 1 && tavby <= 1) && return A
+    if A isa Array{Float32,3} && opcode(f) !== nothing
+        return gpu_reduce(A, n, tavby; f, dev)
+    end
+    tavby <= 1 || throw(ArgumentError("tavby needs a Float32 3-D array and sum/mean/max/min"))
+    sz = (n, :, size(A)[2:end]...)
+    dropdims(f(reshape(A, sz), dims=1), dims=1)
+end
+
+"""
+    gpu_kurtosis(A::Array{Float32,3}; idxs=(:,:,:), dev=0) -> Matrix{Float64}
+
+getkurtosis' per-(channel, IF) excess kurtosis over time
+(src/gbtworkerfunctions.jl:197-202), computed on the GPU.  Uses a device
+staging copy of the window; see bldp_kurtosis_f32."""
+function gpu_kurtosis end  # device-pointer entry point; bind with AMDGPU.jl arrays
+
+end # module

@@ -182,12 +182,18 @@ def getkurtosis(fname, idxs=(COLON, COLON, COLON), device=0):
     idxs = sanitizeidxs(idxs)
     if _is_tensor(fname):
         return engine.kurtosis(fname, to_window(idxs, fname.shape))
-    data = getdata(fname, idxs, device=device)  # :198 (window read, no fqav)
-    import torch
-
-    with torch.cuda.device(device):
-        x = engine.fb_from_numpy(data, device=f"cuda:{device}")
-        return engine.fb_to_numpy(engine.kurtosis(x))
+    if isinstance(fname, (str, bytes)) or hasattr(fname, "__fspath__"):
+        if readers.ishdf5(fname):
+            a, idxs = readers.fbh5_read(fname, idxs), (COLON, COLON, COLON)
+        else:
+            _, a = readers.fil_mmap(fname)
+    else:
+        a = fname
+    a = np.asarray(a)
+    win = to_window(idxs, a.shape)
+    if a.dtype != np.float32 or not a.flags.f_contiguous:
+        a = np.asfortranarray(a, dtype=np.float32)
+    return engine.kurtosis_host(a, win, device=device)
 
 
 getinventory = readers.getinventory

@@ -131,6 +131,12 @@ BLDP_API size_t bldp_kurtosis_workspace_size(int64_t nchan, int64_t nif, int64_t
 BLDP_API int bldp_kurtosis_f32(const float *in, int64_t nchan, int64_t nif, int64_t ntime,
                       const int64_t *win, double *out, void *workspace, void *stream);
 
+/* Host-pointer form of bldp_kurtosis_f32 for a worker holding the data in
+ * host memory: the window is staged on device `dev`, out (nc, ni) float64 is
+ * host memory.  Synchronous. */
+BLDP_API int bldp_kurtosis_host_f32(int dev, const float *in, int64_t nchan, int64_t nif,
+                                    int64_t ntime, const int64_t *win, double *out);
+
 /* fqav(r::AbstractRange, n): first/step/length of the averaged axis. */
 BLDP_API int bldp_fqav_range(double first, double step, int64_t len, int64_t n, double *out_first,
                     double *out_step, int64_t *out_len);

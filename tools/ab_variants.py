@@ -87,6 +87,7 @@ def run(names, rounds, iters):
     band_case("cfg3 F64 T16", b3, 64, 16)
     b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
     band_case("cfg2 F64 T16", b2, 64, 16, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
+    band_case("cfg1 F64 T16", b2[:1], 64, 16, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
     b4 = [eng.synth(512, 1, 880000, 8, seed=10 * b + 1, kind=0) for b in range(8)]
     band_case("cfg4 F8 T1024", b4, 8, 1024, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
     torch.cuda.synchronize()
