@@ -42,7 +42,7 @@ axiswin(r::AbstractRange{<:Integer}, n) = (first(r) - 1, length(r), step(r))
 
 function window(idxs::Tuple, sz)
     @assert length(idxs) == 3 "idxs must have exactly three indices"
-    all(i -> i isa Colon, idxs) && return C_NULL
+    all(i -> i isa Colon, idxs) && return Ptr{Int64}(C_NULL)
     Int64[x for ax in 1:3 for x in axiswin(idxs[ax], sz[ax])]
 end
 
@@ -87,8 +87,27 @@ end
     gpu_kurtosis(A::Array{Float32,3}; idxs=(:,:,:), dev=0) -> Matrix{Float64}
 
 getkurtosis' per-(channel, IF) excess kurtosis over time
-(src/gbtworkerfunctions.jl:197-202), computed on the GPU.  Uses a device
-staging copy of the window; see bldp_kurtosis_f32."""
-function gpu_kurtosis end  # device-pointer entry point; bind with AMDGPU.jl arrays
+(src/gbtworkerfunctions.jl:197-202), computed on GPU `dev`
+(bldp_kurtosis_host_f32: window staged on the device, two-pass StatsBase
+recipe, Float64 result)."""
+function gpu_kurtosis(A::Array{Float32,3}; idxs::Tuple=(:, :, :), dev::Integer=0)
+    win = window(idxs, size(A))
+    shp = zeros(Int64, 3)
+    GC.@preserve win check(ccall((:bldp_reduce_shape, libbldp), Cint,
+        (Int64, Int64, Int64, Ptr{Int64}, Int64, Int64, Ptr{Int64}),
+        size(A, 1), size(A, 2), size(A, 3), win, 1, 1, shp))
+    out = Matrix{Float64}(undef, shp[1], shp[2])
+    GC.@preserve A win out check(ccall((:bldp_kurtosis_host_f32, libbldp), Cint,
+        (Cint, Ptr{Float32}, Int64, Int64, Int64, Ptr{Int64}, Ptr{Float64}),
+        dev, A, size(A, 1), size(A, 2), size(A, 3), win, out))
+    out
+end
+
+"""
+    gpu_band(parts) -> Array{Float32,3}
+
+`reduce(vcat, parts)` of per-bank results in bank order (src/gbt.jl:103):
+what `GBT.getband` returns after `fetch.(futures)`."""
+gpu_band(parts) = reduce(vcat, parts)
 
 end # module
