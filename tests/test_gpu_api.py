@@ -1,0 +1,120 @@
+"""GPU, end to end through the reference-shaped API: files on disk (FBH5 and
+SIGPROC) -> WorkerFunctions.getdata / GBT.getdata / getband / getkurtosis,
+and the N-rank band exchange with the real kernels (gloo transport, two ranks
+sharing cuda:0)."""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+
+from conftest import same_bits
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def files(pkg, orc, tmp_path_factory):
+    d = tmp_path_factory.mktemp("banks")
+    rng = np.random.default_rng(2026)
+    banks, names = [], []
+    for b in range(8):
+        a = np.asfortranarray(rng.integers(0, 256, (4096, 1, 40)).astype(np.float32))
+        banks.append(a)
+        hdr = dict(fch1=8400.0 - b * 187.5, foff=-187.5 / 4096, nchans=4096, nifs=1,
+                   tsamp=1.07, source_name="HIP1234")
+        if b % 2 == 0:
+            p = d / f"BLP0{b}" / f"blc0{b}_guppi_59000_12345_HIP1234_0011.rawspec.0002.h5"
+            p.parent.mkdir()
+            pkg.fbh5.write(p, dict(hdr, nfpc=64), a, chunks=(8, 1, 1024))
+        else:
+            p = d / f"BLP0{b}" / f"blc0{b}_guppi_59000_12345_HIP1234_0011.rawspec.0002.fil"
+            p.parent.mkdir()
+            pkg.readers.write_fil(p, dict(hdr, telescope_id=6, machine_id=10, data_type=1,
+                                          tstart=59000.5, nbits=32), a)
+        names.append(str(p))
+    return banks, names
+
+
+def test_worker_getdata_files(pkg, orc, files):
+    banks, names = files
+    J, C = pkg.JRange, pkg.COLON
+    for a, f in zip(banks, names):
+        got = pkg.WorkerFunctions.getdata(f, (C, C, J(1, 32)), fqavby=64, tavby=8)
+        assert same_bits(got, orc.reduce(a, 64, 8, "sum", [0, 4096, 1, 0, 1, 1, 0, 32, 1]))
+        got = pkg.WorkerFunctions.getdata(f, (J(1025, 2048), 1, C), fqavby=16, fqavfunc="max")
+        assert same_bits(got, orc.reduce(a, 16, 1, "max", [1024, 1024, 1, 0, 1, 1, 0, 40, 1]))
+    with pytest.raises(pkg.DimensionMismatch):
+        pkg.WorkerFunctions.getdata(names[0], fqavby=3)
+
+
+def test_gbt_getdata_getband_kurtosis(pkg, orc, files):
+    banks, names = files
+    J, C = pkg.JRange, pkg.COLON
+    workers = [0] * len(names)  # every "worker" is this box's GPU 0
+    res = pkg.GBT.getdata(workers, names, (C, C, J(1, 40)), fqavby=64, tavby=10)
+    assert res.shape == (8,)
+    for a, r in zip(banks, res):
+        assert same_bits(r, orc.reduce(a, 64, 10))
+    band = pkg.GBT.getband(workers, names, (C, C, C), fqavby=64, tavby=10)
+    assert same_bits(band, orc.stitch([orc.reduce(a, 64, 10) for a in banks]))
+    full = pkg.GBT.getband(workers, names, (C, C, J(1, 3)), despike_nfpc=64)
+    want = orc.despike(orc.stitch([np.asfortranarray(a[:, :, :3]) for a in banks]), 64)
+    assert same_bits(full, want)
+    ks = pkg.GBT.getkurtosis(workers[:2], names[:2], (J(1, 512), C, C))
+    for a, k in zip(banks[:2], ks):
+        np.testing.assert_allclose(k, orc.kurtosis(a, [0, 512, 1, 0, 1, 1, 0, 40, 1]),
+                                   rtol=1e-4, atol=1e-5)
+    hdrs = pkg.GBT.getheaders(workers[:2], names[:2])
+    assert hdrs[0]["nfpc"] == 64 and hdrs[1]["nfpc"] == 64  # FBH5 attr / round(187.5/64/abs(foff))
+
+
+def _rank(rank, world, port, q):
+    import sys
+
+    import torch
+    import torch.distributed as dist
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import __graft_entry__ as entry
+
+    pkg, orc = entry.load_package(), entry.load_oracle()
+    eng = pkg.engine
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(5)
+    banks = [orc.gamma_bandpass(8192, 1, 64, 1024, 50 + b) for b in range(8)]
+    mine = [eng.fb_from_numpy(banks[b], "cuda:0") for b in pkg.band.banks_for_rank(8, rank, world)]
+
+    def reduce_fn(bs, F, T, op, win):  # real kernel; gloo moves host tensors
+        return eng.band_reduce(bs, F, T, op, win).cpu()
+
+    def stitch_fn(g, n):  # real stitch kernel on the gathered blocks
+        return eng.stitch(g.cuda(), n).cpu()
+
+    res = pkg.band.band_reduce_dist(mine, 64, 16, "sum", None, reduce_fn=reduce_fn,
+                                    stitch_fn=stitch_fn)
+    if rank == 0:
+        want = orc.stitch([orc.reduce(b, 64, 16) for b in banks])
+        got = res.permute(2, 1, 0).contiguous().numpy().transpose(2, 1, 0)
+        q.put(bool(np.allclose(got, want, rtol=1e-5)) and got.shape == want.shape)
+    else:
+        q.put(res is None)
+    dist.destroy_process_group()
+    del rng, torch
+
+
+def test_band_dist_two_ranks_real_kernels():
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29700 + os.getpid() % 200
+    ps = [ctx.Process(target=_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(timeout=300)
+    assert all(p.exitcode == 0 for p in ps)
+    assert all(q.get(timeout=5) for _ in ps)

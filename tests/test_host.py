@@ -165,3 +165,27 @@ def test_band_exchange_gloo_world2(F, T, ni, nt):
     results = [q.get(timeout=5) for _ in procs]
     assert all(p.exitcode == 0 for p in procs)
     assert all(results)
+
+
+def test_fbh5_read_and_header(pkg, tmp_path):
+    fb, J, C = pkg.fbh5, pkg.JRange, pkg.COLON
+    d = np.asfortranarray(np.random.default_rng(1).random((64, 2, 10)).astype(np.float32))
+    p = tmp_path / "blc42_guppi_59000_12345_HIP1234_0011.rawspec.0002.h5"
+    fb.write(p, dict(fch1=8400.0, foff=-2.861022949e-3, nchans=64, nifs=2, tsamp=1.07,
+                     source_name="HIP1234", nfpc=1024), d, chunks=(4, 1, 16))
+    assert pkg.readers.ishdf5(p)
+    assert np.array_equal(fb.read_window(p, (C, C, C)), d)  # h5["data"][] (:183)
+    w = fb.read_window(p, (J(60, -3, 5), 2, J(2, 2, 9)))  # hyperslab (:185)
+    assert np.array_equal(w, d[59:3:-3][:, 1:2, 1:9:2]) and w.shape == (19, 1, 4)
+    with pytest.raises(pkg.BoundsError):
+        fb.read_window(p, (J(1, 65), C, C))
+    h = pkg.readers.getheader(p)
+    assert list(h) == sorted(h)  # sorted by key (:153)
+    assert "DIMENSION_LABELS" not in h  # dropped (:145)
+    assert h["nsamps"] == 10 and h["data_size"] == 64 * 2 * 10 * 4 and h["nfpc"] == 1024
+    q = tmp_path / "nonfpc.h5"
+    fb.write(q, dict(foff=-2.7939677238464355e-06), d, deflate=4)
+    assert fb.header(q)["nfpc"] == 1048576
+    with pytest.raises(NameError):  # the reference's :147-150 bug, on request
+        fb.header(q, reference_bug=True)
+    assert np.array_equal(fb.read_window(q, (C, C, C)), d)
