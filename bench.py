@@ -107,6 +107,96 @@ def cpu_baseline(cfg, seconds, eng, torch):
                       f"(float64 accumulate), one pthread per bank"}
 
 
+def bench_kurtosis(args, cfg, eng, torch):
+    """getkurtosis (src/gbtworkerfunctions.jl:197-202) over every bank of the
+    config: two-pass StatsBase recipe, so the algorithm reads the window twice."""
+    win = None
+    if cfg["tw"] != cfg["ntime"]:
+        win = [0, cfg["nchan"], 1, 0, cfg["nif"], 1, 0, cfg["tw"], 1]
+    banks = [eng.synth(cfg["nchan"], cfg["nif"], cfg["ntime"], cfg["nfpc"],
+                       seed=10 * b + cfg["product"], kind=0) for b in range(cfg["nbank"])]
+    stream = torch.cuda.current_stream()
+    for _ in range(args.warmup):
+        for b in banks:
+            eng.kurtosis(b, win)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(args.steps):
+        for b in banks:
+            eng.kurtosis(b, win)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    ms = e0.elapsed_time(e1) / args.steps
+    n = cfg["nbank"] * cfg["nchan"] * cfg["nif"] * cfg["tw"]
+    algo = 2 * 4 * n + 8 * cfg["nbank"] * cfg["nchan"] * cfg["nif"]
+    return {"metric": "getkurtosis GB/s of filterbank input", "value": round(4 * n / ms / 1e6, 2),
+            "unit": "GB/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(el * 1e3 / args.steps, 4), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32->f64",
+            "data": "synthetic (bldp_synth_f32)",
+            "config": {"workload": "kurtosis over " + cfg["workload"], "name": args.config},
+            "roofline": {"bound": "hbm", "achieved": round(algo / ms / 1e6, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(algo / ms / 1e6 / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": "k_kurt_sum + k_kurt_mom (two reads of the window)"}}
+
+
+CFG5_PRODUCTS = ["cfg3", "cfg4", "cfg1"]  # 0000, 0001, 0002 single-bank geometry
+
+
+def bench_host(args, eng, torch, pkg):
+    """cfg5: a session scan streamed from pinned host memory.  This GPU's share
+    is bank b of every band: 4 bands x {0000, 0001, 0002}.  Each array goes
+    through bldp_reduce_host_f32 (the Julia worker drop-in: host array in,
+    reduced host array out).  Bound by PCIe (H2D), reported as such."""
+    import numpy as np
+
+    arrays = []
+    for band in range(4):
+        for name in CFG5_PRODUCTS:
+            c = CONFIGS[name]
+            t = eng.synth(c["nchan"], c["nif"], c["ntime"], c["nfpc"],
+                          seed=1000 * band + c["product"], kind=0)
+            h = torch.empty((c["ntime"], c["nif"], c["nchan"]), dtype=torch.float32,
+                            pin_memory=True)
+            h.copy_(t.permute(2, 1, 0))
+            del t
+            a = h.numpy().transpose(2, 1, 0)  # Julia-order, Fortran-contiguous, pinned
+            win = None if c["tw"] == c["ntime"] else [0, c["nchan"], 1, 0, c["nif"], 1, 0,
+                                                      c["tw"], 1]
+            arrays.append((a, h, c, win))
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    nbytes = sum(4 * c["nchan"] * c["nif"] * c["tw"] for _, _, c, _ in arrays)
+
+    def one_pass():
+        for a, _, c, win in arrays:
+            eng.reduce_host(a, c["F"], c["T"], "sum", win, device=torch.cuda.current_device())
+
+    for _ in range(max(1, args.warmup // 5)):
+        one_pass()
+    steps = max(1, args.steps // 10)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one_pass()
+    el = (time.perf_counter() - t0) / steps
+    gbs = nbytes / el / 1e9
+    del np
+    return {"metric": "session scan GB/s streamed from pinned host memory (per GPU)",
+            "value": round(gbs, 2), "unit": "GB/s", "n_gpus": 1, "steps": steps,
+            "warmup": max(1, args.warmup // 5), "ms_per_step": round(el * 1e3, 2),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic, pinned host memory (torch pin_memory)",
+            "config": {"workload": "cfg5 share of one GPU: 4 bands x {0000, 0001, 0002}, "
+                                   "bldp_reduce_host_f32 per array", "bytes_per_step": nbytes},
+            "roofline": {"bound": "pcie", "achieved": round(gbs, 2), "peak": 63.0,
+                         "unit": "GB/s", "frac": round(gbs / 63.0, 4), "traffic": None,
+                         "kernel": "H2D copy engine (PCIe Gen5 x16 spec 63 GB/s)"}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -115,6 +205,7 @@ def main():
     ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mode", default="reduce", choices=["reduce", "kurtosis", "host"])
     args = ap.parse_args()
 
     import torch
@@ -133,6 +224,13 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     cfg = CONFIGS[args.config]
+    if args.mode != "reduce":
+        if world != 1:
+            raise SystemExit("--mode kurtosis/host are single-GPU measurements")
+        r = (bench_kurtosis(args, cfg, eng, torch) if args.mode == "kurtosis"
+             else bench_host(args, eng, torch, pkg))
+        print(json.dumps(r), flush=True)
+        return r
     nb = cfg["nbank"]
     if nb % world:
         raise SystemExit(f"{nb} banks do not shard over {world} GPUs")

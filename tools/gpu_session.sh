@@ -38,6 +38,8 @@ for s in $STEPS; do
            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv \
              -d "$OUT/pmc_write" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     bench_*) run "$s" 600 python bench.py --config "${s#bench_}" ;;
+    kurt_*) run "$s" 600 python bench.py --mode kurtosis --config "${s#kurt_}" ;;
+    host)  run host 900 python bench.py --mode host ;;
     ab)    run ab 900 python tools/ab_variants.py --run --json "$OUT/ab.json" ;;
   esac
 done
