@@ -68,6 +68,21 @@ __device__ __forceinline__ float fold4(float4 v) {
 #ifndef BLDP_MAX_WG_PER_CU
 #define BLDP_MAX_WG_PER_CU 0
 #endif
+//   BLDP_NACC      independent float4 accumulators per lane (power of two <= 8)
+#ifndef BLDP_NACC
+#define BLDP_NACC 8
+#endif
+constexpr int kNacc = BLDP_NACC;
+
+// Pairwise fold of the per-lane accumulators into acc[0].
+template <int OP>
+__device__ __forceinline__ float4 fold_acc(float4 (&acc)[kNacc]) {
+#pragma unroll
+  for (int w = kNacc / 2; w >= 1; w /= 2)
+#pragma unroll
+    for (int q = 0; q < w; ++q) acc[q] = f4<OP>(acc[q], acc[q + w]);
+  return acc[0];
+}
 typedef float f4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float4 ld4(const float *p) {
 #if BLDP_NT_LOADS
@@ -127,9 +142,9 @@ __device__ __forceinline__ void vec_tile(const RedArgs &a, int64_t tile) {
   const int64_t r1 = min(a.T, r0 + a.rows_per_chunk);
   const float id = R<OP>::id();
 
-  float4 acc[8];
+  float4 acc[kNacc];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) acc[q] = make_float4(id, id, id, id);
+  for (int q = 0; q < kNacc; ++q) acc[q] = make_float4(id, id, id, id);
 
   if (valid) {
     const float *p = a.in[c.bank] + a.in_off + c.i * a.in_ld_i +
@@ -148,11 +163,11 @@ __device__ __forceinline__ void vec_tile(const RedArgs &a, int64_t tile) {
           for (int k = 0; k < K4C; ++k) v[u * K4C + k] = ld4(p + u * rstep + 4 * k * LPG);
         p += RB * rstep;
 #pragma unroll
-        for (int q = 0; q < NV; ++q) acc[q % 8] = f4<OP>(acc[q % 8], v[q]);
+        for (int q = 0; q < NV; ++q) acc[q % kNacc] = f4<OP>(acc[q % kNacc], v[q]);
       }
       for (; nrows > 0; --nrows) {
 #pragma unroll
-        for (int k = 0; k < K4C; ++k) acc[k % 8] = f4<OP>(acc[k % 8], ld4(p + 4 * k * LPG));
+        for (int k = 0; k < K4C; ++k) acc[k % kNacc] = f4<OP>(acc[k % kNacc], ld4(p + 4 * k * LPG));
         p += rstep;
       }
     } else {
@@ -164,18 +179,14 @@ __device__ __forceinline__ void vec_tile(const RedArgs &a, int64_t tile) {
 #pragma unroll
           for (int u = 0; u < 8; ++u) v[u] = ld4(p + 4 * (k + u) * LPG);
 #pragma unroll
-          for (int u = 0; u < 8; ++u) acc[u] = f4<OP>(acc[u], v[u]);
+          for (int u = 0; u < 8; ++u) acc[u % kNacc] = f4<OP>(acc[u % kNacc], v[u]);
         }
         for (; k < K4; ++k) acc[0] = f4<OP>(acc[0], ld4(p + 4 * k * LPG));
         p += rstep;
       }
     }
   }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) acc[q] = f4<OP>(acc[q], acc[q + 4]);
-  acc[0] = f4<OP>(acc[0], acc[2]);
-  acc[1] = f4<OP>(acc[1], acc[3]);
-  float s = fold4<OP>(f4<OP>(acc[0], acc[1]));
+  float s = fold4<OP>(fold_acc<OP>(acc));
 
   // combine the LPG lanes of a group (xor butterfly inside aligned segments)
 #pragma unroll
@@ -210,9 +221,9 @@ __device__ __forceinline__ void narrow_tile(const RedArgs &a, int64_t tile) {
   const int64_t r0 = c.chunk * a.rows_per_chunk;
   const int64_t r1 = min(a.T, r0 + a.rows_per_chunk);
   const float id = R<OP>::id();
-  float4 acc[8];
+  float4 acc[kNacc];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) acc[q] = make_float4(id, id, id, id);
+  for (int q = 0; q < kNacc; ++q) acc[q] = make_float4(id, id, id, id);
   const float *p =
       a.in[c.bank] + a.in_off + c.i * a.in_ld_i + (c.to * a.T + r0) * a.in_ld_t + 4 * q4;
   const int64_t st = a.in_ld_t;
@@ -223,17 +234,13 @@ __device__ __forceinline__ void narrow_tile(const RedArgs &a, int64_t tile) {
     for (int u = 0; u < BLDP_BATCH; ++u) v[u] = ld4(p + u * st);
     p += BLDP_BATCH * st;
 #pragma unroll
-    for (int u = 0; u < BLDP_BATCH; ++u) acc[u % 8] = f4<OP>(acc[u % 8], v[u]);
+    for (int u = 0; u < BLDP_BATCH; ++u) acc[u % kNacc] = f4<OP>(acc[u % kNacc], v[u]);
   }
   for (; nrows > 0; --nrows) {
     acc[0] = f4<OP>(acc[0], ld4(p));
     p += st;
   }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) acc[q] = f4<OP>(acc[q], acc[q + 4]);
-  acc[0] = f4<OP>(acc[0], acc[2]);
-  acc[1] = f4<OP>(acc[1], acc[3]);
-  float4 r = f4<OP>(acc[0], acc[1]);
+  float4 r = fold_acc<OP>(acc);
   const int64_t co = q4 * (4 / F);
   if (a.nchunk == 1) {
     float *o = a.out + c.bank * a.out_bank + c.i * a.out_ld_i + c.to * a.out_ld_t + co;
@@ -371,62 +378,96 @@ __global__ __launch_bounds__(kBlock) void k_despike(float *d, int64_t nchan, int
 }
 
 // ---------------------------------------------------------------------------
-// Kurtosis (StatsBase two-pass recipe).  Lanes map to channels (coalesced),
-// workgroups split time into chunks; FP64 partial moments.
-struct KCoord {
-  int64_t col, i, chunk;
-};
-__device__ __forceinline__ KCoord kdecompose(const KurtArgs &k, int64_t ncols) {
-  const int64_t bcs = (ncols + kBlock - 1) / kBlock;
-  int64_t b = blockIdx.x;
-  KCoord c;
-  const int64_t bc = b % bcs;
-  b /= bcs;
-  c.i = b % k.ni;
-  c.chunk = b / k.ni;
-  c.col = bc * kBlock + threadIdx.x;
-  return c;
-}
-
-template <int VEC>
-__global__ __launch_bounds__(kBlock) void k_kurt_sum(const KurtArgs k) {
+// Kurtosis (StatsBase two-pass recipe).  A tile is 64 lanes of columns
+// (float4 columns when 16-byte loads are legal) x one IF x one time chunk.
+// The 4 waves of a workgroup take every 4th spectrum of the chunk, each lane
+// keeping 8 loads in flight, and combine their Float64 partials through LDS
+// in wave order; chunks are folded in chunk order by k_kurt_mean/k_kurt_final.
+template <int PASS, int VEC>
+__global__ __launch_bounds__(kBlock) void k_kurt_pass(const KurtArgs k) {
+  constexpr int W = VEC ? 4 : 1;              // channels per lane
+  constexpr int NA = PASS == 0 ? W : 2 * W;   // Float64 accumulators per lane
+  constexpr int B = 8;                        // spectra in flight per lane
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t ncols = VEC ? k.nc / 4 : k.nc;
-  const KCoord c = kdecompose(k, ncols);
-  if (c.col >= ncols) return;
-  const int64_t r0 = c.chunk * k.rows_per_chunk, r1 = min(k.nt, r0 + k.rows_per_chunk);
-  const float *p = k.in + k.in_off + c.i * k.in_ld_i + r0 * k.in_ld_t +
-                   (VEC ? 4 * c.col : c.col * k.in_cs);
-  double s[4] = {0.0, 0.0, 0.0, 0.0};
-  int64_t n = r1 - r0;
-  if (VEC) {
-    for (; n >= 4; n -= 4) {
-      float4 v[4];
+  const int64_t ctiles = (ncols + 63) / 64;
+  int64_t b = blockIdx.x;
+  const int64_t ct = b % ctiles;
+  b /= ctiles;
+  const int64_t i = b % k.ni, chunk = b / k.ni;
+  const int64_t col = ct * 64 + lane;
+  const bool valid = col < ncols;
+  const int64_t r0 = chunk * k.rows_per_chunk, r1 = min(k.nt, r0 + k.rows_per_chunk);
+  double acc[NA];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = ld4(p + u * k.in_ld_t);
-      p += 4 * k.in_ld_t;
+  for (int a = 0; a < NA; ++a) acc[a] = 0.0;
+  if (valid) {
+    const float *p = k.in + k.in_off + i * k.in_ld_i + (r0 + wave) * k.in_ld_t +
+                     (VEC ? 4 * col : col * k.in_cs);
+    float m[W];
+    if (PASS == 1) {
+      const float *mp = k.mean + i * k.nc + (VEC ? 4 * col : col);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        s[0] += (double)v[u].x; s[1] += (double)v[u].y;
-        s[2] += (double)v[u].z; s[3] += (double)v[u].w;
+      for (int w = 0; w < W; ++w) m[w] = mp[w];
+    }
+    int64_t n = r1 - r0 - wave;
+    n = n > 0 ? (n + 3) / 4 : 0;
+    const int64_t st = 4 * k.in_ld_t;
+    auto fold = [&](const float *x) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        if (PASS == 0) {
+          acc[w] += (double)x[w];
+        } else {
+          // StatsBase: z = v[i] - m; z2 = z*z (Float32); cm2 += z2; cm4 += z2*z2
+          const float z = x[w] - m[w];
+          const float z2 = z * z;
+          acc[w] += (double)z2;
+          acc[W + w] += (double)(z2 * z2);
+        }
       }
-    }
-    for (; n > 0; --n, p += k.in_ld_t) {
-      const float4 v = ld4(p);
-      s[0] += (double)v.x; s[1] += (double)v.y; s[2] += (double)v.z; s[3] += (double)v.w;
-    }
-    double *o = k.ws_sum + (c.chunk * k.ni + c.i) * k.nc + 4 * c.col;
-    o[0] = s[0]; o[1] = s[1]; o[2] = s[2]; o[3] = s[3];
-  } else {
-    for (; n >= 4; n -= 4) {
-      float v[4];
+    };
+    for (; n >= B; n -= B) {
+      float v[B][W];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = p[u * k.in_ld_t];
-      p += 4 * k.in_ld_t;
+      for (int u = 0; u < B; ++u) {
+        if (VEC) {
+          const float4 q = ld4(p + u * st);
+          v[u][0] = q.x; v[u][W > 1 ? 1 : 0] = q.y;
+          v[u][W > 2 ? 2 : 0] = q.z; v[u][W > 3 ? 3 : 0] = q.w;
+        } else {
+          v[u][0] = p[u * st];
+        }
+      }
+      p += B * st;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) s[u] += (double)v[u];
+      for (int u = 0; u < B; ++u) fold(v[u]);
     }
-    for (; n > 0; --n, p += k.in_ld_t) s[0] += (double)p[0];
-    k.ws_sum[(c.chunk * k.ni + c.i) * k.nc + c.col] = (s[0] + s[1]) + (s[2] + s[3]);
+    for (; n > 0; --n, p += st) {
+      float v[W];
+      if (VEC) {
+        const float4 q = ld4(p);
+        v[0] = q.x; v[W > 1 ? 1 : 0] = q.y; v[W > 2 ? 2 : 0] = q.z; v[W > 3 ? 3 : 0] = q.w;
+      } else {
+        v[0] = p[0];
+      }
+      fold(v);
+    }
+  }
+  __shared__ double red[4][8][64];
+#pragma unroll
+  for (int a = 0; a < NA; ++a) red[wave][a][lane] = acc[a];
+  __syncthreads();
+  if (wave == 0 && valid) {
+    const int64_t n = k.ni * k.nc, e = i * k.nc + (VEC ? 4 * col : col);
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+      const double t = ((acc[a] + red[1][a][lane]) + red[2][a][lane]) + red[3][a][lane];
+      if (PASS == 0)
+        k.ws_sum[chunk * n + e + a] = t;
+      else
+        k.ws_mom[(chunk * 2 + a / W) * n + e + a % W] = t;
+    }
   }
 }
 
@@ -438,47 +479,6 @@ __global__ __launch_bounds__(kBlock) void k_kurt_mean(const KurtArgs k) {
     for (int ch = 0; ch < k.nchunk; ++ch) s += k.ws_sum[ch * n + e];
     // Statistics.mean on Float32: Float32 sum / length, in Float32
     k.mean[e] = (float)s / (float)k.nt;
-  }
-}
-
-template <int VEC>
-__global__ __launch_bounds__(kBlock) void k_kurt_mom(const KurtArgs k) {
-  const int64_t ncols = VEC ? k.nc / 4 : k.nc;
-  const KCoord c = kdecompose(k, ncols);
-  if (c.col >= ncols) return;
-  const int64_t r0 = c.chunk * k.rows_per_chunk, r1 = min(k.nt, r0 + k.rows_per_chunk);
-  const float *p = k.in + k.in_off + c.i * k.in_ld_i + r0 * k.in_ld_t +
-                   (VEC ? 4 * c.col : c.col * k.in_cs);
-  const int64_t mo = c.i * k.nc + (VEC ? 4 * c.col : c.col);
-  const int64_t n = k.ni * k.nc;
-  double *o2 = k.ws_mom + (c.chunk * 2) * n + mo;
-  double *o4 = o2 + n;
-  if (VEC) {
-    const float4 m = ld4(k.mean + mo);
-    double c2[4] = {0, 0, 0, 0}, c4[4] = {0, 0, 0, 0};
-    for (int64_t r = r0; r < r1; ++r, p += k.in_ld_t) {
-      const float4 v = ld4(p);
-      // StatsBase: z = v[i] - m (Float32); z2 = z*z (Float32);
-      // cm2 += z2; cm4 += z2*z2 (Float64 accumulators)
-      const float zx = v.x - m.x, zy = v.y - m.y, zz = v.z - m.z, zw = v.w - m.w;
-      const float qx = zx * zx, qy = zy * zy, qz = zz * zz, qw = zw * zw;
-      c2[0] += (double)qx; c2[1] += (double)qy; c2[2] += (double)qz; c2[3] += (double)qw;
-      c4[0] += (double)(qx * qx); c4[1] += (double)(qy * qy);
-      c4[2] += (double)(qz * qz); c4[3] += (double)(qw * qw);
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) { o2[u] = c2[u]; o4[u] = c4[u]; }
-  } else {
-    const float m = k.mean[mo];
-    double c2 = 0.0, c4 = 0.0;
-    for (int64_t r = r0; r < r1; ++r, p += k.in_ld_t) {
-      const float z = p[0] - m;
-      const float z2 = z * z;
-      c2 += (double)z2;
-      c4 += (double)(z2 * z2);
-    }
-    o2[0] = c2;
-    o4[0] = c4;
   }
 }
 
@@ -675,10 +675,10 @@ hipError_t launch_despike(float *d, int64_t nchan, int64_t nrows, int64_t nfpc, 
 
 void plan_kurtosis(KurtArgs &k, int num_cus) {
   const int64_t ncols = k.vec ? k.nc / 4 : k.nc;
-  const int64_t tiles = cdiv(ncols, 64) * k.ni;
-  const int64_t target = (int64_t)num_cus * 16;
+  const int64_t tiles = cdiv(ncols, 64) * k.ni;  // workgroups before a time split
+  const int64_t target = (int64_t)num_cus * 8;
   int64_t nchunk = 1;
-  if (tiles < target && k.nt >= 128) nchunk = std::min<int64_t>(cdiv(target, tiles), k.nt / 64);
+  if (tiles < target) nchunk = std::min<int64_t>(cdiv(target, tiles), k.nt / 64);
   nchunk = std::max<int64_t>(nchunk, 1);
   k.rows_per_chunk = std::max<int64_t>(1, cdiv(k.nt, nchunk));
   k.nchunk = (int32_t)std::max<int64_t>(1, cdiv(k.nt, k.rows_per_chunk));
@@ -700,17 +700,17 @@ hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s) {
   k.ws_mom = reinterpret_cast<double *>(ws + up(n * k.nchunk * sizeof(double)) +
                                         up(n * sizeof(float)));
   const int64_t ncols = k.vec ? k.nc / 4 : k.nc;
-  const dim3 grid((unsigned)(cdiv(ncols, kBlock) * k.ni * k.nchunk)), block(kBlock);
+  const dim3 grid((unsigned)(cdiv(ncols, 64) * k.ni * k.nchunk)), block(kBlock);
   const unsigned eg = (unsigned)std::min<int64_t>(cdiv((int64_t)n, kBlock), 8192);
   if (k.vec)
-    hipLaunchKernelGGL(k_kurt_sum<1>, grid, block, 0, s, k);
+    hipLaunchKernelGGL((k_kurt_pass<0, 1>), grid, block, 0, s, k);
   else
-    hipLaunchKernelGGL(k_kurt_sum<0>, grid, block, 0, s, k);
+    hipLaunchKernelGGL((k_kurt_pass<0, 0>), grid, block, 0, s, k);
   hipLaunchKernelGGL(k_kurt_mean, dim3(eg), block, 0, s, k);
   if (k.vec)
-    hipLaunchKernelGGL(k_kurt_mom<1>, grid, block, 0, s, k);
+    hipLaunchKernelGGL((k_kurt_pass<1, 1>), grid, block, 0, s, k);
   else
-    hipLaunchKernelGGL(k_kurt_mom<0>, grid, block, 0, s, k);
+    hipLaunchKernelGGL((k_kurt_pass<1, 0>), grid, block, 0, s, k);
   hipLaunchKernelGGL(k_kurt_final, dim3(eg), block, 0, s, k);
   return hipGetLastError();
 }

@@ -25,12 +25,11 @@ VDIR = os.path.join(REPO, "build", "variants")
 CSRC = os.path.join(REPO, "bldistributeddataproducts.jl_amd", "csrc")
 
 VARIANTS = {
-    "base": "",                                # nt loads, batch 8, one WG per tile
-    "plain": "-DBLDP_NT_LOADS=0",
-    "b4": "-DBLDP_BATCH=4",
+    "base": "",                                # nt loads, batch 8, 8 accumulators
+    "acc4": "-DBLDP_NACC=4",
+    "acc2": "-DBLDP_NACC=2",
+    "acc4_b4": "-DBLDP_NACC=4 -DBLDP_BATCH=4",
     "cap4": "-DBLDP_MAX_WG_PER_CU=4",
-    "cap8": "-DBLDP_MAX_WG_PER_CU=8",
-    "cap16": "-DBLDP_MAX_WG_PER_CU=16",
 }
 
 
