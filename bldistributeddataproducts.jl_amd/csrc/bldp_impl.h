@@ -60,6 +60,7 @@ struct KurtArgs {
   int64_t nc, ni, nt;
   int64_t rows_per_chunk;
   int32_t nchunk;
+  int32_t ts;   // waves of a workgroup splitting the spectra of a tile (1, 2, 4)
   int32_t vec;  // float4 along channels legal
   double *ws_sum;   // [nchunk][ni][nc]
   float *mean;      // [ni][nc]

@@ -321,20 +321,41 @@ __global__ __launch_bounds__(kBlock) void k_reduce_scalar(const RedArgs a) {
 // output in chunk order (deterministic), apply the mean divisor, scatter into
 // the (possibly stitched) output layout.
 template <int OP>
+__device__ __forceinline__ void reduce_store(const RedArgs &a, int64_t e, float s) {
+  int64_t r = e;
+  const int64_t co = r % a.nco;
+  r /= a.nco;
+  const int64_t i = r % a.ni;
+  r /= a.ni;
+  const int64_t to = r % a.nto;
+  const int64_t bank = r / a.nto;
+  a.out[bank * a.out_bank + i * a.out_ld_i + to * a.out_ld_t + co] = finish<OP>(s, a);
+}
+
+template <int OP>
 __global__ __launch_bounds__(kBlock) void k_reduce_finalize(const RedArgs a) {
   const int64_t per_chunk = (int64_t)a.nbank * a.nto * a.ni * a.nco;
   for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < per_chunk;
        e += (int64_t)gridDim.x * kBlock) {
     float s = a.ws[e];
     for (int ch = 1; ch < a.nchunk; ++ch) s = R<OP>::f(s, a.ws[ch * per_chunk + e]);
-    int64_t r = e;
-    const int64_t co = r % a.nco;
-    r /= a.nco;
-    const int64_t i = r % a.ni;
-    r /= a.ni;
-    const int64_t to = r % a.nto;
-    const int64_t bank = r / a.nto;
-    a.out[bank * a.out_bank + i * a.out_ld_i + to * a.out_ld_t + co] = finish<OP>(s, a);
+    reduce_store<OP>(a, e, s);
+  }
+}
+
+// Many chunks, few outputs: one wave per output, lanes take chunks lane,
+// lane+64, ... in order, then a fixed xor tree (deterministic).
+template <int OP>
+__global__ __launch_bounds__(kBlock) void k_reduce_finalize_w(const RedArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t per_chunk = (int64_t)a.nbank * a.nto * a.ni * a.nco;
+  for (int64_t e = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); e < per_chunk;
+       e += (int64_t)gridDim.x * 4) {
+    float s = R<OP>::id();
+    for (int ch = lane; ch < a.nchunk; ch += 64) s = R<OP>::f(s, a.ws[ch * per_chunk + e]);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s = R<OP>::f(s, __shfl_xor(s, off, 64));
+    if (lane == 0) reduce_store<OP>(a, e, s);
   }
 }
 
@@ -380,120 +401,140 @@ __global__ __launch_bounds__(kBlock) void k_despike(float *d, int64_t nchan, int
 // ---------------------------------------------------------------------------
 // Kurtosis (StatsBase two-pass recipe).  A tile is 64 lanes of columns
 // (float4 columns when 16-byte loads are legal) x one IF x one time chunk.
-// The 4 waves of a workgroup take every 4th spectrum of the chunk, each lane
-// keeping 8 loads in flight, and combine their Float64 partials through LDS
-// in wave order; chunks are folded in chunk order by k_kurt_mean/k_kurt_final.
+// `ts` waves of a workgroup split the spectra of a tile (4/ts tiles per
+// workgroup), each lane keeping 8 loads in flight, and combine their Float64
+// partials through LDS in wave order.  With one time chunk the epilogue is
+// fused (pass 0 writes the mean, pass 1 the kurtosis); otherwise chunks are
+// folded in a fixed order by k_kurt_fold.
 template <int PASS, int VEC>
 __global__ __launch_bounds__(kBlock) void k_kurt_pass(const KurtArgs k) {
   constexpr int W = VEC ? 4 : 1;              // channels per lane
   constexpr int NA = PASS == 0 ? W : 2 * W;   // Float64 accumulators per lane
   constexpr int B = 8;                        // spectra in flight per lane
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ts = k.ts, wt = wave / ts, tsi = wave - wt * ts;
   const int64_t ncols = VEC ? k.nc / 4 : k.nc;
-  const int64_t ctiles = (ncols + 63) / 64;
+  const int64_t ctiles = (ncols + 63) / 64, tpb = 4 / ts;
+  const int64_t cblocks = (ctiles + tpb - 1) / tpb;
   int64_t b = blockIdx.x;
-  const int64_t ct = b % ctiles;
-  b /= ctiles;
+  const int64_t cb = b % cblocks;
+  b /= cblocks;
   const int64_t i = b % k.ni, chunk = b / k.ni;
-  const int64_t col = ct * 64 + lane;
+  const int64_t col = (cb * tpb + wt) * 64 + lane;
   const bool valid = col < ncols;
   const int64_t r0 = chunk * k.rows_per_chunk, r1 = min(k.nt, r0 + k.rows_per_chunk);
+  const int64_t e = i * k.nc + (VEC ? 4 * col : col);  // first output of this lane
   double acc[NA];
 #pragma unroll
   for (int a = 0; a < NA; ++a) acc[a] = 0.0;
   if (valid) {
-    const float *p = k.in + k.in_off + i * k.in_ld_i + (r0 + wave) * k.in_ld_t +
+    const float *p = k.in + k.in_off + i * k.in_ld_i + (r0 + tsi) * k.in_ld_t +
                      (VEC ? 4 * col : col * k.in_cs);
     float m[W];
-    if (PASS == 1) {
-      const float *mp = k.mean + i * k.nc + (VEC ? 4 * col : col);
 #pragma unroll
-      for (int w = 0; w < W; ++w) m[w] = mp[w];
-    }
-    int64_t n = r1 - r0 - wave;
-    n = n > 0 ? (n + 3) / 4 : 0;
-    const int64_t st = 4 * k.in_ld_t;
-    auto fold = [&](const float *x) {
-#pragma unroll
-      for (int w = 0; w < W; ++w) {
-        if (PASS == 0) {
-          acc[w] += (double)x[w];
-        } else {
-          // StatsBase: z = v[i] - m; z2 = z*z (Float32); cm2 += z2; cm4 += z2*z2
-          const float z = x[w] - m[w];
-          const float z2 = z * z;
-          acc[w] += (double)z2;
-          acc[W + w] += (double)(z2 * z2);
-        }
-      }
-    };
-    for (; n >= B; n -= B) {
+    for (int w = 0; w < W; ++w) m[w] = PASS == 1 ? k.mean[e + w] : 0.0f;
+    int64_t n = r1 - r0 - tsi;
+    n = n > 0 ? (n + ts - 1) / ts : 0;
+    const int64_t st = (int64_t)ts * k.in_ld_t;
+    for (; n > 0; n -= B, p += B * st) {
+      // predicated batch: spectra past the end read as the mean (z = 0) / 0
       float v[B][W];
 #pragma unroll
       for (int u = 0; u < B; ++u) {
-        if (VEC) {
-          const float4 q = ld4(p + u * st);
-          v[u][0] = q.x; v[u][W > 1 ? 1 : 0] = q.y;
-          v[u][W > 2 ? 2 : 0] = q.z; v[u][W > 3 ? 3 : 0] = q.w;
+        if (u < n) {
+          if (VEC) {
+            const float4 q = ld4(p + u * st);
+            v[u][0] = q.x; v[u][W > 1 ? 1 : 0] = q.y;
+            v[u][W > 2 ? 2 : 0] = q.z; v[u][W > 3 ? 3 : 0] = q.w;
+          } else {
+            v[u][0] = p[u * st];
+          }
         } else {
-          v[u][0] = p[u * st];
+#pragma unroll
+          for (int w = 0; w < W; ++w) v[u][w] = m[w];
         }
       }
-      p += B * st;
 #pragma unroll
-      for (int u = 0; u < B; ++u) fold(v[u]);
+      for (int u = 0; u < B; ++u)
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          if (PASS == 0) {
+            acc[w] += (double)v[u][w];
+          } else {
+            // StatsBase: z = v[i] - m; z2 = z*z (Float32); cm2 += z2; cm4 += z2*z2
+            const float z = v[u][w] - m[w];
+            const float z2 = z * z;
+            acc[w] += (double)z2;
+            acc[W + w] += (double)(z2 * z2);
+          }
+        }
     }
-    for (; n > 0; --n, p += st) {
-      float v[W];
-      if (VEC) {
-        const float4 q = ld4(p);
-        v[0] = q.x; v[W > 1 ? 1 : 0] = q.y; v[W > 2 ? 2 : 0] = q.z; v[W > 3 ? 3 : 0] = q.w;
-      } else {
-        v[0] = p[0];
+  }
+  if (ts > 1) {
+    __shared__ double red[4][8][64];
+#pragma unroll
+    for (int a = 0; a < NA; ++a) red[wave][a][lane] = acc[a];
+    __syncthreads();
+    if (tsi == 0)
+      for (int q = 1; q < ts; ++q)
+#pragma unroll
+        for (int a = 0; a < NA; ++a) acc[a] += red[wave + q][a][lane];
+  }
+  if (tsi == 0 && valid) {
+    const int64_t n = k.ni * k.nc;
+    if (k.nchunk == 1) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        if (PASS == 0) {
+          k.mean[e + w] = (float)acc[w] / (float)k.nt;  // Float32 sum / length
+        } else {
+          const double cm2 = acc[w] / (double)k.nt, cm4 = acc[W + w] / (double)k.nt;
+          k.out[e + w] = (cm4 / (cm2 * cm2)) - 3.0;
+        }
       }
-      fold(v);
-    }
-  }
-  __shared__ double red[4][8][64];
+    } else {
 #pragma unroll
-  for (int a = 0; a < NA; ++a) red[wave][a][lane] = acc[a];
-  __syncthreads();
-  if (wave == 0 && valid) {
-    const int64_t n = k.ni * k.nc, e = i * k.nc + (VEC ? 4 * col : col);
-#pragma unroll
-    for (int a = 0; a < NA; ++a) {
-      const double t = ((acc[a] + red[1][a][lane]) + red[2][a][lane]) + red[3][a][lane];
-      if (PASS == 0)
-        k.ws_sum[chunk * n + e + a] = t;
-      else
-        k.ws_mom[(chunk * 2 + a / W) * n + e + a % W] = t;
+      for (int a = 0; a < NA; ++a) {
+        if (PASS == 0)
+          k.ws_sum[chunk * n + e + a] = acc[a];
+        else
+          k.ws_mom[(chunk * 2 + a / W) * n + e + a % W] = acc[a];
+      }
     }
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_kurt_mean(const KurtArgs k) {
+// Fold the time-chunk partials of every (channel, IF): one wave per output,
+// lanes take chunks lane, lane+64, ... in order, then a fixed xor tree.
+// PASS 0 -> mean (Float32), PASS 1 -> excess kurtosis (Float64).
+template <int PASS>
+__global__ __launch_bounds__(kBlock) void k_kurt_fold(const KurtArgs k) {
+  const int lane = threadIdx.x & 63;
   const int64_t n = k.ni * k.nc;
-  for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < n;
-       e += (int64_t)gridDim.x * kBlock) {
-    double s = 0.0;
-    for (int ch = 0; ch < k.nchunk; ++ch) s += k.ws_sum[ch * n + e];
-    // Statistics.mean on Float32: Float32 sum / length, in Float32
-    k.mean[e] = (float)s / (float)k.nt;
-  }
-}
-
-__global__ __launch_bounds__(kBlock) void k_kurt_final(const KurtArgs k) {
-  const int64_t n = k.ni * k.nc;
-  for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < n;
-       e += (int64_t)gridDim.x * kBlock) {
-    double cm2 = 0.0, cm4 = 0.0;
-    for (int ch = 0; ch < k.nchunk; ++ch) {
-      cm2 += k.ws_mom[(ch * 2) * n + e];
-      cm4 += k.ws_mom[(ch * 2 + 1) * n + e];
+  for (int64_t e = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); e < n;
+       e += (int64_t)gridDim.x * 4) {
+    double a = 0.0, c = 0.0;
+    for (int ch = lane; ch < k.nchunk; ch += 64) {
+      if (PASS == 0) {
+        a += k.ws_sum[ch * n + e];
+      } else {
+        a += k.ws_mom[(ch * 2) * n + e];
+        c += k.ws_mom[(ch * 2 + 1) * n + e];
+      }
     }
-    cm4 /= (double)k.nt;
-    cm2 /= (double)k.nt;
-    k.out[e] = (cm4 / (cm2 * cm2)) - 3.0;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      a += __shfl_xor(a, off, 64);
+      if (PASS == 1) c += __shfl_xor(c, off, 64);
+    }
+    if (lane == 0) {
+      if (PASS == 0) {
+        k.mean[e] = (float)a / (float)k.nt;
+      } else {
+        const double cm2 = a / (double)k.nt, cm4 = c / (double)k.nt;
+        k.out[e] = (cm4 / (cm2 * cm2)) - 3.0;
+      }
+    }
   }
 }
 
@@ -575,8 +616,13 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
   }
   if (e != hipSuccess || a.nchunk == 1) return e;
   const int64_t nout = (int64_t)a.nbank * a.nto * a.ni * a.nco;
-  const unsigned fg = (unsigned)std::min<int64_t>(cdiv(nout, kBlock), 8192);
-  hipLaunchKernelGGL((k_reduce_finalize<OP>), dim3(fg), block, 0, s, a);
+  if (a.nchunk > 16) {
+    const unsigned fg = (unsigned)std::min<int64_t>(cdiv(nout, 4), 16384);
+    hipLaunchKernelGGL((k_reduce_finalize_w<OP>), dim3(fg), block, 0, s, a);
+  } else {
+    const unsigned fg = (unsigned)std::min<int64_t>(cdiv(nout, kBlock), 8192);
+    hipLaunchKernelGGL((k_reduce_finalize<OP>), dim3(fg), block, 0, s, a);
+  }
   return hipGetLastError();
 }
 
@@ -675,10 +721,13 @@ hipError_t launch_despike(float *d, int64_t nchan, int64_t nrows, int64_t nfpc, 
 
 void plan_kurtosis(KurtArgs &k, int num_cus) {
   const int64_t ncols = k.vec ? k.nc / 4 : k.nc;
-  const int64_t tiles = cdiv(ncols, 64) * k.ni;  // workgroups before a time split
+  // waves splitting the spectra of a tile: keep >= 16 spectra per wave
+  k.ts = 1;
+  while (k.ts < 4 && k.nt >= (int64_t)32 * k.ts) k.ts *= 2;
+  const int64_t tiles = cdiv(cdiv(ncols, 64), 4 / k.ts) * k.ni;  // workgroups
   const int64_t target = (int64_t)num_cus * 8;
   int64_t nchunk = 1;
-  if (tiles < target) nchunk = std::min<int64_t>(cdiv(target, tiles), k.nt / 64);
+  if (tiles < target) nchunk = std::min<int64_t>(cdiv(target, tiles), k.nt / (16 * k.ts));
   nchunk = std::max<int64_t>(nchunk, 1);
   k.rows_per_chunk = std::max<int64_t>(1, cdiv(k.nt, nchunk));
   k.nchunk = (int32_t)std::max<int64_t>(1, cdiv(k.nt, k.rows_per_chunk));
@@ -700,18 +749,18 @@ hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s) {
   k.ws_mom = reinterpret_cast<double *>(ws + up(n * k.nchunk * sizeof(double)) +
                                         up(n * sizeof(float)));
   const int64_t ncols = k.vec ? k.nc / 4 : k.nc;
-  const dim3 grid((unsigned)(cdiv(ncols, 64) * k.ni * k.nchunk)), block(kBlock);
-  const unsigned eg = (unsigned)std::min<int64_t>(cdiv((int64_t)n, kBlock), 8192);
+  const dim3 grid((unsigned)(cdiv(cdiv(ncols, 64), 4 / k.ts) * k.ni * k.nchunk)), block(kBlock);
+  const unsigned fg = (unsigned)std::min<int64_t>(cdiv((int64_t)n, 4), 16384);
   if (k.vec)
     hipLaunchKernelGGL((k_kurt_pass<0, 1>), grid, block, 0, s, k);
   else
     hipLaunchKernelGGL((k_kurt_pass<0, 0>), grid, block, 0, s, k);
-  hipLaunchKernelGGL(k_kurt_mean, dim3(eg), block, 0, s, k);
+  if (k.nchunk > 1) hipLaunchKernelGGL(k_kurt_fold<0>, dim3(fg), block, 0, s, k);
   if (k.vec)
     hipLaunchKernelGGL((k_kurt_pass<1, 1>), grid, block, 0, s, k);
   else
     hipLaunchKernelGGL((k_kurt_pass<1, 0>), grid, block, 0, s, k);
-  hipLaunchKernelGGL(k_kurt_final, dim3(eg), block, 0, s, k);
+  if (k.nchunk > 1) hipLaunchKernelGGL(k_kurt_fold<1>, dim3(fg), block, 0, s, k);
   return hipGetLastError();
 }
 
