@@ -26,6 +26,7 @@ namespace bldp {
 namespace {
 
 constexpr int kBlock = 256;  // 4 waves of 64
+typedef float f4v __attribute__((ext_vector_type(4)));
 
 template <int OP>
 struct R {
@@ -68,6 +69,18 @@ __device__ __forceinline__ float fold4(float4 v) {
 #ifndef BLDP_MAX_WG_PER_CU
 #define BLDP_MAX_WG_PER_CU 0
 #endif
+//   BLDP_NT_STORES 1 = the narrow path's 16/8-byte output stores carry the nt hint
+#ifndef BLDP_NT_STORES
+#define BLDP_NT_STORES 0
+#endif
+__device__ __forceinline__ void st4(float *p, float4 r) {
+  const f4v v = {r.x, r.y, r.z, r.w};
+#if BLDP_NT_STORES
+  __builtin_nontemporal_store(v, reinterpret_cast<f4v *>(p));
+#else
+  *reinterpret_cast<f4v *>(p) = v;
+#endif
+}
 //   BLDP_NACC      independent float4 accumulators per lane (power of two <= 8)
 #ifndef BLDP_NACC
 #define BLDP_NACC 8
@@ -83,7 +96,6 @@ __device__ __forceinline__ float4 fold_acc(float4 (&acc)[kNacc]) {
     for (int q = 0; q < w; ++q) acc[q] = f4<OP>(acc[q], acc[q + w]);
   return acc[0];
 }
-typedef float f4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float4 ld4(const float *p) {
 #if BLDP_NT_LOADS
   const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(p));
@@ -248,7 +260,7 @@ __device__ __forceinline__ void narrow_tile(const RedArgs &a, int64_t tile) {
       r = make_float4(finish<OP>(r.x, a), finish<OP>(r.y, a), finish<OP>(r.z, a),
                       finish<OP>(r.w, a));
       if (a.vec_out) {
-        *reinterpret_cast<float4 *>(o) = r;
+        st4(o, r);
       } else {
         o[0] = r.x; o[1] = r.y; o[2] = r.z; o[3] = r.w;
       }
@@ -504,7 +516,32 @@ __global__ __launch_bounds__(kBlock) void k_kurt_pass(const KurtArgs k) {
   }
 }
 
-// Fold the time-chunk partials of every (channel, IF): one wave per output,
+// Fold the time-chunk partials of every (channel, IF), few chunks: one lane
+// per output, chunks in order.
+template <int PASS>
+__global__ __launch_bounds__(kBlock) void k_kurt_fold_t(const KurtArgs k) {
+  const int64_t n = k.ni * k.nc;
+  for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * kBlock) {
+    double a = 0.0, c = 0.0;
+    for (int ch = 0; ch < k.nchunk; ++ch) {
+      if (PASS == 0) {
+        a += k.ws_sum[ch * n + e];
+      } else {
+        a += k.ws_mom[(ch * 2) * n + e];
+        c += k.ws_mom[(ch * 2 + 1) * n + e];
+      }
+    }
+    if (PASS == 0) {
+      k.mean[e] = (float)a / (float)k.nt;
+    } else {
+      const double cm2 = a / (double)k.nt, cm4 = c / (double)k.nt;
+      k.out[e] = (cm4 / (cm2 * cm2)) - 3.0;
+    }
+  }
+}
+
+// Many chunks: one wave per output,
 // lanes take chunks lane, lane+64, ... in order, then a fixed xor tree.
 // PASS 0 -> mean (Float32), PASS 1 -> excess kurtosis (Float64).
 template <int PASS>
@@ -750,17 +787,28 @@ hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s) {
                                         up(n * sizeof(float)));
   const int64_t ncols = k.vec ? k.nc / 4 : k.nc;
   const dim3 grid((unsigned)(cdiv(cdiv(ncols, 64), 4 / k.ts) * k.ni * k.nchunk)), block(kBlock);
-  const unsigned fg = (unsigned)std::min<int64_t>(cdiv((int64_t)n, 4), 16384);
+  const bool wide = k.nchunk > 16;  // wave per output only when there is much to fold
+  const unsigned fg = (unsigned)std::min<int64_t>(cdiv((int64_t)n, wide ? 4 : kBlock), 16384);
   if (k.vec)
     hipLaunchKernelGGL((k_kurt_pass<0, 1>), grid, block, 0, s, k);
   else
     hipLaunchKernelGGL((k_kurt_pass<0, 0>), grid, block, 0, s, k);
-  if (k.nchunk > 1) hipLaunchKernelGGL(k_kurt_fold<0>, dim3(fg), block, 0, s, k);
+  if (k.nchunk > 1) {
+    if (wide)
+      hipLaunchKernelGGL(k_kurt_fold<0>, dim3(fg), block, 0, s, k);
+    else
+      hipLaunchKernelGGL(k_kurt_fold_t<0>, dim3(fg), block, 0, s, k);
+  }
   if (k.vec)
     hipLaunchKernelGGL((k_kurt_pass<1, 1>), grid, block, 0, s, k);
   else
     hipLaunchKernelGGL((k_kurt_pass<1, 0>), grid, block, 0, s, k);
-  if (k.nchunk > 1) hipLaunchKernelGGL(k_kurt_fold<1>, dim3(fg), block, 0, s, k);
+  if (k.nchunk > 1) {
+    if (wide)
+      hipLaunchKernelGGL(k_kurt_fold<1>, dim3(fg), block, 0, s, k);
+    else
+      hipLaunchKernelGGL(k_kurt_fold_t<1>, dim3(fg), block, 0, s, k);
+  }
   return hipGetLastError();
 }
 

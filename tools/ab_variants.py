@@ -26,9 +26,7 @@ CSRC = os.path.join(REPO, "bldistributeddataproducts.jl_amd", "csrc")
 
 VARIANTS = {
     "base": "",                                # nt loads, batch 8, 8 accumulators
-    "acc4": "-DBLDP_NACC=4",
-    "acc2": "-DBLDP_NACC=2",
-    "acc4_b4": "-DBLDP_NACC=4 -DBLDP_BATCH=4",
+    "ntst": "-DBLDP_NT_STORES=1",
     "cap4": "-DBLDP_MAX_WG_PER_CU=4",
 }
 
