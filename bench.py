@@ -206,6 +206,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", default="reduce", choices=["reduce", "kurtosis", "host"])
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo only to rehearse the N-rank path on one GPU")
     args = ap.parse_args()
 
     import torch
@@ -220,9 +222,13 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    local = local % max(1, torch.cuda.device_count())  # gloo rehearsal: ranks share GPUs
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     cfg = CONFIGS[args.config]
     if args.mode != "reduce":
         if world != 1:
@@ -280,7 +286,8 @@ def main():
     el = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
     if world > 1:
-        t = torch.tensor([el, kern_ms], dtype=torch.float64, device="cuda")
+        t = torch.tensor([el, kern_ms], dtype=torch.float64,
+                         device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el, kern_ms = float(t[0]), float(t[1])
     ms_step = el * 1e3 / args.steps

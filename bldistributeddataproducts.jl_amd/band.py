@@ -52,9 +52,13 @@ def band_reduce_dist(local_banks, fqavby=1, tavby=1, op="sum", win=None, root=0,
     block = local.permute(2, 1, 0).contiguous() if local.dim() == 3 else local
     if world == 1:
         return local
+    dev = block.device
+    if dist.get_backend(group) == "gloo" and block.is_cuda:
+        block = block.cpu()  # gloo rehearsal of the N-rank path (CPU transport)
     if rank == root:
         gathered = torch.empty((world, nto, ni, ncl), dtype=block.dtype, device=block.device)
         dist.gather(block, gather_list=list(gathered.unbind(0)), dst=root, group=group)
+        gathered = gathered.to(dev)
         if ni * nto == 1:
             res = gathered.reshape(world * ncl, 1, 1)
             if out is not None:

@@ -64,14 +64,17 @@ __device__ __forceinline__ float fold4(float4 v) {
 #ifndef BLDP_BATCH
 #define BLDP_BATCH 8
 #endif
-//   BLDP_MAX_WG_PER_CU  0 (default) = one workgroup per tile; N = grid capped
-//                  at N workgroups per CU, each looping over tiles
+//   BLDP_MAX_WG_PER_CU  -1 (default) = one workgroup per tile, except plans whose
+//                  waves split the time rows (long T blocks), which get a grid of
+//                  4 workgroups per CU looping over tiles (+3% on cfg4; -7% if
+//                  applied to cfg3); N >= 0 forces a cap of N per CU (0 = none)
 #ifndef BLDP_MAX_WG_PER_CU
-#define BLDP_MAX_WG_PER_CU 0
+#define BLDP_MAX_WG_PER_CU -1
 #endif
-//   BLDP_NT_STORES 1 = the narrow path's 16/8-byte output stores carry the nt hint
+//   BLDP_NT_STORES 1 (default) = the narrow path's 16-byte output stores carry
+//                  the nt hint; measured +5% on cfg3 F=1 (5.90 -> 6.21 TB/s)
 #ifndef BLDP_NT_STORES
-#define BLDP_NT_STORES 0
+#define BLDP_NT_STORES 1
 #endif
 __device__ __forceinline__ void st4(float *p, float4 r) {
   const f4v v = {r.x, r.y, r.z, r.w};
@@ -709,7 +712,8 @@ Plan plan_reduce(RedArgs &a, bool aligned, int num_cus) {
   p.ws_bytes = a.nchunk > 1 ? (size_t)a.nchunk * a.nbank * p.nout * sizeof(float) : 0;
   a.ntiles = a.blocks_c * a.ni * a.nchunk * a.nto * a.nbank;
   p.grid = a.ntiles;
-  if (BLDP_MAX_WG_PER_CU > 0) p.grid = std::min<int64_t>(p.grid, (int64_t)BLDP_MAX_WG_PER_CU * num_cus);
+  const int cap = BLDP_MAX_WG_PER_CU >= 0 ? BLDP_MAX_WG_PER_CU : (a.ts > 1 ? 4 : 0);
+  if (cap > 0) p.grid = std::min<int64_t>(p.grid, (int64_t)cap * num_cus);
   // narrow-path vector stores
   a.vec_out = 0;
   if (p.path == PATH_NARROW) {

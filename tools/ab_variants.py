@@ -25,9 +25,9 @@ VDIR = os.path.join(REPO, "build", "variants")
 CSRC = os.path.join(REPO, "bldistributeddataproducts.jl_amd", "csrc")
 
 VARIANTS = {
-    "base": "",                                # nt loads, batch 8, 8 accumulators
-    "ntst": "-DBLDP_NT_STORES=1",
-    "cap4": "-DBLDP_MAX_WG_PER_CU=4",
+    "base": "",                          # nt loads+stores, batch 8, cap 4 WG/CU iff ts > 1
+    "nocap": "-DBLDP_MAX_WG_PER_CU=0",
+    "plain": "-DBLDP_NT_LOADS=0 -DBLDP_NT_STORES=0 -DBLDP_MAX_WG_PER_CU=0",  # round-1 start
 }
 
 
