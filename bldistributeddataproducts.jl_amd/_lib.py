@@ -61,6 +61,10 @@ SIGNATURES = {
     "bldp_kurtosis_host_f32": ([I, P, I64, I64, I64, P, P], I),
     "bldp_fqav_range": ([D, D, I64, I64, P, P, P], I),
     "bldp_synth_f32": ([P, I64, I64, I64, I64, U64, I, P], I),
+    "bldp_bslz4_info": ([P, SZ, P, P], I),
+    "bldp_unchunk_f32": ([P, P, P, P, P, P, P], I),
+    "bldp_bslz4_decode_host": ([P, SZ, I, P, SZ], I),
+    "bldp_bslz4_decode_dev": ([I, P, P, P, P, I, P, P, P], I),
 }
 
 _lib = None

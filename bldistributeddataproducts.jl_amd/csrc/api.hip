@@ -127,7 +127,9 @@ struct Scratch {
 std::mutex g_ws_mu;
 std::map<std::pair<int, void *>, Scratch> g_ws;
 
-int scratch(hipStream_t s, size_t bytes, void **out) {
+}  // namespace
+
+int bldp::scratch_bytes(hipStream_t s, size_t bytes, void **out) {
   int dev = 0;
   HIPCHK(hipGetDevice(&dev));
   std::lock_guard<std::mutex> lk(g_ws_mu);
@@ -149,6 +151,10 @@ int scratch(hipStream_t s, size_t bytes, void **out) {
   *out = w.ptr;
   return BLDP_OK;
 }
+
+namespace {
+
+int scratch(hipStream_t s, size_t bytes, void **out) { return bldp::scratch_bytes(s, bytes, out); }
 
 bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
 
@@ -392,6 +398,29 @@ int bldp_fqav_range(double first, double step, int64_t len, int64_t n, double *o
   *out_first = first + (double)(n - 1) * step / 2.0;  // :29
   *out_step = (double)n * step;                        // :30
   *out_len = len / n;                                  // :31 (floor)
+  return BLDP_OK;
+}
+
+int bldp_unchunk_f32(const float *packed, const int64_t chunk[3], const int64_t box0[3],
+                     const int64_t grid[3], const int64_t *win, float *out, void *stream) {
+  if (!chunk || !box0 || !grid || !win) return fail(BLDP_EINVAL, "null pointer");
+  UnchunkArgs u{chunk[0], chunk[1], chunk[2], box0[0], box0[1], box0[2], grid[0], grid[1],
+                grid[2], win[0], win[1], win[2], win[3], win[4], win[5], win[6], win[7], win[8]};
+  if (u.ct <= 0 || u.ci <= 0 || u.cc <= 0 || u.gt <= 0 || u.gi <= 0 || u.gc <= 0)
+    return fail(BLDP_EINVAL, "bad chunk geometry");
+  // every window element must fall inside the chunk box (no out-of-range reads)
+  const int64_t ext[3][3] = {{u.c0, u.nc, u.cs}, {u.i0, u.ni, u.is}, {u.t0, u.nt, u.ts}};
+  const int64_t lo[3] = {u.bc0, u.bi0, u.bt0}, len[3] = {u.gc * u.cc, u.gi * u.ci, u.gt * u.ct};
+  for (int a = 0; a < 3; ++a) {
+    if (ext[a][1] < 0) return fail(BLDP_EINVAL, "negative window count");
+    if (ext[a][1] == 0) return BLDP_OK;
+    const int64_t first = ext[a][0], last = ext[a][0] + (ext[a][1] - 1) * ext[a][2];
+    if (std::min(first, last) < lo[a] || std::max(first, last) >= lo[a] + len[a])
+      return fail(BLDP_EBOUNDS, "window axis %d outside the decoded chunk box", a + 1);
+  }
+  if (!packed || !out) return fail(BLDP_EINVAL, "null pointer");
+  hipError_t e = launch_unchunk(packed, u, out, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(BLDP_EHIP, "unchunk launch: %s", hipGetErrorString(e));
   return BLDP_OK;
 }
 

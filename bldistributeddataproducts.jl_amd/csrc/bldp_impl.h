@@ -10,6 +10,10 @@ namespace bldp {
 // Record the thread-local error message returned by bldp_last_error; returns code.
 int set_error(int code, const char *fmt, ...);
 
+// Library-owned device scratch cached per (device, stream); growing it
+// synchronizes that stream first.
+int scratch_bytes(hipStream_t s, size_t bytes, void **out);
+
 // One reduction launch: nbank banks with identical geometry.
 // Window element (c, i, t) of bank b sits at
 //   in[b][in_off + c*in_cs + i*in_ld_i + t*in_ld_t]
@@ -70,6 +74,15 @@ struct KurtArgs {
 void plan_kurtosis(KurtArgs &k, int num_cus);
 size_t kurtosis_ws_bytes(const KurtArgs &k);
 hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s);
+
+// Window of a chunked dataset: chunk dims (ct, ci, cc) in C order, a chunk
+// bounding box starting at (bt0, bi0, bc0) with (gt, gi, gc) chunks, and the
+// window {c0, nc, cs, i0, ni, is, t0, nt, ts} in dataset coordinates.
+struct UnchunkArgs {
+  int64_t ct, ci, cc, bt0, bi0, bc0, gt, gi, gc;
+  int64_t c0, nc, cs, i0, ni, is, t0, nt, ts;
+};
+hipError_t launch_unchunk(const float *packed, const UnchunkArgs &u, float *out, hipStream_t s);
 
 hipError_t launch_synth(float *out, int64_t nchan, int64_t nif, int64_t ntime, int64_t nfpc,
                         uint64_t seed, int kind, hipStream_t s);

@@ -828,3 +828,37 @@ hipError_t launch_synth(float *out, int64_t nchan, int64_t nif, int64_t ntime, i
 }
 
 }  // namespace bldp
+
+// ---------------------------------------------------------------------------
+// Window gather from decoded HDF5 chunks (the bitshuffle/LZ4 read path).
+// The chunks covering the window are decoded back to back in chunk-grid
+// order [gt][gi][gc] (each chunk C-order [ct][ci][cc]); this copies the
+// window (nc, ni, nt) out of them into a dense Julia-order tensor.
+namespace bldp {
+namespace {
+__global__ __launch_bounds__(256) void k_unchunk(const float *__restrict__ packed,
+                                                 UnchunkArgs u, float *__restrict__ out) {
+  const int64_t n = u.nc * u.ni * u.nt;
+  const int64_t cvol = u.ct * u.ci * u.cc;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * 256) {
+    const int64_t c = e % u.nc, r = e / u.nc, i = r % u.ni, t = r / u.ni;
+    // absolute dataset coordinates, then relative to the chunk bounding box
+    const int64_t gc = u.c0 + c * u.cs - u.bc0, gi = u.i0 + i * u.is - u.bi0,
+                  gt = u.t0 + t * u.ts - u.bt0;
+    const int64_t kc = gc / u.cc, ki = gi / u.ci, kt = gt / u.ct;
+    const int64_t slot = (kt * u.gi + ki) * u.gc + kc;
+    out[e] = packed[slot * cvol + ((gt - kt * u.ct) * u.ci + (gi - ki * u.ci)) * u.cc +
+                    (gc - kc * u.cc)];
+  }
+}
+}  // namespace
+
+hipError_t launch_unchunk(const float *packed, const UnchunkArgs &u, float *out, hipStream_t s) {
+  const int64_t n = u.nc * u.ni * u.nt;
+  if (n == 0) return hipSuccess;
+  const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 65536);
+  hipLaunchKernelGGL(k_unchunk, dim3(grid), dim3(256), 0, s, packed, u, out);
+  return hipGetLastError();
+}
+}  // namespace bldp

@@ -87,6 +87,21 @@ class _H5:
             "H5Pset_deflate": ([hid_t, ctypes.c_uint], herr_t),
             "H5Dvlen_reclaim": ([hid_t, hid_t, hid_t, ctypes.c_void_p], herr_t),
             "H5Eset_auto2": ([hid_t, ctypes.c_void_p, ctypes.c_void_p], herr_t),
+            "H5Dget_create_plist": ([hid_t], hid_t),
+            "H5Pget_layout": ([hid_t], ctypes.c_int),
+            "H5Pget_chunk": ([hid_t, ctypes.c_int, ctypes.c_void_p], ctypes.c_int),
+            "H5Pget_nfilters": ([hid_t], ctypes.c_int),
+            "H5Pget_filter2": ([hid_t, ctypes.c_uint, ctypes.c_void_p, ctypes.c_void_p,
+                                ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p,
+                                ctypes.c_void_p], ctypes.c_int),
+            "H5Pset_filter": ([hid_t, ctypes.c_int, ctypes.c_uint, ctypes.c_size_t,
+                               ctypes.c_void_p], herr_t),
+            "H5Zfilter_avail": ([ctypes.c_int], ctypes.c_int),
+            "H5Dget_chunk_storage_size": ([hid_t, ctypes.c_void_p, ctypes.c_void_p], herr_t),
+            "H5Dread_chunk": ([hid_t, hid_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p],
+                              herr_t),
+            "H5Dwrite_chunk": ([hid_t, hid_t, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t,
+                                ctypes.c_void_p], herr_t),
         }
         for name, (a, r) in sig.items():
             f = getattr(L, name)
@@ -141,7 +156,11 @@ def _dims(space) -> tuple:
 
 def read_window(fname, idxs) -> np.ndarray:
     """h5["data"][idxs...] as a Fortran-ordered float32 (nc, ni, nt) array
-    (src/gbtworkerfunctions.jl:181-187; whole dataset for (:,:,:))."""
+    (src/gbtworkerfunctions.jl:181-187; whole dataset for (:,:,:)).
+    Bitshuffle/LZ4 chunks that libhdf5 cannot decode (no filter plugin) are
+    read raw and decoded by libbldp_hip (host C++ decoder)."""
+    if needs_bslz4(fname):
+        return read_window_bslz4(fname, idxs, device=None)
     H5 = h5()
     H = H5.L
     f = _ok(H.H5Fopen(os.fsencode(fname), H5F_ACC_RDONLY, H5P_DEFAULT), f"open {fname}")
@@ -348,3 +367,282 @@ def _write_attr(H5, obj, name, v):
         H.H5Sclose(sp)
         if close_t:
             H.H5Tclose(t)
+
+
+# --------------------------------------------------------------------------
+# HDF5 filter 32008 (bitshuffle + LZ4) chunk decoding through libbldp_hip
+# --------------------------------------------------------------------------
+BSHUF_FILTER_ID = 32008
+
+
+def bslz4_info(chunk: bytes) -> tuple[int, int]:
+    """(uncompressed bytes, block bytes) of a bitshuffle-LZ4 chunk."""
+    from . import _lib
+
+    nb, bb = ctypes.c_uint64(), ctypes.c_uint32()
+    buf = np.frombuffer(chunk, np.uint8)
+    _lib.check(_lib.lib().bldp_bslz4_info(buf.ctypes.data, buf.size, ctypes.byref(nb),
+                                          ctypes.byref(bb)), "bldp_bslz4_info")
+    return nb.value, bb.value
+
+
+def bslz4_decode_host(chunk: bytes, dtype=np.float32) -> np.ndarray:
+    """Decode one chunk on the host (C++ in libbldp_hip)."""
+    from . import _lib
+
+    nb, _ = bslz4_info(chunk)
+    es = np.dtype(dtype).itemsize
+    out = np.empty(nb // es, dtype=dtype)
+    buf = np.frombuffer(chunk, np.uint8)
+    _lib.check(_lib.lib().bldp_bslz4_decode_host(buf.ctypes.data, buf.size, es,
+                                                 out.ctypes.data if out.size else None, nb),
+               "bldp_bslz4_decode_host")
+    return out
+
+
+def bslz4_decode_dev(chunks, dtype=np.float32, device=None, stream=None, out=None,
+                     out_offsets=None):
+    """Decode a list of chunks on the GPU in one launch: only the compressed
+    bytes cross PCIe.  Without ``out`` the chunks land back to back in a new
+    1-D device tensor; with ``out``/``out_offsets`` (bytes) they land there."""
+    import torch
+
+    from . import _lib
+
+    es = np.dtype(dtype).itemsize
+    sizes = [bslz4_info(c)[0] for c in chunks]
+    comp = np.frombuffer(b"".join(bytes(c) for c in chunks), np.uint8)
+    coff = np.cumsum([0] + [len(c) for c in chunks[:-1]]).astype(np.uint64)
+    clen = np.array([len(c) for c in chunks], np.uint64)
+    if out is None:
+        dev = torch.device(device or "cuda")
+        tdt = {4: torch.float32, 8: torch.float64, 2: torch.int16, 1: torch.uint8}[es]
+        out = torch.empty(sum(sizes) // es, dtype=tdt, device=dev)
+        ooff = np.cumsum([0] + sizes[:-1]).astype(np.uint64)
+    else:
+        dev = out.device
+        ooff = np.asarray(out_offsets, np.uint64)
+        cap = out.numel() * out.element_size()
+        if len(ooff) != len(chunks) or any(int(o) + s > cap for o, s in zip(ooff, sizes)):
+            raise ValueError("decoded chunks do not fit the output tensor")
+    cdev = torch.from_numpy(comp.copy()).to(dev) if comp.size else None
+    rc = _lib.lib().bldp_bslz4_decode_dev(
+        len(chunks), comp.ctypes.data, cdev.data_ptr() if cdev is not None else None,
+        coff.ctypes.data, clen.ctypes.data, es, out.data_ptr(), ooff.ctypes.data,
+        _lib.stream_ptr(stream))
+    _lib.check(rc, "bldp_bslz4_decode_dev")
+    return out
+
+
+# --------------------------------------------------------------------------
+# Chunked datasets with filter 32008: direct chunk reads + our decoder
+# --------------------------------------------------------------------------
+H5D_CHUNKED = 2
+
+
+def layout(fname) -> dict:
+    """Dataset dims (C order), chunk dims and filter pipeline of ``data``."""
+    H5 = h5()
+    H = H5.L
+    f = _ok(H.H5Fopen(os.fsencode(fname), H5F_ACC_RDONLY, H5P_DEFAULT), f"open {fname}")
+    try:
+        d = _ok(H.H5Dopen2(f, b"data", H5P_DEFAULT), "open dataset 'data'")
+        try:
+            fs = H.H5Dget_space(d)
+            cdims = _dims(fs)
+            H.H5Sclose(fs)
+            pl = _ok(H.H5Dget_create_plist(d), "create_plist")
+            try:
+                chunk = None
+                if H.H5Pget_layout(pl) == H5D_CHUNKED:
+                    cd = (hsize_t * 8)()
+                    nd = H.H5Pget_chunk(pl, 8, cd)
+                    chunk = tuple(int(cd[k]) for k in range(nd))
+                filters = []
+                for k in range(max(0, H.H5Pget_nfilters(pl))):
+                    flags, nel = ctypes.c_uint(), ctypes.c_size_t(16)
+                    vals = (ctypes.c_uint * 16)()
+                    name = ctypes.create_string_buffer(64)
+                    cfg = ctypes.c_uint()
+                    fid = H.H5Pget_filter2(pl, k, ctypes.byref(flags), ctypes.byref(nel), vals,
+                                           64, name, ctypes.byref(cfg))
+                    filters.append(dict(id=fid, flags=flags.value,
+                                        cd_values=[vals[j] for j in range(min(nel.value, 16))],
+                                        name=name.value.decode(errors="replace"),
+                                        available=H.H5Zfilter_avail(fid) > 0))
+            finally:
+                H.H5Pclose(pl)
+        finally:
+            H.H5Dclose(d)
+    finally:
+        H.H5Fclose(f)
+    return dict(cdims=cdims, chunk=chunk, filters=filters)
+
+
+def needs_bslz4(fname) -> bool:
+    """True when ``data`` is bitshuffle/LZ4-compressed and libhdf5 has no
+    plugin for filter 32008 (the case of this image)."""
+    lay = layout(fname)
+    ids = [f["id"] for f in lay["filters"]]
+    if BSHUF_FILTER_ID not in ids:
+        return False
+    if all(f["available"] for f in lay["filters"]):
+        return False
+    if ids != [BSHUF_FILTER_ID]:
+        raise BLDPError(-1, f"{fname}: filter pipeline {ids} not supported (only 32008 alone)")
+    return True
+
+
+def _box(win_axis, cdim):
+    st, ct, sp = win_axis
+    if ct == 0:
+        return 0, 1
+    last = st + (ct - 1) * sp
+    lo, hi = min(st, last), max(st, last)
+    return lo // cdim, hi // cdim - lo // cdim + 1
+
+
+def read_chunks(fname, idxs):
+    """Raw chunks covering the window, in chunk-grid order.  Returns
+    (jshape, window, chunk dims (t, i, c), box origin (t, i, c), grid (t, i, c),
+    [(filter_mask, bytes or None)])."""
+    lay = layout(fname)
+    cdims, chunk = lay["cdims"], lay["chunk"]
+    if chunk is None or len(cdims) != 3:
+        raise BLDPError(-1, f"{fname}: data is not a chunked 3-D dataset")
+    jshape = cdims[::-1]
+    win = to_window(idxs, jshape) or [0, jshape[0], 1, 0, jshape[1], 1, 0, jshape[2], 1]
+    for ax in range(3):
+        st, ct, sp = win[3 * ax: 3 * ax + 3]
+        if ct > 0:
+            last = st + (ct - 1) * sp
+            if min(st, last) < 0 or max(st, last) >= jshape[ax]:
+                raise BoundsError(-6, f"BoundsError: axis {ax + 1} window {st + 1}:{sp}:"
+                                      f"{last + 1} of {jshape[ax]}")
+    # C order axes: t = Julia axis 3, i = axis 2, c = axis 1
+    kt0, gt = _box(win[6:9], chunk[0])
+    ki0, gi = _box(win[3:6], chunk[1])
+    kc0, gc = _box(win[0:3], chunk[2])
+    H5 = h5()
+    H = H5.L
+    out = []
+    f = _ok(H.H5Fopen(os.fsencode(fname), H5F_ACC_RDONLY, H5P_DEFAULT), f"open {fname}")
+    try:
+        d = _ok(H.H5Dopen2(f, b"data", H5P_DEFAULT), "open dataset 'data'")
+        try:
+            for a in range(gt):
+                for b in range(gi):
+                    for c in range(gc):
+                        off = _hs([(kt0 + a) * chunk[0], (ki0 + b) * chunk[1],
+                                   (kc0 + c) * chunk[2]])
+                        nb = hsize_t()
+                        if H.H5Dget_chunk_storage_size(d, off, ctypes.byref(nb)) < 0 or \
+                                nb.value == 0:
+                            out.append((0, None))  # never written: fill value (0)
+                            continue
+                        buf = ctypes.create_string_buffer(nb.value)
+                        mask = ctypes.c_uint32()
+                        _ok(H.H5Dread_chunk(d, H5P_DEFAULT, off, ctypes.byref(mask), buf),
+                            "read_chunk")
+                        out.append((mask.value, buf.raw))
+        finally:
+            H.H5Dclose(d)
+    finally:
+        H.H5Fclose(f)
+    box0 = (kt0 * chunk[0], ki0 * chunk[1], kc0 * chunk[2])
+    return jshape, win, tuple(chunk), box0, (gt, gi, gc), out
+
+
+def read_window_bslz4(fname, idxs, device=None):
+    """The window of a bitshuffle/LZ4 dataset.  device=None: decode on the
+    host (C++), return a Fortran-ordered numpy array.  device="cuda:k":
+    compressed bytes go to the GPU, are decoded there (bldp_bslz4_decode_dev)
+    and the window is gathered on the device (bldp_unchunk_f32); returns a
+    Julia-order device tensor."""
+    from . import _lib
+
+    jshape, win, chunk, box0, grid, raw = read_chunks(fname, idxs)
+    cvol = int(np.prod(chunk))
+    nc, ni, nt = win[1], win[4], win[7]
+    if device is None:
+        packed = np.zeros(len(raw) * cvol, np.float32)
+        for k, (mask, b) in enumerate(raw):
+            if b is None:
+                continue
+            dst = packed[k * cvol:(k + 1) * cvol]
+            if mask & 1:  # filter skipped for this chunk: raw elements
+                dst[:] = np.frombuffer(b, np.float32, count=cvol)
+            else:
+                dst[:] = bslz4_decode_host(b)[:cvol]
+        if nc * ni * nt == 0:
+            return np.zeros((nc, ni, nt), np.float32, order="F")
+        P = packed.reshape((grid[0], grid[1], grid[2]) + chunk)  # [gt][gi][gc][ct][ci][cc]
+        ax = []
+        for a, (o, kdim) in zip((6, 3, 0), zip(box0, chunk)):
+            ax.append(win[a] + win[a + 2] * np.arange(win[a + 1]) - o)
+        t, i, c = np.ix_(*ax)
+        w = P[t // chunk[0], i // chunk[1], c // chunk[2], t % chunk[0], i % chunk[1],
+              c % chunk[2]]  # [t][i][c]
+        return np.asfortranarray(np.transpose(w, (2, 1, 0)))
+    import torch
+
+    from . import engine
+
+    dev = torch.device(device)
+    packed = torch.zeros(len(raw) * cvol, dtype=torch.float32, device=dev)
+    comp = [(k, b) for k, (m, b) in enumerate(raw) if b is not None and not m & 1]
+    for k, (m, b) in enumerate(raw):
+        if b is not None and m & 1:
+            packed[k * cvol:(k + 1) * cvol].copy_(
+                torch.from_numpy(np.frombuffer(b, np.float32, count=cvol).copy()))
+    with torch.cuda.device(dev):
+        if comp:
+            bslz4_decode_dev([b for _, b in comp], out=packed,
+                             out_offsets=[4 * k * cvol for k, _ in comp])
+        out = engine.fb_empty(nc, ni, nt, device=dev)
+        if out.numel():
+            keep = [(ctypes.c_int64 * 3)(*v) for v in (chunk, box0, grid)]
+            w9 = (ctypes.c_int64 * 9)(*win)
+            rc = _lib.lib().bldp_unchunk_f32(packed.data_ptr(), keep[0], keep[1], keep[2], w9,
+                                             out.data_ptr(), _lib.stream_ptr())
+            _lib.check(rc, "bldp_unchunk_f32")
+    return out
+
+
+def write_bslz4(fname, attrs: dict, data: np.ndarray, chunk, encode) -> None:
+    """Test helper: an FBH5 file whose ``data`` carries filter 32008 (bitshuffle,
+    LZ4) with chunks written raw through H5Dwrite_chunk; ``encode(array) ->
+    bytes`` produces each chunk.  The filter is marked optional so libhdf5
+    accepts the pipeline without the plugin."""
+    H5 = h5()
+    H = H5.L
+    a = np.asfortranarray(np.asarray(data, dtype=np.float32))
+    cdims = a.shape[::-1]
+    c = np.ascontiguousarray(a.transpose(2, 1, 0))
+    f = _ok(H.H5Fcreate(os.fsencode(fname), H5F_ACC_TRUNC, H5P_DEFAULT, H5P_DEFAULT), "create")
+    try:
+        sp = _ok(H.H5Screate_simple(3, _hs(cdims), None), "space")
+        dcpl = _ok(H.H5Pcreate(H5.DATASET_CREATE), "dcpl")
+        _ok(H.H5Pset_chunk(dcpl, 3, _hs(chunk)), "set_chunk")
+        cd = (ctypes.c_uint * 5)(0, 3, 4, 0, 2)  # bitshuffle version, elem size, auto, LZ4
+        _ok(H.H5Pset_filter(dcpl, BSHUF_FILTER_ID, 1, 5, cd), "set_filter 32008")
+        d = _ok(H.H5Dcreate2(f, b"data", H5.NATIVE_FLOAT, sp, H5P_DEFAULT, dcpl, H5P_DEFAULT),
+                "create dataset")
+        H.H5Pclose(dcpl)
+        H.H5Sclose(sp)
+        try:
+            for t0 in range(0, cdims[0], chunk[0]):
+                for i0 in range(0, cdims[1], chunk[1]):
+                    for c0 in range(0, cdims[2], chunk[2]):
+                        blk = np.zeros(chunk, np.float32)  # edge chunks are padded
+                        part = c[t0:t0 + chunk[0], i0:i0 + chunk[1], c0:c0 + chunk[2]]
+                        blk[:part.shape[0], :part.shape[1], :part.shape[2]] = part
+                        enc = encode(blk)
+                        _ok(H.H5Dwrite_chunk(d, H5P_DEFAULT, 0, _hs([t0, i0, c0]), len(enc),
+                                             enc), "write_chunk")
+            for k, v in dict(attrs, DIMENSION_LABELS=["time", "feed_id", "frequency"]).items():
+                _write_attr(H5, d, k, v)
+        finally:
+            H.H5Dclose(d)
+    finally:
+        H.H5Fclose(f)

@@ -158,7 +158,19 @@ def getfbh5data(fbh5name, idxs=(COLON, COLON, COLON), fqavby=1, fqavfunc="sum", 
     """FBH5: read the window (whole dataset for (:,:,:)), then reduce
     (src/gbtworkerfunctions.jl:179-189)."""
     assert len(idxs) == 3, "idxs must have exactly three indices"  # :180
-    data = readers.fbh5_read(fbh5name, sanitizeidxs(idxs))
+    idxs = sanitizeidxs(idxs)
+    op = _opname(fqavfunc)
+    from . import fbh5
+
+    if op is not None and fbh5.needs_bslz4(fbh5name):
+        # compressed rawspec product: only the compressed chunks cross PCIe; they
+        # are decoded, windowed and reduced on the GPU, the result comes back
+        x = fbh5.read_window_bslz4(fbh5name, idxs, device=f"cuda:{device}")
+        import torch
+
+        with torch.cuda.device(x.device):
+            return engine.fb_to_numpy(engine.reduce(x, fqavby, tavby, op))
+    data = readers.fbh5_read(fbh5name, idxs)
     return _reduce_array(data, (COLON, COLON, COLON), fqavby, fqavfunc, tavby, device)
 
 

@@ -20,6 +20,8 @@
  *   bldp_kurtosis_f32      getkurtosis (src/gbtworkerfunctions.jl:197-202) with
  *                          StatsBase.kurtosis' two-pass recipe.
  *   bldp_fqav_range        fqav(r::AbstractRange, n) src/gbtworkerfunctions.jl:27-33.
+ *   bldp_bslz4_*           HDF5 filter 32008 decode behind h5["data"][idxs...]
+ *                          (:181-187; H5Zbitshuffle, Project.toml:10).
  *
  * Conventions
  *   - Arrays are Julia column-major (nchan, nif, ntime), channel fastest
@@ -136,6 +138,36 @@ BLDP_API int bldp_kurtosis_f32(const float *in, int64_t nchan, int64_t nif, int6
  * host memory.  Synchronous. */
 BLDP_API int bldp_kurtosis_host_f32(int dev, const float *in, int64_t nchan, int64_t nif,
                                     int64_t ntime, const int64_t *win, double *out);
+
+/* HDF5 filter 32008 (bitshuffle + LZ4) chunks, the codec of compressed
+ * rawspec FBH5 products (H5Zbitshuffle, reference Project.toml:10; read at
+ * src/gbtworkerfunctions.jl:181-187).  A chunk is the raw bytes H5Dread_chunk
+ * returns: 12-byte header (uint64 BE uncompressed bytes, uint32 BE block
+ * bytes), LZ4 blocks of bit-transposed elements, raw tail of n % 8 elements. */
+BLDP_API int bldp_bslz4_info(const void *chunk, size_t nbytes, uint64_t *uncompressed_bytes,
+                             uint32_t *block_bytes);
+/* Decode one chunk on the host into out (exactly uncompressed_bytes). */
+BLDP_API int bldp_bslz4_decode_host(const void *chunk, size_t nbytes, int elem_size, void *out,
+                                    size_t out_bytes);
+/* Decode nchunk chunks on the GPU.  comp_host and comp_dev hold the same
+ * concatenated chunk bytes (the host copy is parsed into a block table, the
+ * device copy is decoded); chunk k spans [chunk_off[k], +chunk_len[k]) and
+ * decodes to out_dev + out_off[k] (bytes).  Synchronous: returns after the
+ * decode finished, BLDP_EINVAL if any block is corrupt. */
+BLDP_API int bldp_bslz4_decode_dev(int nchunk, const uint8_t *comp_host, const uint8_t *comp_dev,
+                                   const uint64_t *chunk_off, const uint64_t *chunk_len,
+                                   int elem_size, uint8_t *out_dev, const uint64_t *out_off,
+                                   void *stream);
+
+/* Gather a window (Julia order, dense (nc, ni, nt) out) from decoded chunks:
+ * packed holds the chunks of a chunk-aligned bounding box back to back in
+ * chunk-grid order [gt][gi][gc], each chunk C-order [ct][ci][cc].
+ * chunk = {ct, ci, cc}, box0 = {t, i, c} of the box's first element,
+ * grid = {gt, gi, gc} chunks in the box, win = the usual 9-int window in
+ * dataset coordinates (must lie inside the box). */
+BLDP_API int bldp_unchunk_f32(const float *packed, const int64_t chunk[3], const int64_t box0[3],
+                              const int64_t grid[3], const int64_t *win, float *out,
+                              void *stream);
 
 /* fqav(r::AbstractRange, n): first/step/length of the averaged axis. */
 BLDP_API int bldp_fqav_range(double first, double step, int64_t len, int64_t n, double *out_first,

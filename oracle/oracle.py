@@ -300,3 +300,47 @@ def gamma_bandpass(nchan, nif, ntime, nfpc, seed):
     bp = (0.2 + 0.8 * np.sin(np.pi * (x + 0.5) / nfpc) ** 2).astype(np.float32)
     bp[x == nfpc // 2] *= 10.0
     return np.asfortranarray(np.transpose(g * bp, (2, 1, 0)))
+
+
+# --------------------------------------------------------------------------
+# HDF5 filter 32008 test encoder (bitshuffle + literal-only LZ4)
+# --------------------------------------------------------------------------
+def np_bitshuffle(a: np.ndarray) -> np.ndarray:
+    """bitshuffle's bit transpose of one block (n % 8 == 0): bit plane
+    r = (byte r//8, bit r%8) of every element, packed LSB-first."""
+    b = np.frombuffer(np.ascontiguousarray(a).tobytes(), np.uint8).reshape(a.size, a.itemsize)
+    bits = np.unpackbits(b, axis=1, bitorder="little")
+    return np.packbits(bits.T, axis=1, bitorder="little").ravel()
+
+
+def lz4_literals(data: bytes) -> bytes:
+    """A valid LZ4 block holding `data` as one literal run (no matches)."""
+    n = len(data)
+    out = bytearray([min(n, 15) << 4])
+    if n >= 15:
+        r = n - 15
+        while r >= 255:
+            out.append(255)
+            r -= 255
+        out.append(r)
+    return bytes(out) + data
+
+
+def np_bslz4_encode(a: np.ndarray, block: int = 2048) -> bytes:
+    """An HDF5-filter-32008 chunk (bitshuffle + LZ4) of `a`, LZ4 literal-only."""
+    import struct
+
+    flat = np.ascontiguousarray(a, dtype=np.float32).ravel()
+    n, es = flat.size, 4
+    parts = [struct.pack(">QI", n * es, block * es)]
+    nfull = n // block
+    last = n % block
+    last -= last % 8
+    sizes = [block] * nfull + ([last] if last else [])
+    pos = 0
+    for sz in sizes:
+        z = lz4_literals(np_bitshuffle(flat[pos:pos + sz]).tobytes())
+        parts.append(struct.pack(">I", len(z)) + z)
+        pos += sz
+    parts.append(flat[pos:].tobytes())
+    return b"".join(parts)

@@ -118,3 +118,53 @@ def test_band_dist_two_ranks_real_kernels():
         p.join(timeout=300)
     assert all(p.exitcode == 0 for p in ps)
     assert all(q.get(timeout=5) for _ in ps)
+
+
+def _bslz4_fixtures():
+    import json
+
+    from conftest import GOLDEN
+
+    z = np.load(os.path.join(GOLDEN, "bslz4_v1.npz"), allow_pickle=False)
+    with open(os.path.join(GOLDEN, "bslz4_manifest.json")) as f:
+        return z, json.load(f)["cases"]
+
+
+def test_bslz4_gpu_decoder_matches_bitshuffle_library(pkg):
+    z, cases = _bslz4_fixtures()
+    chunks = [z["chunk_" + c["name"]].tobytes() for c in cases]
+    out = pkg.fbh5.bslz4_decode_dev(chunks, device="cuda:0").cpu().numpy()
+    pos = 0
+    for c in cases:
+        raw = z["raw_" + c["name"]].ravel()
+        assert np.array_equal(out[pos:pos + raw.size].view(np.uint32), raw.view(np.uint32)), \
+            c["name"]
+        pos += raw.size
+    assert pos == out.size
+
+
+def test_bslz4_gpu_rejects_corrupt_blocks(pkg):
+    import struct
+
+    bad = struct.pack(">QI", 2048 * 4, 2048 * 4) + struct.pack(">I", 3) + b"\0\0\0"
+    with pytest.raises(pkg.BLDPError):  # passes the host plan, fails in the kernel
+        pkg.fbh5.bslz4_decode_dev([bad], device="cuda:0")
+    z, _ = _bslz4_fixtures()
+    good = z["chunk_int_runs_b512"].tobytes()
+    out = pkg.fbh5.bslz4_decode_dev([good], device="cuda:0")  # the device still works
+    assert np.array_equal(out.cpu().numpy(), z["raw_int_runs_b512"].ravel())
+
+
+def test_fbh5_bslz4_on_gpu_end_to_end(pkg, orc, tmp_path):
+    J, C = pkg.JRange, pkg.COLON
+    d = np.asfortranarray(np.random.default_rng(8).integers(0, 256, (4096, 2, 40))
+                          .astype(np.float32))
+    p = tmp_path / "blc00_guppi_59000_12345_HIP1234_0011.rawspec.0002.h5"
+    pkg.fbh5.write_bslz4(p, dict(foff=-0.002861, nfpc=1024), d, (16, 1, 1024),
+                         lambda blk: orc.np_bslz4_encode(blk, 2048))
+    x = pkg.fbh5.read_window_bslz4(p, (J(1025, 3072), C, J(5, 36)), device="cuda:0")
+    assert same_bits(pkg.engine.fb_to_numpy(x), np.asfortranarray(d[1024:3072, :, 4:36]))
+    got = pkg.WorkerFunctions.getdata(str(p), (C, C, J(1, 32)), fqavby=64, tavby=8)
+    assert same_bits(got, orc.reduce(d, 64, 8, "sum", [0, 4096, 1, 0, 2, 1, 0, 32, 1]))
+    got = pkg.GBT.getdata([0], [str(p)], (J(4096, -1, 1), 1, C), fqavby=16, fqavfunc="max")
+    assert same_bits(got[0], orc.reduce(d, 16, 1, "max", [4095, 4096, -1, 0, 1, 1, 0, 40, 1]))

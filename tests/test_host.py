@@ -189,3 +189,69 @@ def test_fbh5_read_and_header(pkg, tmp_path):
     with pytest.raises(NameError):  # the reference's :147-150 bug, on request
         fb.header(q, reference_bug=True)
     assert np.array_equal(fb.read_window(q, (C, C, C)), d)
+
+
+def _bslz4_fixtures():
+    import json
+
+    from conftest import GOLDEN
+
+    z = np.load(os.path.join(GOLDEN, "bslz4_v1.npz"), allow_pickle=False)
+    with open(os.path.join(GOLDEN, "bslz4_manifest.json")) as f:
+        m = json.load(f)
+    return z, m["cases"]
+
+
+def test_bslz4_host_decoder_matches_bitshuffle_library(pkg):
+    """Chunks produced by the bitshuffle + LZ4 C libraries (imagecodecs,
+    oracle/gen_bslz4_fixtures.py) decode bit-exactly."""
+    z, cases = _bslz4_fixtures()
+    assert len(cases) >= 14
+    for c in cases:
+        raw = z["raw_" + c["name"]].ravel()
+        got = pkg.fbh5.bslz4_decode_host(z["chunk_" + c["name"]].tobytes())
+        assert np.array_equal(got.view(np.uint32), raw.view(np.uint32)), c["name"]
+
+
+def test_bslz4_encoder_roundtrip_and_corruption(pkg, orc):
+    import struct
+
+    a = (np.random.default_rng(3).random(2048 * 2 + 77) * 100).astype(np.float32)
+    for block in (2048, 128):
+        enc = orc.np_bslz4_encode(a, block)
+        assert pkg.fbh5.bslz4_info(enc) == (a.nbytes, block * 4)
+        assert np.array_equal(pkg.fbh5.bslz4_decode_host(enc), a)
+    bad = struct.pack(">QI", 2048 * 4, 2048 * 4) + struct.pack(">I", 3) + b"\0\0\0"
+    with pytest.raises(pkg.BLDPError):  # a match with offset 0
+        pkg.fbh5.bslz4_decode_host(bad)
+    with pytest.raises(pkg.BLDPError):  # truncated chunk
+        pkg.fbh5.bslz4_decode_host(orc.np_bslz4_encode(a)[:-9])
+    with pytest.raises(pkg.BLDPError):  # block size field overruns the chunk
+        b = bytearray(orc.np_bslz4_encode(a))
+        b[12:16] = struct.pack(">I", 1 << 30)
+        pkg.fbh5.bslz4_decode_host(bytes(b))
+
+
+def test_fbh5_bslz4_window_host_decode(pkg, orc, tmp_path):
+    """A bitshuffle/LZ4 FBH5 file without the HDF5 plugin: chunks are read raw
+    (H5Dread_chunk) and decoded by libbldp_hip, windows match the data."""
+    J, C = pkg.JRange, pkg.COLON
+    d = np.asfortranarray(np.random.default_rng(8).random((1000, 2, 20)).astype(np.float32))
+    p = tmp_path / "bslz4.h5"
+    pkg.fbh5.write_bslz4(p, dict(foff=-0.002861, nfpc=1024), d, (8, 1, 256),
+                         lambda blk: orc.np_bslz4_encode(blk, 512))
+    assert pkg.fbh5.needs_bslz4(p)
+    lay = pkg.fbh5.layout(p)
+    assert lay["chunk"] == (8, 1, 256) and lay["filters"][0]["id"] == 32008
+    assert np.array_equal(pkg.fbh5.read_window(p, (C, C, C)), d)
+    w = pkg.fbh5.read_window(p, (J(990, -7, 3), 2, J(3, 2, 19)))
+    assert np.array_equal(w, d[989:1:-7][:, 1:2, 2:19:2])
+    # real LZ4 streams (with matches) from the bitshuffle library as chunks
+    z, _ = _bslz4_fixtures()
+    chunks = [z["chunk_gamma_chunk_b2048"].tobytes(), z["chunk_gamma_chunk_b512"].tobytes()]
+    raw = z["raw_gamma_chunk_b2048"]  # (16, 1, 4096) C order [t][i][c]
+    full = np.concatenate([raw, raw], axis=0).transpose(2, 1, 0)  # Julia (4096, 1, 32)
+    q = tmp_path / "lib.h5"
+    it = iter(chunks)
+    pkg.fbh5.write_bslz4(q, dict(foff=-0.002861), full, (16, 1, 4096), lambda blk: next(it))
+    assert np.array_equal(pkg.fbh5.read_window(q, (C, C, C)), np.asfortranarray(full))
