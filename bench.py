@@ -197,6 +197,55 @@ def bench_host(args, eng, torch, pkg):
                          "kernel": "H2D copy engine (PCIe Gen5 x16 spec 63 GB/s)"}}
 
 
+def bench_decode(args, eng, torch, pkg):
+    """HDF5 filter 32008 (bitshuffle + LZ4) decode on the GPU: real LZ4 chunks
+    from the bitshuffle library (tests/golden/bslz4_v1.npz, a 0002-shaped
+    16 x 4096 chunk), replicated to ~1 GiB of output, decoded per call with
+    bldp_bslz4_decode_dev (host block-table walk + one launch + sync)."""
+    import ctypes
+
+    import numpy as np
+
+    z = np.load(os.path.join(REPO, "tests", "golden", "bslz4_v1.npz"), allow_pickle=False)
+    chunk = z["chunk_gamma_chunk_b2048"].tobytes()
+    nrep = 4096
+    L = pkg._lib.lib()
+    comp = np.frombuffer(chunk * nrep, np.uint8)
+    coff = (np.arange(nrep, dtype=np.uint64) * len(chunk))
+    clen = np.full(nrep, len(chunk), np.uint64)
+    raw_b = z["raw_gamma_chunk_b2048"].nbytes
+    ooff = np.arange(nrep, dtype=np.uint64) * raw_b
+    cdev = torch.from_numpy(comp.copy()).cuda()
+    out = torch.empty(nrep * raw_b // 4, dtype=torch.float32, device="cuda")
+    sp = pkg._lib.stream_ptr()
+
+    def go():
+        pkg._lib.check(L.bldp_bslz4_decode_dev(nrep, comp.ctypes.data, cdev.data_ptr(),
+                                               coff.ctypes.data, clen.ctypes.data, 4,
+                                               out.data_ptr(), ooff.ctypes.data, sp))
+    for _ in range(2):
+        go()
+    steps = max(3, args.steps // 4)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        go()
+    el = (time.perf_counter() - t0) / steps
+    ok = bool(np.array_equal(out[:raw_b // 4].cpu().numpy(),
+                             z["raw_gamma_chunk_b2048"].ravel()))
+    del ctypes
+    return {"metric": "bitshuffle+LZ4 (HDF5 filter 32008) GPU decode, GB/s of decoded output",
+            "value": round(nrep * raw_b / el / 1e9, 2), "unit": "GB/s", "n_gpus": 1,
+            "steps": steps, "warmup": 2, "ms_per_step": round(el * 1e3, 3),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8->f32",
+            "data": "bitshuffle-library LZ4 chunks of synthetic 0002 power (x4096)",
+            "config": {"workload": f"{nrep} chunks x {raw_b} B decoded, "
+                                   f"compressed {len(chunk)} B each", "check": ok},
+            "roofline": {"bound": "hbm", "achieved": round(nrep * (raw_b + len(chunk)) / el / 1e9, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(nrep * (raw_b + len(chunk)) / el / 1e9 / HBM_PEAK_GBS, 4),
+                         "traffic": None, "kernel": "k_bslz4 (one wave per 8 KiB block)"}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -205,7 +254,8 @@ def main():
     ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", default="reduce", choices=["reduce", "kurtosis", "host"])
+    ap.add_argument("--mode", default="reduce",
+                    choices=["reduce", "kurtosis", "host", "decode"])
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo only to rehearse the N-rank path on one GPU")
     args = ap.parse_args()
@@ -234,6 +284,7 @@ def main():
         if world != 1:
             raise SystemExit("--mode kurtosis/host are single-GPU measurements")
         r = (bench_kurtosis(args, cfg, eng, torch) if args.mode == "kurtosis"
+             else bench_decode(args, eng, torch, pkg) if args.mode == "decode"
              else bench_host(args, eng, torch, pkg))
         print(json.dumps(r), flush=True)
         return r

@@ -40,6 +40,7 @@ for s in $STEPS; do
     bench_*) run "$s" 600 python bench.py --config "${s#bench_}" ;;
     kurt_*) run "$s" 600 python bench.py --mode kurtosis --config "${s#kurt_}" ;;
     host)  run host 900 python bench.py --mode host ;;
+    decode) run decode 600 python bench.py --mode decode ;;
     dist2) run dist2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
              --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --dist-backend gloo \
              --steps 10 --warmup 3 ;;
