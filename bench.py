@@ -141,7 +141,7 @@ def bench_kurtosis(args, cfg, eng, torch):
             "roofline": {"bound": "hbm", "achieved": round(algo / ms / 1e6, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(algo / ms / 1e6 / HBM_PEAK_GBS, 4), "traffic": None,
-                         "kernel": "k_kurt_sum + k_kurt_mom (two reads of the window)"}}
+                         "kernel": "k_kurt_pass<0> + k_kurt_pass<1> (two reads of the window)"}}
 
 
 CFG5_PRODUCTS = ["cfg3", "cfg4", "cfg1"]  # 0000, 0001, 0002 single-bank geometry
