@@ -117,15 +117,13 @@ def bench_kurtosis(args, cfg, eng, torch):
                        seed=10 * b + cfg["product"], kind=0) for b in range(cfg["nbank"])]
     stream = torch.cuda.current_stream()
     for _ in range(args.warmup):
-        for b in banks:
-            eng.kurtosis(b, win)
+        eng.band_kurtosis(banks, win)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     e0.record(stream)
     for _ in range(args.steps):
-        for b in banks:
-            eng.kurtosis(b, win)
+        eng.band_kurtosis(banks, win)  # every bank in one set of launches
     e1.record(stream)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0

@@ -59,6 +59,7 @@ SIGNATURES = {
     "bldp_kurtosis_workspace_size": ([I64, I64, I64, P], SZ),
     "bldp_kurtosis_f32": ([P, I64, I64, I64, P, P, P, P], I),
     "bldp_kurtosis_host_f32": ([I, P, I64, I64, I64, P, P], I),
+    "bldp_band_kurtosis_f32": ([I, P, I64, I64, I64, P, P, P], I),
     "bldp_fqav_range": ([D, D, I64, I64, P, P, P], I),
     "bldp_synth_f32": ([P, I64, I64, I64, I64, U64, I, P], I),
     "bldp_bslz4_info": ([P, SZ, P, P], I),

@@ -339,13 +339,20 @@ int bldp_despike_f32(float *data, int64_t nchan, int64_t nif, int64_t ntime, int
   return BLDP_OK;
 }
 
-static int kurt_setup(const float *in, int64_t nchan, int64_t nif, int64_t ntime,
-                      const int64_t *win, KurtArgs *k) {
+static int kurt_setup(int nbank, const float *const *in, int64_t nchan, int64_t nif,
+                      int64_t ntime, const int64_t *win, KurtArgs *k) {
+  if (nbank < 1 || nbank > BLDP_MAX_BANKS)
+    return fail(BLDP_EINVAL, "nbank=%d outside 1..%d", nbank, BLDP_MAX_BANKS);
   Geo g;
   int rc = resolve_window(nchan, nif, ntime, win, &g);
   if (rc) return rc;
   *k = KurtArgs{};
-  k->in = in;
+  k->nbank = nbank;
+  bool aligned = true;
+  for (int b = 0; b < nbank; ++b) {
+    k->in[b] = in ? in[b] : nullptr;
+    aligned = aligned && aligned16(k->in[b]);
+  }
   k->in_off = g.off;
   k->in_cs = g.cs;
   k->in_ld_i = g.ld_i;
@@ -353,36 +360,55 @@ static int kurt_setup(const float *in, int64_t nchan, int64_t nif, int64_t ntime
   k->nc = g.nc;
   k->ni = g.ni;
   k->nt = g.nt;
-  k->vec = vec_ok(g) && g.nc % 4 == 0 && aligned16(in);
+  k->nrow = (int64_t)nbank * g.ni;
+  k->vec = vec_ok(g) && g.nc % 4 == 0 && aligned;
   plan_kurtosis(*k, num_cus_current());
+  return BLDP_OK;
+}
+
+static int kurt_run(KurtArgs &k, double *out, void *workspace, void *stream) {
+  if (k.nc * k.nrow == 0) return BLDP_OK;
+  for (int b = 0; b < k.nbank; ++b)
+    if (!k.in[b] && k.nt > 0) return fail(BLDP_EINVAL, "null input pointer (bank %d)", b);
+  if (!out) return fail(BLDP_EINVAL, "null output pointer");
+  k.out = out;
+  hipStream_t s = (hipStream_t)stream;
+  void *ws = workspace;
+  if (!ws) {
+    int rc = scratch(s, kurtosis_ws_bytes(k), &ws);
+    if (rc) return rc;
+  }
+  hipError_t e = launch_kurtosis(k, (char *)ws, s);
+  if (e != hipSuccess) return fail(BLDP_EHIP, "kurtosis launch: %s", hipGetErrorString(e));
   return BLDP_OK;
 }
 
 size_t bldp_kurtosis_workspace_size(int64_t nchan, int64_t nif, int64_t ntime,
                                     const int64_t *win) {
   KurtArgs k;
-  if (kurt_setup(nullptr, nchan, nif, ntime, win, &k)) return 0;
+  const float *none[1] = {nullptr};
+  if (kurt_setup(1, none, nchan, nif, ntime, win, &k)) return 0;
   k.vec = 1;  // the plan does not depend on alignment
+  plan_kurtosis(k, num_cus_current());
   return kurtosis_ws_bytes(k);
 }
 
 int bldp_kurtosis_f32(const float *in, int64_t nchan, int64_t nif, int64_t ntime,
                       const int64_t *win, double *out, void *workspace, void *stream) {
   KurtArgs k;
-  int rc = kurt_setup(in, nchan, nif, ntime, win, &k);
+  const float *ins[1] = {in};
+  int rc = kurt_setup(1, ins, nchan, nif, ntime, win, &k);
   if (rc) return rc;
-  if (k.nc * k.ni == 0) return BLDP_OK;
-  if (!out || (!in && k.nt > 0)) return fail(BLDP_EINVAL, "null pointer");
-  k.out = out;
-  hipStream_t s = (hipStream_t)stream;
-  void *ws = workspace;
-  if (!ws) {
-    rc = scratch(s, kurtosis_ws_bytes(k), &ws);
-    if (rc) return rc;
-  }
-  hipError_t e = launch_kurtosis(k, (char *)ws, s);
-  if (e != hipSuccess) return fail(BLDP_EHIP, "kurtosis launch: %s", hipGetErrorString(e));
-  return BLDP_OK;
+  return kurt_run(k, out, workspace, stream);
+}
+
+int bldp_band_kurtosis_f32(int nbank, const float *const *in, int64_t nchan, int64_t nif,
+                           int64_t ntime, const int64_t *win, double *out, void *stream) {
+  if (!in) return fail(BLDP_EINVAL, "null input pointer array");
+  KurtArgs k;
+  int rc = kurt_setup(nbank, in, nchan, nif, ntime, win, &k);
+  if (rc) return rc;
+  return kurt_run(k, out, nullptr, stream);
 }
 
 int bldp_fqav_range(double first, double step, int64_t len, int64_t n, double *out_first,

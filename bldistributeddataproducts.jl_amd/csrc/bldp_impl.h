@@ -59,17 +59,19 @@ hipError_t launch_despike(float *d, int64_t nchan, int64_t nrows, int64_t nfpc, 
                           hipStream_t s);
 
 struct KurtArgs {
-  const float *in;
+  const float *in[BLDP_MAX_BANKS];  // banks with identical geometry
+  int32_t nbank;
+  int64_t nrow;                     // nbank * ni output rows of nc channels
   int64_t in_off, in_cs, in_ld_i, in_ld_t;
   int64_t nc, ni, nt;
   int64_t rows_per_chunk;
   int32_t nchunk;
   int32_t ts;   // waves of a workgroup splitting the spectra of a tile (1, 2, 4)
   int32_t vec;  // float4 along channels legal
-  double *ws_sum;   // [nchunk][ni][nc]
-  float *mean;      // [ni][nc]
-  double *ws_mom;   // [nchunk][2][ni][nc]
-  double *out;      // [ni][nc]
+  double *ws_sum;   // [nchunk][nbank*ni][nc]
+  float *mean;      // [nbank*ni][nc]
+  double *ws_mom;   // [nchunk][2][nbank*ni][nc]
+  double *out;      // [nbank][ni][nc]
 };
 void plan_kurtosis(KurtArgs &k, int num_cus);
 size_t kurtosis_ws_bytes(const KurtArgs &k);

@@ -434,16 +434,18 @@ __global__ __launch_bounds__(kBlock) void k_kurt_pass(const KurtArgs k) {
   int64_t b = blockIdx.x;
   const int64_t cb = b % cblocks;
   b /= cblocks;
-  const int64_t i = b % k.ni, chunk = b / k.ni;
+  const int64_t ib = b % k.nrow, chunk = b / k.nrow;  // (bank, IF) row, time chunk
+  const int bank = (int)(ib / k.ni);
+  const int64_t i = ib - (int64_t)bank * k.ni;
   const int64_t col = (cb * tpb + wt) * 64 + lane;
   const bool valid = col < ncols;
   const int64_t r0 = chunk * k.rows_per_chunk, r1 = min(k.nt, r0 + k.rows_per_chunk);
-  const int64_t e = i * k.nc + (VEC ? 4 * col : col);  // first output of this lane
+  const int64_t e = ib * k.nc + (VEC ? 4 * col : col);  // first output of this lane
   double acc[NA];
 #pragma unroll
   for (int a = 0; a < NA; ++a) acc[a] = 0.0;
   if (valid) {
-    const float *p = k.in + k.in_off + i * k.in_ld_i + (r0 + tsi) * k.in_ld_t +
+    const float *p = k.in[bank] + k.in_off + i * k.in_ld_i + (r0 + tsi) * k.in_ld_t +
                      (VEC ? 4 * col : col * k.in_cs);
     float m[W];
 #pragma unroll
@@ -496,7 +498,7 @@ __global__ __launch_bounds__(kBlock) void k_kurt_pass(const KurtArgs k) {
         for (int a = 0; a < NA; ++a) acc[a] += red[wave + q][a][lane];
   }
   if (tsi == 0 && valid) {
-    const int64_t n = k.ni * k.nc;
+    const int64_t n = k.nrow * k.nc;
     if (k.nchunk == 1) {
 #pragma unroll
       for (int w = 0; w < W; ++w) {
@@ -523,7 +525,7 @@ __global__ __launch_bounds__(kBlock) void k_kurt_pass(const KurtArgs k) {
 // per output, chunks in order.
 template <int PASS>
 __global__ __launch_bounds__(kBlock) void k_kurt_fold_t(const KurtArgs k) {
-  const int64_t n = k.ni * k.nc;
+  const int64_t n = k.nrow * k.nc;
   for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < n;
        e += (int64_t)gridDim.x * kBlock) {
     double a = 0.0, c = 0.0;
@@ -550,7 +552,7 @@ __global__ __launch_bounds__(kBlock) void k_kurt_fold_t(const KurtArgs k) {
 template <int PASS>
 __global__ __launch_bounds__(kBlock) void k_kurt_fold(const KurtArgs k) {
   const int lane = threadIdx.x & 63;
-  const int64_t n = k.ni * k.nc;
+  const int64_t n = k.nrow * k.nc;
   for (int64_t e = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); e < n;
        e += (int64_t)gridDim.x * 4) {
     double a = 0.0, c = 0.0;
@@ -765,7 +767,7 @@ void plan_kurtosis(KurtArgs &k, int num_cus) {
   // waves splitting the spectra of a tile: keep >= 16 spectra per wave
   k.ts = 1;
   while (k.ts < 4 && k.nt >= (int64_t)32 * k.ts) k.ts *= 2;
-  const int64_t tiles = cdiv(cdiv(ncols, 64), 4 / k.ts) * k.ni;  // workgroups
+  const int64_t tiles = cdiv(cdiv(ncols, 64), 4 / k.ts) * k.nrow;  // workgroups
   const int64_t target = (int64_t)num_cus * 8;
   int64_t nchunk = 1;
   if (tiles < target) nchunk = std::min<int64_t>(cdiv(target, tiles), k.nt / (16 * k.ts));
@@ -775,14 +777,14 @@ void plan_kurtosis(KurtArgs &k, int num_cus) {
 }
 
 size_t kurtosis_ws_bytes(const KurtArgs &k) {
-  const size_t n = (size_t)k.ni * k.nc;
+  const size_t n = (size_t)k.nrow * k.nc;
   auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
   return up(n * k.nchunk * sizeof(double)) + up(n * sizeof(float)) +
          up(2 * n * k.nchunk * sizeof(double));
 }
 
 hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s) {
-  const size_t n = (size_t)k.ni * k.nc;
+  const size_t n = (size_t)k.nrow * k.nc;
   if (n == 0) return hipSuccess;
   auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
   k.ws_sum = reinterpret_cast<double *>(ws);
@@ -790,7 +792,7 @@ hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s) {
   k.ws_mom = reinterpret_cast<double *>(ws + up(n * k.nchunk * sizeof(double)) +
                                         up(n * sizeof(float)));
   const int64_t ncols = k.vec ? k.nc / 4 : k.nc;
-  const dim3 grid((unsigned)(cdiv(cdiv(ncols, 64), 4 / k.ts) * k.ni * k.nchunk)), block(kBlock);
+  const dim3 grid((unsigned)(cdiv(cdiv(ncols, 64), 4 / k.ts) * k.nrow * k.nchunk)), block(kBlock);
   const bool wide = k.nchunk > 16;  // wave per output only when there is much to fold
   const unsigned fg = (unsigned)std::min<int64_t>(cdiv((int64_t)n, wide ? 4 : kBlock), 16384);
   if (k.vec)

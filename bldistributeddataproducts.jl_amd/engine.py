@@ -21,7 +21,7 @@ from .idxs import window_shape
 
 __all__ = [
     "fb_empty", "fb_from_numpy", "fb_to_numpy", "reduce", "band_reduce", "stitch",
-    "despike", "kurtosis", "synth", "plan", "reduce_host", "kurtosis_host",
+    "despike", "kurtosis", "band_kurtosis", "synth", "plan", "reduce_host", "kurtosis_host",
 ]
 
 
@@ -239,6 +239,31 @@ def kurtosis(x, win=None, stream=None):
                              None, _lib.stream_ptr(stream))
     _lib.check(rc, "bldp_kurtosis_f32")
     return out
+
+
+def band_kurtosis(banks, win=None, stream=None):
+    """Kurtosis of every bank of a band on one GPU in one set of launches;
+    returns a list of (nc, ni) float64 tensors (views of one buffer)."""
+    torch = _torch()
+    L = _lib.lib()
+    banks = list(banks)
+    if not banks:
+        raise ValueError("no banks")
+    shape = tuple(banks[0].shape)
+    geo = _abi_dims(banks[0])[1:]
+    for b in banks[1:]:
+        if tuple(b.shape) != shape or _abi_dims(b)[1:] != geo:
+            raise ValueError("all banks of a band must have the same shape and layout")
+    _check_bounds(win, shape)
+    nc, ni, _ = window_shape(win, shape)
+    buf = torch.empty((len(banks), ni, nc), dtype=torch.float64, device=banks[0].device)
+    ptrs = (ctypes.c_void_p * len(banks))(*[b.data_ptr() for b in banks])
+    keep, wp = _lib.win_arg(_full_win(win, shape))
+    rc = L.bldp_band_kurtosis_f32(len(banks), ctypes.cast(ptrs, ctypes.c_void_p), *geo, wp,
+                                  buf.data_ptr() if buf.numel() else None,
+                                  _lib.stream_ptr(stream))
+    _lib.check(rc, "bldp_band_kurtosis_f32")
+    return [buf[k].t() for k in range(len(banks))]
 
 
 def synth(nchan, nif, ntime, nfpc=1024, seed=0, kind=0, device=None, stream=None):

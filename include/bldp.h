@@ -133,6 +133,14 @@ BLDP_API size_t bldp_kurtosis_workspace_size(int64_t nchan, int64_t nif, int64_t
 BLDP_API int bldp_kurtosis_f32(const float *in, int64_t nchan, int64_t nif, int64_t ntime,
                       const int64_t *win, double *out, void *workspace, void *stream);
 
+/* Kurtosis of every bank of a band resident on one device, one set of
+ * launches for all banks (the GBT.getkurtosis fan-out, src/gbt.jl:81-88).
+ * in[] is a HOST array of device pointers; out is nbank (nc, ni) float64
+ * matrices back to back on the device. */
+BLDP_API int bldp_band_kurtosis_f32(int nbank, const float *const *in, int64_t nchan,
+                                    int64_t nif, int64_t ntime, const int64_t *win, double *out,
+                                    void *stream);
+
 /* Host-pointer form of bldp_kurtosis_f32 for a worker holding the data in
  * host memory: the window is staged on device `dev`, out (nc, ni) float64 is
  * host memory.  Synchronous. */

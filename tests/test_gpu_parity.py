@@ -266,3 +266,20 @@ def test_full_size_bank_properties(eng):
     # time integration alone: sum over time of each channel
     t = eng.reduce(x, 1, 16, "sum")
     assert torch.equal(t[:, 0, 0].double(), x[:, 0, :].double().sum(dim=1))
+
+
+def test_band_kurtosis(eng, orc):
+    rng = np.random.default_rng(21)
+    banks = [np.asfortranarray((rng.standard_normal((1024, 2, 300)) ** 2).astype(np.float32))
+             for _ in range(5)]
+    xs = [dev(eng, b) for b in banks]
+    w = [4, 1000, 1, 0, 2, 1, 10, 280, 1]
+    ks = eng.band_kurtosis(xs, w)
+    assert len(ks) == 5
+    for b, k in zip(banks, ks):
+        np.testing.assert_allclose(host(eng, k), orc.kurtosis(b, w), rtol=1e-4, atol=1e-5)
+    long = [np.asfortranarray((rng.standard_normal((64, 1, 30000)) ** 2).astype(np.float32))
+            for _ in range(3)]
+    ks = eng.band_kurtosis([dev(eng, b) for b in long])  # many time chunks, wave folds
+    for b, k in zip(long, ks):
+        np.testing.assert_allclose(host(eng, k), orc.kurtosis(b), rtol=1e-4, atol=1e-5)
