@@ -182,14 +182,23 @@ def bench_host(args, eng, torch, pkg):
         one_pass()
     el = (time.perf_counter() - t0) / steps
     gbs = nbytes / el / 1e9
-    del np
+    # the same arrays in ordinary (pageable) host memory, the Julia Array case
+    pageable = [(np.asfortranarray(np.array(a, copy=True)), None, c, win)
+                for a, _, c, win in arrays[:3]]
+    pbytes = sum(4 * c["nchan"] * c["nif"] * c["tw"] for _, _, c, _ in pageable)
+    t0 = time.perf_counter()
+    for a, _, c, win in pageable:
+        eng.reduce_host(a, c["F"], c["T"], "sum", win, device=torch.cuda.current_device())
+    pg = pbytes / (time.perf_counter() - t0) / 1e9
     return {"metric": "session scan GB/s streamed from pinned host memory (per GPU)",
             "value": round(gbs, 2), "unit": "GB/s", "n_gpus": 1, "steps": steps,
             "warmup": max(1, args.warmup // 5), "ms_per_step": round(el * 1e3, 2),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic, pinned host memory (torch pin_memory)",
             "config": {"workload": "cfg5 share of one GPU: 4 bands x {0000, 0001, 0002}, "
-                                   "bldp_reduce_host_f32 per array", "bytes_per_step": nbytes},
+                                   "bldp_reduce_host_f32 per array", "bytes_per_step": nbytes,
+                       "pageable_GBps": round(pg, 2),
+                       "pageable_sample": "band 0 x {0000, 0001, 0002}, ordinary numpy memory"},
             "roofline": {"bound": "pcie", "achieved": round(gbs, 2), "peak": 63.0,
                          "unit": "GB/s", "frac": round(gbs / 63.0, 4), "traffic": None,
                          "kernel": "H2D copy engine (PCIe Gen5 x16 spec 63 GB/s)"}}

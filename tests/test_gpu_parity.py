@@ -283,3 +283,23 @@ def test_band_kurtosis(eng, orc):
     ks = eng.band_kurtosis([dev(eng, b) for b in long])  # many time chunks, wave folds
     for b, k in zip(long, ks):
         np.testing.assert_allclose(host(eng, k), orc.kurtosis(b), rtol=1e-4, atol=1e-5)
+
+
+def test_full_size_cfg4_and_cfg2_banks(eng, orc):
+    """cfg4 (0001: 512 ch x 880000 spectra, window 1:879616, F=8, T=1024) at
+    full size on integer data: exact totals and a spot group; cfg2 (8 banks of
+    0002) against the oracle directly."""
+    x = eng.synth(512, 1, 880000, 8, seed=4, kind=1)
+    w = [0, 512, 1, 0, 1, 1, 0, 879616, 1]
+    s = eng.reduce(x, 8, 1024, "sum", w)
+    assert tuple(s.shape) == (64, 1, 859)
+    assert s.double().sum().item() == x[:, :, :879616].double().sum().item()
+    blk = x[8 * 5:8 * 6, 0, 1024 * 700:1024 * 701].double().sum().item()
+    assert s[5, 0, 700].item() == blk
+    assert eng.reduce(x, 8, 1024, "max", w).max().item() == x[:, :, :879616].max().item()
+    banks = [orc.gamma_bandpass(65536, 1, 279, 1024, 200 + b) for b in range(8)]
+    got = host(eng, eng.band_reduce([dev(eng, b) for b in banks], 64, 16, "sum",
+                                    [0, 65536, 1, 0, 1, 1, 0, 272, 1]))
+    want = orc.stitch([orc.reduce(b, 64, 16, "sum", [0, 65536, 1, 0, 1, 1, 0, 272, 1])
+                       for b in banks])
+    np.testing.assert_allclose(got, want, rtol=RTOL)
