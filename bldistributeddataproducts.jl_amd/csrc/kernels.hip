@@ -716,6 +716,7 @@ Plan plan_reduce(RedArgs &a, bool aligned, int num_cus) {
   p.grid = a.ntiles;
   const int cap = BLDP_MAX_WG_PER_CU >= 0 ? BLDP_MAX_WG_PER_CU : (a.ts > 1 ? 4 : 0);
   if (cap > 0) p.grid = std::min<int64_t>(p.grid, (int64_t)cap * num_cus);
+  p.grid = std::min<int64_t>(p.grid, INT32_MAX);  // tiles beyond: grid-stride loop
   // narrow-path vector stores
   a.vec_out = 0;
   if (p.path == PATH_NARROW) {

@@ -41,6 +41,10 @@ for s in $STEPS; do
     kurt_*) run "$s" 600 python bench.py --mode kurtosis --config "${s#kurt_}" ;;
     host)  run host 900 python bench.py --mode host ;;
     decode) run decode 600 python bench.py --mode decode ;;
+    prof_decode) run prof_decode 600 rocprofv3 --kernel-trace --stats --output-format csv \
+             -d "$OUT/prof_decode" -o run -- python bench.py --mode decode ;;
+    prof_kurt) run prof_kurt 600 rocprofv3 --kernel-trace --stats --output-format csv \
+             -d "$OUT/prof_kurt" -o run -- python bench.py --mode kurtosis --config cfg3 ;;
     dist2) run dist2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
              --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --dist-backend gloo \
              --steps 10 --warmup 3 ;;
