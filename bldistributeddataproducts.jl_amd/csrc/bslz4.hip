@@ -12,8 +12,9 @@
 //   of every element, packed LSB-first);
 //   then the last n % 8 elements, raw.
 //
-// GPU design: the host walks the block headers (cheap) into a task table;
-// one wave per block stages the compressed bytes in LDS, decodes LZ4 into
+// GPU design: the host reads only each chunk's 12-byte header; a planner
+// kernel (one thread per chunk) walks the block-size fields, already on the
+// device, into a task table; then one wave per block stages the compressed bytes in LDS, decodes LZ4 into
 // LDS (sequence parsing is wave-uniform, literal and match copies are spread
 // over the 64 lanes, overlapping matches in rounds of `offset` bytes), then
 // inverts the bit transpose with an 8x8 bit-matrix transpose per 8 elements
@@ -103,6 +104,70 @@ struct Task {        // one unit of GPU work
 };
 constexpr uint32_t RAW = 0xFFFFFFFFu;
 
+// Per-chunk geometry from its 12-byte header (host side, one read per chunk).
+struct ChunkDesc {
+  uint64_t src, len, dst;      // chunk bytes [src, src+len) -> output bytes at dst
+  uint64_t n, block;           // elements, elements per full block
+  uint32_t nfull, last, tail;  // full blocks, last partial block, raw tail elements
+  uint32_t task0;              // first task index of this chunk
+};
+
+int describe_chunk(const uint8_t *c, uint64_t len, uint64_t src, uint64_t dst, int es,
+                   ChunkDesc *d) {
+  if (len < 12) return bldp::set_error(BLDP_EINVAL, "bslz4: chunk shorter than its header");
+  const uint64_t nb = be64(c);
+  const uint32_t bb = be32(c + 8);
+  if (nb % es || bb % es || bb == 0 || (bb / es) % 8 || bb > (1u << 24))
+    return bldp::set_error(BLDP_EINVAL, "bslz4: bad header (bytes %llu, block %u, elem %d)",
+                           (unsigned long long)nb, bb, es);
+  d->src = src;
+  d->len = len;
+  d->dst = dst;
+  d->n = nb / es;
+  d->block = bb / es;
+  d->nfull = (uint32_t)(d->n / d->block);
+  uint64_t last = d->n % d->block;
+  d->last = (uint32_t)(last - last % 8);
+  d->tail = (uint32_t)(d->n - (uint64_t)d->nfull * d->block - d->last);
+  return BLDP_OK;
+}
+
+inline uint32_t ntasks(const ChunkDesc &d) {
+  return d.nfull + (d.last ? 1 : 0) + (d.tail ? 1 : 0);
+}
+
+// LZ4 worst case for one block (LZ4_COMPRESSBOUND)
+__host__ __device__ inline uint32_t lz4_bound(uint32_t n) { return n + n / 255 + 16; }
+
+__device__ inline uint32_t be32_dev(const uint8_t *p) {
+  return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3];
+}
+
+// One thread per chunk walks its block-size fields (already on the device)
+// into the task table; a block that overruns its chunk sets *err.
+__global__ __launch_bounds__(64) void k_bslz4_plan(const uint8_t *__restrict__ comp,
+                                                   const ChunkDesc *__restrict__ chunks,
+                                                   int nchunk, int es, uint32_t cap,
+                                                   Task *__restrict__ tasks, int *err) {
+  const int k = blockIdx.x * 64 + threadIdx.x;
+  if (k >= nchunk) return;
+  const ChunkDesc d = chunks[k];
+  uint64_t pos = d.src + 12, e = 0;
+  const uint64_t end = d.src + d.len;
+  const uint32_t nblk = d.nfull + (d.last ? 1 : 0);
+  for (uint32_t b = 0; b < nblk; ++b) {
+    const uint32_t ne = b < d.nfull ? (uint32_t)d.block : d.last;
+    if (pos + 4 > end) { atomicOr(err, 2); return; }
+    const uint32_t cl = be32_dev(comp + pos);
+    if (cl > cap || pos + 4 + cl > end) { atomicOr(err, 2); return; }
+    tasks[d.task0 + b] = Task{pos + 4, d.dst + e * es, cl, ne};
+    pos += 4 + cl;
+    e += ne;
+  }
+  if (pos + (uint64_t)d.tail * es != end) { atomicOr(err, 4); return; }
+  if (d.tail) tasks[d.task0 + nblk] = Task{pos, d.dst + e * es, RAW, d.tail};
+}
+
 // Walk one chunk's headers into tasks; returns 0 or an error code.
 int plan_chunk(const uint8_t *c, uint64_t len, uint64_t src0, uint64_t dst0, int es,
                std::vector<Task> &tasks, uint64_t *out_bytes, uint32_t *max_block) {
@@ -145,6 +210,7 @@ __global__ __launch_bounds__(64) void k_bslz4(const uint8_t *__restrict__ comp,
                                               int *err) {
   extern __shared__ uint8_t lds[];
   const int lane = threadIdx.x;
+  if (*err & 6) return;  // the planner rejected a chunk: the task table is incomplete
   const Task t = tasks[blockIdx.x];
   if (t.clen == RAW) {  // raw tail bytes of a chunk
     for (uint32_t i = lane; i < t.nelem * (uint32_t)es; i += 64) out[t.dst + i] = comp[t.src + i];
@@ -152,6 +218,10 @@ __global__ __launch_bounds__(64) void k_bslz4(const uint8_t *__restrict__ comp,
   }
   uint8_t *in = lds, *dec = lds + cap;
   const uint32_t clen = t.clen, nbytes = t.nelem * (uint32_t)es;
+  if (clen > cap) {
+    if (lane == 0) atomicOr(err, 1);
+    return;
+  }
   for (uint32_t i = lane; i < clen; i += 64) in[i] = comp[t.src + i];
   __syncthreads();
   // LZ4: every lane parses the same sequence (wave-uniform control flow)
@@ -286,39 +356,50 @@ BLDP_API int bldp_bslz4_decode_dev(int nchunk, const uint8_t *comp_host, const u
     return bldp::set_error(BLDP_EINVAL, "bslz4: bad argument");
   if (elem_size == 4 && ((uintptr_t)out_dev & 3))
     return bldp::set_error(BLDP_EINVAL, "bslz4: output must be 4-byte aligned");
-  std::vector<Task> tasks;
-  uint32_t maxb = 0;
+  // host: one 12-byte header per chunk -> geometry and task ranges
+  std::vector<ChunkDesc> descs(nchunk);
+  uint64_t ntask = 0;
+  uint32_t maxbb = 0;
   for (int k = 0; k < nchunk; ++k) {
-    uint64_t total = 0;
-    int rc = plan_chunk(comp_host + chunk_off[k], chunk_len[k], chunk_off[k], out_off[k],
-                        elem_size, tasks, &total, &maxb);
+    int rc = describe_chunk(comp_host + chunk_off[k], chunk_len[k], chunk_off[k], out_off[k],
+                            elem_size, &descs[k]);
     if (rc) return rc;
     if (elem_size == 4 && (out_off[k] & 3))
       return bldp::set_error(BLDP_EINVAL, "bslz4: output offsets must be 4-byte aligned");
+    descs[k].task0 = (uint32_t)ntask;
+    ntask += ntasks(descs[k]);
+    if (ntask > INT32_MAX) return bldp::set_error(BLDP_EINVAL, "bslz4: too many blocks");
+    maxbb = std::max<uint32_t>(maxbb, (uint32_t)(descs[k].block * elem_size));
   }
-  if (tasks.empty()) return BLDP_OK;
-  if ((size_t)maxb * 2 > 64 * 1024)
-    return bldp::set_error(BLDP_EINVAL, "bslz4: block of %u bytes exceeds the 32 KiB LDS plan",
-                           maxb);
+  if (ntask == 0) return BLDP_OK;
+  const uint32_t cap = (lz4_bound(maxbb) + 15) & ~15u;
+  if ((size_t)cap + (((size_t)maxbb + 15) & ~(size_t)15) > 64 * 1024)
+    return bldp::set_error(BLDP_EINVAL, "bslz4: block of %u bytes exceeds the LDS plan", maxbb);
   hipStream_t s = (hipStream_t)stream;
-  const size_t tbytes = tasks.size() * sizeof(Task);
+  const size_t dbytes = ((descs.size() * sizeof(ChunkDesc)) + 255) & ~(size_t)255;
+  const size_t tbytes = ((ntask * sizeof(Task)) + 255) & ~(size_t)255;
   void *ws = nullptr;
-  int rc = bldp::scratch_bytes(s, tbytes + 256, &ws);
+  int rc = bldp::scratch_bytes(s, dbytes + tbytes + 256, &ws);
   if (rc) return rc;
-  Task *dtask = (Task *)ws;
-  int *derr = (int *)((char *)ws + ((tbytes + 15) & ~(size_t)15));
-  if (hipMemcpyAsync(dtask, tasks.data(), tbytes, hipMemcpyHostToDevice, s) != hipSuccess ||
+  ChunkDesc *ddesc = (ChunkDesc *)ws;
+  Task *dtask = (Task *)((char *)ws + dbytes);
+  int *derr = (int *)((char *)ws + dbytes + tbytes);
+  if (hipMemcpyAsync(ddesc, descs.data(), descs.size() * sizeof(ChunkDesc),
+                     hipMemcpyHostToDevice, s) != hipSuccess ||
       hipMemsetAsync(derr, 0, sizeof(int), s) != hipSuccess)
-    return bldp::set_error(BLDP_EHIP, "bslz4: task upload failed");
-  const uint32_t cap = (maxb + 15) & ~15u;
-  hipLaunchKernelGGL(k_bslz4, dim3((unsigned)tasks.size()), dim3(64), 2 * cap, s, comp_dev,
-                     dtask, (int)tasks.size(), out_dev, elem_size, cap, derr);
+    return bldp::set_error(BLDP_EHIP, "bslz4: descriptor upload failed");
+  hipLaunchKernelGGL(k_bslz4_plan, dim3((unsigned)((nchunk + 63) / 64)), dim3(64), 0, s,
+                     comp_dev, ddesc, nchunk, elem_size, cap, dtask, derr);
+  const uint32_t dcap = (maxbb + 15) & ~15u;
+  hipLaunchKernelGGL(k_bslz4, dim3((unsigned)ntask), dim3(64), cap + dcap, s, comp_dev, dtask,
+                     (int)ntask, out_dev, elem_size, cap, derr);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return bldp::set_error(BLDP_EHIP, "bslz4 launch: %s", hipGetErrorString(e));
   int herr = 0;
   if (hipMemcpyAsync(&herr, derr, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)
     return bldp::set_error(BLDP_EHIP, "bslz4: synchronize failed");
+  if (herr & 6) return bldp::set_error(BLDP_EINVAL, "bslz4: block table overruns a chunk");
   if (herr) return bldp::set_error(BLDP_EINVAL, "bslz4: corrupt LZ4 block on the device");
   return BLDP_OK;
 }
