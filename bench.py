@@ -253,6 +253,67 @@ def bench_decode(args, eng, torch, pkg):
                          "traffic": None, "kernel": "k_bslz4 (one wave per 8 KiB block)"}}
 
 
+def bench_file(args, eng, torch, pkg):
+    """End to end on a compressed rawspec-style FBH5 file (HDF5 filter 32008,
+    chunks (16, 1, 4096) produced by the bitshuffle library, replicated to
+    1 GiB of Float32): WorkerFunctions.getdata(fname, (:,:,:); fqavby=64,
+    tavby=16) = chunk reads into pinned memory + one H2D of compressed bytes
+    + GPU decode + window gather + reduce.  CPU path beside it: the same file
+    through the host decoder + the oracle reduce (bounded window)."""
+    import numpy as np
+
+    import __graft_entry__ as entry
+
+    z = np.load(os.path.join(REPO, "tests", "golden", "bslz4_v1.npz"), allow_pickle=False)
+    chunk = z["chunk_gamma_chunk_b2048"].tobytes()
+    raw = z["raw_gamma_chunk_b2048"]  # (16, 1, 4096) C order
+    nrep = 4096
+    jshape = (4096, 1, 16 * nrep)
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "bldp_bench_bslz4.h5")
+    pkg.fbh5.write_bslz4_chunks(path, dict(foff=-187.5 / 65536, nfpc=1024), jshape,
+                                (16, 1, 4096), (chunk for _ in range(nrep)))
+    W = pkg.WorkerFunctions
+    C = pkg.COLON
+    nbytes = 4 * int(np.prod(jshape))
+    got = W.getdata(path, (C, C, C), fqavby=64, tavby=16)  # warm (page cache, pinned pool)
+    want_blk = raw.transpose(2, 1, 0).astype(np.float64).reshape(64, 64, 1, 16).sum(axis=(0, 3))
+    ok = bool(np.allclose(got[:, :, 0], want_blk, rtol=1e-5))
+    steps = max(3, args.steps // 5)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        W.getdata(path, (C, C, C), fqavby=64, tavby=16)
+    el = (time.perf_counter() - t0) / steps
+    tm = {}
+    x = pkg.fbh5._read_window_bslz4_dev(path, (C, C, C), "cuda:0", timings=tm)
+    del x
+    # CPU path on a bounded window: host decode (C++) + oracle reduce
+    orc = entry.load_oracle()
+    J = pkg.JRange
+    nt_cpu = 16 * 256
+    t0 = time.perf_counter()
+    w = pkg.fbh5.read_window_bslz4(path, (C, C, J(1, nt_cpu)), device=None)
+    orc.reduce(w, 64, 16)
+    cpu_el = time.perf_counter() - t0
+    os.remove(path)
+    return {"metric": "compressed FBH5 getdata end to end, GB/s of Float32 data",
+            "value": round(nbytes / el / 1e9, 2), "unit": "GB/s", "n_gpus": 1, "steps": steps,
+            "warmup": 1, "ms_per_step": round(el * 1e3, 2), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": "bitshuffle-library LZ4 chunks of synthetic 0002 power",
+            "config": {"workload": f"FBH5 (4096 ch x 1 IF x {16 * nrep} spectra), chunks "
+                                   f"(16,1,4096) bitshuffle+LZ4, getdata fqavby=64 tavby=16",
+                       "check": ok, "stages_s": {k: (round(v, 4) if isinstance(v, float) else v)
+                                                 for k, v in tm.items()}},
+            "roofline": {"bound": "pcie", "achieved": round(tm["compressed_bytes"] / tm["h2d_s"]
+                                                            / 1e9, 2) if tm.get("h2d_s") else None,
+                         "peak": 63.0, "unit": "GB/s", "frac": None, "traffic": None,
+                         "kernel": "H2D of the compressed chunks"},
+            "cpu_baseline": {"value": round(4 * 4096 * nt_cpu / cpu_el / 1e9, 3), "unit": "GB/s",
+                             "cores": 1, "kind": "port",
+                             "sample": f"window (:, :, 1:{nt_cpu}): host bitshuffle/LZ4 decode "
+                                       "(libbldp C++) + oracle reduce, one thread"}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -262,7 +323,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", default="reduce",
-                    choices=["reduce", "kurtosis", "host", "decode"])
+                    choices=["reduce", "kurtosis", "host", "decode", "file"])
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo only to rehearse the N-rank path on one GPU")
     args = ap.parse_args()
@@ -292,6 +353,7 @@ def main():
             raise SystemExit("--mode kurtosis/host are single-GPU measurements")
         r = (bench_kurtosis(args, cfg, eng, torch) if args.mode == "kurtosis"
              else bench_decode(args, eng, torch, pkg) if args.mode == "decode"
+             else bench_file(args, eng, torch, pkg) if args.mode == "file"
              else bench_host(args, eng, torch, pkg))
         print(json.dumps(r), flush=True)
         return r

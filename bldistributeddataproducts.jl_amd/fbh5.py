@@ -502,10 +502,13 @@ def _box(win_axis, cdim):
     return lo // cdim, hi // cdim - lo // cdim + 1
 
 
-def read_chunks(fname, idxs):
+def read_chunks(fname, idxs, alloc=None):
     """Raw chunks covering the window, in chunk-grid order.  Returns
     (jshape, window, chunk dims (t, i, c), box origin (t, i, c), grid (t, i, c),
-    [(filter_mask, bytes or None)])."""
+    chunks).  Without ``alloc`` chunks are [(filter_mask, bytes or None)].
+    With ``alloc(total_bytes) -> (buffer address, keepalive)`` every chunk is
+    read by libhdf5 straight into one buffer (e.g. pinned host memory) and
+    chunks are [(filter_mask, offset, nbytes)] (nbytes 0: never written)."""
     lay = layout(fname)
     cdims, chunk = lay["cdims"], lay["chunk"]
     if chunk is None or len(cdims) != 3:
@@ -530,21 +533,37 @@ def read_chunks(fname, idxs):
     try:
         d = _ok(H.H5Dopen2(f, b"data", H5P_DEFAULT), "open dataset 'data'")
         try:
+            offs, sizes = [], []
             for a in range(gt):
                 for b in range(gi):
                     for c in range(gc):
                         off = _hs([(kt0 + a) * chunk[0], (ki0 + b) * chunk[1],
                                    (kc0 + c) * chunk[2]])
                         nb = hsize_t()
-                        if H.H5Dget_chunk_storage_size(d, off, ctypes.byref(nb)) < 0 or \
-                                nb.value == 0:
-                            out.append((0, None))  # never written: fill value (0)
-                            continue
-                        buf = ctypes.create_string_buffer(nb.value)
-                        mask = ctypes.c_uint32()
-                        _ok(H.H5Dread_chunk(d, H5P_DEFAULT, off, ctypes.byref(mask), buf),
-                            "read_chunk")
-                        out.append((mask.value, buf.raw))
+                        if H.H5Dget_chunk_storage_size(d, off, ctypes.byref(nb)) < 0:
+                            nb.value = 0  # never written: fill value (0)
+                        offs.append(off)
+                        sizes.append(nb.value)
+            mask = ctypes.c_uint32()
+            if alloc is None:
+                for off, nb in zip(offs, sizes):
+                    if nb == 0:
+                        out.append((0, None))
+                        continue
+                    buf = ctypes.create_string_buffer(nb)
+                    _ok(H.H5Dread_chunk(d, H5P_DEFAULT, off, ctypes.byref(mask), buf),
+                        "read_chunk")
+                    out.append((mask.value, buf.raw))
+            else:
+                base, keep = alloc(max(1, sum(sizes)))
+                pos = 0
+                for off, nb in zip(offs, sizes):
+                    if nb:
+                        _ok(H.H5Dread_chunk(d, H5P_DEFAULT, off, ctypes.byref(mask),
+                                            ctypes.c_void_p(base + pos)), "read_chunk")
+                    out.append((mask.value if nb else 0, pos, nb))
+                    pos += nb
+                out = (out, keep)
         finally:
             H.H5Dclose(d)
     finally:
@@ -559,46 +578,72 @@ def read_window_bslz4(fname, idxs, device=None):
     compressed bytes go to the GPU, are decoded there (bldp_bslz4_decode_dev)
     and the window is gathered on the device (bldp_unchunk_f32); returns a
     Julia-order device tensor."""
-    from . import _lib
-
+    if device is not None:
+        return _read_window_bslz4_dev(fname, idxs, device)
     jshape, win, chunk, box0, grid, raw = read_chunks(fname, idxs)
     cvol = int(np.prod(chunk))
     nc, ni, nt = win[1], win[4], win[7]
-    if device is None:
-        packed = np.zeros(len(raw) * cvol, np.float32)
-        for k, (mask, b) in enumerate(raw):
-            if b is None:
-                continue
-            dst = packed[k * cvol:(k + 1) * cvol]
-            if mask & 1:  # filter skipped for this chunk: raw elements
-                dst[:] = np.frombuffer(b, np.float32, count=cvol)
-            else:
-                dst[:] = bslz4_decode_host(b)[:cvol]
-        if nc * ni * nt == 0:
-            return np.zeros((nc, ni, nt), np.float32, order="F")
-        P = packed.reshape((grid[0], grid[1], grid[2]) + chunk)  # [gt][gi][gc][ct][ci][cc]
-        ax = []
-        for a, (o, kdim) in zip((6, 3, 0), zip(box0, chunk)):
-            ax.append(win[a] + win[a + 2] * np.arange(win[a + 1]) - o)
-        t, i, c = np.ix_(*ax)
-        w = P[t // chunk[0], i // chunk[1], c // chunk[2], t % chunk[0], i % chunk[1],
-              c % chunk[2]]  # [t][i][c]
-        return np.asfortranarray(np.transpose(w, (2, 1, 0)))
+    packed = np.zeros(len(raw) * cvol, np.float32)
+    for k, (mask, b) in enumerate(raw):
+        if b is None:
+            continue
+        dst = packed[k * cvol:(k + 1) * cvol]
+        if mask & 1:  # filter skipped for this chunk: raw elements
+            dst[:] = np.frombuffer(b, np.float32, count=cvol)
+        else:
+            dst[:] = bslz4_decode_host(b)[:cvol]
+    if nc * ni * nt == 0:
+        return np.zeros((nc, ni, nt), np.float32, order="F")
+    P = packed.reshape((grid[0], grid[1], grid[2]) + chunk)  # [gt][gi][gc][ct][ci][cc]
+    ax = [win[a] + win[a + 2] * np.arange(win[a + 1]) - o for a, o in zip((6, 3, 0), box0)]
+    t, i, c = np.ix_(*ax)
+    w = P[t // chunk[0], i // chunk[1], c // chunk[2], t % chunk[0], i % chunk[1],
+          c % chunk[2]]  # [t][i][c]
+    return np.asfortranarray(np.transpose(w, (2, 1, 0)))
+
+
+def _read_window_bslz4_dev(fname, idxs, device, timings=None):
+    """Device path: libhdf5 reads every compressed chunk straight into one
+    pinned buffer, one H2D copy moves it (compressed) to the GPU, the chunks
+    are decoded there into chunk-grid order and the window is gathered.
+    ``timings`` (a dict) receives per-stage wall seconds."""
+    import time
+
     import torch
 
-    from . import engine
+    from . import _lib, engine
 
     dev = torch.device(device)
-    packed = torch.zeros(len(raw) * cvol, dtype=torch.float32, device=dev)
-    comp = [(k, b) for k, (m, b) in enumerate(raw) if b is not None and not m & 1]
-    for k, (m, b) in enumerate(raw):
-        if b is not None and m & 1:
-            packed[k * cvol:(k + 1) * cvol].copy_(
-                torch.from_numpy(np.frombuffer(b, np.float32, count=cvol).copy()))
+    t0 = time.perf_counter()
+
+    def alloc(nbytes):
+        pinned = torch.empty(nbytes + 16, dtype=torch.uint8, pin_memory=True)  # +16: readable pad
+        return pinned.data_ptr(), pinned
+
+    jshape, win, chunk, box0, grid, (chunks, pinned) = read_chunks(fname, idxs, alloc)
+    cvol = int(np.prod(chunk))
+    nc, ni, nt = win[1], win[4], win[7]
+    t1 = time.perf_counter()
     with torch.cuda.device(dev):
+        cdev = pinned.to(dev, non_blocking=True)
+        if timings is not None:
+            torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        packed = torch.zeros(len(chunks) * cvol, dtype=torch.float32, device=dev)
+        host = pinned.numpy()
+        comp = [(k, o, nb) for k, (m, o, nb) in enumerate(chunks) if nb and not m & 1]
+        for k, (m, o, nb) in enumerate(chunks):
+            if nb and m & 1:  # filter skipped for this chunk: raw elements
+                packed.view(torch.uint8)[4 * k * cvol:4 * (k + 1) * cvol].copy_(
+                    cdev[o:o + 4 * cvol])
         if comp:
-            bslz4_decode_dev([b for _, b in comp], out=packed,
-                             out_offsets=[4 * k * cvol for k, _ in comp])
+            offs = np.array([o for _, o, _ in comp], np.uint64)
+            lens = np.array([nb for _, _, nb in comp], np.uint64)
+            ooff = np.array([4 * k * cvol for k, _, _ in comp], np.uint64)
+            rc = _lib.lib().bldp_bslz4_decode_dev(
+                len(comp), host.ctypes.data, cdev.data_ptr(), offs.ctypes.data,
+                lens.ctypes.data, 4, packed.data_ptr(), ooff.ctypes.data, _lib.stream_ptr())
+            _lib.check(rc, "bldp_bslz4_decode_dev")
         out = engine.fb_empty(nc, ni, nt, device=dev)
         if out.numel():
             keep = [(ctypes.c_int64 * 3)(*v) for v in (chunk, box0, grid)]
@@ -606,7 +651,46 @@ def read_window_bslz4(fname, idxs, device=None):
             rc = _lib.lib().bldp_unchunk_f32(packed.data_ptr(), keep[0], keep[1], keep[2], w9,
                                              out.data_ptr(), _lib.stream_ptr())
             _lib.check(rc, "bldp_unchunk_f32")
+        if timings is not None:
+            torch.cuda.synchronize()
+            t3 = time.perf_counter()
+            timings.update(read_chunks_s=t1 - t0, h2d_s=t2 - t1, decode_gather_s=t3 - t2,
+                           compressed_bytes=int(sum(nb for _, _, nb in chunks)))
     return out
+
+
+def write_bslz4_chunks(fname, attrs: dict, jshape, chunk, chunks) -> None:
+    """An FBH5 file with filter 32008 whose chunks (C-order chunk grid, each
+    already encoded) are written raw with H5Dwrite_chunk.  jshape is Julia's
+    (nchans, nifs, nsamps); chunk is C-order (ct, ci, cc)."""
+    H5 = h5()
+    H = H5.L
+    cdims = tuple(jshape)[::-1]
+    f = _ok(H.H5Fcreate(os.fsencode(fname), H5F_ACC_TRUNC, H5P_DEFAULT, H5P_DEFAULT), "create")
+    try:
+        sp = _ok(H.H5Screate_simple(3, _hs(cdims), None), "space")
+        dcpl = _ok(H.H5Pcreate(H5.DATASET_CREATE), "dcpl")
+        _ok(H.H5Pset_chunk(dcpl, 3, _hs(chunk)), "set_chunk")
+        cd = (ctypes.c_uint * 5)(0, 3, 4, 0, 2)
+        _ok(H.H5Pset_filter(dcpl, BSHUF_FILTER_ID, 1, 5, cd), "set_filter 32008")
+        d = _ok(H.H5Dcreate2(f, b"data", H5.NATIVE_FLOAT, sp, H5P_DEFAULT, dcpl, H5P_DEFAULT),
+                "create dataset")
+        H.H5Pclose(dcpl)
+        H.H5Sclose(sp)
+        try:
+            it = iter(chunks)
+            for t0 in range(0, cdims[0], chunk[0]):
+                for i0 in range(0, cdims[1], chunk[1]):
+                    for c0 in range(0, cdims[2], chunk[2]):
+                        enc = next(it)
+                        _ok(H.H5Dwrite_chunk(d, H5P_DEFAULT, 0, _hs([t0, i0, c0]), len(enc),
+                                             enc), "write_chunk")
+            for k, v in dict(attrs, DIMENSION_LABELS=["time", "feed_id", "frequency"]).items():
+                _write_attr(H5, d, k, v)
+        finally:
+            H.H5Dclose(d)
+    finally:
+        H.H5Fclose(f)
 
 
 def write_bslz4(fname, attrs: dict, data: np.ndarray, chunk, encode) -> None:
