@@ -255,3 +255,26 @@ def test_fbh5_bslz4_window_host_decode(pkg, orc, tmp_path):
     it = iter(chunks)
     pkg.fbh5.write_bslz4(q, dict(foff=-0.002861), full, (16, 1, 4096), lambda blk: next(it))
     assert np.array_equal(pkg.fbh5.read_window(q, (C, C, C)), np.asfortranarray(full))
+
+
+def test_fbh5_read_chunks_into_one_buffer(pkg, orc, tmp_path):
+    """The pinned-buffer read path (chunks read by libhdf5 straight into one
+    caller buffer) returns the same bytes as per-chunk reads."""
+    J, C = pkg.JRange, pkg.COLON
+    d = np.asfortranarray(np.random.default_rng(4).random((600, 1, 24)).astype(np.float32))
+    p = tmp_path / "c.h5"
+    pkg.fbh5.write_bslz4(p, {}, d, (8, 1, 256), lambda blk: orc.np_bslz4_encode(blk, 256))
+    bufs = []
+
+    def alloc(n):
+        b = np.zeros(n + 16, np.uint8)
+        bufs.append(b)
+        return b.ctypes.data, b
+
+    per = pkg.fbh5.read_chunks(p, (J(100, 590), C, J(3, 20)))
+    one = pkg.fbh5.read_chunks(p, (J(100, 590), C, J(3, 20)), alloc)
+    assert per[:5] == one[:5] and one[4] == (3, 1, 3)
+    chunks, keep = one[5]
+    assert len(chunks) == len(per[5]) == 9
+    for (m1, b), (m2, off, nb) in zip(per[5], chunks):
+        assert m1 == m2 and keep[off:off + nb].tobytes() == b
