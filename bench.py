@@ -276,8 +276,9 @@ def bench_file(args, eng, torch, pkg):
     C = pkg.COLON
     nbytes = 4 * int(np.prod(jshape))
     got = W.getdata(path, (C, C, C), fqavby=64, tavby=16)  # warm (page cache, pinned pool)
-    want_blk = raw.transpose(2, 1, 0).astype(np.float64).reshape(64, 64, 1, 16).sum(axis=(0, 3))
-    ok = bool(np.allclose(got[:, :, 0], want_blk, rtol=1e-5))
+    orc = entry.load_oracle()
+    want = orc.reduce(np.asfortranarray(raw.transpose(2, 1, 0)), 64, 16)  # one chunk = one t'
+    ok = bool(got.shape == (64, 1, nrep) and np.allclose(got, want, rtol=1e-5))
     steps = max(3, args.steps // 5)
     t0 = time.perf_counter()
     for _ in range(steps):
@@ -287,7 +288,6 @@ def bench_file(args, eng, torch, pkg):
     x = pkg.fbh5._read_window_bslz4_dev(path, (C, C, C), "cuda:0", timings=tm)
     del x
     # CPU path on a bounded window: host decode (C++) + oracle reduce
-    orc = entry.load_oracle()
     J = pkg.JRange
     nt_cpu = 16 * 256
     t0 = time.perf_counter()
