@@ -673,12 +673,71 @@ def read_window_bslz4(fname, idxs, device=None):
     return np.asfortranarray(np.transpose(w, (2, 1, 0)))
 
 
-def _read_window_bslz4_dev(fname, idxs, device, timings=None):
-    """Device path: libhdf5 reads every compressed chunk straight into one
-    pinned buffer, one H2D copy moves it (compressed) to the GPU, the chunks
-    are decoded there into chunk-grid order and the window is gathered.
-    ``timings`` (a dict) receives per-stage wall seconds."""
+def chunk_spans(fname, idxs):
+    """File extents of the stored chunks covering the window, in chunk-grid
+    order, without reading them: (jshape, window, chunk, box0, grid,
+    [(filter_mask, file offset or None, nbytes)]); None when this libhdf5 has
+    no chunk index queries."""
+    if not h5().has_chunk_info:
+        return None
+    H = h5().L
+    lay = layout(fname)
+    cdims, chunk = lay["cdims"], lay["chunk"]
+    if chunk is None or len(cdims) != 3:
+        raise BLDPError(-1, f"{fname}: data is not a chunked 3-D dataset")
+    jshape = cdims[::-1]
+    win = to_window(idxs, jshape) or [0, jshape[0], 1, 0, jshape[1], 1, 0, jshape[2], 1]
+    for ax in range(3):
+        st, ct, sp = win[3 * ax: 3 * ax + 3]
+        if ct > 0:
+            last = st + (ct - 1) * sp
+            if min(st, last) < 0 or max(st, last) >= jshape[ax]:
+                raise BoundsError(-6, f"BoundsError: axis {ax + 1} window {st + 1}:{sp}:"
+                                      f"{last + 1} of {jshape[ax]}")
+    kt0, gt = _box(win[6:9], chunk[0])
+    ki0, gi = _box(win[3:6], chunk[1])
+    kc0, gc = _box(win[0:3], chunk[2])
+    spans = []
+    f = _ok(H.H5Fopen(os.fsencode(fname), H5F_ACC_RDONLY, H5P_DEFAULT), f"open {fname}")
+    try:
+        ub = hsize_t(0)
+        fcpl = H.H5Fget_create_plist(f)
+        if fcpl >= 0:
+            H.H5Pget_userblock(fcpl, ctypes.byref(ub))
+            H.H5Pclose(fcpl)
+        d = _ok(H.H5Dopen2(f, b"data", H5P_DEFAULT), "open dataset 'data'")
+        try:
+            for a in range(gt):
+                for b in range(gi):
+                    for c in range(gc):
+                        off = _hs([(kt0 + a) * chunk[0], (ki0 + b) * chunk[1],
+                                   (kc0 + c) * chunk[2]])
+                        m, addr, size = ctypes.c_uint32(), ctypes.c_uint64(), hsize_t()
+                        if H.H5Dget_chunk_info_by_coord(d, off, ctypes.byref(m),
+                                                        ctypes.byref(addr),
+                                                        ctypes.byref(size)) < 0:
+                            return None
+                        if size.value == 0 or addr.value == 0xFFFFFFFFFFFFFFFF:
+                            spans.append((0, None, 0))  # never written: fill value (0)
+                        else:
+                            spans.append((m.value, ub.value + addr.value, size.value))
+        finally:
+            H.H5Dclose(d)
+    finally:
+        H.H5Fclose(f)
+    box0 = (kt0 * chunk[0], ki0 * chunk[1], kc0 * chunk[2])
+    return jshape, win, tuple(chunk), box0, (gt, gi, gc), spans
+
+
+def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 20):
+    """Device path of a compressed window, overlapped in three stages:
+    a reader thread preads batches of chunks (parallel preadv) into pinned
+    memory and queues their H2D copy on a copy stream, while this thread
+    decodes the previous batch on the GPU (bldp_bslz4_decode_dev); then the
+    window is gathered (bldp_unchunk_f32).  Only compressed bytes cross PCIe.
+    ``timings`` (a dict) receives stage times."""
     import time
+    from concurrent.futures import ThreadPoolExecutor
 
     import torch
 
@@ -686,35 +745,83 @@ def _read_window_bslz4_dev(fname, idxs, device, timings=None):
 
     dev = torch.device(device)
     t0 = time.perf_counter()
-
-    def alloc(nbytes):
-        pinned = torch.empty(nbytes + 16, dtype=torch.uint8, pin_memory=True)  # +16: readable pad
-        return pinned.data_ptr(), pinned
-
-    jshape, win, chunk, box0, grid, (chunks, pinned) = read_chunks(fname, idxs, alloc)
+    plan = chunk_spans(fname, idxs)
+    if plan is None:  # old libhdf5: one H5Dread_chunk per chunk into one buffer
+        def alloc(nbytes):
+            pinned = torch.empty(nbytes + 16, dtype=torch.uint8, pin_memory=True)
+            return pinned.data_ptr(), pinned
+        jshape, win, chunk, box0, grid, (chunks, pinned) = read_chunks(fname, idxs, alloc)
+        spans = [(m, None, nb) for m, _, nb in chunks]
+        offsets = [o for _, o, _ in chunks]
+        preloaded = True
+    else:
+        jshape, win, chunk, box0, grid, spans = plan
+        offsets = list(np.cumsum([0] + [nb for _, _, nb in spans[:-1]]))
+        pinned = torch.empty(max(1, sum(nb for _, _, nb in spans)) + 16, dtype=torch.uint8,
+                             pin_memory=True)
+        preloaded = False
     cvol = int(np.prod(chunk))
     nc, ni, nt = win[1], win[4], win[7]
-    t1 = time.perf_counter()
+    total = int(sum(nb for _, _, nb in spans))
+    host = pinned.numpy()
+    # batches of consecutive chunks, ~batch_bytes of compressed data each
+    batches, cur, acc = [], [], 0
+    for k, (_, _, nb) in enumerate(spans):
+        cur.append(k)
+        acc += nb
+        if acc >= batch_bytes:
+            batches.append(cur)
+            cur, acc = [], 0
+    if cur:
+        batches.append(cur)
     with torch.cuda.device(dev):
-        cdev = pinned.to(dev, non_blocking=True)
-        if timings is not None:
-            torch.cuda.synchronize()
-        t2 = time.perf_counter()
-        packed = torch.zeros(len(chunks) * cvol, dtype=torch.float32, device=dev)
-        host = pinned.numpy()
-        comp = [(k, o, nb) for k, (m, o, nb) in enumerate(chunks) if nb and not m & 1]
-        for k, (m, o, nb) in enumerate(chunks):
-            if nb and m & 1:  # filter skipped for this chunk: raw elements
-                packed.view(torch.uint8)[4 * k * cvol:4 * (k + 1) * cvol].copy_(
-                    cdev[o:o + 4 * cvol])
-        if comp:
-            offs = np.array([o for _, o, _ in comp], np.uint64)
-            lens = np.array([nb for _, _, nb in comp], np.uint64)
-            ooff = np.array([4 * k * cvol for k, _, _ in comp], np.uint64)
-            rc = _lib.lib().bldp_bslz4_decode_dev(
-                len(comp), host.ctypes.data, cdev.data_ptr(), offs.ctypes.data,
-                lens.ctypes.data, 4, packed.data_ptr(), ooff.ctypes.data, _lib.stream_ptr())
-            _lib.check(rc, "bldp_bslz4_decode_dev")
+        cdev = torch.empty(total + 16, dtype=torch.uint8, device=dev)
+        packed = torch.zeros(len(spans) * cvol, dtype=torch.float32, device=dev)
+        copy_stream = torch.cuda.Stream(dev)
+        view = memoryview((ctypes.c_char * (total + 16)).from_address(pinned.data_ptr())) \
+            .cast("B")
+
+        def stage(b):  # reader thread: file -> pinned -> (async) device
+            ks = batches[b]
+            if not preloaded:
+                _pread_all(fname, view, [(spans[k][1], offsets[k], spans[k][2])
+                                         for k in ks if spans[k][2]])
+            lo = offsets[ks[0]]
+            hi = offsets[ks[-1]] + spans[ks[-1]][2]
+            with torch.cuda.device(dev):  # this thread's current device
+                ev = torch.cuda.Event()
+                with torch.cuda.stream(copy_stream):
+                    if hi > lo:
+                        cdev[lo:hi].copy_(pinned[lo:hi], non_blocking=True)
+                    ev.record(copy_stream)
+            return ev
+
+        t_io, t_dec = 0.0, 0.0
+        with ThreadPoolExecutor(max_workers=1) as reader:
+            futs = [reader.submit(stage, b) for b in range(len(batches))]  # runs ahead
+            cur_stream = torch.cuda.current_stream()
+            for b, ks in enumerate(batches):
+                tw = time.perf_counter()
+                ev = futs[b].result()
+                cur_stream.wait_event(ev)
+                t_io += time.perf_counter() - tw
+                td = time.perf_counter()
+                for k in ks:  # chunks stored without the filter: raw elements
+                    m, _, nb = spans[k]
+                    if nb and m & 1:
+                        packed.view(torch.uint8)[4 * k * cvol:4 * (k + 1) * cvol].copy_(
+                            cdev[offsets[k]:offsets[k] + 4 * cvol])
+                comp = [k for k in ks if spans[k][2] and not spans[k][0] & 1]
+                if comp:
+                    offs = np.array([offsets[k] for k in comp], np.uint64)
+                    lens = np.array([spans[k][2] for k in comp], np.uint64)
+                    ooff = np.array([4 * k * cvol for k in comp], np.uint64)
+                    rc = _lib.lib().bldp_bslz4_decode_dev(
+                        len(comp), host.ctypes.data, cdev.data_ptr(), offs.ctypes.data,
+                        lens.ctypes.data, 4, packed.data_ptr(), ooff.ctypes.data,
+                        _lib.stream_ptr())
+                    _lib.check(rc, "bldp_bslz4_decode_dev")
+                t_dec += time.perf_counter() - td
         out = engine.fb_empty(nc, ni, nt, device=dev)
         if out.numel():
             keep = [(ctypes.c_int64 * 3)(*v) for v in (chunk, box0, grid)]
@@ -724,9 +831,8 @@ def _read_window_bslz4_dev(fname, idxs, device, timings=None):
             _lib.check(rc, "bldp_unchunk_f32")
         if timings is not None:
             torch.cuda.synchronize()
-            t3 = time.perf_counter()
-            timings.update(read_chunks_s=t1 - t0, h2d_s=t2 - t1, decode_gather_s=t3 - t2,
-                           compressed_bytes=int(sum(nb for _, _, nb in chunks)))
+            timings.update(total_s=time.perf_counter() - t0, wait_io_s=t_io, decode_s=t_dec,
+                           batches=len(batches), compressed_bytes=total)
     return out
 
 
