@@ -102,18 +102,7 @@ class _H5:
                               herr_t),
             "H5Dwrite_chunk": ([hid_t, hid_t, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t,
                                 ctypes.c_void_p], herr_t),
-            "H5Fget_create_plist": ([hid_t], hid_t),
-            "H5Pget_userblock": ([hid_t, ctypes.c_void_p], herr_t),
         }
-        # chunk index queries (libhdf5 >= 1.10.5); absent -> H5Dread_chunk only
-        try:
-            f = L.H5Dget_chunk_info_by_coord
-            f.argtypes = [hid_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                          ctypes.c_void_p]
-            f.restype = herr_t
-            self.has_chunk_info = True
-        except AttributeError:
-            self.has_chunk_info = False
         for name, (a, r) in sig.items():
             f = getattr(L, name)
             f.argtypes, f.restype = a, r
@@ -556,40 +545,6 @@ def read_chunks(fname, idxs, alloc=None):
                         offs.append(off)
                         sizes.append(nb.value)
             mask = ctypes.c_uint32()
-            if alloc is not None and H5.has_chunk_info:
-                # file addresses of the stored chunks, then parallel preads
-                # straight into the caller's buffer (GIL released, no copies)
-                ub = hsize_t(0)
-                fcpl = H.H5Fget_create_plist(f)
-                if fcpl >= 0:
-                    H.H5Pget_userblock(fcpl, ctypes.byref(ub))
-                    H.H5Pclose(fcpl)
-                spans, masks = [], []
-                for off, nb in zip(offs, sizes):
-                    addr, size = ctypes.c_uint64(), hsize_t()
-                    m = ctypes.c_uint32()
-                    if nb and H.H5Dget_chunk_info_by_coord(d, off, ctypes.byref(m),
-                                                           ctypes.byref(addr),
-                                                           ctypes.byref(size)) >= 0 \
-                            and size.value == nb:
-                        spans.append(ub.value + addr.value)
-                        masks.append(m.value)
-                    else:
-                        spans.append(None if nb == 0 else -1)
-                        masks.append(0)
-                if all(a is None or a >= 0 for a in spans):
-                    base, keep = alloc(max(1, sum(sizes)))
-                    view = memoryview((ctypes.c_char * max(1, sum(sizes))).from_address(base)) \
-                        .cast("B")
-                    jobs, pos = [], 0
-                    for addr, nb, m in zip(spans, sizes, masks):
-                        out.append((m, pos, nb))
-                        if nb:
-                            jobs.append((addr, pos, nb))
-                        pos += nb
-                    _pread_all(fname, view, jobs)
-                    box0 = (kt0 * chunk[0], ki0 * chunk[1], kc0 * chunk[2])
-                    return jshape, win, tuple(chunk), box0, (gt, gi, gc), (out, keep)
             if alloc is None:
                 for off, nb in zip(offs, sizes):
                     if nb == 0:
@@ -615,32 +570,6 @@ def read_chunks(fname, idxs, alloc=None):
         H.H5Fclose(f)
     box0 = (kt0 * chunk[0], ki0 * chunk[1], kc0 * chunk[2])
     return jshape, win, tuple(chunk), box0, (gt, gi, gc), out
-
-
-def _pread_all(fname, view, jobs, nthreads=8):
-    """Read (file offset, buffer offset, nbytes) jobs into `view` with
-    parallel os.preadv calls (each releases the GIL)."""
-    from concurrent.futures import ThreadPoolExecutor
-
-    fd = os.open(fname, os.O_RDONLY)
-    try:
-        def one(job):
-            addr, pos, nb = job
-            got = 0
-            while got < nb:
-                n = os.preadv(fd, [view[pos + got:pos + nb]], addr + got)
-                if n <= 0:
-                    raise BLDPError(-1, f"{fname}: short read at {addr + got}")
-                got += n
-
-        if len(jobs) <= 1:
-            for j in jobs:
-                one(j)
-        else:
-            with ThreadPoolExecutor(max_workers=min(nthreads, len(jobs))) as ex:
-                list(ex.map(one, jobs))
-    finally:
-        os.close(fd)
 
 
 def read_window_bslz4(fname, idxs, device=None):
@@ -673,14 +602,38 @@ def read_window_bslz4(fname, idxs, device=None):
     return np.asfortranarray(np.transpose(w, (2, 1, 0)))
 
 
-def chunk_spans(fname, idxs):
-    """File extents of the stored chunks covering the window, in chunk-grid
-    order, without reading them: (jshape, window, chunk, box0, grid,
-    [(filter_mask, file offset or None, nbytes)]); None when this libhdf5 has
-    no chunk index queries."""
-    if not h5().has_chunk_info:
-        return None
+def _chunk_sizes(H, d, chunk, kt0, ki0, kc0, grid):
+    offs, sizes = [], []
+    for a in range(grid[0]):
+        for b in range(grid[1]):
+            for c in range(grid[2]):
+                off = _hs([(kt0 + a) * chunk[0], (ki0 + b) * chunk[1], (kc0 + c) * chunk[2]])
+                nb = hsize_t()
+                if H.H5Dget_chunk_storage_size(d, off, ctypes.byref(nb)) < 0:
+                    nb.value = 0  # never written: fill value (0)
+                offs.append(off)
+                sizes.append(nb.value)
+    return offs, sizes
+
+
+def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 20):
+    """Device path of a compressed window, overlapped in three stages: a
+    reader thread (the only libhdf5 user while it runs) reads batches of
+    stored chunks with H5Dread_chunk straight into pinned memory and queues
+    their H2D copy on a copy stream, while this thread decodes the previous
+    batch on the GPU (bldp_bslz4_decode_dev); then the window is gathered
+    (bldp_unchunk_f32).  Only compressed bytes cross PCIe.  ``timings`` (a
+    dict) receives stage times."""
+    import time
+    from concurrent.futures import ThreadPoolExecutor
+
+    import torch
+
+    from . import _lib, engine
+
     H = h5().L
+    dev = torch.device(device)
+    t0 = time.perf_counter()
     lay = layout(fname)
     cdims, chunk = lay["cdims"], lay["chunk"]
     if chunk is None or len(cdims) != 3:
@@ -697,131 +650,80 @@ def chunk_spans(fname, idxs):
     kt0, gt = _box(win[6:9], chunk[0])
     ki0, gi = _box(win[3:6], chunk[1])
     kc0, gc = _box(win[0:3], chunk[2])
-    spans = []
+    grid, chunk = (gt, gi, gc), tuple(chunk)
+    box0 = (kt0 * chunk[0], ki0 * chunk[1], kc0 * chunk[2])
+    cvol = int(np.prod(chunk))
+    nc, ni, nt = win[1], win[4], win[7]
     f = _ok(H.H5Fopen(os.fsencode(fname), H5F_ACC_RDONLY, H5P_DEFAULT), f"open {fname}")
     try:
-        ub = hsize_t(0)
-        fcpl = H.H5Fget_create_plist(f)
-        if fcpl >= 0:
-            H.H5Pget_userblock(fcpl, ctypes.byref(ub))
-            H.H5Pclose(fcpl)
         d = _ok(H.H5Dopen2(f, b"data", H5P_DEFAULT), "open dataset 'data'")
         try:
-            for a in range(gt):
-                for b in range(gi):
-                    for c in range(gc):
-                        off = _hs([(kt0 + a) * chunk[0], (ki0 + b) * chunk[1],
-                                   (kc0 + c) * chunk[2]])
-                        m, addr, size = ctypes.c_uint32(), ctypes.c_uint64(), hsize_t()
-                        if H.H5Dget_chunk_info_by_coord(d, off, ctypes.byref(m),
-                                                        ctypes.byref(addr),
-                                                        ctypes.byref(size)) < 0:
-                            return None
-                        if size.value == 0 or addr.value == 0xFFFFFFFFFFFFFFFF:
-                            spans.append((0, None, 0))  # never written: fill value (0)
-                        else:
-                            spans.append((m.value, ub.value + addr.value, size.value))
+            coords, sizes = _chunk_sizes(H, d, chunk, kt0, ki0, kc0, grid)
+            offsets = [0] + list(np.cumsum(sizes[:-1]).astype(np.int64))
+            total = int(sum(sizes))
+            masks = [0] * len(sizes)
+            pinned = torch.empty(total + 16, dtype=torch.uint8, pin_memory=True)
+            host = pinned.numpy()
+            batches, cur, acc = [], [], 0
+            for k, nb in enumerate(sizes):
+                cur.append(k)
+                acc += nb
+                if acc >= batch_bytes:
+                    batches.append(cur)
+                    cur, acc = [], 0
+            if cur:
+                batches.append(cur)
+            with torch.cuda.device(dev):
+                cdev = torch.empty(total + 16, dtype=torch.uint8, device=dev)
+                packed = torch.zeros(len(sizes) * cvol, dtype=torch.float32, device=dev)
+                copy_stream = torch.cuda.Stream(dev)
+
+                def stage(ks):  # reader thread: file -> pinned -> (async) device
+                    m = ctypes.c_uint32()
+                    for k in ks:
+                        if sizes[k]:
+                            _ok(H.H5Dread_chunk(d, H5P_DEFAULT, coords[k], ctypes.byref(m),
+                                                ctypes.c_void_p(pinned.data_ptr() + offsets[k])),
+                                "read_chunk")
+                            masks[k] = m.value
+                    lo, hi = offsets[ks[0]], offsets[ks[-1]] + sizes[ks[-1]]
+                    with torch.cuda.device(dev):
+                        ev = torch.cuda.Event()
+                        with torch.cuda.stream(copy_stream):
+                            if hi > lo:
+                                cdev[lo:hi].copy_(pinned[lo:hi], non_blocking=True)
+                            ev.record(copy_stream)
+                    return ev
+
+                t_io = t_dec = 0.0
+                with ThreadPoolExecutor(max_workers=1) as reader:
+                    futs = [reader.submit(stage, ks) for ks in batches]  # reads run ahead
+                    cur_stream = torch.cuda.current_stream()
+                    for b, ks in enumerate(batches):
+                        tw = time.perf_counter()
+                        cur_stream.wait_event(futs[b].result())
+                        t_io += time.perf_counter() - tw
+                        td = time.perf_counter()
+                        for k in ks:  # stored without the filter: raw elements
+                            if sizes[k] and masks[k] & 1:
+                                packed.view(torch.uint8)[4 * k * cvol:4 * (k + 1) * cvol].copy_(
+                                    cdev[offsets[k]:offsets[k] + 4 * cvol])
+                        comp = [k for k in ks if sizes[k] and not masks[k] & 1]
+                        if comp:
+                            offs = np.array([offsets[k] for k in comp], np.uint64)
+                            lens = np.array([sizes[k] for k in comp], np.uint64)
+                            ooff = np.array([4 * k * cvol for k in comp], np.uint64)
+                            rc = _lib.lib().bldp_bslz4_decode_dev(
+                                len(comp), host.ctypes.data, cdev.data_ptr(), offs.ctypes.data,
+                                lens.ctypes.data, 4, packed.data_ptr(), ooff.ctypes.data,
+                                _lib.stream_ptr())
+                            _lib.check(rc, "bldp_bslz4_decode_dev")
+                        t_dec += time.perf_counter() - td
         finally:
             H.H5Dclose(d)
     finally:
         H.H5Fclose(f)
-    box0 = (kt0 * chunk[0], ki0 * chunk[1], kc0 * chunk[2])
-    return jshape, win, tuple(chunk), box0, (gt, gi, gc), spans
-
-
-def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 20):
-    """Device path of a compressed window, overlapped in three stages:
-    a reader thread preads batches of chunks (parallel preadv) into pinned
-    memory and queues their H2D copy on a copy stream, while this thread
-    decodes the previous batch on the GPU (bldp_bslz4_decode_dev); then the
-    window is gathered (bldp_unchunk_f32).  Only compressed bytes cross PCIe.
-    ``timings`` (a dict) receives stage times."""
-    import time
-    from concurrent.futures import ThreadPoolExecutor
-
-    import torch
-
-    from . import _lib, engine
-
-    dev = torch.device(device)
-    t0 = time.perf_counter()
-    plan = chunk_spans(fname, idxs)
-    if plan is None:  # old libhdf5: one H5Dread_chunk per chunk into one buffer
-        def alloc(nbytes):
-            pinned = torch.empty(nbytes + 16, dtype=torch.uint8, pin_memory=True)
-            return pinned.data_ptr(), pinned
-        jshape, win, chunk, box0, grid, (chunks, pinned) = read_chunks(fname, idxs, alloc)
-        spans = [(m, None, nb) for m, _, nb in chunks]
-        offsets = [o for _, o, _ in chunks]
-        preloaded = True
-    else:
-        jshape, win, chunk, box0, grid, spans = plan
-        offsets = list(np.cumsum([0] + [nb for _, _, nb in spans[:-1]]))
-        pinned = torch.empty(max(1, sum(nb for _, _, nb in spans)) + 16, dtype=torch.uint8,
-                             pin_memory=True)
-        preloaded = False
-    cvol = int(np.prod(chunk))
-    nc, ni, nt = win[1], win[4], win[7]
-    total = int(sum(nb for _, _, nb in spans))
-    host = pinned.numpy()
-    # batches of consecutive chunks, ~batch_bytes of compressed data each
-    batches, cur, acc = [], [], 0
-    for k, (_, _, nb) in enumerate(spans):
-        cur.append(k)
-        acc += nb
-        if acc >= batch_bytes:
-            batches.append(cur)
-            cur, acc = [], 0
-    if cur:
-        batches.append(cur)
     with torch.cuda.device(dev):
-        cdev = torch.empty(total + 16, dtype=torch.uint8, device=dev)
-        packed = torch.zeros(len(spans) * cvol, dtype=torch.float32, device=dev)
-        copy_stream = torch.cuda.Stream(dev)
-        view = memoryview((ctypes.c_char * (total + 16)).from_address(pinned.data_ptr())) \
-            .cast("B")
-
-        def stage(b):  # reader thread: file -> pinned -> (async) device
-            ks = batches[b]
-            if not preloaded:
-                _pread_all(fname, view, [(spans[k][1], offsets[k], spans[k][2])
-                                         for k in ks if spans[k][2]])
-            lo = offsets[ks[0]]
-            hi = offsets[ks[-1]] + spans[ks[-1]][2]
-            with torch.cuda.device(dev):  # this thread's current device
-                ev = torch.cuda.Event()
-                with torch.cuda.stream(copy_stream):
-                    if hi > lo:
-                        cdev[lo:hi].copy_(pinned[lo:hi], non_blocking=True)
-                    ev.record(copy_stream)
-            return ev
-
-        t_io, t_dec = 0.0, 0.0
-        with ThreadPoolExecutor(max_workers=1) as reader:
-            futs = [reader.submit(stage, b) for b in range(len(batches))]  # runs ahead
-            cur_stream = torch.cuda.current_stream()
-            for b, ks in enumerate(batches):
-                tw = time.perf_counter()
-                ev = futs[b].result()
-                cur_stream.wait_event(ev)
-                t_io += time.perf_counter() - tw
-                td = time.perf_counter()
-                for k in ks:  # chunks stored without the filter: raw elements
-                    m, _, nb = spans[k]
-                    if nb and m & 1:
-                        packed.view(torch.uint8)[4 * k * cvol:4 * (k + 1) * cvol].copy_(
-                            cdev[offsets[k]:offsets[k] + 4 * cvol])
-                comp = [k for k in ks if spans[k][2] and not spans[k][0] & 1]
-                if comp:
-                    offs = np.array([offsets[k] for k in comp], np.uint64)
-                    lens = np.array([spans[k][2] for k in comp], np.uint64)
-                    ooff = np.array([4 * k * cvol for k in comp], np.uint64)
-                    rc = _lib.lib().bldp_bslz4_decode_dev(
-                        len(comp), host.ctypes.data, cdev.data_ptr(), offs.ctypes.data,
-                        lens.ctypes.data, 4, packed.data_ptr(), ooff.ctypes.data,
-                        _lib.stream_ptr())
-                    _lib.check(rc, "bldp_bslz4_decode_dev")
-                t_dec += time.perf_counter() - td
         out = engine.fb_empty(nc, ni, nt, device=dev)
         if out.numel():
             keep = [(ctypes.c_int64 * 3)(*v) for v in (chunk, box0, grid)]
