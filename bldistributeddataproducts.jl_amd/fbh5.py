@@ -659,7 +659,7 @@ def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 
         d = _ok(H.H5Dopen2(f, b"data", H5P_DEFAULT), "open dataset 'data'")
         try:
             coords, sizes = _chunk_sizes(H, d, chunk, kt0, ki0, kc0, grid)
-            offsets = [0] + list(np.cumsum(sizes[:-1]).astype(np.int64))
+            offsets = [0] + [int(x) for x in np.cumsum(sizes[:-1])]
             total = int(sum(sizes))
             masks = [0] * len(sizes)
             pinned = torch.empty(total + 16, dtype=torch.uint8, pin_memory=True)
