@@ -521,6 +521,55 @@ __global__ __launch_bounds__(kBlock) void k_kurt_pass(const KurtArgs k) {
   }
 }
 
+// Short windows (nt <= NTMAX spectra): each lane keeps its float4 column of
+// every spectrum in registers, so the window is read from HBM once; the
+// arithmetic is the same two-pass StatsBase recipe, run over the registers.
+template <int NTMAX>
+__global__ __launch_bounds__(kBlock) void k_kurt_regs(const KurtArgs k) {
+  const int64_t ncols = k.nc / 4;
+  const int64_t ctiles = (ncols + kBlock - 1) / kBlock;
+  const int64_t b = blockIdx.x;
+  const int64_t ib = b / ctiles, col = (b % ctiles) * kBlock + threadIdx.x;
+  if (col >= ncols) return;
+  const int bank = (int)(ib / k.ni);
+  const int64_t i = ib - (int64_t)bank * k.ni;
+  const float *p = k.in[bank] + k.in_off + i * k.in_ld_i + 4 * col;
+  const int nt = (int)k.nt;
+  float4 v[NTMAX];
+#pragma unroll
+  for (int t = 0; t < NTMAX; ++t)
+    if (t < nt) v[t] = ld4(p + t * k.in_ld_t);
+  double s[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int t = 0; t < NTMAX; ++t)
+    if (t < nt) {
+      s[0] += (double)v[t].x; s[1] += (double)v[t].y;
+      s[2] += (double)v[t].z; s[3] += (double)v[t].w;
+    }
+  float m[4];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) m[w] = (float)s[w] / (float)nt;  // Float32 sum / length
+  double c2[4] = {0, 0, 0, 0}, c4[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int t = 0; t < NTMAX; ++t)
+    if (t < nt) {
+      const float x[4] = {v[t].x, v[t].y, v[t].z, v[t].w};
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const float z = x[w] - m[w];  // StatsBase: z, z2 in Float32; Float64 moments
+        const float z2 = z * z;
+        c2[w] += (double)z2;
+        c4[w] += (double)(z2 * z2);
+      }
+    }
+  const int64_t e = ib * k.nc + 4 * col;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const double cm2 = c2[w] / (double)k.nt, cm4 = c4[w] / (double)k.nt;
+    k.out[e + w] = (cm4 / (cm2 * cm2)) - 3.0;
+  }
+}
+
 // Fold the time-chunk partials of every (channel, IF), few chunks: one lane
 // per output, chunks in order.
 template <int PASS>
@@ -793,6 +842,14 @@ hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s) {
   k.ws_mom = reinterpret_cast<double *>(ws + up(n * k.nchunk * sizeof(double)) +
                                         up(n * sizeof(float)));
   const int64_t ncols = k.vec ? k.nc / 4 : k.nc;
+  if (k.vec && k.nt > 0 && k.nt <= 32) {  // one HBM read: the column fits in registers
+    const dim3 g1((unsigned)(cdiv(ncols, kBlock) * k.nrow));
+    if (k.nt <= 16)
+      hipLaunchKernelGGL(k_kurt_regs<16>, g1, dim3(kBlock), 0, s, k);
+    else
+      hipLaunchKernelGGL(k_kurt_regs<32>, g1, dim3(kBlock), 0, s, k);
+    return hipGetLastError();
+  }
   const dim3 grid((unsigned)(cdiv(cdiv(ncols, 64), 4 / k.ts) * k.nrow * k.nchunk)), block(kBlock);
   const bool wide = k.nchunk > 16;  // wave per output only when there is much to fold
   const unsigned fg = (unsigned)std::min<int64_t>(cdiv((int64_t)n, wide ? 4 : kBlock), 16384);

@@ -303,3 +303,16 @@ def test_full_size_cfg4_and_cfg2_banks(eng, orc):
     want = orc.stitch([orc.reduce(b, 64, 16, "sum", [0, 65536, 1, 0, 1, 1, 0, 272, 1])
                        for b in banks])
     np.testing.assert_allclose(got, want, rtol=RTOL)
+
+
+@pytest.mark.parametrize("nt", [1, 2, 7, 16, 17, 32, 33])
+def test_kurtosis_short_windows(eng, orc, nt):
+    """nt <= 32 runs the register-resident single-read kernel; 33 the two-pass."""
+    rng = np.random.default_rng(nt)
+    a = np.asfortranarray((rng.standard_normal((4096, 2, nt)) ** 2).astype(np.float32) * 1e6)
+    got = host(eng, eng.kurtosis(dev(eng, a)))
+    want = orc.kurtosis(a)
+    assert np.array_equal(np.isnan(got), np.isnan(want))
+    np.testing.assert_allclose(got, want, rtol=1e-4, atol=1e-5)
+    ks = eng.band_kurtosis([dev(eng, a), dev(eng, a[::-1].copy(order="F"))])
+    np.testing.assert_allclose(host(eng, ks[0]), want, rtol=1e-4, atol=1e-5)
