@@ -54,6 +54,7 @@ SIGNATURES = {
     "bldp_reduce_strided_f32": ([P, I64, I64, I64, P, I64, I64, I, P, I64, I64, P], I),
     "bldp_reduce_host_f32": ([I, P, I64, I64, I64, P, I64, I64, I, P], I),
     "bldp_band_reduce_f32": ([I, P, I64, I64, I64, P, I64, I64, I, P, P], I),
+    "bldp_band_reduce_multi_f32": ([I, P, P, I64, I64, I64, P, I64, I64, I, I, P], I),
     "bldp_stitch_f32": ([I, P, I64, I64, I64, P, P], I),
     "bldp_despike_f32": ([P, I64, I64, I64, I64, P], I),
     "bldp_kurtosis_workspace_size": ([I64, I64, I64, P], SZ),

@@ -308,6 +308,82 @@ int bldp_band_reduce_f32(int nbank, const float *const *in, int64_t nchan, int64
                      (hipStream_t)stream, nullptr);
 }
 
+int bldp_band_reduce_multi_f32(int nbank, const int *bank_dev, const float *const *in,
+                               int64_t nchan, int64_t nif, int64_t ntime, const int64_t *win,
+                               int64_t fqavby, int64_t tavby, int op, int root, float *out) {
+  if (nbank < 1 || nbank > BLDP_MAX_BANKS || !bank_dev || !in)
+    return fail(BLDP_EINVAL, "bad bank arguments");
+  int ndev = 0;
+  HIPCHK(hipGetDeviceCount(&ndev));
+  if (root < 0 || root >= ndev) return fail(BLDP_EINVAL, "root device %d not available", root);
+  for (int b = 0; b < nbank; ++b)
+    if (bank_dev[b] < 0 || bank_dev[b] >= ndev)
+      return fail(BLDP_EINVAL, "bank %d: device %d not available", b, bank_dev[b]);
+  int64_t sh[3];
+  int rc = bldp_reduce_shape(nchan, nif, ntime, win, fqavby, tavby, sh);
+  if (rc) return rc;
+  const int64_t nco = sh[0], ni = sh[1], nto = sh[2];
+  if (nco * ni * nto == 0) return BLDP_OK;
+  if (!out) return fail(BLDP_EINVAL, "null output pointer");
+  const int64_t ld_i = (int64_t)nbank * nco, ld_t = ld_i * ni;
+  int prev = 0;
+  HIPCHK(hipGetDevice(&prev));
+  std::vector<hipStream_t> streams(ndev, nullptr);
+  std::vector<float *> staging(nbank, nullptr);
+  rc = BLDP_OK;
+  for (int b = 0; b < nbank && rc == BLDP_OK; ++b) {
+    const int d = bank_dev[b];
+    if (hipSetDevice(d) != hipSuccess) {
+      rc = fail(BLDP_EHIP, "hipSetDevice(%d) failed", d);
+      break;
+    }
+    if (!streams[d] && hipStreamCreateWithFlags(&streams[d], hipStreamNonBlocking) != hipSuccess) {
+      rc = fail(BLDP_EHIP, "stream creation on device %d failed", d);
+      break;
+    }
+    bool direct = d == root;
+    if (!direct) {  // kernels write the root's product over xGMI when peer access works
+      int can = 0;
+      if (hipDeviceCanAccessPeer(&can, d, root) == hipSuccess && can) {
+        hipError_t pe = hipDeviceEnablePeerAccess(root, 0);
+        direct = pe == hipSuccess || pe == hipErrorPeerAccessAlreadyEnabled;
+        (void)hipGetLastError();
+      }
+    }
+    const float *ins[1] = {in[b]};
+    if (direct) {
+      rc = reduce_impl(1, ins, nchan, nif, ntime, win, fqavby, tavby, op, out + b * nco, 0,
+                       ld_i, ld_t, false, streams[d], nullptr);
+    } else {  // reduce locally, then one strided peer copy into the bank's slot
+      if (hipMalloc(&staging[b], (size_t)(nco * ni * nto) * sizeof(float)) != hipSuccess) {
+        rc = fail(BLDP_ENOMEM, "staging allocation on device %d failed", d);
+        break;
+      }
+      rc = reduce_impl(1, ins, nchan, nif, ntime, win, fqavby, tavby, op, staging[b], 0, nco,
+                       nco * ni, false, streams[d], nullptr);
+      if (rc == BLDP_OK &&
+          hipMemcpy2DAsync(out + b * nco, ld_i * sizeof(float), staging[b], nco * sizeof(float),
+                           nco * sizeof(float), (size_t)(ni * nto), hipMemcpyDeviceToDevice,
+                           streams[d]) != hipSuccess)
+        rc = fail(BLDP_EHIP, "peer copy of bank %d failed", b);
+    }
+  }
+  for (int d = 0; d < ndev; ++d)
+    if (streams[d]) {
+      (void)hipSetDevice(d);
+      if (hipStreamSynchronize(streams[d]) != hipSuccess && rc == BLDP_OK)
+        rc = fail(BLDP_EHIP, "device %d failed during the band reduce", d);
+      (void)hipStreamDestroy(streams[d]);
+    }
+  for (int b = 0; b < nbank; ++b)
+    if (staging[b]) {
+      (void)hipSetDevice(bank_dev[b]);
+      (void)hipFree(staging[b]);
+    }
+  (void)hipSetDevice(prev);
+  return rc;
+}
+
 int bldp_stitch_f32(int nbank, const float *gathered, int64_t nc, int64_t nif, int64_t ntime,
                     float *out, void *stream) {
   if (nbank < 1 || nbank > BLDP_MAX_BANKS)

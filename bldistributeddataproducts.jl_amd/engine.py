@@ -20,7 +20,8 @@ from . import _lib
 from .idxs import window_shape
 
 __all__ = [
-    "fb_empty", "fb_from_numpy", "fb_to_numpy", "reduce", "band_reduce", "stitch",
+    "fb_empty", "fb_from_numpy", "fb_to_numpy", "reduce", "band_reduce", "band_reduce_multi",
+    "stitch",
     "despike", "kurtosis", "band_kurtosis", "synth", "plan", "reduce_host", "kurtosis_host",
 ]
 
@@ -190,6 +191,33 @@ def band_reduce(banks, fqavby=1, tavby=1, op="sum", win=None, out=None, stream=N
                                 out.data_ptr() if out.numel() else None,
                                 _lib.stream_ptr(stream))
     _lib.check(rc, "bldp_band_reduce_f32")
+    return out
+
+
+def band_reduce_multi(banks, fqavby=1, tavby=1, op="sum", win=None, root=0):
+    """One process, banks on several GPUs (bldp_band_reduce_multi_f32): each
+    GPU reduces its banks straight into the stitched product on `root`."""
+    torch = _torch()
+    L = _lib.lib()
+    banks = list(banks)
+    shape = tuple(banks[0].shape)
+    geo = _abi_dims(banks[0])[1:]
+    for b in banks[1:]:
+        if tuple(b.shape) != shape or _abi_dims(b)[1:] != geo:
+            raise ValueError("all banks of a band must have the same shape and layout")
+    _check_bounds(win, shape)
+    nco, ni, nto = out_shape(shape, win, fqavby, tavby)
+    out = fb_empty(len(banks) * nco, ni, nto, device=torch.device("cuda", root))
+    devs = (ctypes.c_int * len(banks))(*[b.device.index for b in banks])
+    ptrs = (ctypes.c_void_p * len(banks))(*[b.data_ptr() for b in banks])
+    keep, wp = _lib.win_arg(_full_win(win, shape))
+    for d in {b.device.index for b in banks}:
+        torch.cuda.synchronize(d)  # inputs written on torch streams are complete
+    rc = L.bldp_band_reduce_multi_f32(len(banks), ctypes.cast(devs, ctypes.c_void_p),
+                                      ctypes.cast(ptrs, ctypes.c_void_p), *geo, wp,
+                                      int(fqavby), int(tavby), _lib.OPS[op], int(root),
+                                      out.data_ptr() if out.numel() else None)
+    _lib.check(rc, "bldp_band_reduce_multi_f32")
     return out
 
 

@@ -116,6 +116,17 @@ BLDP_API int bldp_band_reduce_f32(int nbank, const float *const *in, int64_t nch
                          int64_t ntime, const int64_t *win, int64_t fqavby, int64_t tavby,
                          int op, float *out, void *stream);
 
+/* One process, one or more banks per GPU: bank b lives on
+ * device bank_dev[b] (in[b] is a device pointer there).  Every device reduces
+ * its banks and writes each result straight into its vcat slot of `out`, the
+ * stitched (nbank*nco, ni, nto) product on device `root` — over xGMI with peer
+ * access, else through a staged peer copy.  Synchronous; all banks share the
+ * same (nchan, nif, ntime) and window. */
+BLDP_API int bldp_band_reduce_multi_f32(int nbank, const int *bank_dev, const float *const *in,
+                                        int64_t nchan, int64_t nif, int64_t ntime,
+                                        const int64_t *win, int64_t fqavby, int64_t tavby,
+                                        int op, int root, float *out);
+
 /* gathered: nbank dense blocks (nc, nif, ntime) back to back (bank-major,
  * what a gather to the root leaves); out: (nbank*nc, nif, ntime) = vcat. */
 BLDP_API int bldp_stitch_f32(int nbank, const float *gathered, int64_t nc, int64_t nif, int64_t ntime,

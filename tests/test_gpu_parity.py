@@ -316,3 +316,24 @@ def test_kurtosis_short_windows(eng, orc, nt):
     np.testing.assert_allclose(got, want, rtol=1e-4, atol=1e-5)
     ks = eng.band_kurtosis([dev(eng, a), dev(eng, a[::-1].copy(order="F"))])
     np.testing.assert_allclose(host(eng, ks[0]), want, rtol=1e-4, atol=1e-5)
+
+
+def test_band_reduce_multi_device_api(eng, orc, pkg):
+    """The single-process multi-GPU entry point; on a one-GPU box every bank
+    sits on device 0 (the peer path runs on the driver's 8-GPU node)."""
+    import torch
+
+    banks = [orc.gamma_bandpass(8192, 2, 48, 1024, 300 + b) for b in range(8)]
+    xs = [dev(eng, b) for b in banks]
+    w = [0, 8192, 1, 0, 2, 1, 0, 48, 1]
+    got = host(eng, eng.band_reduce_multi(xs, 64, 16, "sum", w))
+    want = orc.stitch([orc.reduce(b, 64, 16, "sum", w) for b in banks])
+    np.testing.assert_allclose(got, want, rtol=RTOL)
+    assert same_bits(got, host(eng, eng.band_reduce(xs, 64, 16, "sum", w)))
+    L = pkg._lib.lib()
+    import ctypes
+
+    devs = (ctypes.c_int * 2)(0, torch.cuda.device_count())  # no such device
+    ptrs = (ctypes.c_void_p * 2)(xs[0].data_ptr(), xs[1].data_ptr())
+    rc = L.bldp_band_reduce_multi_f32(2, devs, ptrs, 8192, 2, 48, None, 64, 16, 0, 0, None)
+    assert rc == pkg._lib.BLDP_EINVAL
