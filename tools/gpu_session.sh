@@ -42,6 +42,7 @@ for s in $STEPS; do
     host)  run host 900 python bench.py --mode host ;;
     decode) run decode 600 python bench.py --mode decode ;;
     file)  run file 600 python bench.py --mode file ;;
+    paths) run paths 300 python tools/probe_paths.py ;;
     prof_decode) run prof_decode 600 rocprofv3 --kernel-trace --stats --output-format csv \
              -d "$OUT/prof_decode" -o run -- python bench.py --mode decode ;;
     prof_kurt) run prof_kurt 600 rocprofv3 --kernel-trace --stats --output-format csv \
