@@ -158,10 +158,10 @@ int scratch(hipStream_t s, size_t bytes, void **out) { return bldp::scratch_byte
 
 bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
 
-bool vec_ok(const Geo &g) {
-  return g.cs == 1 && g.off % 4 == 0 && (g.ni <= 1 || g.ld_i % 4 == 0) &&
-         (g.nt <= 1 || g.ld_t % 4 == 0);
+bool pitch_ok(const Geo &g) {
+  return (g.ni <= 1 || g.ld_i % 4 == 0) && (g.nt <= 1 || g.ld_t % 4 == 0);
 }
+bool vec_ok(const Geo &g) { return g.cs == 1 && g.off % 4 == 0 && pitch_ok(g); }
 
 int valid_op(int op) { return op >= BLDP_OP_SUM && op <= BLDP_OP_MIN; }
 
@@ -201,13 +201,14 @@ int reduce_impl(int nbank, const float *const *in, int64_t nchan, int64_t nif, i
   a.in_ld_t = g.ld_t;
   a.out = out;
   const bool empty = a.nco == 0 || a.ni == 0 || a.nto == 0;
-  bool aligned = vec_ok(g);
+  bool rows16 = pitch_ok(g);
   if (!in) return fail(BLDP_EINVAL, "null input pointer array");
   for (int b = 0; b < nbank; ++b) {
     a.in[b] = in[b];
-    aligned = aligned && aligned16(a.in[b]);
+    rows16 = rows16 && aligned16(a.in[b]);
   }
-  Plan p = plan_reduce(a, aligned, num_cus_current());
+  const bool aligned = rows16 && vec_ok(g);
+  Plan p = plan_reduce(a, aligned, rows16, num_cus_current());
   if (!info) {
     for (int b = 0; b < nbank; ++b)
       if (!in[b] && !empty) return fail(BLDP_EINVAL, "null input pointer (bank %d)", b);

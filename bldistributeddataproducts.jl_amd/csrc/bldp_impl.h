@@ -33,10 +33,11 @@ struct RedArgs {
   int32_t ts;              // waves of a tile that split the T rows (1, 2, 4)
   int32_t k4;              // float4 loads per lane per row (vector path)
   int32_t vec_out;         // narrow path: 16/8-byte output stores are legal
+  int64_t gpt;             // tile path: output channels (groups) per workgroup tile
   float div;               // F*T, the mean divisor
 };
 
-enum Path { PATH_VEC = 0, PATH_NARROW = 1, PATH_SCALAR = 2 };
+enum Path { PATH_VEC = 0, PATH_NARROW = 1, PATH_SCALAR = 2, PATH_TILE = 3 };
 
 struct Plan {
   int path;
@@ -48,8 +49,10 @@ struct Plan {
 
 // Fill the launch geometry (path, lpg, ts, k4, nchunk, rows_per_chunk,
 // blocks_c, grid) for an args struct whose shape/stride fields are set.
-// `aligned` says whether 16-byte vector loads are legal.
-Plan plan_reduce(RedArgs &a, bool aligned, int num_cus);
+// `aligned` says whether 16-byte vector loads of every group are legal;
+// `rows16` whether every bank pointer is 16-byte aligned and the IF/time
+// pitches are multiples of 4 floats (any channel offset and step).
+Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, int num_cus);
 
 hipError_t launch_reduce(const RedArgs &a, const Plan &p, int op, hipStream_t s);
 

@@ -317,6 +317,115 @@ __device__ __forceinline__ void scalar_tile(const RedArgs &a, int64_t tile) {
     a.ws[(((c.chunk * a.nbank + c.bank) * a.nto + c.to) * a.ni + c.i) * a.nco + co] = s;
 }
 
+// ---------------------------------------------------------------------------
+// Tile path: channel step cs in 1..8, any F that fits a tile, any channel
+// alignment (e.g. idxs = (1000:2023, :, :)), aligned row pitches.  Time
+// integration is element-wise, so a workgroup streams the 16-byte-aligned
+// superset of its tile's channels (gpt groups = gpt*F window channels, at most
+// kSpan floats of a row) with 1 KiB-per-wave float4 loads, sums the T rows of
+// every channel in registers, then drops the selected channels into LDS and
+// folds each group of F there: 16-channel segments first, then the segments
+// of a group.  HBM traffic is the window plus <= 3 floats per tile row edge.
+constexpr int kTK = 4;                   // float4 columns per thread
+constexpr int kSpan = kBlock * 4 * kTK;  // floats of one row one tile may read
+constexpr int kSeg = 16;                 // channels folded per thread in stage 1
+__device__ __forceinline__ int lpad(int x) { return x + (x >> 4); }  // LDS bank spread
+
+template <int OP, bool CS1>
+__device__ __forceinline__ void tile_tile(const RedArgs &a, int64_t tile) {
+  __shared__ float lds[kSpan + kSpan / 16];
+  __shared__ float part[2 * kBlock];
+  const Coord c = decompose(a, tile);
+  const int tid = threadIdx.x;
+  const int64_t co0 = c.bc * a.gpt;  // first output channel of the tile
+  const int gt = (int)min<int64_t>(a.gpt, a.nco - co0);
+  const int F = (int)a.F;
+  const int cs = CS1 ? 1 : (int)a.in_cs;
+  const int ncht = gt * F;  // window channels of the tile
+  const int64_t abs0 = a.in_off + c.i * a.in_ld_i + co0 * a.F * cs;
+  const int mis = (int)(abs0 & 3);  // row pitches are multiples of 4 floats
+  const int w4 = (mis + (ncht - 1) * cs + 1 + 3) >> 2;
+  const int64_t r0 = c.chunk * a.rows_per_chunk;
+  const int64_t r1 = min(a.T, r0 + a.rows_per_chunk);
+  const float id = R<OP>::id();
+  const float4 id4 = make_float4(id, id, id, id);
+  const float *p = a.in[c.bank] + (abs0 - mis) + (c.to * a.T + r0) * a.in_ld_t + 4 * tid;
+  const int64_t st = a.in_ld_t;
+
+  float4 acc[2][kTK];
+#pragma unroll
+  for (int k = 0; k < kTK; ++k) acc[0][k] = acc[1][k] = id4;
+  int64_t nrows = r1 - r0;
+  for (; nrows >= 2; nrows -= 2) {
+    float4 v[2][kTK];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int k = 0; k < kTK; ++k)
+        v[u][k] = (tid + k * kBlock < w4) ? ld4(p + u * st + 4 * k * kBlock) : id4;
+    p += 2 * st;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int k = 0; k < kTK; ++k) acc[u][k] = f4<OP>(acc[u][k], v[u][k]);
+  }
+  if (nrows > 0) {
+#pragma unroll
+    for (int k = 0; k < kTK; ++k)
+      if (tid + k * kBlock < w4) acc[0][k] = f4<OP>(acc[0][k], ld4(p + 4 * k * kBlock));
+  }
+#pragma unroll
+  for (int k = 0; k < kTK; ++k) {
+    const int col = tid + k * kBlock;
+    if (col >= w4) continue;
+    const float4 r = f4<OP>(acc[0][k], acc[1][k]);
+    const float e[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int x = 4 * col + q - mis;  // element offset from the tile's first channel
+      if (x < 0) continue;
+      int ch = x;
+      if (!CS1) {
+        if (x % cs) continue;
+        ch = x / cs;
+      }
+      if (ch < ncht) lds[lpad(ch)] = e[q];
+    }
+  }
+  __syncthreads();
+
+  auto store = [&](int g, float s) {
+    const int64_t co = co0 + g;
+    if (a.nchunk == 1)
+      a.out[c.bank * a.out_bank + c.i * a.out_ld_i + c.to * a.out_ld_t + co] = finish<OP>(s, a);
+    else
+      a.ws[(((c.chunk * a.nbank + c.bank) * a.nto + c.to) * a.ni + c.i) * a.nco + co] = s;
+  };
+  if (F <= kSeg) {
+    for (int g = tid; g < gt; g += kBlock) {
+      float s = id;
+      for (int k = 0; k < F; ++k) s = R<OP>::f(s, lds[lpad(g * F + k)]);
+      store(g, s);
+    }
+  } else {
+    const int nseg = (F + kSeg - 1) / kSeg;  // gt * nseg <= 2 * kBlock (F > kSeg)
+    for (int q = tid; q < gt * nseg; q += kBlock) {
+      const int g = q / nseg, sg = q - g * nseg;
+      const int x0 = g * F + sg * kSeg, x1 = min(x0 + kSeg, g * F + F);
+      float s = id;
+      for (int x = x0; x < x1; ++x) s = R<OP>::f(s, lds[lpad(x)]);
+      part[q] = s;
+    }
+    __syncthreads();
+    for (int g = tid; g < gt; g += kBlock) {
+      float s = id;
+      for (int sg = 0; sg < nseg; ++sg) s = R<OP>::f(s, part[g * nseg + sg]);
+      store(g, s);
+    }
+  }
+  __syncthreads();  // lds/part are reused by the next tile of a grid-stride loop
+}
+
 // Grid-stride wrappers: one tile per workgroup when the grid covers every
 // tile (the default), several when plan_reduce caps the grid (BLDP_MAX_WG_PER_CU).
 template <int OP, int LPG, int K4C>
@@ -330,6 +439,10 @@ __global__ __launch_bounds__(kBlock) void k_reduce_narrow(const RedArgs a) {
 template <int OP>
 __global__ __launch_bounds__(kBlock) void k_reduce_scalar(const RedArgs a) {
   for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) scalar_tile<OP>(a, t);
+}
+template <int OP, bool CS1>
+__global__ __launch_bounds__(kBlock) void k_reduce_tile(const RedArgs a) {
+  for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) tile_tile<OP, CS1>(a, t);
 }
 
 // Second stage of a time-chunked reduction: fold the nchunk partials of every
@@ -701,6 +814,12 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
     else
       hipLaunchKernelGGL((k_reduce_narrow<OP, 2>), grid, block, 0, s, a);
     e = hipGetLastError();
+  } else if (p.path == PATH_TILE) {
+    if (a.in_cs == 1)
+      hipLaunchKernelGGL((k_reduce_tile<OP, true>), grid, block, 0, s, a);
+    else
+      hipLaunchKernelGGL((k_reduce_tile<OP, false>), grid, block, 0, s, a);
+    e = hipGetLastError();
   } else {
     hipLaunchKernelGGL((k_reduce_scalar<OP>), grid, block, 0, s, a);
     e = hipGetLastError();
@@ -720,7 +839,7 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
 }  // namespace
 
 // ---------------------------------------------------------------------------
-Plan plan_reduce(RedArgs &a, bool aligned, int num_cus) {
+Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, int num_cus) {
   Plan p{};
   const int64_t F = a.F, T = a.T;
   p.nout = a.nco * a.ni * a.nto;
@@ -745,6 +864,11 @@ Plan plan_reduce(RedArgs &a, bool aligned, int num_cus) {
     const int64_t nc4 = a.nco * F / 4;
     a.blocks_c = cdiv(nc4, kBlock);
     tiles = cdiv(nc4, 64) * a.ni * a.nto * a.nbank;
+  } else if (rows16 && a.in_cs >= 1 && a.in_cs <= 8 && F <= (kSpan - 4) / a.in_cs + 1) {
+    p.path = PATH_TILE;
+    a.gpt = ((kSpan - 4) / a.in_cs + 1) / F;
+    a.blocks_c = cdiv(a.nco, a.gpt);
+    tiles = a.blocks_c * 4 * a.ni * a.nto * a.nbank;
   } else {
     p.path = PATH_SCALAR;
     a.blocks_c = cdiv(a.nco, kBlock);

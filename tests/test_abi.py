@@ -104,10 +104,20 @@ def test_launch_plans_host_only(pkg, L):
     # cfg4: narrow channel, long time -> time split waves and/or chunks
     p = plan(pkg, L, A, 512, 1, 879616, 8, 1024)
     assert p[0] == 0 and p[1] == 2 and (p[2] > 1 or p[4] > 1)
-    # F=1 time-only: narrow path; odd F: scalar path; misaligned pointer: scalar
+    # F=1 time-only: narrow path; odd pitch or misaligned pointer: scalar
     assert plan(pkg, L, A, 4096, 1, 16, 1, 16)[0] == 1
     assert plan(pkg, L, A, 4095, 1, 16, 3, 1)[0] == 2
     assert plan(pkg, L, A + 4, 4096, 1, 16, 64, 1)[0] == 2
+    # tile path: odd F, misaligned channel start, short channel step
+    assert plan(pkg, L, A, 4096, 1, 16, 3, 1, [0, 4095, 1, 0, 1, 1, 0, 16, 1])[0] == 3
+    assert plan(pkg, L, A, 4096, 1, 16, 64, 16, [1, 4032, 1, 0, 1, 1, 0, 16, 1])[0] == 3
+    assert plan(pkg, L, A, 4096, 1, 16, 1, 1, [1, 4092, 1, 0, 1, 1, 0, 16, 1])[0] == 3
+    assert plan(pkg, L, A, 4096, 1, 16, 16, 1, [0, 2048, 2, 0, 1, 1, 0, 16, 1])[0] == 3
+    # ... but not a reversed step, a step > 8, or a group wider than a tile row
+    assert plan(pkg, L, A, 4096, 1, 16, 16, 1, [4095, 2048, -2, 0, 1, 1, 0, 16, 1])[0] == 2
+    assert plan(pkg, L, A, 4096, 1, 16, 16, 1, [0, 256, 16, 0, 1, 1, 0, 16, 1])[0] == 2
+    assert plan(pkg, L, A, 8192, 1, 4, 4094, 1, [1, 8188, 1, 0, 1, 1, 0, 4, 1])[0] == 2
+    assert plan(pkg, L, A, 8192, 1, 4, 4093, 1, [1, 8186, 1, 0, 1, 1, 0, 4, 1])[0] == 3
     # one long time block with few outputs -> chunked across workgroups
     p = plan(pkg, L, A, 64, 1, 100000, 8, 100000)
     assert p[4] > 1 and p[6] > 0

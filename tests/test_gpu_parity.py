@@ -130,7 +130,7 @@ def test_reduce_gamma_rtol(eng, orc, F, T):
 
 WINDOWS = [
     [32, 512, 1, 1, 1, 1, 4, 32, 1],        # (33:544, 2, 5:36): unaligned start? 32 -> aligned
-    [33, 512, 1, 0, 2, 1, 0, 48, 1],        # misaligned channel start -> scalar path
+    [33, 512, 1, 0, 2, 1, 0, 48, 1],        # misaligned channel start -> tile path
     [1020, 96, -3, 0, 2, 1, 44, 12, -3],    # reversed strided channels and times
     [5, 120, 8, 0, 2, 1, 0, 48, 1],         # strided channels
     [0, 1024, 1, 1, 1, 1, 0, 24, 2],        # every other spectrum
@@ -150,6 +150,63 @@ def test_windows(eng, orc, win):
             got = host(eng, eng.reduce(x, F, T, op, win))
             assert same_bits(got, orc.reduce(a, F, T, op, win)), (win, F, T, op)
 
+
+# Tile path (misaligned starts, odd F, channel steps 2..8, groups up to one
+# tile row, several IFs, long T split across workgroups):
+# (nchan, nif, ntime, window, F, T).  Integer data keeps every sum exact.
+TILE_CASES = [
+    (4096, 1, 32, [1, 4032, 1, 0, 1, 1, 0, 32, 1], 64, 16),
+    (4096, 2, 16, [3, 4092, 1, 0, 2, 1, 0, 16, 1], 3, 4),
+    (4096, 1, 16, [0, 4095, 1, 0, 1, 1, 0, 16, 1], 5, 1),
+    (8192, 1, 8, [2, 8184, 1, 0, 1, 1, 0, 8, 1], 1, 8),
+    (8192, 1, 8, [2, 8186, 1, 0, 1, 1, 0, 8, 1], 2, 2),
+    (8192, 1, 4, [1, 8186, 1, 0, 1, 1, 0, 4, 1], 4093, 1),
+    (8192, 1, 4, [5, 8000, 1, 0, 1, 1, 0, 4, 1], 1000, 2),
+    (8192, 1, 8, [0, 4096, 2, 0, 1, 1, 0, 8, 1], 16, 4),
+    (8192, 1, 8, [7, 2720, 3, 0, 1, 1, 0, 8, 1], 17, 8),
+    (8192, 1, 8, [3, 1020, 8, 0, 1, 1, 0, 8, 1], 12, 8),
+    (1028, 1, 5000, [1, 1024, 1, 0, 1, 1, 0, 5000, 1], 4, 5000),
+    (4096, 3, 16, [1, 1020, 1, 1, 2, 1, 0, 16, 1], 20, 4),
+    (65540, 1, 24, [1, 65536, 1, 0, 1, 1, 4, 16, 1], 1024, 16),
+]
+
+
+@pytest.mark.parametrize("case", TILE_CASES, ids=range(len(TILE_CASES)))
+def test_tile_path(eng, orc, case):
+    nc, ni, nt, win, F, T = case
+    rng = np.random.default_rng(nc + F)
+    a = np.asfortranarray(rng.integers(0, 256, (nc, ni, nt)).astype(np.float32))
+    x = dev(eng, a)
+    assert eng.plan(x, F, T, "sum", win)["path"] == "tile"
+    for op in ("sum", "max", "min", "mean"):
+        got = host(eng, eng.reduce(x, F, T, op, win))
+        want = orc.reduce(a, F, T, op, win)
+        if op == "mean":
+            np.testing.assert_allclose(got, want, rtol=RTOL)
+        else:
+            assert same_bits(got, want), (case, op)
+
+
+def test_tile_path_special_values(eng, orc):
+    a = np.zeros((68, 1, 4), np.float32, order="F")
+    a[1:5, 0, 0] = -0.0
+    a[5:9, 0, 1] = [-0.0, 0.0, -0.0, -0.0]
+    a[9:13, 0, 2] = [1.0, np.nan, 2.0, 3.0]
+    a[13:17, 0, 3] = [np.inf, 1.0, -np.inf, 0.0]
+    a[17:21, 0, 0] = [np.inf, 1.0, 5.0, 0.0]
+    x = dev(eng, a)
+    for F, T in [(4, 1), (2, 2), (1, 4), (3, 4), (20, 1)]:
+        win = [1, 60, 1, 0, 1, 1, 0, 4, 1]
+        assert eng.plan(x, F, T, "max", win)["path"] == "tile"
+        for op in ("sum", "max", "min"):
+            got = host(eng, eng.reduce(x, F, T, op, win))
+            want = orc.reduce(a, F, T, op, win)
+            if op == "sum":
+                assert np.array_equal(np.isnan(got), np.isnan(want))
+                fin = np.isfinite(want)
+                assert np.array_equal(got[fin], want[fin])
+            else:
+                assert same_bits(got, want), (F, T, op)
 
 def test_subview_tensor(eng, orc):
     rng = np.random.default_rng(9)
