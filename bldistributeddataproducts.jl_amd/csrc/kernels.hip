@@ -326,7 +326,17 @@ __device__ __forceinline__ void scalar_tile(const RedArgs &a, int64_t tile) {
 // every channel in registers, then drops the selected channels into LDS and
 // folds each group of F there: 16-channel segments first, then the segments
 // of a group.  HBM traffic is the window plus <= 3 floats per tile row edge.
-constexpr int kTK = 4;                   // float4 columns per thread
+//   BLDP_TILE_K    float4 columns per thread (tile row span = 1024 * K floats)
+//   BLDP_TILE_ACC  accumulator sets per column (1 or 2)
+#ifndef BLDP_TILE_K
+#define BLDP_TILE_K 4
+#endif
+#ifndef BLDP_TILE_ACC
+#define BLDP_TILE_ACC 2
+#endif
+constexpr int kTK = BLDP_TILE_K;         // float4 columns per thread
+constexpr int kTA = BLDP_TILE_ACC;
+constexpr int kTRB = BLDP_BATCH / kTK > 0 ? BLDP_BATCH / kTK : 1;  // rows per load batch
 constexpr int kSpan = kBlock * 4 * kTK;  // floats of one row one tile may read
 constexpr int kSeg = 16;                 // channels folded per thread in stage 1
 __device__ __forceinline__ int lpad(int x) { return x + (x >> 4); }  // LDS bank spread
@@ -352,33 +362,40 @@ __device__ __forceinline__ void tile_tile(const RedArgs &a, int64_t tile) {
   const float *p = a.in[c.bank] + (abs0 - mis) + (c.to * a.T + r0) * a.in_ld_t + 4 * tid;
   const int64_t st = a.in_ld_t;
 
-  float4 acc[2][kTK];
+  float4 acc[kTA][kTK];
 #pragma unroll
-  for (int k = 0; k < kTK; ++k) acc[0][k] = acc[1][k] = id4;
+  for (int q = 0; q < kTA; ++q)
+#pragma unroll
+    for (int k = 0; k < kTK; ++k) acc[q][k] = id4;
   int64_t nrows = r1 - r0;
-  for (; nrows >= 2; nrows -= 2) {
-    float4 v[2][kTK];
+  for (; nrows >= kTRB; nrows -= kTRB) {
+    float4 v[kTRB][kTK];
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < kTRB; ++u)
 #pragma unroll
       for (int k = 0; k < kTK; ++k)
         v[u][k] = (tid + k * kBlock < w4) ? ld4(p + u * st + 4 * k * kBlock) : id4;
-    p += 2 * st;
+    p += kTRB * st;
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < kTRB; ++u)
 #pragma unroll
-      for (int k = 0; k < kTK; ++k) acc[u][k] = f4<OP>(acc[u][k], v[u][k]);
+      for (int k = 0; k < kTK; ++k) acc[u % kTA][k] = f4<OP>(acc[u % kTA][k], v[u][k]);
   }
-  if (nrows > 0) {
+  for (; nrows > 0; --nrows) {
 #pragma unroll
     for (int k = 0; k < kTK; ++k)
       if (tid + k * kBlock < w4) acc[0][k] = f4<OP>(acc[0][k], ld4(p + 4 * k * kBlock));
+    p += st;
   }
+#pragma unroll
+  for (int q = 1; q < kTA; ++q)
+#pragma unroll
+    for (int k = 0; k < kTK; ++k) acc[0][k] = f4<OP>(acc[0][k], acc[q][k]);
 #pragma unroll
   for (int k = 0; k < kTK; ++k) {
     const int col = tid + k * kBlock;
     if (col >= w4) continue;
-    const float4 r = f4<OP>(acc[0][k], acc[1][k]);
+    const float4 r = acc[0][k];
     const float e[4] = {r.x, r.y, r.z, r.w};
 #pragma unroll
     for (int q = 0; q < 4; ++q) {

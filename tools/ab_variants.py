@@ -28,6 +28,10 @@ VARIANTS = {
     "base": "",                          # nt loads+stores, batch 8, cap 4 WG/CU iff ts > 1
     "nocap": "-DBLDP_MAX_WG_PER_CU=0",
     "plain": "-DBLDP_NT_LOADS=0 -DBLDP_NT_STORES=0 -DBLDP_MAX_WG_PER_CU=0",  # round-1 start
+    # tile path (misaligned / odd-F windows): columns per thread, accumulator sets
+    "tk4a1": "-DBLDP_TILE_ACC=1",
+    "tk2a1": "-DBLDP_TILE_K=2 -DBLDP_TILE_ACC=1",
+    "tk2a2": "-DBLDP_TILE_K=2",
 }
 
 
@@ -51,7 +55,7 @@ def load(path):
     return L
 
 
-def run(names, rounds, iters):
+def run(names, rounds, iters, suite="main"):
     import torch
 
     import __graft_entry__ as entry
@@ -79,14 +83,27 @@ def run(names, rounds, iters):
         cases.append((label, go, nbytes, out, keep))
 
     b3 = [eng.synth(1 << 26, 1, 16, 1 << 20, seed=10 * b, kind=0) for b in range(8)]
-    band_case("cfg3 F1024 T16", b3, 1024, 16)
-    band_case("cfg3 F1 T16", b3, 1, 16)
-    band_case("cfg3 F64 T16", b3, 64, 16)
-    b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
-    band_case("cfg2 F64 T16", b2, 64, 16, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
-    band_case("cfg1 F64 T16", b2[:1], 64, 16, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
-    b4 = [eng.synth(512, 1, 880000, 8, seed=10 * b + 1, kind=0) for b in range(8)]
-    band_case("cfg4 F8 T1024", b4, 8, 1024, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
+    if suite == "tile":  # tile path: misaligned starts and odd F at cfg3 scale
+        n = 1 << 26
+        band_case("cfg3 c0=1 F1024", b3, 1024, 16, [1, n - 1024, 1, 0, 1, 1, 0, 16, 1])
+        band_case("cfg3 c0=3 F64", b3, 64, 16, [3, n - 64, 1, 0, 1, 1, 0, 16, 1])
+        band_case("cfg3 F3", b3, 3, 16, [0, n - 1, 1, 0, 1, 1, 0, 16, 1])
+        band_case("cfg3 c0=1 F1", b3, 1, 16, [1, n - 4, 1, 0, 1, 1, 0, 16, 1])
+        band_case("cfg3 cs=2 F32", b3, 32, 16, [0, n // 2, 2, 0, 1, 1, 0, 16, 1])
+        b2 = [eng.synth(65540, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
+        band_case("cfg2 c0=1 F64", b2, 64, 16, [1, 65536, 1, 0, 1, 1, 0, 272, 1])
+        cases_done = True
+    else:
+        cases_done = False
+    if not cases_done:
+        band_case("cfg3 F1024 T16", b3, 1024, 16)
+        band_case("cfg3 F1 T16", b3, 1, 16)
+        band_case("cfg3 F64 T16", b3, 64, 16)
+        b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
+        band_case("cfg2 F64 T16", b2, 64, 16, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
+        band_case("cfg1 F64 T16", b2[:1], 64, 16, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
+        b4 = [eng.synth(512, 1, 880000, 8, seed=10 * b + 1, kind=0) for b in range(8)]
+        band_case("cfg4 F8 T1024", b4, 8, 1024, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
     torch.cuda.synchronize()
 
     res = {c[0]: {n: [] for n in names} for c in cases}
@@ -130,12 +147,13 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--suite", default="main", choices=["main", "tile"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:
         build(names)
     if a.run:
-        s = run(names, a.rounds, a.iters)
+        s = run(names, a.rounds, a.iters, a.suite)
         if a.json:
             with open(a.json, "w") as f:
                 json.dump(s, f, indent=1)

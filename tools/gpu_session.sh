@@ -43,6 +43,7 @@ for s in $STEPS; do
     decode) run decode 600 python bench.py --mode decode ;;
     file)  run file 600 python bench.py --mode file ;;
     paths) run paths 300 python tools/probe_paths.py ;;
+    paths_big) run paths_big 300 python tools/probe_paths.py --big ;;
     prof_decode) run prof_decode 600 rocprofv3 --kernel-trace --stats --output-format csv \
              -d "$OUT/prof_decode" -o run -- python bench.py --mode decode ;;
     prof_kurt) run prof_kurt 600 rocprofv3 --kernel-trace --stats --output-format csv \
@@ -54,6 +55,7 @@ for s in $STEPS; do
              --master-addr 127.0.0.1 --master-port 29612 bench.py --gpus 2 --dist-backend gloo \
              --steps 10 --warmup 3 --config cfg2 ;;
     ab)    run ab 900 python tools/ab_variants.py --run --json "$OUT/ab.json" ;;
+    ab_tile) run ab_tile 900 python tools/ab_variants.py --run --suite tile --variants base,tk4a1,tk2a1,tk2a2 --json "$OUT/ab_tile.json" ;;
   esac
 done
 echo "== session done"

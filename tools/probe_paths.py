@@ -19,8 +19,21 @@ def main():
 
     pkg = entry.load_package()
     eng = pkg.engine
-    banks = [eng.synth(65540, 1, 272, 1024, seed=b, kind=0) for b in range(8)]
-    cases = {
+    if "--big" in sys.argv:  # cfg3 scale: 8 banks x 2^26 channels x 16 spectra
+        n = 1 << 26
+        banks = [eng.synth(n + 4, 1, 16, 1024, seed=b, kind=0) for b in range(8)]
+        cases = {
+            "cfg3 aligned F1024": ([0, n, 1, 0, 1, 1, 0, 16, 1], 1024, 16),
+            "cfg3 misaligned F1024 (c0=1)": ([1, n, 1, 0, 1, 1, 0, 16, 1], 1024, 16),
+            "cfg3 misaligned F64 (c0=3)": ([3, n, 1, 0, 1, 1, 0, 16, 1], 64, 16),
+            "cfg3 F3": ([0, n - 1, 1, 0, 1, 1, 0, 16, 1], 3, 16),
+            "cfg3 misaligned F1 (c0=1)": ([1, n, 1, 0, 1, 1, 0, 16, 1], 1, 16),
+        }
+        nt = 16
+    else:
+        banks = [eng.synth(65540, 1, 272, 1024, seed=b, kind=0) for b in range(8)]
+        nt = 272
+    cases = cases if "--big" in sys.argv else {
         "aligned F64": ([0, 65536, 1, 0, 1, 1, 0, 272, 1], 64, 16),
         "misaligned F64 (c0=1)": ([1, 65536, 1, 0, 1, 1, 0, 272, 1], 64, 16),
         "aligned F3": ([0, 65538, 1, 0, 1, 1, 0, 272, 1], 3, 16),
@@ -31,7 +44,7 @@ def main():
     res = {}
     for name, (w, F, T) in cases.items():
         plan = eng.plan(banks[0], F, T, "sum", w)
-        nb = 8 * 4 * (w[1] * 272 + (w[1] // F) * (272 // T))
+        nb = 8 * 4 * (w[1] * nt + (w[1] // F) * (nt // T))
         for _ in range(3):
             eng.band_reduce(banks, F, T, "sum", w)
         ts = []
