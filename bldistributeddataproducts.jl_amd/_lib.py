@@ -48,6 +48,10 @@ SIGNATURES = {
     "bldp_abi_version": ([], I),
     "bldp_last_error": ([ctypes.c_char_p, SZ], I),
     "bldp_device_count": ([P], I),
+    "bldp_init": ([I, P], I),
+    "bldp_finalize": ([], I),
+    "bldp_host_register": ([P, SZ], I),
+    "bldp_host_unregister": ([P], I),
     "bldp_reduce_shape": ([I64, I64, I64, P, I64, I64, P], I),
     "bldp_reduce_plan_f32": ([P, I64, I64, I64, P, I64, I64, I, P, P], I),
     "bldp_reduce_f32": ([P, I64, I64, I64, P, I64, I64, I, P, P], I),

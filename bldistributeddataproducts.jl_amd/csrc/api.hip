@@ -152,6 +152,26 @@ int bldp::scratch_bytes(hipStream_t s, size_t bytes, void **out) {
   return BLDP_OK;
 }
 
+std::vector<int> bldp::scratch_devices() {
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  std::vector<int> d;
+  for (auto &kv : g_ws) d.push_back(kv.first.first);
+  return d;
+}
+
+void bldp::scratch_release_all() {
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  for (auto &kv : g_ws)
+    if (kv.second.ptr) {
+      (void)hipSetDevice(kv.first.first);
+      (void)hipFree(kv.second.ptr);
+    }
+  g_ws.clear();
+  if (prev >= 0) (void)hipSetDevice(prev);
+}
+
 namespace {
 
 int scratch(hipStream_t s, size_t bytes, void **out) { return bldp::scratch_bytes(s, bytes, out); }
@@ -334,12 +354,9 @@ int bldp_band_reduce_multi_f32(int nbank, const int *bank_dev, const float *cons
   rc = BLDP_OK;
   for (int b = 0; b < nbank && rc == BLDP_OK; ++b) {
     const int d = bank_dev[b];
+    if (!streams[d] && (rc = device_stream(d, &streams[d])) != BLDP_OK) break;
     if (hipSetDevice(d) != hipSuccess) {
       rc = fail(BLDP_EHIP, "hipSetDevice(%d) failed", d);
-      break;
-    }
-    if (!streams[d] && hipStreamCreateWithFlags(&streams[d], hipStreamNonBlocking) != hipSuccess) {
-      rc = fail(BLDP_EHIP, "stream creation on device %d failed", d);
       break;
     }
     bool direct = d == root;
@@ -374,7 +391,6 @@ int bldp_band_reduce_multi_f32(int nbank, const int *bank_dev, const float *cons
       (void)hipSetDevice(d);
       if (hipStreamSynchronize(streams[d]) != hipSuccess && rc == BLDP_OK)
         rc = fail(BLDP_EHIP, "device %d failed during the band reduce", d);
-      (void)hipStreamDestroy(streams[d]);
     }
   for (int b = 0; b < nbank; ++b)
     if (staging[b]) {

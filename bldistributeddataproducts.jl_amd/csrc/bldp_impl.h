@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "bldp.h"
 
 namespace bldp {
@@ -13,6 +15,25 @@ int set_error(int code, const char *fmt, ...);
 // Library-owned device scratch cached per (device, stream); growing it
 // synchronizes that stream first.
 int scratch_bytes(hipStream_t s, size_t bytes, void **out);
+std::vector<int> scratch_devices();  // devices holding scratch
+void scratch_release_all();          // frees it (callers drained the devices)
+
+// A host-staging pipeline (runtime.hip): two streams and four cached device
+// buffers (slots 0/1 = input of stream 0/1, 2/3 = output of stream 0/1).
+struct Stager {
+  int dev = -1;
+  hipStream_t st[2] = {nullptr, nullptr};
+  void *buf[4] = {nullptr, nullptr, nullptr, nullptr};
+  size_t bytes[4] = {0, 0, 0, 0};
+  std::vector<void *> temp;  // oversize buffers of the current call
+};
+// Take an idle pipeline of `dev` (created on first use); the device must be gfx950.
+int stager_acquire(int dev, Stager **out);
+// Device buffer of >= need bytes for `slot`, valid until stager_release.
+int stager_buffer(Stager *s, int slot, size_t need, void **p);
+void stager_release(Stager *s);
+// The library's persistent worker stream on `dev`.
+int device_stream(int dev, hipStream_t *out);
 
 // One reduction launch: nbank banks with identical geometry.
 // Window element (c, i, t) of bank b sits at

@@ -1,9 +1,10 @@
 // host.hip — bldp_reduce_host_f32: the drop-in for a worker that already holds
 // the window in host memory (after h5["data"][idxs...] at
 // src/gbtworkerfunctions.jl:185 or dmmap[idxs...] at :174).  The window is
-// streamed to the GPU in chunks of whole output time rows on two HIP streams
-// (copy of chunk k+1 overlaps the reduce of chunk k) and the reduced rows come
-// back into the caller's dense (nco, ni, nto) buffer.
+// streamed to the GPU in chunks of whole output time rows on the two streams
+// of a pooled staging pipeline (runtime.hip; copy of chunk k+1 overlaps the
+// reduce of chunk k) and the reduced rows come back into the caller's dense
+// (nco, ni, nto) buffer.  Nothing is allocated per call.
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
@@ -33,16 +34,82 @@ struct DevGuard {
   }
 };
 
-}  // namespace
-
-#define HCHK(x)                                                         \
-  do {                                                                  \
-    hipError_t e_ = (x);                                                \
-    if (e_ != hipSuccess) {                                             \
-      rc = bldp::set_error(BLDP_EHIP, "%s: %s", #x, hipGetErrorString(e_)); \
-      goto done;                                                        \
-    }                                                                   \
+#define HCHK(x)                                                             \
+  do {                                                                      \
+    hipError_t e_ = (x);                                                    \
+    if (e_ != hipSuccess)                                                   \
+      return bldp::set_error(BLDP_EHIP, "%s: %s", #x, hipGetErrorString(e_)); \
   } while (0)
+
+// Run `body` on an idle staging pipeline of `dev`; both of its streams are
+// drained before the pipeline goes back to the pool (also after an error), so
+// no copy into caller memory is pending when the entry point returns.
+template <class Body>
+int with_stager(int dev, Body body) {
+  bldp::Stager *sg = nullptr;
+  int rc = bldp::stager_acquire(dev, &sg);
+  if (rc) return rc;
+  {
+    DevGuard guard(dev);
+    rc = body(sg);
+    for (int b = 0; b < 2; ++b) {
+      const hipError_t e = hipStreamSynchronize(sg->st[b]);
+      if (e != hipSuccess && rc == BLDP_OK)
+        rc = bldp::set_error(BLDP_EHIP, "device %d: %s", dev, hipGetErrorString(e));
+    }
+  }
+  bldp::stager_release(sg);
+  return rc;
+}
+
+// Staged window rows: element (c, i, t) of the window at
+// row0[c*cs' + i*ld_i + t*ld_t] with c counted from the lowest channel touched.
+struct HostWin {
+  int64_t nc, cs, acs, span, ni, ld_i, ld_t;
+  const float *row0;
+  bool uniform;   // rows are a single 2-D copy
+  int64_t pitch;  // of that copy, in floats
+};
+
+HostWin host_window(const float *in, int64_t nchan, int64_t nif, const int64_t *win,
+                    int64_t nc, int64_t ni) {
+  HostWin h;
+  const int64_t c0 = win ? win[0] : 0, cs = win ? win[2] : 1;
+  const int64_t i0 = win ? win[3] : 0, is = win ? win[5] : 1;
+  const int64_t t0 = win ? win[6] : 0, ts = win ? win[8] : 1;
+  h.nc = nc;
+  h.ni = ni;
+  h.cs = cs;
+  h.acs = cs < 0 ? -cs : cs;
+  h.span = (nc - 1) * h.acs + 1;                        // staged floats per (i, t) row
+  const int64_t c_lo = cs < 0 ? c0 + (nc - 1) * cs : c0;  // lowest channel touched
+  h.ld_i = nchan * is;
+  h.ld_t = nchan * nif * ts;
+  h.row0 = in + c_lo + nchan * (i0 + nif * t0);
+  h.uniform = (ni == 1 && h.ld_t > 0 && h.ld_t >= h.span) ||
+              (h.ld_i > 0 && h.ld_i >= h.span && h.ld_t == ni * h.ld_i);
+  h.pitch = ni == 1 ? h.ld_t : h.ld_i;
+  return h;
+}
+
+// Copy `rows` window time rows starting at window row r0 into dense
+// [t][i][span] device memory.
+int stage_rows(const HostWin &h, int64_t r0, int64_t rows, float *dst, hipStream_t st) {
+  const float *src = h.row0 + r0 * h.ld_t;
+  if (h.uniform) {
+    HCHK(hipMemcpy2DAsync(dst, h.span * sizeof(float), src, h.pitch * sizeof(float),
+                          h.span * sizeof(float), (size_t)(rows * h.ni), hipMemcpyHostToDevice,
+                          st));
+  } else {
+    for (int64_t r = 0; r < rows; ++r)
+      for (int64_t i = 0; i < h.ni; ++i)
+        HCHK(hipMemcpyAsync(dst + (r * h.ni + i) * h.span, src + r * h.ld_t + i * h.ld_i,
+                            h.span * sizeof(float), hipMemcpyHostToDevice, st));
+  }
+  return BLDP_OK;
+}
+
+}  // namespace
 
 extern "C" int bldp_reduce_host_f32(int dev, const float *in, int64_t nchan, int64_t nif,
                                     int64_t ntime, const int64_t *win, int64_t fqavby,
@@ -53,68 +120,36 @@ extern "C" int bldp_reduce_host_f32(int dev, const float *in, int64_t nchan, int
   const int64_t nco = sh[0], ni = sh[1], nto = sh[2];
   if (nco * ni * nto == 0) return BLDP_OK;
   if (!in || !out) return bldp::set_error(BLDP_EINVAL, "null pointer");
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || dev < 0 || dev >= ndev)
-    return bldp::set_error(BLDP_EINVAL, "device %d not available", dev);
-  DevGuard guard(dev);
-
-  // window (same conventions as the device path)
-  const int64_t c0 = win ? win[0] : 0, nc = win ? win[1] : nchan, cs = win ? win[2] : 1;
-  const int64_t i0 = win ? win[3] : 0, is = win ? win[5] : 1;
-  const int64_t t0 = win ? win[6] : 0, ts = win ? win[8] : 1;
   const int64_t F = fqavby <= 1 ? 1 : fqavby, T = tavby <= 1 ? 1 : tavby;
-  const int64_t acs = cs < 0 ? -cs : cs;
-  const int64_t span = (nc - 1) * acs + 1;               // staged floats per (i, t) row
-  const int64_t c_lo = cs < 0 ? c0 + (nc - 1) * cs : c0;  // lowest channel touched
-  const int64_t ld_i = nchan * is, ld_t = nchan * nif * ts;
-  const float *row0 = in + c_lo + nchan * (i0 + nif * t0);
+  const HostWin h = host_window(in, nchan, nif, win, nco * F, ni);
 
   // chunk = q output time rows (q*T input rows), ~128 MiB of staged input
-  const int64_t row_bytes = span * ni * (int64_t)sizeof(float);
+  const int64_t row_bytes = h.span * ni * (int64_t)sizeof(float);
   int64_t q = std::max<int64_t>(1, ((int64_t)128 << 20) / std::max<int64_t>(1, row_bytes * T));
   q = std::min(q, nto);
   const int64_t nchunks = (nto + q - 1) / q;
-  const bool uniform = (ni == 1 && ld_t > 0 && ld_t >= span) ||
-                       (ld_i > 0 && ld_i >= span && ld_t == ni * ld_i);
-  const int64_t pitch = ni == 1 ? ld_t : ld_i;
-
-  float *dbuf[2] = {nullptr, nullptr}, *dout[2] = {nullptr, nullptr};
-  hipStream_t st[2] = {nullptr, nullptr};
-  for (int b = 0; b < 2; ++b) {
-    HCHK(hipStreamCreateWithFlags(&st[b], hipStreamNonBlocking));
-    HCHK(hipMalloc(&dbuf[b], (size_t)(q * T) * row_bytes));
-    HCHK(hipMalloc(&dout[b], (size_t)(nco * ni * q) * sizeof(float)));
-  }
-  for (int64_t k = 0; k < nchunks; ++k) {
-    const int b = (int)(k & 1);
-    const int64_t to0 = k * q, qn = std::min(q, nto - to0), rows = qn * T;
-    const float *src = row0 + (to0 * T) * ld_t;
-    if (uniform) {
-      HCHK(hipMemcpy2DAsync(dbuf[b], span * sizeof(float), src, pitch * sizeof(float),
-                            span * sizeof(float), (size_t)(rows * ni), hipMemcpyHostToDevice,
-                            st[b]));
-    } else {
-      for (int64_t r = 0; r < rows; ++r)
-        for (int64_t i = 0; i < ni; ++i)
-          HCHK(hipMemcpyAsync(dbuf[b] + (r * ni + i) * span, src + r * ld_t + i * ld_i,
-                              span * sizeof(float), hipMemcpyHostToDevice, st[b]));
+  return with_stager(dev, [&](bldp::Stager *sg) -> int {
+    float *dbuf[2], *dout[2];
+    for (int b = 0; b < 2 && b < nchunks; ++b) {
+      int r = bldp::stager_buffer(sg, b, (size_t)(q * T) * row_bytes, (void **)&dbuf[b]);
+      if (!r) r = bldp::stager_buffer(sg, 2 + b, (size_t)(nco * ni * q) * sizeof(float),
+                                     (void **)&dout[b]);
+      if (r) return r;
     }
-    const int64_t dwin[9] = {cs < 0 ? (nc - 1) * acs : 0, nc, cs, 0, ni, 1, 0, rows, 1};
-    rc = bldp_reduce_strided_f32(dbuf[b], span, ni, rows, dwin, F, T, op, dout[b], nco,
-                                 nco * ni, st[b]);
-    if (rc) goto done;  // message already recorded
-    HCHK(hipMemcpyAsync(out + to0 * nco * ni, dout[b], (size_t)(nco * ni * qn) * sizeof(float),
-                        hipMemcpyDeviceToHost, st[b]));
-  }
-  for (int b = 0; b < 2; ++b) HCHK(hipStreamSynchronize(st[b]));
-done:
-  for (int b = 0; b < 2; ++b) {
-    if (st[b]) (void)hipStreamSynchronize(st[b]);
-    if (dbuf[b]) (void)hipFree(dbuf[b]);
-    if (dout[b]) (void)hipFree(dout[b]);
-    if (st[b]) (void)hipStreamDestroy(st[b]);
-  }
-  return rc;
+    for (int64_t k = 0; k < nchunks; ++k) {
+      const int b = (int)(k & 1);
+      const int64_t to0 = k * q, qn = std::min(q, nto - to0), rows = qn * T;
+      int r = stage_rows(h, to0 * T, rows, dbuf[b], sg->st[b]);
+      if (r) return r;
+      const int64_t dwin[9] = {h.cs < 0 ? (h.nc - 1) * h.acs : 0, h.nc, h.cs, 0, ni, 1, 0, rows, 1};
+      r = bldp_reduce_strided_f32(dbuf[b], h.span, ni, rows, dwin, F, T, op, dout[b], nco,
+                                  nco * ni, sg->st[b]);
+      if (r) return r;  // message already recorded
+      HCHK(hipMemcpyAsync(out + to0 * nco * ni, dout[b], (size_t)(nco * ni * qn) * sizeof(float),
+                          hipMemcpyDeviceToHost, sg->st[b]));
+    }
+    return BLDP_OK;
+  });
 }
 
 // Stage the window rows ([t][i][span] dense) on the device with the same copy
@@ -127,47 +162,20 @@ extern "C" int bldp_kurtosis_host_f32(int dev, const float *in, int64_t nchan, i
   const int64_t nc = sh[0], ni = sh[1], nt = sh[2];
   if (nc * ni == 0) return BLDP_OK;
   if (!out || (!in && nt > 0)) return bldp::set_error(BLDP_EINVAL, "null pointer");
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || dev < 0 || dev >= ndev)
-    return bldp::set_error(BLDP_EINVAL, "device %d not available", dev);
-  DevGuard guard(dev);
-  const int64_t c0 = win ? win[0] : 0, cs = win ? win[2] : 1;
-  const int64_t i0 = win ? win[3] : 0, is = win ? win[5] : 1;
-  const int64_t t0 = win ? win[6] : 0, ts = win ? win[8] : 1;
-  const int64_t acs = cs < 0 ? -cs : cs;
-  const int64_t span = (nc - 1) * acs + 1;
-  const int64_t c_lo = cs < 0 ? c0 + (nc - 1) * cs : c0;
-  const int64_t ld_i = nchan * is, ld_t = nchan * nif * ts;
-  const float *row0 = in + c_lo + nchan * (i0 + nif * t0);
-  float *dbuf = nullptr;
-  double *dout = nullptr;
-  hipStream_t st = nullptr;
-  const int64_t dwin[9] = {cs < 0 ? (nc - 1) * acs : 0, nc, cs, 0, ni, 1, 0, nt, 1};
-  HCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-  HCHK(hipMalloc(&dbuf, (size_t)std::max<int64_t>(1, span * ni * nt) * sizeof(float)));
-  HCHK(hipMalloc(&dout, (size_t)(nc * ni) * sizeof(double)));
-  if (nt > 0) {
-    const bool uniform = (ni == 1 && ld_t > 0 && ld_t >= span) ||
-                         (ld_i > 0 && ld_i >= span && ld_t == ni * ld_i);
-    if (uniform) {
-      const int64_t pitch = ni == 1 ? ld_t : ld_i;
-      HCHK(hipMemcpy2DAsync(dbuf, span * sizeof(float), row0, pitch * sizeof(float),
-                            span * sizeof(float), (size_t)(nt * ni), hipMemcpyHostToDevice, st));
-    } else {
-      for (int64_t r = 0; r < nt; ++r)
-        for (int64_t i = 0; i < ni; ++i)
-          HCHK(hipMemcpyAsync(dbuf + (r * ni + i) * span, row0 + r * ld_t + i * ld_i,
-                              span * sizeof(float), hipMemcpyHostToDevice, st));
-    }
-  }
-  rc = bldp_kurtosis_f32(dbuf, span, ni, nt, dwin, dout, nullptr, st);
-  if (rc) goto done;
-  HCHK(hipMemcpyAsync(out, dout, (size_t)(nc * ni) * sizeof(double), hipMemcpyDeviceToHost, st));
-  HCHK(hipStreamSynchronize(st));
-done:
-  if (st) (void)hipStreamSynchronize(st);
-  if (dbuf) (void)hipFree(dbuf);
-  if (dout) (void)hipFree(dout);
-  if (st) (void)hipStreamDestroy(st);
-  return rc;
+  const HostWin h = host_window(in, nchan, nif, win, nc, ni);
+  return with_stager(dev, [&](bldp::Stager *sg) -> int {
+    float *dbuf;
+    double *dout;
+    int r = bldp::stager_buffer(sg, 0, (size_t)std::max<int64_t>(1, h.span * ni * nt) * 4,
+                                (void **)&dbuf);
+    if (!r) r = bldp::stager_buffer(sg, 2, (size_t)(nc * ni) * sizeof(double), (void **)&dout);
+    if (!r && nt > 0) r = stage_rows(h, 0, nt, dbuf, sg->st[0]);
+    if (r) return r;
+    const int64_t dwin[9] = {h.cs < 0 ? (nc - 1) * h.acs : 0, nc, h.cs, 0, ni, 1, 0, nt, 1};
+    r = bldp_kurtosis_f32(dbuf, h.span, ni, nt, dwin, dout, nullptr, sg->st[0]);
+    if (r) return r;
+    HCHK(hipMemcpyAsync(out, dout, (size_t)(nc * ni) * sizeof(double), hipMemcpyDeviceToHost,
+                        sg->st[0]));
+    return BLDP_OK;
+  });
 }

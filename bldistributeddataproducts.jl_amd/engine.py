@@ -23,6 +23,7 @@ __all__ = [
     "fb_empty", "fb_from_numpy", "fb_to_numpy", "reduce", "band_reduce", "band_reduce_multi",
     "stitch",
     "despike", "kurtosis", "band_kurtosis", "synth", "plan", "reduce_host", "kurtosis_host",
+    "init", "finalize", "pinned",
 ]
 
 
@@ -30,6 +31,43 @@ def _torch():
     import torch
 
     return torch
+
+
+def init(devices=None) -> None:
+    """bldp_init: check the devices are gfx950, create their worker streams and
+    a warm host-staging pipeline each, enable peer access between them.
+    ``None`` = every visible device.  Optional (everything initialises lazily)."""
+    L = _lib.lib()
+    if devices is None:
+        _lib.check(L.bldp_init(0, None), "bldp_init")
+        return
+    devs = [int(d) for d in devices]
+    arr = (ctypes.c_int * len(devs))(*devs)
+    _lib.check(L.bldp_init(len(devs), ctypes.cast(arr, ctypes.c_void_p)), "bldp_init")
+
+
+def finalize() -> None:
+    """bldp_finalize: drain the devices and free every library-owned resource."""
+    _lib.check(_lib.lib().bldp_finalize(), "bldp_finalize")
+
+
+class pinned:
+    """Context manager page-locking a long-lived host numpy array for the
+    host-array entry points (bldp_host_register / bldp_host_unregister)."""
+
+    def __init__(self, a: np.ndarray):
+        self.a = a
+
+    def __enter__(self):
+        if self.a.nbytes:
+            _lib.check(_lib.lib().bldp_host_register(self.a.ctypes.data, self.a.nbytes),
+                       "bldp_host_register")
+        return self.a
+
+    def __exit__(self, *exc):
+        if self.a.nbytes:
+            _lib.check(_lib.lib().bldp_host_unregister(self.a.ctypes.data), "bldp_host_unregister")
+        return False
 
 
 def fb_empty(nchan, nif, ntime, device=None, dtype=None):

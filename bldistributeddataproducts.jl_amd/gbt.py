@@ -45,6 +45,9 @@ def setupworkers(hosts=(), **kwargs) -> list[int]:
         raise RuntimeError("no GPU visible: workers run on MI355X devices")
     hosts = list(hosts) or datahosts(kwargs.get("prefix", ""))
     _workers = [k % ndev for k in range(len(hosts))]
+    from . import engine
+
+    engine.init(sorted(set(_workers)))  # streams, staging pipelines, peer access
     return list(_workers)
 
 

@@ -75,6 +75,22 @@ BLDP_API int bldp_last_error(char *buf, size_t len);
 /* Number of visible GPUs. */
 BLDP_API int bldp_device_count(int *n);
 
+/* Library setup (SURVEY §8 B2 bldp_init/bldp_finalize; called where the
+ * reference sets up its workers, GBT.setupworkers, src/gbt.jl:12-46).
+ * devs == NULL selects every visible device.  Checks each device is gfx950
+ * (BLDP_EINVAL otherwise), creates its worker stream and one warm
+ * host-staging pipeline, and enables peer access between the listed devices.
+ * Optional: every entry point initialises what it needs on first use. */
+BLDP_API int bldp_init(int ndev, const int *devs);
+/* Drain the devices and free every library-owned resource (scratch,
+ * staging pipelines, streams).  BLDP_EINVAL while a host call is running.
+ * Later calls re-initialise lazily. */
+BLDP_API int bldp_finalize(void);
+/* Page-lock / unlock a long-lived caller host buffer so the host-array entry
+ * points copy from it at full PCIe rate (hipHostRegister). */
+BLDP_API int bldp_host_register(void *ptr, size_t bytes);
+BLDP_API int bldp_host_unregister(void *ptr);
+
 /* Output shape of a reduction: nco = nc/F, nto = nt/T (after the divisibility
  * checks), ni = window IF count.  Pure host function. */
 BLDP_API int bldp_reduce_shape(int64_t nchan, int64_t nif, int64_t ntime, const int64_t *win,

@@ -168,3 +168,72 @@ def test_fbh5_bslz4_on_gpu_end_to_end(pkg, orc, tmp_path):
     assert same_bits(got, orc.reduce(d, 64, 8, "sum", [0, 4096, 1, 0, 2, 1, 0, 32, 1]))
     got = pkg.GBT.getdata([0], [str(p)], (J(4096, -1, 1), 1, C), fqavby=16, fqavfunc="max")
     assert same_bits(got[0], orc.reduce(d, 16, 1, "max", [4095, 4096, -1, 0, 1, 1, 0, 40, 1]))
+
+
+# --- library runtime: bldp_init / bldp_finalize, staging pool, pinning ------
+
+def test_init_finalize_and_lazy_reinit(pkg, orc):
+    eng = pkg.engine
+    eng.init()
+    eng.init([0])  # idempotent
+    with pytest.raises(pkg._lib.ArgumentError):
+        eng.init([99])
+    rng = np.random.default_rng(31)
+    a = np.asfortranarray(rng.integers(0, 256, (1024, 1, 64)).astype(np.float32))
+    assert same_bits(eng.reduce_host(a, 16, 4), orc.reduce(a, 16, 4))
+    eng.finalize()
+    eng.finalize()  # nothing left to free
+    assert same_bits(eng.reduce_host(a, 16, 4), orc.reduce(a, 16, 4))  # lazily re-created
+    assert same_bits(eng.reduce_host(a, 8, 2, "max"), orc.reduce(a, 8, 2, "max"))
+
+
+def test_concurrent_host_callers_share_one_gpu(pkg, orc):
+    # GBT.getdata fans one call per (worker, file) out concurrently
+    # (src/gbt.jl:75-77); several workers may map to one GPU.
+    from concurrent.futures import ThreadPoolExecutor
+
+    eng = pkg.engine
+    rng = np.random.default_rng(32)
+    arrs = [np.asfortranarray(rng.integers(0, 256, (4096, 1, 96 + 16 * k)).astype(np.float32))
+            for k in range(8)]
+    with ThreadPoolExecutor(8) as ex:
+        got = list(ex.map(lambda a: eng.reduce_host(a, 64, 16), arrs * 3))
+    for g, a in zip(got, arrs * 3):
+        assert same_bits(g, orc.reduce(a, 64, 16))
+    with ThreadPoolExecutor(8) as ex:
+        kur = list(ex.map(eng.kurtosis_host, arrs))
+    for k, a in zip(kur, arrs):
+        np.testing.assert_allclose(k, orc.kurtosis(a), rtol=1e-4, atol=1e-5)
+
+
+def test_host_paths_do_not_leak_device_memory(pkg, orc):
+    import torch
+
+    eng = pkg.engine
+    rng = np.random.default_rng(33)
+    # long time block with few outputs -> chunked plan with library scratch
+    a = np.asfortranarray(rng.integers(0, 256, (64, 1, 60000)).astype(np.float32))
+    want = orc.reduce(a, 8, 60000)
+    for _ in range(2):
+        eng.reduce_host(a, 8, 60000)
+        eng.kurtosis_host(a)
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info()[0]
+    for _ in range(20):
+        got = eng.reduce_host(a, 8, 60000)
+        eng.kurtosis_host(a)
+    torch.cuda.synchronize()
+    free1 = torch.cuda.mem_get_info()[0]
+    assert same_bits(got, want)
+    assert free0 - free1 < (16 << 20), (free0, free1)
+
+
+def test_pinned_host_buffer(pkg, orc):
+    eng = pkg.engine
+    rng = np.random.default_rng(34)
+    a = np.asfortranarray(rng.integers(0, 256, (8192, 1, 64)).astype(np.float32))
+    with eng.pinned(a):
+        got = eng.reduce_host(a, 64, 16)
+    assert same_bits(got, orc.reduce(a, 64, 16))
+    with pytest.raises(pkg._lib.ArgumentError):
+        pkg._lib.check(pkg._lib.lib().bldp_host_register(None, 0))
