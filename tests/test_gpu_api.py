@@ -211,8 +211,9 @@ def test_host_paths_do_not_leak_device_memory(pkg, orc):
 
     eng = pkg.engine
     rng = np.random.default_rng(33)
-    # long time block with few outputs -> chunked plan with library scratch
-    a = np.asfortranarray(rng.integers(0, 256, (64, 1, 60000)).astype(np.float32))
+    # long time block with few outputs -> chunked plan with library scratch;
+    # values 0..31 keep every 8 x 60000 group sum below 2^24 (exact in Float32)
+    a = np.asfortranarray(rng.integers(0, 32, (64, 1, 60000)).astype(np.float32))
     want = orc.reduce(a, 8, 60000)
     for _ in range(2):
         eng.reduce_host(a, 8, 60000)
