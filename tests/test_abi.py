@@ -94,10 +94,17 @@ def plan(pkg, L, ptr, nchan, nif, ntime, F, T, win=None):
 
 def test_launch_plans_host_only(pkg, L):
     A = 1 << 20  # any 16-byte aligned address
-    # cfg3 bank: vector path, one wave per group (64 lanes x 4 float4 per row)
+    # cfg3 bank: interleaved vector path, 4 groups of 1024 channels per
+    # workgroup (64 lanes x 4 float4 per row each)
     p = plan(pkg, L, A, 1 << 26, 1, 16, 1024, 16)
-    assert p[0] == 0 and p[1] == 64 and p[3] == 4 and p[4] == 1
+    assert p[0] == 4 and p[1] == 64 and p[3] == 4 and p[4] == 1
     assert p[5] == 65536 // 4
+    # F = 512 / 2048 / 4096 interleave too; F = 8192 and split time blocks do not
+    assert plan(pkg, L, A, 1 << 26, 1, 16, 512, 16)[0] == 4
+    assert plan(pkg, L, A, 1 << 26, 1, 16, 2048, 16)[0] == 4
+    assert plan(pkg, L, A, 1 << 26, 1, 16, 4096, 16)[0] == 4
+    assert plan(pkg, L, A, 1 << 26, 1, 16, 8192, 16)[0] == 0
+    assert plan(pkg, L, A, 4096, 1, 4096, 1024, 4096)[0] == 0
     # cfg1: F=64 -> 16 lanes per group
     p = plan(pkg, L, A, 65536, 1, 279, 64, 16, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
     assert p[0] == 0 and p[1] == 16 and p[3] == 1

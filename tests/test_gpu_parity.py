@@ -101,6 +101,27 @@ def test_reduce_paths_integer_exact(eng, orc, shape):
             np.testing.assert_allclose(got, want, rtol=RTOL, err_msg=str((shape, op)))
 
 
+# Interleaved vector path (F = 512..4096 with >= 4096 groups): a tail
+# segment of fewer than 4 groups, several IFs and time blocks, every op.
+IL_SHAPES = [(4098, 1, 16, 1024, 16), (8194, 2, 8, 512, 4), (4097, 1, 8, 2048, 8),
+             (4099, 1, 4, 4096, 2)]
+
+
+@pytest.mark.parametrize("shape", IL_SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_reduce_interleaved_integer_exact(eng, orc, shape):
+    nco, ni, nt, F, T = shape
+    x = eng.synth(nco * F, ni, nt, 1024, seed=nco + F, kind=1)  # integers 0..255
+    a = host(eng, x)
+    for op in ("sum", "max", "min", "mean"):
+        assert eng.plan(x, F, T, op)["path"] == "interleaved"
+        got = host(eng, eng.reduce(x, F, T, op))
+        assert same_bits(got, orc.reduce(a, F, T, op)), (shape, op)  # F*T*255 < 2^24
+    # band launch: 3 banks written into their stitched slots
+    banks = [x] + [eng.synth(nco * F, ni, nt, 1024, seed=b, kind=1) for b in (1, 2)]
+    got = host(eng, eng.band_reduce(banks, F, T))
+    assert same_bits(got, orc.stitch([orc.reduce(host(eng, b), F, T) for b in banks]))
+
+
 def test_plan_covers_all_paths(eng):
     import torch
 

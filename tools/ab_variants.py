@@ -32,6 +32,8 @@ VARIANTS = {
     "tk4a1": "-DBLDP_TILE_ACC=1",
     "tk2a1": "-DBLDP_TILE_K=2 -DBLDP_TILE_ACC=1",
     "tk2a2": "-DBLDP_TILE_K=2",
+    # k_reduce_vec instead of the interleaved k_reduce_il for F = 512..4096
+    "noil": "-DBLDP_VEC_IL=0",
 }
 
 

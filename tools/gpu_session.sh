@@ -54,7 +54,7 @@ for s in $STEPS; do
     dist2c2) run dist2c2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
              --master-addr 127.0.0.1 --master-port 29612 bench.py --gpus 2 --dist-backend gloo \
              --steps 10 --warmup 3 --config cfg2 ;;
-    ab)    run ab 900 python tools/ab_variants.py --run --json "$OUT/ab.json" ;;
+    ab)    run ab 900 python tools/ab_variants.py --run --variants "${AB_VARIANTS:-base,noil}" --json "$OUT/ab.json" ;;
     ab_tile) run ab_tile 900 python tools/ab_variants.py --run --suite tile --variants base,tk4a1,tk2a1,tk2a2 --json "$OUT/ab_tile.json" ;;
   esac
 done
