@@ -378,23 +378,27 @@ def main():
     write_b = 4 * nco * ni * nto
     bytes_step = nb * (read_b + write_b)          # whole band (all ranks)
     bytes_launch = len(mine) * (read_b + write_b)  # this rank's single reduce launch
-    out = eng.fb_empty(len(mine) * nco, ni, nto)
     stream = torch.cuda.current_stream()
+    # this rank's slice of the band; N > 1: two slots, the RCCL gather of step
+    # k (to rank 0, over xGMI) overlaps the reduce of step k+1
+    pipe = pkg.band.BandPipeline(len(mine) * nco, ni, nto, device=f"cuda:{local}") \
+        if world > 1 else None
+    out = eng.fb_empty(len(mine) * nco, ni, nto) if world == 1 else None
 
     def step(ev0=None, ev1=None):
+        slot = pipe.begin() if pipe else 0
+        dst = pipe.local(slot) if pipe else out
         if ev0 is not None:
             ev0.record(stream)
-        eng.band_reduce(banks, cfg["F"], cfg["T"], "sum", win, out=out)
+        eng.band_reduce(banks, cfg["F"], cfg["T"], "sum", win, out=dst)
         if ev1 is not None:
             ev1.record(stream)
-        if world > 1:
-            return pkg.band.band_reduce_dist(
-                banks, cfg["F"], cfg["T"], "sum", win,
-                reduce_fn=lambda *a: out)  # exchange + stitch of this step's slice
-        return out
+        return pipe.exchange(slot) if pipe else dst  # root: the stitched band
 
     for _ in range(args.warmup):
         step()
+    if pipe:
+        pipe.drain()
     torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps)]
@@ -404,6 +408,8 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(*evs[k])
+    if pipe:
+        pipe.drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -415,6 +421,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el, kern_ms = float(t[0]), float(t[1])
     ms_step = el * 1e3 / args.steps
+    path = eng.plan(banks[0], cfg["F"], cfg["T"], "sum", win)["path"] if banks else None
+    kernel_name = {"interleaved": "k_reduce_il", "vector": "k_reduce_vec",
+                   "narrow": "k_reduce_narrow", "tile": "k_reduce_tile",
+                   "scalar": "k_reduce_scalar"}.get(path, path) + \
+        f" ({len(mine)}-bank launch)"
     value = bytes_step / (ms_step * 1e-3) / 1e9
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
     traffic = traffic_from_profile(args.config, len(mine))
@@ -437,12 +448,13 @@ def main():
                        "nchan": cfg["nchan"], "nif": cfg["nif"], "ntime": cfg["tw"],
                        "fqavby": cfg["F"], "tavby": cfg["T"],
                        "parallelism": f"{len(mine)} bank(s)/GPU x {world} GPU(s)"
-                                      + (", RCCL gather + stitch" if world > 1 else
+                                      + (", RCCL gather + stitch (gather of step k overlaps "
+                                         "the reduce of step k+1)" if world > 1 else
                                          ", single-launch band reduce+stitch"),
                        "bytes_per_step": bytes_step},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "kernel": "bldp k_reduce_vec (band launch)",
+                         "traffic": traffic, "kernel": kernel_name,
                          "kernel_ms": round(kern_ms, 4), "bytes_per_launch": bytes_launch},
             "cpu_baseline": cpu,
         }

@@ -68,3 +68,104 @@ def band_reduce_dist(local_banks, fqavby=1, tavby=1, op="sum", win=None, root=0,
         return stitch_fn(gathered, world)
     dist.gather(block, gather_list=None, dst=root, group=group)
     return None
+
+
+class BandPipeline:
+    """Repeated band exchange with the gather of step k overlapping the
+    reduce of step k+1 (``depth`` buffer slots, asynchronous gathers).
+
+    Per step, SPMD on every rank::
+
+        s = pipe.begin()                     # a free slot (GPU-side wait only)
+        engine.band_reduce(my_banks, ..., out=pipe.local(s))
+        product = pipe.exchange(s)           # root: the stitched band; else None
+
+    ``local(s)`` is this rank's (nbl*nco, ni, nto) Julia-order slice.  The
+    gather runs on the process group's own stream; the root's product of slot
+    ``s`` may still be in flight: ``wait(s)`` (or ``drain()``) makes the
+    current stream wait for it.  It stays valid until that slot is used again
+    ``depth`` steps later (when
+    every bank's output is one (IF, time) row the gathered bytes already are
+    the product, otherwise the root stitches after waiting for the gather).
+    ``drain()`` waits for every gather in flight.  With the gloo backend (CPU
+    transport, the rehearsal of the N-rank path) every gather completes inside
+    ``exchange``.
+    """
+
+    def __init__(self, ncl, ni, nto, device, depth=2, root=0, group=None, stitch_fn=None):
+        import torch
+        import torch.distributed as dist
+
+        from . import engine
+
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.root, self.group, self.depth = root, group, depth
+        self.shape = (ncl, ni, nto)
+        self.gloo = dist.get_backend(group) == "gloo"
+        self.stitch_fn = stitch_fn or (lambda g, n: engine.stitch(g, n))
+        dev = torch.device(device)
+        # Julia order (ncl, ni, nto), channel fastest = contiguous [nto][ni][ncl]
+        self._local = [torch.empty((nto, ni, ncl), dtype=torch.float32, device=dev)
+                       for _ in range(depth)]
+        self._gathered = None
+        if self.rank == root:
+            gdev = torch.device("cpu") if self.gloo else dev
+            self._gathered = [torch.empty((self.world, nto, ni, ncl), dtype=torch.float32,
+                                          device=gdev) for _ in range(depth)]
+        self._work = [None] * depth
+        self._next = 0
+
+    def local(self, slot):
+        return self._local[slot].permute(2, 1, 0)
+
+    def begin(self):
+        """Next slot; the current stream waits (on the GPU) for the gather
+        that last read it."""
+        s = self._next
+        self._next = (s + 1) % self.depth
+        w = self._work[s]
+        if w is not None:
+            w.wait()
+            self._work[s] = None
+        return s
+
+    def exchange(self, slot):
+        import torch.distributed as dist
+
+        block = self._local[slot]
+        if self.world == 1:
+            return self.local(slot)
+        if self.gloo and block.is_cuda:
+            block = block.cpu()
+        glist = list(self._gathered[slot].unbind(0)) if self.rank == self.root else None
+        w = dist.gather(block, gather_list=glist, dst=self.root, group=self.group,
+                        async_op=True)
+        ncl, ni, nto = self.shape
+        if self.gloo:
+            w.wait()
+        else:
+            self._work[slot] = w
+        if self.rank != self.root:
+            return None
+        g = self._gathered[slot]
+        if self.gloo:
+            g = g.to(self._local[slot].device)
+        if ni * nto == 1:  # rank-major slices of single rows are already vcat order
+            return g.reshape(self.world * ncl, 1, 1)
+        if self._work[slot] is not None:
+            self._work[slot].wait()  # the stitch reads the gathered blocks
+            self._work[slot] = None
+        return self.stitch_fn(g, self.world)
+
+    def wait(self, slot):
+        w = self._work[slot]
+        if w is not None:
+            w.wait()
+            self._work[slot] = None
+
+    def drain(self):
+        for s, w in enumerate(self._work):
+            if w is not None:
+                w.wait()
+                self._work[s] = None

@@ -140,12 +140,24 @@ def _band_worker(rank, world, port, F, T, ni, nt, q):
 
     res = pkg.band.band_reduce_dist(mine, F, T, "sum", None, reduce_fn=reduce_fn,
                                     stitch_fn=stitch_fn)
-    if rank == 0:
-        want = orc.stitch([orc.reduce(b, F, T) for b in banks])
-        got = res.permute(2, 1, 0).contiguous().numpy().transpose(2, 1, 0)
-        q.put(bool(np.array_equal(got, want)) and got.shape == want.shape)
-    else:
-        q.put(res is None)
+    want = orc.stitch([orc.reduce(b, F, T) for b in banks])
+
+    def check(r):
+        got = r.permute(2, 1, 0).contiguous().numpy().transpose(2, 1, 0)
+        return bool(np.array_equal(got, want)) and got.shape == want.shape
+
+    ok = check(res) if rank == 0 else res is None
+    # the pipelined exchange bench.py times: 3 steps over 2 slots, each slot
+    # filled with this rank's slice before its gather
+    loc = reduce_fn(mine, F, T, "sum", None)
+    pipe = pkg.band.BandPipeline(*loc.shape, device="cpu", stitch_fn=stitch_fn)
+    for _ in range(3):
+        s = pipe.begin()
+        pipe.local(s).copy_(loc)
+        r = pipe.exchange(s)
+        ok = ok and (check(r) if rank == 0 else r is None)
+    pipe.drain()
+    q.put(ok)
     dist.destroy_process_group()
 
 
