@@ -68,10 +68,8 @@ def traffic_from_profile(cfg_name, n_local_banks):
             d = json.load(f)
     except (OSError, ValueError):
         return None
-    e = d.get(cfg_name)
-    if not e or e.get("banks_per_launch") != n_local_banks:
-        return None
-    return e.get("hbm_bytes_per_launch")
+    e = d.get(cfg_name, {}).get(str(n_local_banks))
+    return e.get("hbm_bytes_per_launch") if e else None
 
 
 def cpu_baseline(cfg, seconds, eng, torch):
@@ -328,6 +326,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", default="reduce",
                     choices=["reduce", "kurtosis", "host", "decode", "file"])
+    ap.add_argument("--local-banks", type=int, default=None,
+                    help="N=1 only: reduce just this many banks per launch, i.e. one rank's "
+                         "share of an N-GPU run (for per-launch PMC profiles)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo only to rehearse the N-rank path on one GPU")
     args = ap.parse_args()
@@ -365,6 +366,11 @@ def main():
     if nb % world:
         raise SystemExit(f"{nb} banks do not shard over {world} GPUs")
     mine = list(pkg.band.banks_for_rank(nb, rank, world)) if nb >= world else [0]
+    if args.local_banks:
+        if world != 1 or nb % args.local_banks:
+            raise SystemExit("--local-banks: N=1 only, and it must divide the bank count")
+        mine = mine[:args.local_banks]
+        nb = len(mine)  # the job is this share of the band
     win = None
     if cfg["tw"] != cfg["ntime"]:
         win = [0, cfg["nchan"], 1, 0, cfg["nif"], 1, 0, cfg["tw"], 1]  # idxs=(:, :, 1:tw)

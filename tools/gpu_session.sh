@@ -37,6 +37,12 @@ for s in $STEPS; do
              -d "$OUT/pmc_fetch" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline
            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv \
              -d "$OUT/pmc_write" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+    pmclb_*) K=${s#pmclb_}
+           run "pmc_fetch_lb$K" 300 rocprofv3 --pmc FETCH_SIZE --output-format csv \
+             -d "$OUT/pmc_fetch_lb$K" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --local-banks "$K"
+           run "pmc_write_lb$K" 300 rocprofv3 --pmc WRITE_SIZE --output-format csv \
+             -d "$OUT/pmc_write_lb$K" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --local-banks "$K" ;;
+    benchlb_*) run "$s" 300 python bench.py --no-cpu-baseline --local-banks "${s#benchlb_}" ;;
     bench_*) run "$s" 600 python bench.py --config "${s#bench_}" ;;
     kurt_*) run "$s" 600 python bench.py --mode kurtosis --config "${s#kurt_}" ;;
     host)  run host 900 python bench.py --mode host ;;

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Turn two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE; separate runs as
 MI355X_MICROARCH.md §rocprofv3 PMC slots requires) into per-launch HBM bytes
-of the reduce kernel, and record them in profiles/pmc_traffic.json for bench.py.
+of the reduce kernel, and record them in profiles/pmc_traffic.json for bench.py
+(keyed by config, then by banks per launch: 8 at N=1, 8/N for one rank of an
+N-GPU run, profiled with bench.py --local-banks).
 
 gfx950 corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE (KiB) reports half
 the bytes of a wide (16 B/lane) coalesced streaming read -> x2; WRITE_SIZE is
@@ -44,7 +46,10 @@ def main():
             d = json.load(f)
     except (OSError, ValueError):
         d = {}
-    d[cfg] = {"banks_per_launch": nbank, "hbm_bytes_per_launch": int(hbm),
+    d.setdefault(cfg, {})
+    if "banks_per_launch" in d[cfg]:  # older flat layout: one entry per config
+        d[cfg] = {str(d[cfg]["banks_per_launch"]): d[cfg]}
+    d[cfg][str(nbank)] = {"banks_per_launch": nbank, "hbm_bytes_per_launch": int(hbm),
               "fetch_size_kib_median": f_kib, "write_size_kib_median": w_kib,
               "dispatches": [len(fetch), len(write)],
               "correction": "hbm = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 half-count "
@@ -52,7 +57,7 @@ def main():
               "source": [os.path.relpath(fpath, REPO), os.path.relpath(wpath, REPO)]}
     with open(out, "w") as f:
         json.dump(d, f, indent=1)
-    print(json.dumps(d[cfg]))
+    print(json.dumps(d[cfg][str(nbank)]))
 
 
 if __name__ == "__main__":
