@@ -749,8 +749,42 @@ __global__ __launch_bounds__(kBlock) void k_kurt_pass(const KurtArgs k) {
 // Short windows (nt <= NTMAX spectra): each lane keeps its float4 column of
 // every spectrum in registers, so the window is read from HBM once; the
 // arithmetic is the same two-pass StatsBase recipe, run over the registers.
-template <int NTMAX>
-__global__ __launch_bounds__(kBlock) void k_kurt_regs(const KurtArgs k) {
+// EXACT (nt == NTMAX, e.g. the 16-spectrum 0000 product) is straight-line
+// code: all NTMAX loads issue back to back and the Float64 sum starts as the
+// first one lands; otherwise every spectrum beyond nt is predicated off.
+//   BLDP_KURT_EXACT 1 (default) = use the exact-count instantiation
+#ifndef BLDP_KURT_EXACT
+#define BLDP_KURT_EXACT 1
+#endif
+//   BLDP_KURT_F32MEAN 1 = the mean from a Float32 sum (as Julia's mean of a
+//                   Float32 vector); 0 (default) = from a Float64 sum
+//   BLDP_KURT_TIMING_F32 1 = TIMING EXPERIMENT ONLY (wrong numerics): Float32
+//                   moments, to price the Float64 arithmetic
+#ifndef BLDP_KURT_F32MEAN
+#define BLDP_KURT_F32MEAN 0
+#endif
+#ifndef BLDP_KURT_TIMING_F32
+#define BLDP_KURT_TIMING_F32 0
+#endif
+//   BLDP_KURT_STORE 3 (default) = the wave's 256 Float64 results go through
+//                   LDS so every nt store instruction writes 1 KiB contiguous
+//                   (+2.5% on the 0000 band against 1); 1 = each lane's 32 B as
+//                   two nt 16-byte stores; 2 = the same, plain stores;
+//                   0 = TIMING EXPERIMENT ONLY: no store (prices the output writes)
+#ifndef BLDP_KURT_STORE
+#define BLDP_KURT_STORE 3
+#endif
+//   BLDP_KURT_WAVES minimum waves per SIMD the register budget must allow
+//                   (0 = compiler's choice)
+#ifndef BLDP_KURT_WAVES
+#define BLDP_KURT_WAVES 0
+#endif
+template <int NTMAX, bool EXACT>
+__global__ __launch_bounds__(kBlock)
+#if BLDP_KURT_WAVES > 0
+__attribute__((amdgpu_waves_per_eu(BLDP_KURT_WAVES)))
+#endif
+void k_kurt_regs(const KurtArgs k) {
   const int64_t ncols = k.nc / 4;
   const int64_t ctiles = (ncols + kBlock - 1) / kBlock;
   const int64_t b = blockIdx.x;
@@ -759,39 +793,86 @@ __global__ __launch_bounds__(kBlock) void k_kurt_regs(const KurtArgs k) {
   const int bank = (int)(ib / k.ni);
   const int64_t i = ib - (int64_t)bank * k.ni;
   const float *p = k.in[bank] + k.in_off + i * k.in_ld_i + 4 * col;
-  const int nt = (int)k.nt;
+  const int nt = EXACT ? NTMAX : (int)k.nt;
+  const int64_t ld = k.in_ld_t;
   float4 v[NTMAX];
 #pragma unroll
   for (int t = 0; t < NTMAX; ++t)
-    if (t < nt) v[t] = ld4(p + t * k.in_ld_t);
-  double s[4] = {0, 0, 0, 0};
+    if (EXACT || t < nt) v[t] = ld4(p + t * ld);
+#if BLDP_KURT_F32MEAN
+  typedef float acc_t;
+#else
+  typedef double acc_t;
+#endif
+  acc_t s[4] = {0, 0, 0, 0};
 #pragma unroll
   for (int t = 0; t < NTMAX; ++t)
-    if (t < nt) {
-      s[0] += (double)v[t].x; s[1] += (double)v[t].y;
-      s[2] += (double)v[t].z; s[3] += (double)v[t].w;
+    if (EXACT || t < nt) {
+      s[0] += (acc_t)v[t].x; s[1] += (acc_t)v[t].y;
+      s[2] += (acc_t)v[t].z; s[3] += (acc_t)v[t].w;
     }
   float m[4];
 #pragma unroll
   for (int w = 0; w < 4; ++w) m[w] = (float)s[w] / (float)nt;  // Float32 sum / length
+#if BLDP_KURT_TIMING_F32
+  float c2[4] = {0, 0, 0, 0}, c4[4] = {0, 0, 0, 0};
+#else
   double c2[4] = {0, 0, 0, 0}, c4[4] = {0, 0, 0, 0};
+#endif
 #pragma unroll
   for (int t = 0; t < NTMAX; ++t)
-    if (t < nt) {
+    if (EXACT || t < nt) {
       const float x[4] = {v[t].x, v[t].y, v[t].z, v[t].w};
 #pragma unroll
       for (int w = 0; w < 4; ++w) {
         const float z = x[w] - m[w];  // StatsBase: z, z2 in Float32; Float64 moments
         const float z2 = z * z;
+#if BLDP_KURT_TIMING_F32
+        c2[w] += z2;
+        c4[w] += z2 * z2;
+#else
         c2[w] += (double)z2;
         c4[w] += (double)(z2 * z2);
+#endif
       }
     }
-  const int64_t e = ib * k.nc + 4 * col;
+  double r[4];
 #pragma unroll
   for (int w = 0; w < 4; ++w) {
-    const double cm2 = c2[w] / (double)k.nt, cm4 = c4[w] / (double)k.nt;
-    k.out[e + w] = (cm4 / (cm2 * cm2)) - 3.0;
+    const double cm2 = c2[w] / (double)nt, cm4 = c4[w] / (double)nt;
+    r[w] = (cm4 / (cm2 * cm2)) - 3.0;
+  }
+  // 32 contiguous bytes per lane: two 16-byte streaming stores
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  d2v *o = reinterpret_cast<d2v *>(k.out + ib * k.nc + 4 * col);
+  if (BLDP_KURT_STORE == 0) {
+    if (r[0] == 12345.678) k.out[0] = r[1];  // keeps the arithmetic live
+  } else if (BLDP_KURT_STORE == 3 && ncols % 64 == 0 &&
+             (reinterpret_cast<uintptr_t>(k.out + ib * k.nc) & 15) == 0) {
+    // whole wave in range: transpose through this wave's 2 KiB of LDS so each
+    // store instruction writes 1 KiB contiguous (lane L: doubles 2L, 2L+1 of
+    // the wave's 256 outputs, then 128 + 2L, 129 + 2L)
+    __shared__ d2v st[4][128];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    st[wave][2 * lane] = d2v{r[0], r[1]};
+    st[wave][2 * lane + 1] = d2v{r[2], r[3]};
+    __builtin_amdgcn_wave_barrier();
+    const d2v a0 = st[wave][lane], a1 = st[wave][64 + lane];
+    d2v *ow = reinterpret_cast<d2v *>(k.out + ib * k.nc + 4 * (col - lane));
+    __builtin_nontemporal_store(a0, ow + lane);
+    __builtin_nontemporal_store(a1, ow + 64 + lane);
+  } else if ((reinterpret_cast<uintptr_t>(o) & 15) == 0) {
+    if (BLDP_KURT_STORE == 1) {
+      __builtin_nontemporal_store(d2v{r[0], r[1]}, o);
+      __builtin_nontemporal_store(d2v{r[2], r[3]}, o + 1);
+    } else {
+      o[0] = d2v{r[0], r[1]};
+      o[1] = d2v{r[2], r[3]};
+    }
+  } else {
+    double *od = k.out + ib * k.nc + 4 * col;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) od[w] = r[w];
   }
 }
 
@@ -1096,10 +1177,14 @@ hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s) {
   const int64_t ncols = k.vec ? k.nc / 4 : k.nc;
   if (k.vec && k.nt > 0 && k.nt <= 32) {  // one HBM read: the column fits in registers
     const dim3 g1((unsigned)(cdiv(ncols, kBlock) * k.nrow));
-    if (k.nt <= 16)
-      hipLaunchKernelGGL(k_kurt_regs<16>, g1, dim3(kBlock), 0, s, k);
+    if (BLDP_KURT_EXACT && k.nt == 16)
+      hipLaunchKernelGGL((k_kurt_regs<16, true>), g1, dim3(kBlock), 0, s, k);
+    else if (BLDP_KURT_EXACT && k.nt == 32)
+      hipLaunchKernelGGL((k_kurt_regs<32, true>), g1, dim3(kBlock), 0, s, k);
+    else if (k.nt <= 16)
+      hipLaunchKernelGGL((k_kurt_regs<16, false>), g1, dim3(kBlock), 0, s, k);
     else
-      hipLaunchKernelGGL(k_kurt_regs<32>, g1, dim3(kBlock), 0, s, k);
+      hipLaunchKernelGGL((k_kurt_regs<32, false>), g1, dim3(kBlock), 0, s, k);
     return hipGetLastError();
   }
   const dim3 grid((unsigned)(cdiv(cdiv(ncols, 64), 4 / k.ts) * k.nrow * k.nchunk)), block(kBlock);

@@ -383,17 +383,22 @@ def test_full_size_cfg4_and_cfg2_banks(eng, orc):
     np.testing.assert_allclose(got, want, rtol=RTOL)
 
 
-@pytest.mark.parametrize("nt", [1, 2, 7, 16, 17, 32, 33])
-def test_kurtosis_short_windows(eng, orc, nt):
-    """nt <= 32 runs the register-resident single-read kernel; 33 the two-pass."""
-    rng = np.random.default_rng(nt)
-    a = np.asfortranarray((rng.standard_normal((4096, 2, nt)) ** 2).astype(np.float32) * 1e6)
+@pytest.mark.parametrize("nt", [1, 2, 7, 12, 16, 17, 32, 33])
+@pytest.mark.parametrize("nc,ni", [(4096, 2), (4100, 1)])
+def test_kurtosis_short_windows(eng, orc, nt, nc, ni):
+    """nt <= 32 runs the register-resident single-read kernel (exact-count
+    code at 16 and 32; whole waves store through LDS, a partial wave per
+    lane); 33 the two-pass."""
+    rng = np.random.default_rng(nt + nc)
+    a = np.asfortranarray((rng.standard_normal((nc, ni, nt)) ** 2).astype(np.float32) * 1e6)
     got = host(eng, eng.kurtosis(dev(eng, a)))
     want = orc.kurtosis(a)
     assert np.array_equal(np.isnan(got), np.isnan(want))
     np.testing.assert_allclose(got, want, rtol=1e-4, atol=1e-5)
     ks = eng.band_kurtosis([dev(eng, a), dev(eng, a[::-1].copy(order="F"))])
     np.testing.assert_allclose(host(eng, ks[0]), want, rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(host(eng, ks[1]), orc.kurtosis(a[::-1].copy(order="F")),
+                               rtol=1e-4, atol=1e-5)
 
 
 def test_band_reduce_multi_device_api(eng, orc, pkg):

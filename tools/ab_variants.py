@@ -34,6 +34,16 @@ VARIANTS = {
     "tk2a2": "-DBLDP_TILE_K=2",
     # k_reduce_vec instead of the interleaved k_reduce_il for F = 512..4096
     "noil": "-DBLDP_VEC_IL=0",
+    # kurtosis, short windows: predicated kernel for every nt; register budgets
+    "kold": "-DBLDP_KURT_EXACT=0",
+    "kw5": "-DBLDP_KURT_WAVES=5",
+    "kw6": "-DBLDP_KURT_WAVES=6",
+    "kf32mean": "-DBLDP_KURT_F32MEAN=1",
+    "ktimingf32": "-DBLDP_KURT_TIMING_F32=1",  # timing only: wrong numerics
+    "ktimingall": "-DBLDP_KURT_TIMING_F32=1 -DBLDP_KURT_F32MEAN=1",
+    "kplainst": "-DBLDP_KURT_STORE=2",
+    "knostore": "-DBLDP_KURT_STORE=0",  # timing only: no output
+    "kst1": "-DBLDP_KURT_STORE=1",
 }
 
 
@@ -84,8 +94,30 @@ def run(names, rounds, iters, suite="main"):
             assert rc == 0
         cases.append((label, go, nbytes, out, keep))
 
+    def kurt_case(label, banks, win=None):
+        nchan, nif, ntime = banks[0].shape[0], banks[0].shape[1], banks[0].shape[2]
+        nc = win[1] if win else nchan
+        nt = win[7] if win else ntime
+        out = torch.empty(len(banks) * nc * nif, dtype=torch.float64, device="cuda")
+        ptrs = (ctypes.c_void_p * len(banks))(*[b.data_ptr() for b in banks])
+        keep, wp = pkg._lib.win_arg(win)
+        reads = 1 if nt <= 32 else 2
+        nbytes = len(banks) * (reads * 4 * nc * nif * nt + 8 * nc * nif)
+
+        def go(L):
+            rc = L.bldp_band_kurtosis_f32(len(banks), ctypes.cast(ptrs, ctypes.c_void_p), nchan,
+                                          nif, ntime, wp, out.data_ptr(), sp)
+            assert rc == 0
+        cases.append((label, go, nbytes, out, keep))
+
     b3 = [eng.synth(1 << 26, 1, 16, 1 << 20, seed=10 * b, kind=0) for b in range(8)]
-    if suite == "tile":  # tile path: misaligned starts and odd F at cfg3 scale
+    if suite == "kurt":
+        kurt_case("kurt cfg3 nt16", b3)
+        kurt_case("kurt cfg3 nt12", b3, [0, 1 << 26, 1, 0, 1, 1, 0, 12, 1])
+        b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
+        kurt_case("kurt cfg2 nt272", b2, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
+        cases_done = True
+    elif suite == "tile":  # tile path: misaligned starts and odd F at cfg3 scale
         n = 1 << 26
         band_case("cfg3 c0=1 F1024", b3, 1024, 16, [1, n - 1024, 1, 0, 1, 1, 0, 16, 1])
         band_case("cfg3 c0=3 F64", b3, 64, 16, [3, n - 64, 1, 0, 1, 1, 0, 16, 1])
@@ -149,7 +181,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--suite", default="main", choices=["main", "tile"])
+    ap.add_argument("--suite", default="main", choices=["main", "tile", "kurt"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:

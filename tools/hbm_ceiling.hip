@@ -207,6 +207,35 @@ __global__ __launch_bounds__(256) void k_cfg3_pipe(const f4v *in, int64_t row4, 
   if (prev_t >= 0) epi<IL>(prev, lane, wave, red[par], out, prev_t);
 }
 
+// (3c) the kurtosis shape: one float4 column per lane over nrow rows (4 KiB
+// per workgroup per row), then 32 B of output per lane written as two 1 KiB
+// contiguous wave-instructions (STORE 1 = nt, 2 = plain, 0 = none): 1 byte
+// written per 8 read, what k_kurt_regs does on the 0000 product.
+template <int STORE>
+__global__ __launch_bounds__(256) void k_kmix(const f4v *in, int64_t row4, int nrow,
+                                              int64_t segs_per_bank, f4v *out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t bank = blockIdx.x / segs_per_bank, seg = blockIdx.x % segs_per_bank;
+  const f4v *base = in + bank * row4 * nrow + seg * 256 + threadIdx.x;
+  f4v v[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r)
+    v[r] = r < nrow ? __builtin_nontemporal_load(base + (int64_t)r * row4) : f4v{0, 0, 0, 0};
+  f4v a = v[0];
+#pragma unroll
+  for (int r = 1; r < 16; ++r) a += v[r] * v[r];
+  f4v *o = out + (int64_t)blockIdx.x * 512 + (threadIdx.x >> 6) * 128;
+  if (STORE == 1) {
+    __builtin_nontemporal_store(a, o + lane);
+    __builtin_nontemporal_store(a * 2.f, o + 64 + lane);
+  } else if (STORE == 2) {
+    o[lane] = a;
+    o[64 + lane] = a * 2.f;
+  } else if (a.x == 1234.5f) {
+    o[lane] = a;
+  }
+}
+
 __global__ void k_fill(f4v *p, int64_t n4) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256)
     p[i] = f4v{1.f, 2.f, 3.f, (float)(i & 7)};
@@ -355,6 +384,25 @@ int main(int argc, char **argv) {
     PIPE(false, 4)
     PIPE(false, 8)
   }
+  // (3c) kurtosis-shaped read + 1/8 write mix
+  if (gib == 32) {
+    const int nrow = 16;
+    const int64_t row4 = (1ll << 26) / 4, segs = row4 / 256;
+    f4v *wout;
+    CK(hipMalloc(&wout, 4ll << 30));
+    const double mb = (double)bytes + (4ll << 30);
+    report("kurt-shape read 32 GiB + write 4 GiB, nt stores",
+           timeit([&] { hipLaunchKernelGGL((k_kmix<1>), dim3((unsigned)(segs * 8)), dim3(256), 0, 0,
+                                           in, row4, nrow, segs, wout); }, mb, reps));
+    report("kurt-shape read 32 GiB + write 4 GiB, plain stores",
+           timeit([&] { hipLaunchKernelGGL((k_kmix<2>), dim3((unsigned)(segs * 8)), dim3(256), 0, 0,
+                                           in, row4, nrow, segs, wout); }, mb, reps));
+    report("kurt-shape read 32 GiB, no stores (bytes = read only)",
+           timeit([&] { hipLaunchKernelGGL((k_kmix<0>), dim3((unsigned)(segs * 8)), dim3(256), 0, 0,
+                                           in, row4, nrow, segs, wout); }, (double)bytes, reps));
+    CK(hipFree(wout));
+  }
+
   // (4) the library's own band launch on the same buffer (8 banks of 4 GiB
   // carved from it), when libbldp_hip.so is given as argv[3]
   if (argc > 3 && gib == 32) {
