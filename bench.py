@@ -127,7 +127,8 @@ def bench_kurtosis(args, cfg, eng, torch):
     el = time.perf_counter() - t0
     ms = e0.elapsed_time(e1) / args.steps
     n = cfg["nbank"] * cfg["nchan"] * cfg["nif"] * cfg["tw"]
-    reads = 1 if (cfg["tw"] <= 32 and cfg["nchan"] % 4 == 0) else 2  # k_kurt_regs: one read
+    # k_kurt_regs (<= 32 spectra) / k_kurt_mid (<= 512): the window is read once
+    reads = 1 if (cfg["tw"] <= 512 and cfg["nchan"] % 4 == 0) else 2
     algo = reads * 4 * n + 8 * cfg["nbank"] * cfg["nchan"] * cfg["nif"]
     return {"metric": "getkurtosis GB/s of filterbank input", "value": round(4 * n / ms / 1e6, 2),
             "unit": "GB/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
@@ -138,7 +139,8 @@ def bench_kurtosis(args, cfg, eng, torch):
             "roofline": {"bound": "hbm", "achieved": round(algo / ms / 1e6, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(algo / ms / 1e6 / HBM_PEAK_GBS, 4), "traffic": None,
-                         "kernel": "k_kurt_regs (one read)" if reads == 1 else
+                         "kernel": ("k_kurt_regs" if cfg["tw"] <= 32 else "k_kurt_mid") +
+                                   " (one read)" if reads == 1 else
                                    "k_kurt_pass<0> + k_kurt_pass<1> (two reads of the window)"}}
 
 

@@ -462,7 +462,7 @@ static int kurt_setup(int nbank, const float *const *in, int64_t nchan, int64_t 
 static int kurt_run(KurtArgs &k, double *out, void *workspace, void *stream) {
   if (k.nc * k.nrow == 0) return BLDP_OK;
   const int64_t ncols = k.vec ? k.nc / 4 : k.nc;
-  if (((ncols + 63) / 64) * k.nrow * k.nchunk > INT32_MAX)
+  if (((ncols + 63) / 64) * k.nrow * k.nchunk > INT32_MAX || ((ncols + 15) / 16) * k.nrow > INT32_MAX)
     return fail(BLDP_EINVAL, "kurtosis window too large for one launch");
   for (int b = 0; b < k.nbank; ++b)
     if (!k.in[b] && k.nt > 0) return fail(BLDP_EINVAL, "null input pointer (bank %d)", b);

@@ -756,6 +756,12 @@ __global__ __launch_bounds__(kBlock) void k_kurt_pass(const KurtArgs k) {
 #ifndef BLDP_KURT_EXACT
 #define BLDP_KURT_EXACT 1
 #endif
+//   BLDP_KURT_MID_NR rows per thread of the largest k_kurt_mid instantiation
+//                   (windows up to 16 x this many spectra are read once;
+//                   0 = always two passes beyond 32 spectra)
+#ifndef BLDP_KURT_MID_NR
+#define BLDP_KURT_MID_NR 32
+#endif
 //   BLDP_KURT_F32MEAN 1 = the mean from a Float32 sum (as Julia's mean of a
 //                   Float32 vector); 0 (default) = from a Float64 sum
 //   BLDP_KURT_TIMING_F32 1 = TIMING EXPERIMENT ONLY (wrong numerics): Float32
@@ -873,6 +879,91 @@ void k_kurt_regs(const KurtArgs k) {
     double *od = k.out + ib * k.nc + 4 * col;
 #pragma unroll
     for (int w = 0; w < 4; ++w) od[w] = r[w];
+  }
+}
+
+// Mid-length windows (32 < nt <= 16*NR spectra, e.g. the 272-spectrum 0002
+// window): a workgroup holds a 64-channel x nt tile in registers, so the
+// window is still read from HBM once.  Thread (rg, c4) = (tid / 16, tid % 16)
+// keeps float4 column c4 of rows rg, rg + 16, ...; a wave-instruction reads
+// 4 rows x 256 B.  The Float64 sums and moments of the 16 row groups are
+// combined through LDS in row-group order (deterministic); the arithmetic is
+// the StatsBase recipe of k_kurt_regs.
+template <int NR>
+__global__ __launch_bounds__(kBlock) void k_kurt_mid(const KurtArgs k) {
+  const int tid = threadIdx.x, c4 = tid & 15, rg = tid >> 4;
+  const int64_t ncols = k.nc / 4, ctiles = (ncols + 15) / 16;
+  const int64_t b = blockIdx.x;
+  const int64_t ib = b / ctiles, col = (b % ctiles) * 16 + c4;
+  const bool valid = col < ncols;
+  const int bank = (int)(ib / k.ni);
+  const int64_t i = ib - (int64_t)bank * k.ni;
+  const int nt = (int)k.nt;
+  const float *p = k.in[bank] + k.in_off + i * k.in_ld_i + 4 * (valid ? col : 0) +
+                   rg * k.in_ld_t;
+  const int64_t ld16 = 16 * k.in_ld_t;
+  float4 v[NR];
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+    if (valid && rg + 16 * r < nt) v[r] = ld4(p + r * ld16);
+  __shared__ double part[16][16][8];  // [row group][column][moment x channel]
+  __shared__ float mean[16][4];
+  double s[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+    if (valid && rg + 16 * r < nt) {
+      s[0] += (double)v[r].x; s[1] += (double)v[r].y;
+      s[2] += (double)v[r].z; s[3] += (double)v[r].w;
+    }
+#pragma unroll
+  for (int w = 0; w < 4; ++w) part[rg][c4][w] = s[w];
+  __syncthreads();
+  if (rg == 0) {
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      double t = 0;
+      for (int q = 0; q < 16; ++q) t += part[q][c4][w];
+      mean[c4][w] = (float)t / (float)nt;  // Float32 sum / length
+    }
+  }
+  __syncthreads();
+  float m[4];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) m[w] = mean[c4][w];
+  double c2[4] = {0, 0, 0, 0}, cq[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+    if (valid && rg + 16 * r < nt) {
+      const float x[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const float z = x[w] - m[w];  // StatsBase: z, z2 in Float32; Float64 moments
+        const float z2 = z * z;
+        c2[w] += (double)z2;
+        cq[w] += (double)(z2 * z2);
+      }
+    }
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    part[rg][c4][w] = c2[w];
+    part[rg][c4][4 + w] = cq[w];
+  }
+  __syncthreads();
+  if (rg == 0 && valid) {
+    double r[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      double a2 = 0, a4 = 0;
+      for (int q = 0; q < 16; ++q) {
+        a2 += part[q][c4][w];
+        a4 += part[q][c4][4 + w];
+      }
+      const double cm2 = a2 / (double)nt, cm4 = a4 / (double)nt;
+      r[w] = (cm4 / (cm2 * cm2)) - 3.0;
+    }
+    double *o = k.out + ib * k.nc + 4 * col;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) o[w] = r[w];
   }
 }
 
@@ -1185,6 +1276,18 @@ hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s) {
       hipLaunchKernelGGL((k_kurt_regs<16, false>), g1, dim3(kBlock), 0, s, k);
     else
       hipLaunchKernelGGL((k_kurt_regs<32, false>), g1, dim3(kBlock), 0, s, k);
+    return hipGetLastError();
+  }
+  if (k.vec && k.nt > 32 && k.nt <= 16 * BLDP_KURT_MID_NR) {  // one read: the tile fits
+    const dim3 g1((unsigned)(cdiv(ncols, 16) * k.nrow));
+    if (k.nt <= 128)
+      hipLaunchKernelGGL(k_kurt_mid<8>, g1, dim3(kBlock), 0, s, k);
+    else if (k.nt <= 256)
+      hipLaunchKernelGGL(k_kurt_mid<16>, g1, dim3(kBlock), 0, s, k);
+    else if (k.nt <= 384)
+      hipLaunchKernelGGL(k_kurt_mid<24>, g1, dim3(kBlock), 0, s, k);
+    else
+      hipLaunchKernelGGL(k_kurt_mid<32>, g1, dim3(kBlock), 0, s, k);
     return hipGetLastError();
   }
   const dim3 grid((unsigned)(cdiv(cdiv(ncols, 64), 4 / k.ts) * k.nrow * k.nchunk)), block(kBlock);

@@ -401,6 +401,24 @@ def test_kurtosis_short_windows(eng, orc, nt, nc, ni):
                                rtol=1e-4, atol=1e-5)
 
 
+@pytest.mark.parametrize("nt", [33, 100, 128, 129, 272, 384, 385, 512, 513])
+def test_kurtosis_mid_windows(eng, orc, nt):
+    """33..512 spectra: k_kurt_mid keeps a 64-channel tile in registers (one
+    read); a partial last tile; a window with channel/time offsets; 513 is
+    back on the two-pass kernels."""
+    rng = np.random.default_rng(1000 + nt)
+    a = np.asfortranarray((rng.standard_normal((1100, 2, nt + 3)) ** 2).astype(np.float32)
+                          * 1e6)
+    a[5, 1, :] = 7.0  # a constant row -> NaN, as StatsBase
+    got = host(eng, eng.kurtosis(dev(eng, a[:, :, :nt].copy(order="F"))))
+    want = orc.kurtosis(a[:, :, :nt])
+    assert np.array_equal(np.isnan(got), np.isnan(want))
+    np.testing.assert_allclose(got, want, rtol=1e-4, atol=1e-5)
+    w = [8, 1088, 1, 0, 2, 1, 3, nt, 1]  # idxs = (9:1096, :, 4:nt+3)
+    got = host(eng, eng.kurtosis(dev(eng, a), w))
+    np.testing.assert_allclose(got, orc.kurtosis(a, w), rtol=1e-4, atol=1e-5)
+
+
 def test_band_reduce_multi_device_api(eng, orc, pkg):
     """The single-process multi-GPU entry point; on a one-GPU box every bank
     sits on device 0 (the peer path runs on the driver's 8-GPU node)."""

@@ -44,6 +44,7 @@ VARIANTS = {
     "kplainst": "-DBLDP_KURT_STORE=2",
     "knostore": "-DBLDP_KURT_STORE=0",  # timing only: no output
     "kst1": "-DBLDP_KURT_STORE=1",
+    "kmid0": "-DBLDP_KURT_MID_NR=0",  # two passes beyond 32 spectra
 }
 
 
@@ -101,7 +102,7 @@ def run(names, rounds, iters, suite="main"):
         out = torch.empty(len(banks) * nc * nif, dtype=torch.float64, device="cuda")
         ptrs = (ctypes.c_void_p * len(banks))(*[b.data_ptr() for b in banks])
         keep, wp = pkg._lib.win_arg(win)
-        reads = 1 if nt <= 32 else 2
+        reads = 1 if nt <= 512 else 2
         nbytes = len(banks) * (reads * 4 * nc * nif * nt + 8 * nc * nif)
 
         def go(L):
