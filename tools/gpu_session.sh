@@ -44,6 +44,8 @@ for s in $STEPS; do
              -d "$OUT/pmc_write_lb$K" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --local-banks "$K" ;;
     benchlb_*) run "$s" 300 python bench.py --no-cpu-baseline --local-banks "${s#benchlb_}" ;;
     bench_*) run "$s" 600 python bench.py --config "${s#bench_}" ;;
+    benchperbank) run benchperbank 600 python bench.py --band-alloc per-bank --no-cpu-baseline ;;
+    benchnocpu) run benchnocpu 600 python bench.py --no-cpu-baseline ;;
     kurt_*) run "$s" 600 python bench.py --mode kurtosis --config "${s#kurt_}" ;;
     host)  run host 900 python bench.py --mode host ;;
     decode) run decode 600 python bench.py --mode decode ;;
