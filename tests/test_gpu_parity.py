@@ -346,6 +346,32 @@ def test_full_size_bank_properties(eng):
     assert torch.equal(t[:, 0, 0].double(), x[:, 0, :].double().sum(dim=1))
 
 
+def test_full_size_cfg3_band_slab(eng):
+    """The north-star band at full size (8 x 2^26 ch x 16 spectra = 32 GiB in
+    one slab, F=1024, T=16, one launch): on integer data every bank's
+    stitched slot sums to that bank's total, and spot groups of every bank
+    match a host recomputation (exact)."""
+    import torch
+
+    n = 1 << 26
+    banks = eng.band_empty(8, n, 1, 16)
+    for b, v in enumerate(banks):
+        eng.synth(n, 1, 16, 1 << 20, seed=30 + b, kind=1, out=v)
+    out = eng.band_reduce(banks, 1024, 16, "sum")
+    assert tuple(out.shape) == (8 * 65536, 1, 1)
+    assert eng.plan(banks[0], 1024, 16)["path"] == "interleaved"
+    for b, v in enumerate(banks):
+        slot = out[b * 65536:(b + 1) * 65536, 0, 0].double()
+        assert slot.sum().item() == v.double().sum().item(), b
+        for k in (0, 777 * (b + 1), 65535):
+            assert slot[k].item() == v[k * 1024:(k + 1) * 1024].double().sum().item(), (b, k)
+    mx = eng.band_reduce(banks, 1024, 16, "max")
+    assert torch.equal(mx[3 * 65536:4 * 65536, 0, 0],
+                       banks[3][:, 0, :].reshape(65536, 1024, 16).amax(dim=(1, 2)))
+    del banks, out, mx
+    torch.cuda.empty_cache()
+
+
 def test_band_kurtosis(eng, orc):
     rng = np.random.default_rng(21)
     banks = [np.asfortranarray((rng.standard_normal((1024, 2, 300)) ** 2).astype(np.float32))
