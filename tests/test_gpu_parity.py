@@ -122,6 +122,31 @@ def test_reduce_interleaved_integer_exact(eng, orc, shape):
     assert same_bits(got, orc.stitch([orc.reduce(host(eng, b), F, T) for b in banks]))
 
 
+# Time integration (fqavby = 1, the narrow kernel): partial last segments,
+# several IFs / time blocks / banks, every op, a time-offset window.
+TIME_SHAPES = [(4100, 1, 32, 16), (4096, 3, 40, 5), (1 << 20, 2, 48, 16), (1 << 23, 1, 16, 16),
+               (8 * 1024 + 4, 1, 64, 64)]
+
+
+@pytest.mark.parametrize("shape", TIME_SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_reduce_time_integer_exact(eng, orc, shape):
+    nc, ni, nt, T = shape
+    x = eng.synth(nc, ni, nt, 1024, seed=nc + T, kind=1)  # integers 0..255
+    a = host(eng, x)
+    for op in ("sum", "max", "min", "mean"):
+        got = host(eng, eng.reduce(x, 1, T, op))
+        want = orc.reduce(a, 1, T, op)
+        if op == "mean" and T & (T - 1):
+            np.testing.assert_allclose(got, want, rtol=RTOL)
+        else:
+            assert same_bits(got, want), (shape, op)
+    # band: 3 banks written into their stitched slots, a window from spectrum 4
+    w = [0, nc, 1, 0, ni, 1, 3, (nt - 3) // T * T, 1]
+    banks = [x] + [eng.synth(nc, ni, nt, 1024, seed=b, kind=1) for b in (1, 2)]
+    got = host(eng, eng.band_reduce(banks, 1, T, "sum", w))
+    assert same_bits(got, orc.stitch([orc.reduce(host(eng, b), 1, T, "sum", w) for b in banks]))
+
+
 def test_plan_covers_all_paths(eng):
     import torch
 
