@@ -11,7 +11,7 @@ module BLDPHip
 
 using Statistics: mean
 
-export gpu_fqav, gpu_reduce, gpu_kurtosis, gpu_band
+export gpu_init, gpu_finalize, gpu_pin, gpu_unpin, gpu_fqav, gpu_reduce, gpu_kurtosis, gpu_band
 
 const libbldp = get(ENV, "BLDP_LIB", joinpath(@__DIR__, "..", "libbldp_hip.so"))
 
@@ -34,6 +34,37 @@ function check(rc::Integer)
     rc == -1 && throw(ArgumentError(msg))
     error("libbldp_hip error $rc: $msg")
 end
+
+"""
+    gpu_init(devs=nothing)
+
+bldp_init: validate the GPUs (gfx950), create their worker streams and warm
+host-staging pipelines, enable xGMI peer access between them.  Called once per
+worker process after `GBT.setupworkers` (src/gbt.jl:12-46) has started it;
+optional, since every entry point initialises what it needs on first use.
+`nothing` selects every visible device."""
+function gpu_init(devs::Union{Nothing,AbstractVector{<:Integer}}=nothing)
+    if devs === nothing
+        check(ccall((:bldp_init, libbldp), Cint, (Cint, Ptr{Cint}), 0, C_NULL))
+    else
+        d = Cint.(collect(devs))
+        GC.@preserve d check(ccall((:bldp_init, libbldp), Cint, (Cint, Ptr{Cint}), length(d), d))
+    end
+    nothing
+end
+
+"bldp_finalize: drain the devices and free every library-owned resource."
+gpu_finalize() = (check(ccall((:bldp_finalize, libbldp), Cint, ())); nothing)
+
+"""
+    gpu_pin(A::Array) / gpu_unpin(A::Array)
+
+Page-lock a long-lived host array (bldp_host_register) so gpu_reduce and
+gpu_kurtosis copy it at full PCIe rate; the caller keeps `A` alive meanwhile."""
+gpu_pin(A::Array) = (check(ccall((:bldp_host_register, libbldp), Cint, (Ptr{Cvoid}, Csize_t),
+                                 A, sizeof(A))); A)
+gpu_unpin(A::Array) = (check(ccall((:bldp_host_unregister, libbldp), Cint, (Ptr{Cvoid},), A));
+                       A)
 
 # Julia index -> (0-based start, count, step) on an axis of length n
 axiswin(::Colon, n) = (0, n, 1)
@@ -88,8 +119,8 @@ end
 
 getkurtosis' per-(channel, IF) excess kurtosis over time
 (src/gbtworkerfunctions.jl:197-202), computed on GPU `dev`
-(bldp_kurtosis_host_f32: window staged on the device, two-pass StatsBase
-recipe, Float64 result)."""
+(bldp_kurtosis_host_f32: window staged on the device, StatsBase recipe,
+Float64 result)."""
 function gpu_kurtosis(A::Array{Float32,3}; idxs::Tuple=(:, :, :), dev::Integer=0)
     win = window(idxs, size(A))
     shp = zeros(Int64, 3)
