@@ -64,15 +64,22 @@ __device__ __forceinline__ float fold4(float4 v) {
 #ifndef BLDP_BATCH
 #define BLDP_BATCH 8
 #endif
-//   BLDP_MAX_WG_PER_CU  -1 (default) = one workgroup per tile, except plans whose
-//                  waves split the time rows (long T blocks), which get a grid of
-//                  4 workgroups per CU looping over tiles (+3% on cfg4; -7% if
-//                  applied to cfg3); N >= 0 forces a cap of N per CU (0 = none)
+//   BLDP_MAX_WG_PER_CU  0 (default) = one workgroup per tile; N > 0 caps the
+//                  grid at N workgroups per CU looping over tiles; -1 = that cap
+//                  (4) only for plans whose waves split the time rows.  With
+//                  BLDP_TS_FILL the uncapped grid is as fast or faster on every
+//                  measured shape (0001 band F=64 T=16: 6.80 vs 6.05 TB/s)
 #ifndef BLDP_MAX_WG_PER_CU
-#define BLDP_MAX_WG_PER_CU -1
+#define BLDP_MAX_WG_PER_CU 0
 #endif
 //   BLDP_NT_STORES 1 (default) = the narrow path's 16-byte output stores carry
 //                  the nt hint; measured +5% on cfg3 F=1 (5.90 -> 6.21 TB/s)
+//   BLDP_TS_FILL   1 (default) = vector-path plans with fewer than 4 column
+//                  tiles raise ts until no wave of a workgroup idles (0001
+//                  band, 512 channels, F=8 T=1024: 7.05 vs 6.84 TB/s)
+#ifndef BLDP_TS_FILL
+#define BLDP_TS_FILL 1
+#endif
 #ifndef BLDP_NT_STORES
 #define BLDP_NT_STORES 1
 #endif
@@ -1151,6 +1158,11 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, int num_cus) {
     const int64_t ctiles = cdiv(a.nco, 64 / lpg);
     tiles = ctiles * a.ni * a.nto * a.nbank;
     while (a.ts < 4 && tiles * a.ts < target_waves && T >= 2 * a.ts * 8) a.ts *= 2;
+    // no idle waves: a workgroup holds 4/ts column tiles, so narrow windows
+    // (fewer than 4 column tiles, e.g. the 512-channel 0001 product) split
+    // their time rows over the spare waves instead
+    if (BLDP_TS_FILL)
+      while (a.ts < 4 && ctiles < 4 / a.ts && T >= 2 * a.ts * 8) a.ts *= 2;
     a.blocks_c = cdiv(ctiles, 4 / a.ts);
     tiles *= a.ts;
   } else if (aligned && (F == 1 || F == 2) && (a.nco * F) % 4 == 0) {

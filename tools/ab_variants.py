@@ -25,8 +25,8 @@ VDIR = os.path.join(REPO, "build", "variants")
 CSRC = os.path.join(REPO, "bldistributeddataproducts.jl_amd", "csrc")
 
 VARIANTS = {
-    "base": "",                          # nt loads+stores, batch 8, cap 4 WG/CU iff ts > 1
-    "nocap": "-DBLDP_MAX_WG_PER_CU=0",
+    "base": "",                          # nt loads+stores, batch 8, no grid cap
+    "cap4ts": "-DBLDP_MAX_WG_PER_CU=-1",  # 4 WG/CU grid cap for time-split plans
     "plain": "-DBLDP_NT_LOADS=0 -DBLDP_NT_STORES=0 -DBLDP_MAX_WG_PER_CU=0",  # round-1 start
     # tile path (misaligned / odd-F windows): columns per thread, accumulator sets
     "tk4a1": "-DBLDP_TILE_ACC=1",
@@ -34,6 +34,9 @@ VARIANTS = {
     "tk2a2": "-DBLDP_TILE_K=2",
     # k_reduce_vec instead of the interleaved k_reduce_il for F = 512..4096
     "noil": "-DBLDP_VEC_IL=0",
+    # narrow windows: time split over otherwise idle waves, with / without grid cap
+    "notsfill": "-DBLDP_TS_FILL=0",
+
     # kurtosis, short windows: predicated kernel for every nt; register budgets
     "kold": "-DBLDP_KURT_EXACT=0",
     "kw5": "-DBLDP_KURT_WAVES=5",
@@ -139,6 +142,8 @@ def run(names, rounds, iters, suite="main"):
         band_case("cfg1 F64 T16", b2[:1], 64, 16, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
         b4 = [eng.synth(512, 1, 880000, 8, seed=10 * b + 1, kind=0) for b in range(8)]
         band_case("cfg4 F8 T1024", b4, 8, 1024, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
+        band_case("cfg4 1 bank", b4[:1], 8, 1024, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
+        band_case("cfg4 F64 T16", b4, 64, 16, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
     torch.cuda.synchronize()
 
     res = {c[0]: {n: [] for n in names} for c in cases}
