@@ -98,6 +98,8 @@ class _H5:
                                ctypes.c_void_p], herr_t),
             "H5Zfilter_avail": ([ctypes.c_int], ctypes.c_int),
             "H5Dget_chunk_storage_size": ([hid_t, ctypes.c_void_p, ctypes.c_void_p], herr_t),
+            "H5Dget_offset": ([hid_t], ctypes.c_uint64),
+            "H5Tget_order": ([hid_t], ctypes.c_int),
             "H5Dread_chunk": ([hid_t, hid_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p],
                               herr_t),
             "H5Dwrite_chunk": ([hid_t, hid_t, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t,
@@ -477,6 +479,47 @@ def layout(fname) -> dict:
     finally:
         H.H5Fclose(f)
     return dict(cdims=cdims, chunk=chunk, filters=filters)
+
+
+H5D_CONTIGUOUS = 1
+H5T_ORDER_LE = 0
+HADDR_UNDEF = (1 << 64) - 1
+
+
+def raw_layout(fname):
+    """(file offset, Julia shape) when ``data`` is stored as one contiguous
+    block of little-endian float32 with no filter -- what
+    filestream.window_to_device can read with plain preads -- else None."""
+    H5 = h5()
+    H = H5.L
+    f = _ok(H.H5Fopen(os.fsencode(fname), H5F_ACC_RDONLY, H5P_DEFAULT), f"open {fname}")
+    try:
+        d = _ok(H.H5Dopen2(f, b"data", H5P_DEFAULT), "open dataset 'data'")
+        try:
+            pl = _ok(H.H5Dget_create_plist(d), "create_plist")
+            try:
+                if H.H5Pget_layout(pl) != H5D_CONTIGUOUS or H.H5Pget_nfilters(pl) != 0:
+                    return None
+            finally:
+                H.H5Pclose(pl)
+            ty = _ok(H.H5Dget_type(d), "get_type")
+            try:
+                if (H.H5Tget_class(ty) != H5T_FLOAT or H.H5Tget_size(ty) != 4
+                        or H.H5Tget_order(ty) != H5T_ORDER_LE):
+                    return None
+            finally:
+                H.H5Tclose(ty)
+            fs = H.H5Dget_space(d)
+            cdims = _dims(fs)
+            H.H5Sclose(fs)
+            off = H.H5Dget_offset(d)
+            if len(cdims) != 3 or off == HADDR_UNDEF:
+                return None
+            return int(off), tuple(cdims[::-1])
+        finally:
+            H.H5Dclose(d)
+    finally:
+        H.H5Fclose(f)
 
 
 def needs_bslz4(fname) -> bool:

@@ -104,6 +104,15 @@ def fil_mmap(fname):
     return hdr, mm.transpose(2, 1, 0)
 
 
+def fil_raw_layout(fname):
+    """(data offset, Julia shape) of a 32-bit SIGPROC file, whose data block
+    filestream.window_to_device reads with plain preads; None otherwise."""
+    hdr = read_fil_header(fname)
+    if hdr.get("nbits") != 32 or hdr["nsamps"] == 0:
+        return None
+    return hdr["header_size"], (hdr["nchans"], hdr["nifs"], hdr["nsamps"])
+
+
 def getfbheader(fbname) -> dict:
     """src/gbtworkerfunctions.jl:131-139."""
     h = read_fil_header(fbname)

@@ -142,10 +142,46 @@ def _reduce_array(x, idxs, fqavby, fqavfunc, tavby, device):
     return engine.reduce_host(a, fqavby, tavby, op, win, device=device)
 
 
+def _raw_to_device(fname, raw, idxs, device):
+    """The window of a raw (filter-free, contiguous float32) file on GPU
+    ``device``: (Julia-order block tensor, window relative to it), or None for
+    an empty window (the host path returns the empty result)."""
+    from . import filestream
+
+    base, jshape = raw
+    win = to_window(idxs, jshape) or [0, jshape[0], 1, 0, jshape[1], 1, 0, jshape[2], 1]
+    if win[1] * win[4] * win[7] == 0:
+        filestream.plan_window(jshape, win)  # bounds check only
+        return None
+    x, _, rwin = filestream.window_to_device(fname, base, jshape, win, f"cuda:{int(device)}")
+    return x, rwin
+
+
+def _reduce_raw_file(fname, raw, idxs, fqavby, op, tavby, device):
+    import torch
+
+    got = _raw_to_device(fname, raw, idxs, device)
+    if got is None:
+        return None
+    x, rwin = got
+    with torch.cuda.device(x.device):
+        return engine.fb_to_numpy(engine.reduce(x, fqavby, tavby, op, rwin))
+
+
 def getfbdata(fbname, idxs=(COLON, COLON, COLON), fqavby=1, fqavfunc="sum", tavby=1,
               device=0):
-    """SIGPROC filterbank: mmap, window, reduce (src/gbtworkerfunctions.jl:171-177)."""
+    """SIGPROC filterbank: mmap, window, reduce (src/gbtworkerfunctions.jl:171-177).
+    32-bit data with a GPU reduction: only the window's rows / channel spans
+    are read (parallel preads into pinned memory, streamed to the GPU)."""
     assert len(idxs) == 3, "idxs must have exactly three indices"  # :172
+    idxs = sanitizeidxs(idxs)
+    op = _opname(fqavfunc)
+    if op is not None:
+        raw = readers.fil_raw_layout(fbname)
+        if raw is not None:
+            r = _reduce_raw_file(fbname, raw, idxs, fqavby, op, tavby, device)
+            if r is not None:
+                return r
     _, data = readers.fil_mmap(fbname)
     try:
         return _reduce_array(data, idxs, fqavby, fqavfunc, tavby, device)
@@ -170,6 +206,12 @@ def getfbh5data(fbh5name, idxs=(COLON, COLON, COLON), fqavby=1, fqavfunc="sum", 
 
         with torch.cuda.device(x.device):
             return engine.fb_to_numpy(engine.reduce(x, fqavby, tavby, op))
+    if op is not None:
+        raw = fbh5.raw_layout(fbh5name)  # uncompressed contiguous: preads, no libhdf5 copy
+        if raw is not None:
+            r = _reduce_raw_file(fbh5name, raw, idxs, fqavby, op, tavby, device)
+            if r is not None:
+                return r
     data = readers.fbh5_read(fbh5name, idxs)
     return _reduce_array(data, (COLON, COLON, COLON), fqavby, fqavfunc, tavby, device)
 
@@ -195,7 +237,18 @@ def getkurtosis(fname, idxs=(COLON, COLON, COLON), device=0):
     if _is_tensor(fname):
         return engine.kurtosis(fname, to_window(idxs, fname.shape))
     if isinstance(fname, (str, bytes)) or hasattr(fname, "__fspath__"):
-        if readers.ishdf5(fname):
+        from . import fbh5
+
+        h5 = readers.ishdf5(fname)
+        raw = fbh5.raw_layout(fname) if h5 else readers.fil_raw_layout(fname)
+        got = _raw_to_device(fname, raw, idxs, device) if raw is not None else None
+        if got is not None:  # window streamed to the GPU, kurtosis there
+            import torch
+
+            x, rwin = got
+            with torch.cuda.device(x.device):
+                return engine.fb_to_numpy(engine.kurtosis(x, rwin))
+        if h5:
             a, idxs = readers.fbh5_read(fname, idxs), (COLON, COLON, COLON)
         else:
             _, a = readers.fil_mmap(fname)

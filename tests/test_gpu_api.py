@@ -238,3 +238,46 @@ def test_pinned_host_buffer(pkg, orc):
     assert same_bits(got, orc.reduce(a, 64, 16))
     with pytest.raises(pkg._lib.ArgumentError):
         pkg._lib.check(pkg._lib.lib().bldp_host_register(None, 0))
+
+
+def test_raw_files_stream_to_gpu(pkg, orc, tmp_path, monkeypatch):
+    """Uncompressed contiguous FBH5 and 32-bit SIGPROC files: getdata and
+    getkurtosis read only the window (parallel preads into pinned slots,
+    several batches) and reduce on the GPU; exact on integer data."""
+    fs = pkg.filestream
+    monkeypatch.setattr(fs, "BATCH_BYTES", 1 << 20)
+    monkeypatch.setattr(fs, "PIECE_BYTES", 192 << 10)
+    monkeypatch.setattr(fs, "SUBSPAN_MIN_BYTES", 4096)
+    rng = np.random.default_rng(91)
+    a = np.asfortranarray(rng.integers(0, 256, (4096, 2, 300)).astype(np.float32))
+    h5, fil = str(tmp_path / "r.h5"), str(tmp_path / "r.fil")
+    pkg.fbh5.write(h5, dict(foff=-187.5 / 4096, nfpc=64), a)
+    pkg.readers.write_fil(fil, dict(fch1=8000.0, foff=-187.5 / 4096, nchans=4096, nifs=2,
+                                    tsamp=1.0, nbits=32, telescope_id=6, machine_id=10,
+                                    data_type=1, tstart=59000.0, source_name="X"), a)
+    J, C = pkg.JRange, pkg.COLON
+    W = pkg.WorkerFunctions
+    cases = [((C, C, C), 64, 4, "sum"), ((C, 2, J(1, 288)), 16, 8, "max"),
+             ((J(1025, 2048), C, J(300, -3, 1)), 8, 4, "sum"),   # channel span per row
+             ((J(4096, -1, 1), C, J(11, 7, 300)), 4, 1, "min")]
+    for f in (h5, fil):
+        for idxs, F, T, op in cases:
+            win = pkg.idxs.to_window(pkg.sanitizeidxs(idxs), a.shape)
+            got = W.getdata(f, idxs, fqavby=F, fqavfunc=op, tavby=T)
+            assert same_bits(got, orc.reduce(a, F, T, op, win)), (f, idxs)
+        kw = [1024, 1024, 1, 0, 2, 1, 0, 300, 1]
+        got = W.getkurtosis(f, (J(1025, 2048), C, C))
+        np.testing.assert_allclose(got, orc.kurtosis(a, kw), rtol=1e-4, atol=1e-5)
+    tm = {}
+    runs, dshape, rwin = fs.plan_window(a.shape, [0, 4096, 1, 0, 2, 1, 0, 300, 1],
+                                        pkg.fbh5.raw_layout(h5)[0])
+    buf = fs.read_runs_to_device(h5, runs, "cuda:0", timings=tm)
+    assert tm["batches"] > 4 and buf.numel() == a.nbytes
+    assert same_bits(pkg.engine.fb_to_numpy(buf.view(torch_f32()).view(300, 2, 4096)
+                                            .permute(2, 1, 0)), a)
+
+
+def torch_f32():
+    import torch
+
+    return torch.float32

@@ -290,3 +290,50 @@ def test_fbh5_read_chunks_into_one_buffer(pkg, orc, tmp_path):
     assert len(chunks) == len(per[5]) == 9
     for (m1, b), (m2, off, nb) in zip(per[5], chunks):
         assert m1 == m2 and keep[off:off + nb].tobytes() == b
+
+
+RAW_WINDOWS = [
+    None,
+    [0, 1000, 1, 0, 3, 1, 5, 20, 1],
+    [999, 500, -2, 2, 3, -1, 36, 12, -3],
+    [10, 1, 1, 1, 1, 1, 0, 37, 1],
+    [100, 300, 1, 0, 3, 1, 3, 10, 3],
+    [400, 100, 1, 1, 2, 1, 0, 37, 1],
+]
+
+
+@pytest.mark.parametrize("subspan", [False, True])
+def test_raw_file_window_plans(pkg, orc, tmp_path, monkeypatch, subspan):
+    """filestream.plan_window: the byte runs of a window of an uncompressed
+    contiguous FBH5 dataset / a 32-bit SIGPROC data block, read back on the
+    host, hold exactly the window once the relative window is applied (both
+    the whole-row and the channel-span-per-row plans)."""
+    fs = pkg.filestream
+    if subspan:
+        monkeypatch.setattr(fs, "SUBSPAN_MIN_BYTES", 1)
+    rng = np.random.default_rng(77)
+    a = np.asfortranarray(rng.integers(0, 256, (1000, 3, 37)).astype(np.float32))
+    h5, fil = str(tmp_path / "u.h5"), str(tmp_path / "u.fil")
+    pkg.fbh5.write(h5, dict(foff=-1.0, nfpc=64), a)
+    pkg.readers.write_fil(fil, dict(fch1=8000.0, foff=-1.0, nchans=1000, nifs=3, tsamp=1.0,
+                                    nbits=32, telescope_id=6, machine_id=10, data_type=1,
+                                    tstart=59000.0, source_name="X"), a)
+    for f, raw in ((h5, pkg.fbh5.raw_layout(h5)), (fil, pkg.readers.fil_raw_layout(fil))):
+        assert raw is not None and tuple(raw[1]) == a.shape
+        for win in RAW_WINDOWS:
+            w = win or [0, 1000, 1, 0, 3, 1, 0, 37, 1]
+            runs, dshape, rwin = fs.plan_window(raw[1], w, raw[0])
+            blk = fs.read_runs_host(f, runs).view(np.float32)
+            blk = blk.reshape(dshape[::-1]).transpose(2, 1, 0)
+            assert np.array_equal(orc.np_window(blk, rwin), orc.np_window(a, w)), (f, win)
+            if subspan and (w[1] - 1) * abs(w[2]) + 1 < 500:
+                assert dshape[0] < 1000  # channel span only
+    with pytest.raises(pkg.BoundsError):
+        fs.plan_window(a.shape, [0, 1001, 1, 0, 3, 1, 0, 37, 1])
+    # not raw: chunked FBH5, 8-bit SIGPROC
+    pkg.fbh5.write(h5, dict(foff=-1.0), a, chunks=(8, 1, 100))
+    assert pkg.fbh5.raw_layout(h5) is None
+    pkg.readers.write_fil(fil, dict(fch1=8000.0, foff=-1.0, nchans=1000, nifs=3, tsamp=1.0,
+                                    nbits=8, telescope_id=6, machine_id=10, data_type=1,
+                                    tstart=59000.0, source_name="X"), a.astype(np.uint8))
+    assert pkg.readers.fil_raw_layout(fil) is None
