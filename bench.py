@@ -319,6 +319,72 @@ def bench_file(args, eng, torch, pkg):
                                        "(libbldp C++) + oracle reduce, one thread"}}
 
 
+def bench_rawfile(args, eng, torch, pkg):
+    """End to end on an uncompressed contiguous FBH5 file of one 0000 bank's
+    geometry (2^25 ch x 1 IF x 16 spectra = 2 GiB, page cache warm):
+    WorkerFunctions.getdata(fname, (:,:,:); fqavby=1024, tavby=16) = parallel
+    preads into pinned slots + async H2D + one GPU reduce (filestream).  Beside
+    it: the libhdf5 H5Dread + bldp_reduce_host_f32 path (the reference's read,
+    reduce moved to the GPU) and the CPU path (H5Dread + oracle reduce)."""
+    import numpy as np
+
+    import __graft_entry__ as entry
+
+    nchan, nt = 1 << 25, 16
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "bldp_bench_raw.h5")
+    x = eng.synth(nchan, 1, nt, 1 << 20, seed=0, kind=0)
+    a = eng.fb_to_numpy(x)
+    del x
+    pkg.fbh5.write(path, dict(foff=-187.5 / (1 << 20), nfpc=1 << 20), a)
+    nbytes = a.nbytes
+    W, C = pkg.WorkerFunctions, pkg.COLON
+    orc = entry.load_oracle()
+    want = orc.reduce(a, 1024, 16)
+    del a
+    got = W.getdata(path, (C, C, C), fqavby=1024, tavby=16)  # warm: page cache, pinned ring
+    ok = bool(np.allclose(got, want, rtol=1e-5))
+    steps = max(3, args.steps // 4)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        W.getdata(path, (C, C, C), fqavby=1024, tavby=16)
+    el = (time.perf_counter() - t0) / steps
+    tm = {}
+    runs, _, _ = pkg.filestream.plan_window((nchan, 1, nt), [0, nchan, 1, 0, 1, 1, 0, nt, 1],
+                                            pkg.fbh5.raw_layout(path)[0])
+    buf = pkg.filestream.read_runs_to_device(path, runs, "cuda:0", timings=tm)
+    del buf
+    # libhdf5 read (one thread) + host-array GPU reduce
+    t0 = time.perf_counter()
+    h = pkg.fbh5.read_window(path, (C, C, C))
+    t_h5 = time.perf_counter() - t0
+    eng.reduce_host(h, 1024, 16)
+    t_old = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    orc.reduce(h, 1024, 16)
+    t_cpu = t_h5 + time.perf_counter() - t0
+    del h
+    os.remove(path)
+    return {"metric": "uncompressed FBH5 getdata end to end, GB/s of Float32 data",
+            "value": round(nbytes / el / 1e9, 2), "unit": "GB/s", "n_gpus": 1, "steps": steps,
+            "warmup": 1, "ms_per_step": round(el * 1e3, 2), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic 0000-geometry bank written as an uncompressed FBH5 file",
+            "config": {"workload": f"FBH5 ({nchan} ch x 1 IF x {nt} spectra, contiguous), "
+                                   "getdata fqavby=1024 tavby=16", "check": ok,
+                       "stream": {k: (round(v, 4) if isinstance(v, float) else v)
+                                  for k, v in tm.items()},
+                       "h5dread_plus_gpu_reduce_GBps": round(nbytes / t_old / 1e9, 2)},
+            "roofline": {"bound": "host", "achieved": round(nbytes / el / 1e9, 2),
+                         "peak": 63.0, "unit": "GB/s",
+                         "frac": round(nbytes / el / 1e9 / 63.0, 4), "traffic": None,
+                         "kernel": "file bytes to HBM per second (PCIe Gen5 x16 spec 63 GB/s "
+                                   "as the ceiling)"},
+            "cpu_baseline": {"value": round(nbytes / t_cpu / 1e9, 3), "unit": "GB/s",
+                             "cores": 1, "kind": "port",
+                             "sample": "the same file: libhdf5 H5Dread + oracle reduce, "
+                                       "one thread"}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -328,7 +394,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", default="reduce",
-                    choices=["reduce", "kurtosis", "host", "decode", "file"])
+                    choices=["reduce", "kurtosis", "host", "decode", "file", "rawfile"])
     ap.add_argument("--local-banks", type=int, default=None,
                     help="N=1 only: reduce just this many banks per launch, i.e. one rank's "
                          "share of an N-GPU run (for per-launch PMC profiles)")
@@ -364,6 +430,7 @@ def main():
         r = (bench_kurtosis(args, cfg, eng, torch) if args.mode == "kurtosis"
              else bench_decode(args, eng, torch, pkg) if args.mode == "decode"
              else bench_file(args, eng, torch, pkg) if args.mode == "file"
+             else bench_rawfile(args, eng, torch, pkg) if args.mode == "rawfile"
              else bench_host(args, eng, torch, pkg))
         print(json.dumps(r), flush=True)
         return r

@@ -29,9 +29,9 @@ from ._lib import BoundsError
 # only when it is a small part of a wide row; otherwise whole rows are read.
 SUBSPAN_MIN_BYTES = 256 << 10
 SUBSPAN_MAX_FRACTION = 0.5
-PIECE_BYTES = 8 << 20    # largest single pread
+PIECE_BYTES = 4 << 20    # largest single pread
 BATCH_BYTES = 64 << 20   # one pinned slot = one H2D copy
-NSLOTS = 3
+NSLOTS = 4               # up to NSLOTS - 1 batches being read while one is copied
 
 
 def _check(win, jshape):
@@ -179,10 +179,11 @@ def _ring(device):
 def read_runs_to_device(path, runs, device, timings=None):
     """Read ``runs`` of ``path`` into a new dense uint8 device tensor.
 
-    Batches of BATCH_BYTES are read by the ring's threads into a pinned slot
-    (several preads in parallel) and copied to the device on the ring's copy
-    stream; the next batch is read while that copy runs.  The caller's
-    current stream waits for the last copy."""
+    Batches of BATCH_BYTES are read by the ring's threads into pinned slots
+    (several preads per batch, up to NSLOTS - 1 batches in flight) and each
+    is copied to the device on the ring's copy stream as soon as its reads
+    land, while later batches are still being read.  The caller's current
+    stream waits for the last copy."""
     import time
 
     import torch
@@ -209,23 +210,33 @@ def read_runs_to_device(path, runs, device, timings=None):
     fd = os.open(path, os.O_RDONLY)
     try:
         with ring.lock:
-            for k, (blo, bp) in enumerate(batches):
-                s = k % NSLOTS
-                if ring.events[s] is not None:
-                    ring.events[s].synchronize()  # the slot's previous copy is done
-                mv = ring.views[s]
+            reading = []  # (slot, preads, block lo, block hi) in batch order
+
+            def land():  # oldest batch: wait for its preads, queue its H2D copy
+                nonlocal t_read
+                s, futs, blo, hi = reading.pop(0)
                 tr = time.perf_counter()
-                futs = [ring.pool.submit(_pread_into, fd, mv[b - blo:b - blo + n], f)
-                        for f, b, n in bp]
                 for f in futs:
                     f.result()
                 t_read += time.perf_counter() - tr
-                hi = bp[-1][1] + bp[-1][2]
                 with torch.cuda.device(dev), torch.cuda.stream(ring.stream):
                     out[blo:hi].copy_(ring.slots[s][:hi - blo], non_blocking=True)
                     ev = torch.cuda.Event()
                     ev.record(ring.stream)
                 ring.events[s] = ev
+
+            for k, (blo, bp) in enumerate(batches):
+                s = k % NSLOTS
+                if ring.events[s] is not None:
+                    ring.events[s].synchronize()  # the slot's previous copy is done
+                mv = ring.views[s]
+                futs = [ring.pool.submit(_pread_into, fd, mv[b - blo:b - blo + n], f)
+                        for f, b, n in bp]
+                reading.append((s, futs, blo, bp[-1][1] + bp[-1][2]))
+                if len(reading) >= NSLOTS - 1:
+                    land()
+            while reading:
+                land()
             with torch.cuda.device(dev):
                 torch.cuda.current_stream(dev).wait_stream(ring.stream)
                 out.record_stream(ring.stream)

@@ -50,6 +50,7 @@ for s in $STEPS; do
     host)  run host 900 python bench.py --mode host ;;
     decode) run decode 600 python bench.py --mode decode ;;
     file)  run file 600 python bench.py --mode file ;;
+    rawfile) run rawfile 600 python bench.py --mode rawfile ;;
     paths) run paths 300 python tools/probe_paths.py ;;
     paths_big) run paths_big 300 python tools/probe_paths.py --big ;;
     prof_decode) run prof_decode 600 rocprofv3 --kernel-trace --stats --output-format csv \
