@@ -460,30 +460,37 @@ __global__ __launch_bounds__(kBlock) void k_reduce_vec(const RedArgs a) {
 // Vector path, interleaved (PATH_VEC_IL): groups of F = 256*K4 channels
 // (K4 = 2, 4, 8, 16 float4 per lane per row; F = 512 .. 4096, the 0000
 // product's fqavby = 1024 among them), one time block per tile.  A workgroup
-// owns 4 consecutive groups; its 4 waves interleave their loads so that every
+// owns GPW consecutive groups; its 4 waves interleave their loads so that every
 // workgroup-instruction reads 4 KiB contiguous (thread tid reads float4
 // 256*j + tid of the segment) instead of each wave streaming its own group
 // (hbm_ceiling: 7.15 vs 7.09 TB/s on the cfg3 row pattern).  Slot j of a lane
 // belongs to group (4*j + wave)/K4; every group is folded over lanes
 // (xor butterfly), then over waves through LDS in wave order (deterministic).
-// Grid: x = 4-group segment, y = (IF, time block), z = bank: no 64-bit
+// Grid: x = GPW-group segment, y = (IF, time block), z = bank: no 64-bit
 // division on the way to the first load.
 //   BLDP_VEC_IL  1 (default) = use it where it applies; 0 = k_reduce_vec
 #ifndef BLDP_VEC_IL
 #define BLDP_VEC_IL 1
 #endif
-template <int OP, int K4>
+//   BLDP_IL_GPW  groups per workgroup: 2 (default; +0.4% on the 0000 band, +1.3% on one
+//                bank, i.e. one rank at N=8) or 4
+#ifndef BLDP_IL_GPW
+#define BLDP_IL_GPW 2
+#endif
+template <int OP, int K4, int GPW>
 __global__ __launch_bounds__(kBlock) void k_reduce_il(const RedArgs a) {
-  constexpr int NS = K4 < 4 ? K4 : 4;     // group slots per lane
-  constexpr int PER = K4 < 4 ? 1 : K4 / 4; // row loads per slot (K4 >= 4)
-  constexpr int RB = K4 < 8 ? 8 / K4 : 1;  // rows in flight
-  constexpr int JB = K4 < 8 ? K4 : 8;      // loads per batch within a row
+  constexpr int NI = GPW * K4 / 4;           // loads per lane per row
+  constexpr int PER = K4 < 4 ? 1 : K4 / 4;   // consecutive loads of one group slot
+  constexpr int NS = NI / PER;               // group slots per lane
+  constexpr int RB = NI < 8 ? 8 / NI : 1;    // rows in flight
+  constexpr int JB = NI < 8 ? NI : 8;        // loads per batch within a row
+  static_assert(NI >= 1 && NI % PER == 0, "k_reduce_il: GPW * K4 must be a multiple of 4");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t it = blockIdx.y, ni = (uint32_t)a.ni;
   const uint32_t to = it / ni, i = it - to * ni;
   const int bank = blockIdx.z;
-  const int64_t g0 = (int64_t)blockIdx.x * 4;
-  const int ng = (int)min((int64_t)4, a.nco - g0);
+  const int64_t g0 = (int64_t)blockIdx.x * GPW;
+  const int ng = (int)min((int64_t)GPW, a.nco - g0);
   const float id = R<OP>::id();
   float4 acc[NS];
 #pragma unroll
@@ -491,27 +498,27 @@ __global__ __launch_bounds__(kBlock) void k_reduce_il(const RedArgs a) {
   const float *p = a.in[bank] + a.in_off + (int64_t)i * a.in_ld_i +
                    (int64_t)to * a.T * a.in_ld_t + g0 * a.F + 4 * tid;
   const int64_t ld = a.in_ld_t;
-  auto slot = [&](int j) { return K4 < 4 ? j : j / PER; };
+  auto slot = [&](int j) { return j / PER; };
   auto group = [&](int j) { return (4 * j + wave) / K4; };
   int64_t nrows = a.T;
-  if (ng == 4) {
-    if constexpr (K4 < 8) {
+  if (ng == GPW) {
+    if constexpr (NI < 8) {
       for (; nrows >= RB; nrows -= RB) {
-        float4 v[RB * K4];
+        float4 v[RB * NI];
 #pragma unroll
         for (int u = 0; u < RB; ++u)
 #pragma unroll
-          for (int j = 0; j < K4; ++j) v[u * K4 + j] = ld4(p + u * ld + 1024 * j);
+          for (int j = 0; j < NI; ++j) v[u * NI + j] = ld4(p + u * ld + 1024 * j);
         p += RB * ld;
 #pragma unroll
         for (int u = 0; u < RB; ++u)
 #pragma unroll
-          for (int j = 0; j < K4; ++j) acc[slot(j)] = f4<OP>(acc[slot(j)], v[u * K4 + j]);
+          for (int j = 0; j < NI; ++j) acc[slot(j)] = f4<OP>(acc[slot(j)], v[u * NI + j]);
       }
     }
     for (; nrows > 0; --nrows) {
 #pragma unroll
-      for (int jb = 0; jb < K4; jb += JB) {
+      for (int jb = 0; jb < NI; jb += JB) {
         float4 v[JB];
 #pragma unroll
         for (int j = 0; j < JB; ++j) v[j] = ld4(p + 1024 * (jb + j));
@@ -520,10 +527,10 @@ __global__ __launch_bounds__(kBlock) void k_reduce_il(const RedArgs a) {
       }
       p += ld;
     }
-  } else {  // last segment of a row with fewer than 4 groups: skip absent ones
+  } else {  // last segment of a row with fewer than GPW groups: skip absent ones
     for (; nrows > 0; --nrows) {
 #pragma unroll
-      for (int j = 0; j < K4; ++j)
+      for (int j = 0; j < NI; ++j)
         if (group(j) < ng) acc[slot(j)] = f4<OP>(acc[slot(j)], ld4(p + 1024 * j));
       p += ld;
     }
@@ -542,10 +549,8 @@ __global__ __launch_bounds__(kBlock) void k_reduce_il(const RedArgs a) {
 #pragma unroll
     for (int w = 0; w < 4; ++w)
 #pragma unroll
-      for (int q = 0; q < NS; ++q) {
-        const int j = K4 < 4 ? q : q * PER;  // first load index of slot q
-        if ((4 * j + w) / K4 == tid) s = R<OP>::f(s, red[w][q]);
-      }
+      for (int q = 0; q < NS; ++q)
+        if ((4 * q * PER + w) / K4 == tid) s = R<OP>::f(s, red[w][q]);
     a.out[bank * a.out_bank + (int64_t)i * a.out_ld_i + (int64_t)to * a.out_ld_t + g0 + tid] =
         finish<OP>(s, a);
   }
@@ -1100,10 +1105,10 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
   if (p.path == PATH_VEC_IL) {
     const dim3 g3((unsigned)a.blocks_c, (unsigned)(a.ni * a.nto), (unsigned)a.nbank);
     switch (a.k4) {
-      case 2: hipLaunchKernelGGL((k_reduce_il<OP, 2>), g3, block, 0, s, a); break;
-      case 4: hipLaunchKernelGGL((k_reduce_il<OP, 4>), g3, block, 0, s, a); break;
-      case 8: hipLaunchKernelGGL((k_reduce_il<OP, 8>), g3, block, 0, s, a); break;
-      case 16: hipLaunchKernelGGL((k_reduce_il<OP, 16>), g3, block, 0, s, a); break;
+      case 2: hipLaunchKernelGGL((k_reduce_il<OP, 2, BLDP_IL_GPW>), g3, block, 0, s, a); break;
+      case 4: hipLaunchKernelGGL((k_reduce_il<OP, 4, BLDP_IL_GPW>), g3, block, 0, s, a); break;
+      case 8: hipLaunchKernelGGL((k_reduce_il<OP, 8, BLDP_IL_GPW>), g3, block, 0, s, a); break;
+      case 16: hipLaunchKernelGGL((k_reduce_il<OP, 16, BLDP_IL_GPW>), g3, block, 0, s, a); break;
       default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -1200,8 +1205,12 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, int num_cus) {
   // (3-D grid, so every dimension must fit)
   if (BLDP_VEC_IL && p.path == PATH_VEC && p.lpg == 64 &&
       (a.k4 == 2 || a.k4 == 4 || a.k4 == 8 || a.k4 == 16) && a.ts == 1 && a.nchunk == 1 &&
-      a.blocks_c <= INT32_MAX && a.ni * a.nto <= 65535 && a.nbank <= 65535)
+      cdiv(a.nco, BLDP_IL_GPW) <= INT32_MAX && a.ni * a.nto <= 65535 && a.nbank <= 65535) {
     p.path = PATH_VEC_IL;
+    a.blocks_c = cdiv(a.nco, BLDP_IL_GPW);
+    a.ntiles = a.blocks_c * a.ni * a.nto * a.nbank;
+    p.grid = a.ntiles;
+  }
   // narrow-path vector stores
   a.vec_out = 0;
   if (p.path == PATH_NARROW) {

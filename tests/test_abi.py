@@ -94,11 +94,11 @@ def plan(pkg, L, ptr, nchan, nif, ntime, F, T, win=None):
 
 def test_launch_plans_host_only(pkg, L):
     A = 1 << 20  # any 16-byte aligned address
-    # cfg3 bank: interleaved vector path, 4 groups of 1024 channels per
-    # workgroup (64 lanes x 4 float4 per row each)
+    # cfg3 bank: interleaved vector path, 2 groups of 1024 channels per
+    # workgroup (each 4 float4 per row per lane-column)
     p = plan(pkg, L, A, 1 << 26, 1, 16, 1024, 16)
     assert p[0] == 4 and p[1] == 64 and p[3] == 4 and p[4] == 1
-    assert p[5] == 65536 // 4
+    assert p[5] == 65536 // 2
     # F = 512 / 2048 / 4096 interleave too; F = 8192 and split time blocks do not
     assert plan(pkg, L, A, 1 << 26, 1, 16, 512, 16)[0] == 4
     assert plan(pkg, L, A, 1 << 26, 1, 16, 2048, 16)[0] == 4

@@ -34,6 +34,7 @@ VARIANTS = {
     "tk2a2": "-DBLDP_TILE_K=2",
     # k_reduce_vec instead of the interleaved k_reduce_il for F = 512..4096
     "noil": "-DBLDP_VEC_IL=0",
+    "gpw4": "-DBLDP_IL_GPW=4",
     # narrow windows: time split over otherwise idle waves, with / without grid cap
     "notsfill": "-DBLDP_TS_FILL=0",
 
@@ -114,7 +115,8 @@ def run(names, rounds, iters, suite="main"):
             assert rc == 0
         cases.append((label, go, nbytes, out, keep))
 
-    b3 = [eng.synth(1 << 26, 1, 16, 1 << 20, seed=10 * b, kind=0) for b in range(8)]
+    b3 = [eng.synth(1 << 26, 1, 16, 1 << 20, seed=10 * b, kind=0, out=o)
+          for b, o in enumerate(eng.band_empty(8, 1 << 26, 1, 16))]  # one slab, as bench.py
     if suite == "kurt":
         kurt_case("kurt cfg3 nt16", b3)
         kurt_case("kurt cfg3 nt12", b3, [0, 1 << 26, 1, 0, 1, 1, 0, 12, 1])
@@ -144,6 +146,8 @@ def run(names, rounds, iters, suite="main"):
         band_case("cfg4 F8 T1024", b4, 8, 1024, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
         band_case("cfg4 1 bank", b4[:1], 8, 1024, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
         band_case("cfg4 F64 T16", b4, 64, 16, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
+        band_case("cfg3 1 bank", b3[:1], 1024, 16)
+        band_case("cfg3 2 banks", b3[:2], 1024, 16)
     torch.cuda.synchronize()
 
     res = {c[0]: {n: [] for n in names} for c in cases}

@@ -19,6 +19,7 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <string>
 #include <vector>
 
 #define CK(x)                                                                      \
@@ -236,6 +237,34 @@ __global__ __launch_bounds__(256) void k_kmix(const f4v *in, int64_t row4, int n
   }
 }
 
+// (3d) tail study: the interleaved cfg3 pattern with G 1024-channel groups
+// per workgroup (4 KiB x G per row, 16 rows), on nbank banks.
+template <int G>
+__global__ __launch_bounds__(256) void k_cfg3g(const f4v *in, int64_t row4, int nrow,
+                                               int64_t segs_per_bank, float *out) {
+  const int64_t t = blockIdx.x;
+  const int64_t bank = t / segs_per_bank, seg = t % segs_per_bank;
+  const f4v *base = in + bank * row4 * nrow + seg * 256 * G + threadIdx.x;
+  f4v acc[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) acc[g] = f4v{0, 0, 0, 0};
+  constexpr int RB = G >= 8 ? 1 : 8 / G;
+  for (int r = 0; r < nrow; r += RB) {
+    f4v v[RB * G];
+#pragma unroll
+    for (int u = 0; u < RB; ++u)
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+        v[u * G + g] = __builtin_nontemporal_load(base + (int64_t)(r + u) * row4 + g * 256);
+#pragma unroll
+    for (int u = 0; u < RB * G; ++u) acc[u % G] += v[u];
+  }
+  float x = 0.f;
+#pragma unroll
+  for (int g = 0; g < G; ++g) x += fold(acc[g]);
+  if (x == 1234.5f) out[t] = x;
+}
+
 __global__ void k_fill(f4v *p, int64_t n4) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256)
     p[i] = f4v{1.f, 2.f, 3.f, (float)(i & 7)};
@@ -384,6 +413,27 @@ int main(int argc, char **argv) {
     PIPE(false, 4)
     PIPE(false, 8)
   }
+  // (3d) tail study: workgroup size x 1 / 8 banks of the cfg3 shape
+  if (gib == 32 && argc > 4 && std::string(argv[4]) == "tail") {
+    const int nrow = 16;
+    const int64_t row4 = (1ll << 26) / 4;
+    for (int nb : {1, 8}) {
+#define TAILG(G)                                                                             \
+      {                                                                                      \
+        const int64_t segs = row4 / (256 * G);                                               \
+        snprintf(name, sizeof name, "tail: %d bank(s), %d groups (%d KiB) per workgroup", nb, \
+                 G, 64 * G);                                                                 \
+        report(name, timeit([&] { hipLaunchKernelGGL((k_cfg3g<G>), dim3((unsigned)(segs * nb)), \
+                                                     dim3(256), 0, 0, in, row4, nrow, segs, out); }, \
+                            (double)nb * (4ll << 30), reps));                                \
+      }
+      TAILG(1) TAILG(2) TAILG(4) TAILG(8)
+    }
+    CK(hipFree(in));
+    CK(hipFree(out));
+    return 0;
+  }
+
   // (3c) kurtosis-shaped read + 1/8 write mix
   if (gib == 32) {
     const int nrow = 16;
