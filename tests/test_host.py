@@ -161,15 +161,17 @@ def _band_worker(rank, world, port, F, T, ni, nt, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("F,T,ni,nt", [(16, 4, 2, 8), (256, 8, 1, 8)])
-def test_band_exchange_gloo_world2(F, T, ni, nt):
+@pytest.mark.parametrize("F,T,ni,nt,world", [(16, 4, 2, 8, 2), (256, 8, 1, 8, 2),
+                                             (16, 4, 2, 8, 4), (256, 8, 1, 8, 8)])
+def test_band_exchange_gloo(F, T, ni, nt, world):
+    """The N-rank band exchange (as bench.py runs it at N = 2, 4, 8) on CPU."""
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29500 + (os.getpid() % 1000) + F
-    procs = [ctx.Process(target=_band_worker, args=(r, 2, port, F, T, ni, nt, q))
-             for r in range(2)]
+    port = 29500 + (os.getpid() % 1000) + F + 3 * world
+    procs = [ctx.Process(target=_band_worker, args=(r, world, port, F, T, ni, nt, q))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
