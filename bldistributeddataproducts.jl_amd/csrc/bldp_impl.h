@@ -58,7 +58,8 @@ struct RedArgs {
   float div;               // F*T, the mean divisor
 };
 
-enum Path { PATH_VEC = 0, PATH_NARROW = 1, PATH_SCALAR = 2, PATH_TILE = 3, PATH_VEC_IL = 4 };
+enum Path { PATH_VEC = 0, PATH_NARROW = 1, PATH_SCALAR = 2, PATH_TILE = 3, PATH_VEC_IL = 4,
+            PATH_VEC_ROW = 5 };
 
 struct Plan {
   int path;

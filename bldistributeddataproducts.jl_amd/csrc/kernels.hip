@@ -556,6 +556,67 @@ __global__ __launch_bounds__(kBlock) void k_reduce_il(const RedArgs a) {
   }
 }
 
+// Vector path, small groups (PATH_VEC_ROW): F = 4*G4 channels with G4 = 1..64
+// float4 (F = 4 .. 256, e.g. the 0002 product's fqavby = 64), one float4
+// column per lane, one time block per tile.  A workgroup owns 1024
+// consecutive window channels (256 / G4 groups) of one (IF, time block,
+// bank); a workgroup-instruction reads 4 KiB contiguous, 8 rows are in flight
+// per lane, and each group folds over its G4 lanes with an xor butterfly
+// (groups never straddle a wave).  The lean sibling of k_reduce_vec for
+// these plans: 3-D grid, no 64-bit division, no time split.
+//   BLDP_VEC_ROW 1 (default) = use it where it applies; 0 = k_reduce_vec
+#ifndef BLDP_VEC_ROW
+#define BLDP_VEC_ROW 1
+#endif
+//   BLDP_ROW_MAXWAVES  cap on resident waves per SIMD for k_reduce_row (0 = none).
+//                  Default 4: fewer 4 KiB row streams per CU in flight is faster
+//                  on the 0002 shapes (A/B against uncapped / k_reduce_vec:
+//                  cfg1 5.85 vs 5.59 / 5.43 TB/s, cfg2 6.18 vs 5.78 / 6.10)
+#ifndef BLDP_ROW_MAXWAVES
+#define BLDP_ROW_MAXWAVES 4
+#endif
+template <int OP, int G4>
+__global__ __launch_bounds__(kBlock)
+#if BLDP_ROW_MAXWAVES > 0
+__attribute__((amdgpu_waves_per_eu(1, BLDP_ROW_MAXWAVES)))
+#endif
+void k_reduce_row(const RedArgs a) {
+  const int tid = threadIdx.x;
+  const uint32_t it = blockIdx.y, ni = (uint32_t)a.ni;
+  const uint32_t to = it / ni, i = it - to * ni;
+  const int bank = blockIdx.z;
+  const int64_t col = (int64_t)blockIdx.x * kBlock + tid;  // float4 column of the window
+  const bool valid = col < a.nco * G4;
+  const float id = R<OP>::id();
+  float4 acc[kNacc];
+#pragma unroll
+  for (int q = 0; q < kNacc; ++q) acc[q] = make_float4(id, id, id, id);
+  if (valid) {
+    const float *p = a.in[bank] + a.in_off + (int64_t)i * a.in_ld_i +
+                     (int64_t)to * a.T * a.in_ld_t + 4 * col;
+    const int64_t ld = a.in_ld_t;
+    int64_t nrows = a.T;
+    for (; nrows >= BLDP_BATCH; nrows -= BLDP_BATCH) {
+      float4 v[BLDP_BATCH];
+#pragma unroll
+      for (int u = 0; u < BLDP_BATCH; ++u) v[u] = ld4(p + u * ld);
+      p += BLDP_BATCH * ld;
+#pragma unroll
+      for (int u = 0; u < BLDP_BATCH; ++u) acc[u % kNacc] = f4<OP>(acc[u % kNacc], v[u]);
+    }
+    for (; nrows > 0; --nrows) {
+      acc[0] = f4<OP>(acc[0], ld4(p));
+      p += ld;
+    }
+  }
+  float s = fold4<OP>(fold_acc<OP>(acc));
+#pragma unroll
+  for (int off = G4 / 2; off > 0; off >>= 1) s = R<OP>::f(s, __shfl_xor(s, off, 64));
+  if (valid && (tid & (G4 - 1)) == 0)
+    a.out[bank * a.out_bank + (int64_t)i * a.out_ld_i + (int64_t)to * a.out_ld_t + col / G4] =
+        finish<OP>(s, a);
+}
+
 template <int OP, int F>
 __global__ __launch_bounds__(kBlock) void k_reduce_narrow(const RedArgs a) {
   for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) narrow_tile<OP, F>(a, t);
@@ -1102,6 +1163,20 @@ template <int OP>
 hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
   hipError_t e = hipSuccess;
   const dim3 grid((unsigned)p.grid), block(kBlock);
+  if (p.path == PATH_VEC_ROW) {
+    const dim3 g3((unsigned)a.blocks_c, (unsigned)(a.ni * a.nto), (unsigned)a.nbank);
+    switch (a.F / 4) {
+      case 1: hipLaunchKernelGGL((k_reduce_row<OP, 1>), g3, block, 0, s, a); break;
+      case 2: hipLaunchKernelGGL((k_reduce_row<OP, 2>), g3, block, 0, s, a); break;
+      case 4: hipLaunchKernelGGL((k_reduce_row<OP, 4>), g3, block, 0, s, a); break;
+      case 8: hipLaunchKernelGGL((k_reduce_row<OP, 8>), g3, block, 0, s, a); break;
+      case 16: hipLaunchKernelGGL((k_reduce_row<OP, 16>), g3, block, 0, s, a); break;
+      case 32: hipLaunchKernelGGL((k_reduce_row<OP, 32>), g3, block, 0, s, a); break;
+      case 64: hipLaunchKernelGGL((k_reduce_row<OP, 64>), g3, block, 0, s, a); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   if (p.path == PATH_VEC_IL) {
     const dim3 g3((unsigned)a.blocks_c, (unsigned)(a.ni * a.nto), (unsigned)a.nbank);
     switch (a.k4) {
@@ -1208,6 +1283,16 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, int num_cus) {
       cdiv(a.nco, BLDP_IL_GPW) <= INT32_MAX && a.ni * a.nto <= 65535 && a.nbank <= 65535) {
     p.path = PATH_VEC_IL;
     a.blocks_c = cdiv(a.nco, BLDP_IL_GPW);
+    a.ntiles = a.blocks_c * a.ni * a.nto * a.nbank;
+    p.grid = a.ntiles;
+  }
+  // small power-of-two groups, whole time block per tile, no time split:
+  // the lean row kernel (3-D grid, so every dimension must fit)
+  if (BLDP_VEC_ROW && p.path == PATH_VEC && a.k4 == 1 && a.ts == 1 && a.nchunk == 1 &&
+      F >= 4 && F <= 256 && (F & (F - 1)) == 0 && cdiv(a.nco * (F / 4), kBlock) <= INT32_MAX &&
+      a.ni * a.nto <= 65535 && a.nbank <= 65535) {
+    p.path = PATH_VEC_ROW;
+    a.blocks_c = cdiv(a.nco * (F / 4), kBlock);
     a.ntiles = a.blocks_c * a.ni * a.nto * a.nbank;
     p.grid = a.ntiles;
   }

@@ -105,9 +105,11 @@ def test_launch_plans_host_only(pkg, L):
     assert plan(pkg, L, A, 1 << 26, 1, 16, 4096, 16)[0] == 4
     assert plan(pkg, L, A, 1 << 26, 1, 16, 8192, 16)[0] == 0
     assert plan(pkg, L, A, 4096, 1, 4096, 1024, 4096)[0] == 0
-    # cfg1: F=64 -> 16 lanes per group
+    # cfg1: F=64 -> 16 lanes per group, one float4 each: the row kernel
     p = plan(pkg, L, A, 65536, 1, 279, 64, 16, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
-    assert p[0] == 0 and p[1] == 16 and p[3] == 1
+    assert p[0] == 5 and p[1] == 16 and p[3] == 1 and p[5] == 64 * 17
+    # too few tiles for one wave per tile: waves split time, generic kernel
+    assert plan(pkg, L, A, 4096, 1, 64, 64, 16)[0] == 0
     # cfg4: narrow channel, long time -> time split waves and/or chunks
     p = plan(pkg, L, A, 512, 1, 879616, 8, 1024)
     assert p[0] == 0 and p[1] == 2 and (p[2] > 1 or p[4] > 1)

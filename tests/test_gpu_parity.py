@@ -122,6 +122,26 @@ def test_reduce_interleaved_integer_exact(eng, orc, shape):
     assert same_bits(got, orc.stitch([orc.reduce(host(eng, b), F, T) for b in banks]))
 
 
+# Row kernel (F = 4..256, powers of two, one float4 column per lane): a
+# partial last 1024-channel segment, several IFs / time blocks / banks.
+ROW_SHAPES = [(1025, 1, 8, 4, 8), (600, 2, 12, 8, 4), (300, 1, 16, 16, 8), (150, 3, 6, 32, 2),
+              (65, 1, 24, 64, 8), (16384 + 3, 1, 32, 64, 16), (33, 2, 4, 128, 4), (17, 1, 8, 256, 8)]
+
+
+@pytest.mark.parametrize("shape", ROW_SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_reduce_row_integer_exact(eng, orc, shape):
+    nco, ni, nt, F, T = shape
+    x = eng.synth(nco * F, ni, nt, 1024, seed=nco + F, kind=1)  # integers 0..255
+    a = host(eng, x)
+    for op in ("sum", "max", "min", "mean"):
+        assert eng.plan(x, F, T, op)["path"] == "row", (shape, eng.plan(x, F, T, op))
+        got = host(eng, eng.reduce(x, F, T, op))
+        assert same_bits(got, orc.reduce(a, F, T, op)), (shape, op)  # F*T*255 < 2^24
+    banks = [x] + [eng.synth(nco * F, ni, nt, 1024, seed=b, kind=1) for b in (1, 2)]
+    got = host(eng, eng.band_reduce(banks, F, T))
+    assert same_bits(got, orc.stitch([orc.reduce(host(eng, b), F, T) for b in banks]))
+
+
 # Time integration (fqavby = 1, the narrow kernel): partial last segments,
 # several IFs / time blocks / banks, every op, a time-offset window.
 TIME_SHAPES = [(4100, 1, 32, 16), (4096, 3, 40, 5), (1 << 20, 2, 48, 16), (1 << 23, 1, 16, 16),

@@ -35,6 +35,8 @@ VARIANTS = {
     # k_reduce_vec instead of the interleaved k_reduce_il for F = 512..4096
     "noil": "-DBLDP_VEC_IL=0",
     "gpw4": "-DBLDP_IL_GPW=4",
+    "norow": "-DBLDP_VEC_ROW=0",
+    "rownocap": "-DBLDP_ROW_MAXWAVES=0",
     # narrow windows: time split over otherwise idle waves, with / without grid cap
     "notsfill": "-DBLDP_TS_FILL=0",
 
