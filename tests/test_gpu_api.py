@@ -281,3 +281,17 @@ def torch_f32():
     import torch
 
     return torch.float32
+
+
+def test_c_abi_demo_binary():
+    """examples/c_abi_demo.c: the ABI driven from plain C (host arrays,
+    windows, int codes, bldp_last_error), as a Julia ccall drives it."""
+    import subprocess
+
+    from conftest import REPO
+
+    exe = os.path.join(REPO, "build", "c_abi_demo")
+    assert os.path.exists(exe), "run __graft_entry__.build() first"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "all checks passed" in r.stdout
