@@ -625,8 +625,19 @@ template <int OP>
 __global__ __launch_bounds__(kBlock) void k_reduce_scalar(const RedArgs a) {
   for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) scalar_tile<OP>(a, t);
 }
+//   BLDP_TILE_MAXWAVES  cap on resident waves per SIMD for k_reduce_tile (0 = none).
+//                  Default 3 (A/B against uncapped, 5 waves: +0.6 to +4.6% on the
+//                  misaligned / odd-F windows; 2 is better on 0000-sized windows
+//                  but 2.6% worse on a misaligned 0002 band)
+#ifndef BLDP_TILE_MAXWAVES
+#define BLDP_TILE_MAXWAVES 3
+#endif
 template <int OP, bool CS1>
-__global__ __launch_bounds__(kBlock) void k_reduce_tile(const RedArgs a) {
+__global__ __launch_bounds__(kBlock)
+#if BLDP_TILE_MAXWAVES > 0
+__attribute__((amdgpu_waves_per_eu(1, BLDP_TILE_MAXWAVES)))
+#endif
+void k_reduce_tile(const RedArgs a) {
   for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) tile_tile<OP, CS1>(a, t);
 }
 

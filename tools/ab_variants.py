@@ -36,6 +36,7 @@ VARIANTS = {
     "noil": "-DBLDP_VEC_IL=0",
     "gpw4": "-DBLDP_IL_GPW=4",
     "norow": "-DBLDP_VEC_ROW=0",
+    "tilenocap": "-DBLDP_TILE_MAXWAVES=0",
     "rownocap": "-DBLDP_ROW_MAXWAVES=0",
     # narrow windows: time split over otherwise idle waves, with / without grid cap
     "notsfill": "-DBLDP_TS_FILL=0",

@@ -65,7 +65,7 @@ for s in $STEPS; do
              --steps 10 --warmup 3 --config cfg2 ;;
     ab)    run ab 900 python tools/ab_variants.py --run --variants "${AB_VARIANTS:-base,noil}" --json "$OUT/ab.json" ;;
     ab_kurt) run ab_kurt 900 python tools/ab_variants.py --run --suite kurt --variants ${AB_VARIANTS:-base,kold,kw5,kw6} --json "$OUT/ab_kurt.json" ;;
-    ab_tile) run ab_tile 900 python tools/ab_variants.py --run --suite tile --variants base,tk4a1,tk2a1,tk2a2 --json "$OUT/ab_tile.json" ;;
+    ab_tile) run ab_tile 900 python tools/ab_variants.py --run --suite tile --variants "${AB_VARIANTS:-base,tk4a1,tk2a1,tk2a2}" --json "$OUT/ab_tile.json" ;;
   esac
 done
 echo "== session done"
