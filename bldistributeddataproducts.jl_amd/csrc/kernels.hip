@@ -730,8 +730,18 @@ __global__ __launch_bounds__(kBlock) void k_despike(float *d, int64_t nchan, int
 // partials through LDS in wave order.  With one time chunk the epilogue is
 // fused (pass 0 writes the mean, pass 1 the kurtosis); otherwise chunks are
 // folded in a fixed order by k_kurt_fold.
+//   BLDP_KURT_PASS_MAXWAVES  cap on resident waves per SIMD for k_kurt_pass (0 = none).
+//                  Default 4: +1.1..1.2% on long windows (0001 band, 2048
+//                  spectra) against uncapped 5-6 waves; 3 loses 10%
+#ifndef BLDP_KURT_PASS_MAXWAVES
+#define BLDP_KURT_PASS_MAXWAVES 4
+#endif
 template <int PASS, int VEC>
-__global__ __launch_bounds__(kBlock) void k_kurt_pass(const KurtArgs k) {
+__global__ __launch_bounds__(kBlock)
+#if BLDP_KURT_PASS_MAXWAVES > 0
+__attribute__((amdgpu_waves_per_eu(1, BLDP_KURT_PASS_MAXWAVES)))
+#endif
+void k_kurt_pass(const KurtArgs k) {
   constexpr int W = VEC ? 4 : 1;              // channels per lane
   constexpr int NA = PASS == 0 ? W : 2 * W;   // Float64 accumulators per lane
   constexpr int B = 8;                        // spectra in flight per lane

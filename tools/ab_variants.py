@@ -37,6 +37,7 @@ VARIANTS = {
     "gpw4": "-DBLDP_IL_GPW=4",
     "norow": "-DBLDP_VEC_ROW=0",
     "tilenocap": "-DBLDP_TILE_MAXWAVES=0",
+    "kpnocap": "-DBLDP_KURT_PASS_MAXWAVES=0",
     "rownocap": "-DBLDP_ROW_MAXWAVES=0",
     # narrow windows: time split over otherwise idle waves, with / without grid cap
     "notsfill": "-DBLDP_TS_FILL=0",
@@ -125,6 +126,11 @@ def run(names, rounds, iters, suite="main"):
         kurt_case("kurt cfg3 nt12", b3, [0, 1 << 26, 1, 0, 1, 1, 0, 12, 1])
         b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
         kurt_case("kurt cfg2 nt272", b2, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
+        del b3
+        b4 = [eng.synth(512, 1, 880000, 8, seed=10 * b + 1, kind=0) for b in range(8)]
+        kurt_case("kurt cfg4 nt879616", b4, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
+        b5 = [eng.synth(65536, 1, 2048, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
+        kurt_case("kurt 65536ch nt2048", b5)
         cases_done = True
     elif suite == "tile":  # tile path: misaligned starts and odd F at cfg3 scale
         n = 1 << 26
