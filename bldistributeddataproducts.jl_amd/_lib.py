@@ -18,6 +18,8 @@ OPS = {"sum": 0, "mean": 1, "max": 2, "min": 3}
 PATHS = {0: "vector", 1: "narrow", 2: "scalar", 3: "tile", 4: "interleaved", 5: "row"}
 
 BLDP_OK, BLDP_EINVAL, BLDP_EDIM, BLDP_EHIP, BLDP_ENOMEM, BLDP_EBOUNDS = 0, -1, -2, -3, -5, -6
+BLDP_ECOMM = -7
+BLDP_COMM_ID_BYTES = 128
 
 
 class BLDPError(RuntimeError):
@@ -71,6 +73,10 @@ SIGNATURES = {
     "bldp_unchunk_f32": ([P, P, P, P, P, P, P], I),
     "bldp_bslz4_decode_host": ([P, SZ, I, P, SZ], I),
     "bldp_bslz4_decode_dev": ([I, P, P, P, P, I, P, P, P], I),
+    "bldp_comm_id": ([P], I),
+    "bldp_comm_init": ([I, I, I, P, P], I),
+    "bldp_comm_destroy": ([P], I),
+    "bldp_band_gather_f32": ([P, I, P, I64, P, P], I),
 }
 
 _lib = None

@@ -169,3 +169,67 @@ class BandPipeline:
             if w is not None:
                 w.wait()
                 self._work[s] = None
+
+
+class NativeBand:
+    """The band exchange through the C ABI alone (bldp_comm_* +
+    bldp_band_gather_f32: RCCL ncclGather over xGMI), the path a host without
+    torch -- a Julia Distributed.jl worker per GPU -- takes.  ``id_bytes``
+    (128) comes from ``NativeBand.new_id()`` on one rank and is passed to every
+    rank by the host's own means.  Construction is collective."""
+
+    def __init__(self, device, nranks, rank, id_bytes):
+        import ctypes
+
+        from . import _lib
+
+        self.L = _lib.lib()
+        self.nranks, self.rank = int(nranks), int(rank)
+        self.device = int(device)
+        idb = (ctypes.c_uint8 * _lib.BLDP_COMM_ID_BYTES).from_buffer_copy(bytes(id_bytes))
+        h = ctypes.c_void_p()
+        _lib.check(self.L.bldp_comm_init(self.device, self.nranks, self.rank, idb,
+                                         ctypes.byref(h)), "bldp_comm_init")
+        self.handle = h
+
+    @staticmethod
+    def new_id() -> bytes:
+        import ctypes
+
+        from . import _lib
+
+        buf = (ctypes.c_uint8 * _lib.BLDP_COMM_ID_BYTES)()
+        _lib.check(_lib.lib().bldp_comm_id(buf), "bldp_comm_id")
+        return bytes(buf)
+
+    def gather(self, local, root=0, stream=None):
+        """``local``: this rank's Julia-order (ncl, ni, nto) slice, dense.
+        Returns the stitched band on the root (a new tensor), None elsewhere."""
+        import torch
+
+        from . import _lib, engine
+
+        ncl, ni, nto = (int(x) for x in local.shape)
+        block = local.permute(2, 1, 0)
+        if not block.is_contiguous():
+            raise ValueError("local slice must be a dense Julia-order tensor")
+        g = None
+        if self.rank == root:
+            g = torch.empty((self.nranks, nto, ni, ncl), dtype=torch.float32,
+                            device=local.device)
+        _lib.check(self.L.bldp_band_gather_f32(self.handle, int(root), block.data_ptr(),
+                                               ncl * ni * nto, g.data_ptr() if g is not None
+                                               else None, _lib.stream_ptr(stream)),
+                   "bldp_band_gather_f32")
+        if g is None:
+            return None
+        if ni * nto == 1:
+            return g.reshape(self.nranks * ncl, 1, 1)
+        return engine.stitch(g, self.nranks, stream=stream)
+
+    def close(self):
+        if self.handle:
+            from . import _lib
+
+            _lib.check(self.L.bldp_comm_destroy(self.handle), "bldp_comm_destroy")
+            self.handle = None

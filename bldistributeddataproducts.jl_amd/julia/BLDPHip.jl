@@ -11,7 +11,8 @@ module BLDPHip
 
 using Statistics: mean
 
-export gpu_init, gpu_finalize, gpu_pin, gpu_unpin, gpu_fqav, gpu_reduce, gpu_kurtosis, gpu_band
+export gpu_init, gpu_finalize, gpu_pin, gpu_unpin, gpu_fqav, gpu_reduce, gpu_kurtosis, gpu_band,
+       gpu_comm_id, gpu_comm_init, gpu_comm_destroy, gpu_band_gather
 
 const libbldp = get(ENV, "BLDP_LIB", joinpath(@__DIR__, "..", "libbldp_hip.so"))
 
@@ -140,5 +141,42 @@ end
 `reduce(vcat, parts)` of per-bank results in bank order (src/gbt.jl:103):
 what `GBT.getband` returns after `fetch.(futures)`."""
 gpu_band(parts) = reduce(vcat, parts)
+
+# ---------------------------------------------------------------------------
+# Band stitch across worker processes, one GPU each, over RCCL (xGMI): the
+# device-side replacement of GBT.getdata's fetch of every worker's result
+# (src/gbt.jl:75-78).  The 128-byte id travels between workers through
+# Distributed (e.g. `remotecall_fetch(gpu_comm_id, first(workers))`).
+
+"RCCL unique id for a new band communicator (call on one worker)."
+function gpu_comm_id()
+    id = zeros(UInt8, 128)
+    check(ccall((:bldp_comm_id, libbldp), Cint, (Ptr{UInt8},), id))
+    id
+end
+
+"Join the band communicator (collective over all `nranks` workers)."
+function gpu_comm_init(id::Vector{UInt8}, nranks::Integer, rank::Integer; dev::Integer=0)
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    check(ccall((:bldp_comm_init, libbldp), Cint, (Cint, Cint, Cint, Ptr{UInt8}, Ptr{Ptr{Cvoid}}),
+                dev, nranks, rank, id, h))
+    h[]
+end
+
+gpu_comm_destroy(comm::Ptr{Cvoid}) =
+    (check(ccall((:bldp_comm_destroy, libbldp), Cint, (Ptr{Cvoid},), comm)); nothing)
+
+"""
+    gpu_band_gather(comm, slice::Ptr{Float32}, count, gathered::Ptr{Float32}; root=0, stream=C_NULL)
+
+ncclGather of every worker's reduced slice (a device buffer of `count`
+Float32, its banks in vcat order) into `gathered` (nranks*count) on `root`,
+rank-major; then `bldp_stitch_f32` when the product has more than one
+(IF, time) row.  Device pointers; asynchronous on `stream`."""
+gpu_band_gather(comm::Ptr{Cvoid}, slice::Ptr{Float32}, count::Integer, gathered::Ptr{Float32};
+                root::Integer=0, stream::Ptr{Cvoid}=C_NULL) =
+    (check(ccall((:bldp_band_gather_f32, libbldp), Cint,
+                 (Ptr{Cvoid}, Cint, Ptr{Float32}, Int64, Ptr{Float32}, Ptr{Cvoid}),
+                 comm, root, slice, count, gathered, stream)); nothing)
 
 end # module

@@ -15,6 +15,8 @@
  *                          resident on one GPU.
  *   bldp_stitch_f32        reduce(vcat, banks) (src/gbt.jl:103) of bank-major
  *                          gathered blocks.
+ *   bldp_comm_* /          GBT.getdata's fetch of every worker's result to the
+ *   bldp_band_gather_f32   caller (src/gbt.jl:75-78) as an RCCL gather over xGMI.
  *   bldp_despike_f32       d[spike:nfpc:end,:,:] .= d[spike-1:nfpc:end,:,:]
  *                          (src/gbt.jl:101-102,111).
  *   bldp_kurtosis_f32      getkurtosis (src/gbtworkerfunctions.jl:197-202) with
@@ -66,6 +68,7 @@ enum bldp_op { BLDP_OP_SUM = 0, BLDP_OP_MEAN = 1, BLDP_OP_MAX = 2, BLDP_OP_MIN =
 #define BLDP_EHIP (-3)    /* HIP runtime error                                   */
 #define BLDP_ENOMEM (-5)  /* device or pinned allocation failed                  */
 #define BLDP_EBOUNDS (-6) /* window outside the array (BoundsError analogue)     */
+#define BLDP_ECOMM (-7)   /* RCCL error in the cross-GPU band exchange          */
 
 #define BLDP_MAX_BANKS 64
 
@@ -142,6 +145,24 @@ BLDP_API int bldp_band_reduce_multi_f32(int nbank, const int *bank_dev, const fl
                                         int64_t nchan, int64_t nif, int64_t ntime,
                                         const int64_t *win, int64_t fqavby, int64_t tavby,
                                         int op, int root, float *out);
+
+/* Band stitch across processes, one GPU each (the reference's one
+ * Distributed.jl worker per bank, src/gbt.jl:75-77): an RCCL communicator
+ * and ncclGather over xGMI (RCCL is loaded at run time).
+ *   rank 0: bldp_comm_id(id), sends the 128 bytes to every rank;
+ *   every rank: bldp_comm_init (collective), reduces its banks into a dense
+ *   slice with bldp_band_reduce_f32, then bldp_band_gather_f32: the root's
+ *   `gathered` receives nranks slices of `count` floats, rank-major;
+ *   root: bldp_stitch_f32(nranks, gathered, ...) puts rank-major slices in
+ *   vcat order (no-op layout when every bank's output is one (IF, time) row).
+ * The gather is asynchronous on `stream`. */
+#define BLDP_COMM_ID_BYTES 128
+BLDP_API int bldp_comm_id(uint8_t id[BLDP_COMM_ID_BYTES]);
+BLDP_API int bldp_comm_init(int dev, int nranks, int rank, const uint8_t id[BLDP_COMM_ID_BYTES],
+                            void **comm);
+BLDP_API int bldp_comm_destroy(void *comm);
+BLDP_API int bldp_band_gather_f32(void *comm, int root, const float *slice, int64_t count,
+                                  float *gathered, void *stream);
 
 /* gathered: nbank dense blocks (nc, nif, ntime) back to back (bank-major,
  * what a gather to the root leaves); out: (nbank*nc, nif, ntime) = vcat. */

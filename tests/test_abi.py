@@ -152,3 +152,19 @@ def test_despike_and_stitch_argument_checks(pkg, L):
     buf = np.zeros(16, np.float32)
     assert L.bldp_stitch_f32(2, buf.ctypes.data, 4, 2, 1, buf.ctypes.data, None) == \
         pkg._lib.BLDP_EINVAL
+
+
+def test_native_comm_host_checks(pkg, L):
+    """bldp_comm_*: an RCCL unique id is made on the host; the argument
+    checks answer without a GPU (the cross-GPU band stitch
+    through the C ABI)."""
+    import ctypes
+
+    nid = pkg.band.NativeBand.new_id()
+    assert len(nid) == pkg._lib.BLDP_COMM_ID_BYTES and any(nid)
+    assert L.bldp_comm_id(None) == pkg._lib.BLDP_EINVAL
+    assert L.bldp_band_gather_f32(None, 0, None, 4, None, None) == pkg._lib.BLDP_EINVAL
+    assert "communicator" in pkg._lib.last_error()
+    assert L.bldp_comm_destroy(None) == pkg._lib.BLDP_OK
+    h = ctypes.c_void_p()
+    assert L.bldp_comm_init(0, 2, 2, None, ctypes.byref(h)) == pkg._lib.BLDP_EINVAL

@@ -295,3 +295,22 @@ def test_c_abi_demo_binary():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "all checks passed" in r.stdout
+
+
+def test_native_band_gather_world1(pkg, orc):
+    """The C-ABI band exchange (bldp_comm_* + bldp_band_gather_f32, RCCL
+    ncclGather) on a one-rank communicator: the gathered band equals the
+    rank's slice, single-row and multi-row (stitch) outputs."""
+    import torch
+
+    eng = pkg.engine
+    nb = pkg.band.NativeBand(0, 1, 0, pkg.band.NativeBand.new_id())
+    try:
+        for ni, F, T in ((1, 1024, 32), (2, 1024, 32), (2, 64, 8)):
+            banks = [eng.synth(4096, ni, 32, 64, seed=b, kind=1) for b in range(3)]
+            local = eng.band_reduce(banks, F, T)
+            got = nb.gather(local)
+            torch.cuda.synchronize()
+            assert same_bits(eng.fb_to_numpy(got), eng.fb_to_numpy(local))
+    finally:
+        nb.close()
