@@ -477,13 +477,19 @@ __global__ __launch_bounds__(kBlock) void k_reduce_vec(const RedArgs a) {
 #ifndef BLDP_IL_GPW
 #define BLDP_IL_GPW 2
 #endif
+//   BLDP_IL_INFLIGHT  16-byte loads a lane issues per batch (power of two); 4
+//                  measured +0.1..0.7% against 8 on 1-, 2- and 8-bank launches
+#ifndef BLDP_IL_INFLIGHT
+#define BLDP_IL_INFLIGHT 4
+#endif
 template <int OP, int K4, int GPW>
 __global__ __launch_bounds__(kBlock) void k_reduce_il(const RedArgs a) {
   constexpr int NI = GPW * K4 / 4;           // loads per lane per row
   constexpr int PER = K4 < 4 ? 1 : K4 / 4;   // consecutive loads of one group slot
   constexpr int NS = NI / PER;               // group slots per lane
-  constexpr int RB = NI < 8 ? 8 / NI : 1;    // rows in flight
-  constexpr int JB = NI < 8 ? NI : 8;        // loads per batch within a row
+  constexpr int IF = BLDP_IL_INFLIGHT;       // loads in flight per lane
+  constexpr int RB = NI < IF ? IF / NI : 1;  // rows in flight
+  constexpr int JB = NI < IF ? NI : IF;      // loads per batch within a row
   static_assert(NI >= 1 && NI % PER == 0, "k_reduce_il: GPW * K4 must be a multiple of 4");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t it = blockIdx.y, ni = (uint32_t)a.ni;

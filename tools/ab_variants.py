@@ -35,6 +35,7 @@ VARIANTS = {
     # k_reduce_vec instead of the interleaved k_reduce_il for F = 512..4096
     "noil": "-DBLDP_VEC_IL=0",
     "gpw4": "-DBLDP_IL_GPW=4",
+    "ilb8": "-DBLDP_IL_INFLIGHT=8",
     "norow": "-DBLDP_VEC_ROW=0",
     "tilenocap": "-DBLDP_TILE_MAXWAVES=0",
     "kpnocap": "-DBLDP_KURT_PASS_MAXWAVES=0",
