@@ -574,6 +574,12 @@ __global__ __launch_bounds__(kBlock) void k_reduce_il(const RedArgs a) {
 #ifndef BLDP_VEC_ROW
 #define BLDP_VEC_ROW 1
 #endif
+//   BLDP_ROW_BATCH rows in flight per lane in k_reduce_row.  16 (default):
+//                  +2.6% / +3.2% on the 0002 band / bank against 8, -0.4% on
+//                  0000 F=64, -1.7% on 0001 F=64
+#ifndef BLDP_ROW_BATCH
+#define BLDP_ROW_BATCH 16
+#endif
 //   BLDP_ROW_MAXWAVES  cap on resident waves per SIMD for k_reduce_row (0 = none).
 //                  Default 4: fewer 4 KiB row streams per CU in flight is faster
 //                  on the 0002 shapes (A/B against uncapped / k_reduce_vec:
@@ -602,13 +608,13 @@ void k_reduce_row(const RedArgs a) {
                      (int64_t)to * a.T * a.in_ld_t + 4 * col;
     const int64_t ld = a.in_ld_t;
     int64_t nrows = a.T;
-    for (; nrows >= BLDP_BATCH; nrows -= BLDP_BATCH) {
-      float4 v[BLDP_BATCH];
+    for (; nrows >= BLDP_ROW_BATCH; nrows -= BLDP_ROW_BATCH) {
+      float4 v[BLDP_ROW_BATCH];
 #pragma unroll
-      for (int u = 0; u < BLDP_BATCH; ++u) v[u] = ld4(p + u * ld);
-      p += BLDP_BATCH * ld;
+      for (int u = 0; u < BLDP_ROW_BATCH; ++u) v[u] = ld4(p + u * ld);
+      p += BLDP_ROW_BATCH * ld;
 #pragma unroll
-      for (int u = 0; u < BLDP_BATCH; ++u) acc[u % kNacc] = f4<OP>(acc[u % kNacc], v[u]);
+      for (int u = 0; u < BLDP_ROW_BATCH; ++u) acc[u % kNacc] = f4<OP>(acc[u % kNacc], v[u]);
     }
     for (; nrows > 0; --nrows) {
       acc[0] = f4<OP>(acc[0], ld4(p));

@@ -36,6 +36,9 @@ VARIANTS = {
     "noil": "-DBLDP_VEC_IL=0",
     "gpw4": "-DBLDP_IL_GPW=4",
     "ilb8": "-DBLDP_IL_INFLIGHT=8",
+    "batch4": "-DBLDP_BATCH=4",
+    "batch16": "-DBLDP_BATCH=16",
+    "rowb8": "-DBLDP_ROW_BATCH=8",
     "norow": "-DBLDP_VEC_ROW=0",
     "tilenocap": "-DBLDP_TILE_MAXWAVES=0",
     "kpnocap": "-DBLDP_KURT_PASS_MAXWAVES=0",
