@@ -8,7 +8,7 @@ of include/bldp.h; this package is the Python host side over that ABI.
 The directory name is not a Python identifier; load it with
 ``__graft_entry__.load_package()`` (registers it as ``bldp_amd``).
 """
-from . import _lib, band, engine, fbh5, filestream, gbt, idxs, readers, worker  # noqa: F401
+from . import _lib, band, engine, fbh5, filestream, gbt, h5chunks, idxs, readers, worker  # noqa: F401
 from ._lib import ArgumentError, BLDPError, BoundsError, DimensionMismatch  # noqa: F401
 from .idxs import COLON, JRange, sanitizeidxs  # noqa: F401
 from .worker import FRange, fqav  # noqa: F401

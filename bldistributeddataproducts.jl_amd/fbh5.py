@@ -99,6 +99,9 @@ class _H5:
             "H5Zfilter_avail": ([ctypes.c_int], ctypes.c_int),
             "H5Dget_chunk_storage_size": ([hid_t, ctypes.c_void_p, ctypes.c_void_p], herr_t),
             "H5Dget_offset": ([hid_t], ctypes.c_uint64),
+            "H5Oget_info2": ([hid_t, ctypes.c_void_p, ctypes.c_uint], herr_t),
+            "H5Dget_chunk_info_by_coord": ([hid_t, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_void_p], herr_t),
             "H5Tget_order": ([hid_t], ctypes.c_int),
             "H5Dread_chunk": ([hid_t, hid_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p],
                               herr_t),
@@ -661,14 +664,14 @@ def _chunk_sizes(H, d, chunk, kt0, ki0, kc0, grid):
 
 def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 20):
     """Device path of a compressed window, overlapped in three stages: a
-    reader thread (the only libhdf5 user while it runs) reads batches of
-    stored chunks with H5Dread_chunk straight into pinned memory and queues
-    their H2D copy on a copy stream, while this thread decodes the previous
-    batch on the GPU (bldp_bslz4_decode_dev); then the window is gathered
-    (bldp_unchunk_f32).  Only compressed bytes cross PCIe.  ``timings`` (a
-    dict) receives stage times."""
+    reader thread reads batches of stored chunks straight into pinned memory
+    and queues their H2D copy on a copy stream, while this thread decodes the
+    previous batch on the GPU (bldp_bslz4_decode_dev); then the window is
+    gathered (bldp_unchunk_f32).  Only compressed bytes cross PCIe.  The
+    chunks are read by parallel preads at the offsets of the chunk index
+    parsed from the file (h5chunks.py), or, outside that parser's scope, one
+    H5Dread_chunk at a time.  ``timings`` (a dict) receives stage times."""
     import time
-    from concurrent.futures import ThreadPoolExecutor
 
     import torch
 
@@ -701,10 +704,26 @@ def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 
     try:
         d = _ok(H.H5Dopen2(f, b"data", H5P_DEFAULT), "open dataset 'data'")
         try:
-            coords, sizes = _chunk_sizes(H, d, chunk, kt0, ki0, kc0, grid)
+            from . import h5chunks
+
+            tab = h5chunks.chunk_table(fname, H, d)  # parsed chunk B-tree, or None
+            if tab is not None:
+                coords, sizes, faddr, masks = [], [], [], []
+                for a in range(gt):
+                    for b in range(gi):
+                        for c in range(gc):
+                            key = ((kt0 + a) * chunk[0], (ki0 + b) * chunk[1],
+                                   (kc0 + c) * chunk[2])
+                            ent = tab["index"].get(key, (0, 0, 0))  # absent: fill (0)
+                            coords.append(key)
+                            faddr.append(ent[0])
+                            sizes.append(ent[1])
+                            masks.append(ent[2])
+            else:
+                coords, sizes = _chunk_sizes(H, d, chunk, kt0, ki0, kc0, grid)
+                masks = [0] * len(sizes)
             offsets = [0] + [int(x) for x in np.cumsum(sizes[:-1])]
             total = int(sum(sizes))
-            masks = [0] * len(sizes)
             pinned = torch.empty(total + 16, dtype=torch.uint8, pin_memory=True)
             host = pinned.numpy()
             batches, cur, acc = [], [], 0
@@ -721,14 +740,55 @@ def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 
                 packed = torch.zeros(len(sizes) * cvol, dtype=torch.float32, device=dev)
                 copy_stream = torch.cuda.Stream(dev)
 
+                hostmv = memoryview(host)
+                if tab is not None:
+                    from . import filestream
+
+                    pool = filestream._ring(dev).pool
+                    fd = os.open(fname, os.O_RDONLY)
+
                 def stage(ks):  # reader thread: file -> pinned -> (async) device
-                    m = ctypes.c_uint32()
-                    for k in ks:
-                        if sizes[k]:
-                            _ok(H.H5Dread_chunk(d, H5P_DEFAULT, coords[k], ctypes.byref(m),
-                                                ctypes.c_void_p(pinned.data_ptr() + offsets[k])),
-                                "read_chunk")
-                            masks[k] = m.value
+                    if tab is not None:  # parallel preads at the parsed chunk offsets
+                        # chunks adjacent in the file and in the batch merge into
+                        # runs; runs split into pieces of <= PIECE_BYTES (one
+                        # pool task each: per-chunk tasks are GIL-bound)
+                        runs = []
+                        for k in ks:
+                            if not sizes[k]:
+                                continue
+                            if runs and runs[-1][0] + runs[-1][2] == faddr[k] and \
+                                    runs[-1][1] + runs[-1][2] == offsets[k]:
+                                runs[-1][2] += sizes[k]
+                            else:
+                                runs.append([faddr[k], offsets[k], sizes[k]])
+                        tasks, cur, cur_n = [], [], 0  # preads grouped ~PIECE_BYTES a task
+                        for fo, do, n in runs:
+                            for q in range(0, n, filestream.PIECE_BYTES):
+                                m = min(filestream.PIECE_BYTES, n - q)
+                                cur.append((fo + q, do + q, m))
+                                cur_n += m
+                                if cur_n >= filestream.PIECE_BYTES:
+                                    tasks.append(cur)
+                                    cur, cur_n = [], 0
+                        if cur:
+                            tasks.append(cur)
+
+                        def read_task(task):
+                            for fo, do, n in task:
+                                filestream._pread_into(fd, hostmv[do:do + n], fo)
+                        futs = [pool.submit(read_task, t) for t in tasks]
+                        for fu in futs:
+                            fu.result()
+                    else:  # libhdf5, one chunk at a time
+                        m = ctypes.c_uint32()
+                        for k in ks:
+                            if sizes[k]:
+                                _ok(H.H5Dread_chunk(d, H5P_DEFAULT, _hs(coords[k]),
+                                                    ctypes.byref(m),
+                                                    ctypes.c_void_p(pinned.data_ptr() +
+                                                                    offsets[k])),
+                                    "read_chunk")
+                                masks[k] = m.value
                     lo, hi = offsets[ks[0]], offsets[ks[-1]] + sizes[ks[-1]]
                     with torch.cuda.device(dev):
                         ev = torch.cuda.Event()
@@ -739,33 +799,59 @@ def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 
                     return ev
 
                 t_io = t_dec = 0.0
-                with ThreadPoolExecutor(max_workers=1) as reader:
-                    futs = [reader.submit(stage, ks) for ks in batches]  # reads run ahead
-                    cur_stream = torch.cuda.current_stream()
-                    for b, ks in enumerate(batches):
-                        tw = time.perf_counter()
-                        cur_stream.wait_event(futs[b].result())
-                        t_io += time.perf_counter() - tw
-                        td = time.perf_counter()
-                        for k in ks:  # stored without the filter: raw elements
-                            if sizes[k] and masks[k] & 1:
-                                packed.view(torch.uint8)[4 * k * cvol:4 * (k + 1) * cvol].copy_(
-                                    cdev[offsets[k]:offsets[k] + 4 * cvol])
-                        comp = [k for k in ks if sizes[k] and not masks[k] & 1]
-                        if comp:
-                            offs = np.array([offsets[k] for k in comp], np.uint64)
-                            lens = np.array([sizes[k] for k in comp], np.uint64)
-                            ooff = np.array([4 * k * cvol for k in comp], np.uint64)
-                            rc = _lib.lib().bldp_bslz4_decode_dev(
-                                len(comp), host.ctypes.data, cdev.data_ptr(), offs.ctypes.data,
-                                lens.ctypes.data, 4, packed.data_ptr(), ooff.ctypes.data,
-                                _lib.stream_ptr())
-                            _lib.check(rc, "bldp_bslz4_decode_dev")
-                        t_dec += time.perf_counter() - td
+                try:
+                    t_dec, t_io = _decode_batches(
+                        batches, stage, sizes, masks, offsets, cvol, packed, cdev, host, _lib,
+                        torch)
+                finally:
+                    if tab is not None:
+                        os.close(fd)
         finally:
             H.H5Dclose(d)
     finally:
         H.H5Fclose(f)
+    return _unchunk_out(dev, torch, engine, _lib, nc, ni, nt, chunk, box0, grid, win, packed,
+                        timings, t0, t_io, t_dec, batches, total, tab is not None)
+
+
+def _decode_batches(batches, stage, sizes, masks, offsets, cvol, packed, cdev, host, _lib,
+                    torch):
+    """A reader thread runs ``stage`` over the batches ahead of this thread,
+    which decodes each batch on the GPU as soon as its copy has landed.
+    Returns (decode seconds, seconds waited for reads)."""
+    import time
+    from concurrent.futures import ThreadPoolExecutor
+
+    t_io = t_dec = 0.0
+    with ThreadPoolExecutor(max_workers=1) as reader:
+        futs = [reader.submit(stage, ks) for ks in batches]  # reads run ahead
+        cur_stream = torch.cuda.current_stream()
+        for b, ks in enumerate(batches):
+            tw = time.perf_counter()
+            cur_stream.wait_event(futs[b].result())
+            t_io += time.perf_counter() - tw
+            td = time.perf_counter()
+            for k in ks:  # stored without the filter: raw elements
+                if sizes[k] and masks[k] & 1:
+                    packed.view(torch.uint8)[4 * k * cvol:4 * (k + 1) * cvol].copy_(
+                        cdev[offsets[k]:offsets[k] + 4 * cvol])
+            comp = [k for k in ks if sizes[k] and not masks[k] & 1]
+            if comp:
+                offs = np.array([offsets[k] for k in comp], np.uint64)
+                lens = np.array([sizes[k] for k in comp], np.uint64)
+                ooff = np.array([4 * k * cvol for k in comp], np.uint64)
+                rc = _lib.lib().bldp_bslz4_decode_dev(
+                    len(comp), host.ctypes.data, cdev.data_ptr(), offs.ctypes.data,
+                    lens.ctypes.data, 4, packed.data_ptr(), ooff.ctypes.data, _lib.stream_ptr())
+                _lib.check(rc, "bldp_bslz4_decode_dev")
+            t_dec += time.perf_counter() - td
+    return t_dec, t_io
+
+
+def _unchunk_out(dev, torch, engine, _lib, nc, ni, nt, chunk, box0, grid, win, packed, timings,
+                 t0, t_io, t_dec, batches, total, parsed_index):
+    import time
+
     with torch.cuda.device(dev):
         out = engine.fb_empty(nc, ni, nt, device=dev)
         if out.numel():
@@ -777,7 +863,8 @@ def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 
         if timings is not None:
             torch.cuda.synchronize()
             timings.update(total_s=time.perf_counter() - t0, wait_io_s=t_io, decode_s=t_dec,
-                           batches=len(batches), compressed_bytes=total)
+                           batches=len(batches), compressed_bytes=total,
+                           parsed_chunk_index=parsed_index)
     return out
 
 

@@ -155,13 +155,23 @@ def test_bslz4_gpu_rejects_corrupt_blocks(pkg):
     assert np.array_equal(out.cpu().numpy(), z["raw_int_runs_b512"].ravel())
 
 
-def test_fbh5_bslz4_on_gpu_end_to_end(pkg, orc, tmp_path):
+@pytest.mark.parametrize("parsed_index", [True, False])
+def test_fbh5_bslz4_on_gpu_end_to_end(pkg, orc, tmp_path, monkeypatch, parsed_index):
+    """Compressed FBH5 through the GPU decoder; chunks read by parallel preads
+    at the parsed chunk index, and (parsed_index=False) one H5Dread_chunk at a
+    time, as for files outside the parser's scope."""
     J, C = pkg.JRange, pkg.COLON
     d = np.asfortranarray(np.random.default_rng(8).integers(0, 256, (4096, 2, 40))
                           .astype(np.float32))
     p = tmp_path / "blc00_guppi_59000_12345_HIP1234_0011.rawspec.0002.h5"
     pkg.fbh5.write_bslz4(p, dict(foff=-0.002861, nfpc=1024), d, (16, 1, 1024),
                          lambda blk: orc.np_bslz4_encode(blk, 2048))
+    if not parsed_index:
+        monkeypatch.setattr(pkg.h5chunks, "chunk_table", lambda *a, **k: None)
+    tm = {}
+    x = pkg.fbh5._read_window_bslz4_dev(p, (C, C, C), "cuda:0", timings=tm)
+    assert tm["parsed_chunk_index"] is parsed_index
+    assert same_bits(pkg.engine.fb_to_numpy(x), d)
     x = pkg.fbh5.read_window_bslz4(p, (J(1025, 3072), C, J(5, 36)), device="cuda:0")
     assert same_bits(pkg.engine.fb_to_numpy(x), np.asfortranarray(d[1024:3072, :, 4:36]))
     got = pkg.WorkerFunctions.getdata(str(p), (C, C, J(1, 32)), fqavby=64, tavby=8)

@@ -339,3 +339,43 @@ def test_raw_file_window_plans(pkg, orc, tmp_path, monkeypatch, subspan):
                                     nbits=8, telescope_id=6, machine_id=10, data_type=1,
                                     tstart=59000.0, source_name="X"), a.astype(np.uint8))
     assert pkg.readers.fil_raw_layout(fil) is None
+
+
+def test_h5_chunk_index_parser(pkg, tmp_path):
+    """h5chunks.chunk_table reads the chunk B-tree of ``data`` from the file;
+    every entry must equal libhdf5's H5Dget_chunk_info_by_coord, and files
+    outside its scope (contiguous layout) give None."""
+    import ctypes
+
+    from conftest import GOLDEN
+
+    h5chunks = pkg.h5chunks
+    fb = pkg.fbh5
+    z = np.load(os.path.join(GOLDEN, "bslz4_v1.npz"), allow_pickle=False)
+    chunk = z["chunk_gamma_chunk_b2048"].tobytes()
+    c = str(tmp_path / "c.h5")
+    fb.write_bslz4_chunks(c, dict(foff=-1.0, nfpc=64), (4096, 1, 16 * 300), (16, 1, 4096),
+                          (chunk for _ in range(300)))
+    a = np.asfortranarray(np.random.default_rng(1).random((1000, 3, 50), dtype=np.float32))
+    dfl, cont = str(tmp_path / "d.h5"), str(tmp_path / "u.h5")
+    fb.write(dfl, dict(foff=-1.0), a, chunks=(7, 1, 100), deflate=1)
+    fb.write(cont, dict(foff=-1.0), a)
+    H = fb.h5().L
+    for f, nchunks in ((c, 300), (dfl, 8 * 3 * 10), (cont, None)):
+        fid = H.H5Fopen(f.encode(), 0, 0)
+        d = H.H5Dopen2(fid, b"data", 0)
+        try:
+            tab = h5chunks.chunk_table(f, H, d)
+            if nchunks is None:
+                assert tab is None
+                continue
+            assert len(tab["index"]) == nchunks
+            for k, ent in tab["index"].items():
+                off = (ctypes.c_uint64 * 3)(*k)
+                m, ad, sz = ctypes.c_uint(), ctypes.c_uint64(), ctypes.c_uint64()
+                assert H.H5Dget_chunk_info_by_coord(d, off, ctypes.byref(m), ctypes.byref(ad),
+                                                    ctypes.byref(sz)) >= 0
+                assert (ad.value, sz.value, m.value) == ent
+        finally:
+            H.H5Dclose(d)
+            H.H5Fclose(fid)
