@@ -346,10 +346,13 @@ BLDP_API int bldp_bslz4_decode_host(const void *chunk, size_t nbytes, int elem_s
   return BLDP_OK;
 }
 
-BLDP_API int bldp_bslz4_decode_dev(int nchunk, const uint8_t *comp_host, const uint8_t *comp_dev,
-                                   const uint64_t *chunk_off, const uint64_t *chunk_len,
-                                   int elem_size, uint8_t *out_dev, const uint64_t *out_off,
-                                   void *stream) {
+// Shared by the synchronous and asynchronous entry points: describe the
+// chunks on the host, then queue the planner and the decoder on `s`; error
+// bits are OR-ed into *derr (device memory).
+static int decode_launch(int nchunk, const uint8_t *comp_host, const uint8_t *comp_dev,
+                         const uint64_t *chunk_off, const uint64_t *chunk_len, int elem_size,
+                         uint8_t *out_dev, const uint64_t *out_off, int *derr_user,
+                         hipStream_t s, int **derr_used) {
   if (nchunk < 0 || (nchunk && (!comp_host || !comp_dev || !chunk_off || !chunk_len ||
                                 !out_dev || !out_off)) ||
       elem_size <= 0 || elem_size > 64)
@@ -371,11 +374,11 @@ BLDP_API int bldp_bslz4_decode_dev(int nchunk, const uint8_t *comp_host, const u
     if (ntask > INT32_MAX) return bldp::set_error(BLDP_EINVAL, "bslz4: too many blocks");
     maxbb = std::max<uint32_t>(maxbb, (uint32_t)(descs[k].block * elem_size));
   }
+  *derr_used = nullptr;
   if (ntask == 0) return BLDP_OK;
   const uint32_t cap = (lz4_bound(maxbb) + 15) & ~15u;
   if ((size_t)cap + (((size_t)maxbb + 15) & ~(size_t)15) > 64 * 1024)
     return bldp::set_error(BLDP_EINVAL, "bslz4: block of %u bytes exceeds the LDS plan", maxbb);
-  hipStream_t s = (hipStream_t)stream;
   const size_t dbytes = ((descs.size() * sizeof(ChunkDesc)) + 255) & ~(size_t)255;
   const size_t tbytes = ((ntask * sizeof(Task)) + 255) & ~(size_t)255;
   void *ws = nullptr;
@@ -383,10 +386,10 @@ BLDP_API int bldp_bslz4_decode_dev(int nchunk, const uint8_t *comp_host, const u
   if (rc) return rc;
   ChunkDesc *ddesc = (ChunkDesc *)ws;
   Task *dtask = (Task *)((char *)ws + dbytes);
-  int *derr = (int *)((char *)ws + dbytes + tbytes);
+  int *derr = derr_user ? derr_user : (int *)((char *)ws + dbytes + tbytes);
   if (hipMemcpyAsync(ddesc, descs.data(), descs.size() * sizeof(ChunkDesc),
                      hipMemcpyHostToDevice, s) != hipSuccess ||
-      hipMemsetAsync(derr, 0, sizeof(int), s) != hipSuccess)
+      (!derr_user && hipMemsetAsync(derr, 0, sizeof(int), s) != hipSuccess))
     return bldp::set_error(BLDP_EHIP, "bslz4: descriptor upload failed");
   hipLaunchKernelGGL(k_bslz4_plan, dim3((unsigned)((nchunk + 63) / 64)), dim3(64), 0, s,
                      comp_dev, ddesc, nchunk, elem_size, cap, dtask, derr);
@@ -395,13 +398,51 @@ BLDP_API int bldp_bslz4_decode_dev(int nchunk, const uint8_t *comp_host, const u
                      (int)ntask, out_dev, elem_size, cap, derr);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return bldp::set_error(BLDP_EHIP, "bslz4 launch: %s", hipGetErrorString(e));
+  *derr_used = derr;
+  return BLDP_OK;
+}
+
+static int decode_error(int herr) {
+  if (herr & 6) return bldp::set_error(BLDP_EINVAL, "bslz4: block table overruns a chunk");
+  if (herr) return bldp::set_error(BLDP_EINVAL, "bslz4: corrupt LZ4 block on the device");
+  return BLDP_OK;
+}
+
+BLDP_API int bldp_bslz4_decode_dev(int nchunk, const uint8_t *comp_host, const uint8_t *comp_dev,
+                                   const uint64_t *chunk_off, const uint64_t *chunk_len,
+                                   int elem_size, uint8_t *out_dev, const uint64_t *out_off,
+                                   void *stream) {
+  hipStream_t s = (hipStream_t)stream;
+  int *derr = nullptr;
+  int rc = decode_launch(nchunk, comp_host, comp_dev, chunk_off, chunk_len, elem_size, out_dev,
+                         out_off, nullptr, s, &derr);
+  if (rc || !derr) return rc;
   int herr = 0;
   if (hipMemcpyAsync(&herr, derr, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)
     return bldp::set_error(BLDP_EHIP, "bslz4: synchronize failed");
-  if (herr & 6) return bldp::set_error(BLDP_EINVAL, "bslz4: block table overruns a chunk");
-  if (herr) return bldp::set_error(BLDP_EINVAL, "bslz4: corrupt LZ4 block on the device");
-  return BLDP_OK;
+  return decode_error(herr);
+}
+
+BLDP_API int bldp_bslz4_decode_dev_async(int nchunk, const uint8_t *comp_host,
+                                         const uint8_t *comp_dev, const uint64_t *chunk_off,
+                                         const uint64_t *chunk_len, int elem_size,
+                                         uint8_t *out_dev, const uint64_t *out_off, int *err_dev,
+                                         void *stream) {
+  if (!err_dev) return bldp::set_error(BLDP_EINVAL, "bslz4: null error word");
+  int *derr = nullptr;
+  return decode_launch(nchunk, comp_host, comp_dev, chunk_off, chunk_len, elem_size, out_dev,
+                       out_off, err_dev, (hipStream_t)stream, &derr);
+}
+
+BLDP_API int bldp_bslz4_error(const int *err_dev, void *stream) {
+  if (!err_dev) return bldp::set_error(BLDP_EINVAL, "bslz4: null error word");
+  int herr = 0;
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemcpyAsync(&herr, err_dev, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return bldp::set_error(BLDP_EHIP, "bslz4: synchronize failed");
+  return decode_error(herr);
 }
 
 }  // extern "C"

@@ -817,12 +817,14 @@ def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 
 def _decode_batches(batches, stage, sizes, masks, offsets, cvol, packed, cdev, host, _lib,
                     torch):
     """A reader thread runs ``stage`` over the batches ahead of this thread,
-    which decodes each batch on the GPU as soon as its copy has landed.
+    which queues each batch's GPU decode as soon as its copy has landed
+    (asynchronously; the decoder's error bits are checked once at the end).
     Returns (decode seconds, seconds waited for reads)."""
     import time
     from concurrent.futures import ThreadPoolExecutor
 
     t_io = t_dec = 0.0
+    err = torch.zeros(1, dtype=torch.int32, device=packed.device)  # decoder error bits
     with ThreadPoolExecutor(max_workers=1) as reader:
         futs = [reader.submit(stage, ks) for ks in batches]  # reads run ahead
         cur_stream = torch.cuda.current_stream()
@@ -840,11 +842,15 @@ def _decode_batches(batches, stage, sizes, masks, offsets, cvol, packed, cdev, h
                 offs = np.array([offsets[k] for k in comp], np.uint64)
                 lens = np.array([sizes[k] for k in comp], np.uint64)
                 ooff = np.array([4 * k * cvol for k in comp], np.uint64)
-                rc = _lib.lib().bldp_bslz4_decode_dev(
+                rc = _lib.lib().bldp_bslz4_decode_dev_async(
                     len(comp), host.ctypes.data, cdev.data_ptr(), offs.ctypes.data,
-                    lens.ctypes.data, 4, packed.data_ptr(), ooff.ctypes.data, _lib.stream_ptr())
-                _lib.check(rc, "bldp_bslz4_decode_dev")
+                    lens.ctypes.data, 4, packed.data_ptr(), ooff.ctypes.data, err.data_ptr(),
+                    _lib.stream_ptr())
+                _lib.check(rc, "bldp_bslz4_decode_dev_async")
             t_dec += time.perf_counter() - td
+    td = time.perf_counter()
+    _lib.check(_lib.lib().bldp_bslz4_error(err.data_ptr(), _lib.stream_ptr()), "bslz4 decode")
+    t_dec += time.perf_counter() - td
     return t_dec, t_io
 
 

@@ -215,6 +215,18 @@ BLDP_API int bldp_bslz4_decode_dev(int nchunk, const uint8_t *comp_host, const u
                                    int elem_size, uint8_t *out_dev, const uint64_t *out_off,
                                    void *stream);
 
+/* Asynchronous form: queues the decode on `stream` and returns; error bits
+ * are OR-ed into *err_dev (device int, zeroed by the caller before its first
+ * call).  The host copy comp_host may be reused once the call returns.
+ * bldp_bslz4_error synchronizes `stream` and turns *err_dev into a return
+ * code (BLDP_EINVAL for a corrupt block). */
+BLDP_API int bldp_bslz4_decode_dev_async(int nchunk, const uint8_t *comp_host,
+                                         const uint8_t *comp_dev, const uint64_t *chunk_off,
+                                         const uint64_t *chunk_len, int elem_size,
+                                         uint8_t *out_dev, const uint64_t *out_off, int *err_dev,
+                                         void *stream);
+BLDP_API int bldp_bslz4_error(const int *err_dev, void *stream);
+
 /* Gather a window (Julia order, dense (nc, ni, nt) out) from decoded chunks:
  * packed holds the chunks of a chunk-aligned bounding box back to back in
  * chunk-grid order [gt][gi][gc], each chunk C-order [ct][ci][cc].
