@@ -153,6 +153,26 @@ def test_bslz4_gpu_rejects_corrupt_blocks(pkg):
     good = z["chunk_int_runs_b512"].tobytes()
     out = pkg.fbh5.bslz4_decode_dev([good], device="cuda:0")  # the device still works
     assert np.array_equal(out.cpu().numpy(), z["raw_int_runs_b512"].ravel())
+    # asynchronous form: a good and a corrupt call share one error word, which
+    # bldp_bslz4_error reports after the fact
+    import torch
+
+    L, lib = pkg._lib.lib(), pkg._lib
+    err = torch.zeros(1, dtype=torch.int32, device="cuda:0")
+    res = torch.empty(max(z["raw_int_runs_b512"].nbytes, 2048 * 4), dtype=torch.uint8,
+                      device="cuda:0")
+    for blob in (good, bad):
+        h = np.frombuffer(blob, np.uint8)
+        dv = torch.from_numpy(h.copy()).cuda()
+        o = np.zeros(1, np.uint64)
+        n = np.array([len(blob)], np.uint64)
+        assert L.bldp_bslz4_decode_dev_async(1, h.ctypes.data, dv.data_ptr(), o.ctypes.data,
+                                             n.ctypes.data, 4, res.data_ptr(), o.ctypes.data,
+                                             err.data_ptr(), lib.stream_ptr()) == 0
+        if blob is good:
+            assert L.bldp_bslz4_error(err.data_ptr(), lib.stream_ptr()) == 0
+    assert L.bldp_bslz4_error(err.data_ptr(), lib.stream_ptr()) == lib.BLDP_EINVAL
+    assert "corrupt" in lib.last_error() or "overruns" in lib.last_error()
 
 
 @pytest.mark.parametrize("parsed_index", [True, False])
