@@ -344,3 +344,31 @@ def test_native_band_gather_world1(pkg, orc):
             assert same_bits(eng.fb_to_numpy(got), eng.fb_to_numpy(local))
     finally:
         nb.close()
+
+
+def test_bench_json_contract():
+    """bench.py prints one JSON line with the keys the driver reads (a short
+    cfg1 run; the default cfg3 run is the round-end bench)."""
+    import json
+    import subprocess
+    import sys
+
+    from conftest import REPO
+
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "3",
+                        "--warmup", "1", "--config", "cfg1", "--cpu-seconds", "0.5"],
+                       capture_output=True, text=True, timeout=300, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+              "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["value"] > 0
+    rf = d["roofline"]
+    assert rf["bound"] == "hbm" and 0 < rf["frac"] < 1 and rf["peak"] == 8000.0
+    cb = d["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1
+    assert "workload" in d["config"]
