@@ -525,6 +525,31 @@ def raw_layout(fname):
         H.H5Fclose(f)
 
 
+def raw_chunked(fname) -> bool:
+    """True when ``data`` is a chunked dataset with no filter, stored as
+    little-endian float32: its chunks are the elements, read like the
+    compressed ones and gathered on the GPU without a decode."""
+    lay = layout(fname)
+    if lay["chunk"] is None or lay["filters"] or len(lay["cdims"]) != 3:
+        return False
+    H5 = h5()
+    H = H5.L
+    f = _ok(H.H5Fopen(os.fsencode(fname), H5F_ACC_RDONLY, H5P_DEFAULT), f"open {fname}")
+    try:
+        d = _ok(H.H5Dopen2(f, b"data", H5P_DEFAULT), "open dataset 'data'")
+        try:
+            ty = _ok(H.H5Dget_type(d), "get_type")
+            try:
+                return (H.H5Tget_class(ty) == H5T_FLOAT and H.H5Tget_size(ty) == 4
+                        and H.H5Tget_order(ty) == H5T_ORDER_LE)
+            finally:
+                H.H5Tclose(ty)
+        finally:
+            H.H5Dclose(d)
+    finally:
+        H.H5Fclose(f)
+
+
 def needs_bslz4(fname) -> bool:
     """True when ``data`` is bitshuffle/LZ4-compressed and libhdf5 has no
     plugin for filter 32008 (the case of this image)."""
@@ -662,7 +687,8 @@ def _chunk_sizes(H, d, chunk, kt0, ki0, kc0, grid):
     return offs, sizes
 
 
-def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 20):
+def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 20,
+                           raw_chunks=False):
     """Device path of a compressed window, overlapped in three stages: a
     reader thread reads batches of stored chunks straight into pinned memory
     and queues their H2D copy on a copy stream, while this thread decodes the
@@ -670,7 +696,10 @@ def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 
     gathered (bldp_unchunk_f32).  Only compressed bytes cross PCIe.  The
     chunks are read by parallel preads at the offsets of the chunk index
     parsed from the file (h5chunks.py), or, outside that parser's scope, one
-    H5Dread_chunk at a time.  ``timings`` (a dict) receives stage times."""
+    H5Dread_chunk at a time.  ``raw_chunks``: the dataset has no filter, every
+    stored chunk is raw float32 (no decode; when every chunk is stored, the
+    device copy of the chunks is the packed chunk grid itself).  ``timings``
+    (a dict) receives stage times."""
     import time
 
     import torch
@@ -737,7 +766,9 @@ def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 
                 batches.append(cur)
             with torch.cuda.device(dev):
                 cdev = torch.empty(total + 16, dtype=torch.uint8, device=dev)
-                packed = torch.zeros(len(sizes) * cvol, dtype=torch.float32, device=dev)
+                dense_raw = raw_chunks and all(n == 4 * cvol for n in sizes)
+                packed = cdev[:total].view(torch.float32) if dense_raw else \
+                    torch.zeros(len(sizes) * cvol, dtype=torch.float32, device=dev)
                 copy_stream = torch.cuda.Stream(dev)
 
                 hostmv = memoryview(host)
@@ -800,9 +831,11 @@ def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 
 
                 t_io = t_dec = 0.0
                 try:
+                    if raw_chunks:  # no filter: stored chunks are raw elements
+                        masks = [1] * len(sizes)
                     t_dec, t_io = _decode_batches(
-                        batches, stage, sizes, masks, offsets, cvol, packed, cdev, host, _lib,
-                        torch)
+                        batches, stage, sizes, masks, offsets, cvol,
+                        None if dense_raw else packed, cdev, host, _lib, torch)
                 finally:
                     if tab is not None:
                         os.close(fd)
@@ -824,7 +857,7 @@ def _decode_batches(batches, stage, sizes, masks, offsets, cvol, packed, cdev, h
     from concurrent.futures import ThreadPoolExecutor
 
     t_io = t_dec = 0.0
-    err = torch.zeros(1, dtype=torch.int32, device=packed.device)  # decoder error bits
+    err = torch.zeros(1, dtype=torch.int32, device=cdev.device)  # decoder error bits
     with ThreadPoolExecutor(max_workers=1) as reader:
         futs = [reader.submit(stage, ks) for ks in batches]  # reads run ahead
         cur_stream = torch.cuda.current_stream()
@@ -834,7 +867,7 @@ def _decode_batches(batches, stage, sizes, masks, offsets, cvol, packed, cdev, h
             t_io += time.perf_counter() - tw
             td = time.perf_counter()
             for k in ks:  # stored without the filter: raw elements
-                if sizes[k] and masks[k] & 1:
+                if packed is not None and sizes[k] and masks[k] & 1:
                     packed.view(torch.uint8)[4 * k * cvol:4 * (k + 1) * cvol].copy_(
                         cdev[offsets[k]:offsets[k] + 4 * cvol])
             comp = [k for k in ks if sizes[k] and not masks[k] & 1]

@@ -198,10 +198,12 @@ def getfbh5data(fbh5name, idxs=(COLON, COLON, COLON), fqavby=1, fqavfunc="sum", 
     op = _opname(fqavfunc)
     from . import fbh5
 
-    if op is not None and fbh5.needs_bslz4(fbh5name):
+    if op is not None and (fbh5.needs_bslz4(fbh5name) or fbh5.raw_chunked(fbh5name)):
         # compressed rawspec product: only the compressed chunks cross PCIe; they
-        # are decoded, windowed and reduced on the GPU, the result comes back
-        x = fbh5.read_window_bslz4(fbh5name, idxs, device=f"cuda:{device}")
+        # are decoded, windowed and reduced on the GPU, the result comes back.
+        # Unfiltered chunked data takes the same chunk reader without a decode.
+        x = fbh5._read_window_bslz4_dev(fbh5name, idxs, f"cuda:{device}",
+                                        raw_chunks=not fbh5.needs_bslz4(fbh5name))
         import torch
 
         with torch.cuda.device(x.device):

@@ -372,3 +372,20 @@ def test_bench_json_contract():
     cb = d["cpu_baseline"]
     assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1
     assert "workload" in d["config"]
+
+
+def test_unfiltered_chunked_fbh5_on_gpu(pkg, orc, tmp_path):
+    """Chunked FBH5 without a filter (edge chunks padded by HDF5): the chunk
+    reader moves the stored chunks to the GPU, which gathers the window and
+    reduces it (no decode)."""
+    J, C = pkg.JRange, pkg.COLON
+    a = np.asfortranarray(np.random.default_rng(12).integers(0, 256, (1000, 3, 50))
+                          .astype(np.float32))
+    p = str(tmp_path / "chunked.h5")
+    pkg.fbh5.write(p, dict(foff=-1.0, nfpc=100), a, chunks=(7, 1, 100))
+    assert pkg.fbh5.raw_chunked(p) and not pkg.fbh5.needs_bslz4(p)
+    for idxs, F, T, op in [((C, C, C), 10, 5, "sum"), ((J(101, 900), 2, J(3, 50)), 8, 4, "max"),
+                           ((J(1000, -1, 1), C, J(50, -7, 1)), 4, 1, "min")]:
+        win = pkg.idxs.to_window(pkg.sanitizeidxs(idxs), a.shape)
+        got = pkg.WorkerFunctions.getdata(p, idxs, fqavby=F, fqavfunc=op, tavby=T)
+        assert same_bits(got, orc.reduce(a, F, T, op, win)), idxs
