@@ -60,6 +60,9 @@ for s in $STEPS; do
     dist2) run dist2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
              --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --dist-backend gloo \
              --steps 10 --warmup 3 ;;
+    dist4|dist8) run "$s" 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node "${s#dist}" \
+             --master-addr 127.0.0.1 --master-port 29613 bench.py --gpus "${s#dist}" --dist-backend gloo \
+             --steps 10 --warmup 3 ;;
     dist2c2) run dist2c2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
              --master-addr 127.0.0.1 --master-port 29612 bench.py --gpus 2 --dist-backend gloo \
              --steps 10 --warmup 3 --config cfg2 ;;
