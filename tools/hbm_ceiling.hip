@@ -226,7 +226,14 @@ __global__ __launch_bounds__(256) void k_kmix(const f4v *in, int64_t row4, int n
 #pragma unroll
   for (int r = 1; r < 16; ++r) a += v[r] * v[r];
   f4v *o = out + (int64_t)blockIdx.x * 512 + (threadIdx.x >> 6) * 128;
-  if (STORE == 1) {
+  if (STORE >= 10) {  // buffer stores with cache-policy bits STORE - 10
+    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)o, 0, 128 * 16,
+                                                                  0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, a),
+                                           rs, lane * 16, 0, STORE - 10);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, a * 2.f),
+                                           rs, (64 + lane) * 16, 0, STORE - 10);
+  } else if (STORE == 1) {
     __builtin_nontemporal_store(a, o + lane);
     __builtin_nontemporal_store(a * 2.f, o + 64 + lane);
   } else if (STORE == 2) {
@@ -320,6 +327,8 @@ int main(int argc, char **argv) {
   CK(hipDeviceSynchronize());
   char name[160];
 
+  const bool kmix_only = argc > 4 && std::string(argv[4]) == "kmix";
+  if (kmix_only) goto kmix;
   // (1) contiguous per workgroup: chunk size x loads in flight x policy
 #define CONTIG(B, POL, CHUNK_KIB, GRID_PER_CU)                                             \
   {                                                                                        \
@@ -435,6 +444,7 @@ int main(int argc, char **argv) {
   }
 
   // (3c) kurtosis-shaped read + 1/8 write mix
+kmix:
   if (gib == 32) {
     const int nrow = 16;
     const int64_t row4 = (1ll << 26) / 4, segs = row4 / 256;
@@ -447,6 +457,12 @@ int main(int argc, char **argv) {
     report("kurt-shape read 32 GiB + write 4 GiB, plain stores",
            timeit([&] { hipLaunchKernelGGL((k_kmix<2>), dim3((unsigned)(segs * 8)), dim3(256), 0, 0,
                                            in, row4, nrow, segs, wout); }, mb, reps));
+#define KMIX(AUX, NAME)                                                                      \
+    report("kurt-shape read 32 GiB + write 4 GiB, buffer stores " NAME,                      \
+           timeit([&] { hipLaunchKernelGGL((k_kmix<10 + AUX>), dim3((unsigned)(segs * 8)),     \
+                                           dim3(256), 0, 0, in, row4, nrow, segs, wout); }, mb, reps));
+    KMIX(0, "plain") KMIX(2, "nt") KMIX(16, "sc1") KMIX(1, "sc0") KMIX(17, "sc0 sc1")
+    KMIX(18, "nt sc1") KMIX(3, "nt sc0") KMIX(19, "nt sc0 sc1")
     report("kurt-shape read 32 GiB, no stores (bytes = read only)",
            timeit([&] { hipLaunchKernelGGL((k_kmix<0>), dim3((unsigned)(segs * 8)), dim3(256), 0, 0,
                                            in, row4, nrow, segs, wout); }, (double)bytes, reps));
