@@ -1296,7 +1296,7 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, int num_cus) {
   // Long time blocks with too few tiles: split the T rows across workgroups.
   const int64_t rows_per_wave = cdiv(T, a.ts);
   int64_t nchunk = 1;
-  if (tiles < target_waves && rows_per_wave >= 128) {
+  if (tiles > 0 && tiles < target_waves && rows_per_wave >= 128) {  // (empty windows: no split)
     nchunk = std::min<int64_t>(cdiv(target_waves, tiles), rows_per_wave / 64);
     nchunk = std::max<int64_t>(nchunk, 1);
   }
@@ -1383,7 +1383,8 @@ void plan_kurtosis(KurtArgs &k, int num_cus) {
   const int64_t tiles = cdiv(cdiv(ncols, 64), 4 / k.ts) * k.nrow;  // workgroups
   const int64_t target = (int64_t)num_cus * 8;
   int64_t nchunk = 1;
-  if (tiles < target) nchunk = std::min<int64_t>(cdiv(target, tiles), k.nt / (16 * k.ts));
+  if (tiles > 0 && tiles < target)  // (empty windows: no split)
+    nchunk = std::min<int64_t>(cdiv(target, tiles), k.nt / (16 * k.ts));
   nchunk = std::max<int64_t>(nchunk, 1);
   k.rows_per_chunk = std::max<int64_t>(1, cdiv(k.nt, nchunk));
   k.nchunk = (int32_t)std::max<int64_t>(1, cdiv(k.nt, k.rows_per_chunk));

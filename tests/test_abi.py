@@ -168,3 +168,19 @@ def test_native_comm_host_checks(pkg, L):
     assert L.bldp_comm_destroy(None) == pkg._lib.BLDP_OK
     h = ctypes.c_void_p()
     assert L.bldp_comm_init(0, 2, 2, None, ctypes.byref(h)) == pkg._lib.BLDP_EINVAL
+
+
+def test_empty_windows_plan_without_fault(pkg, L):
+    """Regression (found by the random-window test): an empty window with a
+    long time block used to divide by zero while planning the time split
+    (SIGFPE in the host process).  Planning, reducing and kurtosis of empty
+    windows are no-ops."""
+    A = 1 << 20
+    for win, F, T in (([155, 115, 1, 1, 1, 1, 25, 0, 1], 5, 128),
+                      ([0, 0, 1, 0, 1, 1, 0, 64, 1], 8, 64),
+                      ([0, 64, 1, 0, 0, 1, 0, 256, 1], 8, 256)):
+        info = (ctypes.c_int64 * 8)()
+        keep, wp = pkg._lib.win_arg(win)
+        assert L.bldp_reduce_plan_f32(A, 271, 2, 300, wp, F, T, 0, None, info) == 0
+        assert L.bldp_reduce_f32(A, 271, 2, 300, wp, F, T, 0, None, None) == 0
+        assert L.bldp_kurtosis_workspace_size(271, 2, 300, wp) >= 0

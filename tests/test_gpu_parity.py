@@ -509,3 +509,81 @@ def test_band_reduce_multi_device_api(eng, orc, pkg):
     ptrs = (ctypes.c_void_p * 2)(xs[0].data_ptr(), xs[1].data_ptr())
     rc = L.bldp_band_reduce_multi_f32(2, devs, ptrs, 8192, 2, 48, None, 64, 16, 0, 0, None)
     assert rc == pkg._lib.BLDP_EINVAL
+
+
+def _random_case(rng):
+    """A random window / factors / op over a small random array, biased so
+    that every plan (row, vector, narrow, tile, scalar, time chunks) shows up
+    (the interleaved kernel needs >= 4096 large groups: IL_SHAPES)."""
+    nchan = int(rng.choice([rng.integers(1, 300), rng.integers(300, 5000), 4096, 8192, 16384]))
+    nif = int(rng.integers(1, 4))
+    ntime = int(rng.choice([rng.integers(1, 70), rng.integers(70, 400)]))
+    cs = int(rng.choice([1, 1, 1, 1, 1, 2, 3, -1, -2, 5, 9]))
+    c0 = int(rng.integers(0, nchan))
+    if rng.random() < 0.5:
+        c0 -= c0 % 4  # 16-byte aligned start
+    if rng.random() < 0.25:
+        c0 = 0
+    cmax = (nchan - 1 - c0) // cs + 1 if cs > 0 else c0 // (-cs) + 1
+    F = int(rng.choice([1, 2, 3, 4, 8, 16, 64, 256, 5, 12, 32]))
+    if cmax // F == 0:
+        F = 1
+    g = cmax // F
+    ngroups = int(rng.integers(1, g + 1)) if rng.random() < 0.95 else 0
+    if ngroups and rng.random() < 0.5:
+        ngroups = g  # the widest window this start allows
+    nc = ngroups * F
+    i0 = int(rng.integers(0, nif))
+    ni = int(rng.integers(1, nif - i0 + 1))
+    T = int(rng.choice([1, 2, 3, 4, 8, 16, 7, 32, 128]))
+    t0 = int(rng.integers(0, ntime)) if rng.random() < 0.7 else 0
+    if (ntime - t0) // T == 0:
+        T = 1
+    m = (ntime - t0) // T
+    nto = int(rng.integers(1, m + 1)) if rng.random() < 0.95 else 0
+    win = [c0, nc, cs, i0, ni, 1, t0, nto * T, 1]
+    op = str(rng.choice(["sum", "max", "min", "mean"]))
+    return (nchan, nif, ntime), win, F, T, op
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_reduce_random_windows_against_oracle(eng, orc, seed):
+    """300 random (shape, window, fqavby, tavby, op) cases per seed on
+    integer data: bit-exact against the oracle whenever the Float32 group
+    sums are exact (< 2^24), rtol 1e-5 otherwise; every plan the planner can
+    pick is reached."""
+    rng = np.random.default_rng(1234 + seed)
+    seen = set()
+    for _ in range(40):
+        shape, win, F, T, op = _random_case(rng)
+        a = np.asfortranarray(rng.integers(0, 256, shape).astype(np.float32))
+        x = dev(eng, a)
+        got = host(eng, eng.reduce(x, F, T, op, win))
+        want = orc.reduce(a, F, T, op, win)
+        assert got.shape == want.shape, (shape, win, F, T, op)
+        if win[1] * win[4] * win[7]:
+            seen.add(eng.plan(x, F, T, op, win)["path"])
+        if op in ("max", "min") or (op == "sum" and F * T * 255 < 2 ** 24):
+            assert same_bits(got, want), (shape, win, F, T, op)
+        else:
+            np.testing.assert_allclose(got, want, rtol=RTOL, err_msg=str((shape, win, F, T, op)))
+    assert seen  # the plan set is reported for coverage inspection
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_kurtosis_random_windows_against_oracle(eng, orc, seed):
+    """Random windows for getkurtosis: register (<= 32 spectra), tile (<= 512)
+    and two-pass kernels, aligned and unaligned channel windows."""
+    rng = np.random.default_rng(777 + seed)
+    for _ in range(12):
+        shape, win, _, _, _ = _random_case(rng)
+        nt = int(rng.choice([rng.integers(1, 40), rng.integers(40, 600), rng.integers(600, 1500)]))
+        shape = (shape[0], shape[1], nt)
+        win[6] = int(rng.integers(0, nt))
+        win[7] = int(rng.integers(0, nt - win[6] + 1))
+        a = np.asfortranarray((rng.standard_normal(shape) ** 2).astype(np.float32) * 100)
+        got = host(eng, eng.kurtosis(dev(eng, a), win))
+        want = orc.kurtosis(a, win)
+        assert got.shape == want.shape, (shape, win)
+        assert np.array_equal(np.isnan(got), np.isnan(want)), (shape, win)
+        np.testing.assert_allclose(got, want, rtol=1e-4, atol=1e-5, err_msg=str((shape, win)))
