@@ -587,3 +587,30 @@ def test_kurtosis_random_windows_against_oracle(eng, orc, seed):
         assert got.shape == want.shape, (shape, win)
         assert np.array_equal(np.isnan(got), np.isnan(want)), (shape, win)
         np.testing.assert_allclose(got, want, rtol=1e-4, atol=1e-5, err_msg=str((shape, win)))
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_host_and_band_random_windows(eng, orc, seed):
+    """Random windows through the host-array drop-in (bldp_reduce_host_f32,
+    staged through pinned pipelines) and through band launches of 1-5 banks
+    (stitched output slots)."""
+    rng = np.random.default_rng(4242 + seed)
+    for _ in range(12):
+        shape, win, F, T, op = _random_case(rng)
+        a = np.asfortranarray(rng.integers(0, 256, shape).astype(np.float32))
+        exact = op in ("max", "min") or (op == "sum" and F * T * 255 < 2 ** 24)
+        got = eng.reduce_host(a, F, T, op, win)
+        want = orc.reduce(a, F, T, op, win)
+        if exact:
+            assert same_bits(got, want), (shape, win, F, T, op)
+        else:
+            np.testing.assert_allclose(got, want, rtol=RTOL)
+        nb = int(rng.integers(1, 6))
+        banks = [a] + [np.asfortranarray(rng.integers(0, 256, shape).astype(np.float32))
+                       for _ in range(nb - 1)]
+        got = host(eng, eng.band_reduce([dev(eng, b) for b in banks], F, T, op, win))
+        want = orc.stitch([orc.reduce(b, F, T, op, win) for b in banks])
+        if exact:
+            assert same_bits(got, want), (nb, shape, win, F, T, op)
+        else:
+            np.testing.assert_allclose(got, want, rtol=RTOL)

@@ -379,3 +379,32 @@ def test_h5_chunk_index_parser(pkg, tmp_path):
         finally:
             H.H5Dclose(d)
             H.H5Fclose(fid)
+
+
+def test_raw_file_window_plans_random(pkg, orc, tmp_path, monkeypatch):
+    """filestream.plan_window on random windows (steps of either sign on every
+    axis, both read plans) against numpy indexing of the same file."""
+    fs = pkg.filestream
+    rng = np.random.default_rng(5)
+    a = np.asfortranarray(rng.integers(0, 256, (300, 3, 41)).astype(np.float32))
+    f = str(tmp_path / "r.fil")
+    pkg.readers.write_fil(f, dict(fch1=8000.0, foff=-1.0, nchans=300, nifs=3, tsamp=1.0,
+                                  nbits=32, telescope_id=6, machine_id=10, data_type=1,
+                                  tstart=59000.0, source_name="X"), a)
+    base, jshape = pkg.readers.fil_raw_layout(f)
+    for sub in (False, True):
+        monkeypatch.setattr(fs, "SUBSPAN_MIN_BYTES", 1 if sub else 1 << 30)
+        for _ in range(200):
+            w = []
+            for n in jshape:
+                st = int(rng.integers(0, n))
+                sp = int(rng.choice([1, 1, 2, 3, -1, -2]))
+                cmax = (n - 1 - st) // sp + 1 if sp > 0 else st // (-sp) + 1
+                w += [st, int(rng.integers(0, cmax + 1)), sp]
+            runs, dshape, rwin = fs.plan_window(jshape, w, base)
+            if not len(runs):
+                assert w[1] * w[4] * w[7] == 0
+                continue
+            blk = fs.read_runs_host(f, runs).view(np.float32)
+            blk = blk.reshape(dshape[::-1]).transpose(2, 1, 0)
+            assert np.array_equal(orc.np_window(blk, rwin), orc.np_window(a, w)), w
