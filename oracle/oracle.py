@@ -326,8 +326,56 @@ def lz4_literals(data: bytes) -> bytes:
     return bytes(out) + data
 
 
-def np_bslz4_encode(a: np.ndarray, block: int = 2048) -> bytes:
-    """An HDF5-filter-32008 chunk (bitshuffle + LZ4) of `a`, LZ4 literal-only."""
+def _lz4_len(out: bytearray, r: int) -> None:
+    while r >= 255:
+        out.append(255)
+        r -= 255
+    out.append(r)
+
+
+def lz4_compress(src: bytes) -> bytes:
+    """A greedy LZ4 block compressor (public LZ4 block format: token, literal
+    length extension, literals, 16-bit little-endian offset, match length
+    extension), for test data with real matches -- overlapping ones
+    (offset < length) included.  Follows the format's end-of-block rules:
+    the last 5 bytes are literals and no match starts within the last 12."""
+    n = len(src)
+    out = bytearray()
+    table: dict = {}
+    i = anchor = 0
+
+    def emit(lit: bytes, off: int = 0, mlen: int = 0) -> None:
+        ll = len(lit)
+        ml = mlen - 4 if off else 0
+        out.append((min(ll, 15) << 4) | (min(ml, 15) if off else 0))
+        if ll >= 15:
+            _lz4_len(out, ll - 15)
+        out.extend(lit)
+        if off:
+            out.extend(off.to_bytes(2, "little"))
+            if ml >= 15:
+                _lz4_len(out, ml - 15)
+
+    while i + 12 <= n:
+        key = src[i:i + 4]
+        cand = table.get(key)
+        table[key] = i
+        if cand is not None and i - cand <= 65535:
+            m = 4
+            while i + m < n - 5 and src[cand + m] == src[i + m]:
+                m += 1
+            emit(src[anchor:i], i - cand, m)
+            i += m
+            anchor = i
+        else:
+            i += 1
+    emit(src[anchor:])
+    return bytes(out)
+
+
+def np_bslz4_encode(a: np.ndarray, block: int = 2048, lz4=None) -> bytes:
+    """An HDF5-filter-32008 chunk (bitshuffle + LZ4) of `a`; LZ4 literal-only
+    unless ``lz4`` (e.g. lz4_compress) is given."""
     import struct
 
     flat = np.ascontiguousarray(a, dtype=np.float32).ravel()
@@ -339,7 +387,7 @@ def np_bslz4_encode(a: np.ndarray, block: int = 2048) -> bytes:
     sizes = [block] * nfull + ([last] if last else [])
     pos = 0
     for sz in sizes:
-        z = lz4_literals(np_bitshuffle(flat[pos:pos + sz]).tobytes())
+        z = (lz4 or lz4_literals)(np_bitshuffle(flat[pos:pos + sz]).tobytes())
         parts.append(struct.pack(">I", len(z)) + z)
         pos += sz
     parts.append(flat[pos:].tobytes())

@@ -389,3 +389,18 @@ def test_unfiltered_chunked_fbh5_on_gpu(pkg, orc, tmp_path):
         win = pkg.idxs.to_window(pkg.sanitizeidxs(idxs), a.shape)
         got = pkg.WorkerFunctions.getdata(p, idxs, fqavby=F, fqavfunc=op, tavby=T)
         assert same_bits(got, orc.reduce(a, F, T, op, win)), idxs
+
+
+def test_bslz4_gpu_decoder_random_lz4(pkg, orc):
+    """The GPU decoder on the same kind of random chunks (real LZ4 matches,
+    all block sizes, raw tails), 40 chunks in one call."""
+    from test_host import _random_bslz4_cases
+
+    cases = _random_bslz4_cases(orc, 100, 40)
+    out = pkg.fbh5.bslz4_decode_dev([c for _, c in cases], device="cuda:0").cpu().numpy()
+    pos = 0
+    for a, c in cases:
+        got = out[pos:pos + a.size]
+        assert np.array_equal(got.view(np.uint32), a.view(np.uint32)), (a.size, len(c))
+        pos += a.size
+    assert pos == out.size

@@ -408,3 +408,34 @@ def test_raw_file_window_plans_random(pkg, orc, tmp_path, monkeypatch):
             blk = fs.read_runs_host(f, runs).view(np.float32)
             blk = blk.reshape(dshape[::-1]).transpose(2, 1, 0)
             assert np.array_equal(orc.np_window(blk, rwin), orc.np_window(a, w)), w
+
+
+def _random_bslz4_cases(orc, seed, count):
+    rng = np.random.default_rng(seed)
+    out = []
+    for k in range(count):
+        n = int(rng.integers(1, 20000))
+        kind = k % 5
+        if kind == 0:
+            a = np.zeros(n, np.float32)
+        elif kind == 1:
+            a = rng.integers(0, 4, n).astype(np.float32)
+        elif kind == 2:
+            a = rng.random(n).astype(np.float32)
+        elif kind == 3:
+            a = np.tile(rng.random(int(rng.integers(1, 40))).astype(np.float32), n)[:n]
+        else:  # gamma power with a bandpass, like a filterbank
+            a = (rng.gamma(2.0, 5e8, n) * (0.2 + 0.8 * np.cos(np.arange(n) / 200.0) ** 2)
+                 ).astype(np.float32)
+        block = int(rng.choice([8, 64, 256, 1024, 2048, 4096]))
+        out.append((a, orc.np_bslz4_encode(a, block, lz4=orc.lz4_compress)))
+    return out
+
+
+def test_bslz4_host_decoder_random_lz4(pkg, orc):
+    """The host bitshuffle/LZ4 decoder on random chunks whose LZ4 blocks carry
+    real matches (overlapping ones included; oracle.lz4_compress), block sizes
+    8..4096 elements, element counts with a raw tail."""
+    for a, c in _random_bslz4_cases(orc, 99, 40):
+        d = pkg.fbh5.bslz4_decode_host(c)
+        assert np.array_equal(d.view(np.uint32), a.view(np.uint32)), (a.size, len(c))
