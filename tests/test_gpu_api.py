@@ -404,3 +404,35 @@ def test_bslz4_gpu_decoder_random_lz4(pkg, orc):
         assert np.array_equal(got.view(np.uint32), a.view(np.uint32)), (a.size, len(c))
         pos += a.size
     assert pos == out.size
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_compressed_and_raw_files_random_windows(pkg, orc, tmp_path, seed):
+    """Random chunk geometries and windows: a bitshuffle/LZ4 FBH5 (real LZ4
+    matches), an unfiltered chunked FBH5 and a contiguous one, each through
+    WorkerFunctions.getdata on the GPU, against the oracle (exact on integer
+    data)."""
+    rng = np.random.default_rng(31 + seed)
+    nc, ni, nt = int(rng.integers(200, 3000)), int(rng.integers(1, 3)), int(rng.integers(20, 90))
+    a = np.asfortranarray(rng.integers(0, 64, (nc, ni, nt)).astype(np.float32))
+    chunk = (int(rng.integers(1, 17)), 1, int(rng.integers(64, 1500)))
+    comp, plain, cont = (str(tmp_path / f"{k}.h5") for k in ("c", "p", "u"))
+    pkg.fbh5.write_bslz4(comp, dict(foff=-1.0), a, chunk,
+                         lambda blk: orc.np_bslz4_encode(blk, 512, lz4=orc.lz4_compress))
+    pkg.fbh5.write(plain, dict(foff=-1.0), a, chunks=chunk)
+    pkg.fbh5.write(cont, dict(foff=-1.0), a)
+    J, C = pkg.JRange, pkg.COLON
+    for _ in range(6):
+        F = int(rng.choice([1, 2, 4, 5, 8]))
+        T = int(rng.choice([1, 2, 3, 4]))
+        c0 = int(rng.integers(1, nc // 2))
+        ncw = (int(rng.integers(F, nc - c0 + 1)) // F) * F
+        t0 = int(rng.integers(1, nt // 2))
+        ntw = (int(rng.integers(T, nt - t0 + 1)) // T) * T
+        idxs = (J(c0, c0 + ncw - 1), C, J(t0, t0 + ntw - 1))
+        op = str(rng.choice(["sum", "max", "min"]))
+        win = [c0 - 1, ncw, 1, 0, ni, 1, t0 - 1, ntw, 1]
+        want = orc.reduce(a, F, T, op, win)
+        for f in (comp, plain, cont):
+            got = pkg.WorkerFunctions.getdata(f, idxs, fqavby=F, fqavfunc=op, tavby=T)
+            assert same_bits(got, want), (f, idxs, F, T, op, chunk)
