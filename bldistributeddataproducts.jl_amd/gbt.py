@@ -18,7 +18,7 @@ from . import readers, worker as W
 from .idxs import COLON
 
 __all__ = ["datahosts", "setupworkers", "getinventories", "getheaders", "getdata",
-           "getkurtosis", "getband", "fqav"]
+           "getkurtosis", "getband", "bandaxis", "fqav"]
 
 fqav = W.fqav  # `using .WorkerFunctions` re-exports fqav (src/gbt.jl:6)
 
@@ -87,16 +87,68 @@ def getkurtosis(workers, fnames, idxs=(COLON, COLON, COLON)):
     return _fanout(workers, fnames, lambda w, f: W.getkurtosis(f, idxs, device=int(w)))
 
 
+def _chan_window(idxs, nchans):
+    """(start0, count, step) of the channel index (idxs[0]) over nchans."""
+    from .idxs import JRange, is_colon, sanitizeidxs
+
+    if len(idxs) != 3:  # @assert length(idxs) == 3 (src/gbtworkerfunctions.jl:172,180)
+        raise AssertionError("idxs must have exactly three indices")
+    c = sanitizeidxs(idxs)[0]
+    if is_colon(c):
+        return 0, int(nchans), 1
+    if isinstance(c, JRange):
+        if len(c) and not (1 <= c.first <= nchans and 1 <= c.first + (len(c) - 1) * c.step <= nchans):
+            raise IndexError(f"BoundsError: channel index {c!r} outside 1:{nchans}")
+        return c.first - 1, len(c), c.step
+    raise TypeError(f"unsupported channel index {c!r}")
+
+
+def bandaxis(headers, idxs=(COLON, COLON, COLON), fqavby=1):
+    """Frequency axis (MHz) of the stitched band product that ``getband``
+    returns for the same ``idxs``/``fqavby``.
+
+    Bank b's window is ``range(fch1_b + foff_b*c0; step=foff_b*cs, length=nc)``
+    (headers from getheaders, src/gbtworkerfunctions.jl:131-159), decimated
+    by ``fqav(r, fqavby)`` (:27-33) and concatenated in bank order like the
+    data (src/gbt.jl:103).  Returns one ``FRange`` when every bank's axis
+    continues the previous one (a full-band window of adjacent banks), else
+    a float64 array of channel centres."""
+    parts = []
+    for h in list(np.asarray(headers, dtype=object).ravel()):
+        c0, nc, cs = _chan_window(idxs, int(h["nchans"]))
+        r = W.FRange(float(h["fch1"]) + float(h["foff"]) * c0, float(h["foff"]) * cs, nc)
+        parts.append(W.fqav_range(r, fqavby) if fqavby > 1 else r)
+    if not parts:
+        return W.FRange(0.0, 1.0, 0)
+    step = parts[0].step
+    contiguous = all(p.step == step for p in parts)
+    for a, b in zip(parts, parts[1:]):
+        if not contiguous:
+            break
+        nxt = a.first + a.length * a.step
+        contiguous = a.length > 0 and abs(b.first - nxt) <= 1e-9 * max(1.0, abs(nxt))
+    if contiguous:
+        return W.FRange(parts[0].first, step, sum(p.length for p in parts))
+    return np.concatenate([p.values() for p in parts])
+
+
 def getband(workers, fnames, idxs=(COLON, COLON, COLON), fqavby=1, fqavfunc="sum", tavby=1,
-            despike_nfpc=None):
+            despike_nfpc=None, freqs=False):
     """The stitched band product: reduce(vcat, getdata(...)) in the given
     bank order (src/gbt.jl:103).  With ``despike_nfpc`` the DC bin of every
-    coarse channel is patched as in loadscan (src/gbt.jl:101-102,111)."""
+    coarse channel is patched as in loadscan (src/gbt.jl:101-102,111);
+    ``despike_nfpc=True`` takes loadscan's own ``nfpc = size(ds[1], 1) ÷ 64``
+    (64 coarse channels per bank, :100).  ``freqs=True`` returns
+    ``(band, bandaxis(...))``."""
     parts = list(getdata(workers, fnames, idxs, fqavby, fqavfunc, tavby).ravel())
     band = np.asfortranarray(np.concatenate(parts, axis=0))
+    if despike_nfpc is True:
+        despike_nfpc = parts[0].shape[0] // 64
     if despike_nfpc:
         from . import engine
 
         x = engine.fb_from_numpy(band, device=f"cuda:{int(np.asarray(workers).ravel()[0])}")
         band = engine.fb_to_numpy(engine.despike(x, despike_nfpc))
+    if freqs:
+        return band, bandaxis(getheaders(workers, fnames), idxs, fqavby)
     return band

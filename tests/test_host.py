@@ -35,6 +35,27 @@ def test_fqav_range_mirror(pkg):
     assert pkg.fqav(rr, 1) is rr
 
 
+def test_bandaxis(pkg):
+    J, C = pkg.JRange, pkg.COLON
+    foff = -187.5 / 1024
+    hdrs = [dict(fch1=8400.0 - b * 187.5, foff=foff, nchans=1024) for b in range(8)]
+    ax = pkg.GBT.bandaxis(hdrs, (C, C, C), 16)  # adjacent banks: one range
+    assert isinstance(ax, pkg.worker.FRange) and len(ax) == 512
+    np.testing.assert_allclose(ax.values(), 8400.0 + 15 * foff / 2 + 16 * foff * np.arange(512),
+                               rtol=0, atol=1e-9)
+    assert pkg.GBT.bandaxis(hdrs, (C, C, C), 1).step == foff
+    # a channel window per bank: the pieces no longer continue each other
+    ax = pkg.GBT.bandaxis(hdrs[:2], (J(3, 2, 9), 1, C), 2)
+    want = [8400.0 + foff * (2 + 1), 8400.0 + foff * (6 + 1)]  # fqav(3:2:9 -> 2 centres)
+    want += [w - 187.5 for w in want]
+    np.testing.assert_allclose(ax, want, rtol=0, atol=1e-9)
+    with pytest.raises(IndexError):
+        pkg.GBT.bandaxis(hdrs, (J(1, 2000), C, C))
+    with pytest.raises(AssertionError):
+        pkg.GBT.bandaxis(hdrs, (C, C))
+    assert len(pkg.GBT.bandaxis([], (C, C, C))) == 0
+
+
 def test_fqav_passthrough_and_generic_host(pkg):
     a = np.arange(24, dtype=np.float32).reshape((4, 2, 3), order="F")
     assert pkg.fqav(a, 1) is a  # n <= 1 returns A itself (:17)
