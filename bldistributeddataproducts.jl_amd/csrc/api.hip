@@ -536,6 +536,10 @@ int bldp_unchunk_f32(const float *packed, const int64_t chunk[3], const int64_t 
   for (int a = 0; a < 3; ++a) {
     if (ext[a][1] < 0) return fail(BLDP_EINVAL, "negative window count");
     if (ext[a][1] == 0) return BLDP_OK;
+    // counts and steps beyond the box cannot stay inside it; checked first so
+    // the last-index product below cannot overflow
+    if (ext[a][1] > 1 && (ext[a][1] > len[a] || ext[a][2] > len[a] || ext[a][2] < -len[a]))
+      return fail(BLDP_EBOUNDS, "window axis %d outside the decoded chunk box", a + 1);
     const int64_t first = ext[a][0], last = ext[a][0] + (ext[a][1] - 1) * ext[a][2];
     if (std::min(first, last) < lo[a] || std::max(first, last) >= lo[a] + len[a])
       return fail(BLDP_EBOUNDS, "window axis %d outside the decoded chunk box", a + 1);

@@ -184,3 +184,34 @@ def test_empty_windows_plan_without_fault(pkg, L):
         assert L.bldp_reduce_plan_f32(A, 271, 2, 300, wp, F, T, 0, None, info) == 0
         assert L.bldp_reduce_f32(A, 271, 2, 300, wp, F, T, 0, None, None) == 0
         assert L.bldp_kurtosis_workspace_size(271, 2, 300, wp) >= 0
+
+
+def test_unchunk_argument_checks(pkg, L):
+    """bldp_unchunk_f32 (the device gather from decoded FBH5 chunks) checks
+    the window against the chunk box on the host, before any launch: no
+    window element may fall outside the decoded bytes, and counts/steps that
+    would overflow the last-index product are refused too."""
+    i3 = lambda *v: (ctypes.c_int64 * 3)(*v)  # noqa: E731
+    chunk, box0, grid = i3(4, 1, 64), i3(8, 0, 128), i3(2, 1, 3)  # t 8..15, c 128..319
+
+    def call(win, packed=None, out=None):
+        return L.bldp_unchunk_f32(packed, chunk, box0, grid, (ctypes.c_int64 * 9)(*win), out,
+                                  None)
+
+    ok = [128, 192, 1, 0, 1, 1, 8, 8, 1]
+    assert call(ok) == pkg._lib.BLDP_EINVAL  # in bounds: only the null buffers remain
+    assert "null" in pkg._lib.last_error()
+    for bad in ([127, 4, 1, 0, 1, 1, 8, 2, 1],       # channel before the box
+                [300, 21, 1, 0, 1, 1, 8, 2, 1],      # channel past the box
+                [319, 193, -1, 0, 1, 1, 8, 1, 1],    # reversed, one past the start
+                [128, 2, 1, 0, 1, 1, 15, 2, 1],      # time past the box
+                [128, 2, 1, 0, 2, 1, 8, 1, 1],       # IF past the box
+                [128, 1 << 62, 4, 0, 1, 1, 8, 1, 1],  # count x step would overflow
+                [128, 2, 1 << 62, 0, 1, 1, 8, 1, 1],
+                [128, 2, -(1 << 62), 0, 1, 1, 8, 1, 1]):
+        assert call(bad) == pkg._lib.BLDP_EBOUNDS, bad
+    assert call([128, 0, 1, 0, 1, 1, 8, 2, 1]) == 0  # empty window: no-op, no pointers
+    assert call([128, 2, 1, 0, 1, 1, 8, 2, -1]) == pkg._lib.BLDP_EBOUNDS  # t 8, 7
+    assert L.bldp_unchunk_f32(None, i3(0, 1, 64), box0, grid, (ctypes.c_int64 * 9)(*ok), None,
+                              None) == pkg._lib.BLDP_EINVAL
+    assert L.bldp_unchunk_f32(None, None, box0, grid, None, None, None) == pkg._lib.BLDP_EINVAL

@@ -62,14 +62,16 @@ def test_gbt_getdata_getband_kurtosis(pkg, orc, files):
     full = pkg.GBT.getband(workers, names, (C, C, J(1, 3)), despike_nfpc=64)
     want = orc.despike(orc.stitch([np.asfortranarray(a[:, :, :3]) for a in banks]), 64)
     assert same_bits(full, want)
-    band2, ax = pkg.GBT.getband(workers, names, (C, C, J(1, 3)), fqavby=64, freqs=True,
-                                despike_nfpc=True)  # loadscan's nfpc = 64 ÷ 64 = 1: no-op
-    assert same_bits(band2, orc.stitch([orc.reduce(a, 64, 1, "sum", [0, 4096, 1, 0, 1, 1, 0, 3, 1])
-                                        for a in banks]))
+    band2, ax = pkg.GBT.getband(workers, names, (C, C, J(1, 3)), freqs=True, despike_nfpc=True)
+    assert same_bits(band2, want)  # loadscan's nfpc = 4096 ÷ 64 = 64 (src/gbt.jl:100)
     foff = -187.5 / 4096
-    assert isinstance(ax, pkg.worker.FRange) and len(ax) == band2.shape[0] == 8 * 64
+    assert isinstance(ax, pkg.worker.FRange) and len(ax) == band2.shape[0] == 8 * 4096
+    assert ax.first == 8400.0 and ax.step == foff
+    _, ax = pkg.GBT.getband(workers, names, (C, C, J(1, 3)), fqavby=64, freqs=True)
     np.testing.assert_allclose(ax.values(), 8400.0 + 63 * foff / 2 + 64 * foff * np.arange(512),
                                rtol=0, atol=1e-9)
+    with pytest.raises(pkg.BoundsError):  # nfpc = 64 ÷ 64 = 1: d[0:1:end] in the reference
+        pkg.GBT.getband(workers, names, (C, C, J(1, 3)), fqavby=64, despike_nfpc=True)
     ks = pkg.GBT.getkurtosis(workers[:2], names[:2], (J(1, 512), C, C))
     for a, k in zip(banks[:2], ks):
         np.testing.assert_allclose(k, orc.kurtosis(a, [0, 512, 1, 0, 1, 1, 0, 40, 1]),

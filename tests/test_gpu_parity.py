@@ -614,3 +614,76 @@ def test_host_and_band_random_windows(eng, orc, seed):
             assert same_bits(got, want), (nb, shape, win, F, T, op)
         else:
             np.testing.assert_allclose(got, want, rtol=RTOL)
+
+
+def _random_axis(rng, lo, n):
+    """(start, count, step) inside [lo, lo + n): steps of either sign."""
+    step = int(rng.choice([1, 1, 1, 2, 3, -1, -2]))
+    a, b = sorted(int(v) for v in rng.integers(lo, lo + n, 2))
+    if step < 0:
+        a, b = b, a
+    count = (b - a) // step + 1
+    return a, int(rng.integers(0, count + 1)) if rng.random() < 0.1 else count, step
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_unchunk_random_boxes(eng, pkg, seed):
+    """bldp_unchunk_f32 directly: a random chunk box (chunk dims, grid, box
+    origin) packed chunk by chunk in grid order, and random windows of either
+    step sign inside it; bit-exact against numpy indexing of the unpacked box
+    (the decoded-FBH5 gather, src/gbtworkerfunctions.jl:185)."""
+    import ctypes
+
+    import torch
+
+    rng = np.random.default_rng(99 + seed)
+    L = pkg._lib.lib()
+    for _ in range(25):
+        ct, ci, cc = int(rng.integers(1, 6)), int(rng.integers(1, 3)), int(rng.integers(1, 70))
+        gt, gi, gc = int(rng.integers(1, 5)), int(rng.integers(1, 3)), int(rng.integers(1, 5))
+        bt0, bi0, bc0 = (ct * int(rng.integers(0, 4)), ci * int(rng.integers(0, 2)),
+                         cc * int(rng.integers(0, 4)))
+        box = rng.integers(0, 1 << 20, (gt * ct, gi * ci, gc * cc)).astype(np.float32)
+        packed = np.concatenate([
+            box[a * ct:(a + 1) * ct, b * ci:(b + 1) * ci, c * cc:(c + 1) * cc].ravel()
+            for a in range(gt) for b in range(gi) for c in range(gc)])
+        (t0, nt, ts), (i0, ni, is_), (c0, nc, cs) = (
+            _random_axis(rng, bt0, gt * ct), _random_axis(rng, bi0, gi * ci),
+            _random_axis(rng, bc0, gc * cc))
+        win = [c0, nc, cs, i0, ni, is_, t0, nt, ts]
+        sel = lambda s, n, st, lo: s - lo + st * np.arange(n)  # noqa: E731
+        want = box[np.ix_(sel(t0, nt, ts, bt0), sel(i0, ni, is_, bi0), sel(c0, nc, cs, bc0))]
+        pk = torch.from_numpy(packed).to("cuda:0")
+        out = eng.fb_empty(nc, ni, nt, device="cuda:0")
+        i3 = lambda *v: (ctypes.c_int64 * 3)(*v)  # noqa: E731
+        rc = L.bldp_unchunk_f32(pk.data_ptr(), i3(ct, ci, cc), i3(bt0, bi0, bc0), i3(gt, gi, gc),
+                                (ctypes.c_int64 * 9)(*win), out.data_ptr() if out.numel() else None,
+                                pkg._lib.stream_ptr())
+        assert rc == 0, pkg._lib.last_error()
+        got = host(eng, out)
+        assert got.shape == (nc, ni, nt)
+        assert same_bits(got, np.asfortranarray(want.transpose(2, 1, 0))), (
+            (ct, ci, cc), (gt, gi, gc), (bt0, bi0, bc0), win)
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_stitch_despike_random(eng, orc, seed):
+    """Random bank counts and block shapes through bldp_stitch_f32 (vcat of
+    bank-major gathered blocks, src/gbt.jl:103) and random nfpc through
+    bldp_despike_f32 (src/gbt.jl:101-102,111): bit-exact copies."""
+    import torch
+
+    rng = np.random.default_rng(31 + seed)
+    for _ in range(20):
+        nb = int(rng.integers(1, 9))
+        nc, ni, nt = int(rng.integers(1, 3000)), int(rng.integers(1, 4)), int(rng.integers(1, 9))
+        blocks = [rng.standard_normal((nc, ni, nt)).astype(np.float32, order="F")
+                  for _ in range(nb)]
+        g = torch.from_numpy(np.stack([b.transpose(2, 1, 0) for b in blocks])).to("cuda:0")
+        got = host(eng, eng.stitch(g.contiguous(), nb))
+        assert same_bits(got, orc.stitch(blocks)), (nb, nc, ni, nt)
+        nfpc = int(rng.integers(2, 65))
+        whole = nfpc * int(rng.integers(1, 40))
+        d = np.asfortranarray(rng.standard_normal((whole, ni, nt)).astype(np.float32))
+        got = host(eng, eng.despike(dev(eng, d), nfpc))
+        assert same_bits(got, orc.despike(d, nfpc)), (whole, ni, nt, nfpc)
