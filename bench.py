@@ -402,6 +402,9 @@ def main():
                     help="banks as separate allocations or as views of one slab")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo only to rehearse the N-rank path on one GPU")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="N=1: run the N>1 exchange anyway (a one-rank process group, "
+                         "RCCL gather + stitch of every step) to exercise it on one GPU")
     args = ap.parse_args()
 
     import torch
@@ -418,7 +421,12 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     local = local % max(1, torch.cuda.device_count())  # gloo rehearsal: ranks share GPUs
     torch.cuda.set_device(local)
-    if world > 1:
+    use_pg = world > 1 or args.pipeline
+    if use_pg:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -464,9 +472,9 @@ def main():
     stream = torch.cuda.current_stream()
     # this rank's slice of the band; N > 1: two slots, the RCCL gather of step
     # k (to rank 0, over xGMI) overlaps the reduce of step k+1
-    pipe = pkg.band.BandPipeline(len(mine) * nco, ni, nto, device=f"cuda:{local}") \
-        if world > 1 else None
-    out = eng.fb_empty(len(mine) * nco, ni, nto) if world == 1 else None
+    pipe = pkg.band.BandPipeline(len(mine) * nco, ni, nto, device=f"cuda:{local}",
+                                 gather_single=args.pipeline) if use_pg else None
+    out = eng.fb_empty(len(mine) * nco, ni, nto) if pipe is None else None
 
     def step(ev0=None, ev1=None):
         slot = pipe.begin() if pipe else 0
@@ -533,7 +541,7 @@ def main():
                        "band_alloc": args.band_alloc,
                        "parallelism": f"{len(mine)} bank(s)/GPU x {world} GPU(s)"
                                       + (", RCCL gather + stitch (gather of step k overlaps "
-                                         "the reduce of step k+1)" if world > 1 else
+                                         "the reduce of step k+1)" if pipe else
                                          ", single-launch band reduce+stitch"),
                        "bytes_per_step": bytes_step},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -543,7 +551,7 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if use_pg:
         dist.barrier()
         dist.destroy_process_group()
     return result

@@ -92,7 +92,8 @@ class BandPipeline:
     ``exchange``.
     """
 
-    def __init__(self, ncl, ni, nto, device, depth=2, root=0, group=None, stitch_fn=None):
+    def __init__(self, ncl, ni, nto, device, depth=2, root=0, group=None, stitch_fn=None,
+                 gather_single=False):
         import torch
         import torch.distributed as dist
 
@@ -101,6 +102,7 @@ class BandPipeline:
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.root, self.group, self.depth = root, group, depth
+        self.gather_single = gather_single  # one rank: gather + stitch anyway (tests)
         self.shape = (ncl, ni, nto)
         self.gloo = dist.get_backend(group) == "gloo"
         self.stitch_fn = stitch_fn or (lambda g, n: engine.stitch(g, n))
@@ -134,7 +136,7 @@ class BandPipeline:
         import torch.distributed as dist
 
         block = self._local[slot]
-        if self.world == 1:
+        if self.world == 1 and not self.gather_single:
             return self.local(slot)
         if self.gloo and block.is_cuda:
             block = block.cpu()

@@ -130,6 +130,79 @@ def test_band_dist_two_ranks_real_kernels():
     assert all(q.get(timeout=5) for _ in ps)
 
 
+def _nccl_pipeline_rank(port, q):
+    """One rank of an RCCL (torch "nccl") process group driving BandPipeline
+    with the gather forced on: what every rank of bench.py N>1 runs."""
+    import sys
+
+    import torch
+    import torch.distributed as dist
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import __graft_entry__ as entry
+
+    pkg, orc = entry.load_package(), entry.load_oracle()
+    eng = pkg.engine
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    ok = []
+    for ni, F, T, nt in ((1, 1024, 16, 16), (2, 64, 4, 32)):  # single-row and stitched
+        banks = [orc.gamma_bandpass(8192, ni, nt, 1024, 70 + b) for b in range(4)]
+        dbanks = [eng.fb_from_numpy(b, "cuda:0") for b in banks]
+        want = orc.stitch([orc.reduce(b, F, T) for b in banks])
+        pipe = pkg.band.BandPipeline(4 * 8192 // F, ni, nt // T, device="cuda:0",
+                                     gather_single=True)
+        for _ in range(3):  # slots reused: the gather of step k overlaps step k+1
+            slot = pipe.begin()
+            eng.band_reduce(dbanks, F, T, "sum", None, out=pipe.local(slot))
+            res = pipe.exchange(slot)
+            pipe.wait(slot)
+            torch.cuda.synchronize()
+            got = eng.fb_to_numpy(res)
+            ok.append(got.shape == want.shape and bool(np.allclose(got, want, rtol=1e-5)))
+        pipe.drain()
+    t = torch.tensor([1.0, 2.0], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)  # bench.py's max-over-ranks timing
+    ok.append(t.tolist() == [1.0, 2.0])
+    dist.barrier()
+    dist.destroy_process_group()
+    q.put(ok)
+
+
+def test_band_pipeline_over_rccl_one_rank():
+    """The N>1 exchange of bench.py (BandPipeline: async torch "nccl" = RCCL
+    gather to the root, then the stitch kernel) on a one-rank group, the most
+    of it one GPU can run (RCCL refuses two ranks on one device)."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_pipeline_rank, args=(29900 + os.getpid() % 90, q))
+    p.start()
+    p.join(timeout=240)
+    assert p.exitcode == 0
+    ok = q.get(timeout=5)
+    assert ok and all(ok), ok
+
+
+def test_bench_pipeline_flag():
+    """bench.py --pipeline: the N>1 step (reduce + RCCL gather + stitch) timed
+    on a one-rank group."""
+    import json
+    import subprocess
+    import sys
+
+    from conftest import REPO
+
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "3",
+                        "--warmup", "1", "--config", "cfg2", "--pipeline", "--no-cpu-baseline"],
+                       capture_output=True, text=True, timeout=300, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["n_gpus"] == 1 and d["value"] > 0 and "RCCL gather" in d["config"]["parallelism"]
+
+
 def _bslz4_fixtures():
     import json
 
