@@ -128,9 +128,20 @@ def bench_kurtosis(args, cfg, eng, torch):
     el = time.perf_counter() - t0
     ms = e0.elapsed_time(e1) / args.steps
     n = cfg["nbank"] * cfg["nchan"] * cfg["nif"] * cfg["tw"]
-    # k_kurt_regs (<= 32 spectra) / k_kurt_mid (<= 512): the window is read once
-    reads = 1 if (cfg["tw"] <= 512 and cfg["nchan"] % 4 == 0) else 2
-    algo = reads * 4 * n + 8 * cfg["nbank"] * cfg["nchan"] * cfg["nif"]
+    # k_kurt_regs (<= 32 spectra) / k_kurt_mid (<= 512) / k_kurt_chunk (longer):
+    # the window is read once; the chunk path also writes and re-reads six
+    # Float64 moments per output and 256-spectrum chunk
+    nout = cfg["nbank"] * cfg["nchan"] * cfg["nif"]
+    vec = cfg["nchan"] % 4 == 0
+    reads = 1 if vec else 2
+    algo = reads * 4 * n + 8 * nout
+    if vec and cfg["tw"] > 512:
+        algo += 2 * 48 * nout * -(-cfg["tw"] // 256)
+    kern = ("k_kurt_regs (one read)" if cfg["tw"] <= 32 else
+            "k_kurt_mid (one read)" if cfg["tw"] <= 512 else
+            "k_kurt_chunk + k_kurt_merge_seq + k_kurt_merge (one read, chunk moments merged)")
+    if not vec:
+        kern = "k_kurt_pass<0> + k_kurt_pass<1> (two reads of the window)"
     return {"metric": "getkurtosis GB/s of filterbank input", "value": round(4 * n / ms / 1e6, 2),
             "unit": "GB/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(el * 1e3 / args.steps, 4), "higher_is_better": True,
@@ -140,9 +151,7 @@ def bench_kurtosis(args, cfg, eng, torch):
             "roofline": {"bound": "hbm", "achieved": round(algo / ms / 1e6, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(algo / ms / 1e6 / HBM_PEAK_GBS, 4), "traffic": None,
-                         "kernel": ("k_kurt_regs" if cfg["tw"] <= 32 else "k_kurt_mid") +
-                                   " (one read)" if reads == 1 else
-                                   "k_kurt_pass<0> + k_kurt_pass<1> (two reads of the window)"}}
+                         "kernel": kern}}
 
 
 CFG5_PRODUCTS = ["cfg3", "cfg4", "cfg1"]  # 0000, 0001, 0002 single-bank geometry

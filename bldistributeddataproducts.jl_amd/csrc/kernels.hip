@@ -1133,6 +1133,227 @@ __global__ __launch_bounds__(kBlock) void k_kurt_fold(const KurtArgs k) {
 }
 
 // ---------------------------------------------------------------------------
+// Long windows (> 16*BLDP_KURT_MID_NR spectra) read once: k_kurt_chunk takes
+// a k_kurt_mid-shaped tile (64 channels x 256 spectra in registers) of one time
+// chunk and writes that chunk's Float64 (mean, M2, M3, M4) about its own
+// mean (two passes over registers, so an outlier anywhere costs no digits;
+// z = x - mean is Float32, as in StatsBase);
+// k_kurt_merge combines the chunks with the pairwise central-moment update
+// (Chan et al. / Pebay), chunks in a fixed order, then moves the moments from
+// the Float64 mean to StatsBase's Float32 mean m before the final ratio.
+// Sums, moments and the merge are Float64, so the result sits within ~1e-7 relative
+// of the StatsBase recipe (whose z and z^2 are Float32).
+//   BLDP_KURT_CHUNKED 1 (default) = this path; 0 = k_kurt_pass two passes
+#ifndef BLDP_KURT_CHUNKED
+#define BLDP_KURT_CHUNKED 1
+#endif
+constexpr int kKurtChunkNR = 16;                   // rows per thread
+constexpr int64_t kKurtTile = 16 * kKurtChunkNR;   // spectra per register tile
+constexpr int64_t kKurtChunk = kKurtTile;          // spectra per written chunk
+// (merging 8 tiles per workgroup in LDS measured 30% slower: the tiles serialise)
+// per chunk and output: mean, M2, M3, M4, max, min (the extremes decide
+// whether StatsBase's Float32 z^2 / z^4 overflow to Inf)
+constexpr int kKurtSlots = 6;
+
+__device__ __forceinline__ void moments_merge(double &na, double &ma, double &a2, double &a3,
+                                              double &a4, double nb, double mb, double b2,
+                                              double b3, double b4) {
+  if (nb == 0.0) return;
+  if (na == 0.0) {
+    na = nb; ma = mb; a2 = b2; a3 = b3; a4 = b4;
+    return;
+  }
+  const double n = na + nb, d = mb - ma, dn = d / n, dn2 = dn * dn, nab = na * nb;
+  const double m4 = a4 + b4 + d * dn2 * dn * nab * (na * na - nab + nb * nb) +
+                    6.0 * dn2 * (na * na * b2 + nb * nb * a2) + 4.0 * dn * (na * b3 - nb * a3);
+  const double m3 = a3 + b3 + d * dn2 * nab * (na - nb) + 3.0 * dn * (na * b2 - nb * a2);
+  const double m2 = a2 + b2 + d * dn * nab;
+  na = n; ma += dn * nb; a2 = m2; a3 = m3; a4 = m4;
+}
+
+#ifndef BLDP_KURT_CHUNK_WAVES
+#define BLDP_KURT_CHUNK_WAVES 3
+#endif
+__global__ __launch_bounds__(kBlock)
+__attribute__((amdgpu_waves_per_eu(BLDP_KURT_CHUNK_WAVES))) void k_kurt_chunk(const KurtArgs k) {
+  constexpr int NR = kKurtChunkNR;
+  const int tid = threadIdx.x, c4 = tid & 15, rg = tid >> 4;
+  const int64_t ncols = k.nc / 4, ctiles = (ncols + 15) / 16;
+  int64_t b = blockIdx.x;
+  const int64_t ct = b % ctiles;
+  b /= ctiles;
+  const int64_t ib = b % k.nrow, chunk = b / k.nrow;
+  const int64_t col = ct * 16 + c4;
+  const bool valid = col < ncols;
+  const int bank = (int)(ib / k.ni);
+  const int64_t i = ib - (int64_t)bank * k.ni;
+  const int64_t ld16 = 16 * k.in_ld_t;
+  const int64_t t0 = chunk * kKurtChunk;
+  const int cnt = (int)min<int64_t>(kKurtTile, k.nt - t0);
+  const float *p = k.in[bank] + k.in_off + i * k.in_ld_i + 4 * (valid ? col : 0) +
+                   (t0 + rg) * k.in_ld_t;
+  float4 v[NR];
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+    if (valid && rg + 16 * r < cnt) v[r] = ld4(p + r * ld16);
+  __shared__ double part[16][16][12];  // [row group][column][moment x channel]
+  __shared__ double mean[16][4];
+  double s[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+    if (valid && rg + 16 * r < cnt) {
+      s[0] += (double)v[r].x; s[1] += (double)v[r].y;
+      s[2] += (double)v[r].z; s[3] += (double)v[r].w;
+    }
+#pragma unroll
+  for (int w = 0; w < 4; ++w) part[rg][c4][w] = s[w];
+  __syncthreads();
+  if (rg == 0) {
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      double t = 0;
+      for (int q = 0; q < 16; ++q) t += part[q][c4][w];
+      mean[c4][w] = t / (double)cnt;
+    }
+  }
+  __syncthreads();
+  // deviations z = x - c about the Float32-rounded chunk mean c (z in Float32,
+  // as StatsBase's), power sums in Float64, then moved to the exact chunk mean
+  float cf[4];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) cf[w] = (float)mean[c4][w];
+  double s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0}, s3[4] = {0, 0, 0, 0}, s4[4] = {0, 0, 0, 0};
+  float hi[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  float lo[4] = {INFINITY, INFINITY, INFINITY, INFINITY};
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+    if (valid && rg + 16 * r < cnt) {
+      const float x[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        hi[w] = fmaxf(hi[w], x[w]);
+        lo[w] = fminf(lo[w], x[w]);
+        const double d = (double)(x[w] - cf[w]), d2 = d * d;
+        s1[w] += d;
+        s2[w] += d2;
+        s3[w] += d2 * d;
+        s4[w] += d2 * d2;
+      }
+    }
+  __syncthreads();  // part[] reuse
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    part[rg][c4][w] = s1[w];
+    part[rg][c4][4 + w] = s2[w];
+    part[rg][c4][8 + w] = s3[w];
+  }
+  __shared__ double part4[16][16][4];
+  __shared__ float ext[16][16][8];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    part4[rg][c4][w] = s4[w];
+    ext[rg][c4][w] = hi[w];
+    ext[rg][c4][4 + w] = lo[w];
+  }
+  __syncthreads();
+  if (rg == 0 && valid) {
+    const int64_t n = k.nrow * k.nc, e = ib * k.nc + 4 * col;
+    double *o = k.ws_mom + chunk * kKurtSlots * n + e;
+    const double nc = (double)cnt;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      double a1 = 0, a2 = 0, a3 = 0, a4 = 0;
+      float h = -INFINITY, l = INFINITY;
+      for (int q = 0; q < 16; ++q) {
+        a1 += part[q][c4][w];
+        a2 += part[q][c4][4 + w];
+        a3 += part[q][c4][8 + w];
+        a4 += part4[q][c4][w];
+        h = fmaxf(h, ext[q][c4][w]);
+        l = fminf(l, ext[q][c4][4 + w]);
+      }
+      const double dl = a1 / nc, dl2 = dl * dl;  // exact mean - c, << the spread
+      o[w] = (double)cf[w] + dl;
+      o[n + w] = a2 - a1 * dl;
+      o[2 * n + w] = a3 - 3.0 * dl * a2 + 2.0 * nc * dl2 * dl;
+      o[3 * n + w] = a4 - 4.0 * dl * a3 + 6.0 * dl2 * a2 - 3.0 * nc * dl2 * dl2;
+      o[4 * n + w] = h;
+      o[5 * n + w] = l;
+    }
+  }
+}
+
+// Stage 1: thread (group g, output e) merges chunks [g*per, (g+1)*per) in
+// order (adjacent threads read adjacent outputs, so the loads coalesce).
+__global__ __launch_bounds__(kBlock) void k_kurt_merge_seq(const KurtArgs k) {
+  const int64_t n = k.nrow * k.nc, per = k.rows_per_chunk;
+  const int64_t G = (k.nchunk + per - 1) / per;
+  for (int64_t x = (int64_t)blockIdx.x * kBlock + threadIdx.x; x < n * G;
+       x += (int64_t)gridDim.x * kBlock) {
+    const int64_t g = x / n, e = x - g * n;
+    double na = 0, ma = 0, a2 = 0, a3 = 0, a4 = 0, hi = -INFINITY, lo = INFINITY;
+    const int64_t c1 = min<int64_t>(k.nchunk, (g + 1) * per);
+    for (int64_t ch = g * per; ch < c1; ++ch) {
+      const double *q = k.ws_mom + ch * kKurtSlots * n + e;
+      const double nb = (double)min<int64_t>(kKurtChunk, k.nt - ch * kKurtChunk);
+      moments_merge(na, ma, a2, a3, a4, nb, q[0], q[n], q[2 * n], q[3 * n]);
+      hi = fmax(hi, q[4 * n]);
+      lo = fmin(lo, q[5 * n]);
+    }
+    double *o = k.ws_sum + g * kKurtSlots * n + e;
+    o[0] = ma; o[n] = a2; o[2 * n] = a3; o[3 * n] = a4; o[4 * n] = hi; o[5 * n] = lo;
+  }
+}
+
+// Stage 2, one wave per output: lane L merges groups L, L+64, ... in order,
+// then a fixed xor tree (lower lane's moments first, so both lanes of a pair
+// agree), then the StatsBase epilogue.
+__global__ __launch_bounds__(kBlock) void k_kurt_merge(const KurtArgs k) {
+  const int lane = threadIdx.x & 63;
+  const int64_t n = k.nrow * k.nc, per = k.rows_per_chunk;
+  const int64_t G = (k.nchunk + per - 1) / per, span = per * kKurtChunk;
+  for (int64_t e = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); e < n;
+       e += (int64_t)gridDim.x * 4) {
+    double na = 0, ma = 0, a2 = 0, a3 = 0, a4 = 0, hi = -INFINITY, lo = INFINITY;
+    for (int64_t g = lane; g < G; g += 64) {
+      const double *q = k.ws_sum + g * kKurtSlots * n + e;
+      const double nb = (double)(min<int64_t>(k.nt, (g + 1) * span) - g * span);
+      moments_merge(na, ma, a2, a3, a4, nb, q[0], q[n], q[2 * n], q[3 * n]);
+      hi = fmax(hi, q[4 * n]);
+      lo = fmin(lo, q[5 * n]);
+    }
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      hi = fmax(hi, __shfl_xor(hi, off, 64));
+      lo = fmin(lo, __shfl_xor(lo, off, 64));
+      const double nb = __shfl_xor(na, off, 64), mb = __shfl_xor(ma, off, 64);
+      const double b2 = __shfl_xor(a2, off, 64), b3 = __shfl_xor(a3, off, 64);
+      const double b4 = __shfl_xor(a4, off, 64);
+      if (lane & off) {  // the partner is the lower lane: it goes first
+        double xn = nb, xm = mb, x2 = b2, x3 = b3, x4 = b4;
+        moments_merge(xn, xm, x2, x3, x4, na, ma, a2, a3, a4);
+        na = xn; ma = xm; a2 = x2; a3 = x3; a4 = x4;
+      } else {
+        moments_merge(na, ma, a2, a3, a4, nb, mb, b2, b3, b4);
+      }
+    }
+    if (lane == 0) {
+      const double nt = (double)k.nt;
+      const float m = (float)(ma * nt) / (float)k.nt;  // Float32 sum / length
+      const double eps = ma - (double)m, e2 = eps * eps;
+      double cm2 = (a2 + nt * e2) / nt;
+      double cm4 = (a4 + 4.0 * eps * a3 + 6.0 * e2 * a2 + nt * e2 * e2) / nt;
+      // StatsBase's largest Float32 z^2 and z^4 come from the extremes
+      const float zh = (float)hi - m, zl = (float)lo - m;
+      const float h2 = zh * zh, l2 = zl * zl;
+      if (isinf(h2) || isinf(l2)) cm2 = INFINITY;
+      if (isinf(h2 * h2) || isinf(l2 * l2)) cm4 = INFINITY;
+      k.out[e] = (cm4 / (cm2 * cm2)) - 3.0;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Synthetic filterbank generator (counter-based, so any element is
 // reproducible from (seed, index) alone).
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
@@ -1390,11 +1611,23 @@ void plan_kurtosis(KurtArgs &k, int num_cus) {
   k.nchunk = (int32_t)std::max<int64_t>(1, cdiv(k.nt, k.rows_per_chunk));
 }
 
+// chunks merged per stage-1 thread: about 256k stage-1 threads in all
+static int64_t kurt_group_span(int64_t n, int64_t nchunk) {
+  const int64_t groups = std::max<int64_t>(1, std::min<int64_t>(nchunk, cdiv(262144, n)));
+  return cdiv(nchunk, groups);
+}
+
 size_t kurtosis_ws_bytes(const KurtArgs &k) {
   const size_t n = (size_t)k.nrow * k.nc;
   auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
-  return up(n * k.nchunk * sizeof(double)) + up(n * sizeof(float)) +
-         up(2 * n * k.nchunk * sizeof(double));
+  size_t b = up(n * k.nchunk * sizeof(double)) + up(n * sizeof(float)) +
+             up(2 * n * k.nchunk * sizeof(double));
+  if (BLDP_KURT_CHUNKED && k.vec && k.nt > 32) {  // chunk partials + group partials
+    const int64_t nch = cdiv(k.nt, kKurtChunk), per = kurt_group_span(n, nch);
+    b = std::max(b, up(kKurtSlots * n * (size_t)nch * sizeof(double)) +
+                        up(kKurtSlots * n * (size_t)cdiv(nch, per) * sizeof(double)));
+  }
+  return b;
 }
 
 hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s) {
@@ -1428,6 +1661,21 @@ hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s) {
       hipLaunchKernelGGL(k_kurt_mid<24>, g1, dim3(kBlock), 0, s, k);
     else
       hipLaunchKernelGGL(k_kurt_mid<32>, g1, dim3(kBlock), 0, s, k);
+    return hipGetLastError();
+  }
+  if (BLDP_KURT_CHUNKED && k.vec && k.nt > 32) {  // one read, chunks merged
+    k.nchunk = (int32_t)cdiv(k.nt, kKurtChunk);
+    k.ws_mom = reinterpret_cast<double *>(ws);
+    k.rows_per_chunk = kurt_group_span((int64_t)n, k.nchunk);  // chunks per group
+    k.ws_sum = reinterpret_cast<double *>(ws + up(kKurtSlots * n * (size_t)k.nchunk *
+                                                  sizeof(double)));
+    const dim3 g1((unsigned)(cdiv(ncols, 16) * k.nrow * k.nchunk));
+    hipLaunchKernelGGL(k_kurt_chunk, g1, dim3(kBlock), 0, s, k);
+    const int64_t G = cdiv(k.nchunk, k.rows_per_chunk);
+    const unsigned sg = (unsigned)std::min<int64_t>(cdiv((int64_t)n * G, kBlock), 65536);
+    hipLaunchKernelGGL(k_kurt_merge_seq, dim3(sg), dim3(kBlock), 0, s, k);
+    const unsigned fg = (unsigned)std::min<int64_t>(cdiv((int64_t)n, 4), 16384);
+    hipLaunchKernelGGL(k_kurt_merge, dim3(fg), dim3(kBlock), 0, s, k);
     return hipGetLastError();
   }
   const dim3 grid((unsigned)(cdiv(cdiv(ncols, 64), 4 / k.ts) * k.nrow * k.nchunk)), block(kBlock);

@@ -475,8 +475,8 @@ def test_kurtosis_short_windows(eng, orc, nt, nc, ni):
 @pytest.mark.parametrize("nt", [33, 100, 128, 129, 272, 384, 385, 512, 513])
 def test_kurtosis_mid_windows(eng, orc, nt):
     """33..512 spectra: k_kurt_mid keeps a 64-channel tile in registers (one
-    read); a partial last tile; a window with channel/time offsets; 513 is
-    back on the two-pass kernels."""
+    read); a partial last tile; a window with channel/time offsets; 513 goes
+    to the chunk-merge kernels."""
     rng = np.random.default_rng(1000 + nt)
     a = np.asfortranarray((rng.standard_normal((1100, 2, nt + 3)) ** 2).astype(np.float32)
                           * 1e6)
@@ -687,3 +687,32 @@ def test_stitch_despike_random(eng, orc, seed):
         d = np.asfortranarray(rng.standard_normal((whole, ni, nt)).astype(np.float32))
         got = host(eng, eng.despike(dev(eng, d), nfpc))
         assert same_bits(got, orc.despike(d, nfpc)), (whole, ni, nt, nfpc)
+
+
+@pytest.mark.parametrize("nt", [513, 1024, 1025, 5007])
+def test_kurtosis_long_windows_chunk_merge(eng, orc, nt):
+    """> 512 spectra: k_kurt_chunk reads each 256-spectrum chunk once and
+    k_kurt_merge combines the chunks' central moments.  Covers a ragged last
+    chunk, a constant row (NaN, as StatsBase), an RFI-like outlier in the
+    first spectrum of a row (StatsBase's Float32 z^4 overflows to Inf there,
+    which the merge reproduces from the chunk extremes), a window with
+    channel/time offsets and a band launch.  (A row whose mean dwarfs its
+    spread is left out: there the oracle's Julia-style pairwise Float32 sum
+    and every GPU path's Float64 sum give different Float32 means.)"""
+    rng = np.random.default_rng(7000 + nt)
+    a = np.asfortranarray((rng.standard_normal((1100, 2, nt + 5)) ** 2).astype(np.float32)
+                          * 1e6)
+    a[5, 1, :] = 7.0
+    a[9, 0, 0] = 3e12
+    x = a[:, :, :nt].copy(order="F")
+    got = host(eng, eng.kurtosis(dev(eng, x)))
+    want = orc.kurtosis(x)
+    assert np.array_equal(np.isnan(got), np.isnan(want))
+    np.testing.assert_allclose(got, want, rtol=1e-4, atol=1e-5)
+    w = [8, 1088, 1, 0, 2, 1, 5, nt, 1]  # idxs = (9:1096, :, 6:nt+5)
+    got = host(eng, eng.kurtosis(dev(eng, a), w))
+    np.testing.assert_allclose(got, orc.kurtosis(a, w), rtol=1e-4, atol=1e-5)
+    ks = eng.band_kurtosis([dev(eng, x), dev(eng, x[::-1].copy(order="F"))])
+    np.testing.assert_allclose(host(eng, ks[0]), want, rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(host(eng, ks[1]), orc.kurtosis(x[::-1].copy(order="F")),
+                               rtol=1e-4, atol=1e-5)
