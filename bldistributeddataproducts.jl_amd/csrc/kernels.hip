@@ -1613,6 +1613,7 @@ void plan_kurtosis(KurtArgs &k, int num_cus) {
 
 // chunks merged per stage-1 thread: about 256k stage-1 threads in all
 static int64_t kurt_group_span(int64_t n, int64_t nchunk) {
+  if (n <= 0 || nchunk <= 0) return 1;  // empty windows (no division by zero)
   const int64_t groups = std::max<int64_t>(1, std::min<int64_t>(nchunk, cdiv(262144, n)));
   return cdiv(nchunk, groups);
 }
