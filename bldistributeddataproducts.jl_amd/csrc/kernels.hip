@@ -1147,7 +1147,10 @@ __global__ __launch_bounds__(kBlock) void k_kurt_fold(const KurtArgs k) {
 #ifndef BLDP_KURT_CHUNKED
 #define BLDP_KURT_CHUNKED 1
 #endif
-constexpr int kKurtChunkNR = 16;                   // rows per thread
+#ifndef BLDP_KURT_CHUNK_NR
+#define BLDP_KURT_CHUNK_NR 16
+#endif
+constexpr int kKurtChunkNR = BLDP_KURT_CHUNK_NR;   // rows per thread
 constexpr int64_t kKurtTile = 16 * kKurtChunkNR;   // spectra per register tile
 constexpr int64_t kKurtChunk = kKurtTile;          // spectra per written chunk
 // (merging 8 tiles per workgroup in LDS measured 30% slower: the tiles serialise)
