@@ -1147,6 +1147,11 @@ __global__ __launch_bounds__(kBlock) void k_kurt_fold(const KurtArgs k) {
 #ifndef BLDP_KURT_CHUNKED
 #define BLDP_KURT_CHUNKED 1
 #endif
+//   BLDP_KURT_CHUNK_S1F32 1 (default) = per-thread sum of z in Float32: no VGPR
+//                   spills at 2 waves/SIMD, +2.7% on cfg4 (0 = Float64, 10 spilled)
+#ifndef BLDP_KURT_CHUNK_S1F32
+#define BLDP_KURT_CHUNK_S1F32 1
+#endif
 #ifndef BLDP_KURT_CHUNK_NR
 #define BLDP_KURT_CHUNK_NR 24
 #endif
@@ -1225,7 +1230,12 @@ __attribute__((amdgpu_waves_per_eu(BLDP_KURT_CHUNK_WAVES))) void k_kurt_chunk(co
   float cf[4];
 #pragma unroll
   for (int w = 0; w < 4; ++w) cf[w] = (float)mean[c4][w];
-  double s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0}, s3[4] = {0, 0, 0, 0}, s4[4] = {0, 0, 0, 0};
+#if BLDP_KURT_CHUNK_S1F32
+  float s1[4] = {0, 0, 0, 0};  // sum of z only recentres: Float32 costs nothing measurable
+#else
+  double s1[4] = {0, 0, 0, 0};
+#endif
+  double s2[4] = {0, 0, 0, 0}, s3[4] = {0, 0, 0, 0}, s4[4] = {0, 0, 0, 0};
   float hi[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
   float lo[4] = {INFINITY, INFINITY, INFINITY, INFINITY};
 #pragma unroll
@@ -1236,8 +1246,9 @@ __attribute__((amdgpu_waves_per_eu(BLDP_KURT_CHUNK_WAVES))) void k_kurt_chunk(co
       for (int w = 0; w < 4; ++w) {
         hi[w] = fmaxf(hi[w], x[w]);
         lo[w] = fminf(lo[w], x[w]);
-        const double d = (double)(x[w] - cf[w]), d2 = d * d;
-        s1[w] += d;
+        const float z = x[w] - cf[w];
+        const double d = (double)z, d2 = d * d;
+        s1[w] += z;
         s2[w] += d2;
         s3[w] += d2 * d;
         s4[w] += d2 * d2;
