@@ -130,13 +130,13 @@ def bench_kurtosis(args, cfg, eng, torch):
     n = cfg["nbank"] * cfg["nchan"] * cfg["nif"] * cfg["tw"]
     # k_kurt_regs (<= 32 spectra) / k_kurt_mid (<= 512) / k_kurt_chunk (longer):
     # the window is read once; the chunk path also writes and re-reads six
-    # Float64 moments per output and 384-spectrum chunk
+    # Float64 moments per output and 448-spectrum chunk
     nout = cfg["nbank"] * cfg["nchan"] * cfg["nif"]
     vec = cfg["nchan"] % 4 == 0
     reads = 1 if vec else 2
     algo = reads * 4 * n + 8 * nout
     if vec and cfg["tw"] > 512:
-        algo += 2 * 48 * nout * -(-cfg["tw"] // 384)
+        algo += 2 * 48 * nout * -(-cfg["tw"] // 448)
     kern = ("k_kurt_regs (one read)" if cfg["tw"] <= 32 else
             "k_kurt_mid (one read)" if cfg["tw"] <= 512 else
             "k_kurt_chunk + k_kurt_merge_seq + k_kurt_merge (one read, chunk moments merged)")

@@ -1134,7 +1134,7 @@ __global__ __launch_bounds__(kBlock) void k_kurt_fold(const KurtArgs k) {
 
 // ---------------------------------------------------------------------------
 // Long windows (> 16*BLDP_KURT_MID_NR spectra) read once: k_kurt_chunk takes
-// a k_kurt_mid-shaped tile (64 channels x 384 spectra in registers) of one time
+// a k_kurt_mid-shaped tile (64 channels x 448 spectra in registers) of one time
 // chunk and writes that chunk's Float64 (mean, M2, M3, M4) about its own
 // mean (two passes over registers, so an outlier anywhere costs no digits;
 // z = x - mean is Float32, as in StatsBase);
@@ -1153,7 +1153,7 @@ __global__ __launch_bounds__(kBlock) void k_kurt_fold(const KurtArgs k) {
 #define BLDP_KURT_CHUNK_S1F32 1
 #endif
 #ifndef BLDP_KURT_CHUNK_NR
-#define BLDP_KURT_CHUNK_NR 24
+#define BLDP_KURT_CHUNK_NR 28
 #endif
 constexpr int kKurtChunkNR = BLDP_KURT_CHUNK_NR;   // rows per thread
 constexpr int64_t kKurtTile = 16 * kKurtChunkNR;   // spectra per register tile

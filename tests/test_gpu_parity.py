@@ -691,7 +691,7 @@ def test_stitch_despike_random(eng, orc, seed):
 
 @pytest.mark.parametrize("nt", [513, 1024, 1025, 5007])
 def test_kurtosis_long_windows_chunk_merge(eng, orc, nt):
-    """> 512 spectra: k_kurt_chunk reads each 384-spectrum chunk once and
+    """> 512 spectra: k_kurt_chunk reads each 448-spectrum chunk once and
     k_kurt_merge combines the chunks' central moments.  Covers a ragged last
     chunk, a constant row (NaN, as StatsBase), an RFI-like outlier in the
     first spectrum of a row (StatsBase's Float32 z^4 overflows to Inf there,
