@@ -105,15 +105,26 @@ def cpu_baseline(cfg, seconds, eng, torch):
                       f"(float64 accumulate), one pthread per bank"}
 
 
+def pairwise_leaves(n):
+    """Leaves of Julia's pairwise sum over n elements (pieces of <= 1024)."""
+    if n <= 1024:
+        return 1
+    return pairwise_leaves((n + 1) // 2) + pairwise_leaves(n // 2)
+
+
 def bench_kurtosis(args, cfg, eng, torch):
     """getkurtosis (src/gbtworkerfunctions.jl:197-202) over every bank of the
-    config: two-pass StatsBase recipe, so the algorithm reads the window twice."""
+    config in one band launch (StatsBase recipe, Julia's pairwise Float32 mean).
+    Algorithmic bytes: the window read once, plus (streamed-leaf path) the
+    leaf partials written and read back by the tree merge, plus the Float64
+    results."""
     win = None
     if cfg["tw"] != cfg["ntime"]:
         win = [0, cfg["nchan"], 1, 0, cfg["nif"], 1, 0, cfg["tw"], 1]
     dst = eng.band_empty(cfg["nbank"], cfg["nchan"], cfg["nif"], cfg["ntime"])
     banks = [eng.synth(cfg["nchan"], cfg["nif"], cfg["ntime"], cfg["nfpc"],
                        seed=10 * b + cfg["product"], kind=0, out=o) for b, o in enumerate(dst)]
+    plan = eng.kurtosis_plan(banks[0], win)
     stream = torch.cuda.current_stream()
     for _ in range(args.warmup):
         eng.band_kurtosis(banks, win)
@@ -128,30 +139,28 @@ def bench_kurtosis(args, cfg, eng, torch):
     el = time.perf_counter() - t0
     ms = e0.elapsed_time(e1) / args.steps
     n = cfg["nbank"] * cfg["nchan"] * cfg["nif"] * cfg["tw"]
-    # k_kurt_regs (<= 32 spectra) / k_kurt_mid (<= 512) / k_kurt_chunk (longer):
-    # the window is read once; the chunk path also writes and re-reads six
-    # Float64 moments per output and 448-spectrum chunk
     nout = cfg["nbank"] * cfg["nchan"] * cfg["nif"]
-    vec = cfg["nchan"] % 4 == 0
-    reads = 1 if vec else 2
+    path = plan["path"]
+    reads = 2 if path == "twopass" else 1
     algo = reads * 4 * n + 8 * nout
-    if vec and cfg["tw"] > 512:
-        algo += 2 * 48 * nout * -(-cfg["tw"] // 448)
-    kern = ("k_kurt_regs (one read)" if cfg["tw"] <= 32 else
-            "k_kurt_mid (one read)" if cfg["tw"] <= 512 else
-            "k_kurt_chunk + k_kurt_merge_seq + k_kurt_merge (one read, chunk moments merged)")
-    if not vec:
-        kern = "k_kurt_pass<0> + k_kurt_pass<1> (two reads of the window)"
+    if path == "leaf":  # (mean, M2, M3, M4) Float64 + (sum, max, min) Float32 per leaf
+        algo += 2 * 44 * nout * pairwise_leaves(cfg["tw"])
+    kern = {"regs": "k_kurt_regs (one read, bit-exact recipe)",
+            "mid": "k_kurt_mid (one read, register tile)",
+            "leaf": "k_kurt_leaf + k_kurt_tree/k_kurt_final (one read, leaves of Julia's "
+                    "pairwise sum streamed, moments merged)",
+            "twopass": "k_kurt_leafsum + tree + k_kurt_pass (two reads)"}[path]
     return {"metric": "getkurtosis GB/s of filterbank input", "value": round(4 * n / ms / 1e6, 2),
             "unit": "GB/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(el * 1e3 / args.steps, 4), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f32->f64",
             "data": "synthetic (bldp_synth_f32)",
-            "config": {"workload": "kurtosis over " + cfg["workload"], "name": args.config},
+            "config": {"workload": "kurtosis over " + cfg["workload"], "name": args.config,
+                       "plan": plan},
             "roofline": {"bound": "hbm", "achieved": round(algo / ms / 1e6, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(algo / ms / 1e6 / HBM_PEAK_GBS, 4), "traffic": None,
-                         "kernel": kern}}
+                         "kernel": kern, "call_ms": round(ms, 4), "bytes_per_call": algo}}
 
 
 CFG5_PRODUCTS = ["cfg3", "cfg4", "cfg1"]  # 0000, 0001, 0002 single-bank geometry

@@ -16,6 +16,7 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 
 OPS = {"sum": 0, "mean": 1, "max": 2, "min": 3}
 PATHS = {0: "vector", 1: "narrow", 2: "scalar", 3: "tile", 4: "interleaved", 5: "row"}
+KURT_PATHS = {0: "regs", 1: "mid", 2: "leaf", 3: "twopass"}
 
 BLDP_OK, BLDP_EINVAL, BLDP_EDIM, BLDP_EHIP, BLDP_ENOMEM, BLDP_EBOUNDS = 0, -1, -2, -3, -5, -6
 BLDP_ECOMM = -7
@@ -65,6 +66,7 @@ SIGNATURES = {
     "bldp_despike_f32": ([P, I64, I64, I64, I64, P], I),
     "bldp_kurtosis_workspace_size": ([I64, I64, I64, P], SZ),
     "bldp_kurtosis_f32": ([P, I64, I64, I64, P, P, P, P], I),
+    "bldp_kurtosis_plan_f32": ([P, I64, I64, I64, P, P], I),
     "bldp_kurtosis_host_f32": ([I, P, I64, I64, I64, P, P], I),
     "bldp_band_kurtosis_f32": ([I, P, I64, I64, I64, P, P, P], I),
     "bldp_fqav_range": ([D, D, I64, I64, P, P, P], I),

@@ -461,8 +461,7 @@ static int kurt_setup(int nbank, const float *const *in, int64_t nchan, int64_t 
 
 static int kurt_run(KurtArgs &k, double *out, void *workspace, void *stream) {
   if (k.nc * k.nrow == 0) return BLDP_OK;
-  const int64_t ncols = k.vec ? k.nc / 4 : k.nc;
-  if (((ncols + 63) / 64) * k.nrow * k.nchunk > INT32_MAX || ((ncols + 15) / 16) * k.nrow > INT32_MAX)
+  if (kurtosis_max_grid(k) > INT32_MAX)
     return fail(BLDP_EINVAL, "kurtosis window too large for one launch");
   for (int b = 0; b < k.nbank; ++b)
     if (!k.in[b] && k.nt > 0) return fail(BLDP_EINVAL, "null input pointer (bank %d)", b);
@@ -484,9 +483,25 @@ size_t bldp_kurtosis_workspace_size(int64_t nchan, int64_t nif, int64_t ntime,
   KurtArgs k;
   const float *none[1] = {nullptr};
   if (kurt_setup(1, none, nchan, nif, ntime, win, &k)) return 0;
-  k.vec = 1;  // the plan does not depend on alignment
-  plan_kurtosis(k, num_cus_current());
-  return kurtosis_ws_bytes(k);
+  // enough for either plan: the path depends on the pointer's alignment
+  k.vec = 1;
+  const size_t a = kurtosis_ws_bytes(k);
+  k.vec = 0;
+  return std::max(a, kurtosis_ws_bytes(k));
+}
+
+int bldp_kurtosis_plan_f32(const float *in, int64_t nchan, int64_t nif, int64_t ntime,
+                           const int64_t *win, int64_t info[4]) {
+  if (!info) return fail(BLDP_EINVAL, "null info");
+  KurtArgs k;
+  const float *ins[1] = {in};
+  int rc = kurt_setup(1, ins, nchan, nif, ntime, win, &k);
+  if (rc) return rc;
+  info[0] = kurtosis_path(k);
+  info[1] = k.K;
+  info[2] = k.nslot;
+  info[3] = (int64_t)kurtosis_ws_bytes(k);
+  return BLDP_OK;
 }
 
 int bldp_kurtosis_f32(const float *in, int64_t nchan, int64_t nif, int64_t ntime,

@@ -83,24 +83,38 @@ hipError_t launch_stitch(int nbank, const float *g, int64_t nc, int64_t nrows, f
 hipError_t launch_despike(float *d, int64_t nchan, int64_t nrows, int64_t nfpc, int64_t nspike,
                           hipStream_t s);
 
+// Kurtosis launch (kurtosis.hip).  Julia's Float32 mean is a pairwise sum
+// whose halving tree is perfect down to level K ("blocks", <= 2048 spectra),
+// each block being one or two sequentially summed leaves (<= 1024 spectra).
 struct KurtArgs {
   const float *in[BLDP_MAX_BANKS];  // banks with identical geometry
   int32_t nbank;
   int64_t nrow;                     // nbank * ni output rows of nc channels
   int64_t in_off, in_cs, in_ld_i, in_ld_t;
   int64_t nc, ni, nt;
+  int32_t vec;  // float4 along channels legal
+  int32_t K;    // level of the blocks of the pairwise-sum tree
+  int64_t nslot;  // leaf slots, 2 per block (2^(K+1))
+  int64_t nseg;   // 64-lane column segments per row (k_kurt_leaf)
+  // two-pass (unaligned) z pass
   int64_t rows_per_chunk;
   int32_t nchunk;
-  int32_t ts;   // waves of a workgroup splitting the spectra of a tile (1, 2, 4)
-  int32_t vec;  // float4 along channels legal
-  double *ws_sum;   // [nchunk][nbank*ni][nc]
-  float *mean;      // [nbank*ni][nc]
+  int32_t ts;       // waves of a workgroup splitting the spectra of a tile (1, 2, 4)
+  float *mean;      // [nbank*ni][nc]  Float32 mean (two-pass path)
   double *ws_mom;   // [nchunk][2][nbank*ni][nc]
+  // leaf / tree-node partials: pm [4][nodes][n] Float64 (mean, M2, M3, M4
+  // about the node's own mean), pf [3][nodes][n] Float32 (pairwise sum, max, min)
+  double *pm;
+  float *pf;
   double *out;      // [nbank][ni][nc]
 };
 void plan_kurtosis(KurtArgs &k, int num_cus);
 size_t kurtosis_ws_bytes(const KurtArgs &k);
 hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s);
+// Which kurtosis path a plan takes (0 registers, 1 register tile, 2 streamed
+// leaves + tree merge, 3 two passes), for tests and bench.
+int kurtosis_path(const KurtArgs &k);
+int64_t kurtosis_max_grid(const KurtArgs &k);  // largest grid of the plan
 
 // Window of a chunked dataset: chunk dims (ct, ci, cc) in C order, a chunk
 // bounding box starting at (bt0, bi0, bc0) with (gt, gi, gc) chunks, and the

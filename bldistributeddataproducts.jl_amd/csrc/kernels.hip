@@ -735,639 +735,6 @@ __global__ __launch_bounds__(kBlock) void k_despike(float *d, int64_t nchan, int
 }
 
 // ---------------------------------------------------------------------------
-// Kurtosis (StatsBase two-pass recipe).  A tile is 64 lanes of columns
-// (float4 columns when 16-byte loads are legal) x one IF x one time chunk.
-// `ts` waves of a workgroup split the spectra of a tile (4/ts tiles per
-// workgroup), each lane keeping 8 loads in flight, and combine their Float64
-// partials through LDS in wave order.  With one time chunk the epilogue is
-// fused (pass 0 writes the mean, pass 1 the kurtosis); otherwise chunks are
-// folded in a fixed order by k_kurt_fold.
-//   BLDP_KURT_PASS_MAXWAVES  cap on resident waves per SIMD for k_kurt_pass (0 = none).
-//                  Default 4: +1.1..1.2% on long windows (0001 band, 2048
-//                  spectra) against uncapped 5-6 waves; 3 loses 10%
-#ifndef BLDP_KURT_PASS_MAXWAVES
-#define BLDP_KURT_PASS_MAXWAVES 4
-#endif
-template <int PASS, int VEC>
-__global__ __launch_bounds__(kBlock)
-#if BLDP_KURT_PASS_MAXWAVES > 0
-__attribute__((amdgpu_waves_per_eu(1, BLDP_KURT_PASS_MAXWAVES)))
-#endif
-void k_kurt_pass(const KurtArgs k) {
-  constexpr int W = VEC ? 4 : 1;              // channels per lane
-  constexpr int NA = PASS == 0 ? W : 2 * W;   // Float64 accumulators per lane
-  constexpr int B = 8;                        // spectra in flight per lane
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int ts = k.ts, wt = wave / ts, tsi = wave - wt * ts;
-  const int64_t ncols = VEC ? k.nc / 4 : k.nc;
-  const int64_t ctiles = (ncols + 63) / 64, tpb = 4 / ts;
-  const int64_t cblocks = (ctiles + tpb - 1) / tpb;
-  int64_t b = blockIdx.x;
-  const int64_t cb = b % cblocks;
-  b /= cblocks;
-  const int64_t ib = b % k.nrow, chunk = b / k.nrow;  // (bank, IF) row, time chunk
-  const int bank = (int)(ib / k.ni);
-  const int64_t i = ib - (int64_t)bank * k.ni;
-  const int64_t col = (cb * tpb + wt) * 64 + lane;
-  const bool valid = col < ncols;
-  const int64_t r0 = chunk * k.rows_per_chunk, r1 = min(k.nt, r0 + k.rows_per_chunk);
-  const int64_t e = ib * k.nc + (VEC ? 4 * col : col);  // first output of this lane
-  double acc[NA];
-#pragma unroll
-  for (int a = 0; a < NA; ++a) acc[a] = 0.0;
-  if (valid) {
-    const float *p = k.in[bank] + k.in_off + i * k.in_ld_i + (r0 + tsi) * k.in_ld_t +
-                     (VEC ? 4 * col : col * k.in_cs);
-    float m[W];
-#pragma unroll
-    for (int w = 0; w < W; ++w) m[w] = PASS == 1 ? k.mean[e + w] : 0.0f;
-    int64_t n = r1 - r0 - tsi;
-    n = n > 0 ? (n + ts - 1) / ts : 0;
-    const int64_t st = (int64_t)ts * k.in_ld_t;
-    for (; n > 0; n -= B, p += B * st) {
-      // predicated batch: spectra past the end read as the mean (z = 0) / 0
-      float v[B][W];
-#pragma unroll
-      for (int u = 0; u < B; ++u) {
-        if (u < n) {
-          if (VEC) {
-            const float4 q = ld4(p + u * st);
-            v[u][0] = q.x; v[u][W > 1 ? 1 : 0] = q.y;
-            v[u][W > 2 ? 2 : 0] = q.z; v[u][W > 3 ? 3 : 0] = q.w;
-          } else {
-            v[u][0] = p[u * st];
-          }
-        } else {
-#pragma unroll
-          for (int w = 0; w < W; ++w) v[u][w] = m[w];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < B; ++u)
-#pragma unroll
-        for (int w = 0; w < W; ++w) {
-          if (PASS == 0) {
-            acc[w] += (double)v[u][w];
-          } else {
-            // StatsBase: z = v[i] - m; z2 = z*z (Float32); cm2 += z2; cm4 += z2*z2
-            const float z = v[u][w] - m[w];
-            const float z2 = z * z;
-            acc[w] += (double)z2;
-            acc[W + w] += (double)(z2 * z2);
-          }
-        }
-    }
-  }
-  if (ts > 1) {
-    __shared__ double red[4][8][64];
-#pragma unroll
-    for (int a = 0; a < NA; ++a) red[wave][a][lane] = acc[a];
-    __syncthreads();
-    if (tsi == 0)
-      for (int q = 1; q < ts; ++q)
-#pragma unroll
-        for (int a = 0; a < NA; ++a) acc[a] += red[wave + q][a][lane];
-  }
-  if (tsi == 0 && valid) {
-    const int64_t n = k.nrow * k.nc;
-    if (k.nchunk == 1) {
-#pragma unroll
-      for (int w = 0; w < W; ++w) {
-        if (PASS == 0) {
-          k.mean[e + w] = (float)acc[w] / (float)k.nt;  // Float32 sum / length
-        } else {
-          const double cm2 = acc[w] / (double)k.nt, cm4 = acc[W + w] / (double)k.nt;
-          k.out[e + w] = (cm4 / (cm2 * cm2)) - 3.0;
-        }
-      }
-    } else {
-#pragma unroll
-      for (int a = 0; a < NA; ++a) {
-        if (PASS == 0)
-          k.ws_sum[chunk * n + e + a] = acc[a];
-        else
-          k.ws_mom[(chunk * 2 + a / W) * n + e + a % W] = acc[a];
-      }
-    }
-  }
-}
-
-// Short windows (nt <= NTMAX spectra): each lane keeps its float4 column of
-// every spectrum in registers, so the window is read from HBM once; the
-// arithmetic is the same two-pass StatsBase recipe, run over the registers.
-// EXACT (nt == NTMAX, e.g. the 16-spectrum 0000 product) is straight-line
-// code: all NTMAX loads issue back to back and the Float64 sum starts as the
-// first one lands; otherwise every spectrum beyond nt is predicated off.
-//   BLDP_KURT_EXACT 1 (default) = use the exact-count instantiation
-#ifndef BLDP_KURT_EXACT
-#define BLDP_KURT_EXACT 1
-#endif
-//   BLDP_KURT_MID_NR rows per thread of the largest k_kurt_mid instantiation
-//                   (windows up to 16 x this many spectra are read once;
-//                   0 = always two passes beyond 32 spectra)
-#ifndef BLDP_KURT_MID_NR
-#define BLDP_KURT_MID_NR 32
-#endif
-//   BLDP_KURT_F32MEAN 1 = the mean from a Float32 sum (as Julia's mean of a
-//                   Float32 vector); 0 (default) = from a Float64 sum
-//   BLDP_KURT_TIMING_F32 1 = TIMING EXPERIMENT ONLY (wrong numerics): Float32
-//                   moments, to price the Float64 arithmetic
-#ifndef BLDP_KURT_F32MEAN
-#define BLDP_KURT_F32MEAN 0
-#endif
-#ifndef BLDP_KURT_TIMING_F32
-#define BLDP_KURT_TIMING_F32 0
-#endif
-//   BLDP_KURT_STORE 3 (default) = the wave's 256 Float64 results go through
-//                   LDS so every nt store instruction writes 1 KiB contiguous
-//                   (+2.5% on the 0000 band against 1); 1 = each lane's 32 B as
-//                   two nt 16-byte stores; 2 = the same, plain stores;
-//                   0 = TIMING EXPERIMENT ONLY: no store (prices the output writes)
-#ifndef BLDP_KURT_STORE
-#define BLDP_KURT_STORE 3
-#endif
-//   BLDP_KURT_WAVES minimum waves per SIMD the register budget must allow
-//                   (0 = compiler's choice)
-#ifndef BLDP_KURT_WAVES
-#define BLDP_KURT_WAVES 0
-#endif
-template <int NTMAX, bool EXACT>
-__global__ __launch_bounds__(kBlock)
-#if BLDP_KURT_WAVES > 0
-__attribute__((amdgpu_waves_per_eu(BLDP_KURT_WAVES)))
-#endif
-void k_kurt_regs(const KurtArgs k) {
-  const int64_t ncols = k.nc / 4;
-  const int64_t ctiles = (ncols + kBlock - 1) / kBlock;
-  const int64_t b = blockIdx.x;
-  const int64_t ib = b / ctiles, col = (b % ctiles) * kBlock + threadIdx.x;
-  if (col >= ncols) return;
-  const int bank = (int)(ib / k.ni);
-  const int64_t i = ib - (int64_t)bank * k.ni;
-  const float *p = k.in[bank] + k.in_off + i * k.in_ld_i + 4 * col;
-  const int nt = EXACT ? NTMAX : (int)k.nt;
-  const int64_t ld = k.in_ld_t;
-  float4 v[NTMAX];
-#pragma unroll
-  for (int t = 0; t < NTMAX; ++t)
-    if (EXACT || t < nt) v[t] = ld4(p + t * ld);
-#if BLDP_KURT_F32MEAN
-  typedef float acc_t;
-#else
-  typedef double acc_t;
-#endif
-  acc_t s[4] = {0, 0, 0, 0};
-#pragma unroll
-  for (int t = 0; t < NTMAX; ++t)
-    if (EXACT || t < nt) {
-      s[0] += (acc_t)v[t].x; s[1] += (acc_t)v[t].y;
-      s[2] += (acc_t)v[t].z; s[3] += (acc_t)v[t].w;
-    }
-  float m[4];
-#pragma unroll
-  for (int w = 0; w < 4; ++w) m[w] = (float)s[w] / (float)nt;  // Float32 sum / length
-#if BLDP_KURT_TIMING_F32
-  float c2[4] = {0, 0, 0, 0}, c4[4] = {0, 0, 0, 0};
-#else
-  double c2[4] = {0, 0, 0, 0}, c4[4] = {0, 0, 0, 0};
-#endif
-#pragma unroll
-  for (int t = 0; t < NTMAX; ++t)
-    if (EXACT || t < nt) {
-      const float x[4] = {v[t].x, v[t].y, v[t].z, v[t].w};
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        const float z = x[w] - m[w];  // StatsBase: z, z2 in Float32; Float64 moments
-        const float z2 = z * z;
-#if BLDP_KURT_TIMING_F32
-        c2[w] += z2;
-        c4[w] += z2 * z2;
-#else
-        c2[w] += (double)z2;
-        c4[w] += (double)(z2 * z2);
-#endif
-      }
-    }
-  double r[4];
-#pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    const double cm2 = c2[w] / (double)nt, cm4 = c4[w] / (double)nt;
-    r[w] = (cm4 / (cm2 * cm2)) - 3.0;
-  }
-  // 32 contiguous bytes per lane: two 16-byte streaming stores
-  typedef double d2v __attribute__((ext_vector_type(2)));
-  d2v *o = reinterpret_cast<d2v *>(k.out + ib * k.nc + 4 * col);
-  if (BLDP_KURT_STORE == 0) {
-    if (r[0] == 12345.678) k.out[0] = r[1];  // keeps the arithmetic live
-  } else if (BLDP_KURT_STORE == 3 && ncols % 64 == 0 &&
-             (reinterpret_cast<uintptr_t>(k.out + ib * k.nc) & 15) == 0) {
-    // whole wave in range: transpose through this wave's 2 KiB of LDS so each
-    // store instruction writes 1 KiB contiguous (lane L: doubles 2L, 2L+1 of
-    // the wave's 256 outputs, then 128 + 2L, 129 + 2L)
-    __shared__ d2v st[4][128];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    st[wave][2 * lane] = d2v{r[0], r[1]};
-    st[wave][2 * lane + 1] = d2v{r[2], r[3]};
-    __builtin_amdgcn_wave_barrier();
-    const d2v a0 = st[wave][lane], a1 = st[wave][64 + lane];
-    d2v *ow = reinterpret_cast<d2v *>(k.out + ib * k.nc + 4 * (col - lane));
-    __builtin_nontemporal_store(a0, ow + lane);
-    __builtin_nontemporal_store(a1, ow + 64 + lane);
-  } else if ((reinterpret_cast<uintptr_t>(o) & 15) == 0) {
-    if (BLDP_KURT_STORE == 1) {
-      __builtin_nontemporal_store(d2v{r[0], r[1]}, o);
-      __builtin_nontemporal_store(d2v{r[2], r[3]}, o + 1);
-    } else {
-      o[0] = d2v{r[0], r[1]};
-      o[1] = d2v{r[2], r[3]};
-    }
-  } else {
-    double *od = k.out + ib * k.nc + 4 * col;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) od[w] = r[w];
-  }
-}
-
-// Mid-length windows (32 < nt <= 16*NR spectra, e.g. the 272-spectrum 0002
-// window): a workgroup holds a 64-channel x nt tile in registers, so the
-// window is still read from HBM once.  Thread (rg, c4) = (tid / 16, tid % 16)
-// keeps float4 column c4 of rows rg, rg + 16, ...; a wave-instruction reads
-// 4 rows x 256 B.  The Float64 sums and moments of the 16 row groups are
-// combined through LDS in row-group order (deterministic); the arithmetic is
-// the StatsBase recipe of k_kurt_regs.
-template <int NR>
-__global__ __launch_bounds__(kBlock) void k_kurt_mid(const KurtArgs k) {
-  const int tid = threadIdx.x, c4 = tid & 15, rg = tid >> 4;
-  const int64_t ncols = k.nc / 4, ctiles = (ncols + 15) / 16;
-  const int64_t b = blockIdx.x;
-  const int64_t ib = b / ctiles, col = (b % ctiles) * 16 + c4;
-  const bool valid = col < ncols;
-  const int bank = (int)(ib / k.ni);
-  const int64_t i = ib - (int64_t)bank * k.ni;
-  const int nt = (int)k.nt;
-  const float *p = k.in[bank] + k.in_off + i * k.in_ld_i + 4 * (valid ? col : 0) +
-                   rg * k.in_ld_t;
-  const int64_t ld16 = 16 * k.in_ld_t;
-  float4 v[NR];
-#pragma unroll
-  for (int r = 0; r < NR; ++r)
-    if (valid && rg + 16 * r < nt) v[r] = ld4(p + r * ld16);
-  __shared__ double part[16][16][8];  // [row group][column][moment x channel]
-  __shared__ float mean[16][4];
-  double s[4] = {0, 0, 0, 0};
-#pragma unroll
-  for (int r = 0; r < NR; ++r)
-    if (valid && rg + 16 * r < nt) {
-      s[0] += (double)v[r].x; s[1] += (double)v[r].y;
-      s[2] += (double)v[r].z; s[3] += (double)v[r].w;
-    }
-#pragma unroll
-  for (int w = 0; w < 4; ++w) part[rg][c4][w] = s[w];
-  __syncthreads();
-  if (rg == 0) {
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      double t = 0;
-      for (int q = 0; q < 16; ++q) t += part[q][c4][w];
-      mean[c4][w] = (float)t / (float)nt;  // Float32 sum / length
-    }
-  }
-  __syncthreads();
-  float m[4];
-#pragma unroll
-  for (int w = 0; w < 4; ++w) m[w] = mean[c4][w];
-  double c2[4] = {0, 0, 0, 0}, cq[4] = {0, 0, 0, 0};
-#pragma unroll
-  for (int r = 0; r < NR; ++r)
-    if (valid && rg + 16 * r < nt) {
-      const float x[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        const float z = x[w] - m[w];  // StatsBase: z, z2 in Float32; Float64 moments
-        const float z2 = z * z;
-        c2[w] += (double)z2;
-        cq[w] += (double)(z2 * z2);
-      }
-    }
-#pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    part[rg][c4][w] = c2[w];
-    part[rg][c4][4 + w] = cq[w];
-  }
-  __syncthreads();
-  if (rg == 0 && valid) {
-    double r[4];
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      double a2 = 0, a4 = 0;
-      for (int q = 0; q < 16; ++q) {
-        a2 += part[q][c4][w];
-        a4 += part[q][c4][4 + w];
-      }
-      const double cm2 = a2 / (double)nt, cm4 = a4 / (double)nt;
-      r[w] = (cm4 / (cm2 * cm2)) - 3.0;
-    }
-    double *o = k.out + ib * k.nc + 4 * col;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) o[w] = r[w];
-  }
-}
-
-// Fold the time-chunk partials of every (channel, IF), few chunks: one lane
-// per output, chunks in order.
-template <int PASS>
-__global__ __launch_bounds__(kBlock) void k_kurt_fold_t(const KurtArgs k) {
-  const int64_t n = k.nrow * k.nc;
-  for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < n;
-       e += (int64_t)gridDim.x * kBlock) {
-    double a = 0.0, c = 0.0;
-    for (int ch = 0; ch < k.nchunk; ++ch) {
-      if (PASS == 0) {
-        a += k.ws_sum[ch * n + e];
-      } else {
-        a += k.ws_mom[(ch * 2) * n + e];
-        c += k.ws_mom[(ch * 2 + 1) * n + e];
-      }
-    }
-    if (PASS == 0) {
-      k.mean[e] = (float)a / (float)k.nt;
-    } else {
-      const double cm2 = a / (double)k.nt, cm4 = c / (double)k.nt;
-      k.out[e] = (cm4 / (cm2 * cm2)) - 3.0;
-    }
-  }
-}
-
-// Many chunks: one wave per output,
-// lanes take chunks lane, lane+64, ... in order, then a fixed xor tree.
-// PASS 0 -> mean (Float32), PASS 1 -> excess kurtosis (Float64).
-template <int PASS>
-__global__ __launch_bounds__(kBlock) void k_kurt_fold(const KurtArgs k) {
-  const int lane = threadIdx.x & 63;
-  const int64_t n = k.nrow * k.nc;
-  for (int64_t e = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); e < n;
-       e += (int64_t)gridDim.x * 4) {
-    double a = 0.0, c = 0.0;
-    for (int ch = lane; ch < k.nchunk; ch += 64) {
-      if (PASS == 0) {
-        a += k.ws_sum[ch * n + e];
-      } else {
-        a += k.ws_mom[(ch * 2) * n + e];
-        c += k.ws_mom[(ch * 2 + 1) * n + e];
-      }
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      a += __shfl_xor(a, off, 64);
-      if (PASS == 1) c += __shfl_xor(c, off, 64);
-    }
-    if (lane == 0) {
-      if (PASS == 0) {
-        k.mean[e] = (float)a / (float)k.nt;
-      } else {
-        const double cm2 = a / (double)k.nt, cm4 = c / (double)k.nt;
-        k.out[e] = (cm4 / (cm2 * cm2)) - 3.0;
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Long windows (> 16*BLDP_KURT_MID_NR spectra) read once: k_kurt_chunk takes
-// a k_kurt_mid-shaped tile (64 channels x 448 spectra in registers) of one time
-// chunk and writes that chunk's Float64 (mean, M2, M3, M4) about its own
-// mean (two passes over registers, so an outlier anywhere costs no digits;
-// z = x - mean is Float32, as in StatsBase);
-// k_kurt_merge combines the chunks with the pairwise central-moment update
-// (Chan et al. / Pebay), chunks in a fixed order, then moves the moments from
-// the Float64 mean to StatsBase's Float32 mean m before the final ratio.
-// Sums, moments and the merge are Float64, so the result sits within ~1e-7 relative
-// of the StatsBase recipe (whose z and z^2 are Float32).
-//   BLDP_KURT_CHUNKED 1 (default) = this path; 0 = k_kurt_pass two passes
-#ifndef BLDP_KURT_CHUNKED
-#define BLDP_KURT_CHUNKED 1
-#endif
-//   BLDP_KURT_CHUNK_S1F32 1 (default) = per-thread sum of z in Float32: no VGPR
-//                   spills at 2 waves/SIMD, +2.7% on cfg4 (0 = Float64, 10 spilled)
-#ifndef BLDP_KURT_CHUNK_S1F32
-#define BLDP_KURT_CHUNK_S1F32 1
-#endif
-#ifndef BLDP_KURT_CHUNK_NR
-#define BLDP_KURT_CHUNK_NR 28
-#endif
-constexpr int kKurtChunkNR = BLDP_KURT_CHUNK_NR;   // rows per thread
-constexpr int64_t kKurtTile = 16 * kKurtChunkNR;   // spectra per register tile
-constexpr int64_t kKurtChunk = kKurtTile;          // spectra per written chunk
-// (merging 8 tiles per workgroup in LDS measured 30% slower: the tiles serialise)
-// per chunk and output: mean, M2, M3, M4, max, min (the extremes decide
-// whether StatsBase's Float32 z^2 / z^4 overflow to Inf)
-constexpr int kKurtSlots = 6;
-
-__device__ __forceinline__ void moments_merge(double &na, double &ma, double &a2, double &a3,
-                                              double &a4, double nb, double mb, double b2,
-                                              double b3, double b4) {
-  if (nb == 0.0) return;
-  if (na == 0.0) {
-    na = nb; ma = mb; a2 = b2; a3 = b3; a4 = b4;
-    return;
-  }
-  const double n = na + nb, d = mb - ma, dn = d / n, dn2 = dn * dn, nab = na * nb;
-  const double m4 = a4 + b4 + d * dn2 * dn * nab * (na * na - nab + nb * nb) +
-                    6.0 * dn2 * (na * na * b2 + nb * nb * a2) + 4.0 * dn * (na * b3 - nb * a3);
-  const double m3 = a3 + b3 + d * dn2 * nab * (na - nb) + 3.0 * dn * (na * b2 - nb * a2);
-  const double m2 = a2 + b2 + d * dn * nab;
-  na = n; ma += dn * nb; a2 = m2; a3 = m3; a4 = m4;
-}
-
-#ifndef BLDP_KURT_CHUNK_WAVES
-#define BLDP_KURT_CHUNK_WAVES 2
-#endif
-__global__ __launch_bounds__(kBlock)
-__attribute__((amdgpu_waves_per_eu(BLDP_KURT_CHUNK_WAVES))) void k_kurt_chunk(const KurtArgs k) {
-  constexpr int NR = kKurtChunkNR;
-  const int tid = threadIdx.x, c4 = tid & 15, rg = tid >> 4;
-  const int64_t ncols = k.nc / 4, ctiles = (ncols + 15) / 16;
-  int64_t b = blockIdx.x;
-  const int64_t ct = b % ctiles;
-  b /= ctiles;
-  const int64_t ib = b % k.nrow, chunk = b / k.nrow;
-  const int64_t col = ct * 16 + c4;
-  const bool valid = col < ncols;
-  const int bank = (int)(ib / k.ni);
-  const int64_t i = ib - (int64_t)bank * k.ni;
-  const int64_t ld16 = 16 * k.in_ld_t;
-  const int64_t t0 = chunk * kKurtChunk;
-  const int cnt = (int)min<int64_t>(kKurtTile, k.nt - t0);
-  const float *p = k.in[bank] + k.in_off + i * k.in_ld_i + 4 * (valid ? col : 0) +
-                   (t0 + rg) * k.in_ld_t;
-  float4 v[NR];
-#pragma unroll
-  for (int r = 0; r < NR; ++r)
-    if (valid && rg + 16 * r < cnt) v[r] = ld4(p + r * ld16);
-  __shared__ double part[16][16][12];  // [row group][column][moment x channel]
-  __shared__ double mean[16][4];
-  double s[4] = {0, 0, 0, 0};
-#pragma unroll
-  for (int r = 0; r < NR; ++r)
-    if (valid && rg + 16 * r < cnt) {
-      s[0] += (double)v[r].x; s[1] += (double)v[r].y;
-      s[2] += (double)v[r].z; s[3] += (double)v[r].w;
-    }
-#pragma unroll
-  for (int w = 0; w < 4; ++w) part[rg][c4][w] = s[w];
-  __syncthreads();
-  if (rg == 0) {
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      double t = 0;
-      for (int q = 0; q < 16; ++q) t += part[q][c4][w];
-      mean[c4][w] = t / (double)cnt;
-    }
-  }
-  __syncthreads();
-  // deviations z = x - c about the Float32-rounded chunk mean c (z in Float32,
-  // as StatsBase's), power sums in Float64, then moved to the exact chunk mean
-  float cf[4];
-#pragma unroll
-  for (int w = 0; w < 4; ++w) cf[w] = (float)mean[c4][w];
-#if BLDP_KURT_CHUNK_S1F32
-  float s1[4] = {0, 0, 0, 0};  // sum of z only recentres: Float32 costs nothing measurable
-#else
-  double s1[4] = {0, 0, 0, 0};
-#endif
-  double s2[4] = {0, 0, 0, 0}, s3[4] = {0, 0, 0, 0}, s4[4] = {0, 0, 0, 0};
-  float hi[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-  float lo[4] = {INFINITY, INFINITY, INFINITY, INFINITY};
-#pragma unroll
-  for (int r = 0; r < NR; ++r)
-    if (valid && rg + 16 * r < cnt) {
-      const float x[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        hi[w] = fmaxf(hi[w], x[w]);
-        lo[w] = fminf(lo[w], x[w]);
-        const float z = x[w] - cf[w];
-        const double d = (double)z, d2 = d * d;
-        s1[w] += z;
-        s2[w] += d2;
-        s3[w] += d2 * d;
-        s4[w] += d2 * d2;
-      }
-    }
-  __syncthreads();  // part[] reuse
-#pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    part[rg][c4][w] = s1[w];
-    part[rg][c4][4 + w] = s2[w];
-    part[rg][c4][8 + w] = s3[w];
-  }
-  __shared__ double part4[16][16][4];
-  __shared__ float ext[16][16][8];
-#pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    part4[rg][c4][w] = s4[w];
-    ext[rg][c4][w] = hi[w];
-    ext[rg][c4][4 + w] = lo[w];
-  }
-  __syncthreads();
-  if (rg == 0 && valid) {
-    const int64_t n = k.nrow * k.nc, e = ib * k.nc + 4 * col;
-    double *o = k.ws_mom + chunk * kKurtSlots * n + e;
-    const double nc = (double)cnt;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      double a1 = 0, a2 = 0, a3 = 0, a4 = 0;
-      float h = -INFINITY, l = INFINITY;
-      for (int q = 0; q < 16; ++q) {
-        a1 += part[q][c4][w];
-        a2 += part[q][c4][4 + w];
-        a3 += part[q][c4][8 + w];
-        a4 += part4[q][c4][w];
-        h = fmaxf(h, ext[q][c4][w]);
-        l = fminf(l, ext[q][c4][4 + w]);
-      }
-      const double dl = a1 / nc, dl2 = dl * dl;  // exact mean - c, << the spread
-      o[w] = (double)cf[w] + dl;
-      o[n + w] = a2 - a1 * dl;
-      o[2 * n + w] = a3 - 3.0 * dl * a2 + 2.0 * nc * dl2 * dl;
-      o[3 * n + w] = a4 - 4.0 * dl * a3 + 6.0 * dl2 * a2 - 3.0 * nc * dl2 * dl2;
-      o[4 * n + w] = h;
-      o[5 * n + w] = l;
-    }
-  }
-}
-
-// Stage 1: thread (group g, output e) merges chunks [g*per, (g+1)*per) in
-// order (adjacent threads read adjacent outputs, so the loads coalesce).
-__global__ __launch_bounds__(kBlock) void k_kurt_merge_seq(const KurtArgs k) {
-  const int64_t n = k.nrow * k.nc, per = k.rows_per_chunk;
-  const int64_t G = (k.nchunk + per - 1) / per;
-  for (int64_t x = (int64_t)blockIdx.x * kBlock + threadIdx.x; x < n * G;
-       x += (int64_t)gridDim.x * kBlock) {
-    const int64_t g = x / n, e = x - g * n;
-    double na = 0, ma = 0, a2 = 0, a3 = 0, a4 = 0, hi = -INFINITY, lo = INFINITY;
-    const int64_t c1 = min<int64_t>(k.nchunk, (g + 1) * per);
-    for (int64_t ch = g * per; ch < c1; ++ch) {
-      const double *q = k.ws_mom + ch * kKurtSlots * n + e;
-      const double nb = (double)min<int64_t>(kKurtChunk, k.nt - ch * kKurtChunk);
-      moments_merge(na, ma, a2, a3, a4, nb, q[0], q[n], q[2 * n], q[3 * n]);
-      hi = fmax(hi, q[4 * n]);
-      lo = fmin(lo, q[5 * n]);
-    }
-    double *o = k.ws_sum + g * kKurtSlots * n + e;
-    o[0] = ma; o[n] = a2; o[2 * n] = a3; o[3 * n] = a4; o[4 * n] = hi; o[5 * n] = lo;
-  }
-}
-
-// Stage 2, one wave per output: lane L merges groups L, L+64, ... in order,
-// then a fixed xor tree (lower lane's moments first, so both lanes of a pair
-// agree), then the StatsBase epilogue.
-__global__ __launch_bounds__(kBlock) void k_kurt_merge(const KurtArgs k) {
-  const int lane = threadIdx.x & 63;
-  const int64_t n = k.nrow * k.nc, per = k.rows_per_chunk;
-  const int64_t G = (k.nchunk + per - 1) / per, span = per * kKurtChunk;
-  for (int64_t e = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); e < n;
-       e += (int64_t)gridDim.x * 4) {
-    double na = 0, ma = 0, a2 = 0, a3 = 0, a4 = 0, hi = -INFINITY, lo = INFINITY;
-    for (int64_t g = lane; g < G; g += 64) {
-      const double *q = k.ws_sum + g * kKurtSlots * n + e;
-      const double nb = (double)(min<int64_t>(k.nt, (g + 1) * span) - g * span);
-      moments_merge(na, ma, a2, a3, a4, nb, q[0], q[n], q[2 * n], q[3 * n]);
-      hi = fmax(hi, q[4 * n]);
-      lo = fmin(lo, q[5 * n]);
-    }
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      hi = fmax(hi, __shfl_xor(hi, off, 64));
-      lo = fmin(lo, __shfl_xor(lo, off, 64));
-      const double nb = __shfl_xor(na, off, 64), mb = __shfl_xor(ma, off, 64);
-      const double b2 = __shfl_xor(a2, off, 64), b3 = __shfl_xor(a3, off, 64);
-      const double b4 = __shfl_xor(a4, off, 64);
-      if (lane & off) {  // the partner is the lower lane: it goes first
-        double xn = nb, xm = mb, x2 = b2, x3 = b3, x4 = b4;
-        moments_merge(xn, xm, x2, x3, x4, na, ma, a2, a3, a4);
-        na = xn; ma = xm; a2 = x2; a3 = x3; a4 = x4;
-      } else {
-        moments_merge(na, ma, a2, a3, a4, nb, mb, b2, b3, b4);
-      }
-    }
-    if (lane == 0) {
-      const double nt = (double)k.nt;
-      const float m = (float)(ma * nt) / (float)k.nt;  // Float32 sum / length
-      const double eps = ma - (double)m, e2 = eps * eps;
-      double cm2 = (a2 + nt * e2) / nt;
-      double cm4 = (a4 + 4.0 * eps * a3 + 6.0 * e2 * a2 + nt * e2 * e2) / nt;
-      // StatsBase's largest Float32 z^2 and z^4 come from the extremes
-      const float zh = (float)hi - m, zl = (float)lo - m;
-      const float h2 = zh * zh, l2 = zl * zl;
-      if (isinf(h2) || isinf(l2)) cm2 = INFINITY;
-      if (isinf(h2 * h2) || isinf(l2 * l2)) cm4 = INFINITY;
-      k.out[e] = (cm4 / (cm2 * cm2)) - 3.0;
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
 // Synthetic filterbank generator (counter-based, so any element is
 // reproducible from (seed, index) alone).
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
@@ -1607,115 +974,6 @@ hipError_t launch_despike(float *d, int64_t nchan, int64_t nrows, int64_t nfpc, 
   if (n == 0) return hipSuccess;
   const unsigned grid = (unsigned)std::min<int64_t>(cdiv(n, kBlock), 16384);
   hipLaunchKernelGGL(k_despike, dim3(grid), dim3(kBlock), 0, s, d, nchan, nrows, nfpc, nspike);
-  return hipGetLastError();
-}
-
-void plan_kurtosis(KurtArgs &k, int num_cus) {
-  const int64_t ncols = k.vec ? k.nc / 4 : k.nc;
-  // waves splitting the spectra of a tile: keep >= 16 spectra per wave
-  k.ts = 1;
-  while (k.ts < 4 && k.nt >= (int64_t)32 * k.ts) k.ts *= 2;
-  const int64_t tiles = cdiv(cdiv(ncols, 64), 4 / k.ts) * k.nrow;  // workgroups
-  const int64_t target = (int64_t)num_cus * 8;
-  int64_t nchunk = 1;
-  if (tiles > 0 && tiles < target)  // (empty windows: no split)
-    nchunk = std::min<int64_t>(cdiv(target, tiles), k.nt / (16 * k.ts));
-  nchunk = std::max<int64_t>(nchunk, 1);
-  k.rows_per_chunk = std::max<int64_t>(1, cdiv(k.nt, nchunk));
-  k.nchunk = (int32_t)std::max<int64_t>(1, cdiv(k.nt, k.rows_per_chunk));
-}
-
-// chunks merged per stage-1 thread: about 256k stage-1 threads in all
-static int64_t kurt_group_span(int64_t n, int64_t nchunk) {
-  if (n <= 0 || nchunk <= 0) return 1;  // empty windows (no division by zero)
-  const int64_t groups = std::max<int64_t>(1, std::min<int64_t>(nchunk, cdiv(262144, n)));
-  return cdiv(nchunk, groups);
-}
-
-size_t kurtosis_ws_bytes(const KurtArgs &k) {
-  const size_t n = (size_t)k.nrow * k.nc;
-  auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
-  size_t b = up(n * k.nchunk * sizeof(double)) + up(n * sizeof(float)) +
-             up(2 * n * k.nchunk * sizeof(double));
-  if (BLDP_KURT_CHUNKED && k.vec && k.nt > 32) {  // chunk partials + group partials
-    const int64_t nch = cdiv(k.nt, kKurtChunk), per = kurt_group_span(n, nch);
-    b = std::max(b, up(kKurtSlots * n * (size_t)nch * sizeof(double)) +
-                        up(kKurtSlots * n * (size_t)cdiv(nch, per) * sizeof(double)));
-  }
-  return b;
-}
-
-hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s) {
-  const size_t n = (size_t)k.nrow * k.nc;
-  if (n == 0) return hipSuccess;
-  auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
-  k.ws_sum = reinterpret_cast<double *>(ws);
-  k.mean = reinterpret_cast<float *>(ws + up(n * k.nchunk * sizeof(double)));
-  k.ws_mom = reinterpret_cast<double *>(ws + up(n * k.nchunk * sizeof(double)) +
-                                        up(n * sizeof(float)));
-  const int64_t ncols = k.vec ? k.nc / 4 : k.nc;
-  if (k.vec && k.nt > 0 && k.nt <= 32) {  // one HBM read: the column fits in registers
-    const dim3 g1((unsigned)(cdiv(ncols, kBlock) * k.nrow));
-    if (BLDP_KURT_EXACT && k.nt == 16)
-      hipLaunchKernelGGL((k_kurt_regs<16, true>), g1, dim3(kBlock), 0, s, k);
-    else if (BLDP_KURT_EXACT && k.nt == 32)
-      hipLaunchKernelGGL((k_kurt_regs<32, true>), g1, dim3(kBlock), 0, s, k);
-    else if (k.nt <= 16)
-      hipLaunchKernelGGL((k_kurt_regs<16, false>), g1, dim3(kBlock), 0, s, k);
-    else
-      hipLaunchKernelGGL((k_kurt_regs<32, false>), g1, dim3(kBlock), 0, s, k);
-    return hipGetLastError();
-  }
-  if (k.vec && k.nt > 32 && k.nt <= 16 * BLDP_KURT_MID_NR) {  // one read: the tile fits
-    const dim3 g1((unsigned)(cdiv(ncols, 16) * k.nrow));
-    if (k.nt <= 128)
-      hipLaunchKernelGGL(k_kurt_mid<8>, g1, dim3(kBlock), 0, s, k);
-    else if (k.nt <= 256)
-      hipLaunchKernelGGL(k_kurt_mid<16>, g1, dim3(kBlock), 0, s, k);
-    else if (k.nt <= 384)
-      hipLaunchKernelGGL(k_kurt_mid<24>, g1, dim3(kBlock), 0, s, k);
-    else
-      hipLaunchKernelGGL(k_kurt_mid<32>, g1, dim3(kBlock), 0, s, k);
-    return hipGetLastError();
-  }
-  if (BLDP_KURT_CHUNKED && k.vec && k.nt > 32) {  // one read, chunks merged
-    k.nchunk = (int32_t)cdiv(k.nt, kKurtChunk);
-    k.ws_mom = reinterpret_cast<double *>(ws);
-    k.rows_per_chunk = kurt_group_span((int64_t)n, k.nchunk);  // chunks per group
-    k.ws_sum = reinterpret_cast<double *>(ws + up(kKurtSlots * n * (size_t)k.nchunk *
-                                                  sizeof(double)));
-    const dim3 g1((unsigned)(cdiv(ncols, 16) * k.nrow * k.nchunk));
-    hipLaunchKernelGGL(k_kurt_chunk, g1, dim3(kBlock), 0, s, k);
-    const int64_t G = cdiv(k.nchunk, k.rows_per_chunk);
-    const unsigned sg = (unsigned)std::min<int64_t>(cdiv((int64_t)n * G, kBlock), 65536);
-    hipLaunchKernelGGL(k_kurt_merge_seq, dim3(sg), dim3(kBlock), 0, s, k);
-    const unsigned fg = (unsigned)std::min<int64_t>(cdiv((int64_t)n, 4), 16384);
-    hipLaunchKernelGGL(k_kurt_merge, dim3(fg), dim3(kBlock), 0, s, k);
-    return hipGetLastError();
-  }
-  const dim3 grid((unsigned)(cdiv(cdiv(ncols, 64), 4 / k.ts) * k.nrow * k.nchunk)), block(kBlock);
-  const bool wide = k.nchunk > 16;  // wave per output only when there is much to fold
-  const unsigned fg = (unsigned)std::min<int64_t>(cdiv((int64_t)n, wide ? 4 : kBlock), 16384);
-  if (k.vec)
-    hipLaunchKernelGGL((k_kurt_pass<0, 1>), grid, block, 0, s, k);
-  else
-    hipLaunchKernelGGL((k_kurt_pass<0, 0>), grid, block, 0, s, k);
-  if (k.nchunk > 1) {
-    if (wide)
-      hipLaunchKernelGGL(k_kurt_fold<0>, dim3(fg), block, 0, s, k);
-    else
-      hipLaunchKernelGGL(k_kurt_fold_t<0>, dim3(fg), block, 0, s, k);
-  }
-  if (k.vec)
-    hipLaunchKernelGGL((k_kurt_pass<1, 1>), grid, block, 0, s, k);
-  else
-    hipLaunchKernelGGL((k_kurt_pass<1, 0>), grid, block, 0, s, k);
-  if (k.nchunk > 1) {
-    if (wide)
-      hipLaunchKernelGGL(k_kurt_fold<1>, dim3(fg), block, 0, s, k);
-    else
-      hipLaunchKernelGGL(k_kurt_fold_t<1>, dim3(fg), block, 0, s, k);
-  }
   return hipGetLastError();
 }
 

@@ -1,0 +1,973 @@
+// kurtosis.hip — getkurtosis (src/gbtworkerfunctions.jl:197-202) on gfx950.
+//
+// The reference maps StatsBase.kurtosis over the rows of
+// reshape(data, nchan*nif, ntime) (:199-200), i.e. over time for every
+// (channel, IF):
+//   kurtosis(v) = kurtosis(v, mean(v))
+//   m    = mean(v)             Float32: Base.sum(v) / length(v)
+//   z    = v[i] - m            Float32
+//   z2   = z * z               Float32
+//   cm2 += z2; cm4 += z2 * z2  Float64 accumulators
+//   (cm4 / n) / (cm2 / n)^2 - 3.0
+// Base.sum of a Float32 vector (Base.mapreduce_impl, pairwise_blocksize 1024)
+// splits the index range in halves (left half ceil(len/2)) until a piece
+// holds <= 1024 elements, sums every piece sequentially from its first
+// element, and adds the halves back up the tree in Float32.  Every path here
+// reproduces that Float32 sum bit for bit, so m is the reference's m
+// (oracle/bldp_oracle.c jl_pairwise_sum restates it).
+//
+// The tree is perfect down to level K = pw_level(n), the first level whose
+// pieces ("blocks") hold <= 2048 elements; each block is one leaf (<= 1024)
+// or two leaves split at its midpoint.  Leaves hold >= 512 elements once
+// n > 1024.
+//
+// Paths (the window is read from HBM once on the first three):
+//   nt <= 32    k_kurt_regs : a lane keeps its float4 column in registers and
+//               runs the recipe in order: bit-identical to it.
+//   33..512     k_kurt_mid  : a 64-channel tile in registers over 16 row
+//               groups of consecutive spectra.  The Float32 sum runs through
+//               the row groups in order (lane shuffles inside a wave, LDS
+//               between waves); z, z2 and the Float64 sums follow the recipe,
+//               the 16 partial sums are added in row-group order.
+//   > 512       k_kurt_leaf : one wave per (leaf, 256 channels) streams the
+//               leaf once: its sequential Float32 sum, and Float64 power sums
+//               about its first spectrum, moved to the leaf's own mean.
+//               k_kurt_tree / k_kurt_final_{t,w} add the leaf sums up Julia's
+//               tree (-> m) and merge the central moments pairwise
+//               (Chan et al. / Pebay), then move them from the exact mean to m.
+//               The only difference from the recipe: z^2 and z^4 are exact
+//               (Float64) instead of rounded to Float32 (relative 2^-24 per
+//               term, averaging out); overflow and underflow of the Float32
+//               squares are reproduced from the row's max and min.
+//   unaligned   k_kurt_leafsum + the same tree (sum only) -> m, then the
+//               recipe in a second pass (k_kurt_pass, k_kurt_fold).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "bldp_impl.h"
+
+namespace bldp {
+
+// ---- Julia's pairwise-sum tree (host and device) --------------------------
+// Level of the blocks: the first level whose nodes hold <= 2048 elements.
+__host__ __device__ inline int pw_level(int64_t n) {
+  int K = 0;
+  while (((n + ((int64_t)1 << K) - 1) >> K) > 2048) ++K;
+  return K;
+}
+// Node j of level L of the halving of [0, n): mapreduce_impl's
+// imid = ifirst + (ilast - ifirst) >> 1 gives the left half ceil(len/2).
+__host__ __device__ inline void pw_node(int64_t n, int L, int64_t j, int64_t &lo, int64_t &len) {
+  lo = 0;
+  len = n;
+  for (int l = L - 1; l >= 0; --l) {
+    const int64_t left = (len + 1) >> 1;
+    if ((j >> l) & 1) {
+      lo += left;
+      len -= left;
+    } else {
+      len = left;
+    }
+  }
+}
+// Leaf slot s = 2j + h of block j: a block of <= 1024 elements is one leaf
+// (slot 2j + 1 is empty), a longer one splits at its midpoint.
+__host__ __device__ inline void pw_leaf(int64_t n, int K, int64_t slot, int64_t &lo,
+                                        int64_t &len) {
+  pw_node(n, K, slot >> 1, lo, len);
+  if (len > 1024) {
+    const int64_t left = (len + 1) >> 1;
+    if (slot & 1) {
+      lo += left;
+      len -= left;
+    } else {
+      len = left;
+    }
+  } else if (slot & 1) {
+    lo += len;
+    len = 0;
+  }
+}
+
+namespace {
+
+constexpr int kB = 256;  // 4 waves of 64
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef double d2v __attribute__((ext_vector_type(2)));
+
+int64_t cdivk(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// the window is read once: non-temporal 16-byte loads
+__device__ __forceinline__ float4 ldnt(const float *p) {
+  const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+
+// Pairwise update of (count, mean, M2, M3, M4) with a second set
+// (Chan et al.; Pebay 2008), all central moments about their own means.
+__device__ __forceinline__ void moments_merge(double &na, double &ma, double &a2, double &a3,
+                                              double &a4, double nb, double mb, double b2,
+                                              double b3, double b4) {
+  if (nb == 0.0) return;
+  if (na == 0.0) {
+    na = nb; ma = mb; a2 = b2; a3 = b3; a4 = b4;
+    return;
+  }
+  const double n = na + nb, d = mb - ma, dn = d / n, dn2 = dn * dn, nab = na * nb;
+  const double m4 = a4 + b4 + d * dn2 * dn * nab * (na * na - nab + nb * nb) +
+                    6.0 * dn2 * (na * na * b2 + nb * nb * a2) + 4.0 * dn * (na * b3 - nb * a3);
+  const double m3 = a3 + b3 + d * dn2 * nab * (na - nb) + 3.0 * dn * (na * b2 - nb * a2);
+  const double m2 = a2 + b2 + d * dn * nab;
+  na = n; ma += dn * nb; a2 = m2; a3 = m3; a4 = m4;
+}
+
+// StatsBase's ratio from central moments about the exact mean `ma`: move them
+// to the recipe's Float32 m = S / n (z = x - m = (x - ma) + eps).  The recipe
+// squares z in Float32, so cm2 (cm4) is Inf exactly when the largest z^2 (z^4)
+// overflows and 0 when every one underflows; the largest |x - m| comes from
+// the row's max or min.
+__device__ __forceinline__ double kurt_ratio(int64_t nt, float S, double ma, double a2,
+                                             double a3, double a4, float hi, float lo) {
+  const float m = S / (float)nt;  // mean(v): Float32 sum / length
+  const double n = (double)nt, eps = ma - (double)m, e2 = eps * eps;
+  double cm2 = (a2 + n * e2) / n;
+  double cm4 = (a4 + 4.0 * eps * a3 + 6.0 * e2 * a2 + n * e2 * e2) / n;
+  const float zh = hi - m, zl = lo - m;
+  const float h2 = zh * zh, l2 = zl * zl, h4 = h2 * h2, l4 = l2 * l2;
+  if (isinf(h2) || isinf(l2))
+    cm2 = INFINITY;
+  else if (h2 == 0.0f && l2 == 0.0f)
+    cm2 = 0.0;
+  if (isinf(h4) || isinf(l4))
+    cm4 = INFINITY;
+  else if (h4 == 0.0f && l4 == 0.0f)
+    cm4 = 0.0;
+  return (cm4 / (cm2 * cm2)) - 3.0;
+}
+
+// ---------------------------------------------------------------------------
+// nt <= NTMAX (<= 32): each lane keeps its float4 column of every spectrum in
+// registers and runs the recipe in the recipe's own order, so the result is
+// bit-identical to it.  EXACT (nt == NTMAX, e.g. the 16-spectrum 0000
+// product) is straight-line code: all NTMAX loads issue back to back.
+//   BLDP_KURT_EXACT 1 (default) = use the exact-count instantiation
+#ifndef BLDP_KURT_EXACT
+#define BLDP_KURT_EXACT 1
+#endif
+//   BLDP_KURT_STORE 3 (default) = the wave's 256 Float64 results go through
+//                   LDS so every nt store instruction writes 1 KiB contiguous
+//                   (+2.5% on the 0000 band against 1); 1 = each lane's 32 B as
+//                   two nt 16-byte stores
+#ifndef BLDP_KURT_STORE
+#define BLDP_KURT_STORE 3
+#endif
+template <int NTMAX, bool EXACT>
+__global__ __launch_bounds__(kB) void k_kurt_regs(const KurtArgs k) {
+  const int64_t ncols = k.nc / 4;
+  const int64_t ctiles = (ncols + kB - 1) / kB;
+  const int64_t b = blockIdx.x;
+  const int64_t ib = b / ctiles, col = (b % ctiles) * kB + threadIdx.x;
+  if (col >= ncols) return;
+  const int bank = (int)(ib / k.ni);
+  const int64_t i = ib - (int64_t)bank * k.ni;
+  const float *p = k.in[bank] + k.in_off + i * k.in_ld_i + 4 * col;
+  const int nt = EXACT ? NTMAX : (int)k.nt;
+  const int64_t ld = k.in_ld_t;
+  float4 v[NTMAX];
+#pragma unroll
+  for (int t = 0; t < NTMAX; ++t)
+    if (EXACT || t < nt) v[t] = ldnt(p + t * ld);
+  // Base.sum: sequential Float32 from the first element (nt <= 1024)
+  f2v sa = {v[0].x, v[0].y}, sb = {v[0].z, v[0].w};
+#pragma unroll
+  for (int t = 1; t < NTMAX; ++t)
+    if (EXACT || t < nt) {
+      sa += f2v{v[t].x, v[t].y};
+      sb += f2v{v[t].z, v[t].w};
+    }
+  const float m[4] = {sa.x / (float)nt, sa.y / (float)nt, sb.x / (float)nt, sb.y / (float)nt};
+  double c2[4] = {0, 0, 0, 0}, c4[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int t = 0; t < NTMAX; ++t)
+    if (EXACT || t < nt) {
+      const float x[4] = {v[t].x, v[t].y, v[t].z, v[t].w};
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const float z = x[w] - m[w];  // StatsBase: z, z2 in Float32; Float64 moments
+        const float z2 = z * z;
+        c2[w] += (double)z2;
+        c4[w] += (double)(z2 * z2);
+      }
+    }
+  double r[4];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const double cm2 = c2[w] / (double)nt, cm4 = c4[w] / (double)nt;
+    r[w] = (cm4 / (cm2 * cm2)) - 3.0;
+  }
+  d2v *o = reinterpret_cast<d2v *>(k.out + ib * k.nc + 4 * col);
+  if (BLDP_KURT_STORE == 3 && ncols % 64 == 0 &&
+      (reinterpret_cast<uintptr_t>(k.out + ib * k.nc) & 15) == 0) {
+    // whole wave in range: transpose through this wave's 2 KiB of LDS so each
+    // store instruction writes 1 KiB contiguous (lane L: doubles 2L, 2L+1 of
+    // the wave's 256 outputs, then 128 + 2L, 129 + 2L)
+    __shared__ d2v st[4][128];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    st[wave][2 * lane] = d2v{r[0], r[1]};
+    st[wave][2 * lane + 1] = d2v{r[2], r[3]};
+    __builtin_amdgcn_wave_barrier();
+    const d2v a0 = st[wave][lane], a1 = st[wave][64 + lane];
+    d2v *ow = reinterpret_cast<d2v *>(k.out + ib * k.nc + 4 * (col - lane));
+    __builtin_nontemporal_store(a0, ow + lane);
+    __builtin_nontemporal_store(a1, ow + 64 + lane);
+  } else if ((reinterpret_cast<uintptr_t>(o) & 15) == 0) {
+    __builtin_nontemporal_store(d2v{r[0], r[1]}, o);
+    __builtin_nontemporal_store(d2v{r[2], r[3]}, o + 1);
+  } else {
+    double *od = k.out + ib * k.nc + 4 * col;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) od[w] = r[w];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// 32 < nt <= 16*NR (<= 512, one leaf): a workgroup holds a 64-channel x nt
+// tile in registers.  Thread (rg, c4) = (tid / 16, tid % 16) keeps float4
+// column c4 of the consecutive spectra [rg*nt/16, (rg+1)*nt/16); a
+// wave-instruction reads 4 rows x 256 B.  The sequential Float32 sum visits
+// the row groups in order: the 4 groups of a wave hand the running sum on by
+// lane shuffle, the waves by LDS and a barrier.  Then z, z2 and the Float64
+// sums run over the registers and the 16 partial sums are added through LDS
+// in row-group order.
+template <int NR>
+__global__ __launch_bounds__(kB) void k_kurt_mid(const KurtArgs k) {
+  const int tid = threadIdx.x, c4 = tid & 15, rg = tid >> 4, lane = tid & 63, wave = tid >> 6;
+  const int64_t ncols = k.nc / 4, ctiles = (ncols + 15) / 16;
+  const int64_t b = blockIdx.x;
+  const int64_t ib = b / ctiles, col = (b % ctiles) * 16 + c4;
+  const bool valid = col < ncols;
+  const int bank = (int)(ib / k.ni);
+  const int64_t i = ib - (int64_t)bank * k.ni;
+  const int nt = (int)k.nt;
+  const int r0 = (rg * nt) >> 4, cnt = (((rg + 1) * nt) >> 4) - r0;
+  const int64_t ld = k.in_ld_t;
+  const float *p = k.in[bank] + k.in_off + i * k.in_ld_i + 4 * (valid ? col : 0) + r0 * ld;
+  float4 v[NR];
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+    v[r] = (valid && r < cnt) ? ldnt(p + r * ld) : make_float4(0.f, 0.f, 0.f, 0.f);
+  // Base.sum, sequential over the whole window (nt <= 1024 is one leaf)
+  __shared__ float4 carry[16];
+  f2v sa = {0.f, 0.f}, sb = {0.f, 0.f};
+#pragma unroll 1
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w) {
+      if (w > 0) {
+        const float4 c = carry[c4];
+        sa = f2v{c.x, c.y};
+        sb = f2v{c.z, c.w};
+      }
+#pragma unroll 1
+      for (int g = 0; g < 4; ++g) {
+        if ((lane >> 4) == g) {
+#pragma unroll
+          for (int r = 0; r < NR; ++r)
+            if (r < cnt) {
+              const f2v xa = {v[r].x, v[r].y}, xb = {v[r].z, v[r].w};
+              if (rg == 0 && r == 0) {  // the sum starts from the first element
+                sa = xa;
+                sb = xb;
+              } else {
+                sa += xa;
+                sb += xb;
+              }
+            }
+        }
+        const int src = 16 * g + c4;
+        sa.x = __shfl(sa.x, src, 64);
+        sa.y = __shfl(sa.y, src, 64);
+        sb.x = __shfl(sb.x, src, 64);
+        sb.y = __shfl(sb.y, src, 64);
+      }
+      if (lane < 16) carry[c4] = make_float4(sa.x, sa.y, sb.x, sb.y);
+    }
+    __syncthreads();
+  }
+  const float4 S = carry[c4];
+  const float m[4] = {S.x / (float)nt, S.y / (float)nt, S.z / (float)nt, S.w / (float)nt};
+  __shared__ double part[16][16][8];  // [row group][column][moment x channel]
+  double c2[4] = {0, 0, 0, 0}, cq[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+    if (valid && r < cnt) {
+      const float x[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const float z = x[w] - m[w];  // StatsBase: z, z2 in Float32; Float64 moments
+        const float z2 = z * z;
+        c2[w] += (double)z2;
+        cq[w] += (double)(z2 * z2);
+      }
+    }
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    part[rg][c4][w] = c2[w];
+    part[rg][c4][4 + w] = cq[w];
+  }
+  __syncthreads();
+  if (rg == 0 && valid) {
+    double r[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      double a2 = 0, a4 = 0;
+      for (int q = 0; q < 16; ++q) {
+        a2 += part[q][c4][w];
+        a4 += part[q][c4][4 + w];
+      }
+      const double cm2 = a2 / (double)nt, cm4 = a4 / (double)nt;
+      r[w] = (cm4 / (cm2 * cm2)) - 3.0;
+    }
+    double *o = k.out + ib * k.nc + 4 * col;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) o[w] = r[w];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// nt > 512: one wave per (leaf slot, 64 float4 columns, bank x IF row).  Each
+// lane streams its column down the leaf (<= 1024 spectra, B loads in flight):
+//   * the leaf's sequential Float32 sum (Base.mapreduce_impl's inner loop),
+//   * max and min,
+//   * Float64 power sums of d = x - c about the leaf's first spectrum c.  Any
+//     |c - mean| is at most the largest deviation, which also bounds M4 from
+//     below, so moving the sums to the leaf's mean loses at most ~len ulps.
+// Writes the leaf's (mean, M2, M3, M4) and (sum, max, min), 32 contiguous
+// bytes per lane per quantity.
+//   BLDP_KURT_LEAF_B  spectra in flight per lane
+#ifndef BLDP_KURT_LEAF_B
+#define BLDP_KURT_LEAF_B 8
+#endif
+struct LeafAcc {
+  f2v sa, sb;  // Float32 sums of channels (0,1) and (2,3)
+  float hi[4], lo[4];
+  double c[4], a1[4], a2[4], a3[4], a4[4];
+};
+__device__ __forceinline__ void leaf_step(LeafAcc &A, const float4 q) {
+  A.sa += f2v{q.x, q.y};
+  A.sb += f2v{q.z, q.w};
+  const float x[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    A.hi[w] = fmaxf(A.hi[w], x[w]);
+    A.lo[w] = fminf(A.lo[w], x[w]);
+    const double d = (double)x[w] - A.c[w], d2 = d * d;
+    A.a1[w] += d;
+    A.a2[w] += d2;
+    A.a3[w] = fma(d2, d, A.a3[w]);
+    A.a4[w] = fma(d2, d2, A.a4[w]);
+  }
+}
+
+__global__ __launch_bounds__(kB) void k_kurt_leaf(const KurtArgs k) {
+  constexpr int B = BLDP_KURT_LEAF_B;
+  const int lane = threadIdx.x & 63;
+  const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t seg = u % k.nseg, r = u / k.nseg;
+  const int64_t slot = r % k.nslot, row = r / k.nslot;
+  const int64_t col = seg * 64 + lane;
+  if (row >= k.nrow || col >= k.nc / 4) return;
+  int64_t t0, len;
+  pw_leaf(k.nt, k.K, slot, t0, len);
+  if (len <= 0) return;
+  const int bank = (int)(row / k.ni);
+  const int64_t i = row - (int64_t)bank * k.ni;
+  const int64_t ld = k.in_ld_t;
+  const float *p = k.in[bank] + k.in_off + i * k.in_ld_i + 4 * col + t0 * ld;
+  LeafAcc A;
+  {
+    const float4 x0 = ldnt(p);
+    A.sa = f2v{x0.x, x0.y};
+    A.sb = f2v{x0.z, x0.w};
+    const float x[4] = {x0.x, x0.y, x0.z, x0.w};
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      A.hi[w] = A.lo[w] = x[w];
+      A.c[w] = (double)x[w];
+      A.a1[w] = A.a2[w] = A.a3[w] = A.a4[w] = 0.0;
+    }
+  }
+  p += ld;
+  int64_t rem = len - 1;
+  for (; rem >= B; rem -= B, p += B * ld) {
+    float4 v[B];
+#pragma unroll
+    for (int q = 0; q < B; ++q) v[q] = ldnt(p + q * ld);
+#pragma unroll
+    for (int q = 0; q < B; ++q) leaf_step(A, v[q]);
+  }
+  if (rem > 0) {
+    float4 v[B];
+#pragma unroll
+    for (int q = 0; q < B; ++q)
+      if (q < rem) v[q] = ldnt(p + q * ld);
+#pragma unroll
+    for (int q = 0; q < B; ++q)
+      if (q < rem) leaf_step(A, v[q]);
+  }
+  const int64_t n = k.nrow * k.nc, e = row * k.nc + 4 * col;
+  const double cnt = (double)len;
+  double mo[4][4];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const double dl = A.a1[w] / cnt, dl2 = dl * dl;
+    mo[0][w] = A.c[w] + dl;
+    mo[1][w] = A.a2[w] - A.a1[w] * dl;
+    mo[2][w] = A.a3[w] - 3.0 * dl * A.a2[w] + 2.0 * cnt * dl2 * dl;
+    mo[3][w] = A.a4[w] - 4.0 * dl * A.a3[w] + 6.0 * dl2 * A.a2[w] - 3.0 * cnt * dl2 * dl2;
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    d2v *o = reinterpret_cast<d2v *>(k.pm + (q * k.nslot + slot) * n + e);
+    o[0] = d2v{mo[q][0], mo[q][1]};
+    o[1] = d2v{mo[q][2], mo[q][3]};
+  }
+  f4v *of = reinterpret_cast<f4v *>(k.pf + slot * n + e);
+  of[0] = f4v{A.sa.x, A.sa.y, A.sb.x, A.sb.y};
+  of = reinterpret_cast<f4v *>(k.pf + (k.nslot + slot) * n + e);
+  of[0] = f4v{A.hi[0], A.hi[1], A.hi[2], A.hi[3]};
+  of = reinterpret_cast<f4v *>(k.pf + (2 * k.nslot + slot) * n + e);
+  of[0] = f4v{A.lo[0], A.lo[1], A.lo[2], A.lo[3]};
+}
+
+// Unaligned windows: one lane per (column, leaf) runs the sequential Float32
+// sum of the leaf (any channel step); sums only.
+__global__ __launch_bounds__(kB) void k_kurt_leafsum(const KurtArgs k) {
+  const int64_t ctiles = (k.nc + kB - 1) / kB;
+  int64_t b = blockIdx.x;
+  const int64_t ct = b % ctiles;
+  b /= ctiles;
+  const int64_t slot = b % k.nslot, row = b / k.nslot;
+  const int64_t c = ct * kB + threadIdx.x;
+  if (row >= k.nrow || c >= k.nc) return;
+  int64_t t0, len;
+  pw_leaf(k.nt, k.K, slot, t0, len);
+  if (len <= 0) return;
+  const int bank = (int)(row / k.ni);
+  const int64_t i = row - (int64_t)bank * k.ni;
+  const int64_t ld = k.in_ld_t;
+  const float *p = k.in[bank] + k.in_off + i * k.in_ld_i + c * k.in_cs + t0 * ld;
+  float s = p[0];
+  int64_t t = 1;
+  for (; t + 8 <= len; t += 8) {
+    float v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = p[(t + q) * ld];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s += v[q];
+  }
+  for (; t < len; ++t) s += p[t * ld];
+  k.pf[slot * (k.nrow * k.nc) + row * k.nc + c] = s;
+}
+
+// ---- the tree: leaf sums -> m, leaf moments -> row moments ----------------
+// Partials of the nodes of one level: component q of node j of output e at
+// [(q * nodes + j) * n + e] (pm: mean, M2, M3, M4; pf: sum, max, min).
+struct TreeIO {
+  const double *pm;
+  const float *pf;
+  int64_t nin;   // input nodes (FIRST: leaf slots)
+  double *pmo;
+  float *pfo;
+  int64_t nout;  // output nodes
+  int L;         // level of the input nodes (FIRST: K, blocks built from leaves)
+};
+struct Node {
+  float S, hi, lo;
+  double n, m, a2, a3, a4;
+};
+// Input node j of output e.  FIRST: block j of leaves 2j and 2j+1
+// (mapreduce_impl's op(v1, v2) = v1 + v2 for a split block).
+template <bool FIRST, bool MOM>
+__device__ __forceinline__ Node load_node(const KurtArgs &k, const TreeIO &io, int64_t n,
+                                          int64_t e, int64_t j) {
+  Node x;
+  x.hi = -INFINITY;
+  x.lo = INFINITY;
+  x.n = x.m = x.a2 = x.a3 = x.a4 = 0.0;
+  const int64_t ns = io.nin * n;  // stride between components
+  if (FIRST) {
+    int64_t lo0, len0, lo1, len1;
+    pw_leaf(k.nt, k.K, 2 * j, lo0, len0);
+    pw_leaf(k.nt, k.K, 2 * j + 1, lo1, len1);
+    const int64_t s0 = 2 * j * n + e, s1 = s0 + n;
+    x.S = io.pf[s0];
+    if (MOM) {
+      x.hi = io.pf[ns + s0];
+      x.lo = io.pf[2 * ns + s0];
+      x.n = (double)len0;
+      x.m = io.pm[s0];
+      x.a2 = io.pm[ns + s0];
+      x.a3 = io.pm[2 * ns + s0];
+      x.a4 = io.pm[3 * ns + s0];
+    }
+    if (len1 > 0) {
+      x.S = x.S + io.pf[s1];
+      if (MOM) {
+        x.hi = fmaxf(x.hi, io.pf[ns + s1]);
+        x.lo = fminf(x.lo, io.pf[2 * ns + s1]);
+        moments_merge(x.n, x.m, x.a2, x.a3, x.a4, (double)len1, io.pm[s1], io.pm[ns + s1],
+                      io.pm[2 * ns + s1], io.pm[3 * ns + s1]);
+      }
+    }
+  } else {
+    const int64_t s0 = j * n + e;
+    x.S = io.pf[s0];
+    if (MOM) {
+      int64_t lo, len;
+      pw_node(k.nt, io.L, j, lo, len);
+      x.hi = io.pf[ns + s0];
+      x.lo = io.pf[2 * ns + s0];
+      x.n = (double)len;
+      x.m = io.pm[s0];
+      x.a2 = io.pm[ns + s0];
+      x.a3 = io.pm[2 * ns + s0];
+      x.a4 = io.pm[3 * ns + s0];
+    }
+  }
+  return x;
+}
+
+// Q consecutive input nodes of one output into one node (a perfect subtree):
+// the sums pairwise in tree order, the moments merged in node order.
+template <int Q, bool FIRST, bool MOM>
+__device__ __forceinline__ Node fold_nodes(const KurtArgs &k, const TreeIO &io, int64_t n,
+                                           int64_t e, int64_t g) {
+  float s[Q];
+  Node acc;
+  acc.hi = -INFINITY;
+  acc.lo = INFINITY;
+  acc.n = acc.m = acc.a2 = acc.a3 = acc.a4 = 0.0;
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const Node x = load_node<FIRST, MOM>(k, io, n, e, g * Q + q);
+    s[q] = x.S;
+    if (MOM) {
+      acc.hi = fmaxf(acc.hi, x.hi);
+      acc.lo = fminf(acc.lo, x.lo);
+      moments_merge(acc.n, acc.m, acc.a2, acc.a3, acc.a4, x.n, x.m, x.a2, x.a3, x.a4);
+    }
+  }
+#pragma unroll
+  for (int w = 1; w < Q; w *= 2)
+#pragma unroll
+    for (int q = 0; q < Q; q += 2 * w) s[q] = s[q] + s[q + w];
+  acc.S = s[0];
+  return acc;
+}
+
+template <int Q, bool FIRST, bool MOM>
+__global__ __launch_bounds__(kB) void k_kurt_tree(const KurtArgs k, const TreeIO io) {
+  const int64_t n = k.nrow * k.nc, total = io.nout * n;
+  for (int64_t x = (int64_t)blockIdx.x * kB + threadIdx.x; x < total;
+       x += (int64_t)gridDim.x * kB) {
+    const int64_t g = x / n, e = x - g * n;
+    const Node a = fold_nodes<Q, FIRST, MOM>(k, io, n, e, g);
+    const int64_t ns = io.nout * n, s0 = g * n + e;
+    io.pfo[s0] = a.S;
+    if (MOM) {
+      io.pfo[ns + s0] = a.hi;
+      io.pfo[2 * ns + s0] = a.lo;
+      io.pmo[s0] = a.m;
+      io.pmo[ns + s0] = a.a2;
+      io.pmo[2 * ns + s0] = a.a3;
+      io.pmo[3 * ns + s0] = a.a4;
+    }
+  }
+}
+
+// Last level, one thread per output (Q = all remaining nodes): MOM -> the
+// excess kurtosis, else the Float32 mean for the two-pass path.
+template <int Q, bool FIRST, bool MOM>
+__global__ __launch_bounds__(kB) void k_kurt_final_t(const KurtArgs k, const TreeIO io) {
+  const int64_t n = k.nrow * k.nc;
+  for (int64_t e = (int64_t)blockIdx.x * kB + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * kB) {
+    const Node a = fold_nodes<Q, FIRST, MOM>(k, io, n, e, 0);
+    if (MOM)
+      k.out[e] = kurt_ratio(k.nt, a.S, a.m, a.a2, a.a3, a.a4, a.hi, a.lo);
+    else
+      k.mean[e] = a.S / (float)k.nt;
+  }
+}
+
+// Last level, one wave per output, lane j holding node j (<= 64 nodes): an xor
+// butterfly over consecutive lanes is exactly the perfect tree of the sums
+// (Float32 addition commutes); the moments merge the lower lane's first, so
+// both lanes of a pair agree.
+template <bool FIRST, bool MOM>
+__global__ __launch_bounds__(kB) void k_kurt_final_w(const KurtArgs k, const TreeIO io) {
+  const int lane = threadIdx.x & 63;
+  const int64_t n = k.nrow * k.nc;
+  const int nn = 1 << io.L;
+  for (int64_t e = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); e < n;
+       e += (int64_t)gridDim.x * 4) {
+    Node a;
+    a.S = 0.0f;
+    a.hi = -INFINITY;
+    a.lo = INFINITY;
+    a.n = a.m = a.a2 = a.a3 = a.a4 = 0.0;
+    if (lane < nn) a = load_node<FIRST, MOM>(k, io, n, e, lane);
+    for (int off = 1; off < nn; off <<= 1) {
+      a.S = a.S + __shfl_xor(a.S, off, 64);
+      if (MOM) {
+        a.hi = fmaxf(a.hi, __shfl_xor(a.hi, off, 64));
+        a.lo = fminf(a.lo, __shfl_xor(a.lo, off, 64));
+        const double nb = __shfl_xor(a.n, off, 64), mb = __shfl_xor(a.m, off, 64);
+        const double b2 = __shfl_xor(a.a2, off, 64), b3 = __shfl_xor(a.a3, off, 64);
+        const double b4 = __shfl_xor(a.a4, off, 64);
+        if (lane & off) {  // the partner is the lower lane: it goes first
+          double xn = nb, xm = mb, x2 = b2, x3 = b3, x4 = b4;
+          moments_merge(xn, xm, x2, x3, x4, a.n, a.m, a.a2, a.a3, a.a4);
+          a.n = xn; a.m = xm; a.a2 = x2; a.a3 = x3; a.a4 = x4;
+        } else {
+          moments_merge(a.n, a.m, a.a2, a.a3, a.a4, nb, mb, b2, b3, b4);
+        }
+      }
+    }
+    if (lane == 0) {
+      if (MOM)
+        k.out[e] = kurt_ratio(k.nt, a.S, a.m, a.a2, a.a3, a.a4, a.hi, a.lo);
+      else
+        k.mean[e] = a.S / (float)k.nt;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Two-pass recipe for unaligned windows, given the Float32 mean: one lane per
+// column, `ts` waves of a workgroup splitting the spectra of a tile (4/ts
+// tiles per workgroup), 8 loads in flight, Float64 partials combined through
+// LDS in wave order.  With one time chunk the ratio is written here;
+// otherwise chunks are folded in a fixed order by k_kurt_fold.
+//   BLDP_KURT_PASS_MAXWAVES  cap on resident waves per SIMD (0 = none)
+#ifndef BLDP_KURT_PASS_MAXWAVES
+#define BLDP_KURT_PASS_MAXWAVES 4
+#endif
+__global__ __launch_bounds__(kB)
+#if BLDP_KURT_PASS_MAXWAVES > 0
+__attribute__((amdgpu_waves_per_eu(1, BLDP_KURT_PASS_MAXWAVES)))
+#endif
+void k_kurt_pass(const KurtArgs k) {
+  constexpr int B = 8;  // spectra in flight per lane
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ts = k.ts, wt = wave / ts, tsi = wave - wt * ts;
+  const int64_t ctiles = (k.nc + 63) / 64, tpb = 4 / ts;
+  const int64_t cblocks = (ctiles + tpb - 1) / tpb;
+  int64_t b = blockIdx.x;
+  const int64_t cb = b % cblocks;
+  b /= cblocks;
+  const int64_t ib = b % k.nrow, chunk = b / k.nrow;  // (bank, IF) row, time chunk
+  const int bank = (int)(ib / k.ni);
+  const int64_t i = ib - (int64_t)bank * k.ni;
+  const int64_t col = (cb * tpb + wt) * 64 + lane;
+  const bool valid = col < k.nc;
+  const int64_t r0 = chunk * k.rows_per_chunk, r1 = min(k.nt, r0 + k.rows_per_chunk);
+  const int64_t e = ib * k.nc + col;
+  double a2 = 0.0, a4 = 0.0;
+  if (valid) {
+    const float *p = k.in[bank] + k.in_off + i * k.in_ld_i + (r0 + tsi) * k.in_ld_t + col * k.in_cs;
+    const float m = k.mean[e];
+    int64_t n = r1 - r0 - tsi;
+    n = n > 0 ? (n + ts - 1) / ts : 0;
+    const int64_t st = (int64_t)ts * k.in_ld_t;
+    for (; n > 0; n -= B, p += B * st) {
+      float v[B];  // predicated batch: spectra past the end read as the mean (z = 0)
+#pragma unroll
+      for (int u = 0; u < B; ++u) v[u] = u < n ? p[u * st] : m;
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        // StatsBase: z = v[i] - m; z2 = z*z (Float32); cm2 += z2; cm4 += z2*z2
+        const float z = v[u] - m;
+        const float z2 = z * z;
+        a2 += (double)z2;
+        a4 += (double)(z2 * z2);
+      }
+    }
+  }
+  if (ts > 1) {
+    __shared__ double red[4][2][64];
+    red[wave][0][lane] = a2;
+    red[wave][1][lane] = a4;
+    __syncthreads();
+    if (tsi == 0)
+      for (int q = 1; q < ts; ++q) {
+        a2 += red[wave + q][0][lane];
+        a4 += red[wave + q][1][lane];
+      }
+  }
+  if (tsi == 0 && valid) {
+    const int64_t n = k.nrow * k.nc;
+    if (k.nchunk == 1) {
+      const double cm2 = a2 / (double)k.nt, cm4 = a4 / (double)k.nt;
+      k.out[e] = (cm4 / (cm2 * cm2)) - 3.0;
+    } else {
+      k.ws_mom[(chunk * 2) * n + e] = a2;
+      k.ws_mom[(chunk * 2 + 1) * n + e] = a4;
+    }
+  }
+}
+
+// Fold the time-chunk partials of every output, chunks in order.
+__global__ __launch_bounds__(kB) void k_kurt_fold(const KurtArgs k) {
+  const int64_t n = k.nrow * k.nc;
+  for (int64_t e = (int64_t)blockIdx.x * kB + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * kB) {
+    double a = 0.0, c = 0.0;
+    for (int ch = 0; ch < k.nchunk; ++ch) {
+      a += k.ws_mom[(ch * 2) * n + e];
+      c += k.ws_mom[(ch * 2 + 1) * n + e];
+    }
+    const double cm2 = a / (double)k.nt, cm4 = c / (double)k.nt;
+    k.out[e] = (cm4 / (cm2 * cm2)) - 3.0;
+  }
+}
+
+__global__ __launch_bounds__(kB) void k_fill_nan(double *out, int64_t n) {
+  for (int64_t e = (int64_t)blockIdx.x * kB + threadIdx.x; e < n; e += (int64_t)gridDim.x * kB)
+    out[e] = NAN;
+}
+
+// ---- host side -------------------------------------------------------------
+//   BLDP_KURT_MID_NR rows per thread of the largest k_kurt_mid instantiation
+//                   (windows up to 16 x this many spectra use it, <= 32)
+#ifndef BLDP_KURT_MID_NR
+#define BLDP_KURT_MID_NR 32
+#endif
+
+enum KPath { KP_REGS = 0, KP_MID = 1, KP_LEAF = 2, KP_TWOPASS = 3 };
+
+int path_of(const KurtArgs &k) {
+  if (k.vec && k.nt <= 32) return KP_REGS;
+  if (k.vec && k.nt <= 16 * BLDP_KURT_MID_NR) return KP_MID;
+  if (k.vec) return KP_LEAF;
+  return KP_TWOPASS;
+}
+
+// Workspace regions: A holds the leaf partials, B the first tree level's;
+// later tree levels alternate between them (each is smaller than A).
+struct KLayout {
+  size_t a_pm, a_pf, b_pm, b_pf, mean, mom, total;
+};
+size_t up256(size_t b) { return (b + 255) & ~(size_t)255; }
+KLayout layout(const KurtArgs &k) {
+  KLayout L{};
+  const size_t n = (size_t)k.nrow * k.nc, ns = (size_t)k.nslot, nb = ns / 2;
+  const int p = path_of(k);
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    const size_t o = off;
+    off += up256(bytes);
+    return o;
+  };
+  if (p == KP_LEAF) {
+    L.a_pm = take(4 * ns * n * sizeof(double));
+    L.a_pf = take(3 * ns * n * sizeof(float));
+    L.b_pm = take(4 * nb * n * sizeof(double));
+    L.b_pf = take(3 * nb * n * sizeof(float));
+  } else if (p == KP_TWOPASS) {
+    L.a_pf = take(ns * n * sizeof(float));
+    L.b_pf = take(nb * n * sizeof(float));
+    L.mean = take(n * sizeof(float));
+    L.mom = k.nchunk > 1 ? take(2 * (size_t)k.nchunk * n * sizeof(double)) : off;
+  }
+  L.total = off;
+  return L;
+}
+
+template <bool MOM>
+hipError_t launch_tree_pass(const KurtArgs &k, const TreeIO &io, int q, bool first, hipStream_t s) {
+  const int64_t total = io.nout * k.nrow * k.nc;
+  const dim3 g((unsigned)std::min<int64_t>(cdivk(total, kB), 1 << 20)), b(kB);
+#define BLDP_TREE(Q)                                                          \
+  if (first)                                                                  \
+    hipLaunchKernelGGL((k_kurt_tree<Q, true, MOM>), g, b, 0, s, k, io);       \
+  else                                                                        \
+    hipLaunchKernelGGL((k_kurt_tree<Q, false, MOM>), g, b, 0, s, k, io);
+  switch (q) {
+    case 1: BLDP_TREE(2) break;
+    case 2: BLDP_TREE(4) break;
+    case 3: BLDP_TREE(8) break;
+    case 4: BLDP_TREE(16) break;
+    default: return hipErrorInvalidValue;
+  }
+#undef BLDP_TREE
+  return hipGetLastError();
+}
+
+template <bool MOM>
+hipError_t launch_final(const KurtArgs &k, const TreeIO &io, bool first, hipStream_t s) {
+  const int64_t n = k.nrow * k.nc;
+  const dim3 b(kB);
+  if (io.L >= 3) {
+    const dim3 g((unsigned)std::min<int64_t>(cdivk(n, 4), 1 << 20));
+    if (first)
+      hipLaunchKernelGGL((k_kurt_final_w<true, MOM>), g, b, 0, s, k, io);
+    else
+      hipLaunchKernelGGL((k_kurt_final_w<false, MOM>), g, b, 0, s, k, io);
+    return hipGetLastError();
+  }
+  const dim3 g((unsigned)std::min<int64_t>(cdivk(n, kB), 1 << 20));
+#define BLDP_FINAL(Q)                                                         \
+  if (first)                                                                  \
+    hipLaunchKernelGGL((k_kurt_final_t<Q, true, MOM>), g, b, 0, s, k, io);    \
+  else                                                                        \
+    hipLaunchKernelGGL((k_kurt_final_t<Q, false, MOM>), g, b, 0, s, k, io);
+  switch (io.L) {
+    case 0: BLDP_FINAL(1) break;
+    case 1: BLDP_FINAL(2) break;
+    case 2: BLDP_FINAL(4) break;
+    default: return hipErrorInvalidValue;
+  }
+#undef BLDP_FINAL
+  return hipGetLastError();
+}
+
+// Leaf partials in region A -> the row results.  Passes of up to 4 levels
+// (16 nodes per thread) run while more than 64 nodes remain; the last <= 64
+// nodes go to one wave per output (or one thread when <= 4 remain).
+template <bool MOM>
+hipError_t launch_tree(const KurtArgs &k, char *ws, const KLayout &L, hipStream_t s) {
+  double *pm[2] = {reinterpret_cast<double *>(ws + L.a_pm), reinterpret_cast<double *>(ws + L.b_pm)};
+  float *pf[2] = {reinterpret_cast<float *>(ws + L.a_pf), reinterpret_cast<float *>(ws + L.b_pf)};
+  TreeIO io{};
+  int cur = 0;
+  io.pm = pm[0];
+  io.pf = pf[0];
+  io.nin = k.nslot;
+  io.L = k.K;
+  bool first = true;
+  while (io.L > 6) {
+    const int q = std::min(4, io.L - 6);
+    io.nout = (int64_t)1 << (io.L - q);
+    io.pmo = pm[1 - cur];
+    io.pfo = pf[1 - cur];
+    hipError_t e = launch_tree_pass<MOM>(k, io, q, first, s);
+    if (e != hipSuccess) return e;
+    cur = 1 - cur;
+    io.pm = pm[cur];
+    io.pf = pf[cur];
+    io.nin = io.nout;
+    io.L -= q;
+    first = false;
+  }
+  return launch_final<MOM>(k, io, first, s);
+}
+
+}  // namespace
+
+void plan_kurtosis(KurtArgs &k, int num_cus) {
+  k.K = pw_level(std::max<int64_t>(k.nt, 1));
+  k.nslot = (int64_t)2 << k.K;
+  k.nseg = cdivk(k.nc / 4, 64);
+  // two-pass z pass: waves splitting the spectra of a tile, >= 16 spectra per wave
+  k.ts = 1;
+  while (k.ts < 4 && k.nt >= (int64_t)32 * k.ts) k.ts *= 2;
+  const int64_t tiles = cdivk(cdivk(k.nc, 64), 4 / k.ts) * k.nrow;  // workgroups
+  const int64_t target = (int64_t)num_cus * 8;
+  int64_t nchunk = 1;
+  if (tiles > 0 && tiles < target)  // (empty windows: no split)
+    nchunk = std::min<int64_t>(cdivk(target, tiles), k.nt / (16 * k.ts));
+  nchunk = std::max<int64_t>(nchunk, 1);
+  k.rows_per_chunk = std::max<int64_t>(1, cdivk(k.nt, nchunk));
+  k.nchunk = (int32_t)std::max<int64_t>(1, cdivk(k.nt, k.rows_per_chunk));
+}
+
+int kurtosis_path(const KurtArgs &k) { return path_of(k); }
+
+size_t kurtosis_ws_bytes(const KurtArgs &k) { return layout(k).total; }
+
+hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s) {
+  const int64_t n = k.nrow * k.nc;
+  if (n == 0) return hipSuccess;
+  const dim3 block(kB);
+  const int p = path_of(k);
+  if (k.nt == 0) {  // mean of nothing: StatsBase gives 0/0 - 3 = NaN
+    const unsigned g = (unsigned)std::min<int64_t>(cdivk(n, kB), 16384);
+    hipLaunchKernelGGL(k_fill_nan, dim3(g), block, 0, s, k.out, n);
+    return hipGetLastError();
+  }
+  const int64_t ncols = k.nc / 4;
+  if (p == KP_REGS) {
+    const dim3 g1((unsigned)(cdivk(ncols, kB) * k.nrow));
+    if (BLDP_KURT_EXACT && k.nt == 16)
+      hipLaunchKernelGGL((k_kurt_regs<16, true>), g1, block, 0, s, k);
+    else if (BLDP_KURT_EXACT && k.nt == 32)
+      hipLaunchKernelGGL((k_kurt_regs<32, true>), g1, block, 0, s, k);
+    else if (k.nt <= 16)
+      hipLaunchKernelGGL((k_kurt_regs<16, false>), g1, block, 0, s, k);
+    else
+      hipLaunchKernelGGL((k_kurt_regs<32, false>), g1, block, 0, s, k);
+    return hipGetLastError();
+  }
+  if (p == KP_MID) {
+    const dim3 g1((unsigned)(cdivk(ncols, 16) * k.nrow));
+    if (k.nt <= 128)
+      hipLaunchKernelGGL(k_kurt_mid<8>, g1, block, 0, s, k);
+    else if (k.nt <= 256)
+      hipLaunchKernelGGL(k_kurt_mid<16>, g1, block, 0, s, k);
+    else if (k.nt <= 384)
+      hipLaunchKernelGGL(k_kurt_mid<24>, g1, block, 0, s, k);
+    else
+      hipLaunchKernelGGL(k_kurt_mid<32>, g1, block, 0, s, k);
+    return hipGetLastError();
+  }
+  const KLayout L = layout(k);
+  if (p == KP_LEAF) {
+    k.pm = reinterpret_cast<double *>(ws + L.a_pm);
+    k.pf = reinterpret_cast<float *>(ws + L.a_pf);
+    const dim3 g1((unsigned)cdivk(k.nrow * k.nslot * k.nseg, 4));
+    hipLaunchKernelGGL(k_kurt_leaf, g1, block, 0, s, k);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return launch_tree<true>(k, ws, L, s);
+  }
+  // unaligned: Float32 mean through the tree, then the z pass
+  k.pf = reinterpret_cast<float *>(ws + L.a_pf);
+  k.mean = reinterpret_cast<float *>(ws + L.mean);
+  k.ws_mom = reinterpret_cast<double *>(ws + L.mom);
+  {
+    const dim3 g0((unsigned)(cdivk(k.nc, kB) * k.nrow * k.nslot));
+    hipLaunchKernelGGL(k_kurt_leafsum, g0, block, 0, s, k);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    e = launch_tree<false>(k, ws, L, s);
+    if (e != hipSuccess) return e;
+  }
+  const dim3 grid((unsigned)(cdivk(cdivk(k.nc, 64), 4 / k.ts) * k.nrow * k.nchunk));
+  hipLaunchKernelGGL(k_kurt_pass, grid, block, 0, s, k);
+  if (k.nchunk > 1) {
+    const unsigned fg = (unsigned)std::min<int64_t>(cdivk(n, kB), 16384);
+    hipLaunchKernelGGL(k_kurt_fold, dim3(fg), block, 0, s, k);
+  }
+  return hipGetLastError();
+}
+
+// The largest grid of the plan, for the ABI's one-launch check.
+int64_t kurtosis_max_grid(const KurtArgs &k) {
+  const int p = path_of(k);
+  const int64_t ncols = k.nc / 4;
+  switch (p) {
+    case KP_REGS: return cdivk(ncols, kB) * k.nrow;
+    case KP_MID: return cdivk(ncols, 16) * k.nrow;
+    case KP_LEAF: return cdivk(k.nrow * k.nslot * k.nseg, 4);
+    default:
+      return std::max(cdivk(k.nc, kB) * k.nrow * k.nslot,
+                      cdivk(cdivk(k.nc, 64), 4 / k.ts) * k.nrow * k.nchunk);
+  }
+}
+
+}  // namespace bldp

@@ -320,6 +320,20 @@ def kurtosis(x, win=None, stream=None):
     return out
 
 
+def kurtosis_plan(x, win=None) -> dict:
+    """Kurtosis plan for this tensor and window: path ("regs", "mid", "leaf",
+    "twopass"), K (level of the pairwise-sum blocks), leaf slots, workspace."""
+    L = _lib.lib()
+    shape = tuple(x.shape)
+    _check_bounds(win, shape)
+    ptr, nchan, nif, ntime = _abi_dims(x)
+    info = (ctypes.c_int64 * 4)()
+    keep, wp = _lib.win_arg(_full_win(win, shape))
+    _lib.check(L.bldp_kurtosis_plan_f32(ptr, nchan, nif, ntime, wp, info), "bldp_kurtosis_plan_f32")
+    return {"path": _lib.KURT_PATHS[info[0]], "K": info[1], "leaf_slots": info[2],
+            "workspace_bytes": info[3]}
+
+
 def band_kurtosis(banks, win=None, stream=None):
     """Kurtosis of every bank of a band on one GPU in one set of launches;
     returns a list of (nc, ni) float64 tensors (views of one buffer)."""

@@ -178,6 +178,12 @@ BLDP_API int bldp_despike_f32(float *data, int64_t nchan, int64_t nif, int64_t n
  * out is (nc, ni) float64 on the device. workspace: device scratch of
  * bldp_kurtosis_workspace_size() bytes, or NULL for a library-cached one. */
 BLDP_API size_t bldp_kurtosis_workspace_size(int64_t nchan, int64_t nif, int64_t ntime, const int64_t *win);
+/* Introspection (tests/bench): the kurtosis plan for this pointer and window.
+ * info = {path (0 registers, 1 register tile, 2 streamed leaves + tree
+ * merge, 3 two passes), K (level of the pairwise-sum blocks), leaf slots,
+ * workspace bytes}.  Launches nothing. */
+BLDP_API int bldp_kurtosis_plan_f32(const float *in, int64_t nchan, int64_t nif, int64_t ntime,
+                                    const int64_t *win, int64_t info[4]);
 BLDP_API int bldp_kurtosis_f32(const float *in, int64_t nchan, int64_t nif, int64_t ntime,
                       const int64_t *win, double *out, void *workspace, void *stream);
 

@@ -172,6 +172,21 @@ int oracle_kurtosis(const float *in, int64_t nchan, int64_t nif, int64_t ntime,
   return 0;
 }
 
+/* mean(v) of every (channel, IF) row of the window: StatsBase's m, the
+ * Float32 pairwise sum over time / length (Statistics.mean -> sum / n). */
+int oracle_mean_f32(const float *in, int64_t nchan, int64_t nif, int64_t ntime,
+                    const int64_t *win, float *out) {
+  geo_t g;
+  int rc = resolve(nchan, nif, ntime, win, &g);
+  if (rc) return rc;
+  for (int64_t i = 0; i < g.ni; ++i)
+    for (int64_t c = 0; c < g.nc; ++c) {
+      const float *p = in + g.off + i * g.ldi + c * g.cs;
+      out[c + g.nc * i] = g.nt > 0 ? jl_pairwise_sum(p, g.ldt, 0, g.nt - 1) / (float)g.nt : NAN;
+    }
+  return 0;
+}
+
 /* reduce(vcat, banks) along dim 1 (src/gbt.jl:103): banks are (nc, nif, nt)
  * each, output (nbank*nc, nif, nt). */
 int oracle_stitch(int nbank, const float *const *banks, int64_t nc, int64_t nif, int64_t nt,

@@ -67,6 +67,8 @@ def lib():
         L.oracle_reduce.restype = I
         L.oracle_kurtosis.argtypes = [P, I64, I64, I64, P, P]
         L.oracle_kurtosis.restype = I
+        L.oracle_mean_f32.argtypes = [P, I64, I64, I64, P, P]
+        L.oracle_mean_f32.restype = I
         L.oracle_stitch.argtypes = [I, P, I64, I64, I64, P]
         L.oracle_stitch.restype = I
         L.oracle_despike.argtypes = [P, I64, I64, I64, I64]
@@ -135,6 +137,39 @@ def kurtosis(a, win=None) -> np.ndarray:
                                out.ctypes.data)
     _check(rc, "oracle_kurtosis")
     return out
+
+
+def mean_f32(a, win=None) -> np.ndarray:
+    """StatsBase's m of every (channel, IF) row: Julia's Float32 pairwise sum
+    over time / length; (nc, ni) float32."""
+    a = _fa(a)
+    nc, ni, nt = window_shape(a.shape, win)
+    out = np.empty((nc, ni), dtype=np.float32, order="F")
+    keep, wp = _win(win)
+    rc = lib().oracle_mean_f32(a.ctypes.data, a.shape[0], a.shape[1], a.shape[2], wp,
+                               out.ctypes.data)
+    _check(rc, "oracle_mean_f32")
+    return out
+
+
+def py_pairwise_sum(v) -> np.float32:
+    """Base.mapreduce_impl(identity, +, v, 1, n) line by line (pure Python
+    loops over np.float32 scalars; small n only): the third restatement of
+    Julia's Float32 sum, written from base/reduce.jl's structure."""
+    v = [np.float32(x) for x in v]
+
+    def impl(ifirst, ilast, blksize=1024):
+        if ifirst == ilast:
+            return v[ifirst]
+        if ifirst + blksize > ilast:
+            a = v[ifirst] + v[ifirst + 1]
+            for i in range(ifirst + 2, ilast + 1):
+                a = np.float32(a + v[i])
+            return np.float32(a)
+        imid = ifirst + ((ilast - ifirst) >> 1)
+        return np.float32(impl(ifirst, imid) + impl(imid + 1, ilast))
+
+    return impl(0, len(v) - 1)
 
 
 def stitch(banks) -> np.ndarray:
@@ -250,17 +285,38 @@ def np_reduce(a, fqavby=1, tavby=1, op="sum", win=None) -> np.ndarray:
     return np_tavby(np_fqav(w, int(fqavby), op), int(tavby), op)
 
 
+def np_pairwise_sum(rows: np.ndarray) -> np.ndarray:
+    """Base.sum of each Float32 row (Base.mapreduce_impl, pairwise_blocksize
+    1024): pieces of <= 1024 elements summed sequentially from their first
+    element (np.add.accumulate is a sequential loop), halves split at
+    ifirst + (ilast - ifirst) >> 1 and added back up the tree in Float32."""
+    rows = np.asarray(rows, dtype=np.float32)
+
+    def rec(lo, hi):  # inclusive, 0-based
+        if hi - lo < 1024:
+            return np.add.accumulate(rows[:, lo:hi + 1], axis=1, dtype=np.float32)[:, -1]
+        mid = lo + ((hi - lo) >> 1)
+        return (rec(lo, mid) + rec(mid + 1, hi)).astype(np.float32)
+
+    if rows.shape[1] == 0:
+        return np.full(rows.shape[0], np.nan, dtype=np.float32)
+    return rec(0, rows.shape[1] - 1)
+
+
 def np_kurtosis(a, win=None) -> np.ndarray:
-    """getkurtosis (src/gbtworkerfunctions.jl:197-202), StatsBase recipe."""
+    """getkurtosis (src/gbtworkerfunctions.jl:197-202), StatsBase recipe:
+    m = mean(v) (Float32 pairwise sum / length), z and z2 in Float32,
+    Float64 cm2 and cm4."""
     w = np_window(np.asarray(a, dtype=np.float32), win)
     nc, ni, nt = w.shape
     rows = w.reshape((nc * ni, nt), order="F")  # :199-200
-    m = (rows.astype(np.float64).sum(axis=1).astype(np.float32) / np.float32(nt))[:, None]
-    z = (rows - m).astype(np.float32)
-    z2 = (z * z).astype(np.float32)
-    cm2 = z2.astype(np.float64).sum(axis=1) / nt
-    cm4 = (z2 * z2).astype(np.float64).sum(axis=1) / nt
-    with np.errstate(divide="ignore", invalid="ignore"):
+    with np.errstate(invalid="ignore", over="ignore"):
+        m = (np_pairwise_sum(rows) / np.float32(nt))[:, None]
+    with np.errstate(divide="ignore", invalid="ignore", over="ignore", under="ignore"):
+        z = (rows - m).astype(np.float32)
+        z2 = (z * z).astype(np.float32)
+        cm2 = z2.astype(np.float64).sum(axis=1) / nt
+        cm4 = (z2 * z2).astype(np.float64).sum(axis=1) / nt
         k = cm4 / (cm2 * cm2) - 3.0
     return np.asfortranarray(k.reshape((nc, ni), order="F"))  # :201
 

@@ -57,6 +57,39 @@ def golden():
     return Golden()
 
 
+# Kurtosis of windows > 512 spectra (k_kurt_leaf): the moments are exact
+# Float64 about m, where StatsBase rounds z (2^-24 relative unless x - m is
+# exact), z^2 and z^4 to Float32.  First order, |d cm2 / cm2| <= 3u and
+# |d cm4 / cm4| <= 7u (u = 2^-24), so the ratio cm4/cm2^2 = k + 3 moves by at
+# most 13u relative: |got - want| <= KURT_LEAF_TOL * |want + 3| (5% margin for
+# the second-order terms).  m itself is exact on every path.
+KURT_LEAF_TOL = 13 * 2.0 ** -24 * 1.05
+# register-tile and two-pass paths: the recipe itself, only cm2 and cm4 (sums
+# of nonnegative Float64 terms) added in another order: each within
+# (nt - 1) 2^-53 relative of the exact sum, so k + 3 within 6 nt 2^-53.
+def kurt_sum_tol(nt: int) -> float:
+    return 6.0 * max(nt, 1) * 2.0 ** -53
+
+
+def assert_kurtosis(got, want, path: str, nt: int, msg="") -> None:
+    """GPU kurtosis against the oracle at the tolerance of the path that ran:
+    bit-exact for "regs", kurt_sum_tol for "mid"/"twopass", KURT_LEAF_TOL for
+    "leaf"; NaN and +-Inf positions must match exactly everywhere."""
+    got, want = np.asarray(got, np.float64), np.asarray(want, np.float64)
+    assert got.shape == want.shape, msg
+    fin = np.isfinite(want)
+    assert np.array_equal(np.isnan(got), np.isnan(want)), msg
+    assert np.array_equal(got[~fin & ~np.isnan(want)], want[~fin & ~np.isnan(want)]), msg
+    if path == "regs":
+        assert same_bits(got, want), msg
+        return
+    tol = KURT_LEAF_TOL if path == "leaf" else kurt_sum_tol(nt)
+    err = np.abs(got[fin] - want[fin])
+    lim = tol * np.abs(want[fin] + 3.0)
+    bad = err > lim
+    assert not bad.any(), (msg, path, nt, float(err.max()), float((err / lim).max()))
+
+
 def same_bits(a, b) -> bool:
     """Bit-exact float compare that treats every NaN as equal."""
     a, b = np.asarray(a), np.asarray(b)

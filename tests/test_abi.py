@@ -215,3 +215,83 @@ def test_unchunk_argument_checks(pkg, L):
     assert L.bldp_unchunk_f32(None, i3(0, 1, 64), box0, grid, (ctypes.c_int64 * 9)(*ok), None,
                               None) == pkg._lib.BLDP_EINVAL
     assert L.bldp_unchunk_f32(None, None, box0, grid, None, None, None) == pkg._lib.BLDP_EINVAL
+
+
+def test_kurtosis_empty_windows_long_time_plan_without_fault(pkg, L):
+    """Regression for the kurtosis planner's sibling of the SIGFPE above (an
+    empty channel or IF window with more than 512 spectra divided by zero
+    while sizing the merge): workspace size, plan and the calls themselves are
+    host-side no-ops for empty windows, whatever the time span."""
+    A = 1 << 20
+    ptrs = (ctypes.c_void_p * 2)(A, A)
+    for win in ([5, 0, 1, 0, 2, 1, 0, 5000, 1],      # no channels, 5000 spectra
+                [0, 64, 1, 1, 0, 1, 0, 880000, 1],    # no IFs
+                [0, 0, 1, 0, 0, 1, 10, 600, 1]):
+        keep, wp = pkg._lib.win_arg(win)
+        assert L.bldp_kurtosis_workspace_size(271, 2, 880000, wp) == 0
+        info = (ctypes.c_int64 * 4)()
+        assert L.bldp_kurtosis_plan_f32(A, 271, 2, 880000, wp, info) == 0
+        assert L.bldp_kurtosis_f32(A, 271, 2, 880000, wp, None, None, None) == 0
+        assert L.bldp_band_kurtosis_f32(2, ptrs, 271, 2, 880000, wp, None, None) == 0
+
+
+def _pw_leaves(n):
+    """Leaves of Base.mapreduce_impl's recursion over [0, n) (0-based, inclusive)."""
+    out = []
+
+    def rec(lo, hi):
+        if hi - lo < 1024:
+            out.append((lo, hi - lo + 1))
+        else:
+            mid = lo + ((hi - lo) >> 1)
+            rec(lo, mid)
+            rec(mid + 1, hi)
+
+    rec(0, n - 1)
+    return out
+
+
+@pytest.mark.parametrize("n", [1, 33, 512, 513, 1024, 1025, 2048, 2049, 4095, 4096, 4097,
+                               70001, 131073, 879616, 880000, 2200001])
+def test_kurtosis_plan_pairwise_blocks(pkg, L, n):
+    """bldp_kurtosis_plan_f32 reports the level K of the pairwise-sum blocks
+    and 2^(K+1) leaf slots; slot s = 2j + h of block j (kurtosis.hip pw_leaf,
+    restated here) reproduces exactly the leaves of Julia's recursion, in
+    order, so the kernels' Float32 leaf sums and the perfect tree above them
+    are Base.sum's."""
+    A = 1 << 20
+    info = (ctypes.c_int64 * 4)()
+    assert L.bldp_kurtosis_plan_f32(A, 64, 1, n, None, info) == 0
+    path, K, nslot, ws = list(info)
+    assert path == (0 if n <= 32 else 1 if n <= 512 else 2)
+    assert nslot == 2 << K
+
+    def node(L_, j):
+        lo, ln = 0, n
+        for l_ in range(L_ - 1, -1, -1):
+            left = (ln + 1) >> 1
+            if (j >> l_) & 1:
+                lo, ln = lo + left, ln - left
+            else:
+                ln = left
+        return lo, ln
+
+    leaves = []
+    for s in range(nslot):
+        lo, ln = node(K, s >> 1)
+        if ln > 1024:
+            left = (ln + 1) >> 1
+            lo, ln = (lo + left, ln - left) if s & 1 else (lo, left)
+        elif s & 1:
+            ln = 0
+        if ln:
+            leaves.append((lo, ln))
+    assert leaves == _pw_leaves(n)
+    # the tree above level K is perfect: every node there is split (> 1024)
+    for lev in range(K):
+        assert all(node(lev, j)[1] > 1024 for j in range(1 << lev))
+    if path == 2:
+        assert ws >= 64 * nslot * (4 * 8 + 3 * 4)
+    # the unaligned plan (two passes) for the same window
+    assert L.bldp_kurtosis_plan_f32(A + 4, 64, 1, n, None, info) == 0
+    assert info[0] == 3 and info[1] == K

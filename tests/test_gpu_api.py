@@ -9,7 +9,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import same_bits
+from conftest import assert_kurtosis, same_bits
 
 pytestmark = pytest.mark.gpu
 
@@ -74,8 +74,8 @@ def test_gbt_getdata_getband_kurtosis(pkg, orc, files):
         pkg.GBT.getband(workers, names, (C, C, J(1, 3)), fqavby=64, despike_nfpc=True)
     ks = pkg.GBT.getkurtosis(workers[:2], names[:2], (J(1, 512), C, C))
     for a, k in zip(banks[:2], ks):
-        np.testing.assert_allclose(k, orc.kurtosis(a, [0, 512, 1, 0, 1, 1, 0, 40, 1]),
-                                   rtol=1e-4, atol=1e-5)
+        # (the loosest path bound: the staged buffer's alignment picks the path)
+        assert_kurtosis(k, orc.kurtosis(a, [0, 512, 1, 0, 1, 1, 0, 40, 1]), "leaf", 40)
     hdrs = pkg.GBT.getheaders(workers[:2], names[:2])
     assert hdrs[0]["nfpc"] == 64 and hdrs[1]["nfpc"] == 64  # FBH5 attr / round(187.5/64/abs(foff))
 
@@ -316,7 +316,7 @@ def test_concurrent_host_callers_share_one_gpu(pkg, orc):
     with ThreadPoolExecutor(8) as ex:
         kur = list(ex.map(eng.kurtosis_host, arrs))
     for k, a in zip(kur, arrs):
-        np.testing.assert_allclose(k, orc.kurtosis(a), rtol=1e-4, atol=1e-5)
+        assert_kurtosis(k, orc.kurtosis(a), "leaf", a.shape[2])
 
 
 def test_host_paths_do_not_leak_device_memory(pkg, orc):
@@ -380,7 +380,7 @@ def test_raw_files_stream_to_gpu(pkg, orc, tmp_path, monkeypatch):
             assert same_bits(got, orc.reduce(a, F, T, op, win)), (f, idxs)
         kw = [1024, 1024, 1, 0, 2, 1, 0, 300, 1]
         got = W.getkurtosis(f, (J(1025, 2048), C, C))
-        np.testing.assert_allclose(got, orc.kurtosis(a, kw), rtol=1e-4, atol=1e-5)
+        assert_kurtosis(got, orc.kurtosis(a, kw), "leaf", 300)
     tm = {}
     runs, dshape, rwin = fs.plan_window(a.shape, [0, 4096, 1, 0, 2, 1, 0, 300, 1],
                                         pkg.fbh5.raw_layout(h5)[0])

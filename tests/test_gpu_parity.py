@@ -7,11 +7,18 @@ from __future__ import annotations
 import numpy as np
 import pytest
 
-from conftest import same_bits
+from conftest import assert_kurtosis, same_bits
 
 pytestmark = pytest.mark.gpu
 
 RTOL = 1e-5  # north_star: "within 1e-5 relative for Float32 sums"
+
+
+def kurt_ok(eng, x, win, got, want, msg=""):
+    """Kurtosis at the tolerance of the path the plan picked (conftest)."""
+    shape = tuple(x.shape)
+    nt = shape[2] if win is None else int(win[7])
+    assert_kurtosis(got, want, eng.kurtosis_plan(x, win)["path"], nt, msg)
 
 
 @pytest.fixture(scope="module")
@@ -66,10 +73,8 @@ def test_golden_band_stitch_despike_kurtosis(eng, golden):
     x = dev(eng, np.asfortranarray(a))
     assert same_bits(host(eng, eng.despike(x, ds["nfpc"])), golden.output(ds))
     for c in golden.cases("kurtosis"):
-        got = host(eng, eng.kurtosis(dev(eng, golden.input(c["input"])), c["win"]))
-        want = golden.output(c)
-        assert np.array_equal(np.isnan(got), np.isnan(want))
-        np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-5)
+        x = dev(eng, golden.input(c["input"]))
+        kurt_ok(eng, x, c["win"], host(eng, eng.kurtosis(x, c["win"])), golden.output(c), c)
 
 
 # (nchan, nif, ntime, F, T) covering the vector path at every lanes-per-group
@@ -354,12 +359,12 @@ def test_host_pipeline(eng, orc):
 def test_kurtosis_long_and_strided(eng, orc):
     rng = np.random.default_rng(1)
     a = np.asfortranarray((rng.standard_normal((512, 1, 20000)) ** 2).astype(np.float32) * 1e9)
-    got = host(eng, eng.kurtosis(dev(eng, a)))
-    np.testing.assert_allclose(got, orc.kurtosis(a), rtol=1e-4, atol=1e-5)
+    x = dev(eng, a)
+    kurt_ok(eng, x, None, host(eng, eng.kurtosis(x)), orc.kurtosis(a))
     b = np.asfortranarray((rng.standard_normal((257, 3, 300)) ** 2).astype(np.float32))
     w = [3, 200, 1, 1, 2, 1, 10, 250, 1]
-    got = host(eng, eng.kurtosis(dev(eng, b), w))
-    np.testing.assert_allclose(got, orc.kurtosis(b, w), rtol=1e-4, atol=1e-5)
+    y = dev(eng, b)
+    kurt_ok(eng, y, w, host(eng, eng.kurtosis(y, w)), orc.kurtosis(b, w))
 
 
 def test_synth_integer_kind_matches_oracle(eng, orc):
@@ -425,13 +430,14 @@ def test_band_kurtosis(eng, orc):
     w = [4, 1000, 1, 0, 2, 1, 10, 280, 1]
     ks = eng.band_kurtosis(xs, w)
     assert len(ks) == 5
-    for b, k in zip(banks, ks):
-        np.testing.assert_allclose(host(eng, k), orc.kurtosis(b, w), rtol=1e-4, atol=1e-5)
+    for b, x, k in zip(banks, xs, ks):
+        kurt_ok(eng, x, w, host(eng, k), orc.kurtosis(b, w))
     long = [np.asfortranarray((rng.standard_normal((64, 1, 30000)) ** 2).astype(np.float32))
             for _ in range(3)]
-    ks = eng.band_kurtosis([dev(eng, b) for b in long])  # many time chunks, wave folds
-    for b, k in zip(long, ks):
-        np.testing.assert_allclose(host(eng, k), orc.kurtosis(b), rtol=1e-4, atol=1e-5)
+    xs = [dev(eng, b) for b in long]
+    ks = eng.band_kurtosis(xs)  # many leaves, tree merge
+    for b, x, k in zip(long, xs, ks):
+        kurt_ok(eng, x, None, host(eng, k), orc.kurtosis(b))
 
 
 def test_full_size_cfg4_and_cfg2_banks(eng, orc):
@@ -459,17 +465,16 @@ def test_full_size_cfg4_and_cfg2_banks(eng, orc):
 def test_kurtosis_short_windows(eng, orc, nt, nc, ni):
     """nt <= 32 runs the register-resident single-read kernel (exact-count
     code at 16 and 32; whole waves store through LDS, a partial wave per
-    lane); 33 the two-pass."""
+    lane), bit-exact; 33 the register tile."""
     rng = np.random.default_rng(nt + nc)
     a = np.asfortranarray((rng.standard_normal((nc, ni, nt)) ** 2).astype(np.float32) * 1e6)
-    got = host(eng, eng.kurtosis(dev(eng, a)))
+    x = dev(eng, a)
     want = orc.kurtosis(a)
-    assert np.array_equal(np.isnan(got), np.isnan(want))
-    np.testing.assert_allclose(got, want, rtol=1e-4, atol=1e-5)
-    ks = eng.band_kurtosis([dev(eng, a), dev(eng, a[::-1].copy(order="F"))])
-    np.testing.assert_allclose(host(eng, ks[0]), want, rtol=1e-4, atol=1e-5)
-    np.testing.assert_allclose(host(eng, ks[1]), orc.kurtosis(a[::-1].copy(order="F")),
-                               rtol=1e-4, atol=1e-5)
+    kurt_ok(eng, x, None, host(eng, eng.kurtosis(x)), want)
+    r = a[::-1].copy(order="F")
+    ks = eng.band_kurtosis([x, dev(eng, r)])
+    kurt_ok(eng, x, None, host(eng, ks[0]), want)
+    kurt_ok(eng, x, None, host(eng, ks[1]), orc.kurtosis(r))
 
 
 @pytest.mark.parametrize("nt", [33, 100, 128, 129, 272, 384, 385, 512, 513])
@@ -481,13 +486,12 @@ def test_kurtosis_mid_windows(eng, orc, nt):
     a = np.asfortranarray((rng.standard_normal((1100, 2, nt + 3)) ** 2).astype(np.float32)
                           * 1e6)
     a[5, 1, :] = 7.0  # a constant row -> NaN, as StatsBase
-    got = host(eng, eng.kurtosis(dev(eng, a[:, :, :nt].copy(order="F"))))
-    want = orc.kurtosis(a[:, :, :nt])
-    assert np.array_equal(np.isnan(got), np.isnan(want))
-    np.testing.assert_allclose(got, want, rtol=1e-4, atol=1e-5)
+    b = a[:, :, :nt].copy(order="F")
+    x = dev(eng, b)
+    kurt_ok(eng, x, None, host(eng, eng.kurtosis(x)), orc.kurtosis(b))
     w = [8, 1088, 1, 0, 2, 1, 3, nt, 1]  # idxs = (9:1096, :, 4:nt+3)
-    got = host(eng, eng.kurtosis(dev(eng, a), w))
-    np.testing.assert_allclose(got, orc.kurtosis(a, w), rtol=1e-4, atol=1e-5)
+    y = dev(eng, a)
+    kurt_ok(eng, y, w, host(eng, eng.kurtosis(y, w)), orc.kurtosis(a, w))
 
 
 def test_band_reduce_multi_device_api(eng, orc, pkg):
@@ -582,11 +586,8 @@ def test_kurtosis_random_windows_against_oracle(eng, orc, seed):
         win[6] = int(rng.integers(0, nt))
         win[7] = int(rng.integers(0, nt - win[6] + 1))
         a = np.asfortranarray((rng.standard_normal(shape) ** 2).astype(np.float32) * 100)
-        got = host(eng, eng.kurtosis(dev(eng, a), win))
-        want = orc.kurtosis(a, win)
-        assert got.shape == want.shape, (shape, win)
-        assert np.array_equal(np.isnan(got), np.isnan(want)), (shape, win)
-        np.testing.assert_allclose(got, want, rtol=1e-4, atol=1e-5, err_msg=str((shape, win)))
+        x = dev(eng, a)
+        kurt_ok(eng, x, win, host(eng, eng.kurtosis(x, win)), orc.kurtosis(a, win), (shape, win))
 
 
 @pytest.mark.parametrize("seed", range(3))
@@ -690,29 +691,28 @@ def test_stitch_despike_random(eng, orc, seed):
 
 
 @pytest.mark.parametrize("nt", [513, 1024, 1025, 5007])
-def test_kurtosis_long_windows_chunk_merge(eng, orc, nt):
-    """> 512 spectra: k_kurt_chunk reads each 448-spectrum chunk once and
-    k_kurt_merge combines the chunks' central moments.  Covers a ragged last
-    chunk, a constant row (NaN, as StatsBase), an RFI-like outlier in the
-    first spectrum of a row (StatsBase's Float32 z^4 overflows to Inf there,
-    which the merge reproduces from the chunk extremes), a window with
-    channel/time offsets and a band launch.  (A row whose mean dwarfs its
-    spread is left out: there the oracle's Julia-style pairwise Float32 sum
-    and every GPU path's Float64 sum give different Float32 means.)"""
+def test_kurtosis_long_windows_leaf_merge(eng, orc, nt):
+    """> 512 spectra: k_kurt_leaf streams each leaf of Julia's pairwise sum
+    once and the tree kernels merge them.  Covers ragged leaves, a constant
+    row (NaN, as StatsBase), an RFI-like outlier in the first spectrum of a
+    row (the leaf's shift point; StatsBase's Float32 z^4 overflows to Inf
+    there, which the merge reproduces from the row's extremes), a row whose
+    mean dwarfs its spread, a window with channel/time offsets and a band
+    launch."""
     rng = np.random.default_rng(7000 + nt)
     a = np.asfortranarray((rng.standard_normal((1100, 2, nt + 5)) ** 2).astype(np.float32)
                           * 1e6)
     a[5, 1, :] = 7.0
     a[9, 0, 0] = 3e12
+    a[11, 1, :] += np.float32(3e9)  # mean / sigma ~ 2000
     x = a[:, :, :nt].copy(order="F")
-    got = host(eng, eng.kurtosis(dev(eng, x)))
+    xd = dev(eng, x)
     want = orc.kurtosis(x)
-    assert np.array_equal(np.isnan(got), np.isnan(want))
-    np.testing.assert_allclose(got, want, rtol=1e-4, atol=1e-5)
+    kurt_ok(eng, xd, None, host(eng, eng.kurtosis(xd)), want)
     w = [8, 1088, 1, 0, 2, 1, 5, nt, 1]  # idxs = (9:1096, :, 6:nt+5)
-    got = host(eng, eng.kurtosis(dev(eng, a), w))
-    np.testing.assert_allclose(got, orc.kurtosis(a, w), rtol=1e-4, atol=1e-5)
-    ks = eng.band_kurtosis([dev(eng, x), dev(eng, x[::-1].copy(order="F"))])
-    np.testing.assert_allclose(host(eng, ks[0]), want, rtol=1e-4, atol=1e-5)
-    np.testing.assert_allclose(host(eng, ks[1]), orc.kurtosis(x[::-1].copy(order="F")),
-                               rtol=1e-4, atol=1e-5)
+    y = dev(eng, a)
+    kurt_ok(eng, y, w, host(eng, eng.kurtosis(y, w)), orc.kurtosis(a, w))
+    r = x[::-1].copy(order="F")
+    ks = eng.band_kurtosis([xd, dev(eng, r)])
+    kurt_ok(eng, xd, None, host(eng, ks[0]), want)
+    kurt_ok(eng, xd, None, host(eng, ks[1]), orc.kurtosis(r))

@@ -5,7 +5,7 @@ from __future__ import annotations
 import numpy as np
 import pytest
 
-from conftest import same_bits
+from conftest import KURT_LEAF_TOL, same_bits
 
 
 def test_reference_range_kats(orc, golden):
@@ -73,7 +73,54 @@ def test_c_and_numpy_restatements_agree(orc, seed):
             assert same_bits(c, n)
         else:
             np.testing.assert_allclose(c, n, rtol=1e-6)
-    np.testing.assert_allclose(orc.kurtosis(a), orc.np_kurtosis(a), rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(orc.kurtosis(a), orc.np_kurtosis(a), rtol=1e-12, atol=0)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 15, 16, 17, 1023, 1024, 1025, 2047, 2048, 2049, 3001,
+                               4096, 4097, 70001])
+def test_pairwise_mean_three_restatements(orc, n):
+    """StatsBase's m = Float32 pairwise sum / n (Base.mapreduce_impl,
+    blocksize 1024) from three independent restatements, bit for bit: the C
+    oracle, the NumPy tree, and a literal pure-Python loop (small n)."""
+    rng = np.random.default_rng(n)
+    # integrated-power rows: mean/sigma from 30 to 30000, where the Float32
+    # rounding of every partial sum matters
+    R = np.repeat([30.0, 300.0, 3000.0, 30000.0], 4)[:, None]
+    rows = (1e9 + 1e9 / R * rng.standard_normal((16, n))).astype(np.float32)
+    a = np.asfortranarray(rows.reshape(16, 1, n))
+    c = orc.mean_f32(a)[:, 0]
+    npm = orc.np_pairwise_sum(rows) / np.float32(n)
+    assert same_bits(c, npm.astype(np.float32))
+    if n <= 5000:
+        for r in range(16):
+            assert same_bits(np.float32(orc.py_pairwise_sum(rows[r]) / np.float32(n)), c[r])
+    # a Float64 sum rounded to Float32 is NOT this value for long rows: the
+    # test data does exercise the Float32 rounding of the partial sums
+    if n >= 1025:
+        f64 = (rows.astype(np.float64).sum(axis=1) / n).astype(np.float32)
+        assert not same_bits(f64, c)
+
+
+def test_kurtosis_oracle_high_mean_rows(orc):
+    """The regime of integrated BL power (mean/sigma = sqrt(N_avg) >> 1): the C
+    oracle and the NumPy restatement agree, and a one-ulp change of m moves
+    the excess kurtosis beyond the streamed path's worst-case bound (so the
+    GPU tests resolve m on those rows)."""
+    rng = np.random.default_rng(5)
+    for nt in (16, 300, 1500, 5007):
+        R = np.repeat([30.0, 300.0, 3000.0, 30000.0], 8)[:, None]
+        rows = rng.gamma(R ** 2, 1e9 / R ** 2, (32, nt)).astype(np.float32)
+        a = np.asfortranarray(rows.reshape(32, 1, nt))
+        k = orc.kurtosis(a)[:, 0]
+        np.testing.assert_allclose(k, orc.np_kurtosis(a)[:, 0], rtol=1e-12)
+        m = orc.mean_f32(a)[:, 0]
+        mp = np.nextafter(m, np.float32(np.inf))[:, None]
+        z = (rows - mp).astype(np.float32)
+        z2 = (z * z).astype(np.float32)
+        k1 = (z2 * z2).astype(np.float64).sum(1) / nt / ((z2.astype(np.float64).sum(1) / nt) ** 2) - 3
+        big = R[:, 0] >= 3000
+        # the shift moves k by ~4 * skew * ulp(m) / sigma (sample skew varies)
+        assert np.mean(np.abs(k1 - k)[big] > KURT_LEAF_TOL * np.abs(k[big] + 3)) >= 0.75
 
 
 def test_errors(orc):
