@@ -243,6 +243,7 @@ def bench_decode(args, eng, torch, pkg):
     clen = np.full(nrep, len(chunk), np.uint64)
     raw_b = z["raw_gamma_chunk_b2048"].nbytes
     ooff = np.arange(nrep, dtype=np.uint64) * raw_b
+    olen = np.full(nrep, raw_b, np.uint64)
     cdev = torch.from_numpy(comp.copy()).cuda()
     out = torch.empty(nrep * raw_b // 4, dtype=torch.float32, device="cuda")
     sp = pkg._lib.stream_ptr()
@@ -250,7 +251,8 @@ def bench_decode(args, eng, torch, pkg):
     def go():
         pkg._lib.check(L.bldp_bslz4_decode_dev(nrep, comp.ctypes.data, cdev.data_ptr(),
                                                coff.ctypes.data, clen.ctypes.data, 4,
-                                               out.data_ptr(), ooff.ctypes.data, sp))
+                                               out.data_ptr(), ooff.ctypes.data, olen.ctypes.data,
+                                               sp))
     for _ in range(2):
         go()
     steps = max(3, args.steps // 4)

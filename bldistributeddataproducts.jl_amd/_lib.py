@@ -74,8 +74,8 @@ SIGNATURES = {
     "bldp_bslz4_info": ([P, SZ, P, P], I),
     "bldp_unchunk_f32": ([P, P, P, P, P, P, P], I),
     "bldp_bslz4_decode_host": ([P, SZ, I, P, SZ], I),
-    "bldp_bslz4_decode_dev": ([I, P, P, P, P, I, P, P, P], I),
-    "bldp_bslz4_decode_dev_async": ([I, P, P, P, P, I, P, P, P, P], I),
+    "bldp_bslz4_decode_dev": ([I, P, P, P, P, I, P, P, P, P], I),
+    "bldp_bslz4_decode_dev_async": ([I, P, P, P, P, I, P, P, P, P, P], I),
     "bldp_bslz4_error": ([P, P], I),
     "bldp_comm_id": ([P], I),
     "bldp_comm_init": ([I, I, I, P, P], I),

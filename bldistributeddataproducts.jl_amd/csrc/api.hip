@@ -119,8 +119,13 @@ int num_cus_current() {
 }
 
 // Library-owned scratch, cached per (device, stream) so that concurrent
-// streams never share a buffer.  Growing synchronizes that stream first.
+// streams never share a buffer.  Host threads sharing one stream (the GBT
+// fan-out runs a thread per (worker, file) on torch's current stream) take
+// turns: a call holds the entry's lock from the lookup until its last launch
+// is queued, so its kernels sit back to back in the stream and the next
+// call's kernels run after them.  Growing synchronizes the stream first.
 struct Scratch {
+  std::mutex mu;
   void *ptr = nullptr;
   size_t bytes = 0;
 };
@@ -129,26 +134,31 @@ std::map<std::pair<int, void *>, Scratch> g_ws;
 
 }  // namespace
 
-int bldp::scratch_bytes(hipStream_t s, size_t bytes, void **out) {
+int bldp::scratch_lease(hipStream_t s, size_t bytes, ScratchLease *lease) {
   int dev = 0;
   HIPCHK(hipGetDevice(&dev));
-  std::lock_guard<std::mutex> lk(g_ws_mu);
-  Scratch &w = g_ws[{dev, (void *)s}];
-  if (w.bytes < bytes) {
-    if (w.ptr) {
-      HIPCHK(hipStreamSynchronize(s));
-      HIPCHK(hipFree(w.ptr));
-      w.ptr = nullptr;
-      w.bytes = 0;
+  Scratch *w;
+  {
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    w = &g_ws[{dev, (void *)s}];  // map nodes are stable
+  }
+  std::unique_lock<std::mutex> hold(w->mu);
+  if (w->bytes < bytes) {
+    if (w->ptr) {
+      HIPCHK(hipStreamSynchronize(s));  // earlier calls on this stream still use it
+      HIPCHK(hipFree(w->ptr));
+      w->ptr = nullptr;
+      w->bytes = 0;
     }
     size_t want = std::max<size_t>(bytes, 1 << 20);
-    if (hipMalloc(&w.ptr, want) != hipSuccess) {
-      w.ptr = nullptr;
+    if (hipMalloc(&w->ptr, want) != hipSuccess) {
+      w->ptr = nullptr;
       return fail(BLDP_ENOMEM, "hipMalloc of %zu bytes of scratch failed", want);
     }
-    w.bytes = want;
+    w->bytes = want;
   }
-  *out = w.ptr;
+  lease->ptr = w->ptr;
+  lease->hold = std::move(hold);
   return BLDP_OK;
 }
 
@@ -163,18 +173,19 @@ void bldp::scratch_release_all() {
   std::lock_guard<std::mutex> lk(g_ws_mu);
   int prev = -1;
   (void)hipGetDevice(&prev);
-  for (auto &kv : g_ws)
+  for (auto &kv : g_ws) {
+    std::lock_guard<std::mutex> hold(kv.second.mu);  // (callers drained the devices)
     if (kv.second.ptr) {
       (void)hipSetDevice(kv.first.first);
       (void)hipFree(kv.second.ptr);
     }
+  }
   g_ws.clear();
   if (prev >= 0) (void)hipSetDevice(prev);
 }
 
 namespace {
 
-int scratch(hipStream_t s, size_t bytes, void **out) { return bldp::scratch_bytes(s, bytes, out); }
 
 bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
 
@@ -246,11 +257,11 @@ int reduce_impl(int nbank, const float *const *in, int64_t nchan, int64_t nif, i
     return BLDP_OK;  // plan query only
   }
   if (empty) return BLDP_OK;
+  ScratchLease lease;  // held until the launches are queued
   if (p.ws_bytes) {
-    void *ws = nullptr;
-    rc = scratch(s, p.ws_bytes, &ws);
+    rc = scratch_lease(s, p.ws_bytes, &lease);
     if (rc) return rc;
-    a.ws = (float *)ws;
+    a.ws = (float *)lease.ptr;
   }
   hipError_t e = launch_reduce(a, p, op, s);
   if (e != hipSuccess) return fail(BLDP_EHIP, "reduce launch: %s", hipGetErrorString(e));
@@ -469,9 +480,11 @@ static int kurt_run(KurtArgs &k, double *out, void *workspace, void *stream) {
   k.out = out;
   hipStream_t s = (hipStream_t)stream;
   void *ws = workspace;
+  ScratchLease lease;  // held until the launches are queued
   if (!ws) {
-    int rc = scratch(s, kurtosis_ws_bytes(k), &ws);
+    int rc = scratch_lease(s, kurtosis_ws_bytes(k), &lease);
     if (rc) return rc;
+    ws = lease.ptr;
   }
   hipError_t e = launch_kurtosis(k, (char *)ws, s);
   if (e != hipSuccess) return fail(BLDP_EHIP, "kurtosis launch: %s", hipGetErrorString(e));

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
 #include <vector>
 
 #include "bldp.h"
@@ -12,9 +13,16 @@ namespace bldp {
 // Record the thread-local error message returned by bldp_last_error; returns code.
 int set_error(int code, const char *fmt, ...);
 
-// Library-owned device scratch cached per (device, stream); growing it
-// synchronizes that stream first.
-int scratch_bytes(hipStream_t s, size_t bytes, void **out);
+// Library-owned device scratch cached per (device, stream).  A lease keeps
+// the (device, stream) entry locked until it is destroyed: take it before the
+// first launch that uses the buffer and keep it until the last is queued, so
+// host threads sharing a stream never interleave their kernels on it.
+// Growing synchronizes that stream first.
+struct ScratchLease {
+  void *ptr = nullptr;
+  std::unique_lock<std::mutex> hold;
+};
+int scratch_lease(hipStream_t s, size_t bytes, ScratchLease *lease);
 std::vector<int> scratch_devices();  // devices holding scratch
 void scratch_release_all();          // frees it (callers drained the devices)
 

@@ -351,10 +351,11 @@ BLDP_API int bldp_bslz4_decode_host(const void *chunk, size_t nbytes, int elem_s
 // bits are OR-ed into *derr (device memory).
 static int decode_launch(int nchunk, const uint8_t *comp_host, const uint8_t *comp_dev,
                          const uint64_t *chunk_off, const uint64_t *chunk_len, int elem_size,
-                         uint8_t *out_dev, const uint64_t *out_off, int *derr_user,
-                         hipStream_t s, int **derr_used) {
+                         uint8_t *out_dev, const uint64_t *out_off, const uint64_t *out_len,
+                         int *derr_user, hipStream_t s, int **derr_used,
+                         bldp::ScratchLease &lease) {
   if (nchunk < 0 || (nchunk && (!comp_host || !comp_dev || !chunk_off || !chunk_len ||
-                                !out_dev || !out_off)) ||
+                                !out_dev || !out_off || !out_len)) ||
       elem_size <= 0 || elem_size > 64)
     return bldp::set_error(BLDP_EINVAL, "bslz4: bad argument");
   if (elem_size == 4 && ((uintptr_t)out_dev & 3))
@@ -367,6 +368,13 @@ static int decode_launch(int nchunk, const uint8_t *comp_host, const uint8_t *co
     int rc = describe_chunk(comp_host + chunk_off[k], chunk_len[k], chunk_off[k], out_off[k],
                             elem_size, &descs[k]);
     if (rc) return rc;
+    // the header's byte count decides how much the kernels write: it must be
+    // the caller's slot exactly (a corrupt or foreign chunk never spills over)
+    if (descs[k].n * (uint64_t)elem_size != out_len[k])
+      return bldp::set_error(BLDP_EINVAL,
+                             "bslz4: chunk %d decodes to %llu bytes, its output slot holds %llu",
+                             k, (unsigned long long)(descs[k].n * elem_size),
+                             (unsigned long long)out_len[k]);
     if (elem_size == 4 && (out_off[k] & 3))
       return bldp::set_error(BLDP_EINVAL, "bslz4: output offsets must be 4-byte aligned");
     descs[k].task0 = (uint32_t)ntask;
@@ -381,9 +389,10 @@ static int decode_launch(int nchunk, const uint8_t *comp_host, const uint8_t *co
     return bldp::set_error(BLDP_EINVAL, "bslz4: block of %u bytes exceeds the LDS plan", maxbb);
   const size_t dbytes = ((descs.size() * sizeof(ChunkDesc)) + 255) & ~(size_t)255;
   const size_t tbytes = ((ntask * sizeof(Task)) + 255) & ~(size_t)255;
-  void *ws = nullptr;
-  int rc = bldp::scratch_bytes(s, dbytes + tbytes + 256, &ws);
+  // the caller holds the lease until it no longer reads the scratch
+  int rc = bldp::scratch_lease(s, dbytes + tbytes + 256, &lease);
   if (rc) return rc;
+  void *ws = lease.ptr;
   ChunkDesc *ddesc = (ChunkDesc *)ws;
   Task *dtask = (Task *)((char *)ws + dbytes);
   int *derr = derr_user ? derr_user : (int *)((char *)ws + dbytes + tbytes);
@@ -411,11 +420,12 @@ static int decode_error(int herr) {
 BLDP_API int bldp_bslz4_decode_dev(int nchunk, const uint8_t *comp_host, const uint8_t *comp_dev,
                                    const uint64_t *chunk_off, const uint64_t *chunk_len,
                                    int elem_size, uint8_t *out_dev, const uint64_t *out_off,
-                                   void *stream) {
+                                   const uint64_t *out_len, void *stream) {
   hipStream_t s = (hipStream_t)stream;
   int *derr = nullptr;
+  bldp::ScratchLease lease;  // held through the error read-back (derr lives in scratch)
   int rc = decode_launch(nchunk, comp_host, comp_dev, chunk_off, chunk_len, elem_size, out_dev,
-                         out_off, nullptr, s, &derr);
+                         out_off, out_len, nullptr, s, &derr, lease);
   if (rc || !derr) return rc;
   int herr = 0;
   if (hipMemcpyAsync(&herr, derr, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -427,12 +437,13 @@ BLDP_API int bldp_bslz4_decode_dev(int nchunk, const uint8_t *comp_host, const u
 BLDP_API int bldp_bslz4_decode_dev_async(int nchunk, const uint8_t *comp_host,
                                          const uint8_t *comp_dev, const uint64_t *chunk_off,
                                          const uint64_t *chunk_len, int elem_size,
-                                         uint8_t *out_dev, const uint64_t *out_off, int *err_dev,
-                                         void *stream) {
+                                         uint8_t *out_dev, const uint64_t *out_off,
+                                         const uint64_t *out_len, int *err_dev, void *stream) {
   if (!err_dev) return bldp::set_error(BLDP_EINVAL, "bslz4: null error word");
   int *derr = nullptr;
+  bldp::ScratchLease lease;  // until the planner and decoder are queued
   return decode_launch(nchunk, comp_host, comp_dev, chunk_off, chunk_len, elem_size, out_dev,
-                       out_off, err_dev, (hipStream_t)stream, &derr);
+                       out_off, out_len, err_dev, (hipStream_t)stream, &derr, lease);
 }
 
 BLDP_API int bldp_bslz4_error(const int *err_dev, void *stream) {

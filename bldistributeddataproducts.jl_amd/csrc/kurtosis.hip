@@ -24,11 +24,11 @@
 // Paths (the window is read from HBM once on the first three):
 //   nt <= 32    k_kurt_regs : a lane keeps its float4 column in registers and
 //               runs the recipe in order: bit-identical to it.
-//   33..512     k_kurt_mid  : a 64-channel tile in registers over 16 row
-//               groups of consecutive spectra.  The Float32 sum runs through
-//               the row groups in order (lane shuffles inside a wave, LDS
-//               between waves); z, z2 and the Float64 sums follow the recipe,
-//               the 16 partial sums are added in row-group order.
+//   33..512     k_kurt_mid  : a 64-channel tile in registers, lane = channel,
+//               the 4 waves holding consecutive quarters of the spectra (any
+//               channel alignment or step).  The Float32 sum runs down the
+//               registers wave after wave; z, z2 and the Float64 sums follow
+//               the recipe, the 4 partial sums are added in wave order.
 //   > 512       k_kurt_leaf : one wave per (leaf, 256 channels) streams the
 //               leaf once: its sequential Float32 sum, and Float64 power sums
 //               about its first spectrum, moved to the leaf's own mean.
@@ -235,105 +235,67 @@ __global__ __launch_bounds__(kB) void k_kurt_regs(const KurtArgs k) {
 }
 
 // ---------------------------------------------------------------------------
-// 32 < nt <= 16*NR (<= 512, one leaf): a workgroup holds a 64-channel x nt
-// tile in registers.  Thread (rg, c4) = (tid / 16, tid % 16) keeps float4
-// column c4 of the consecutive spectra [rg*nt/16, (rg+1)*nt/16); a
-// wave-instruction reads 4 rows x 256 B.  The sequential Float32 sum visits
-// the row groups in order: the 4 groups of a wave hand the running sum on by
-// lane shuffle, the waves by LDS and a barrier.  Then z, z2 and the Float64
-// sums run over the registers and the 16 partial sums are added through LDS
-// in row-group order.
+// 32 < nt <= 4*NR (<= 512, one leaf), any window: a workgroup holds 64
+// channels x nt spectra in registers, lane = channel, wave w = the spectra
+// [w*nt/4, (w+1)*nt/4); a wave-instruction reads one row's 64 channels.  The
+// sequential Float32 sum runs down each lane's registers wave after wave (the
+// running sum handed on through LDS), every lane doing its own channel.  Then
+// z, z2 and the Float64 sums run over the registers and the 4 partial sums are
+// added through LDS in wave order.
 template <int NR>
 __global__ __launch_bounds__(kB) void k_kurt_mid(const KurtArgs k) {
-  const int tid = threadIdx.x, c4 = tid & 15, rg = tid >> 4, lane = tid & 63, wave = tid >> 6;
-  const int64_t ncols = k.nc / 4, ctiles = (ncols + 15) / 16;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t ctiles = (k.nc + 63) / 64;
   const int64_t b = blockIdx.x;
-  const int64_t ib = b / ctiles, col = (b % ctiles) * 16 + c4;
-  const bool valid = col < ncols;
+  const int64_t ib = b / ctiles, c = (b % ctiles) * 64 + lane;
+  const bool valid = c < k.nc;
   const int bank = (int)(ib / k.ni);
   const int64_t i = ib - (int64_t)bank * k.ni;
   const int nt = (int)k.nt;
-  const int r0 = (rg * nt) >> 4, cnt = (((rg + 1) * nt) >> 4) - r0;
+  const int r0 = (wave * nt) >> 2, cnt = (((wave + 1) * nt) >> 2) - r0;
   const int64_t ld = k.in_ld_t;
-  const float *p = k.in[bank] + k.in_off + i * k.in_ld_i + 4 * (valid ? col : 0) + r0 * ld;
-  float4 v[NR];
+  const float *p = k.in[bank] + k.in_off + i * k.in_ld_i + (valid ? c : 0) * k.in_cs + r0 * ld;
+  float v[NR];
 #pragma unroll
   for (int r = 0; r < NR; ++r)
-    v[r] = (valid && r < cnt) ? ldnt(p + r * ld) : make_float4(0.f, 0.f, 0.f, 0.f);
+    v[r] = (valid && r < cnt) ? __builtin_nontemporal_load(p + r * ld) : 0.0f;
   // Base.sum, sequential over the whole window (nt <= 1024 is one leaf)
-  __shared__ float4 carry[16];
-  f2v sa = {0.f, 0.f}, sb = {0.f, 0.f};
+  __shared__ float carry[64];
+  float s = 0.0f;
 #pragma unroll 1
   for (int w = 0; w < 4; ++w) {
     if (wave == w) {
-      if (w > 0) {
-        const float4 c = carry[c4];
-        sa = f2v{c.x, c.y};
-        sb = f2v{c.z, c.w};
-      }
-#pragma unroll 1
-      for (int g = 0; g < 4; ++g) {
-        if ((lane >> 4) == g) {
+      if (w > 0) s = carry[lane];
 #pragma unroll
-          for (int r = 0; r < NR; ++r)
-            if (r < cnt) {
-              const f2v xa = {v[r].x, v[r].y}, xb = {v[r].z, v[r].w};
-              if (rg == 0 && r == 0) {  // the sum starts from the first element
-                sa = xa;
-                sb = xb;
-              } else {
-                sa += xa;
-                sb += xb;
-              }
-            }
-        }
-        const int src = 16 * g + c4;
-        sa.x = __shfl(sa.x, src, 64);
-        sa.y = __shfl(sa.y, src, 64);
-        sb.x = __shfl(sb.x, src, 64);
-        sb.y = __shfl(sb.y, src, 64);
-      }
-      if (lane < 16) carry[c4] = make_float4(sa.x, sa.y, sb.x, sb.y);
+      for (int r = 0; r < NR; ++r)
+        if (r < cnt) s = (w == 0 && r == 0) ? v[0] : s + v[r];  // from the first element
+      carry[lane] = s;
     }
     __syncthreads();
   }
-  const float4 S = carry[c4];
-  const float m[4] = {S.x / (float)nt, S.y / (float)nt, S.z / (float)nt, S.w / (float)nt};
-  __shared__ double part[16][16][8];  // [row group][column][moment x channel]
-  double c2[4] = {0, 0, 0, 0}, cq[4] = {0, 0, 0, 0};
+  const float m = carry[lane] / (float)nt;
+  double c2 = 0.0, c4 = 0.0;
 #pragma unroll
   for (int r = 0; r < NR; ++r)
-    if (valid && r < cnt) {
-      const float x[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        const float z = x[w] - m[w];  // StatsBase: z, z2 in Float32; Float64 moments
-        const float z2 = z * z;
-        c2[w] += (double)z2;
-        cq[w] += (double)(z2 * z2);
-      }
+    if (r < cnt) {
+      const float z = v[r] - m;  // StatsBase: z, z2 in Float32; Float64 moments
+      const float z2 = z * z;
+      c2 += (double)z2;
+      c4 += (double)(z2 * z2);
     }
-#pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    part[rg][c4][w] = c2[w];
-    part[rg][c4][4 + w] = cq[w];
-  }
+  __shared__ double part[4][2][64];
+  part[wave][0][lane] = c2;
+  part[wave][1][lane] = c4;
   __syncthreads();
-  if (rg == 0 && valid) {
-    double r[4];
+  if (wave == 0 && valid) {
+    double a2 = 0.0, a4 = 0.0;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      double a2 = 0, a4 = 0;
-      for (int q = 0; q < 16; ++q) {
-        a2 += part[q][c4][w];
-        a4 += part[q][c4][4 + w];
-      }
-      const double cm2 = a2 / (double)nt, cm4 = a4 / (double)nt;
-      r[w] = (cm4 / (cm2 * cm2)) - 3.0;
+    for (int q = 0; q < 4; ++q) {
+      a2 += part[q][0][lane];
+      a4 += part[q][1][lane];
     }
-    double *o = k.out + ib * k.nc + 4 * col;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) o[w] = r[w];
+    const double cm2 = a2 / (double)nt, cm4 = a4 / (double)nt;
+    k.out[ib * k.nc + c] = (cm4 / (cm2 * cm2)) - 3.0;
   }
 }
 
@@ -350,6 +312,10 @@ __global__ __launch_bounds__(kB) void k_kurt_mid(const KurtArgs k) {
 //   BLDP_KURT_LEAF_B  spectra in flight per lane
 #ifndef BLDP_KURT_LEAF_B
 #define BLDP_KURT_LEAF_B 8
+#endif
+//   BLDP_KURT_LEAF_WAVES  cap on resident waves per SIMD (0 = the register budget's)
+#ifndef BLDP_KURT_LEAF_WAVES
+#define BLDP_KURT_LEAF_WAVES 0
 #endif
 struct LeafAcc {
   f2v sa, sb;  // Float32 sums of channels (0,1) and (2,3)
@@ -372,7 +338,11 @@ __device__ __forceinline__ void leaf_step(LeafAcc &A, const float4 q) {
   }
 }
 
-__global__ __launch_bounds__(kB) void k_kurt_leaf(const KurtArgs k) {
+__global__ __launch_bounds__(kB)
+#if BLDP_KURT_LEAF_WAVES > 0
+__attribute__((amdgpu_waves_per_eu(1, BLDP_KURT_LEAF_WAVES)))
+#endif
+void k_kurt_leaf(const KurtArgs k) {
   constexpr int B = BLDP_KURT_LEAF_B;
   const int lane = threadIdx.x & 63;
   const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -742,17 +712,17 @@ __global__ __launch_bounds__(kB) void k_fill_nan(double *out, int64_t n) {
 }
 
 // ---- host side -------------------------------------------------------------
-//   BLDP_KURT_MID_NR rows per thread of the largest k_kurt_mid instantiation
-//                   (windows up to 16 x this many spectra use it, <= 32)
+//   BLDP_KURT_MID_NR spectra per wave of the largest k_kurt_mid instantiation
+//                   (windows up to 4 x this many spectra use it, <= 128)
 #ifndef BLDP_KURT_MID_NR
-#define BLDP_KURT_MID_NR 32
+#define BLDP_KURT_MID_NR 128
 #endif
 
 enum KPath { KP_REGS = 0, KP_MID = 1, KP_LEAF = 2, KP_TWOPASS = 3 };
 
 int path_of(const KurtArgs &k) {
   if (k.vec && k.nt <= 32) return KP_REGS;
-  if (k.vec && k.nt <= 16 * BLDP_KURT_MID_NR) return KP_MID;
+  if (k.nt <= 4 * BLDP_KURT_MID_NR) return KP_MID;  // any channel alignment and step
   if (k.vec) return KP_LEAF;
   return KP_TWOPASS;
 }
@@ -914,15 +884,15 @@ hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s) {
     return hipGetLastError();
   }
   if (p == KP_MID) {
-    const dim3 g1((unsigned)(cdivk(ncols, 16) * k.nrow));
+    const dim3 g1((unsigned)(cdivk(k.nc, 64) * k.nrow));
     if (k.nt <= 128)
-      hipLaunchKernelGGL(k_kurt_mid<8>, g1, block, 0, s, k);
-    else if (k.nt <= 256)
-      hipLaunchKernelGGL(k_kurt_mid<16>, g1, block, 0, s, k);
-    else if (k.nt <= 384)
-      hipLaunchKernelGGL(k_kurt_mid<24>, g1, block, 0, s, k);
-    else
       hipLaunchKernelGGL(k_kurt_mid<32>, g1, block, 0, s, k);
+    else if (k.nt <= 256)
+      hipLaunchKernelGGL(k_kurt_mid<64>, g1, block, 0, s, k);
+    else if (k.nt <= 384)
+      hipLaunchKernelGGL(k_kurt_mid<96>, g1, block, 0, s, k);
+    else
+      hipLaunchKernelGGL(k_kurt_mid<128>, g1, block, 0, s, k);
     return hipGetLastError();
   }
   const KLayout L = layout(k);
@@ -962,7 +932,7 @@ int64_t kurtosis_max_grid(const KurtArgs &k) {
   const int64_t ncols = k.nc / 4;
   switch (p) {
     case KP_REGS: return cdivk(ncols, kB) * k.nrow;
-    case KP_MID: return cdivk(ncols, 16) * k.nrow;
+    case KP_MID: return cdivk(k.nc, 64) * k.nrow;
     case KP_LEAF: return cdivk(k.nrow * k.nslot * k.nseg, 4);
     default:
       return std::max(cdivk(k.nc, kB) * k.nrow * k.nslot,

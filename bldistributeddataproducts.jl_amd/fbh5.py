@@ -430,11 +430,12 @@ def bslz4_decode_dev(chunks, dtype=np.float32, device=None, stream=None, out=Non
         cap = out.numel() * out.element_size()
         if len(ooff) != len(chunks) or any(int(o) + s > cap for o, s in zip(ooff, sizes)):
             raise ValueError("decoded chunks do not fit the output tensor")
+    olen = np.array(sizes, np.uint64)  # each chunk's slot: the size its header states
     cdev = torch.from_numpy(comp.copy()).to(dev) if comp.size else None
     rc = _lib.lib().bldp_bslz4_decode_dev(
         len(chunks), comp.ctypes.data, cdev.data_ptr() if cdev is not None else None,
         coff.ctypes.data, clen.ctypes.data, es, out.data_ptr(), ooff.ctypes.data,
-        _lib.stream_ptr(stream))
+        olen.ctypes.data, _lib.stream_ptr(stream))
     _lib.check(rc, "bldp_bslz4_decode_dev")
     return out
 
@@ -875,10 +876,11 @@ def _decode_batches(batches, stage, sizes, masks, offsets, cvol, packed, cdev, h
                 offs = np.array([offsets[k] for k in comp], np.uint64)
                 lens = np.array([sizes[k] for k in comp], np.uint64)
                 ooff = np.array([4 * k * cvol for k in comp], np.uint64)
+                olen = np.full(len(comp), 4 * cvol, np.uint64)  # a whole chunk per slot
                 rc = _lib.lib().bldp_bslz4_decode_dev_async(
                     len(comp), host.ctypes.data, cdev.data_ptr(), offs.ctypes.data,
-                    lens.ctypes.data, 4, packed.data_ptr(), ooff.ctypes.data, err.data_ptr(),
-                    _lib.stream_ptr())
+                    lens.ctypes.data, 4, packed.data_ptr(), ooff.ctypes.data, olen.ctypes.data,
+                    err.data_ptr(), _lib.stream_ptr())
                 _lib.check(rc, "bldp_bslz4_decode_dev_async")
             t_dec += time.perf_counter() - td
     td = time.perf_counter()

@@ -135,20 +135,35 @@ def bandaxis(headers, idxs=(COLON, COLON, COLON), fqavby=1):
 def getband(workers, fnames, idxs=(COLON, COLON, COLON), fqavby=1, fqavfunc="sum", tavby=1,
             despike_nfpc=None, freqs=False):
     """The stitched band product: reduce(vcat, getdata(...)) in the given
-    bank order (src/gbt.jl:103).  With ``despike_nfpc`` the DC bin of every
-    coarse channel is patched as in loadscan (src/gbt.jl:101-102,111);
-    ``despike_nfpc=True`` takes loadscan's own ``nfpc = size(ds[1], 1) ÷ 64``
-    (64 coarse channels per bank, :100).  ``freqs=True`` returns
-    ``(band, bandaxis(...))``."""
-    parts = list(getdata(workers, fnames, idxs, fqavby, fqavfunc, tavby).ravel())
-    band = np.asfortranarray(np.concatenate(parts, axis=0))
-    if despike_nfpc is True:
-        despike_nfpc = parts[0].shape[0] // 64
-    if despike_nfpc:
-        from . import engine
+    bank order (src/gbt.jl:103).  ``workers``/``fnames`` are one band's banks
+    (1-D), or a (nbank, nband) matrix like loadscan's ``ds``, whose columns are
+    bands: then one stitched band per column is returned, as
+    ``map(c -> reduce(vcat, c), eachcol(ds))`` (:103).  With ``despike_nfpc``
+    the DC bin of every coarse channel is patched as in loadscan
+    (src/gbt.jl:101-102,111); ``despike_nfpc=True`` takes loadscan's own
+    ``nfpc = size(ds[1], 1) ÷ 64`` (64 coarse channels per bank, :101).
+    ``freqs=True`` returns ``(band, bandaxis(...))`` (lists for a matrix)."""
+    w = np.asarray(workers, dtype=object)
+    f = np.asarray(fnames, dtype=object)
+    if w.ndim not in (1, 2):
+        raise AssertionError("getband takes one band (1-D) or a (nbank, nband) matrix")
+    res = getdata(workers, fnames, idxs, fqavby, fqavfunc, tavby)
+    cols = [list(res)] if res.ndim == 1 else [list(res[:, j]) for j in range(res.shape[1])]
+    wcol = [list(w)] if w.ndim == 1 else [list(w[:, j]) for j in range(w.shape[1])]
+    fcol = [list(f)] if f.ndim == 1 else [list(f[:, j]) for j in range(f.shape[1])]
+    nfpc = despike_nfpc
+    if nfpc is True:
+        nfpc = cols[0][0].shape[0] // 64  # size(ds[1], 1) ÷ 64
+    bands = []
+    for parts, ws in zip(cols, wcol):
+        band = np.asfortranarray(np.concatenate(parts, axis=0))
+        if nfpc:
+            from . import engine
 
-        x = engine.fb_from_numpy(band, device=f"cuda:{int(np.asarray(workers).ravel()[0])}")
-        band = engine.fb_to_numpy(engine.despike(x, despike_nfpc))
+            x = engine.fb_from_numpy(band, device=f"cuda:{int(ws[0])}")
+            band = engine.fb_to_numpy(engine.despike(x, nfpc))
+        bands.append(band)
     if freqs:
-        return band, bandaxis(getheaders(workers, fnames), idxs, fqavby)
-    return band
+        axes = [bandaxis(getheaders(ws, fs), idxs, fqavby) for ws, fs in zip(wcol, fcol)]
+        return (bands[0], axes[0]) if w.ndim == 1 else (bands, axes)
+    return bands[0] if w.ndim == 1 else bands

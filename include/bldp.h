@@ -214,12 +214,14 @@ BLDP_API int bldp_bslz4_decode_host(const void *chunk, size_t nbytes, int elem_s
 /* Decode nchunk chunks on the GPU.  comp_host and comp_dev hold the same
  * concatenated chunk bytes (the host copy is parsed into a block table, the
  * device copy is decoded); chunk k spans [chunk_off[k], +chunk_len[k]) and
- * decodes to out_dev + out_off[k] (bytes).  Synchronous: returns after the
- * decode finished, BLDP_EINVAL if any block is corrupt. */
+ * decodes to out_dev + out_off[k] (bytes), a slot of out_len[k] bytes: a
+ * chunk whose header claims any other size is rejected (BLDP_EINVAL) before
+ * anything is launched, so no chunk writes outside its slot.  Synchronous:
+ * returns after the decode finished, BLDP_EINVAL if any block is corrupt. */
 BLDP_API int bldp_bslz4_decode_dev(int nchunk, const uint8_t *comp_host, const uint8_t *comp_dev,
                                    const uint64_t *chunk_off, const uint64_t *chunk_len,
                                    int elem_size, uint8_t *out_dev, const uint64_t *out_off,
-                                   void *stream);
+                                   const uint64_t *out_len, void *stream);
 
 /* Asynchronous form: queues the decode on `stream` and returns; error bits
  * are OR-ed into *err_dev (device int, zeroed by the caller before its first
@@ -229,8 +231,8 @@ BLDP_API int bldp_bslz4_decode_dev(int nchunk, const uint8_t *comp_host, const u
 BLDP_API int bldp_bslz4_decode_dev_async(int nchunk, const uint8_t *comp_host,
                                          const uint8_t *comp_dev, const uint64_t *chunk_off,
                                          const uint64_t *chunk_len, int elem_size,
-                                         uint8_t *out_dev, const uint64_t *out_off, int *err_dev,
-                                         void *stream);
+                                         uint8_t *out_dev, const uint64_t *out_off,
+                                         const uint64_t *out_len, int *err_dev, void *stream);
 BLDP_API int bldp_bslz4_error(const int *err_dev, void *stream);
 
 /* Gather a window (Julia order, dense (nc, ni, nt) out) from decoded chunks:

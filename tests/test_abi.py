@@ -292,6 +292,32 @@ def test_kurtosis_plan_pairwise_blocks(pkg, L, n):
         assert all(node(lev, j)[1] > 1024 for j in range(1 << lev))
     if path == 2:
         assert ws >= 64 * nslot * (4 * 8 + 3 * 4)
-    # the unaligned plan (two passes) for the same window
+    # the unaligned plan for the same window: register tile up to 512 spectra
+    # (any alignment), else two passes
     assert L.bldp_kurtosis_plan_f32(A + 4, 64, 1, n, None, info) == 0
-    assert info[0] == 3 and info[1] == K
+    assert info[0] == (1 if n <= 512 else 3) and info[1] == K
+
+
+def test_bslz4_slot_size_checked_before_launch(pkg, L):
+    """the device decode takes each chunk's output slot size and
+    refuses a chunk whose header claims another size on the host, before any
+    launch (so this runs without a GPU: the device pointers are never used)."""
+    import struct
+
+    body = struct.pack(">I", 3) + b"\0\0\0"
+    for claim, slot in ((2 * 8192, 8192), (8192 - 32, 8192)):
+        chunk = struct.pack(">QI", claim, 8192) + body
+        h = np.frombuffer(chunk, np.uint8)
+        off = np.zeros(1, np.uint64)
+        n = np.array([len(chunk)], np.uint64)
+        olen = np.array([slot], np.uint64)
+        fake = 1 << 20  # never dereferenced: the check precedes every HIP call
+        rc = L.bldp_bslz4_decode_dev(1, h.ctypes.data, fake, off.ctypes.data, n.ctypes.data, 4,
+                                     fake, off.ctypes.data, olen.ctypes.data, None)
+        assert rc == pkg._lib.BLDP_EINVAL and "slot" in pkg._lib.last_error()
+        rc = L.bldp_bslz4_decode_dev_async(1, h.ctypes.data, fake, off.ctypes.data,
+                                           n.ctypes.data, 4, fake, off.ctypes.data,
+                                           olen.ctypes.data, fake, None)
+        assert rc == pkg._lib.BLDP_EINVAL
+    assert L.bldp_bslz4_decode_dev(1, h.ctypes.data, fake, off.ctypes.data, n.ctypes.data, 4,
+                                   fake, off.ctypes.data, None, None) == pkg._lib.BLDP_EINVAL

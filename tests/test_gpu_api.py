@@ -78,6 +78,37 @@ def test_gbt_getdata_getband_kurtosis(pkg, orc, files):
         assert_kurtosis(k, orc.kurtosis(a, [0, 512, 1, 0, 1, 1, 0, 40, 1]), "leaf", 40)
     hdrs = pkg.GBT.getheaders(workers[:2], names[:2])
     assert hdrs[0]["nfpc"] == 64 and hdrs[1]["nfpc"] == 64  # FBH5 attr / round(187.5/64/abs(foff))
+    # a (nbank, nband) matrix like loadscan's ds: one stitched band per column,
+    # map(c -> reduce(vcat, c), eachcol(ds)) (src/gbt.jl:103)
+    wm = np.array(workers, dtype=object).reshape(4, 2)
+    fm = np.array(names, dtype=object).reshape(4, 2)
+    bands = pkg.GBT.getband(wm, fm, (C, C, C), fqavby=64, tavby=10)
+    assert len(bands) == 2
+    for j in range(2):
+        col = [banks[2 * r + j] for r in range(4)]  # fm[:, j]
+        assert same_bits(bands[j], orc.stitch([orc.reduce(a, 64, 10) for a in col]))
+    bands, axes = pkg.GBT.getband(wm, fm, (C, C, J(1, 3)), freqs=True)
+    assert len(axes) == 2 and len(axes[1]) == bands[1].shape[0] == 4 * 4096
+    with pytest.raises(AssertionError):
+        pkg.GBT.getband(np.zeros((2, 2, 2), object), np.zeros((2, 2, 2), object))
+
+
+def test_gbt_getkurtosis_fanout_long_windows(pkg, orc, tmp_path):
+    """GBT.getkurtosis over 6 files on one device with > 512 spectra: one
+    thread per (worker, file) on the same stream and scratch (the leaf
+    partials and tree levels), each result against the oracle."""
+    rng = np.random.default_rng(61)
+    arrs, names = [], []
+    for b in range(6):
+        a = np.asfortranarray((rng.gamma(400.0, 1e6, (256, 1, 1500 + 300 * b))).astype(np.float32))
+        p = tmp_path / f"k{b}.h5"
+        pkg.fbh5.write(p, dict(fch1=1000.0, foff=-0.1, nchans=256, nifs=1, tsamp=1.0, nfpc=64), a)
+        arrs.append(a)
+        names.append(str(p))
+    for _ in range(2):
+        ks = pkg.GBT.getkurtosis([0] * 6, names)
+        for a, k in zip(arrs, ks):
+            assert_kurtosis(k, orc.kurtosis(a), "leaf", a.shape[2])
 
 
 def _rank(rank, world, port, q):
@@ -226,6 +257,41 @@ def test_bslz4_gpu_decoder_matches_bitshuffle_library(pkg):
     assert pos == out.size
 
 
+def test_bslz4_gpu_rejects_chunks_larger_than_their_slot(pkg):
+    """A chunk whose header claims more (or fewer) bytes than its output slot
+    is refused on the host before any launch (BLDP_EINVAL): nothing is written
+    into the neighbouring slots."""
+    import struct
+
+    import torch
+
+    z, _ = _bslz4_fixtures()
+    good = z["chunk_int_runs_b512"].tobytes()
+    raw = z["raw_int_runs_b512"].ravel()
+    nb = raw.nbytes
+    L, lib = pkg._lib.lib(), pkg._lib
+    for claim in (2 * nb, nb - 32):
+        evil = struct.pack(">Q", claim) + good[8:]  # same blocks, forged byte count
+        blobs = [good, evil, good]
+        comp = np.frombuffer(b"".join(blobs), np.uint8)
+        coff = np.array([0, len(good), len(good) + len(evil)], np.uint64)
+        clen = np.array([len(b) for b in blobs], np.uint64)
+        ooff = np.array([0, nb, 2 * nb], np.uint64)
+        olen = np.full(3, nb, np.uint64)
+        out = torch.full((3 * nb // 4,), -1, dtype=torch.int32, device="cuda:0")
+        cdev = torch.from_numpy(comp.copy()).cuda()
+        rc = L.bldp_bslz4_decode_dev(3, comp.ctypes.data, cdev.data_ptr(), coff.ctypes.data,
+                                     clen.ctypes.data, 4, out.data_ptr(), ooff.ctypes.data,
+                                     olen.ctypes.data, lib.stream_ptr())
+        assert rc == lib.BLDP_EINVAL and "slot" in lib.last_error()
+        torch.cuda.synchronize()
+        assert (out == -1).all()  # refused before the launch: no slot touched
+    with pytest.raises(ValueError):  # the Python wrapper checks the slots too
+        pkg.fbh5.bslz4_decode_dev([good, good], device="cuda:0",
+                                  out=torch.empty(nb // 4, dtype=torch.float32, device="cuda:0"),
+                                  out_offsets=[0, nb // 2])
+
+
 def test_bslz4_gpu_rejects_corrupt_blocks(pkg):
     import struct
 
@@ -249,9 +315,11 @@ def test_bslz4_gpu_rejects_corrupt_blocks(pkg):
         dv = torch.from_numpy(h.copy()).cuda()
         o = np.zeros(1, np.uint64)
         n = np.array([len(blob)], np.uint64)
+        olen = np.array([pkg.fbh5.bslz4_info(blob)[0]], np.uint64)
         assert L.bldp_bslz4_decode_dev_async(1, h.ctypes.data, dv.data_ptr(), o.ctypes.data,
                                              n.ctypes.data, 4, res.data_ptr(), o.ctypes.data,
-                                             err.data_ptr(), lib.stream_ptr()) == 0
+                                             olen.ctypes.data, err.data_ptr(),
+                                             lib.stream_ptr()) == 0
         if blob is good:
             assert L.bldp_bslz4_error(err.data_ptr(), lib.stream_ptr()) == 0
     assert L.bldp_bslz4_error(err.data_ptr(), lib.stream_ptr()) == lib.BLDP_EINVAL

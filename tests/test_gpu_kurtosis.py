@@ -7,10 +7,11 @@ Float32 sum exactly (tests/test_oracle.py pins the oracle's).
 
 Tolerances (tests/conftest.py assert_kurtosis), by the path that ran:
   regs     (<= 32 spectra)      bit-exact
-  mid      (33..512)            6 nt 2^-53 relative on k + 3 (Float64 order)
+  mid      (33..512, or <= 32 unaligned)  6 nt 2^-53 relative on k + 3
+                                 (Float64 order)
   leaf     (> 512, aligned)     13 * 2^-24 * 1.05 relative on k + 3 (Float32
                                  rounding of z^2, z^4 in the recipe)
-  twopass  (unaligned windows)  6 nt 2^-53 relative on k + 3
+  twopass  (unaligned, > 512)   6 nt 2^-53 relative on k + 3
 """
 from __future__ import annotations
 
@@ -50,6 +51,11 @@ def power_rows(rng, nc, ni, nt, nfpc=64):
     return np.asfortranarray(g.astype(np.float32).transpose(2, 1, 0))
 
 
+def unaligned(nt):
+    """The path of a window whose channels cannot be read as float4."""
+    return "mid" if nt <= 512 else "twopass"
+
+
 def check(eng, orc, a, win=None, expect=None, msg=""):
     x = dev(eng, a)
     plan = eng.kurtosis_plan(x, win)
@@ -75,9 +81,9 @@ def test_kurtosis_integrated_power_rows(eng, orc, nt, path):
     nc = 1000 if nt <= 512 else 260
     a = power_rows(rng, nc, 2, nt)
     check(eng, orc, a, None, path, "aligned")
-    # unaligned channel start -> the two-pass path (same Float32 mean)
+    # unaligned channel start -> lane-per-channel tile or two passes (same m)
     w = [1, nc - 3, 1, 0, 2, 1, 0, nt, 1]
-    check(eng, orc, a, w, "twopass", "unaligned")
+    check(eng, orc, a, w, unaligned(nt), "unaligned")
     # time window starting inside the data (aligned channels, shifted leaves)
     if nt > 8:
         w = [4, nc - 4, 1, 1, 1, 1, 3, nt - 5, 1]
@@ -144,7 +150,7 @@ def test_kurtosis_special_rows(eng, orc, nt):
     a[7, 0, :] = np.float32(1e9) + ulp * rng.integers(-3, 4, nt).astype(np.float32)
     a[8, 0, :] = -a[0, 0, :]
     check(eng, orc, a, None, None, "aligned")
-    check(eng, orc, a, [1, 62, 1, 0, 1, 1, 0, nt, 1], "twopass", "unaligned")
+    check(eng, orc, a, [1, 62, 1, 0, 1, 1, 0, nt, 1], unaligned(nt), "unaligned")
 
 
 def test_kurtosis_empty_and_degenerate_windows(eng, orc):
@@ -154,8 +160,10 @@ def test_kurtosis_empty_and_degenerate_windows(eng, orc):
     k = host(eng, eng.kurtosis(x, [0, 64, 1, 0, 2, 1, 5, 0, 1]))  # no spectra: NaN
     assert k.shape == (64, 2) and np.isnan(k).all()
     assert np.isnan(orc.kurtosis(a, [0, 64, 1, 0, 2, 1, 5, 0, 1])).all()
-    check(eng, orc, a, [63, 64, -1, 1, 2, -1, 39, 40, -1], "twopass", "reversed")
-    check(eng, orc, a, [0, 32, 2, 0, 2, 1, 0, 20, 2], "twopass", "strided")
+    check(eng, orc, a, [63, 64, -1, 1, 2, -1, 39, 40, -1], "mid", "reversed")
+    check(eng, orc, a, [0, 32, 2, 0, 2, 1, 0, 20, 2], "mid", "strided")
+    b = power_rows(np.random.default_rng(4), 64, 2, 1500)
+    check(eng, orc, b, [63, 64, -1, 1, 2, -1, 1499, 1500, -1], "twopass", "reversed long")
 
 
 def test_kurtosis_caller_workspace(eng, orc, pkg):
@@ -192,3 +200,38 @@ def test_kurtosis_host_drop_in_long_window(eng, orc):
     w = [2, 500, 1, 0, 1, 1, 10, 3000, 1]
     got = eng.kurtosis_host(a, w)  # (leaf or two-pass, by the staged buffer's alignment)
     assert_kurtosis(got, orc.kurtosis(a, w), "leaf", 3000)
+
+
+def test_kurtosis_and_chunked_reduce_from_threads_share_scratch(eng, orc):
+    """Host threads sharing torch's current stream (the GBT fan-out runs one
+    thread per (worker, file)) and the library scratch of that stream:
+    long-window kurtosis (leaf partials + tree) and time-chunked reductions
+    (partials + finalize) from 8 threads at once, every result against the
+    oracle.  The scratch lease serialises the calls' launches on the stream."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import torch
+
+    rng = np.random.default_rng(123)
+    arrs = [power_rows(rng, 256, 1, int(n)) for n in (1500, 2600, 5007, 7000)] * 2
+    ints = [np.asfortranarray(rng.integers(0, 256, (64, 1, 20000)).astype(np.float32))
+            for _ in range(4)]
+    xs = [dev(eng, a) for a in arrs]
+    ys = [dev(eng, a) for a in ints]
+    assert eng.plan(ys[0], 8, 20000)["time_chunks"] > 1  # scratch partials
+
+    def kjob(x):
+        return host(eng, eng.kurtosis(x))
+
+    def rjob(y):
+        return host(eng, eng.reduce(y, 8, 20000))
+
+    for _ in range(3):
+        with ThreadPoolExecutor(8) as ex:
+            ks = list(ex.map(kjob, xs))
+            rs = list(ex.map(rjob, ys * 2))
+        torch.cuda.synchronize()
+        for a, k in zip(arrs, ks):
+            assert_kurtosis(k, orc.kurtosis(a), "leaf", a.shape[2])
+        for a, r in zip(ints * 2, rs):
+            assert np.array_equal(r, orc.reduce(a, 8, 20000))

@@ -46,17 +46,14 @@ VARIANTS = {
     # narrow windows: time split over otherwise idle waves, with / without grid cap
     "notsfill": "-DBLDP_TS_FILL=0",
 
-    # kurtosis, short windows: predicated kernel for every nt; register budgets
+    # kurtosis: exact-count register kernel, LDS-transposed stores
     "kold": "-DBLDP_KURT_EXACT=0",
-    "kw5": "-DBLDP_KURT_WAVES=5",
-    "kw6": "-DBLDP_KURT_WAVES=6",
-    "kf32mean": "-DBLDP_KURT_F32MEAN=1",
-    "ktimingf32": "-DBLDP_KURT_TIMING_F32=1",  # timing only: wrong numerics
-    "ktimingall": "-DBLDP_KURT_TIMING_F32=1 -DBLDP_KURT_F32MEAN=1",
-    "kplainst": "-DBLDP_KURT_STORE=2",
-    "knostore": "-DBLDP_KURT_STORE=0",  # timing only: no output
     "kst1": "-DBLDP_KURT_STORE=1",
-    "kmid0": "-DBLDP_KURT_MID_NR=0",  # two passes beyond 32 spectra
+    # kurtosis, streamed leaves: spectra in flight per lane, waves/SIMD caps
+    "kleaf4": "-DBLDP_KURT_LEAF_B=4",
+    "kleaf16": "-DBLDP_KURT_LEAF_B=16",
+    "kleafw2": "-DBLDP_KURT_LEAF_WAVES=2",
+    "kleafw3": "-DBLDP_KURT_LEAF_WAVES=3",
 }
 
 
@@ -114,8 +111,7 @@ def run(names, rounds, iters, suite="main"):
         out = torch.empty(len(banks) * nc * nif, dtype=torch.float64, device="cuda")
         ptrs = (ctypes.c_void_p * len(banks))(*[b.data_ptr() for b in banks])
         keep, wp = pkg._lib.win_arg(win)
-        reads = 1 if nt <= 512 else 2
-        nbytes = len(banks) * (reads * 4 * nc * nif * nt + 8 * nc * nif)
+        nbytes = len(banks) * (4 * nc * nif * nt + 8 * nc * nif)  # input read once
 
         def go(L):
             rc = L.bldp_band_kurtosis_f32(len(banks), ctypes.cast(ptrs, ctypes.c_void_p), nchan,
@@ -135,6 +131,7 @@ def run(names, rounds, iters, suite="main"):
         kurt_case("kurt cfg4 nt879616", b4, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
         b5 = [eng.synth(65536, 1, 2048, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
         kurt_case("kurt 65536ch nt2048", b5)
+        kurt_case("kurt cfg4 1 bank", b4[:1], [0, 512, 1, 0, 1, 1, 0, 879616, 1])
         cases_done = True
     elif suite == "tile":  # tile path: misaligned starts and odd F at cfg3 scale
         n = 1 << 26
