@@ -242,6 +242,11 @@ __global__ __launch_bounds__(kB) void k_kurt_regs(const KurtArgs k) {
 // running sum handed on through LDS), every lane doing its own channel.  Then
 // z, z2 and the Float64 sums run over the registers and the 4 partial sums are
 // added through LDS in wave order.
+//   BLDP_KURT_MID_TIMING_NOCHAIN 1 = TIMING EXPERIMENT ONLY (wrong numerics):
+//                   the waves sum their quarters at once, pricing the hand-off
+#ifndef BLDP_KURT_MID_TIMING_NOCHAIN
+#define BLDP_KURT_MID_TIMING_NOCHAIN 0
+#endif
 template <int NR>
 __global__ __launch_bounds__(kB) void k_kurt_mid(const KurtArgs k) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -262,6 +267,12 @@ __global__ __launch_bounds__(kB) void k_kurt_mid(const KurtArgs k) {
   // Base.sum, sequential over the whole window (nt <= 1024 is one leaf)
   __shared__ float carry[64];
   float s = 0.0f;
+#if BLDP_KURT_MID_TIMING_NOCHAIN  // TIMING EXPERIMENT ONLY (wrong m): waves in parallel
+  for (int r = 0; r < NR; ++r)
+    if (r < cnt) s += v[r];
+  carry[lane] = s;
+  __syncthreads();
+#else
 #pragma unroll 1
   for (int w = 0; w < 4; ++w) {
     if (wave == w) {
@@ -273,6 +284,7 @@ __global__ __launch_bounds__(kB) void k_kurt_mid(const KurtArgs k) {
     }
     __syncthreads();
   }
+#endif
   const float m = carry[lane] / (float)nt;
   double c2 = 0.0, c4 = 0.0;
 #pragma unroll
@@ -311,7 +323,7 @@ __global__ __launch_bounds__(kB) void k_kurt_mid(const KurtArgs k) {
 // bytes per lane per quantity.
 //   BLDP_KURT_LEAF_B  spectra in flight per lane
 #ifndef BLDP_KURT_LEAF_B
-#define BLDP_KURT_LEAF_B 8
+#define BLDP_KURT_LEAF_B 4
 #endif
 //   BLDP_KURT_LEAF_WAVES  cap on resident waves per SIMD (0 = the register budget's)
 #ifndef BLDP_KURT_LEAF_WAVES
@@ -883,16 +895,18 @@ hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s) {
       hipLaunchKernelGGL((k_kurt_regs<32, false>), g1, block, 0, s, k);
     return hipGetLastError();
   }
-  if (p == KP_MID) {
+  if (p == KP_MID) {  // registers sized to the quarter window, 16 spectra at a time
     const dim3 g1((unsigned)(cdivk(k.nc, 64) * k.nrow));
-    if (k.nt <= 128)
-      hipLaunchKernelGGL(k_kurt_mid<32>, g1, block, 0, s, k);
-    else if (k.nt <= 256)
-      hipLaunchKernelGGL(k_kurt_mid<64>, g1, block, 0, s, k);
-    else if (k.nt <= 384)
-      hipLaunchKernelGGL(k_kurt_mid<96>, g1, block, 0, s, k);
-    else
-      hipLaunchKernelGGL(k_kurt_mid<128>, g1, block, 0, s, k);
+    switch (cdivk(cdivk(k.nt, 4), 16)) {
+      case 1: hipLaunchKernelGGL(k_kurt_mid<16>, g1, block, 0, s, k); break;
+      case 2: hipLaunchKernelGGL(k_kurt_mid<32>, g1, block, 0, s, k); break;
+      case 3: hipLaunchKernelGGL(k_kurt_mid<48>, g1, block, 0, s, k); break;
+      case 4: hipLaunchKernelGGL(k_kurt_mid<64>, g1, block, 0, s, k); break;
+      case 5: hipLaunchKernelGGL(k_kurt_mid<80>, g1, block, 0, s, k); break;
+      case 6: hipLaunchKernelGGL(k_kurt_mid<96>, g1, block, 0, s, k); break;
+      case 7: hipLaunchKernelGGL(k_kurt_mid<112>, g1, block, 0, s, k); break;
+      default: hipLaunchKernelGGL(k_kurt_mid<128>, g1, block, 0, s, k); break;
+    }
     return hipGetLastError();
   }
   const KLayout L = layout(k);

@@ -54,6 +54,7 @@ VARIANTS = {
     "kleaf16": "-DBLDP_KURT_LEAF_B=16",
     "kleafw2": "-DBLDP_KURT_LEAF_WAVES=2",
     "kleafw3": "-DBLDP_KURT_LEAF_WAVES=3",
+    "kmidnochain": "-DBLDP_KURT_MID_TIMING_NOCHAIN=1",  # timing only: wrong numerics
 }
 
 

@@ -29,7 +29,7 @@ run() {  # name seconds cmd...
 for s in $STEPS; do
   case $s in
     smoke) run smoke 300 python -c "import __graft_entry__ as e; e.smoke()" ;;
-    tests) run tests 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    tests) run tests 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     bench) run bench 600 python bench.py ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv \
              -d "$OUT/prof" -o run -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
@@ -57,6 +57,13 @@ for s in $STEPS; do
              -d "$OUT/prof_decode" -o run -- python bench.py --mode decode ;;
     prof_kurt) run prof_kurt 600 rocprofv3 --kernel-trace --stats --output-format csv \
              -d "$OUT/prof_kurt" -o run -- python bench.py --mode kurtosis --config cfg3 ;;
+    prof_kurt_*) run "$s" 600 rocprofv3 --kernel-trace --stats --output-format csv \
+             -d "$OUT/$s" -o run -- python bench.py --mode kurtosis --config "${s#prof_kurt_}" ;;
+    pmc_kurt_*) C=${s#pmc_kurt_}
+           run "pmc_fetch_kurt_$C" 300 rocprofv3 --pmc FETCH_SIZE --output-format csv \
+             -d "$OUT/pmc_fetch_kurt_$C" -o run -- python bench.py --mode kurtosis --config "$C" --steps 5 --warmup 2
+           run "pmc_write_kurt_$C" 300 rocprofv3 --pmc WRITE_SIZE --output-format csv \
+             -d "$OUT/pmc_write_kurt_$C" -o run -- python bench.py --mode kurtosis --config "$C" --steps 5 --warmup 2 ;;
     dist2) run dist2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
              --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --dist-backend gloo \
              --steps 10 --warmup 3 ;;
