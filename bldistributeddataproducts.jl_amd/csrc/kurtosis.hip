@@ -312,34 +312,62 @@ __global__ __launch_bounds__(kB) void k_kurt_mid(const KurtArgs k) {
 }
 
 // ---------------------------------------------------------------------------
-// nt > 512: one wave per (leaf slot, 64 float4 columns, bank x IF row).  Each
-// lane streams its column down the leaf (<= 1024 spectra, B loads in flight):
+// nt > 512: one wave per (leaf slot, 64 columns of W channels, bank x IF
+// row).  Each lane streams its column down the leaf (<= 1024 spectra, B
+// spectra per batch, the next batch's loads in flight while one is
+// processed):
 //   * the leaf's sequential Float32 sum (Base.mapreduce_impl's inner loop),
 //   * max and min,
 //   * Float64 power sums of d = x - c about the leaf's first spectrum c.  Any
 //     |c - mean| is at most the largest deviation, which also bounds M4 from
 //     below, so moving the sums to the leaf's mean loses at most ~len ulps.
-// Writes the leaf's (mean, M2, M3, M4) and (sum, max, min), 32 contiguous
-// bytes per lane per quantity.
-//   BLDP_KURT_LEAF_B  spectra in flight per lane
+// Writes the leaf's (mean, M2, M3, M4) and (sum, max, min), W contiguous
+// values per lane per quantity.
+//   BLDP_KURT_LEAF_B      spectra per batch
+//   BLDP_KURT_LEAF_W      channels per lane (4: 16-byte loads, 1 KiB per
+//                         wave-instruction; 2: 8-byte loads, twice the waves)
+//   BLDP_KURT_LEAF_PIPE   1 = the next batch's loads issue before this batch
+//                         is processed
+//   BLDP_KURT_LEAF_WAVES  cap on resident waves per SIMD (0 = the register budget's)
 #ifndef BLDP_KURT_LEAF_B
 #define BLDP_KURT_LEAF_B 4
 #endif
-//   BLDP_KURT_LEAF_WAVES  cap on resident waves per SIMD (0 = the register budget's)
+#ifndef BLDP_KURT_LEAF_W
+#define BLDP_KURT_LEAF_W 4
+#endif
+#ifndef BLDP_KURT_LEAF_PIPE
+#define BLDP_KURT_LEAF_PIPE 0
+#endif
 #ifndef BLDP_KURT_LEAF_WAVES
 #define BLDP_KURT_LEAF_WAVES 0
 #endif
+constexpr int kLeafW = BLDP_KURT_LEAF_W;
+static_assert(kLeafW == 1 || kLeafW == 2 || kLeafW == 4, "BLDP_KURT_LEAF_W: 1, 2 or 4");
+
+template <int W>
+__device__ __forceinline__ void ldw(const float *p, float (&x)[W]) {
+  if constexpr (W == 4) {
+    const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(p));
+    x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+  } else if constexpr (W == 2) {
+    const f2v v = __builtin_nontemporal_load(reinterpret_cast<const f2v *>(p));
+    x[0] = v.x; x[1] = v.y;
+  } else {
+    x[0] = __builtin_nontemporal_load(p);
+  }
+}
+
+template <int W>
 struct LeafAcc {
-  f2v sa, sb;  // Float32 sums of channels (0,1) and (2,3)
-  float hi[4], lo[4];
-  double c[4], a1[4], a2[4], a3[4], a4[4];
+  float s[W];  // Float32 sums
+  float hi[W], lo[W];
+  double c[W], a1[W], a2[W], a3[W], a4[W];
 };
-__device__ __forceinline__ void leaf_step(LeafAcc &A, const float4 q) {
-  A.sa += f2v{q.x, q.y};
-  A.sb += f2v{q.z, q.w};
-  const float x[4] = {q.x, q.y, q.z, q.w};
+template <int W>
+__device__ __forceinline__ void leaf_step(LeafAcc<W> &A, const float (&x)[W]) {
 #pragma unroll
-  for (int w = 0; w < 4; ++w) {
+  for (int w = 0; w < W; ++w) {
+    A.s[w] += x[w];
     A.hi[w] = fmaxf(A.hi[w], x[w]);
     A.lo[w] = fminf(A.lo[w], x[w]);
     const double d = (double)x[w] - A.c[w], d2 = d * d;
@@ -350,61 +378,93 @@ __device__ __forceinline__ void leaf_step(LeafAcc &A, const float4 q) {
   }
 }
 
+template <int W, typename T>
+__device__ __forceinline__ void stw(T *p, const T (&v)[W]) {
+  if constexpr (W == 4 && sizeof(T) == 4) {
+    *reinterpret_cast<f4v *>(p) = f4v{v[0], v[1], v[2], v[3]};
+  } else if constexpr (W >= 2) {
+    typedef T t2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int w = 0; w < W; w += 2) *reinterpret_cast<t2 *>(p + w) = t2{v[w], v[w + 1]};
+  } else {
+    p[0] = v[0];
+  }
+}
+
 __global__ __launch_bounds__(kB)
 #if BLDP_KURT_LEAF_WAVES > 0
 __attribute__((amdgpu_waves_per_eu(1, BLDP_KURT_LEAF_WAVES)))
 #endif
 void k_kurt_leaf(const KurtArgs k) {
-  constexpr int B = BLDP_KURT_LEAF_B;
+  constexpr int B = BLDP_KURT_LEAF_B, W = kLeafW;
   const int lane = threadIdx.x & 63;
   const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t seg = u % k.nseg, r = u / k.nseg;
   const int64_t slot = r % k.nslot, row = r / k.nslot;
   const int64_t col = seg * 64 + lane;
-  if (row >= k.nrow || col >= k.nc / 4) return;
+  if (row >= k.nrow || col >= k.nc / W) return;
   int64_t t0, len;
   pw_leaf(k.nt, k.K, slot, t0, len);
   if (len <= 0) return;
   const int bank = (int)(row / k.ni);
   const int64_t i = row - (int64_t)bank * k.ni;
   const int64_t ld = k.in_ld_t;
-  const float *p = k.in[bank] + k.in_off + i * k.in_ld_i + 4 * col + t0 * ld;
-  LeafAcc A;
+  const float *p = k.in[bank] + k.in_off + i * k.in_ld_i + W * col + t0 * ld;
+  LeafAcc<W> A;
   {
-    const float4 x0 = ldnt(p);
-    A.sa = f2v{x0.x, x0.y};
-    A.sb = f2v{x0.z, x0.w};
-    const float x[4] = {x0.x, x0.y, x0.z, x0.w};
+    float x0[W];
+    ldw<W>(p, x0);
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      A.hi[w] = A.lo[w] = x[w];
-      A.c[w] = (double)x[w];
+    for (int w = 0; w < W; ++w) {
+      A.s[w] = A.hi[w] = A.lo[w] = x0[w];  // the sum starts from the first element
+      A.c[w] = (double)x0[w];
       A.a1[w] = A.a2[w] = A.a3[w] = A.a4[w] = 0.0;
     }
   }
   p += ld;
-  int64_t rem = len - 1;
-  for (; rem >= B; rem -= B, p += B * ld) {
-    float4 v[B];
+  const int64_t rem = len - 1, nb = rem / B;
+  float cur[B][W];
+  if (nb > 0) {
 #pragma unroll
-    for (int q = 0; q < B; ++q) v[q] = ldnt(p + q * ld);
-#pragma unroll
-    for (int q = 0; q < B; ++q) leaf_step(A, v[q]);
+    for (int q = 0; q < B; ++q) ldw<W>(p + q * ld, cur[q]);
   }
-  if (rem > 0) {
-    float4 v[B];
+  for (int64_t bt = 0; bt < nb; ++bt) {
+    p += B * ld;
+#if BLDP_KURT_LEAF_PIPE
+    float nxt[B][W];
+    if (bt + 1 < nb) {
+#pragma unroll
+      for (int q = 0; q < B; ++q) ldw<W>(p + q * ld, nxt[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < B; ++q) leaf_step<W>(A, cur[q]);
 #pragma unroll
     for (int q = 0; q < B; ++q)
-      if (q < rem) v[q] = ldnt(p + q * ld);
+#pragma unroll
+      for (int w = 0; w < W; ++w) cur[q][w] = nxt[q][w];
+#else
+#pragma unroll
+    for (int q = 0; q < B; ++q) leaf_step<W>(A, cur[q]);
+    if (bt + 1 < nb) {
+#pragma unroll
+      for (int q = 0; q < B; ++q) ldw<W>(p + q * ld, cur[q]);
+    }
+#endif
+  }
+  const int tail = (int)(rem - nb * B);
+  if (tail > 0) {
 #pragma unroll
     for (int q = 0; q < B; ++q)
-      if (q < rem) leaf_step(A, v[q]);
+      if (q < tail) ldw<W>(p + q * ld, cur[q]);
+#pragma unroll
+    for (int q = 0; q < B; ++q)
+      if (q < tail) leaf_step<W>(A, cur[q]);
   }
-  const int64_t n = k.nrow * k.nc, e = row * k.nc + 4 * col;
+  const int64_t n = k.nrow * k.nc, e = row * k.nc + W * col;
   const double cnt = (double)len;
-  double mo[4][4];
+  double mo[4][W];
 #pragma unroll
-  for (int w = 0; w < 4; ++w) {
+  for (int w = 0; w < W; ++w) {
     const double dl = A.a1[w] / cnt, dl2 = dl * dl;
     mo[0][w] = A.c[w] + dl;
     mo[1][w] = A.a2[w] - A.a1[w] * dl;
@@ -412,17 +472,10 @@ void k_kurt_leaf(const KurtArgs k) {
     mo[3][w] = A.a4[w] - 4.0 * dl * A.a3[w] + 6.0 * dl2 * A.a2[w] - 3.0 * cnt * dl2 * dl2;
   }
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    d2v *o = reinterpret_cast<d2v *>(k.pm + (q * k.nslot + slot) * n + e);
-    o[0] = d2v{mo[q][0], mo[q][1]};
-    o[1] = d2v{mo[q][2], mo[q][3]};
-  }
-  f4v *of = reinterpret_cast<f4v *>(k.pf + slot * n + e);
-  of[0] = f4v{A.sa.x, A.sa.y, A.sb.x, A.sb.y};
-  of = reinterpret_cast<f4v *>(k.pf + (k.nslot + slot) * n + e);
-  of[0] = f4v{A.hi[0], A.hi[1], A.hi[2], A.hi[3]};
-  of = reinterpret_cast<f4v *>(k.pf + (2 * k.nslot + slot) * n + e);
-  of[0] = f4v{A.lo[0], A.lo[1], A.lo[2], A.lo[3]};
+  for (int q = 0; q < 4; ++q) stw<W, double>(k.pm + (q * k.nslot + slot) * n + e, mo[q]);
+  stw<W, float>(k.pf + slot * n + e, A.s);
+  stw<W, float>(k.pf + (k.nslot + slot) * n + e, A.hi);
+  stw<W, float>(k.pf + (2 * k.nslot + slot) * n + e, A.lo);
 }
 
 // Unaligned windows: one lane per (column, leaf) runs the sequential Float32
@@ -854,7 +907,7 @@ hipError_t launch_tree(const KurtArgs &k, char *ws, const KLayout &L, hipStream_
 void plan_kurtosis(KurtArgs &k, int num_cus) {
   k.K = pw_level(std::max<int64_t>(k.nt, 1));
   k.nslot = (int64_t)2 << k.K;
-  k.nseg = cdivk(k.nc / 4, 64);
+  k.nseg = cdivk(k.nc / kLeafW, 64);
   // two-pass z pass: waves splitting the spectra of a tile, >= 16 spectra per wave
   k.ts = 1;
   while (k.ts < 4 && k.nt >= (int64_t)32 * k.ts) k.ts *= 2;

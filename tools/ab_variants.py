@@ -50,8 +50,12 @@ VARIANTS = {
     "kold": "-DBLDP_KURT_EXACT=0",
     "kst1": "-DBLDP_KURT_STORE=1",
     # kurtosis, streamed leaves: spectra in flight per lane, waves/SIMD caps
-    "kleaf4": "-DBLDP_KURT_LEAF_B=4",
-    "kleaf16": "-DBLDP_KURT_LEAF_B=16",
+    "kleaf8": "-DBLDP_KURT_LEAF_B=8",
+    "kleafpipe": "-DBLDP_KURT_LEAF_PIPE=1",
+    "kleafpipe8": "-DBLDP_KURT_LEAF_PIPE=1 -DBLDP_KURT_LEAF_B=8",
+    "kleafw2ch": "-DBLDP_KURT_LEAF_W=2",
+    "kleafw2chpipe": "-DBLDP_KURT_LEAF_W=2 -DBLDP_KURT_LEAF_PIPE=1",
+    "kleafw1ch": "-DBLDP_KURT_LEAF_W=1 -DBLDP_KURT_LEAF_B=8",
     "kleafw2": "-DBLDP_KURT_LEAF_WAVES=2",
     "kleafw3": "-DBLDP_KURT_LEAF_WAVES=3",
     "kmidnochain": "-DBLDP_KURT_MID_TIMING_NOCHAIN=1",  # timing only: wrong numerics
