@@ -72,37 +72,66 @@ def traffic_from_profile(cfg_name, n_local_banks):
     return e.get("hbm_bytes_per_launch") if e else None
 
 
+def host_cpu_info():
+    """The host this runs on: CPU model, the machine's logical CPUs (nproc)
+    and the CPUs this process may use (the GPU box's share of a node)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    return {"cpu_model": model, "host_nproc": os.cpu_count(), "affinity_cpus": aff,
+            "omp_num_threads": int(omp) if omp.isdigit() else None}
+
+
 def cpu_baseline(cfg, seconds, eng, torch):
-    """The oracle (C restatement, one thread per bank like one Distributed
-    worker per bank) on a bounded sample of the same workload."""
+    """The oracle (C restatement) on the FULL banks of the workload, on this
+    host's cores: one pthread per bank (GBT.getdata's one Distributed worker
+    per bank, src/gbt.jl:75-77) is the baseline; the same arithmetic over a
+    pool of every CPU this process may use is reported beside it."""
     import __graft_entry__ as entry
 
     orc = entry.load_oracle()
     nb = cfg["nbank"]
-    nch = min(cfg["nchan"], 1 << 22) if cfg["nchan"] >= 1 << 22 else cfg["nchan"]
-    nt = min(cfg["tw"], 16 * 1024) if cfg["T"] <= 16 * 1024 else cfg["tw"]
-    nt -= nt % cfg["T"]
+    nch, nt = cfg["nchan"], cfg["tw"] - cfg["tw"] % cfg["T"]
     banks = []
-    for b in range(nb):
+    for b in range(nb):  # the window's bytes, generated on the GPU, copied to host memory
         t = eng.synth(nch, cfg["nif"], nt, cfg["nfpc"], seed=10 * b + cfg["product"], kind=0)
         banks.append(eng.fb_to_numpy(t))
         del t
     torch.cuda.empty_cache()
-    per_rep = sum(4 * (nch * cfg["nif"] * nt + (nch // cfg["F"]) * cfg["nif"] * (nt // cfg["T"]))
-                  for _ in range(nb))
-    orc.reduce_banks_mt(banks, cfg["F"], cfg["T"])  # warm
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        orc.reduce_banks_mt(banks, cfg["F"], cfg["T"])
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= seconds and reps >= 3:
-            break
-    return {"value": round(per_rep * reps / el / 1e9, 3), "unit": "GB/s", "cores": nb,
-            "kind": "port",
-            "sample": f"{nb} banks x ({nch} ch x {cfg['nif']} IF x {nt} spectra), F={cfg['F']} "
-                      f"T={cfg['T']}, {reps} reps in {el:.1f} s, oracle/bldp_oracle.c "
-                      f"(float64 accumulate), one pthread per bank"}
+    per_rep = nb * 4 * (nch * cfg["nif"] * nt + (nch // cfg["F"]) * cfg["nif"] * (nt // cfg["T"]))
+    info = host_cpu_info()
+    nthr = info["omp_num_threads"] or info["affinity_cpus"]
+
+    def timed(fn, secs):
+        fn()  # warm (page faults)
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            fn()
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= secs and reps >= 2:
+                return per_rep * reps / el / 1e9, reps, el
+
+    gbs, reps, el = timed(lambda: orc.reduce_banks_mt(banks, cfg["F"], cfg["T"]), 0.6 * seconds)
+    gall, reps_all, el_all = timed(
+        lambda: orc.reduce_banks_pool(banks, cfg["F"], cfg["T"], "sum", nthr), 0.4 * seconds)
+    return dict({"value": round(gbs, 3), "unit": "GB/s", "cores": nb, "kind": "port",
+                 "sample": f"the full workload: {nb} banks x ({nch} ch x {cfg['nif']} IF x {nt} "
+                           f"spectra), F={cfg['F']} T={cfg['T']}, {reps} passes in {el:.1f} s; "
+                           "oracle/bldp_oracle.c (Float64 accumulate, gcc -O3 x86-64-v3), "
+                           "one pthread per bank as one Distributed worker per bank",
+                 "all_cores": {"value": round(gall, 3), "threads": nthr,
+                               "sample": f"same banks, output channels split over {nthr} "
+                                         f"threads, {reps_all} passes in {el_all:.1f} s"}},
+                **info)
 
 
 def pairwise_leaves(n):
@@ -166,63 +195,101 @@ def bench_kurtosis(args, cfg, eng, torch):
 CFG5_PRODUCTS = ["cfg3", "cfg4", "cfg1"]  # 0000, 0001, 0002 single-bank geometry
 
 
-def bench_host(args, eng, torch, pkg):
-    """cfg5: a session scan streamed from pinned host memory.  This GPU's share
-    is bank b of every band: 4 bands x {0000, 0001, 0002}.  Each array goes
-    through bldp_reduce_host_f32 (the Julia worker drop-in: host array in,
-    reduced host array out).  Bound by PCIe (H2D), reported as such."""
+def bench_host(args, eng, torch, pkg, rank=0, world=1, dist=None):
+    """cfg5, the multi-band session scan streamed from pinned host memory:
+    rank r takes bank r of every band, 4 bands x {0000, 0001, 0002} (12
+    arrays, 24.7 GB), each through bldp_reduce_host_f32 (the Julia worker
+    drop-in: host array in, reduced host array out).  At N ranks the node
+    streams N banks of every band (weak scaling; N = 8 is all of cfg5: 4
+    bands x 8 banks x 3 products).  Bound by PCIe (H2D), reported per GPU and
+    for the node, beside the reduce kernels' HBM rate on device-resident
+    copies of the same arrays."""
     import numpy as np
 
-    arrays = []
+    dev = torch.cuda.current_device()
+    bank = rank
+    arrays, krate = [], []
     for band in range(4):
         for name in CFG5_PRODUCTS:
             c = CONFIGS[name]
+            # seed = 1000*band + 10*bank + product (SURVEY.md §8d D2)
             t = eng.synth(c["nchan"], c["nif"], c["ntime"], c["nfpc"],
-                          seed=1000 * band + c["product"], kind=0)
+                          seed=1000 * band + 10 * bank + c["product"], kind=0)
+            win = None if c["tw"] == c["ntime"] else [0, c["nchan"], 1, 0, c["nif"], 1, 0,
+                                                      c["tw"], 1]
+            if band == 0:  # the kernel's HBM rate on a device-resident copy
+                eng.reduce(t, c["F"], c["T"], "sum", win)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(5):
+                    eng.reduce(t, c["F"], c["T"], "sum", win)
+                e1.record()
+                e1.synchronize()
+                b = 4 * c["nif"] * (c["nchan"] * c["tw"] + (c["nchan"] // c["F"]) * (c["tw"] // c["T"]))
+                krate.append((b, e0.elapsed_time(e1) / 5))
             h = torch.empty((c["ntime"], c["nif"], c["nchan"]), dtype=torch.float32,
                             pin_memory=True)
             h.copy_(t.permute(2, 1, 0))
             del t
             a = h.numpy().transpose(2, 1, 0)  # Julia-order, Fortran-contiguous, pinned
-            win = None if c["tw"] == c["ntime"] else [0, c["nchan"], 1, 0, c["nif"], 1, 0,
-                                                      c["tw"], 1]
             arrays.append((a, h, c, win))
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     nbytes = sum(4 * c["nchan"] * c["nif"] * c["tw"] for _, _, c, _ in arrays)
+    kern_gbs = sum(b for b, _ in krate) / (sum(ms for _, ms in krate) * 1e-3) / 1e9
 
     def one_pass():
         for a, _, c, win in arrays:
-            eng.reduce_host(a, c["F"], c["T"], "sum", win, device=torch.cuda.current_device())
+            eng.reduce_host(a, c["F"], c["T"], "sum", win, device=dev)
 
-    for _ in range(max(1, args.warmup // 5)):
+    warm = max(1, args.warmup // 5)
+    for _ in range(warm):
         one_pass()
     steps = max(1, args.steps // 10)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
         one_pass()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     el = (time.perf_counter() - t0) / steps
-    gbs = nbytes / el / 1e9
-    # the same arrays in ordinary (pageable) host memory, the Julia Array case
-    pageable = [(np.asfortranarray(np.array(a, copy=True)), None, c, win)
-                for a, _, c, win in arrays[:3]]
-    pbytes = sum(4 * c["nchan"] * c["nif"] * c["tw"] for _, _, c, _ in pageable)
-    t0 = time.perf_counter()
-    for a, _, c, win in pageable:
-        eng.reduce_host(a, c["F"], c["T"], "sum", win, device=torch.cuda.current_device())
-    pg = pbytes / (time.perf_counter() - t0) / 1e9
-    return {"metric": "session scan GB/s streamed from pinned host memory (per GPU)",
-            "value": round(gbs, 2), "unit": "GB/s", "n_gpus": 1, "steps": steps,
-            "warmup": max(1, args.warmup // 5), "ms_per_step": round(el * 1e3, 2),
+    el_max = el
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64,
+                          device="cuda" if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el_max = float(tt[0])
+    per_gpu = nbytes / el / 1e9
+    node = world * nbytes / el_max / 1e9
+    pg = None
+    if rank == 0 and world == 1:  # the same arrays in ordinary (pageable) host memory
+        pageable = [(np.asfortranarray(np.array(a, copy=True)), None, c, win)
+                    for a, _, c, win in arrays[:3]]
+        pbytes = sum(4 * c["nchan"] * c["nif"] * c["tw"] for _, _, c, _ in pageable)
+        t1 = time.perf_counter()
+        for a, _, c, win in pageable:
+            eng.reduce_host(a, c["F"], c["T"], "sum", win, device=dev)
+        pg = round(pbytes / (time.perf_counter() - t1) / 1e9, 2)
+    return {"metric": "session scan GB/s streamed from pinned host memory (node)",
+            "value": round(node, 2), "unit": "GB/s", "n_gpus": world, "steps": steps,
+            "warmup": warm, "ms_per_step": round(el_max * 1e3, 2),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic, pinned host memory (torch pin_memory)",
-            "config": {"workload": "cfg5 share of one GPU: 4 bands x {0000, 0001, 0002}, "
-                                   "bldp_reduce_host_f32 per array", "bytes_per_step": nbytes,
-                       "pageable_GBps": round(pg, 2),
+            "data": "synthetic (bldp_synth_f32), pinned host memory (torch pin_memory)",
+            "config": {"workload": f"cfg5: rank r streams bank r of 4 bands x {{0000, 0001, "
+                                   f"0002}} through bldp_reduce_host_f32 ({world} bank(s) of "
+                                   f"every band on the node; 8 = all 96 arrays)",
+                       "bytes_per_step_per_gpu": nbytes, "per_gpu_GBps": round(per_gpu, 2),
+                       "kernel_hbm_GBps": round(kern_gbs, 1),
+                       "kernel_hbm_note": "reduce kernels on device-resident copies of band "
+                                          "0's three arrays (HIP events)",
+                       "pageable_GBps": pg,
                        "pageable_sample": "band 0 x {0000, 0001, 0002}, ordinary numpy memory"},
-            "roofline": {"bound": "pcie", "achieved": round(gbs, 2), "peak": 63.0,
-                         "unit": "GB/s", "frac": round(gbs / 63.0, 4), "traffic": None,
-                         "kernel": "H2D copy engine (PCIe Gen5 x16 spec 63 GB/s)"}}
+            "roofline": {"bound": "pcie", "achieved": round(per_gpu, 2), "peak": 63.0,
+                         "unit": "GB/s", "frac": round(per_gpu / 63.0, 4), "traffic": None,
+                         "kernel": "H2D copy engine (PCIe Gen5 x16 spec 63 GB/s per GPU)"}}
 
 
 def bench_decode(args, eng, torch, pkg):
@@ -452,14 +519,26 @@ def main():
         else:
             dist.init_process_group("gloo")
     cfg = CONFIGS[args.config]
+    run_info = {"dist_backend": args.dist_backend if use_pg else None,
+                "world_size": dist.get_world_size() if use_pg else 1,
+                "device_count": torch.cuda.device_count()}
+    if args.mode == "host":
+        r = bench_host(args, eng, torch, pkg, rank, world, dist if use_pg else None)
+        r["config"].update(run_info)
+        if rank == 0:
+            print(json.dumps(r), flush=True)
+        if use_pg:
+            dist.barrier()
+            dist.destroy_process_group()
+        return r
     if args.mode != "reduce":
         if world != 1:
-            raise SystemExit("--mode kurtosis/host are single-GPU measurements")
+            raise SystemExit("--mode kurtosis/decode/file/rawfile are single-GPU measurements")
         r = (bench_kurtosis(args, cfg, eng, torch) if args.mode == "kurtosis"
              else bench_decode(args, eng, torch, pkg) if args.mode == "decode"
              else bench_file(args, eng, torch, pkg) if args.mode == "file"
-             else bench_rawfile(args, eng, torch, pkg) if args.mode == "rawfile"
-             else bench_host(args, eng, torch, pkg))
+             else bench_rawfile(args, eng, torch, pkg))
+        r["config"].update(run_info)
         print(json.dumps(r), flush=True)
         return r
     nb = cfg["nbank"]
@@ -541,6 +620,15 @@ def main():
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
     traffic = traffic_from_profile(args.config, len(mine))
 
+    ndev = torch.cuda.device_count()
+    if not pipe:
+        parallelism = f"{len(mine)} bank(s) x 1 GPU, single-launch band reduce + stitch"
+    elif args.dist_backend == "nccl":
+        parallelism = (f"{len(mine)} bank(s)/GPU x {world} GPU(s), RCCL (nccl backend) gather "
+                       "over xGMI + stitch; the gather of step k overlaps the reduce of step k+1")
+    else:
+        parallelism = (f"REHEARSAL, not a scaling number: {world} ranks on {ndev} GPU(s), gloo "
+                       f"backend (CPU transport) gather + stitch, {len(mine)} bank(s)/rank")
     result = None
     if rank == 0:
         cpu = None
@@ -559,11 +647,8 @@ def main():
                        "nchan": cfg["nchan"], "nif": cfg["nif"], "ntime": cfg["tw"],
                        "fqavby": cfg["F"], "tavby": cfg["T"],
                        "band_alloc": args.band_alloc,
-                       "parallelism": f"{len(mine)} bank(s)/GPU x {world} GPU(s)"
-                                      + (", RCCL gather + stitch (gather of step k overlaps "
-                                         "the reduce of step k+1)" if pipe else
-                                         ", single-launch band reduce+stitch"),
-                       "bytes_per_step": bytes_step},
+                       "parallelism": parallelism,
+                       "bytes_per_step": bytes_step, **run_info},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "kernel": kernel_name,

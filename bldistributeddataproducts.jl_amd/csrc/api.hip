@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -358,6 +359,10 @@ int bldp_band_reduce_multi_f32(int nbank, const int *bank_dev, const float *cons
   if (nco * ni * nto == 0) return BLDP_OK;
   if (!out) return fail(BLDP_EINVAL, "null output pointer");
   const int64_t ld_i = (int64_t)nbank * nco, ld_t = ld_i * ni;
+  // BLDP_FORCE_STAGED=1 (tests): every bank takes the staged branch (local
+  // reduce + strided copy into the root's slot), even on the root device
+  const char *fs = std::getenv("BLDP_FORCE_STAGED");
+  const bool force_staged = fs && fs[0] == '1';
   int prev = 0;
   HIPCHK(hipGetDevice(&prev));
   std::vector<hipStream_t> streams(ndev, nullptr);
@@ -370,8 +375,8 @@ int bldp_band_reduce_multi_f32(int nbank, const int *bank_dev, const float *cons
       rc = fail(BLDP_EHIP, "hipSetDevice(%d) failed", d);
       break;
     }
-    bool direct = d == root;
-    if (!direct) {  // kernels write the root's product over xGMI when peer access works
+    bool direct = d == root && !force_staged;
+    if (!direct && !force_staged) {  // kernels write the root's product over xGMI when peer access works
       int can = 0;
       if (hipDeviceCanAccessPeer(&can, d, root) == hipSuccess && can) {
         hipError_t pe = hipDeviceEnablePeerAccess(root, 0);

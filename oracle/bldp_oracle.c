@@ -83,6 +83,39 @@ static int resolve(int64_t nchan, int64_t nif, int64_t ntime, const int64_t *win
  * :19  dropdims(f(...; dims=1))    -> one value per group
  * Output dense (nco, ni, nto), Julia column-major.
  */
+/* Outputs [co0, co1) of IF row i, time block to (the body of oracle_reduce). */
+static void reduce_range(const float *in, const geo_t *g, int64_t F, int64_t T, int op, float *out,
+                         int64_t nco, int64_t i, int64_t to, int64_t co0, int64_t co1) {
+  for (int64_t co = co0; co < co1; ++co) {
+    const float *p = in + g->off + i * g->ldi + to * T * g->ldt + co * F * g->cs;
+    float *o = out + co + nco * (i + g->ni * to);
+    if (op == OP_SUM || op == OP_MEAN) {
+      double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int64_t tt = 0; tt < T; ++tt) {
+        const float *r = p + tt * g->ldt;
+        int64_t k = 0;
+        if (g->cs == 1)
+          for (; k + 8 <= F; k += 8)
+            for (int u = 0; u < 8; ++u) acc[u] += (double)r[k + u];
+        for (; k < F; ++k) acc[0] += (double)r[k * g->cs];
+      }
+      double s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+      /* Julia's reducedim init is zero(Float32) = +0.0, so an all -0.0
+       * group sums to +0.0; 0.0 + s reproduces that. */
+      if (op == OP_MEAN) s = s / (double)(F * T);
+      *o = (float)(0.0 + s);
+    } else {
+      float m = op == OP_MAX ? -INFINITY : INFINITY;
+      for (int64_t tt = 0; tt < T; ++tt)
+        for (int64_t k = 0; k < F; ++k) {
+          const float v = p[tt * g->ldt + k * g->cs];
+          m = op == OP_MAX ? jmax(m, v) : jmin(m, v);
+        }
+      *o = m;
+    }
+  }
+}
+
 int oracle_reduce(const float *in, int64_t nchan, int64_t nif, int64_t ntime, const int64_t *win,
                   int64_t fqavby, int64_t tavby, int op, float *out) {
   geo_t g;
@@ -93,35 +126,7 @@ int oracle_reduce(const float *in, int64_t nchan, int64_t nif, int64_t ntime, co
   if (g.nc % F || g.nt % T) return -2;
   const int64_t nco = g.nc / F, nto = g.nt / T;
   for (int64_t to = 0; to < nto; ++to)
-    for (int64_t i = 0; i < g.ni; ++i)
-      for (int64_t co = 0; co < nco; ++co) {
-        const float *p = in + g.off + i * g.ldi + to * T * g.ldt + co * F * g.cs;
-        float *o = out + co + nco * (i + g.ni * to);
-        if (op == OP_SUM || op == OP_MEAN) {
-          double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-          for (int64_t tt = 0; tt < T; ++tt) {
-            const float *r = p + tt * g.ldt;
-            int64_t k = 0;
-            if (g.cs == 1)
-              for (; k + 8 <= F; k += 8)
-                for (int u = 0; u < 8; ++u) acc[u] += (double)r[k + u];
-            for (; k < F; ++k) acc[0] += (double)r[k * g.cs];
-          }
-          double s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
-          /* Julia's reducedim init is zero(Float32) = +0.0, so an all -0.0
-           * group sums to +0.0; 0.0 + s reproduces that. */
-          if (op == OP_MEAN) s = s / (double)(F * T);
-          *o = (float)(0.0 + s);
-        } else {
-          float m = op == OP_MAX ? -INFINITY : INFINITY;
-          for (int64_t tt = 0; tt < T; ++tt)
-            for (int64_t k = 0; k < F; ++k) {
-              const float v = p[tt * g.ldt + k * g.cs];
-              m = op == OP_MAX ? jmax(m, v) : jmin(m, v);
-            }
-          *o = m;
-        }
-      }
+    for (int64_t i = 0; i < g.ni; ++i) reduce_range(in, &g, F, T, op, out, nco, i, to, 0, nco);
   return 0;
 }
 
@@ -261,7 +266,59 @@ void oracle_synth(float *out, int64_t nchan, int64_t nif, int64_t ntime, int64_t
 }
 
 /* CPU baseline: one thread per bank, the way GBT.getdata runs one
- * Distributed worker per bank file (src/gbt.jl:75-77). */
+ * Distributed worker per bank file (src/gbt.jl:75-77).  With nthreads > 0
+ * the banks' output channels are instead split into pieces taken by
+ * nthreads threads (all cores on one node, same arithmetic). */
+typedef struct {
+  const float *const *in;
+  float *const *out;
+  int64_t nchan, nif, ntime, F, T;
+  int op, nbank;
+  int64_t piece, npiece;        /* outputs per piece, pieces per (bank, i, to) row */
+  int64_t next, total;          /* work counter (pieces over every bank and row) */
+  pthread_mutex_t mu;
+  int rc;
+} pool_t;
+static void *pool_run(void *arg) {
+  pool_t *P = (pool_t *)arg;
+  geo_t g;
+  resolve(P->nchan, P->nif, P->ntime, NULL, &g);
+  const int64_t nco = g.nc / P->F, nto = g.nt / P->T;
+  for (;;) {
+    pthread_mutex_lock(&P->mu);
+    const int64_t w = P->next++;
+    pthread_mutex_unlock(&P->mu);
+    if (w >= P->total) break;
+    const int64_t pc = w % P->npiece, row = w / P->npiece;
+    const int64_t b = row / (g.ni * nto), r2 = row % (g.ni * nto), i = r2 % g.ni, to = r2 / g.ni;
+    const int64_t co0 = pc * P->piece, co1 = co0 + P->piece < nco ? co0 + P->piece : nco;
+    reduce_range(P->in[b], &g, P->F, P->T, P->op, P->out[b], nco, i, to, co0, co1);
+  }
+  return NULL;
+}
+int oracle_reduce_banks_pool(int nbank, const float *const *in, int64_t nchan, int64_t nif,
+                             int64_t ntime, int64_t F, int64_t T, int op, float *const *out,
+                             int nthreads) {
+  if (nbank < 1 || nthreads < 1 || nthreads > 1024) return -1;
+  const int64_t Fx = F <= 1 ? 1 : F, Tx = T <= 1 ? 1 : T;
+  if (nchan % Fx || ntime % Tx) return -2;
+  pool_t P;
+  P.in = in; P.out = out; P.nchan = nchan; P.nif = nif; P.ntime = ntime; P.F = Fx; P.T = Tx;
+  P.op = op; P.nbank = nbank; P.rc = 0; P.next = 0;
+  const int64_t nco = nchan / Fx;
+  P.piece = nco / 64 > 1 ? nco / 64 : 1;  /* 64 pieces per row */
+  P.npiece = (nco + P.piece - 1) / P.piece;
+  P.total = P.npiece * nbank * nif * (ntime / Tx);
+  pthread_mutex_init(&P.mu, NULL);
+  pthread_t th[1024];
+  int started = 0;
+  for (int t = 0; t < nthreads; ++t)
+    if (pthread_create(&th[t], NULL, pool_run, &P) == 0) ++started;
+  for (int t = 0; t < started; ++t) pthread_join(th[t], NULL);
+  pthread_mutex_destroy(&P.mu);
+  return started ? 0 : -1;
+}
+
 typedef struct {
   const float *in;
   float *out;

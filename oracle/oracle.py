@@ -80,6 +80,8 @@ def lib():
         L.oracle_synth.restype = None
         L.oracle_reduce_banks_mt.argtypes = [I, P, I64, I64, I64, I64, I64, I, P]
         L.oracle_reduce_banks_mt.restype = I
+        L.oracle_reduce_banks_pool.argtypes = [I, P, I64, I64, I64, I64, I64, I, P, I]
+        L.oracle_reduce_banks_pool.restype = I
         _lib = L
     return _lib
 
@@ -214,6 +216,22 @@ def reduce_banks_mt(banks, fqavby, tavby, op="sum"):
     rc = lib().oracle_reduce_banks_mt(len(banks), ctypes.cast(ip, ctypes.c_void_p), nchan, nif,
                                       ntime, F, T, OPS[op], ctypes.cast(op_, ctypes.c_void_p))
     _check(rc, "oracle_reduce_banks_mt")
+    return outs
+
+
+def reduce_banks_pool(banks, fqavby, tavby, op="sum", nthreads=1):
+    """CPU baseline on every core: the banks' output channels split into
+    pieces over ``nthreads`` threads (same arithmetic as ``reduce``)."""
+    banks = [_fa(b) for b in banks]
+    nchan, nif, ntime = banks[0].shape
+    F, T = max(int(fqavby), 1), max(int(tavby), 1)
+    outs = [np.empty((nchan // F, nif, ntime // T), np.float32, order="F") for _ in banks]
+    ip = (ctypes.c_void_p * len(banks))(*[b.ctypes.data for b in banks])
+    op_ = (ctypes.c_void_p * len(banks))(*[o.ctypes.data for o in outs])
+    rc = lib().oracle_reduce_banks_pool(len(banks), ctypes.cast(ip, ctypes.c_void_p), nchan, nif,
+                                        ntime, F, T, OPS[op], ctypes.cast(op_, ctypes.c_void_p),
+                                        int(nthreads))
+    _check(rc, "oracle_reduce_banks_pool")
     return outs
 
 

@@ -587,3 +587,43 @@ def test_compressed_and_raw_files_random_windows(pkg, orc, tmp_path, seed):
         for f in (comp, plain, cont):
             got = pkg.WorkerFunctions.getdata(f, idxs, fqavby=F, fqavfunc=op, tavby=T)
             assert same_bits(got, want), (f, idxs, F, T, op, chunk)
+
+
+def test_cfg5_share_full_size_host_path(pkg, orc):
+    """One GPU's share of cfg5 (bank b of 4 bands x {0000, 0001, 0002}) at the
+    full per-array sizes (4 GiB, 1.8 GB, 73 MB) through bldp_reduce_host_f32
+    from pinned host memory, as bench.py --mode host streams it (SURVEY §8d
+    D2(5), the GBT.getdata fan-out src/gbt.jl:69-79): the 0002 arrays
+    (gamma power) against the oracle; the 0000/0001 arrays as integer data,
+    bit-exact against the device-resident reduce and checked by exact
+    totals and spot groups."""
+    import torch
+
+    eng = pkg.engine
+    prods = [  # name, nchan, ntime, window, F, T, nfpc, product
+        ("0000", 1 << 26, 16, 16, 1024, 16, 1 << 20, 0),
+        ("0001", 512, 880000, 879616, 8, 1024, 8, 1),
+        ("0002", 65536, 279, 272, 64, 16, 1024, 2)]
+    bank = 3
+    for name, nchan, ntime, tw, F, T, nfpc, pr in prods:
+        h = torch.empty((ntime, 1, nchan), dtype=torch.float32, pin_memory=True)
+        win = None if tw == ntime else [0, nchan, 1, 0, 1, 1, 0, tw, 1]
+        for band in range(4):
+            seed = 1000 * band + 10 * bank + pr
+            t = eng.synth(nchan, 1, ntime, nfpc, seed=seed, kind=0 if name == "0002" else 1)
+            h.copy_(t.permute(2, 1, 0))
+            a = h.numpy().transpose(2, 1, 0)  # Julia order, Fortran-contiguous, pinned
+            got = eng.reduce_host(a, F, T, "sum", win)
+            assert got.shape == (nchan // F, 1, tw // T)
+            if name == "0002":
+                np.testing.assert_allclose(got, orc.reduce(a, F, T, "sum", win), rtol=1e-5)
+                continue
+            ref = eng.fb_to_numpy(eng.reduce(t, F, T, "sum", win))
+            assert same_bits(got, ref), (name, band)
+            assert got.astype(np.float64).sum() == t[:, :, :tw].double().sum().item()
+            for g in (0, (nchan // F) // 2 + band, nchan // F - 1):
+                blk = a[g * F:(g + 1) * F, 0, :T].astype(np.float64).sum()
+                assert got[g, 0, 0] == blk, (name, band, g)
+            del t
+        del h
+        torch.cuda.empty_cache()

@@ -515,6 +515,25 @@ def test_band_reduce_multi_device_api(eng, orc, pkg):
     assert rc == pkg._lib.BLDP_EINVAL
 
 
+def test_band_reduce_multi_staged_branch(eng, orc, monkeypatch):
+    """BLDP_FORCE_STAGED=1 sends every bank of bldp_band_reduce_multi_f32
+    through the staged branch a bank off the root takes without peer access
+    (local reduce into a staging buffer, then one strided hipMemcpy2DAsync
+    into the bank's slot of the root's product): bit-exact against the
+    single-launch band reduce, for a one-row and a many-row product."""
+    monkeypatch.setenv("BLDP_FORCE_STAGED", "1")
+    rng = np.random.default_rng(88)
+    for shape, F, T, w in (((8192, 2, 48), 64, 16, [0, 8192, 1, 0, 2, 1, 0, 48, 1]),
+                           ((4096, 1, 64), 1024, 64, None),
+                           ((1000, 3, 20), 8, 5, [4, 992, 1, 0, 3, 1, 0, 20, 1])):
+        banks = [np.asfortranarray(rng.integers(0, 256, shape).astype(np.float32))
+                 for _ in range(5)]
+        xs = [dev(eng, b) for b in banks]
+        got = host(eng, eng.band_reduce_multi(xs, F, T, "sum", w))
+        assert same_bits(got, host(eng, eng.band_reduce(xs, F, T, "sum", w))), shape
+        assert same_bits(got, orc.stitch([orc.reduce(b, F, T, "sum", w) for b in banks]))
+
+
 def _random_case(rng):
     """A random window / factors / op over a small random array, biased so
     that every plan (row, vector, narrow, tile, scalar, time chunks) shows up

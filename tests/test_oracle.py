@@ -174,3 +174,8 @@ def test_baseline_threads_match_single(orc):
     outs = orc.reduce_banks_mt(banks, 16, 4)
     for b, o in zip(banks, outs):
         assert same_bits(o, orc.reduce(b, 16, 4))
+    for nth in (1, 3, 16):  # all-cores form: pieces of output channels over a pool
+        for F, T, op in ((16, 4, "sum"), (1, 8, "mean"), (256, 1, "max")):
+            outs = orc.reduce_banks_pool(banks, F, T, op, nth)
+            for b, o in zip(banks, outs):
+                assert same_bits(o, orc.reduce(b, F, T, op)), (nth, F, T, op)
