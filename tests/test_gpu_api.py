@@ -231,7 +231,9 @@ def test_bench_pipeline_flag():
                        capture_output=True, text=True, timeout=300, cwd=REPO)
     assert r.returncode == 0, r.stderr[-2000:]
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
-    assert d["n_gpus"] == 1 and d["value"] > 0 and "RCCL gather" in d["config"]["parallelism"]
+    c = d["config"]
+    assert d["n_gpus"] == 1 and d["value"] > 0 and "RCCL (nccl backend) gather" in c["parallelism"]
+    assert c["dist_backend"] == "nccl" and c["world_size"] == 1 and c["device_count"] >= 1
 
 
 def _bslz4_fixtures():

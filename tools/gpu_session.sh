@@ -48,6 +48,9 @@ for s in $STEPS; do
     benchnocpu) run benchnocpu 600 python bench.py --no-cpu-baseline ;;
     kurt_*) run "$s" 600 python bench.py --mode kurtosis --config "${s#kurt_}" ;;
     host)  run host 900 python bench.py --mode host ;;
+    host2) run host2 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+             --master-addr 127.0.0.1 --master-port 29614 bench.py --gpus 2 --dist-backend gloo \
+             --mode host ;;
     decode) run decode 600 python bench.py --mode decode ;;
     file)  run file 600 python bench.py --mode file ;;
     rawfile) run rawfile 600 python bench.py --mode rawfile ;;
