@@ -67,7 +67,7 @@ struct RedArgs {
 };
 
 enum Path { PATH_VEC = 0, PATH_NARROW = 1, PATH_SCALAR = 2, PATH_TILE = 3, PATH_VEC_IL = 4,
-            PATH_VEC_ROW = 5 };
+            PATH_VEC_ROW = 5, PATH_NARROW_MIS = 6 };
 
 struct Plan {
   int path;

@@ -83,6 +83,12 @@ __device__ __forceinline__ float fold4(float4 v) {
 #ifndef BLDP_NT_STORES
 #define BLDP_NT_STORES 1
 #endif
+//   BLDP_NARROW_MIS 1 (default) = misaligned F = 1 windows take the
+//                  realigning narrow kernel instead of the tile path; 2 = F = 2
+//                  too; 0 = neither
+#ifndef BLDP_NARROW_MIS
+#define BLDP_NARROW_MIS 1
+#endif
 __device__ __forceinline__ void st4(float *p, float4 r) {
   const f4v v = {r.x, r.y, r.z, r.w};
 #if BLDP_NT_STORES
@@ -289,6 +295,99 @@ __device__ __forceinline__ void narrow_tile(const RedArgs &a, int64_t tile) {
     } else {
       *reinterpret_cast<float2 *>(o) = make_float2(R<OP>::f(r.x, r.y), R<OP>::f(r.z, r.w));
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Narrow path for windows that start off a 16-byte boundary (unit channel
+// step, F = 1, e.g. idxs = (2:n, :, :) with time integration; F = 2 with
+// BLDP_NARROW_MIS=2).  Each wave owns 256 window channels = 64 output float4
+// (1 KiB of output, aligned like the output row).  Lane L streams the ALIGNED
+// input float4 column L (lane 63 also column 64) and sums its T rows in
+// registers exactly like narrow_tile; output float4 L is then elements
+// mis..3 of column L and 0..mis-1 of column L+1, taken from the next lane by
+// shuffle.  No LDS, no barrier; the input read is the window plus one float4
+// per wave.
+constexpr int kMisSpan = 4 * 256;  // window channels per workgroup (4 waves x 256)
+template <int OP, int F>
+__device__ __forceinline__ void narrow_mis_tile(const RedArgs &a, int64_t tile) {
+  const Coord c = decompose(a, tile);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t nwin = a.nco * F;  // window channels
+  const int64_t x0 = c.bc * kMisSpan + wave * 256;
+  if (x0 >= nwin) return;  // a wave past the window's end (no barrier follows)
+  const int64_t abs0 = a.in_off + c.i * a.in_ld_i + x0;
+  const int mis = (int)(abs0 & 3);  // bank pointers and row pitches are 16-byte aligned
+  const int cnt = (int)min<int64_t>(256, nwin - x0);
+  const int ncol = (mis + cnt + 3) >> 2;  // <= 65
+  const bool extra = lane == 63 && ncol > 64;
+  const int64_t r0 = c.chunk * a.rows_per_chunk;
+  const int64_t r1 = min(a.T, r0 + a.rows_per_chunk);
+  const float id = R<OP>::id();
+  float4 acc[kNacc], ax = make_float4(id, id, id, id);
+#pragma unroll
+  for (int q = 0; q < kNacc; ++q) acc[q] = ax;
+  if (lane < ncol) {
+    const float *p = a.in[c.bank] + (abs0 - mis) + (c.to * a.T + r0) * a.in_ld_t + 4 * lane;
+    const int64_t st = a.in_ld_t;
+    int64_t nrows = r1 - r0;
+    for (; nrows >= BLDP_BATCH; nrows -= BLDP_BATCH) {
+      float4 v[BLDP_BATCH], w[BLDP_BATCH];
+#pragma unroll
+      for (int u = 0; u < BLDP_BATCH; ++u) v[u] = ld4(p + u * st);
+      if (extra) {
+#pragma unroll
+        for (int u = 0; u < BLDP_BATCH; ++u) w[u] = ld4(p + 4 + u * st);
+#pragma unroll
+        for (int u = 0; u < BLDP_BATCH; ++u) ax = f4<OP>(ax, w[u]);
+      }
+      p += BLDP_BATCH * st;
+#pragma unroll
+      for (int u = 0; u < BLDP_BATCH; ++u) acc[u % kNacc] = f4<OP>(acc[u % kNacc], v[u]);
+    }
+    for (; nrows > 0; --nrows) {
+      acc[0] = f4<OP>(acc[0], ld4(p));
+      if (extra) ax = f4<OP>(ax, ld4(p + 4));
+      p += st;
+    }
+  }
+  const float4 lo = fold_acc<OP>(acc);
+  float4 hi = make_float4(__shfl_down(lo.x, 1, 64), __shfl_down(lo.y, 1, 64),
+                          __shfl_down(lo.z, 1, 64), __shfl_down(lo.w, 1, 64));
+  if (lane == 63) hi = ax;
+  const int nv = min(4, cnt - 4 * lane);  // window channels of this lane's output float4
+  if (nv <= 0) return;
+  float4 r;
+  switch (mis) {
+    case 1: r = make_float4(lo.y, lo.z, lo.w, hi.x); break;
+    case 2: r = make_float4(lo.z, lo.w, hi.x, hi.y); break;
+    case 3: r = make_float4(lo.w, hi.x, hi.y, hi.z); break;
+    default: r = lo;
+  }
+  const int64_t co = (x0 + 4 * lane) / F;  // first output of this lane (x0 is even)
+  float o[4] = {r.x, r.y, r.z, r.w};
+  int no = nv;
+  if (F == 2) {
+    o[0] = R<OP>::f(r.x, r.y);
+    o[1] = R<OP>::f(r.z, r.w);
+    no = nv / 2;
+  }
+  float *dst;
+  if (a.nchunk == 1) {
+    dst = a.out + c.bank * a.out_bank + c.i * a.out_ld_i + c.to * a.out_ld_t + co;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = finish<OP>(o[q], a);
+  } else {
+    dst = a.ws + (((c.chunk * a.nbank + c.bank) * a.nto + c.to) * a.ni + c.i) * a.nco + co;
+  }
+  if (F == 1 && no == 4 && a.nchunk == 1 && a.vec_out) {
+    st4(dst, make_float4(o[0], o[1], o[2], o[3]));
+  } else if (F == 2 && no == 2 && (a.nchunk > 1 || a.vec_out)) {  // (ws: dense, even co)
+    *reinterpret_cast<float2 *>(dst) = make_float2(o[0], o[1]);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (q < no) dst[q] = o[q];
   }
 }
 
@@ -633,6 +732,10 @@ template <int OP, int F>
 __global__ __launch_bounds__(kBlock) void k_reduce_narrow(const RedArgs a) {
   for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) narrow_tile<OP, F>(a, t);
 }
+template <int OP, int F>
+__global__ __launch_bounds__(kBlock) void k_reduce_narrow_mis(const RedArgs a) {
+  for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) narrow_mis_tile<OP, F>(a, t);
+}
 template <int OP>
 __global__ __launch_bounds__(kBlock) void k_reduce_scalar(const RedArgs a) {
   for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) scalar_tile<OP>(a, t);
@@ -830,6 +933,12 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
     else
       hipLaunchKernelGGL((k_reduce_narrow<OP, 2>), grid, block, 0, s, a);
     e = hipGetLastError();
+  } else if (p.path == PATH_NARROW_MIS) {
+    if (a.F == 1)
+      hipLaunchKernelGGL((k_reduce_narrow_mis<OP, 1>), grid, block, 0, s, a);
+    else
+      hipLaunchKernelGGL((k_reduce_narrow_mis<OP, 2>), grid, block, 0, s, a);
+    e = hipGetLastError();
   } else if (p.path == PATH_TILE) {
     if (a.in_cs == 1)
       hipLaunchKernelGGL((k_reduce_tile<OP, true>), grid, block, 0, s, a);
@@ -885,6 +994,12 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, int num_cus) {
     const int64_t nc4 = a.nco * F / 4;
     a.blocks_c = cdiv(nc4, kBlock);
     tiles = cdiv(nc4, 64) * a.ni * a.nto * a.nbank;
+  } else if (rows16 && a.in_cs == 1 && ((BLDP_NARROW_MIS >= 1 && F == 1) ||
+                                         (BLDP_NARROW_MIS >= 2 && F == 2))) {
+    // misaligned start, time integration (+ pairs): aligned columns realigned in LDS
+    p.path = PATH_NARROW_MIS;
+    a.blocks_c = cdiv(a.nco * F, kMisSpan);
+    tiles = a.blocks_c * 4 * a.ni * a.nto * a.nbank;
   } else if (rows16 && a.in_cs >= 1 && a.in_cs <= 8 && F <= (kSpan - 4) / a.in_cs + 1) {
     p.path = PATH_TILE;
     a.gpt = ((kSpan - 4) / a.in_cs + 1) / F;
@@ -933,6 +1048,12 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, int num_cus) {
   }
   // narrow-path vector stores
   a.vec_out = 0;
+  if (p.path == PATH_NARROW_MIS) {  // float4 (F = 1) / float2 (F = 2) stores at aligned co
+    const int64_t w = 4 / F;            // outputs per lane
+    const uintptr_t op = (uintptr_t)a.out;
+    a.vec_out = (op % (4 * w) == 0) && a.out_bank % w == 0 && a.out_ld_i % w == 0 &&
+                a.out_ld_t % w == 0;
+  }
   if (p.path == PATH_NARROW) {
     const int64_t w = 4 / F;  // outputs per lane
     const uintptr_t op = (uintptr_t)a.out;

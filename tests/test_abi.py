@@ -120,7 +120,10 @@ def test_launch_plans_host_only(pkg, L):
     # tile path: odd F, misaligned channel start, short channel step
     assert plan(pkg, L, A, 4096, 1, 16, 3, 1, [0, 4095, 1, 0, 1, 1, 0, 16, 1])[0] == 3
     assert plan(pkg, L, A, 4096, 1, 16, 64, 16, [1, 4032, 1, 0, 1, 1, 0, 16, 1])[0] == 3
-    assert plan(pkg, L, A, 4096, 1, 16, 1, 1, [1, 4092, 1, 0, 1, 1, 0, 16, 1])[0] == 3
+    # misaligned start with F = 1: the realigning narrow kernel
+    assert plan(pkg, L, A, 4096, 1, 16, 1, 1, [1, 4092, 1, 0, 1, 1, 0, 16, 1])[0] == 6
+    assert plan(pkg, L, A, 4096, 1, 16, 2, 4, [3, 4092, 1, 0, 1, 1, 0, 16, 1])[0] == 3  # F=2: tile
+    assert plan(pkg, L, A, 4096, 1, 16, 1, 1, [0, 2048, 2, 0, 1, 1, 0, 16, 1])[0] == 3
     assert plan(pkg, L, A, 4096, 1, 16, 16, 1, [0, 2048, 2, 0, 1, 1, 0, 16, 1])[0] == 3
     # ... but not a reversed step, a step > 8, or a group wider than a tile row
     assert plan(pkg, L, A, 4096, 1, 16, 16, 1, [4095, 2048, -2, 0, 1, 1, 0, 16, 1])[0] == 2

@@ -248,7 +248,9 @@ def test_tile_path(eng, orc, case):
     rng = np.random.default_rng(nc + F)
     a = np.asfortranarray(rng.integers(0, 256, (nc, ni, nt)).astype(np.float32))
     x = dev(eng, a)
-    assert eng.plan(x, F, T, "sum", win)["path"] == "tile"
+    # (misaligned unit-step windows with F in {1, 2} take the realigning narrow kernel)
+    expect = "narrow_mis" if F == 1 and win[2] == 1 else "tile"
+    assert eng.plan(x, F, T, "sum", win)["path"] == expect
     for op in ("sum", "max", "min", "mean"):
         got = host(eng, eng.reduce(x, F, T, op, win))
         want = orc.reduce(a, F, T, op, win)
@@ -268,7 +270,7 @@ def test_tile_path_special_values(eng, orc):
     x = dev(eng, a)
     for F, T in [(4, 1), (2, 2), (1, 4), (3, 4), (20, 1)]:
         win = [1, 60, 1, 0, 1, 1, 0, 4, 1]
-        assert eng.plan(x, F, T, "max", win)["path"] == "tile"
+        assert eng.plan(x, F, T, "max", win)["path"] == ("narrow_mis" if F == 1 else "tile")
         for op in ("sum", "max", "min"):
             got = host(eng, eng.reduce(x, F, T, op, win))
             want = orc.reduce(a, F, T, op, win)
@@ -735,3 +737,38 @@ def test_kurtosis_long_windows_leaf_merge(eng, orc, nt):
     ks = eng.band_kurtosis([xd, dev(eng, r)])
     kurt_ok(eng, xd, None, host(eng, ks[0]), want)
     kurt_ok(eng, xd, None, host(eng, ks[1]), orc.kurtosis(r))
+
+
+@pytest.mark.parametrize("c0", [1, 2, 3, 5])
+@pytest.mark.parametrize("F", [1])
+def test_narrow_misaligned_windows(eng, orc, c0, F):
+    """Windows starting off a 16-byte boundary with F = 1 (time integration
+    of a zoom window, e.g. idxs = (2:n, :, :)) take the realigning narrow
+    kernel: aligned float4 columns summed over T, realigned by lane shuffle.  Integer data, bit-exact for every op, two IFs, a ragged last tile,
+    stitched band slots, and a long time block split into chunks."""
+    rng = np.random.default_rng(10 * c0 + F)
+    a = np.asfortranarray(rng.integers(0, 256, (4100, 2, 48)).astype(np.float32))
+    nc = (4100 - c0) - (4100 - c0) % 2
+    x = dev(eng, a)
+    for T, tw in ((8, 48), (48, 48), (3, 12)):
+        w = [c0, nc, 1, 0, 2, 1, 0, tw, 1]
+        assert eng.plan(x, F, T, "sum", w)["path"] == "narrow_mis"
+        for op in ("sum", "mean", "max", "min"):
+            got = host(eng, eng.reduce(x, F, T, op, w))
+            want = orc.reduce(a, F, T, op, w)
+            if op == "mean":
+                np.testing.assert_allclose(got, want, rtol=RTOL)
+            else:
+                assert same_bits(got, want), (T, op)
+    banks = [a] + [np.asfortranarray(rng.integers(0, 256, a.shape).astype(np.float32))
+                   for _ in range(2)]
+    w = [c0, nc, 1, 1, 1, 1, 4, 40, 1]
+    got = host(eng, eng.band_reduce([dev(eng, b) for b in banks], F, 8, "sum", w))
+    assert same_bits(got, orc.stitch([orc.reduce(b, F, 8, "sum", w) for b in banks]))
+    # few tiles, long time block: partials over time chunks + the finalize
+    b = np.asfortranarray(rng.integers(0, 256, (72, 1, 20000)).astype(np.float32))
+    y = dev(eng, b)
+    w = [c0, 64, 1, 0, 1, 1, 0, 20000, 1]
+    p = eng.plan(y, F, 20000, "sum", w)
+    assert p["path"] == "narrow_mis" and p["time_chunks"] > 1
+    assert same_bits(host(eng, eng.reduce(y, F, 20000, "sum", w)), orc.reduce(b, F, 20000, "sum", w))

@@ -41,6 +41,8 @@ VARIANTS = {
     "rowb8": "-DBLDP_ROW_BATCH=8",
     "norow": "-DBLDP_VEC_ROW=0",
     "tilenocap": "-DBLDP_TILE_MAXWAVES=0",
+    "nomis": "-DBLDP_NARROW_MIS=0",  # misaligned F = 1, 2 windows on the tile path
+    "misf2": "-DBLDP_NARROW_MIS=2",  # F = 2 on the realigning narrow kernel too
     "kpnocap": "-DBLDP_KURT_PASS_MAXWAVES=0",
     "rownocap": "-DBLDP_ROW_MAXWAVES=0",
     # narrow windows: time split over otherwise idle waves, with / without grid cap
@@ -144,6 +146,8 @@ def run(names, rounds, iters, suite="main"):
         band_case("cfg3 c0=3 F64", b3, 64, 16, [3, n - 64, 1, 0, 1, 1, 0, 16, 1])
         band_case("cfg3 F3", b3, 3, 16, [0, n - 1, 1, 0, 1, 1, 0, 16, 1])
         band_case("cfg3 c0=1 F1", b3, 1, 16, [1, n - 4, 1, 0, 1, 1, 0, 16, 1])
+        band_case("cfg3 aligned F1", b3, 1, 16)
+        band_case("cfg3 c0=2 F2", b3, 2, 16, [2, n - 4, 1, 0, 1, 1, 0, 16, 1])
         band_case("cfg3 cs=2 F32", b3, 32, 16, [0, n // 2, 2, 0, 1, 1, 0, 16, 1])
         b2 = [eng.synth(65540, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
         band_case("cfg2 c0=1 F64", b2, 64, 16, [1, 65536, 1, 0, 1, 1, 0, 272, 1])

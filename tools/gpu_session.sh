@@ -56,6 +56,12 @@ for s in $STEPS; do
     rawfile) run rawfile 600 python bench.py --mode rawfile ;;
     paths) run paths 300 python tools/probe_paths.py ;;
     paths_big) run paths_big 300 python tools/probe_paths.py --big ;;
+    prof_paths) run prof_paths 300 rocprofv3 --kernel-trace --stats --output-format csv \
+             -d "$OUT/prof_paths" -o run -- python tools/probe_paths.py --big
+           run pmc_fetch_paths 300 rocprofv3 --pmc FETCH_SIZE --output-format csv \
+             -d "$OUT/pmc_fetch_paths" -o run -- python tools/probe_paths.py --big
+           run pmc_write_paths 300 rocprofv3 --pmc WRITE_SIZE --output-format csv \
+             -d "$OUT/pmc_write_paths" -o run -- python tools/probe_paths.py --big ;;
     prof_decode) run prof_decode 600 rocprofv3 --kernel-trace --stats --output-format csv \
              -d "$OUT/prof_decode" -o run -- python bench.py --mode decode ;;
     prof_kurt) run prof_kurt 600 rocprofv3 --kernel-trace --stats --output-format csv \
