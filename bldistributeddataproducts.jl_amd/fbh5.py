@@ -446,6 +446,41 @@ def bslz4_decode_dev(chunks, dtype=np.float32, device=None, stream=None, out=Non
 H5D_CHUNKED = 2
 
 
+_META_MAX = 256
+_meta_cache: dict = {}
+_meta_lock = __import__("threading").Lock()
+
+
+def _file_key(fname):
+    """Identity of a file's current contents: a rewritten file (new inode,
+    size or change time) gets new metadata."""
+    st = os.stat(fname)
+    return (os.path.realpath(fname), st.st_dev, st.st_ino, st.st_size, st.st_mtime_ns,
+            st.st_ctime_ns)
+
+
+def _cached(fn):
+    """Per-file memo of a metadata function (layout, chunk index, ...): a
+    worker reads the same files over and over; the libhdf5 open and the
+    B-tree walk are paid once per file version, not per getdata."""
+    import functools
+
+    @functools.wraps(fn)
+    def wrap(fname):
+        key = (fn.__name__,) + _file_key(fname)
+        with _meta_lock:
+            if key in _meta_cache:
+                return _meta_cache[key]
+        val = fn(fname)
+        with _meta_lock:
+            if len(_meta_cache) >= _META_MAX:
+                _meta_cache.pop(next(iter(_meta_cache)))
+            _meta_cache[key] = val
+        return val
+    return wrap
+
+
+@_cached
 def layout(fname) -> dict:
     """Dataset dims (C order), chunk dims and filter pipeline of ``data``."""
     H5 = h5()
@@ -490,6 +525,7 @@ H5T_ORDER_LE = 0
 HADDR_UNDEF = (1 << 64) - 1
 
 
+@_cached
 def raw_layout(fname):
     """(file offset, Julia shape) when ``data`` is stored as one contiguous
     block of little-endian float32 with no filter -- what
@@ -526,6 +562,7 @@ def raw_layout(fname):
         H.H5Fclose(f)
 
 
+@_cached
 def raw_chunked(fname) -> bool:
     """True when ``data`` is a chunked dataset with no filter, stored as
     little-endian float32: its chunks are the elements, read like the
@@ -551,6 +588,7 @@ def raw_chunked(fname) -> bool:
         H.H5Fclose(f)
 
 
+@_cached
 def needs_bslz4(fname) -> bool:
     """True when ``data`` is bitshuffle/LZ4-compressed and libhdf5 has no
     plugin for filter 32008 (the case of this image)."""
@@ -563,6 +601,40 @@ def needs_bslz4(fname) -> bool:
     if ids != [BSHUF_FILTER_ID]:
         raise BLDPError(-1, f"{fname}: filter pipeline {ids} not supported (only 32008 alone)")
     return True
+
+
+@_cached
+def chunk_index(fname):
+    """The chunk index of ``data`` as dense C-order grids over the chunk grid
+    [gt][gi][gc]: file offset, stored bytes (0: never written, fill value) and
+    filter mask of every chunk, parsed straight from the file (h5chunks.py),
+    or None outside that parser's scope."""
+    from . import h5chunks
+
+    lay = layout(fname)
+    cdims, chunk = lay["cdims"], lay["chunk"]
+    if chunk is None or len(cdims) != 3:
+        return None
+    H = h5().L
+    f = _ok(H.H5Fopen(os.fsencode(fname), H5F_ACC_RDONLY, H5P_DEFAULT), f"open {fname}")
+    try:
+        d = _ok(H.H5Dopen2(f, b"data", H5P_DEFAULT), "open dataset 'data'")
+        try:
+            tab = h5chunks.chunk_table(fname, H, d)
+        finally:
+            H.H5Dclose(d)
+    finally:
+        H.H5Fclose(f)
+    if tab is None:
+        return None
+    grid = tuple(-(-int(n) // int(c)) for n, c in zip(cdims, chunk))
+    addr = np.zeros(grid, np.int64)
+    size = np.zeros(grid, np.int64)
+    mask = np.zeros(grid, np.int64)
+    for key, (a, n, m) in tab["index"].items():
+        g = tuple(int(k) // int(c) for k, c in zip(key, chunk))
+        addr[g], size[g], mask[g] = a, n, m
+    return dict(addr=addr, size=size, mask=mask, grid=grid)
 
 
 def _box(win_axis, cdim):
@@ -688,26 +760,90 @@ def _chunk_sizes(H, d, chunk, kt0, ki0, kc0, grid):
     return offs, sizes
 
 
+_copy_streams: dict = {}
+
+
+def _copy_stream(dev, priority, j=0):
+    """Cached H2D streams per (device, priority)."""
+    import torch
+
+    key = (dev.index if dev.index is not None else torch.cuda.current_device(), priority, j)
+    s = _copy_streams.get(key)
+    if s is None:
+        s = _copy_streams[key] = torch.cuda.Stream(torch.device("cuda", key[0]), priority=priority)
+    return s
+
+
+def _batches_of(sizes, first_bytes, batch_bytes):
+    """Split chunk indices 0..n-1 into contiguous ranges [k0, k1) of about
+    ``batch_bytes`` stored bytes (the first about ``first_bytes``, so the
+    first H2D copy starts early)."""
+    n = len(sizes)
+    if n == 0:
+        return []
+    cum = np.cumsum(sizes)
+    out, k0, target = [], 0, first_bytes
+    base = 0
+    while k0 < n:
+        k1 = int(np.searchsorted(cum, base + target, side="left")) + 1
+        k1 = min(max(k1, k0 + 1), n)
+        out.append((k0, k1))
+        base = int(cum[k1 - 1])
+        k0, target = k1, batch_bytes
+    return out
+
+
+def _read_tasks(faddr, sizes, offsets, k0, k1, piece):
+    """Preads of chunks [k0, k1): chunks adjacent in the file and in the
+    buffer merge into runs, runs are cut into pieces of <= ``piece`` bytes and
+    grouped into tasks of about ``piece`` bytes (one pool task each: per-chunk
+    tasks are GIL-bound).  Vectorised: a batch holds hundreds of chunks."""
+    fa, sz, of = faddr[k0:k1], sizes[k0:k1], offsets[k0:k1]
+    keep = sz > 0
+    fa, sz, of = fa[keep], sz[keep], of[keep]
+    if not len(sz):
+        return []
+    brk = np.ones(len(sz), bool)
+    brk[1:] = (fa[1:] != fa[:-1] + sz[:-1]) | (of[1:] != of[:-1] + sz[:-1])
+    starts = np.flatnonzero(brk)
+    ends = np.append(starts[1:], len(sz))
+    run_len = np.add.reduceat(sz, starts)
+    tasks, cur, cur_n = [], [], 0
+    for s, n in zip(starts.tolist(), run_len.tolist()):
+        fo, do = int(fa[s]), int(of[s])
+        for q in range(0, n, piece):
+            m = min(piece, n - q)
+            cur.append((fo + q, do + q, m))
+            cur_n += m
+            if cur_n >= piece:
+                tasks.append(cur)
+                cur, cur_n = [], 0
+    if cur:
+        tasks.append(cur)
+    del ends
+    return tasks
+
+
 def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 20,
-                           raw_chunks=False):
+                           raw_chunks=False, first_batch_bytes=16 << 20):
     """Device path of a compressed window, overlapped in three stages: a
     reader thread reads batches of stored chunks straight into pinned memory
     and queues their H2D copy on a copy stream, while this thread decodes the
-    previous batch on the GPU (bldp_bslz4_decode_dev); then the window is
-    gathered (bldp_unchunk_f32).  Only compressed bytes cross PCIe.  The
+    previous batch on the GPU (bldp_bslz4_decode_dev_async); then the window
+    is gathered (bldp_unchunk_f32).  Only compressed bytes cross PCIe.  The
     chunks are read by parallel preads at the offsets of the chunk index
-    parsed from the file (h5chunks.py), or, outside that parser's scope, one
-    H5Dread_chunk at a time.  ``raw_chunks``: the dataset has no filter, every
-    stored chunk is raw float32 (no decode; when every chunk is stored, the
-    device copy of the chunks is the packed chunk grid itself).  ``timings``
-    (a dict) receives stage times."""
+    parsed from the file once per file version (``chunk_index``), or,
+    outside that parser's scope, one H5Dread_chunk at a time.
+    ``raw_chunks``: the dataset has no filter, every stored chunk is raw
+    float32 (no decode; when every chunk is stored, the device copy of the
+    chunks is the packed chunk grid itself).  ``timings`` (a dict) receives
+    stage times."""
     import time
 
     import torch
 
-    from . import _lib, engine
+    from . import _lib, engine, filestream
 
-    H = h5().L
     dev = torch.device(device)
     t0 = time.perf_counter()
     lay = layout(fname)
@@ -730,152 +866,147 @@ def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 
     box0 = (kt0 * chunk[0], ki0 * chunk[1], kc0 * chunk[2])
     cvol = int(np.prod(chunk))
     nc, ni, nt = win[1], win[4], win[7]
-    f = _ok(H.H5Fopen(os.fsencode(fname), H5F_ACC_RDONLY, H5P_DEFAULT), f"open {fname}")
-    try:
+    t_tab = time.perf_counter()
+    tab = chunk_index(fname)  # dense index grids, cached per file version, or None
+    H = d = f = None
+    if tab is not None:
+        sl = (slice(kt0, kt0 + gt), slice(ki0, ki0 + gi), slice(kc0, kc0 + gc))
+        faddr = tab["addr"][sl].ravel()
+        sizes = tab["size"][sl].ravel()
+        masks = tab["mask"][sl].ravel().copy()
+        coords = None
+    else:  # libhdf5 one chunk at a time
+        H = h5().L
+        f = _ok(H.H5Fopen(os.fsencode(fname), H5F_ACC_RDONLY, H5P_DEFAULT), f"open {fname}")
         d = _ok(H.H5Dopen2(f, b"data", H5P_DEFAULT), "open dataset 'data'")
-        try:
-            from . import h5chunks
+        coords, szl = _chunk_sizes(H, d, chunk, kt0, ki0, kc0, grid)
+        sizes = np.array(szl, np.int64)
+        faddr = np.zeros(len(sizes), np.int64)
+        masks = np.zeros(len(sizes), np.int64)
+    t_tab = time.perf_counter() - t_tab
+    try:
+        offsets = np.zeros(len(sizes), np.int64)
+        if len(sizes) > 1:
+            offsets[1:] = np.cumsum(sizes[:-1])
+        total = int(sizes.sum())
+        t_pin = time.perf_counter()
+        pinned = torch.empty(total + 16, dtype=torch.uint8, pin_memory=True)
+        host = pinned.numpy()
+        t_pin = time.perf_counter() - t_pin
+        batches = _batches_of(sizes, first_batch_bytes, batch_bytes)
+        with torch.cuda.device(dev):
+            cdev = torch.empty(total + 16, dtype=torch.uint8, device=dev)
+            dense_raw = raw_chunks and bool(np.all(sizes == 4 * cvol))
+            packed = cdev[:total].view(torch.float32) if dense_raw else \
+                torch.zeros(len(sizes) * cvol, dtype=torch.float32, device=dev)
+            # the H2D copies (the critical path) on a cached high-priority stream
+            copy_streams = [_copy_stream(dev, -1)]
+            hostmv = memoryview(host)
+            fd = os.open(fname, os.O_RDONLY) if tab is not None else None
+            pool = filestream._ring(dev).pool
 
-            tab = h5chunks.chunk_table(fname, H, d)  # parsed chunk B-tree, or None
-            if tab is not None:
-                coords, sizes, faddr, masks = [], [], [], []
-                for a in range(gt):
-                    for b in range(gi):
-                        for c in range(gc):
-                            key = ((kt0 + a) * chunk[0], (ki0 + b) * chunk[1],
-                                   (kc0 + c) * chunk[2])
-                            ent = tab["index"].get(key, (0, 0, 0))  # absent: fill (0)
-                            coords.append(key)
-                            faddr.append(ent[0])
-                            sizes.append(ent[1])
-                            masks.append(ent[2])
-            else:
-                coords, sizes = _chunk_sizes(H, d, chunk, kt0, ki0, kc0, grid)
-                masks = [0] * len(sizes)
-            offsets = [0] + [int(x) for x in np.cumsum(sizes[:-1])]
-            total = int(sum(sizes))
-            pinned = torch.empty(total + 16, dtype=torch.uint8, pin_memory=True)
-            host = pinned.numpy()
-            batches, cur, acc = [], [], 0
-            for k, nb in enumerate(sizes):
-                cur.append(k)
-                acc += nb
-                if acc >= batch_bytes:
-                    batches.append(cur)
-                    cur, acc = [], 0
-            if cur:
-                batches.append(cur)
-            with torch.cuda.device(dev):
-                cdev = torch.empty(total + 16, dtype=torch.uint8, device=dev)
-                dense_raw = raw_chunks and all(n == 4 * cvol for n in sizes)
-                packed = cdev[:total].view(torch.float32) if dense_raw else \
-                    torch.zeros(len(sizes) * cvol, dtype=torch.float32, device=dev)
-                copy_stream = torch.cuda.Stream(dev)
+            def read_task(task):
+                for fo, do, n in task:
+                    filestream._pread_into(fd, hostmv[do:do + n], fo)
 
-                hostmv = memoryview(host)
-                if tab is not None:
-                    from . import filestream
+            # BLDP_TRACE_READ=1: GPU-event timeline of the copies (timings["trace"])
+            trace = [] if timings is not None and os.environ.get("BLDP_TRACE_READ") else None
+            # every batch's preads go to the pool at once, in batch order, so the
+            # pool never idles between batches; the reader thread below only
+            # waits for a batch's reads and queues its H2D copy
+            pending = [[pool.submit(read_task, t) for t in
+                        _read_tasks(faddr, sizes, offsets, k0, k1, filestream.PIECE_BYTES)]
+                       for k0, k1 in batches] if tab is not None else None
 
-                    pool = filestream._ring(dev).pool
-                    fd = os.open(fname, os.O_RDONLY)
+            def stage(b):  # reader thread: (reads landed) -> (async) device
+                k0, k1 = batches[b]
+                if tab is not None:  # parallel preads at the parsed chunk offsets
+                    for fu in pending[b]:
+                        fu.result()
+                else:
+                    m = ctypes.c_uint32()
+                    for k in range(k0, k1):
+                        if sizes[k]:
+                            _ok(H.H5Dread_chunk(d, H5P_DEFAULT, _hs(coords[k]), ctypes.byref(m),
+                                                ctypes.c_void_p(pinned.data_ptr() +
+                                                                int(offsets[k]))), "read_chunk")
+                            masks[k] = m.value
+                lo, hi = int(offsets[k0]), int(offsets[k1 - 1] + sizes[k1 - 1])
+                copy_stream = copy_streams[b % len(copy_streams)]
+                with torch.cuda.device(dev):
+                    ev = torch.cuda.Event(enable_timing=trace is not None)
+                    with torch.cuda.stream(copy_stream):
+                        if trace is not None:
+                            e0 = torch.cuda.Event(enable_timing=True)
+                            e0.record(copy_stream)
+                            trace.append(("copy", b, time.perf_counter() - t0, e0, ev, hi - lo))
+                        if hi > lo:
+                            cdev[lo:hi].copy_(pinned[lo:hi], non_blocking=True)
+                        ev.record(copy_stream)
+                return ev
 
-                def stage(ks):  # reader thread: file -> pinned -> (async) device
-                    if tab is not None:  # parallel preads at the parsed chunk offsets
-                        # chunks adjacent in the file and in the batch merge into
-                        # runs; runs split into pieces of <= PIECE_BYTES (one
-                        # pool task each: per-chunk tasks are GIL-bound)
-                        runs = []
-                        for k in ks:
-                            if not sizes[k]:
-                                continue
-                            if runs and runs[-1][0] + runs[-1][2] == faddr[k] and \
-                                    runs[-1][1] + runs[-1][2] == offsets[k]:
-                                runs[-1][2] += sizes[k]
-                            else:
-                                runs.append([faddr[k], offsets[k], sizes[k]])
-                        tasks, cur, cur_n = [], [], 0  # preads grouped ~PIECE_BYTES a task
-                        for fo, do, n in runs:
-                            for q in range(0, n, filestream.PIECE_BYTES):
-                                m = min(filestream.PIECE_BYTES, n - q)
-                                cur.append((fo + q, do + q, m))
-                                cur_n += m
-                                if cur_n >= filestream.PIECE_BYTES:
-                                    tasks.append(cur)
-                                    cur, cur_n = [], 0
-                        if cur:
-                            tasks.append(cur)
-
-                        def read_task(task):
-                            for fo, do, n in task:
-                                filestream._pread_into(fd, hostmv[do:do + n], fo)
-                        futs = [pool.submit(read_task, t) for t in tasks]
-                        for fu in futs:
-                            fu.result()
-                    else:  # libhdf5, one chunk at a time
-                        m = ctypes.c_uint32()
-                        for k in ks:
-                            if sizes[k]:
-                                _ok(H.H5Dread_chunk(d, H5P_DEFAULT, _hs(coords[k]),
-                                                    ctypes.byref(m),
-                                                    ctypes.c_void_p(pinned.data_ptr() +
-                                                                    offsets[k])),
-                                    "read_chunk")
-                                masks[k] = m.value
-                    lo, hi = offsets[ks[0]], offsets[ks[-1]] + sizes[ks[-1]]
-                    with torch.cuda.device(dev):
-                        ev = torch.cuda.Event()
-                        with torch.cuda.stream(copy_stream):
-                            if hi > lo:
-                                cdev[lo:hi].copy_(pinned[lo:hi], non_blocking=True)
-                            ev.record(copy_stream)
-                    return ev
-
-                t_io = t_dec = 0.0
-                try:
-                    if raw_chunks:  # no filter: stored chunks are raw elements
-                        masks = [1] * len(sizes)
-                    t_dec, t_io = _decode_batches(
-                        batches, stage, sizes, masks, offsets, cvol,
-                        None if dense_raw else packed, cdev, host, _lib, torch)
-                finally:
-                    if tab is not None:
-                        os.close(fd)
-        finally:
-            H.H5Dclose(d)
+            t_io = t_dec = 0.0
+            try:
+                if raw_chunks:  # no filter: stored chunks are raw elements
+                    masks[:] = 1
+                t_dec, t_io = _decode_batches(
+                    batches, stage, sizes, masks, offsets, cvol,
+                    None if dense_raw else packed, cdev, host, _lib, torch)
+            finally:
+                if pending is not None:  # (an error above: let the reads finish first)
+                    for fl in pending:
+                        for fu in fl:
+                            fu.cancel() or fu.exception()
+                if fd is not None:
+                    os.close(fd)
     finally:
-        H.H5Fclose(f)
+        if d is not None:
+            H.H5Dclose(d)
+        if f is not None:
+            H.H5Fclose(f)
+    if timings is not None:
+        timings.update(chunk_index_s=t_tab, pinned_alloc_s=t_pin,
+                       before_unchunk_s=time.perf_counter() - t0)
+        if trace:
+            torch.cuda.synchronize(dev)
+            first = trace[0][3]
+            timings["trace"] = [(b, round(1e3 * tq, 3), round(first.elapsed_time(e0), 3),
+                                 round(first.elapsed_time(e1), 3), nb)
+                                for _, b, tq, e0, e1, nb in trace]
     return _unchunk_out(dev, torch, engine, _lib, nc, ni, nt, chunk, box0, grid, win, packed,
                         timings, t0, t_io, t_dec, batches, total, tab is not None)
 
 
 def _decode_batches(batches, stage, sizes, masks, offsets, cvol, packed, cdev, host, _lib,
                     torch):
-    """A reader thread runs ``stage`` over the batches ahead of this thread,
-    which queues each batch's GPU decode as soon as its copy has landed
-    (asynchronously; the decoder's error bits are checked once at the end).
-    Returns (decode seconds, seconds waited for reads)."""
+    """A reader thread runs ``stage`` over the batches (chunk ranges) ahead of
+    this thread, which queues each batch's GPU decode as soon as its copy has
+    landed (asynchronously; the decoder's error bits are checked once at the
+    end).  Returns (decode seconds, seconds waited for reads)."""
     import time
     from concurrent.futures import ThreadPoolExecutor
 
     t_io = t_dec = 0.0
     err = torch.zeros(1, dtype=torch.int32, device=cdev.device)  # decoder error bits
     with ThreadPoolExecutor(max_workers=1) as reader:
-        futs = [reader.submit(stage, ks) for ks in batches]  # reads run ahead
+        futs = [reader.submit(stage, b) for b in range(len(batches))]  # reads run ahead
         cur_stream = torch.cuda.current_stream()
-        for b, ks in enumerate(batches):
+        for b, (k0, k1) in enumerate(batches):
             tw = time.perf_counter()
             cur_stream.wait_event(futs[b].result())
             t_io += time.perf_counter() - tw
             td = time.perf_counter()
-            for k in ks:  # stored without the filter: raw elements
-                if packed is not None and sizes[k] and masks[k] & 1:
+            sz, mk, of = sizes[k0:k1], masks[k0:k1], offsets[k0:k1]
+            if packed is not None:  # stored without the filter: raw elements
+                for j in np.flatnonzero((sz > 0) & ((mk & 1) == 1)).tolist():
+                    k = k0 + j
                     packed.view(torch.uint8)[4 * k * cvol:4 * (k + 1) * cvol].copy_(
-                        cdev[offsets[k]:offsets[k] + 4 * cvol])
-            comp = [k for k in ks if sizes[k] and not masks[k] & 1]
-            if comp:
-                offs = np.array([offsets[k] for k in comp], np.uint64)
-                lens = np.array([sizes[k] for k in comp], np.uint64)
-                ooff = np.array([4 * k * cvol for k in comp], np.uint64)
+                        cdev[int(of[j]):int(of[j]) + 4 * cvol])
+            comp = np.flatnonzero((sz > 0) & ((mk & 1) == 0))
+            if len(comp):
+                offs = of[comp].astype(np.uint64)
+                lens = sz[comp].astype(np.uint64)
+                ooff = ((comp + k0) * (4 * cvol)).astype(np.uint64)
                 olen = np.full(len(comp), 4 * cvol, np.uint64)  # a whole chunk per slot
                 rc = _lib.lib().bldp_bslz4_decode_dev_async(
                     len(comp), host.ctypes.data, cdev.data_ptr(), offs.ctypes.data,

@@ -460,3 +460,51 @@ def test_bslz4_host_decoder_random_lz4(pkg, orc):
     for a, c in _random_bslz4_cases(orc, 99, 40):
         d = pkg.fbh5.bslz4_decode_host(c)
         assert np.array_equal(d.view(np.uint32), a.view(np.uint32)), (a.size, len(c))
+
+
+def test_compressed_read_planning(pkg):
+    """The vectorised planning of the compressed-FBH5 device read: batches
+    are contiguous chunk ranges covering every chunk (a small first batch),
+    and the pread tasks cover every stored chunk byte exactly once, each at
+    the file offset of its chunk (adjacent chunks merged into one read)."""
+    fb = pkg.fbh5
+    rng = np.random.default_rng(5)
+    for _ in range(20):
+        n = int(rng.integers(1, 60))
+        sizes = rng.integers(0, 50, n).astype(np.int64)
+        sizes[rng.random(n) < 0.2] = 0
+        b = fb._batches_of(sizes, 30, 120)
+        assert b[0][0] == 0 and b[-1][1] == n
+        assert all(x[1] == y[0] and x[0] < x[1] for x, y in zip(b, b[1:]))
+        offsets = np.zeros(n, np.int64)
+        offsets[1:] = np.cumsum(sizes[:-1])
+        faddr = np.cumsum(sizes + rng.integers(0, 2, n) * 7) + 1000  # some gaps
+        seen = np.zeros(int(sizes.sum()), np.int64)
+        for k0, k1 in b:
+            for task in fb._read_tasks(faddr, sizes, offsets, k0, k1, piece=16):
+                for fo, do, m in task:
+                    assert 0 < m <= 16
+                    for q in range(m):
+                        k = int(np.searchsorted(offsets, do + q, side="right")) - 1
+                        while sizes[k] == 0:
+                            k -= 1
+                        assert fo + q == faddr[k] + (do + q - offsets[k])
+                        seen[do + q] += 1
+        assert np.all(seen == 1)
+
+
+def test_file_metadata_cache_follows_rewrites(pkg, tmp_path):
+    """layout/raw_layout/chunk_index are memoised per file version: a file
+    rewritten in place (new size / inode / change time) is parsed again."""
+    import time
+
+    fb = pkg.fbh5
+    p = tmp_path / "m.h5"
+    a = np.zeros((64, 1, 8), np.float32, order="F")
+    fb.write(p, dict(foff=-1.0, nfpc=8), a, chunks=(4, 1, 64))
+    assert fb.layout(p)["cdims"] == (8, 1, 64)
+    assert fb.layout(p) is fb.layout(p)  # cached
+    time.sleep(0.01)
+    fb.write(p, dict(foff=-1.0, nfpc=8), np.zeros((128, 1, 4), np.float32, order="F"))
+    assert fb.layout(p)["cdims"] == (4, 1, 128)
+    assert fb.raw_layout(p) is not None
