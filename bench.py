@@ -188,7 +188,10 @@ def bench_kurtosis(args, cfg, eng, torch):
                        "plan": plan},
             "roofline": {"bound": "hbm", "achieved": round(algo / ms / 1e6, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(algo / ms / 1e6 / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(algo / ms / 1e6 / HBM_PEAK_GBS, 4),
+                         # HBM bytes per call from the committed PMC passes (every
+                         # kernel of the call; profiles/pmc_traffic.json "kurt_<cfg>")
+                         "traffic": traffic_from_profile("kurt_" + args.config, cfg["nbank"]),
                          "kernel": kern, "call_ms": round(ms, 4), "bytes_per_call": algo}}
 
 

@@ -189,11 +189,38 @@ namespace {
 
 
 bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
+bool aligned4(const void *p) { return ((uintptr_t)p & 3) == 0; }
 
 bool pitch_ok(const Geo &g) {
   return (g.ni <= 1 || g.ld_i % 4 == 0) && (g.nt <= 1 || g.ld_t % 4 == 0);
 }
 bool vec_ok(const Geo &g) { return g.cs == 1 && g.off % 4 == 0 && pitch_ok(g); }
+//   BLDP_UNALIGNED_VEC  unit-step windows that start off a 16-byte boundary
+//                  (or have row pitches that are not multiples of 4 floats)
+//                  on the vector paths: gfx950 executes global_load_dwordx4 at
+//                  any dword alignment (LLVM: unaligned-buffer-access), so the
+//                  lanes load the window's own float4 columns and no
+//                  realignment is needed.  A/B on MI355X
+//                  (profiles/r02/ab_unaligned_vec.json, 8 banks):
+//                    c0=3 F=64 cfg3 5.42 -> 5.08 ms, c0=1 F=8 T=1024 cfg4
+//                    3.30 -> 2.19 ms, c0=1 F=1 5.92 -> 5.78 ms; but c0=1/3
+//                    F=1024 4.92 -> 5.12 ms and c0=2 F=2 5.83 -> 6.03 ms (the
+//                    tile / realigning kernels keep those); kurtosis c0=1 cfg4
+//                    5.79 -> 2.45 ms, cfg3 11.85 -> 6.64 ms (leaf / register
+//                    paths instead of the two-pass / mid ones)
+//                  0 = off; 1 = reduce windows where it pays (below); 2 (default)
+//                  = 1 + kurtosis; 3 = every unit-step reduce window + kurtosis
+#ifndef BLDP_UNALIGNED_VEC
+#define BLDP_UNALIGNED_VEC 2
+#endif
+// A dword-aligned unit-step reduce window that is not 16-byte aligned goes to
+// the vector / narrow paths when that measured faster than the realigning
+// kernels, or when the alternative is the scalar path (pitches that are not
+// multiples of 4 floats).
+bool unaligned_vec_pays(int64_t F, bool rows16) {
+  if (BLDP_UNALIGNED_VEC >= 3 || !rows16) return true;
+  return F == 1 || (F % 4 == 0 && F <= 256);
+}
 
 int valid_op(int op) { return op >= BLDP_OP_SUM && op <= BLDP_OP_MIN; }
 
@@ -233,13 +260,16 @@ int reduce_impl(int nbank, const float *const *in, int64_t nchan, int64_t nif, i
   a.in_ld_t = g.ld_t;
   a.out = out;
   const bool empty = a.nco == 0 || a.ni == 0 || a.nto == 0;
-  bool rows16 = pitch_ok(g);
+  bool rows16 = pitch_ok(g), words = true;
   if (!in) return fail(BLDP_EINVAL, "null input pointer array");
   for (int b = 0; b < nbank; ++b) {
     a.in[b] = in[b];
     rows16 = rows16 && aligned16(a.in[b]);
+    words = words && aligned4(a.in[b]);
   }
-  const bool aligned = rows16 && vec_ok(g);
+  const bool aligned = (rows16 && vec_ok(g)) ||
+                       (BLDP_UNALIGNED_VEC >= 1 && words && g.cs == 1 &&
+                        unaligned_vec_pays(F, rows16));
   Plan p = plan_reduce(a, aligned, rows16, num_cus_current());
   if (!info) {
     for (int b = 0; b < nbank; ++b)
@@ -457,10 +487,11 @@ static int kurt_setup(int nbank, const float *const *in, int64_t nchan, int64_t 
   if (rc) return rc;
   *k = KurtArgs{};
   k->nbank = nbank;
-  bool aligned = true;
+  bool aligned = true, words = true;
   for (int b = 0; b < nbank; ++b) {
     k->in[b] = in ? in[b] : nullptr;
     aligned = aligned && aligned16(k->in[b]);
+    words = words && aligned4(k->in[b]);
   }
   k->in_off = g.off;
   k->in_cs = g.cs;
@@ -470,7 +501,8 @@ static int kurt_setup(int nbank, const float *const *in, int64_t nchan, int64_t 
   k->ni = g.ni;
   k->nt = g.nt;
   k->nrow = (int64_t)nbank * g.ni;
-  k->vec = vec_ok(g) && g.nc % 4 == 0 && aligned;
+  k->vec = BLDP_UNALIGNED_VEC >= 2 ? (g.cs == 1 && g.nc % 4 == 0 && words)
+                                   : (vec_ok(g) && g.nc % 4 == 0 && aligned);
   plan_kurtosis(*k, num_cus_current());
   return BLDP_OK;
 }

@@ -27,6 +27,10 @@ namespace {
 
 constexpr int kBlock = 256;  // 4 waves of 64
 typedef float f4v __attribute__((ext_vector_type(4)));
+// What the streaming loads point at: a float4 that may sit on any dword
+// boundary (BLDP_UNALIGNED_VEC windows start off a 16-byte boundary).  gfx950
+// executes global_load_dwordx4 at dword alignment, so the code is unchanged.
+typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
 
 template <int OP>
 struct R {
@@ -114,9 +118,9 @@ __device__ __forceinline__ float4 fold_acc(float4 (&acc)[kNacc]) {
 }
 __device__ __forceinline__ float4 ld4(const float *p) {
 #if BLDP_NT_LOADS
-  const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(p));
+  const f4u v = __builtin_nontemporal_load(reinterpret_cast<const f4u *>(p));
 #else
-  const f4v v = *reinterpret_cast<const f4v *>(p);
+  const f4u v = *reinterpret_cast<const f4u *>(p);
 #endif
   return make_float4(v.x, v.y, v.z, v.w);
 }

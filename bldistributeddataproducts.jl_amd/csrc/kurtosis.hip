@@ -97,13 +97,17 @@ namespace {
 constexpr int kB = 256;  // 4 waves of 64
 typedef float f4v __attribute__((ext_vector_type(4)));
 typedef float f2v __attribute__((ext_vector_type(2)));
+// streamed input: dword alignment is all gfx950's global_load_dwordx4 needs
+// (BLDP_UNALIGNED_VEC >= 2 windows start off a 16-byte boundary)
+typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
 typedef double d2v __attribute__((ext_vector_type(2)));
 
 int64_t cdivk(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // the window is read once: non-temporal 16-byte loads
 __device__ __forceinline__ float4 ldnt(const float *p) {
-  const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(p));
+  const f4u v = __builtin_nontemporal_load(reinterpret_cast<const f4u *>(p));
   return make_float4(v.x, v.y, v.z, v.w);
 }
 
@@ -347,10 +351,10 @@ static_assert(kLeafW == 1 || kLeafW == 2 || kLeafW == 4, "BLDP_KURT_LEAF_W: 1, 2
 template <int W>
 __device__ __forceinline__ void ldw(const float *p, float (&x)[W]) {
   if constexpr (W == 4) {
-    const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(p));
+    const f4u v = __builtin_nontemporal_load(reinterpret_cast<const f4u *>(p));
     x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
   } else if constexpr (W == 2) {
-    const f2v v = __builtin_nontemporal_load(reinterpret_cast<const f2v *>(p));
+    const f2u v = __builtin_nontemporal_load(reinterpret_cast<const f2u *>(p));
     x[0] = v.x; x[1] = v.y;
   } else {
     x[0] = __builtin_nontemporal_load(p);

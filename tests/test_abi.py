@@ -113,15 +113,23 @@ def test_launch_plans_host_only(pkg, L):
     # cfg4: narrow channel, long time -> time split waves and/or chunks
     p = plan(pkg, L, A, 512, 1, 879616, 8, 1024)
     assert p[0] == 0 and p[1] == 2 and (p[2] > 1 or p[4] > 1)
-    # F=1 time-only: narrow path; odd pitch or misaligned pointer: scalar
+    # F=1 time-only: narrow path; odd pitch with odd F: scalar
     assert plan(pkg, L, A, 4096, 1, 16, 1, 16)[0] == 1
     assert plan(pkg, L, A, 4095, 1, 16, 3, 1)[0] == 2
-    assert plan(pkg, L, A + 4, 4096, 1, 16, 64, 1)[0] == 2
-    # tile path: odd F, misaligned channel start, short channel step
+    # a dword-aligned pointer or window start off a 16-byte boundary: dword-aligned
+    # 16-byte loads on the row / narrow / interleaved kernels (BLDP_UNALIGNED_VEC);
+    # a pointer that is not even dword-aligned: scalar
+    assert plan(pkg, L, A + 4, 4096, 1, 16, 64, 1)[0] == 5
+    assert plan(pkg, L, A + 2, 4096, 1, 16, 64, 1)[0] == 2
+    assert plan(pkg, L, A, 4096, 1, 16, 64, 16, [1, 4032, 1, 0, 1, 1, 0, 16, 1])[0] in (0, 5)
+    assert plan(pkg, L, A, 4096, 1, 16, 1, 1, [1, 4092, 1, 0, 1, 1, 0, 16, 1])[0] == 1
+    assert plan(pkg, L, A, 4097, 1, 8, 1024, 8, [0, 4096, 1, 0, 1, 1, 0, 8, 1])[0] == 4
+    # tile path: odd F, misaligned channel start with F >= 512, short channel step
     assert plan(pkg, L, A, 4096, 1, 16, 3, 1, [0, 4095, 1, 0, 1, 1, 0, 16, 1])[0] == 3
-    assert plan(pkg, L, A, 4096, 1, 16, 64, 16, [1, 4032, 1, 0, 1, 1, 0, 16, 1])[0] == 3
-    # misaligned start with F = 1: the realigning narrow kernel
-    assert plan(pkg, L, A, 4096, 1, 16, 1, 1, [1, 4092, 1, 0, 1, 1, 0, 16, 1])[0] == 6
+    assert plan(pkg, L, A, 4096, 1, 16, 1024, 16, [1, 3072, 1, 0, 1, 1, 0, 16, 1])[0] == 3
+    # misaligned start, F = 1, a channel count that is not a multiple of 4:
+    # the realigning narrow kernel
+    assert plan(pkg, L, A, 4096, 1, 16, 1, 1, [1, 4094, 1, 0, 1, 1, 0, 16, 1])[0] == 6
     assert plan(pkg, L, A, 4096, 1, 16, 2, 4, [3, 4092, 1, 0, 1, 1, 0, 16, 1])[0] == 3  # F=2: tile
     assert plan(pkg, L, A, 4096, 1, 16, 1, 1, [0, 2048, 2, 0, 1, 1, 0, 16, 1])[0] == 3
     assert plan(pkg, L, A, 4096, 1, 16, 16, 1, [0, 2048, 2, 0, 1, 1, 0, 16, 1])[0] == 3
@@ -295,9 +303,14 @@ def test_kurtosis_plan_pairwise_blocks(pkg, L, n):
         assert all(node(lev, j)[1] > 1024 for j in range(1 << lev))
     if path == 2:
         assert ws >= 64 * nslot * (4 * 8 + 3 * 4)
-    # the unaligned plan for the same window: register tile up to 512 spectra
-    # (any alignment), else two passes
+    # a dword-aligned (not 16-byte aligned) pointer keeps the float4 plan
+    # (gfx950 16-byte loads at dword alignment); a channel count that is not a
+    # multiple of 4 takes the register tile up to 512 spectra (any alignment),
+    # else two passes
     assert L.bldp_kurtosis_plan_f32(A + 4, 64, 1, n, None, info) == 0
+    assert info[0] == path and info[1] == K
+    w = (ctypes.c_int64 * 9)(1, 62, 1, 0, 1, 1, 0, n, 1)
+    assert L.bldp_kurtosis_plan_f32(A, 64, 1, n, w, info) == 0
     assert info[0] == (1 if n <= 512 else 3) and info[1] == K
 
 

@@ -7,11 +7,13 @@ Float32 sum exactly (tests/test_oracle.py pins the oracle's).
 
 Tolerances (tests/conftest.py assert_kurtosis), by the path that ran:
   regs     (<= 32 spectra)      bit-exact
-  mid      (33..512, or <= 32 unaligned)  6 nt 2^-53 relative on k + 3
-                                 (Float64 order)
-  leaf     (> 512, aligned)     13 * 2^-24 * 1.05 relative on k + 3 (Float32
-                                 rounding of z^2, z^4 in the recipe)
-  twopass  (unaligned, > 512)   6 nt 2^-53 relative on k + 3
+  mid      (33..512, or <= 32 without float4 columns)  6 nt 2^-53 relative
+                                 on k + 3 (Float64 order)
+  leaf     (> 512, float4 columns)  13 * 2^-24 * 1.05 relative on k + 3
+                                 (Float32 rounding of z^2, z^4 in the recipe)
+  twopass  (> 512 without float4 columns)  6 nt 2^-53 relative on k + 3
+"float4 columns": unit channel step and a channel count that is a multiple of
+4; the start and the pitches need only dword alignment (gfx950 16-byte loads).
 """
 from __future__ import annotations
 
@@ -52,7 +54,8 @@ def power_rows(rng, nc, ni, nt, nfpc=64):
 
 
 def unaligned(nt):
-    """The path of a window whose channels cannot be read as float4."""
+    """The path of a window whose channels cannot be read as float4 (count
+    not a multiple of 4, or a channel step)."""
     return "mid" if nt <= 512 else "twopass"
 
 
@@ -151,6 +154,24 @@ def test_kurtosis_special_rows(eng, orc, nt):
     a[8, 0, :] = -a[0, 0, :]
     check(eng, orc, a, None, None, "aligned")
     check(eng, orc, a, [1, 62, 1, 0, 1, 1, 0, nt, 1], unaligned(nt), "unaligned")
+
+
+@pytest.mark.parametrize("nt,path", [(16, "regs"), (32, "regs"), (600, "leaf"), (5007, "leaf")])
+def test_kurtosis_unaligned_float4_windows(eng, orc, nt, path):
+    """Windows starting off a 16-byte boundary whose channel count is a
+    multiple of 4, and arrays with an odd channel pitch: the register and
+    streamed-leaf paths on dword-aligned 16-byte loads (bit-exact on regs)."""
+    rng = np.random.default_rng(1000 + nt)
+    a = power_rows(rng, 260, 2, nt)
+    check(eng, orc, a, [1, 256, 1, 0, 2, 1, 0, nt, 1], path, "c0=1")
+    check(eng, orc, a, [3, 252, 1, 1, 1, 1, 0, nt, 1], path, "c0=3, second IF")
+    b = power_rows(rng, 257, 2, nt)  # channel pitch 257 floats
+    check(eng, orc, b, [1, 256, 1, 0, 2, 1, 0, nt, 1], path, "odd pitch")
+    check(eng, orc, b, [0, 256, 1, 1, 1, 1, 0, nt, 1], path, "odd pitch, c0=0")
+    ks = eng.band_kurtosis([dev(eng, b), dev(eng, b)], [2, 252, 1, 0, 2, 1, 0, nt, 1])
+    want = orc.kurtosis(b, [2, 252, 1, 0, 2, 1, 0, nt, 1])
+    for k in ks:
+        assert_kurtosis(host(eng, k), want, path, nt, "band")
 
 
 def test_kurtosis_empty_and_degenerate_windows(eng, orc):

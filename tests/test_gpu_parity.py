@@ -201,7 +201,7 @@ def test_reduce_gamma_rtol(eng, orc, F, T):
 
 WINDOWS = [
     [32, 512, 1, 1, 1, 1, 4, 32, 1],        # (33:544, 2, 5:36): unaligned start? 32 -> aligned
-    [33, 512, 1, 0, 2, 1, 0, 48, 1],        # misaligned channel start -> tile path
+    [33, 512, 1, 0, 2, 1, 0, 48, 1],        # misaligned start -> dword-aligned vector loads / tile
     [1020, 96, -3, 0, 2, 1, 44, 12, -3],    # reversed strided channels and times
     [5, 120, 8, 0, 2, 1, 0, 48, 1],         # strided channels
     [0, 1024, 1, 1, 1, 1, 0, 24, 2],        # every other spectrum
@@ -242,15 +242,28 @@ TILE_CASES = [
 ]
 
 
+def misaligned_paths(win, F):
+    """Paths a window that starts off a 16-byte boundary takes (16-byte row
+    pitches; BLDP_UNALIGNED_VEC=2): unit-step windows with F = 1 or F % 4 == 0,
+    F <= 256 read their own float4 columns with dword-aligned 16-byte loads on
+    the vector / narrow paths; F = 1 windows whose channel count is not a
+    multiple of 4 take the realigning narrow kernel; the rest the tile path."""
+    if win[2] != 1:
+        return {"tile"}
+    if F == 1:
+        return {"narrow"} if win[1] % 4 == 0 else {"narrow_mis"}
+    if F % 4 == 0 and F <= 256:
+        return {"vector", "row"}
+    return {"tile"}
+
+
 @pytest.mark.parametrize("case", TILE_CASES, ids=range(len(TILE_CASES)))
 def test_tile_path(eng, orc, case):
     nc, ni, nt, win, F, T = case
     rng = np.random.default_rng(nc + F)
     a = np.asfortranarray(rng.integers(0, 256, (nc, ni, nt)).astype(np.float32))
     x = dev(eng, a)
-    # (misaligned unit-step windows with F in {1, 2} take the realigning narrow kernel)
-    expect = "narrow_mis" if F == 1 and win[2] == 1 else "tile"
-    assert eng.plan(x, F, T, "sum", win)["path"] == expect
+    assert eng.plan(x, F, T, "sum", win)["path"] in misaligned_paths(win, F)
     for op in ("sum", "max", "min", "mean"):
         got = host(eng, eng.reduce(x, F, T, op, win))
         want = orc.reduce(a, F, T, op, win)
@@ -270,7 +283,7 @@ def test_tile_path_special_values(eng, orc):
     x = dev(eng, a)
     for F, T in [(4, 1), (2, 2), (1, 4), (3, 4), (20, 1)]:
         win = [1, 60, 1, 0, 1, 1, 0, 4, 1]
-        assert eng.plan(x, F, T, "max", win)["path"] == ("narrow_mis" if F == 1 else "tile")
+        assert eng.plan(x, F, T, "max", win)["path"] in misaligned_paths(win, F)
         for op in ("sum", "max", "min"):
             got = host(eng, eng.reduce(x, F, T, op, win))
             want = orc.reduce(a, F, T, op, win)
@@ -743,16 +756,19 @@ def test_kurtosis_long_windows_leaf_merge(eng, orc, nt):
 @pytest.mark.parametrize("F", [1])
 def test_narrow_misaligned_windows(eng, orc, c0, F):
     """Windows starting off a 16-byte boundary with F = 1 (time integration
-    of a zoom window, e.g. idxs = (2:n, :, :)) take the realigning narrow
-    kernel: aligned float4 columns summed over T, realigned by lane shuffle.  Integer data, bit-exact for every op, two IFs, a ragged last tile,
-    stitched band slots, and a long time block split into chunks."""
+    of a zoom window, e.g. idxs = (2:n, :, :)): the narrow kernel on the
+    window's own (dword-aligned) float4 columns when the channel count is a
+    multiple of 4, else the realigning narrow kernel (aligned float4 columns
+    summed over T, realigned by lane shuffle).  Integer data, bit-exact for
+    every op, two IFs, a ragged last tile, stitched band slots, and a long
+    time block split into chunks."""
     rng = np.random.default_rng(10 * c0 + F)
     a = np.asfortranarray(rng.integers(0, 256, (4100, 2, 48)).astype(np.float32))
     nc = (4100 - c0) - (4100 - c0) % 2
     x = dev(eng, a)
     for T, tw in ((8, 48), (48, 48), (3, 12)):
         w = [c0, nc, 1, 0, 2, 1, 0, tw, 1]
-        assert eng.plan(x, F, T, "sum", w)["path"] == "narrow_mis"
+        assert eng.plan(x, F, T, "sum", w)["path"] in misaligned_paths(w, F)
         for op in ("sum", "mean", "max", "min"):
             got = host(eng, eng.reduce(x, F, T, op, w))
             want = orc.reduce(a, F, T, op, w)
@@ -768,7 +784,73 @@ def test_narrow_misaligned_windows(eng, orc, c0, F):
     # few tiles, long time block: partials over time chunks + the finalize
     b = np.asfortranarray(rng.integers(0, 256, (72, 1, 20000)).astype(np.float32))
     y = dev(eng, b)
-    w = [c0, 64, 1, 0, 1, 1, 0, 20000, 1]
-    p = eng.plan(y, F, 20000, "sum", w)
-    assert p["path"] == "narrow_mis" and p["time_chunks"] > 1
-    assert same_bits(host(eng, eng.reduce(y, F, 20000, "sum", w)), orc.reduce(b, F, 20000, "sum", w))
+    for ncw, path in ((64, "narrow"), (62, "narrow_mis")):
+        w = [c0, ncw, 1, 0, 1, 1, 0, 20000, 1]
+        p = eng.plan(y, F, 20000, "sum", w)
+        assert p["path"] == path and p["time_chunks"] > 1
+        assert same_bits(host(eng, eng.reduce(y, F, 20000, "sum", w)),
+                         orc.reduce(b, F, 20000, "sum", w))
+
+
+# Unaligned vector paths (BLDP_UNALIGNED_VEC=2): windows that start off a
+# 16-byte boundary, and arrays whose channel pitch is not a multiple of 4
+# floats (odd nchan), read their own float4 columns with dword-aligned 16-byte
+# loads.  (nchan, nif, ntime, window, F, T, expected paths)
+UNALIGNED_CASES = [
+    (4100, 2, 48, [1, 4096, 1, 0, 2, 1, 0, 48, 1], 64, 16, {"row", "vector"}),
+    (4100, 1, 48, [3, 4096, 1, 0, 1, 1, 0, 48, 1], 4, 48, {"row", "vector"}),
+    (4100, 2, 32, [2, 4080, 1, 1, 1, 1, 0, 32, 1], 20, 8, {"vector"}),
+    (4100, 1, 64, [1, 4096, 1, 0, 1, 1, 0, 64, 1], 256, 2, {"row"}),
+    (4100, 1, 16, [1, 4096, 1, 0, 1, 1, 0, 16, 1], 1, 16, {"narrow"}),
+    (516, 1, 20000, [3, 512, 1, 0, 1, 1, 0, 19456, 1], 8, 1024, {"vector"}),  # cfg4-like
+    (4097, 3, 40, [0, 4096, 1, 0, 3, 1, 0, 40, 1], 1024, 8, {"interleaved"}),  # odd pitch
+    (4097, 2, 40, [1, 4096, 1, 0, 2, 1, 0, 40, 1], 64, 8, {"row"}),            # odd pitch
+    (4097, 2, 40, [1, 4092, 1, 0, 2, 1, 0, 40, 1], 2, 8, {"narrow"}),         # odd pitch
+    (4097, 1, 24, [1, 4095, 1, 0, 1, 1, 0, 24, 1], 3, 8, {"scalar"}),         # odd pitch, odd F
+]
+
+
+@pytest.mark.parametrize("case", UNALIGNED_CASES, ids=range(len(UNALIGNED_CASES)))
+def test_unaligned_vector_paths(eng, orc, case):
+    """Integer data: bit-exact for sum/max/min against the oracle, mean at
+    RTOL; the path is the one the plan rule names; a 3-bank stitched band."""
+    nc, ni, nt, win, F, T, paths = case
+    rng = np.random.default_rng(nc * 7 + F)
+    a = np.asfortranarray(rng.integers(0, 256, (nc, ni, nt)).astype(np.float32))
+    x = dev(eng, a)
+    assert eng.plan(x, F, T, "sum", win)["path"] in paths, case
+    for op in ("sum", "max", "min", "mean"):
+        got = host(eng, eng.reduce(x, F, T, op, win))
+        want = orc.reduce(a, F, T, op, win)
+        if op == "mean":
+            np.testing.assert_allclose(got, want, rtol=RTOL)
+        else:
+            assert same_bits(got, want), (case, op)
+    banks = [a] + [np.asfortranarray(rng.integers(0, 256, a.shape).astype(np.float32))
+                   for _ in range(2)]
+    got = host(eng, eng.band_reduce([dev(eng, b) for b in banks], F, T, "sum", win))
+    assert same_bits(got, orc.stitch([orc.reduce(b, F, T, "sum", win) for b in banks]))
+
+
+def test_unaligned_vector_special_values(eng, orc):
+    """NaN / Inf / -0.0 through the unaligned row and narrow paths (Julia's
+    max/min semantics, bit-exact)."""
+    a = np.zeros((68, 1, 4), np.float32, order="F")
+    a[1:5, 0, 0] = -0.0
+    a[5:9, 0, 1] = [-0.0, 0.0, -0.0, -0.0]
+    a[9:13, 0, 2] = [1.0, np.nan, 2.0, 3.0]
+    a[13:17, 0, 3] = [np.inf, 1.0, -np.inf, 0.0]
+    a[17:21, 0, 0] = [np.inf, 1.0, 5.0, 0.0]
+    x = dev(eng, a)
+    win = [1, 64, 1, 0, 1, 1, 0, 4, 1]
+    for F, T in [(4, 1), (8, 2), (1, 4), (16, 4)]:
+        assert eng.plan(x, F, T, "max", win)["path"] in ("row", "vector", "narrow")
+        for op in ("sum", "max", "min"):
+            got = host(eng, eng.reduce(x, F, T, op, win))
+            want = orc.reduce(a, F, T, op, win)
+            if op == "sum":
+                assert np.array_equal(np.isnan(got), np.isnan(want))
+                fin = np.isfinite(want)
+                assert np.array_equal(got[fin], want[fin])
+            else:
+                assert same_bits(got, want), (F, T, op)

@@ -61,6 +61,10 @@ VARIANTS = {
     "kleafw2": "-DBLDP_KURT_LEAF_WAVES=2",
     "kleafw3": "-DBLDP_KURT_LEAF_WAVES=3",
     "kmidnochain": "-DBLDP_KURT_MID_TIMING_NOCHAIN=1",  # timing only: wrong numerics
+    # misaligned unit-step windows on the vector paths (dword-aligned 16-byte loads);
+    # 2 = the kurtosis register / leaf paths too
+    "unal": "-DBLDP_UNALIGNED_VEC=1",
+    "unal2": "-DBLDP_UNALIGNED_VEC=2",
 }
 
 
@@ -131,6 +135,7 @@ def run(names, rounds, iters, suite="main"):
     if suite == "kurt":
         kurt_case("kurt cfg3 nt16", b3)
         kurt_case("kurt cfg3 nt12", b3, [0, 1 << 26, 1, 0, 1, 1, 0, 12, 1])
+        kurt_case("kurt cfg3 c0=1 nt16", b3, [1, (1 << 26) - 4, 1, 0, 1, 1, 0, 16, 1])
         b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
         kurt_case("kurt cfg2 nt272", b2, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
         del b3
@@ -139,6 +144,8 @@ def run(names, rounds, iters, suite="main"):
         b5 = [eng.synth(65536, 1, 2048, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
         kurt_case("kurt 65536ch nt2048", b5)
         kurt_case("kurt cfg4 1 bank", b4[:1], [0, 512, 1, 0, 1, 1, 0, 879616, 1])
+        kurt_case("kurt cfg4 c0=1", b4, [1, 508, 1, 0, 1, 1, 0, 879616, 1])
+        kurt_case("kurt 65536ch nt2048 c0=3", b5, [3, 65532, 1, 0, 1, 1, 0, 2048, 1])
         cases_done = True
     elif suite == "tile":  # tile path: misaligned starts and odd F at cfg3 scale
         n = 1 << 26
@@ -151,6 +158,10 @@ def run(names, rounds, iters, suite="main"):
         band_case("cfg3 cs=2 F32", b3, 32, 16, [0, n // 2, 2, 0, 1, 1, 0, 16, 1])
         b2 = [eng.synth(65540, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
         band_case("cfg2 c0=1 F64", b2, 64, 16, [1, 65536, 1, 0, 1, 1, 0, 272, 1])
+        band_case("cfg3 c0=3 F1024", b3, 1024, 16, [3, n - 1024, 1, 0, 1, 1, 0, 16, 1])
+        band_case("cfg3 c0=2 F8", b3, 8, 16, [2, n - 8, 1, 0, 1, 1, 0, 16, 1])
+        b4 = [eng.synth(512, 1, 880000, 8, seed=10 * b + 1, kind=0) for b in range(8)]
+        band_case("cfg4 c0=1 F8 T1024", b4, 8, 1024, [1, 504, 1, 0, 1, 1, 0, 879616, 1])
         cases_done = True
     else:
         cases_done = False

@@ -11,6 +11,9 @@ exact for 16 B/lane stores (the reduce kernel's output writes are 4 B and tiny;
 taken as reported).
 
     python tools/pmc_traffic.py CONFIG BANKS_PER_LAUNCH FETCH.csv WRITE.csv
+    python tools/pmc_traffic.py --kurt CONFIG BANKS FETCH.csv WRITE.csv   (getkurtosis call:
+        k_kurt_leaf (16 B/lane streaming, x2) + the tree merge kernels (8 B
+        loads, taken as reported), summed per call; key "kurt_CONFIG")
 """
 from __future__ import annotations
 
@@ -34,12 +37,37 @@ def per_dispatch(path, counter, kernel_substr="k_reduce"):
     return vals
 
 
+def kurt_call(fpath, wpath):
+    """Per-call HBM bytes of the streamed-leaf kurtosis: every kernel of the
+    call, medians per kernel, FETCH of the 16 B/lane leaf stream x2."""
+    kern, hbm = {}, 0.0
+    for name in ("k_kurt_leaf", "k_kurt_tree", "k_kurt_final"):
+        try:
+            f = statistics.median(per_dispatch(fpath, "FETCH_SIZE", name))
+            w = statistics.median(per_dispatch(wpath, "WRITE_SIZE", name))
+        except SystemExit:
+            continue
+        mult = 2 if name == "k_kurt_leaf" else 1
+        kern[name] = {"fetch_size_kib_median": f, "write_size_kib_median": w,
+                      "hbm_bytes": int(mult * f * 1024 + w * 1024)}
+        hbm += mult * f * 1024 + w * 1024
+    return kern, hbm
+
+
 def main():
-    cfg, nbank, fpath, wpath = sys.argv[1], int(sys.argv[2]), sys.argv[3], sys.argv[4]
-    fetch = per_dispatch(fpath, "FETCH_SIZE")
-    write = per_dispatch(wpath, "WRITE_SIZE")
-    f_kib, w_kib = statistics.median(fetch), statistics.median(write)
-    hbm = 2 * f_kib * 1024 + w_kib * 1024
+    if sys.argv[1] == "--kurt":
+        cfg, nbank, fpath, wpath = "kurt_" + sys.argv[2], int(sys.argv[3]), sys.argv[4], sys.argv[5]
+        kern, hbm = kurt_call(fpath, wpath)
+        fetch = write = [0]
+        f_kib = sum(k["fetch_size_kib_median"] for k in kern.values())
+        w_kib = sum(k["write_size_kib_median"] for k in kern.values())
+    else:
+        cfg, nbank, fpath, wpath = sys.argv[1], int(sys.argv[2]), sys.argv[3], sys.argv[4]
+        kern = None
+        fetch = per_dispatch(fpath, "FETCH_SIZE")
+        write = per_dispatch(wpath, "WRITE_SIZE")
+        f_kib, w_kib = statistics.median(fetch), statistics.median(write)
+        hbm = 2 * f_kib * 1024 + w_kib * 1024
     out = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(out) as f:
@@ -55,6 +83,12 @@ def main():
               "correction": "hbm = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 half-count "
                             "of 16B/lane streaming reads)",
               "source": [os.path.relpath(fpath, REPO), os.path.relpath(wpath, REPO)]}
+    if kern:
+        d[cfg][str(nbank)]["kernels"] = kern
+        d[cfg][str(nbank)]["dispatches"] = None
+        d[cfg][str(nbank)]["correction"] = ("per call: k_kurt_leaf 2*FETCH_SIZE*1024 + "
+                                            "WRITE_SIZE*1024; tree/final kernels FETCH_SIZE*1024 "
+                                            "+ WRITE_SIZE*1024 (8-byte loads)")
     with open(out, "w") as f:
         json.dump(d, f, indent=1)
     print(json.dumps(d[cfg][str(nbank)]))
