@@ -16,7 +16,7 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 
 OPS = {"sum": 0, "mean": 1, "max": 2, "min": 3}
 PATHS = {0: "vector", 1: "narrow", 2: "scalar", 3: "tile", 4: "interleaved", 5: "row",
-         6: "narrow_mis"}
+         6: "narrow_mis", 7: "lane"}
 KURT_PATHS = {0: "regs", 1: "mid", 2: "leaf", 3: "twopass"}
 
 BLDP_OK, BLDP_EINVAL, BLDP_EDIM, BLDP_EHIP, BLDP_ENOMEM, BLDP_EBOUNDS = 0, -1, -2, -3, -5, -6

@@ -270,7 +270,7 @@ int reduce_impl(int nbank, const float *const *in, int64_t nchan, int64_t nif, i
   const bool aligned = (rows16 && vec_ok(g)) ||
                        (BLDP_UNALIGNED_VEC >= 1 && words && g.cs == 1 &&
                         unaligned_vec_pays(F, rows16));
-  Plan p = plan_reduce(a, aligned, rows16, num_cus_current());
+  Plan p = plan_reduce(a, aligned, rows16, words && g.cs == 1, num_cus_current());
   if (!info) {
     for (int b = 0; b < nbank; ++b)
       if (!in[b] && !empty) return fail(BLDP_EINVAL, "null input pointer (bank %d)", b);

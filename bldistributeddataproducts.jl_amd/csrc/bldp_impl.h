@@ -67,7 +67,7 @@ struct RedArgs {
 };
 
 enum Path { PATH_VEC = 0, PATH_NARROW = 1, PATH_SCALAR = 2, PATH_TILE = 3, PATH_VEC_IL = 4,
-            PATH_VEC_ROW = 5, PATH_NARROW_MIS = 6 };
+            PATH_VEC_ROW = 5, PATH_NARROW_MIS = 6, PATH_LANE = 7 };
 
 struct Plan {
   int path;
@@ -81,8 +81,9 @@ struct Plan {
 // blocks_c, grid) for an args struct whose shape/stride fields are set.
 // `aligned` says whether 16-byte vector loads of every group are legal;
 // `rows16` whether every bank pointer is 16-byte aligned and the IF/time
-// pitches are multiples of 4 floats (any channel offset and step).
-Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, int num_cus);
+// pitches are multiples of 4 floats (any channel offset and step); `words`
+// whether the channel step is 1 and every bank pointer is dword-aligned.
+Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus);
 
 hipError_t launch_reduce(const RedArgs &a, const Plan &p, int op, hipStream_t s);
 

@@ -396,6 +396,68 @@ __device__ __forceinline__ void narrow_mis_tile(const RedArgs &a, int64_t tile) 
 }
 
 // ---------------------------------------------------------------------------
+// Lane path (PATH_LANE): unit channel step, small F that is not a multiple of
+// 4 (2, 3, 5, 6, 7), any dword alignment (odd F, or F = 2 off a 16-byte
+// boundary).  One lane per output group: its F channels of a row are adjacent
+// floats, which the compiler issues as one dwordx{2,3} (F = 2, 3) or
+// dwordx4 + dwordx{1,2,3} (F = 5..7) load, so a wave-instruction streams 64*F*4
+// contiguous bytes with no LDS and no cross-lane work; 8 rows in flight, two
+// accumulator sets.  A/B against the tile path's LDS fold (8 banks x 2^26
+// channels x 16 spectra, profiles/r02/ab_lane.json): F = 3 6.69 vs 6.74 ms,
+// F = 2 (c0 = 1) 6.85 vs 6.92, but F = 5 10.4 vs 6.5 and F = 7 7.8 vs 6.4 (a
+// dwordx4 + dwordx{1,3} pair per lane at a 20- / 28-byte lane pitch splits
+// every wave-instruction into many partial lines).  So:
+//   BLDP_LANE  1 (default) = F = 3 always; F in {2, 5, 6, 7} only where the tile
+//              path cannot run (row pitches that are not multiples of 4 floats;
+//              the alternative is the scalar path); 2 = F in {2, 3, 5, 6, 7}
+//              always; 0 = off
+#ifndef BLDP_LANE
+#define BLDP_LANE 1
+#endif
+template <int OP, int F>
+__device__ __forceinline__ void lane_tile(const RedArgs &a, int64_t tile) {
+  const Coord c = decompose(a, tile);
+  const int64_t co = c.bc * kBlock + threadIdx.x;
+  if (co >= a.nco) return;
+  const int64_t r0 = c.chunk * a.rows_per_chunk;
+  const int64_t r1 = min(a.T, r0 + a.rows_per_chunk);
+  const float id = R<OP>::id();
+  float acc[2][F];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int f = 0; f < F; ++f) acc[q][f] = id;
+  const float *p =
+      a.in[c.bank] + a.in_off + c.i * a.in_ld_i + (c.to * a.T + r0) * a.in_ld_t + co * F;
+  const int64_t st = a.in_ld_t;
+  int64_t nrows = r1 - r0;
+  for (; nrows >= BLDP_BATCH; nrows -= BLDP_BATCH) {
+    float v[BLDP_BATCH][F];
+#pragma unroll
+    for (int u = 0; u < BLDP_BATCH; ++u)
+#pragma unroll
+      for (int f = 0; f < F; ++f) v[u][f] = __builtin_nontemporal_load(p + u * st + f);
+    p += BLDP_BATCH * st;
+#pragma unroll
+    for (int u = 0; u < BLDP_BATCH; ++u)
+#pragma unroll
+      for (int f = 0; f < F; ++f) acc[u & 1][f] = R<OP>::f(acc[u & 1][f], v[u][f]);
+  }
+  for (; nrows > 0; --nrows) {
+#pragma unroll
+    for (int f = 0; f < F; ++f) acc[0][f] = R<OP>::f(acc[0][f], __builtin_nontemporal_load(p + f));
+    p += st;
+  }
+  float s = R<OP>::f(acc[0][0], acc[1][0]);
+#pragma unroll
+  for (int f = 1; f < F; ++f) s = R<OP>::f(s, R<OP>::f(acc[0][f], acc[1][f]));
+  if (a.nchunk == 1)
+    a.out[c.bank * a.out_bank + c.i * a.out_ld_i + c.to * a.out_ld_t + co] = finish<OP>(s, a);
+  else
+    a.ws[(((c.chunk * a.nbank + c.bank) * a.nto + c.to) * a.ni + c.i) * a.nco + co] = s;
+}
+
+// ---------------------------------------------------------------------------
 // Scalar path: any F, any channel step, any alignment.  One lane per output.
 template <int OP>
 __device__ __forceinline__ void scalar_tile(const RedArgs &a, int64_t tile) {
@@ -740,6 +802,10 @@ template <int OP, int F>
 __global__ __launch_bounds__(kBlock) void k_reduce_narrow_mis(const RedArgs a) {
   for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) narrow_mis_tile<OP, F>(a, t);
 }
+template <int OP, int F>
+__global__ __launch_bounds__(kBlock) void k_reduce_lane(const RedArgs a) {
+  for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) lane_tile<OP, F>(a, t);
+}
 template <int OP>
 __global__ __launch_bounds__(kBlock) void k_reduce_scalar(const RedArgs a) {
   for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) scalar_tile<OP>(a, t);
@@ -943,6 +1009,16 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
     else
       hipLaunchKernelGGL((k_reduce_narrow_mis<OP, 2>), grid, block, 0, s, a);
     e = hipGetLastError();
+  } else if (p.path == PATH_LANE) {
+    switch (a.F) {
+      case 2: hipLaunchKernelGGL((k_reduce_lane<OP, 2>), grid, block, 0, s, a); break;
+      case 3: hipLaunchKernelGGL((k_reduce_lane<OP, 3>), grid, block, 0, s, a); break;
+      case 5: hipLaunchKernelGGL((k_reduce_lane<OP, 5>), grid, block, 0, s, a); break;
+      case 6: hipLaunchKernelGGL((k_reduce_lane<OP, 6>), grid, block, 0, s, a); break;
+      case 7: hipLaunchKernelGGL((k_reduce_lane<OP, 7>), grid, block, 0, s, a); break;
+      default: return hipErrorInvalidValue;
+    }
+    e = hipGetLastError();
   } else if (p.path == PATH_TILE) {
     if (a.in_cs == 1)
       hipLaunchKernelGGL((k_reduce_tile<OP, true>), grid, block, 0, s, a);
@@ -968,7 +1044,7 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
 }  // namespace
 
 // ---------------------------------------------------------------------------
-Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, int num_cus) {
+Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus) {
   Plan p{};
   const int64_t F = a.F, T = a.T;
   p.nout = a.nco * a.ni * a.nto;
@@ -998,9 +1074,16 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, int num_cus) {
     const int64_t nc4 = a.nco * F / 4;
     a.blocks_c = cdiv(nc4, kBlock);
     tiles = cdiv(nc4, 64) * a.ni * a.nto * a.nbank;
+  } else if (words && a.in_cs == 1 && BLDP_LANE >= 1 &&
+             (F == 3 || ((F == 2 || F == 5 || F == 6 || F == 7) &&
+                         (BLDP_LANE >= 2 || !rows16)))) {
+    // small odd / not-multiple-of-4 groups: one lane per output
+    p.path = PATH_LANE;
+    a.blocks_c = cdiv(a.nco, kBlock);
+    tiles = cdiv(a.nco, 64) * a.ni * a.nto * a.nbank;
   } else if (rows16 && a.in_cs == 1 && ((BLDP_NARROW_MIS >= 1 && F == 1) ||
                                          (BLDP_NARROW_MIS >= 2 && F == 2))) {
-    // misaligned start, time integration (+ pairs): aligned columns realigned in LDS
+    // misaligned start, time integration (+ pairs): aligned columns realigned by shuffle
     p.path = PATH_NARROW_MIS;
     a.blocks_c = cdiv(a.nco * F, kMisSpan);
     tiles = a.blocks_c * 4 * a.ni * a.nto * a.nbank;

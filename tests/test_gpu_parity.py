@@ -179,7 +179,8 @@ def test_plan_covers_all_paths(eng):
     assert eng.plan(x, 64, 16)["path"] == "vector"
     assert eng.plan(x, 1, 16)["path"] == "narrow"
     assert eng.plan(x, 2, 16)["path"] == "narrow"
-    assert eng.plan(eng.fb_empty(4095, 1, 4), 3, 1)["path"] == "scalar"
+    assert eng.plan(eng.fb_empty(4095, 1, 4), 3, 1)["path"] == "lane"
+    assert eng.plan(eng.fb_empty(4095, 1, 4), 4095, 1)["path"] == "scalar"
     y = eng.fb_empty(512, 1, 8192)
     assert eng.plan(y, 8, 8192)["time_chunks"] > 1
     assert eng.plan(y, 8, 1024)["time_split_waves"] in (2, 4)
@@ -246,10 +247,13 @@ def misaligned_paths(win, F):
     """Paths a window that starts off a 16-byte boundary takes (16-byte row
     pitches; BLDP_UNALIGNED_VEC=2): unit-step windows with F = 1 or F % 4 == 0,
     F <= 256 read their own float4 columns with dword-aligned 16-byte loads on
-    the vector / narrow paths; F = 1 windows whose channel count is not a
-    multiple of 4 take the realigning narrow kernel; the rest the tile path."""
+    the vector / narrow paths; F = 3 takes one lane per output group;
+    F = 1 windows whose channel count is not a multiple of 4 take the
+    realigning narrow kernel; the rest the tile path."""
     if win[2] != 1:
         return {"tile"}
+    if F == 3:
+        return {"lane"}
     if F == 1:
         return {"narrow"} if win[1] % 4 == 0 else {"narrow_mis"}
     if F % 4 == 0 and F <= 256:
@@ -806,7 +810,15 @@ UNALIGNED_CASES = [
     (4097, 3, 40, [0, 4096, 1, 0, 3, 1, 0, 40, 1], 1024, 8, {"interleaved"}),  # odd pitch
     (4097, 2, 40, [1, 4096, 1, 0, 2, 1, 0, 40, 1], 64, 8, {"row"}),            # odd pitch
     (4097, 2, 40, [1, 4092, 1, 0, 2, 1, 0, 40, 1], 2, 8, {"narrow"}),         # odd pitch
-    (4097, 1, 24, [1, 4095, 1, 0, 1, 1, 0, 24, 1], 3, 8, {"scalar"}),         # odd pitch, odd F
+    (4097, 1, 24, [1, 4095, 1, 0, 1, 1, 0, 24, 1], 3, 8, {"lane"}),           # odd pitch, odd F
+    (4097, 2, 24, [2, 4090, 1, 0, 2, 1, 0, 24, 1], 5, 4, {"lane"}),
+    (4100, 1, 40, [3, 4092, 1, 0, 1, 1, 0, 40, 1], 6, 8, {"tile"}),
+    (4100, 1, 40, [0, 4095, 1, 0, 1, 1, 0, 40, 1], 7, 20, {"tile"}),
+    (4097, 1, 40, [3, 4092, 1, 0, 1, 1, 0, 40, 1], 6, 8, {"lane"}),           # odd pitch
+    (4097, 1, 40, [0, 4095, 1, 0, 1, 1, 0, 40, 1], 7, 20, {"lane"}),          # odd pitch
+    (4097, 1, 40, [1, 4094, 1, 0, 1, 1, 0, 40, 1], 2, 8, {"lane"}),           # odd pitch
+    (70, 1, 30000, [1, 63, 1, 0, 1, 1, 0, 30000, 1], 3, 30000, {"lane"}),  # time chunks
+    (4097, 1, 24, [1, 4095, 1, 0, 1, 1, 0, 24, 1], 4095, 8, {"scalar"}),      # odd pitch, wide F
 ]
 
 

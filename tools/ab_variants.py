@@ -65,6 +65,11 @@ VARIANTS = {
     # 2 = the kurtosis register / leaf paths too
     "unal": "-DBLDP_UNALIGNED_VEC=1",
     "unal2": "-DBLDP_UNALIGNED_VEC=2",
+    "unal0": "-DBLDP_UNALIGNED_VEC=0",
+    "unal3": "-DBLDP_UNALIGNED_VEC=3",
+    # small odd F on one lane per output (dwordx3 etc.) vs the tile path's LDS fold
+    "nolane": "-DBLDP_LANE=0",
+    "lane2": "-DBLDP_LANE=2",
 }
 
 
@@ -160,6 +165,9 @@ def run(names, rounds, iters, suite="main"):
         band_case("cfg2 c0=1 F64", b2, 64, 16, [1, 65536, 1, 0, 1, 1, 0, 272, 1])
         band_case("cfg3 c0=3 F1024", b3, 1024, 16, [3, n - 1024, 1, 0, 1, 1, 0, 16, 1])
         band_case("cfg3 c0=2 F8", b3, 8, 16, [2, n - 8, 1, 0, 1, 1, 0, 16, 1])
+        band_case("cfg3 F5", b3, 5, 16, [0, n - 4, 1, 0, 1, 1, 0, 16, 1])
+        band_case("cfg3 c0=1 F7", b3, 7, 16, [1, n - 4, 1, 0, 1, 1, 0, 16, 1])
+        band_case("cfg3 c0=1 F2", b3, 2, 16, [1, n - 4, 1, 0, 1, 1, 0, 16, 1])
         b4 = [eng.synth(512, 1, 880000, 8, seed=10 * b + 1, kind=0) for b in range(8)]
         band_case("cfg4 c0=1 F8 T1024", b4, 8, 1024, [1, 504, 1, 0, 1, 1, 0, 879616, 1])
         cases_done = True
