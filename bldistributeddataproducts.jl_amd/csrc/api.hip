@@ -501,8 +501,8 @@ static int kurt_setup(int nbank, const float *const *in, int64_t nchan, int64_t 
   k->ni = g.ni;
   k->nt = g.nt;
   k->nrow = (int64_t)nbank * g.ni;
-  k->vec = BLDP_UNALIGNED_VEC >= 2 ? (g.cs == 1 && g.nc % 4 == 0 && words)
-                                   : (vec_ok(g) && g.nc % 4 == 0 && aligned);
+  k->rows16 = vec_ok(g) && g.nc % 4 == 0 && aligned;
+  k->vec = BLDP_UNALIGNED_VEC >= 2 ? (g.cs == 1 && g.nc % 4 == 0 && words) : k->rows16;
   plan_kurtosis(*k, num_cus_current());
   return BLDP_OK;
 }

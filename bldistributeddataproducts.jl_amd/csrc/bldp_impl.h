@@ -102,6 +102,7 @@ struct KurtArgs {
   int64_t in_off, in_cs, in_ld_i, in_ld_t;
   int64_t nc, ni, nt;
   int32_t vec;  // float4 along channels legal
+  int32_t rows16;  // ... and every float4 is 16-byte aligned (global_load_lds)
   int32_t K;    // level of the blocks of the pairwise-sum tree
   int64_t nslot;  // leaf slots, 2 per block (2^(K+1))
   int64_t nseg;   // 64-lane column segments per row (k_kurt_leaf)

@@ -395,6 +395,29 @@ __device__ __forceinline__ void stw(T *p, const T (&v)[W]) {
   }
 }
 
+// The leaf's (mean, M2, M3, M4) about its own mean, from the power sums about
+// its first spectrum c, and its (sum, max, min).
+template <int W>
+__device__ __forceinline__ void leaf_store(const KurtArgs &k, const LeafAcc<W> &A, int64_t row,
+                                           int64_t col, int64_t slot, int64_t len) {
+  const int64_t n = k.nrow * k.nc, e = row * k.nc + W * col;
+  const double cnt = (double)len;
+  double mo[4][W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    const double dl = A.a1[w] / cnt, dl2 = dl * dl;
+    mo[0][w] = A.c[w] + dl;
+    mo[1][w] = A.a2[w] - A.a1[w] * dl;
+    mo[2][w] = A.a3[w] - 3.0 * dl * A.a2[w] + 2.0 * cnt * dl2 * dl;
+    mo[3][w] = A.a4[w] - 4.0 * dl * A.a3[w] + 6.0 * dl2 * A.a2[w] - 3.0 * cnt * dl2 * dl2;
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) stw<W, double>(k.pm + (q * k.nslot + slot) * n + e, mo[q]);
+  stw<W, float>(k.pf + slot * n + e, A.s);
+  stw<W, float>(k.pf + (k.nslot + slot) * n + e, A.hi);
+  stw<W, float>(k.pf + (2 * k.nslot + slot) * n + e, A.lo);
+}
+
 __global__ __launch_bounds__(kB)
 #if BLDP_KURT_LEAF_WAVES > 0
 __attribute__((amdgpu_waves_per_eu(1, BLDP_KURT_LEAF_WAVES)))
@@ -464,22 +487,103 @@ void k_kurt_leaf(const KurtArgs k) {
     for (int q = 0; q < B; ++q)
       if (q < tail) leaf_step<W>(A, cur[q]);
   }
-  const int64_t n = k.nrow * k.nc, e = row * k.nc + W * col;
-  const double cnt = (double)len;
-  double mo[4][W];
+  leaf_store<W>(k, A, row, col, slot, len);
+}
+
+// 16-byte-aligned windows: the same leaf stream, fed through a per-wave LDS
+// ring of R spectra (1 KiB each: 64 lanes x 4 channels) that
+// global_load_lds_dwordx4 fills.  The loads have no VGPR destination, so R
+// spectra stay in flight per wave the whole time the wave computes (the
+// register-staged kernel has at most B in flight, and none while it computes).
+// Lane L's 16 bytes of a spectrum land at slot + 16 L and are read back by lane
+// L only, so no barrier is needed: the wave's own in-order vmcnt retires a slot
+// (vmcnt(R - B) leaves the B most recent batches' refills in flight), and a
+// slot is refilled only after its values have been used.
+// Measured and not taken (A/B on MI355X, profiles/r02/ab_kurt_leaf_lds.json,
+// bit-identical results): cfg4 2.52 ms against 2.45 ms for k_kurt_leaf with R = 8,
+// B = 4; R = 16 and B = 2 or 8 no better.  Twice the bytes in flight per wave
+// did not raise the rate, so the register-staged kernel's 4 KiB per wave is not
+// what bounds it.
+//   BLDP_KURT_LEAF_LDS  ring slots R (power of two, >= 2 B); 0 (default) = off
+//   BLDP_KURT_LEAF_LB   spectra per batch B
+#ifndef BLDP_KURT_LEAF_LDS
+#define BLDP_KURT_LEAF_LDS 0
+#endif
+#ifndef BLDP_KURT_LEAF_LB
+#define BLDP_KURT_LEAF_LB 4
+#endif
+constexpr int kRing = BLDP_KURT_LEAF_LDS > 0 ? BLDP_KURT_LEAF_LDS : 2 * BLDP_KURT_LEAF_LB;
+constexpr int kRingB = BLDP_KURT_LEAF_LB;
+static_assert((kRing & (kRing - 1)) == 0 && kRing >= 2 * kRingB && kRing <= 16,
+              "BLDP_KURT_LEAF_LDS: a power of two, >= 2 * BLDP_KURT_LEAF_LB, <= 16");
+// s_waitcnt vmcnt(N) (gfx9 encoding; expcnt and lgkmcnt left at their maxima)
+#define BLDP_VMCNT(N) __builtin_amdgcn_s_waitcnt(0x0F70 | ((N) & 15) | (((N) >> 4) << 14))
+
+__global__ __launch_bounds__(kB) void k_kurt_leaf_lds(const KurtArgs k) {
+  constexpr int R = kRing, B = kRingB;
+  __shared__ f4v ring[4][R][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t u = (int64_t)blockIdx.x * 4 + wave;
+  const int64_t seg = u % k.nseg, r = u / k.nseg;
+  const int64_t slot = r % k.nslot, row = r / k.nslot;
+  const int64_t col = seg * 64 + lane;
+  if (row >= k.nrow || col >= k.nc / 4) return;
+  int64_t t0, len;
+  pw_leaf(k.nt, k.K, slot, t0, len);
+  if (len <= 0) return;  // (leaves hold >= 257 spectra on this path: len > R)
+  const int bank = (int)(row / k.ni);
+  const int64_t i = row - (int64_t)bank * k.ni;
+  const int64_t ld = k.in_ld_t;
+  const float *p = k.in[bank] + k.in_off + i * k.in_ld_i + 4 * col + t0 * ld;
+  auto fill = [&](int64_t t) {  // spectrum t of the leaf -> its ring slot
+    __builtin_amdgcn_global_load_lds(
+        (const void *)(p + t * ld),
+        (__attribute__((address_space(3))) void *)&ring[wave][t & (R - 1)][0], 16, 0, 2 /* nt */);
+  };
+  auto take = [&](int64_t t, float (&x)[4]) {
+    const f4v v = ring[wave][t & (R - 1)][lane];
+    x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+  };
 #pragma unroll
-  for (int w = 0; w < W; ++w) {
-    const double dl = A.a1[w] / cnt, dl2 = dl * dl;
-    mo[0][w] = A.c[w] + dl;
-    mo[1][w] = A.a2[w] - A.a1[w] * dl;
-    mo[2][w] = A.a3[w] - 3.0 * dl * A.a2[w] + 2.0 * cnt * dl2 * dl;
-    mo[3][w] = A.a4[w] - 4.0 * dl * A.a3[w] + 6.0 * dl2 * A.a2[w] - 3.0 * cnt * dl2 * dl2;
+  for (int q = 0; q < R; ++q) fill(q);
+  LeafAcc<4> A;
+  {
+    float x0[4];
+    BLDP_VMCNT(R - 1);
+    take(0, x0);
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      A.s[w] = A.hi[w] = A.lo[w] = x0[w];  // the sum starts from the first element
+      A.c[w] = (double)x0[w];
+      A.a1[w] = A.a2[w] = A.a3[w] = A.a4[w] = 0.0;
+    }
   }
+  fill(R);  // spectra 1..R in flight
+  int64_t j = 1;
+  for (; j + R + B <= len; j += B) {  // refills j+R .. j+R+B-1 exist
+    float x[B][4];
+    BLDP_VMCNT(R - B);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) stw<W, double>(k.pm + (q * k.nslot + slot) * n + e, mo[q]);
-  stw<W, float>(k.pf + slot * n + e, A.s);
-  stw<W, float>(k.pf + (k.nslot + slot) * n + e, A.hi);
-  stw<W, float>(k.pf + (2 * k.nslot + slot) * n + e, A.lo);
+    for (int q = 0; q < B; ++q) take(j + q, x[q]);
+#pragma unroll
+    for (int q = 0; q < B; ++q) leaf_step<4>(A, x[q]);
+#pragma unroll
+    for (int q = 0; q < B; ++q) fill(j + R + q);
+  }
+  for (; j + R < len; ++j) {  // one refill per spectrum
+    float x[4];
+    BLDP_VMCNT(R - 1);
+    take(j, x);
+    leaf_step<4>(A, x);
+    fill(j + R);
+  }
+  BLDP_VMCNT(0);
+  for (; j < len; ++j) {
+    float x[4];
+    take(j, x);
+    leaf_step<4>(A, x);
+  }
+  leaf_store<4>(k, A, row, col, slot, len);
 }
 
 // Unaligned windows: one lane per (column, leaf) runs the sequential Float32
@@ -971,7 +1075,10 @@ hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s) {
     k.pm = reinterpret_cast<double *>(ws + L.a_pm);
     k.pf = reinterpret_cast<float *>(ws + L.a_pf);
     const dim3 g1((unsigned)cdivk(k.nrow * k.nslot * k.nseg, 4));
-    hipLaunchKernelGGL(k_kurt_leaf, g1, block, 0, s, k);
+    if (BLDP_KURT_LEAF_LDS > 0 && kLeafW == 4 && k.rows16)
+      hipLaunchKernelGGL(k_kurt_leaf_lds, g1, block, 0, s, k);
+    else
+      hipLaunchKernelGGL(k_kurt_leaf, g1, block, 0, s, k);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return launch_tree<true>(k, ws, L, s);

@@ -70,6 +70,11 @@ VARIANTS = {
     # small odd F on one lane per output (dwordx3 etc.) vs the tile path's LDS fold
     "nolane": "-DBLDP_LANE=0",
     "lane2": "-DBLDP_LANE=2",
+    # streamed kurtosis leaves through a per-wave LDS ring filled by global_load_lds
+    "klds8": "-DBLDP_KURT_LEAF_LDS=8",
+    "klds16": "-DBLDP_KURT_LEAF_LDS=16",
+    "klds8b2": "-DBLDP_KURT_LEAF_LDS=8 -DBLDP_KURT_LEAF_LB=2",
+    "klds16b8": "-DBLDP_KURT_LEAF_LDS=16 -DBLDP_KURT_LEAF_LB=8",
 }
 
 
@@ -189,7 +194,7 @@ def run(names, rounds, iters, suite="main"):
     torch.cuda.synchronize()
 
     res = {c[0]: {n: [] for n in names} for c in cases}
-    ref = {}
+    ref, first, exact = {}, {}, {}
     for r in range(rounds):
         for label, go, nbytes, out, _ in cases:
             for n in names:
@@ -208,6 +213,13 @@ def run(names, rounds, iters, suite="main"):
                     ref.setdefault(label, o)
                     if abs(o - ref[label]) > 1e-4 * abs(ref[label]):
                         print(f"WARNING {label} {n}: checksum {o} vs {ref[label]}")
+                    if label not in first:
+                        first[label] = (n, out.clone())
+                    else:  # same bits as the first variant?  (same arithmetic order)
+                        same = bool(torch.equal(out, first[label][1]))
+                        exact.setdefault(label, {})[n] = same
+                        print(f"{label} {n} vs {first[label][0]}: "
+                              f"{'bit-identical' if same else 'DIFFERENT BITS'}", flush=True)
         print(f"round {r} done", file=sys.stderr, flush=True)
     summary = {}
     for label, go, nbytes, out, _ in cases:
@@ -217,6 +229,8 @@ def run(names, rounds, iters, suite="main"):
             med = ts[len(ts) // 2]
             summary[label][n] = {"median_ms": round(med, 4), "min_ms": round(ts[0], 4),
                                  "GBps_median": round(nbytes / med / 1e6, 1)}
+            if n in exact.get(label, {}):
+                summary[label][n]["bit_identical_to_" + names[0]] = exact[label][n]
         print(label, json.dumps(summary[label]))
     return summary
 
