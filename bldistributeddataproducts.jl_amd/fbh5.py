@@ -774,10 +774,12 @@ def _copy_stream(dev, priority, j=0):
     return s
 
 
-def _batches_of(sizes, first_bytes, batch_bytes):
+def _batches_of(sizes, first_bytes, batch_bytes, ramp=True):
     """Split chunk indices 0..n-1 into contiguous ranges [k0, k1) of about
-    ``batch_bytes`` stored bytes (the first about ``first_bytes``, so the
-    first H2D copy starts early)."""
+    ``batch_bytes`` stored bytes.  The first holds about ``first_bytes`` so
+    the first H2D copy starts early; with ``ramp`` the next ones double from
+    there up to ``batch_bytes`` (the copy engine is fed while the reader pool
+    gets ahead)."""
     n = len(sizes)
     if n == 0:
         return []
@@ -789,7 +791,7 @@ def _batches_of(sizes, first_bytes, batch_bytes):
         k1 = min(max(k1, k0 + 1), n)
         out.append((k0, k1))
         base = int(cum[k1 - 1])
-        k0, target = k1, batch_bytes
+        k0, target = k1, (min(2 * target, batch_bytes) if ramp else batch_bytes)
     return out
 
 
@@ -825,7 +827,7 @@ def _read_tasks(faddr, sizes, offsets, k0, k1, piece):
 
 
 def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 20,
-                           raw_chunks=False, first_batch_bytes=16 << 20):
+                           raw_chunks=False, first_batch_bytes=16 << 20, ramp=True, dense=True):
     """Device path of a compressed window, overlapped in three stages: a
     reader thread reads batches of stored chunks straight into pinned memory
     and queues their H2D copy on a copy stream, while this thread decodes the
@@ -836,8 +838,13 @@ def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 
     outside that parser's scope, one H5Dread_chunk at a time.
     ``raw_chunks``: the dataset has no filter, every stored chunk is raw
     float32 (no decode; when every chunk is stored, the device copy of the
-    chunks is the packed chunk grid itself).  ``timings`` (a dict) receives
-    stage times."""
+    chunks is the packed chunk grid itself).  ``dense=False``: when the chunk
+    box is one chunk wide in IF and channel (gi = gc = 1: the chunks cover the
+    window's channel span, as in rawspec products) and the steps are
+    positive, the decoded chunk grid [gt*ct][ci][cc] already holds the window
+    at fixed pitches, so a strided Julia-order view of it is returned and the
+    gather is skipped (the reduce takes the pitches).  ``timings`` (a dict)
+    receives stage times."""
     import time
 
     import torch
@@ -893,12 +900,15 @@ def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 
         pinned = torch.empty(total + 16, dtype=torch.uint8, pin_memory=True)
         host = pinned.numpy()
         t_pin = time.perf_counter() - t_pin
-        batches = _batches_of(sizes, first_batch_bytes, batch_bytes)
+        batches = _batches_of(sizes, first_batch_bytes, batch_bytes, ramp)
         with torch.cuda.device(dev):
             cdev = torch.empty(total + 16, dtype=torch.uint8, device=dev)
             dense_raw = raw_chunks and bool(np.all(sizes == 4 * cvol))
+            # chunks never written read as the fill value 0; when every chunk is
+            # stored each slot is written whole (decode or raw copy)
             packed = cdev[:total].view(torch.float32) if dense_raw else \
-                torch.zeros(len(sizes) * cvol, dtype=torch.float32, device=dev)
+                (torch.empty if bool(np.all(sizes > 0)) else torch.zeros)(
+                    len(sizes) * cvol, dtype=torch.float32, device=dev)
             # the H2D copies (the critical path) on a cached high-priority stream
             copy_streams = [_copy_stream(dev, -1)]
             hostmv = memoryview(host)
@@ -913,10 +923,20 @@ def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 
             trace = [] if timings is not None and os.environ.get("BLDP_TRACE_READ") else None
             # every batch's preads go to the pool at once, in batch order, so the
             # pool never idles between batches; the reader thread below only
-            # waits for a batch's reads and queues its H2D copy
-            pending = [[pool.submit(read_task, t) for t in
-                        _read_tasks(faddr, sizes, offsets, k0, k1, filestream.PIECE_BYTES)]
-                       for k0, k1 in batches] if tab is not None else None
+            # waits for a batch's reads and queues its H2D copy.  A batch is cut
+            # into >= 16 pieces (<= PIECE_BYTES each) so that the small first
+            # batches are read by the whole pool
+            t_sub = time.perf_counter()
+            t_setup = t_sub - t0
+            pending = None
+            if tab is not None:
+                pending = []
+                for k0, k1 in batches:
+                    bb = int(offsets[k1 - 1] + sizes[k1 - 1] - offsets[k0])
+                    piece = max(256 << 10, min(filestream.PIECE_BYTES, bb // 16))
+                    pending.append([pool.submit(read_task, t) for t in
+                                    _read_tasks(faddr, sizes, offsets, k0, k1, piece)])
+            t_sub = time.perf_counter() - t_sub
 
             def stage(b):  # reader thread: (reads landed) -> (async) device
                 k0, k1 = batches[b]
@@ -965,7 +985,7 @@ def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 
         if f is not None:
             H.H5Fclose(f)
     if timings is not None:
-        timings.update(chunk_index_s=t_tab, pinned_alloc_s=t_pin,
+        timings.update(chunk_index_s=t_tab, pinned_alloc_s=t_pin, setup_s=t_setup, submit_s=t_sub,
                        before_unchunk_s=time.perf_counter() - t0)
         if trace:
             torch.cuda.synchronize(dev)
@@ -973,6 +993,19 @@ def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 
             timings["trace"] = [(b, round(1e3 * tq, 3), round(first.elapsed_time(e0), 3),
                                  round(first.elapsed_time(e1), 3), nb)
                                 for _, b, tq, e0, e1, nb in trace]
+    if not dense and gi == 1 and gc == 1 and win[2] > 0 and win[5] > 0 and win[8] > 0 \
+            and nc * ni * nt > 0:
+        # the window inside the packed grid [gt*ct][ci][cc], Julia order
+        ct, ci, cc = chunk
+        off = (win[6] - box0[0]) * ci * cc + (win[3] - box0[1]) * cc + (win[0] - box0[2])
+        out = torch.as_strided(packed, (nc, ni, nt), (win[2], win[5] * cc, win[8] * ci * cc), off)
+        if timings is not None:
+            with torch.cuda.device(dev):
+                torch.cuda.synchronize()
+            timings.update(total_s=time.perf_counter() - t0, wait_io_s=t_io, decode_s=t_dec,
+                           batches=len(batches), compressed_bytes=total,
+                           parsed_chunk_index=tab is not None, gather="view")
+        return out
     return _unchunk_out(dev, torch, engine, _lib, nc, ni, nt, chunk, box0, grid, win, packed,
                         timings, t0, t_io, t_dec, batches, total, tab is not None)
 

@@ -203,7 +203,8 @@ def getfbh5data(fbh5name, idxs=(COLON, COLON, COLON), fqavby=1, fqavfunc="sum", 
         # are decoded, windowed and reduced on the GPU, the result comes back.
         # Unfiltered chunked data takes the same chunk reader without a decode.
         x = fbh5._read_window_bslz4_dev(fbh5name, idxs, f"cuda:{device}",
-                                        raw_chunks=not fbh5.needs_bslz4(fbh5name))
+                                        raw_chunks=not fbh5.needs_bslz4(fbh5name),
+                                        dense=False)  # (a view of the chunks when it can)
         import torch
 
         with torch.cuda.device(x.device):

@@ -65,16 +65,28 @@ def main():
     os.environ.pop("BLDP_TRACE_READ")
     res["pipeline_total_ms"] = round(1e3 * sorted(ts)[2], 2)
     res["pipeline_copy_span_ms"] = round(tr[-1][3] - tr[0][2], 3) if tr else None
-    for bb in (64, 128):  # batch size sweep (ms before the gather, median of 5)
-        for fbb in (16,):
-            ts = []
-            for _ in range(5):
-                tm = {}
-                x = fb._read_window_bslz4_dev(path, (C, C, C), "cuda:0", timings=tm,
-                                              batch_bytes=bb << 20, first_batch_bytes=fbb << 20)
-                del x
-                ts.append(tm["total_s"])
-            res[f"batch_{bb}MiB_first_{fbb}MiB_total_ms"] = round(1e3 * sorted(ts)[2], 2)
+    # batch schedule x gather sweep (device read total, ms, median of 7, interleaved)
+    sweep = [(64, 16, False, True), (64, 16, True, True), (64, 16, True, False),
+             (64, 8, True, False), (64, 4, True, False), (128, 16, True, False),
+             (32, 8, True, False)]
+    tsw = {k: [] for k in sweep}
+    for _ in range(7):
+        for bb, fbb, ramp, dense in sweep:
+            tm = {}
+            x = fb._read_window_bslz4_dev(path, (C, C, C), "cuda:0", timings=tm,
+                                          batch_bytes=bb << 20, first_batch_bytes=fbb << 20,
+                                          ramp=ramp, dense=dense)
+            del x
+            tsw[(bb, fbb, ramp, dense)].append(tm["total_s"])
+    for (bb, fbb, ramp, dense), ts in tsw.items():
+        res[f"batch_{bb}MiB_first_{fbb}MiB_{'ramp' if ramp else 'flat'}_"
+            f"{'gather' if dense else 'view'}_total_ms"] = round(1e3 * sorted(ts)[3], 2)
+    os.environ["BLDP_TRACE_READ"] = "1"
+    tm = {}
+    x = fb._read_window_bslz4_dev(path, (C, C, C), "cuda:0", timings=tm, dense=False)
+    del x
+    os.environ.pop("BLDP_TRACE_READ")
+    res["trace_ramp_view"] = tm.get("trace")
     # ceilings
     H = fb.h5().L
     f = H.H5Fopen(path.encode(), 0, 0)

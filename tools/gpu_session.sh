@@ -53,6 +53,7 @@ for s in $STEPS; do
              --mode host ;;
     decode) run decode 600 python bench.py --mode decode ;;
     file)  run file 600 python bench.py --mode file ;;
+    file_probe) run file_probe 600 python tools/file_probe.py ;;
     rawfile) run rawfile 600 python bench.py --mode rawfile ;;
     paths) run paths 300 python tools/probe_paths.py ;;
     paths_big) run paths_big 300 python tools/probe_paths.py --big ;;
