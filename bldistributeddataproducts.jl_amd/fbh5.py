@@ -838,13 +838,14 @@ def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 
     outside that parser's scope, one H5Dread_chunk at a time.
     ``raw_chunks``: the dataset has no filter, every stored chunk is raw
     float32 (no decode; when every chunk is stored, the device copy of the
-    chunks is the packed chunk grid itself).  ``dense=False``: when the chunk
-    box is one chunk wide in IF and channel (gi = gc = 1: the chunks cover the
-    window's channel span, as in rawspec products) and the steps are
-    positive, the decoded chunk grid [gt*ct][ci][cc] already holds the window
-    at fixed pitches, so a strided Julia-order view of it is returned and the
-    gather is skipped (the reduce takes the pitches).  ``timings`` (a dict)
-    receives stage times."""
+    chunks is the packed chunk grid itself).  ``dense=False`` returns
+    (tensor, window): when the chunk box is one chunk wide in IF and channel
+    (gi = gc = 1: the chunks cover the window's channel span, as in rawspec
+    products) the decoded chunk grid [gt*ct][ci][cc] already is a Julia-order
+    (cc, ci, gt*ct) array holding the window, so it is returned with the
+    window relative to it and the gather is skipped (the reduce kernels take
+    the window, steps included); otherwise (gathered tensor, None).
+    ``timings`` (a dict) receives stage times."""
     import time
 
     import torch
@@ -993,21 +994,23 @@ def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 
             timings["trace"] = [(b, round(1e3 * tq, 3), round(first.elapsed_time(e0), 3),
                                  round(first.elapsed_time(e1), 3), nb)
                                 for _, b, tq, e0, e1, nb in trace]
-    if not dense and gi == 1 and gc == 1 and win[2] > 0 and win[5] > 0 and win[8] > 0 \
-            and nc * ni * nt > 0:
-        # the window inside the packed grid [gt*ct][ci][cc], Julia order
+    if not dense and gi == 1 and gc == 1 and nc * ni * nt > 0:
+        # the packed grid [gt*ct][ci][cc] as a Julia-order array, and the
+        # window relative to it
         ct, ci, cc = chunk
-        off = (win[6] - box0[0]) * ci * cc + (win[3] - box0[1]) * cc + (win[0] - box0[2])
-        out = torch.as_strided(packed, (nc, ni, nt), (win[2], win[5] * cc, win[8] * ci * cc), off)
+        grid_t = packed[:gt * ct * ci * cc].view(gt * ct, ci, cc).permute(2, 1, 0)
+        rwin = [win[0] - box0[2], nc, win[2], win[3] - box0[1], ni, win[5],
+                win[6] - box0[0], nt, win[8]]
         if timings is not None:
             with torch.cuda.device(dev):
                 torch.cuda.synchronize()
             timings.update(total_s=time.perf_counter() - t0, wait_io_s=t_io, decode_s=t_dec,
                            batches=len(batches), compressed_bytes=total,
-                           parsed_chunk_index=tab is not None, gather="view")
-        return out
-    return _unchunk_out(dev, torch, engine, _lib, nc, ni, nt, chunk, box0, grid, win, packed,
-                        timings, t0, t_io, t_dec, batches, total, tab is not None)
+                           parsed_chunk_index=tab is not None, gather="window of the chunk grid")
+        return grid_t, rwin
+    out = _unchunk_out(dev, torch, engine, _lib, nc, ni, nt, chunk, box0, grid, win, packed,
+                       timings, t0, t_io, t_dec, batches, total, tab is not None)
+    return out if dense else (out, None)
 
 
 def _decode_batches(batches, stage, sizes, masks, offsets, cvol, packed, cdev, host, _lib,

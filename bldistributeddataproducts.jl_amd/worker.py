@@ -202,13 +202,15 @@ def getfbh5data(fbh5name, idxs=(COLON, COLON, COLON), fqavby=1, fqavfunc="sum", 
         # compressed rawspec product: only the compressed chunks cross PCIe; they
         # are decoded, windowed and reduced on the GPU, the result comes back.
         # Unfiltered chunked data takes the same chunk reader without a decode.
-        x = fbh5._read_window_bslz4_dev(fbh5name, idxs, f"cuda:{device}",
-                                        raw_chunks=not fbh5.needs_bslz4(fbh5name),
-                                        dense=False)  # (a view of the chunks when it can)
+        # (the decoded chunk grid plus the window inside it when the chunks
+        # span the window's channels: no gather copy)
+        x, rwin = fbh5._read_window_bslz4_dev(fbh5name, idxs, f"cuda:{device}",
+                                              raw_chunks=not fbh5.needs_bslz4(fbh5name),
+                                              dense=False)
         import torch
 
         with torch.cuda.device(x.device):
-            return engine.fb_to_numpy(engine.reduce(x, fqavby, tavby, op))
+            return engine.fb_to_numpy(engine.reduce(x, fqavby, tavby, op, rwin))
     if op is not None:
         raw = fbh5.raw_layout(fbh5name)  # uncompressed contiguous: preads, no libhdf5 copy
         if raw is not None:

@@ -544,6 +544,40 @@ def test_unfiltered_chunked_fbh5_on_gpu(pkg, orc, tmp_path):
         assert same_bits(got, orc.reduce(a, F, T, op, win)), idxs
 
 
+@pytest.mark.parametrize("ci", [1, 2])
+def test_chunks_spanning_the_channels_reduce_in_place(pkg, orc, tmp_path, ci):
+    """Chunks that span the whole channel axis (gi = gc = 1, the rawspec
+    layout): getdata reduces the window straight out of the decoded chunk grid
+    (no gather), for windows with channel / IF / time steps, reversed axes,
+    integer indices and partial first and last chunks; compressed and
+    unfiltered files, every op, against the oracle (integer data: exact)."""
+    J, C = pkg.JRange, pkg.COLON
+    rng = np.random.default_rng(40 + ci)
+    nc, ni, nt = 1500, 2, 61
+    a = np.asfortranarray(rng.integers(0, 128, (nc, ni, nt)).astype(np.float32))
+    comp, plain = str(tmp_path / "c.h5"), str(tmp_path / "p.h5")
+    chunk = (8, ci, nc)
+    pkg.fbh5.write_bslz4(comp, dict(foff=-1.0), a, chunk,
+                         lambda blk: orc.np_bslz4_encode(blk, 512, lz4=orc.lz4_compress))
+    pkg.fbh5.write(plain, dict(foff=-1.0), a, chunks=chunk)
+    cases = [((C, C, C), 4, 1, "sum"), ((J(3, 1498), C, J(5, 60)), 8, 4, "max"),
+             ((J(1, 2, 1500), 2, J(2, 3, 59)), 5, 2, "min"),
+             ((J(1500, -1, 1), J(2, -1, 1), J(61, -2, 1)), 3, 31, "sum"),
+             ((J(11, 3, 1490), C, 17), 1, 1, "sum")]
+    for idxs, F, T, op in cases:
+        win = pkg.idxs.to_window(pkg.sanitizeidxs(idxs), a.shape) or \
+            [0, nc, 1, 0, ni, 1, 0, nt, 1]
+        want = orc.reduce(a, F, T, op, win)
+        for f in (comp, plain):
+            x, rwin = pkg.fbh5._read_window_bslz4_dev(f, pkg.sanitizeidxs(idxs), "cuda:0",
+                                                      raw_chunks=f == plain, dense=False)
+            # the chunk box is one chunk wide in IF unless the window takes
+            # both IFs from one-IF chunks
+            assert (rwin is not None) == (ci == 2 or win[4] == 1), (idxs, ci)
+            got = pkg.WorkerFunctions.getdata(f, idxs, fqavby=F, fqavfunc=op, tavby=T)
+            assert same_bits(got, want), (f, idxs, F, T, op)
+
+
 def test_bslz4_gpu_decoder_random_lz4(pkg, orc):
     """The GPU decoder on the same kind of random chunks (real LZ4 matches,
     all block sizes, raw tails), 40 chunks in one call."""
