@@ -245,6 +245,16 @@ def getkurtosis(fname, idxs=(COLON, COLON, COLON), device=0):
         from . import fbh5
 
         h5 = readers.ishdf5(fname)
+        if h5 and (fbh5.needs_bslz4(fname) or fbh5.raw_chunked(fname)):
+            # compressed / chunked: the chunks go to the GPU, are decoded there
+            # and the kurtosis runs on the window inside the chunk grid
+            import torch
+
+            x, rwin = fbh5._read_window_bslz4_dev(fname, idxs, f"cuda:{device}",
+                                                  raw_chunks=not fbh5.needs_bslz4(fname),
+                                                  dense=False)
+            with torch.cuda.device(x.device):
+                return engine.fb_to_numpy(engine.kurtosis(x, rwin))
         raw = fbh5.raw_layout(fname) if h5 else readers.fil_raw_layout(fname)
         got = _raw_to_device(fname, raw, idxs, device) if raw is not None else None
         if got is not None:  # window streamed to the GPU, kurtosis there

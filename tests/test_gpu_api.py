@@ -578,6 +578,35 @@ def test_chunks_spanning_the_channels_reduce_in_place(pkg, orc, tmp_path, ci):
             assert same_bits(got, want), (f, idxs, F, T, op)
 
 
+def test_getkurtosis_compressed_and_chunked_files(pkg, orc, tmp_path):
+    """getkurtosis on a bitshuffle/LZ4 FBH5 and an unfiltered chunked one: the
+    chunks are decoded on the GPU and the kurtosis runs on the window inside
+    the chunk grid (chunks spanning the channels) or on the gathered window
+    (narrower chunks); long and short windows against the oracle."""
+    from conftest import assert_kurtosis
+
+    J, C = pkg.JRange, pkg.COLON
+    rng = np.random.default_rng(77)
+    nc, ni, nt = 512, 1, 1500
+    a = np.asfortranarray(rng.gamma(4.0, 1e9, (nc, ni, nt)).astype(np.float32))
+    W, eng = pkg.WorkerFunctions, pkg.engine
+    for chunk in ((16, 1, nc), (16, 1, 96)):
+        comp, plain = str(tmp_path / f"c{chunk[2]}.h5"), str(tmp_path / f"p{chunk[2]}.h5")
+        pkg.fbh5.write_bslz4(comp, dict(foff=-1.0), a, chunk,
+                             lambda blk: orc.np_bslz4_encode(blk, 512, lz4=orc.lz4_compress))
+        pkg.fbh5.write(plain, dict(foff=-1.0), a, chunks=chunk)
+        for idxs in ((C, C, C), (J(5, 508), C, J(7, 1406)), (J(2, 2, 511), C, J(1, 300))):
+            win = pkg.idxs.to_window(pkg.sanitizeidxs(idxs), a.shape) or \
+                [0, nc, 1, 0, ni, 1, 0, nt, 1]
+            want = orc.kurtosis(a, win)
+            for f in (comp, plain):
+                got = W.getkurtosis(f, idxs)
+                x, rwin = pkg.fbh5._read_window_bslz4_dev(f, pkg.sanitizeidxs(idxs), "cuda:0",
+                                                          raw_chunks=f == plain, dense=False)
+                path = eng.kurtosis_plan(x, rwin)["path"]
+                assert_kurtosis(got, want, path, win[7], (f, idxs))
+
+
 def test_bslz4_gpu_decoder_random_lz4(pkg, orc):
     """The GPU decoder on the same kind of random chunks (real LZ4 matches,
     all block sizes, raw tails), 40 chunks in one call."""
