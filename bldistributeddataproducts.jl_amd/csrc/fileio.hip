@@ -1,0 +1,306 @@
+// fileio.hip — native reader for chunked FBH5 windows: the stored chunks of
+// the window's chunk box are read with parallel preads into the caller's
+// pinned host buffer, copied to the device in batches and decoded there.
+//
+// The reference reads the window with h5["data"][idxs...]
+// (src/gbtworkerfunctions.jl:181-187): libhdf5 reads each chunk, H5Zbitshuffle
+// (Project.toml:10) decompresses it on the host, libhdf5 assembles the
+// hyperslab.  Here only compressed bytes cross PCIe and the decode runs on the
+// GPU; the window is then a view of, or a gather from, the decoded chunk grid
+// (fbh5.py).  Everything up to the GPU queue is native C++ threads, so the
+// reads never wait on the Python interpreter lock:
+//   * a persistent pool of reader threads pulls pread pieces in batch order
+//     (adjacent chunks merged into runs, runs cut into pieces);
+//   * the calling thread waits for each batch's pieces, queues its H2D copy on
+//     `copy_stream`, makes `stream` wait for it and queues the batch's decode
+//     (bldp_bslz4_decode_dev_async) or raw-chunk copies on `stream`.
+// Batch b+1 is being read while batch b is copied and decoded.
+#include <errno.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <cstdlib>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "bldp_impl.h"
+
+namespace {
+
+struct Piece {
+  int64_t foff, hoff, len;
+  int32_t batch;
+};
+
+// One call's reads.  `left[b]` counts the pieces of batch b still unread.
+struct Job {
+  int fd = -1;
+  uint8_t *host = nullptr;
+  std::vector<Piece> pieces;
+  std::unique_ptr<std::atomic<int64_t>[]> left;
+  std::atomic<int64_t> next{0};
+  std::atomic<int> err{0};
+  std::mutex mu;
+  std::condition_variable cv;
+};
+
+class ReadPool {
+ public:
+  explicit ReadPool(int n) {
+    for (int i = 0; i < n; ++i) th_.emplace_back([this] { work(); });
+  }
+  ~ReadPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto &t : th_) t.join();
+  }
+  int threads() const { return (int)th_.size(); }
+  // Publish `j`; its pieces are read by the pool (and by the caller's waits).
+  void post(Job *j) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = j;
+      ++gen_;
+    }
+    cv_.notify_all();
+  }
+  // Withdraw the job and wait until no reader thread still holds it.
+  void retire() {
+    std::unique_lock<std::mutex> lk(mu_);
+    job_ = nullptr;
+    idle_.wait(lk, [&] { return busy_ == 0; });
+  }
+
+ private:
+  void work() {
+    uint64_t seen = 0;
+    for (;;) {
+      Job *j;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || (job_ && gen_ != seen); });
+        if (stop_) return;
+        seen = gen_;
+        j = job_;
+        ++busy_;
+      }
+      run(j);
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        --busy_;
+      }
+      idle_.notify_all();
+    }
+  }
+
+ public:
+  static void run(Job *j) {
+    const int64_t n = (int64_t)j->pieces.size();
+    for (;;) {
+      const int64_t i = j->next.fetch_add(1);
+      if (i >= n) return;
+      const Piece &p = j->pieces[i];
+      int64_t got = 0;
+      while (got < p.len && !j->err.load(std::memory_order_relaxed)) {
+        const ssize_t r = pread(j->fd, j->host + p.hoff + got, (size_t)(p.len - got), p.foff + got);
+        if (r < 0 && errno == EINTR) continue;
+        if (r <= 0) {
+          int expect = 0;
+          j->err.compare_exchange_strong(expect, r < 0 ? errno : EIO);
+          break;
+        }
+        got += r;
+      }
+      if (j->left[p.batch].fetch_sub(1) == 1 || j->err.load()) {
+        std::lock_guard<std::mutex> lk(j->mu);
+        j->cv.notify_all();
+      }
+    }
+  }
+
+ private:
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_, idle_;
+  Job *job_ = nullptr;
+  uint64_t gen_ = 0;
+  int busy_ = 0;
+  bool stop_ = false;
+};
+
+// One pool for the process (lazily created; BLDP_READ_THREADS or 16 threads),
+// one call at a time on it.
+std::mutex g_pool_mu, g_call_mu;
+std::unique_ptr<ReadPool> g_pool;
+
+ReadPool *pool() {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  if (!g_pool) {
+    int n = 0;
+    if (const char *e = getenv("BLDP_READ_THREADS")) n = atoi(e);
+    if (n <= 0) n = std::min(16, std::max(2, (int)std::thread::hardware_concurrency()));
+    g_pool.reset(new ReadPool(n));
+  }
+  return g_pool.get();
+}
+
+double ms_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+}  // namespace
+
+extern "C" BLDP_API int bldp_chunks_to_device(
+    int fd, int64_t nchunk, const int64_t *file_off, const int64_t *stored_len,
+    const int64_t *stage_off, const uint32_t *filter_mask, int64_t nbatch, const int64_t *batch_end,
+    void *host_pinned, void *dev_stage, void *dev_out, int64_t out_chunk_bytes, int *err_dev,
+    void *copy_stream, void *stream, double *stats) {
+  const auto t0 = std::chrono::steady_clock::now();
+  if (nchunk < 0 || nbatch < 0 || (nchunk && (!file_off || !stored_len || !stage_off ||
+                                               !filter_mask || !batch_end || !host_pinned ||
+                                               !dev_stage || nbatch < 1)))
+    return bldp::set_error(BLDP_EINVAL, "chunks_to_device: bad argument");
+  if (nchunk == 0) return BLDP_OK;
+  if (batch_end[nbatch - 1] != nchunk)
+    return bldp::set_error(BLDP_EINVAL, "chunks_to_device: batches must end at chunk %lld",
+                           (long long)nchunk);
+  bool any_comp = false;
+  for (int64_t k = 0; k < nchunk; ++k) {
+    if (stored_len[k] < 0 || stage_off[k] < 0 || file_off[k] < 0)
+      return bldp::set_error(BLDP_EINVAL, "chunks_to_device: negative offset or size");
+    if (stored_len[k] && (filter_mask[k] & 1) && dev_out && stored_len[k] != out_chunk_bytes)
+      return bldp::set_error(BLDP_EINVAL,
+                             "chunks_to_device: unfiltered chunk %lld holds %lld bytes, not %lld",
+                             (long long)k, (long long)stored_len[k], (long long)out_chunk_bytes);
+    any_comp = any_comp || (stored_len[k] && !(filter_mask[k] & 1));
+  }
+  if (any_comp && (!dev_out || !err_dev))
+    return bldp::set_error(BLDP_EINVAL, "chunks_to_device: compressed chunks need an output");
+
+  // pieces: per batch, chunks adjacent in the file and in the staging buffer
+  // merge into runs; a batch of <= 32 MiB is cut into ~16 pieces (the whole
+  // pool reads it), larger ones into ~8
+  Job j;
+  j.fd = fd;
+  j.host = (uint8_t *)host_pinned;
+  j.left.reset(new std::atomic<int64_t>[nbatch]);
+  std::vector<std::pair<int64_t, int64_t>> brange(nbatch);  // staged byte range of a batch
+  int64_t k0 = 0;
+  for (int64_t b = 0; b < nbatch; ++b) {
+    const int64_t k1 = batch_end[b];
+    if (k1 < k0 || k1 > nchunk)
+      return bldp::set_error(BLDP_EINVAL, "chunks_to_device: batch ends out of order");
+    int64_t lo = INT64_MAX, hi = 0, bytes = 0;
+    for (int64_t k = k0; k < k1; ++k)
+      if (stored_len[k]) {
+        lo = std::min(lo, stage_off[k]);
+        hi = std::max(hi, stage_off[k] + stored_len[k]);
+        bytes += stored_len[k];
+      }
+    brange[b] = {lo == INT64_MAX ? 0 : lo, hi};
+    const int64_t piece =
+        std::max<int64_t>(256 << 10, bytes <= (32ll << 20) ? bytes / 16 : bytes / 8);
+    const size_t first = j.pieces.size();
+    for (int64_t k = k0; k < k1;) {
+      if (!stored_len[k]) {
+        ++k;
+        continue;
+      }
+      int64_t f = file_off[k], h = stage_off[k], n = stored_len[k];
+      int64_t q = k + 1;
+      while (q < k1 && stored_len[q] && file_off[q] == f + n && stage_off[q] == h + n) {
+        n += stored_len[q];
+        ++q;
+      }
+      for (int64_t x = 0; x < n; x += piece)
+        j.pieces.push_back({f + x, h + x, std::min(piece, n - x), (int32_t)b});
+      k = q;
+    }
+    j.left[b].store((int64_t)(j.pieces.size() - first));
+    k0 = k1;
+  }
+
+  std::lock_guard<std::mutex> call(g_call_mu);
+  ReadPool *rp = pool();
+  rp->post(&j);
+  hipStream_t cs = (hipStream_t)copy_stream, s = (hipStream_t)stream;
+  int rc = BLDP_OK;
+  double t_first = -1.0;
+  std::vector<hipEvent_t> evs;
+  std::vector<uint64_t> offs, lens, ooff, olen;
+  k0 = 0;
+  for (int64_t b = 0; b < nbatch && rc == BLDP_OK; ++b) {
+    const int64_t k1 = batch_end[b];
+    {  // this batch's reads
+      std::unique_lock<std::mutex> lk(j.mu);
+      j.cv.wait(lk, [&] { return j.left[b].load() == 0 || j.err.load(); });
+    }
+    if (int e = j.err.load()) {
+      rc = bldp::set_error(BLDP_EINVAL, "chunks_to_device: pread failed: %s", strerror(e));
+      break;
+    }
+    const int64_t lo = brange[b].first, hi = brange[b].second;
+    if (hi > lo) {
+      hipEvent_t ev;
+      if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+        rc = bldp::set_error(BLDP_EHIP, "chunks_to_device: event create failed");
+        break;
+      }
+      evs.push_back(ev);
+      if (hipMemcpyAsync((uint8_t *)dev_stage + lo, (uint8_t *)host_pinned + lo, (size_t)(hi - lo),
+                         hipMemcpyHostToDevice, cs) != hipSuccess ||
+          hipEventRecord(ev, cs) != hipSuccess || hipStreamWaitEvent(s, ev, 0) != hipSuccess) {
+        rc = bldp::set_error(BLDP_EHIP, "chunks_to_device: H2D copy of batch %lld failed",
+                             (long long)b);
+        break;
+      }
+      if (t_first < 0) t_first = ms_since(t0);
+    }
+    offs.clear();
+    lens.clear();
+    ooff.clear();
+    olen.clear();
+    for (int64_t k = k0; k < k1 && rc == BLDP_OK; ++k) {
+      if (!stored_len[k]) continue;
+      if (filter_mask[k] & 1) {  // stored without the filter: raw elements
+        if (dev_out && hipMemcpyAsync((uint8_t *)dev_out + k * out_chunk_bytes,
+                                      (uint8_t *)dev_stage + stage_off[k],
+                                      (size_t)out_chunk_bytes, hipMemcpyDeviceToDevice,
+                                      s) != hipSuccess)
+          rc = bldp::set_error(BLDP_EHIP, "chunks_to_device: raw chunk copy failed");
+        continue;
+      }
+      offs.push_back((uint64_t)stage_off[k]);
+      lens.push_back((uint64_t)stored_len[k]);
+      ooff.push_back((uint64_t)(k * out_chunk_bytes));
+      olen.push_back((uint64_t)out_chunk_bytes);
+    }
+    if (rc == BLDP_OK && !offs.empty())
+      rc = bldp_bslz4_decode_dev_async((int)offs.size(), (const uint8_t *)host_pinned,
+                                       (const uint8_t *)dev_stage, offs.data(), lens.data(), 4,
+                                       (uint8_t *)dev_out, ooff.data(), olen.data(), err_dev, s);
+    k0 = k1;
+  }
+  const double t_reads = ms_since(t0);
+  if (rc != BLDP_OK) {  // let the readers finish before the buffers go away
+    j.err.store(j.err.load() ? j.err.load() : ECANCELED);
+    ReadPool::run(&j);
+  }
+  rp->retire();
+  for (hipEvent_t ev : evs) (void)hipEventDestroy(ev);
+  if (stats) {
+    stats[0] = t_first;
+    stats[1] = t_reads;
+    stats[2] = (double)j.pieces.size();
+    stats[3] = (double)rp->threads();
+  }
+  return rc;
+}

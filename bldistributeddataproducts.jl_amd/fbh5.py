@@ -27,6 +27,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import threading
 
 import numpy as np
 
@@ -912,36 +913,79 @@ def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 
                     len(sizes) * cvol, dtype=torch.float32, device=dev)
             # the H2D copies (the critical path) on a cached high-priority stream
             copy_streams = [_copy_stream(dev, -1)]
+            if tab is not None and os.environ.get("BLDP_NATIVE_READ", "1") != "0":
+                # parsed chunk index: reads, copies and decodes queued natively
+                # (bldp_chunks_to_device: C++ reader threads, no interpreter lock)
+                t_setup = time.perf_counter() - t0
+                if raw_chunks:  # no filter: stored chunks are raw elements
+                    masks[:] = 1
+                stats = _native_chunks(fname, faddr, sizes, offsets, masks, batches, pinned, cdev,
+                                       None if dense_raw else packed, cvol, copy_streams[0],
+                                       _lib, torch)
+                if timings is not None:
+                    timings.update(chunk_index_s=t_tab, pinned_alloc_s=t_pin, setup_s=t_setup,
+                                   native_first_copy_s=stats[0] / 1e3,
+                                   native_queued_s=stats[1] / 1e3, pieces=int(stats[2]),
+                                   reader_threads=int(stats[3]),
+                                   before_unchunk_s=time.perf_counter() - t0)
+                return _window_out(dense, dev, torch, engine, _lib, nc, ni, nt, chunk, box0, grid,
+                                   win, packed, timings, t0, 0.0, stats[1] / 1e3, batches, total,
+                                   True)
             hostmv = memoryview(host)
             fd = os.open(fname, os.O_RDONLY) if tab is not None else None
             pool = filestream._ring(dev).pool
 
-            def read_task(task):
+            # BLDP_TRACE_READ=1: host timeline of the first batch's preads too
+            tr_host = [] if timings is not None and os.environ.get("BLDP_TRACE_READ") else None
+
+            def read_task(task, b=-1):
+                ts = time.perf_counter()
                 for fo, do, n in task:
                     filestream._pread_into(fd, hostmv[do:do + n], fo)
+                if tr_host is not None and b == 0:
+                    tr_host.append((round(1e3 * (ts - t0), 3),
+                                    round(1e3 * (time.perf_counter() - t0), 3)))
 
             # BLDP_TRACE_READ=1: GPU-event timeline of the copies (timings["trace"])
             trace = [] if timings is not None and os.environ.get("BLDP_TRACE_READ") else None
-            # every batch's preads go to the pool at once, in batch order, so the
-            # pool never idles between batches; the reader thread below only
-            # waits for a batch's reads and queues its H2D copy.  A batch is cut
-            # into >= 16 pieces (<= PIECE_BYTES each) so that the small first
-            # batches are read by the whole pool
+            # every batch's preads go to the pool, in batch order, so the pool
+            # never idles between batches; the reader thread below only waits
+            # for a batch's reads and queues its H2D copy.  The first batch is
+            # submitted here and the rest by a pool task, so its copy can start
+            # while the later batches are still being queued.  Batches up to
+            # 32 MiB are cut into 16 pieces (the whole pool reads them), larger
+            # ones into pieces of 1/8 (fewer submissions)
             t_sub = time.perf_counter()
             t_setup = t_sub - t0
-            pending = None
+            pending = rest = None
             if tab is not None:
-                pending = []
-                for k0, k1 in batches:
+                pending = [None] * len(batches)
+                queued = [threading.Event() for _ in batches]
+
+                def submit(b):
+                    k0, k1 = batches[b]
                     bb = int(offsets[k1 - 1] + sizes[k1 - 1] - offsets[k0])
-                    piece = max(256 << 10, min(filestream.PIECE_BYTES, bb // 16))
-                    pending.append([pool.submit(read_task, t) for t in
-                                    _read_tasks(faddr, sizes, offsets, k0, k1, piece)])
+                    piece = max(256 << 10, bb // 16 if bb <= (32 << 20) else bb // 8)
+                    pending[b] = [pool.submit(read_task, t, b) for t in
+                                  _read_tasks(faddr, sizes, offsets, k0, k1, piece)]
+                    queued[b].set()
+
+                def submit_rest():
+                    for b in range(1, len(batches)):
+                        submit(b)
+
+                submit(0)
+                rest = pool.submit(submit_rest) if len(batches) > 1 else None
             t_sub = time.perf_counter() - t_sub
 
             def stage(b):  # reader thread: (reads landed) -> (async) device
                 k0, k1 = batches[b]
+                if tr_host is not None and b == 0:
+                    tr_host.append(("stage0", round(1e3 * (time.perf_counter() - t0), 3)))
                 if tab is not None:  # parallel preads at the parsed chunk offsets
+                    if not queued[b].wait(60):
+                        rest.result()  # (raises if the submitting task failed)
+                        raise BLDPError(-1, f"{fname}: batch {b} reads were never queued")
                     for fu in pending[b]:
                         fu.result()
                 else:
@@ -975,8 +1019,10 @@ def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 
                     None if dense_raw else packed, cdev, host, _lib, torch)
             finally:
                 if pending is not None:  # (an error above: let the reads finish first)
+                    if rest is not None:
+                        rest.exception()  # every batch has been queued
                     for fl in pending:
-                        for fu in fl:
+                        for fu in fl or ():
                             fu.cancel() or fu.exception()
                 if fd is not None:
                     os.close(fd)
@@ -994,6 +1040,50 @@ def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 
             timings["trace"] = [(b, round(1e3 * tq, 3), round(first.elapsed_time(e0), 3),
                                  round(first.elapsed_time(e1), 3), nb)
                                 for _, b, tq, e0, e1, nb in trace]
+            timings["trace_batch0_host_ms"] = tr_host
+    return _window_out(dense, dev, torch, engine, _lib, nc, ni, nt, chunk, box0, grid, win,
+                       packed, timings, t0, t_io, t_dec, batches, total, tab is not None)
+
+
+def _native_chunks(fname, faddr, sizes, offsets, masks, batches, pinned, cdev, packed, cvol,
+                   copy_stream, _lib, torch):
+    """bldp_chunks_to_device for the chunks of the box, then the decoder's
+    error check (which also waits for the copies: the pinned buffer is free
+    once this returns).  Returns the call's stats (4 doubles)."""
+    import ctypes as ct
+
+    fa = np.ascontiguousarray(faddr, np.int64)
+    sz = np.ascontiguousarray(sizes, np.int64)
+    of = np.ascontiguousarray(offsets, np.int64)
+    mk = np.ascontiguousarray(masks, np.uint32)
+    bend = np.array([k1 for _, k1 in batches], np.int64)
+    err = torch.zeros(1, dtype=torch.int32, device=cdev.device)
+    stats = (ct.c_double * 4)()
+    L = _lib.lib()
+    fd = os.open(fname, os.O_RDONLY)
+    try:
+        rc = L.bldp_chunks_to_device(
+            fd, len(sz), fa.ctypes.data, sz.ctypes.data, of.ctypes.data, mk.ctypes.data,
+            len(bend), bend.ctypes.data, pinned.data_ptr(), cdev.data_ptr(),
+            packed.data_ptr() if packed is not None else None, 4 * cvol, err.data_ptr(),
+            copy_stream.cuda_stream, _lib.stream_ptr(), stats)
+        # (waits for every queued copy and decode, also after a failed call)
+        rc2 = L.bldp_bslz4_error(err.data_ptr(), _lib.stream_ptr())
+    finally:
+        os.close(fd)
+    _lib.check(rc, "bldp_chunks_to_device")
+    _lib.check(rc2, "bslz4 decode")
+    return list(stats)
+
+
+def _window_out(dense, dev, torch, engine, _lib, nc, ni, nt, chunk, box0, grid, win, packed,
+                timings, t0, t_io, t_dec, batches, total, parsed_index):
+    """The window from the decoded chunk grid: with ``dense`` a gathered
+    Julia-order tensor; otherwise (chunk grid, window inside it) when the box
+    is one chunk wide in IF and channel, else (gathered tensor, None)."""
+    import time
+
+    gt, gi, gc = grid
     if not dense and gi == 1 and gc == 1 and nc * ni * nt > 0:
         # the packed grid [gt*ct][ci][cc] as a Julia-order array, and the
         # window relative to it
@@ -1006,10 +1096,10 @@ def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 
                 torch.cuda.synchronize()
             timings.update(total_s=time.perf_counter() - t0, wait_io_s=t_io, decode_s=t_dec,
                            batches=len(batches), compressed_bytes=total,
-                           parsed_chunk_index=tab is not None, gather="window of the chunk grid")
+                           parsed_chunk_index=parsed_index, gather="window of the chunk grid")
         return grid_t, rwin
     out = _unchunk_out(dev, torch, engine, _lib, nc, ni, nt, chunk, box0, grid, win, packed,
-                       timings, t0, t_io, t_dec, batches, total, tab is not None)
+                       timings, t0, t_io, t_dec, batches, total, parsed_index)
     return out if dense else (out, None)
 
 

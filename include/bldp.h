@@ -235,6 +235,30 @@ BLDP_API int bldp_bslz4_decode_dev_async(int nchunk, const uint8_t *comp_host,
                                          const uint64_t *out_len, int *err_dev, void *stream);
 BLDP_API int bldp_bslz4_error(const int *err_dev, void *stream);
 
+/* The stored chunks of a chunked FBH5 window, file -> device, natively (the
+ * chunk reads and filter 32008 of h5["data"][idxs...],
+ * src/gbtworkerfunctions.jl:181-187).  Chunk k (stored_len[k] bytes at
+ * file_off[k] of the open file `fd`; 0 bytes = never written) is read with
+ * parallel preads (a persistent pool of reader threads, BLDP_READ_THREADS)
+ * into host_pinned + stage_off[k].  Chunks [batch_end[b-1], batch_end[b]) form
+ * batch b: once its reads land, its staged byte range is copied to dev_stage
+ * (same offsets) on copy_stream, `stream` waits for that copy, and the batch's
+ * chunks are decoded on `stream` into dev_out + k * out_chunk_bytes
+ * (bitshuffle + LZ4, bldp_bslz4_decode_dev_async with err_dev; filter_mask
+ * bit 0 set = stored without the filter: copied raw; dev_out may be NULL when
+ * every chunk is raw: the staged bytes are the output).  Batch b + 1 is read
+ * while batch b is copied and decoded.  Returns once every read has landed
+ * and every copy and decode is queued; bldp_bslz4_error(err_dev, stream)
+ * then synchronizes and reports corrupt blocks.  stats (NULL or 4 doubles):
+ * ms to the first queued copy, ms to the last queued work, pread pieces,
+ * reader threads. */
+BLDP_API int bldp_chunks_to_device(int fd, int64_t nchunk, const int64_t *file_off,
+                                   const int64_t *stored_len, const int64_t *stage_off,
+                                   const uint32_t *filter_mask, int64_t nbatch,
+                                   const int64_t *batch_end, void *host_pinned, void *dev_stage,
+                                   void *dev_out, int64_t out_chunk_bytes, int *err_dev,
+                                   void *copy_stream, void *stream, double *stats);
+
 /* Gather a window (Julia order, dense (nc, ni, nt) out) from decoded chunks:
  * packed holds the chunks of a chunk-aligned bounding box back to back in
  * chunk-grid order [gt][gi][gc], each chunk C-order [ct][ci][cc].

@@ -341,3 +341,29 @@ def test_bslz4_slot_size_checked_before_launch(pkg, L):
         assert rc == pkg._lib.BLDP_EINVAL
     assert L.bldp_bslz4_decode_dev(1, h.ctypes.data, fake, off.ctypes.data, n.ctypes.data, 4,
                                    fake, off.ctypes.data, None, None) == pkg._lib.BLDP_EINVAL
+
+
+def test_chunks_to_device_validates_before_any_read(pkg, L):
+    """bldp_chunks_to_device (the native chunk reader) checks its tables on the
+    host before it reads or touches a device: batches that do not end at the
+    last chunk, negative sizes, an unfiltered chunk of the wrong size,
+    compressed chunks without an output."""
+    fake = 1 << 20  # never dereferenced: every check precedes the reads
+    fa = np.array([0, 100], np.int64)
+    sz = np.array([100, 100], np.int64)
+    of = np.array([0, 100], np.int64)
+    mk = np.zeros(2, np.uint32)
+
+    def call(fa=fa, sz=sz, of=of, mk=mk, bend=(2,), out=fake, ocb=400):
+        be = np.array(bend, np.int64)
+        return L.bldp_chunks_to_device(-1, len(sz), fa.ctypes.data, sz.ctypes.data,
+                                       of.ctypes.data, mk.ctypes.data, len(be), be.ctypes.data,
+                                       fake, fake, out, ocb, fake, None, None, None)
+
+    assert call(bend=(1,)) == pkg._lib.BLDP_EINVAL and "end at chunk" in pkg._lib.last_error()
+    assert call(bend=(2, 1)) == pkg._lib.BLDP_EINVAL
+    assert call(sz=np.array([100, -1], np.int64)) == pkg._lib.BLDP_EINVAL
+    assert call(mk=np.ones(2, np.uint32)) == pkg._lib.BLDP_EINVAL  # raw chunk of 100 B, slot 400
+    assert call(out=None) == pkg._lib.BLDP_EINVAL and "output" in pkg._lib.last_error()
+    assert L.bldp_chunks_to_device(-1, 0, None, None, None, None, 0, None, None, None, None, 0,
+                                   None, None, None, None) == 0  # nothing to do

@@ -66,27 +66,42 @@ def main():
     res["pipeline_total_ms"] = round(1e3 * sorted(ts)[2], 2)
     res["pipeline_copy_span_ms"] = round(tr[-1][3] - tr[0][2], 3) if tr else None
     # batch schedule x gather sweep (device read total, ms, median of 7, interleaved)
-    sweep = [(64, 16, False, True), (64, 16, True, True), (64, 16, True, False),
-             (64, 8, True, False), (64, 4, True, False), (128, 16, True, False),
-             (32, 8, True, False)]
+    # (native: bldp_chunks_to_device; python: the reader pool in fbh5.py)
+    sweep = [(64, 16, False, True, "python"), (64, 16, True, False, "python"),
+             (64, 16, True, False, "native"), (64, 8, True, False, "native"),
+             (32, 8, True, False, "native"), (128, 16, True, False, "native"),
+             (64, 16, True, True, "native")]
     tsw = {k: [] for k in sweep}
+    stages = {}
     for _ in range(7):
-        for bb, fbb, ramp, dense in sweep:
+        for key in sweep:
+            bb, fbb, ramp, dense, impl = key
+            os.environ["BLDP_NATIVE_READ"] = "1" if impl == "native" else "0"
             tm = {}
             x = fb._read_window_bslz4_dev(path, (C, C, C), "cuda:0", timings=tm,
                                           batch_bytes=bb << 20, first_batch_bytes=fbb << 20,
                                           ramp=ramp, dense=dense)
             del x
-            tsw[(bb, fbb, ramp, dense)].append(tm["total_s"])
-    for (bb, fbb, ramp, dense), ts in tsw.items():
-        res[f"batch_{bb}MiB_first_{fbb}MiB_{'ramp' if ramp else 'flat'}_"
+            tsw[key].append(tm["total_s"])
+            stages[key] = tm
+    os.environ.pop("BLDP_NATIVE_READ")
+    for key, ts in tsw.items():
+        bb, fbb, ramp, dense, impl = key
+        res[f"{impl}_batch_{bb}MiB_first_{fbb}MiB_{'ramp' if ramp else 'flat'}_"
             f"{'gather' if dense else 'view'}_total_ms"] = round(1e3 * sorted(ts)[3], 2)
+    res["native_stages_ms"] = {k: (round(v * 1e3, 3) if isinstance(v, float) else v)
+                               for k, v in stages[(64, 16, True, False, "native")].items()}
     os.environ["BLDP_TRACE_READ"] = "1"
+    os.environ["BLDP_NATIVE_READ"] = "0"  # (the trace is the python reader's)
     tm = {}
     x = fb._read_window_bslz4_dev(path, (C, C, C), "cuda:0", timings=tm, dense=False)
     del x
     os.environ.pop("BLDP_TRACE_READ")
+    os.environ.pop("BLDP_NATIVE_READ")
     res["trace_ramp_view"] = tm.get("trace")
+    res["trace_batch0_host_ms (task start, end; stage0 start)"] = tm.get("trace_batch0_host_ms")
+    res["trace_stages_ms"] = {k: (round(v * 1e3, 3) if isinstance(v, float) else v)
+                              for k, v in tm.items() if not k.startswith("trace")}
     # ceilings
     H = fb.h5().L
     f = H.H5Fopen(path.encode(), 0, 0)
