@@ -38,15 +38,21 @@ struct Piece {
 };
 
 // One call's reads.  `left[b]` counts the pieces of batch b still unread.
+// Pieces land at host + hoff, or, with a slot ring, in slot (batch % nslot)
+// at hoff - batch * slot_bytes; then only batches below `open` may be read
+// (their slot's previous copy is done).
 struct Job {
   int fd = -1;
   uint8_t *host = nullptr;
+  const std::vector<void *> *slot_base = nullptr;
+  int64_t slot_bytes = 0;
   std::vector<Piece> pieces;
   std::unique_ptr<std::atomic<int64_t>[]> left;
   std::atomic<int64_t> next{0};
+  std::atomic<int64_t> open{INT64_MAX};
   std::atomic<int> err{0};
   std::mutex mu;
-  std::condition_variable cv;
+  std::condition_variable cv, gate;
 };
 
 class ReadPool {
@@ -108,9 +114,18 @@ class ReadPool {
       const int64_t i = j->next.fetch_add(1);
       if (i >= n) return;
       const Piece &p = j->pieces[i];
+      uint8_t *dst = j->host + p.hoff;
+      if (j->slot_base) {
+        if (p.batch >= j->open.load()) {  // wait for the slot
+          std::unique_lock<std::mutex> lk(j->mu);
+          j->gate.wait(lk, [&] { return p.batch < j->open.load() || j->err.load(); });
+        }
+        const std::vector<void *> &sl = *j->slot_base;
+        dst = (uint8_t *)sl[p.batch % sl.size()] + (p.hoff - p.batch * j->slot_bytes);
+      }
       int64_t got = 0;
       while (got < p.len && !j->err.load(std::memory_order_relaxed)) {
-        const ssize_t r = pread(j->fd, j->host + p.hoff + got, (size_t)(p.len - got), p.foff + got);
+        const ssize_t r = pread(j->fd, dst + got, (size_t)(p.len - got), p.foff + got);
         if (r < 0 && errno == EINTR) continue;
         if (r <= 0) {
           int expect = 0;
@@ -296,6 +311,151 @@ extern "C" BLDP_API int bldp_chunks_to_device(
   }
   rp->retire();
   for (hipEvent_t ev : evs) (void)hipEventDestroy(ev);
+  if (stats) {
+    stats[0] = t_first;
+    stats[1] = t_reads;
+    stats[2] = (double)j.pieces.size();
+    stats[3] = (double)rp->threads();
+  }
+  return rc;
+}
+
+// ---------------------------------------------------------------------------
+// Raw runs (uncompressed contiguous FBH5 `data`, SIGPROC data blocks) into a
+// dense device block through a ring of library-owned pinned slots.
+namespace {
+
+// nslot pinned host slots of slot_bytes, reused across calls (one call at a
+// time, under g_call_mu).
+struct Slots {
+  int64_t bytes = 0;
+  std::vector<void *> p;
+};
+Slots g_slots;
+
+int ensure_slots(int64_t bytes, int nslot) {
+  if (g_slots.bytes == bytes && (int)g_slots.p.size() == nslot) return BLDP_OK;
+  for (void *q : g_slots.p) (void)hipHostFree(q);
+  g_slots.p.clear();
+  g_slots.bytes = 0;
+  for (int i = 0; i < nslot; ++i) {
+    void *q = nullptr;
+    if (hipHostMalloc(&q, (size_t)bytes, hipHostMallocDefault) != hipSuccess) {
+      for (void *r : g_slots.p) (void)hipHostFree(r);
+      g_slots.p.clear();
+      return bldp::set_error(BLDP_ENOMEM, "runs_to_device: %lld bytes of pinned slots",
+                             (long long)bytes);
+    }
+    g_slots.p.push_back(q);
+  }
+  g_slots.bytes = bytes;
+  return BLDP_OK;
+}
+
+}  // namespace
+
+extern "C" BLDP_API int bldp_runs_to_device(int fd, int64_t nrun, const int64_t *file_off,
+                                            const int64_t *len, void *dev_dst, int64_t slot_bytes,
+                                            int nslot, void *copy_stream, void *stream,
+                                            double *stats) {
+  const auto t0 = std::chrono::steady_clock::now();
+  if (nrun < 0 || (nrun && (!file_off || !len || !dev_dst)) || slot_bytes < (1 << 20) ||
+      nslot < 2 || nslot > 16)
+    return bldp::set_error(BLDP_EINVAL, "runs_to_device: bad argument");
+  int64_t total = 0;
+  for (int64_t r = 0; r < nrun; ++r) {
+    if (len[r] < 0 || file_off[r] < 0)
+      return bldp::set_error(BLDP_EINVAL, "runs_to_device: negative offset or size");
+    total += len[r];
+  }
+  if (total == 0) return BLDP_OK;
+  const int64_t nbatch = (total + slot_bytes - 1) / slot_bytes;
+  // pieces: runs cut at batch (slot) boundaries and into ~8 pieces per slot;
+  // piece.hoff is the offset in the whole block (the slot is batch % nslot)
+  const int64_t piece = std::max<int64_t>(256 << 10, slot_bytes / 8);
+  Job j;
+  j.fd = fd;
+  j.left.reset(new std::atomic<int64_t>[nbatch]);
+  for (int64_t b = 0; b < nbatch; ++b) j.left[b].store(0);
+  int64_t pos = 0;
+  for (int64_t r = 0; r < nrun; ++r) {
+    int64_t x = 0;
+    while (x < len[r]) {
+      const int64_t b = (pos + x) / slot_bytes;
+      const int64_t n = std::min({piece, len[r] - x, (b + 1) * slot_bytes - (pos + x)});
+      j.pieces.push_back({file_off[r] + x, pos + x, n, (int32_t)b});
+      j.left[b].fetch_add(1);
+      x += n;
+    }
+    pos += len[r];
+  }
+  std::lock_guard<std::mutex> call(g_call_mu);
+  int rc = ensure_slots(slot_bytes, nslot);
+  if (rc) return rc;
+  // reads of batch b go to slot b % nslot at (hoff - b * slot_bytes); a batch
+  // may be read once the copy out of its slot two rounds back is done
+  j.slot_base = &g_slots.p;
+  j.slot_bytes = slot_bytes;
+  j.open.store(std::min<int64_t>(nbatch, nslot));
+  ReadPool *rp = pool();
+  rp->post(&j);
+  hipStream_t cs = (hipStream_t)copy_stream, s = (hipStream_t)stream;
+  std::vector<hipEvent_t> evs(nbatch, nullptr);
+  double t_first = -1.0;
+  for (int64_t b = 0; b < nbatch && rc == BLDP_OK; ++b) {
+    {
+      std::unique_lock<std::mutex> lk(j.mu);
+      j.cv.wait(lk, [&] { return j.left[b].load() == 0 || j.err.load(); });
+    }
+    if (int e = j.err.load()) {
+      rc = bldp::set_error(BLDP_EINVAL, "runs_to_device: pread failed: %s", strerror(e));
+      break;
+    }
+    const int64_t lo = b * slot_bytes, n = std::min(slot_bytes, total - lo);
+    if (hipEventCreateWithFlags(&evs[b], hipEventDisableTiming) != hipSuccess ||
+        hipMemcpyAsync((uint8_t *)dev_dst + lo, g_slots.p[b % nslot], (size_t)n,
+                       hipMemcpyHostToDevice, cs) != hipSuccess ||
+        hipEventRecord(evs[b], cs) != hipSuccess) {
+      rc = bldp::set_error(BLDP_EHIP, "runs_to_device: H2D copy of batch %lld failed",
+                           (long long)b);
+      break;
+    }
+    if (t_first < 0) t_first = ms_since(t0);
+    if (b >= 1) {  // the slot of batch b - 1 is free once its copy is done
+      if (hipEventSynchronize(evs[b - 1]) != hipSuccess) {
+        rc = bldp::set_error(BLDP_EHIP, "runs_to_device: copy of batch %lld failed",
+                             (long long)(b - 1));
+        break;
+      }
+      {
+        std::lock_guard<std::mutex> lk(j.mu);
+        j.open.store(std::min<int64_t>(nbatch, b - 1 + nslot + 1));
+      }
+      j.gate.notify_all();
+    }
+  }
+  const double t_reads = ms_since(t0);
+  if (rc != BLDP_OK) {
+    {
+      std::lock_guard<std::mutex> lk(j.mu);
+      j.err.store(j.err.load() ? j.err.load() : ECANCELED);
+      j.open.store(nbatch);
+    }
+    j.gate.notify_all();
+    ReadPool::run(&j);
+  }
+  rp->retire();
+  // the slots are reused by the next call: every copy out of them is done
+  // before returning; the caller's stream waits for the last one
+  for (int64_t b = 0; b < nbatch; ++b)
+    if (evs[b]) {
+      if (hipEventSynchronize(evs[b]) != hipSuccess && rc == BLDP_OK)
+        rc = bldp::set_error(BLDP_EHIP, "runs_to_device: copy failed");
+    }
+  if (rc == BLDP_OK && evs[nbatch - 1] && hipStreamWaitEvent(s, evs[nbatch - 1], 0) != hipSuccess)
+    rc = bldp::set_error(BLDP_EHIP, "runs_to_device: stream wait failed");
+  for (hipEvent_t ev : evs)
+    if (ev) (void)hipEventDestroy(ev);
   if (stats) {
     stats[0] = t_first;
     stats[1] = t_reads;

@@ -189,6 +189,8 @@ def read_runs_to_device(path, runs, device, timings=None):
     import torch
 
     total = int(runs[:, 1].sum()) if len(runs) else 0
+    if os.environ.get("BLDP_NATIVE_READ", "1") != "0":
+        return _runs_native(path, runs, device, total, timings)
     ring = _ring(device)
     dev = ring.device
     out = torch.empty(total, dtype=torch.uint8, device=dev)
@@ -246,6 +248,49 @@ def read_runs_to_device(path, runs, device, timings=None):
         torch.cuda.synchronize(dev)
         timings.update(total_s=time.perf_counter() - t0, read_s=t_read, bytes=total,
                        batches=len(batches), runs=len(runs), threads=ring.pool._max_workers)
+    return out
+
+
+_native_streams: dict = {}
+
+
+def _runs_native(path, runs, device, total, timings):
+    """read_runs_to_device through bldp_runs_to_device: the library's reader
+    threads and pinned slot ring (no Python thread on the read path)."""
+    import ctypes
+    import time
+
+    import torch
+
+    from . import _lib
+
+    dev = torch.device(device)
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    out = torch.empty(total, dtype=torch.uint8, device=dev)
+    if total == 0:
+        return out
+    cs = _native_streams.get(dev.index)
+    if cs is None:
+        cs = _native_streams[dev.index] = torch.cuda.Stream(dev, priority=-1)
+    r = np.ascontiguousarray(runs, np.int64)
+    fo, ln = np.ascontiguousarray(r[:, 0]), np.ascontiguousarray(r[:, 1])
+    stats = (ctypes.c_double * 4)()
+    t0 = time.perf_counter()
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        with torch.cuda.device(dev):
+            rc = _lib.lib().bldp_runs_to_device(fd, len(ln), fo.ctypes.data, ln.ctypes.data,
+                                                out.data_ptr(), BATCH_BYTES, NSLOTS,
+                                                cs.cuda_stream, _lib.stream_ptr(), stats)
+    finally:
+        os.close(fd)
+    _lib.check(rc, "bldp_runs_to_device")
+    if timings is not None:
+        torch.cuda.synchronize(dev)
+        timings.update(total_s=time.perf_counter() - t0, first_copy_s=stats[0] / 1e3,
+                       reads_s=stats[1] / 1e3, bytes=total, batches=-(-total // BATCH_BYTES),
+                       runs=len(runs), pieces=int(stats[2]), threads=int(stats[3]), native=True)
     return out
 
 

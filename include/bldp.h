@@ -259,6 +259,18 @@ BLDP_API int bldp_chunks_to_device(int fd, int64_t nchunk, const int64_t *file_o
                                    void *dev_out, int64_t out_chunk_bytes, int *err_dev,
                                    void *copy_stream, void *stream, double *stats);
 
+/* Raw byte runs of a file (an uncompressed contiguous FBH5 `data` dataset or
+ * a SIGPROC data block: src/gbtworkerfunctions.jl:171-189) into a dense device
+ * block: run r (len[r] bytes at file_off[r]) lands at dev_dst + the sum of
+ * the earlier runs' lengths.  The block is cut into batches of slot_bytes;
+ * the reader threads pread batch b into library-owned pinned slot b % nslot
+ * once that slot's previous copy is done, and each batch is copied to the
+ * device on copy_stream as soon as its reads land.  Returns after every copy
+ * is done; `stream` waits for the last.  stats as bldp_chunks_to_device. */
+BLDP_API int bldp_runs_to_device(int fd, int64_t nrun, const int64_t *file_off,
+                                 const int64_t *len, void *dev_dst, int64_t slot_bytes,
+                                 int nslot, void *copy_stream, void *stream, double *stats);
+
 /* Gather a window (Julia order, dense (nc, ni, nt) out) from decoded chunks:
  * packed holds the chunks of a chunk-aligned bounding box back to back in
  * chunk-grid order [gt][gi][gc], each chunk C-order [ct][ci][cc].

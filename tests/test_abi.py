@@ -367,3 +367,18 @@ def test_chunks_to_device_validates_before_any_read(pkg, L):
     assert call(out=None) == pkg._lib.BLDP_EINVAL and "output" in pkg._lib.last_error()
     assert L.bldp_chunks_to_device(-1, 0, None, None, None, None, 0, None, None, None, None, 0,
                                    None, None, None, None) == 0  # nothing to do
+
+
+def test_runs_to_device_validates_before_any_read(pkg, L):
+    """bldp_runs_to_device rejects bad tables and slot geometry on the host."""
+    fake = 1 << 20
+    fo = np.array([0, 10], np.int64)
+    ln = np.array([10, -1], np.int64)
+    assert L.bldp_runs_to_device(-1, 2, fo.ctypes.data, ln.ctypes.data, fake, 64 << 20, 4,
+                                 None, None, None) == pkg._lib.BLDP_EINVAL
+    ln = np.array([10, 10], np.int64)
+    assert L.bldp_runs_to_device(-1, 2, fo.ctypes.data, ln.ctypes.data, fake, 1024, 4,
+                                 None, None, None) == pkg._lib.BLDP_EINVAL  # slots < 1 MiB
+    assert L.bldp_runs_to_device(-1, 2, fo.ctypes.data, ln.ctypes.data, fake, 64 << 20, 1,
+                                 None, None, None) == pkg._lib.BLDP_EINVAL  # one slot
+    assert L.bldp_runs_to_device(-1, 0, None, None, None, 64 << 20, 4, None, None, None) == 0

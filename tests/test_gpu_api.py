@@ -328,11 +328,14 @@ def test_bslz4_gpu_rejects_corrupt_blocks(pkg):
     assert "corrupt" in lib.last_error() or "overruns" in lib.last_error()
 
 
-@pytest.mark.parametrize("parsed_index", [True, False])
-def test_fbh5_bslz4_on_gpu_end_to_end(pkg, orc, tmp_path, monkeypatch, parsed_index):
+@pytest.mark.parametrize("parsed_index,native", [(True, True), (True, False), (False, True)])
+def test_fbh5_bslz4_on_gpu_end_to_end(pkg, orc, tmp_path, monkeypatch, parsed_index, native):
     """Compressed FBH5 through the GPU decoder; chunks read by parallel preads
-    at the parsed chunk index, and (parsed_index=False) one H5Dread_chunk at a
-    time, as for files outside the parser's scope."""
+    at the parsed chunk index (the library's reader threads,
+    bldp_chunks_to_device, or with BLDP_NATIVE_READ=0 the Python reader), and
+    (parsed_index=False) one H5Dread_chunk at a time, as for files outside the
+    parser's scope."""
+    monkeypatch.setenv("BLDP_NATIVE_READ", "1" if native else "0")
     J, C = pkg.JRange, pkg.COLON
     d = np.asfortranarray(np.random.default_rng(8).integers(0, 256, (4096, 2, 40))
                           .astype(np.float32))
@@ -423,10 +426,14 @@ def test_pinned_host_buffer(pkg, orc):
         pkg._lib.check(pkg._lib.lib().bldp_host_register(None, 0))
 
 
-def test_raw_files_stream_to_gpu(pkg, orc, tmp_path, monkeypatch):
+@pytest.mark.parametrize("native", [True, False])
+def test_raw_files_stream_to_gpu(pkg, orc, tmp_path, monkeypatch, native):
     """Uncompressed contiguous FBH5 and 32-bit SIGPROC files: getdata and
     getkurtosis read only the window (parallel preads into pinned slots,
-    several batches) and reduce on the GPU; exact on integer data."""
+    several batches: the library's reader threads, bldp_runs_to_device, or the
+    Python reader with BLDP_NATIVE_READ=0) and reduce on the GPU; exact on
+    integer data."""
+    monkeypatch.setenv("BLDP_NATIVE_READ", "1" if native else "0")
     fs = pkg.filestream
     monkeypatch.setattr(fs, "BATCH_BYTES", 1 << 20)
     monkeypatch.setattr(fs, "PIECE_BYTES", 192 << 10)

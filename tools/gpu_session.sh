@@ -55,6 +55,8 @@ for s in $STEPS; do
     file)  run file 600 python bench.py --mode file ;;
     file_probe) run file_probe 600 python tools/file_probe.py ;;
     rawfile) run rawfile 600 python bench.py --mode rawfile ;;
+    rawfile_py) BLDP_NATIVE_READ=0 run rawfile_py 600 python bench.py --mode rawfile ;;
+    file_py) BLDP_NATIVE_READ=0 run file_py 600 python bench.py --mode file ;;
     paths) run paths 300 python tools/probe_paths.py ;;
     paths_big) run paths_big 300 python tools/probe_paths.py --big ;;
     prof_paths) run prof_paths 300 rocprofv3 --kernel-trace --stats --output-format csv \
