@@ -101,6 +101,22 @@ __device__ __forceinline__ void st4(float *p, float4 r) {
   *reinterpret_cast<f4v *>(p) = v;
 #endif
 }
+//   BLDP_NT_SCALAR_STORES  one-float-per-lane output stores with the nt hint
+//                  (written once, never re-read here): 1 (default) = the row and
+//                  interleaved kernels (A/B, profiles/r02/ab_nt_scalar_stores.json:
+//                  c0=2 F=8 +3.9%, c0=3 F=64 +2.7%, cfg3 F=64 +1.8%, cfg2 +1.6%,
+//                  cfg3 F=1024 +0.5%); 2 = every path (the tile path lost up to
+//                  1.9% with it); 0 = none
+#ifndef BLDP_NT_SCALAR_STORES
+#define BLDP_NT_SCALAR_STORES 1
+#endif
+template <int MIN_LEVEL = 2>
+__device__ __forceinline__ void st1(float *p, float v) {
+  if constexpr (BLDP_NT_SCALAR_STORES >= MIN_LEVEL)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
+}
 //   BLDP_NACC      independent float4 accumulators per lane (power of two <= 8)
 #ifndef BLDP_NACC
 #define BLDP_NACC 8
@@ -234,7 +250,7 @@ __device__ __forceinline__ void vec_tile(const RedArgs &a, int64_t tile) {
   }
   if (tsi == 0 && j == 0 && valid) {
     if (a.nchunk == 1) {
-      a.out[c.bank * a.out_bank + c.i * a.out_ld_i + c.to * a.out_ld_t + co] = finish<OP>(s, a);
+      st1(a.out + c.bank * a.out_bank + c.i * a.out_ld_i + c.to * a.out_ld_t + co, finish<OP>(s, a));
     } else {
       a.ws[(((c.chunk * a.nbank + c.bank) * a.nto + c.to) * a.ni + c.i) * a.nco + co] = s;
     }
@@ -452,7 +468,7 @@ __device__ __forceinline__ void lane_tile(const RedArgs &a, int64_t tile) {
 #pragma unroll
   for (int f = 1; f < F; ++f) s = R<OP>::f(s, R<OP>::f(acc[0][f], acc[1][f]));
   if (a.nchunk == 1)
-    a.out[c.bank * a.out_bank + c.i * a.out_ld_i + c.to * a.out_ld_t + co] = finish<OP>(s, a);
+    st1(a.out + c.bank * a.out_bank + c.i * a.out_ld_i + c.to * a.out_ld_t + co, finish<OP>(s, a));
   else
     a.ws[(((c.chunk * a.nbank + c.bank) * a.nto + c.to) * a.ni + c.i) * a.nco + co] = s;
 }
@@ -484,7 +500,7 @@ __device__ __forceinline__ void scalar_tile(const RedArgs &a, int64_t tile) {
   }
   const float s = R<OP>::f(R<OP>::f(acc[0], acc[1]), R<OP>::f(acc[2], acc[3]));
   if (a.nchunk == 1)
-    a.out[c.bank * a.out_bank + c.i * a.out_ld_i + c.to * a.out_ld_t + co] = finish<OP>(s, a);
+    st1(a.out + c.bank * a.out_bank + c.i * a.out_ld_i + c.to * a.out_ld_t + co, finish<OP>(s, a));
   else
     a.ws[(((c.chunk * a.nbank + c.bank) * a.nto + c.to) * a.ni + c.i) * a.nco + co] = s;
 }
@@ -586,7 +602,7 @@ __device__ __forceinline__ void tile_tile(const RedArgs &a, int64_t tile) {
   auto store = [&](int g, float s) {
     const int64_t co = co0 + g;
     if (a.nchunk == 1)
-      a.out[c.bank * a.out_bank + c.i * a.out_ld_i + c.to * a.out_ld_t + co] = finish<OP>(s, a);
+      st1(a.out + c.bank * a.out_bank + c.i * a.out_ld_i + c.to * a.out_ld_t + co, finish<OP>(s, a));
     else
       a.ws[(((c.chunk * a.nbank + c.bank) * a.nto + c.to) * a.ni + c.i) * a.nco + co] = s;
   };
@@ -722,8 +738,8 @@ __global__ __launch_bounds__(kBlock) void k_reduce_il(const RedArgs a) {
 #pragma unroll
       for (int q = 0; q < NS; ++q)
         if ((4 * q * PER + w) / K4 == tid) s = R<OP>::f(s, red[w][q]);
-    a.out[bank * a.out_bank + (int64_t)i * a.out_ld_i + (int64_t)to * a.out_ld_t + g0 + tid] =
-        finish<OP>(s, a);
+    st1<1>(a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + (int64_t)to * a.out_ld_t + g0 + tid,
+           finish<OP>(s, a));
   }
 }
 
@@ -790,8 +806,8 @@ void k_reduce_row(const RedArgs a) {
 #pragma unroll
   for (int off = G4 / 2; off > 0; off >>= 1) s = R<OP>::f(s, __shfl_xor(s, off, 64));
   if (valid && (tid & (G4 - 1)) == 0)
-    a.out[bank * a.out_bank + (int64_t)i * a.out_ld_i + (int64_t)to * a.out_ld_t + col / G4] =
-        finish<OP>(s, a);
+    st1<1>(a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + (int64_t)to * a.out_ld_t + col / G4,
+           finish<OP>(s, a));
 }
 
 template <int OP, int F>
@@ -838,7 +854,7 @@ __device__ __forceinline__ void reduce_store(const RedArgs &a, int64_t e, float 
   r /= a.ni;
   const int64_t to = r % a.nto;
   const int64_t bank = r / a.nto;
-  a.out[bank * a.out_bank + i * a.out_ld_i + to * a.out_ld_t + co] = finish<OP>(s, a);
+  st1(a.out + bank * a.out_bank + i * a.out_ld_i + to * a.out_ld_t + co, finish<OP>(s, a));
 }
 
 template <int OP>

@@ -71,6 +71,8 @@ VARIANTS = {
     "nolane": "-DBLDP_LANE=0",
     "lane2": "-DBLDP_LANE=2",
     # streamed kurtosis leaves through a per-wave LDS ring filled by global_load_lds
+    "nts0": "-DBLDP_NT_SCALAR_STORES=0",
+    "nts2": "-DBLDP_NT_SCALAR_STORES=2",
     "klds8": "-DBLDP_KURT_LEAF_LDS=8",
     "klds16": "-DBLDP_KURT_LEAF_LDS=16",
     "klds8b2": "-DBLDP_KURT_LEAF_LDS=8 -DBLDP_KURT_LEAF_LB=2",
