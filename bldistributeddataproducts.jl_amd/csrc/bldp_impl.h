@@ -25,6 +25,9 @@ struct ScratchLease {
 int scratch_lease(hipStream_t s, size_t bytes, ScratchLease *lease);
 std::vector<int> scratch_devices();  // devices holding scratch
 void scratch_release_all();          // frees it (callers drained the devices)
+// The native file readers (fileio.hip): stop the reader threads and free the
+// pinned slot ring (waits for a read call in progress).
+void fileio_release();
 
 // A host-staging pipeline (runtime.hip): two streams and four cached device
 // buffers (slots 0/1 = input of stream 0/1, 2/3 = output of stream 0/1).

@@ -464,3 +464,14 @@ extern "C" BLDP_API int bldp_runs_to_device(int fd, int64_t nrun, const int64_t 
   }
   return rc;
 }
+
+void bldp::fileio_release() {
+  std::lock_guard<std::mutex> call(g_call_mu);  // no read call in progress
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    g_pool.reset();  // joins the reader threads
+  }
+  for (void *q : g_slots.p) (void)hipHostFree(q);
+  g_slots.p.clear();
+  g_slots.bytes = 0;
+}

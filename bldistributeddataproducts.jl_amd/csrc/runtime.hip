@@ -223,6 +223,7 @@ int bldp_finalize(void) {
   }
   g_dev_stream.clear();
   scratch_release_all();
+  fileio_release();  // the file readers' pinned slots and threads
   if (prev >= 0) (void)hipSetDevice(prev);
   return BLDP_OK;
 }
