@@ -244,6 +244,33 @@ __global__ __launch_bounds__(256) void k_kmix(const f4v *in, int64_t row4, int n
   }
 }
 
+// (3e) the time-integration shape (fqavby = 1, tavby = 16, k_reduce_narrow):
+// one float4 column per lane over nrow rows, then ONE float4 of output per
+// lane (1 byte written per 16 read) as a 1 KiB wave-instruction; 8 rows in
+// flight.  STORE 1 = nt, 2 = plain.
+template <int STORE>
+__global__ __launch_bounds__(256) void k_nmix(const f4v *in, int64_t row4, int nrow,
+                                              int64_t segs_per_bank, f4v *out) {
+  const int64_t bank = blockIdx.x / segs_per_bank, seg = blockIdx.x % segs_per_bank;
+  const f4v *base = in + bank * row4 * nrow + seg * 256 + threadIdx.x;
+  f4v a = f4v{0, 0, 0, 0}, b = a;
+  for (int r = 0; r < nrow; r += 8) {
+    f4v v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(base + (int64_t)(r + u) * row4);
+#pragma unroll
+    for (int u = 0; u < 8; u += 2) {
+      a += v[u];
+      b += v[u + 1];
+    }
+  }
+  f4v *o = out + (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (STORE == 1)
+    __builtin_nontemporal_store(a + b, o);
+  else
+    *o = a + b;
+}
+
 // (3d) tail study: the interleaved cfg3 pattern with G 1024-channel groups
 // per workgroup (4 KiB x G per row, 16 rows), on nbank banks.
 template <int G>
@@ -328,6 +355,38 @@ int main(int argc, char **argv) {
   char name[160];
 
   const bool kmix_only = argc > 4 && std::string(argv[4]) == "kmix";
+  if (argc > 4 && std::string(argv[4]) == "nmix" && gib == 32) {
+    // (3e) read 32 GiB in the cfg3 row pattern + write 2 GiB (F = 1, T = 16)
+    const int nrow = 16;
+    const int64_t row4 = (1ll << 26) / 4, segs = row4 / 256;
+    f4v *wout;
+    CK(hipMalloc(&wout, 2ll << 30));
+    const double mb = (double)bytes + (2ll << 30);
+    report("narrow-shape read 32 GiB + write 2 GiB (1/16), nt stores",
+           timeit([&] { hipLaunchKernelGGL((k_nmix<1>), dim3((unsigned)(segs * 8)), dim3(256), 0, 0,
+                                           in, row4, nrow, segs, wout); }, mb, reps));
+    report("narrow-shape read 32 GiB + write 2 GiB (1/16), plain stores",
+           timeit([&] { hipLaunchKernelGGL((k_nmix<2>), dim3((unsigned)(segs * 8)), dim3(256), 0, 0,
+                                           in, row4, nrow, segs, wout); }, mb, reps));
+    if (argc > 3) {  // the library's narrow path on the same buffer
+      void *h = dlopen(argv[3], RTLD_NOW);
+      typedef int (*band_fn)(int, const float *const *, int64_t, int64_t, int64_t, const int64_t *,
+                             int64_t, int64_t, int, float *, void *);
+      band_fn f = h ? (band_fn)dlsym(h, "bldp_band_reduce_f32") : nullptr;
+      if (f) {
+        const float *banks[8];
+        for (int b = 0; b < 8; ++b) banks[b] = (const float *)in + (int64_t)b * (1ll << 30);
+        report("libbldp band reduce, F=1 T=16 (k_reduce_narrow), same buffer",
+               timeit([&] {
+                 if (f(8, banks, 1ll << 26, 1, 16, nullptr, 1, 16, 0, (float *)wout, nullptr)) exit(2);
+               }, mb, reps));
+      }
+    }
+    CK(hipFree(wout));
+    CK(hipFree(in));
+    CK(hipFree(out));
+    return 0;
+  }
   if (kmix_only) goto kmix;
   // (1) contiguous per workgroup: chunk size x loads in flight x policy
 #define CONTIG(B, POL, CHUNK_KIB, GRID_PER_CU)                                             \
