@@ -419,14 +419,16 @@ __device__ __forceinline__ void narrow_mis_tile(const RedArgs &a, int64_t tile) 
 // dwordx4 + dwordx{1,2,3} (F = 5..7) load, so a wave-instruction streams 64*F*4
 // contiguous bytes with no LDS and no cross-lane work; 8 rows in flight, two
 // accumulator sets.  A/B against the tile path's LDS fold (8 banks x 2^26
-// channels x 16 spectra, profiles/r02/ab_lane.json): F = 3 6.69 vs 6.74 ms,
-// F = 2 (c0 = 1) 6.85 vs 6.92, but F = 5 10.4 vs 6.5 and F = 7 7.8 vs 6.4 (a
-// dwordx4 + dwordx{1,3} pair per lane at a 20- / 28-byte lane pitch splits
-// every wave-instruction into many partial lines).  So:
-//   BLDP_LANE  1 (default) = F = 3 always; F in {2, 5, 6, 7} only where the tile
-//              path cannot run (row pitches that are not multiples of 4 floats;
-//              the alternative is the scalar path); 2 = F in {2, 3, 5, 6, 7}
-//              always; 0 = off
+// channels x 16 spectra, profiles/r02/ab_lane.json, ab_cluster.json): F = 3
+// 6.69 vs 6.74 ms on one box but 5.78 vs 5.57 on another, F = 2 (c0 = 1) 6.85
+// vs 6.92, F = 5 10.4 vs 6.5 and F = 7 7.8 vs 6.4 (a dwordx4 + dwordx{1,3}
+// pair per lane at a 20- / 28-byte lane pitch splits every wave-instruction
+// into many partial lines).  A third form, float4 columns in clusters of F
+// lanes gathered by shuffles, lost to both (F = 3 6.18, F = 7 5.77 ms: its
+// one-float stores are scattered over 4 instructions).  So:
+//   BLDP_LANE  1 (default) = F in {2, 3, 5, 6, 7} only where the tile path
+//              cannot run (row pitches that are not multiples of 4 floats; the
+//              alternative is the scalar path); 2 = always; 0 = off
 #ifndef BLDP_LANE
 #define BLDP_LANE 1
 #endif
@@ -1091,8 +1093,7 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
     a.blocks_c = cdiv(nc4, kBlock);
     tiles = cdiv(nc4, 64) * a.ni * a.nto * a.nbank;
   } else if (words && a.in_cs == 1 && BLDP_LANE >= 1 &&
-             (F == 3 || ((F == 2 || F == 5 || F == 6 || F == 7) &&
-                         (BLDP_LANE >= 2 || !rows16)))) {
+             (F == 2 || F == 3 || F == 5 || F == 6 || F == 7) && (BLDP_LANE >= 2 || !rows16)) {
     // small odd / not-multiple-of-4 groups: one lane per output
     p.path = PATH_LANE;
     a.blocks_c = cdiv(a.nco, kBlock);

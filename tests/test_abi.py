@@ -113,8 +113,9 @@ def test_launch_plans_host_only(pkg, L):
     # cfg4: narrow channel, long time -> time split waves and/or chunks
     p = plan(pkg, L, A, 512, 1, 879616, 8, 1024)
     assert p[0] == 0 and p[1] == 2 and (p[2] > 1 or p[4] > 1)
-    # F=1 time-only: narrow path; F = 3, 5, 6, 7 (any pitch, dword-aligned):
-    # one lane per output; odd pitch with a wide F: scalar
+    # F=1 time-only: narrow path; F = 2, 3, 5, 6, 7 with an odd pitch (the tile
+    # path needs 16-byte pitches): one lane per output; odd pitch with a wide
+    # F: scalar
     assert plan(pkg, L, A, 4096, 1, 16, 1, 16)[0] == 1
     assert plan(pkg, L, A, 4095, 1, 16, 3, 1)[0] == 7
     assert plan(pkg, L, A + 2, 4095, 1, 16, 3, 1)[0] == 2
@@ -128,7 +129,7 @@ def test_launch_plans_host_only(pkg, L):
     assert plan(pkg, L, A, 4096, 1, 16, 1, 1, [1, 4092, 1, 0, 1, 1, 0, 16, 1])[0] == 1
     assert plan(pkg, L, A, 4097, 1, 8, 1024, 8, [0, 4096, 1, 0, 1, 1, 0, 8, 1])[0] == 4
     # tile path: odd F > 7, misaligned channel start with F >= 512, short channel step
-    assert plan(pkg, L, A, 4096, 1, 16, 3, 1, [0, 4095, 1, 0, 1, 1, 0, 16, 1])[0] == 7
+    assert plan(pkg, L, A, 4096, 1, 16, 3, 1, [0, 4095, 1, 0, 1, 1, 0, 16, 1])[0] == 3
     assert plan(pkg, L, A, 4096, 1, 16, 9, 1, [0, 4095, 1, 0, 1, 1, 0, 16, 1])[0] == 3
     assert plan(pkg, L, A, 4096, 1, 16, 1024, 16, [1, 3072, 1, 0, 1, 1, 0, 16, 1])[0] == 3
     # misaligned start, F = 1, a channel count that is not a multiple of 4:

@@ -247,13 +247,11 @@ def misaligned_paths(win, F):
     """Paths a window that starts off a 16-byte boundary takes (16-byte row
     pitches; BLDP_UNALIGNED_VEC=2): unit-step windows with F = 1 or F % 4 == 0,
     F <= 256 read their own float4 columns with dword-aligned 16-byte loads on
-    the vector / narrow paths; F = 3 takes one lane per output group;
+    the vector / narrow paths;
     F = 1 windows whose channel count is not a multiple of 4 take the
     realigning narrow kernel; the rest the tile path."""
     if win[2] != 1:
         return {"tile"}
-    if F == 3:
-        return {"lane"}
     if F == 1:
         return {"narrow"} if win[1] % 4 == 0 else {"narrow_mis"}
     if F % 4 == 0 and F <= 256:
@@ -817,7 +815,9 @@ UNALIGNED_CASES = [
     (4097, 1, 40, [3, 4092, 1, 0, 1, 1, 0, 40, 1], 6, 8, {"lane"}),           # odd pitch
     (4097, 1, 40, [0, 4095, 1, 0, 1, 1, 0, 40, 1], 7, 20, {"lane"}),          # odd pitch
     (4097, 1, 40, [1, 4094, 1, 0, 1, 1, 0, 40, 1], 2, 8, {"lane"}),           # odd pitch
-    (70, 1, 30000, [1, 63, 1, 0, 1, 1, 0, 30000, 1], 3, 30000, {"lane"}),  # time chunks
+    (71, 1, 30000, [1, 63, 1, 0, 1, 1, 0, 30000, 1], 3, 30000, {"lane"}),  # time chunks
+    (4095, 1, 8, [0, 4095, 1, 0, 1, 1, 0, 8, 1], 5, 8, {"lane"}),             # ends at the array end
+    (4096, 2, 8, [4, 4089, 1, 0, 2, 1, 0, 8, 1], 3, 8, {"tile"}),
     (4097, 1, 24, [1, 4095, 1, 0, 1, 1, 0, 24, 1], 4095, 8, {"scalar"}),      # odd pitch, wide F
 ]
 

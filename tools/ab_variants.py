@@ -69,7 +69,7 @@ VARIANTS = {
     "unal3": "-DBLDP_UNALIGNED_VEC=3",
     # small odd F on one lane per output (dwordx3 etc.) vs the tile path's LDS fold
     "nolane": "-DBLDP_LANE=0",
-    "lane2": "-DBLDP_LANE=2",
+    "lane2": "-DBLDP_LANE=2",  # F in {2, 3, 5, 6, 7} on one lane per output everywhere
     # streamed kurtosis leaves through a per-wave LDS ring filled by global_load_lds
     "nts0": "-DBLDP_NT_SCALAR_STORES=0",
     "nts2": "-DBLDP_NT_SCALAR_STORES=2",
