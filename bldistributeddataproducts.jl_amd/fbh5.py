@@ -1169,7 +1169,9 @@ def _unchunk_out(dev, torch, engine, _lib, nc, ni, nt, chunk, box0, grid, win, p
 def write_bslz4_chunks(fname, attrs: dict, jshape, chunk, chunks) -> None:
     """An FBH5 file with filter 32008 whose chunks (C-order chunk grid, each
     already encoded) are written raw with H5Dwrite_chunk.  jshape is Julia's
-    (nchans, nifs, nsamps); chunk is C-order (ct, ci, cc)."""
+    (nchans, nifs, nsamps); chunk is C-order (ct, ci, cc).  An item may also
+    be None (the chunk is never written: it reads as the fill value 0) or
+    (filter_mask, bytes) (mask bit 0 set: stored without the filter)."""
     H5 = h5()
     H = H5.L
     cdims = tuple(jshape)[::-1]
@@ -1189,8 +1191,12 @@ def write_bslz4_chunks(fname, attrs: dict, jshape, chunk, chunks) -> None:
             for t0 in range(0, cdims[0], chunk[0]):
                 for i0 in range(0, cdims[1], chunk[1]):
                     for c0 in range(0, cdims[2], chunk[2]):
-                        enc = next(it)
-                        _ok(H.H5Dwrite_chunk(d, H5P_DEFAULT, 0, _hs([t0, i0, c0]), len(enc),
+                        enc, mask = next(it), 0
+                        if enc is None:
+                            continue
+                        if isinstance(enc, tuple):
+                            mask, enc = enc
+                        _ok(H.H5Dwrite_chunk(d, H5P_DEFAULT, mask, _hs([t0, i0, c0]), len(enc),
                                              enc), "write_chunk")
             for k, v in dict(attrs, DIMENSION_LABELS=["time", "feed_id", "frequency"]).items():
                 _write_attr(H5, d, k, v)

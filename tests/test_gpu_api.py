@@ -614,6 +614,47 @@ def test_getkurtosis_compressed_and_chunked_files(pkg, orc, tmp_path):
                 assert_kurtosis(got, want, path, win[7], (f, idxs))
 
 
+@pytest.mark.parametrize("native", [True, False])
+def test_compressed_file_missing_and_unfiltered_chunks(pkg, orc, tmp_path, monkeypatch, native):
+    """HDF5 chunk states the readers must honour: a chunk never written reads
+    as the fill value 0, a chunk stored with filter mask bit 0 set holds raw
+    elements (the filter was skipped for it), the rest are bitshuffle/LZ4.
+    getdata and getkurtosis through the native and the Python readers against
+    the oracle on the array those states describe (integer data: exact)."""
+    from conftest import assert_kurtosis
+
+    monkeypatch.setenv("BLDP_NATIVE_READ", "1" if native else "0")
+    J, C = pkg.JRange, pkg.COLON
+    rng = np.random.default_rng(5150)
+    nc, ni, nt = 512, 2, 70
+    a = np.asfortranarray(rng.integers(0, 200, (nc, ni, nt)).astype(np.float32))
+    chunk = (8, 1, 512)  # C order (t, i, c): 9 x 2 chunks, the last time block partial
+    c = np.ascontiguousarray(a.transpose(2, 1, 0))  # [t][i][c]
+    items, want = [], a.copy(order="F")
+    for k, t0 in enumerate(range(0, nt, 8)):
+        for i0 in range(ni):
+            blk = np.zeros(chunk, np.float32)
+            part = c[t0:t0 + 8, i0:i0 + 1, :]
+            blk[:part.shape[0]] = part
+            if (k, i0) in ((2, 0), (6, 1)):
+                items.append(None)  # never written
+                want[:, i0, t0:t0 + 8] = 0.0
+            elif (k, i0) in ((4, 1), (8, 0)):
+                items.append((1, blk.tobytes()))  # stored raw, filter skipped
+            else:
+                items.append(orc.np_bslz4_encode(blk, 512, lz4=orc.lz4_compress))
+    p = str(tmp_path / "holes.h5")
+    pkg.fbh5.write_bslz4_chunks(p, dict(foff=-1.0), (nc, ni, nt), chunk, items)
+    for idxs, F, T, op in [((C, C, C), 4, 5, "sum"), ((J(3, 510), 2, J(9, 64)), 4, 8, "max"),
+                           ((C, 1, J(70, -1, 1)), 8, 1, "min")]:
+        win = pkg.idxs.to_window(pkg.sanitizeidxs(idxs), a.shape) or \
+            [0, nc, 1, 0, ni, 1, 0, nt, 1]
+        got = pkg.WorkerFunctions.getdata(p, idxs, fqavby=F, fqavfunc=op, tavby=T)
+        assert same_bits(got, orc.reduce(want, F, T, op, win)), idxs
+    k = pkg.WorkerFunctions.getkurtosis(p, (C, C, C))
+    assert_kurtosis(k, orc.kurtosis(want), "mid", nt)
+
+
 def test_bslz4_gpu_decoder_random_lz4(pkg, orc):
     """The GPU decoder on the same kind of random chunks (real LZ4 matches,
     all block sizes, raw tails), 40 chunks in one call."""

@@ -87,6 +87,7 @@ for s in $STEPS; do
              --steps 10 --warmup 3 --config cfg2 ;;
     unal_check) run unal_check 300 python tools/unaligned_check.py --variant "${UNAL_VARIANT:-unal2}" ;;
     nmix)  run nmix 300 ./build/hbm_ceiling 32 10 bldistributeddataproducts.jl_amd/libbldp_hip.so nmix ;;  # (built here: hipcc -o build/hbm_ceiling tools/hbm_ceiling.hip -ldl)
+    pipeline) run pipeline 600 python bench.py --pipeline --no-cpu-baseline ;;
     ab)    run ab 900 python tools/ab_variants.py --run --variants "${AB_VARIANTS:-base,noil}" --json "$OUT/ab.json" ;;
     ab_kurt) run ab_kurt 900 python tools/ab_variants.py --run --suite kurt --variants ${AB_VARIANTS:-base,kold,kw5,kw6} --json "$OUT/ab_kurt.json" ;;
     ab_tile) run ab_tile 900 python tools/ab_variants.py --run --suite tile --variants "${AB_VARIANTS:-base,tk4a1,tk2a1,tk2a2}" --json "$OUT/ab_tile.json" ;;
