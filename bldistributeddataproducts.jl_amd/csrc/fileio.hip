@@ -23,6 +23,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <cstdlib>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <thread>
@@ -151,20 +152,37 @@ class ReadPool {
   bool stop_ = false;
 };
 
-// One pool for the process (lazily created; BLDP_READ_THREADS or 16 threads),
-// one call at a time on it.
-std::mutex g_pool_mu, g_call_mu;
-std::unique_ptr<ReadPool> g_pool;
+// nslot pinned host slots of `bytes` each (bldp_runs_to_device's ring).
+struct Slots {
+  int64_t bytes = 0;
+  std::vector<void *> p;
+};
 
-ReadPool *pool() {
-  std::lock_guard<std::mutex> lk(g_pool_mu);
-  if (!g_pool) {
+// Per device (the caller's current device): a pool of reader threads
+// (BLDP_READ_THREADS, default 16), the slot ring and the lock that lets one
+// read call at a time use them.  Reads for different GPUs (the GBT fan-out
+// over several GPUs of a node) run side by side.
+struct DevIO {
+  std::mutex call;
+  std::unique_ptr<ReadPool> pool;
+  Slots slots;
+};
+std::mutex g_io_mu;
+std::map<int, std::unique_ptr<DevIO>> g_io;
+
+DevIO *dev_io() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  std::lock_guard<std::mutex> lk(g_io_mu);
+  std::unique_ptr<DevIO> &io = g_io[dev];
+  if (!io) {
     int n = 0;
     if (const char *e = getenv("BLDP_READ_THREADS")) n = atoi(e);
     if (n <= 0) n = std::min(16, std::max(2, (int)std::thread::hardware_concurrency()));
-    g_pool.reset(new ReadPool(n));
+    io.reset(new DevIO);
+    io->pool.reset(new ReadPool(n));
   }
-  return g_pool.get();
+  return io.get();
 }
 
 double ms_since(std::chrono::steady_clock::time_point t0) {
@@ -243,8 +261,9 @@ extern "C" BLDP_API int bldp_chunks_to_device(
     k0 = k1;
   }
 
-  std::lock_guard<std::mutex> call(g_call_mu);
-  ReadPool *rp = pool();
+  DevIO *io = dev_io();
+  std::lock_guard<std::mutex> call(io->call);
+  ReadPool *rp = io->pool.get();
   rp->post(&j);
   hipStream_t cs = (hipStream_t)copy_stream, s = (hipStream_t)stream;
   int rc = BLDP_OK;
@@ -325,30 +344,25 @@ extern "C" BLDP_API int bldp_chunks_to_device(
 // dense device block through a ring of library-owned pinned slots.
 namespace {
 
-// nslot pinned host slots of slot_bytes, reused across calls (one call at a
-// time, under g_call_mu).
-struct Slots {
-  int64_t bytes = 0;
-  std::vector<void *> p;
-};
-Slots g_slots;
-
-int ensure_slots(int64_t bytes, int nslot) {
-  if (g_slots.bytes == bytes && (int)g_slots.p.size() == nslot) return BLDP_OK;
-  for (void *q : g_slots.p) (void)hipHostFree(q);
-  g_slots.p.clear();
-  g_slots.bytes = 0;
+// The ring reused across calls of one device (under its call lock).
+void free_slots(Slots &sl) {
+  for (void *q : sl.p) (void)hipHostFree(q);
+  sl.p.clear();
+  sl.bytes = 0;
+}
+int ensure_slots(Slots &sl, int64_t bytes, int nslot) {
+  if (sl.bytes == bytes && (int)sl.p.size() == nslot) return BLDP_OK;
+  free_slots(sl);
   for (int i = 0; i < nslot; ++i) {
     void *q = nullptr;
     if (hipHostMalloc(&q, (size_t)bytes, hipHostMallocDefault) != hipSuccess) {
-      for (void *r : g_slots.p) (void)hipHostFree(r);
-      g_slots.p.clear();
+      free_slots(sl);
       return bldp::set_error(BLDP_ENOMEM, "runs_to_device: %lld bytes of pinned slots",
                              (long long)bytes);
     }
-    g_slots.p.push_back(q);
+    sl.p.push_back(q);
   }
-  g_slots.bytes = bytes;
+  sl.bytes = bytes;
   return BLDP_OK;
 }
 
@@ -389,15 +403,16 @@ extern "C" BLDP_API int bldp_runs_to_device(int fd, int64_t nrun, const int64_t 
     }
     pos += len[r];
   }
-  std::lock_guard<std::mutex> call(g_call_mu);
-  int rc = ensure_slots(slot_bytes, nslot);
+  DevIO *io = dev_io();
+  std::lock_guard<std::mutex> call(io->call);
+  int rc = ensure_slots(io->slots, slot_bytes, nslot);
   if (rc) return rc;
   // reads of batch b go to slot b % nslot at (hoff - b * slot_bytes); a batch
   // may be read once the copy out of its slot two rounds back is done
-  j.slot_base = &g_slots.p;
+  j.slot_base = &io->slots.p;
   j.slot_bytes = slot_bytes;
   j.open.store(std::min<int64_t>(nbatch, nslot));
-  ReadPool *rp = pool();
+  ReadPool *rp = io->pool.get();
   rp->post(&j);
   hipStream_t cs = (hipStream_t)copy_stream, s = (hipStream_t)stream;
   std::vector<hipEvent_t> evs(nbatch, nullptr);
@@ -413,7 +428,7 @@ extern "C" BLDP_API int bldp_runs_to_device(int fd, int64_t nrun, const int64_t 
     }
     const int64_t lo = b * slot_bytes, n = std::min(slot_bytes, total - lo);
     if (hipEventCreateWithFlags(&evs[b], hipEventDisableTiming) != hipSuccess ||
-        hipMemcpyAsync((uint8_t *)dev_dst + lo, g_slots.p[b % nslot], (size_t)n,
+        hipMemcpyAsync((uint8_t *)dev_dst + lo, io->slots.p[b % nslot], (size_t)n,
                        hipMemcpyHostToDevice, cs) != hipSuccess ||
         hipEventRecord(evs[b], cs) != hipSuccess) {
       rc = bldp::set_error(BLDP_EHIP, "runs_to_device: H2D copy of batch %lld failed",
@@ -466,12 +481,11 @@ extern "C" BLDP_API int bldp_runs_to_device(int fd, int64_t nrun, const int64_t 
 }
 
 void bldp::fileio_release() {
-  std::lock_guard<std::mutex> call(g_call_mu);  // no read call in progress
-  {
-    std::lock_guard<std::mutex> lk(g_pool_mu);
-    g_pool.reset();  // joins the reader threads
+  std::lock_guard<std::mutex> lk(g_io_mu);
+  for (auto &kv : g_io) {
+    std::lock_guard<std::mutex> call(kv.second->call);  // no read call in progress
+    kv.second->pool.reset();                            // joins the reader threads
+    free_slots(kv.second->slots);
   }
-  for (void *q : g_slots.p) (void)hipHostFree(q);
-  g_slots.p.clear();
-  g_slots.bytes = 0;
+  g_io.clear();
 }

@@ -655,6 +655,32 @@ def test_compressed_file_missing_and_unfiltered_chunks(pkg, orc, tmp_path, monke
     assert_kurtosis(k, orc.kurtosis(want), "mid", nt)
 
 
+def test_gbt_fanout_over_compressed_and_raw_files(pkg, orc, tmp_path):
+    """GBT.getdata fans one call per (worker, file) out on threads
+    (src/gbt.jl:75-77): compressed, unfiltered-chunked and contiguous files
+    read at once on one device share the native reader (one read call at a
+    time per device) and the decode scratch; every result against the oracle."""
+    J, C = pkg.JRange, pkg.COLON
+    rng = np.random.default_rng(808)
+    names, arrs = [], []
+    for k in range(6):
+        a = np.asfortranarray(rng.integers(0, 128, (1024, 1, 96 + 8 * k)).astype(np.float32))
+        f = str(tmp_path / f"f{k}.h5")
+        if k % 3 == 0:
+            pkg.fbh5.write_bslz4(f, dict(foff=-1.0), a, (16, 1, 1024),
+                                 lambda blk: orc.np_bslz4_encode(blk, 512, lz4=orc.lz4_compress))
+        elif k % 3 == 1:
+            pkg.fbh5.write(f, dict(foff=-1.0), a, chunks=(16, 1, 256))
+        else:
+            pkg.fbh5.write(f, dict(foff=-1.0), a)
+        names.append(f)
+        arrs.append(a)
+    for _ in range(3):
+        got = pkg.GBT.getdata([0] * 6, names, (J(1, 1024), C, J(1, 96)), fqavby=16, tavby=8)
+        for g, a in zip(got, arrs):
+            assert same_bits(g, orc.reduce(a, 16, 8, "sum", [0, 1024, 1, 0, 1, 1, 0, 96, 1]))
+
+
 def test_bslz4_gpu_decoder_random_lz4(pkg, orc):
     """The GPU decoder on the same kind of random chunks (real LZ4 matches,
     all block sizes, raw tails), 40 chunks in one call."""
