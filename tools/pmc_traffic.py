@@ -12,8 +12,9 @@ taken as reported).
 
     python tools/pmc_traffic.py CONFIG BANKS_PER_LAUNCH FETCH.csv WRITE.csv
     python tools/pmc_traffic.py --kurt CONFIG BANKS FETCH.csv WRITE.csv   (getkurtosis call:
-        k_kurt_leaf (16 B/lane streaming, x2) + the tree merge kernels (8 B
-        loads, taken as reported), summed per call; key "kurt_CONFIG")
+        every kernel of the call (k_kurt_regs / mid / leaf and the tree merge),
+        FETCH x2 (coalesced streams: 128-B requests tallied at 64 B), summed
+        per call; key "kurt_CONFIG")
 """
 from __future__ import annotations
 
@@ -41,13 +42,16 @@ def kurt_call(fpath, wpath):
     """Per-call HBM bytes of the streamed-leaf kurtosis: every kernel of the
     call, medians per kernel, FETCH of the 16 B/lane leaf stream x2."""
     kern, hbm = {}, 0.0
-    for name in ("k_kurt_leaf", "k_kurt_tree", "k_kurt_final"):
+    for name in ("k_kurt_regs", "k_kurt_mid", "k_kurt_leaf", "k_kurt_tree", "k_kurt_final"):
         try:
             f = statistics.median(per_dispatch(fpath, "FETCH_SIZE", name))
             w = statistics.median(per_dispatch(wpath, "WRITE_SIZE", name))
         except SystemExit:
             continue
-        mult = 2 if name == "k_kurt_leaf" else 1
+        # every one of these is a coalesced stream whose 128-B requests gfx950
+        # tallies at 64 B (4, 8 and 16 B per lane alike: k_kurt_mid's FETCH is
+        # exactly half its 4 B/lane window, the tree's half its partials)
+        mult = 2
         kern[name] = {"fetch_size_kib_median": f, "write_size_kib_median": w,
                       "hbm_bytes": int(mult * f * 1024 + w * 1024)}
         hbm += mult * f * 1024 + w * 1024
@@ -86,9 +90,9 @@ def main():
     if kern:
         d[cfg][str(nbank)]["kernels"] = kern
         d[cfg][str(nbank)]["dispatches"] = None
-        d[cfg][str(nbank)]["correction"] = ("per call: k_kurt_leaf 2*FETCH_SIZE*1024 + "
-                                            "WRITE_SIZE*1024; tree/final kernels FETCH_SIZE*1024 "
-                                            "+ WRITE_SIZE*1024 (8-byte loads)")
+        d[cfg][str(nbank)]["correction"] = ("per call, every kernel: 2*FETCH_SIZE*1024 + "
+                                            "WRITE_SIZE*1024 (gfx950 half-count of coalesced "
+                                            "streaming reads)")
     with open(out, "w") as f:
         json.dump(d, f, indent=1)
     print(json.dumps(d[cfg][str(nbank)]))
