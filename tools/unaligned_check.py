@@ -71,6 +71,10 @@ def main():
         ((1 << 20, 1, 16), [3, (1 << 20) - 1024, 1, 0, 1, 1, 0, 16, 1], 1024, 16),
         ((515, 1, 20000), [1, 512, 1, 0, 1, 1, 0, 19456, 1], 8, 1024),
         ((515, 1, 20000), [3, 512, 1, 0, 1, 1, 0, 20000, 1], 4, 1),
+        # aligned F = 1024 (interleaved / segment kernels), full and ragged rows
+        ((1 << 20, 2, 32), [0, 1 << 20, 1, 0, 2, 1, 0, 32, 1], 1024, 16),
+        ((1 << 20, 1, 64), [0, 1 << 20, 1, 0, 1, 1, 0, 64, 1], 1024, 4),
+        ((17 * 1024, 1, 48), [0, 17 * 1024, 1, 0, 1, 1, 0, 48, 1], 1024, 48),
     ]
     for shape, win, F, T in red_cases:
         banks = [eng.synth(*shape, 64, seed=s, kind=1) for s in range(3)]
