@@ -78,8 +78,9 @@ SIGNATURES = {
     "bldp_bslz4_decode_dev": ([I, P, P, P, P, I, P, P, P, P], I),
     "bldp_bslz4_decode_dev_async": ([I, P, P, P, P, I, P, P, P, P, P], I),
     "bldp_bslz4_error": ([P, P], I),
-    "bldp_chunks_to_device": ([I, I64, P, P, P, P, I64, P, P, P, P, I64, P, P, P, P], I),
-    "bldp_runs_to_device": ([I, I64, P, P, P, I64, I, P, P, P], I),
+    "bldp_chunks_to_device": ([I, I64, P, P, P, P, I64, P, P, P, I64, P, I64, I64, P, P, P, P],
+                              I),
+    "bldp_runs_to_device": ([I, I64, P, P, P, I64, I64, I, P, P, P], I),
     "bldp_comm_id": ([P], I),
     "bldp_comm_init": ([I, I, I, P, P], I),
     "bldp_comm_destroy": ([P], I),

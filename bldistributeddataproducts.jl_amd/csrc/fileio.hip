@@ -194,8 +194,8 @@ double ms_since(std::chrono::steady_clock::time_point t0) {
 extern "C" BLDP_API int bldp_chunks_to_device(
     int fd, int64_t nchunk, const int64_t *file_off, const int64_t *stored_len,
     const int64_t *stage_off, const uint32_t *filter_mask, int64_t nbatch, const int64_t *batch_end,
-    void *host_pinned, void *dev_stage, void *dev_out, int64_t out_chunk_bytes, int *err_dev,
-    void *copy_stream, void *stream, double *stats) {
+    void *host_pinned, void *dev_stage, int64_t stage_bytes, void *dev_out, int64_t out_chunk_bytes,
+    int64_t out_bytes, int *err_dev, void *copy_stream, void *stream, double *stats) {
   const auto t0 = std::chrono::steady_clock::now();
   if (nchunk < 0 || nbatch < 0 || (nchunk && (!file_off || !stored_len || !stage_off ||
                                                !filter_mask || !batch_end || !host_pinned ||
@@ -206,9 +206,16 @@ extern "C" BLDP_API int bldp_chunks_to_device(
     return bldp::set_error(BLDP_EINVAL, "chunks_to_device: batches must end at chunk %lld",
                            (long long)nchunk);
   bool any_comp = false;
+  if (dev_out && (out_chunk_bytes < 0 || nchunk > out_bytes / std::max<int64_t>(1, out_chunk_bytes)))
+    return bldp::set_error(BLDP_EINVAL, "chunks_to_device: %lld chunks of %lld bytes exceed the "
+                           "%lld-byte output", (long long)nchunk, (long long)out_chunk_bytes,
+                           (long long)out_bytes);
   for (int64_t k = 0; k < nchunk; ++k) {
     if (stored_len[k] < 0 || stage_off[k] < 0 || file_off[k] < 0)
       return bldp::set_error(BLDP_EINVAL, "chunks_to_device: negative offset or size");
+    if (stored_len[k] > stage_bytes - stage_off[k])
+      return bldp::set_error(BLDP_EINVAL, "chunks_to_device: chunk %lld overruns the %lld-byte "
+                             "staging buffers", (long long)k, (long long)stage_bytes);
     if (stored_len[k] && (filter_mask[k] & 1) && dev_out && stored_len[k] != out_chunk_bytes)
       return bldp::set_error(BLDP_EINVAL,
                              "chunks_to_device: unfiltered chunk %lld holds %lld bytes, not %lld",
@@ -369,9 +376,9 @@ int ensure_slots(Slots &sl, int64_t bytes, int nslot) {
 }  // namespace
 
 extern "C" BLDP_API int bldp_runs_to_device(int fd, int64_t nrun, const int64_t *file_off,
-                                            const int64_t *len, void *dev_dst, int64_t slot_bytes,
-                                            int nslot, void *copy_stream, void *stream,
-                                            double *stats) {
+                                            const int64_t *len, void *dev_dst, int64_t dst_bytes,
+                                            int64_t slot_bytes, int nslot, void *copy_stream,
+                                            void *stream, double *stats) {
   const auto t0 = std::chrono::steady_clock::now();
   if (nrun < 0 || (nrun && (!file_off || !len || !dev_dst)) || slot_bytes < (1 << 20) ||
       nslot < 2 || nslot > 16)
@@ -382,6 +389,9 @@ extern "C" BLDP_API int bldp_runs_to_device(int fd, int64_t nrun, const int64_t 
       return bldp::set_error(BLDP_EINVAL, "runs_to_device: negative offset or size");
     total += len[r];
   }
+  if (total > dst_bytes)
+    return bldp::set_error(BLDP_EINVAL, "runs_to_device: %lld bytes exceed the %lld-byte "
+                           "destination", (long long)total, (long long)dst_bytes);
   if (total == 0) return BLDP_OK;
   const int64_t nbatch = (total + slot_bytes - 1) / slot_bytes;
   // pieces: runs cut at batch (slot) boundaries and into ~8 pieces per slot;

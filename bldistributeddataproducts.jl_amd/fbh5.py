@@ -1065,7 +1065,9 @@ def _native_chunks(fname, faddr, sizes, offsets, masks, batches, pinned, cdev, p
         rc = L.bldp_chunks_to_device(
             fd, len(sz), fa.ctypes.data, sz.ctypes.data, of.ctypes.data, mk.ctypes.data,
             len(bend), bend.ctypes.data, pinned.data_ptr(), cdev.data_ptr(),
-            packed.data_ptr() if packed is not None else None, 4 * cvol, err.data_ptr(),
+            min(pinned.numel(), cdev.numel()),
+            packed.data_ptr() if packed is not None else None, 4 * cvol,
+            4 * packed.numel() if packed is not None else 0, err.data_ptr(),
             copy_stream.cuda_stream, _lib.stream_ptr(), stats)
         # (waits for every queued copy and decode, also after a failed call)
         rc2 = L.bldp_bslz4_error(err.data_ptr(), _lib.stream_ptr())

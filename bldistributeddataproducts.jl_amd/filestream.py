@@ -281,7 +281,7 @@ def _runs_native(path, runs, device, total, timings):
     try:
         with torch.cuda.device(dev):
             rc = _lib.lib().bldp_runs_to_device(fd, len(ln), fo.ctypes.data, ln.ctypes.data,
-                                                out.data_ptr(), BATCH_BYTES, NSLOTS,
+                                                out.data_ptr(), out.numel(), BATCH_BYTES, NSLOTS,
                                                 cs.cuda_stream, _lib.stream_ptr(), stats)
     finally:
         os.close(fd)

@@ -240,7 +240,9 @@ BLDP_API int bldp_bslz4_error(const int *err_dev, void *stream);
  * src/gbtworkerfunctions.jl:181-187).  Chunk k (stored_len[k] bytes at
  * file_off[k] of the open file `fd`; 0 bytes = never written) is read with
  * parallel preads (a persistent pool of reader threads, BLDP_READ_THREADS)
- * into host_pinned + stage_off[k].  Chunks [batch_end[b-1], batch_end[b]) form
+ * into host_pinned + stage_off[k] (both staging buffers hold stage_bytes;
+ * dev_out holds out_bytes: every table entry is checked against them before
+ * anything is read).  Chunks [batch_end[b-1], batch_end[b]) form
  * batch b: once its reads land, its staged byte range is copied to dev_stage
  * (same offsets) on copy_stream, `stream` waits for that copy, and the batch's
  * chunks are decoded on `stream` into dev_out + k * out_chunk_bytes
@@ -256,20 +258,23 @@ BLDP_API int bldp_chunks_to_device(int fd, int64_t nchunk, const int64_t *file_o
                                    const int64_t *stored_len, const int64_t *stage_off,
                                    const uint32_t *filter_mask, int64_t nbatch,
                                    const int64_t *batch_end, void *host_pinned, void *dev_stage,
-                                   void *dev_out, int64_t out_chunk_bytes, int *err_dev,
-                                   void *copy_stream, void *stream, double *stats);
+                                   int64_t stage_bytes, void *dev_out, int64_t out_chunk_bytes,
+                                   int64_t out_bytes, int *err_dev, void *copy_stream,
+                                   void *stream, double *stats);
 
 /* Raw byte runs of a file (an uncompressed contiguous FBH5 `data` dataset or
  * a SIGPROC data block: src/gbtworkerfunctions.jl:171-189) into a dense device
  * block: run r (len[r] bytes at file_off[r]) lands at dev_dst + the sum of
- * the earlier runs' lengths.  The block is cut into batches of slot_bytes;
+ * the earlier runs' lengths (dev_dst holds dst_bytes).  The block is cut
+ * into batches of slot_bytes;
  * the reader threads pread batch b into library-owned pinned slot b % nslot
  * once that slot's previous copy is done, and each batch is copied to the
  * device on copy_stream as soon as its reads land.  Returns after every copy
  * is done; `stream` waits for the last.  stats as bldp_chunks_to_device. */
 BLDP_API int bldp_runs_to_device(int fd, int64_t nrun, const int64_t *file_off,
-                                 const int64_t *len, void *dev_dst, int64_t slot_bytes,
-                                 int nslot, void *copy_stream, void *stream, double *stats);
+                                 const int64_t *len, void *dev_dst, int64_t dst_bytes,
+                                 int64_t slot_bytes, int nslot, void *copy_stream, void *stream,
+                                 double *stats);
 
 /* Gather a window (Julia order, dense (nc, ni, nt) out) from decoded chunks:
  * packed holds the chunks of a chunk-aligned bounding box back to back in

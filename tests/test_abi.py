@@ -355,19 +355,21 @@ def test_chunks_to_device_validates_before_any_read(pkg, L):
     of = np.array([0, 100], np.int64)
     mk = np.zeros(2, np.uint32)
 
-    def call(fa=fa, sz=sz, of=of, mk=mk, bend=(2,), out=fake, ocb=400):
+    def call(fa=fa, sz=sz, of=of, mk=mk, bend=(2,), out=fake, ocb=400, stage=200, obytes=800):
         be = np.array(bend, np.int64)
         return L.bldp_chunks_to_device(-1, len(sz), fa.ctypes.data, sz.ctypes.data,
                                        of.ctypes.data, mk.ctypes.data, len(be), be.ctypes.data,
-                                       fake, fake, out, ocb, fake, None, None, None)
+                                       fake, fake, stage, out, ocb, obytes, fake, None, None, None)
 
     assert call(bend=(1,)) == pkg._lib.BLDP_EINVAL and "end at chunk" in pkg._lib.last_error()
     assert call(bend=(2, 1)) == pkg._lib.BLDP_EINVAL
     assert call(sz=np.array([100, -1], np.int64)) == pkg._lib.BLDP_EINVAL
     assert call(mk=np.ones(2, np.uint32)) == pkg._lib.BLDP_EINVAL  # raw chunk of 100 B, slot 400
     assert call(out=None) == pkg._lib.BLDP_EINVAL and "output" in pkg._lib.last_error()
-    assert L.bldp_chunks_to_device(-1, 0, None, None, None, None, 0, None, None, None, None, 0,
-                                   None, None, None, None) == 0  # nothing to do
+    assert call(stage=199) == pkg._lib.BLDP_EINVAL and "staging" in pkg._lib.last_error()
+    assert call(obytes=799) == pkg._lib.BLDP_EINVAL and "exceed" in pkg._lib.last_error()
+    assert L.bldp_chunks_to_device(-1, 0, None, None, None, None, 0, None, None, None, 0, None, 0,
+                                   0, None, None, None, None) == 0  # nothing to do
 
 
 def test_runs_to_device_validates_before_any_read(pkg, L):
@@ -375,11 +377,13 @@ def test_runs_to_device_validates_before_any_read(pkg, L):
     fake = 1 << 20
     fo = np.array([0, 10], np.int64)
     ln = np.array([10, -1], np.int64)
-    assert L.bldp_runs_to_device(-1, 2, fo.ctypes.data, ln.ctypes.data, fake, 64 << 20, 4,
+    assert L.bldp_runs_to_device(-1, 2, fo.ctypes.data, ln.ctypes.data, fake, 20, 64 << 20, 4,
                                  None, None, None) == pkg._lib.BLDP_EINVAL
     ln = np.array([10, 10], np.int64)
-    assert L.bldp_runs_to_device(-1, 2, fo.ctypes.data, ln.ctypes.data, fake, 1024, 4,
+    assert L.bldp_runs_to_device(-1, 2, fo.ctypes.data, ln.ctypes.data, fake, 20, 1024, 4,
                                  None, None, None) == pkg._lib.BLDP_EINVAL  # slots < 1 MiB
-    assert L.bldp_runs_to_device(-1, 2, fo.ctypes.data, ln.ctypes.data, fake, 64 << 20, 1,
+    assert L.bldp_runs_to_device(-1, 2, fo.ctypes.data, ln.ctypes.data, fake, 20, 64 << 20, 1,
                                  None, None, None) == pkg._lib.BLDP_EINVAL  # one slot
-    assert L.bldp_runs_to_device(-1, 0, None, None, None, 64 << 20, 4, None, None, None) == 0
+    assert L.bldp_runs_to_device(-1, 2, fo.ctypes.data, ln.ctypes.data, fake, 19, 64 << 20, 4,
+                                 None, None, None) == pkg._lib.BLDP_EINVAL  # 20 bytes into 19
+    assert L.bldp_runs_to_device(-1, 0, None, None, None, 0, 64 << 20, 4, None, None, None) == 0
