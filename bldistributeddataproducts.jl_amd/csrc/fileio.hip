@@ -189,9 +189,35 @@ double ms_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
+// A job published to a pool; whatever way the call leaves (error return or
+// C++ exception), the readers are cancelled and withdrawn before the job (a
+// local of the call) goes away.
+struct PostedJob {
+  ReadPool *rp;
+  Job *j;
+  bool done = false;
+  PostedJob(ReadPool *r, Job *jj) : rp(r), j(jj) { rp->post(j); }
+  void finish(bool cancel) {
+    if (done) return;
+    done = true;
+    if (cancel) {
+      {
+        std::lock_guard<std::mutex> lk(j->mu);
+        int expect = 0;
+        j->err.compare_exchange_strong(expect, ECANCELED);
+        j->open.store(INT64_MAX);
+      }
+      j->gate.notify_all();
+      ReadPool::run(j);  // the remaining pieces, skipped
+    }
+    rp->retire();
+  }
+  ~PostedJob() { finish(true); }
+};
+
 }  // namespace
 
-extern "C" BLDP_API int bldp_chunks_to_device(
+static int chunks_to_device(
     int fd, int64_t nchunk, const int64_t *file_off, const int64_t *stored_len,
     const int64_t *stage_off, const uint32_t *filter_mask, int64_t nbatch, const int64_t *batch_end,
     void *host_pinned, void *dev_stage, int64_t stage_bytes, void *dev_out, int64_t out_chunk_bytes,
@@ -268,15 +294,21 @@ extern "C" BLDP_API int bldp_chunks_to_device(
     k0 = k1;
   }
 
+  // every buffer of the queueing loop is allocated before the readers start
+  int64_t maxb = 0;
+  for (int64_t b = 0, q = 0; b < nbatch; q = batch_end[b], ++b)
+    maxb = std::max(maxb, batch_end[b] - q);
+  std::vector<hipEvent_t> evs;
+  std::vector<uint64_t> offs, lens, ooff, olen;
+  evs.reserve(nbatch);
+  for (auto *v : {&offs, &lens, &ooff, &olen}) v->reserve(maxb);
   DevIO *io = dev_io();
   std::lock_guard<std::mutex> call(io->call);
   ReadPool *rp = io->pool.get();
-  rp->post(&j);
+  PostedJob posted(rp, &j);
   hipStream_t cs = (hipStream_t)copy_stream, s = (hipStream_t)stream;
   int rc = BLDP_OK;
   double t_first = -1.0;
-  std::vector<hipEvent_t> evs;
-  std::vector<uint64_t> offs, lens, ooff, olen;
   k0 = 0;
   for (int64_t b = 0; b < nbatch && rc == BLDP_OK; ++b) {
     const int64_t k1 = batch_end[b];
@@ -331,11 +363,7 @@ extern "C" BLDP_API int bldp_chunks_to_device(
     k0 = k1;
   }
   const double t_reads = ms_since(t0);
-  if (rc != BLDP_OK) {  // let the readers finish before the buffers go away
-    j.err.store(j.err.load() ? j.err.load() : ECANCELED);
-    ReadPool::run(&j);
-  }
-  rp->retire();
+  posted.finish(rc != BLDP_OK);  // (an error: cancel the readers first)
   for (hipEvent_t ev : evs) (void)hipEventDestroy(ev);
   if (stats) {
     stats[0] = t_first;
@@ -375,10 +403,9 @@ int ensure_slots(Slots &sl, int64_t bytes, int nslot) {
 
 }  // namespace
 
-extern "C" BLDP_API int bldp_runs_to_device(int fd, int64_t nrun, const int64_t *file_off,
-                                            const int64_t *len, void *dev_dst, int64_t dst_bytes,
-                                            int64_t slot_bytes, int nslot, void *copy_stream,
-                                            void *stream, double *stats) {
+static int runs_to_device(int fd, int64_t nrun, const int64_t *file_off, const int64_t *len,
+                          void *dev_dst, int64_t dst_bytes, int64_t slot_bytes, int nslot,
+                          void *copy_stream, void *stream, double *stats) {
   const auto t0 = std::chrono::steady_clock::now();
   if (nrun < 0 || (nrun && (!file_off || !len || !dev_dst)) || slot_bytes < (1 << 20) ||
       nslot < 2 || nslot > 16)
@@ -422,10 +449,10 @@ extern "C" BLDP_API int bldp_runs_to_device(int fd, int64_t nrun, const int64_t 
   j.slot_base = &io->slots.p;
   j.slot_bytes = slot_bytes;
   j.open.store(std::min<int64_t>(nbatch, nslot));
-  ReadPool *rp = io->pool.get();
-  rp->post(&j);
-  hipStream_t cs = (hipStream_t)copy_stream, s = (hipStream_t)stream;
   std::vector<hipEvent_t> evs(nbatch, nullptr);
+  ReadPool *rp = io->pool.get();
+  PostedJob posted(rp, &j);
+  hipStream_t cs = (hipStream_t)copy_stream, s = (hipStream_t)stream;
   double t_first = -1.0;
   for (int64_t b = 0; b < nbatch && rc == BLDP_OK; ++b) {
     {
@@ -460,16 +487,7 @@ extern "C" BLDP_API int bldp_runs_to_device(int fd, int64_t nrun, const int64_t 
     }
   }
   const double t_reads = ms_since(t0);
-  if (rc != BLDP_OK) {
-    {
-      std::lock_guard<std::mutex> lk(j.mu);
-      j.err.store(j.err.load() ? j.err.load() : ECANCELED);
-      j.open.store(nbatch);
-    }
-    j.gate.notify_all();
-    ReadPool::run(&j);
-  }
-  rp->retire();
+  posted.finish(rc != BLDP_OK);  // (an error: cancel the readers first)
   // the slots are reused by the next call: every copy out of them is done
   // before returning; the caller's stream waits for the last one
   for (int64_t b = 0; b < nbatch; ++b)
@@ -488,6 +506,36 @@ extern "C" BLDP_API int bldp_runs_to_device(int fd, int64_t nrun, const int64_t 
     stats[3] = (double)rp->threads();
   }
   return rc;
+}
+
+extern "C" BLDP_API int bldp_chunks_to_device(
+    int fd, int64_t nchunk, const int64_t *file_off, const int64_t *stored_len,
+    const int64_t *stage_off, const uint32_t *filter_mask, int64_t nbatch, const int64_t *batch_end,
+    void *host_pinned, void *dev_stage, int64_t stage_bytes, void *dev_out, int64_t out_chunk_bytes,
+    int64_t out_bytes, int *err_dev, void *copy_stream, void *stream, double *stats) {
+  try {
+    return chunks_to_device(fd, nchunk, file_off, stored_len, stage_off, filter_mask, nbatch,
+                            batch_end, host_pinned, dev_stage, stage_bytes, dev_out,
+                            out_chunk_bytes, out_bytes, err_dev, copy_stream, stream, stats);
+  } catch (const std::bad_alloc &) {
+    return bldp::set_error(BLDP_ENOMEM, "chunks_to_device: out of host memory");
+  } catch (...) {
+    return bldp::set_error(BLDP_EINVAL, "chunks_to_device: unexpected C++ exception");
+  }
+}
+
+extern "C" BLDP_API int bldp_runs_to_device(int fd, int64_t nrun, const int64_t *file_off,
+                                            const int64_t *len, void *dev_dst, int64_t dst_bytes,
+                                            int64_t slot_bytes, int nslot, void *copy_stream,
+                                            void *stream, double *stats) {
+  try {
+    return runs_to_device(fd, nrun, file_off, len, dev_dst, dst_bytes, slot_bytes, nslot,
+                          copy_stream, stream, stats);
+  } catch (const std::bad_alloc &) {
+    return bldp::set_error(BLDP_ENOMEM, "runs_to_device: out of host memory");
+  } catch (...) {
+    return bldp::set_error(BLDP_EINVAL, "runs_to_device: unexpected C++ exception");
+  }
 }
 
 void bldp::fileio_release() {
