@@ -492,6 +492,10 @@ def main():
                     help="banks as separate allocations or as views of one slab")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo only to rehearse the N-rank path on one GPU")
+    ap.add_argument("--exchange", default="native", choices=["native", "torch"],
+                    help="nccl backend: the per-step gather through libbldp_hip's "
+                         "bldp_band_gather_f32 on a stream of its own (native) or "
+                         "torch.distributed.gather (torch)")
     ap.add_argument("--pipeline", action="store_true",
                     help="N=1: run the N>1 exchange anyway (a one-rank process group, "
                          "RCCL gather + stitch of every step) to exercise it on one GPU")
@@ -523,6 +527,8 @@ def main():
             dist.init_process_group("gloo")
     cfg = CONFIGS[args.config]
     run_info = {"dist_backend": args.dist_backend if use_pg else None,
+                "exchange": (args.exchange if args.dist_backend == "nccl" else "torch")
+                if use_pg else None,
                 "world_size": dist.get_world_size() if use_pg else 1,
                 "device_count": torch.cuda.device_count()}
     if args.mode == "host":
@@ -574,8 +580,14 @@ def main():
     stream = torch.cuda.current_stream()
     # this rank's slice of the band; N > 1: two slots, the RCCL gather of step
     # k (to rank 0, over xGMI) overlaps the reduce of step k+1
-    pipe = pkg.band.BandPipeline(len(mine) * nco, ni, nto, device=f"cuda:{local}",
-                                 gather_single=args.pipeline) if use_pg else None
+    native_x = use_pg and args.dist_backend == "nccl" and args.exchange == "native"
+    if not use_pg:
+        pipe = None
+    elif native_x:
+        pipe = pkg.band.NativeBandPipeline(len(mine) * nco, ni, nto, device=f"cuda:{local}")
+    else:
+        pipe = pkg.band.BandPipeline(len(mine) * nco, ni, nto, device=f"cuda:{local}",
+                                     gather_single=args.pipeline)
     out = eng.fb_empty(len(mine) * nco, ni, nto) if pipe is None else None
 
     def step(ev0=None, ev1=None):
@@ -601,6 +613,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(*evs[k])
+    host_ms = (time.perf_counter() - t0) * 1e3 / args.steps  # enqueue cost per step
     if pipe:
         pipe.drain()
     torch.cuda.synchronize()
@@ -627,8 +640,11 @@ def main():
     if not pipe:
         parallelism = f"{len(mine)} bank(s) x 1 GPU, single-launch band reduce + stitch"
     elif args.dist_backend == "nccl":
+        via = ("ncclGather through libbldp_hip (bldp_band_gather_f32) on its own stream"
+               if native_x else "torch.distributed.gather")
         parallelism = (f"{len(mine)} bank(s)/GPU x {world} GPU(s), RCCL (nccl backend) gather "
-                       "over xGMI + stitch; the gather of step k overlaps the reduce of step k+1")
+                       f"over xGMI + stitch ({via}); the gather of step k overlaps the reduce "
+                       "of step k+1")
     else:
         parallelism = (f"REHEARSAL, not a scaling number: {world} ranks on {ndev} GPU(s), gloo "
                        f"backend (CPU transport) gather + stitch, {len(mine)} bank(s)/rank")
@@ -656,11 +672,14 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "kernel": kernel_name,
                          "kernel_ms": round(kern_ms, 4), "bytes_per_launch": bytes_launch},
+            "host_enqueue_ms_per_step": round(host_ms, 4),
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)
     if use_pg:
         dist.barrier()
+        if native_x:
+            pipe.close()
         dist.destroy_process_group()
     return result
 

@@ -204,6 +204,23 @@ class NativeBand:
         _lib.check(_lib.lib().bldp_comm_id(buf), "bldp_comm_id")
         return bytes(buf)
 
+    def gather_into(self, block, gathered, root=0, stream=None):
+        """Raw exchange: the dense ``block`` (every rank the same size) lands
+        rank-major in ``gathered`` (root only; None elsewhere), queued on
+        ``stream``."""
+        from . import _lib
+
+        if not block.is_contiguous() or (gathered is not None and not gathered.is_contiguous()):
+            raise ValueError("gather_into: dense blocks only")
+        if gathered is not None and gathered.numel() != self.nranks * block.numel():
+            raise ValueError("gather_into: gathered holds %d floats, not %d x %d"
+                             % (gathered.numel(), self.nranks, block.numel()))
+        _lib.check(self.L.bldp_band_gather_f32(self.handle, int(root), block.data_ptr(),
+                                               block.numel(), gathered.data_ptr()
+                                               if gathered is not None else None,
+                                               _lib.stream_ptr(stream)),
+                   "bldp_band_gather_f32")
+
     def gather(self, local, root=0, stream=None):
         """``local``: this rank's Julia-order (ncl, ni, nto) slice, dense.
         Returns the stitched band on the root (a new tensor), None elsewhere."""
@@ -235,3 +252,100 @@ class NativeBand:
 
             _lib.check(self.L.bldp_comm_destroy(self.handle), "bldp_comm_destroy")
             self.handle = None
+
+
+class NativeBandPipeline:
+    """``BandPipeline``'s interface over the C-ABI exchange: every step's
+    gather is ``bldp_band_gather_f32`` (RCCL ncclGather) queued on a stream of
+    the pipeline's own, after an event on the reducing stream, so it runs on
+    another hardware queue beside the next step's reduce.  On MI355X this costs
+    the step ~10 us against ~27 us for torch.distributed.gather, whose
+    work lands on the reducing stream's queue (``tools/stream_probe.py``,
+    ``profiles/r02/stream_probe.json``).
+
+    The communicator is made from the process group: the root draws the
+    RCCL id and ``broadcast_object_list`` hands it to every rank (pass
+    ``comm=`` to reuse a ``NativeBand``)."""
+
+    def __init__(self, ncl, ni, nto, device, depth=2, root=0, group=None, stitch_fn=None,
+                 comm=None, priority=-1):
+        import torch
+        import torch.distributed as dist
+
+        from . import engine
+
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.root, self.depth = root, depth
+        self.shape = (ncl, ni, nto)
+        self.stitch_fn = stitch_fn or (lambda g, n: engine.stitch(g, n))
+        dev = torch.device(device)
+        self._own = comm is None
+        if comm is None:
+            obj = [NativeBand.new_id() if self.rank == root else None]
+            dist.broadcast_object_list(obj, src=root, group=group)
+            comm = NativeBand(dev.index if dev.index is not None else torch.cuda.current_device(),
+                              self.world, self.rank, obj[0])
+        self.comm = comm
+        self._local = [torch.empty((nto, ni, ncl), dtype=torch.float32, device=dev)
+                       for _ in range(depth)]
+        self._gathered = [torch.empty((self.world, nto, ni, ncl), dtype=torch.float32,
+                                      device=dev) for _ in range(depth)] \
+            if self.rank == root else [None] * depth
+        # high priority: HIP gives it a hardware queue of its own, so the
+        # gather never sits behind the next reduce (a normal-priority stream
+        # may share the reducing stream's queue, GPU_MAX_HW_QUEUES = 4)
+        self.stream = torch.cuda.Stream(device=dev, priority=priority)
+        self._reduced = [torch.cuda.Event() for _ in range(depth)]
+        self._done = [torch.cuda.Event() for _ in range(depth)]
+        self._pending = [False] * depth
+        self._next = 0
+
+    def local(self, slot):
+        return self._local[slot].permute(2, 1, 0)
+
+    def begin(self):
+        """Next slot; the current stream waits (on the GPU) for the gather
+        that last read it."""
+        s = self._next
+        self._next = (s + 1) % self.depth
+        self.wait(s)
+        return s
+
+    def exchange(self, slot):
+        import torch
+
+        cur = torch.cuda.current_stream()
+        self._reduced[slot].record(cur)
+        self.stream.wait_event(self._reduced[slot])
+        self.comm.gather_into(self._local[slot], self._gathered[slot], self.root, self.stream)
+        self._done[slot].record(self.stream)
+        self._pending[slot] = True
+        if self.rank != self.root:
+            return None
+        ncl, ni, nto = self.shape
+        g = self._gathered[slot]
+        if ni * nto == 1:  # rank-major slices of single rows are already vcat order
+            return g.reshape(self.world * ncl, 1, 1)
+        self.wait(slot)  # the stitch reads the gathered blocks
+        return self.stitch_fn(g, self.world)
+
+    def wait(self, slot):
+        import torch
+
+        if self._pending[slot]:
+            torch.cuda.current_stream().wait_event(self._done[slot])
+            self._pending[slot] = False
+
+    def drain(self):
+        for s in range(self.depth):
+            self.wait(s)
+
+    def close(self):
+        if self._own and self.comm is not None:
+            import torch
+
+            self.stream.synchronize()
+            torch.cuda.current_stream().synchronize()
+            self.comm.close()
+        self.comm = None

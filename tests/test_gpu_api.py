@@ -161,9 +161,10 @@ def test_band_dist_two_ranks_real_kernels():
     assert all(q.get(timeout=5) for _ in ps)
 
 
-def _nccl_pipeline_rank(port, q):
+def _nccl_pipeline_rank(port, q, kind="torch"):
     """One rank of an RCCL (torch "nccl") process group driving BandPipeline
-    with the gather forced on: what every rank of bench.py N>1 runs."""
+    (torch.distributed.gather) or NativeBandPipeline (bldp_band_gather_f32 on
+    its own stream) with the gather on: what every rank of bench.py N>1 runs."""
     import sys
 
     import torch
@@ -182,8 +183,11 @@ def _nccl_pipeline_rank(port, q):
         banks = [orc.gamma_bandpass(8192, ni, nt, 1024, 70 + b) for b in range(4)]
         dbanks = [eng.fb_from_numpy(b, "cuda:0") for b in banks]
         want = orc.stitch([orc.reduce(b, F, T) for b in banks])
-        pipe = pkg.band.BandPipeline(4 * 8192 // F, ni, nt // T, device="cuda:0",
-                                     gather_single=True)
+        if kind == "native":
+            pipe = pkg.band.NativeBandPipeline(4 * 8192 // F, ni, nt // T, device="cuda:0")
+        else:
+            pipe = pkg.band.BandPipeline(4 * 8192 // F, ni, nt // T, device="cuda:0",
+                                         gather_single=True)
         for _ in range(3):  # slots reused: the gather of step k overlaps step k+1
             slot = pipe.begin()
             eng.band_reduce(dbanks, F, T, "sum", None, out=pipe.local(slot))
@@ -193,6 +197,8 @@ def _nccl_pipeline_rank(port, q):
             got = eng.fb_to_numpy(res)
             ok.append(got.shape == want.shape and bool(np.allclose(got, want, rtol=1e-5)))
         pipe.drain()
+        if kind == "native":
+            pipe.close()
     t = torch.tensor([1.0, 2.0], dtype=torch.float64, device="cuda")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)  # bench.py's max-over-ranks timing
     ok.append(t.tolist() == [1.0, 2.0])
@@ -201,15 +207,18 @@ def _nccl_pipeline_rank(port, q):
     q.put(ok)
 
 
-def test_band_pipeline_over_rccl_one_rank():
-    """The N>1 exchange of bench.py (BandPipeline: async torch "nccl" = RCCL
-    gather to the root, then the stitch kernel) on a one-rank group, the most
-    of it one GPU can run (RCCL refuses two ranks on one device)."""
+@pytest.mark.parametrize("kind", ["torch", "native"])
+def test_band_pipeline_over_rccl_one_rank(kind):
+    """The N>1 exchange of bench.py (async RCCL gather to the root, then the
+    stitch kernel; torch.distributed.gather or the C ABI's ncclGather on the
+    pipeline's own stream) on a one-rank group, the most of it one GPU can run
+    (RCCL refuses two ranks on one device)."""
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=_nccl_pipeline_rank, args=(29900 + os.getpid() % 90, q))
+    p = ctx.Process(target=_nccl_pipeline_rank,
+                    args=(29900 + os.getpid() % 90 + (kind == "native"), q, kind))
     p.start()
     p.join(timeout=240)
     assert p.exitcode == 0
@@ -234,6 +243,7 @@ def test_bench_pipeline_flag():
     c = d["config"]
     assert d["n_gpus"] == 1 and d["value"] > 0 and "RCCL (nccl backend) gather" in c["parallelism"]
     assert c["dist_backend"] == "nccl" and c["world_size"] == 1 and c["device_count"] >= 1
+    assert c["exchange"] == "native" and "bldp_band_gather_f32" in c["parallelism"]
 
 
 def _bslz4_fixtures():

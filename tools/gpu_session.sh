@@ -88,6 +88,15 @@ for s in $STEPS; do
     unal_check) run unal_check 300 python tools/unaligned_check.py --variant "${UNAL_VARIANT:-unal2}" ;;
     nmix)  run nmix 300 ./build/hbm_ceiling 32 10 bldistributeddataproducts.jl_amd/libbldp_hip.so nmix ;;  # (built here: hipcc -o build/hbm_ceiling tools/hbm_ceiling.hip -ldl)
     pipeline) run pipeline 600 python bench.py --pipeline --no-cpu-baseline ;;
+    prof_pipelb_*) run "$s" 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/$s" -o run \
+             -- python bench.py --pipeline --no-cpu-baseline --local-banks "${s#prof_pipelb_}" --steps 20 --warmup 5 ;;
+    stream_probe) run stream_probe 300 python tools/stream_probe.py ;;
+    stream_probe_hi) TORCH_NCCL_HIGH_PRIORITY=1 run stream_probe_hi 300 python tools/stream_probe.py --variants none,torch_async,torch_side ;;
+    prof_bench_pipe) run prof_bench_pipe 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/$s" -o run \
+             -- python bench.py --pipeline --no-cpu-baseline --local-banks 1 --steps 20 --warmup 5 ;;
+    prof_stream_probe) run prof_stream_probe 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/$s" -o run \
+             -- python tools/stream_probe.py --steps 20 --warmup 5 ;;
+    pipelb_*) run "$s" 300 python bench.py --pipeline --no-cpu-baseline --local-banks "${s#pipelb_}" --steps 50 --warmup 10 ;;
     ab)    run ab 900 python tools/ab_variants.py --run --variants "${AB_VARIANTS:-base,noil}" --json "$OUT/ab.json" ;;
     ab_kurt) run ab_kurt 900 python tools/ab_variants.py --run --suite kurt --variants ${AB_VARIANTS:-base,kold,kw5,kw6} --json "$OUT/ab_kurt.json" ;;
     ab_tile) run ab_tile 900 python tools/ab_variants.py --run --suite tile --variants "${AB_VARIANTS:-base,tk4a1,tk2a1,tk2a2}" --json "$OUT/ab_tile.json" ;;
