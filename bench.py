@@ -605,8 +605,10 @@ def main():
     if pipe:
         pipe.drain()
     torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
+    # timing-only events without the system-scope fence: no L2 write-back
+    # after every launch (3-4 us a step, tools/stream_probe.py none_tev*)
+    evs = [(pkg._lib.HipEvent(timing=True, fence=False),
+            pkg._lib.HipEvent(timing=True, fence=False)) for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

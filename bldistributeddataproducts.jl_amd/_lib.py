@@ -151,3 +151,68 @@ def stream_ptr(stream=None) -> int:
 
     s = stream if stream is not None else torch.cuda.current_stream()
     return int(s.cuda_stream)
+
+
+HIP_EVENT_DISABLE_TIMING = 0x2
+HIP_EVENT_DISABLE_SYSTEM_FENCE = 0x20000000
+_hip = None
+
+
+def hip():
+    """The HIP runtime libbldp_hip.so is linked to (its soname, so the copy
+    already loaded -- torch's, when torch came first -- is the one bound)."""
+    global _hip
+    if _hip is None:
+        lib()
+        h = ctypes.CDLL("libamdhip64.so.7")
+        h.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+        h.hipEventRecord.argtypes = [P, P]
+        h.hipStreamWaitEvent.argtypes = [P, P, ctypes.c_uint]
+        h.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), P, P]
+        h.hipEventSynchronize.argtypes = [P]
+        h.hipEventDestroy.argtypes = [P]
+        _hip = h
+    return _hip
+
+
+class HipEvent:
+    """A HIP event with the flags torch.cuda.Event does not expose.  With
+    ``fence=False`` (hipEventDisableSystemFence) recording it does no
+    system-scope release (no L2 write-back to host scope), which is all a
+    consumer on the same device needs: a timing event, or a stream of the same
+    GPU waiting for a kernel's output (the band exchange's gather)."""
+
+    def __init__(self, timing=False, fence=True):
+        self._h = hip()
+        e = ctypes.c_void_p()
+        flags = (0 if timing else HIP_EVENT_DISABLE_TIMING) | \
+            (0 if fence else HIP_EVENT_DISABLE_SYSTEM_FENCE)
+        rc = self._h.hipEventCreateWithFlags(ctypes.byref(e), flags)
+        if rc:
+            raise BLDPError(BLDP_EHIP, f"hipEventCreateWithFlags(0x{flags:x}) failed: {rc}")
+        self.ev = e
+
+    def _ok(self, rc, what):
+        if rc:
+            raise BLDPError(BLDP_EHIP, f"{what} failed: {rc}")
+
+    def record(self, stream=None):
+        self._ok(self._h.hipEventRecord(self.ev, stream_ptr(stream)), "hipEventRecord")
+
+    def wait(self, stream=None):
+        """``stream`` (default: torch's current) waits on the GPU for it."""
+        self._ok(self._h.hipStreamWaitEvent(stream_ptr(stream), self.ev, 0), "hipStreamWaitEvent")
+
+    def synchronize(self):
+        self._ok(self._h.hipEventSynchronize(self.ev), "hipEventSynchronize")
+
+    def elapsed_time(self, end) -> float:
+        ms = ctypes.c_float()
+        self._ok(self._h.hipEventElapsedTime(ctypes.byref(ms), self.ev, end.ev),
+                 "hipEventElapsedTime")
+        return float(ms.value)
+
+    def __del__(self):
+        if getattr(self, "ev", None):
+            self._h.hipEventDestroy(self.ev)
+            self.ev = None

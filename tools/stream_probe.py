@@ -11,6 +11,13 @@ one cfg3 bank (4 GiB, F=1024 T=16), K steps per variant, ms per step.
   native_async   bldp_band_gather_f32 on a second stream, two slots, events
   native_hi      the same, the second stream at high priority
   pipe_native    band.NativeBandPipeline (high-priority stream), as bench.py
+  hi_nowait      native_hi with a slot per step: the reducing stream never
+                 waits for the gathers (the cost of the event record alone)
+  hi_wait2       native_hi with 4 slots, the reducing stream waiting every
+                 second step (for the gather two slots back)
+  hi_nofence     native_hi with events recorded without the system-scope fence
+  none_tev       reduce only, torch timing events around every reduce
+  none_tev_nf    reduce only, fence-less HIP timing events around every reduce
 
     python tools/stream_probe.py [--steps 50] [--variants a,b,...]
 """
@@ -30,8 +37,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--variants", default="none,torch_async,native_inline,native_async,"
-                    "native_hi,pipe_native")
+    ap.add_argument("--variants", default="none,torch_async,native_inline,native_hi,"
+                    "pipe_native,hi_nowait,hi_nofence,none_tev,none_tev_nf")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -55,7 +62,7 @@ def main():
     def run(name):
         main_s = torch.cuda.current_stream()
         side = torch.cuda.Stream()
-        comm = torch.cuda.Stream(priority=-1 if name == "native_hi" else 0)
+        comm = torch.cuda.Stream(priority=-1 if name.startswith(("native_hi", "hi_")) else 0)
         if name in ("torch_async", "torch_side", "pipe_native"):
             pipe = pkg.band.NativeBandPipeline(nco, 1, 1, device="cuda:0", comm=nb) \
                 if name == "pipe_native" else \
@@ -70,22 +77,39 @@ def main():
 
             def drain():
                 pipe.drain()
-        elif name in ("native_inline", "native_async", "native_hi"):
-            loc = [torch.empty((nco, 1, 1), device="cuda") for _ in range(2)]
-            done = [torch.cuda.Event() for _ in range(2)]
-            red = [torch.cuda.Event() for _ in range(2)]
+        elif name in ("native_inline", "native_async", "native_hi", "hi_nowait", "hi_wait2",
+                      "hi_nofence"):
+            D = {"hi_nowait": a.steps + a.warmup + 1, "hi_wait2": 4}.get(name, 2)
+            loc = [torch.empty((nco, 1, 1), device="cuda") for _ in range(D)]
+            if name == "hi_nofence":
+                HE = pkg._lib.HipEvent
+                done = [HE(fence=False) for _ in range(D)]
+                red = [HE(fence=False) for _ in range(D)]
+            else:
+                done = [torch.cuda.Event() for _ in range(D)]
+                red = [torch.cuda.Event() for _ in range(D)]
             k = [0]
             res = []
 
             def step():
-                s = k[0] % 2
+                s = k[0] % D
                 k[0] += 1
+                if name == "hi_wait2" and k[0] > 4 and k[0] % 2 == 1:
+                    # slots s and s+1 were last gathered at steps k-4, k-3
+                    main_s.wait_event(done[(s + 1) % D])
+                elif D == 2 and k[0] > 2 and name == "hi_nofence":
+                    done[s].wait(main_s)
+                elif D == 2 and k[0] > 2 and name != "native_inline":
+                    main_s.wait_event(done[s])  # the gather that last read slot s
                 eng.band_reduce([bank], F, T, "sum", None, out=loc[s])
                 if name == "native_inline":
                     res.append(nb.gather(loc[s], stream=main_s))
+                elif name == "hi_nofence":
+                    red[s].record(main_s)
+                    red[s].wait(comm)
+                    res.append(nb.gather(loc[s], stream=comm))
+                    done[s].record(comm)
                 else:
-                    if k[0] > 2:
-                        main_s.wait_event(done[s])  # (before the next reduce into s)
                     red[s].record(main_s)
                     comm.wait_event(red[s])
                     res.append(nb.gather(loc[s], stream=comm))
@@ -97,9 +121,17 @@ def main():
                 torch.cuda.current_stream().wait_stream(comm)
         else:
             out = eng.fb_empty(nco, 1, 1)
+            if name == "none_tev_nf":
+                tev = [pkg._lib.HipEvent(timing=True, fence=False) for _ in range(2)]
+            elif name == "none_tev":
+                tev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
 
             def step():
+                if name.startswith("none_tev"):
+                    tev[0].record(main_s)
                 eng.band_reduce([bank], F, T, "sum", None, out=out)
+                if name.startswith("none_tev"):
+                    tev[1].record(main_s)
 
             def drain():
                 pass
