@@ -345,6 +345,11 @@ __global__ __launch_bounds__(kB) void k_kurt_mid(const KurtArgs k) {
 #ifndef BLDP_KURT_LEAF_WAVES
 #define BLDP_KURT_LEAF_WAVES 0
 #endif
+//   BLDP_KURT_LEAF_MINWAVES  resident waves per SIMD the register allocation must
+//                         allow (0 = the compiler's choice)
+#ifndef BLDP_KURT_LEAF_MINWAVES
+#define BLDP_KURT_LEAF_MINWAVES 0
+#endif
 constexpr int kLeafW = BLDP_KURT_LEAF_W;
 static_assert(kLeafW == 1 || kLeafW == 2 || kLeafW == 4, "BLDP_KURT_LEAF_W: 1, 2 or 4");
 
@@ -419,7 +424,11 @@ __device__ __forceinline__ void leaf_store(const KurtArgs &k, const LeafAcc<W> &
 }
 
 __global__ __launch_bounds__(kB)
-#if BLDP_KURT_LEAF_WAVES > 0
+#if BLDP_KURT_LEAF_MINWAVES > 0 && BLDP_KURT_LEAF_WAVES > 0
+__attribute__((amdgpu_waves_per_eu(BLDP_KURT_LEAF_MINWAVES, BLDP_KURT_LEAF_WAVES)))
+#elif BLDP_KURT_LEAF_MINWAVES > 0
+__attribute__((amdgpu_waves_per_eu(BLDP_KURT_LEAF_MINWAVES)))
+#elif BLDP_KURT_LEAF_WAVES > 0
 __attribute__((amdgpu_waves_per_eu(1, BLDP_KURT_LEAF_WAVES)))
 #endif
 void k_kurt_leaf(const KurtArgs k) {

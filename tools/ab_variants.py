@@ -60,6 +60,9 @@ VARIANTS = {
     "kleafw1ch": "-DBLDP_KURT_LEAF_W=1 -DBLDP_KURT_LEAF_B=8",
     "kleafw2": "-DBLDP_KURT_LEAF_WAVES=2",
     "kleafw3": "-DBLDP_KURT_LEAF_WAVES=3",
+    "kleafb2": "-DBLDP_KURT_LEAF_B=2",
+    "kleafpipe2": "-DBLDP_KURT_LEAF_PIPE=1 -DBLDP_KURT_LEAF_B=2",
+    "kleafpipe2w5": "-DBLDP_KURT_LEAF_PIPE=1 -DBLDP_KURT_LEAF_B=2 -DBLDP_KURT_LEAF_MINWAVES=5",
     "kmidnochain": "-DBLDP_KURT_MID_TIMING_NOCHAIN=1",  # timing only: wrong numerics
     # misaligned unit-step windows on the vector paths (dword-aligned 16-byte loads);
     # 2 = the kurtosis register / leaf paths too
@@ -159,6 +162,14 @@ def run(names, rounds, iters, suite="main"):
         kurt_case("kurt cfg4 c0=1", b4, [1, 508, 1, 0, 1, 1, 0, 879616, 1])
         kurt_case("kurt 65536ch nt2048 c0=3", b5, [3, 65532, 1, 0, 1, 1, 0, 2048, 1])
         cases_done = True
+    elif suite == "kleaf":  # the streamed-leaf kurtosis path only
+        del b3
+        b4 = [eng.synth(512, 1, 880000, 8, seed=10 * b + 1, kind=0) for b in range(8)]
+        kurt_case("kurt cfg4 nt879616", b4, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
+        kurt_case("kurt cfg4 1 bank", b4[:1], [0, 512, 1, 0, 1, 1, 0, 879616, 1])
+        b5 = [eng.synth(65536, 1, 2048, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
+        kurt_case("kurt 65536ch nt2048", b5)
+        cases_done = True
     elif suite == "tile":  # tile path: misaligned starts and odd F at cfg3 scale
         n = 1 << 26
         band_case("cfg3 c0=1 F1024", b3, 1024, 16, [1, n - 1024, 1, 0, 1, 1, 0, 16, 1])
@@ -245,7 +256,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--suite", default="main", choices=["main", "tile", "kurt"])
+    ap.add_argument("--suite", default="main", choices=["main", "tile", "kurt", "kleaf"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:

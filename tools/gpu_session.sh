@@ -99,6 +99,12 @@ for s in $STEPS; do
     pipelb_*) run "$s" 300 python bench.py --pipeline --no-cpu-baseline --local-banks "${s#pipelb_}" --steps 50 --warmup 10 ;;
     ab)    run ab 900 python tools/ab_variants.py --run --variants "${AB_VARIANTS:-base,noil}" --json "$OUT/ab.json" ;;
     ab_kurt) run ab_kurt 900 python tools/ab_variants.py --run --suite kurt --variants ${AB_VARIANTS:-base,kold,kw5,kw6} --json "$OUT/ab_kurt.json" ;;
+    ab_kleaf) run ab_kleaf 600 python tools/ab_variants.py --run --suite kleaf --variants "${AB_VARIANTS:-base,kleafb2,kleafpipe2,kleafpipe2w5}" --json "$OUT/ab_kleaf.json" ;;
+    counters) run counters 60 rocprofv3 -L ;;
+    sq_kurt_*) run "$s" 120 rocprofv3 --pmc ${SQC:-SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE GRBM_COUNT} \
+             --output-format csv -d "$OUT/$s" -o run -- python bench.py --mode kurtosis --config "${s#sq_kurt_}" --steps 5 --warmup 2 ;;
+    sq_red_*) run "$s" 120 rocprofv3 --pmc ${SQC:-SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE GRBM_COUNT} \
+             --output-format csv -d "$OUT/$s" -o run -- python bench.py --config "${s#sq_red_}" --steps 5 --warmup 2 --no-cpu-baseline ;;
     ab_tile) run ab_tile 900 python tools/ab_variants.py --run --suite tile --variants "${AB_VARIANTS:-base,tk4a1,tk2a1,tk2a2}" --json "$OUT/ab_tile.json" ;;
   esac
 done
