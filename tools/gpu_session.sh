@@ -55,6 +55,8 @@ for s in $STEPS; do
     file)  run file 600 python bench.py --mode file ;;
     file_probe) run file_probe 600 python tools/file_probe.py ;;
     rawfile) run rawfile 600 python bench.py --mode rawfile ;;
+    rawfile_ring) BLDP_PAGECACHE_DMA=0 run rawfile_ring 600 python bench.py --mode rawfile ;;
+    rawtests) run rawtests 300 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "raw or fil or gbt" ;;
     rawfile_py) BLDP_NATIVE_READ=0 run rawfile_py 600 python bench.py --mode rawfile ;;
     file_py) BLDP_NATIVE_READ=0 run file_py 600 python bench.py --mode file ;;
     paths) run paths 300 python tools/probe_paths.py ;;
@@ -100,6 +102,7 @@ for s in $STEPS; do
     ab)    run ab 900 python tools/ab_variants.py --run --variants "${AB_VARIANTS:-base,noil}" --json "$OUT/ab.json" ;;
     ab_kurt) run ab_kurt 900 python tools/ab_variants.py --run --suite kurt --variants ${AB_VARIANTS:-base,kold,kw5,kw6} --json "$OUT/ab_kurt.json" ;;
     ab_kleaf) run ab_kleaf 600 python tools/ab_variants.py --run --suite kleaf --variants "${AB_VARIANTS:-base,kleafb2,kleafpipe2,kleafpipe2w5}" --json "$OUT/ab_kleaf.json" ;;
+    mmap_probe) run mmap_probe 300 python tools/mmap_register_probe.py ;;
     counters) run counters 60 rocprofv3 -L ;;
     sq_kurt_*) run "$s" 120 rocprofv3 --pmc ${SQC:-SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE GRBM_COUNT} \
              --output-format csv -d "$OUT/$s" -o run -- python bench.py --mode kurtosis --config "${s#sq_kurt_}" --steps 5 --warmup 2 ;;
