@@ -29,6 +29,8 @@
 //               channel alignment or step).  The Float32 sum runs down the
 //               registers wave after wave; z, z2 and the Float64 sums follow
 //               the recipe, the 4 partial sums are added in wave order.
+//               k_kurt_mid2 (float4-column windows up to 384 spectra): the
+//               same with 128 channels, two per lane, and 8 waves.
 //   > 512       k_kurt_leaf : one wave per (leaf, 256 channels) streams the
 //               leaf once: its sequential Float32 sum, and Float64 power sums
 //               about its first spectrum, moved to the leaf's own mean.
@@ -312,6 +314,97 @@ __global__ __launch_bounds__(kB) void k_kurt_mid(const KurtArgs k) {
     }
     const double cm2 = a2 / (double)nt, cm4 = a4 / (double)nt;
     k.out[ib * k.nc + c] = (cm4 / (cm2 * cm2)) - 3.0;
+  }
+}
+
+// The same register tile with two adjacent channels per lane (one 8-byte load
+// per lane: 512 contiguous bytes per wave-instruction instead of 256) and NW
+// waves splitting the spectra (NW hand-offs of the running sums; the Float64
+// sums are added in NW partials).  Float4-column windows whose waves hold <= 48
+// spectra each (nt <= 384 with NW = 8, <= 115 VGPRs: 4 waves/SIMD).  A/B on
+// MI355X against k_kurt_mid (profiles/r02/ab_kurt_mid2.json): the 0002 band
+// (279 spectra) +4%, one 0002 bank +17%, a window 16 bytes off a 256-byte
+// boundary +27%, 100 spectra +6%; at 512 spectra (3 waves/SIMD, one workgroup
+// per CU) -18%, so longer windows stay on k_kurt_mid.
+//   BLDP_KURT_MID_CPL  2 (default) = this kernel where it applies; 1 = k_kurt_mid only
+//   BLDP_KURT_MID_NW   its waves per workgroup (8 default, or 4)
+#ifndef BLDP_KURT_MID_CPL
+#define BLDP_KURT_MID_CPL 2
+#endif
+#ifndef BLDP_KURT_MID_NW
+#define BLDP_KURT_MID_NW 8
+#endif
+template <int NR, int NW>
+__global__ __launch_bounds__(64 * NW) void k_kurt_mid2(const KurtArgs k) {
+  constexpr int TW = 128;  // channels per tile
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t ctiles = (k.nc + TW - 1) / TW;
+  const int64_t b = blockIdx.x;
+  const int64_t ib = b / ctiles, c = (b % ctiles) * TW + 2 * lane;
+  const bool valid = c < k.nc;  // (nc even: c + 1 < nc too)
+  const int bank = (int)(ib / k.ni);
+  const int64_t i = ib - (int64_t)bank * k.ni;
+  const int nt = (int)k.nt;
+  const int r0 = (wave * nt) / NW, cnt = (((wave + 1) * nt) / NW) - r0;
+  const int64_t ld = k.in_ld_t;
+  const float *p = k.in[bank] + k.in_off + i * k.in_ld_i + (valid ? c : 0) + r0 * ld;
+  f2v v[NR];
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+    v[r] = (valid && r < cnt) ? __builtin_nontemporal_load(reinterpret_cast<const f2u *>(p + r * ld))
+                              : f2v{0.0f, 0.0f};
+  // Base.sum, sequential over the whole window, wave after wave
+  __shared__ f2v carry[64];
+  f2v s = {0.0f, 0.0f};
+#pragma unroll 1
+  for (int w = 0; w < NW; ++w) {
+    if (wave == w) {
+      if (w > 0) s = carry[lane];
+#pragma unroll
+      for (int r = 0; r < NR; ++r)
+        if (r < cnt) s = (w == 0 && r == 0) ? v[0] : s + v[r];  // from the first element
+      carry[lane] = s;
+    }
+    __syncthreads();
+  }
+  const f2v sm = carry[lane];
+  const float m0 = sm.x / (float)nt, m1 = sm.y / (float)nt;
+  double a2 = 0.0, a4 = 0.0, b2 = 0.0, b4 = 0.0;
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+    if (r < cnt) {
+      const float z0 = v[r].x - m0, z1 = v[r].y - m1;  // StatsBase: Float32 z, z2
+      const float q0 = z0 * z0, q1 = z1 * z1;
+      a2 += (double)q0;
+      a4 += (double)(q0 * q0);
+      b2 += (double)q1;
+      b4 += (double)(q1 * q1);
+    }
+  __shared__ double part[NW][4][64];
+  part[wave][0][lane] = a2;
+  part[wave][1][lane] = a4;
+  part[wave][2][lane] = b2;
+  part[wave][3][lane] = b4;
+  __syncthreads();
+  if (wave == 0 && valid) {
+    double x2 = 0.0, x4 = 0.0, y2 = 0.0, y4 = 0.0;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      x2 += part[q][0][lane];
+      x4 += part[q][1][lane];
+      y2 += part[q][2][lane];
+      y4 += part[q][3][lane];
+    }
+    const double n = (double)nt;
+    const double k0 = ((x4 / n) / ((x2 / n) * (x2 / n))) - 3.0;
+    const double k1 = ((y4 / n) / ((y2 / n) * (y2 / n))) - 3.0;
+    double *o = k.out + ib * k.nc + c;
+    if ((reinterpret_cast<uintptr_t>(o) & 15) == 0) {
+      *reinterpret_cast<d2v *>(o) = d2v{k0, k1};
+    } else {
+      o[0] = k0;
+      o[1] = k1;
+    }
   }
 }
 
@@ -1065,6 +1158,18 @@ hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s) {
       hipLaunchKernelGGL((k_kurt_regs<32, false>), g1, block, 0, s, k);
     return hipGetLastError();
   }
+  if (p == KP_MID && BLDP_KURT_MID_CPL == 2 && k.vec && cdivk(k.nt, BLDP_KURT_MID_NW) <= 48) {
+    constexpr int NW = BLDP_KURT_MID_NW;
+    static_assert(NW == 4 || NW == 8, "BLDP_KURT_MID_NW: 4 or 8");
+    const dim3 g1((unsigned)(cdivk(k.nc, 128) * k.nrow)), b2(64 * NW);
+    switch (cdivk(cdivk(k.nt, NW), 16)) {
+      case 1: hipLaunchKernelGGL((k_kurt_mid2<16, NW>), g1, b2, 0, s, k); break;
+      case 2: hipLaunchKernelGGL((k_kurt_mid2<32, NW>), g1, b2, 0, s, k); break;
+      case 3: hipLaunchKernelGGL((k_kurt_mid2<48, NW>), g1, b2, 0, s, k); break;
+      default: hipLaunchKernelGGL((k_kurt_mid2<48, NW>), g1, b2, 0, s, k); break;
+    }
+    return hipGetLastError();
+  }
   if (p == KP_MID) {  // registers sized to the quarter window, 16 spectra at a time
     const dim3 g1((unsigned)(cdivk(k.nc, 64) * k.nrow));
     switch (cdivk(cdivk(k.nt, 4), 16)) {
@@ -1119,7 +1224,7 @@ int64_t kurtosis_max_grid(const KurtArgs &k) {
   const int64_t ncols = k.nc / 4;
   switch (p) {
     case KP_REGS: return cdivk(ncols, kB) * k.nrow;
-    case KP_MID: return cdivk(k.nc, 64) * k.nrow;
+    case KP_MID: return cdivk(k.nc, 64) * k.nrow;  // (k_kurt_mid2: half of it)
     case KP_LEAF: return cdivk(k.nrow * k.nslot * k.nseg, 4);
     default:
       return std::max(cdivk(k.nc, kB) * k.nrow * k.nslot,

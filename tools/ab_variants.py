@@ -61,6 +61,9 @@ VARIANTS = {
     "kleafw2": "-DBLDP_KURT_LEAF_WAVES=2",
     "kleafw3": "-DBLDP_KURT_LEAF_WAVES=3",
     "kleafb2": "-DBLDP_KURT_LEAF_B=2",
+    # k_kurt_mid with two channels per lane (512-byte wave loads), 8 or 4 waves
+    "kmid2w8": "-DBLDP_KURT_MID_CPL=2 -DBLDP_KURT_MID_NW=8",
+    "kmid2w4": "-DBLDP_KURT_MID_CPL=2 -DBLDP_KURT_MID_NW=4",
     "kleafpipe2": "-DBLDP_KURT_LEAF_PIPE=1 -DBLDP_KURT_LEAF_B=2",
     "kleafpipe2w5": "-DBLDP_KURT_LEAF_PIPE=1 -DBLDP_KURT_LEAF_B=2 -DBLDP_KURT_LEAF_MINWAVES=5",
     "kmidnochain": "-DBLDP_KURT_MID_TIMING_NOCHAIN=1",  # timing only: wrong numerics
@@ -162,6 +165,17 @@ def run(names, rounds, iters, suite="main"):
         kurt_case("kurt cfg4 c0=1", b4, [1, 508, 1, 0, 1, 1, 0, 879616, 1])
         kurt_case("kurt 65536ch nt2048 c0=3", b5, [3, 65532, 1, 0, 1, 1, 0, 2048, 1])
         cases_done = True
+    elif suite == "kmid":  # the register-tile kurtosis path (0002 products)
+        del b3
+        b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
+        kurt_case("kurt cfg2 nt272", b2, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
+        kurt_case("kurt cfg2 nt279", b2)
+        kurt_case("kurt cfg1 nt279", b2[:1])
+        kurt_case("kurt cfg2 nt100", b2, [0, 65536, 1, 0, 1, 1, 0, 100, 1])
+        kurt_case("kurt cfg2 c0=4 nt272", b2, [4, 65532, 1, 0, 1, 1, 0, 272, 1])
+        b6 = [eng.synth(32768, 1, 512, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
+        kurt_case("kurt 32768ch nt512", b6)
+        cases_done = True
     elif suite == "kleaf":  # the streamed-leaf kurtosis path only
         del b3
         b4 = [eng.synth(512, 1, 880000, 8, seed=10 * b + 1, kind=0) for b in range(8)]
@@ -256,7 +270,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--suite", default="main", choices=["main", "tile", "kurt", "kleaf"])
+    ap.add_argument("--suite", default="main", choices=["main", "tile", "kurt", "kleaf", "kmid"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:
