@@ -387,3 +387,75 @@ def test_runs_to_device_validates_before_any_read(pkg, L):
     assert L.bldp_runs_to_device(-1, 2, fo.ctypes.data, ln.ctypes.data, fake, 19, 64 << 20, 4,
                                  None, None, None) == pkg._lib.BLDP_EINVAL  # 20 bytes into 19
     assert L.bldp_runs_to_device(-1, 0, None, None, None, 0, 64 << 20, 4, None, None, None) == 0
+
+
+# ---- the Julia binding's ccalls against the header --------------------------
+# Julia is absent here and on the GPU box, so julia/BLDPHip.jl cannot run; its
+# ABI contract can still be checked: every ccall names a declared entry point
+# with the same return type and the same argument types, position by position.
+_C_TO_JL = {"int": "Cint", "int64_t": "Int64", "size_t": "Csize_t", "uint64_t": "UInt64",
+            "uint32_t": "UInt32", "uint8_t": "UInt8", "char": "UInt8", "float": "Float32",
+            "double": "Float64", "void": "Cvoid"}
+
+
+def _c_param_to_jl(p):
+    p = p.replace("const", " ").strip()
+    arrays = p.count("[")
+    p = re.sub(r"\[[^\]]*\]", "", p)
+    stars = p.count("*")
+    words = p.replace("*", " ").split()
+    base = words[0] if words else ""
+    t = _C_TO_JL[base]
+    for _ in range(stars + arrays):
+        t = "Ptr{%s}" % t
+    return t
+
+
+def _header_signatures():
+    src = open(os.path.join(REPO, "include", "bldp.h")).read()
+    sigs = {}
+    for ret, name, params in re.findall(r"BLDP_API\s+(\w+)\s+(bldp_\w+)\s*\(([^)]*)\)\s*;", src):
+        params = " ".join(params.split())
+        args = [] if params in ("", "void") else [_c_param_to_jl(x) for x in params.split(",")]
+        sigs[name] = (_C_TO_JL[ret], args)
+    return sigs
+
+
+def _split_top(s):
+    out, depth, cur = [], 0, ""
+    for ch in s:
+        if ch == "{":
+            depth += 1
+        elif ch == "}":
+            depth -= 1
+        if ch == "," and depth == 0:
+            out.append(cur.strip())
+            cur = ""
+        else:
+            cur += ch
+    if cur.strip():
+        out.append(cur.strip())
+    return out
+
+
+def _julia_ccalls():
+    src = open(os.path.join(REPO, "bldistributeddataproducts.jl_amd", "julia", "BLDPHip.jl")).read()
+    calls = re.findall(r"ccall\(\(:(bldp_\w+),\s*libbldp\),\s*(\w+),\s*\(([^()]*)\)", src, re.S)
+    return [(n, r, _split_top(" ".join(a.split()))) for n, r, a in calls]
+
+
+def test_julia_binding_ccalls_match_the_header():
+    sigs = _header_signatures()
+    calls = _julia_ccalls()
+    assert len(calls) >= 12
+    for name, ret, args in calls:
+        assert name in sigs, name
+        want_ret, want_args = sigs[name]
+        assert ret == want_ret, (name, ret, want_ret)
+        # Julia passes a C array parameter as Ptr{T} and const pointers alike
+        assert args == want_args, (name, args, want_args)
+    # the binding covers the Julia worker's whole drop-in surface
+    named = {n for n, _, _ in calls}
+    for n in ("bldp_reduce_host_f32", "bldp_kurtosis_host_f32", "bldp_reduce_shape",
+              "bldp_last_error", "bldp_band_gather_f32", "bldp_comm_init"):
+        assert n in named, n
