@@ -156,11 +156,14 @@ def test_kurtosis_special_rows(eng, orc, nt):
     check(eng, orc, a, [1, 62, 1, 0, 1, 1, 0, nt, 1], unaligned(nt), "unaligned")
 
 
-@pytest.mark.parametrize("nt,path", [(16, "regs"), (32, "regs"), (600, "leaf"), (5007, "leaf")])
+@pytest.mark.parametrize("nt,path", [(16, "regs"), (32, "regs"), (100, "mid"), (384, "mid"),
+                                     (600, "leaf"), (5007, "leaf")])
 def test_kurtosis_unaligned_float4_windows(eng, orc, nt, path):
     """Windows starting off a 16-byte boundary whose channel count is a
     multiple of 4, and arrays with an odd channel pitch: the register and
-    streamed-leaf paths on dword-aligned 16-byte loads (bit-exact on regs)."""
+    streamed-leaf paths on dword-aligned 16-byte loads (bit-exact on regs),
+    k_kurt_mid2 on dword-aligned 8-byte loads (100 and 384 spectra: 13 and 48
+    per wave)."""
     rng = np.random.default_rng(1000 + nt)
     a = power_rows(rng, 260, 2, nt)
     check(eng, orc, a, [1, 256, 1, 0, 2, 1, 0, nt, 1], path, "c0=1")
