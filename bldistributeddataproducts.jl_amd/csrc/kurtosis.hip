@@ -480,6 +480,44 @@ __device__ __forceinline__ void leaf_step(LeafAcc<W> &A, const float (&x)[W]) {
   }
 }
 
+// BLDP_KURT_LEAF_TIMING_F32 1 = TIMING EXPERIMENT ONLY (wrong numerics): the
+// power sums of a batch in Float32 about a Float32 shift, added to the Float64
+// sums once per batch, pricing a scheme with 2 instead of 7 Float64
+// instructions per element
+#ifndef BLDP_KURT_LEAF_TIMING_F32
+#define BLDP_KURT_LEAF_TIMING_F32 0
+#endif
+// BLDP_KURT_LEAF_TIMING_LOADONLY 1 = TIMING EXPERIMENT ONLY (wrong numerics):
+// the main loop keeps only the loads and the Float32 sum (the access
+// pattern's own ceiling)
+#ifndef BLDP_KURT_LEAF_TIMING_LOADONLY
+#define BLDP_KURT_LEAF_TIMING_LOADONLY 0
+#endif
+template <int W, int B>
+__device__ __forceinline__ void leaf_batch_f32(LeafAcc<W> &A, const float (&cur)[B][W]) {
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    const float cf = (float)A.c[w];
+    float p1 = 0.f, p2 = 0.f, p3 = 0.f, p4 = 0.f;
+#pragma unroll
+    for (int q = 0; q < B; ++q) {
+      const float x = cur[q][w];
+      A.s[w] += x;
+      A.hi[w] = fmaxf(A.hi[w], x);
+      A.lo[w] = fminf(A.lo[w], x);
+      const float d = x - cf, d2 = d * d;
+      p1 += d;
+      p2 += d2;
+      p3 = fmaf(d2, d, p3);
+      p4 = fmaf(d2, d2, p4);
+    }
+    A.a1[w] += (double)p1;
+    A.a2[w] += (double)p2;
+    A.a3[w] += (double)p3;
+    A.a4[w] += (double)p4;
+  }
+}
+
 template <int W, typename T>
 __device__ __forceinline__ void stw(T *p, const T (&v)[W]) {
   if constexpr (W == 4 && sizeof(T) == 4) {
@@ -572,8 +610,17 @@ void k_kurt_leaf(const KurtArgs k) {
 #pragma unroll
       for (int w = 0; w < W; ++w) cur[q][w] = nxt[q][w];
 #else
+#if BLDP_KURT_LEAF_TIMING_LOADONLY  // TIMING EXPERIMENT ONLY: the loads and the Float32 sum
+#pragma unroll
+    for (int q = 0; q < B; ++q)
+#pragma unroll
+      for (int w = 0; w < W; ++w) A.s[w] += cur[q][w];
+#elif BLDP_KURT_LEAF_TIMING_F32
+    leaf_batch_f32<W, B>(A, cur);
+#else
 #pragma unroll
     for (int q = 0; q < B; ++q) leaf_step<W>(A, cur[q]);
+#endif
     if (bt + 1 < nb) {
 #pragma unroll
       for (int q = 0; q < B; ++q) ldw<W>(p + q * ld, cur[q]);

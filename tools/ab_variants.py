@@ -61,6 +61,12 @@ VARIANTS = {
     "kleafw2": "-DBLDP_KURT_LEAF_WAVES=2",
     "kleafw3": "-DBLDP_KURT_LEAF_WAVES=3",
     "kleafb2": "-DBLDP_KURT_LEAF_B=2",
+    "kleaft32": "-DBLDP_KURT_LEAF_TIMING_F32=1",  # timing only: wrong numerics
+    "kleaft32b8": "-DBLDP_KURT_LEAF_TIMING_F32=1 -DBLDP_KURT_LEAF_B=8",
+    "kleaflo": "-DBLDP_KURT_LEAF_TIMING_LOADONLY=1",  # timing only: loads + sum
+    "kleaflow4": "-DBLDP_KURT_LEAF_TIMING_LOADONLY=1 -DBLDP_KURT_LEAF_WAVES=4",
+    "kleaflob8w4": "-DBLDP_KURT_LEAF_TIMING_LOADONLY=1 -DBLDP_KURT_LEAF_B=8 -DBLDP_KURT_LEAF_WAVES=4",
+    "kleaflob8": "-DBLDP_KURT_LEAF_TIMING_LOADONLY=1 -DBLDP_KURT_LEAF_B=8",
     # k_kurt_mid with two channels per lane (512-byte wave loads), 8 or 4 waves
     "kmid2w8": "-DBLDP_KURT_MID_CPL=2 -DBLDP_KURT_MID_NW=8",
     "kmid2w4": "-DBLDP_KURT_MID_CPL=2 -DBLDP_KURT_MID_NW=4",
