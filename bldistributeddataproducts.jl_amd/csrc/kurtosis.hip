@@ -639,6 +639,150 @@ void k_kurt_leaf(const KurtArgs k) {
   leaf_store<W>(k, A, row, col, slot, len);
 }
 
+// The same leaf stream read the way the reduce reads its tiles: a workgroup
+// owns ONE leaf of two adjacent 256-channel column segments, and its 4 waves
+// interleave the rows -- waves 0 / 1 (one per segment) load the spectra 1, 3,
+// 5, ... of the leaf into registers and do all the arithmetic; waves 2 / 3
+// load the spectra 2, 4, 6, ... and hand them over through LDS (double
+// buffered, one barrier per batch of B spectrum pairs).  Each workgroup-
+// instruction pair reads 4 KiB contiguous (two whole rows of a 512-channel
+// window) instead of two 2 KiB pieces of two leaves 1.7 MB apart.  The
+// computing lane consumes the spectra in the leaf's order with leaf_step, so
+// the results are bit-identical to k_kurt_leaf.  Timing-only builds priced the
+// pattern at -3..-10% of the cfg4 kernel time by box
+// (profiles/r02/ab_kurt_leaf_timing_builds.json).
+//   BLDP_KURT_LEAF_ILV  1 = use it for float4-column leaves (W = 4); 0 = k_kurt_leaf
+//   BLDP_KURT_ILV_B     spectrum pairs per batch
+#ifndef BLDP_KURT_LEAF_ILV
+#define BLDP_KURT_LEAF_ILV 0
+#endif
+#ifndef BLDP_KURT_ILV_B
+#define BLDP_KURT_ILV_B 4
+#endif
+__global__ __launch_bounds__(kB) void k_kurt_leaf_ilv(const KurtArgs k) {
+  constexpr int B = BLDP_KURT_ILV_B;
+  __shared__ f4v hand[2][2][B][64];  // [buffer][segment][pair][lane]: 2 * B KiB per buffer
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int half = wave & 1, loader = wave >> 1;
+  const int64_t nseg2 = (k.nseg + 1) / 2;
+  const int64_t sp = (int64_t)blockIdx.x % nseg2, r = (int64_t)blockIdx.x / nseg2;
+  const int64_t slot = r % k.nslot, row = r / k.nslot;
+  const int64_t col = (2 * sp + half) * 64 + lane;
+  int64_t t0, len;
+  pw_leaf(k.nt, k.K, slot, t0, len);
+  if (row >= k.nrow || len <= 0) return;  // the whole workgroup (same leaf, same row)
+  const bool valid = col < k.nc / 4;
+  const int bank = (int)(row / k.ni);
+  const int64_t i = row - (int64_t)bank * k.ni;
+  const int64_t ld = k.in_ld_t;
+  const float *p = k.in[bank] + k.in_off + i * k.in_ld_i + 4 * (valid ? col : 0) + t0 * ld;
+  auto get = [&](int64_t t, float (&x)[4]) {  // spectrum t of the leaf (zeros off the window)
+    if (valid) {
+      ldw<4>(p + t * ld, x);
+    } else {
+      x[0] = x[1] = x[2] = x[3] = 0.0f;
+    }
+  };
+  LeafAcc<4> A;
+  if (!loader) {
+    float x0[4];
+    get(0, x0);
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      A.s[w] = A.hi[w] = A.lo[w] = x0[w];  // the sum starts from the first element
+      A.c[w] = (double)x0[w];
+      A.a1[w] = A.a2[w] = A.a3[w] = A.a4[w] = 0.0;
+    }
+  }
+  // spectra 1 .. len-1 as pairs (1 + 2j: this wave's registers, 2 + 2j: the
+  // loader's, through LDS); an odd count leaves the last spectrum unpaired
+  const int64_t npair = (len - 1) / 2, nb = (npair + B - 1) / B;
+  for (int64_t bt = 0; bt < nb; ++bt) {
+    const int64_t j0 = bt * B;
+    const int n = (int)min((int64_t)B, npair - j0);
+    const int buf = (int)(bt & 1);
+    float cur[B][4];
+    if (loader) {
+#pragma unroll
+      for (int q = 0; q < B; ++q)
+        if (q < n) get(2 + 2 * (j0 + q), cur[q]);
+#pragma unroll
+      for (int q = 0; q < B; ++q)
+        if (q < n) hand[buf][half][q][lane] = f4v{cur[q][0], cur[q][1], cur[q][2], cur[q][3]};
+    } else {
+#pragma unroll
+      for (int q = 0; q < B; ++q)
+        if (q < n) get(1 + 2 * (j0 + q), cur[q]);
+    }
+    __syncthreads();  // batch bt handed over; batch bt - 1's buffer is free again
+    if (!loader) {
+#pragma unroll
+      for (int q = 0; q < B; ++q)
+        if (q < n) {
+          const f4v h = hand[buf][half][q][lane];
+          const float y[4] = {h.x, h.y, h.z, h.w};
+          leaf_step<4>(A, cur[q]);
+          leaf_step<4>(A, y);
+        }
+    }
+  }
+  if (loader) return;
+  if ((len - 1) & 1) {  // the unpaired last spectrum
+    float x[4];
+    get(len - 1, x);
+    leaf_step<4>(A, x);
+  }
+  if (valid) leaf_store<4>(k, A, row, col, slot, len);
+}
+
+// BLDP_KURT_LEAF_TIMING_ILV 1 = TIMING EXPERIMENT ONLY (wrong numerics): the
+// reduce's access pattern on the leaves -- the 4 waves of a workgroup stream
+// ONE leaf of 512 channels, two column halves x two waves interleaving the
+// rows (loads and a Float32 sum only), pricing a loader-wave design
+#ifndef BLDP_KURT_LEAF_TIMING_ILV
+#define BLDP_KURT_LEAF_TIMING_ILV 0
+#endif
+__global__ __launch_bounds__(kB)
+#if BLDP_KURT_LEAF_WAVES > 0
+__attribute__((amdgpu_waves_per_eu(1, BLDP_KURT_LEAF_WAVES)))
+#endif
+void k_kurt_leaf_ilv_timing(const KurtArgs k) {
+  constexpr int B = BLDP_KURT_LEAF_B;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t r = blockIdx.x;  // (row, slot); 2 column halves of 256 channels
+  const int64_t slot = r % k.nslot, row = r / k.nslot;
+  const int64_t col = (wave & 1) * 64 + lane;
+  const int par = wave >> 1;
+  if (row >= k.nrow || col >= k.nc / 4) return;
+  int64_t t0, len;
+  pw_leaf(k.nt, k.K, slot, t0, len);
+  if (len <= 0) return;
+  const int bank = (int)(row / k.ni);
+  const int64_t i = row - (int64_t)bank * k.ni;
+  const int64_t ld = k.in_ld_t;
+  const float *p = k.in[bank] + k.in_off + i * k.in_ld_i + 4 * col + (t0 + par) * ld;
+  const int64_t nr = (len - par + 1) / 2;
+  float s4[4] = {0.f, 0.f, 0.f, 0.f};
+  int64_t t = 0;
+  for (; t + B <= nr; t += B) {
+    float4 v[B];
+#pragma unroll
+    for (int q = 0; q < B; ++q) v[q] = ldnt(p + (t + q) * 2 * ld);
+#pragma unroll
+    for (int q = 0; q < B; ++q) {
+      s4[0] += v[q].x; s4[1] += v[q].y; s4[2] += v[q].z; s4[3] += v[q].w;
+    }
+  }
+  for (; t < nr; ++t) {
+    const float4 v = ldnt(p + t * 2 * ld);
+    s4[0] += v.x; s4[1] += v.y; s4[2] += v.z; s4[3] += v.w;
+  }
+  if (par == 0) {
+    const int64_t n = k.nrow * k.nc, e = row * k.nc + 4 * col;
+    stw<4, float>(k.pf + slot * n + e, s4);
+  }
+}
+
 // 16-byte-aligned windows: the same leaf stream, fed through a per-wave LDS
 // ring of R spectra (1 KiB each: 64 lanes x 4 channels) that
 // global_load_lds_dwordx4 fills.  The loads have no VGPR destination, so R
@@ -1236,7 +1380,12 @@ hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s) {
     k.pm = reinterpret_cast<double *>(ws + L.a_pm);
     k.pf = reinterpret_cast<float *>(ws + L.a_pf);
     const dim3 g1((unsigned)cdivk(k.nrow * k.nslot * k.nseg, 4));
-    if (BLDP_KURT_LEAF_LDS > 0 && kLeafW == 4 && k.rows16)
+    if (BLDP_KURT_LEAF_ILV && kLeafW == 4)
+      hipLaunchKernelGGL(k_kurt_leaf_ilv, dim3((unsigned)(k.nrow * k.nslot * ((k.nseg + 1) / 2))),
+                         block, 0, s, k);
+    else if (BLDP_KURT_LEAF_TIMING_ILV && k.nc == 512)
+      hipLaunchKernelGGL(k_kurt_leaf_ilv_timing, dim3((unsigned)(k.nrow * k.nslot)), block, 0, s, k);
+    else if (BLDP_KURT_LEAF_LDS > 0 && kLeafW == 4 && k.rows16)
       hipLaunchKernelGGL(k_kurt_leaf_lds, g1, block, 0, s, k);
     else
       hipLaunchKernelGGL(k_kurt_leaf, g1, block, 0, s, k);
@@ -1272,7 +1421,9 @@ int64_t kurtosis_max_grid(const KurtArgs &k) {
   switch (p) {
     case KP_REGS: return cdivk(ncols, kB) * k.nrow;
     case KP_MID: return cdivk(k.nc, 64) * k.nrow;  // (k_kurt_mid2: half of it)
-    case KP_LEAF: return cdivk(k.nrow * k.nslot * k.nseg, 4);
+    case KP_LEAF:
+      return BLDP_KURT_LEAF_ILV && kLeafW == 4 ? k.nrow * k.nslot * ((k.nseg + 1) / 2)
+                                               : cdivk(k.nrow * k.nslot * k.nseg, 4);
     default:
       return std::max(cdivk(k.nc, kB) * k.nrow * k.nslot,
                       cdivk(cdivk(k.nc, 64), 4 / k.ts) * k.nrow * k.nchunk);

@@ -67,6 +67,13 @@ VARIANTS = {
     "kleaflow4": "-DBLDP_KURT_LEAF_TIMING_LOADONLY=1 -DBLDP_KURT_LEAF_WAVES=4",
     "kleaflob8w4": "-DBLDP_KURT_LEAF_TIMING_LOADONLY=1 -DBLDP_KURT_LEAF_B=8 -DBLDP_KURT_LEAF_WAVES=4",
     "kleaflob8": "-DBLDP_KURT_LEAF_TIMING_LOADONLY=1 -DBLDP_KURT_LEAF_B=8",
+    "kleafilv": "-DBLDP_KURT_LEAF_TIMING_ILV=1",  # timing only: reduce-like leaf streams
+    "kleafilvb8": "-DBLDP_KURT_LEAF_TIMING_ILV=1 -DBLDP_KURT_LEAF_B=8",
+    "kleafilvw4": "-DBLDP_KURT_LEAF_TIMING_ILV=1 -DBLDP_KURT_LEAF_WAVES=4",
+    "kilv": "-DBLDP_KURT_LEAF_ILV=1",  # k_kurt_leaf_ilv (bit-identical to base)
+    "kilvb2": "-DBLDP_KURT_LEAF_ILV=1 -DBLDP_KURT_ILV_B=2",
+    "kilvb8": "-DBLDP_KURT_LEAF_ILV=1 -DBLDP_KURT_ILV_B=8",
+    "kleafilvw2": "-DBLDP_KURT_LEAF_TIMING_ILV=1 -DBLDP_KURT_LEAF_WAVES=2",
     # k_kurt_mid with two channels per lane (512-byte wave loads), 8 or 4 waves
     "kmid2w8": "-DBLDP_KURT_MID_CPL=2 -DBLDP_KURT_MID_NW=8",
     "kmid2w4": "-DBLDP_KURT_MID_CPL=2 -DBLDP_KURT_MID_NW=4",
