@@ -66,6 +66,7 @@ struct RedArgs {
   int32_t k4;              // float4 loads per lane per row (vector path)
   int32_t vec_out;         // narrow path: 16/8-byte output stores are legal
   int64_t gpt;             // tile path: output channels (groups) per workgroup tile
+  int32_t tpb;             // row path: time blocks per workgroup (k_reduce_rowt when > 1)
   float div;               // F*T, the mean divisor
 };
 

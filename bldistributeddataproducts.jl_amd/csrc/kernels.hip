@@ -812,6 +812,73 @@ void k_reduce_row(const RedArgs a) {
            finish<OP>(s, a));
 }
 
+// The row path for short time blocks (T = 1, 2, 4: tavby = 1 is the
+// reference's own fqav, src/gbtworkerfunctions.jl:16-20, with no time
+// integration).  k_reduce_row gives every workgroup one time block, so at T = 1
+// a workgroup reads a single 4 KiB row segment and the launch is dominated by
+// workgroup turnover (3.1 TB/s on the 0002 band at F = 16).  Here a workgroup
+// takes TPB = 16 / T consecutive time blocks of its 1024 channels: 16 rows in
+// flight per lane, as k_reduce_row at T = 16.  Each block is summed exactly as
+// k_reduce_row sums it (rows chained into the first accumulator, the same
+// folds), so the results are bit-identical to it.
+//   BLDP_ROW_TPB  1 (default) = use it for T in {1, 2, 4}; 0 = k_reduce_row
+#ifndef BLDP_ROW_TPB
+#define BLDP_ROW_TPB 1
+#endif
+//   BLDP_ROWT_MAXWAVES  cap on resident waves per SIMD for k_reduce_rowt (0 = none)
+//                      6 (default): A/B against 4 and none, profiles/r02/ab_row_tpb.json
+#ifndef BLDP_ROWT_MAXWAVES
+#define BLDP_ROWT_MAXWAVES 6
+#endif
+template <int OP, int G4, int T>
+__global__ __launch_bounds__(kBlock)
+#if BLDP_ROWT_MAXWAVES > 0
+__attribute__((amdgpu_waves_per_eu(1, BLDP_ROWT_MAXWAVES)))
+#endif
+void k_reduce_rowt(const RedArgs a) {
+  constexpr int TPB = 16 / T, NR = TPB * T;
+  const int tid = threadIdx.x;
+  const uint32_t it = blockIdx.y, ni = (uint32_t)a.ni;
+  const uint32_t tg = it / ni, i = it - tg * ni;
+  const int bank = blockIdx.z;
+  const int64_t col = (int64_t)blockIdx.x * kBlock + tid;  // float4 column of the window
+  const bool valid = col < a.nco * G4;
+  const int64_t to0 = (int64_t)tg * TPB;
+  const int nb = (int)min((int64_t)TPB, a.nto - to0);  // time blocks of this workgroup
+  const float id = R<OP>::id();
+  float4 v[NR];
+  if (valid) {
+    const float *p = a.in[bank] + a.in_off + (int64_t)i * a.in_ld_i + to0 * T * a.in_ld_t + 4 * col;
+    const int64_t ld = a.in_ld_t;
+#pragma unroll
+    for (int u = 0; u < NR; ++u)
+      if (u < nb * T) v[u] = ld4(p + u * ld);
+  }
+#pragma unroll
+  for (int b = 0; b < TPB; ++b) {
+    if (b < nb) {  // (uniform)
+    // k_reduce_row's accumulators for a block of T < 16 rows: the rows chained
+    // into the first, the others left at the identity; its pairwise fold of
+    // them then amounts to one more op with the identity (f is idempotent
+    // there), which is all that is done here
+    const float4 id4 = make_float4(id, id, id, id);
+    float4 acc = id4;
+    if (valid) {
+#pragma unroll
+      for (int r = 0; r < T; ++r) acc = f4<OP>(acc, v[b * T + r]);
+    }
+    if constexpr (kNacc > 1) acc = f4<OP>(acc, id4);
+    float s = fold4<OP>(acc);
+#pragma unroll
+    for (int off = G4 / 2; off > 0; off >>= 1) s = R<OP>::f(s, __shfl_xor(s, off, 64));
+    if (valid && (tid & (G4 - 1)) == 0)
+      st1<1>(a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + (to0 + b) * a.out_ld_t +
+                 col / G4,
+             finish<OP>(s, a));
+    }
+  }
+}
+
 template <int OP, int F>
 __global__ __launch_bounds__(kBlock) void k_reduce_narrow(const RedArgs a) {
   for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) narrow_tile<OP, F>(a, t);
@@ -989,6 +1056,28 @@ template <int OP>
 hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
   hipError_t e = hipSuccess;
   const dim3 grid((unsigned)p.grid), block(kBlock);
+  if (p.path == PATH_VEC_ROW && a.tpb > 1) {  // short time blocks, several per workgroup
+    const dim3 g3((unsigned)a.blocks_c, (unsigned)(a.ni * cdiv(a.nto, a.tpb)), (unsigned)a.nbank);
+#define BLDP_ROWT(T)                                                                     \
+  switch (a.F / 4) {                                                                     \
+    case 1: hipLaunchKernelGGL((k_reduce_rowt<OP, 1, T>), g3, block, 0, s, a); break;    \
+    case 2: hipLaunchKernelGGL((k_reduce_rowt<OP, 2, T>), g3, block, 0, s, a); break;    \
+    case 4: hipLaunchKernelGGL((k_reduce_rowt<OP, 4, T>), g3, block, 0, s, a); break;    \
+    case 8: hipLaunchKernelGGL((k_reduce_rowt<OP, 8, T>), g3, block, 0, s, a); break;    \
+    case 16: hipLaunchKernelGGL((k_reduce_rowt<OP, 16, T>), g3, block, 0, s, a); break;  \
+    case 32: hipLaunchKernelGGL((k_reduce_rowt<OP, 32, T>), g3, block, 0, s, a); break;  \
+    case 64: hipLaunchKernelGGL((k_reduce_rowt<OP, 64, T>), g3, block, 0, s, a); break;  \
+    default: return hipErrorInvalidValue;                                                \
+  }
+    switch (a.T) {
+      case 1: BLDP_ROWT(1) break;
+      case 2: BLDP_ROWT(2) break;
+      case 4: BLDP_ROWT(4) break;
+      default: return hipErrorInvalidValue;
+    }
+#undef BLDP_ROWT
+    return hipGetLastError();
+  }
   if (p.path == PATH_VEC_ROW) {
     const dim3 g3((unsigned)a.blocks_c, (unsigned)(a.ni * a.nto), (unsigned)a.nbank);
     switch (a.F / 4) {
@@ -1070,6 +1159,7 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
   int64_t tiles;  // independent wave/thread tiles before any time split
   a.ts = 1;
   a.k4 = 1;
+  a.tpb = 1;
   if (aligned && F % 4 == 0) {
     p.path = PATH_VEC;
     const int64_t g4 = F / 4;
@@ -1149,6 +1239,11 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
     a.blocks_c = cdiv(a.nco * (F / 4), kBlock);
     a.ntiles = a.blocks_c * a.ni * a.nto * a.nbank;
     p.grid = a.ntiles;
+    if (BLDP_ROW_TPB && (T == 1 || T == 2 || T == 4) && a.nto > 1) {  // k_reduce_rowt
+      a.tpb = (int32_t)(16 / T);
+      a.ntiles = a.blocks_c * a.ni * cdiv(a.nto, a.tpb) * a.nbank;
+      p.grid = a.ntiles;
+    }
   }
   // narrow-path vector stores
   a.vec_out = 0;

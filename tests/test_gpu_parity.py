@@ -147,6 +147,37 @@ def test_reduce_row_integer_exact(eng, orc, shape):
     assert same_bits(got, orc.stitch([orc.reduce(host(eng, b), F, T) for b in banks]))
 
 
+# Short time blocks (T in {1, 2, 4}; T = 1 is the reference's fqav with no
+# time integration): k_reduce_rowt takes 16 / T time blocks per workgroup,
+# the last group partial; bit-exact, and the same bits k_reduce_row gives.
+ROWT_SHAPES = [(1025, 2, 37, 16, 1), (64, 1, 279, 64, 1), (33, 3, 10, 4, 2), (257, 1, 28, 256, 4),
+               (300, 2, 1, 8, 1)]
+
+
+@pytest.mark.parametrize("shape", ROWT_SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_reduce_short_time_blocks_integer_exact(eng, orc, shape):
+    nco, ni, nt, F, T = shape
+    x = eng.synth(nco * F, ni, nt, 1024, seed=7 * nco + F, kind=1)
+    a = host(eng, x)
+    nto = nt // T
+    tpb = 16 // T if nto > 1 else 1
+    for op in ("sum", "max", "min", "mean"):
+        plan = eng.plan(x, F, T, op)
+        assert plan["path"] == "row", (shape, plan)
+        blocks_c = -(-(nco * F // 4) // 256)
+        assert plan["workgroups"] == blocks_c * ni * -(-nto // tpb), (shape, plan)
+        got = host(eng, eng.reduce(x, F, T, op))
+        assert same_bits(got, orc.reduce(a, F, T, op)), (shape, op)
+    # a time window starting inside the data, and a band of three banks
+    if nt > T:
+        w = [0, nco * F, 1, 0, ni, 1, 1, (nt - 1) // T * T, 1]
+        got = host(eng, eng.reduce(x, F, T, "sum", w))
+        assert same_bits(got, orc.reduce(a, F, T, "sum", w)), (shape, "window")
+    banks = [x] + [eng.synth(nco * F, ni, nt, 1024, seed=b, kind=1) for b in (1, 2)]
+    got = host(eng, eng.band_reduce(banks, F, T))
+    assert same_bits(got, orc.stitch([orc.reduce(host(eng, b), F, T) for b in banks]))
+
+
 # Time integration (fqavby = 1, the narrow kernel): partial last segments,
 # several IFs / time blocks / banks, every op, a time-offset window.
 TIME_SHAPES = [(4100, 1, 32, 16), (4096, 3, 40, 5), (1 << 20, 2, 48, 16), (1 << 23, 1, 16, 16),

@@ -45,6 +45,13 @@ VARIANTS = {
     "misf2": "-DBLDP_NARROW_MIS=2",  # F = 2 on the realigning narrow kernel too
     "kpnocap": "-DBLDP_KURT_PASS_MAXWAVES=0",
     "rownocap": "-DBLDP_ROW_MAXWAVES=0",
+    "rowmw3": "-DBLDP_ROW_MAXWAVES=3",
+    "rowmw5": "-DBLDP_ROW_MAXWAVES=5",
+    "rowmw6": "-DBLDP_ROW_MAXWAVES=6",
+    "norowt": "-DBLDP_ROW_TPB=0",  # k_reduce_row for short time blocks too (one block per WG)
+    "rowtmw6": "-DBLDP_ROWT_MAXWAVES=6",
+    "rowtmw4": "-DBLDP_ROWT_MAXWAVES=4",
+    "rowtmw8": "-DBLDP_ROWT_MAXWAVES=0",
     # narrow windows: time split over otherwise idle waves, with / without grid cap
     "notsfill": "-DBLDP_TS_FILL=0",
 
@@ -178,6 +185,19 @@ def run(names, rounds, iters, suite="main"):
         kurt_case("kurt cfg4 c0=1", b4, [1, 508, 1, 0, 1, 1, 0, 879616, 1])
         kurt_case("kurt 65536ch nt2048 c0=3", b5, [3, 65532, 1, 0, 1, 1, 0, 2048, 1])
         cases_done = True
+    elif suite == "row":  # the 0002-product reduce (k_reduce_row)
+        del b3
+        b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
+        band_case("cfg2 F64 T16", b2, 64, 16, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
+        band_case("cfg1 F64 T16", b2[:1], 64, 16, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
+        band_case("cfg2 F16 T1", b2, 16, 1, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
+        band_case("cfg2 F64 T9 whole", b2, 64, 9, [0, 65536, 1, 0, 1, 1, 0, 279, 1])
+        band_case("cfg2 F64 T1 whole", b2, 64, 1)
+        band_case("cfg1 F64 T1 whole", b2[:1], 64, 1)
+        band_case("cfg2 F4 T1 whole", b2, 4, 1)
+        band_case("cfg2 F256 T2", b2, 256, 2, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
+        band_case("cfg2 F64 T4", b2, 64, 4, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
+        cases_done = True
     elif suite == "kmid":  # the register-tile kurtosis path (0002 products)
         del b3
         b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
@@ -283,7 +303,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--suite", default="main", choices=["main", "tile", "kurt", "kleaf", "kmid"])
+    ap.add_argument("--suite", default="main", choices=["main", "tile", "kurt", "kleaf", "kmid", "row"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:
