@@ -67,6 +67,7 @@ struct RedArgs {
   int32_t vec_out;         // narrow path: 16/8-byte output stores are legal
   int64_t gpt;             // tile path: output channels (groups) per workgroup tile
   int32_t tpb;             // row path: time blocks per workgroup (k_reduce_rowt when > 1)
+  int32_t tsub_log2;       // k_reduce_rowt: log2 of the time groups sharing a workgroup
   float div;               // F*T, the mean divisor
 };
 

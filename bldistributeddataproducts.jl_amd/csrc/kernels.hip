@@ -825,6 +825,11 @@ void k_reduce_row(const RedArgs a) {
 #ifndef BLDP_ROW_TPB
 #define BLDP_ROW_TPB 1
 #endif
+//   BLDP_ROWT_PACK  1 (default) = windows of <= 128 float4 columns share a
+//                  workgroup between 2 or 4 time groups (no idle lanes)
+#ifndef BLDP_ROWT_PACK
+#define BLDP_ROWT_PACK 1
+#endif
 //   BLDP_ROWT_MAXWAVES  cap on resident waves per SIMD for k_reduce_rowt (0 = none)
 //                      6 (default): A/B against 4 and none, profiles/r02/ab_row_tpb.json
 #ifndef BLDP_ROWT_MAXWAVES
@@ -838,13 +843,19 @@ __attribute__((amdgpu_waves_per_eu(1, BLDP_ROWT_MAXWAVES)))
 void k_reduce_rowt(const RedArgs a) {
   constexpr int TPB = 16 / T, NR = TPB * T;
   const int tid = threadIdx.x;
-  const uint32_t it = blockIdx.y, ni = (uint32_t)a.ni;
-  const uint32_t tg = it / ni, i = it - tg * ni;
+  // grid: x = (column block, time group) column block fastest, y = IF, z = bank.
+  // Windows of <= 128 float4 columns (the 512-channel 0001 product) share a
+  // workgroup between 2^tsub_log2 time groups, 256 >> tsub_log2 lanes each.
+  const uint32_t bx = blockIdx.x, bc = (uint32_t)a.blocks_c;
+  const int sh = a.tsub_log2, cw = kBlock >> sh;
+  const uint32_t tq = bx / bc, i = blockIdx.y;
+  const int64_t tg = ((int64_t)tq << sh) + (tid >> (8 - sh));  // (kBlock = 256)
   const int bank = blockIdx.z;
-  const int64_t col = (int64_t)blockIdx.x * kBlock + tid;  // float4 column of the window
-  const bool valid = col < a.nco * G4;
-  const int64_t to0 = (int64_t)tg * TPB;
-  const int nb = (int)min((int64_t)TPB, a.nto - to0);  // time blocks of this workgroup
+  const int64_t col = (int64_t)(bx - tq * bc) * kBlock + (tid & (cw - 1));  // float4 column
+  const int64_t to0 = tg * TPB;
+  const bool valid = col < a.nco * G4 && to0 < a.nto;
+  // time blocks of this lane's group (uniform over each wave: groups hold >= 64 lanes)
+  const int nb = (int)max((int64_t)0, min((int64_t)TPB, a.nto - to0));
   const float id = R<OP>::id();
   float4 v[NR];
   if (valid) {
@@ -1057,7 +1068,8 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
   hipError_t e = hipSuccess;
   const dim3 grid((unsigned)p.grid), block(kBlock);
   if (p.path == PATH_VEC_ROW && a.tpb > 1) {  // short time blocks, several per workgroup
-    const dim3 g3((unsigned)a.blocks_c, (unsigned)(a.ni * cdiv(a.nto, a.tpb)), (unsigned)a.nbank);
+    const dim3 g3((unsigned)(a.blocks_c * cdiv(cdiv(a.nto, a.tpb), 1 << a.tsub_log2)),
+                  (unsigned)a.ni, (unsigned)a.nbank);
 #define BLDP_ROWT(T)                                                                     \
   switch (a.F / 4) {                                                                     \
     case 1: hipLaunchKernelGGL((k_reduce_rowt<OP, 1, T>), g3, block, 0, s, a); break;    \
@@ -1160,6 +1172,7 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
   a.ts = 1;
   a.k4 = 1;
   a.tpb = 1;
+  a.tsub_log2 = 0;
   if (aligned && F % 4 == 0) {
     p.path = PATH_VEC;
     const int64_t g4 = F / 4;
@@ -1233,15 +1246,25 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
   // small power-of-two groups, whole time block per tile, no time split:
   // the lean row kernel (3-D grid, so every dimension must fit)
   if (BLDP_VEC_ROW && p.path == PATH_VEC && a.k4 == 1 && a.ts == 1 && a.nchunk == 1 &&
-      F >= 4 && F <= 256 && (F & (F - 1)) == 0 && cdiv(a.nco * (F / 4), kBlock) <= INT32_MAX &&
-      a.ni * a.nto <= 65535 && a.nbank <= 65535) {
-    p.path = PATH_VEC_ROW;
-    a.blocks_c = cdiv(a.nco * (F / 4), kBlock);
-    a.ntiles = a.blocks_c * a.ni * a.nto * a.nbank;
-    p.grid = a.ntiles;
-    if (BLDP_ROW_TPB && (T == 1 || T == 2 || T == 4) && a.nto > 1) {  // k_reduce_rowt
-      a.tpb = (int32_t)(16 / T);
-      a.ntiles = a.blocks_c * a.ni * cdiv(a.nto, a.tpb) * a.nbank;
+      F >= 4 && F <= 256 && (F & (F - 1)) == 0 && a.nbank <= 65535) {
+    const int64_t bc = cdiv(a.nco * (F / 4), kBlock);
+    // short time blocks: 16 / T of them per workgroup (k_reduce_rowt; grid x =
+    // column blocks x time groups, so long 0001-product windows fit too)
+    const int64_t tpb = (T == 1 || T == 2 || T == 4) ? 16 / T : 1;
+    if (BLDP_ROW_TPB && tpb > 1 && a.nto > 1 && bc * cdiv(a.nto, tpb) <= INT32_MAX &&
+        a.ni <= 65535) {
+      p.path = PATH_VEC_ROW;
+      a.blocks_c = bc;
+      a.tpb = (int32_t)tpb;
+      // <= 128 float4 columns: 2 or 4 time groups per workgroup (>= 64 lanes each)
+      const int64_t cols = a.nco * (F / 4);
+      a.tsub_log2 = BLDP_ROWT_PACK ? (cols <= 64 ? 2 : cols <= 128 ? 1 : 0) : 0;
+      a.ntiles = bc * cdiv(cdiv(a.nto, tpb), (int64_t)1 << a.tsub_log2) * a.ni * a.nbank;
+      p.grid = a.ntiles;
+    } else if (bc <= INT32_MAX && a.ni * a.nto <= 65535) {
+      p.path = PATH_VEC_ROW;
+      a.blocks_c = bc;
+      a.ntiles = a.blocks_c * a.ni * a.nto * a.nbank;
       p.grid = a.ntiles;
     }
   }

@@ -149,9 +149,11 @@ def test_reduce_row_integer_exact(eng, orc, shape):
 
 # Short time blocks (T in {1, 2, 4}; T = 1 is the reference's fqav with no
 # time integration): k_reduce_rowt takes 16 / T time blocks per workgroup,
-# the last group partial; bit-exact, and the same bits k_reduce_row gives.
+# the last group partial, and windows of <= 128 float4 columns (the 512-channel
+# 0001 product) share a workgroup between 2 or 4 time groups; bit-exact, and
+# the same bits k_reduce_row gives.
 ROWT_SHAPES = [(1025, 2, 37, 16, 1), (64, 1, 279, 64, 1), (33, 3, 10, 4, 2), (257, 1, 28, 256, 4),
-               (300, 2, 1, 8, 1)]
+               (300, 2, 1, 8, 1), (64, 1, 200, 8, 1), (64, 2, 150, 8, 2), (20, 1, 70, 8, 1)]
 
 
 @pytest.mark.parametrize("shape", ROWT_SHAPES, ids=lambda s: "x".join(map(str, s)))
@@ -161,11 +163,13 @@ def test_reduce_short_time_blocks_integer_exact(eng, orc, shape):
     a = host(eng, x)
     nto = nt // T
     tpb = 16 // T if nto > 1 else 1
+    cols = nco * F // 4  # float4 columns; <= 128 of them: 2 or 4 time groups per workgroup
+    tsub = 1 if tpb == 1 else 4 if cols <= 64 else 2 if cols <= 128 else 1
     for op in ("sum", "max", "min", "mean"):
         plan = eng.plan(x, F, T, op)
         assert plan["path"] == "row", (shape, plan)
-        blocks_c = -(-(nco * F // 4) // 256)
-        assert plan["workgroups"] == blocks_c * ni * -(-nto // tpb), (shape, plan)
+        blocks_c = -(-cols // 256)
+        assert plan["workgroups"] == blocks_c * ni * -(-(-(-nto // tpb)) // tsub), (shape, plan)
         got = host(eng, eng.reduce(x, F, T, op))
         assert same_bits(got, orc.reduce(a, F, T, op)), (shape, op)
     # a time window starting inside the data, and a band of three banks

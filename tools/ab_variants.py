@@ -51,6 +51,7 @@ VARIANTS = {
     "norowt": "-DBLDP_ROW_TPB=0",  # k_reduce_row for short time blocks too (one block per WG)
     "rowtmw6": "-DBLDP_ROWT_MAXWAVES=6",
     "rowtmw4": "-DBLDP_ROWT_MAXWAVES=4",
+    "rowtnopack": "-DBLDP_ROWT_PACK=0",
     "rowtmw8": "-DBLDP_ROWT_MAXWAVES=0",
     # narrow windows: time split over otherwise idle waves, with / without grid cap
     "notsfill": "-DBLDP_TS_FILL=0",
@@ -185,6 +186,20 @@ def run(names, rounds, iters, suite="main"):
         kurt_case("kurt cfg4 c0=1", b4, [1, 508, 1, 0, 1, 1, 0, 879616, 1])
         kurt_case("kurt 65536ch nt2048 c0=3", b5, [3, 65532, 1, 0, 1, 1, 0, 2048, 1])
         cases_done = True
+    elif suite == "t1":  # no time integration (the reference's own fqav) on every product
+        n = 1 << 26
+        band_case("cfg3 F1024 T1", b3, 1024, 1)
+        band_case("cfg3 F1024 T16", b3, 1024, 16)
+        band_case("cfg3 F64 T1", b3, 64, 1)
+        band_case("cfg3 F4096 T1", b3, 4096, 1)
+        band_case("cfg3 F1 T16", b3, 1, 16)
+        band_case("cfg3 F2 T1", b3, 2, 1)
+        del b3
+        b4 = [eng.synth(512, 1, 880000, 8, seed=10 * b + 1, kind=0) for b in range(8)]
+        band_case("cfg4 F8 T1", b4, 8, 1, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
+        band_case("cfg4 F64 T1", b4, 64, 1, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
+        band_case("cfg4 F8 T1024", b4, 8, 1024, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
+        cases_done = True
     elif suite == "row":  # the 0002-product reduce (k_reduce_row)
         del b3
         b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
@@ -303,7 +318,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--suite", default="main", choices=["main", "tile", "kurt", "kleaf", "kmid", "row"])
+    ap.add_argument("--suite", default="main", choices=["main", "tile", "kurt", "kleaf", "kmid", "row", "t1"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:
