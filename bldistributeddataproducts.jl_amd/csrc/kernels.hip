@@ -890,6 +890,81 @@ void k_reduce_rowt(const RedArgs a) {
   }
 }
 
+// Large groups (F = 512..4096: 64 lanes x K4 float4 per row, one output per
+// wave per time block) with short time blocks (T = 1, 2, 4) on windows where
+// the interleaved kernel is a poor fit (few groups per row, or more (IF, time
+// block) pairs than its 3-D grid holds): e.g. fqavby = 512 on the 512-channel
+// 0001 product, one output per spectrum, which k_reduce_vec ran one row per
+// 4-wave workgroup (0.95 TB/s).  Each wave owns one group and RW consecutive
+// time blocks, TB of them per batch (>= 16 loads per lane in flight); a time
+// block is summed exactly as k_reduce_vec sums it (its batched and remainder
+// accumulator patterns, the same folds), so the results are bit-identical.
+//   BLDP_WAVET  1 (default) = use it where the interleaved kernel cannot run or a
+//               row holds fewer than 4 groups; 0 = never
+#ifndef BLDP_WAVET
+#define BLDP_WAVET 1
+#endif
+template <int OP, int K4, int T>
+__global__ __launch_bounds__(kBlock) void k_reduce_wavet(const RedArgs a) {
+  constexpr int TB = (16 / (T * K4)) > 0 ? 16 / (T * K4) : 1;  // time blocks per batch
+  constexpr int NBAT = 4, RW = TB * NBAT;                        // per wave
+  // k_reduce_vec's accumulation of one time block: K4 in {2, 4} take RB-row
+  // batches (accumulator (u * K4 + k) % kNacc) then single rows (k % kNacc);
+  // K4 >= 8 always the latter
+  constexpr int RB = (K4 == 2 || K4 == 4) ? (K4 >= BLDP_BATCH ? 1 : BLDP_BATCH / K4) : 0;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t bx = blockIdx.x, g = bx % a.nco, chunk = bx / a.nco;
+  const int64_t i = blockIdx.y;
+  const int bank = blockIdx.z;
+  const int64_t tb0 = (chunk * 4 + wave) * RW;
+  const float id = R<OP>::id();
+  const float *base = a.in[bank] + a.in_off + i * a.in_ld_i + g * a.F + 4 * lane;
+  const int64_t ld = a.in_ld_t;
+  for (int bt = 0; bt < NBAT; ++bt) {
+    const int64_t t0 = tb0 + (int64_t)bt * TB;
+    if (t0 >= a.nto) break;  // (uniform over the wave)
+    const int nb = (int)min((int64_t)TB, a.nto - t0);
+    float4 v[TB * T * K4];
+#pragma unroll
+    for (int b = 0; b < TB; ++b)
+#pragma unroll
+      for (int r = 0; r < T; ++r)
+#pragma unroll
+        for (int k = 0; k < K4; ++k)
+          if (b < nb) v[(b * T + r) * K4 + k] = ld4(base + ((t0 + b) * T + r) * ld + 256 * k);
+#pragma unroll
+    for (int b = 0; b < TB; ++b) {
+      if (b < nb) {
+        float4 acc[kNacc];
+#pragma unroll
+        for (int q = 0; q < kNacc; ++q) acc[q] = make_float4(id, id, id, id);
+        int r = 0;
+        if constexpr (RB > 0) {
+#pragma unroll
+          for (; r + RB <= T; r += RB)
+#pragma unroll
+            for (int u = 0; u < RB; ++u)
+#pragma unroll
+              for (int k = 0; k < K4; ++k)
+                acc[(u * K4 + k) % kNacc] =
+                    f4<OP>(acc[(u * K4 + k) % kNacc], v[(b * T + r + u) * K4 + k]);
+        }
+#pragma unroll
+        for (; r < T; ++r)
+#pragma unroll
+          for (int k = 0; k < K4; ++k)
+            acc[k % kNacc] = f4<OP>(acc[k % kNacc], v[(b * T + r) * K4 + k]);
+        float s = fold4<OP>(fold_acc<OP>(acc));
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) s = R<OP>::f(s, __shfl_xor(s, off, 64));
+        if (lane == 0)
+          st1<1>(a.out + bank * a.out_bank + i * a.out_ld_i + (t0 + b) * a.out_ld_t + g,
+                 finish<OP>(s, a));
+      }
+    }
+  }
+}
+
 template <int OP, int F>
 __global__ __launch_bounds__(kBlock) void k_reduce_narrow(const RedArgs a) {
   for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) narrow_tile<OP, F>(a, t);
@@ -1067,6 +1142,31 @@ template <int OP>
 hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
   hipError_t e = hipSuccess;
   const dim3 grid((unsigned)p.grid), block(kBlock);
+  if (p.path == PATH_VEC && a.tpb > 1) {  // large groups, short time blocks: k_reduce_wavet
+    constexpr int NW = 4 * 4;  // time blocks per batch x batches: see k_reduce_wavet
+    (void)NW;
+    const int64_t rw = (int64_t)a.tpb;  // time blocks per wave
+    const dim3 g3((unsigned)(a.nco * cdiv(a.nto, 4 * rw)), (unsigned)a.ni, (unsigned)a.nbank);
+#define BLDP_WAVETL(K, T) hipLaunchKernelGGL((k_reduce_wavet<OP, K, T>), g3, block, 0, s, a); break;
+#define BLDP_WAVET_T(K)                      \
+  switch (a.T) {                             \
+    case 1: BLDP_WAVETL(K, 1)                \
+    case 2: BLDP_WAVETL(K, 2)                \
+    case 4: BLDP_WAVETL(K, 4)                \
+    default: return hipErrorInvalidValue;    \
+  }                                          \
+  break;
+    switch (a.k4) {
+      case 2: BLDP_WAVET_T(2)
+      case 4: BLDP_WAVET_T(4)
+      case 8: BLDP_WAVET_T(8)
+      case 16: BLDP_WAVET_T(16)
+      default: return hipErrorInvalidValue;
+    }
+#undef BLDP_WAVET_T
+#undef BLDP_WAVETL
+    return hipGetLastError();
+  }
   if (p.path == PATH_VEC_ROW && a.tpb > 1) {  // short time blocks, several per workgroup
     const dim3 g3((unsigned)(a.blocks_c * cdiv(cdiv(a.nto, a.tpb), 1 << a.tsub_log2)),
                   (unsigned)a.ni, (unsigned)a.nbank);
@@ -1233,9 +1333,23 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
   const int cap = BLDP_MAX_WG_PER_CU >= 0 ? BLDP_MAX_WG_PER_CU : (a.ts > 1 ? 4 : 0);
   if (cap > 0) p.grid = std::min<int64_t>(p.grid, (int64_t)cap * num_cus);
   p.grid = std::min<int64_t>(p.grid, INT32_MAX);  // tiles beyond: grid-stride loop
+  // large groups with short time blocks where the interleaved kernel is a
+  // poor fit (few groups per row, or its 3-D grid too small): k_reduce_wavet
+  // (path "vector", a.tpb = time blocks per wave)
+  if (BLDP_WAVET && p.path == PATH_VEC && p.lpg == 64 &&
+      (a.k4 == 2 || a.k4 == 4 || a.k4 == 8 || a.k4 == 16) && (T == 1 || T == 2 || T == 4) &&
+      a.ts == 1 && a.nchunk == 1 && (a.nco < 4 || a.ni * a.nto > 65535) && a.ni <= 65535 &&
+      a.nbank <= 65535) {
+    const int64_t tb = std::max<int64_t>(1, 16 / (T * a.k4)), rw = tb * 4;
+    if (a.nco * cdiv(a.nto, 4 * rw) <= INT32_MAX) {
+      a.tpb = (int32_t)rw;
+      a.ntiles = a.nco * cdiv(a.nto, 4 * rw) * a.ni * a.nbank;
+      p.grid = a.ntiles;
+    }
+  }
   // whole-time-block tiles of 512..4096-channel groups: interleaved kernel
   // (3-D grid, so every dimension must fit)
-  if (BLDP_VEC_IL && p.path == PATH_VEC && p.lpg == 64 &&
+  if (BLDP_VEC_IL && p.path == PATH_VEC && p.lpg == 64 && a.tpb == 1 &&
       (a.k4 == 2 || a.k4 == 4 || a.k4 == 8 || a.k4 == 16) && a.ts == 1 && a.nchunk == 1 &&
       cdiv(a.nco, BLDP_IL_GPW) <= INT32_MAX && a.ni * a.nto <= 65535 && a.nbank <= 65535) {
     p.path = PATH_VEC_IL;

@@ -182,6 +182,34 @@ def test_reduce_short_time_blocks_integer_exact(eng, orc, shape):
     assert same_bits(got, orc.stitch([orc.reduce(host(eng, b), F, T) for b in banks]))
 
 
+# Large groups (F = 512..4096) with short time blocks on windows with few
+# groups per row or more (IF, time block) pairs than the interleaved kernel's
+# grid holds (fqavby = 512 on the 512-channel 0001 product: one output per
+# spectrum): k_reduce_wavet, one wave per group and 4 x 16 / (T K4) time
+# blocks; bit-exact, and the same bits k_reduce_vec gives.
+WAVET_SHAPES = [(1, 1, 300, 512, 1), (2, 2, 40, 1024, 2), (3, 1, 64, 4096, 4), (1, 1, 66000, 512, 1),
+                (2, 1, 37, 2048, 1)]
+
+
+@pytest.mark.parametrize("shape", WAVET_SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_reduce_large_groups_short_time_blocks_integer_exact(eng, orc, shape):
+    nco, ni, nt, F, T = shape
+    x = eng.synth(nco * F, ni, nt, 1024, seed=3 * nco + F + nt, kind=1)
+    a = host(eng, x)
+    nto, k4 = nt // T, F // 256
+    rw = 4 * max(1, 16 // (T * k4))  # time blocks per wave
+    for op in ("sum", "max", "min", "mean"):
+        plan = eng.plan(x, F, T, op)
+        assert plan["path"] == "vector", (shape, plan)
+        assert plan["workgroups"] == nco * ni * -(-nto // (4 * rw)), (shape, plan)
+        got = host(eng, eng.reduce(x, F, T, op))
+        assert same_bits(got, orc.reduce(a, F, T, op)), (shape, op)
+    if nt > T:
+        w = [0, nco * F, 1, 0, ni, 1, 1, (nt - 1) // T * T, 1]
+        got = host(eng, eng.reduce(x, F, T, "sum", w))
+        assert same_bits(got, orc.reduce(a, F, T, "sum", w)), (shape, "window")
+
+
 # Time integration (fqavby = 1, the narrow kernel): partial last segments,
 # several IFs / time blocks / banks, every op, a time-offset window.
 TIME_SHAPES = [(4100, 1, 32, 16), (4096, 3, 40, 5), (1 << 20, 2, 48, 16), (1 << 23, 1, 16, 16),

@@ -52,6 +52,7 @@ VARIANTS = {
     "rowtmw6": "-DBLDP_ROWT_MAXWAVES=6",
     "rowtmw4": "-DBLDP_ROWT_MAXWAVES=4",
     "rowtnopack": "-DBLDP_ROWT_PACK=0",
+    "nowavet": "-DBLDP_WAVET=0",
     "rowtmw8": "-DBLDP_ROWT_MAXWAVES=0",
     # narrow windows: time split over otherwise idle waves, with / without grid cap
     "notsfill": "-DBLDP_TS_FILL=0",
@@ -200,6 +201,18 @@ def run(names, rounds, iters, suite="main"):
         band_case("cfg4 F64 T1", b4, 64, 1, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
         band_case("cfg4 F8 T1024", b4, 8, 1024, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
         cases_done = True
+    elif suite == "sweep":  # T = 1 (the reference's own fqav) over fqavby, every product
+        for F in (8, 256, 4096, 1 << 20):
+            band_case(f"0000 F{F} T1", b3, F, 1)
+        del b3
+        b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
+        for F in (2, 3, 8, 12, 128, 256, 1024, 65536):
+            band_case(f"0002 F{F} T1", b2, F, 1, [0, 65535 // F * F, 1, 0, 1, 1, 0, 279, 1])
+        del b2
+        b4 = [eng.synth(512, 1, 880000, 8, seed=10 * b + 1, kind=0) for b in range(8)]
+        for F in (2, 4, 16, 128, 512):
+            band_case(f"0001 F{F} T1", b4, F, 1, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
+        cases_done = True
     elif suite == "row":  # the 0002-product reduce (k_reduce_row)
         del b3
         b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
@@ -318,7 +331,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--suite", default="main", choices=["main", "tile", "kurt", "kleaf", "kmid", "row", "t1"])
+    ap.add_argument("--suite", default="main", choices=["main", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:
