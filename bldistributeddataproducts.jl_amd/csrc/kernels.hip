@@ -318,6 +318,71 @@ __device__ __forceinline__ void narrow_tile(const RedArgs &a, int64_t tile) {
   }
 }
 
+// The narrow path for short time blocks (T = 1, 2, 4; e.g. fqavby = 2 with
+// the reference's own fqav, no time integration), organised like
+// k_reduce_rowt: 16 / T time blocks per workgroup, 2 or 4 time groups per
+// workgroup for windows of <= 128 float4 columns.  Each block is summed and
+// stored exactly as narrow_tile does it (bit-identical).
+//   BLDP_NARROW_TPB  1 (default) = use it for T in {1, 2, 4}; 0 = k_reduce_narrow
+#ifndef BLDP_NARROW_TPB
+#define BLDP_NARROW_TPB 1
+#endif
+template <int OP, int F, int T>
+__global__ __launch_bounds__(kBlock)
+#if BLDP_ROWT_MAXWAVES > 0
+__attribute__((amdgpu_waves_per_eu(1, BLDP_ROWT_MAXWAVES)))
+#endif
+void k_reduce_narrowt(const RedArgs a) {
+  constexpr int TPB = 16 / T, NR = TPB * T;
+  const int tid = threadIdx.x;
+  const uint32_t bx = blockIdx.x, bc = (uint32_t)a.blocks_c;
+  const int sh = a.tsub_log2, cw = kBlock >> sh;
+  const uint32_t tq = bx / bc, i = blockIdx.y;
+  const int64_t tg = ((int64_t)tq << sh) + (tid >> (8 - sh));
+  const int bank = blockIdx.z;
+  const int64_t q4 = (int64_t)(bx - tq * bc) * kBlock + (tid & (cw - 1));  // float4 column
+  const int64_t to0 = tg * TPB;
+  if (q4 >= a.nco * F / 4 || to0 >= a.nto) return;  // (no cross-lane work below)
+  const int nb = (int)min((int64_t)TPB, a.nto - to0);
+  const float id = R<OP>::id();
+  const float4 id4 = make_float4(id, id, id, id);
+  const float *p = a.in[bank] + a.in_off + (int64_t)i * a.in_ld_i + to0 * T * a.in_ld_t + 4 * q4;
+  const int64_t ld = a.in_ld_t;
+  float4 v[NR];
+#pragma unroll
+  for (int u = 0; u < NR; ++u)
+    if (u < nb * T) v[u] = ld4(p + u * ld);
+  const int64_t co = q4 * (4 / F);
+#pragma unroll
+  for (int b = 0; b < TPB; ++b) {
+    if (b < nb) {
+      // narrow_tile's accumulators for T < BLDP_BATCH rows: chained into the
+      // first, then its fold with the identities = one op with the identity
+      float4 r = id4;
+#pragma unroll
+      for (int u = 0; u < T; ++u) r = f4<OP>(r, v[b * T + u]);
+      if constexpr (kNacc > 1) r = f4<OP>(r, id4);
+      float *o = a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + (to0 + b) * a.out_ld_t + co;
+      if (F == 1) {
+        r = make_float4(finish<OP>(r.x, a), finish<OP>(r.y, a), finish<OP>(r.z, a),
+                        finish<OP>(r.w, a));
+        if (a.vec_out) {
+          st4(o, r);
+        } else {
+          o[0] = r.x; o[1] = r.y; o[2] = r.z; o[3] = r.w;
+        }
+      } else {
+        const float x = finish<OP>(R<OP>::f(r.x, r.y), a), y = finish<OP>(R<OP>::f(r.z, r.w), a);
+        if (a.vec_out) {
+          *reinterpret_cast<float2 *>(o) = make_float2(x, y);
+        } else {
+          o[0] = x; o[1] = y;
+        }
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Narrow path for windows that start off a 16-byte boundary (unit channel
 // step, F = 1, e.g. idxs = (2:n, :, :) with time integration; F = 2 with
@@ -1142,6 +1207,19 @@ template <int OP>
 hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
   hipError_t e = hipSuccess;
   const dim3 grid((unsigned)p.grid), block(kBlock);
+  if (p.path == PATH_NARROW && a.tpb > 1) {  // short time blocks, several per workgroup
+    const dim3 g3((unsigned)(a.blocks_c * cdiv(cdiv(a.nto, a.tpb), 1 << a.tsub_log2)),
+                  (unsigned)a.ni, (unsigned)a.nbank);
+#define BLDP_NARROWT(FF, TT) hipLaunchKernelGGL((k_reduce_narrowt<OP, FF, TT>), g3, block, 0, s, a);
+    if (a.F == 1 && a.T == 2) { BLDP_NARROWT(1, 2) }
+    else if (a.F == 1 && a.T == 4) { BLDP_NARROWT(1, 4) }
+    else if (a.F == 2 && a.T == 1) { BLDP_NARROWT(2, 1) }
+    else if (a.F == 2 && a.T == 2) { BLDP_NARROWT(2, 2) }
+    else if (a.F == 2 && a.T == 4) { BLDP_NARROWT(2, 4) }
+    else return hipErrorInvalidValue;
+#undef BLDP_NARROWT
+    return hipGetLastError();
+  }
   if (p.path == PATH_VEC && a.tpb > 1) {  // large groups, short time blocks: k_reduce_wavet
     constexpr int NW = 4 * 4;  // time blocks per batch x batches: see k_reduce_wavet
     (void)NW;
@@ -1379,6 +1457,19 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
       p.path = PATH_VEC_ROW;
       a.blocks_c = bc;
       a.ntiles = a.blocks_c * a.ni * a.nto * a.nbank;
+      p.grid = a.ntiles;
+    }
+  }
+  // narrow path, short time blocks: k_reduce_narrowt (grid as k_reduce_rowt's)
+  if (BLDP_NARROW_TPB && p.path == PATH_NARROW && a.nchunk == 1 && (T == 1 || T == 2 || T == 4) &&
+      !(F == 1 && T == 1) && a.nto > 1 && a.ni <= 65535 && a.nbank <= 65535) {
+    const int64_t cols = a.nco * F / 4, tpb = 16 / T;
+    const int sh = cols <= 64 ? 2 : cols <= 128 ? 1 : 0;
+    const int64_t x = a.blocks_c * cdiv(cdiv(a.nto, tpb), (int64_t)1 << sh);
+    if (x <= INT32_MAX) {
+      a.tpb = (int32_t)tpb;
+      a.tsub_log2 = sh;
+      a.ntiles = x * a.ni * a.nbank;
       p.grid = a.ntiles;
     }
   }

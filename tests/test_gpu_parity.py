@@ -210,6 +210,32 @@ def test_reduce_large_groups_short_time_blocks_integer_exact(eng, orc, shape):
         assert same_bits(got, orc.reduce(a, F, T, "sum", w)), (shape, "window")
 
 
+# The narrow path (fqavby = 1, 2) with short time blocks: k_reduce_narrowt,
+# 16 / T time blocks per workgroup (2 or 4 time groups per workgroup on
+# windows of <= 128 float4 columns); bit-exact, the same bits as k_reduce_narrow.
+NARROWT_SHAPES = [(512, 1, 300, 2, 1), (128, 2, 50, 2, 2), (2048, 1, 32, 1, 4), (256, 3, 20, 1, 2),
+                  (6000, 1, 17, 2, 1)]
+
+
+@pytest.mark.parametrize("shape", NARROWT_SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_reduce_narrow_short_time_blocks_integer_exact(eng, orc, shape):
+    nco, ni, nt, F, T = shape
+    x = eng.synth(nco * F, ni, nt, 1024, seed=5 * nco + F + nt, kind=1)
+    a = host(eng, x)
+    nto, cols = nt // T, nco * F // 4
+    tsub = 4 if cols <= 64 else 2 if cols <= 128 else 1
+    for op in ("sum", "max", "min", "mean"):
+        plan = eng.plan(x, F, T, op)
+        assert plan["path"] == "narrow", (shape, plan)
+        assert plan["workgroups"] == -(-cols // 256) * ni * -(-(-(-nto // (16 // T))) // tsub), \
+            (shape, plan)
+        got = host(eng, eng.reduce(x, F, T, op))
+        assert same_bits(got, orc.reduce(a, F, T, op)), (shape, op)
+    w = [0, nco * F, 1, 0, ni, 1, 1, (nt - 1) // T * T, 1]
+    got = host(eng, eng.reduce(x, F, T, "sum", w))
+    assert same_bits(got, orc.reduce(a, F, T, "sum", w)), (shape, "window")
+
+
 # Time integration (fqavby = 1, the narrow kernel): partial last segments,
 # several IFs / time blocks / banks, every op, a time-offset window.
 TIME_SHAPES = [(4100, 1, 32, 16), (4096, 3, 40, 5), (1 << 20, 2, 48, 16), (1 << 23, 1, 16, 16),

@@ -53,6 +53,7 @@ VARIANTS = {
     "rowtmw4": "-DBLDP_ROWT_MAXWAVES=4",
     "rowtnopack": "-DBLDP_ROWT_PACK=0",
     "nowavet": "-DBLDP_WAVET=0",
+    "nonarrowt": "-DBLDP_NARROW_TPB=0",
     "rowtmw8": "-DBLDP_ROWT_MAXWAVES=0",
     # narrow windows: time split over otherwise idle waves, with / without grid cap
     "notsfill": "-DBLDP_TS_FILL=0",
@@ -212,6 +213,8 @@ def run(names, rounds, iters, suite="main"):
         b4 = [eng.synth(512, 1, 880000, 8, seed=10 * b + 1, kind=0) for b in range(8)]
         for F in (2, 4, 16, 128, 512):
             band_case(f"0001 F{F} T1", b4, F, 1, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
+        band_case("0001 F1 T2", b4, 1, 2, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
+        band_case("0001 F1 T4", b4, 1, 4, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
         cases_done = True
     elif suite == "row":  # the 0002-product reduce (k_reduce_row)
         del b3
