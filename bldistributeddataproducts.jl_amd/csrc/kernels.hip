@@ -965,7 +965,7 @@ void k_reduce_rowt(const RedArgs a) {
 // block is summed exactly as k_reduce_vec sums it (its batched and remainder
 // accumulator patterns, the same folds), so the results are bit-identical.
 //   BLDP_WAVET  1 (default) = use it where the interleaved kernel cannot run or a
-//               row holds fewer than 4 groups; 0 = never
+//               row holds fewer than 4 groups; 2 = for every such shape; 0 = never
 #ifndef BLDP_WAVET
 #define BLDP_WAVET 1
 #endif
@@ -1416,7 +1416,8 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
   // (path "vector", a.tpb = time blocks per wave)
   if (BLDP_WAVET && p.path == PATH_VEC && p.lpg == 64 &&
       (a.k4 == 2 || a.k4 == 4 || a.k4 == 8 || a.k4 == 16) && (T == 1 || T == 2 || T == 4) &&
-      a.ts == 1 && a.nchunk == 1 && (a.nco < 4 || a.ni * a.nto > 65535) && a.ni <= 65535 &&
+      a.ts == 1 && a.nchunk == 1 &&
+      (BLDP_WAVET >= 2 || a.nco < 4 || a.ni * a.nto > 65535) && a.ni <= 65535 &&
       a.nbank <= 65535) {
     const int64_t tb = std::max<int64_t>(1, 16 / (T * a.k4)), rw = tb * 4;
     if (a.nco * cdiv(a.nto, 4 * rw) <= INT32_MAX) {

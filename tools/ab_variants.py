@@ -53,6 +53,7 @@ VARIANTS = {
     "rowtmw4": "-DBLDP_ROWT_MAXWAVES=4",
     "rowtnopack": "-DBLDP_ROWT_PACK=0",
     "nowavet": "-DBLDP_WAVET=0",
+    "wavet2": "-DBLDP_WAVET=2",
     "nonarrowt": "-DBLDP_NARROW_TPB=0",
     "rowtmw8": "-DBLDP_ROWT_MAXWAVES=0",
     # narrow windows: time split over otherwise idle waves, with / without grid cap
@@ -216,6 +217,15 @@ def run(names, rounds, iters, suite="main"):
         band_case("0001 F1 T2", b4, 1, 2, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
         band_case("0001 F1 T4", b4, 1, 4, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
         cases_done = True
+    elif suite == "il1":  # large groups with short time blocks: interleaved vs wave kernel
+        for F, T in ((1024, 1), (512, 1), (2048, 1), (4096, 1), (1024, 2), (1024, 4)):
+            band_case(f"0000 F{F} T{T}", b3, F, T)
+        del b3
+        b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
+        band_case("0002 F1024 T1", b2, 1024, 1)
+        band_case("0002 F512 T1", b2, 512, 1)
+        band_case("0002 F4096 T1", b2, 4096, 1)
+        cases_done = True
     elif suite == "row":  # the 0002-product reduce (k_reduce_row)
         del b3
         b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
@@ -334,7 +344,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--suite", default="main", choices=["main", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep"])
+    ap.add_argument("--suite", default="main", choices=["main", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:

@@ -107,6 +107,7 @@ for s in $STEPS; do
     ab_row) run ab_row 600 python tools/ab_variants.py --run --suite row --variants "${AB_VARIANTS:-base,rowmw3,rowmw5,rowmw6}" --json "$OUT/ab_row.json" ;;
     ab_t1) run ab_t1 600 python tools/ab_variants.py --run --suite t1 --variants "${AB_VARIANTS:-base,norowt}" --json "$OUT/ab_t1.json" ;;
     sweep) run sweep 600 python tools/ab_variants.py --run --suite sweep --rounds 3 --variants "${AB_VARIANTS:-base}" --json "$OUT/sweep.json" ;;
+    ab_il1) run ab_il1 600 python tools/ab_variants.py --run --suite il1 --variants "${AB_VARIANTS:-base,wavet2}" --json "$OUT/ab_il1.json" ;;
     counters) run counters 60 rocprofv3 -L ;;
     sq_kurt_*) run "$s" 120 rocprofv3 --pmc ${SQC:-SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE GRBM_COUNT} \
              --output-format csv -d "$OUT/$s" -o run -- python bench.py --mode kurtosis --config "${s#sq_kurt_}" --steps 5 --warmup 2 ;;
