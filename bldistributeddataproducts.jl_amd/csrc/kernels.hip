@@ -810,6 +810,94 @@ __global__ __launch_bounds__(kBlock) void k_reduce_il(const RedArgs a) {
   }
 }
 
+// The interleaved kernel for short time blocks (T = 1, 2, 4; fqavby = 1024
+// with the reference's own fqav, no time integration, on the 0000 product):
+// k_reduce_il gives a workgroup one time block, at T = 1 a single 8 KiB row
+// segment.  Here it takes TPB = 16 / T consecutive blocks of its GPW groups,
+// rows loaded 16 loads per lane at a time, every block folded exactly as
+// k_reduce_il folds it (same slots, butterflies, wave order: bit-identical),
+// the wave partials of all blocks parked in LDS behind ONE barrier.
+// Measured and not taken (A/B on MI355X, bit-identical, profiles/r02/sweep_t1.json
+// r02bf): slower than k_reduce_il on every shape but F = 512 on the 0000 band
+// (+8%; 0000 F=1024 T=1 -7%, the 0002 band F=512 T=1 -14%): the interleaved
+// kernel's short one-row workgroups are not its bottleneck.
+//   BLDP_IL_TPB  1 = use it for T in {1, 2, 4}; 0 (default) = k_reduce_il
+#ifndef BLDP_IL_TPB
+#define BLDP_IL_TPB 0
+#endif
+template <int OP, int K4, int GPW, int T>
+__global__ __launch_bounds__(kBlock) void k_reduce_ilt(const RedArgs a) {
+  constexpr int NI = GPW * K4 / 4;
+  constexpr int PER = K4 < 4 ? 1 : K4 / 4;
+  constexpr int NS = NI / PER;
+  constexpr int TPB = 16 / T;
+  constexpr int RB = NI >= 16 ? 1 : 16 / NI;  // rows per load batch (<= 16 loads per lane)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t bx = blockIdx.x, bc = (uint32_t)a.blocks_c;
+  const uint32_t tq = bx / bc, i = blockIdx.y;
+  const int bank = blockIdx.z;
+  const int64_t g0 = (int64_t)(bx - tq * bc) * GPW;
+  const int ng = (int)min((int64_t)GPW, a.nco - g0);
+  const int64_t to0 = (int64_t)tq * TPB;
+  const int nb = (int)min((int64_t)TPB, a.nto - to0);
+  const int nrow = nb * T;
+  const float id = R<OP>::id();
+  auto slot = [&](int j) { return j / PER; };
+  auto group = [&](int j) { return (4 * j + wave) / K4; };
+  const float *p = a.in[bank] + a.in_off + (int64_t)i * a.in_ld_i + to0 * T * a.in_ld_t + g0 * a.F +
+                   4 * tid;
+  const int64_t ld = a.in_ld_t;
+  __shared__ float red[TPB][4][NS];
+  float4 acc[NS];
+#pragma unroll
+  for (int q = 0; q < NS; ++q) acc[q] = make_float4(id, id, id, id);
+  // rows in order, RB at a time; a time block's last row closes it
+#pragma unroll
+  for (int r0 = 0; r0 < TPB * T; r0 += RB) {
+    if (r0 < nrow) {
+      float4 v[RB * NI];
+#pragma unroll
+      for (int u = 0; u < RB; ++u)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          if (r0 + u < nrow && (ng == GPW || group(j) < ng))
+            v[u * NI + j] = ld4(p + (int64_t)(r0 + u) * ld + 1024 * j);
+#pragma unroll
+      for (int u = 0; u < RB; ++u) {
+        if (r0 + u < nrow) {
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+            if (ng == GPW || group(j) < ng) acc[slot(j)] = f4<OP>(acc[slot(j)], v[u * NI + j]);
+          if ((r0 + u) % T == T - 1) {  // block (r0 + u) / T complete: its wave partials
+            const int b = (r0 + u) / T;
+#pragma unroll
+            for (int q = 0; q < NS; ++q) {
+              float s = fold4<OP>(acc[q]);
+#pragma unroll
+              for (int off = 32; off > 0; off >>= 1) s = R<OP>::f(s, __shfl_xor(s, off, 64));
+              if (lane == 0) red[b][wave][q] = s;
+              acc[q] = make_float4(id, id, id, id);
+            }
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // thread (b, g) combines block b's wave partials of group g in k_reduce_il's order
+  for (int e = tid; e < nb * ng; e += kBlock) {
+    const int b = e / ng, gi = e - b * ng;
+    float s = id;
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+#pragma unroll
+      for (int q = 0; q < NS; ++q)
+        if ((4 * q * PER + w) / K4 == gi) s = R<OP>::f(s, red[b][w][q]);
+    st1<1>(a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + (to0 + b) * a.out_ld_t + g0 + gi,
+           finish<OP>(s, a));
+  }
+}
+
 // Vector path, small groups (PATH_VEC_ROW): F = 4*G4 channels with G4 = 1..64
 // float4 (F = 4 .. 256, e.g. the 0002 product's fqavby = 64), one float4
 // column per lane, one time block per tile.  A workgroup owns 1024
@@ -1282,6 +1370,30 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
     }
     return hipGetLastError();
   }
+#if BLDP_IL_TPB
+  if (p.path == PATH_VEC_IL && a.tpb > 1) {  // short time blocks, several per workgroup
+    const dim3 g3((unsigned)(a.blocks_c * cdiv(a.nto, a.tpb)), (unsigned)a.ni, (unsigned)a.nbank);
+#define BLDP_ILTL(K, T) hipLaunchKernelGGL((k_reduce_ilt<OP, K, BLDP_IL_GPW, T>), g3, block, 0, s, a); break;
+#define BLDP_ILT_T(K)                      \
+  switch (a.T) {                           \
+    case 1: BLDP_ILTL(K, 1)                \
+    case 2: BLDP_ILTL(K, 2)                \
+    case 4: BLDP_ILTL(K, 4)                \
+    default: return hipErrorInvalidValue;  \
+  }                                        \
+  break;
+    switch (a.k4) {
+      case 2: BLDP_ILT_T(2)
+      case 4: BLDP_ILT_T(4)
+      case 8: BLDP_ILT_T(8)
+      case 16: BLDP_ILT_T(16)
+      default: return hipErrorInvalidValue;
+    }
+#undef BLDP_ILT_T
+#undef BLDP_ILTL
+    return hipGetLastError();
+  }
+#endif
   if (p.path == PATH_VEC_IL) {
     const dim3 g3((unsigned)a.blocks_c, (unsigned)(a.ni * a.nto), (unsigned)a.nbank);
     switch (a.k4) {
@@ -1435,6 +1547,12 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
     a.blocks_c = cdiv(a.nco, BLDP_IL_GPW);
     a.ntiles = a.blocks_c * a.ni * a.nto * a.nbank;
     p.grid = a.ntiles;
+    if (BLDP_IL_TPB && (T == 1 || T == 2 || T == 4) && a.nto > 1 &&
+        a.blocks_c * cdiv(a.nto, 16 / T) <= INT32_MAX) {  // k_reduce_ilt
+      a.tpb = (int32_t)(16 / T);
+      a.ntiles = a.blocks_c * cdiv(a.nto, a.tpb) * a.ni * a.nbank;
+      p.grid = a.ntiles;
+    }
   }
   // small power-of-two groups, whole time block per tile, no time split:
   // the lean row kernel (3-D grid, so every dimension must fit)

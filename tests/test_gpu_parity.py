@@ -109,7 +109,11 @@ def test_reduce_paths_integer_exact(eng, orc, shape):
 # Interleaved vector path (F = 512..4096 with >= 4096 groups): a tail
 # segment of fewer than 4 groups, several IFs and time blocks, every op.
 IL_SHAPES = [(4098, 1, 16, 1024, 16), (8194, 2, 8, 512, 4), (4097, 1, 8, 2048, 8),
-             (4099, 1, 4, 4096, 2)]
+             (4099, 1, 4, 4096, 2),
+             # short time blocks (k_reduce_ilt: 16 / T blocks per workgroup, the
+             # last group partial): T = 1 is the reference's fqav, no integration
+             (4098, 1, 16, 1024, 1), (4097, 2, 20, 512, 1), (4096, 1, 5, 2048, 1),
+             (4099, 1, 36, 1024, 4)]
 
 
 @pytest.mark.parametrize("shape", IL_SHAPES, ids=lambda s: "x".join(map(str, s)))

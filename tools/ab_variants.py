@@ -54,6 +54,7 @@ VARIANTS = {
     "rowtnopack": "-DBLDP_ROWT_PACK=0",
     "nowavet": "-DBLDP_WAVET=0",
     "wavet2": "-DBLDP_WAVET=2",
+    "noilt": "-DBLDP_IL_TPB=0",
     "nonarrowt": "-DBLDP_NARROW_TPB=0",
     "rowtmw8": "-DBLDP_ROWT_MAXWAVES=0",
     # narrow windows: time split over otherwise idle waves, with / without grid cap
