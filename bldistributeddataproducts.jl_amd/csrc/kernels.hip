@@ -983,6 +983,11 @@ void k_reduce_row(const RedArgs a) {
 #ifndef BLDP_ROWT_PACK
 #define BLDP_ROWT_PACK 1
 #endif
+//   BLDP_ROWT_TIMING_NOBFLY 1 = TIMING EXPERIMENT ONLY (wrong numerics): no
+//                  cross-lane butterfly, pricing it
+#ifndef BLDP_ROWT_TIMING_NOBFLY
+#define BLDP_ROWT_TIMING_NOBFLY 0
+#endif
 //   BLDP_ROWT_MAXWAVES  cap on resident waves per SIMD for k_reduce_rowt (0 = none)
 //                      6 (default): A/B against 4 and none, profiles/r02/ab_row_tpb.json
 #ifndef BLDP_ROWT_MAXWAVES
@@ -1033,8 +1038,10 @@ void k_reduce_rowt(const RedArgs a) {
     }
     if constexpr (kNacc > 1) acc = f4<OP>(acc, id4);
     float s = fold4<OP>(acc);
+#if !BLDP_ROWT_TIMING_NOBFLY  // (TIMING EXPERIMENT ONLY when set: wrong results)
 #pragma unroll
     for (int off = G4 / 2; off > 0; off >>= 1) s = R<OP>::f(s, __shfl_xor(s, off, 64));
+#endif
     if (valid && (tid & (G4 - 1)) == 0)
       st1<1>(a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + (to0 + b) * a.out_ld_t +
                  col / G4,

@@ -55,6 +55,7 @@ VARIANTS = {
     "nowavet": "-DBLDP_WAVET=0",
     "wavet2": "-DBLDP_WAVET=2",
     "noilt": "-DBLDP_IL_TPB=0",
+    "rowtnobfly": "-DBLDP_ROWT_TIMING_NOBFLY=1",  # timing only: wrong numerics
     "nonarrowt": "-DBLDP_NARROW_TPB=0",
     "rowtmw8": "-DBLDP_ROWT_MAXWAVES=0",
     # narrow windows: time split over otherwise idle waves, with / without grid cap
