@@ -988,6 +988,11 @@ void k_reduce_row(const RedArgs a) {
 #ifndef BLDP_ROWT_TIMING_NOBFLY
 #define BLDP_ROWT_TIMING_NOBFLY 0
 #endif
+//   BLDP_ROWT_HALVING  1 = the block sums reduced across lanes by recursive
+//                  halving; 0 = a butterfly per block
+#ifndef BLDP_ROWT_HALVING
+#define BLDP_ROWT_HALVING 0
+#endif
 //   BLDP_ROWT_MAXWAVES  cap on resident waves per SIMD for k_reduce_rowt (0 = none)
 //                      6 (default): A/B against 4 and none, profiles/r02/ab_row_tpb.json
 #ifndef BLDP_ROWT_MAXWAVES
@@ -1023,6 +1028,57 @@ void k_reduce_rowt(const RedArgs a) {
     for (int u = 0; u < NR; ++u)
       if (u < nb * T) v[u] = ld4(p + u * ld);
   }
+#if BLDP_ROWT_HALVING
+  // every block's k_reduce_row sum, then the TPB block sums of a lane reduced
+  // over its group's lanes by recursive halving: at each xor step a lane keeps
+  // half of its blocks (the lower half when its step bit is 0) and sends the
+  // other half, so the halving steps cost TPB - 1 shuffles instead of TPB each;
+  // every block still gets the butterfly's sums (same pairs, same tree), so the
+  // results are bit-identical
+  float sv[TPB];
+#pragma unroll
+  for (int b = 0; b < TPB; ++b) {
+    const float4 id4 = make_float4(id, id, id, id);
+    float4 acc = id4;
+    if (valid && b < nb) {
+#pragma unroll
+      for (int r = 0; r < T; ++r) acc = f4<OP>(acc, v[b * T + r]);
+    }
+    if constexpr (kNacc > 1) acc = f4<OP>(acc, id4);
+    sv[b] = fold4<OP>(acc);
+  }
+  constexpr int LG = G4 >= 64 ? 6 : G4 >= 32 ? 5 : G4 >= 16 ? 4 : G4 >= 8 ? 3 : G4 >= 4 ? 2 : G4 >= 2 ? 1 : 0;
+  constexpr int LT = TPB >= 16 ? 4 : TPB >= 8 ? 3 : TPB >= 4 ? 2 : TPB >= 2 ? 1 : 0;
+  constexpr int H = LG < LT ? LG : LT;  // halving steps
+  int bofs = 0;                         // block index of sv[0] on this lane
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    const int off = G4 >> (h + 1), n = TPB >> h;
+    const bool up = (tid & off) != 0;
+#pragma unroll
+    for (int k = 0; k < (TPB >> (h + 1)); ++k) {
+      const float keep = up ? sv[k + n / 2] : sv[k], send = up ? sv[k] : sv[k + n / 2];
+      sv[k] = R<OP>::f(keep, __shfl_xor(send, off, 64));
+    }
+    if (up) bofs += n / 2;
+  }
+  // the rest of the butterfly on the TPB >> H blocks a lane still holds
+#pragma unroll
+  for (int k = 0; k < (TPB >> H); ++k)
+#pragma unroll
+    for (int off = (G4 >> H) / 2; off > 0; off >>= 1)
+      sv[k] = R<OP>::f(sv[k], __shfl_xor(sv[k], off, 64));
+  if (valid && (tid & ((G4 >> H) - 1)) == 0) {
+#pragma unroll
+    for (int k = 0; k < (TPB >> H); ++k) {
+      const int b = bofs + k;
+      if (b < nb)
+        st1<1>(a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + (to0 + b) * a.out_ld_t +
+                   col / G4,
+               finish<OP>(sv[k], a));
+    }
+  }
+#else
 #pragma unroll
   for (int b = 0; b < TPB; ++b) {
     if (b < nb) {  // (uniform)
@@ -1048,6 +1104,7 @@ void k_reduce_rowt(const RedArgs a) {
              finish<OP>(s, a));
     }
   }
+#endif
 }
 
 // Large groups (F = 512..4096: 64 lanes x K4 float4 per row, one output per

@@ -56,6 +56,7 @@ VARIANTS = {
     "wavet2": "-DBLDP_WAVET=2",
     "noilt": "-DBLDP_IL_TPB=0",
     "rowtnobfly": "-DBLDP_ROWT_TIMING_NOBFLY=1",  # timing only: wrong numerics
+    "rowthalv": "-DBLDP_ROWT_HALVING=1",
     "nonarrowt": "-DBLDP_NARROW_TPB=0",
     "rowtmw8": "-DBLDP_ROWT_MAXWAVES=0",
     # narrow windows: time split over otherwise idle waves, with / without grid cap
