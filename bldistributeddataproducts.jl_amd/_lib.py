@@ -20,7 +20,8 @@ PATHS = {0: "vector", 1: "narrow", 2: "scalar", 3: "tile", 4: "interleaved", 5: 
 KURT_PATHS = {0: "regs", 1: "mid", 2: "leaf", 3: "twopass"}
 
 BLDP_OK, BLDP_EINVAL, BLDP_EDIM, BLDP_EHIP, BLDP_ENOMEM, BLDP_EBOUNDS = 0, -1, -2, -3, -5, -6
-BLDP_ECOMM = -7
+BLDP_ECOMM, BLDP_EIO = -7, -8
+ABI_VERSION = 2
 BLDP_COMM_ID_BYTES = 128
 
 
@@ -43,6 +44,11 @@ class BoundsError(BLDPError, IndexError):
 
 class ArgumentError(BLDPError, ValueError):
     """Invalid argument (Julia AssertionError / ArgumentError analogues)."""
+
+
+class ReadError(BLDPError, OSError):
+    """A file read failed or ended early (truncated file, stale chunk index):
+    Julia's SystemError / EOFError from the HDF5 / mmap read."""
 
 
 # every symbol include/bldp.h declares, with its ctypes signature
@@ -112,8 +118,9 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = res
-        if L.bldp_abi_version() != 1:
-            raise BLDPError(BLDP_EINVAL, "libbldp_hip ABI version mismatch")
+        if L.bldp_abi_version() != ABI_VERSION:
+            raise BLDPError(BLDP_EINVAL, f"libbldp_hip ABI version {L.bldp_abi_version()}, "
+                                         f"expected {ABI_VERSION}: rebuild it")
         _lib = L
     return _lib
 
@@ -134,6 +141,8 @@ def check(rc: int, what: str = "") -> None:
         raise BoundsError(rc, msg)
     if rc == BLDP_EINVAL:
         raise ArgumentError(rc, msg)
+    if rc == BLDP_EIO:
+        raise ReadError(rc, msg)
     raise BLDPError(rc, msg)
 
 

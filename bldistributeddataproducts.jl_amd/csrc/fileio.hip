@@ -166,23 +166,38 @@ struct DevIO {
   std::mutex call;
   std::unique_ptr<ReadPool> pool;
   Slots slots;
+  bool retired = false;  // released by bldp_finalize (under `call`)
 };
 std::mutex g_io_mu;
-std::map<int, std::unique_ptr<DevIO>> g_io;
+std::map<int, std::shared_ptr<DevIO>> g_io;
 
-DevIO *dev_io() {
+// The current device's DevIO, returned with its call lock held in `call`.
+// The shared_ptr keeps it alive across a concurrent fileio_release; one
+// released while this thread waited for its call lock is retired, and the
+// loop takes the fresh one instead.
+std::shared_ptr<DevIO> dev_io(std::unique_lock<std::mutex> &call) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-  std::lock_guard<std::mutex> lk(g_io_mu);
-  std::unique_ptr<DevIO> &io = g_io[dev];
-  if (!io) {
-    int n = 0;
-    if (const char *e = getenv("BLDP_READ_THREADS")) n = atoi(e);
-    if (n <= 0) n = std::min(16, std::max(2, (int)std::thread::hardware_concurrency()));
-    io.reset(new DevIO);
-    io->pool.reset(new ReadPool(n));
+  for (;;) {
+    std::shared_ptr<DevIO> io;
+    {
+      std::lock_guard<std::mutex> lk(g_io_mu);
+      std::shared_ptr<DevIO> &slot = g_io[dev];
+      if (!slot) {
+        int n = 0;
+        if (const char *e = getenv("BLDP_READ_THREADS")) n = atoi(e);
+        if (n <= 0) n = std::min(16, std::max(2, (int)std::thread::hardware_concurrency()));
+        slot = std::make_shared<DevIO>();
+        slot->pool.reset(new ReadPool(n));
+      }
+      io = slot;
+    }
+    std::unique_lock<std::mutex> lk(io->call);
+    if (!io->retired) {
+      call = std::move(lk);
+      return io;
+    }
   }
-  return io.get();
 }
 
 double ms_since(std::chrono::steady_clock::time_point t0) {
@@ -302,8 +317,8 @@ static int chunks_to_device(
   std::vector<uint64_t> offs, lens, ooff, olen;
   evs.reserve(nbatch);
   for (auto *v : {&offs, &lens, &ooff, &olen}) v->reserve(maxb);
-  DevIO *io = dev_io();
-  std::lock_guard<std::mutex> call(io->call);
+  std::unique_lock<std::mutex> call;
+  const std::shared_ptr<DevIO> io = dev_io(call);
   ReadPool *rp = io->pool.get();
   PostedJob posted(rp, &j);
   hipStream_t cs = (hipStream_t)copy_stream, s = (hipStream_t)stream;
@@ -317,7 +332,8 @@ static int chunks_to_device(
       j.cv.wait(lk, [&] { return j.left[b].load() == 0 || j.err.load(); });
     }
     if (int e = j.err.load()) {
-      rc = bldp::set_error(BLDP_EINVAL, "chunks_to_device: pread failed: %s", strerror(e));
+      rc = bldp::set_error(BLDP_EIO, "chunks_to_device: read failed (%s): truncated file or "
+                           "stale chunk index?", strerror(e));
       break;
     }
     const int64_t lo = brange[b].first, hi = brange[b].second;
@@ -440,8 +456,8 @@ static int runs_to_device(int fd, int64_t nrun, const int64_t *file_off, const i
     }
     pos += len[r];
   }
-  DevIO *io = dev_io();
-  std::lock_guard<std::mutex> call(io->call);
+  std::unique_lock<std::mutex> call;
+  const std::shared_ptr<DevIO> io = dev_io(call);
   int rc = ensure_slots(io->slots, slot_bytes, nslot);
   if (rc) return rc;
   // reads of batch b go to slot b % nslot at (hoff - b * slot_bytes); a batch
@@ -460,7 +476,8 @@ static int runs_to_device(int fd, int64_t nrun, const int64_t *file_off, const i
       j.cv.wait(lk, [&] { return j.left[b].load() == 0 || j.err.load(); });
     }
     if (int e = j.err.load()) {
-      rc = bldp::set_error(BLDP_EINVAL, "runs_to_device: pread failed: %s", strerror(e));
+      rc = bldp::set_error(BLDP_EIO, "runs_to_device: read failed (%s): truncated file?",
+                           strerror(e));
       break;
     }
     const int64_t lo = b * slot_bytes, n = std::min(slot_bytes, total - lo);
@@ -544,6 +561,7 @@ void bldp::fileio_release() {
     std::lock_guard<std::mutex> call(kv.second->call);  // no read call in progress
     kv.second->pool.reset();                            // joins the reader threads
     free_slots(kv.second->slots);
+    kv.second->retired = true;  // a caller already holding it takes a fresh one
   }
   g_io.clear();
 }

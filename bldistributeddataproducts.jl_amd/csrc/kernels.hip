@@ -58,6 +58,49 @@ template <int OP>
 __device__ __forceinline__ float fold4(float4 v) {
   return R<OP>::f(R<OP>::f(v.x, v.y), R<OP>::f(v.z, v.w));
 }
+
+//   BLDP_DPP  1 (default) = the lane folds of the reduce kernels run on DPP row
+//             permutes and gfx950's v_permlane16/32_swap (VALU only); 0 =
+//             __shfl_xor, which is a ds_bpermute (an LDS round trip) per step
+#ifndef BLDP_DPP
+#define BLDP_DPP 1
+#endif
+template <int CTRL>
+__device__ __forceinline__ float dpp(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL,
+                                                              0xF, 0xF, false));
+}
+// Fold of op over aligned groups of W lanes (W a power of two <= 64); every
+// lane of a group ends with the group's result.  An xor butterfly with the
+// partners in ascending order (1, 2, 4, ...): the 4- and 8-apart steps take
+// the half-mirror / mirror of a 16-lane row, which after the smaller steps
+// holds exactly what the xor partner holds (every lane of an aligned block of
+// 4 (8) lanes holds the same value by then); 16 and 32 apart are the gfx950
+// half-swaps.  Every step is op(own, partner) on identical operands in both
+// lanes, so the result is the same on every lane of the group.
+template <int OP, int W>
+__device__ __forceinline__ float lanes_fold(float s) {
+#if BLDP_DPP
+  if constexpr (W >= 2) s = R<OP>::f(s, dpp<0xB1>(s));   // quad_perm [1,0,3,2]
+  if constexpr (W >= 4) s = R<OP>::f(s, dpp<0x4E>(s));   // quad_perm [2,3,0,1]
+  if constexpr (W >= 8) s = R<OP>::f(s, dpp<0x141>(s));  // row_half_mirror
+  if constexpr (W >= 16) s = R<OP>::f(s, dpp<0x140>(s)); // row_mirror
+  if constexpr (W >= 32) {
+    const unsigned u = __builtin_bit_cast(unsigned, s);
+    const auto p = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    s = R<OP>::f(__builtin_bit_cast(float, (unsigned)p[0]), __builtin_bit_cast(float, (unsigned)p[1]));
+  }
+  if constexpr (W >= 64) {
+    const unsigned u = __builtin_bit_cast(unsigned, s);
+    const auto p = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    s = R<OP>::f(__builtin_bit_cast(float, (unsigned)p[0]), __builtin_bit_cast(float, (unsigned)p[1]));
+  }
+#else
+#pragma unroll
+  for (int off = W / 2; off > 0; off >>= 1) s = R<OP>::f(s, __shfl_xor(s, off, 64));
+#endif
+  return s;
+}
 // Build-time variants (A/B tested with tools/ab_variants.py):
 //   BLDP_NT_LOADS  1 (default) = streaming loads carry the non-temporal hint:
 //                  the window is read once; measured +10% on cfg3 (6.35 -> 6.98 TB/s)
@@ -237,8 +280,7 @@ __device__ __forceinline__ void vec_tile(const RedArgs &a, int64_t tile) {
   float s = fold4<OP>(fold_acc<OP>(acc));
 
   // combine the LPG lanes of a group (xor butterfly inside aligned segments)
-#pragma unroll
-  for (int off = LPG / 2; off > 0; off >>= 1) s = R<OP>::f(s, __shfl_xor(s, off, 64));
+  s = lanes_fold<OP, LPG>(s);
 
   if (ts > 1) {  // combine the waves that split the time rows, through LDS
     __shared__ float red[4][64];
@@ -540,6 +582,96 @@ __device__ __forceinline__ void lane_tile(const RedArgs &a, int64_t tile) {
     a.ws[(((c.chunk * a.nbank + c.bank) * a.nto + c.to) * a.ni + c.i) * a.nco + co] = s;
 }
 
+// The lane path for short time blocks (T = 1, 2, 4; T = 1 is the reference's
+// own fqav with no time integration) and small groups that are not a power of
+// two: F = 3, 5, 6, 7, 12 (e.g. fqavby = 3 or 12 on a 65535- / 65532-channel
+// window of a 0002 product).  One lane per output group as in lane_tile, but a
+// workgroup takes TPB = NRW / T consecutive time blocks of its 256 groups, so
+// NRW rows (F * NRW <= 48 floats) are in flight per lane and every workgroup
+// streams NRW x 1 KiB..3 KiB of rows instead of a single row segment (the tile
+// path's one-row workgroups at T = 1: 0.44 of the read/write-mix ceiling on the
+// 0002 band at F = 3, profiles/r03/).  A row's F floats are one dwordx2 / x3 /
+// x4 per lane where F <= 4 (one wave-instruction covers whole 128-byte lines:
+// non-temporal), else several 16-byte pieces at an F*4-byte lane pitch, which
+// each cover every line only in part: those are plain loads, so the lines the
+// next piece needs are still in L1 (nt loads there read every line from HBM
+// about twice, the vector path's 1.98x at F = 12).  Stores: one float per lane,
+// 1 KiB per workgroup-instruction.
+//   BLDP_LANET  1 (default) = use it for T in {1, 2, 4}; 0 = the lane / tile / vector paths
+#ifndef BLDP_LANET
+#define BLDP_LANET 1
+#endif
+typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
+typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
+template <int F>
+__device__ __forceinline__ void ldF(const float *p, float (&x)[F]) {
+  if constexpr (F == 3) {
+    const f3u v = __builtin_nontemporal_load(reinterpret_cast<const f3u *>(p));
+    x[0] = v.x; x[1] = v.y; x[2] = v.z;
+  } else {
+    int f = 0;
+#pragma unroll
+    for (; f + 4 <= F; f += 4) {
+      const f4u v = *reinterpret_cast<const f4u *>(p + f);
+      x[f] = v.x; x[f + 1] = v.y; x[f + 2] = v.z; x[f + 3] = v.w;
+    }
+    if constexpr (F % 4 == 3) {
+      const f3u v = *reinterpret_cast<const f3u *>(p + f);
+      x[f] = v.x; x[f + 1] = v.y; x[f + 2] = v.z;
+    } else if constexpr (F % 4 == 2) {
+      const f2u v = *reinterpret_cast<const f2u *>(p + f);
+      x[f] = v.x; x[f + 1] = v.y;
+    } else if constexpr (F % 4 == 1) {
+      x[f] = p[f];
+    }
+  }
+}
+template <int F>
+constexpr int lanet_rows() { return F <= 3 ? 16 : F <= 6 ? 8 : 4; }  // = lanet_rows_host
+template <int OP, int F, int T>
+__global__ __launch_bounds__(kBlock) void k_reduce_lanet(const RedArgs a) {
+  constexpr int NRW = lanet_rows<F>(), TPB = NRW / T;
+  static_assert(NRW % T == 0 && TPB >= 1, "k_reduce_lanet: rows per lane");
+  const int tid = threadIdx.x;
+  const uint32_t bx = blockIdx.x, bc = (uint32_t)a.blocks_c;
+  const uint32_t tq = bx / bc, i = blockIdx.y;
+  const int bank = blockIdx.z;
+  const int64_t co = (int64_t)(bx - tq * bc) * kBlock + tid;
+  const int64_t to0 = (int64_t)tq * TPB;
+  const bool valid = co < a.nco;
+  const int nb = (int)min((int64_t)TPB, a.nto - to0);
+  const float id = R<OP>::id();
+  const float *p = a.in[bank] + a.in_off + (int64_t)i * a.in_ld_i + to0 * T * a.in_ld_t + co * F;
+  const int64_t ld = a.in_ld_t;
+  float v[NRW][F];
+  if (valid && nb == TPB) {
+#pragma unroll
+    for (int u = 0; u < NRW; ++u) ldF<F>(p + u * ld, v[u]);
+  } else {
+#pragma unroll
+    for (int u = 0; u < NRW; ++u) {
+      if (valid && u < nb * T) {
+        ldF<F>(p + u * ld, v[u]);
+      } else {
+#pragma unroll
+        for (int f = 0; f < F; ++f) v[u][f] = id;
+      }
+    }
+  }
+  float *o = a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + co;
+#pragma unroll
+  for (int b = 0; b < TPB; ++b) {
+    // a block's F x T values in the reference's order: the F channels of a
+    // spectrum in sequence (fqav's sum over dims = 1), spectrum after spectrum
+    float acc = id;
+#pragma unroll
+    for (int r = 0; r < T; ++r)
+#pragma unroll
+      for (int f = 0; f < F; ++f) acc = R<OP>::f(acc, v[b * T + r][f]);
+    if (valid && b < nb) st1<1>(o + (to0 + b) * a.out_ld_t, finish<OP>(acc, a));
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Scalar path: any F, any channel step, any alignment.  One lane per output.
 template <int OP>
@@ -792,9 +924,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce_il(const RedArgs a) {
   __shared__ float red[4][NS];
 #pragma unroll
   for (int q = 0; q < NS; ++q) {
-    float s = fold4<OP>(acc[q]);
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) s = R<OP>::f(s, __shfl_xor(s, off, 64));
+    const float s = lanes_fold<OP, 64>(fold4<OP>(acc[q]));
     if (lane == 0) red[wave][q] = s;
   }
   __syncthreads();
@@ -806,94 +936,6 @@ __global__ __launch_bounds__(kBlock) void k_reduce_il(const RedArgs a) {
       for (int q = 0; q < NS; ++q)
         if ((4 * q * PER + w) / K4 == tid) s = R<OP>::f(s, red[w][q]);
     st1<1>(a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + (int64_t)to * a.out_ld_t + g0 + tid,
-           finish<OP>(s, a));
-  }
-}
-
-// The interleaved kernel for short time blocks (T = 1, 2, 4; fqavby = 1024
-// with the reference's own fqav, no time integration, on the 0000 product):
-// k_reduce_il gives a workgroup one time block, at T = 1 a single 8 KiB row
-// segment.  Here it takes TPB = 16 / T consecutive blocks of its GPW groups,
-// rows loaded 16 loads per lane at a time, every block folded exactly as
-// k_reduce_il folds it (same slots, butterflies, wave order: bit-identical),
-// the wave partials of all blocks parked in LDS behind ONE barrier.
-// Measured and not taken (A/B on MI355X, bit-identical, profiles/r02/sweep_t1.json
-// r02bf): slower than k_reduce_il on every shape but F = 512 on the 0000 band
-// (+8%; 0000 F=1024 T=1 -7%, the 0002 band F=512 T=1 -14%): the interleaved
-// kernel's short one-row workgroups are not its bottleneck.
-//   BLDP_IL_TPB  1 = use it for T in {1, 2, 4}; 0 (default) = k_reduce_il
-#ifndef BLDP_IL_TPB
-#define BLDP_IL_TPB 0
-#endif
-template <int OP, int K4, int GPW, int T>
-__global__ __launch_bounds__(kBlock) void k_reduce_ilt(const RedArgs a) {
-  constexpr int NI = GPW * K4 / 4;
-  constexpr int PER = K4 < 4 ? 1 : K4 / 4;
-  constexpr int NS = NI / PER;
-  constexpr int TPB = 16 / T;
-  constexpr int RB = NI >= 16 ? 1 : 16 / NI;  // rows per load batch (<= 16 loads per lane)
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t bx = blockIdx.x, bc = (uint32_t)a.blocks_c;
-  const uint32_t tq = bx / bc, i = blockIdx.y;
-  const int bank = blockIdx.z;
-  const int64_t g0 = (int64_t)(bx - tq * bc) * GPW;
-  const int ng = (int)min((int64_t)GPW, a.nco - g0);
-  const int64_t to0 = (int64_t)tq * TPB;
-  const int nb = (int)min((int64_t)TPB, a.nto - to0);
-  const int nrow = nb * T;
-  const float id = R<OP>::id();
-  auto slot = [&](int j) { return j / PER; };
-  auto group = [&](int j) { return (4 * j + wave) / K4; };
-  const float *p = a.in[bank] + a.in_off + (int64_t)i * a.in_ld_i + to0 * T * a.in_ld_t + g0 * a.F +
-                   4 * tid;
-  const int64_t ld = a.in_ld_t;
-  __shared__ float red[TPB][4][NS];
-  float4 acc[NS];
-#pragma unroll
-  for (int q = 0; q < NS; ++q) acc[q] = make_float4(id, id, id, id);
-  // rows in order, RB at a time; a time block's last row closes it
-#pragma unroll
-  for (int r0 = 0; r0 < TPB * T; r0 += RB) {
-    if (r0 < nrow) {
-      float4 v[RB * NI];
-#pragma unroll
-      for (int u = 0; u < RB; ++u)
-#pragma unroll
-        for (int j = 0; j < NI; ++j)
-          if (r0 + u < nrow && (ng == GPW || group(j) < ng))
-            v[u * NI + j] = ld4(p + (int64_t)(r0 + u) * ld + 1024 * j);
-#pragma unroll
-      for (int u = 0; u < RB; ++u) {
-        if (r0 + u < nrow) {
-#pragma unroll
-          for (int j = 0; j < NI; ++j)
-            if (ng == GPW || group(j) < ng) acc[slot(j)] = f4<OP>(acc[slot(j)], v[u * NI + j]);
-          if ((r0 + u) % T == T - 1) {  // block (r0 + u) / T complete: its wave partials
-            const int b = (r0 + u) / T;
-#pragma unroll
-            for (int q = 0; q < NS; ++q) {
-              float s = fold4<OP>(acc[q]);
-#pragma unroll
-              for (int off = 32; off > 0; off >>= 1) s = R<OP>::f(s, __shfl_xor(s, off, 64));
-              if (lane == 0) red[b][wave][q] = s;
-              acc[q] = make_float4(id, id, id, id);
-            }
-          }
-        }
-      }
-    }
-  }
-  __syncthreads();
-  // thread (b, g) combines block b's wave partials of group g in k_reduce_il's order
-  for (int e = tid; e < nb * ng; e += kBlock) {
-    const int b = e / ng, gi = e - b * ng;
-    float s = id;
-#pragma unroll
-    for (int w = 0; w < 4; ++w)
-#pragma unroll
-      for (int q = 0; q < NS; ++q)
-        if ((4 * q * PER + w) / K4 == gi) s = R<OP>::f(s, red[b][w][q]);
-    st1<1>(a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + (to0 + b) * a.out_ld_t + g0 + gi,
            finish<OP>(s, a));
   }
 }
@@ -957,9 +999,7 @@ void k_reduce_row(const RedArgs a) {
       p += ld;
     }
   }
-  float s = fold4<OP>(fold_acc<OP>(acc));
-#pragma unroll
-  for (int off = G4 / 2; off > 0; off >>= 1) s = R<OP>::f(s, __shfl_xor(s, off, 64));
+  const float s = lanes_fold<OP, G4>(fold4<OP>(fold_acc<OP>(acc)));
   if (valid && (tid & (G4 - 1)) == 0)
     st1<1>(a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + (int64_t)to * a.out_ld_t + col / G4,
            finish<OP>(s, a));
@@ -982,16 +1022,6 @@ void k_reduce_row(const RedArgs a) {
 //                  workgroup between 2 or 4 time groups (no idle lanes)
 #ifndef BLDP_ROWT_PACK
 #define BLDP_ROWT_PACK 1
-#endif
-//   BLDP_ROWT_TIMING_NOBFLY 1 = TIMING EXPERIMENT ONLY (wrong numerics): no
-//                  cross-lane butterfly, pricing it
-#ifndef BLDP_ROWT_TIMING_NOBFLY
-#define BLDP_ROWT_TIMING_NOBFLY 0
-#endif
-//   BLDP_ROWT_HALVING  1 = the block sums reduced across lanes by recursive
-//                  halving; 0 = a butterfly per block
-#ifndef BLDP_ROWT_HALVING
-#define BLDP_ROWT_HALVING 0
 #endif
 //   BLDP_ROWT_MAXWAVES  cap on resident waves per SIMD for k_reduce_rowt (0 = none)
 //                      6 (default): A/B against 4 and none, profiles/r02/ab_row_tpb.json
@@ -1020,91 +1050,46 @@ void k_reduce_rowt(const RedArgs a) {
   // time blocks of this lane's group (uniform over each wave: groups hold >= 64 lanes)
   const int nb = (int)max((int64_t)0, min((int64_t)TPB, a.nto - to0));
   const float id = R<OP>::id();
+  const float4 id4 = make_float4(id, id, id, id);
+  const float *p = a.in[bank] + a.in_off + (int64_t)i * a.in_ld_i + to0 * T * a.in_ld_t + 4 * col;
+  const int64_t ld = a.in_ld_t;
   float4 v[NR];
-  if (valid) {
-    const float *p = a.in[bank] + a.in_off + (int64_t)i * a.in_ld_i + to0 * T * a.in_ld_t + 4 * col;
-    const int64_t ld = a.in_ld_t;
+  if (valid && nb == TPB) {  // every tile but the last time group: no predication
 #pragma unroll
-    for (int u = 0; u < NR; ++u)
-      if (u < nb * T) v[u] = ld4(p + u * ld);
+    for (int u = 0; u < NR; ++u) v[u] = ld4(p + u * ld);
+  } else {
+#pragma unroll
+    for (int u = 0; u < NR; ++u) v[u] = (valid && u < nb * T) ? ld4(p + u * ld) : id4;
   }
-#if BLDP_ROWT_HALVING
-  // every block's k_reduce_row sum, then the TPB block sums of a lane reduced
-  // over its group's lanes by recursive halving: at each xor step a lane keeps
-  // half of its blocks (the lower half when its step bit is 0) and sends the
-  // other half, so the halving steps cost TPB - 1 shuffles instead of TPB each;
-  // every block still gets the butterfly's sums (same pairs, same tree), so the
-  // results are bit-identical
+  // k_reduce_row's accumulators for a block of T < 16 rows: the rows chained
+  // into the first, the others left at the identity; its pairwise fold of
+  // them then amounts to one more op with the identity (f is idempotent
+  // there), which is all that is done here.  Every lane of a group ends with
+  // the group's sums of all TPB blocks (lanes_fold).
   float sv[TPB];
 #pragma unroll
   for (int b = 0; b < TPB; ++b) {
-    const float4 id4 = make_float4(id, id, id, id);
     float4 acc = id4;
-    if (valid && b < nb) {
 #pragma unroll
-      for (int r = 0; r < T; ++r) acc = f4<OP>(acc, v[b * T + r]);
-    }
+    for (int r = 0; r < T; ++r) acc = f4<OP>(acc, v[b * T + r]);
     if constexpr (kNacc > 1) acc = f4<OP>(acc, id4);
-    sv[b] = fold4<OP>(acc);
+    sv[b] = lanes_fold<OP, G4>(fold4<OP>(acc));
   }
-  constexpr int LG = G4 >= 64 ? 6 : G4 >= 32 ? 5 : G4 >= 16 ? 4 : G4 >= 8 ? 3 : G4 >= 4 ? 2 : G4 >= 2 ? 1 : 0;
-  constexpr int LT = TPB >= 16 ? 4 : TPB >= 8 ? 3 : TPB >= 4 ? 2 : TPB >= 2 ? 1 : 0;
-  constexpr int H = LG < LT ? LG : LT;  // halving steps
-  int bofs = 0;                         // block index of sv[0] on this lane
+  // Stores: lane j of a group writes block j (j + G4, ... when the group has
+  // fewer lanes than blocks), so a store instruction has every lane busy
+  // (k_reduce_row's one-lane-per-group store would take TPB instructions).
+  const int j = tid & (G4 - 1);
+  constexpr int NS = TPB > G4 ? TPB / G4 : 1;  // store instructions
+  constexpr int NSEL = TPB < G4 ? TPB : G4;    // blocks a lane chooses from
+  float *o = a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + col / G4;
 #pragma unroll
-  for (int h = 0; h < H; ++h) {
-    const int off = G4 >> (h + 1), n = TPB >> h;
-    const bool up = (tid & off) != 0;
+  for (int m = 0; m < NS; ++m) {
+    const int b = m * G4 + j;
+    float val = sv[m * G4];
 #pragma unroll
-    for (int k = 0; k < (TPB >> (h + 1)); ++k) {
-      const float keep = up ? sv[k + n / 2] : sv[k], send = up ? sv[k] : sv[k + n / 2];
-      sv[k] = R<OP>::f(keep, __shfl_xor(send, off, 64));
-    }
-    if (up) bofs += n / 2;
+    for (int q = 1; q < NSEL; ++q) val = (j == q) ? sv[m * G4 + q] : val;
+    if (valid && b < nb) st1<1>(o + (to0 + b) * a.out_ld_t, finish<OP>(val, a));
   }
-  // the rest of the butterfly on the TPB >> H blocks a lane still holds
-#pragma unroll
-  for (int k = 0; k < (TPB >> H); ++k)
-#pragma unroll
-    for (int off = (G4 >> H) / 2; off > 0; off >>= 1)
-      sv[k] = R<OP>::f(sv[k], __shfl_xor(sv[k], off, 64));
-  if (valid && (tid & ((G4 >> H) - 1)) == 0) {
-#pragma unroll
-    for (int k = 0; k < (TPB >> H); ++k) {
-      const int b = bofs + k;
-      if (b < nb)
-        st1<1>(a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + (to0 + b) * a.out_ld_t +
-                   col / G4,
-               finish<OP>(sv[k], a));
-    }
-  }
-#else
-#pragma unroll
-  for (int b = 0; b < TPB; ++b) {
-    if (b < nb) {  // (uniform)
-    // k_reduce_row's accumulators for a block of T < 16 rows: the rows chained
-    // into the first, the others left at the identity; its pairwise fold of
-    // them then amounts to one more op with the identity (f is idempotent
-    // there), which is all that is done here
-    const float4 id4 = make_float4(id, id, id, id);
-    float4 acc = id4;
-    if (valid) {
-#pragma unroll
-      for (int r = 0; r < T; ++r) acc = f4<OP>(acc, v[b * T + r]);
-    }
-    if constexpr (kNacc > 1) acc = f4<OP>(acc, id4);
-    float s = fold4<OP>(acc);
-#if !BLDP_ROWT_TIMING_NOBFLY  // (TIMING EXPERIMENT ONLY when set: wrong results)
-#pragma unroll
-    for (int off = G4 / 2; off > 0; off >>= 1) s = R<OP>::f(s, __shfl_xor(s, off, 64));
-#endif
-    if (valid && (tid & (G4 - 1)) == 0)
-      st1<1>(a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + (to0 + b) * a.out_ld_t +
-                 col / G4,
-             finish<OP>(s, a));
-    }
-  }
-#endif
 }
 
 // Large groups (F = 512..4096: 64 lanes x K4 float4 per row, one output per
@@ -1171,9 +1156,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce_wavet(const RedArgs a) {
 #pragma unroll
           for (int k = 0; k < K4; ++k)
             acc[k % kNacc] = f4<OP>(acc[k % kNacc], v[(b * T + r) * K4 + k]);
-        float s = fold4<OP>(fold_acc<OP>(acc));
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) s = R<OP>::f(s, __shfl_xor(s, off, 64));
+        const float s = lanes_fold<OP, 64>(fold4<OP>(fold_acc<OP>(acc)));
         if (lane == 0)
           st1<1>(a.out + bank * a.out_bank + i * a.out_ld_i + (t0 + b) * a.out_ld_t + g,
                  finish<OP>(s, a));
@@ -1397,6 +1380,29 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
 #undef BLDP_WAVETL
     return hipGetLastError();
   }
+  if (p.path == PATH_LANE && a.tpb > 1) {  // short time blocks, small odd groups: k_reduce_lanet
+    const dim3 g3((unsigned)(a.blocks_c * cdiv(a.nto, a.tpb)), (unsigned)a.ni, (unsigned)a.nbank);
+#define BLDP_LANETL(FF, TT) hipLaunchKernelGGL((k_reduce_lanet<OP, FF, TT>), g3, block, 0, s, a); break;
+#define BLDP_LANET_T(FF)                   \
+  switch (a.T) {                           \
+    case 1: BLDP_LANETL(FF, 1)             \
+    case 2: BLDP_LANETL(FF, 2)             \
+    case 4: BLDP_LANETL(FF, 4)             \
+    default: return hipErrorInvalidValue;  \
+  }                                        \
+  break;
+    switch (a.F) {
+      case 3: BLDP_LANET_T(3)
+      case 5: BLDP_LANET_T(5)
+      case 6: BLDP_LANET_T(6)
+      case 7: BLDP_LANET_T(7)
+      case 12: BLDP_LANET_T(12)
+      default: return hipErrorInvalidValue;
+    }
+#undef BLDP_LANET_T
+#undef BLDP_LANETL
+    return hipGetLastError();
+  }
   if (p.path == PATH_VEC_ROW && a.tpb > 1) {  // short time blocks, several per workgroup
     const dim3 g3((unsigned)(a.blocks_c * cdiv(cdiv(a.nto, a.tpb), 1 << a.tsub_log2)),
                   (unsigned)a.ni, (unsigned)a.nbank);
@@ -1434,30 +1440,6 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
     }
     return hipGetLastError();
   }
-#if BLDP_IL_TPB
-  if (p.path == PATH_VEC_IL && a.tpb > 1) {  // short time blocks, several per workgroup
-    const dim3 g3((unsigned)(a.blocks_c * cdiv(a.nto, a.tpb)), (unsigned)a.ni, (unsigned)a.nbank);
-#define BLDP_ILTL(K, T) hipLaunchKernelGGL((k_reduce_ilt<OP, K, BLDP_IL_GPW, T>), g3, block, 0, s, a); break;
-#define BLDP_ILT_T(K)                      \
-  switch (a.T) {                           \
-    case 1: BLDP_ILTL(K, 1)                \
-    case 2: BLDP_ILTL(K, 2)                \
-    case 4: BLDP_ILTL(K, 4)                \
-    default: return hipErrorInvalidValue;  \
-  }                                        \
-  break;
-    switch (a.k4) {
-      case 2: BLDP_ILT_T(2)
-      case 4: BLDP_ILT_T(4)
-      case 8: BLDP_ILT_T(8)
-      case 16: BLDP_ILT_T(16)
-      default: return hipErrorInvalidValue;
-    }
-#undef BLDP_ILT_T
-#undef BLDP_ILTL
-    return hipGetLastError();
-  }
-#endif
   if (p.path == PATH_VEC_IL) {
     const dim3 g3((unsigned)a.blocks_c, (unsigned)(a.ni * a.nto), (unsigned)a.nbank);
     switch (a.k4) {
@@ -1517,6 +1499,8 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
 }  // namespace
 
 // ---------------------------------------------------------------------------
+static int64_t lanet_rows_host(int64_t F) { return F <= 3 ? 16 : F <= 6 ? 8 : 4; }
+
 Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus) {
   Plan p{};
   const int64_t F = a.F, T = a.T;
@@ -1527,6 +1511,22 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
   a.k4 = 1;
   a.tpb = 1;
   a.tsub_log2 = 0;
+  if (BLDP_LANET && words && a.in_cs == 1 && (T == 1 || T == 2 || T == 4) &&
+      (F == 3 || F == 5 || F == 6 || F == 7 || F == 12) && a.ni <= 65535 && a.nbank <= 65535 &&
+      cdiv(a.nco, kBlock) * cdiv(a.nto, lanet_rows_host(F) / T) <= INT32_MAX) {
+    // small odd groups, short time blocks: one lane per group, NRW rows per lane
+    p.path = PATH_LANE;
+    a.tpb = (int32_t)(lanet_rows_host(F) / T);
+    a.blocks_c = cdiv(a.nco, kBlock);
+    a.nchunk = 1;
+    a.rows_per_chunk = T;
+    a.ntiles = a.blocks_c * cdiv(a.nto, a.tpb) * a.ni * a.nbank;
+    p.grid = a.ntiles;
+    p.ws_bytes = 0;
+    a.vec_out = 0;
+    a.div = (float)(F * T);
+    return p;
+  }
   if (aligned && F % 4 == 0) {
     p.path = PATH_VEC;
     const int64_t g4 = F / 4;
@@ -1611,12 +1611,6 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
     a.blocks_c = cdiv(a.nco, BLDP_IL_GPW);
     a.ntiles = a.blocks_c * a.ni * a.nto * a.nbank;
     p.grid = a.ntiles;
-    if (BLDP_IL_TPB && (T == 1 || T == 2 || T == 4) && a.nto > 1 &&
-        a.blocks_c * cdiv(a.nto, 16 / T) <= INT32_MAX) {  // k_reduce_ilt
-      a.tpb = (int32_t)(16 / T);
-      a.ntiles = a.blocks_c * cdiv(a.nto, a.tpb) * a.ni * a.nbank;
-      p.grid = a.ntiles;
-    }
   }
   // small power-of-two groups, whole time block per tile, no time split:
   // the lean row kernel (3-D grid, so every dimension must fit)

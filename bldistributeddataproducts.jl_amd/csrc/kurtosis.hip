@@ -248,11 +248,6 @@ __global__ __launch_bounds__(kB) void k_kurt_regs(const KurtArgs k) {
 // running sum handed on through LDS), every lane doing its own channel.  Then
 // z, z2 and the Float64 sums run over the registers and the 4 partial sums are
 // added through LDS in wave order.
-//   BLDP_KURT_MID_TIMING_NOCHAIN 1 = TIMING EXPERIMENT ONLY (wrong numerics):
-//                   the waves sum their quarters at once, pricing the hand-off
-#ifndef BLDP_KURT_MID_TIMING_NOCHAIN
-#define BLDP_KURT_MID_TIMING_NOCHAIN 0
-#endif
 template <int NR>
 __global__ __launch_bounds__(kB) void k_kurt_mid(const KurtArgs k) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -273,12 +268,6 @@ __global__ __launch_bounds__(kB) void k_kurt_mid(const KurtArgs k) {
   // Base.sum, sequential over the whole window (nt <= 1024 is one leaf)
   __shared__ float carry[64];
   float s = 0.0f;
-#if BLDP_KURT_MID_TIMING_NOCHAIN  // TIMING EXPERIMENT ONLY (wrong m): waves in parallel
-  for (int r = 0; r < NR; ++r)
-    if (r < cnt) s += v[r];
-  carry[lane] = s;
-  __syncthreads();
-#else
 #pragma unroll 1
   for (int w = 0; w < 4; ++w) {
     if (wave == w) {
@@ -290,7 +279,6 @@ __global__ __launch_bounds__(kB) void k_kurt_mid(const KurtArgs k) {
     }
     __syncthreads();
   }
-#endif
   const float m = carry[lane] / (float)nt;
   double c2 = 0.0, c4 = 0.0;
 #pragma unroll
@@ -480,44 +468,6 @@ __device__ __forceinline__ void leaf_step(LeafAcc<W> &A, const float (&x)[W]) {
   }
 }
 
-// BLDP_KURT_LEAF_TIMING_F32 1 = TIMING EXPERIMENT ONLY (wrong numerics): the
-// power sums of a batch in Float32 about a Float32 shift, added to the Float64
-// sums once per batch, pricing a scheme with 2 instead of 7 Float64
-// instructions per element
-#ifndef BLDP_KURT_LEAF_TIMING_F32
-#define BLDP_KURT_LEAF_TIMING_F32 0
-#endif
-// BLDP_KURT_LEAF_TIMING_LOADONLY 1 = TIMING EXPERIMENT ONLY (wrong numerics):
-// the main loop keeps only the loads and the Float32 sum (the access
-// pattern's own ceiling)
-#ifndef BLDP_KURT_LEAF_TIMING_LOADONLY
-#define BLDP_KURT_LEAF_TIMING_LOADONLY 0
-#endif
-template <int W, int B>
-__device__ __forceinline__ void leaf_batch_f32(LeafAcc<W> &A, const float (&cur)[B][W]) {
-#pragma unroll
-  for (int w = 0; w < W; ++w) {
-    const float cf = (float)A.c[w];
-    float p1 = 0.f, p2 = 0.f, p3 = 0.f, p4 = 0.f;
-#pragma unroll
-    for (int q = 0; q < B; ++q) {
-      const float x = cur[q][w];
-      A.s[w] += x;
-      A.hi[w] = fmaxf(A.hi[w], x);
-      A.lo[w] = fminf(A.lo[w], x);
-      const float d = x - cf, d2 = d * d;
-      p1 += d;
-      p2 += d2;
-      p3 = fmaf(d2, d, p3);
-      p4 = fmaf(d2, d2, p4);
-    }
-    A.a1[w] += (double)p1;
-    A.a2[w] += (double)p2;
-    A.a3[w] += (double)p3;
-    A.a4[w] += (double)p4;
-  }
-}
-
 template <int W, typename T>
 __device__ __forceinline__ void stw(T *p, const T (&v)[W]) {
   if constexpr (W == 4 && sizeof(T) == 4) {
@@ -610,17 +560,8 @@ void k_kurt_leaf(const KurtArgs k) {
 #pragma unroll
       for (int w = 0; w < W; ++w) cur[q][w] = nxt[q][w];
 #else
-#if BLDP_KURT_LEAF_TIMING_LOADONLY  // TIMING EXPERIMENT ONLY: the loads and the Float32 sum
-#pragma unroll
-    for (int q = 0; q < B; ++q)
-#pragma unroll
-      for (int w = 0; w < W; ++w) A.s[w] += cur[q][w];
-#elif BLDP_KURT_LEAF_TIMING_F32
-    leaf_batch_f32<W, B>(A, cur);
-#else
 #pragma unroll
     for (int q = 0; q < B; ++q) leaf_step<W>(A, cur[q]);
-#endif
     if (bt + 1 < nb) {
 #pragma unroll
       for (int q = 0; q < B; ++q) ldw<W>(p + q * ld, cur[q]);
@@ -637,246 +578,6 @@ void k_kurt_leaf(const KurtArgs k) {
       if (q < tail) leaf_step<W>(A, cur[q]);
   }
   leaf_store<W>(k, A, row, col, slot, len);
-}
-
-// The same leaf stream read the way the reduce reads its tiles: a workgroup
-// owns ONE leaf of two adjacent 256-channel column segments, and its 4 waves
-// interleave the rows -- waves 0 / 1 (one per segment) load the spectra 1, 3,
-// 5, ... of the leaf into registers and do all the arithmetic; waves 2 / 3
-// load the spectra 2, 4, 6, ... and hand them over through LDS (double
-// buffered, one barrier per batch of B spectrum pairs).  Each workgroup-
-// instruction pair reads 4 KiB contiguous (two whole rows of a 512-channel
-// window) instead of two 2 KiB pieces of two leaves 1.7 MB apart.  The
-// computing lane consumes the spectra in the leaf's order with leaf_step, so
-// the results are bit-identical to k_kurt_leaf.  Timing-only builds priced the
-// pattern at -3..-10% of the cfg4 kernel time by box
-// (profiles/r02/ab_kurt_leaf_timing_builds.json).
-//   BLDP_KURT_LEAF_ILV  1 = use it for float4-column leaves (W = 4); 0 = k_kurt_leaf
-//   BLDP_KURT_ILV_B     spectrum pairs per batch
-#ifndef BLDP_KURT_LEAF_ILV
-#define BLDP_KURT_LEAF_ILV 0
-#endif
-#ifndef BLDP_KURT_ILV_B
-#define BLDP_KURT_ILV_B 4
-#endif
-__global__ __launch_bounds__(kB) void k_kurt_leaf_ilv(const KurtArgs k) {
-  constexpr int B = BLDP_KURT_ILV_B;
-  __shared__ f4v hand[2][2][B][64];  // [buffer][segment][pair][lane]: 2 * B KiB per buffer
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int half = wave & 1, loader = wave >> 1;
-  const int64_t nseg2 = (k.nseg + 1) / 2;
-  const int64_t sp = (int64_t)blockIdx.x % nseg2, r = (int64_t)blockIdx.x / nseg2;
-  const int64_t slot = r % k.nslot, row = r / k.nslot;
-  const int64_t col = (2 * sp + half) * 64 + lane;
-  int64_t t0, len;
-  pw_leaf(k.nt, k.K, slot, t0, len);
-  if (row >= k.nrow || len <= 0) return;  // the whole workgroup (same leaf, same row)
-  const bool valid = col < k.nc / 4;
-  const int bank = (int)(row / k.ni);
-  const int64_t i = row - (int64_t)bank * k.ni;
-  const int64_t ld = k.in_ld_t;
-  const float *p = k.in[bank] + k.in_off + i * k.in_ld_i + 4 * (valid ? col : 0) + t0 * ld;
-  auto get = [&](int64_t t, float (&x)[4]) {  // spectrum t of the leaf (zeros off the window)
-    if (valid) {
-      ldw<4>(p + t * ld, x);
-    } else {
-      x[0] = x[1] = x[2] = x[3] = 0.0f;
-    }
-  };
-  LeafAcc<4> A;
-  if (!loader) {
-    float x0[4];
-    get(0, x0);
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      A.s[w] = A.hi[w] = A.lo[w] = x0[w];  // the sum starts from the first element
-      A.c[w] = (double)x0[w];
-      A.a1[w] = A.a2[w] = A.a3[w] = A.a4[w] = 0.0;
-    }
-  }
-  // spectra 1 .. len-1 as pairs (1 + 2j: this wave's registers, 2 + 2j: the
-  // loader's, through LDS); an odd count leaves the last spectrum unpaired
-  const int64_t npair = (len - 1) / 2, nb = (npair + B - 1) / B;
-  for (int64_t bt = 0; bt < nb; ++bt) {
-    const int64_t j0 = bt * B;
-    const int n = (int)min((int64_t)B, npair - j0);
-    const int buf = (int)(bt & 1);
-    float cur[B][4];
-    if (loader) {
-#pragma unroll
-      for (int q = 0; q < B; ++q)
-        if (q < n) get(2 + 2 * (j0 + q), cur[q]);
-#pragma unroll
-      for (int q = 0; q < B; ++q)
-        if (q < n) hand[buf][half][q][lane] = f4v{cur[q][0], cur[q][1], cur[q][2], cur[q][3]};
-    } else {
-#pragma unroll
-      for (int q = 0; q < B; ++q)
-        if (q < n) get(1 + 2 * (j0 + q), cur[q]);
-    }
-    __syncthreads();  // batch bt handed over; batch bt - 1's buffer is free again
-    if (!loader) {
-#pragma unroll
-      for (int q = 0; q < B; ++q)
-        if (q < n) {
-          const f4v h = hand[buf][half][q][lane];
-          const float y[4] = {h.x, h.y, h.z, h.w};
-          leaf_step<4>(A, cur[q]);
-          leaf_step<4>(A, y);
-        }
-    }
-  }
-  if (loader) return;
-  if ((len - 1) & 1) {  // the unpaired last spectrum
-    float x[4];
-    get(len - 1, x);
-    leaf_step<4>(A, x);
-  }
-  if (valid) leaf_store<4>(k, A, row, col, slot, len);
-}
-
-// BLDP_KURT_LEAF_TIMING_ILV 1 = TIMING EXPERIMENT ONLY (wrong numerics): the
-// reduce's access pattern on the leaves -- the 4 waves of a workgroup stream
-// ONE leaf of 512 channels, two column halves x two waves interleaving the
-// rows (loads and a Float32 sum only), pricing a loader-wave design
-#ifndef BLDP_KURT_LEAF_TIMING_ILV
-#define BLDP_KURT_LEAF_TIMING_ILV 0
-#endif
-__global__ __launch_bounds__(kB)
-#if BLDP_KURT_LEAF_WAVES > 0
-__attribute__((amdgpu_waves_per_eu(1, BLDP_KURT_LEAF_WAVES)))
-#endif
-void k_kurt_leaf_ilv_timing(const KurtArgs k) {
-  constexpr int B = BLDP_KURT_LEAF_B;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t r = blockIdx.x;  // (row, slot); 2 column halves of 256 channels
-  const int64_t slot = r % k.nslot, row = r / k.nslot;
-  const int64_t col = (wave & 1) * 64 + lane;
-  const int par = wave >> 1;
-  if (row >= k.nrow || col >= k.nc / 4) return;
-  int64_t t0, len;
-  pw_leaf(k.nt, k.K, slot, t0, len);
-  if (len <= 0) return;
-  const int bank = (int)(row / k.ni);
-  const int64_t i = row - (int64_t)bank * k.ni;
-  const int64_t ld = k.in_ld_t;
-  const float *p = k.in[bank] + k.in_off + i * k.in_ld_i + 4 * col + (t0 + par) * ld;
-  const int64_t nr = (len - par + 1) / 2;
-  float s4[4] = {0.f, 0.f, 0.f, 0.f};
-  int64_t t = 0;
-  for (; t + B <= nr; t += B) {
-    float4 v[B];
-#pragma unroll
-    for (int q = 0; q < B; ++q) v[q] = ldnt(p + (t + q) * 2 * ld);
-#pragma unroll
-    for (int q = 0; q < B; ++q) {
-      s4[0] += v[q].x; s4[1] += v[q].y; s4[2] += v[q].z; s4[3] += v[q].w;
-    }
-  }
-  for (; t < nr; ++t) {
-    const float4 v = ldnt(p + t * 2 * ld);
-    s4[0] += v.x; s4[1] += v.y; s4[2] += v.z; s4[3] += v.w;
-  }
-  if (par == 0) {
-    const int64_t n = k.nrow * k.nc, e = row * k.nc + 4 * col;
-    stw<4, float>(k.pf + slot * n + e, s4);
-  }
-}
-
-// 16-byte-aligned windows: the same leaf stream, fed through a per-wave LDS
-// ring of R spectra (1 KiB each: 64 lanes x 4 channels) that
-// global_load_lds_dwordx4 fills.  The loads have no VGPR destination, so R
-// spectra stay in flight per wave the whole time the wave computes (the
-// register-staged kernel has at most B in flight, and none while it computes).
-// Lane L's 16 bytes of a spectrum land at slot + 16 L and are read back by lane
-// L only, so no barrier is needed: the wave's own in-order vmcnt retires a slot
-// (vmcnt(R - B) leaves the B most recent batches' refills in flight), and a
-// slot is refilled only after its values have been used.
-// Measured and not taken (A/B on MI355X, profiles/r02/ab_kurt_leaf_lds.json,
-// bit-identical results): cfg4 2.52 ms against 2.45 ms for k_kurt_leaf with R = 8,
-// B = 4; R = 16 and B = 2 or 8 no better.  Twice the bytes in flight per wave
-// did not raise the rate, so the register-staged kernel's 4 KiB per wave is not
-// what bounds it.
-//   BLDP_KURT_LEAF_LDS  ring slots R (power of two, >= 2 B); 0 (default) = off
-//   BLDP_KURT_LEAF_LB   spectra per batch B
-#ifndef BLDP_KURT_LEAF_LDS
-#define BLDP_KURT_LEAF_LDS 0
-#endif
-#ifndef BLDP_KURT_LEAF_LB
-#define BLDP_KURT_LEAF_LB 4
-#endif
-constexpr int kRing = BLDP_KURT_LEAF_LDS > 0 ? BLDP_KURT_LEAF_LDS : 2 * BLDP_KURT_LEAF_LB;
-constexpr int kRingB = BLDP_KURT_LEAF_LB;
-static_assert((kRing & (kRing - 1)) == 0 && kRing >= 2 * kRingB && kRing <= 16,
-              "BLDP_KURT_LEAF_LDS: a power of two, >= 2 * BLDP_KURT_LEAF_LB, <= 16");
-// s_waitcnt vmcnt(N) (gfx9 encoding; expcnt and lgkmcnt left at their maxima)
-#define BLDP_VMCNT(N) __builtin_amdgcn_s_waitcnt(0x0F70 | ((N) & 15) | (((N) >> 4) << 14))
-
-__global__ __launch_bounds__(kB) void k_kurt_leaf_lds(const KurtArgs k) {
-  constexpr int R = kRing, B = kRingB;
-  __shared__ f4v ring[4][R][64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t u = (int64_t)blockIdx.x * 4 + wave;
-  const int64_t seg = u % k.nseg, r = u / k.nseg;
-  const int64_t slot = r % k.nslot, row = r / k.nslot;
-  const int64_t col = seg * 64 + lane;
-  if (row >= k.nrow || col >= k.nc / 4) return;
-  int64_t t0, len;
-  pw_leaf(k.nt, k.K, slot, t0, len);
-  if (len <= 0) return;  // (leaves hold >= 257 spectra on this path: len > R)
-  const int bank = (int)(row / k.ni);
-  const int64_t i = row - (int64_t)bank * k.ni;
-  const int64_t ld = k.in_ld_t;
-  const float *p = k.in[bank] + k.in_off + i * k.in_ld_i + 4 * col + t0 * ld;
-  auto fill = [&](int64_t t) {  // spectrum t of the leaf -> its ring slot
-    __builtin_amdgcn_global_load_lds(
-        (const void *)(p + t * ld),
-        (__attribute__((address_space(3))) void *)&ring[wave][t & (R - 1)][0], 16, 0, 2 /* nt */);
-  };
-  auto take = [&](int64_t t, float (&x)[4]) {
-    const f4v v = ring[wave][t & (R - 1)][lane];
-    x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
-  };
-#pragma unroll
-  for (int q = 0; q < R; ++q) fill(q);
-  LeafAcc<4> A;
-  {
-    float x0[4];
-    BLDP_VMCNT(R - 1);
-    take(0, x0);
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      A.s[w] = A.hi[w] = A.lo[w] = x0[w];  // the sum starts from the first element
-      A.c[w] = (double)x0[w];
-      A.a1[w] = A.a2[w] = A.a3[w] = A.a4[w] = 0.0;
-    }
-  }
-  fill(R);  // spectra 1..R in flight
-  int64_t j = 1;
-  for (; j + R + B <= len; j += B) {  // refills j+R .. j+R+B-1 exist
-    float x[B][4];
-    BLDP_VMCNT(R - B);
-#pragma unroll
-    for (int q = 0; q < B; ++q) take(j + q, x[q]);
-#pragma unroll
-    for (int q = 0; q < B; ++q) leaf_step<4>(A, x[q]);
-#pragma unroll
-    for (int q = 0; q < B; ++q) fill(j + R + q);
-  }
-  for (; j + R < len; ++j) {  // one refill per spectrum
-    float x[4];
-    BLDP_VMCNT(R - 1);
-    take(j, x);
-    leaf_step<4>(A, x);
-    fill(j + R);
-  }
-  BLDP_VMCNT(0);
-  for (; j < len; ++j) {
-    float x[4];
-    take(j, x);
-    leaf_step<4>(A, x);
-  }
-  leaf_store<4>(k, A, row, col, slot, len);
 }
 
 // Unaligned windows: one lane per (column, leaf) runs the sequential Float32
@@ -1380,15 +1081,7 @@ hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s) {
     k.pm = reinterpret_cast<double *>(ws + L.a_pm);
     k.pf = reinterpret_cast<float *>(ws + L.a_pf);
     const dim3 g1((unsigned)cdivk(k.nrow * k.nslot * k.nseg, 4));
-    if (BLDP_KURT_LEAF_ILV && kLeafW == 4)
-      hipLaunchKernelGGL(k_kurt_leaf_ilv, dim3((unsigned)(k.nrow * k.nslot * ((k.nseg + 1) / 2))),
-                         block, 0, s, k);
-    else if (BLDP_KURT_LEAF_TIMING_ILV && k.nc == 512)
-      hipLaunchKernelGGL(k_kurt_leaf_ilv_timing, dim3((unsigned)(k.nrow * k.nslot)), block, 0, s, k);
-    else if (BLDP_KURT_LEAF_LDS > 0 && kLeafW == 4 && k.rows16)
-      hipLaunchKernelGGL(k_kurt_leaf_lds, g1, block, 0, s, k);
-    else
-      hipLaunchKernelGGL(k_kurt_leaf, g1, block, 0, s, k);
+    hipLaunchKernelGGL(k_kurt_leaf, g1, block, 0, s, k);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return launch_tree<true>(k, ws, L, s);
@@ -1422,8 +1115,7 @@ int64_t kurtosis_max_grid(const KurtArgs &k) {
     case KP_REGS: return cdivk(ncols, kB) * k.nrow;
     case KP_MID: return cdivk(k.nc, 64) * k.nrow;  // (k_kurt_mid2: half of it)
     case KP_LEAF:
-      return BLDP_KURT_LEAF_ILV && kLeafW == 4 ? k.nrow * k.nslot * ((k.nseg + 1) / 2)
-                                               : cdivk(k.nrow * k.nslot * k.nseg, 4);
+      return cdivk(k.nrow * k.nslot * k.nseg, 4);
     default:
       return std::max(cdivk(k.nc, kB) * k.nrow * k.nslot,
                       cdivk(cdivk(k.nc, 64), 4 / k.ts) * k.nrow * k.nchunk);

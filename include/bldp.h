@@ -50,7 +50,9 @@
 extern "C" {
 #endif
 
-#define BLDP_ABI_VERSION 1
+/* 2: bldp_bslz4_decode_dev / _async take out_len (round 2); BLDP_EIO; the
+ *    typed (non-Float32) entry points */
+#define BLDP_ABI_VERSION 2
 
 #if defined(BLDP_BUILD)
 #define BLDP_API __attribute__((visibility("default")))
@@ -69,6 +71,7 @@ enum bldp_op { BLDP_OP_SUM = 0, BLDP_OP_MEAN = 1, BLDP_OP_MAX = 2, BLDP_OP_MIN =
 #define BLDP_ENOMEM (-5)  /* device or pinned allocation failed                  */
 #define BLDP_EBOUNDS (-6) /* window outside the array (BoundsError analogue)     */
 #define BLDP_ECOMM (-7)   /* RCCL error in the cross-GPU band exchange          */
+#define BLDP_EIO (-8)     /* a file read failed or ended early (truncated file)  */
 
 #define BLDP_MAX_BANKS 64
 

@@ -110,8 +110,8 @@ def test_reduce_paths_integer_exact(eng, orc, shape):
 # segment of fewer than 4 groups, several IFs and time blocks, every op.
 IL_SHAPES = [(4098, 1, 16, 1024, 16), (8194, 2, 8, 512, 4), (4097, 1, 8, 2048, 8),
              (4099, 1, 4, 4096, 2),
-             # short time blocks (k_reduce_ilt: 16 / T blocks per workgroup, the
-             # last group partial): T = 1 is the reference's fqav, no integration
+             # short time blocks, one per workgroup: T = 1 is the reference's
+             # fqav, no integration
              (4098, 1, 16, 1024, 1), (4097, 2, 20, 512, 1), (4096, 1, 5, 2048, 1),
              (4099, 1, 36, 1024, 4)]
 
@@ -184,6 +184,59 @@ def test_reduce_short_time_blocks_integer_exact(eng, orc, shape):
     banks = [x] + [eng.synth(nco * F, ni, nt, 1024, seed=b, kind=1) for b in (1, 2)]
     got = host(eng, eng.band_reduce(banks, F, T))
     assert same_bits(got, orc.stitch([orc.reduce(host(eng, b), F, T) for b in banks]))
+
+
+# Small groups that are not a power of two (F = 3, 5, 6, 7, 12) with short time
+# blocks: k_reduce_lanet, one lane per group and NRW / T time blocks per
+# workgroup (the last time group partial); the 0002-band windows of 65535 and
+# 65532 channels among them; bit-exact on integer data, windows and bands.
+LANET_SHAPES = [(1000, 1, 37, 3, 1), (21845, 1, 18, 3, 1), (300, 2, 20, 5, 2), (257, 1, 33, 6, 1),
+                (100, 3, 12, 7, 4), (513, 1, 19, 12, 1), (5461, 1, 9, 12, 1), (200, 1, 8, 12, 2),
+                (70, 2, 24, 3, 4), (90, 1, 17, 6, 2)]
+
+
+def lanet_rows(F):
+    return 16 if F <= 3 else 8 if F <= 6 else 4
+
+
+@pytest.mark.parametrize("shape", LANET_SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_reduce_small_odd_groups_short_time_blocks_integer_exact(eng, orc, shape):
+    nco, ni, nt, F, T = shape
+    x = eng.synth(nco * F, ni, nt, 1024, seed=11 * nco + F + nt, kind=1)
+    a = host(eng, x)
+    nto, tpb = nt // T, lanet_rows(F) // T
+    for op in ("sum", "max", "min", "mean"):
+        plan = eng.plan(x, F, T, op)
+        assert plan["path"] == "lane", (shape, plan)
+        assert plan["workgroups"] == -(-nco // 256) * ni * -(-nto // tpb), (shape, plan)
+        got = host(eng, eng.reduce(x, F, T, op))
+        want = orc.reduce(a, F, T, op)
+        if op == "mean" and (F * T) & (F * T - 1):
+            np.testing.assert_allclose(got, want, rtol=RTOL)  # s / (F T) in Float32 vs Float64
+        else:
+            assert same_bits(got, want), (shape, op)
+    # a window one group and one spectrum in, and a band of three banks
+    if nco > 1 and nt > T:
+        w = [F, (nco - 1) * F, 1, 0, ni, 1, 1, (nt - 1) // T * T, 1]
+        got = host(eng, eng.reduce(x, F, T, "sum", w))
+        assert same_bits(got, orc.reduce(a, F, T, "sum", w)), (shape, "window")
+    banks = [x] + [eng.synth(nco * F, ni, nt, 1024, seed=b, kind=1) for b in (1, 2)]
+    got = host(eng, eng.band_reduce(banks, F, T))
+    assert same_bits(got, orc.stitch([orc.reduce(host(eng, b), F, T) for b in banks]))
+
+
+def test_reduce_small_odd_groups_gamma_rtol(eng, orc):
+    """Float data through k_reduce_lanet at the 1e-5 tolerance."""
+    for F, T in ((3, 1), (12, 1), (5, 2), (7, 4)):
+        nc = 4096 // F * F
+        a = orc.gamma_bandpass(nc, 1, 40, 1024, 31 * F + T)
+        x = dev(eng, a)
+        assert eng.plan(x, F, T)["path"] == "lane"
+        for op in ("sum", "mean"):
+            np.testing.assert_allclose(host(eng, eng.reduce(x, F, T, op)), orc.reduce(a, F, T, op),
+                                       rtol=RTOL, err_msg=str((F, T, op)))
+        for op in ("max", "min"):
+            assert same_bits(host(eng, eng.reduce(x, F, T, op)), orc.reduce(a, F, T, op))
 
 
 # Large groups (F = 512..4096) with short time blocks on windows with few

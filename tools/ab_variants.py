@@ -21,11 +21,19 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 VDIR = os.path.join(REPO, "build", "variants")
 CSRC = os.path.join(REPO, "bldistributeddataproducts.jl_amd", "csrc")
 
+# Variants that only exist in an earlier source tree (experiments measured
+# and then taken out of the product sources) are built from that revision:
+# {"rev": commit, "extra": flags}.  R02 is the last round-2 commit.
+R02 = "5f5c135"
 VARIANTS = {
-    "base": "",                          # nt loads+stores, batch 8, no grid cap
+    "base": "",
+    "nodpp": "-DBLDP_DPP=0",  # lane folds on __shfl_xor (ds_bpermute) instead of DPP / permlane swaps
+    "r02": {"rev": R02, "extra": ""},  # the round-2 product build
+    "nolanet": "-DBLDP_LANET=0",  # small odd F, short time blocks: the lane / tile / vector paths                          # nt loads+stores, batch 8, no grid cap
     "cap4ts": "-DBLDP_MAX_WG_PER_CU=-1",  # 4 WG/CU grid cap for time-split plans
     "plain": "-DBLDP_NT_LOADS=0 -DBLDP_NT_STORES=0 -DBLDP_MAX_WG_PER_CU=0",  # round-1 start
     # tile path (misaligned / odd-F windows): columns per thread, accumulator sets
@@ -54,9 +62,9 @@ VARIANTS = {
     "rowtnopack": "-DBLDP_ROWT_PACK=0",
     "nowavet": "-DBLDP_WAVET=0",
     "wavet2": "-DBLDP_WAVET=2",
-    "noilt": "-DBLDP_IL_TPB=0",
-    "rowtnobfly": "-DBLDP_ROWT_TIMING_NOBFLY=1",  # timing only: wrong numerics
-    "rowthalv": "-DBLDP_ROWT_HALVING=1",
+    "ilt": {"rev": R02, "extra": "-DBLDP_IL_TPB=1"},  # k_reduce_ilt (removed in round 3)
+    "rowtnobfly": {"rev": R02, "extra": "-DBLDP_ROWT_TIMING_NOBFLY=1"},  # timing only: wrong numerics
+    "rowthalv": {"rev": R02, "extra": "-DBLDP_ROWT_HALVING=1"},
     "nonarrowt": "-DBLDP_NARROW_TPB=0",
     "rowtmw8": "-DBLDP_ROWT_MAXWAVES=0",
     # narrow windows: time split over otherwise idle waves, with / without grid cap
@@ -75,25 +83,25 @@ VARIANTS = {
     "kleafw2": "-DBLDP_KURT_LEAF_WAVES=2",
     "kleafw3": "-DBLDP_KURT_LEAF_WAVES=3",
     "kleafb2": "-DBLDP_KURT_LEAF_B=2",
-    "kleaft32": "-DBLDP_KURT_LEAF_TIMING_F32=1",  # timing only: wrong numerics
-    "kleaft32b8": "-DBLDP_KURT_LEAF_TIMING_F32=1 -DBLDP_KURT_LEAF_B=8",
-    "kleaflo": "-DBLDP_KURT_LEAF_TIMING_LOADONLY=1",  # timing only: loads + sum
-    "kleaflow4": "-DBLDP_KURT_LEAF_TIMING_LOADONLY=1 -DBLDP_KURT_LEAF_WAVES=4",
-    "kleaflob8w4": "-DBLDP_KURT_LEAF_TIMING_LOADONLY=1 -DBLDP_KURT_LEAF_B=8 -DBLDP_KURT_LEAF_WAVES=4",
-    "kleaflob8": "-DBLDP_KURT_LEAF_TIMING_LOADONLY=1 -DBLDP_KURT_LEAF_B=8",
-    "kleafilv": "-DBLDP_KURT_LEAF_TIMING_ILV=1",  # timing only: reduce-like leaf streams
-    "kleafilvb8": "-DBLDP_KURT_LEAF_TIMING_ILV=1 -DBLDP_KURT_LEAF_B=8",
-    "kleafilvw4": "-DBLDP_KURT_LEAF_TIMING_ILV=1 -DBLDP_KURT_LEAF_WAVES=4",
-    "kilv": "-DBLDP_KURT_LEAF_ILV=1",  # k_kurt_leaf_ilv (bit-identical to base)
-    "kilvb2": "-DBLDP_KURT_LEAF_ILV=1 -DBLDP_KURT_ILV_B=2",
-    "kilvb8": "-DBLDP_KURT_LEAF_ILV=1 -DBLDP_KURT_ILV_B=8",
-    "kleafilvw2": "-DBLDP_KURT_LEAF_TIMING_ILV=1 -DBLDP_KURT_LEAF_WAVES=2",
+    "kleaft32": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_TIMING_F32=1"},  # timing only: wrong numerics
+    "kleaft32b8": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_TIMING_F32=1 -DBLDP_KURT_LEAF_B=8"},
+    "kleaflo": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_TIMING_LOADONLY=1"},  # timing only: loads + sum
+    "kleaflow4": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_TIMING_LOADONLY=1 -DBLDP_KURT_LEAF_WAVES=4"},
+    "kleaflob8w4": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_TIMING_LOADONLY=1 -DBLDP_KURT_LEAF_B=8 -DBLDP_KURT_LEAF_WAVES=4"},
+    "kleaflob8": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_TIMING_LOADONLY=1 -DBLDP_KURT_LEAF_B=8"},
+    "kleafilv": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_TIMING_ILV=1"},  # timing only: reduce-like leaf streams
+    "kleafilvb8": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_TIMING_ILV=1 -DBLDP_KURT_LEAF_B=8"},
+    "kleafilvw4": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_TIMING_ILV=1 -DBLDP_KURT_LEAF_WAVES=4"},
+    "kilv": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_ILV=1"},  # k_kurt_leaf_ilv (bit-identical to base)
+    "kilvb2": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_ILV=1 -DBLDP_KURT_ILV_B=2"},
+    "kilvb8": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_ILV=1 -DBLDP_KURT_ILV_B=8"},
+    "kleafilvw2": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_TIMING_ILV=1 -DBLDP_KURT_LEAF_WAVES=2"},
     # k_kurt_mid with two channels per lane (512-byte wave loads), 8 or 4 waves
     "kmid2w8": "-DBLDP_KURT_MID_CPL=2 -DBLDP_KURT_MID_NW=8",
     "kmid2w4": "-DBLDP_KURT_MID_CPL=2 -DBLDP_KURT_MID_NW=4",
     "kleafpipe2": "-DBLDP_KURT_LEAF_PIPE=1 -DBLDP_KURT_LEAF_B=2",
     "kleafpipe2w5": "-DBLDP_KURT_LEAF_PIPE=1 -DBLDP_KURT_LEAF_B=2 -DBLDP_KURT_LEAF_MINWAVES=5",
-    "kmidnochain": "-DBLDP_KURT_MID_TIMING_NOCHAIN=1",  # timing only: wrong numerics
+    "kmidnochain": {"rev": R02, "extra": "-DBLDP_KURT_MID_TIMING_NOCHAIN=1"},  # timing only: wrong numerics
     # misaligned unit-step windows on the vector paths (dword-aligned 16-byte loads);
     # 2 = the kurtosis register / leaf paths too
     "unal": "-DBLDP_UNALIGNED_VEC=1",
@@ -106,19 +114,32 @@ VARIANTS = {
     # streamed kurtosis leaves through a per-wave LDS ring filled by global_load_lds
     "nts0": "-DBLDP_NT_SCALAR_STORES=0",
     "nts2": "-DBLDP_NT_SCALAR_STORES=2",
-    "klds8": "-DBLDP_KURT_LEAF_LDS=8",
-    "klds16": "-DBLDP_KURT_LEAF_LDS=16",
-    "klds8b2": "-DBLDP_KURT_LEAF_LDS=8 -DBLDP_KURT_LEAF_LB=2",
-    "klds16b8": "-DBLDP_KURT_LEAF_LDS=16 -DBLDP_KURT_LEAF_LB=8",
+    "klds8": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_LDS=8"},
+    "klds16": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_LDS=16"},
+    "klds8b2": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_LDS=8 -DBLDP_KURT_LEAF_LB=2"},
+    "klds16b8": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_LDS=16 -DBLDP_KURT_LEAF_LB=8"},
 }
+
+
+def source_tree(rev):
+    """csrc/ and include/ of an earlier commit, unpacked under build/variants/src_REV."""
+    root = os.path.join(VDIR, f"src_{rev}")
+    if not os.path.isdir(root):
+        os.makedirs(root)
+        arch = subprocess.run(["git", "-C", REPO, "archive", rev, "include",
+                               "bldistributeddataproducts.jl_amd/csrc"], check=True,
+                              capture_output=True).stdout
+        subprocess.run(["tar", "-x", "-C", root], input=arch, check=True)
+    return os.path.join(root, "bldistributeddataproducts.jl_amd", "csrc")
 
 
 def build(names):
     os.makedirs(VDIR, exist_ok=True)
     for n in names:
         out = os.path.join(VDIR, f"libbldp_{n}.so")
-        subprocess.run(["make", "-s", "-B", "-C", CSRC, f"OUT={out}", f"EXTRA={VARIANTS[n]}"],
-                       check=True)
+        v = VARIANTS[n]
+        csrc, extra = (CSRC, v) if isinstance(v, str) else (source_tree(v["rev"]), v["extra"])
+        subprocess.run(["make", "-s", "-B", "-C", csrc, f"OUT={out}", f"EXTRA={extra}"], check=True)
         print("built", out)
 
 
@@ -177,7 +198,15 @@ def run(names, rounds, iters, suite="main"):
 
     b3 = [eng.synth(1 << 26, 1, 16, 1 << 20, seed=10 * b, kind=0, out=o)
           for b, o in enumerate(eng.band_empty(8, 1 << 26, 1, 16))]  # one slab, as bench.py
-    if suite == "kurt":
+    if suite == "t1v":  # the reference's own fqav (T = 1) shapes
+        del b3
+        import t1_probe
+
+        for c in t1_probe.build_cases(pkg):
+            cases.append((c["label"], lambda L, c=c: c["go"](L, sp), c["bytes"], c["out"],
+                          (c["keep"], c["banks"])))
+        cases_done = True
+    elif suite == "kurt":
         kurt_case("kurt cfg3 nt16", b3)
         kurt_case("kurt cfg3 nt12", b3, [0, 1 << 26, 1, 0, 1, 1, 0, 12, 1])
         kurt_case("kurt cfg3 c0=1 nt16", b3, [1, (1 << 26) - 4, 1, 0, 1, 1, 0, 16, 1])
@@ -347,7 +376,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--suite", default="main", choices=["main", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1"])
+    ap.add_argument("--suite", default="main", choices=["main", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:

@@ -1,0 +1,167 @@
+// mix_ceiling.hip — what a streaming kernel can reach on MI355X when it reads
+// R bytes for every byte it writes (the read:write mix of fqav at fqavby = R
+// with no time integration: F floats in, 1 out), at the sizes the reduce
+// actually runs at (one 0002 file, the 0002 band, the 0000 band).
+//
+// k_mix<R>: a workgroup chunk is UB units; a unit is R x 4 KiB read
+// contiguously (thread t reads float4 t + 256 k, k < R: every
+// workgroup-instruction reads 4 KiB contiguous) and one 4 KiB contiguous write
+// (thread t writes the sum of its R float4).  ~16 loads in flight per lane.
+// This is the best case for the mix: every read and every write instruction
+// covers whole 128-byte lines, writes are 1 KiB per wave-instruction.
+//
+//   hipcc --offload-arch=gfx950 -O3 -o build/mix_ceiling tools/mix_ceiling.hip
+//   ./build/mix_ceiling [reps]          (JSON lines on stdout)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+#define CK(x)                                                                    \
+  do {                                                                           \
+    hipError_t e_ = (x);                                                         \
+    if (e_ != hipSuccess) {                                                      \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                   \
+    }                                                                            \
+  } while (0)
+
+// ST: 1 = nt store, 2 = plain store, 0 = no store (pure read; the store is
+// kept behind an impossible condition so the loads are not dead)
+template <int R, int ST>
+__global__ __launch_bounds__(256) void k_mix(const f4v *__restrict__ in, f4v *__restrict__ out,
+                                             int64_t nunits) {
+  constexpr int UB = R >= 16 ? 1 : 16 / R;  // units per chunk
+  constexpr int KB = R >= 16 ? 16 : R;      // loads per batch per unit
+  const int t = threadIdx.x;
+  const int64_t nchunks = (nunits + UB - 1) / UB;
+  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const int64_t u0 = c * UB;
+    f4v acc[UB];
+#pragma unroll
+    for (int b = 0; b < UB; ++b) acc[b] = f4v{0, 0, 0, 0};
+#pragma unroll
+    for (int k0 = 0; k0 < R; k0 += KB) {
+      f4v v[UB * KB];
+#pragma unroll
+      for (int b = 0; b < UB; ++b)
+#pragma unroll
+        for (int k = 0; k < KB; ++k)
+          v[b * KB + k] = (u0 + b < nunits)
+                              ? __builtin_nontemporal_load(in + (u0 + b) * R * 256 + 256 * (k0 + k) + t)
+                              : f4v{0, 0, 0, 0};
+#pragma unroll
+      for (int b = 0; b < UB; ++b)
+#pragma unroll
+        for (int k = 0; k < KB; ++k) acc[b] += v[b * KB + k];
+    }
+#pragma unroll
+    for (int b = 0; b < UB; ++b) {
+      if (u0 + b >= nunits) break;
+      f4v *o = out + (u0 + b) * 256 + t;
+      if (ST == 1)
+        __builtin_nontemporal_store(acc[b], o);
+      else if (ST == 2)
+        *o = acc[b];
+      else if (acc[b].x == 1234.5f)
+        *o = acc[b];
+    }
+  }
+}
+
+__global__ void k_fill(f4v *p, int64_t n4) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256)
+    p[i] = f4v{1.f, 2.f, 3.f, 4.f};
+}
+
+static float median(std::vector<float> v) {
+  std::sort(v.begin(), v.end());
+  return v[v.size() / 2];
+}
+
+template <int R, int ST>
+static void run(const f4v *in, f4v *out, int64_t read_bytes, int grid_mode, int reps,
+                const char *label, int ncu) {
+  const int64_t nunits = read_bytes / ((int64_t)R * 4096);
+  if (nunits <= 0) return;
+  constexpr int UB = R >= 16 ? 1 : 16 / R;
+  const int64_t nchunks = (nunits + UB - 1) / UB;
+  // grid_mode 0: one workgroup per chunk; k > 0: k workgroups per CU (persistent)
+  const int64_t grid = grid_mode == 0 ? nchunks : std::min<int64_t>(nchunks, (int64_t)grid_mode * ncu);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  std::vector<float> ms;
+  for (int r = 0; r < reps + 2; ++r) {
+    CK(hipEventRecord(e0, 0));
+    for (int i = 0; i < 5; ++i)  // back to back, as the library's timings are taken
+      hipLaunchKernelGGL((k_mix<R, ST>), dim3((unsigned)grid), dim3(256), 0, 0, in, out, nunits);
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float m;
+    CK(hipEventElapsedTime(&m, e0, e1));
+    if (r >= 2) ms.push_back(m / 5);
+  }
+  const double rb = (double)nunits * R * 4096, wb = ST ? (double)nunits * 4096 : 0.0;
+  const float med = median(ms);
+  printf("{\"size\": \"%s\", \"read_bytes\": %.0f, \"write_bytes\": %.0f, \"R\": %d, \"store\": \"%s\", "
+         "\"grid\": \"%s\", \"ms_median\": %.4f, \"ms_min\": %.4f, \"GBps_median\": %.1f}\n",
+         label, rb, wb, R, ST == 1 ? "nt" : ST == 2 ? "plain" : "none",
+         grid_mode == 0 ? "chunk" : (grid_mode == 1 ? "1/CU" : grid_mode == 2 ? "2/CU" : "4/CU"),
+         med, *std::min_element(ms.begin(), ms.end()), (rb + wb) / med / 1e6);
+  fflush(stdout);
+  CK(hipEventDestroy(e0));
+  CK(hipEventDestroy(e1));
+}
+
+template <int R>
+static void run_r(const f4v *in, f4v *out, int64_t bytes, int reps, const char *label, int ncu,
+                  bool grids) {
+  run<R, 1>(in, out, bytes, 0, reps, label, ncu);
+  run<R, 2>(in, out, bytes, 0, reps, label, ncu);
+  if (grids)
+    for (int g : {1, 2, 4}) run<R, 1>(in, out, bytes, g, reps, label, ncu);
+}
+
+int main(int argc, char **argv) {
+  const int reps = argc > 1 ? atoi(argv[1]) : 20;
+  hipDeviceProp_t prop;
+  CK(hipGetDeviceProperties(&prop, 0));
+  const int ncu = prop.multiProcessorCount;
+  const int64_t big = 32ll << 30;
+  f4v *in, *out;
+  CK(hipMalloc(&in, big));
+  CK(hipMalloc(&out, big));  // R = 1 (copy) writes as much as it reads
+  hipLaunchKernelGGL(k_fill, dim3(65536), dim3(256), 0, 0, in, big / 16);
+  CK(hipDeviceSynchronize());
+  struct Size {
+    const char *label;
+    int64_t bytes;
+  };
+  // one 0002 file (65536 x 279 floats), the 0002 band (8 of them), the 0000 band
+  const Size sizes[] = {{"0002 file 73 MB", 65536ll * 279 * 4},
+                        {"0002 band 585 MB", 8ll * 65536 * 279 * 4},
+                        {"0000 band 32 GiB", big}};
+  for (const Size &s : sizes) {
+    const bool grids = s.bytes < big;
+    run_r<1>(in, out, s.bytes, reps, s.label, ncu, grids);
+    run_r<2>(in, out, s.bytes, reps, s.label, ncu, grids);
+    run_r<3>(in, out, s.bytes, reps, s.label, ncu, grids);
+    run_r<4>(in, out, s.bytes, reps, s.label, ncu, grids);
+    run_r<8>(in, out, s.bytes, reps, s.label, ncu, grids);
+    run_r<12>(in, out, s.bytes, reps, s.label, ncu, grids);
+    run_r<16>(in, out, s.bytes, reps, s.label, ncu, grids);
+    run_r<64>(in, out, s.bytes, reps, s.label, ncu, grids);
+    run_r<256>(in, out, s.bytes, reps, s.label, ncu, grids);
+    run<16, 0>(in, out, s.bytes, 0, reps, s.label, ncu);  // pure read, 64 KiB per workgroup
+    if (grids)
+      for (int g : {1, 2, 4}) run<16, 0>(in, out, s.bytes, g, reps, s.label, ncu);
+  }
+  CK(hipFree(in));
+  CK(hipFree(out));
+  return 0;
+}
