@@ -60,16 +60,27 @@ def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
-def traffic_from_profile(cfg_name, n_local_banks):
-    """HBM bytes per launch from the committed PMC profile (profiles/), or None."""
+def traffic_from_profile(cfg_name, n_local_banks, with_source=False):
+    """HBM bytes per launch from the committed PMC profile (profiles/), or None.
+    with_source: (bytes, where they come from) — a committed counter session,
+    not a measurement taken in this run."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
     except (OSError, ValueError):
-        return None
+        return (None, None) if with_source else None
     e = d.get(cfg_name, {}).get(str(n_local_banks))
-    return e.get("hbm_bytes_per_launch") if e else None
+    b = e.get("hbm_bytes_per_launch") if e else None
+    if not with_source:
+        return b
+    src = None
+    if e:
+        files = e.get("source") or []
+        src = (f"profiles/pmc_traffic.json [{cfg_name!r}][{str(n_local_banks)!r}]: committed "
+               f"rocprofv3 --pmc session ({', '.join(files) or 'per-kernel medians'}; "
+               f"{e.get('correction', '')}), not measured in this run")
+    return b, src
 
 
 def host_cpu_info():
@@ -108,6 +119,9 @@ def cpu_baseline(cfg, seconds, eng, torch):
     torch.cuda.empty_cache()
     per_rep = nb * 4 * (nch * cfg["nif"] * nt + (nch // cfg["F"]) * cfg["nif"] * (nt // cfg["T"]))
     info = host_cpu_info()
+    # the pool runs on the box's CPU share (OMP_NUM_THREADS, 16 on the GPU
+    # box), not on every CPU the host has (host_nproc) or this process could
+    # be scheduled on (affinity_cpus): the key names the thread count
     nthr = info["omp_num_threads"] or info["affinity_cpus"]
 
     def timed(fn, secs):
@@ -128,9 +142,12 @@ def cpu_baseline(cfg, seconds, eng, torch):
                            f"spectra), F={cfg['F']} T={cfg['T']}, {reps} passes in {el:.1f} s; "
                            "oracle/bldp_oracle.c (Float64 accumulate, gcc -O3 x86-64-v3), "
                            "one pthread per bank as one Distributed worker per bank",
-                 "all_cores": {"value": round(gall, 3), "threads": nthr,
-                               "sample": f"same banks, output channels split over {nthr} "
-                                         f"threads, {reps_all} passes in {el_all:.1f} s"}},
+                 f"pool_{nthr}_threads": {
+                     "value": round(gall, 3), "threads": nthr,
+                     "sample": f"same banks, output channels split over {nthr} threads "
+                               f"(OMP_NUM_THREADS, this box's CPU share; not all "
+                               f"{info['host_nproc']} host CPUs), {reps_all} passes in "
+                               f"{el_all:.1f} s"}},
                 **info)
 
 
@@ -192,6 +209,8 @@ def bench_kurtosis(args, cfg, eng, torch):
                          # HBM bytes per call from the committed PMC passes (every
                          # kernel of the call; profiles/pmc_traffic.json "kurt_<cfg>")
                          "traffic": traffic_from_profile("kurt_" + args.config, cfg["nbank"]),
+                         "traffic_source": traffic_from_profile("kurt_" + args.config,
+                                                                cfg["nbank"], True)[1],
                          "kernel": kern, "call_ms": round(ms, 4), "bytes_per_call": algo}}
 
 
@@ -636,7 +655,7 @@ def main():
         f" ({len(mine)}-bank launch)"
     value = bytes_step / (ms_step * 1e-3) / 1e9
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
-    traffic = traffic_from_profile(args.config, len(mine))
+    traffic, traffic_src = traffic_from_profile(args.config, len(mine), with_source=True)
 
     ndev = torch.cuda.device_count()
     if not pipe:
@@ -672,7 +691,8 @@ def main():
                        "bytes_per_step": bytes_step, **run_info},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "kernel": kernel_name,
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel": kernel_name,
                          "kernel_ms": round(kern_ms, 4), "bytes_per_launch": bytes_launch},
             "host_enqueue_ms_per_step": round(host_ms, 4),
             "cpu_baseline": cpu,

@@ -9,7 +9,7 @@ The directory name is not a Python identifier; load it with
 ``__graft_entry__.load_package()`` (registers it as ``bldp_amd``).
 """
 from . import _lib, band, engine, fbh5, filestream, gbt, h5chunks, idxs, readers, worker  # noqa: F401
-from ._lib import ArgumentError, BLDPError, BoundsError, DimensionMismatch  # noqa: F401
+from ._lib import ArgumentError, BLDPError, BoundsError, DimensionMismatch, ReadError  # noqa: F401
 from .idxs import COLON, JRange, sanitizeidxs  # noqa: F401
 from .worker import FRange, fqav  # noqa: F401
 
@@ -18,4 +18,4 @@ GBT.WorkerFunctions = worker
 WorkerFunctions = worker
 
 __all__ = ["GBT", "WorkerFunctions", "fqav", "JRange", "FRange", "COLON", "sanitizeidxs",
-           "engine", "band", "DimensionMismatch", "BoundsError", "BLDPError"]
+           "engine", "band", "DimensionMismatch", "BoundsError", "BLDPError", "ReadError"]

@@ -572,6 +572,79 @@ int bldp_band_kurtosis_f32(int nbank, const float *const *in, int64_t nchan, int
   return kurt_run(k, out, nullptr, stream);
 }
 
+int bldp_reduce_out_dtype(int dtype, int op) {
+  const int d = typed_out_dtype(dtype, op);
+  if (d < 0) return fail(BLDP_EINVAL, "unknown element type %d or op %d", dtype, op);
+  return d;
+}
+
+int bldp_reduce_strided(int dtype, const void *in, int64_t nchan, int64_t nif, int64_t ntime,
+                        const int64_t *win, int64_t fqavby, int64_t tavby, int op, void *out,
+                        int64_t out_ld_i, int64_t out_ld_t, void *stream) {
+  if (dtype == BLDP_DT_F32)
+    return bldp_reduce_strided_f32(static_cast<const float *>(in), nchan, nif, ntime, win, fqavby,
+                                   tavby, op, static_cast<float *>(out), out_ld_i, out_ld_t,
+                                   stream);
+  if (!dtype_size(dtype)) return fail(BLDP_EINVAL, "unknown element type %d", dtype);
+  if (!valid_op(op)) return fail(BLDP_EINVAL, "unknown op %d (0=sum 1=mean 2=max 3=min)", op);
+  Geo g;
+  int rc = resolve_window(nchan, nif, ntime, win, &g);
+  if (rc) return rc;
+  int64_t F, T;
+  rc = resolve_factors(g, fqavby, tavby, &F, &T);
+  if (rc) return rc;
+  TypedArgs a{};
+  a.dtype = dtype;
+  a.nbank = 1;
+  a.in[0] = in;
+  a.out = out;
+  a.out_ld_i = out_ld_i;
+  a.out_ld_t = out_ld_t;
+  a.in_off = g.off;
+  a.in_cs = g.cs;
+  a.in_ld_i = g.ld_i;
+  a.in_ld_t = g.ld_t;
+  a.nco = g.nc / F;
+  a.ni = g.ni;
+  a.nto = g.nt / T;
+  a.F = F;
+  a.T = T;
+  if (a.nco * a.ni * a.nto == 0) return BLDP_OK;
+  if (!in || !out) return fail(BLDP_EINVAL, "null pointer");
+  hipError_t e = launch_reduce_typed(a, op, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(BLDP_EHIP, "typed reduce launch: %s", hipGetErrorString(e));
+  return BLDP_OK;
+}
+
+int bldp_kurtosis(int dtype, const void *in, int64_t nchan, int64_t nif, int64_t ntime,
+                  const int64_t *win, double *out, void *stream) {
+  if (dtype == BLDP_DT_F32)
+    return bldp_kurtosis_f32(static_cast<const float *>(in), nchan, nif, ntime, win, out, nullptr,
+                             stream);
+  if (!dtype_size(dtype)) return fail(BLDP_EINVAL, "unknown element type %d", dtype);
+  Geo g;
+  int rc = resolve_window(nchan, nif, ntime, win, &g);
+  if (rc) return rc;
+  TypedArgs a{};
+  a.dtype = dtype;
+  a.nbank = 1;
+  a.in[0] = in;
+  a.out = out;
+  a.in_off = g.off;
+  a.in_cs = g.cs;
+  a.in_ld_i = g.ld_i;
+  a.in_ld_t = g.ld_t;
+  a.nco = g.nc;
+  a.ni = g.ni;
+  a.nto = g.nt;
+  a.F = a.T = 1;
+  if (a.nco * a.ni == 0) return BLDP_OK;
+  if (!out || (!in && g.nt > 0)) return fail(BLDP_EINVAL, "null pointer");
+  hipError_t e = launch_kurtosis_typed(a, out, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(BLDP_EHIP, "typed kurtosis launch: %s", hipGetErrorString(e));
+  return BLDP_OK;
+}
+
 int bldp_fqav_range(double first, double step, int64_t len, int64_t n, double *out_first,
                     double *out_step, int64_t *out_len) {
   if (!out_first || !out_step || !out_len) return fail(BLDP_EINVAL, "null pointer");

@@ -140,6 +140,23 @@ struct UnchunkArgs {
 };
 hipError_t launch_unchunk(const float *packed, const UnchunkArgs &u, float *out, hipStream_t s);
 
+// Reductions and kurtosis of non-Float32 elements (typed.hip).  Element
+// (c, i, t) of bank b at in[b][in_off + c*in_cs + i*in_ld_i + t*in_ld_t],
+// output (c', i, t') at out[b*out_bank + c' + i*out_ld_i + t'*out_ld_t]
+// (kurtosis: out dense [nbank][ni][nco], nto = the spectra).
+struct TypedArgs {
+  const void *in[BLDP_MAX_BANKS];
+  void *out;
+  int32_t dtype, nbank;
+  int64_t out_bank, out_ld_i, out_ld_t;
+  int64_t in_off, in_cs, in_ld_i, in_ld_t;
+  int64_t nco, ni, nto, F, T;
+};
+size_t dtype_size(int dtype);              // 0 = unknown
+int typed_out_dtype(int dtype, int op);    // -1 = invalid
+hipError_t launch_reduce_typed(const TypedArgs &a, int op, hipStream_t s);
+hipError_t launch_kurtosis_typed(const TypedArgs &a, double *out, hipStream_t s);
+
 hipError_t launch_synth(float *out, int64_t nchan, int64_t nif, int64_t ntime, int64_t nfpc,
                         uint64_t seed, int kind, hipStream_t s);
 

@@ -179,3 +179,93 @@ extern "C" int bldp_kurtosis_host_f32(int dev, const float *in, int64_t nchan, i
     return BLDP_OK;
   });
 }
+
+// ---------------------------------------------------------------------------
+// Host forms of the typed entry points (include/bldp.h): the span of host
+// memory the window touches is copied to device `dev` in one piece, the typed
+// kernels run on it (addressed through a pointer shifted by the span's first
+// element, so the caller's window applies unchanged) and the dense result is
+// copied back.  Synchronous.
+namespace {
+
+// First and last element offsets a window touches (nothing when empty).
+bool window_span(int64_t nchan, int64_t nif, int64_t ntime, const int64_t *win, int64_t *lo,
+                 int64_t *hi) {
+  const int64_t dims[3] = {nchan, nif, ntime};
+  const int64_t pitch[3] = {1, nchan, nchan * nif};
+  *lo = *hi = 0;
+  for (int ax = 0; ax < 3; ++ax) {
+    const int64_t start = win ? win[3 * ax] : 0, count = win ? win[3 * ax + 1] : dims[ax],
+                  step = win ? win[3 * ax + 2] : 1;
+    if (count <= 0) return false;
+    const int64_t a = start * pitch[ax], b = (start + (count - 1) * step) * pitch[ax];
+    *lo += std::min(a, b);
+    *hi += std::max(a, b);
+  }
+  return true;
+}
+
+template <class Fn>
+int typed_host(int dev, int dtype, const void *in, int64_t nchan, int64_t nif, int64_t ntime,
+               const int64_t *win, size_t out_bytes, void *out, Fn &&run) {
+  const size_t esz = bldp::dtype_size(dtype);
+  int64_t lo, hi;
+  if (!window_span(nchan, nif, ntime, win, &lo, &hi)) return BLDP_OK;
+  if (!in || !out) return bldp::set_error(BLDP_EINVAL, "null pointer");
+  return with_stager(dev, [&](bldp::Stager *sg) -> int {
+    void *dbuf, *dout;
+    int r = bldp::stager_buffer(sg, 0, (size_t)(hi - lo + 1) * esz, &dbuf);
+    if (!r) r = bldp::stager_buffer(sg, 2, std::max<size_t>(out_bytes, 8), &dout);
+    if (r) return r;
+    HCHK(hipMemcpyAsync(dbuf, (const char *)in + lo * esz, (size_t)(hi - lo + 1) * esz,
+                        hipMemcpyHostToDevice, sg->st[0]));
+    r = run((const char *)dbuf - lo * esz, dout, sg->st[0]);
+    if (r) return r;
+    HCHK(hipMemcpyAsync(out, dout, out_bytes, hipMemcpyDeviceToHost, sg->st[0]));
+    return BLDP_OK;
+  });
+}
+
+}  // namespace
+
+extern "C" int bldp_reduce_host(int dev, int dtype, const void *in, int64_t nchan, int64_t nif,
+                                int64_t ntime, const int64_t *win, int64_t fqavby, int64_t tavby,
+                                int op, void *out) {
+  if (dtype == BLDP_DT_F32)
+    return bldp_reduce_host_f32(dev, static_cast<const float *>(in), nchan, nif, ntime, win,
+                                fqavby, tavby, op, static_cast<float *>(out));
+  const int od = bldp_reduce_out_dtype(dtype, op);
+  if (od < 0) return od;
+  int64_t sh[3];
+  int rc = bldp_reduce_shape(nchan, nif, ntime, win, fqavby, tavby, sh);
+  if (rc) return rc;
+  if (sh[0] * sh[1] * sh[2] == 0) return BLDP_OK;
+  const size_t ob = (size_t)(sh[0] * sh[1] * sh[2]) * bldp::dtype_size(od);
+  return typed_host(dev, dtype, in, nchan, nif, ntime, win, ob, out,
+                    [&](const void *din, void *dout, hipStream_t st) {
+                      return bldp_reduce_strided(dtype, din, nchan, nif, ntime, win, fqavby,
+                                                 tavby, op, dout, sh[0], sh[0] * sh[1], st);
+                    });
+}
+
+extern "C" int bldp_kurtosis_host(int dev, int dtype, const void *in, int64_t nchan, int64_t nif,
+                                  int64_t ntime, const int64_t *win, double *out) {
+  if (dtype == BLDP_DT_F32)
+    return bldp_kurtosis_host_f32(dev, static_cast<const float *>(in), nchan, nif, ntime, win,
+                                  out);
+  if (!bldp::dtype_size(dtype)) return bldp::set_error(BLDP_EINVAL, "unknown element type %d", dtype);
+  int64_t sh[3];
+  int rc = bldp_reduce_shape(nchan, nif, ntime, win, 1, 1, sh);
+  if (rc) return rc;
+  if (sh[0] * sh[1] == 0) return BLDP_OK;
+  if (sh[2] == 0) {  // no spectra: every row NaN (mean of nothing), as the Float32 path
+    if (!out) return bldp::set_error(BLDP_EINVAL, "null pointer");
+    for (int64_t k = 0; k < sh[0] * sh[1]; ++k) out[k] = NAN;
+    return BLDP_OK;
+  }
+  return typed_host(dev, dtype, in, nchan, nif, ntime, win, (size_t)(sh[0] * sh[1]) * 8, out,
+                    [&](const void *din, void *dout, hipStream_t st) {
+                      return bldp_kurtosis(dtype, din, nchan, nif, ntime, win,
+                                           static_cast<double *>(dout), st);
+                    });
+}

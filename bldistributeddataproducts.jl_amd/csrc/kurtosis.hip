@@ -325,7 +325,10 @@ __global__ __launch_bounds__(kB) void k_kurt_mid(const KurtArgs k) {
 template <int NR, int NW>
 __global__ __launch_bounds__(64 * NW) void k_kurt_mid2(const KurtArgs k) {
   constexpr int TW = 128;  // channels per tile
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // wave and the per-wave spectrum counts are uniform over a wave: scalar
+  // values make every `r < cnt` / `wave == w` test a scalar branch instead of
+  // an exec-mask save/restore per spectrum
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t ctiles = (k.nc + TW - 1) / TW;
   const int64_t b = blockIdx.x;
   const int64_t ib = b / ctiles, c = (b % ctiles) * TW + 2 * lane;
@@ -333,7 +336,8 @@ __global__ __launch_bounds__(64 * NW) void k_kurt_mid2(const KurtArgs k) {
   const int bank = (int)(ib / k.ni);
   const int64_t i = ib - (int64_t)bank * k.ni;
   const int nt = (int)k.nt;
-  const int r0 = (wave * nt) / NW, cnt = (((wave + 1) * nt) / NW) - r0;
+  const int r0 = __builtin_amdgcn_readfirstlane((wave * nt) / NW);
+  const int cnt = __builtin_amdgcn_readfirstlane((((wave + 1) * nt) / NW) - r0);
   const int64_t ld = k.in_ld_t;
   const float *p = k.in[bank] + k.in_off + i * k.in_ld_i + (valid ? c : 0) + r0 * ld;
   f2v v[NR];
@@ -356,17 +360,20 @@ __global__ __launch_bounds__(64 * NW) void k_kurt_mid2(const KurtArgs k) {
     __syncthreads();
   }
   const f2v sm = carry[lane];
-  const float m0 = sm.x / (float)nt, m1 = sm.y / (float)nt;
+  const f2v mv = {sm.x / (float)nt, sm.y / (float)nt};
   double a2 = 0.0, a4 = 0.0, b2 = 0.0, b4 = 0.0;
 #pragma unroll
   for (int r = 0; r < NR; ++r)
     if (r < cnt) {
-      const float z0 = v[r].x - m0, z1 = v[r].y - m1;  // StatsBase: Float32 z, z2
-      const float q0 = z0 * z0, q1 = z1 * z1;
-      a2 += (double)q0;
-      a4 += (double)(q0 * q0);
-      b2 += (double)q1;
-      b4 += (double)(q1 * q1);
+      // StatsBase: Float32 z, z2 (and z2*z2) for both channels at once
+      // (v_pk_add_f32 / v_pk_mul_f32), Float64 moments
+      const f2v z = v[r] - mv;
+      const f2v q = z * z;
+      const f2v q2 = q * q;
+      a2 += (double)q.x;
+      a4 += (double)q2.x;
+      b2 += (double)q.y;
+      b4 += (double)q2.y;
     }
   __shared__ double part[NW][4][64];
   part[wave][0][lane] = a2;

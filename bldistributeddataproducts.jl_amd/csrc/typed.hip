@@ -32,6 +32,10 @@
 
 #include "bldp_impl.h"
 
+// StatsBase rounds z*z before adding it (Julia contracts nothing without
+// @fastmath / muladd); hipcc would otherwise fuse z2 = z*z; cm2 += z2 into fma.
+#pragma clang fp contract(off)
+
 namespace bldp {
 namespace {
 

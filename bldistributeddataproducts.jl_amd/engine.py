@@ -112,9 +112,8 @@ def _abi_dims(t):
     """Map a channel-fastest tensor to (ptr, nchan, nif, ntime) of an array
     that contains it, so that its logical index (c, i, t) is element
     c + nchan*(i + nif*t) of the ABI array."""
-    torch = _torch()
-    if t.dtype != torch.float32:
-        raise TypeError("filterbank tensors are Float32")
+    if _dtype_code(t.dtype) is None:
+        raise TypeError(f"unsupported filterbank element type {t.dtype}")
     if not t.is_cuda:
         raise TypeError("device tensor expected (use getdata/reduce_host for host arrays)")
     if t.dim() != 3:
@@ -137,6 +136,40 @@ def _abi_dims(t):
             raise ValueError(f"unsupported strides {t.stride()}")
         nif = 1
     return t.data_ptr(), int(nchan), int(nif), int(n2)
+
+
+# bldp_dtype codes (include/bldp.h) by numpy element type
+DTYPE_CODES = {np.dtype(np.float32): 0, np.dtype(np.float64): 1, np.dtype(np.uint8): 2,
+               np.dtype(np.uint16): 3, np.dtype(np.uint32): 4, np.dtype(np.uint64): 5,
+               np.dtype(np.int8): 6, np.dtype(np.int16): 7, np.dtype(np.int32): 8,
+               np.dtype(np.int64): 9}
+DTYPE_OF_CODE = {v: k for k, v in DTYPE_CODES.items()}
+
+
+def _dtype_code(dt):
+    """bldp_dtype of a numpy dtype or torch dtype (None if unsupported)."""
+    if not isinstance(dt, np.dtype):
+        try:
+            dt = np.dtype(str(dt).replace("torch.", ""))
+        except TypeError:
+            return None
+    return DTYPE_CODES.get(np.dtype(dt))
+
+
+def out_dtype(dtype, op: str) -> np.dtype:
+    """fqav's result element type for input `dtype` (Julia's; bldp_reduce_out_dtype):
+    sum widens integers to (U)Int64, mean is Float64, max / min keep the type."""
+    code = _dtype_code(dtype)
+    if code is None:
+        raise TypeError(f"unsupported element type {dtype}")
+    rc = _lib.lib().bldp_reduce_out_dtype(code, _lib.OPS[op])
+    _lib.check(min(rc, 0), "bldp_reduce_out_dtype")
+    return DTYPE_OF_CODE[rc]
+
+
+def _torch_dtype(dt: np.dtype):
+    torch = _torch()
+    return getattr(torch, np.dtype(dt).name)
 
 
 def _check_bounds(win, shape):
@@ -178,13 +211,22 @@ def reduce(x, fqavby=1, tavby=1, op="sum", win=None, out=None, stream=None):
     shape = tuple(x.shape)
     _check_bounds(win, shape)
     nco, ni, nto = out_shape(shape, win, fqavby, tavby)
+    torch = _torch()
+    typed = x.dtype != torch.float32
+    odt = _torch_dtype(out_dtype(x.dtype, op)) if typed else torch.float32
     if out is None:
-        out = fb_empty(nco, ni, nto, device=x.device)
-    elif tuple(out.shape) != (nco, ni, nto):
-        raise ValueError(f"out has shape {tuple(out.shape)}, expected {(nco, ni, nto)}")
+        out = fb_empty(nco, ni, nto, device=x.device, dtype=odt)
+    elif tuple(out.shape) != (nco, ni, nto) or out.dtype != odt:
+        raise ValueError(f"out is {out.dtype} {tuple(out.shape)}, expected {odt} {(nco, ni, nto)}")
     optr, onc, oni, _ = _abi_dims(out) if out.numel() else (0, nco, ni, nto)
     ptr, nchan, nif, ntime = _abi_dims(x)
     keep, wp = _lib.win_arg(_full_win(win, shape))
+    if typed:  # fqav's Julia result types for integer / Float64 data (bldp_reduce_strided)
+        rc = L.bldp_reduce_strided(_dtype_code(x.dtype), ptr, nchan, nif, ntime, wp, int(fqavby),
+                                   int(tavby), _lib.OPS[op], optr, onc, onc * oni,
+                                   _lib.stream_ptr(stream))
+        _lib.check(rc, "bldp_reduce_strided")
+        return out
     rc = L.bldp_reduce_strided_f32(ptr, nchan, nif, ntime, wp, int(fqavby), int(tavby),
                                    _lib.OPS[op], optr, onc, onc * oni, _lib.stream_ptr(stream))
     _lib.check(rc, "bldp_reduce_strided_f32")
@@ -314,6 +356,11 @@ def kurtosis(x, win=None, stream=None):
     out = torch.empty((ni, nc), dtype=torch.float64, device=x.device).t()
     ptr, nchan, nif, ntime = _abi_dims(x)
     keep, wp = _lib.win_arg(_full_win(win, shape))
+    if x.dtype != torch.float32:  # StatsBase in Float64 for integer / Float64 rows
+        rc = L.bldp_kurtosis(_dtype_code(x.dtype), ptr, nchan, nif, ntime, wp,
+                             out.data_ptr() if out.numel() else None, _lib.stream_ptr(stream))
+        _lib.check(rc, "bldp_kurtosis")
+        return out
     rc = L.bldp_kurtosis_f32(ptr, nchan, nif, ntime, wp, out.data_ptr() if out.numel() else None,
                              None, _lib.stream_ptr(stream))
     _lib.check(rc, "bldp_kurtosis_f32")
@@ -406,4 +453,45 @@ def kurtosis_host(a: np.ndarray, win=None, device=0) -> np.ndarray:
     rc = L.bldp_kurtosis_host_f32(int(device), a.ctypes.data if a.size else None, a.shape[0],
                                   a.shape[1], a.shape[2], wp, out.ctypes.data if out.size else None)
     _lib.check(rc, "bldp_kurtosis_host_f32")
+    return out
+
+
+def reduce_host_typed(a: np.ndarray, fqavby=1, tavby=1, op="sum", win=None, device=0) -> np.ndarray:
+    """Host array of any supported element type in, host array of fqav's
+    Julia result type out (bldp_reduce_host): e.g. UInt8 SIGPROC data summed
+    into UInt64, averaged into Float64, max / min kept as UInt8."""
+    L = _lib.lib()
+    a = np.asarray(a)
+    code = _dtype_code(a.dtype)
+    if code is None or a.ndim != 3:
+        raise TypeError(f"unsupported host filterbank {a.dtype} {a.shape}")
+    a = np.asfortranarray(a)
+    shape = a.shape
+    _check_bounds(win, shape)
+    nco, ni, nto = out_shape(shape, win, fqavby, tavby)
+    out = np.empty((nco, ni, nto), dtype=out_dtype(a.dtype, op), order="F")
+    keep, wp = _lib.win_arg(_full_win(win, shape))
+    rc = L.bldp_reduce_host(int(device), code, a.ctypes.data if a.size else None, shape[0],
+                            shape[1], shape[2], wp, int(fqavby), int(tavby), _lib.OPS[op],
+                            out.ctypes.data if out.size else None)
+    _lib.check(rc, "bldp_reduce_host")
+    return out
+
+
+def kurtosis_host_typed(a: np.ndarray, win=None, device=0) -> np.ndarray:
+    """Host array of any supported element type in, (nc, ni) float64 out
+    (bldp_kurtosis_host; StatsBase's recipe in Float64 for non-Float32 rows)."""
+    L = _lib.lib()
+    a = np.asarray(a)
+    code = _dtype_code(a.dtype)
+    if code is None or a.ndim != 3:
+        raise TypeError(f"unsupported host filterbank {a.dtype} {a.shape}")
+    a = np.asfortranarray(a)
+    _check_bounds(win, a.shape)
+    nc, ni, _ = window_shape(win, a.shape)
+    out = np.empty((nc, ni), dtype=np.float64, order="F")
+    keep, wp = _lib.win_arg(_full_win(win, a.shape))
+    rc = L.bldp_kurtosis_host(int(device), code, a.ctypes.data if a.size else None, a.shape[0],
+                              a.shape[1], a.shape[2], wp, out.ctypes.data if out.size else None)
+    _lib.check(rc, "bldp_kurtosis_host")
     return out

@@ -132,8 +132,71 @@ def bandaxis(headers, idxs=(COLON, COLON, COLON), fqavby=1):
     return np.concatenate([p.values() for p in parts])
 
 
+def _bank_shape(f):
+    """(nchan, nif, ntime) of a bank: an in-memory array / tensor, or a file's
+    header (src/gbtworkerfunctions.jl:131-159)."""
+    if not isinstance(f, (str, bytes)) and not hasattr(f, "__fspath__"):
+        return tuple(int(n) for n in f.shape)
+    h = readers.getheader(f)
+    return int(h["nchans"]), int(h.get("nifs", 1)), int(h["nsamps"])
+
+
+def _band_on_device(ws, fs, idxs, fqavby, op, tavby, nfpc):
+    """One band stitched on the GPU (src/gbt.jl:103): every
+    bank is read and reduced on its worker's GPU straight into its vcat slot
+    of the band product on the first worker's GPU (a bank on another GPU is
+    reduced there and its result copied into the slot), the DC-spike patch
+    runs on the stitched product in place (src/gbt.jl:101-102,111), and the
+    band crosses PCIe once.  None when the banks' products differ in shape or
+    are not Float32: the caller then concatenates on the host."""
+    import os
+
+    import torch
+
+    from . import engine
+    from .idxs import sanitizeidxs, to_window
+
+    idxs = sanitizeidxs(idxs)
+    shapes = []
+    for f in fs:
+        shape = _bank_shape(f)
+        shapes.append(engine.out_shape(shape, to_window(idxs, shape), fqavby, tavby))
+    if len(set(shapes)) != 1 or 0 in shapes[0]:
+        return None
+    nco, ni, nto = shapes[0]
+    nb, root = len(fs), int(ws[0])
+    band = engine.fb_empty(nb * nco, ni, nto, device=f"cuda:{root}")
+    # BLDP_BAND_FORCE_COPY=1 takes the other-GPU branch (reduce, then copy into
+    # the slot) for every bank: how a one-GPU box tests it
+    force_copy = os.environ.get("BLDP_BAND_FORCE_COPY", "0") == "1"
+
+    def bank(b):
+        slot = band[b * nco:(b + 1) * nco]
+        dev = int(ws[b])
+        if dev == root and not force_copy:
+            return W.getdata_device(fs[b], idxs, fqavby, op, tavby, device=dev, out=slot)
+        r = W.getdata_device(fs[b], idxs, fqavby, op, tavby, device=dev)
+        if r is not None:
+            with torch.cuda.device(dev):
+                torch.cuda.current_stream().synchronize()
+            with torch.cuda.device(root):
+                slot.copy_(r)
+        return r
+
+    with ThreadPoolExecutor(max_workers=max(1, nb)) as ex:  # @spawnat per bank
+        got = list(ex.map(bank, range(nb)))
+    for d in sorted({int(w) for w in ws}):
+        torch.cuda.synchronize(d)
+    if any(r is None for r in got):
+        return None
+    with torch.cuda.device(root):
+        if nfpc:
+            engine.despike(band, nco // 64 if nfpc is True else int(nfpc))
+        return engine.fb_to_numpy(band)  # the one device -> host copy
+
+
 def getband(workers, fnames, idxs=(COLON, COLON, COLON), fqavby=1, fqavfunc="sum", tavby=1,
-            despike_nfpc=None, freqs=False):
+            despike_nfpc=None, freqs=False, stitch="device"):
     """The stitched band product: reduce(vcat, getdata(...)) in the given
     bank order (src/gbt.jl:103).  ``workers``/``fnames`` are one band's banks
     (1-D), or a (nbank, nband) matrix like loadscan's ``ds``, whose columns are
@@ -142,27 +205,40 @@ def getband(workers, fnames, idxs=(COLON, COLON, COLON), fqavby=1, fqavfunc="sum
     the DC bin of every coarse channel is patched as in loadscan
     (src/gbt.jl:101-102,111); ``despike_nfpc=True`` takes loadscan's own
     ``nfpc = size(ds[1], 1) ÷ 64`` (64 coarse channels per bank, :101).
-    ``freqs=True`` returns ``(band, bandaxis(...))`` (lists for a matrix)."""
+    ``freqs=True`` returns ``(band, bandaxis(...))`` (lists for a matrix).
+
+    ``stitch="device"`` (default) stitches each band on the GPU
+    (:func:`_band_on_device`); ``stitch="host"`` reduces every bank on its GPU,
+    copies each bank's product to the host and concatenates there (also what
+    bands of unequal bank products or non-Float32 data get)."""
     w = np.asarray(workers, dtype=object)
     f = np.asarray(fnames, dtype=object)
     if w.ndim not in (1, 2):
         raise AssertionError("getband takes one band (1-D) or a (nbank, nband) matrix")
-    res = getdata(workers, fnames, idxs, fqavby, fqavfunc, tavby)
-    cols = [list(res)] if res.ndim == 1 else [list(res[:, j]) for j in range(res.shape[1])]
+    assert w.shape == f.shape, "workers and fnames must have the same size"
+    if stitch not in ("device", "host"):
+        raise ValueError("stitch must be 'device' or 'host'")
     wcol = [list(w)] if w.ndim == 1 else [list(w[:, j]) for j in range(w.shape[1])]
     fcol = [list(f)] if f.ndim == 1 else [list(f[:, j]) for j in range(f.shape[1])]
-    nfpc = despike_nfpc
-    if nfpc is True:
-        nfpc = cols[0][0].shape[0] // 64  # size(ds[1], 1) ÷ 64
-    bands = []
-    for parts, ws in zip(cols, wcol):
+    op = W._opname(fqavfunc)
+    bands = [None] * len(wcol)
+    if stitch == "device" and op is not None:
+        for j, (ws, fs) in enumerate(zip(wcol, fcol)):
+            bands[j] = _band_on_device(ws, fs, idxs, fqavby, op, tavby, despike_nfpc)
+    for j, (ws, fs) in enumerate(zip(wcol, fcol)):
+        if bands[j] is not None:
+            continue
+        parts = list(getdata(ws, fs, idxs, fqavby, fqavfunc, tavby))
+        nfpc = despike_nfpc
+        if nfpc is True:
+            nfpc = parts[0].shape[0] // 64  # size(ds[1], 1) ÷ 64
         band = np.asfortranarray(np.concatenate(parts, axis=0))
         if nfpc:
             from . import engine
 
             x = engine.fb_from_numpy(band, device=f"cuda:{int(ws[0])}")
             band = engine.fb_to_numpy(engine.despike(x, nfpc))
-        bands.append(band)
+        bands[j] = band
     if freqs:
         axes = [bandaxis(getheaders(ws, fs), idxs, fqavby) for ws, fs in zip(wcol, fcol)]
         return (bands[0], axes[0]) if w.ndim == 1 else (bands, axes)

@@ -16,6 +16,18 @@ export gpu_init, gpu_finalize, gpu_pin, gpu_unpin, gpu_fqav, gpu_reduce, gpu_kur
 
 const libbldp = get(ENV, "BLDP_LIB", joinpath(@__DIR__, "..", "libbldp_hip.so"))
 
+# include/bldp.h BLDP_ABI_VERSION this binding is written against
+const ABI_VERSION = 2
+function __init__()
+    v = ccall((:bldp_abi_version, libbldp), Cint, ())
+    v == ABI_VERSION || error("libbldp_hip ABI version $v, BLDPHip expects $ABI_VERSION: rebuild it")
+end
+
+# bldp_dtype codes (include/bldp.h) and the element type of each code
+const GPUElt = Union{Float32,Float64,UInt8,UInt16,UInt32,UInt64,Int8,Int16,Int32,Int64}
+const ELTYPES = (Float32, Float64, UInt8, UInt16, UInt32, UInt64, Int8, Int16, Int32, Int64)
+dtypecode(::Type{T}) where {T<:GPUElt} = Cint(findfirst(==(T), ELTYPES) - 1)
+
 # fqavfunc values with a GPU implementation (README.md:192-195); anything
 # else keeps the reference's host fqav.
 opcode(f) = f === sum ? Cint(0) : f === mean ? Cint(1) : f === maximum ? Cint(2) :
@@ -33,6 +45,7 @@ function check(rc::Integer)
     rc == -2 && throw(DimensionMismatch(msg))   # fqavby/tavby does not divide
     rc == -6 && throw(BoundsError(msg))         # window outside the array
     rc == -1 && throw(ArgumentError(msg))
+    rc == -8 && throw(SystemError(msg))         # a file read failed or ended early
     error("libbldp_hip error $rc: $msg")
 end
 
@@ -100,6 +113,31 @@ function gpu_reduce(A::Array{Float32,3}, fqavby::Integer, tavby::Integer=1;
 end
 
 """
+    gpu_reduce(A::Array{T,3}, fqavby, tavby=1; f=sum, idxs=(:,:,:), dev=0) for T other than Float32
+
+The same for integer and Float64 data (SIGPROC nbits 8 / 16 mmaps to UInt8 /
+UInt16, src/gbtworkerfunctions.jl:173), with fqav's Julia result type:
+bldp_reduce_out_dtype (sum widened to (U)Int64 exactly, mean Float64,
+maximum / minimum the input type), reduced on GPU `dev` (bldp_reduce_host)."""
+function gpu_reduce(A::Array{T,3}, fqavby::Integer, tavby::Integer=1;
+                    f=sum, idxs::Tuple=(:, :, :), dev::Integer=0) where {T<:GPUElt}
+    op = opcode(f)
+    op === nothing && throw(ArgumentError("no GPU kernel for $f"))
+    od = ccall((:bldp_reduce_out_dtype, libbldp), Cint, (Cint, Cint), dtypecode(T), op)
+    od < 0 && check(od)
+    win = window(idxs, size(A))
+    shp = zeros(Int64, 3)
+    GC.@preserve win check(ccall((:bldp_reduce_shape, libbldp), Cint,
+        (Int64, Int64, Int64, Ptr{Int64}, Int64, Int64, Ptr{Int64}),
+        size(A, 1), size(A, 2), size(A, 3), win, fqavby, tavby, shp))
+    out = Array{ELTYPES[od + 1],3}(undef, shp...)
+    GC.@preserve A win out check(ccall((:bldp_reduce_host, libbldp), Cint,
+        (Cint, Cint, Ptr{Cvoid}, Int64, Int64, Int64, Ptr{Int64}, Int64, Int64, Cint, Ptr{Cvoid}),
+        dev, dtypecode(T), A, size(A, 1), size(A, 2), size(A, 3), win, fqavby, tavby, op, out))
+    out
+end
+
+"""
     gpu_fqav(A, n; f=sum, tavby=1)
 
 Drop-in for `fqav(A, n; f)` (src/gbtworkerfunctions.jl:16-20): same
@@ -107,10 +145,10 @@ pass-through for `n <= 1`, same DimensionMismatch, GPU for sum/mean/maximum/
 minimum, the reference's host code for any other `f`."""
 function gpu_fqav(A, n::Integer; f=sum, tavby::Integer=1, dev::Integer=0)
     (n <= 1 && tavby <= 1) && return A
-    if A isa Array{Float32,3} && opcode(f) !== nothing
+    if A isa Array{<:GPUElt,3} && opcode(f) !== nothing
         return gpu_reduce(A, n, tavby; f, dev)
     end
-    tavby <= 1 || throw(ArgumentError("tavby needs a Float32 3-D array and sum/mean/max/min"))
+    tavby <= 1 || throw(ArgumentError("tavby needs a 3-D array and sum/mean/max/min"))
     sz = (n, :, size(A)[2:end]...)
     dropdims(f(reshape(A, sz), dims=1), dims=1)
 end
@@ -132,6 +170,24 @@ function gpu_kurtosis(A::Array{Float32,3}; idxs::Tuple=(:, :, :), dev::Integer=0
     GC.@preserve A win out check(ccall((:bldp_kurtosis_host_f32, libbldp), Cint,
         (Cint, Ptr{Float32}, Int64, Int64, Int64, Ptr{Int64}, Ptr{Float64}),
         dev, A, size(A, 1), size(A, 2), size(A, 3), win, out))
+    out
+end
+
+"""
+    gpu_kurtosis(A::Array{T,3}; idxs=(:,:,:), dev=0) for T other than Float32
+
+StatsBase.kurtosis of integer or Float64 rows (Float64 throughout: Base.sum's
+pairwise mean, sequential moments), on GPU `dev` (bldp_kurtosis_host)."""
+function gpu_kurtosis(A::Array{T,3}; idxs::Tuple=(:, :, :), dev::Integer=0) where {T<:GPUElt}
+    win = window(idxs, size(A))
+    shp = zeros(Int64, 3)
+    GC.@preserve win check(ccall((:bldp_reduce_shape, libbldp), Cint,
+        (Int64, Int64, Int64, Ptr{Int64}, Int64, Int64, Ptr{Int64}),
+        size(A, 1), size(A, 2), size(A, 3), win, 1, 1, shp))
+    out = Matrix{Float64}(undef, shp[1], shp[2])
+    GC.@preserve A win out check(ccall((:bldp_kurtosis_host, libbldp), Cint,
+        (Cint, Cint, Ptr{Cvoid}, Int64, Int64, Int64, Ptr{Int64}, Ptr{Float64}),
+        dev, dtypecode(T), A, size(A, 1), size(A, 2), size(A, 3), win, out))
     out
 end
 

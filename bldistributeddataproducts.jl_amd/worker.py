@@ -115,11 +115,24 @@ def fqav(A, n: int, f="sum"):
     A = np.asarray(A)
     if op is None:
         return _host_generic(A, n, f)
-    a3 = A.reshape(A.shape + (1,) * (3 - A.ndim)) if A.ndim < 3 else A
+    a3 = A.reshape(A.shape + (1,) * (3 - A.ndim), order="F") if A.ndim < 3 else A
     if a3.ndim != 3:
         raise ValueError("fqav arrays are at most 3-D (nchan, nif, ntime)")
-    out = engine.reduce_host(np.asfortranarray(a3, dtype=np.float32), n, 1, op)
-    return out.reshape((out.shape[0],) + A.shape[1:])
+    out = _reduce_host(a3, n, 1, op, None, 0)
+    return out.reshape((out.shape[0],) + A.shape[1:], order="F")
+
+
+def _reduce_host(a, fqavby, tavby, op, win, device):
+    """A host array through the GPU with fqav's Julia result type: Float32
+    stays Float32; integer and Float64 arrays take the typed kernels (sum
+    widened to (U)Int64, mean Float64, max / min the input type,
+    src/gbtworkerfunctions.jl:19).  Nothing is converted on the way."""
+    if a.dtype == np.float32:
+        return engine.reduce_host(np.asfortranarray(a), fqavby, tavby, op, win, device=device)
+    if engine._dtype_code(a.dtype) is None:
+        raise TypeError(f"fqav: element type {a.dtype} is not supported (Float32, Float64, "
+                        f"8- to 64-bit integers)")
+    return engine.reduce_host_typed(a, fqavby, tavby, op, win, device=device)
 
 
 def _reduce_array(x, idxs, fqavby, fqavfunc, tavby, device):
@@ -137,9 +150,16 @@ def _reduce_array(x, idxs, fqavby, fqavfunc, tavby, device):
     if _is_tensor(x):
         return engine.reduce(x, fqavby, tavby, op, win)
     a = np.asarray(x)
-    if a.dtype != np.float32 or not a.flags.f_contiguous:
-        a = np.asfortranarray(a, dtype=np.float32)
-    return engine.reduce_host(a, fqavby, tavby, op, win, device=device)
+    if a.dtype != np.float32 and fqavby <= 1 and tavby <= 1:
+        # fqav(A, n <= 1) returns A (:17): the window itself, in its own type
+        if engine._dtype_code(a.dtype) is None:
+            raise TypeError(f"element type {a.dtype} is not supported")
+        engine._check_bounds(win, a.shape)
+        if win is None:
+            return a
+        ax = [win[3 * k] + win[3 * k + 2] * np.arange(win[3 * k + 1]) for k in range(3)]
+        return np.asfortranarray(a[np.ix_(*ax)])
+    return _reduce_host(a, fqavby, tavby, op, win, device)
 
 
 def _raw_to_device(fname, raw, idxs, device):
@@ -221,6 +241,68 @@ def getfbh5data(fbh5name, idxs=(COLON, COLON, COLON), fqavby=1, fqavfunc="sum", 
     return _reduce_array(data, (COLON, COLON, COLON), fqavby, fqavfunc, tavby, device)
 
 
+def window_on_device(fname, idxs, device=0):
+    """The Float32 window of a file (or host / device array) on GPU
+    ``device`` as (tensor, window relative to it), reading it the way
+    getfbh5data / getfbdata do (compressed chunks decoded on the GPU, raw
+    data block preads, else libhdf5 / mmap then one H2D copy); None when the
+    data are not Float32 (those keep their own types through the host-array
+    path) or the window is empty."""
+    import torch
+
+    idxs = sanitizeidxs(idxs)
+    dev = f"cuda:{int(device)}"
+    if _is_tensor(fname):
+        if fname.dtype != torch.float32:
+            return None
+        return fname, to_window(idxs, fname.shape)
+    if isinstance(fname, (str, bytes)) or hasattr(fname, "__fspath__"):
+        from . import fbh5
+
+        h5 = readers.ishdf5(fname)
+        if h5 and (fbh5.needs_bslz4(fname) or fbh5.raw_chunked(fname)):
+            return fbh5._read_window_bslz4_dev(fname, idxs, dev,
+                                               raw_chunks=not fbh5.needs_bslz4(fname), dense=False)
+        raw = fbh5.raw_layout(fname) if h5 else readers.fil_raw_layout(fname)
+        if raw is not None:
+            return _raw_to_device(fname, raw, idxs, device)
+        if h5:
+            a, win = readers.fbh5_read(fname, idxs), None
+        else:
+            _, a = readers.fil_mmap(fname)
+            win = to_window(idxs, a.shape)
+    else:
+        a = fname
+        win = to_window(idxs, np.asarray(a).shape)
+    a = np.asarray(a)
+    if a.dtype != np.float32:
+        return None
+    if win is not None:
+        a = np.asfortranarray(a[np.ix_(*[win[3 * k] + win[3 * k + 2] * np.arange(win[3 * k + 1])
+                                         for k in range(3)])])
+    if a.size == 0:
+        return None
+    return engine.fb_from_numpy(a, device=dev), None
+
+
+def getdata_device(fname, idxs=(COLON, COLON, COLON), fqavby=1, fqavfunc="sum", tavby=1,
+                   device=0, out=None):
+    """getdata with the result left on GPU ``device`` (a Julia-order Float32
+    tensor), written into ``out`` when given — e.g. a bank's slot of a stitched
+    band product (GBT.getband); None when the data are not Float32."""
+    op = _opname(fqavfunc)
+    if op is None:
+        raise TypeError("the device path takes fqavfunc in sum/mean/max/min")
+    got = window_on_device(fname, idxs, device)
+    if got is None:
+        return None
+    x, rwin = got
+    import torch
+
+    with torch.cuda.device(x.device):
+        return engine.reduce(x, fqavby, tavby, op, rwin, out=out)
+
+
 def getdata(fname, idxs=(COLON, COLON, COLON), fqavby=1, fqavfunc="sum", tavby=1, device=0):
     """WorkerFunctions.getdata (src/gbtworkerfunctions.jl:191-195).
 
@@ -271,9 +353,11 @@ def getkurtosis(fname, idxs=(COLON, COLON, COLON), device=0):
         a = fname
     a = np.asarray(a)
     win = to_window(idxs, a.shape)
-    if a.dtype != np.float32 or not a.flags.f_contiguous:
-        a = np.asfortranarray(a, dtype=np.float32)
-    return engine.kurtosis_host(a, win, device=device)
+    if a.dtype != np.float32:  # StatsBase in Float64 for integer / Float64 rows (:200)
+        if engine._dtype_code(a.dtype) is None:
+            raise TypeError(f"getkurtosis: element type {a.dtype} is not supported")
+        return engine.kurtosis_host_typed(a, win, device=device)
+    return engine.kurtosis_host(np.asfortranarray(a), win, device=device)
 
 
 getinventory = readers.getinventory

@@ -204,6 +204,43 @@ BLDP_API int bldp_band_kurtosis_f32(int nbank, const float *const *in, int64_t n
 BLDP_API int bldp_kurtosis_host_f32(int dev, const float *in, int64_t nchan, int64_t nif,
                                     int64_t ntime, const int64_t *win, double *out);
 
+/* Element types other than Float32 (what Blio maps SIGPROC nbits 8 / 16 to, and
+ * what HDF5.jl returns for an integer or Float64 dataset: the reference's
+ * readers hand any of them to fqav / kurtosis, src/gbtworkerfunctions.jl:173,
+ * 181-188, 197-202). */
+enum bldp_dtype {
+  BLDP_DT_F32 = 0, BLDP_DT_F64 = 1, BLDP_DT_U8 = 2, BLDP_DT_U16 = 3, BLDP_DT_U32 = 4,
+  BLDP_DT_U64 = 5, BLDP_DT_I8 = 6, BLDP_DT_I16 = 7, BLDP_DT_I32 = 8, BLDP_DT_I64 = 9
+};
+/* Element type of fqav's result for input `dtype` and `op`, Julia's:
+ *   sum   UInt8/16/32/64 -> UInt64, Int8/16/32/64 -> Int64 (Base.add_sum
+ *         widening; exact, wrapping on 64-bit overflow), Float32 / Float64 kept;
+ *   mean  Float64 (Float32 kept);  max / min  the input type.
+ * Returns the bldp_dtype, or BLDP_EINVAL. */
+BLDP_API int bldp_reduce_out_dtype(int dtype, int op);
+/* bldp_reduce_strided_f32 for any bldp_dtype: in holds `dtype` elements, out
+ * bldp_reduce_out_dtype(dtype, op) elements (strides in elements).  Float32
+ * input takes the Float32 kernels; the others one lane per output in the
+ * reference's order (integer sums exact).  Device pointers, asynchronous. */
+BLDP_API int bldp_reduce_strided(int dtype, const void *in, int64_t nchan, int64_t nif,
+                                 int64_t ntime, const int64_t *win, int64_t fqavby, int64_t tavby,
+                                 int op, void *out, int64_t out_ld_i, int64_t out_ld_t,
+                                 void *stream);
+/* getkurtosis for any bldp_dtype (StatsBase's recipe; Float64 arithmetic for
+ * integer and Float64 rows: Base.sum's pairwise Float64 mean, sequential
+ * moments).  out (nc, ni) float64 on the device.  Asynchronous. */
+BLDP_API int bldp_kurtosis(int dtype, const void *in, int64_t nchan, int64_t nif, int64_t ntime,
+                           const int64_t *win, double *out, void *stream);
+/* Host-memory forms (what a Julia worker holding the mmap'ed / read array
+ * calls): the window's span is copied to device `dev`, reduced there, and the
+ * result copied back into host `out` (dense (nco, ni, nto) of the output type;
+ * (nc, ni) float64 for kurtosis).  Synchronous. */
+BLDP_API int bldp_reduce_host(int dev, int dtype, const void *in, int64_t nchan, int64_t nif,
+                              int64_t ntime, const int64_t *win, int64_t fqavby, int64_t tavby,
+                              int op, void *out);
+BLDP_API int bldp_kurtosis_host(int dev, int dtype, const void *in, int64_t nchan, int64_t nif,
+                                int64_t ntime, const int64_t *win, double *out);
+
 /* HDF5 filter 32008 (bitshuffle + LZ4) chunks, the codec of compressed
  * rawspec FBH5 products (H5Zbitshuffle, reference Project.toml:10; read at
  * src/gbtworkerfunctions.jl:181-187).  A chunk is the raw bytes H5Dread_chunk

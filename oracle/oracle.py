@@ -339,6 +339,91 @@ def np_kurtosis(a, win=None) -> np.ndarray:
     return np.asfortranarray(k.reshape((nc, ni), order="F"))  # :201
 
 
+# --------------------------------------------------------------------------
+# Element types other than Float32 (NumPy restatement; the C oracle covers the
+# Float32 path).  Julia's result types (Base.add_sum widening, Statistics.mean,
+# StatsBase.kurtosis in Float64) — see csrc/typed.hip.
+# --------------------------------------------------------------------------
+def jl_sum_type(dt) -> np.dtype:
+    """Base.add_sum's result type: small unsigned -> UInt64, small signed ->
+    Int64, everything else unchanged."""
+    dt = np.dtype(dt)
+    if dt.kind == "u":
+        return np.dtype(np.uint64)
+    if dt.kind == "i":
+        return np.dtype(np.int64)
+    return dt
+
+
+def np_reduce_typed(a, fqavby=1, tavby=1, op="sum", win=None) -> np.ndarray:
+    """fqav (src/gbtworkerfunctions.jl:16-20) fused with the time integration
+    for a non-Float32 array, with Julia's result element types: integer sums
+    exact in (U)Int64 (wrapping), Float64 sums in the reference's order (the F
+    channels of a spectrum in sequence, spectrum after spectrum), mean = that
+    sum / (F T) in Float64, max / min in the input type."""
+    w = np_window(np.asarray(a), win)
+    F, T = max(int(fqavby), 1), max(int(tavby), 1)
+    nc, ni, nt = w.shape
+    if nc % F or nt % T:
+        raise DimensionMismatch("factor does not divide window")
+    # (F, co, ni, T, to) -> (F*T, co, ni, to) with the channel fastest in a block
+    R = w.reshape((F, nc // F, ni, T, nt // T), order="F").transpose(0, 3, 1, 2, 4)
+    R = R.reshape((F * T, nc // F, ni, nt // T), order="F")
+    if op in ("max", "min"):
+        if R.shape[0] == 0 or R.size == 0:
+            return np.asfortranarray(np.empty(R.shape[1:], dtype=w.dtype))
+        m = R.max(axis=0) if op == "max" else R.min(axis=0)
+        if w.dtype.kind == "f":
+            m = _fix_zero(m, R, 0, op)
+        return np.asfortranarray(m.astype(w.dtype))
+    st = jl_sum_type(w.dtype)
+    if st.kind == "f":  # sequential (np.add.accumulate is a sequential loop)
+        s = np.add.accumulate(R.astype(np.float64), axis=0)[-1] if R.shape[0] else \
+            np.zeros(R.shape[1:])
+    else:  # exact, wrapping modulo 2^64 like Julia's (U)Int64
+        s = R.astype(st).sum(axis=0, dtype=st)
+    if op == "mean":
+        return np.asfortranarray(s.astype(np.float64) / float(F * T))
+    return np.asfortranarray(s.astype(st))
+
+
+def np_pairwise_sum_f64(rows: np.ndarray) -> np.ndarray:
+    """Base.sum of each row converted to Float64 (mapreduce_impl, blocks of
+    <= 1024 summed in sequence, halves at ifirst + (ilast - ifirst) >> 1)."""
+    rows = np.asarray(rows, dtype=np.float64)
+
+    def rec(lo, hi):
+        if hi - lo < 1024:
+            return np.add.accumulate(rows[:, lo:hi + 1], axis=1)[:, -1]
+        mid = lo + ((hi - lo) >> 1)
+        return rec(lo, mid) + rec(mid + 1, hi)
+
+    if rows.shape[1] == 0:
+        return np.zeros(rows.shape[0])
+    return rec(0, rows.shape[1] - 1)
+
+
+def np_kurtosis_typed(a, win=None) -> np.ndarray:
+    """getkurtosis (src/gbtworkerfunctions.jl:197-202) of an integer or
+    Float64 array: StatsBase.kurtosis(v) = kurtosis(v, mean(v)) entirely in
+    Float64 — m = Base.sum (pairwise) / n, then z = v[i] - m, z2 = z*z,
+    cm2 += z2, cm4 += z2*z2 in sequence, (cm4/n) / (cm2/n)^2 - 3."""
+    w = np_window(np.asarray(a), win)
+    nc, ni, nt = w.shape
+    rows = w.reshape((nc * ni, nt), order="F").astype(np.float64)
+    with np.errstate(divide="ignore", invalid="ignore", over="ignore", under="ignore"):
+        m = (np_pairwise_sum_f64(rows) / float(nt))[:, None]
+        z = rows - m
+        z2 = z * z
+        if nt:
+            cm2 = np.add.accumulate(z2, axis=1)[:, -1] / float(nt)
+            cm4 = np.add.accumulate(z2 * z2, axis=1)[:, -1] / float(nt)
+        else:
+            cm2 = cm4 = np.full(nc * ni, np.nan)
+        k = cm4 / (cm2 * cm2) - 3.0
+    return np.asfortranarray(k.reshape((nc, ni), order="F"))
+
+
 def np_stitch(banks) -> np.ndarray:
     """reduce(vcat, banks) (src/gbt.jl:103)."""
     return np.asfortranarray(np.concatenate([np.asarray(b) for b in banks], axis=0))

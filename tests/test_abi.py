@@ -464,3 +464,31 @@ def test_julia_binding_ccalls_match_the_header():
     for n in ("bldp_reduce_host_f32", "bldp_kurtosis_host_f32", "bldp_reduce_shape",
               "bldp_last_error", "bldp_band_gather_f32", "bldp_comm_init"):
         assert n in named, n
+
+
+def test_typed_entry_points_host_checks(pkg, L):
+    """Julia's fqav result element types (bldp_reduce_out_dtype, host only) and
+    the typed entry points' argument checks (nothing is launched)."""
+    D = {"f32": 0, "f64": 1, "u8": 2, "u16": 3, "u32": 4, "u64": 5, "i8": 6, "i16": 7, "i32": 8,
+         "i64": 9}
+    for t in ("u8", "u16", "u32", "u64"):
+        assert L.bldp_reduce_out_dtype(D[t], 0) == D["u64"]
+    for t in ("i8", "i16", "i32", "i64"):
+        assert L.bldp_reduce_out_dtype(D[t], 0) == D["i64"]
+    for t in D:
+        assert L.bldp_reduce_out_dtype(D[t], 1) == (D["f32"] if t == "f32" else D["f64"])
+        assert L.bldp_reduce_out_dtype(D[t], 2) == D[t] == L.bldp_reduce_out_dtype(D[t], 3)
+    assert L.bldp_reduce_out_dtype(D["f64"], 0) == D["f64"]
+    assert L.bldp_reduce_out_dtype(42, 0) == pkg._lib.BLDP_EINVAL
+    assert L.bldp_reduce_out_dtype(D["u8"], 9) == pkg._lib.BLDP_EINVAL
+    assert L.bldp_reduce_strided(42, None, 64, 1, 4, None, 4, 1, 0, None, 16, 16, None) == \
+        pkg._lib.BLDP_EINVAL
+    assert L.bldp_reduce_strided(D["u8"], None, 64, 1, 4, None, 3, 1, 0, None, 16, 16, None) == \
+        pkg._lib.BLDP_EDIM
+    assert L.bldp_reduce_strided(D["u8"], None, 64, 1, 4, None, 4, 1, 0, None, 16, 16, None) == \
+        pkg._lib.BLDP_EINVAL  # null pointers
+    assert L.bldp_kurtosis(42, None, 64, 1, 4, None, None, None) == pkg._lib.BLDP_EINVAL
+    w = (ctypes.c_int64 * 9)(0, 65, 1, 0, 1, 1, 0, 4, 1)
+    assert L.bldp_kurtosis(D["u16"], None, 64, 1, 4, w, None, None) == pkg._lib.BLDP_EBOUNDS
+    assert pkg.engine.out_dtype(np.dtype(np.uint8), "sum") == np.uint64
+    assert pkg.engine.out_dtype(np.dtype(np.int16), "mean") == np.float64

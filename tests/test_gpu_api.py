@@ -93,6 +93,39 @@ def test_gbt_getdata_getband_kurtosis(pkg, orc, files):
         pkg.GBT.getband(np.zeros((2, 2, 2), object), np.zeros((2, 2, 2), object))
 
 
+@pytest.mark.parametrize("force_copy", ["0", "1"])
+def test_getband_device_stitch_matches_host_concat(pkg, orc, files, monkeypatch, force_copy):
+    """GBT.getband's device stitch (every bank reduced into its vcat slot on
+    the GPU, despike in place, one copy to the host) is bit-exact against the
+    host concatenation of per-bank results, with and without despike; with
+    BLDP_BAND_FORCE_COPY=1 every bank takes the other-GPU branch (reduced on
+    its own device, then copied into the slot)."""
+    monkeypatch.setenv("BLDP_BAND_FORCE_COPY", force_copy)
+    banks, names = files
+    J, C = pkg.JRange, pkg.COLON
+    workers = [0] * len(names)
+    for idxs, F, T, op, nfpc in (((C, C, C), 64, 10, "sum", None),
+                                 ((C, C, J(1, 32)), 1, 8, "mean", None),
+                                 ((C, C, J(1, 3)), 1, 1, "sum", 64),
+                                 ((J(1, 2048), C, J(2, 40)), 2, 1, "max", True)):
+        dev = pkg.GBT.getband(workers, names, idxs, fqavby=F, tavby=T, fqavfunc=op,
+                              despike_nfpc=nfpc)
+        host = pkg.GBT.getband(workers, names, idxs, fqavby=F, tavby=T, fqavfunc=op,
+                               despike_nfpc=nfpc, stitch="host")
+        assert same_bits(dev, host), (idxs, F, T, op, nfpc)
+        win = pkg.idxs.to_window(pkg.sanitizeidxs(idxs), banks[0].shape)
+        want = orc.stitch([orc.reduce(a, F, T, op, win) for a in banks])
+        if nfpc:
+            want = orc.despike(want, want.shape[0] // 8 // 64 if nfpc is True else nfpc)
+        assert same_bits(dev, want), (idxs, F, T, op, nfpc)
+    # banks whose products differ in shape: the host concatenation takes over
+    short = [names[0], names[1]]
+    assert pkg.GBT._band_on_device([0, 0], [banks[0], banks[1][:2048]], (C, C, C), 1, "sum", 1,
+                                   None) is None
+    got = pkg.GBT.getband([0, 0], short, (C, C, C), fqavby=4)
+    assert same_bits(got, orc.stitch([orc.reduce(a, 4, 1) for a in banks[:2]]))
+
+
 def test_gbt_getkurtosis_fanout_long_windows(pkg, orc, tmp_path):
     """GBT.getkurtosis over 6 files on one device with > 512 spectra: one
     thread per (worker, file) on the same stream and scratch (the leaf

@@ -1,0 +1,158 @@
+"""GPU parity for element types other than Float32 (VERDICT r02 missing #2):
+fqav and getkurtosis return the reference's result types — Base.add_sum
+widening (UInt8/16/32 -> UInt64, Int8/16/32 -> Int64), Float64 means, max /
+min in the input type, StatsBase.kurtosis in Float64
+(src/gbtworkerfunctions.jl:16-20, 173-174, 188, 197-202) — and the values of
+the NumPy restatement (oracle.np_reduce_typed / np_kurtosis_typed), through
+the C ABI (bldp_reduce_strided, bldp_kurtosis, bldp_reduce_host,
+bldp_kurtosis_host).
+
+Tolerances: integer results are exact; Float64 sums follow the reference's
+sequence (the F channels of a spectrum, spectrum after spectrum) and
+kurtosis follows StatsBase's (Base.sum's pairwise mean, sequential moments),
+so they are compared bit for bit as well (the oracle runs the same
+sequence).  The reference itself may reassociate inside a 1024-element leaf
+under @simd; that machine dependence is not something either restatement
+pins."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+INT_TYPES = [np.uint8, np.uint16, np.uint32, np.uint64, np.int8, np.int16, np.int32, np.int64]
+ALL_TYPES = INT_TYPES + [np.float64]
+
+
+@pytest.fixture(scope="module")
+def eng(pkg):
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    pkg._lib.lib()
+    return pkg.engine
+
+
+def rand(dt, shape, seed):
+    rng = np.random.default_rng(seed)
+    dt = np.dtype(dt)
+    if dt.kind == "f":
+        return np.asfortranarray(rng.gamma(2.0, 3.0, shape).astype(dt))
+    info = np.iinfo(dt)
+    lo, hi = max(info.min, -(1 << 40)), min(info.max, 1 << 40)
+    return np.asfortranarray(rng.integers(lo, hi, shape, endpoint=True).astype(dt))
+
+
+def to_dev(eng, a):
+    import torch
+
+    t = torch.from_numpy(np.ascontiguousarray(a.transpose(2, 1, 0))).to("cuda")
+    return t.permute(2, 1, 0)
+
+
+def same(got, want):
+    got, want = np.asarray(got), np.asarray(want)
+    assert got.dtype == want.dtype, (got.dtype, want.dtype)
+    assert got.shape == want.shape, (got.shape, want.shape)
+    if got.dtype.kind == "f":
+        return np.array_equal(got.view(np.uint64), want.view(np.uint64)) or \
+            np.array_equal(got, want, equal_nan=True)
+    return np.array_equal(got, want)
+
+
+JULIA_OUT = {("sum", np.uint8): np.uint64, ("sum", np.uint16): np.uint64,
+             ("sum", np.uint32): np.uint64, ("sum", np.uint64): np.uint64,
+             ("sum", np.int8): np.int64, ("sum", np.int16): np.int64,
+             ("sum", np.int32): np.int64, ("sum", np.int64): np.int64,
+             ("sum", np.float64): np.float64}
+
+
+@pytest.mark.parametrize("dt", ALL_TYPES, ids=lambda d: np.dtype(d).name)
+def test_result_types_are_julias(pkg, eng, dt):
+    for op in ("sum", "mean", "max", "min"):
+        want = JULIA_OUT[("sum", dt)] if op == "sum" else np.float64 if op == "mean" else dt
+        assert eng.out_dtype(np.dtype(dt), op) == np.dtype(want), (dt, op)
+    assert eng.out_dtype(np.dtype(np.float32), "sum") == np.float32
+    assert eng.out_dtype(np.dtype(np.float32), "mean") == np.float32
+
+
+SHAPES = [(64, 1, 20, 4, 1), (96, 2, 12, 3, 4), (1000, 1, 7, 8, 1), (33, 3, 5, 1, 5),
+          (4096, 1, 3, 64, 1)]
+
+
+@pytest.mark.parametrize("dt", ALL_TYPES, ids=lambda d: np.dtype(d).name)
+def test_reduce_typed_device_and_host(pkg, eng, orc, dt):
+    for k, (nc, ni, nt, F, T) in enumerate(SHAPES):
+        a = rand(dt, (nc, ni, nt), seed=k + 17 * np.dtype(dt).num)
+        x = to_dev(eng, a)
+        for op in ("sum", "mean", "max", "min"):
+            want = orc.np_reduce_typed(a, F, T, op)
+            got = eng.fb_to_numpy(eng.reduce(x, F, T, op))
+            assert same(got, want), (dt, (nc, ni, nt, F, T), op)
+            goth = eng.reduce_host_typed(a, F, T, op)
+            assert same(goth, want), (dt, (nc, ni, nt, F, T), op, "host")
+        # a strided window (reversed channels, every other spectrum)
+        if nt >= 2 * T and nc >= 2 * F:
+            w = [nc - 1, (nc // F) * F - F, -1, 0, ni, 1, 0, (nt // (2 * T)) * T, 2]
+            for op in ("sum", "max"):
+                want = orc.np_reduce_typed(a, F, T, op, w)
+                assert same(eng.fb_to_numpy(eng.reduce(x, F, T, op, w)), want), (dt, op, w)
+                assert same(eng.reduce_host_typed(a, F, T, op, w), want), (dt, op, w, "host")
+
+
+def test_reduce_typed_wraps_like_julia(pkg, eng, orc):
+    """(U)Int64 sums wrap modulo 2^64, as Julia's do."""
+    a = np.asfortranarray(np.full((8, 1, 2), np.iinfo(np.uint64).max, dtype=np.uint64))
+    got = eng.reduce_host_typed(a, 4, 1, "sum")
+    assert same(got, orc.np_reduce_typed(a, 4, 1, "sum"))
+    assert got[0, 0, 0] == np.uint64(2**64 - 4)
+
+
+@pytest.mark.parametrize("dt", ALL_TYPES, ids=lambda d: np.dtype(d).name)
+def test_kurtosis_typed(pkg, eng, orc, dt):
+    for k, (nc, ni, nt) in enumerate([(64, 1, 100), (37, 2, 1500), (5, 1, 5000), (3, 1, 1)]):
+        a = rand(dt, (nc, ni, nt), seed=5 * k + np.dtype(dt).num)
+        if np.dtype(dt).kind != "f":  # keep the Float64 mean's sums exact (< 2^53)
+            a = np.asfortranarray((a % 1000).astype(dt))
+        want = orc.np_kurtosis_typed(a)
+        got = eng.fb_to_numpy(eng.kurtosis(to_dev(eng, a)))
+        assert same(got, want), (dt, (nc, ni, nt))
+        assert same(eng.kurtosis_host_typed(a), want), (dt, (nc, ni, nt), "host")
+    # windows: a spectrum range of every other channel; an empty time window -> NaN
+    a = rand(dt, (40, 1, 300), seed=3)
+    w = [1, 19, 2, 0, 1, 1, 10, 250, 1]
+    assert same(eng.kurtosis_host_typed(a, w), orc.np_kurtosis_typed(a, w))
+    e = eng.kurtosis_host_typed(a, [0, 40, 1, 0, 1, 1, 0, 0, 1])
+    assert e.shape == (40, 1) and np.isnan(e).all()
+
+
+def test_worker_api_keeps_reference_types(pkg, eng, orc, tmp_path):
+    """getdata / getkurtosis / fqav on 8- and 16-bit SIGPROC files and on a
+    Float64 array: Julia's result types and values (no Float32 detour)."""
+    W = pkg.WorkerFunctions
+    rng = np.random.default_rng(8)
+    for nbits, dt in ((8, np.uint8), (16, np.uint16)):
+        a = np.asfortranarray(rng.integers(0, np.iinfo(dt).max, (256, 2, 50), endpoint=True)
+                              .astype(dt))
+        f = str(tmp_path / f"b{nbits}.fil")
+        pkg.readers.write_fil(f, dict(fch1=8000.0, foff=-1.0, nchans=256, nifs=2, tsamp=1.0,
+                                      nbits=nbits, telescope_id=6, machine_id=10, data_type=1,
+                                      tstart=59000.0, source_name="X"), a)
+        d = W.getdata(f)  # fqavby = 1: the data itself (fqav returns A, :17)
+        assert d.dtype == dt and np.array_equal(d, a)
+        for op in ("sum", "mean", "max", "min"):
+            got = W.getdata(f, fqavby=16, fqavfunc=op)
+            assert same(got, orc.np_reduce_typed(a, 16, 1, op)), (nbits, op)
+        idxs = (pkg.JRange(1, 128), 2, pkg.JRange(5, 44))
+        got = W.getdata(f, idxs, fqavby=8, tavby=4)
+        w = [0, 128, 1, 1, 1, 1, 4, 40, 1]
+        assert same(got, orc.np_reduce_typed(a, 8, 4, "sum", w))
+        k = W.getkurtosis(f)
+        assert same(k, orc.np_kurtosis_typed(a)), nbits
+    b = np.asfortranarray(rng.standard_normal((512, 1, 30)))
+    assert same(W.fqav(b, 8), orc.np_reduce_typed(b, 8, 1, "sum"))
+    assert same(W.fqav(b, 8, "mean"), orc.np_reduce_typed(b, 8, 1, "mean"))
+    assert W.fqav(b.astype(np.int16), 4).dtype == np.int64
+    with pytest.raises(TypeError):
+        W.fqav(b.astype(np.float16), 4)

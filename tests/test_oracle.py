@@ -179,3 +179,76 @@ def test_baseline_threads_match_single(orc):
             outs = orc.reduce_banks_pool(banks, F, T, op, nth)
             for b, o in zip(banks, outs):
                 assert same_bits(o, orc.reduce(b, F, T, op)), (nth, F, T, op)
+
+
+# ---------------------------------------------------------------------------
+# Non-Float32 element types (oracle.np_reduce_typed / np_kurtosis_typed),
+# pinned against literal Python loops of the Julia source and against SciPy's
+# independent kurtosis.
+def py_kurtosis_statsbase(v):
+    """StatsBase.kurtosis(v) for an integer / Float64 row, written as the
+    package writes it: m = mean(v) (Base.sum pairwise / n), then one loop."""
+    v = [float(x) for x in v]
+    n = len(v)
+
+    def impl(ifirst, ilast):  # Base.mapreduce_impl, pairwise_blocksize 1024
+        if ifirst == ilast:
+            return v[ifirst]
+        if ifirst + 1024 > ilast:
+            a = v[ifirst] + v[ifirst + 1]
+            for i in range(ifirst + 2, ilast + 1):
+                a = a + v[i]
+            return a
+        imid = ifirst + ((ilast - ifirst) >> 1)
+        return impl(ifirst, imid) + impl(imid + 1, ilast)
+
+    m = impl(0, n - 1) / n
+    cm2 = cm4 = 0.0
+    for x in v:
+        z = x - m
+        z2 = z * z
+        cm2 += z2
+        cm4 += z2 * z2
+    cm4 /= n
+    cm2 /= n
+    return cm4 / (cm2 * cm2) - 3.0
+
+
+@pytest.mark.parametrize("dt", [np.uint8, np.int16, np.float64])
+def test_typed_kurtosis_oracle_pinned(orc, dt):
+    import scipy.stats
+
+    rng = np.random.default_rng(3)
+    for nt in (2, 7, 1024, 1025, 2500):
+        a = rng.gamma(2.0, 30.0, (3, 1, nt)).astype(dt)
+        a = np.asfortranarray(a)
+        got = orc.np_kurtosis_typed(a)
+        for c in range(3):
+            want = py_kurtosis_statsbase(a[c, 0, :])
+            assert got[c, 0] == want, (dt, nt, c)  # same operations, same order
+        np.testing.assert_allclose(got[:, 0], scipy.stats.kurtosis(a[:, 0, :].astype(np.float64),
+                                                                   axis=1), rtol=1e-10)
+
+
+def test_typed_reduce_oracle_pinned(orc):
+    rng = np.random.default_rng(5)
+    a = np.asfortranarray(rng.integers(0, 256, (12, 2, 6)).astype(np.uint8))
+    F, T = 3, 2
+    s = orc.np_reduce_typed(a, F, T, "sum")
+    assert s.dtype == np.uint64 and s.shape == (4, 2, 3)
+    for co in range(4):
+        for i in range(2):
+            for to in range(3):
+                blk = [int(a[co * F + k, i, to * T + t]) for t in range(T) for k in range(F)]
+                assert s[co, i, to] == sum(blk)
+                assert orc.np_reduce_typed(a, F, T, "mean")[co, i, to] == sum(blk) / (F * T)
+                assert orc.np_reduce_typed(a, F, T, "max")[co, i, to] == max(blk)
+    assert orc.np_reduce_typed(a, F, T, "max").dtype == np.uint8
+    b = np.asfortranarray(rng.standard_normal((8, 1, 4)))
+    sb = orc.np_reduce_typed(b, 4, 2, "sum")
+    acc = 0.0
+    for t in range(2):  # the channels of a spectrum in sequence, spectrum after spectrum
+        for k in range(4):
+            acc = acc + float(b[k, 0, t])
+    assert sb[0, 0, 0] == acc
+    assert orc.np_reduce_typed(a.astype(np.int32), 3, 1, "sum").dtype == np.int64

@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""GBT.getband end to end, device stitch against the host concatenation
+(VERDICT r02 next-2): one 0002-shaped band of 8 files (65536 ch x 1 IF x 279
+spectra, integer-valued Float32, uncompressed FBH5 in the page cache), all
+workers on GPU 0; each mode timed over --reps calls after one warm call, and
+checked bit for bit against the other.
+
+    python tools/getband_probe.py [--reps 5] [--json out.json]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--json", default=None)
+    ap.add_argument("--nchan", type=int, default=65536)
+    ap.add_argument("--ntime", type=int, default=279)
+    a = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    import __graft_entry__ as entry
+
+    pkg = entry.load_package()
+    eng, G = pkg.engine, pkg.GBT
+    d = tempfile.mkdtemp(prefix="bldp_band_")
+    names = []
+    for b in range(8):
+        x = eng.synth(a.nchan, 1, a.ntime, 1024, seed=10 * b + 2, kind=1)  # integers 0..255
+        p = os.path.join(d, f"blc0{b}_guppi_59000_12345_X_0011.rawspec.0002.h5")
+        pkg.fbh5.write(p, dict(fch1=8400.0 - 187.5 * b, foff=-187.5 / a.nchan, nchans=a.nchan,
+                               nifs=1, tsamp=1.07, nfpc=1024), eng.fb_to_numpy(x))
+        names.append(p)
+    torch.cuda.synchronize()
+    workers = [0] * 8
+    C = pkg.COLON
+    cases = [("F64 T1", dict(fqavby=64)), ("F64 T1 despike", dict(fqavby=64, despike_nfpc=16)),
+             ("F1 T1 despike", dict(despike_nfpc=1024)), ("F64 T9", dict(fqavby=64, tavby=9))]
+    res = {}
+    for label, kw in cases:
+        out = {}
+        for mode in ("host", "device"):
+            G.getband(workers, names, (C, C, C), stitch=mode, **kw)  # warm (page cache, plans)
+            ts = []
+            for _ in range(a.reps):
+                t0 = time.perf_counter()
+                band = G.getband(workers, names, (C, C, C), stitch=mode, **kw)
+                ts.append((time.perf_counter() - t0) * 1e3)
+            ts.sort()
+            out[mode] = {"median_ms": round(ts[len(ts) // 2], 3), "min_ms": round(ts[0], 3),
+                         "shape": list(band.shape)}
+            out[mode + "_band"] = band
+        same = bool(np.array_equal(out["host_band"].view(np.uint32),
+                                   out["device_band"].view(np.uint32)))
+        res[label] = {"host": out["host"], "device": out["device"], "bit_identical": same,
+                      "speedup": round(out["host"]["median_ms"] / out["device"]["median_ms"], 3)}
+        print(label, json.dumps(res[label]), flush=True)
+        assert same, label
+    for p in names:
+        os.remove(p)
+    os.rmdir(d)
+    res["what"] = ("GBT.getband on 8 uncompressed FBH5 files of (%d ch x 1 IF x %d spectra) "
+                   "Float32, every worker on GPU 0, files in the page cache; 'host' = each bank "
+                   "reduced on the GPU, copied to the host and concatenated there (round 2), "
+                   "despike H2D + kernel + D2H; 'device' = each bank reduced into its slot of the "
+                   "band on the GPU, despike in place, one D2H" % (a.nchan, a.ntime))
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -38,6 +38,8 @@ for s in $STEPS; do
     smoke) run smoke 300 python -c "import __graft_entry__ as e; e.smoke()" ;;
     ab) run ab 900 python tools/ab_variants.py --run --suite t1v --rounds 5 \
           --variants "${AB_VARIANTS:-base,dpp,r02}" --json "$OUT/ab_t1v.json" ;;
+    ab_*) run "$s" 900 python tools/ab_variants.py --run --suite "${s#ab_}" --rounds 5 \
+          --variants "${AB_VARIANTS:-base,r02}" --json "$OUT/$s.json" ;;
     stats) run stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run \
           -- python tools/t1_probe.py --rounds 3 --iters 10 --json "$OUT/t1_probe.json" ;;
     pmc)
