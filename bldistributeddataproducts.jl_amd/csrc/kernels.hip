@@ -1023,6 +1023,12 @@ void k_reduce_row(const RedArgs a) {
 #ifndef BLDP_ROWT_PACK
 #define BLDP_ROWT_PACK 1
 #endif
+//   BLDP_ROWT_LDS_OUT  1 (default) = k_reduce_rowt stages its output tile in LDS
+//                  and stores whole row segments (16-byte stores where legal);
+//                  0 = each wave stores its own groups' outputs
+#ifndef BLDP_ROWT_LDS_OUT
+#define BLDP_ROWT_LDS_OUT 1
+#endif
 //   BLDP_ROWT_MAXWAVES  cap on resident waves per SIMD for k_reduce_rowt (0 = none)
 //                      6 (default): A/B against 4 and none, profiles/r02/ab_row_tpb.json
 #ifndef BLDP_ROWT_MAXWAVES
@@ -1075,6 +1081,60 @@ void k_reduce_rowt(const RedArgs a) {
     if constexpr (kNacc > 1) acc = f4<OP>(acc, id4);
     sv[b] = lanes_fold<OP, G4>(fold4<OP>(acc));
   }
+#if BLDP_ROWT_LDS_OUT
+  // Output tile through LDS: the workgroup's outputs are (time groups x TPB)
+  // rows of 256/G4 >> tsub_log2 consecutive groups.  Lane j of a group
+  // deposits block j (j + G4, ...); then each row segment is stored by
+  // consecutive lanes, 16 bytes per lane where the output layout allows, so
+  // every row segment leaves the CU as whole writes (storing per wave put 4
+  // pieces of each 64-byte segment in flight at F = 64, and 1 float per
+  // wave per row at F = 256: 32-byte partial write requests, PMC WRITE_SIZE
+  // 2x-5x the output, profiles/r03/t1_pmc_r03a.json).
+  __shared__ float tile[kBlock / G4 * TPB];
+  const int j = tid & (G4 - 1);
+  constexpr int NS = TPB > G4 ? TPB / G4 : 1;
+  constexpr int NSEL = TPB < G4 ? TPB : G4;
+  constexpr int LG4 = G4 >= 64 ? 6 : G4 >= 32 ? 5 : G4 >= 16 ? 4 : G4 >= 8 ? 3 : G4 >= 4 ? 2 : G4 >= 2 ? 1 : 0;
+  const int lng = 8 - sh - LG4;  // log2 of the groups per row segment (>= 0: cw >= G4)
+  const int tgl = tid >> (8 - sh), gl = (tid & (cw - 1)) >> LG4;
+#pragma unroll
+  for (int m = 0; m < NS; ++m) {
+    const int b = m * G4 + j;
+    float val = sv[m * G4];
+#pragma unroll
+    for (int q = 1; q < NSEL; ++q) val = (j == q) ? sv[m * G4 + q] : val;
+    if (b < TPB) tile[((tgl * TPB + b) << lng) + gl] = finish<OP>(val, a);
+  }
+  __syncthreads();
+  const int64_t gcol0 = (int64_t)(bx - tq * bc) * (kBlock / G4);
+  float *ob = a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + gcol0;
+  const int nrow = TPB << sh;
+  if (a.vec_out && lng >= 2) {
+    const int lq = lng - 2;  // log2 of the float4 per row segment
+    for (int e = tid; e < (nrow << lq); e += kBlock) {
+      const int r = e >> lq, q = e & ((1 << lq) - 1);
+      const int64_t to = ((int64_t)tq << sh) * TPB + r;  // r = tgl * TPB + b
+      const int64_t g = gcol0 + 4 * q;
+      if (to >= a.nto || g >= a.nco) continue;
+      const float *src = &tile[(r << lng) + 4 * q];
+      float *dst = ob + to * a.out_ld_t + 4 * q;
+      if (g + 3 < a.nco) {
+        st4(dst, make_float4(src[0], src[1], src[2], src[3]));
+      } else {
+        for (int k = 0; k < 4; ++k)
+          if (g + k < a.nco) st1<1>(dst + k, src[k]);
+      }
+    }
+  } else {
+    for (int e = tid; e < (nrow << lng); e += kBlock) {
+      const int r = e >> lng, q = e & ((1 << lng) - 1);
+      const int64_t to = ((int64_t)tq << sh) * TPB + r;
+      if (to >= a.nto || gcol0 + q >= a.nco) continue;
+      st1<1>(ob + to * a.out_ld_t + q, tile[e]);
+    }
+  }
+  (void)valid;
+#else
   // Stores: lane j of a group writes block j (j + G4, ... when the group has
   // fewer lanes than blocks), so a store instruction has every lane busy
   // (k_reduce_row's one-lane-per-group store would take TPB instructions).
@@ -1090,6 +1150,7 @@ void k_reduce_rowt(const RedArgs a) {
     for (int q = 1; q < NSEL; ++q) val = (j == q) ? sv[m * G4 + q] : val;
     if (valid && b < nb) st1<1>(o + (to0 + b) * a.out_ld_t, finish<OP>(val, a));
   }
+#endif
 }
 
 // Large groups (F = 512..4096: 64 lanes x K4 float4 per row, one output per
@@ -1652,6 +1713,11 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
   }
   // narrow-path vector stores
   a.vec_out = 0;
+  if (p.path == PATH_VEC_ROW && a.tpb > 1) {  // k_reduce_rowt's 16-byte row-segment stores
+    const uintptr_t op = (uintptr_t)a.out;
+    a.vec_out = (op % 16 == 0) && a.out_bank % 4 == 0 && a.out_ld_i % 4 == 0 &&
+                a.out_ld_t % 4 == 0;
+  }
   if (p.path == PATH_NARROW_MIS) {  // float4 (F = 1) / float2 (F = 2) stores at aligned co
     const int64_t w = 4 / F;            // outputs per lane
     const uintptr_t op = (uintptr_t)a.out;

@@ -510,6 +510,26 @@ def test_raw_files_stream_to_gpu(pkg, orc, tmp_path, monkeypatch, native):
                                             .permute(2, 1, 0)), a)
 
 
+def test_truncated_file_raises_read_error(pkg, tmp_path, monkeypatch):
+    """A read past the end of a file (truncated after its layout was taken, or
+    a stale index) is an I/O error (BLDP_EIO -> ReadError, an OSError), not an
+    argument error."""
+    monkeypatch.setenv("BLDP_NATIVE_READ", "1")
+    a = np.asfortranarray(np.ones((4096, 1, 64), np.float32))
+    fil = str(tmp_path / "t.fil")
+    pkg.readers.write_fil(fil, dict(fch1=8000.0, foff=-1.0, nchans=4096, nifs=1, tsamp=1.0,
+                                    nbits=32, telescope_id=6, machine_id=10, data_type=1,
+                                    tstart=59000.0, source_name="X"), a)
+    raw = pkg.readers.fil_raw_layout(fil)
+    assert raw is not None
+    os.truncate(fil, os.path.getsize(fil) - 4096 * 4 * 10)  # the last 10 spectra gone
+    C = pkg.COLON
+    with pytest.raises(pkg.ReadError) as e:
+        pkg.worker._reduce_raw_file(fil, raw, (C, C, C), 64, "sum", 1, 0)
+    assert isinstance(e.value, OSError) and e.value.code == pkg._lib.BLDP_EIO
+    assert "truncated" in str(e.value)
+
+
 def torch_f32():
     import torch
 

@@ -33,7 +33,8 @@ VARIANTS = {
     "base": "",
     "nodpp": "-DBLDP_DPP=0",  # lane folds on __shfl_xor (ds_bpermute) instead of DPP / permlane swaps
     "r02": {"rev": R02, "extra": ""},  # the round-2 product build
-    "nolanet": "-DBLDP_LANET=0",  # small odd F, short time blocks: the lane / tile / vector paths                          # nt loads+stores, batch 8, no grid cap
+    "nolanet": "-DBLDP_LANET=0",
+    "rowtst": "-DBLDP_ROWT_LDS_OUT=0",  # k_reduce_rowt: each wave stores its own outputs  # small odd F, short time blocks: the lane / tile / vector paths                          # nt loads+stores, batch 8, no grid cap
     "cap4ts": "-DBLDP_MAX_WG_PER_CU=-1",  # 4 WG/CU grid cap for time-split plans
     "plain": "-DBLDP_NT_LOADS=0 -DBLDP_NT_STORES=0 -DBLDP_MAX_WG_PER_CU=0",  # round-1 start
     # tile path (misaligned / odd-F windows): columns per thread, accumulator sets
@@ -149,8 +150,12 @@ def load(path):
     pkg = entry.load_package()
     L = ctypes.CDLL(path)
     for name, (args, res) in pkg._lib.SIGNATURES.items():
-        getattr(L, name).argtypes = args
-        getattr(L, name).restype = res
+        try:  # (a variant built from an earlier revision lacks the newer entry points)
+            fn = getattr(L, name)
+        except AttributeError:
+            continue
+        fn.argtypes = args
+        fn.restype = res
     return L
 
 

@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import csv
 import json
+import re
 import statistics
 import sys
 
@@ -55,7 +56,8 @@ def main():
         for c in cases:
             part = seq[i:i + c["calls"]]
             i += c["calls"]
-            r = res.setdefault(c["label"], {"kernel": part[0]["name"].split("(")[0],
+            m = re.search(r"(k_\w+(<[^>]*>)?)", part[0]["name"])
+            r = res.setdefault(c["label"], {"kernel": m.group(1) if m else part[0]["name"],
                                             "bytes_algorithmic": c["bytes"], "plan": c["plan"]})
             for k in part[0]:
                 if k in ("name",):

@@ -35,6 +35,7 @@ for s in $STEPS; do
           --timeout-method thread ;;
     tests_*) run "$s" 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 \
           --timeout-method thread -k "${s#tests_}" ;;
+    getband) run getband 600 python tools/getband_probe.py --json "$OUT/getband.json" ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as e; e.smoke()" ;;
     ab) run ab 900 python tools/ab_variants.py --run --suite t1v --rounds 5 \
           --variants "${AB_VARIANTS:-base,dpp,r02}" --json "$OUT/ab_t1v.json" ;;

@@ -82,8 +82,9 @@ def main():
     if a.lib:
         L = ctypes.CDLL(a.lib)
         for name, (args, res) in pkg._lib.SIGNATURES.items():
-            getattr(L, name).argtypes = args
-            getattr(L, name).restype = res
+            if hasattr(L, name):  # (variants of earlier revisions lack newer entry points)
+                getattr(L, name).argtypes = args
+                getattr(L, name).restype = res
     stream = torch.cuda.current_stream()
     sp = int(stream.cuda_stream)
     cases = build_cases(pkg, a.which)
