@@ -596,12 +596,17 @@ __device__ __forceinline__ void lane_tile(const RedArgs &a, int64_t tile) {
 // each cover every line only in part: those are plain loads, so the lines the
 // next piece needs are still in L1 (nt loads there read every line from HBM
 // about twice, the vector path's 1.98x at F = 12).  Stores: one float per lane,
-// 1 KiB per workgroup-instruction.
+// 1 KiB per workgroup-instruction.  Measured and not taken (round 3,
+// profiles/r03/ab_t1v_r03d.json): each wave staging its rows through LDS with
+// coalesced float4 loads and every lane reading its group back, F = 12 0.144
+// vs 0.125 ms, F = 3 0.171 vs 0.162 ms on the 0002 band (the LDS round trip
+// and the workgroup barrier cost more than the partial-line loads).
 //   BLDP_LANET  1 (default) = use it for T in {1, 2, 4}; 0 = the lane / tile / vector paths
 #ifndef BLDP_LANET
 #define BLDP_LANET 1
 #endif
 typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
+typedef float f2v __attribute__((ext_vector_type(2)));
 typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
 template <int F>
 __device__ __forceinline__ void ldF(const float *p, float (&x)[F]) {
@@ -626,35 +631,44 @@ __device__ __forceinline__ void ldF(const float *p, float (&x)[F]) {
     }
   }
 }
-template <int F>
-constexpr int lanet_rows() { return F <= 3 ? 16 : F <= 6 ? 8 : 4; }  // = lanet_rows_host
+//   BLDP_LANET_G  1 = F = 3 / 6 take 4 / 2 consecutive groups per lane (whole
+//                 float4 loads and a float4 / float2 store per lane and row);
+//                 0 (default) = one group per lane
+#ifndef BLDP_LANET_G
+#define BLDP_LANET_G 0
+#endif
+// groups per lane and rows per lane (G F NRW <= 48 floats in registers)
+constexpr int lanet_g(int F) { return BLDP_LANET_G ? (F == 3 ? 4 : F == 6 ? 2 : 1) : 1; }
+constexpr int lanet_rows(int F) {
+  return lanet_g(F) * F <= 3 ? 16 : lanet_g(F) * F <= 6 ? 8 : 4;
+}
 template <int OP, int F, int T>
 __global__ __launch_bounds__(kBlock) void k_reduce_lanet(const RedArgs a) {
-  constexpr int NRW = lanet_rows<F>(), TPB = NRW / T;
+  constexpr int G = lanet_g(F), GF = G * F, NRW = lanet_rows(F), TPB = NRW / T;
   static_assert(NRW % T == 0 && TPB >= 1, "k_reduce_lanet: rows per lane");
   const int tid = threadIdx.x;
   const uint32_t bx = blockIdx.x, bc = (uint32_t)a.blocks_c;
   const uint32_t tq = bx / bc, i = blockIdx.y;
   const int bank = blockIdx.z;
-  const int64_t co = (int64_t)(bx - tq * bc) * kBlock + tid;
+  const int64_t co = ((int64_t)(bx - tq * bc) * kBlock + tid) * G;  // first group of the lane
   const int64_t to0 = (int64_t)tq * TPB;
-  const bool valid = co < a.nco;
+  const int ng = (int)max((int64_t)0, min((int64_t)G, a.nco - co));  // groups of this lane
   const int nb = (int)min((int64_t)TPB, a.nto - to0);
   const float id = R<OP>::id();
-  const float *p = a.in[bank] + a.in_off + (int64_t)i * a.in_ld_i + to0 * T * a.in_ld_t + co * F;
   const int64_t ld = a.in_ld_t;
-  float v[NRW][F];
-  if (valid && nb == TPB) {
+  float v[NRW][GF];
+  const float *p = a.in[bank] + a.in_off + (int64_t)i * a.in_ld_i + to0 * T * ld + co * F;
+  if (ng == G && nb == TPB) {
 #pragma unroll
-    for (int u = 0; u < NRW; ++u) ldF<F>(p + u * ld, v[u]);
+    for (int u = 0; u < NRW; ++u) ldF<GF>(p + u * ld, v[u]);
   } else {
 #pragma unroll
     for (int u = 0; u < NRW; ++u) {
-      if (valid && u < nb * T) {
-        ldF<F>(p + u * ld, v[u]);
+      if (ng == G && u < nb * T) {
+        ldF<GF>(p + u * ld, v[u]);
       } else {
 #pragma unroll
-        for (int f = 0; f < F; ++f) v[u][f] = id;
+        for (int f = 0; f < GF; ++f) v[u][f] = (f < ng * F && u < nb * T) ? p[u * ld + f] : id;
       }
     }
   }
@@ -663,12 +677,34 @@ __global__ __launch_bounds__(kBlock) void k_reduce_lanet(const RedArgs a) {
   for (int b = 0; b < TPB; ++b) {
     // a block's F x T values in the reference's order: the F channels of a
     // spectrum in sequence (fqav's sum over dims = 1), spectrum after spectrum
-    float acc = id;
+    float acc[G];
 #pragma unroll
-    for (int r = 0; r < T; ++r)
+    for (int k = 0; k < G; ++k) {
+      acc[k] = id;
 #pragma unroll
-      for (int f = 0; f < F; ++f) acc = R<OP>::f(acc, v[b * T + r][f]);
-    if (valid && b < nb) st1<1>(o + (to0 + b) * a.out_ld_t, finish<OP>(acc, a));
+      for (int r = 0; r < T; ++r)
+#pragma unroll
+        for (int f = 0; f < F; ++f) acc[k] = R<OP>::f(acc[k], v[b * T + r][k * F + f]);
+      acc[k] = finish<OP>(acc[k], a);
+    }
+    if (b < nb && ng > 0) {
+      float *ob = o + (to0 + b) * a.out_ld_t;
+      if constexpr (G == 4) {
+        if (ng == 4 && a.vec_out) {
+          st4(ob, make_float4(acc[0], acc[1], acc[2], acc[3]));
+          continue;
+        }
+      } else if constexpr (G == 2) {
+        if (ng == 2 && a.vec_out) {
+          const f2v w = {acc[0], acc[1]};
+          __builtin_nontemporal_store(w, reinterpret_cast<f2v *>(ob));
+          continue;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < G; ++k)
+        if (k < ng) st1<1>(ob + k, acc[k]);
+    }
   }
 }
 
@@ -1560,7 +1596,6 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
 }  // namespace
 
 // ---------------------------------------------------------------------------
-static int64_t lanet_rows_host(int64_t F) { return F <= 3 ? 16 : F <= 6 ? 8 : 4; }
 
 Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus) {
   Plan p{};
@@ -1574,17 +1609,20 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
   a.tsub_log2 = 0;
   if (BLDP_LANET && words && a.in_cs == 1 && (T == 1 || T == 2 || T == 4) &&
       (F == 3 || F == 5 || F == 6 || F == 7 || F == 12) && a.ni <= 65535 && a.nbank <= 65535 &&
-      cdiv(a.nco, kBlock) * cdiv(a.nto, lanet_rows_host(F) / T) <= INT32_MAX) {
+      cdiv(a.nco, (int64_t)kBlock * lanet_g((int)F)) * cdiv(a.nto, lanet_rows((int)F) / T) <=
+          INT32_MAX) {
     // small odd groups, short time blocks: one lane per group, NRW rows per lane
     p.path = PATH_LANE;
-    a.tpb = (int32_t)(lanet_rows_host(F) / T);
-    a.blocks_c = cdiv(a.nco, kBlock);
+    a.tpb = (int32_t)(lanet_rows((int)F) / T);
+    a.blocks_c = cdiv(a.nco, (int64_t)kBlock * lanet_g((int)F));
     a.nchunk = 1;
     a.rows_per_chunk = T;
     a.ntiles = a.blocks_c * cdiv(a.nto, a.tpb) * a.ni * a.nbank;
     p.grid = a.ntiles;
     p.ws_bytes = 0;
-    a.vec_out = 0;
+    const int64_t g = lanet_g((int)F);  // outputs per lane: float4 / float2 stores when aligned
+    a.vec_out = g > 1 && (uintptr_t)a.out % (4 * g) == 0 && a.out_bank % g == 0 &&
+                a.out_ld_i % g == 0 && a.out_ld_t % g == 0;
     a.div = (float)(F * T);
     return p;
   }

@@ -30,11 +30,25 @@ CSRC = os.path.join(REPO, "bldistributeddataproducts.jl_amd", "csrc")
 # {"rev": commit, "extra": flags}.  R02 is the last round-2 commit.
 R02 = "5f5c135"
 VARIANTS = {
-    "base": "",
+    "base": "",  # nt loads+stores, batch 8, no grid cap
     "nodpp": "-DBLDP_DPP=0",  # lane folds on __shfl_xor (ds_bpermute) instead of DPP / permlane swaps
     "r02": {"rev": R02, "extra": ""},  # the round-2 product build
-    "nolanet": "-DBLDP_LANET=0",
-    "rowtst": "-DBLDP_ROWT_LDS_OUT=0",  # k_reduce_rowt: each wave stores its own outputs  # small odd F, short time blocks: the lane / tile / vector paths                          # nt loads+stores, batch 8, no grid cap
+    "nolanet": "-DBLDP_LANET=0",  # small odd F, short time blocks: the lane / tile / vector paths
+    "rowtst": "-DBLDP_ROWT_LDS_OUT=0",  # k_reduce_rowt: each wave stores its own outputs
+    "lanetg": "-DBLDP_LANET_G=1",  # k_reduce_lanet: F = 3 / 6 take 4 / 2 groups per lane
+    # TIMING-ONLY patch variants (wrong numerics, never in the product sources):
+    # the current sources with a text substitution, built under build/variants/
+    "kmid2f32": {"patch": [("kurtosis.hip", "double a2 = 0.0, a4 = 0.0, b2 = 0.0, b4 = 0.0;",
+                            "float a2 = 0.f, a4 = 0.f, b2 = 0.f, b4 = 0.f;"),
+                           ("kurtosis.hip", "      a2 += (double)q.x;\n      a4 += (double)q2.x;\n"
+                            "      b2 += (double)q.y;\n      b4 += (double)q2.y;",
+                            "      a2 += q.x;\n      a4 += q2.x;\n      b2 += q.y;\n      b4 += q2.y;")]},
+    "kmid2nochain": {"patch": [("kurtosis.hip",
+                                "    if (wave == w) {\n      if (w > 0) s = carry[lane];",
+                                "    if (wave == w) {\n      if (false) s = carry[lane];")]},
+}
+VARIANTS["kmid2min"] = {"patch": VARIANTS["kmid2f32"]["patch"] + VARIANTS["kmid2nochain"]["patch"]}
+VARIANTS.update({
     "cap4ts": "-DBLDP_MAX_WG_PER_CU=-1",  # 4 WG/CU grid cap for time-split plans
     "plain": "-DBLDP_NT_LOADS=0 -DBLDP_NT_STORES=0 -DBLDP_MAX_WG_PER_CU=0",  # round-1 start
     # tile path (misaligned / odd-F windows): columns per thread, accumulator sets
@@ -119,7 +133,7 @@ VARIANTS = {
     "klds16": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_LDS=16"},
     "klds8b2": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_LDS=8 -DBLDP_KURT_LEAF_LB=2"},
     "klds16b8": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_LDS=16 -DBLDP_KURT_LEAF_LB=8"},
-}
+})
 
 
 def source_tree(rev):
@@ -134,12 +148,37 @@ def source_tree(rev):
     return os.path.join(root, "bldistributeddataproducts.jl_amd", "csrc")
 
 
+def patched_tree(name, patches):
+    """The current csrc/ and include/ with text substitutions (timing-only
+    experiments), under build/variants/src_NAME; each substitution must apply."""
+    import shutil
+
+    root = os.path.join(VDIR, f"src_{name}")
+    if os.path.isdir(root):
+        shutil.rmtree(root)
+    shutil.copytree(os.path.join(REPO, "include"), os.path.join(root, "include"))
+    csrc = os.path.join(root, "bldistributeddataproducts.jl_amd", "csrc")
+    shutil.copytree(CSRC, csrc)
+    for fname, old, new in patches:
+        path = os.path.join(csrc, fname)
+        src = open(path).read()
+        if old not in src:
+            raise SystemExit(f"variant {name}: patch text not found in {fname}: {old[:60]!r}")
+        open(path, "w").write(src.replace(old, new))
+    return csrc
+
+
 def build(names):
     os.makedirs(VDIR, exist_ok=True)
     for n in names:
         out = os.path.join(VDIR, f"libbldp_{n}.so")
         v = VARIANTS[n]
-        csrc, extra = (CSRC, v) if isinstance(v, str) else (source_tree(v["rev"]), v["extra"])
+        if isinstance(v, str):
+            csrc, extra = CSRC, v
+        elif "patch" in v:
+            csrc, extra = patched_tree(n, v["patch"]), v.get("extra", "")
+        else:
+            csrc, extra = source_tree(v["rev"]), v["extra"]
         subprocess.run(["make", "-s", "-B", "-C", csrc, f"OUT={out}", f"EXTRA={extra}"], check=True)
         print("built", out)
 

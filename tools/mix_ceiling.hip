@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 typedef float f4v __attribute__((ext_vector_type(4)));
@@ -63,12 +64,19 @@ __global__ __launch_bounds__(256) void k_mix(const f4v *__restrict__ in, f4v *__
     for (int b = 0; b < UB; ++b) {
       if (u0 + b >= nunits) break;
       f4v *o = out + (u0 + b) * 256 + t;
-      if (ST == 1)
+      if (ST == 1) {
         __builtin_nontemporal_store(acc[b], o);
-      else if (ST == 2)
+      } else if (ST == 2) {
         *o = acc[b];
-      else if (acc[b].x == 1234.5f)
+      } else if (ST == 3) {  // the same 4 KiB as 4 dword stores per lane, 256 B per wave-instruction
+        float *of = reinterpret_cast<float *>(out + (u0 + b) * 256);
+        __builtin_nontemporal_store(acc[b].x, of + t);
+        __builtin_nontemporal_store(acc[b].y, of + 256 + t);
+        __builtin_nontemporal_store(acc[b].z, of + 512 + t);
+        __builtin_nontemporal_store(acc[b].w, of + 768 + t);
+      } else if (acc[b].x == 1234.5f) {
         *o = acc[b];
+      }
     }
   }
 }
@@ -110,7 +118,7 @@ static void run(const f4v *in, f4v *out, int64_t read_bytes, int grid_mode, int 
   const float med = median(ms);
   printf("{\"size\": \"%s\", \"read_bytes\": %.0f, \"write_bytes\": %.0f, \"R\": %d, \"store\": \"%s\", "
          "\"grid\": \"%s\", \"ms_median\": %.4f, \"ms_min\": %.4f, \"GBps_median\": %.1f}\n",
-         label, rb, wb, R, ST == 1 ? "nt" : ST == 2 ? "plain" : "none",
+         label, rb, wb, R, ST == 1 ? "nt" : ST == 2 ? "plain" : ST == 3 ? "nt dword" : "none",
          grid_mode == 0 ? "chunk" : (grid_mode == 1 ? "1/CU" : grid_mode == 2 ? "2/CU" : "4/CU"),
          med, *std::min_element(ms.begin(), ms.end()), (rb + wb) / med / 1e6);
   fflush(stdout);
@@ -138,6 +146,20 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&out, big));  // R = 1 (copy) writes as much as it reads
   hipLaunchKernelGGL(k_fill, dim3(65536), dim3(256), 0, 0, in, big / 16);
   CK(hipDeviceSynchronize());
+  if (argc > 2 && std::string(argv[2]) == "dword") {  // store width at the 0002 band size
+    const int64_t b2 = 8ll * 65536 * 279 * 4;
+    for (int ST : {1, 3}) {
+      const char *l = "0002 band 585 MB";
+      if (ST == 1) {
+        run<2, 1>(in, out, b2, 0, reps, l, ncu); run<3, 1>(in, out, b2, 0, reps, l, ncu);
+        run<4, 1>(in, out, b2, 0, reps, l, ncu); run<12, 1>(in, out, b2, 0, reps, l, ncu);
+      } else {
+        run<2, 3>(in, out, b2, 0, reps, l, ncu); run<3, 3>(in, out, b2, 0, reps, l, ncu);
+        run<4, 3>(in, out, b2, 0, reps, l, ncu); run<12, 3>(in, out, b2, 0, reps, l, ncu);
+      }
+    }
+    return 0;
+  }
   struct Size {
     const char *label;
     int64_t bytes;
