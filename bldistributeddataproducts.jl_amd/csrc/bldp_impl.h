@@ -77,7 +77,8 @@ enum Path { PATH_VEC = 0, PATH_NARROW = 1, PATH_SCALAR = 2, PATH_TILE = 3, PATH_
 struct Plan {
   int path;
   int lpg;                   // lanes per output group (vector path)
-  int64_t grid;              // blocks of 256 threads
+  bool lanet;                // lane path: k_reduce_lanet (NRW rows per lane) not k_reduce_lane
+  int64_t grid;             // blocks of 256 threads
   int64_t nout;              // outputs per bank
   size_t ws_bytes;           // partial workspace required (0 if nchunk == 1)
 };

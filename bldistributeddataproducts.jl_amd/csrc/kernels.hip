@@ -605,70 +605,89 @@ __device__ __forceinline__ void lane_tile(const RedArgs &a, int64_t tile) {
 #ifndef BLDP_LANET
 #define BLDP_LANET 1
 #endif
+//   BLDP_LANET_NT3 1 (default) = F = 3 rows as non-temporal dwordx3 loads; 0 = plain
+//   BLDP_LANET_ROWS_S / _M / _L  rows per lane for F <= 3 / F <= 6 / F > 6
+//                 (16 / 8 / 4 by default: F x rows <= 48 floats in registers)
+//   BLDP_LANET_NTL 1 = F > 4 pieces as non-temporal loads; 0 (default) = plain
+// (G consecutive groups per lane with whole float4 loads and float4 / float2
+// stores was measured too, profiles/r03/ab_t1v_r03e.json: F = 3 with 4 groups
+// per lane 0.297 vs 0.164 ms, not taken.)
+#ifndef BLDP_LANET_NT3
+#define BLDP_LANET_NT3 1
+#endif
+#ifndef BLDP_LANET_ROWS_S
+#define BLDP_LANET_ROWS_S 16
+#endif
+#ifndef BLDP_LANET_ROWS_M
+#define BLDP_LANET_ROWS_M 8
+#endif
+#ifndef BLDP_LANET_ROWS_L
+#define BLDP_LANET_ROWS_L 4
+#endif
+#ifndef BLDP_LANET_NTL
+#define BLDP_LANET_NTL 0
+#endif
 typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
+template <typename V>
+__device__ __forceinline__ V ldv(const float *p, bool nt) {
+  return nt ? __builtin_nontemporal_load(reinterpret_cast<const V *>(p))
+            : *reinterpret_cast<const V *>(p);
+}
 template <int F>
 __device__ __forceinline__ void ldF(const float *p, float (&x)[F]) {
   if constexpr (F == 3) {
-    const f3u v = __builtin_nontemporal_load(reinterpret_cast<const f3u *>(p));
+    const f3u v = ldv<f3u>(p, BLDP_LANET_NT3);
     x[0] = v.x; x[1] = v.y; x[2] = v.z;
   } else {
     int f = 0;
 #pragma unroll
     for (; f + 4 <= F; f += 4) {
-      const f4u v = *reinterpret_cast<const f4u *>(p + f);
+      const f4u v = ldv<f4u>(p + f, BLDP_LANET_NTL);
       x[f] = v.x; x[f + 1] = v.y; x[f + 2] = v.z; x[f + 3] = v.w;
     }
     if constexpr (F % 4 == 3) {
-      const f3u v = *reinterpret_cast<const f3u *>(p + f);
+      const f3u v = ldv<f3u>(p + f, BLDP_LANET_NTL);
       x[f] = v.x; x[f + 1] = v.y; x[f + 2] = v.z;
     } else if constexpr (F % 4 == 2) {
-      const f2u v = *reinterpret_cast<const f2u *>(p + f);
+      const f2u v = ldv<f2u>(p + f, BLDP_LANET_NTL);
       x[f] = v.x; x[f + 1] = v.y;
     } else if constexpr (F % 4 == 1) {
       x[f] = p[f];
     }
   }
 }
-//   BLDP_LANET_G  1 = F = 3 / 6 take 4 / 2 consecutive groups per lane (whole
-//                 float4 loads and a float4 / float2 store per lane and row);
-//                 0 (default) = one group per lane
-#ifndef BLDP_LANET_G
-#define BLDP_LANET_G 0
-#endif
-// groups per lane and rows per lane (G F NRW <= 48 floats in registers)
-constexpr int lanet_g(int F) { return BLDP_LANET_G ? (F == 3 ? 4 : F == 6 ? 2 : 1) : 1; }
 constexpr int lanet_rows(int F) {
-  return lanet_g(F) * F <= 3 ? 16 : lanet_g(F) * F <= 6 ? 8 : 4;
+  return F <= 3 ? BLDP_LANET_ROWS_S : F <= 6 ? BLDP_LANET_ROWS_M : BLDP_LANET_ROWS_L;
 }
 template <int OP, int F, int T>
 __global__ __launch_bounds__(kBlock) void k_reduce_lanet(const RedArgs a) {
-  constexpr int G = lanet_g(F), GF = G * F, NRW = lanet_rows(F), TPB = NRW / T;
+  constexpr int NRW = lanet_rows(F), TPB = NRW / T;
   static_assert(NRW % T == 0 && TPB >= 1, "k_reduce_lanet: rows per lane");
   const int tid = threadIdx.x;
   const uint32_t bx = blockIdx.x, bc = (uint32_t)a.blocks_c;
   const uint32_t tq = bx / bc, i = blockIdx.y;
   const int bank = blockIdx.z;
-  const int64_t co = ((int64_t)(bx - tq * bc) * kBlock + tid) * G;  // first group of the lane
+  const int64_t co = (int64_t)(bx - tq * bc) * kBlock + tid;  // this lane's group
   const int64_t to0 = (int64_t)tq * TPB;
-  const int ng = (int)max((int64_t)0, min((int64_t)G, a.nco - co));  // groups of this lane
   const int nb = (int)min((int64_t)TPB, a.nto - to0);
   const float id = R<OP>::id();
   const int64_t ld = a.in_ld_t;
-  float v[NRW][GF];
+  if (co >= a.nco) return;  // (no barrier below)
+  float v[NRW][F];
   const float *p = a.in[bank] + a.in_off + (int64_t)i * a.in_ld_i + to0 * T * ld + co * F;
-  if (ng == G && nb == TPB) {
+  if (nb == TPB) {
 #pragma unroll
-    for (int u = 0; u < NRW; ++u) ldF<GF>(p + u * ld, v[u]);
+    for (int u = 0; u < NRW; ++u) ldF<F>(p + u * ld, v[u]);
   } else {
 #pragma unroll
     for (int u = 0; u < NRW; ++u) {
-      if (ng == G && u < nb * T) {
-        ldF<GF>(p + u * ld, v[u]);
+      if (u < nb * T) {
+        ldF<F>(p + u * ld, v[u]);
       } else {
 #pragma unroll
-        for (int f = 0; f < GF; ++f) v[u][f] = (f < ng * F && u < nb * T) ? p[u * ld + f] : id;
+        for (int f = 0; f < F; ++f) v[u][f] = id;
       }
     }
   }
@@ -677,34 +696,12 @@ __global__ __launch_bounds__(kBlock) void k_reduce_lanet(const RedArgs a) {
   for (int b = 0; b < TPB; ++b) {
     // a block's F x T values in the reference's order: the F channels of a
     // spectrum in sequence (fqav's sum over dims = 1), spectrum after spectrum
-    float acc[G];
+    float acc = id;
 #pragma unroll
-    for (int k = 0; k < G; ++k) {
-      acc[k] = id;
+    for (int r = 0; r < T; ++r)
 #pragma unroll
-      for (int r = 0; r < T; ++r)
-#pragma unroll
-        for (int f = 0; f < F; ++f) acc[k] = R<OP>::f(acc[k], v[b * T + r][k * F + f]);
-      acc[k] = finish<OP>(acc[k], a);
-    }
-    if (b < nb && ng > 0) {
-      float *ob = o + (to0 + b) * a.out_ld_t;
-      if constexpr (G == 4) {
-        if (ng == 4 && a.vec_out) {
-          st4(ob, make_float4(acc[0], acc[1], acc[2], acc[3]));
-          continue;
-        }
-      } else if constexpr (G == 2) {
-        if (ng == 2 && a.vec_out) {
-          const f2v w = {acc[0], acc[1]};
-          __builtin_nontemporal_store(w, reinterpret_cast<f2v *>(ob));
-          continue;
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < G; ++k)
-        if (k < ng) st1<1>(ob + k, acc[k]);
-    }
+      for (int f = 0; f < F; ++f) acc = R<OP>::f(acc, v[b * T + r][f]);
+    if (b < nb) st1<1>(o + (to0 + b) * a.out_ld_t, finish<OP>(acc, a));
   }
 }
 
@@ -1477,7 +1474,7 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
 #undef BLDP_WAVETL
     return hipGetLastError();
   }
-  if (p.path == PATH_LANE && a.tpb > 1) {  // short time blocks, small odd groups: k_reduce_lanet
+  if (p.path == PATH_LANE && p.lanet) {  // short time blocks, small odd groups: k_reduce_lanet
     const dim3 g3((unsigned)(a.blocks_c * cdiv(a.nto, a.tpb)), (unsigned)a.ni, (unsigned)a.nbank);
 #define BLDP_LANETL(FF, TT) hipLaunchKernelGGL((k_reduce_lanet<OP, FF, TT>), g3, block, 0, s, a); break;
 #define BLDP_LANET_T(FF)                   \
@@ -1609,20 +1606,17 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
   a.tsub_log2 = 0;
   if (BLDP_LANET && words && a.in_cs == 1 && (T == 1 || T == 2 || T == 4) &&
       (F == 3 || F == 5 || F == 6 || F == 7 || F == 12) && a.ni <= 65535 && a.nbank <= 65535 &&
-      cdiv(a.nco, (int64_t)kBlock * lanet_g((int)F)) * cdiv(a.nto, lanet_rows((int)F) / T) <=
-          INT32_MAX) {
+      cdiv(a.nco, (int64_t)kBlock) * cdiv(a.nto, lanet_rows((int)F) / T) <= INT32_MAX) {
     // small odd groups, short time blocks: one lane per group, NRW rows per lane
     p.path = PATH_LANE;
+    p.lanet = true;
     a.tpb = (int32_t)(lanet_rows((int)F) / T);
-    a.blocks_c = cdiv(a.nco, (int64_t)kBlock * lanet_g((int)F));
+    a.blocks_c = cdiv(a.nco, (int64_t)kBlock);
     a.nchunk = 1;
     a.rows_per_chunk = T;
     a.ntiles = a.blocks_c * cdiv(a.nto, a.tpb) * a.ni * a.nbank;
     p.grid = a.ntiles;
     p.ws_bytes = 0;
-    const int64_t g = lanet_g((int)F);  // outputs per lane: float4 / float2 stores when aligned
-    a.vec_out = g > 1 && (uintptr_t)a.out % (4 * g) == 0 && a.out_bank % g == 0 &&
-                a.out_ld_i % g == 0 && a.out_ld_t % g == 0;
     a.div = (float)(F * T);
     return p;
   }

@@ -35,7 +35,12 @@ VARIANTS = {
     "r02": {"rev": R02, "extra": ""},  # the round-2 product build
     "nolanet": "-DBLDP_LANET=0",  # small odd F, short time blocks: the lane / tile / vector paths
     "rowtst": "-DBLDP_ROWT_LDS_OUT=0",  # k_reduce_rowt: each wave stores its own outputs
-    "lanetg": "-DBLDP_LANET_G=1",  # k_reduce_lanet: F = 3 / 6 take 4 / 2 groups per lane
+    "lanetg": {"rev": "bbf0328", "extra": "-DBLDP_LANET_G=1"},  # F = 3 / 6: 4 / 2 groups per lane (removed)
+    "lanetp3": "-DBLDP_LANET_NT3=0",  # k_reduce_lanet: F = 3 rows as plain dwordx3 loads
+    "lanetntl": "-DBLDP_LANET_NTL=1",  # k_reduce_lanet: F > 4 pieces as nt loads
+    "lanets8": "-DBLDP_LANET_ROWS_S=8",  # rows per lane for F <= 3
+    "lanets32": "-DBLDP_LANET_ROWS_S=32",
+    "lanetl8": "-DBLDP_LANET_ROWS_L=8",  # rows per lane for F > 6
     # TIMING-ONLY patch variants (wrong numerics, never in the product sources):
     # the current sources with a text substitution, built under build/variants/
     "kmid2f32": {"patch": [("kurtosis.hip", "double a2 = 0.0, a4 = 0.0, b2 = 0.0, b4 = 0.0;",
