@@ -627,6 +627,10 @@ __device__ __forceinline__ void lane_tile(const RedArgs &a, int64_t tile) {
 #ifndef BLDP_LANET_NTL
 #define BLDP_LANET_NTL 0
 #endif
+//   BLDP_LANET_CS_S  column sets per lane for F <= 3 (1 default)
+#ifndef BLDP_LANET_CS_S
+#define BLDP_LANET_CS_S 1
+#endif
 typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
@@ -661,47 +665,59 @@ __device__ __forceinline__ void ldF(const float *p, float (&x)[F]) {
 constexpr int lanet_rows(int F) {
   return F <= 3 ? BLDP_LANET_ROWS_S : F <= 6 ? BLDP_LANET_ROWS_M : BLDP_LANET_ROWS_L;
 }
+// column sets per lane: a workgroup's groups are CS x 256 consecutive ones
+// (lane t: t, t + 256, ...), so every row it reads is CS x 256 x F floats long
+constexpr int lanet_cs(int F) { return F <= 3 ? BLDP_LANET_CS_S : 1; }
 template <int OP, int F, int T>
 __global__ __launch_bounds__(kBlock) void k_reduce_lanet(const RedArgs a) {
-  constexpr int NRW = lanet_rows(F), TPB = NRW / T;
+  constexpr int NRW = lanet_rows(F), TPB = NRW / T, CS = lanet_cs(F);
   static_assert(NRW % T == 0 && TPB >= 1, "k_reduce_lanet: rows per lane");
   const int tid = threadIdx.x;
   const uint32_t bx = blockIdx.x, bc = (uint32_t)a.blocks_c;
   const uint32_t tq = bx / bc, i = blockIdx.y;
   const int bank = blockIdx.z;
-  const int64_t co = (int64_t)(bx - tq * bc) * kBlock + tid;  // this lane's group
+  const int64_t co = (int64_t)(bx - tq * bc) * (kBlock * CS) + tid;  // this lane's first group
   const int64_t to0 = (int64_t)tq * TPB;
   const int nb = (int)min((int64_t)TPB, a.nto - to0);
   const float id = R<OP>::id();
   const int64_t ld = a.in_ld_t;
   if (co >= a.nco) return;  // (no barrier below)
-  float v[NRW][F];
+  float v[CS][NRW][F];
   const float *p = a.in[bank] + a.in_off + (int64_t)i * a.in_ld_i + to0 * T * ld + co * F;
-  if (nb == TPB) {
 #pragma unroll
-    for (int u = 0; u < NRW; ++u) ldF<F>(p + u * ld, v[u]);
-  } else {
+  for (int j = 0; j < CS; ++j) {
+    const bool cj = j == 0 || co + j * kBlock < a.nco;
+    const float *pj = p + j * kBlock * F;
+    if (nb == TPB && cj) {
 #pragma unroll
-    for (int u = 0; u < NRW; ++u) {
-      if (u < nb * T) {
-        ldF<F>(p + u * ld, v[u]);
-      } else {
+      for (int u = 0; u < NRW; ++u) ldF<F>(pj + u * ld, v[j][u]);
+    } else {
 #pragma unroll
-        for (int f = 0; f < F; ++f) v[u][f] = id;
+      for (int u = 0; u < NRW; ++u) {
+        if (cj && u < nb * T) {
+          ldF<F>(pj + u * ld, v[j][u]);
+        } else {
+#pragma unroll
+          for (int f = 0; f < F; ++f) v[j][u][f] = id;
+        }
       }
     }
   }
   float *o = a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + co;
 #pragma unroll
   for (int b = 0; b < TPB; ++b) {
-    // a block's F x T values in the reference's order: the F channels of a
-    // spectrum in sequence (fqav's sum over dims = 1), spectrum after spectrum
-    float acc = id;
 #pragma unroll
-    for (int r = 0; r < T; ++r)
+    for (int j = 0; j < CS; ++j) {
+      // a block's F x T values in the reference's order: the F channels of a
+      // spectrum in sequence (fqav's sum over dims = 1), spectrum after spectrum
+      float acc = id;
 #pragma unroll
-      for (int f = 0; f < F; ++f) acc = R<OP>::f(acc, v[b * T + r][f]);
-    if (b < nb) st1<1>(o + (to0 + b) * a.out_ld_t, finish<OP>(acc, a));
+      for (int r = 0; r < T; ++r)
+#pragma unroll
+        for (int f = 0; f < F; ++f) acc = R<OP>::f(acc, v[j][b * T + r][f]);
+      if (b < nb && (j == 0 || co + j * kBlock < a.nco))
+        st1<1>(o + (to0 + b) * a.out_ld_t + j * kBlock, finish<OP>(acc, a));
+    }
   }
 }
 
@@ -1606,12 +1622,13 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
   a.tsub_log2 = 0;
   if (BLDP_LANET && words && a.in_cs == 1 && (T == 1 || T == 2 || T == 4) &&
       (F == 3 || F == 5 || F == 6 || F == 7 || F == 12) && a.ni <= 65535 && a.nbank <= 65535 &&
-      cdiv(a.nco, (int64_t)kBlock) * cdiv(a.nto, lanet_rows((int)F) / T) <= INT32_MAX) {
+      cdiv(a.nco, (int64_t)kBlock * lanet_cs((int)F)) * cdiv(a.nto, lanet_rows((int)F) / T) <=
+          INT32_MAX) {
     // small odd groups, short time blocks: one lane per group, NRW rows per lane
     p.path = PATH_LANE;
     p.lanet = true;
     a.tpb = (int32_t)(lanet_rows((int)F) / T);
-    a.blocks_c = cdiv(a.nco, (int64_t)kBlock);
+    a.blocks_c = cdiv(a.nco, (int64_t)kBlock * lanet_cs((int)F));
     a.nchunk = 1;
     a.rows_per_chunk = T;
     a.ntiles = a.blocks_c * cdiv(a.nto, a.tpb) * a.ni * a.nbank;

@@ -315,7 +315,7 @@ __global__ __launch_bounds__(kB) void k_kurt_mid(const KurtArgs k) {
 // boundary +27%, 100 spectra +6%; at 512 spectra (3 waves/SIMD, one workgroup
 // per CU) -18%, so longer windows stay on k_kurt_mid.
 //   BLDP_KURT_MID_CPL  2 (default) = this kernel where it applies; 1 = k_kurt_mid only
-//   BLDP_KURT_MID_NW   its waves per workgroup (8 default, or 4)
+//   BLDP_KURT_MID_NW   its waves per workgroup (8 default, 4 or 16)
 #ifndef BLDP_KURT_MID_CPL
 #define BLDP_KURT_MID_CPL 2
 #endif
@@ -1057,15 +1057,30 @@ hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s) {
       hipLaunchKernelGGL((k_kurt_regs<32, false>), g1, block, 0, s, k);
     return hipGetLastError();
   }
-  if (p == KP_MID && BLDP_KURT_MID_CPL == 2 && k.vec && cdivk(k.nt, BLDP_KURT_MID_NW) <= 48) {
+  if (p == KP_MID && BLDP_KURT_MID_CPL == 2 && k.vec && cdivk(k.nt, 8) <= 48) {
     constexpr int NW = BLDP_KURT_MID_NW;
-    static_assert(NW == 4 || NW == 8, "BLDP_KURT_MID_NW: 4 or 8");
+    static_assert(NW == 4 || NW == 8 || NW == 16, "BLDP_KURT_MID_NW: 4, 8 or 16");
     const dim3 g1((unsigned)(cdivk(k.nc, 128) * k.nrow)), b2(64 * NW);
-    switch (cdivk(cdivk(k.nt, NW), 16)) {
-      case 1: hipLaunchKernelGGL((k_kurt_mid2<16, NW>), g1, b2, 0, s, k); break;
-      case 2: hipLaunchKernelGGL((k_kurt_mid2<32, NW>), g1, b2, 0, s, k); break;
-      case 3: hipLaunchKernelGGL((k_kurt_mid2<48, NW>), g1, b2, 0, s, k); break;
-      default: hipLaunchKernelGGL((k_kurt_mid2<48, NW>), g1, b2, 0, s, k); break;
+    // registers sized to a wave's spectra, 8 at a time (occupancy: 113 VGPRs
+    // at 48 spectra = 4 waves/SIMD, 80 at 32 = 6, 48 at 16 = 8)
+    switch (cdivk(cdivk(k.nt, NW), 8)) {
+#define BLDP_MID2(NR) hipLaunchKernelGGL((k_kurt_mid2<NR, NW>), g1, b2, 0, s, k); break;
+      case 1: BLDP_MID2(8)
+      case 2: BLDP_MID2(16)
+      case 3: BLDP_MID2(24)
+      case 4: BLDP_MID2(32)
+      case 5: BLDP_MID2(40)
+      case 6: BLDP_MID2(48)
+#if BLDP_KURT_MID_NW < 8
+      case 7: BLDP_MID2(56)
+      case 8: BLDP_MID2(64)
+      case 9: BLDP_MID2(72)
+      case 10: BLDP_MID2(80)
+      case 11: BLDP_MID2(88)
+      case 12: BLDP_MID2(96)
+#endif
+#undef BLDP_MID2
+      default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
   }

@@ -192,7 +192,7 @@ def test_reduce_short_time_blocks_integer_exact(eng, orc, shape):
 # 65532 channels among them; bit-exact on integer data, windows and bands.
 LANET_SHAPES = [(1000, 1, 37, 3, 1), (21845, 1, 18, 3, 1), (300, 2, 20, 5, 2), (257, 1, 33, 6, 1),
                 (100, 3, 12, 7, 4), (513, 1, 19, 12, 1), (5461, 1, 9, 12, 1), (200, 1, 8, 12, 2),
-                (70, 2, 24, 3, 4), (90, 1, 18, 6, 2), (600, 2, 17, 12, 4), (300, 1, 9, 5, 4)]
+                (70, 2, 24, 3, 4), (90, 1, 18, 6, 2), (600, 2, 16, 12, 4), (300, 1, 12, 5, 4)]
 
 
 def lanet_rows(F):

@@ -114,7 +114,7 @@ def test_kurtosis_typed(pkg, eng, orc, dt):
     for k, (nc, ni, nt) in enumerate([(64, 1, 100), (37, 2, 1500), (5, 1, 5000), (3, 1, 1)]):
         a = rand(dt, (nc, ni, nt), seed=5 * k + np.dtype(dt).num)
         if np.dtype(dt).kind != "f":  # keep the Float64 mean's sums exact (< 2^53)
-            a = np.asfortranarray((a % 1000).astype(dt))
+            a = np.asfortranarray((a.astype(np.int64) % 1000).astype(dt))
         want = orc.np_kurtosis_typed(a)
         got = eng.fb_to_numpy(eng.kurtosis(to_dev(eng, a)))
         assert same(got, want), (dt, (nc, ni, nt))

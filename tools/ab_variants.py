@@ -41,6 +41,12 @@ VARIANTS = {
     "lanets8": "-DBLDP_LANET_ROWS_S=8",  # rows per lane for F <= 3
     "lanets32": "-DBLDP_LANET_ROWS_S=32",
     "lanetl8": "-DBLDP_LANET_ROWS_L=8",  # rows per lane for F > 6
+    "lanets4": "-DBLDP_LANET_ROWS_S=4",
+    "lanets12": "-DBLDP_LANET_ROWS_S=12",
+    "lanets8c2": "-DBLDP_LANET_ROWS_S=8 -DBLDP_LANET_CS_S=2",  # F <= 3: 512 groups per workgroup
+    "lanets4c4": "-DBLDP_LANET_ROWS_S=4 -DBLDP_LANET_CS_S=4",
+    "kmidnr16": {"rev": "7474fea", "extra": ""},  # k_kurt_mid2 registers in steps of 16 spectra
+    "kmid2w16": "-DBLDP_KURT_MID_NW=16",  # k_kurt_mid2 with 16 waves (<= 24 spectra each)
     # TIMING-ONLY patch variants (wrong numerics, never in the product sources):
     # the current sources with a text substitution, built under build/variants/
     "kmid2f32": {"patch": [("kurtosis.hip", "double a2 = 0.0, a4 = 0.0, b2 = 0.0, b4 = 0.0;",

@@ -81,14 +81,80 @@ __global__ __launch_bounds__(256) void k_mix(const f4v *__restrict__ in, f4v *__
   }
 }
 
-__global__ void k_fill(f4v *p, int64_t n4) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256)
-    p[i] = f4v{1.f, 2.f, 3.f, 4.f};
-}
-
 static float median(std::vector<float> v) {
   std::sort(v.begin(), v.end());
   return v[v.size() / 2];
+}
+
+// k_coltile<W, NW, NR>: the read pattern of the kurtosis register kernels
+// (k_kurt_mid2: W = 8 bytes per lane, NW = 8 waves): a workgroup owns a
+// (64 x W bytes) x nt column tile of one (nc x nt) bank, its NW waves split
+// the nt rows, every wave-instruction reads 64 x W contiguous bytes at the
+// row pitch; no arithmetic beyond a sum, one double per channel written (the
+// kurtosis output).  Floor of that access pattern, not of the kernel.
+template <int W, int NW, int NR>
+__global__ __launch_bounds__(64 * NW) void k_coltile(const float *__restrict__ in,
+                                                     double *__restrict__ out, int nc, int nt) {
+  typedef float vt __attribute__((ext_vector_type(W / 4)));
+  constexpr int CPW = 16 * W;  // channels per tile
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ctiles = nc / CPW;
+  const int ib = blockIdx.x / ctiles, c = (blockIdx.x % ctiles) * CPW + lane * (W / 4);
+  const int r0 = __builtin_amdgcn_readfirstlane((wave * nt) / NW);
+  const int cnt = __builtin_amdgcn_readfirstlane((((wave + 1) * nt) / NW) - r0);
+  const float *p = in + (int64_t)ib * nc * nt + (int64_t)r0 * nc + c;
+  vt v[NR];
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+    v[r] = r < cnt ? __builtin_nontemporal_load(reinterpret_cast<const vt *>(p + (int64_t)r * nc)) : vt{};
+  vt s = {};
+#pragma unroll
+  for (int r = 0; r < NR; ++r) s += v[r];
+  __shared__ vt part[NW][64];
+  part[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0) {
+    vt t = {};
+#pragma unroll
+    for (int q = 0; q < NW; ++q) t += part[q][lane];
+    double *o = out + (int64_t)ib * nc + c;
+#pragma unroll
+    for (int k = 0; k < W / 4; ++k) o[k] = (double)t[k];
+  }
+}
+
+template <int W, int NW, int NR>
+static void run_coltile(const float *in, double *out, int nrow, int nc, int nt, int reps) {
+  const unsigned grid = (unsigned)(nrow * (nc / (16 * W)));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  std::vector<float> ms;
+  for (int r = 0; r < reps + 2; ++r) {
+    CK(hipEventRecord(e0, 0));
+    for (int i = 0; i < 5; ++i)
+      hipLaunchKernelGGL((k_coltile<W, NW, NR>), dim3(grid), dim3(64 * NW), 0, 0, in, out, nc, nt);
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float m;
+    CK(hipEventElapsedTime(&m, e0, e1));
+    if (r >= 2) ms.push_back(m / 5);
+  }
+  const double rb = (double)nrow * nc * nt * 4, wb = (double)nrow * nc * 8;
+  const float med = median(ms);
+  printf("{\"size\": \"coltile %d x %d x %d\", \"bytes_per_lane\": %d, \"waves\": %d, \"rows_per_wave\": %d, "
+         "\"read_bytes\": %.0f, \"write_bytes\": %.0f, \"ms_median\": %.4f, \"ms_min\": %.4f, "
+         "\"GBps_median\": %.1f}\n",
+         nrow, nc, nt, W, NW, NR, rb, wb, med, *std::min_element(ms.begin(), ms.end()),
+         (rb + wb) / med / 1e6);
+  fflush(stdout);
+  CK(hipEventDestroy(e0));
+  CK(hipEventDestroy(e1));
+}
+
+__global__ void k_fill(f4v *p, int64_t n4) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256)
+    p[i] = f4v{1.f, 2.f, 3.f, 4.f};
 }
 
 template <int R, int ST>
@@ -157,6 +223,19 @@ int main(int argc, char **argv) {
         run<2, 3>(in, out, b2, 0, reps, l, ncu); run<3, 3>(in, out, b2, 0, reps, l, ncu);
         run<4, 3>(in, out, b2, 0, reps, l, ncu); run<12, 3>(in, out, b2, 0, reps, l, ncu);
       }
+    }
+    return 0;
+  }
+  if (argc > 2 && std::string(argv[2]) == "coltile") {  // the 0002 band as the kurtosis reads it
+    const float *fi = reinterpret_cast<const float *>(in);
+    double *fo = reinterpret_cast<double *>(out);
+    for (int nt : {279, 272}) {
+      run_coltile<8, 8, 35>(fi, fo, 8, 65536, nt, reps);    // k_kurt_mid2's geometry
+      run_coltile<8, 4, 70>(fi, fo, 8, 65536, nt, reps);
+      run_coltile<16, 8, 35>(fi, fo, 8, 65536, nt, reps);
+      run_coltile<16, 16, 18>(fi, fo, 8, 65536, nt, reps);
+      run_coltile<8, 16, 18>(fi, fo, 8, 65536, nt, reps);
+      run_coltile<4, 8, 35>(fi, fo, 8, 65536, nt, reps);    // k_kurt_mid's 256 B per wave
     }
     return 0;
   }

@@ -32,6 +32,7 @@ for s in $STEPS; do
   case $s in
     mix) run mix 300 ./build/mix_ceiling 10 ;;
     mixdword) run mixdword 120 ./build/mix_ceiling 10 dword ;;
+    coltile) run coltile 120 ./build/mix_ceiling 10 coltile ;;
     tests) run tests 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 \
           --timeout-method thread ;;
     tests_*) run "$s" 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 \
