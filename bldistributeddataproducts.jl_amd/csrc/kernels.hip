@@ -607,7 +607,8 @@ __device__ __forceinline__ void lane_tile(const RedArgs &a, int64_t tile) {
 #endif
 //   BLDP_LANET_NT3 1 (default) = F = 3 rows as non-temporal dwordx3 loads; 0 = plain
 //   BLDP_LANET_ROWS_S / _M / _L  rows per lane for F <= 3 / F <= 6 / F > 6
-//                 (16 / 8 / 4 by default: F x rows <= 48 floats in registers)
+//                 (8 / 8 / 4 by default; 16 for F <= 3 was the default until the
+//                 aligned output segments below, with which 8 is 10% faster)
 //   BLDP_LANET_NTL 1 = F > 4 pieces as non-temporal loads; 0 (default) = plain
 // (G consecutive groups per lane with whole float4 loads and float4 / float2
 // stores was measured too, profiles/r03/ab_t1v_r03e.json: F = 3 with 4 groups
@@ -616,7 +617,7 @@ __device__ __forceinline__ void lane_tile(const RedArgs &a, int64_t tile) {
 #define BLDP_LANET_NT3 1
 #endif
 #ifndef BLDP_LANET_ROWS_S
-#define BLDP_LANET_ROWS_S 16
+#define BLDP_LANET_ROWS_S 8
 #endif
 #ifndef BLDP_LANET_ROWS_M
 #define BLDP_LANET_ROWS_M 8
@@ -631,6 +632,20 @@ __device__ __forceinline__ void lane_tile(const RedArgs &a, int64_t tile) {
 #ifndef BLDP_LANET_CS_S
 #define BLDP_LANET_CS_S 1
 #endif
+//   BLDP_LANET_OALIGN 1 = each output row's 256-group segments start on a
+//                 64-byte boundary of the product (the segment grid shifted by
+//                 that row's misalignment), so no two workgroups share a line
+//                 and only row ends are partial writes; 0 = segments at k x 256.
+//                 A product row of nco groups starts on a line only when nco is a
+//                 multiple of 16; otherwise every workgroup boundary fell inside a
+//                 line and each of those lines went out as two partial writes from
+//                 two workgroups.  0002 band, fqavby = 3 (21845 groups a row):
+//                 0.169 -> 0.134 ms with 8 rows per lane; fqavby = 12 0.125 -> 0.122
+//                 (profiles/r03/ab_t1v_r03g_oalign.json, bit-identical)
+#ifndef BLDP_LANET_OALIGN
+#define BLDP_LANET_OALIGN 1
+#endif
+constexpr int lanet_oalign_pad() { return BLDP_LANET_OALIGN ? 15 : 0; }
 typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
@@ -681,6 +696,42 @@ __global__ __launch_bounds__(kBlock) void k_reduce_lanet(const RedArgs a) {
   const int nb = (int)min((int64_t)TPB, a.nto - to0);
   const float id = R<OP>::id();
   const int64_t ld = a.in_ld_t;
+  if constexpr (BLDP_LANET_OALIGN && CS == 1) {
+    // per output row b: this lane's group, shifted so the workgroup's 256
+    // outputs of that row start on a 64-byte line of the product
+    float *orow[TPB];
+    int64_t g[TPB];
+    bool ok[TPB];
+    const int64_t cb = co - tid;
+#pragma unroll
+    for (int b = 0; b < TPB; ++b) {
+      orow[b] = a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + (to0 + b) * a.out_ld_t;
+      const int64_t s = (int64_t)((reinterpret_cast<uintptr_t>(orow[b]) >> 2) & 15);
+      g[b] = cb - s + tid;
+      ok[b] = b < nb && g[b] >= 0 && g[b] < a.nco;
+    }
+    float v[NRW][F];
+    const float *p = a.in[bank] + a.in_off + (int64_t)i * a.in_ld_i + to0 * T * ld;
+#pragma unroll
+    for (int u = 0; u < NRW; ++u) {
+      if (ok[u / T]) {
+        ldF<F>(p + u * ld + g[u / T] * F, v[u]);
+      } else {
+#pragma unroll
+        for (int f = 0; f < F; ++f) v[u][f] = id;
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < TPB; ++b) {
+      float acc = id;
+#pragma unroll
+      for (int r = 0; r < T; ++r)
+#pragma unroll
+        for (int f = 0; f < F; ++f) acc = R<OP>::f(acc, v[b * T + r][f]);
+      if (ok[b]) st1<1>(orow[b] + g[b], finish<OP>(acc, a));
+    }
+    return;
+  }
   if (co >= a.nco) return;  // (no barrier below)
   float v[CS][NRW][F];
   const float *p = a.in[bank] + a.in_off + (int64_t)i * a.in_ld_i + to0 * T * ld + co * F;
@@ -1083,13 +1134,18 @@ void k_reduce_row(const RedArgs a) {
 #ifndef BLDP_ROWT_MAXWAVES
 #define BLDP_ROWT_MAXWAVES 6
 #endif
+//   BLDP_ROWT_ROWS  rows in flight per lane (TPB = ROWS / T time blocks per
+//                  workgroup): 16 (default) or 8
+#ifndef BLDP_ROWT_ROWS
+#define BLDP_ROWT_ROWS 16
+#endif
 template <int OP, int G4, int T>
 __global__ __launch_bounds__(kBlock)
 #if BLDP_ROWT_MAXWAVES > 0
 __attribute__((amdgpu_waves_per_eu(1, BLDP_ROWT_MAXWAVES)))
 #endif
 void k_reduce_rowt(const RedArgs a) {
-  constexpr int TPB = 16 / T, NR = TPB * T;
+  constexpr int TPB = BLDP_ROWT_ROWS / T, NR = TPB * T;
   const int tid = threadIdx.x;
   // grid: x = (column block, time group) column block fastest, y = IF, z = bank.
   // Windows of <= 128 float4 columns (the 512-channel 0001 product) share a
@@ -1622,13 +1678,15 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
   a.tsub_log2 = 0;
   if (BLDP_LANET && words && a.in_cs == 1 && (T == 1 || T == 2 || T == 4) &&
       (F == 3 || F == 5 || F == 6 || F == 7 || F == 12) && a.ni <= 65535 && a.nbank <= 65535 &&
-      cdiv(a.nco, (int64_t)kBlock * lanet_cs((int)F)) * cdiv(a.nto, lanet_rows((int)F) / T) <=
+      cdiv(a.nco + lanet_oalign_pad(), (int64_t)kBlock * lanet_cs((int)F)) *
+              cdiv(a.nto, lanet_rows((int)F) / T) <=
           INT32_MAX) {
     // small odd groups, short time blocks: one lane per group, NRW rows per lane
     p.path = PATH_LANE;
     p.lanet = true;
     a.tpb = (int32_t)(lanet_rows((int)F) / T);
-    a.blocks_c = cdiv(a.nco, (int64_t)kBlock * lanet_cs((int)F));
+    a.blocks_c = cdiv(a.nco + (lanet_cs((int)F) == 1 ? lanet_oalign_pad() : 0),
+                      (int64_t)kBlock * lanet_cs((int)F));
     a.nchunk = 1;
     a.rows_per_chunk = T;
     a.ntiles = a.blocks_c * cdiv(a.nto, a.tpb) * a.ni * a.nbank;
@@ -1729,7 +1787,7 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
     const int64_t bc = cdiv(a.nco * (F / 4), kBlock);
     // short time blocks: 16 / T of them per workgroup (k_reduce_rowt; grid x =
     // column blocks x time groups, so long 0001-product windows fit too)
-    const int64_t tpb = (T == 1 || T == 2 || T == 4) ? 16 / T : 1;
+    const int64_t tpb = (T == 1 || T == 2 || T == 4) ? BLDP_ROWT_ROWS / T : 1;
     if (BLDP_ROW_TPB && tpb > 1 && a.nto > 1 && bc * cdiv(a.nto, tpb) <= INT32_MAX &&
         a.ni <= 65535) {
       p.path = PATH_VEC_ROW;

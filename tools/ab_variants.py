@@ -45,6 +45,11 @@ VARIANTS = {
     "lanets12": "-DBLDP_LANET_ROWS_S=12",
     "lanets8c2": "-DBLDP_LANET_ROWS_S=8 -DBLDP_LANET_CS_S=2",  # F <= 3: 512 groups per workgroup
     "lanets4c4": "-DBLDP_LANET_ROWS_S=4 -DBLDP_LANET_CS_S=4",
+    "lanetoa": "-DBLDP_LANET_OALIGN=1",  # output segments on 64-byte lines of each product row
+    "lanetoas8": "-DBLDP_LANET_OALIGN=1 -DBLDP_LANET_ROWS_S=8",
+    "lanetoap3": "-DBLDP_LANET_OALIGN=1 -DBLDP_LANET_NT3=0",
+    "lanetold": "-DBLDP_LANET_OALIGN=0 -DBLDP_LANET_ROWS_S=16",  # the r03f defaults
+    "rowt8": "-DBLDP_ROWT_ROWS=8",  # k_reduce_rowt: 8 rows per lane, twice the workgroups
     "kmidnr16": {"rev": "7474fea", "extra": ""},  # k_kurt_mid2 registers in steps of 16 spectra
     "kmid2w16": "-DBLDP_KURT_MID_NW=16",  # k_kurt_mid2 with 16 waves (<= 24 spectra each)
     # TIMING-ONLY patch variants (wrong numerics, never in the product sources):
