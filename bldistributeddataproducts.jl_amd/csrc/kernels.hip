@@ -607,8 +607,9 @@ __device__ __forceinline__ void lane_tile(const RedArgs &a, int64_t tile) {
 #endif
 //   BLDP_LANET_NT3 1 (default) = F = 3 rows as non-temporal dwordx3 loads; 0 = plain
 //   BLDP_LANET_ROWS_S / _M / _L  rows per lane for F <= 3 / F <= 6 / F > 6
-//                 (8 / 8 / 4 by default; 16 for F <= 3 was the default until the
-//                 aligned output segments below, with which 8 is 10% faster)
+//                 (8 / 8 / 8 by default; 16 for F <= 3 and 4 for F > 6 were the
+//                 defaults until the aligned output segments below, with which 8
+//                 is 10% (F = 3) and 3% (F = 12) faster, profiles/r03/ab_t1v_r03h.json)
 //   BLDP_LANET_NTL 1 = F > 4 pieces as non-temporal loads; 0 (default) = plain
 // (G consecutive groups per lane with whole float4 loads and float4 / float2
 // stores was measured too, profiles/r03/ab_t1v_r03e.json: F = 3 with 4 groups
@@ -623,7 +624,7 @@ __device__ __forceinline__ void lane_tile(const RedArgs &a, int64_t tile) {
 #define BLDP_LANET_ROWS_M 8
 #endif
 #ifndef BLDP_LANET_ROWS_L
-#define BLDP_LANET_ROWS_L 4
+#define BLDP_LANET_ROWS_L 8
 #endif
 #ifndef BLDP_LANET_NTL
 #define BLDP_LANET_NTL 0
@@ -1134,18 +1135,23 @@ void k_reduce_row(const RedArgs a) {
 #ifndef BLDP_ROWT_MAXWAVES
 #define BLDP_ROWT_MAXWAVES 6
 #endif
-//   BLDP_ROWT_ROWS  rows in flight per lane (TPB = ROWS / T time blocks per
-//                  workgroup): 16 (default) or 8
-#ifndef BLDP_ROWT_ROWS
-#define BLDP_ROWT_ROWS 16
+//   BLDP_ROWT_SMALL  launches that would have fewer than this many workgroups
+//                  per CU with 16 rows per lane take 8 rows per lane (TPB = 8 / T,
+//                  twice the workgroups; 0 = always 16).  A/B, profiles/r03/
+//                  ab_rowt_r03i.json (bit-identical): 8 rows win on one 0002 file
+//                  (1152 workgroups, 4.5 per CU: +10-18% at F = 16..256, T = 1, 2, 4)
+//                  and on the 0002 band (9216: +1.5-3.5%), and lose on the 0000 and
+//                  0001 bands (>= 200k workgroups: -1.5-3.5%)
+#ifndef BLDP_ROWT_SMALL
+#define BLDP_ROWT_SMALL 64
 #endif
-template <int OP, int G4, int T>
+template <int OP, int G4, int T, int NRW>
 __global__ __launch_bounds__(kBlock)
 #if BLDP_ROWT_MAXWAVES > 0
 __attribute__((amdgpu_waves_per_eu(1, BLDP_ROWT_MAXWAVES)))
 #endif
 void k_reduce_rowt(const RedArgs a) {
-  constexpr int TPB = BLDP_ROWT_ROWS / T, NR = TPB * T;
+  constexpr int TPB = NRW / T, NR = TPB * T;
   const int tid = threadIdx.x;
   // grid: x = (column block, time group) column block fastest, y = IF, z = bank.
   // Windows of <= 128 float4 columns (the 512-channel 0001 product) share a
@@ -1572,16 +1578,24 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
   if (p.path == PATH_VEC_ROW && a.tpb > 1) {  // short time blocks, several per workgroup
     const dim3 g3((unsigned)(a.blocks_c * cdiv(cdiv(a.nto, a.tpb), 1 << a.tsub_log2)),
                   (unsigned)a.ni, (unsigned)a.nbank);
-#define BLDP_ROWT(T)                                                                     \
-  switch (a.F / 4) {                                                                     \
-    case 1: hipLaunchKernelGGL((k_reduce_rowt<OP, 1, T>), g3, block, 0, s, a); break;    \
-    case 2: hipLaunchKernelGGL((k_reduce_rowt<OP, 2, T>), g3, block, 0, s, a); break;    \
-    case 4: hipLaunchKernelGGL((k_reduce_rowt<OP, 4, T>), g3, block, 0, s, a); break;    \
-    case 8: hipLaunchKernelGGL((k_reduce_rowt<OP, 8, T>), g3, block, 0, s, a); break;    \
-    case 16: hipLaunchKernelGGL((k_reduce_rowt<OP, 16, T>), g3, block, 0, s, a); break;  \
-    case 32: hipLaunchKernelGGL((k_reduce_rowt<OP, 32, T>), g3, block, 0, s, a); break;  \
-    case 64: hipLaunchKernelGGL((k_reduce_rowt<OP, 64, T>), g3, block, 0, s, a); break;  \
-    default: return hipErrorInvalidValue;                                                \
+#define BLDP_ROWTN(T, N)                                                                    \
+  switch (a.F / 4) {                                                                        \
+    case 1: hipLaunchKernelGGL((k_reduce_rowt<OP, 1, T, N>), g3, block, 0, s, a); break;    \
+    case 2: hipLaunchKernelGGL((k_reduce_rowt<OP, 2, T, N>), g3, block, 0, s, a); break;    \
+    case 4: hipLaunchKernelGGL((k_reduce_rowt<OP, 4, T, N>), g3, block, 0, s, a); break;    \
+    case 8: hipLaunchKernelGGL((k_reduce_rowt<OP, 8, T, N>), g3, block, 0, s, a); break;    \
+    case 16: hipLaunchKernelGGL((k_reduce_rowt<OP, 16, T, N>), g3, block, 0, s, a); break;  \
+    case 32: hipLaunchKernelGGL((k_reduce_rowt<OP, 32, T, N>), g3, block, 0, s, a); break;  \
+    case 64: hipLaunchKernelGGL((k_reduce_rowt<OP, 64, T, N>), g3, block, 0, s, a); break;  \
+    default: return hipErrorInvalidValue;                                                   \
+  }
+#define BLDP_ROWT(T)                 \
+  if (a.tpb * (T) == 8) {            \
+    BLDP_ROWTN(T, 8)                 \
+  } else if (a.tpb * (T) == 16) {    \
+    BLDP_ROWTN(T, 16)                \
+  } else {                           \
+    return hipErrorInvalidValue;     \
   }
     switch (a.T) {
       case 1: BLDP_ROWT(1) break;
@@ -1590,6 +1604,7 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
       default: return hipErrorInvalidValue;
     }
 #undef BLDP_ROWT
+#undef BLDP_ROWTN
     return hipGetLastError();
   }
   if (p.path == PATH_VEC_ROW) {
@@ -1787,15 +1802,19 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
     const int64_t bc = cdiv(a.nco * (F / 4), kBlock);
     // short time blocks: 16 / T of them per workgroup (k_reduce_rowt; grid x =
     // column blocks x time groups, so long 0001-product windows fit too)
-    const int64_t tpb = (T == 1 || T == 2 || T == 4) ? BLDP_ROWT_ROWS / T : 1;
+    int64_t tpb = (T == 1 || T == 2 || T == 4) ? 16 / T : 1;
     if (BLDP_ROW_TPB && tpb > 1 && a.nto > 1 && bc * cdiv(a.nto, tpb) <= INT32_MAX &&
         a.ni <= 65535) {
       p.path = PATH_VEC_ROW;
       a.blocks_c = bc;
-      a.tpb = (int32_t)tpb;
       // <= 128 float4 columns: 2 or 4 time groups per workgroup (>= 64 lanes each)
       const int64_t cols = a.nco * (F / 4);
       a.tsub_log2 = BLDP_ROWT_PACK ? (cols <= 64 ? 2 : cols <= 128 ? 1 : 0) : 0;
+      // small launches: 8 rows per lane, twice the workgroups (BLDP_ROWT_SMALL)
+      if (bc * cdiv(cdiv(a.nto, tpb), (int64_t)1 << a.tsub_log2) * a.ni * a.nbank <
+          (int64_t)BLDP_ROWT_SMALL * num_cus)
+        tpb = 8 / T;
+      a.tpb = (int32_t)tpb;
       a.ntiles = bc * cdiv(cdiv(a.nto, tpb), (int64_t)1 << a.tsub_log2) * a.ni * a.nbank;
       p.grid = a.ntiles;
     } else if (bc <= INT32_MAX && a.ni * a.nto <= 65535) {

@@ -5,6 +5,7 @@ means of gamma-distributed data (the tolerance BASELINE.json names)."""
 from __future__ import annotations
 
 import numpy as np
+import torch
 import pytest
 
 from conftest import assert_kurtosis, same_bits
@@ -156,8 +157,11 @@ def test_reduce_row_integer_exact(eng, orc, shape):
 # the last group partial, and windows of <= 128 float4 columns (the 512-channel
 # 0001 product) share a workgroup between 2 or 4 time groups; bit-exact, and
 # the same bits k_reduce_row gives.
+# Launches of fewer than 64 workgroups per CU with 16 rows per lane take 8 rows
+# per lane (TPB = 8 / T); the last two shapes are large enough for 16.
 ROWT_SHAPES = [(1025, 2, 37, 16, 1), (64, 1, 279, 64, 1), (33, 3, 10, 4, 2), (257, 1, 28, 256, 4),
-               (300, 2, 1, 8, 1), (64, 1, 200, 8, 1), (64, 2, 150, 8, 2), (20, 1, 70, 8, 1)]
+               (300, 2, 1, 8, 1), (64, 1, 200, 8, 1), (64, 2, 150, 8, 2), (20, 1, 70, 8, 1),
+               (4096, 2, 2051, 16, 1), (128, 1, 8200, 256, 4)]
 
 
 @pytest.mark.parametrize("shape", ROWT_SHAPES, ids=lambda s: "x".join(map(str, s)))
@@ -169,13 +173,19 @@ def test_reduce_short_time_blocks_integer_exact(eng, orc, shape):
     tpb = 16 // T if nto > 1 else 1
     cols = nco * F // 4  # float4 columns; <= 128 of them: 2 or 4 time groups per workgroup
     tsub = 1 if tpb == 1 else 4 if cols <= 64 else 2 if cols <= 128 else 1
+    blocks_c = -(-cols // 256)
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    if tpb > 1 and blocks_c * ni * -(-(-(-nto // tpb)) // tsub) < 64 * ncu:
+        tpb = 8 // T  # small launch: 8 rows per lane
     for op in ("sum", "max", "min", "mean"):
         plan = eng.plan(x, F, T, op)
         assert plan["path"] == "row", (shape, plan)
-        blocks_c = -(-cols // 256)
         assert plan["workgroups"] == blocks_c * ni * -(-(-(-nto // tpb)) // tsub), (shape, plan)
         got = host(eng, eng.reduce(x, F, T, op))
         assert same_bits(got, orc.reduce(a, F, T, op)), (shape, op)
+    if a.nbytes > 1 << 28:
+        assert tpb * T == 16, (shape, tpb)
+        return  # (the large shapes: the 16-row kernel; windows and bands run above)
     # a time window starting inside the data, and a band of three banks
     if nt > T:
         w = [0, nco * F, 1, 0, ni, 1, 1, (nt - 1) // T * T, 1]
@@ -199,7 +209,7 @@ LANET_SHAPES = [(1000, 1, 37, 3, 1), (21845, 1, 18, 3, 1), (300, 2, 20, 5, 2), (
 
 
 def lanet_rows(F):
-    return 8 if F <= 6 else 4
+    return 8
 
 
 @pytest.mark.parametrize("shape", LANET_SHAPES, ids=lambda s: "x".join(map(str, s)))

@@ -49,7 +49,7 @@ VARIANTS = {
     "lanetoas8": "-DBLDP_LANET_OALIGN=1 -DBLDP_LANET_ROWS_S=8",
     "lanetoap3": "-DBLDP_LANET_OALIGN=1 -DBLDP_LANET_NT3=0",
     "lanetold": "-DBLDP_LANET_OALIGN=0 -DBLDP_LANET_ROWS_S=16",  # the r03f defaults
-    "rowt8": "-DBLDP_ROWT_ROWS=8",  # k_reduce_rowt: 8 rows per lane, twice the workgroups
+    "rowt16": "-DBLDP_ROWT_SMALL=0",  # k_reduce_rowt: always 16 rows per lane (r03h default)
     "kmidnr16": {"rev": "7474fea", "extra": ""},  # k_kurt_mid2 registers in steps of 16 spectra
     "kmid2w16": "-DBLDP_KURT_MID_NW=16",  # k_kurt_mid2 with 16 waves (<= 24 spectra each)
     # TIMING-ONLY patch variants (wrong numerics, never in the product sources):
@@ -318,6 +318,20 @@ def run(names, rounds, iters, suite="main"):
         band_case("0002 F512 T1", b2, 512, 1)
         band_case("0002 F4096 T1", b2, 4096, 1)
         cases_done = True
+    elif suite == "rowt":  # k_reduce_rowt (F = 4..256 with T = 1, 2, 4) on every product
+        band_case("0000 F64 T1", b3, 64, 1)
+        band_case("0000 F16 T2", b3, 16, 2)
+        del b3
+        b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
+        for F, T in ((4, 1), (16, 1), (64, 1), (256, 1), (64, 2), (64, 4), (256, 4), (16, 2)):
+            band_case(f"0002 band F{F} T{T}", b2, F, T, [0, 65536, 1, 0, 1, 1, 0, 279 // T * T, 1])
+        for F, T in ((64, 1), (64, 2), (64, 4), (16, 1), (256, 1)):
+            band_case(f"0002 file F{F} T{T}", b2[:1], F, T, [0, 65536, 1, 0, 1, 1, 0, 279 // T * T, 1])
+        del b2
+        b4 = [eng.synth(512, 1, 880000, 8, seed=10 * b + 1, kind=0) for b in range(8)]
+        for F, T in ((8, 1), (64, 1), (16, 2), (64, 4)):
+            band_case(f"0001 band F{F} T{T}", b4, F, T, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
+        cases_done = True
     elif suite == "row":  # the 0002-product reduce (k_reduce_row)
         del b3
         b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
@@ -436,7 +450,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--suite", default="main", choices=["main", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v"])
+    ap.add_argument("--suite", default="main", choices=["main", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:
