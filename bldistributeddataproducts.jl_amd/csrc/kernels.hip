@@ -165,6 +165,15 @@ __device__ __forceinline__ void st1(float *p, float v) {
 #define BLDP_NACC 8
 #endif
 constexpr int kNacc = BLDP_NACC;
+//   BLDP_TAIL_BATCH  1 (default) = the rows of a block left after the last full
+//                  batch (all of them when T is below the batch size: tavby = 3,
+//                  8, 9, ...) are loaded together and then chained into the first
+//                  accumulator in row order -- the same sums as one row at a
+//                  time, with up to batch - 1 loads in flight per lane instead of
+//                  one; 0 = one row at a time
+#ifndef BLDP_TAIL_BATCH
+#define BLDP_TAIL_BATCH 1
+#endif
 
 // Pairwise fold of the per-lane accumulators into acc[0].
 template <int OP>
@@ -182,6 +191,21 @@ __device__ __forceinline__ float4 ld4(const float *p) {
   const f4u v = *reinterpret_cast<const f4u *>(p);
 #endif
   return make_float4(v.x, v.y, v.z, v.w);
+}
+template <int OP, int N>
+__device__ __forceinline__ float4 tail_rows(float4 acc, const float *p, int64_t st, int64_t nrows) {
+#if BLDP_TAIL_BATCH
+  float4 v[N - 1];
+#pragma unroll
+  for (int u = 0; u < N - 1; ++u)
+    if (u < nrows) v[u] = ld4(p + u * st);
+#pragma unroll
+  for (int u = 0; u < N - 1; ++u)
+    if (u < nrows) acc = f4<OP>(acc, v[u]);
+#else
+  for (; nrows > 0; --nrows, p += st) acc = f4<OP>(acc, ld4(p));
+#endif
+  return acc;
 }
 
 // blockIdx.x -> (bc, i, chunk, to, bank); bc fastest so that consecutive
@@ -256,6 +280,23 @@ __device__ __forceinline__ void vec_tile(const RedArgs &a, int64_t tile) {
 #pragma unroll
         for (int q = 0; q < NV; ++q) acc[q % kNacc] = f4<OP>(acc[q % kNacc], v[q]);
       }
+#if BLDP_TAIL_BATCH
+      if constexpr (RB > 1) {  // the last rows (< RB) together, summed in row order
+        float4 v[NV];
+#pragma unroll
+        for (int u = 0; u < RB - 1; ++u)
+          if (u < nrows)
+#pragma unroll
+            for (int k = 0; k < K4C; ++k) v[u * K4C + k] = ld4(p + u * rstep + 4 * k * LPG);
+#pragma unroll
+        for (int u = 0; u < RB - 1; ++u)
+          if (u < nrows)
+#pragma unroll
+            for (int k = 0; k < K4C; ++k)
+              acc[k % kNacc] = f4<OP>(acc[k % kNacc], v[u * K4C + k]);
+        nrows = 0;
+      }
+#endif
       for (; nrows > 0; --nrows) {
 #pragma unroll
         for (int k = 0; k < K4C; ++k) acc[k % kNacc] = f4<OP>(acc[k % kNacc], ld4(p + 4 * k * LPG));
@@ -326,10 +367,7 @@ __device__ __forceinline__ void narrow_tile(const RedArgs &a, int64_t tile) {
 #pragma unroll
     for (int u = 0; u < BLDP_BATCH; ++u) acc[u % kNacc] = f4<OP>(acc[u % kNacc], v[u]);
   }
-  for (; nrows > 0; --nrows) {
-    acc[0] = f4<OP>(acc[0], ld4(p));
-    p += st;
-  }
+  acc[0] = tail_rows<OP, BLDP_BATCH>(acc[0], p, st, nrows);
   float4 r = fold_acc<OP>(acc);
   const int64_t co = q4 * (4 / F);
   if (a.nchunk == 1) {
@@ -472,11 +510,8 @@ __device__ __forceinline__ void narrow_mis_tile(const RedArgs &a, int64_t tile) 
 #pragma unroll
       for (int u = 0; u < BLDP_BATCH; ++u) acc[u % kNacc] = f4<OP>(acc[u % kNacc], v[u]);
     }
-    for (; nrows > 0; --nrows) {
-      acc[0] = f4<OP>(acc[0], ld4(p));
-      if (extra) ax = f4<OP>(ax, ld4(p + 4));
-      p += st;
-    }
+    acc[0] = tail_rows<OP, BLDP_BATCH>(acc[0], p, st, nrows);
+    if (extra) ax = tail_rows<OP, BLDP_BATCH>(ax, p + 4, st, nrows);
   }
   const float4 lo = fold_acc<OP>(acc);
   float4 hi = make_float4(__shfl_down(lo.x, 1, 64), __shfl_down(lo.y, 1, 64),
@@ -1095,10 +1130,7 @@ void k_reduce_row(const RedArgs a) {
 #pragma unroll
       for (int u = 0; u < BLDP_ROW_BATCH; ++u) acc[u % kNacc] = f4<OP>(acc[u % kNacc], v[u]);
     }
-    for (; nrows > 0; --nrows) {
-      acc[0] = f4<OP>(acc[0], ld4(p));
-      p += ld;
-    }
+    acc[0] = tail_rows<OP, BLDP_ROW_BATCH>(acc[0], p, ld, nrows);
   }
   const float s = lanes_fold<OP, G4>(fold4<OP>(fold_acc<OP>(acc)));
   if (valid && (tid & (G4 - 1)) == 0)

@@ -1028,3 +1028,29 @@ def test_unaligned_vector_special_values(eng, orc):
                 assert np.array_equal(got[fin], want[fin])
             else:
                 assert same_bits(got, want), (F, T, op)
+
+
+# Time blocks that are not a multiple of a kernel's row batch (tavby = 3, 8, 9,
+# 15, 17, 24): the rows after the last full batch are loaded together and then
+# chained in row order (BLDP_TAIL_BATCH); row, narrow, misaligned narrow and
+# vector plans, bit-exact on integer data, with a partial window.
+TAIL_CASES = [(64, None, ("row",)), (2, None, ("narrow",)), (1, None, ("narrow",)),
+              (8, None, ("vector", "row")), (1, [1, 4094, 1, 0, 1, 1, 0, None, 1], ("narrow_mis",))]
+
+
+@pytest.mark.parametrize("T", [3, 8, 9, 15, 17, 24])
+@pytest.mark.parametrize("case", TAIL_CASES, ids=lambda c: f"F{c[0]}-{c[2][0]}")
+def test_reduce_block_tails_integer_exact(eng, orc, case, T):
+    F, w, path = case
+    nt = 3 * T + 5  # three blocks and a few spectra over
+    x = eng.synth(4096, 1, nt, 1024, seed=97 * F + T, kind=1)
+    a = host(eng, x)
+    win = None
+    if w is not None:
+        win = list(w)
+        win[7] = nt // T * T
+    for op in ("sum", "max", "min"):
+        plan = eng.plan(x, F, T, op, win)
+        assert plan["path"] in path, (F, T, plan)
+        got = host(eng, eng.reduce(x, F, T, op, win))
+        assert same_bits(got, orc.reduce(a, F, T, op, win)), (F, T, op, path)

@@ -49,6 +49,7 @@ VARIANTS = {
     "lanetoas8": "-DBLDP_LANET_OALIGN=1 -DBLDP_LANET_ROWS_S=8",
     "lanetoap3": "-DBLDP_LANET_OALIGN=1 -DBLDP_LANET_NT3=0",
     "lanetold": "-DBLDP_LANET_OALIGN=0 -DBLDP_LANET_ROWS_S=16",  # the r03f defaults
+    "tail1": "-DBLDP_TAIL_BATCH=0",  # the rows after the last full batch one at a time
     "rowt16": "-DBLDP_ROWT_SMALL=0",  # k_reduce_rowt: always 16 rows per lane (r03h default)
     "kmidnr16": {"rev": "7474fea", "extra": ""},  # k_kurt_mid2 registers in steps of 16 spectra
     "kmid2w16": "-DBLDP_KURT_MID_NW=16",  # k_kurt_mid2 with 16 waves (<= 24 spectra each)
@@ -342,6 +343,13 @@ def run(names, rounds, iters, suite="main"):
         band_case("cfg2 F64 T1 whole", b2, 64, 1)
         band_case("cfg1 F64 T1 whole", b2[:1], 64, 1)
         band_case("cfg2 F4 T1 whole", b2, 4, 1)
+        band_case("cfg2 F64 T8", b2, 64, 8, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
+        band_case("cfg2 F64 T3 whole", b2, 64, 3)
+        band_case("cfg2 F16 T24", b2, 16, 24, [0, 65536, 1, 0, 1, 1, 0, 264, 1])
+        band_case("cfg1 F64 T8", b2[:1], 64, 8, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
+        band_case("cfg2 F2 T8", b2, 2, 8, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
+        band_case("cfg2 F1 T3 whole", b2, 1, 3)
+        band_case("cfg2 F8 T9 whole", b2, 8, 9)
         band_case("cfg2 F256 T2", b2, 256, 2, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
         band_case("cfg2 F64 T4", b2, 64, 4, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
         cases_done = True
