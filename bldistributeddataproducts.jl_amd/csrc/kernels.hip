@@ -194,14 +194,43 @@ __device__ __forceinline__ float4 ld4(const float *p) {
 }
 template <int OP, int N>
 __device__ __forceinline__ float4 tail_rows(float4 acc, const float *p, int64_t st, int64_t nrows) {
+  static_assert(N <= 16, "tail_rows: at most 15 rows");
 #if BLDP_TAIL_BATCH
-  float4 v[N - 1];
+  // nrows (< N, wave-uniform) as 8 + 4 + 2 + 1 rows: every load issued before
+  // the first add, no predicated array elements
+  float4 v8[8], v4[4], v2[2], v1;
+  const bool b8 = N > 8 && (nrows & 8), b4 = N > 4 && (nrows & 4), b2 = N > 2 && (nrows & 2),
+             b1 = nrows & 1;
+  const float *q = p;
+  if (b8) {
 #pragma unroll
-  for (int u = 0; u < N - 1; ++u)
-    if (u < nrows) v[u] = ld4(p + u * st);
+    for (int u = 0; u < 8; ++u) v8[u] = ld4(q + u * st);
+    q += 8 * st;
+  }
+  if (b4) {
 #pragma unroll
-  for (int u = 0; u < N - 1; ++u)
-    if (u < nrows) acc = f4<OP>(acc, v[u]);
+    for (int u = 0; u < 4; ++u) v4[u] = ld4(q + u * st);
+    q += 4 * st;
+  }
+  if (b2) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) v2[u] = ld4(q + u * st);
+    q += 2 * st;
+  }
+  if (b1) v1 = ld4(q);
+  if (b8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc = f4<OP>(acc, v8[u]);
+  }
+  if (b4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc = f4<OP>(acc, v4[u]);
+  }
+  if (b2) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) acc = f4<OP>(acc, v2[u]);
+  }
+  if (b1) acc = f4<OP>(acc, v1);
 #else
   for (; nrows > 0; --nrows, p += st) acc = f4<OP>(acc, ld4(p));
 #endif
@@ -280,23 +309,14 @@ __device__ __forceinline__ void vec_tile(const RedArgs &a, int64_t tile) {
 #pragma unroll
         for (int q = 0; q < NV; ++q) acc[q % kNacc] = f4<OP>(acc[q % kNacc], v[q]);
       }
-#if BLDP_TAIL_BATCH
-      if constexpr (RB > 1) {  // the last rows (< RB) together, summed in row order
-        float4 v[NV];
+      if constexpr (RB > 1 && K4C <= kNacc) {
+        // the last rows (< RB) together; column k's rows go to accumulator k
+        // alone, in row order, as in the loop below
 #pragma unroll
-        for (int u = 0; u < RB - 1; ++u)
-          if (u < nrows)
-#pragma unroll
-            for (int k = 0; k < K4C; ++k) v[u * K4C + k] = ld4(p + u * rstep + 4 * k * LPG);
-#pragma unroll
-        for (int u = 0; u < RB - 1; ++u)
-          if (u < nrows)
-#pragma unroll
-            for (int k = 0; k < K4C; ++k)
-              acc[k % kNacc] = f4<OP>(acc[k % kNacc], v[u * K4C + k]);
+        for (int k = 0; k < K4C; ++k)
+          acc[k] = tail_rows<OP, RB>(acc[k], p + 4 * k * LPG, rstep, nrows);
         nrows = 0;
       }
-#endif
       for (; nrows > 0; --nrows) {
 #pragma unroll
         for (int k = 0; k < K4C; ++k) acc[k % kNacc] = f4<OP>(acc[k % kNacc], ld4(p + 4 * k * LPG));

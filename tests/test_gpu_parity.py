@@ -1034,7 +1034,7 @@ def test_unaligned_vector_special_values(eng, orc):
 # 15, 17, 24): the rows after the last full batch are loaded together and then
 # chained in row order (BLDP_TAIL_BATCH); row, narrow, misaligned narrow and
 # vector plans, bit-exact on integer data, with a partial window.
-TAIL_CASES = [(64, None, ("row",)), (2, None, ("narrow",)), (1, None, ("narrow",)),
+TAIL_CASES = [(64, None, ("row", "vector")), (2, None, ("narrow",)), (1, None, ("narrow",)),
               (8, None, ("vector", "row")), (1, [1, 4094, 1, 0, 1, 1, 0, None, 1], ("narrow_mis",))]
 
 
@@ -1045,10 +1045,8 @@ def test_reduce_block_tails_integer_exact(eng, orc, case, T):
     nt = 3 * T + 5  # three blocks and a few spectra over
     x = eng.synth(4096, 1, nt, 1024, seed=97 * F + T, kind=1)
     a = host(eng, x)
-    win = None
-    if w is not None:
-        win = list(w)
-        win[7] = nt // T * T
+    win = list(w) if w is not None else [0, 4096, 1, 0, 1, 1, 0, None, 1]
+    win[7] = nt // T * T
     for op in ("sum", "max", "min"):
         plan = eng.plan(x, F, T, op, win)
         assert plan["path"] in path, (F, T, plan)
