@@ -192,7 +192,24 @@ __device__ __forceinline__ float4 ld4(const float *p) {
 #endif
   return make_float4(v.x, v.y, v.z, v.w);
 }
-template <int OP, int N>
+//   BLDP_VEC_K3  groups of 3 float4 per lane on the vector path (fqavby = 12,
+//               24, 48, ..., 768): 0 = the generic K4 loop (one load at a time), 1 = a
+//               compiled K4 = 3 form with nt loads, 2 (default) = the same with
+//               plain loads (an nt load covers a third of each line at the
+//               48-byte lane pitch; the next instruction re-reads it from HBM)
+#ifndef BLDP_VEC_K3
+#define BLDP_VEC_K3 2
+#endif
+template <bool PLAIN>
+__device__ __forceinline__ float4 ld4x(const float *p) {
+  if constexpr (PLAIN) {
+    const f4u v = *reinterpret_cast<const f4u *>(p);
+    return make_float4(v.x, v.y, v.z, v.w);
+  } else {
+    return ld4(p);
+  }
+}
+template <int OP, int N, bool PLAIN = false>
 __device__ __forceinline__ float4 tail_rows(float4 acc, const float *p, int64_t st, int64_t nrows) {
   static_assert(N <= 16, "tail_rows: at most 15 rows");
 #if BLDP_TAIL_BATCH
@@ -204,20 +221,20 @@ __device__ __forceinline__ float4 tail_rows(float4 acc, const float *p, int64_t 
   const float *q = p;
   if (b8) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v8[u] = ld4(q + u * st);
+    for (int u = 0; u < 8; ++u) v8[u] = ld4x<PLAIN>(q + u * st);
     q += 8 * st;
   }
   if (b4) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v4[u] = ld4(q + u * st);
+    for (int u = 0; u < 4; ++u) v4[u] = ld4x<PLAIN>(q + u * st);
     q += 4 * st;
   }
   if (b2) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) v2[u] = ld4(q + u * st);
+    for (int u = 0; u < 2; ++u) v2[u] = ld4x<PLAIN>(q + u * st);
     q += 2 * st;
   }
-  if (b1) v1 = ld4(q);
+  if (b1) v1 = ld4x<PLAIN>(q);
   if (b8) {
 #pragma unroll
     for (int u = 0; u < 8; ++u) acc = f4<OP>(acc, v8[u]);
@@ -232,7 +249,7 @@ __device__ __forceinline__ float4 tail_rows(float4 acc, const float *p, int64_t 
   }
   if (b1) acc = f4<OP>(acc, v1);
 #else
-  for (; nrows > 0; --nrows, p += st) acc = f4<OP>(acc, ld4(p));
+  for (; nrows > 0; --nrows, p += st) acc = f4<OP>(acc, ld4x<PLAIN>(p));
 #endif
   return acc;
 }
@@ -299,12 +316,13 @@ __device__ __forceinline__ void vec_tile(const RedArgs &a, int64_t tile) {
     if constexpr (K4C > 0) {
       constexpr int RB = (K4C >= BLDP_BATCH) ? 1 : BLDP_BATCH / K4C;
       constexpr int NV = RB * K4C;
+      constexpr bool PL = K4C == 3 && BLDP_VEC_K3 == 2;
       for (; nrows >= RB; nrows -= RB) {
         float4 v[NV];
 #pragma unroll
         for (int u = 0; u < RB; ++u)
 #pragma unroll
-          for (int k = 0; k < K4C; ++k) v[u * K4C + k] = ld4(p + u * rstep + 4 * k * LPG);
+          for (int k = 0; k < K4C; ++k) v[u * K4C + k] = ld4x<PL>(p + u * rstep + 4 * k * LPG);
         p += RB * rstep;
 #pragma unroll
         for (int q = 0; q < NV; ++q) acc[q % kNacc] = f4<OP>(acc[q % kNacc], v[q]);
@@ -314,12 +332,13 @@ __device__ __forceinline__ void vec_tile(const RedArgs &a, int64_t tile) {
         // alone, in row order, as in the loop below
 #pragma unroll
         for (int k = 0; k < K4C; ++k)
-          acc[k] = tail_rows<OP, RB>(acc[k], p + 4 * k * LPG, rstep, nrows);
+          acc[k] = tail_rows<OP, RB, PL>(acc[k], p + 4 * k * LPG, rstep, nrows);
         nrows = 0;
       }
       for (; nrows > 0; --nrows) {
 #pragma unroll
-        for (int k = 0; k < K4C; ++k) acc[k % kNacc] = f4<OP>(acc[k % kNacc], ld4(p + 4 * k * LPG));
+        for (int k = 0; k < K4C; ++k)
+          acc[k % kNacc] = f4<OP>(acc[k % kNacc], ld4x<PL>(p + 4 * k * LPG));
         p += rstep;
       }
     } else {
@@ -1548,7 +1567,7 @@ int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 template <int OP>
 hipError_t launch_vec(const RedArgs &a, const Plan &p, hipStream_t s) {
   const dim3 grid((unsigned)p.grid), block(kBlock);
-  const int k4c = (a.k4 == 1 || a.k4 == 2 || a.k4 == 4) ? a.k4 : 0;
+  const int k4c = (a.k4 == 1 || a.k4 == 2 || a.k4 == 4 || (BLDP_VEC_K3 && a.k4 == 3)) ? a.k4 : 0;
 #define BLDP_VEC(L, K)                                                 \
   if (p.lpg == L && k4c == K) {                                        \
     hipLaunchKernelGGL((k_reduce_vec<OP, L, K>), grid, block, 0, s, a); \
@@ -1558,6 +1577,10 @@ hipError_t launch_vec(const RedArgs &a, const Plan &p, hipStream_t s) {
   BLDP_VEC(32, 1) BLDP_VEC(32, 0) BLDP_VEC(16, 1) BLDP_VEC(16, 0)
   BLDP_VEC(8, 1) BLDP_VEC(8, 0) BLDP_VEC(4, 1) BLDP_VEC(4, 0)
   BLDP_VEC(2, 1) BLDP_VEC(2, 0) BLDP_VEC(1, 1) BLDP_VEC(1, 0)
+#if BLDP_VEC_K3
+  BLDP_VEC(1, 3) BLDP_VEC(2, 3) BLDP_VEC(4, 3) BLDP_VEC(8, 3) BLDP_VEC(16, 3) BLDP_VEC(32, 3)
+  BLDP_VEC(64, 3)
+#endif
 #undef BLDP_VEC
   return hipErrorInvalidValue;
 }

@@ -1035,7 +1035,9 @@ def test_unaligned_vector_special_values(eng, orc):
 # chained in row order (BLDP_TAIL_BATCH); row, narrow, misaligned narrow and
 # vector plans, bit-exact on integer data, with a partial window.
 TAIL_CASES = [(64, None, ("row", "vector")), (2, None, ("narrow",)), (1, None, ("narrow",)),
-              (8, None, ("vector", "row")), (1, [1, 4094, 1, 0, 1, 1, 0, None, 1], ("narrow_mis",))]
+              (8, None, ("vector", "row")), (1, [1, 4094, 1, 0, 1, 1, 0, None, 1], ("narrow_mis",)),
+              (12, None, ("vector",)), (24, None, ("vector",)), (48, None, ("vector",)),
+              (96, None, ("vector",)), (768, None, ("vector", "interleaved"))]
 
 
 @pytest.mark.parametrize("T", [3, 8, 9, 15, 17, 24])
@@ -1045,7 +1047,7 @@ def test_reduce_block_tails_integer_exact(eng, orc, case, T):
     nt = 3 * T + 5  # three blocks and a few spectra over
     x = eng.synth(4096, 1, nt, 1024, seed=97 * F + T, kind=1)
     a = host(eng, x)
-    win = list(w) if w is not None else [0, 4096, 1, 0, 1, 1, 0, None, 1]
+    win = list(w) if w is not None else [0, 4096 // F * F, 1, 0, 1, 1, 0, None, 1]
     win[7] = nt // T * T
     for op in ("sum", "max", "min"):
         plan = eng.plan(x, F, T, op, win)

@@ -49,6 +49,8 @@ VARIANTS = {
     "lanetoas8": "-DBLDP_LANET_OALIGN=1 -DBLDP_LANET_ROWS_S=8",
     "lanetoap3": "-DBLDP_LANET_OALIGN=1 -DBLDP_LANET_NT3=0",
     "lanetold": "-DBLDP_LANET_OALIGN=0 -DBLDP_LANET_ROWS_S=16",  # the r03f defaults
+    "veck3off": "-DBLDP_VEC_K3=0",  # fqavby = 12 / 24: the generic K4 loop
+    "veck3nt": "-DBLDP_VEC_K3=1",  # the K4 = 3 form with nt loads
     "tail1": "-DBLDP_TAIL_BATCH=0",  # the rows after the last full batch one at a time
     "rowt16": "-DBLDP_ROWT_SMALL=0",  # k_reduce_rowt: always 16 rows per lane (r03h default)
     "kmidnr16": {"rev": "7474fea", "extra": ""},  # k_kurt_mid2 registers in steps of 16 spectra
@@ -333,6 +335,23 @@ def run(names, rounds, iters, suite="main"):
         for F, T in ((8, 1), (64, 1), (16, 2), (64, 4)):
             band_case(f"0001 band F{F} T{T}", b4, F, T, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
         cases_done = True
+    elif suite == "grid":  # fqavby x tavby over the 0002 band: every plan, looking for outliers
+        del b3
+        b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
+        for F in (1, 2, 3, 4, 5, 6, 7, 8, 12, 16, 32, 64, 128, 256, 512, 1024, 4096, 65536):
+            for T in (1, 2, 3, 4, 8, 9, 16, 31):
+                w = [0, 65536 // F * F, 1, 0, 1, 1, 0, 279 // T * T, 1]
+                band_case(f"0002 F{F} T{T} {eng.plan(b2[0], F, T, 'sum', w)['path']}", b2, F, T, w)
+        cases_done = True
+    elif suite == "k3":  # 3 float4 per lane on the vector path (fqavby = 12, 24)
+        band_case("0000 F12 T16", b3, 12, 16, [0, (1 << 26) // 12 * 12, 1, 0, 1, 1, 0, 16, 1])
+        del b3
+        b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
+        for F, T in ((12, 3), (12, 8), (12, 9), (12, 16), (12, 31), (24, 8), (24, 16), (24, 3)):
+            w = [0, 65536 // F * F, 1, 0, 1, 1, 0, 279 // T * T, 1]
+            band_case(f"0002 F{F} T{T}", b2, F, T, w)
+        band_case("0002 file F12 T16", b2[:1], 12, 16, [0, 65532, 1, 0, 1, 1, 0, 272, 1])
+        cases_done = True
     elif suite == "row":  # the 0002-product reduce (k_reduce_row)
         del b3
         b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
@@ -458,7 +477,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--suite", default="main", choices=["main", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt"])
+    ap.add_argument("--suite", default="main", choices=["main", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:
