@@ -442,9 +442,11 @@ __device__ __forceinline__ void narrow_tile(const RedArgs &a, int64_t tile) {
 // k_reduce_rowt: 16 / T time blocks per workgroup, 2 or 4 time groups per
 // workgroup for windows of <= 128 float4 columns.  Each block is summed and
 // stored exactly as narrow_tile does it (bit-identical).
-//   BLDP_NARROW_TPB  1 (default) = use it for T in {1, 2, 4}; 0 = k_reduce_narrow
+//   BLDP_NARROW_TPB  2 (default) = use it for T in {1, 2, 4}, the copy
+//                  (fqavby = tavby = 1) included; 1 = not for the copy;
+//                  0 = k_reduce_narrow
 #ifndef BLDP_NARROW_TPB
-#define BLDP_NARROW_TPB 1
+#define BLDP_NARROW_TPB 2
 #endif
 template <int OP, int F, int T>
 __global__ __launch_bounds__(kBlock)
@@ -1593,7 +1595,8 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
     const dim3 g3((unsigned)(a.blocks_c * cdiv(cdiv(a.nto, a.tpb), 1 << a.tsub_log2)),
                   (unsigned)a.ni, (unsigned)a.nbank);
 #define BLDP_NARROWT(FF, TT) hipLaunchKernelGGL((k_reduce_narrowt<OP, FF, TT>), g3, block, 0, s, a);
-    if (a.F == 1 && a.T == 2) { BLDP_NARROWT(1, 2) }
+    if (a.F == 1 && a.T == 1) { BLDP_NARROWT(1, 1) }
+    else if (a.F == 1 && a.T == 2) { BLDP_NARROWT(1, 2) }
     else if (a.F == 1 && a.T == 4) { BLDP_NARROWT(1, 4) }
     else if (a.F == 2 && a.T == 1) { BLDP_NARROWT(2, 1) }
     else if (a.F == 2 && a.T == 2) { BLDP_NARROWT(2, 2) }
@@ -1901,7 +1904,7 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
   }
   // narrow path, short time blocks: k_reduce_narrowt (grid as k_reduce_rowt's)
   if (BLDP_NARROW_TPB && p.path == PATH_NARROW && a.nchunk == 1 && (T == 1 || T == 2 || T == 4) &&
-      !(F == 1 && T == 1) && a.nto > 1 && a.ni <= 65535 && a.nbank <= 65535) {
+      (BLDP_NARROW_TPB >= 1 + (F == 1 && T == 1)) && a.nto > 1 && a.ni <= 65535 && a.nbank <= 65535) {
     const int64_t cols = a.nco * F / 4, tpb = 16 / T;
     const int sh = cols <= 64 ? 2 : cols <= 128 ? 1 : 0;
     const int64_t x = a.blocks_c * cdiv(cdiv(a.nto, tpb), (int64_t)1 << sh);

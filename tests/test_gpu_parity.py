@@ -285,7 +285,7 @@ def test_reduce_large_groups_short_time_blocks_integer_exact(eng, orc, shape):
 # 16 / T time blocks per workgroup (2 or 4 time groups per workgroup on
 # windows of <= 128 float4 columns); bit-exact, the same bits as k_reduce_narrow.
 NARROWT_SHAPES = [(512, 1, 300, 2, 1), (128, 2, 50, 2, 2), (2048, 1, 32, 1, 4), (256, 3, 20, 1, 2),
-                  (6000, 1, 17, 2, 1)]
+                  (6000, 1, 17, 2, 1), (4096, 1, 37, 1, 1), (100, 2, 9, 1, 1)]  # (F = T = 1: the copy)
 
 
 @pytest.mark.parametrize("shape", NARROWT_SHAPES, ids=lambda s: "x".join(map(str, s)))
