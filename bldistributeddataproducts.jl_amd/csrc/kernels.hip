@@ -192,6 +192,12 @@ __device__ __forceinline__ float4 ld4(const float *p) {
 #endif
   return make_float4(v.x, v.y, v.z, v.w);
 }
+//   BLDP_WIDE_SPLIT  1 (default) = groups wider than 4096 channels split their
+//               time rows over waves (ts) and workgroups (time chunks) by the
+//               work in a row, not only by the row count; 0 = by rows only
+#ifndef BLDP_WIDE_SPLIT
+#define BLDP_WIDE_SPLIT 1
+#endif
 //   BLDP_VEC_K3  groups of 3 float4 per lane on the vector path (fqavby = 12,
 //               24, 48, ..., 768): 0 = the generic K4 loop (one load at a time), 1 = a
 //               compiled K4 = 3 form with nt loads, 2 (default) = the same with
@@ -1797,7 +1803,11 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
     a.k4 = (int32_t)(g4 / lpg);
     const int64_t ctiles = cdiv(a.nco, 64 / lpg);
     tiles = ctiles * a.ni * a.nto * a.nbank;
-    while (a.ts < 4 && tiles * a.ts < target_waves && T >= 2 * a.ts * 8) a.ts *= 2;
+    // rows a time-split wave needs at least: groups wider than the interleaved
+    // kernel's (G4 > 1024: one wave reads K4 > 16 float4 per lane per row) have
+    // enough work in one row (fqavby = 65536 at tavby = 8 was 272 waves)
+    const int64_t tsrows = (BLDP_WIDE_SPLIT && a.k4 > 16) ? 1 : 8;
+    while (a.ts < 4 && tiles * a.ts < target_waves && T >= 2 * a.ts * tsrows) a.ts *= 2;
     // no idle waves: a workgroup holds 4/ts column tiles, so narrow windows
     // (fewer than 4 column tiles, e.g. the 512-channel 0001 product) split
     // their time rows over the spare waves instead
@@ -1834,9 +1844,13 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
   }
   // Long time blocks with too few tiles: split the T rows across workgroups.
   const int64_t rows_per_wave = cdiv(T, a.ts);
+  // float4 per lane in a wave's rows (wide groups: K4 of them per row)
+  const int64_t wave_work =
+      rows_per_wave * ((BLDP_WIDE_SPLIT && p.path == PATH_VEC && a.k4 > 16) ? a.k4 : 1);
   int64_t nchunk = 1;
-  if (tiles > 0 && tiles < target_waves && rows_per_wave >= 128) {  // (empty windows: no split)
-    nchunk = std::min<int64_t>(cdiv(target_waves, tiles), rows_per_wave / 64);
+  if (tiles > 0 && tiles < target_waves && wave_work >= 128) {  // (empty windows: no split)
+    nchunk = std::min<int64_t>(cdiv(target_waves, tiles), wave_work / 64);
+    nchunk = std::min<int64_t>(nchunk, rows_per_wave);
     nchunk = std::max<int64_t>(nchunk, 1);
   }
   a.rows_per_chunk = cdiv(T, nchunk);

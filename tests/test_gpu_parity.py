@@ -1054,3 +1054,26 @@ def test_reduce_block_tails_integer_exact(eng, orc, case, T):
         assert plan["path"] in path, (F, T, plan)
         got = host(eng, eng.reduce(x, F, T, op, win))
         assert same_bits(got, orc.reduce(a, F, T, op, win)), (F, T, op, path)
+
+
+# Groups wider than 4096 channels (fqavby = 16384, 65536: K4 > 16 float4 per
+# lane per row) with few outputs split their rows over waves and time chunks by
+# the work in a row (BLDP_WIDE_SPLIT); max / min bit-exact, sums within 1e-5.
+@pytest.mark.parametrize("F", [16384, 65536])
+@pytest.mark.parametrize("T", [3, 8, 9, 31])
+def test_reduce_wide_groups_time_split(eng, orc, F, T):
+    nt = 279 // T * T
+    x = eng.synth(65536, 1, 279, 1024, seed=F + T, kind=1)
+    a = host(eng, x)
+    w = [0, 65536, 1, 0, 1, 1, 0, nt, 1]
+    plan = eng.plan(x, F, T, "sum", w)
+    assert plan["path"] == "vector", plan
+    for op in ("max", "min"):
+        got = host(eng, eng.reduce(x, F, T, op, w))
+        assert same_bits(got, orc.reduce(a, F, T, op, w)), (F, T, op, plan)
+    # (sums of F x T bytes pass 2^24: Float32 rounds them, so the 1e-5 bound)
+    got = host(eng, eng.reduce(x, F, T, "sum", w))
+    np.testing.assert_allclose(got, orc.reduce(a, F, T, "sum", w), rtol=RTOL)
+    g = orc.gamma_bandpass(65536, 1, nt, 1024, 3 * T)
+    got = host(eng, eng.reduce(dev(eng, g), F, T, "mean"))
+    np.testing.assert_allclose(got, orc.reduce(g, F, T, "mean"), rtol=RTOL)

@@ -49,6 +49,7 @@ VARIANTS = {
     "lanetoas8": "-DBLDP_LANET_OALIGN=1 -DBLDP_LANET_ROWS_S=8",
     "lanetoap3": "-DBLDP_LANET_OALIGN=1 -DBLDP_LANET_NT3=0",
     "lanetold": "-DBLDP_LANET_OALIGN=0 -DBLDP_LANET_ROWS_S=16",  # the r03f defaults
+    "nowide": "-DBLDP_WIDE_SPLIT=0",  # fqavby > 4096: time split by row count only
     "nocopyt": "-DBLDP_NARROW_TPB=1",  # fqavby = tavby = 1 on k_reduce_narrow (one row per WG)
     "veck3off": "-DBLDP_VEC_K3=0",  # fqavby = 12 / 24: the generic K4 loop
     "veck3nt": "-DBLDP_VEC_K3=1",  # the K4 = 3 form with nt loads
@@ -353,6 +354,14 @@ def run(names, rounds, iters, suite="main"):
             band_case(f"0002 F{F} T{T}", b2, F, T, w)
         band_case("0002 file F12 T16", b2[:1], 12, 16, [0, 65532, 1, 0, 1, 1, 0, 272, 1])
         cases_done = True
+    elif suite == "wide":  # groups wider than 4096 channels with few outputs
+        del b3
+        b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
+        for F, T in ((65536, 1), (65536, 8), (65536, 9), (65536, 31), (16384, 8), (16384, 31),
+                     (8192, 16), (65536, 279)):
+            band_case(f"0002 band F{F} T{T}", b2, F, T, [0, 65536, 1, 0, 1, 1, 0, 279 // T * T, 1])
+        band_case("0002 file F65536 T16", b2[:1], 65536, 16, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
+        cases_done = True
     elif suite == "copy":  # fqavby = tavby = 1 (the window itself)
         band_case("0000 F1 T1 (one bank)", b3[:1], 1, 1)
         del b3
@@ -487,7 +496,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--suite", default="main", choices=["main", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy"])
+    ap.add_argument("--suite", default="main", choices=["main", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy", "wide"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:
