@@ -165,6 +165,18 @@ __device__ __forceinline__ void st1(float *p, float v) {
 #define BLDP_NACC 8
 #endif
 constexpr int kNacc = BLDP_NACC;
+//   BLDP_T38  1 (default) = the short-time-block kernels (k_reduce_rowt,
+//             k_reduce_narrowt, k_reduce_lanet) also take tavby = 3 and 8, not
+//             only 1, 2, 4 (the 512-channel 0001 product at tavby = 3 ran one
+//             3-row block per wave with half the waves idle: 2.4-2.7 TB/s)
+#ifndef BLDP_T38
+#define BLDP_T38 1
+#endif
+#if BLDP_T38
+#define BLDP_T38_CASES(M, X) case 3: M(X, 3) case 8: M(X, 8)
+#else
+#define BLDP_T38_CASES(M, X)
+#endif
 //   BLDP_TAIL_BATCH  1 (default) = the rows of a block left after the last full
 //                  batch (all of them when T is below the batch size: tavby = 3,
 //                  8, 9, ...) are loaded together and then chained into the first
@@ -768,8 +780,8 @@ constexpr int lanet_rows(int F) {
 constexpr int lanet_cs(int F) { return F <= 3 ? BLDP_LANET_CS_S : 1; }
 template <int OP, int F, int T>
 __global__ __launch_bounds__(kBlock) void k_reduce_lanet(const RedArgs a) {
-  constexpr int NRW = lanet_rows(F), TPB = NRW / T, CS = lanet_cs(F);
-  static_assert(NRW % T == 0 && TPB >= 1, "k_reduce_lanet: rows per lane");
+  constexpr int TPB = lanet_rows(F) / T, NRW = TPB * T, CS = lanet_cs(F);  // (T = 3: 6 rows)
+  static_assert(TPB >= 1, "k_reduce_lanet: rows per lane");
   const int tid = threadIdx.x;
   const uint32_t bx = blockIdx.x, bc = (uint32_t)a.blocks_c;
   const uint32_t tq = bx / bc, i = blockIdx.y;
@@ -1282,7 +1294,7 @@ void k_reduce_rowt(const RedArgs a) {
   // 2x-5x the output, profiles/r03/t1_pmc_r03a.json).
   __shared__ float tile[kBlock / G4 * TPB];
   const int j = tid & (G4 - 1);
-  constexpr int NS = TPB > G4 ? TPB / G4 : 1;
+  constexpr int NS = TPB > G4 ? (TPB + G4 - 1) / G4 : 1;  // (TPB = 5 at T = 3)
   constexpr int NSEL = TPB < G4 ? TPB : G4;
   constexpr int LG4 = G4 >= 64 ? 6 : G4 >= 32 ? 5 : G4 >= 16 ? 4 : G4 >= 8 ? 3 : G4 >= 4 ? 2 : G4 >= 2 ? 1 : 0;
   const int lng = 8 - sh - LG4;  // log2 of the groups per row segment (>= 0: cw >= G4)
@@ -1292,7 +1304,8 @@ void k_reduce_rowt(const RedArgs a) {
     const int b = m * G4 + j;
     float val = sv[m * G4];
 #pragma unroll
-    for (int q = 1; q < NSEL; ++q) val = (j == q) ? sv[m * G4 + q] : val;
+    for (int q = 1; q < NSEL; ++q)
+      if (m * G4 + q < TPB) val = (j == q) ? sv[m * G4 + q] : val;
     if (b < TPB) tile[((tgl * TPB + b) << lng) + gl] = finish<OP>(val, a);
   }
   __syncthreads();
@@ -1329,15 +1342,16 @@ void k_reduce_rowt(const RedArgs a) {
   // fewer lanes than blocks), so a store instruction has every lane busy
   // (k_reduce_row's one-lane-per-group store would take TPB instructions).
   const int j = tid & (G4 - 1);
-  constexpr int NS = TPB > G4 ? TPB / G4 : 1;  // store instructions
-  constexpr int NSEL = TPB < G4 ? TPB : G4;    // blocks a lane chooses from
+  constexpr int NS = TPB > G4 ? (TPB + G4 - 1) / G4 : 1;  // store instructions
+  constexpr int NSEL = TPB < G4 ? TPB : G4;                // blocks a lane chooses from
   float *o = a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + col / G4;
 #pragma unroll
   for (int m = 0; m < NS; ++m) {
     const int b = m * G4 + j;
     float val = sv[m * G4];
 #pragma unroll
-    for (int q = 1; q < NSEL; ++q) val = (j == q) ? sv[m * G4 + q] : val;
+    for (int q = 1; q < NSEL; ++q)
+      if (m * G4 + q < TPB) val = (j == q) ? sv[m * G4 + q] : val;
     if (valid && b < nb) st1<1>(o + (to0 + b) * a.out_ld_t, finish<OP>(val, a));
   }
 #endif
@@ -1607,6 +1621,10 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
     else if (a.F == 2 && a.T == 1) { BLDP_NARROWT(2, 1) }
     else if (a.F == 2 && a.T == 2) { BLDP_NARROWT(2, 2) }
     else if (a.F == 2 && a.T == 4) { BLDP_NARROWT(2, 4) }
+#if BLDP_T38
+    else if (a.F == 1 && a.T == 3) { BLDP_NARROWT(1, 3) }
+    else if (a.F == 2 && a.T == 3) { BLDP_NARROWT(2, 3) }
+#endif
     else return hipErrorInvalidValue;
 #undef BLDP_NARROWT
     return hipGetLastError();
@@ -1644,6 +1662,7 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
     case 1: BLDP_LANETL(FF, 1)             \
     case 2: BLDP_LANETL(FF, 2)             \
     case 4: BLDP_LANETL(FF, 4)             \
+    BLDP_T38_CASES(BLDP_LANETL, FF)        \
     default: return hipErrorInvalidValue;  \
   }                                        \
   break;
@@ -1674,19 +1693,22 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
     default: return hipErrorInvalidValue;                                                   \
   }
 #define BLDP_ROWT(T)                 \
-  if (a.tpb * (T) == 8) {            \
+  if (a.tpb == 8 / (T)) {            \
     BLDP_ROWTN(T, 8)                 \
-  } else if (a.tpb * (T) == 16) {    \
+  } else if (a.tpb == 16 / (T)) {    \
     BLDP_ROWTN(T, 16)                \
   } else {                           \
     return hipErrorInvalidValue;     \
   }
+#define BLDP_ROWTC(X, T) BLDP_ROWT(T) break;
     switch (a.T) {
       case 1: BLDP_ROWT(1) break;
       case 2: BLDP_ROWT(2) break;
       case 4: BLDP_ROWT(4) break;
+      BLDP_T38_CASES(BLDP_ROWTC, 0)
       default: return hipErrorInvalidValue;
     }
+#undef BLDP_ROWTC
 #undef BLDP_ROWT
 #undef BLDP_ROWTN
     return hipGetLastError();
@@ -1775,7 +1797,7 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
   a.k4 = 1;
   a.tpb = 1;
   a.tsub_log2 = 0;
-  if (BLDP_LANET && words && a.in_cs == 1 && (T == 1 || T == 2 || T == 4) &&
+  if (BLDP_LANET && words && a.in_cs == 1 && (T == 1 || T == 2 || T == 4 || (BLDP_T38 && (T == 3 || T == 8))) &&
       (F == 3 || F == 5 || F == 6 || F == 7 || F == 12) && a.ni <= 65535 && a.nbank <= 65535 &&
       cdiv(a.nco + lanet_oalign_pad(), (int64_t)kBlock * lanet_cs((int)F)) *
               cdiv(a.nto, lanet_rows((int)F) / T) <=
@@ -1894,7 +1916,7 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
     const int64_t bc = cdiv(a.nco * (F / 4), kBlock);
     // short time blocks: 16 / T of them per workgroup (k_reduce_rowt; grid x =
     // column blocks x time groups, so long 0001-product windows fit too)
-    int64_t tpb = (T == 1 || T == 2 || T == 4) ? 16 / T : 1;
+    int64_t tpb = (T == 1 || T == 2 || T == 4 || (BLDP_T38 && (T == 3 || T == 8))) ? 16 / T : 1;
     if (BLDP_ROW_TPB && tpb > 1 && a.nto > 1 && bc * cdiv(a.nto, tpb) <= INT32_MAX &&
         a.ni <= 65535) {
       p.path = PATH_VEC_ROW;
@@ -1917,7 +1939,8 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
     }
   }
   // narrow path, short time blocks: k_reduce_narrowt (grid as k_reduce_rowt's)
-  if (BLDP_NARROW_TPB && p.path == PATH_NARROW && a.nchunk == 1 && (T == 1 || T == 2 || T == 4) &&
+  if (BLDP_NARROW_TPB && p.path == PATH_NARROW && a.nchunk == 1 &&
+      (T == 1 || T == 2 || T == 4 || (BLDP_T38 && T == 3)) &&
       (BLDP_NARROW_TPB >= 1 + (F == 1 && T == 1)) && a.nto > 1 && a.ni <= 65535 && a.nbank <= 65535) {
     const int64_t cols = a.nco * F / 4, tpb = 16 / T;
     const int sh = cols <= 64 ? 2 : cols <= 128 ? 1 : 0;

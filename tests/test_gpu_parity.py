@@ -161,7 +161,10 @@ def test_reduce_row_integer_exact(eng, orc, shape):
 # per lane (TPB = 8 / T); the last two shapes are large enough for 16.
 ROWT_SHAPES = [(1025, 2, 37, 16, 1), (64, 1, 279, 64, 1), (33, 3, 10, 4, 2), (257, 1, 28, 256, 4),
                (300, 2, 1, 8, 1), (64, 1, 200, 8, 1), (64, 2, 150, 8, 2), (20, 1, 70, 8, 1),
-               (4096, 2, 2051, 16, 1), (128, 1, 8200, 256, 4)]
+               (4096, 2, 2051, 16, 1), (128, 1, 8200, 256, 4),
+               # tavby = 3 and 8 (BLDP_T38): 5 / 2 blocks per workgroup (2 / 1 when small)
+               (1025, 2, 37, 16, 3), (64, 1, 279, 64, 3), (257, 1, 50, 256, 8), (33, 3, 30, 4, 3),
+               (20, 1, 70, 8, 3), (64, 2, 150, 8, 8), (300, 1, 97, 32, 3), (4096, 2, 2051, 16, 3)]
 
 
 @pytest.mark.parametrize("shape", ROWT_SHAPES, ids=lambda s: "x".join(map(str, s)))
@@ -184,7 +187,7 @@ def test_reduce_short_time_blocks_integer_exact(eng, orc, shape):
         got = host(eng, eng.reduce(x, F, T, op))
         assert same_bits(got, orc.reduce(a, F, T, op)), (shape, op)
     if a.nbytes > 1 << 28:
-        assert tpb * T == 16, (shape, tpb)
+        assert tpb == 16 // T, (shape, tpb)
         return  # (the large shapes: the 16-row kernel; windows and bands run above)
     # a time window starting inside the data, and a band of three banks
     if nt > T:
@@ -205,7 +208,10 @@ LANET_SHAPES = [(1000, 1, 37, 3, 1), (21845, 1, 18, 3, 1), (300, 2, 20, 5, 2), (
                 (70, 2, 24, 3, 4), (90, 1, 18, 6, 2), (600, 2, 16, 12, 4), (300, 1, 12, 5, 4),
                 # segments shifted onto 64-byte product lines: nco % 256 > 240 takes one
                 # more column block; odd nco moves every row's (and bank's) alignment
-                (241, 2, 17, 3, 1), (497, 1, 10, 7, 2), (767, 3, 9, 5, 1), (16, 1, 5, 12, 1)]
+                (241, 2, 17, 3, 1), (497, 1, 10, 7, 2), (767, 3, 9, 5, 1), (16, 1, 5, 12, 1),
+                # tavby = 3 and 8 (BLDP_T38): 2 / 1 blocks of 6 / 8 rows per lane
+                (1000, 1, 37, 3, 3), (300, 2, 20, 5, 8), (513, 1, 19, 12, 3), (90, 1, 33, 7, 3),
+                (600, 2, 16, 12, 8), (170, 1, 40, 6, 3)]
 
 
 def lanet_rows(F):
@@ -285,7 +291,8 @@ def test_reduce_large_groups_short_time_blocks_integer_exact(eng, orc, shape):
 # 16 / T time blocks per workgroup (2 or 4 time groups per workgroup on
 # windows of <= 128 float4 columns); bit-exact, the same bits as k_reduce_narrow.
 NARROWT_SHAPES = [(512, 1, 300, 2, 1), (128, 2, 50, 2, 2), (2048, 1, 32, 1, 4), (256, 3, 20, 1, 2),
-                  (6000, 1, 17, 2, 1), (4096, 1, 37, 1, 1), (100, 2, 9, 1, 1)]  # (F = T = 1: the copy)
+                  (6000, 1, 17, 2, 1), (4096, 1, 37, 1, 1), (100, 2, 9, 1, 1),  # (F = T = 1: the copy)
+                  (512, 1, 300, 2, 3), (2048, 1, 32, 1, 3), (100, 2, 31, 2, 3)]  # tavby = 3
 
 
 @pytest.mark.parametrize("shape", NARROWT_SHAPES, ids=lambda s: "x".join(map(str, s)))

@@ -49,6 +49,7 @@ VARIANTS = {
     "lanetoas8": "-DBLDP_LANET_OALIGN=1 -DBLDP_LANET_ROWS_S=8",
     "lanetoap3": "-DBLDP_LANET_OALIGN=1 -DBLDP_LANET_NT3=0",
     "lanetold": "-DBLDP_LANET_OALIGN=0 -DBLDP_LANET_ROWS_S=16",  # the r03f defaults
+    "not38": "-DBLDP_T38=0",  # tavby = 3, 8 off the short-time-block kernels
     "nowide": "-DBLDP_WIDE_SPLIT=0",  # fqavby > 4096: time split by row count only
     "nocopyt": "-DBLDP_NARROW_TPB=1",  # fqavby = tavby = 1 on k_reduce_narrow (one row per WG)
     "veck3off": "-DBLDP_VEC_K3=0",  # fqavby = 12 / 24: the generic K4 loop
@@ -337,6 +338,23 @@ def run(names, rounds, iters, suite="main"):
         for F, T in ((8, 1), (64, 1), (16, 2), (64, 4)):
             band_case(f"0001 band F{F} T{T}", b4, F, T, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
         cases_done = True
+    elif suite == "grid0":  # fqavby x tavby over the 0000 band (2^26 ch x 16 spectra x 8)
+        n = 1 << 26
+        for F in (1, 2, 3, 4, 5, 8, 12, 16, 64, 256, 1024, 4096, 65536, 1 << 20):
+            for T in (1, 2, 3, 4, 8, 16):
+                if F * T < 16:  # (every case's product is kept: <= 2 GiB each)
+                    continue
+                w = [0, n // F * F, 1, 0, 1, 1, 0, 16 // T * T, 1]
+                band_case(f"0000 F{F} T{T} {eng.plan(b3[0], F, T, 'sum', w)['path']}", b3, F, T, w)
+        cases_done = True
+    elif suite == "grid1":  # fqavby x tavby over the 0001 band (512 ch x 879616 spectra x 8)
+        del b3
+        b4 = [eng.synth(512, 1, 880000, 8, seed=10 * b + 1, kind=0) for b in range(8)]
+        for F in (1, 2, 3, 4, 8, 12, 16, 64, 128, 512):
+            for T in (1, 2, 3, 4, 8, 16, 64, 1024):
+                w = [0, 512 // F * F, 1, 0, 1, 1, 0, 879616 // T * T, 1]
+                band_case(f"0001 F{F} T{T} {eng.plan(b4[0], F, T, 'sum', w)['path']}", b4, F, T, w)
+        cases_done = True
     elif suite == "grid":  # fqavby x tavby over the 0002 band: every plan, looking for outliers
         del b3
         b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
@@ -353,6 +371,23 @@ def run(names, rounds, iters, suite="main"):
             w = [0, 65536 // F * F, 1, 0, 1, 1, 0, 279 // T * T, 1]
             band_case(f"0002 F{F} T{T}", b2, F, T, w)
         band_case("0002 file F12 T16", b2[:1], 12, 16, [0, 65532, 1, 0, 1, 1, 0, 272, 1])
+        cases_done = True
+    elif suite == "t38":  # tavby = 3 and 8 on every product
+        for F in (2, 3, 16, 64):
+            for T in (3, 8):
+                band_case(f"0000 F{F} T{T}", b3, F, T, [0, (1 << 26) // F * F, 1, 0, 1, 1, 0, 16 // T * T, 1])
+        del b3
+        b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
+        for F in (1, 2, 3, 5, 8, 12, 64, 256):
+            for T in (3, 8):
+                band_case(f"0002 band F{F} T{T}", b2, F, T, [0, 65536 // F * F, 1, 0, 1, 1, 0, 279 // T * T, 1])
+        band_case("0002 file F64 T3", b2[:1], 64, 3)
+        band_case("0002 file F64 T8", b2[:1], 64, 8, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
+        del b2
+        b4 = [eng.synth(512, 1, 880000, 8, seed=10 * b + 1, kind=0) for b in range(8)]
+        for F in (1, 2, 3, 4, 8, 12, 64, 128):
+            for T in (3, 8):
+                band_case(f"0001 band F{F} T{T}", b4, F, T, [0, 512 // F * F, 1, 0, 1, 1, 0, 879616 // T * T, 1])
         cases_done = True
     elif suite == "wide":  # groups wider than 4096 channels with few outputs
         del b3
@@ -496,7 +531,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--suite", default="main", choices=["main", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy", "wide"])
+    ap.add_argument("--suite", default="main", choices=["main", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy", "wide", "grid0", "grid1", "t38"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:
