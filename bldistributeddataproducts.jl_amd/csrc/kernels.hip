@@ -168,7 +168,10 @@ constexpr int kNacc = BLDP_NACC;
 //   BLDP_T38  1 (default) = the short-time-block kernels (k_reduce_rowt,
 //             k_reduce_narrowt, k_reduce_lanet) also take tavby = 3 and 8, not
 //             only 1, 2, 4 (the 512-channel 0001 product at tavby = 3 ran one
-//             3-row block per wave with half the waves idle: 2.4-2.7 TB/s)
+//             3-row block per wave with half the waves idle: 2.4-2.7 TB/s).
+//             narrowt: fqavby = 2 at tavby = 3 only (fqavby = 1 lost 7% on the
+//             0002 band; at tavby = 8 narrow_tile's one full batch sums in
+//             another order).  profiles/r03/ab_t38_r03t.json
 #ifndef BLDP_T38
 #define BLDP_T38 1
 #endif
@@ -1622,7 +1625,6 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
     else if (a.F == 2 && a.T == 2) { BLDP_NARROWT(2, 2) }
     else if (a.F == 2 && a.T == 4) { BLDP_NARROWT(2, 4) }
 #if BLDP_T38
-    else if (a.F == 1 && a.T == 3) { BLDP_NARROWT(1, 3) }
     else if (a.F == 2 && a.T == 3) { BLDP_NARROWT(2, 3) }
 #endif
     else return hipErrorInvalidValue;
@@ -1940,7 +1942,7 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
   }
   // narrow path, short time blocks: k_reduce_narrowt (grid as k_reduce_rowt's)
   if (BLDP_NARROW_TPB && p.path == PATH_NARROW && a.nchunk == 1 &&
-      (T == 1 || T == 2 || T == 4 || (BLDP_T38 && T == 3)) &&
+      (T == 1 || T == 2 || T == 4 || (BLDP_T38 && T == 3 && F == 2)) &&
       (BLDP_NARROW_TPB >= 1 + (F == 1 && T == 1)) && a.nto > 1 && a.ni <= 65535 && a.nbank <= 65535) {
     const int64_t cols = a.nco * F / 4, tpb = 16 / T;
     const int sh = cols <= 64 ? 2 : cols <= 128 ? 1 : 0;

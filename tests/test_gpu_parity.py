@@ -163,8 +163,8 @@ ROWT_SHAPES = [(1025, 2, 37, 16, 1), (64, 1, 279, 64, 1), (33, 3, 10, 4, 2), (25
                (300, 2, 1, 8, 1), (64, 1, 200, 8, 1), (64, 2, 150, 8, 2), (20, 1, 70, 8, 1),
                (4096, 2, 2051, 16, 1), (128, 1, 8200, 256, 4),
                # tavby = 3 and 8 (BLDP_T38): 5 / 2 blocks per workgroup (2 / 1 when small)
-               (1025, 2, 37, 16, 3), (64, 1, 279, 64, 3), (257, 1, 50, 256, 8), (33, 3, 30, 4, 3),
-               (20, 1, 70, 8, 3), (64, 2, 150, 8, 8), (300, 1, 97, 32, 3), (4096, 2, 2051, 16, 3)]
+               (1025, 2, 36, 16, 3), (64, 1, 279, 64, 3), (257, 1, 48, 256, 8), (33, 3, 30, 4, 3),
+               (20, 1, 69, 8, 3), (64, 2, 152, 8, 8), (300, 1, 96, 32, 3), (4096, 2, 2052, 16, 3)]
 
 
 @pytest.mark.parametrize("shape", ROWT_SHAPES, ids=lambda s: "x".join(map(str, s)))
@@ -210,8 +210,8 @@ LANET_SHAPES = [(1000, 1, 37, 3, 1), (21845, 1, 18, 3, 1), (300, 2, 20, 5, 2), (
                 # more column block; odd nco moves every row's (and bank's) alignment
                 (241, 2, 17, 3, 1), (497, 1, 10, 7, 2), (767, 3, 9, 5, 1), (16, 1, 5, 12, 1),
                 # tavby = 3 and 8 (BLDP_T38): 2 / 1 blocks of 6 / 8 rows per lane
-                (1000, 1, 37, 3, 3), (300, 2, 20, 5, 8), (513, 1, 19, 12, 3), (90, 1, 33, 7, 3),
-                (600, 2, 16, 12, 8), (170, 1, 40, 6, 3)]
+                (1000, 1, 36, 3, 3), (300, 2, 24, 5, 8), (513, 1, 18, 12, 3), (90, 1, 33, 7, 3),
+                (600, 2, 16, 12, 8), (170, 1, 39, 6, 3)]
 
 
 def lanet_rows(F):
@@ -292,7 +292,7 @@ def test_reduce_large_groups_short_time_blocks_integer_exact(eng, orc, shape):
 # windows of <= 128 float4 columns); bit-exact, the same bits as k_reduce_narrow.
 NARROWT_SHAPES = [(512, 1, 300, 2, 1), (128, 2, 50, 2, 2), (2048, 1, 32, 1, 4), (256, 3, 20, 1, 2),
                   (6000, 1, 17, 2, 1), (4096, 1, 37, 1, 1), (100, 2, 9, 1, 1),  # (F = T = 1: the copy)
-                  (512, 1, 300, 2, 3), (2048, 1, 32, 1, 3), (100, 2, 31, 2, 3)]  # tavby = 3
+                  (512, 1, 300, 2, 3), (100, 2, 30, 2, 3), (2048, 3, 33, 2, 3)]  # tavby = 3
 
 
 @pytest.mark.parametrize("shape", NARROWT_SHAPES, ids=lambda s: "x".join(map(str, s)))
@@ -979,14 +979,14 @@ UNALIGNED_CASES = [
     (4097, 2, 40, [1, 4092, 1, 0, 2, 1, 0, 40, 1], 2, 8, {"narrow"}),         # odd pitch
     (4097, 1, 24, [1, 4095, 1, 0, 1, 1, 0, 24, 1], 3, 8, {"lane"}),           # odd pitch, odd F
     (4097, 2, 24, [2, 4090, 1, 0, 2, 1, 0, 24, 1], 5, 4, {"lane"}),
-    (4100, 1, 40, [3, 4092, 1, 0, 1, 1, 0, 40, 1], 6, 8, {"tile"}),
+    (4100, 1, 40, [3, 4092, 1, 0, 1, 1, 0, 40, 1], 6, 8, {"lane"}),           # (lanet at tavby 8)
     (4100, 1, 40, [0, 4095, 1, 0, 1, 1, 0, 40, 1], 7, 20, {"tile"}),
     (4097, 1, 40, [3, 4092, 1, 0, 1, 1, 0, 40, 1], 6, 8, {"lane"}),           # odd pitch
     (4097, 1, 40, [0, 4095, 1, 0, 1, 1, 0, 40, 1], 7, 20, {"lane"}),          # odd pitch
     (4097, 1, 40, [1, 4094, 1, 0, 1, 1, 0, 40, 1], 2, 8, {"lane"}),           # odd pitch
     (71, 1, 30000, [1, 63, 1, 0, 1, 1, 0, 30000, 1], 3, 30000, {"lane"}),  # time chunks
     (4095, 1, 8, [0, 4095, 1, 0, 1, 1, 0, 8, 1], 5, 8, {"lane"}),             # ends at the array end
-    (4096, 2, 8, [4, 4089, 1, 0, 2, 1, 0, 8, 1], 3, 8, {"tile"}),
+    (4096, 2, 8, [4, 4089, 1, 0, 2, 1, 0, 8, 1], 3, 8, {"lane"}),
     (4097, 1, 24, [1, 4095, 1, 0, 1, 1, 0, 24, 1], 4095, 8, {"scalar"}),      # odd pitch, wide F
 ]
 
