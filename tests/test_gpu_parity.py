@@ -1043,7 +1043,7 @@ def test_unaligned_vector_special_values(eng, orc):
 # vector plans, bit-exact on integer data, with a partial window.
 TAIL_CASES = [(64, None, ("row", "vector")), (2, None, ("narrow",)), (1, None, ("narrow",)),
               (8, None, ("vector", "row")), (1, [1, 4094, 1, 0, 1, 1, 0, None, 1], ("narrow_mis",)),
-              (12, None, ("vector",)), (24, None, ("vector",)), (48, None, ("vector",)),
+              (12, None, ("vector", "lane")), (24, None, ("vector",)), (48, None, ("vector",)),
               (96, None, ("vector",)), (768, None, ("vector", "interleaved"))]
 
 
