@@ -633,6 +633,14 @@ __device__ __forceinline__ void narrow_mis_tile(const RedArgs &a, int64_t tile) 
 //   BLDP_LANE  1 (default) = F in {2, 3, 5, 6, 7} only where the tile path
 //              cannot run (row pitches that are not multiples of 4 floats; the
 //              alternative is the scalar path); 2 = always; 0 = off
+//   BLDP_LANE3  1 (default) = F = 3 on the lane kernel everywhere: one dwordx3
+//              per lane covers whole lines, and on narrow windows (the
+//              512-channel 0001 product, 170 groups a row) the tile path ran at
+//              2.8-4.3 TB/s against the lane kernel's 1.6x more
+//              (profiles/r03/ab_grid1_lane2_r03v.json)
+#ifndef BLDP_LANE3
+#define BLDP_LANE3 1
+#endif
 #ifndef BLDP_LANE
 #define BLDP_LANE 1
 #endif
@@ -1845,7 +1853,8 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
     a.blocks_c = cdiv(nc4, kBlock);
     tiles = cdiv(nc4, 64) * a.ni * a.nto * a.nbank;
   } else if (words && a.in_cs == 1 && BLDP_LANE >= 1 &&
-             (F == 2 || F == 3 || F == 5 || F == 6 || F == 7) && (BLDP_LANE >= 2 || !rows16)) {
+             (F == 2 || F == 3 || F == 5 || F == 6 || F == 7) &&
+             (BLDP_LANE >= 2 || !rows16 || (BLDP_LANE3 && F == 3))) {
     // small odd / not-multiple-of-4 groups: one lane per output
     p.path = PATH_LANE;
     a.blocks_c = cdiv(a.nco, kBlock);

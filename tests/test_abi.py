@@ -128,12 +128,14 @@ def test_launch_plans_host_only(pkg, L):
     assert plan(pkg, L, A, 4096, 1, 16, 64, 16, [1, 4032, 1, 0, 1, 1, 0, 16, 1])[0] in (0, 5)
     assert plan(pkg, L, A, 4096, 1, 16, 1, 1, [1, 4092, 1, 0, 1, 1, 0, 16, 1])[0] == 1
     assert plan(pkg, L, A, 4097, 1, 8, 1024, 8, [0, 4096, 1, 0, 1, 1, 0, 8, 1])[0] == 4
-    # F = 3, 5, 6, 7, 12 with short time blocks (T = 1, 2, 4): one lane per group,
-    # several time blocks per workgroup (k_reduce_lanet); with long time blocks
-    # and 16-byte pitches the tile path keeps them
+    # F = 3, 5, 6, 7, 12 with short time blocks (T = 1, 2, 3, 4, 8): one lane per
+    # group, several time blocks per workgroup (k_reduce_lanet); with long time
+    # blocks and 16-byte pitches the tile path keeps them, except F = 3 (one
+    # dwordx3 per lane: the lane kernel everywhere)
     assert plan(pkg, L, A, 4096, 1, 16, 3, 1, [0, 4095, 1, 0, 1, 1, 0, 16, 1])[0] == 7
     assert plan(pkg, L, A, 4096, 1, 16, 12, 1, [0, 4092, 1, 0, 1, 1, 0, 16, 1])[0] == 7
-    assert plan(pkg, L, A, 4096, 1, 16, 3, 16, [0, 4095, 1, 0, 1, 1, 0, 16, 1])[0] == 3
+    assert plan(pkg, L, A, 4096, 1, 16, 3, 16, [0, 4095, 1, 0, 1, 1, 0, 16, 1])[0] == 7
+    assert plan(pkg, L, A, 4096, 1, 16, 5, 16, [0, 4095, 1, 0, 1, 1, 0, 16, 1])[0] == 3
     # tile path: odd F > 7, misaligned channel start with F >= 512, short channel step
     assert plan(pkg, L, A, 4096, 1, 16, 9, 1, [0, 4095, 1, 0, 1, 1, 0, 16, 1])[0] == 3
     assert plan(pkg, L, A, 4096, 1, 16, 1024, 16, [1, 3072, 1, 0, 1, 1, 0, 16, 1])[0] == 3

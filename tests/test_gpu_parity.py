@@ -421,8 +421,10 @@ def misaligned_paths(win, F, T=16):
         return {"tile"}
     if F == 1:
         return {"narrow"} if win[1] % 4 == 0 else {"narrow_mis"}
-    if F in (3, 5, 6, 7, 12) and T in (1, 2, 4):
+    if F in (3, 5, 6, 7, 12) and T in (1, 2, 3, 4, 8):
         return {"lane"}  # k_reduce_lanet: short time blocks of small odd groups
+    if F == 3:
+        return {"lane"}  # one dwordx3 per lane (BLDP_LANE3)
     if F % 4 == 0 and F <= 256:
         return {"vector", "row"}
     return {"tile"}
