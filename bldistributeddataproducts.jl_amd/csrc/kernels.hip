@@ -1650,6 +1650,12 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
     case 1: BLDP_WAVETL(K, 1)                \
     case 2: BLDP_WAVETL(K, 2)                \
     case 4: BLDP_WAVETL(K, 4)                \
+    case 3: BLDP_WAVETL(K, 3)                \
+    case 8:                                  \
+      if constexpr (K <= 4) {                \
+        BLDP_WAVETL(K, 8)                    \
+      }                                      \
+      return hipErrorInvalidValue;           \
     default: return hipErrorInvalidValue;    \
   }                                          \
   break;
@@ -1899,7 +1905,8 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
   // poor fit (few groups per row, or its 3-D grid too small): k_reduce_wavet
   // (path "vector", a.tpb = time blocks per wave)
   if (BLDP_WAVET && p.path == PATH_VEC && p.lpg == 64 &&
-      (a.k4 == 2 || a.k4 == 4 || a.k4 == 8 || a.k4 == 16) && (T == 1 || T == 2 || T == 4) &&
+      (a.k4 == 2 || a.k4 == 4 || a.k4 == 8 || a.k4 == 16) &&
+      (T == 1 || T == 2 || T == 4 || (BLDP_T38 && (T == 3 || (T == 8 && a.k4 <= 4)))) &&
       a.ts == 1 && a.nchunk == 1 &&
       (BLDP_WAVET >= 2 || a.nco < 4 || a.ni * a.nto > 65535) && a.ni <= 65535 &&
       a.nbank <= 65535) {

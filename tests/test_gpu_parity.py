@@ -265,7 +265,9 @@ def test_reduce_small_odd_groups_gamma_rtol(eng, orc):
 # spectrum): k_reduce_wavet, one wave per group and 4 x 16 / (T K4) time
 # blocks; bit-exact, and the same bits k_reduce_vec gives.
 WAVET_SHAPES = [(1, 1, 300, 512, 1), (2, 2, 40, 1024, 2), (3, 1, 64, 4096, 4), (1, 1, 66000, 512, 1),
-                (2, 1, 37, 2048, 1)]
+                (2, 1, 37, 2048, 1),
+                # tavby = 3 (every K4) and 8 (K4 <= 4) (BLDP_T38)
+                (1, 1, 300, 512, 3), (2, 2, 42, 4096, 3), (1, 1, 800, 1024, 8), (3, 1, 64, 512, 8)]
 
 
 @pytest.mark.parametrize("shape", WAVET_SHAPES, ids=lambda s: "x".join(map(str, s)))

@@ -386,7 +386,7 @@ def run(names, rounds, iters, suite="main"):
         band_case("0002 file F64 T8", b2[:1], 64, 8, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
         del b2
         b4 = [eng.synth(512, 1, 880000, 8, seed=10 * b + 1, kind=0) for b in range(8)]
-        for F in (1, 2, 3, 4, 8, 12, 64, 128):
+        for F in (1, 2, 3, 4, 8, 12, 64, 128, 512):
             for T in (3, 8):
                 band_case(f"0001 band F{F} T{T}", b4, F, T, [0, 512 // F * F, 1, 0, 1, 1, 0, 879616 // T * T, 1])
         cases_done = True
