@@ -1651,11 +1651,6 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
     case 2: BLDP_WAVETL(K, 2)                \
     case 4: BLDP_WAVETL(K, 4)                \
     case 3: BLDP_WAVETL(K, 3)                \
-    case 8:                                  \
-      if constexpr (K <= 4) {                \
-        BLDP_WAVETL(K, 8)                    \
-      }                                      \
-      return hipErrorInvalidValue;           \
     default: return hipErrorInvalidValue;    \
   }                                          \
   break;
@@ -1906,7 +1901,7 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
   // (path "vector", a.tpb = time blocks per wave)
   if (BLDP_WAVET && p.path == PATH_VEC && p.lpg == 64 &&
       (a.k4 == 2 || a.k4 == 4 || a.k4 == 8 || a.k4 == 16) &&
-      (T == 1 || T == 2 || T == 4 || (BLDP_T38 && (T == 3 || (T == 8 && a.k4 <= 4)))) &&
+      (T == 1 || T == 2 || T == 4 || (BLDP_T38 && T == 3)) &&  // (T = 8: -8%, ab_t38_r03w)
       a.ts == 1 && a.nchunk == 1 &&
       (BLDP_WAVET >= 2 || a.nco < 4 || a.ni * a.nto > 65535) && a.ni <= 65535 &&
       a.nbank <= 65535) {
