@@ -112,6 +112,7 @@ struct KurtArgs {
   int32_t K;    // level of the blocks of the pairwise-sum tree
   int64_t nslot;  // leaf slots, 2 per block (2^(K+1))
   int64_t nseg;   // 64-lane column segments per row (k_kurt_leaf)
+  int32_t leafw;  // channels per lane of k_kurt_leaf (kLeafW; 1 for short narrow windows)
   // two-pass (unaligned) z pass
   int64_t rows_per_chunk;
   int32_t nchunk;

@@ -438,6 +438,18 @@ __global__ __launch_bounds__(64 * NW) void k_kurt_mid2(const KurtArgs k) {
 #ifndef BLDP_KURT_LEAF_MINWAVES
 #define BLDP_KURT_LEAF_MINWAVES 0
 #endif
+//   BLDP_KURT_LEAF_NARROW  plans whose leaves would give fewer than this many
+//                         waves per CU at W channels per lane take one channel
+//                         per lane (4x the waves) and BLDP_KURT_LEAF_NB spectra per
+//                         batch: short windows of narrow products (0001: 512
+//                         channels, nt = 513..8192 had 32-128 waves on the chip);
+//                         0 = never.  Each channel's arithmetic is unchanged.
+#ifndef BLDP_KURT_LEAF_NARROW
+#define BLDP_KURT_LEAF_NARROW 4
+#endif
+#ifndef BLDP_KURT_LEAF_NB
+#define BLDP_KURT_LEAF_NB 16
+#endif
 constexpr int kLeafW = BLDP_KURT_LEAF_W;
 static_assert(kLeafW == 1 || kLeafW == 2 || kLeafW == 4, "BLDP_KURT_LEAF_W: 1, 2 or 4");
 
@@ -511,6 +523,7 @@ __device__ __forceinline__ void leaf_store(const KurtArgs &k, const LeafAcc<W> &
   stw<W, float>(k.pf + (2 * k.nslot + slot) * n + e, A.lo);
 }
 
+template <int W, int B>
 __global__ __launch_bounds__(kB)
 #if BLDP_KURT_LEAF_MINWAVES > 0 && BLDP_KURT_LEAF_WAVES > 0
 __attribute__((amdgpu_waves_per_eu(BLDP_KURT_LEAF_MINWAVES, BLDP_KURT_LEAF_WAVES)))
@@ -520,7 +533,6 @@ __attribute__((amdgpu_waves_per_eu(BLDP_KURT_LEAF_MINWAVES)))
 __attribute__((amdgpu_waves_per_eu(1, BLDP_KURT_LEAF_WAVES)))
 #endif
 void k_kurt_leaf(const KurtArgs k) {
-  constexpr int B = BLDP_KURT_LEAF_B, W = kLeafW;
   const int lane = threadIdx.x & 63;
   const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t seg = u % k.nseg, r = u / k.nseg;
@@ -1016,7 +1028,11 @@ hipError_t launch_tree(const KurtArgs &k, char *ws, const KLayout &L, hipStream_
 void plan_kurtosis(KurtArgs &k, int num_cus) {
   k.K = pw_level(std::max<int64_t>(k.nt, 1));
   k.nslot = (int64_t)2 << k.K;
-  k.nseg = cdivk(k.nc / kLeafW, 64);
+  k.leafw = kLeafW;
+  if (BLDP_KURT_LEAF_NARROW > 0 && kLeafW > 1 &&
+      k.nrow * k.nslot * cdivk(k.nc / kLeafW, 64) < (int64_t)num_cus * BLDP_KURT_LEAF_NARROW)
+    k.leafw = 1;
+  k.nseg = cdivk(k.nc / k.leafw, 64);
   // two-pass z pass: waves splitting the spectra of a tile, >= 16 spectra per wave
   k.ts = 1;
   while (k.ts < 4 && k.nt >= (int64_t)32 * k.ts) k.ts *= 2;
@@ -1103,7 +1119,10 @@ hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s) {
     k.pm = reinterpret_cast<double *>(ws + L.a_pm);
     k.pf = reinterpret_cast<float *>(ws + L.a_pf);
     const dim3 g1((unsigned)cdivk(k.nrow * k.nslot * k.nseg, 4));
-    hipLaunchKernelGGL(k_kurt_leaf, g1, block, 0, s, k);
+    if (k.leafw == 1)
+      hipLaunchKernelGGL((k_kurt_leaf<1, BLDP_KURT_LEAF_NB>), g1, block, 0, s, k);
+    else
+      hipLaunchKernelGGL((k_kurt_leaf<kLeafW, BLDP_KURT_LEAF_B>), g1, block, 0, s, k);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return launch_tree<true>(k, ws, L, s);

@@ -49,6 +49,7 @@ VARIANTS = {
     "lanetoas8": "-DBLDP_LANET_OALIGN=1 -DBLDP_LANET_ROWS_S=8",
     "lanetoap3": "-DBLDP_LANET_OALIGN=1 -DBLDP_LANET_NT3=0",
     "lanetold": "-DBLDP_LANET_OALIGN=0 -DBLDP_LANET_ROWS_S=16",  # the r03f defaults
+    "kleafwide": "-DBLDP_KURT_LEAF_NARROW=0",  # k_kurt_leaf always 4 channels per lane
     "lane3off": "-DBLDP_LANE3=0",  # fqavby = 3 with long time blocks on the tile path
     "not38": "-DBLDP_T38=0",  # tavby = 3, 8 off the short-time-block kernels
     "nowide": "-DBLDP_WIDE_SPLIT=0",  # fqavby > 4096: time split by row count only
@@ -249,6 +250,8 @@ def run(names, rounds, iters, suite="main"):
         cases.append((label, go, nbytes, out, keep))
 
     def kurt_case(label, banks, win=None):
+        if suite == "kgrid":
+            label += " " + eng.kurtosis_plan(banks[0], win)["path"]
         nchan, nif, ntime = banks[0].shape[0], banks[0].shape[1], banks[0].shape[2]
         nc = win[1] if win else nchan
         nt = win[7] if win else ntime
@@ -338,6 +341,24 @@ def run(names, rounds, iters, suite="main"):
         b4 = [eng.synth(512, 1, 880000, 8, seed=10 * b + 1, kind=0) for b in range(8)]
         for F, T in ((8, 1), (64, 1), (16, 2), (64, 4)):
             band_case(f"0001 band F{F} T{T}", b4, F, T, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
+        cases_done = True
+    elif suite == "kgrid":  # getkurtosis over window lengths and offsets on every product
+        for nt in (2, 4, 8, 16):
+            kurt_case(f"kurt 0000 nt{nt}", b3, [0, 1 << 26, 1, 0, 1, 1, 0, nt, 1])
+        kurt_case("kurt 0000 c0=1 nt16", b3, [1, (1 << 26) - 4, 1, 0, 1, 1, 0, 16, 1])
+        del b3
+        b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
+        for nt in (2, 8, 17, 32, 33, 64, 100, 128, 200, 279):
+            kurt_case(f"kurt 0002 nt{nt}", b2, [0, 65536, 1, 0, 1, 1, 0, nt, 1])
+        for c0 in (1, 2, 3):
+            kurt_case(f"kurt 0002 c0={c0} nt279", b2, [c0, 65528, 1, 0, 1, 1, 0, 279, 1])
+        kurt_case("kurt 0002 file nt279", b2[:1])
+        kurt_case("kurt 0002 half window nt279", b2, [16384, 32768, 1, 0, 1, 1, 0, 279, 1])
+        del b2
+        b4 = [eng.synth(512, 1, 880000, 8, seed=10 * b + 1, kind=0) for b in range(8)]
+        for nt in (513, 1024, 8192, 100000, 879616):
+            kurt_case(f"kurt 0001 nt{nt}", b4, [0, 512, 1, 0, 1, 1, 0, nt, 1])
+        kurt_case("kurt 0001 c0=2 nt879616", b4, [2, 508, 1, 0, 1, 1, 0, 879616, 1])
         cases_done = True
     elif suite == "grid0":  # fqavby x tavby over the 0000 band (2^26 ch x 16 spectra x 8)
         n = 1 << 26
@@ -545,7 +566,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--suite", default="main", choices=["main", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy", "wide", "grid0", "grid1", "t38", "lane3"])
+    ap.add_argument("--suite", default="main", choices=["main", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy", "wide", "grid0", "grid1", "t38", "lane3", "kgrid"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:
