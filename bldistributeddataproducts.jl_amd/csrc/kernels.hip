@@ -752,6 +752,11 @@ __device__ __forceinline__ void lane_tile(const RedArgs &a, int64_t tile) {
 #define BLDP_LANET_OALIGN 1
 #endif
 constexpr int lanet_oalign_pad() { return BLDP_LANET_OALIGN ? 15 : 0; }
+//   BLDP_LANET_PACK  1 (default) = windows of <= 113 groups share a workgroup
+//                 between 2 or 4 time groups (with BLDP_LANET_OALIGN)
+#ifndef BLDP_LANET_PACK
+#define BLDP_LANET_PACK 1
+#endif
 typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
@@ -803,21 +808,26 @@ __global__ __launch_bounds__(kBlock) void k_reduce_lanet(const RedArgs a) {
   const float id = R<OP>::id();
   const int64_t ld = a.in_ld_t;
   if constexpr (BLDP_LANET_OALIGN && CS == 1) {
-    // per output row b: this lane's group, shifted so the workgroup's 256
-    // outputs of that row start on a 64-byte line of the product
+    // narrow windows (nco + 15 <= 128 / 64 groups): 2 / 4 time groups share the
+    // workgroup, 256 >> sh lanes each (a.tsub_log2 = sh; 0 otherwise)
+    const int sh = a.tsub_log2, cw = kBlock >> sh, lt = tid & (cw - 1);
+    const int64_t tp0 = (((int64_t)tq << sh) + (tid >> (8 - sh))) * TPB;  // first time block
+    const int nbp = (int)max((int64_t)0, min((int64_t)TPB, a.nto - tp0));
+    // per output row b: this lane's group, shifted so the workgroup's outputs
+    // of that row start on a 64-byte line of the product
     float *orow[TPB];
     int64_t g[TPB];
     bool ok[TPB];
-    const int64_t cb = co - tid;
+    const int64_t cb = (int64_t)(bx - tq * bc) * cw;
 #pragma unroll
     for (int b = 0; b < TPB; ++b) {
-      orow[b] = a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + (to0 + b) * a.out_ld_t;
+      orow[b] = a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + (tp0 + b) * a.out_ld_t;
       const int64_t s = (int64_t)((reinterpret_cast<uintptr_t>(orow[b]) >> 2) & 15);
-      g[b] = cb - s + tid;
-      ok[b] = b < nb && g[b] >= 0 && g[b] < a.nco;
+      g[b] = cb - s + lt;
+      ok[b] = b < nbp && g[b] >= 0 && g[b] < a.nco;
     }
     float v[NRW][F];
-    const float *p = a.in[bank] + a.in_off + (int64_t)i * a.in_ld_i + to0 * T * ld;
+    const float *p = a.in[bank] + a.in_off + (int64_t)i * a.in_ld_i + tp0 * T * ld;
 #pragma unroll
     for (int u = 0; u < NRW; ++u) {
       if (ok[u / T]) {
@@ -1666,7 +1676,8 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
     return hipGetLastError();
   }
   if (p.path == PATH_LANE && p.lanet) {  // short time blocks, small odd groups: k_reduce_lanet
-    const dim3 g3((unsigned)(a.blocks_c * cdiv(a.nto, a.tpb)), (unsigned)a.ni, (unsigned)a.nbank);
+    const dim3 g3((unsigned)(a.blocks_c * cdiv(cdiv(a.nto, a.tpb), 1 << a.tsub_log2)),
+                  (unsigned)a.ni, (unsigned)a.nbank);
 #define BLDP_LANETL(FF, TT) hipLaunchKernelGGL((k_reduce_lanet<OP, FF, TT>), g3, block, 0, s, a); break;
 #define BLDP_LANET_T(FF)                   \
   switch (a.T) {                           \
@@ -1819,9 +1830,13 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
     a.tpb = (int32_t)(lanet_rows((int)F) / T);
     a.blocks_c = cdiv(a.nco + (lanet_cs((int)F) == 1 ? lanet_oalign_pad() : 0),
                       (int64_t)kBlock * lanet_cs((int)F));
+    // narrow windows: 2 or 4 time groups per workgroup (the 0001 product at
+    // fqavby = 12: 42 groups a row kept 42 of 256 lanes busy)
+    if (BLDP_LANET_OALIGN && BLDP_LANET_PACK && lanet_cs((int)F) == 1)
+      a.tsub_log2 = a.nco + 15 <= 64 ? 2 : a.nco + 15 <= 128 ? 1 : 0;
     a.nchunk = 1;
     a.rows_per_chunk = T;
-    a.ntiles = a.blocks_c * cdiv(a.nto, a.tpb) * a.ni * a.nbank;
+    a.ntiles = a.blocks_c * cdiv(cdiv(a.nto, a.tpb), (int64_t)1 << a.tsub_log2) * a.ni * a.nbank;
     p.grid = a.ntiles;
     p.ws_bytes = 0;
     a.div = (float)(F * T);

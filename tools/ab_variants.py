@@ -49,6 +49,7 @@ VARIANTS = {
     "lanetoas8": "-DBLDP_LANET_OALIGN=1 -DBLDP_LANET_ROWS_S=8",
     "lanetoap3": "-DBLDP_LANET_OALIGN=1 -DBLDP_LANET_NT3=0",
     "lanetold": "-DBLDP_LANET_OALIGN=0 -DBLDP_LANET_ROWS_S=16",  # the r03f defaults
+    "nolanetpack": "-DBLDP_LANET_PACK=0",  # lanet: one time group per workgroup on narrow windows
     "kleafwide": "-DBLDP_KURT_LEAF_NARROW=0",  # k_kurt_leaf always 4 channels per lane
     "lane3off": "-DBLDP_LANE3=0",  # fqavby = 3 with long time blocks on the tile path
     "not38": "-DBLDP_T38=0",  # tavby = 3, 8 off the short-time-block kernels
@@ -411,6 +412,17 @@ def run(names, rounds, iters, suite="main"):
             for T in (3, 8):
                 band_case(f"0001 band F{F} T{T}", b4, F, T, [0, 512 // F * F, 1, 0, 1, 1, 0, 879616 // T * T, 1])
         cases_done = True
+    elif suite == "lanetpack":  # small odd groups with short time blocks on narrow windows
+        del b3
+        b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
+        band_case("0002 band F3 T1", b2, 3, 1, [0, 65535, 1, 0, 1, 1, 0, 279, 1])
+        band_case("0002 band F12 T1", b2, 12, 1, [0, 65532, 1, 0, 1, 1, 0, 279, 1])
+        band_case("0002 band zoom 1200 ch F12 T1", b2, 12, 1, [30000, 1200, 1, 0, 1, 1, 0, 279, 1])
+        del b2
+        b4 = [eng.synth(512, 1, 880000, 8, seed=10 * b + 1, kind=0) for b in range(8)]
+        for F, T in ((3, 1), (12, 1), (12, 2), (7, 1), (5, 4), (6, 3), (12, 8)):
+            band_case(f"0001 band F{F} T{T}", b4, F, T, [0, 512 // F * F, 1, 0, 1, 1, 0, 879616 // T * T, 1])
+        cases_done = True
     elif suite == "lane3":  # fqavby = 3 with long time blocks: lane kernel vs tile path
         for T in (16,):
             band_case(f"0000 F3 T{T}", b3, 3, T, [0, (1 << 26) // 3 * 3, 1, 0, 1, 1, 0, 16, 1])
@@ -566,7 +578,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--suite", default="main", choices=["main", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy", "wide", "grid0", "grid1", "t38", "lane3", "kgrid"])
+    ap.add_argument("--suite", default="main", choices=["main", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy", "wide", "grid0", "grid1", "t38", "lane3", "kgrid", "lanetpack"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:
