@@ -113,6 +113,7 @@ struct KurtArgs {
   int64_t nslot;  // leaf slots, 2 per block (2^(K+1))
   int64_t nseg;   // 64-lane column segments per row (k_kurt_leaf)
   int32_t leafw;  // channels per lane of k_kurt_leaf (kLeafW; 1 for short narrow windows)
+  int32_t leaftile;  // leaves read whole into registers: k_kurt_tile's lane groups per channel (0 = streamed)
   // two-pass (unaligned) z pass
   int64_t rows_per_chunk;
   int32_t nchunk;

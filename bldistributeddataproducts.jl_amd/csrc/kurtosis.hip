@@ -41,6 +41,9 @@
 //               (Float64) instead of rounded to Float32 (relative 2^-24 per
 //               term, averaging out); overflow and underflow of the Float32
 //               squares are reproduced from the row's max and min.
+//               k_kurt_tile: short windows of narrow products (few leaves,
+//               few channels): each leaf read whole into the registers of a
+//               16-wave workgroup; the recipe itself for nt <= 1024.
 //   unaligned   k_kurt_leafsum + the same tree (sum only) -> m, then the
 //               recipe in a second pass (k_kurt_pass, k_kurt_fold).
 #include <hip/hip_runtime.h>
@@ -599,6 +602,175 @@ void k_kurt_leaf(const KurtArgs k) {
   leaf_store<W>(k, A, row, col, slot, len);
 }
 
+// ---------------------------------------------------------------------------
+// Leaves read whole into registers: one workgroup of kTileW waves per (64/Q
+// channels, leaf, bank x IF row).  Wave w holds the spectra [w*len/kTileW,
+// (w+1)*len/kTileW) of the leaf (<= 64: leaves hold <= 1024), split into Q
+// consecutive pieces over Q (1 or 2) groups of 64/Q lanes (lane = piece *
+// 64/Q + channel).  Every load of the leaf is in flight at once, where a streaming
+// lane of k_kurt_leaf waits one memory round trip per batch: short windows of
+// narrow products (0001: 512 channels, nt = 513..8192) are a few leaves deep
+// and have too few lanes to hide that.  Q > 1 spreads a leaf's channels over
+// Q times the workgroups (the bytes a CU can have in flight bound these
+// launches).  The sequential Float32 sum runs down the registers piece after
+// piece (handed on to the next lane group by a shuffle) and wave after wave
+// (through LDS), as in k_kurt_mid.
+//   RECIPE  (nt <= 1024, one leaf): then StatsBase's recipe over the
+//           registers (Float32 m, z, z2; Float64 moments; partials added in
+//           spectrum order) -> the excess kurtosis, no tree.
+//   !RECIPE the leaf's partials for the tree: (sum, max, min) and (mean,
+//           M2, M3, M4) about the leaf's own Float64 mean, both passes over
+//           the registers.
+//   BLDP_KURT_LEAF_TILE  1 (default) = this kernel for the plans that would
+//                        take one channel per lane on k_kurt_leaf
+//                        (BLDP_KURT_LEAF_NARROW) and fit one workgroup per CU:
+//                        Q = 2 if that many fit, else Q = 1, else the streamed
+//                        leaf (A/B, profiles/r03/ab_ktile_r03ab.json: at 2-4
+//                        workgroups per CU the streamed lanes win, and Q = 4
+//                        lost to Q = 2 everywhere); 2 = every leaf plan (Q = 2);
+//                        0 = never
+#ifndef BLDP_KURT_LEAF_TILE
+#define BLDP_KURT_LEAF_TILE 1
+#endif
+constexpr int kTileW = 16;
+
+template <int Q, bool RECIPE>
+__global__ __launch_bounds__(64 * kTileW) void k_kurt_tile(const KurtArgs k) {
+  constexpr int CH = 64 / Q, NR = 1024 / kTileW / Q;  // channels, registers per lane
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int grp = lane / CH, ch = lane % CH;
+  const int64_t ctiles = (k.nc + CH - 1) / CH;
+  const int64_t b = blockIdx.x;
+  const int64_t r = b / ctiles, c = (b % ctiles) * CH + ch;
+  const int64_t slot = RECIPE ? 0 : r % k.nslot, row = RECIPE ? r : r / k.nslot;
+  const bool valid = c < k.nc;
+  int64_t t0 = 0, len = k.nt;
+  if (!RECIPE) pw_leaf(k.nt, k.K, slot, t0, len);
+  if (len <= 0) return;  // (uniform over the workgroup)
+  const int bank = (int)(row / k.ni);
+  const int64_t i = row - (int64_t)bank * k.ni;
+  const int ln = (int)len;
+  const int r0 = __builtin_amdgcn_readfirstlane((wave * ln) / kTileW);
+  const int cnt = __builtin_amdgcn_readfirstlane(((wave + 1) * ln) / kTileW - r0);
+  const int g0 = (grp * cnt) / Q, gn = ((grp + 1) * cnt) / Q - g0;  // this lane's piece
+  const int64_t ld = k.in_ld_t;
+  // lanes past the window read channel 0 of the row (results not stored)
+  const float *p =
+      k.in[bank] + k.in_off + i * k.in_ld_i + (valid ? c : 0) * k.in_cs + (t0 + r0 + g0) * ld;
+  float v[NR];
+#pragma unroll
+  for (int q = 0; q < NR; ++q) v[q] = q < gn ? __builtin_nontemporal_load(p + q * ld) : 0.0f;
+  // the leaf's sequential Float32 sum, from its first element
+  __shared__ float carry[CH];
+  float s = 0.0f;
+#pragma unroll 1
+  for (int w = 0; w < kTileW; ++w) {
+    if (wave == w) {
+      if (w > 0) s = carry[ch];
+#pragma unroll
+      for (int g = 0; g < Q; ++g) {
+        if (grp == g) {
+#pragma unroll
+          for (int q = 0; q < NR; ++q)
+            if (q < gn) s = (w == 0 && g == 0 && q == 0) ? v[0] : s + v[q];
+        }
+        if (g + 1 < Q) s = __shfl_up(s, CH, 64);  // group g's sums to group g + 1
+      }
+      if (grp == Q - 1) carry[ch] = s;
+    }
+    __syncthreads();
+  }
+  const float S = carry[ch];
+  if constexpr (RECIPE) {
+    const float m = S / (float)ln;  // mean(v): Float32 sum / length
+    double c2 = 0.0, c4 = 0.0;
+#pragma unroll
+    for (int q = 0; q < NR; ++q)
+      if (q < gn) {
+        const float z = v[q] - m;  // StatsBase: z, z2 in Float32; Float64 moments
+        const float z2 = z * z;
+        c2 += (double)z2;
+        c4 += (double)(z2 * z2);
+      }
+    __shared__ double part[kTileW][2][64];
+    part[wave][0][lane] = c2;
+    part[wave][1][lane] = c4;
+    __syncthreads();
+    if (wave == 0 && grp == 0 && valid) {
+      double a2 = 0.0, a4 = 0.0;
+#pragma unroll
+      for (int w = 0; w < kTileW; ++w)
+#pragma unroll
+        for (int g = 0; g < Q; ++g) {
+          a2 += part[w][0][g * CH + ch];
+          a4 += part[w][1][g * CH + ch];
+        }
+      const double cm2 = a2 / (double)ln, cm4 = a4 / (double)ln;
+      k.out[row * k.nc + c] = (cm4 / (cm2 * cm2)) - 3.0;
+    }
+  } else {
+    // pass 1: max, min and the Float64 sum -> the leaf's mean (gn >= 8: leaves
+    // of a tree hold >= 512 spectra)
+    float hi = v[0], lo = v[0];
+    double d1 = 0.0;
+#pragma unroll
+    for (int q = 0; q < NR; ++q)
+      if (q < gn) {
+        hi = fmaxf(hi, v[q]);
+        lo = fminf(lo, v[q]);
+        d1 += (double)v[q];
+      }
+    __shared__ double p1[kTileW][64];
+    __shared__ float ph[kTileW][64], pl[kTileW][64];
+    p1[wave][lane] = d1;
+    ph[wave][lane] = hi;
+    pl[wave][lane] = lo;
+    __syncthreads();
+    double tot = 0.0;  // in spectrum order: every lane of a channel agrees
+#pragma unroll
+    for (int w = 0; w < kTileW; ++w)
+#pragma unroll
+      for (int g = 0; g < Q; ++g) tot += p1[w][g * CH + ch];
+    const double md = tot / (double)ln;
+    // pass 2: central moments about it
+    double a2 = 0.0, a3 = 0.0, a4 = 0.0;
+#pragma unroll
+    for (int q = 0; q < NR; ++q)
+      if (q < gn) {
+        const double d = (double)v[q] - md, d2 = d * d;
+        a2 += d2;
+        a3 = fma(d2, d, a3);
+        a4 = fma(d2, d2, a4);
+      }
+    __shared__ double p2[kTileW][3][64];
+    p2[wave][0][lane] = a2;
+    p2[wave][1][lane] = a3;
+    p2[wave][2][lane] = a4;
+    __syncthreads();
+    if (wave == 0 && grp == 0 && valid) {
+      double m2 = 0.0, m3 = 0.0, m4 = 0.0;
+#pragma unroll
+      for (int w = 0; w < kTileW; ++w)
+#pragma unroll
+        for (int g = 0; g < Q; ++g) {
+          m2 += p2[w][0][g * CH + ch];
+          m3 += p2[w][1][g * CH + ch];
+          m4 += p2[w][2][g * CH + ch];
+          hi = fmaxf(hi, ph[w][g * CH + ch]);
+          lo = fminf(lo, pl[w][g * CH + ch]);
+        }
+      const int64_t n = k.nrow * k.nc, e = row * k.nc + c;
+      k.pm[slot * n + e] = md;
+      k.pm[(k.nslot + slot) * n + e] = m2;
+      k.pm[(2 * k.nslot + slot) * n + e] = m3;
+      k.pm[(3 * k.nslot + slot) * n + e] = m4;
+      k.pf[slot * n + e] = S;
+      k.pf[(k.nslot + slot) * n + e] = hi;
+      k.pf[(2 * k.nslot + slot) * n + e] = lo;
+    }
+  }
+}
+
 // Unaligned windows: one lane per (column, leaf) runs the sequential Float32
 // sum of the leaf (any channel step); sums only.
 __global__ __launch_bounds__(kB) void k_kurt_leafsum(const KurtArgs k) {
@@ -1032,6 +1204,16 @@ void plan_kurtosis(KurtArgs &k, int num_cus) {
   if (BLDP_KURT_LEAF_NARROW > 0 && kLeafW > 1 &&
       k.nrow * k.nslot * cdivk(k.nc / kLeafW, 64) < (int64_t)num_cus * BLDP_KURT_LEAF_NARROW)
     k.leafw = 1;
+  k.leaftile = 0;  // lane groups per channel of k_kurt_tile; 0 = streamed leaves
+  if (BLDP_KURT_LEAF_TILE == 2) {
+    k.leaftile = 2;
+  } else if (BLDP_KURT_LEAF_TILE == 1 && k.leafw == 1) {
+    const int64_t units = k.nrow * (k.nt <= 1024 ? 1 : k.nslot);  // leaves x rows
+    if (units * cdivk(k.nc, 32) <= num_cus)
+      k.leaftile = 2;
+    else if (units * cdivk(k.nc, 64) <= num_cus)
+      k.leaftile = 1;
+  }
   k.nseg = cdivk(k.nc / k.leafw, 64);
   // two-pass z pass: waves splitting the spectra of a tile, >= 16 spectra per wave
   k.ts = 1;
@@ -1118,6 +1300,25 @@ hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s) {
   if (p == KP_LEAF) {
     k.pm = reinterpret_cast<double *>(ws + L.a_pm);
     k.pf = reinterpret_cast<float *>(ws + L.a_pf);
+    if (k.leaftile) {
+      const bool recipe = k.nt <= 1024;  // one leaf: the recipe itself, no tree
+      const int Q = k.leaftile;
+      const dim3 gt((unsigned)(cdivk(k.nc, 64 / Q) * k.nrow * (recipe ? 1 : k.nslot))), bt(64 * kTileW);
+      if (recipe) {
+        if (Q == 2)
+          hipLaunchKernelGGL((k_kurt_tile<2, true>), gt, bt, 0, s, k);
+        else
+          hipLaunchKernelGGL((k_kurt_tile<1, true>), gt, bt, 0, s, k);
+        return hipGetLastError();
+      }
+      if (Q == 2)
+        hipLaunchKernelGGL((k_kurt_tile<2, false>), gt, bt, 0, s, k);
+      else
+        hipLaunchKernelGGL((k_kurt_tile<1, false>), gt, bt, 0, s, k);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+      return launch_tree<true>(k, ws, L, s);
+    }
     const dim3 g1((unsigned)cdivk(k.nrow * k.nslot * k.nseg, 4));
     if (k.leafw == 1)
       hipLaunchKernelGGL((k_kurt_leaf<1, BLDP_KURT_LEAF_NB>), g1, block, 0, s, k);
@@ -1156,6 +1357,7 @@ int64_t kurtosis_max_grid(const KurtArgs &k) {
     case KP_REGS: return cdivk(ncols, kB) * k.nrow;
     case KP_MID: return cdivk(k.nc, 64) * k.nrow;  // (k_kurt_mid2: half of it)
     case KP_LEAF:
+      if (k.leaftile) return cdivk(k.nc, 64 / k.leaftile) * k.nrow * (k.nt <= 1024 ? 1 : k.nslot);
       return cdivk(k.nrow * k.nslot * k.nseg, 4);
     default:
       return std::max(cdivk(k.nc, kB) * k.nrow * k.nslot,

@@ -98,6 +98,22 @@ def test_kurtosis_integrated_power_rows(eng, orc, nt, path):
         assert_kurtosis(host(eng, k), orc.kurtosis(arr), pth, nt, "band")
 
 
+@pytest.mark.parametrize("nt", [513, 1000, 1024, 1025, 3000, 8192])
+def test_kurtosis_short_windows_of_narrow_products(eng, orc, nt):
+    """Short windows of a narrow product (the 0001 shape: 512 channels, a
+    band of 3 banks): few leaves and few channels, so every leaf is read
+    whole into registers (k_kurt_tile: the recipe itself for nt <= 1024, leaf
+    partials and the tree above that).  Also a window whose channel count is
+    not a multiple of a workgroup's channels and that starts off a float4."""
+    rng = np.random.default_rng(7000 + nt)
+    arrs = [power_rows(rng, 512, 1, nt + 3) for _ in range(3)]
+    for w in ([0, 512, 1, 0, 1, 1, 0, nt, 1], [4, 500, 1, 0, 1, 1, 3, nt, 1]):
+        assert eng.kurtosis_plan(dev(eng, arrs[0]), w)["path"] == "leaf"
+        ks = eng.band_kurtosis([dev(eng, a) for a in arrs], w)
+        for a, k in zip(arrs, ks):
+            assert_kurtosis(host(eng, k), orc.kurtosis(a, w), "leaf", nt, w)
+
+
 @pytest.mark.parametrize("nt,nc", [(140000, 64), (600000, 16), (2200001, 8)])
 def test_kurtosis_tree_passes(eng, orc, nt, nc):
     """Long windows whose pairwise tree has K > 6 levels above the blocks, so
