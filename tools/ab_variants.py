@@ -33,6 +33,7 @@ VARIANTS = {
     "base": "",  # nt loads+stores, batch 8, no grid cap
     "nodpp": "-DBLDP_DPP=0",  # lane folds on __shfl_xor (ds_bpermute) instead of DPP / permlane swaps
     "r02": {"rev": R02, "extra": ""},  # the round-2 product build
+    "r03x": {"rev": "ae8255c", "extra": ""},  # the r03x product build (before the r03z..ab kurtosis changes)
     "nolanet": "-DBLDP_LANET=0",  # small odd F, short time blocks: the lane / tile / vector paths
     "rowtst": "-DBLDP_ROWT_LDS_OUT=0",  # k_reduce_rowt: each wave stores its own outputs
     "lanetg": {"rev": "bbf0328", "extra": "-DBLDP_LANET_G=1"},  # F = 3 / 6: 4 / 2 groups per lane (removed)
