@@ -325,6 +325,12 @@ __global__ __launch_bounds__(kB) void k_kurt_mid(const KurtArgs k) {
 #ifndef BLDP_KURT_MID_NW
 #define BLDP_KURT_MID_NW 8
 #endif
+//   BLDP_KURT_MID_SMALL  1 (default) = windows of <= 64 spectra take 4 waves (A/B,
+//                        profiles/r03/ab_kfile_r03ad.json: 0002 band nt = 33 / 48 /
+//                        64 1.34 / 1.22 / 1.04x; nt >= 100 and one file no gain)
+#ifndef BLDP_KURT_MID_SMALL
+#define BLDP_KURT_MID_SMALL 1
+#endif
 template <int NR, int NW>
 __global__ __launch_bounds__(64 * NW) void k_kurt_mid2(const KurtArgs k) {
   constexpr int TW = 128;  // channels per tile
@@ -1259,6 +1265,10 @@ hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s) {
     constexpr int NW = BLDP_KURT_MID_NW;
     static_assert(NW == 4 || NW == 8 || NW == 16, "BLDP_KURT_MID_NW: 4, 8 or 16");
     const dim3 g1((unsigned)(cdivk(k.nc, 128) * k.nrow)), b2(64 * NW);
+    if (BLDP_KURT_MID_SMALL && NW > 4 && k.nt <= 64) {  // (33..64 here) 4 waves of <= 16 spectra
+      hipLaunchKernelGGL((k_kurt_mid2<16, 4>), g1, dim3(256), 0, s, k);
+      return hipGetLastError();
+    }
     // registers sized to a wave's spectra, 8 at a time (occupancy: 113 VGPRs
     // at 48 spectra = 4 waves/SIMD, 80 at 32 = 6, 48 at 16 = 8)
     switch (cdivk(cdivk(k.nt, NW), 8)) {

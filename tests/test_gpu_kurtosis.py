@@ -71,7 +71,8 @@ def check(eng, orc, a, win=None, expect=None, msg=""):
     return plan
 
 
-PATH_NT = [(7, "regs"), (16, "regs"), (32, "regs"), (33, "mid"), (100, "mid"), (272, "mid"),
+PATH_NT = [(7, "regs"), (16, "regs"), (32, "regs"), (33, "mid"), (48, "mid"), (64, "mid"),
+           (65, "mid"), (100, "mid"), (272, "mid"),
            (385, "mid"), (512, "mid"), (513, "leaf"), (1024, "leaf"), (1025, "leaf"),
            (2048, "leaf"), (2049, "leaf"), (5007, "leaf"), (20000, "leaf")]
 

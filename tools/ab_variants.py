@@ -68,6 +68,9 @@ VARIANTS = {
     "rowt16": "-DBLDP_ROWT_SMALL=0",  # k_reduce_rowt: always 16 rows per lane (r03h default)
     "kmidnr16": {"rev": "7474fea", "extra": ""},  # k_kurt_mid2 registers in steps of 16 spectra
     "kmid2w16": "-DBLDP_KURT_MID_NW=16",  # k_kurt_mid2 with 16 waves (<= 24 spectra each)
+    "kmid2w4": "-DBLDP_KURT_MID_NW=4",  # k_kurt_mid2 with 4 waves
+    "kmidsmall0": "-DBLDP_KURT_MID_SMALL=0",  # windows of <= 64 spectra on 8 waves too
+    "kmid1": "-DBLDP_KURT_MID_CPL=1",  # k_kurt_mid only (64 channels per workgroup, 4 waves)
     # TIMING-ONLY patch variants (wrong numerics, never in the product sources):
     # the current sources with a text substitution, built under build/variants/
     "kmid2f32": {"patch": [("kurtosis.hip", "double a2 = 0.0, a4 = 0.0, b2 = 0.0, b4 = 0.0;",
@@ -382,6 +385,15 @@ def run(names, rounds, iters, suite="main"):
         kurt_case("kurt 65536ch nt1024", b5, [0, 65536, 1, 0, 1, 1, 0, 1024, 1])
         kurt_case("kurt 65536ch nt600", b5, [0, 65536, 1, 0, 1, 1, 0, 600, 1])
         cases_done = True
+    elif suite == "kfile":  # the register-tile kurtosis on one file and short windows of the band
+        del b3
+        b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
+        kurt_case("kurt 0002 file nt279", b2[:1])
+        kurt_case("kurt 0002 file nt100", b2[:1], [0, 65536, 1, 0, 1, 1, 0, 100, 1])
+        kurt_case("kurt 0002 band nt279", b2)
+        for nt in (33, 48, 64, 100):
+            kurt_case(f"kurt 0002 band nt{nt}", b2, [0, 65536, 1, 0, 1, 1, 0, nt, 1])
+        cases_done = True
     elif suite == "grid0":  # fqavby x tavby over the 0000 band (2^26 ch x 16 spectra x 8)
         n = 1 << 26
         for F in (1, 2, 3, 4, 5, 8, 12, 16, 64, 256, 1024, 4096, 65536, 1 << 20):
@@ -602,7 +614,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--suite", default="main", choices=["main", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy", "wide", "grid0", "grid1", "t38", "lane3", "kgrid", "lanetpack", "kshort"])
+    ap.add_argument("--suite", default="main", choices=["main", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy", "wide", "grid0", "grid1", "t38", "lane3", "kgrid", "lanetpack", "kshort", "kfile"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:
