@@ -8,12 +8,15 @@
 // own arithmetic on it (:16-20, :197-202):
 //   * sum(reshape(A, (n, :, ...)); dims = 1) widens small integers
 //     (Base.add_sum: UInt8/16/32 -> UInt64, Int8/16/32 -> Int64; 64-bit and
-//     Float64 stay as they are), so every sum here is exact (wrapping like
-//     Julia's Int64 / UInt64 on overflow) or a Float64 sum taken in the
-//     reference's order (the n channels in sequence, spectrum after spectrum);
-//   * mean(...; dims = 1) is Float64 for integer and Float64 input: the sum of
-//     the values converted to Float64, divided by n (for integers the exact sum
-//     converted once, which is the same number while it stays below 2^53);
+//     Float64 stay as they are), so every integer sum here is exact (wrapping
+//     like Julia's Int64 / UInt64 on overflow) and a Float64 sum is taken in
+//     the reference's order: Base's reducedim seeds zero(T) and adds
+//     mapreduce_impl of the group, i.e. up to 1024 channels in sequence and
+//     pairwise halves above that (jl_dimsum_f64); the time integration is fqav
+//     on axis 3, so a time block's spectral sums are combined the same way;
+//   * mean(...; dims = 1) is Float64 for integer and Float64 input: the
+//     values converted to Float64 (Statistics' _mean_promote) summed in that
+//     same order, divided by n;
 //   * maximum / minimum keep the element type (Float64: NaN propagates,
 //     -0.0 < +0.0, as Julia's max / min);
 //   * StatsBase.kurtosis of an integer or Float64 row is Float64 throughout:
@@ -59,50 +62,18 @@ __device__ __forceinline__ T jmin(T a, T b) {
   else return a < b ? a : b;
 }
 
-template <typename TI, int OP>
-__global__ __launch_bounds__(256) void k_reduce_typed(const TypedArgs a) {
-  typedef typename SumT<TI>::type TS;
-  const int64_t nout = a.nco * a.ni * a.nto * a.nbank;
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < nout;
-       e += (int64_t)gridDim.x * 256) {
-    const int64_t co = e % a.nco;
-    int64_t r = e / a.nco;
-    const int64_t i = r % a.ni;
-    r /= a.ni;
-    const int64_t to = r % a.nto;
-    const int64_t bank = r / a.nto;
-    const TI *p = static_cast<const TI *>(a.in[bank]) + a.in_off + i * a.in_ld_i +
-                  to * a.T * a.in_ld_t + co * a.F * a.in_cs;
-    const int64_t oe = bank * a.out_bank + i * a.out_ld_i + to * a.out_ld_t + co;
-    if constexpr (OP == BLDP_OP_MAX || OP == BLDP_OP_MIN) {
-      TI acc = p[0];  // Julia seeds the reduction with the first element
-      for (int64_t t = 0; t < a.T; ++t) {
-        const TI *q = p + t * a.in_ld_t;
-        for (int64_t k = (t == 0); k < a.F; ++k)
-          acc = OP == BLDP_OP_MAX ? jmax<TI>(acc, q[k * a.in_cs]) : jmin<TI>(acc, q[k * a.in_cs]);
-      }
-      static_cast<TI *>(a.out)[oe] = acc;
-    } else {
-      TS acc = 0;
-      for (int64_t t = 0; t < a.T; ++t) {
-        const TI *q = p + t * a.in_ld_t;
-        for (int64_t k = 0; k < a.F; ++k) acc += (TS)q[k * a.in_cs];
-      }
-      if constexpr (OP == BLDP_OP_MEAN)
-        static_cast<double *>(a.out)[oe] = (double)acc / (double)(a.F * a.T);
-      else
-        static_cast<TS *>(a.out)[oe] = acc;
-    }
-  }
-}
-
-// Base.sum of a Float64 row (the values converted to Float64): mapreduce_impl
-// with pairwise_blocksize 1024 — halves [lo, mid], [mid+1, hi] with
-// mid = lo + (hi - lo) >> 1 until a piece is shorter than 1024 + 1, which is
+// Base.mapreduce_impl (Base/reduce.jl) over n Float64 values v(0 .. n-1)
+// with pairwise_blocksize 1024: halves [lo, mid], [mid+1, hi] with
+// mid = lo + (hi - lo) >> 1 until a piece is no longer than 1024, which is
 // summed in sequence from its first element.  Iterative, explicit stack.
-template <typename TI>
-__device__ double jl_pairwise_f64(const TI *p, int64_t ld, int64_t n) {
+template <typename V>
+__device__ double jl_mapreduce_f64(int64_t n, const V &v) {
   if (n <= 0) return 0.0;
+  if (n <= 1024) {  // one leaf (every fqavby of the BL products)
+    double s = v(0);
+    for (int64_t k = 1; k < n; ++k) s += v(k);
+    return s;
+  }
   int64_t lo[48], hi[48];
   double left[48];
   int state[48];
@@ -114,9 +85,9 @@ __device__ double jl_pairwise_f64(const TI *p, int64_t ld, int64_t n) {
   for (;;) {
     const int64_t L = lo[sp], H = hi[sp], M = L + ((H - L) >> 1);
     if (state[sp] == 0 && H - L < 1024) {
-      double v = (double)p[L * ld];
-      for (int64_t t = L + 1; t <= H; ++t) v += (double)p[t * ld];
-      val = v;
+      double s = v(L);
+      for (int64_t t = L + 1; t <= H; ++t) s += v(t);
+      val = s;
     } else if (state[sp] == 0) {
       state[sp] = 1;
       ++sp;
@@ -141,6 +112,65 @@ __device__ double jl_pairwise_f64(const TI *p, int64_t ld, int64_t n) {
   return val;
 }
 
+// sum(A; dims) of one slice as Base's reducedim takes it (_mapreducedim!):
+// R = zero(Float64), R + mapreduce_impl(slice).  (Slices of <= 16 take the
+// r = zero; r += A[i] loop instead: the same value, 0.0 + a1 = a1 but for
+// a1 = -0.0, which the outer 0.0 + settles the same way.)
+template <typename V>
+__device__ double jl_dimsum_f64(int64_t n, const V &v) {
+  return 0.0 + jl_mapreduce_f64(n, v);
+}
+
+template <typename TI, int OP>
+__global__ __launch_bounds__(256) void k_reduce_typed(const TypedArgs a) {
+  typedef typename SumT<TI>::type TS;
+  // Float64 accumulation: Float64 sums, and every mean (Statistics.mean sums
+  // the values converted to Float64: _mean_promote)
+  constexpr bool F64ACC = OP == BLDP_OP_MEAN || (TI)0.5 != 0;
+  const int64_t nout = a.nco * a.ni * a.nto * a.nbank;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < nout;
+       e += (int64_t)gridDim.x * 256) {
+    const int64_t co = e % a.nco;
+    int64_t r = e / a.nco;
+    const int64_t i = r % a.ni;
+    r /= a.ni;
+    const int64_t to = r % a.nto;
+    const int64_t bank = r / a.nto;
+    const TI *p = static_cast<const TI *>(a.in[bank]) + a.in_off + i * a.in_ld_i +
+                  to * a.T * a.in_ld_t + co * a.F * a.in_cs;
+    const int64_t oe = bank * a.out_bank + i * a.out_ld_i + to * a.out_ld_t + co;
+    if constexpr (OP == BLDP_OP_MAX || OP == BLDP_OP_MIN) {
+      TI acc = p[0];  // Julia seeds the reduction with the first element
+      for (int64_t t = 0; t < a.T; ++t) {
+        const TI *q = p + t * a.in_ld_t;
+        for (int64_t k = (t == 0); k < a.F; ++k)
+          acc = OP == BLDP_OP_MAX ? jmax<TI>(acc, q[k * a.in_cs]) : jmin<TI>(acc, q[k * a.in_cs]);
+      }
+      static_cast<TI *>(a.out)[oe] = acc;
+    } else if constexpr (F64ACC) {
+      // each spectrum's F channels as sum(reshape(A, (F, :, ...)); dims=1)
+      // sums them (src/gbtworkerfunctions.jl:19), then the T spectral sums of
+      // the time block the same way (time integration = fqav on axis 3)
+      const int64_t F = a.F, cs = a.in_cs, ld = a.in_ld_t;
+      const double s = jl_dimsum_f64(a.T, [&](int64_t t) {
+        const TI *q = p + t * ld;
+        return jl_dimsum_f64(F, [&](int64_t k) { return (double)q[k * cs]; });
+      });
+      if constexpr (OP == BLDP_OP_MEAN)
+        static_cast<double *>(a.out)[oe] = s / (double)(a.F * a.T);
+      else
+        static_cast<double *>(a.out)[oe] = s;
+    } else {  // integer sums: exact, wrapping like Julia's (U)Int64
+      TS acc = 0;
+      for (int64_t t = 0; t < a.T; ++t) {
+        const TI *q = p + t * a.in_ld_t;
+        for (int64_t k = 0; k < a.F; ++k) acc += (TS)q[k * a.in_cs];
+      }
+      static_cast<TS *>(a.out)[oe] = acc;
+    }
+  }
+}
+
 template <typename TI>
 __global__ __launch_bounds__(256) void k_kurt_typed(const TypedArgs a, double *out) {
   const int64_t nrow = a.nco * a.ni * a.nbank;
@@ -151,7 +181,9 @@ __global__ __launch_bounds__(256) void k_kurt_typed(const TypedArgs a, double *o
     const int64_t r = e / a.nco;
     const int64_t i = r % a.ni, bank = r / a.ni;
     const TI *p = static_cast<const TI *>(a.in[bank]) + a.in_off + i * a.in_ld_i + c * a.in_cs;
-    const double m = jl_pairwise_f64<TI>(p, a.in_ld_t, n) / (double)n;
+    // m = mean(v) = Base.sum(v) / n: mapreduce_impl over the whole row (no zero seed)
+    const int64_t ld = a.in_ld_t;
+    const double m = jl_mapreduce_f64(n, [&](int64_t t) { return (double)p[t * ld]; }) / (double)n;
     double cm2 = 0.0, cm4 = 0.0;
     for (int64_t t = 0; t < n; ++t) {
       const double z = (double)p[t * a.in_ld_t] - m;

@@ -108,12 +108,17 @@ def fb_to_numpy(t) -> np.ndarray:
     return np.asfortranarray(t.t().contiguous().cpu().numpy().T)
 
 
-def _abi_dims(t):
+def _abi_dims(t, allow_typed=False):
     """Map a channel-fastest tensor to (ptr, nchan, nif, ntime) of an array
     that contains it, so that its logical index (c, i, t) is element
-    c + nchan*(i + nif*t) of the ABI array."""
-    if _dtype_code(t.dtype) is None:
-        raise TypeError(f"unsupported filterbank element type {t.dtype}")
+    c + nchan*(i + nif*t) of the ABI array.
+
+    Float32 only unless ``allow_typed``: every caller but the typed entry
+    points (reduce / kurtosis, which branch to bldp_reduce_strided and
+    bldp_kurtosis) hands the pointer to an ``_f32`` function."""
+    code = _dtype_code(t.dtype)
+    if code is None or (code != 0 and not allow_typed):
+        raise TypeError(f"unsupported filterbank element type {t.dtype} (Float32 expected)")
     if not t.is_cuda:
         raise TypeError("device tensor expected (use getdata/reduce_host for host arrays)")
     if t.dim() != 3:
@@ -218,8 +223,8 @@ def reduce(x, fqavby=1, tavby=1, op="sum", win=None, out=None, stream=None):
         out = fb_empty(nco, ni, nto, device=x.device, dtype=odt)
     elif tuple(out.shape) != (nco, ni, nto) or out.dtype != odt:
         raise ValueError(f"out is {out.dtype} {tuple(out.shape)}, expected {odt} {(nco, ni, nto)}")
-    optr, onc, oni, _ = _abi_dims(out) if out.numel() else (0, nco, ni, nto)
-    ptr, nchan, nif, ntime = _abi_dims(x)
+    optr, onc, oni, _ = _abi_dims(out, allow_typed=True) if out.numel() else (0, nco, ni, nto)
+    ptr, nchan, nif, ntime = _abi_dims(x, allow_typed=True)
     keep, wp = _lib.win_arg(_full_win(win, shape))
     if typed:  # fqav's Julia result types for integer / Float64 data (bldp_reduce_strided)
         rc = L.bldp_reduce_strided(_dtype_code(x.dtype), ptr, nchan, nif, ntime, wp, int(fqavby),
@@ -273,6 +278,8 @@ def band_reduce(banks, fqavby=1, tavby=1, op="sum", win=None, out=None, stream=N
     nb = len(banks)
     if out is None:
         out = fb_empty(nb * nco, ni, nto, device=banks[0].device)
+    if _dtype_code(out.dtype) != 0:
+        raise TypeError(f"out must be Float32, not {out.dtype}")
     if tuple(out.shape) != (nb * nco, ni, nto) or (
             out.numel() and out.stride() != (1, nb * nco, nb * nco * ni) and ni * nto > 1):
         raise ValueError("out must be a dense Julia-order (nbank*nco, ni, nto) tensor")
@@ -354,7 +361,7 @@ def kurtosis(x, win=None, stream=None):
     _check_bounds(win, shape)
     nc, ni, _ = window_shape(win, shape)
     out = torch.empty((ni, nc), dtype=torch.float64, device=x.device).t()
-    ptr, nchan, nif, ntime = _abi_dims(x)
+    ptr, nchan, nif, ntime = _abi_dims(x, allow_typed=True)
     keep, wp = _lib.win_arg(_full_win(win, shape))
     if x.dtype != torch.float32:  # StatsBase in Float64 for integer / Float64 rows
         rc = L.bldp_kurtosis(_dtype_code(x.dtype), ptr, nchan, nif, ntime, wp,

@@ -90,12 +90,15 @@ def fqav_range(r, n: int):
 
 
 def _host_generic(A: np.ndarray, n: int, f) -> np.ndarray:
-    """Reference semantics for an arbitrary Julia-style f(X; dims=1)."""
+    """Reference semantics for an arbitrary Julia-style f(X; dims=1): the
+    result is whatever f returns, in f's own element type (fqav returns
+    dropdims(f(reshape(A, ...); dims=1); dims=1), src/gbtworkerfunctions.jl:19:
+    e.g. median or std of an integer array is Float64)."""
     if A.shape[0] % n:
         raise _lib.DimensionMismatch(_lib.BLDP_EDIM,
                                      f"DimensionMismatch: fqavby={n} does not divide {A.shape[0]}")
     R = np.asarray(A).reshape((n, A.shape[0] // n) + A.shape[1:], order="F")
-    return np.asfortranarray(np.asarray(f(R, axis=0), dtype=A.dtype))
+    return np.asfortranarray(np.asarray(f(R, axis=0)))
 
 
 def fqav(A, n: int, f="sum"):

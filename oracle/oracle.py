@@ -355,21 +355,41 @@ def jl_sum_type(dt) -> np.dtype:
     return dt
 
 
+def np_jl_sum_f64(x: np.ndarray, axis: int = 0) -> np.ndarray:
+    """sum(x; dims=axis) of Float64 values as Julia's reducedim takes it:
+    R = zero(Float64), then R + Base.mapreduce_impl over the axis (pairwise
+    halves at ifirst + (ilast - ifirst) >> 1 down to pieces of <= 1024 summed in
+    sequence from their first element; Base/reducedim.jl `_mapreducedim!`,
+    Base/reduce.jl `mapreduce_impl`).  Axes of <= 16 take the other branch of
+    `_mapreducedim!` (r = zero; r += A[i] in sequence), which gives the same
+    value: 0.0 + a1 = a1 for every a1 but -0.0, and the final 0.0 + v below
+    settles that case the same way."""
+    x = np.moveaxis(np.asarray(x, dtype=np.float64), axis, -1)
+    shape = x.shape[:-1]
+    rows = x.reshape((-1, x.shape[-1]))
+    s = np_pairwise_sum_f64(rows) if rows.shape[0] else np.zeros(0)
+    return 0.0 + s.reshape(shape)
+
+
 def np_reduce_typed(a, fqavby=1, tavby=1, op="sum", win=None) -> np.ndarray:
     """fqav (src/gbtworkerfunctions.jl:16-20) fused with the time integration
     for a non-Float32 array, with Julia's result element types: integer sums
-    exact in (U)Int64 (wrapping), Float64 sums in the reference's order (the F
-    channels of a spectrum in sequence, spectrum after spectrum), mean = that
-    sum / (F T) in Float64, max / min in the input type."""
+    exact in (U)Int64 (wrapping); Float64 sums, and every mean, in the
+    reference's order: each spectrum's F channels summed as Julia's
+    sum(reshape(A, (F, :, ...)); dims=1) sums them (np_jl_sum_f64: pairwise
+    above 1024), then the T spectral sums of a time block the same way (the
+    time integration is fqav on axis 3); mean = that Float64
+    sum of the values converted to Float64 (Statistics.mean's
+    `_mean_promote`) / (F T); max / min in the input type."""
     w = np_window(np.asarray(a), win)
     F, T = max(int(fqavby), 1), max(int(tavby), 1)
     nc, ni, nt = w.shape
     if nc % F or nt % T:
         raise DimensionMismatch("factor does not divide window")
-    # (F, co, ni, T, to) -> (F*T, co, ni, to) with the channel fastest in a block
-    R = w.reshape((F, nc // F, ni, T, nt // T), order="F").transpose(0, 3, 1, 2, 4)
-    R = R.reshape((F * T, nc // F, ni, nt // T), order="F")
+    # (F, co, ni, T, to): channel group on axis 0, time block on axis 3
+    B = w.reshape((F, nc // F, ni, T, nt // T), order="F")
     if op in ("max", "min"):
+        R = B.transpose(0, 3, 1, 2, 4).reshape((F * T, nc // F, ni, nt // T), order="F")
         if R.shape[0] == 0 or R.size == 0:
             return np.asfortranarray(np.empty(R.shape[1:], dtype=w.dtype))
         m = R.max(axis=0) if op == "max" else R.min(axis=0)
@@ -377,13 +397,16 @@ def np_reduce_typed(a, fqavby=1, tavby=1, op="sum", win=None) -> np.ndarray:
             m = _fix_zero(m, R, 0, op)
         return np.asfortranarray(m.astype(w.dtype))
     st = jl_sum_type(w.dtype)
-    if st.kind == "f":  # sequential (np.add.accumulate is a sequential loop)
-        s = np.add.accumulate(R.astype(np.float64), axis=0)[-1] if R.shape[0] else \
-            np.zeros(R.shape[1:])
-    else:  # exact, wrapping modulo 2^64 like Julia's (U)Int64
-        s = R.astype(st).sum(axis=0, dtype=st)
-    if op == "mean":
-        return np.asfortranarray(s.astype(np.float64) / float(F * T))
+    if st.kind == "f" or op == "mean":
+        with np.errstate(over="ignore", invalid="ignore"):
+            spec = np_jl_sum_f64(B, axis=0)           # (co, ni, T, to)
+            s = np_jl_sum_f64(spec, axis=2)           # (co, ni, to)
+        if op == "mean":
+            return np.asfortranarray(s / float(F * T))
+        return np.asfortranarray(s)
+    # exact, wrapping modulo 2^64 like Julia's (U)Int64
+    R = B.reshape((F, nc // F, ni, T, nt // T), order="F").astype(st)
+    s = R.sum(axis=(0, 3), dtype=st)
     return np.asfortranarray(s.astype(st))
 
 

@@ -101,6 +101,47 @@ def test_reduce_typed_device_and_host(pkg, eng, orc, dt):
                 assert same(eng.reduce_host_typed(a, F, T, op, w), want), (dt, op, w, "host")
 
 
+@pytest.mark.parametrize("F,T", [(2048, 1), (4096, 2), (1500, 3), (8, 1100)])
+def test_reduce_float64_wide_groups_pairwise(pkg, eng, orc, F, T):
+    """Float64 sums (and integer means) of groups or time blocks longer than
+    1024 take Base.mapreduce_impl's pairwise halves (src/gbtworkerfunctions.jl:19),
+    bit for bit against the restatement pinned to Julia's loop
+    (tests/test_oracle.py::test_typed_float64_sum_order_pinned)."""
+    rng = np.random.default_rng(F + T)
+    nc, nt = 3 * F, 2 * T
+    b = np.asfortranarray(rng.standard_normal((nc, 1, nt)) * 1e8 + rng.standard_normal((nc, 1, nt)))
+    x = to_dev(eng, b)
+    for op in ("sum", "mean"):
+        want = orc.np_reduce_typed(b, F, T, op)
+        assert same(eng.fb_to_numpy(eng.reduce(x, F, T, op)), want), (F, T, op)
+        assert same(eng.reduce_host_typed(b, F, T, op), want), (F, T, op, "host")
+    big = np.asfortranarray(rng.integers(2**60, 2**62, (nc, 1, nt), dtype=np.int64))
+    want = orc.np_reduce_typed(big, F, T, "mean")
+    assert same(eng.fb_to_numpy(eng.reduce(to_dev(eng, big), F, T, "mean")), want), (F, T)
+    # a strided window: every other channel, reversed time
+    w = [0, F, 2, 0, 1, 1, nt - 1, T, -1]
+    assert same(eng.fb_to_numpy(eng.reduce(x, F, T, "sum", w)),
+                orc.np_reduce_typed(b, F, T, "sum", w)), (F, T, w)
+
+
+def test_f32_entry_points_reject_other_types(pkg, eng):
+    """Only reduce / kurtosis branch to the typed kernels; the Float32-only
+    entry points refuse other element types instead of reading them as
+    Float32."""
+    import torch
+
+    u = torch.zeros((256, 1, 8), dtype=torch.uint8, device="cuda")
+    x = u.permute(2, 1, 0).contiguous().permute(2, 1, 0)
+    for fn in (lambda: eng.band_reduce([x], 4, 1), lambda: eng.despike(x, 64),
+               lambda: eng.band_kurtosis([x]), lambda: eng.plan(x, 4, 1),
+               lambda: eng.kurtosis_plan(x)):
+        with pytest.raises(TypeError):
+            fn()
+    f = eng.fb_empty(256, 1, 8)
+    with pytest.raises(TypeError):
+        eng.band_reduce([f], 4, 1, out=eng.fb_empty(64, 1, 8, dtype=torch.float64))
+
+
 def test_reduce_typed_wraps_like_julia(pkg, eng, orc):
     """(U)Int64 sums wrap modulo 2^64, as Julia's do."""
     a = np.asfortranarray(np.full((8, 1, 2), np.iinfo(np.uint64).max, dtype=np.uint64))

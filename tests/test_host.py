@@ -65,6 +65,19 @@ def test_fqav_passthrough_and_generic_host(pkg):
         pkg.fqav(a, 3, np.median)
 
 
+def test_fqav_generic_keeps_f_result_type(pkg):
+    """fqav returns f(reshape(A, ...); dims=1) as f makes it
+    (src/gbtworkerfunctions.jl:19): median / std of an Int16 array are Float64
+    (Julia's Statistics), not truncated back to Int16."""
+    a = np.asfortranarray(np.array([1, 2, 4, 7, -3, 8, 10, 11], dtype=np.int16).reshape((8, 1, 1)))
+    med = pkg.fqav(a, 2, np.median)
+    assert med.dtype == np.float64
+    np.testing.assert_array_equal(med[:, 0, 0], [1.5, 5.5, 2.5, 10.5])
+    sd = pkg.fqav(a, 4, np.std)
+    assert sd.dtype == np.float64 and sd.shape == (2, 1, 1)
+    assert pkg.fqav(a.astype(np.float32), 2, np.median).dtype == np.float32
+
+
 def test_sigproc_roundtrip_and_header(pkg, tmp_path):
     rd = pkg.readers
     data = np.asfortranarray(np.random.default_rng(0).random((64, 2, 5)).astype(np.float32))

@@ -241,14 +241,56 @@ def test_typed_reduce_oracle_pinned(orc):
             for to in range(3):
                 blk = [int(a[co * F + k, i, to * T + t]) for t in range(T) for k in range(F)]
                 assert s[co, i, to] == sum(blk)
-                assert orc.np_reduce_typed(a, F, T, "mean")[co, i, to] == sum(blk) / (F * T)
+                assert orc.np_reduce_typed(a, F, T, "mean")[co, i, to] == \
+                    (float(sum(blk[:F])) + float(sum(blk[F:]))) / (F * T)
                 assert orc.np_reduce_typed(a, F, T, "max")[co, i, to] == max(blk)
     assert orc.np_reduce_typed(a, F, T, "max").dtype == np.uint8
-    b = np.asfortranarray(rng.standard_normal((8, 1, 4)))
-    sb = orc.np_reduce_typed(b, 4, 2, "sum")
-    acc = 0.0
-    for t in range(2):  # the channels of a spectrum in sequence, spectrum after spectrum
-        for k in range(4):
-            acc = acc + float(b[k, 0, t])
-    assert sb[0, 0, 0] == acc
     assert orc.np_reduce_typed(a.astype(np.int32), 3, 1, "sum").dtype == np.int64
+
+
+def py_jl_sum(v):
+    """sum(v) of Float64 values as Base's reducedim takes one slice: zero(T)
+    plus mapreduce_impl (pairwise_blocksize 1024), written as Base writes it."""
+    v = [float(x) for x in v]
+
+    def impl(ifirst, ilast):
+        if ifirst == ilast:
+            return v[ifirst]
+        if ilast - ifirst < 1024:
+            a = v[ifirst] + v[ifirst + 1]
+            for i in range(ifirst + 2, ilast + 1):
+                a = a + v[i]
+            return a
+        imid = ifirst + ((ilast - ifirst) >> 1)
+        return impl(ifirst, imid) + impl(imid + 1, ilast)
+
+    return 0.0 + impl(0, len(v) - 1) if v else 0.0
+
+
+@pytest.mark.parametrize("F,T", [(4, 2), (3, 1), (2048, 1), (4096, 2), (1500, 3), (5, 1100)])
+def test_typed_float64_sum_order_pinned(orc, F, T):
+    """Float64 fqav sums (and every typed mean) in Julia's order: each
+    spectrum's F channels by mapreduce_impl (pairwise above 1024,
+    src/gbtworkerfunctions.jl:19), then the T spectral sums of a time block the
+    same way (time integration = fqav on axis 3).  Literal loops vs the
+    vectorised restatement, bit for bit."""
+    rng = np.random.default_rng(F * 7 + T)
+    nco, nto = 2, 2
+    b = np.asfortranarray(rng.standard_normal((nco * F, 1, nto * T)) * 1e8 +
+                          rng.standard_normal((nco * F, 1, nto * T)))
+    sb = orc.np_reduce_typed(b, F, T, "sum")
+    mb = orc.np_reduce_typed(b, F, T, "mean")
+    for co in range(nco):
+        for to in range(nto):
+            spec = [py_jl_sum(b[co * F:(co + 1) * F, 0, to * T + t]) for t in range(T)]
+            want = py_jl_sum(spec)
+            assert sb[co, 0, to] == want, (F, T, co, to)
+            assert mb[co, 0, to] == want / (F * T)
+    # integers: exact (U)Int64 sums; means in Float64 over the converted values
+    # in the same order (sums beyond 2^53 round as Julia's do)
+    big = np.asfortranarray(rng.integers(2**60, 2**62, (nco * F, 1, nto * T), dtype=np.int64))
+    mi = orc.np_reduce_typed(big, F, T, "mean")
+    for co in range(nco):
+        for to in range(nto):
+            spec = [py_jl_sum(big[co * F:(co + 1) * F, 0, to * T + t]) for t in range(T)]
+            assert mi[co, 0, to] == py_jl_sum(spec) / (F * T)

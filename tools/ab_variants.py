@@ -214,7 +214,8 @@ def build(names):
             csrc, extra = patched_tree(n, v["patch"]), v.get("extra", "")
         else:
             csrc, extra = source_tree(v["rev"]), v["extra"]
-        subprocess.run(["make", "-s", "-B", "-C", csrc, f"OUT={out}", f"EXTRA={extra}"], check=True)
+        subprocess.run(["make", "-s", "-B", "-j8", "-C", csrc, f"OUT={out}", f"EXTRA={extra}"],
+                       check=True)
         print("built", out)
 
 
