@@ -21,7 +21,7 @@ KURT_PATHS = {0: "regs", 1: "mid", 2: "leaf", 3: "twopass"}
 
 BLDP_OK, BLDP_EINVAL, BLDP_EDIM, BLDP_EHIP, BLDP_ENOMEM, BLDP_EBOUNDS = 0, -1, -2, -3, -5, -6
 BLDP_ECOMM, BLDP_EIO = -7, -8
-ABI_VERSION = 2
+ABI_VERSION = 3
 BLDP_COMM_ID_BYTES = 128
 
 
@@ -62,12 +62,16 @@ SIGNATURES = {
     "bldp_finalize": ([], I),
     "bldp_host_register": ([P, SZ], I),
     "bldp_host_unregister": ([P], I),
+    "bldp_plan_option": ([ctypes.c_char_p, I64, P], I),
     "bldp_reduce_shape": ([I64, I64, I64, P, I64, I64, P], I),
     "bldp_reduce_plan_f32": ([P, I64, I64, I64, P, I64, I64, I, P, P], I),
     "bldp_reduce_f32": ([P, I64, I64, I64, P, I64, I64, I, P, P], I),
     "bldp_reduce_strided_f32": ([P, I64, I64, I64, P, I64, I64, I, P, I64, I64, P], I),
     "bldp_reduce_host_f32": ([I, P, I64, I64, I64, P, I64, I64, I, P], I),
     "bldp_band_reduce_f32": ([I, P, I64, I64, I64, P, I64, I64, I, P, P], I),
+    "bldp_band_reduce_prepare_f32": ([I, P, I64, I64, I64, P, I64, I64, I, P, P], I),
+    "bldp_reduce_launch": ([P, P], I),
+    "bldp_reduce_release": ([P], I),
     "bldp_band_reduce_multi_f32": ([I, P, P, I64, I64, I64, P, I64, I64, I, I, P], I),
     "bldp_stitch_f32": ([I, P, I64, I64, I64, P, P], I),
     "bldp_despike_f32": ([P, I64, I64, I64, I64, P], I),
@@ -130,6 +134,26 @@ def lib():
     return _lib
 
 
+class plan_option:
+    """Context manager forcing a plan option (bldp_plan_option) and restoring
+    it: ``with plan_option("row_split", 4): ...``; value -1 = the planner's
+    choice."""
+
+    def __init__(self, name: str, value: int):
+        self.name, self.value = name, int(value)
+
+    def __enter__(self):
+        prev = ctypes.c_int64()
+        check(lib().bldp_plan_option(self.name.encode(), self.value, ctypes.byref(prev)),
+              "bldp_plan_option")
+        self.prev = prev.value
+        return self
+
+    def __exit__(self, *exc):
+        check(lib().bldp_plan_option(self.name.encode(), self.prev, None), "bldp_plan_option")
+        return False
+
+
 def last_error() -> str:
     buf = ctypes.create_string_buffer(1024)
     lib().bldp_last_error(buf, len(buf))
@@ -160,7 +184,10 @@ def win_arg(win):
 
 
 def stream_ptr(stream=None) -> int:
-    """hipStream_t of a torch stream (default: torch's current stream)."""
+    """hipStream_t of a torch stream (default: torch's current stream); a raw
+    hipStream_t (int) passes through."""
+    if isinstance(stream, int):
+        return stream
     import torch
 
     s = stream if stream is not None else torch.cuda.current_stream()

@@ -14,6 +14,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <new>
 #include <string>
 #include <utility>
 #include <vector>
@@ -224,11 +225,12 @@ bool unaligned_vec_pays(int64_t F, bool rows16) {
 
 int valid_op(int op) { return op >= BLDP_OP_SUM && op <= BLDP_OP_MIN; }
 
-// Shared by every reduce entry point.
-int reduce_impl(int nbank, const float *const *in, int64_t nchan, int64_t nif, int64_t ntime,
-                const int64_t *win, int64_t fqavby, int64_t tavby, int op, float *out,
-                int64_t out_bank, int64_t out_ld_i, int64_t out_ld_t, bool stitched,
-                hipStream_t s, int64_t *info) {
+// Checks, window and plan of a reduce (shared by every reduce entry point and
+// by the prepared form): fills *a and *p; *empty when there is nothing to do.
+int prepare_reduce(int nbank, const float *const *in, int64_t nchan, int64_t nif, int64_t ntime,
+                   const int64_t *win, int64_t fqavby, int64_t tavby, int op, float *out,
+                   int64_t out_bank, int64_t out_ld_i, int64_t out_ld_t, bool stitched,
+                   bool query, RedArgs *ap, Plan *pp, bool *empty) {
   if (nbank < 1 || nbank > BLDP_MAX_BANKS)
     return fail(BLDP_EINVAL, "nbank=%d outside 1..%d", nbank, BLDP_MAX_BANKS);
   if (!valid_op(op)) return fail(BLDP_EINVAL, "unknown op %d (0=sum 1=mean 2=max 3=min)", op);
@@ -238,7 +240,8 @@ int reduce_impl(int nbank, const float *const *in, int64_t nchan, int64_t nif, i
   int64_t F, T;
   rc = resolve_factors(g, fqavby, tavby, &F, &T);
   if (rc) return rc;
-  RedArgs a{};
+  RedArgs &a = *ap;
+  a = RedArgs{};
   a.nco = g.nc / F;
   a.ni = g.ni;
   a.nto = g.nt / T;
@@ -259,7 +262,7 @@ int reduce_impl(int nbank, const float *const *in, int64_t nchan, int64_t nif, i
   a.in_ld_i = g.ld_i;
   a.in_ld_t = g.ld_t;
   a.out = out;
-  const bool empty = a.nco == 0 || a.ni == 0 || a.nto == 0;
+  *empty = a.nco == 0 || a.ni == 0 || a.nto == 0;
   bool rows16 = pitch_ok(g), words = true;
   if (!in) return fail(BLDP_EINVAL, "null input pointer array");
   for (int b = 0; b < nbank; ++b) {
@@ -270,16 +273,42 @@ int reduce_impl(int nbank, const float *const *in, int64_t nchan, int64_t nif, i
   const bool aligned = (rows16 && vec_ok(g)) ||
                        (BLDP_UNALIGNED_VEC >= 1 && words && g.cs == 1 &&
                         unaligned_vec_pays(F, rows16));
-  Plan p = plan_reduce(a, aligned, rows16, words && g.cs == 1, num_cus_current());
-  if (!info) {
+  *pp = plan_reduce(a, aligned, rows16, words && g.cs == 1, num_cus_current());
+  if (!query) {
     for (int b = 0; b < nbank; ++b)
-      if (!in[b] && !empty) return fail(BLDP_EINVAL, "null input pointer (bank %d)", b);
-    if (!out && !empty) return fail(BLDP_EINVAL, "null output pointer");
+      if (!in[b] && !*empty) return fail(BLDP_EINVAL, "null input pointer (bank %d)", b);
+    if (!out && !*empty) return fail(BLDP_EINVAL, "null output pointer");
   }
+  return BLDP_OK;
+}
+
+// Queue a prepared reduce on stream s (scratch leased for time-chunk partials).
+int run_reduce(RedArgs a, const Plan &p, int op, hipStream_t s) {
+  ScratchLease lease;  // held until the launches are queued
+  if (p.ws_bytes) {
+    int rc = scratch_lease(s, p.ws_bytes, &lease);
+    if (rc) return rc;
+    a.ws = (float *)lease.ptr;
+  }
+  hipError_t e = launch_reduce(a, p, op, s);
+  if (e != hipSuccess) return fail(BLDP_EHIP, "reduce launch: %s", hipGetErrorString(e));
+  return BLDP_OK;
+}
+
+int reduce_impl(int nbank, const float *const *in, int64_t nchan, int64_t nif, int64_t ntime,
+                const int64_t *win, int64_t fqavby, int64_t tavby, int op, float *out,
+                int64_t out_bank, int64_t out_ld_i, int64_t out_ld_t, bool stitched,
+                hipStream_t s, int64_t *info) {
+  RedArgs a;
+  Plan p;
+  bool empty = false;
+  int rc = prepare_reduce(nbank, in, nchan, nif, ntime, win, fqavby, tavby, op, out, out_bank,
+                          out_ld_i, out_ld_t, stitched, info != nullptr, &a, &p, &empty);
+  if (rc) return rc;
   if (info) {
     info[0] = p.path;
     info[1] = p.lpg;
-    info[2] = a.ts;
+    info[2] = p.path == PATH_VEC_ROW ? a.rsplit : a.ts;  // (k_reduce_rows: slices splitting T)
     info[3] = a.k4;
     info[4] = a.nchunk;
     info[5] = p.grid;
@@ -288,15 +317,7 @@ int reduce_impl(int nbank, const float *const *in, int64_t nchan, int64_t nif, i
     return BLDP_OK;  // plan query only
   }
   if (empty) return BLDP_OK;
-  ScratchLease lease;  // held until the launches are queued
-  if (p.ws_bytes) {
-    rc = scratch_lease(s, p.ws_bytes, &lease);
-    if (rc) return rc;
-    a.ws = (float *)lease.ptr;
-  }
-  hipError_t e = launch_reduce(a, p, op, s);
-  if (e != hipSuccess) return fail(BLDP_EHIP, "reduce launch: %s", hipGetErrorString(e));
-  return BLDP_OK;
+  return run_reduce(a, p, op, s);
 }
 
 }  // namespace
@@ -314,6 +335,15 @@ int bldp_last_error(char *buf, size_t len) {
 int bldp_device_count(int *n) {
   if (!n) return fail(BLDP_EINVAL, "null pointer");
   HIPCHK(hipGetDeviceCount(n));
+  return BLDP_OK;
+}
+
+int bldp_plan_option(const char *name, int64_t value, int64_t *previous) {
+  if (!name) return fail(BLDP_EINVAL, "null option name");
+  const int k = plan_opt_index(name);
+  if (k < 0) return fail(BLDP_EINVAL, "unknown plan option '%s'", name);
+  if (previous) *previous = plan_opt(k);
+  plan_opt_set(k, value < 0 ? -1 : value);
   return BLDP_OK;
 }
 
@@ -369,6 +399,53 @@ int bldp_band_reduce_f32(int nbank, const float *const *in, int64_t nchan, int64
                          int op, float *out, void *stream) {
   return reduce_impl(nbank, in, nchan, nif, ntime, win, fqavby, tavby, op, out, 0, 0, 0, true,
                      (hipStream_t)stream, nullptr);
+}
+
+// A prepared band reduce: the checks, window, plan and kernel arguments of
+// bldp_band_reduce_f32 computed once, so that a launch costs the host nothing
+// but the kernel launch itself (a worker re-reducing the same buffers, bench
+// loops).
+struct bldp_reduce_op {
+  RedArgs a;
+  Plan p;
+  int op;
+  int dev;
+  bool empty;
+};
+
+int bldp_band_reduce_prepare_f32(int nbank, const float *const *in, int64_t nchan, int64_t nif,
+                                 int64_t ntime, const int64_t *win, int64_t fqavby,
+                                 int64_t tavby, int op, float *out, bldp_reduce_op_t *handle) {
+  if (!handle) return fail(BLDP_EINVAL, "null handle pointer");
+  *handle = nullptr;
+  auto *h = new (std::nothrow) bldp_reduce_op{};
+  if (!h) return fail(BLDP_ENOMEM, "out of host memory");
+  int rc = prepare_reduce(nbank, in, nchan, nif, ntime, win, fqavby, tavby, op, out, 0, 0, 0,
+                          true, false, &h->a, &h->p, &h->empty);
+  if (rc == BLDP_OK && hipGetDevice(&h->dev) != hipSuccess)
+    rc = fail(BLDP_EHIP, "hipGetDevice failed");
+  if (rc) {
+    delete h;
+    return rc;
+  }
+  h->op = op;
+  *handle = h;
+  return BLDP_OK;
+}
+
+int bldp_reduce_launch(bldp_reduce_op_t h, void *stream) {
+  if (!h) return fail(BLDP_EINVAL, "null reduce handle");
+  if (h->empty) return BLDP_OK;
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess || dev != h->dev)
+    return fail(BLDP_EINVAL, "reduce handle prepared on device %d, current device %d", h->dev,
+                dev);
+  return run_reduce(h->a, h->p, h->op, (hipStream_t)stream);
+}
+
+int bldp_reduce_release(bldp_reduce_op_t h) {
+  delete h;
+  return BLDP_OK;
 }
 
 int bldp_band_reduce_multi_f32(int nbank, const int *bank_dev, const float *const *in,

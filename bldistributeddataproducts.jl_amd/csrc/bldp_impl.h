@@ -68,8 +68,18 @@ struct RedArgs {
   int64_t gpt;             // tile path: output channels (groups) per workgroup tile
   int32_t tpb;             // row path: time blocks per workgroup (k_reduce_rowt when > 1)
   int32_t tsub_log2;       // k_reduce_rowt: log2 of the time groups sharing a workgroup
+  int32_t rsplit;          // k_reduce_rows: slices of a workgroup splitting a block's rows (1 = k_reduce_row)
   float div;               // F*T, the mean divisor
 };
+
+// Runtime plan options (bldp_plan_option): process-wide overrides of the
+// planners' choices, for tests that enumerate every form of a plan and for
+// A/B timing in one process.  -1 = the planner's own choice.
+enum PlanOpt { OPT_ROW_SPLIT = 0, OPT_COUNT };
+int64_t plan_opt(int k);
+// name -> option index, or -1
+int plan_opt_index(const char *name);
+void plan_opt_set(int k, int64_t v);
 
 enum Path { PATH_VEC = 0, PATH_NARROW = 1, PATH_SCALAR = 2, PATH_TILE = 3, PATH_VEC_IL = 4,
             PATH_VEC_ROW = 5, PATH_NARROW_MIS = 6, PATH_LANE = 7 };

@@ -20,6 +20,9 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <atomic>
+#include <cstring>
+
 #include "bldp_impl.h"
 
 namespace bldp {
@@ -1218,6 +1221,74 @@ void k_reduce_row(const RedArgs a) {
            finish<OP>(s, a));
 }
 
+// k_reduce_row with a time block's rows split over S slices of the
+// workgroup (S = 2, 4; T a multiple of 16): 256 / S float4 columns per
+// workgroup, S times the workgroups.  A launch of one file (one 0002 bank at
+// fqavby = 64, tavby = 16: 1088 row tiles of 64 KiB on 256 CUs) otherwise
+// ends on a partial round of workgroups.  Slice s keeps k_reduce_row's
+// accumulators s*8/S .. (s+1)*8/S - 1, i.e. exactly the rows k_reduce_row adds
+// into them (row r of every 16-row batch goes to accumulator r % 8), in the
+// same order; slice 0 collects the others' accumulators through LDS and runs
+// k_reduce_row's folds, so the results are bit-identical to it.
+template <int OP, int G4, int S>
+__global__ __launch_bounds__(kBlock)
+#if BLDP_ROW_MAXWAVES > 0
+__attribute__((amdgpu_waves_per_eu(1, BLDP_ROW_MAXWAVES)))
+#endif
+void k_reduce_rows(const RedArgs a) {
+  constexpr int CW = kBlock / S;      // float4 columns per workgroup
+  constexpr int NA = kNacc / S;       // accumulators per slice
+  constexpr int RPB = 16 / S;         // rows per 16-row batch per slice
+  static_assert(kNacc == 8 && BLDP_ROW_BATCH == 16, "k_reduce_rows mirrors k_reduce_row's 16 x 8");
+  static_assert(CW >= 64 && G4 <= 64, "groups never straddle a wave");
+  const int tid = threadIdx.x;
+  const int sl = tid / CW, c = tid - sl * CW;  // slice (wave-uniform), column within the workgroup
+  const uint32_t it = blockIdx.y, ni = (uint32_t)a.ni;
+  const uint32_t to = it / ni, i = it - to * ni;
+  const int bank = blockIdx.z;
+  const int64_t col = (int64_t)blockIdx.x * CW + c;  // float4 column of the window
+  const bool valid = col < a.nco * G4;
+  const float id = R<OP>::id();
+  float4 acc[NA];
+#pragma unroll
+  for (int q = 0; q < NA; ++q) acc[q] = make_float4(id, id, id, id);
+  if (valid) {
+    // slice sl owns accumulators sl*NA .. sl*NA + NA - 1: rows
+    // 8h + sl*NA + q (h = 0, 1) of every 16-row batch
+    const float *p = a.in[bank] + a.in_off + (int64_t)i * a.in_ld_i +
+                     ((int64_t)to * a.T + sl * NA) * a.in_ld_t + 4 * col;
+    const int64_t ld = a.in_ld_t;
+    for (int64_t nb = a.T / 16; nb > 0; --nb) {
+      float4 v[RPB];
+#pragma unroll
+      for (int u = 0; u < RPB; ++u) v[u] = ld4(p + ((u / NA) * 8 + u % NA) * ld);
+      p += 16 * ld;
+#pragma unroll
+      for (int u = 0; u < RPB; ++u) acc[u % NA] = f4<OP>(acc[u % NA], v[u]);
+    }
+  }
+  __shared__ float4 xs[S - 1][NA][CW];
+  if (sl > 0) {
+#pragma unroll
+    for (int q = 0; q < NA; ++q) xs[sl - 1][q][c] = acc[q];
+  }
+  __syncthreads();
+  if (sl == 0) {
+    float4 all[kNacc];
+#pragma unroll
+    for (int q = 0; q < NA; ++q) all[q] = acc[q];
+#pragma unroll
+    for (int s2 = 1; s2 < S; ++s2)
+#pragma unroll
+      for (int q = 0; q < NA; ++q) all[s2 * NA + q] = xs[s2 - 1][q][c];
+    const float s = lanes_fold<OP, G4>(fold4<OP>(fold_acc<OP>(all)));
+    if (valid && (c & (G4 - 1)) == 0)
+      st1<1>(a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + (int64_t)to * a.out_ld_t +
+                 col / G4,
+             finish<OP>(s, a));
+  }
+}
+
 // The row path for short time blocks (T = 1, 2, 4: tavby = 1 is the
 // reference's own fqav, src/gbtworkerfunctions.jl:16-20, with no time
 // integration).  k_reduce_row gives every workgroup one time block, so at T = 1
@@ -1735,6 +1806,29 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
 #undef BLDP_ROWTN
     return hipGetLastError();
   }
+  if (p.path == PATH_VEC_ROW && a.rsplit > 1) {  // a block's rows over 2 / 4 slices
+    const dim3 g3((unsigned)a.blocks_c, (unsigned)(a.ni * a.nto), (unsigned)a.nbank);
+#define BLDP_ROWS(S)                                                                          \
+  switch (a.F / 4) {                                                                          \
+    case 1: hipLaunchKernelGGL((k_reduce_rows<OP, 1, S>), g3, block, 0, s, a); break;         \
+    case 2: hipLaunchKernelGGL((k_reduce_rows<OP, 2, S>), g3, block, 0, s, a); break;         \
+    case 4: hipLaunchKernelGGL((k_reduce_rows<OP, 4, S>), g3, block, 0, s, a); break;         \
+    case 8: hipLaunchKernelGGL((k_reduce_rows<OP, 8, S>), g3, block, 0, s, a); break;         \
+    case 16: hipLaunchKernelGGL((k_reduce_rows<OP, 16, S>), g3, block, 0, s, a); break;       \
+    case 32: hipLaunchKernelGGL((k_reduce_rows<OP, 32, S>), g3, block, 0, s, a); break;       \
+    case 64: hipLaunchKernelGGL((k_reduce_rows<OP, 64, S>), g3, block, 0, s, a); break;       \
+    default: return hipErrorInvalidValue;                                                     \
+  }
+    if (a.rsplit == 2) {
+      BLDP_ROWS(2)
+    } else if (a.rsplit == 4) {
+      BLDP_ROWS(4)
+    } else {
+      return hipErrorInvalidValue;
+    }
+#undef BLDP_ROWS
+    return hipGetLastError();
+  }
   if (p.path == PATH_VEC_ROW) {
     const dim3 g3((unsigned)a.blocks_c, (unsigned)(a.ni * a.nto), (unsigned)a.nbank);
     switch (a.F / 4) {
@@ -1809,6 +1903,19 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
 
 // ---------------------------------------------------------------------------
 
+namespace {
+std::atomic<int64_t> g_plan_opt[OPT_COUNT] = {{-1}};
+const char *const kPlanOptNames[OPT_COUNT] = {"row_split"};
+}  // namespace
+
+int64_t plan_opt(int k) { return g_plan_opt[k].load(std::memory_order_relaxed); }
+int plan_opt_index(const char *name) {
+  for (int k = 0; k < OPT_COUNT; ++k)
+    if (std::strcmp(name, kPlanOptNames[k]) == 0) return k;
+  return -1;
+}
+void plan_opt_set(int k, int64_t v) { g_plan_opt[k].store(v, std::memory_order_relaxed); }
+
 Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus) {
   Plan p{};
   const int64_t F = a.F, T = a.T;
@@ -1819,6 +1926,7 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
   a.k4 = 1;
   a.tpb = 1;
   a.tsub_log2 = 0;
+  a.rsplit = 1;
   if (BLDP_LANET && words && a.in_cs == 1 && (T == 1 || T == 2 || T == 4 || (BLDP_T38 && (T == 3 || T == 8))) &&
       (F == 3 || F == 5 || F == 6 || F == 7 || F == 12) && a.ni <= 65535 && a.nbank <= 65535 &&
       cdiv(a.nco + lanet_oalign_pad(), (int64_t)kBlock * lanet_cs((int)F)) *
@@ -1963,6 +2071,21 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
       p.path = PATH_VEC_ROW;
       a.blocks_c = bc;
       a.ntiles = a.blocks_c * a.ni * a.nto * a.nbank;
+      // small launches of whole 16-row batches: the block's rows split over
+      // 2 or 4 slices of the workgroup (k_reduce_rows), so that the launch
+      // does not end on a partial round of 64 KiB tiles
+      int64_t S = plan_opt(OPT_ROW_SPLIT);
+      if (T % 16 != 0) {
+        S = 1;
+      } else if (S < 0) {
+        S = 1;
+        while (S < 4 && a.ntiles * S < (int64_t)8 * num_cus) S *= 2;
+      }
+      if (S == 2 || S == 4) {
+        a.rsplit = (int32_t)S;
+        a.blocks_c = cdiv(a.nco * (F / 4), kBlock / S);
+        a.ntiles = a.blocks_c * a.ni * a.nto * a.nbank;
+      }
       p.grid = a.ntiles;
     }
   }

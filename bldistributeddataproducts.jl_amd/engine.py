@@ -20,7 +20,8 @@ from . import _lib
 from .idxs import window_shape
 
 __all__ = [
-    "fb_empty", "fb_from_numpy", "fb_to_numpy", "reduce", "band_reduce", "band_reduce_multi",
+    "fb_empty", "fb_from_numpy", "fb_to_numpy", "reduce", "band_reduce", "PreparedBandReduce",
+    "band_reduce_multi",
     "stitch",
     "despike", "kurtosis", "band_kurtosis", "synth", "plan", "reduce_host", "kurtosis_host",
     "init", "finalize", "pinned",
@@ -256,10 +257,8 @@ def plan(x, fqavby=1, tavby=1, op="sum", win=None) -> dict:
     return d
 
 
-def band_reduce(banks, fqavby=1, tavby=1, op="sum", win=None, out=None, stream=None):
-    """Reduce every bank of a band resident on ONE GPU and stitch them in bank
-    order (reduce(vcat, ...), src/gbt.jl:103) in a single launch."""
-    L = _lib.lib()
+def _band_args(banks, fqavby, tavby, win, out):
+    """Checks of a one-GPU band reduce; (banks, geometry, out, ptr array, window keepalive)."""
     banks = list(banks)
     if not banks:
         raise ValueError("no banks")
@@ -285,13 +284,59 @@ def band_reduce(banks, fqavby=1, tavby=1, op="sum", win=None, out=None, stream=N
         raise ValueError("out must be a dense Julia-order (nbank*nco, ni, nto) tensor")
     ptrs = (ctypes.c_void_p * nb)(*[b.data_ptr() for b in banks])
     keep, wp = _lib.win_arg(_full_win(win, shape))
+    return banks, geo, out, ptrs, (keep, wp)
+
+
+def band_reduce(banks, fqavby=1, tavby=1, op="sum", win=None, out=None, stream=None):
+    """Reduce every bank of a band resident on ONE GPU and stitch them in bank
+    order (reduce(vcat, ...), src/gbt.jl:103) in a single launch."""
+    L = _lib.lib()
+    banks, geo, out, ptrs, (keep, wp) = _band_args(banks, fqavby, tavby, win, out)
     nchan, nif, ntime = geo
-    rc = L.bldp_band_reduce_f32(nb, ctypes.cast(ptrs, ctypes.c_void_p), nchan, nif, ntime, wp,
-                                int(fqavby), int(tavby), _lib.OPS[op],
+    rc = L.bldp_band_reduce_f32(len(banks), ctypes.cast(ptrs, ctypes.c_void_p), nchan, nif, ntime,
+                                wp, int(fqavby), int(tavby), _lib.OPS[op],
                                 out.data_ptr() if out.numel() else None,
                                 _lib.stream_ptr(stream))
     _lib.check(rc, "bldp_band_reduce_f32")
     return out
+
+
+class PreparedBandReduce:
+    """band_reduce prepared once for fixed buffers (bldp_band_reduce_prepare_f32):
+    checks, plan and kernel arguments are computed here, and ``launch`` only
+    queues the kernel — one ctypes call, no Python-side work.  Results are
+    those of ``band_reduce`` with the same arguments.  The banks and ``out``
+    are kept alive by the object; ``close`` releases the handle."""
+
+    def __init__(self, banks, fqavby=1, tavby=1, op="sum", win=None, out=None):
+        L = _lib.lib()
+        banks, geo, out, ptrs, (keep, wp) = _band_args(banks, fqavby, tavby, win, out)
+        h = ctypes.c_void_p()
+        with _torch().cuda.device(banks[0].device):
+            rc = L.bldp_band_reduce_prepare_f32(len(banks), ctypes.cast(ptrs, ctypes.c_void_p),
+                                                *geo, wp, int(fqavby), int(tavby), _lib.OPS[op],
+                                                out.data_ptr() if out.numel() else None,
+                                                ctypes.byref(h))
+        _lib.check(rc, "bldp_band_reduce_prepare_f32")
+        self._L, self._h = L, h
+        self._fn = L.bldp_reduce_launch
+        self.banks, self.out = banks, out
+
+    def launch(self, stream=None) -> None:
+        """Queue the reduce on ``stream`` (a torch stream, a raw hipStream_t
+        int, or None for torch's current stream)."""
+        sp = stream if isinstance(stream, int) else _lib.stream_ptr(stream)
+        rc = self._fn(self._h, sp)
+        if rc:
+            _lib.check(rc, "bldp_reduce_launch")
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.bldp_reduce_release(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
 
 
 def band_reduce_multi(banks, fqavby=1, tavby=1, op="sum", win=None, root=0):

@@ -51,8 +51,10 @@ extern "C" {
 #endif
 
 /* 2: bldp_bslz4_decode_dev / _async take out_len (round 2); BLDP_EIO; the
- *    typed (non-Float32) entry points */
-#define BLDP_ABI_VERSION 2
+ *    typed (non-Float32) entry points
+ * 3: prepared band reduces (bldp_band_reduce_prepare_f32 / bldp_reduce_launch /
+ *    bldp_reduce_release) */
+#define BLDP_ABI_VERSION 3
 
 #if defined(BLDP_BUILD)
 #define BLDP_API __attribute__((visibility("default")))
@@ -103,12 +105,21 @@ BLDP_API int bldp_reduce_shape(int64_t nchan, int64_t nif, int64_t ntime, const 
                       int64_t fqavby, int64_t tavby, int64_t out_shape[3]);
 
 /* Introspection (tests/bench): the launch plan bldp_reduce_f32 would use for
- * these pointers.  info = {path (0 vector, 1 narrow, 2 scalar), lanes per
- * group, waves splitting T, float4 per lane per row, time chunks, workgroups,
- * workspace bytes, vector output stores}.  Launches nothing. */
+ * these pointers.  info = {path (0 vector, 1 narrow, 2 scalar, 3 tile,
+ * 4 interleaved, 5 row, 6 narrow_mis, 7 lane), lanes per group, waves (row
+ * path: workgroup slices) splitting T, float4 per lane per row, time chunks,
+ * workgroups, workspace bytes, vector output stores}.  Launches nothing. */
 BLDP_API int bldp_reduce_plan_f32(const float *in, int64_t nchan, int64_t nif, int64_t ntime,
                          const int64_t *win, int64_t fqavby, int64_t tavby, int op,
                          const float *out, int64_t info[8]);
+
+/* Process-wide plan options (tests and tuning): force one form of a plan the
+ * planner would otherwise choose by shape.  value -1 = the planner's choice
+ * (the default); *previous (may be NULL) receives the old value.  Options:
+ *   "row_split"  k_reduce_row's time block over 1, 2 or 4 slices of a
+ *                workgroup (whole 16-row batches only; bit-identical forms).
+ * Unknown names: BLDP_EINVAL. */
+BLDP_API int bldp_plan_option(const char *name, int64_t value, int64_t *previous);
 
 /* out[c', i, t'] = op over the F x T block of the window (device pointers).
  * out is dense (nco, ni, nto). */
@@ -137,6 +148,21 @@ BLDP_API int bldp_reduce_host_f32(int dev, const float *in, int64_t nchan, int64
 BLDP_API int bldp_band_reduce_f32(int nbank, const float *const *in, int64_t nchan, int64_t nif,
                          int64_t ntime, const int64_t *win, int64_t fqavby, int64_t tavby,
                          int op, float *out, void *stream);
+
+/* bldp_band_reduce_f32 prepared once for fixed buffers: the argument checks,
+ * window, launch plan and kernel arguments are computed here, so each
+ * bldp_reduce_launch only queues the kernel(s) on `stream` (same results as
+ * bldp_band_reduce_f32 with these arguments).  The handle is bound to the
+ * current device and to these pointers; the caller keeps them alive until
+ * bldp_reduce_release.  Same errors as bldp_band_reduce_f32 at prepare time;
+ * a launch from another current device is BLDP_EINVAL. */
+typedef struct bldp_reduce_op *bldp_reduce_op_t;
+BLDP_API int bldp_band_reduce_prepare_f32(int nbank, const float *const *in, int64_t nchan,
+                                          int64_t nif, int64_t ntime, const int64_t *win,
+                                          int64_t fqavby, int64_t tavby, int op, float *out,
+                                          bldp_reduce_op_t *handle);
+BLDP_API int bldp_reduce_launch(bldp_reduce_op_t handle, void *stream);
+BLDP_API int bldp_reduce_release(bldp_reduce_op_t handle);
 
 /* One process, one or more banks per GPU: bank b lives on
  * device bank_dev[b] (in[b] is a device pointer there).  Every device reduces

@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol(pkg, L):
     assert not missing, missing
     for s in declared_symbols():
         assert getattr(L, s) is not None
-    assert L.bldp_abi_version() == pkg._lib.ABI_VERSION == 2
+    assert L.bldp_abi_version() == pkg._lib.ABI_VERSION == 3
 
 
 def test_library_is_gfx950_code(pkg):
@@ -402,7 +402,7 @@ def test_runs_to_device_validates_before_any_read(pkg, L):
 # with the same return type and the same argument types, position by position.
 _C_TO_JL = {"int": "Cint", "int64_t": "Int64", "size_t": "Csize_t", "uint64_t": "UInt64",
             "uint32_t": "UInt32", "uint8_t": "UInt8", "char": "UInt8", "float": "Float32",
-            "double": "Float64", "void": "Cvoid"}
+            "double": "Float64", "void": "Cvoid", "bldp_reduce_op_t": "Ptr{Cvoid}"}
 
 
 def _c_param_to_jl(p):

@@ -1091,3 +1091,38 @@ def test_reduce_wide_groups_time_split(eng, orc, F, T):
     g = orc.gamma_bandpass(65536, 1, nt, 1024, 3 * T)
     got = host(eng, eng.reduce(dev(eng, g), F, T, "mean"))
     np.testing.assert_allclose(got, orc.reduce(g, F, T, "mean"), rtol=RTOL)
+
+
+@pytest.mark.parametrize("F", [4, 16, 64, 256])
+def test_row_split_forms_bit_identical(pkg, eng, orc, F):
+    """k_reduce_row and its row-split forms (k_reduce_rows, a time block's
+    16-row batches over 2 / 4 slices of a workgroup: the single-file launch
+    of the per-file getdata shape) give the same bits, for every op; integer
+    data matches the oracle exactly, gamma data within RTOL; partial last
+    column blocks, several banks, an IF axis and a stitched band."""
+    rng = np.random.default_rng(F)
+    # (shapes with >= 16 waves' worth of row tiles: fewer take the vector
+    # path's time split over waves instead of the row kernel)
+    for nc, ni, nt, T, nb in ((65536, 1, 272, 16, 1), (65536 + 4 * F, 8, 64, 32, 1),
+                              (65536, 1, 272, 16, 3)):
+        ints = [np.asfortranarray(rng.integers(0, 256, (nc, ni, nt)).astype(np.float32))
+                for _ in range(nb)]
+        gam = [orc.gamma_bandpass(nc, ni, nt, 64, 100 * F + k) for k in range(nb)]
+        for data, exact in ((ints, True), (gam, False)):
+            xs = [dev(eng, a) for a in data]
+            for op in ("sum", "mean", "max", "min"):
+                outs = {}
+                for S in (1, 2, 4):
+                    with pkg._lib.plan_option("row_split", S):
+                        pl = eng.plan(xs[0], F, T, op)
+                        assert pl["path"] == "row" and pl["time_split_waves"] == S, pl
+                        outs[S] = host(eng, eng.band_reduce(xs, F, T, op))
+                assert same_bits(outs[2], outs[1]) and same_bits(outs[4], outs[1]), (nc, F, T, op)
+                want = orc.stitch([orc.reduce(a, F, T, op) for a in data])
+                if exact or op in ("max", "min"):
+                    assert same_bits(outs[1], want), (nc, F, T, op)
+                else:
+                    np.testing.assert_allclose(outs[1], want, rtol=RTOL)
+    # the planner's own choice on one 0002 file at fqavby = 64, tavby = 16
+    x = dev(eng, np.zeros((65536, 1, 16), np.float32))
+    assert eng.plan(x, 64, 16)["time_split_waves"] in (2, 4)

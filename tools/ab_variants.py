@@ -83,6 +83,13 @@ VARIANTS = {
                                 "    if (wave == w) {\n      if (false) s = carry[lane];")]},
 }
 VARIANTS["kmid2min"] = {"patch": VARIANTS["kmid2f32"]["patch"] + VARIANTS["kmid2nochain"]["patch"]}
+# Runtime plan options (bldp_plan_option) on the base build: no rebuild, the
+# option is set around every call of the variant.
+VARIANTS.update({
+    "rows1": {"opts": {"row_split": 1}},  # k_reduce_row: one workgroup per time block
+    "rows2": {"opts": {"row_split": 2}},  # k_reduce_rows: block rows over 2 slices
+    "rows4": {"opts": {"row_split": 4}},
+})
 VARIANTS.update({
     "cap4ts": "-DBLDP_MAX_WG_PER_CU=-1",  # 4 WG/CU grid cap for time-split plans
     "plain": "-DBLDP_NT_LOADS=0 -DBLDP_NT_STORES=0 -DBLDP_MAX_WG_PER_CU=0",  # round-1 start
@@ -208,6 +215,8 @@ def build(names):
     for n in names:
         out = os.path.join(VDIR, f"libbldp_{n}.so")
         v = VARIANTS[n]
+        if isinstance(v, dict) and "opts" in v:
+            continue  # runtime plan option on the base build
         if isinstance(v, str):
             csrc, extra = CSRC, v
         elif "patch" in v:
@@ -241,7 +250,24 @@ def run(names, rounds, iters, suite="main"):
 
     pkg = entry.load_package()
     eng = pkg.engine
-    libs = {n: load(os.path.join(VDIR, f"libbldp_{n}.so")) for n in names}
+    def lib_path(n):
+        v = VARIANTS.get(n)
+        if isinstance(v, dict) and "opts" in v:
+            return os.path.join(VDIR, "libbldp_base.so")
+        return os.path.join(VDIR, f"libbldp_{n}.so")
+
+    libs = {n: load(lib_path(n)) for n in names}
+
+    def with_opts(n, L, fn):
+        v = VARIANTS.get(n)
+        opts = v.get("opts", {}) if isinstance(v, dict) else {}
+        for k, val in opts.items():
+            assert L.bldp_plan_option(k.encode(), val, None) == 0, k
+        try:
+            fn()
+        finally:
+            for k in opts:
+                L.bldp_plan_option(k.encode(), -1, None)
     stream = torch.cuda.current_stream()
     sp = int(stream.cuda_stream)
     cases = []
@@ -507,6 +533,22 @@ def run(names, rounds, iters, suite="main"):
         band_case("cfg2 F256 T2", b2, 256, 2, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
         band_case("cfg2 F64 T4", b2, 64, 4, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
         cases_done = True
+    elif suite == "rows":  # k_reduce_row with the time block split over workgroup slices
+        del b3
+        b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
+        w272 = [0, 65536, 1, 0, 1, 1, 0, 272, 1]
+        for F in (64, 16, 256, 4):
+            band_case(f"0002 file F{F} T16", b2[:1], F, 16, w272)
+        band_case("0002 file F64 T32", b2[:1], 64, 32, [0, 65536, 1, 0, 1, 1, 0, 256, 1])
+        band_case("0002 file F64 T48", b2[:1], 64, 48, [0, 65536, 1, 0, 1, 1, 0, 240, 1])
+        for nb in (2, 4, 8):
+            band_case(f"0002 {nb} files F64 T16", b2[:nb], 64, 16, w272)
+        band_case("0002 band F16 T16", b2, 16, 16, w272)
+        band_case("0002 band F256 T32", b2, 256, 32, [0, 65536, 1, 0, 1, 1, 0, 256, 1])
+        del b2
+        b4 = [eng.synth(512, 1, 880000, 8, seed=10 * b + 1, kind=0) for b in range(2)]
+        band_case("0001 1 bank F64 T16 (64k spectra)", b4[:1], 64, 16, [0, 512, 1, 0, 1, 1, 0, 65536, 1])
+        cases_done = True
     elif suite == "kmid":  # the register-tile kurtosis path (0002 products)
         del b3
         b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
@@ -568,13 +610,16 @@ def run(names, rounds, iters, suite="main"):
         for label, go, nbytes, out, _ in cases:
             for n in names:
                 L = libs[n]
-                go(L)  # warm
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
-                for _ in range(iters):
-                    go(L)
-                e1.record(stream)
-                e1.synchronize()
+
+                def timed():
+                    go(L)  # warm
+                    e0.record(stream)
+                    for _ in range(iters):
+                        go(L)
+                    e1.record(stream)
+                    e1.synchronize()
+                with_opts(n, L, timed)
                 ms = e0.elapsed_time(e1) / iters
                 res[label][n].append(ms)
                 if r == 0:
@@ -615,7 +660,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--suite", default="main", choices=["main", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy", "wide", "grid0", "grid1", "t38", "lane3", "kgrid", "lanetpack", "kshort", "kfile"])
+    ap.add_argument("--suite", default="main", choices=["main", "rows", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy", "wide", "grid0", "grid1", "t38", "lane3", "kgrid", "lanetpack", "kshort", "kfile"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:
