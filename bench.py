@@ -17,6 +17,8 @@ written, summed over banks.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg3]
     torchrun --nproc-per-node N bench.py --gpus N ...   (N > 1)
+    python bench.py --gpus N ...   (N > 1, no launcher: bench.py starts the N
+                                    rank processes itself, see spawn_ranks)
 """
 from __future__ import annotations
 
@@ -494,6 +496,60 @@ def bench_rawfile(args, eng, torch, pkg):
                                        "one thread"}}
 
 
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def spawn_ranks(n: int) -> int:
+    """`python bench.py --gpus N` without a launcher: start N rank processes of
+    this same command (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, one GPU
+    each) and wait for them.  Runs before anything imports torch or touches
+    HIP in this process, and starts children instead of re-exec'ing; rank 0
+    prints the JSON line.  Returns the exit status (the first failing rank's)."""
+    import subprocess
+
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rcs = [p.wait() for p in procs]
+    return next((rc for rc in rcs if rc), 0)
+
+
+def rendezvous_check(args, dist, rank, world):
+    """--mode rendezvous: the N-rank launch and exchange path without the GPU
+    (process group, barrier, max-over-ranks timing, rank 0's JSON line), so a
+    CPU-only machine can check the launch forms."""
+    import torch
+
+    dist.barrier()
+    t0 = time.perf_counter()
+    t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    g = [torch.zeros(1, dtype=torch.float64) for _ in range(world)] if rank == 0 else None
+    dist.gather(torch.tensor([float(rank)], dtype=torch.float64), g, dst=0)
+    dist.barrier()
+    el = time.perf_counter() - t0
+    r = {"metric": "bench launch rendezvous check (no GPU work)", "value": float(t[0]),
+         "unit": "ranks", "n_gpus": world, "steps": 0, "warmup": 0,
+         "ms_per_step": round(el * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+         "vs_baseline": None, "dtype": None, "data": "none",
+         "config": {"workload": "rendezvous", "world_size": dist.get_world_size(),
+                    "gathered_ranks": [int(x) for x in torch.cat(g)] if g else None,
+                    "dist_backend": dist.get_backend()}}
+    if rank == 0:
+        print(json.dumps(r), flush=True)
+    dist.destroy_process_group()
+    return r
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -503,7 +559,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", default="reduce",
-                    choices=["reduce", "kurtosis", "host", "decode", "file", "rawfile"])
+                    choices=["reduce", "kurtosis", "host", "decode", "file", "rawfile",
+                             "rendezvous"])
     ap.add_argument("--local-banks", type=int, default=None,
                     help="N=1 only: reduce just this many banks per launch, i.e. one rank's "
                          "share of an N-GPU run (for per-launch PMC profiles)")
@@ -519,19 +576,30 @@ def main():
                     help="N=1: run the N>1 exchange anyway (a one-rank process group, "
                          "RCCL gather + stitch of every step) to exercise it on one GPU")
     args = ap.parse_args()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher: this process only starts the N ranks (no torch, no HIP here)
+        sys.exit(spawn_ranks(args.gpus))
 
     import torch
     import torch.distributed as dist
 
-    import __graft_entry__ as entry
-
-    pkg = entry.load_package()
-    eng = pkg.engine
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.mode == "rendezvous":
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(free_port()))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+        dist.init_process_group("gloo")
+        return rendezvous_check(args, dist, rank, world)
+
+    import __graft_entry__ as entry
+
+    pkg = entry.load_package()
+    eng = pkg.engine
     local = local % max(1, torch.cuda.device_count())  # gloo rehearsal: ranks share GPUs
     torch.cuda.set_device(local)
     use_pg = world > 1 or args.pipeline

@@ -96,6 +96,7 @@ SIGNATURES = {
     "bldp_chunks_to_device": ([I, I64, P, P, P, P, I64, P, P, P, I64, P, I64, I64, P, P, P, P],
                               I),
     "bldp_runs_to_device": ([I, I64, P, P, P, I64, I64, I, P, P, P], I),
+    "bldp_file_runs_to_device": ([I64, P, P, P, P, I64, I64, I, P, P, P], I),
     "bldp_comm_id": ([P], I),
     "bldp_comm_init": ([I, I, I, P, P], I),
     "bldp_comm_destroy": ([P], I),

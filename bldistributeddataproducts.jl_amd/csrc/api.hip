@@ -164,6 +164,43 @@ int bldp::scratch_lease(hipStream_t s, size_t bytes, ScratchLease *lease) {
   return BLDP_OK;
 }
 
+namespace {
+// Staging of bldp_band_reduce_multi_f32's staged banks, one buffer per device
+// (kept apart from the per-stream scratch, which the reduces of the same call
+// may lease on the same stream).
+struct StageBuf {
+  std::mutex mu;
+  void *ptr = nullptr;
+  size_t bytes = 0;
+};
+std::mutex g_stage_mu;
+std::map<int, StageBuf> g_stage;
+
+// The current device's staging buffer of >= bytes, locked into *hold until
+// the caller drops the lock (callers synchronize their work before that).
+int staging_buffer(int dev, size_t bytes, void **ptr, std::vector<std::unique_lock<std::mutex>> *hold) {
+  StageBuf *sb;
+  {
+    std::lock_guard<std::mutex> lk(g_stage_mu);
+    sb = &g_stage[dev];
+  }
+  std::unique_lock<std::mutex> lk(sb->mu);
+  if (sb->bytes < bytes) {
+    if (sb->ptr) (void)hipFree(sb->ptr);  // (no work in flight: calls synchronize)
+    sb->ptr = nullptr;
+    sb->bytes = 0;
+    if (hipMalloc(&sb->ptr, bytes) != hipSuccess) {
+      sb->ptr = nullptr;
+      return fail(BLDP_ENOMEM, "staging allocation of %zu bytes on device %d failed", bytes, dev);
+    }
+    sb->bytes = bytes;
+  }
+  *ptr = sb->ptr;
+  hold->push_back(std::move(lk));
+  return BLDP_OK;
+}
+}  // namespace
+
 std::vector<int> bldp::scratch_devices() {
   std::lock_guard<std::mutex> lk(g_ws_mu);
   std::vector<int> d;
@@ -183,6 +220,17 @@ void bldp::scratch_release_all() {
     }
   }
   g_ws.clear();
+  {
+    std::lock_guard<std::mutex> lk(g_stage_mu);
+    for (auto &kv : g_stage) {
+      std::lock_guard<std::mutex> hold(kv.second.mu);
+      if (kv.second.ptr) {
+        (void)hipSetDevice(kv.first);
+        (void)hipFree(kv.second.ptr);
+      }
+    }
+    g_stage.clear();
+  }
   if (prev >= 0) (void)hipSetDevice(prev);
 }
 
@@ -473,7 +521,10 @@ int bldp_band_reduce_multi_f32(int nbank, const int *bank_dev, const float *cons
   int prev = 0;
   HIPCHK(hipGetDevice(&prev));
   std::vector<hipStream_t> streams(ndev, nullptr);
-  std::vector<float *> staging(nbank, nullptr);
+  // which banks write the root's product directly (same device, or peer
+  // access over xGMI) and which are reduced into staging on their own device
+  std::vector<char> direct(nbank, 0);
+  std::vector<int> nstaged(ndev, 0), slot(nbank, -1);
   rc = BLDP_OK;
   for (int b = 0; b < nbank && rc == BLDP_OK; ++b) {
     const int d = bank_dev[b];
@@ -482,28 +533,48 @@ int bldp_band_reduce_multi_f32(int nbank, const int *bank_dev, const float *cons
       rc = fail(BLDP_EHIP, "hipSetDevice(%d) failed", d);
       break;
     }
-    bool direct = d == root && !force_staged;
-    if (!direct && !force_staged) {  // kernels write the root's product over xGMI when peer access works
+    bool dir = d == root && !force_staged;
+    if (!dir && !force_staged) {
       int can = 0;
       if (hipDeviceCanAccessPeer(&can, d, root) == hipSuccess && can) {
         hipError_t pe = hipDeviceEnablePeerAccess(root, 0);
-        direct = pe == hipSuccess || pe == hipErrorPeerAccessAlreadyEnabled;
+        dir = pe == hipSuccess || pe == hipErrorPeerAccessAlreadyEnabled;
         (void)hipGetLastError();
       }
     }
+    direct[b] = dir;
+    if (!dir) slot[b] = nstaged[d]++;
+  }
+  // staging: a library-owned buffer per device (no allocation per call once
+  // it has grown), one slot per staged bank, held until every launch and copy
+  // of this call is done (the call synchronizes before it returns)
+  const size_t per = (size_t)(nco * ni * nto) * sizeof(float);
+  std::vector<std::unique_lock<std::mutex>> hold;
+  std::vector<void *> stage(ndev, nullptr);
+  for (int d = 0; d < ndev && rc == BLDP_OK; ++d)
+    if (nstaged[d]) {
+      if (hipSetDevice(d) != hipSuccess) {
+        rc = fail(BLDP_EHIP, "hipSetDevice(%d) failed", d);
+        break;
+      }
+      rc = staging_buffer(d, per * nstaged[d], &stage[d], &hold);
+    }
+  for (int b = 0; b < nbank && rc == BLDP_OK; ++b) {
+    const int d = bank_dev[b];
+    if (hipSetDevice(d) != hipSuccess) {
+      rc = fail(BLDP_EHIP, "hipSetDevice(%d) failed", d);
+      break;
+    }
     const float *ins[1] = {in[b]};
-    if (direct) {
+    if (direct[b]) {
       rc = reduce_impl(1, ins, nchan, nif, ntime, win, fqavby, tavby, op, out + b * nco, 0,
                        ld_i, ld_t, false, streams[d], nullptr);
     } else {  // reduce locally, then one strided peer copy into the bank's slot
-      if (hipMalloc(&staging[b], (size_t)(nco * ni * nto) * sizeof(float)) != hipSuccess) {
-        rc = fail(BLDP_ENOMEM, "staging allocation on device %d failed", d);
-        break;
-      }
-      rc = reduce_impl(1, ins, nchan, nif, ntime, win, fqavby, tavby, op, staging[b], 0, nco,
-                       nco * ni, false, streams[d], nullptr);
+      float *st = (float *)((char *)stage[d] + per * slot[b]);
+      rc = reduce_impl(1, ins, nchan, nif, ntime, win, fqavby, tavby, op, st, 0, nco, nco * ni,
+                       false, streams[d], nullptr);
       if (rc == BLDP_OK &&
-          hipMemcpy2DAsync(out + b * nco, ld_i * sizeof(float), staging[b], nco * sizeof(float),
+          hipMemcpy2DAsync(out + b * nco, ld_i * sizeof(float), st, nco * sizeof(float),
                            nco * sizeof(float), (size_t)(ni * nto), hipMemcpyDeviceToDevice,
                            streams[d]) != hipSuccess)
         rc = fail(BLDP_EHIP, "peer copy of bank %d failed", b);
@@ -514,11 +585,6 @@ int bldp_band_reduce_multi_f32(int nbank, const int *bank_dev, const float *cons
       (void)hipSetDevice(d);
       if (hipStreamSynchronize(streams[d]) != hipSuccess && rc == BLDP_OK)
         rc = fail(BLDP_EHIP, "device %d failed during the band reduce", d);
-    }
-  for (int b = 0; b < nbank; ++b)
-    if (staging[b]) {
-      (void)hipSetDevice(bank_dev[b]);
-      (void)hipFree(staging[b]);
     }
   (void)hipSetDevice(prev);
   return rc;

@@ -36,6 +36,7 @@ namespace {
 struct Piece {
   int64_t foff, hoff, len;
   int32_t batch;
+  int32_t fd;  // -1 = the job's fd
 };
 
 // One call's reads.  `left[b]` counts the pieces of batch b still unread.
@@ -126,7 +127,8 @@ class ReadPool {
       }
       int64_t got = 0;
       while (got < p.len && !j->err.load(std::memory_order_relaxed)) {
-        const ssize_t r = pread(j->fd, dst + got, (size_t)(p.len - got), p.foff + got);
+        const ssize_t r = pread(p.fd >= 0 ? p.fd : j->fd, dst + got, (size_t)(p.len - got),
+                                p.foff + got);
         if (r < 0 && errno == EINTR) continue;
         if (r <= 0) {
           int expect = 0;
@@ -302,7 +304,7 @@ static int chunks_to_device(
         ++q;
       }
       for (int64_t x = 0; x < n; x += piece)
-        j.pieces.push_back({f + x, h + x, std::min(piece, n - x), (int32_t)b});
+        j.pieces.push_back({f + x, h + x, std::min(piece, n - x), (int32_t)b, -1});
       k = q;
     }
     j.left[b].store((int64_t)(j.pieces.size() - first));
@@ -419,9 +421,12 @@ int ensure_slots(Slots &sl, int64_t bytes, int nslot) {
 
 }  // namespace
 
-static int runs_to_device(int fd, int64_t nrun, const int64_t *file_off, const int64_t *len,
-                          void *dev_dst, int64_t dst_bytes, int64_t slot_bytes, int nslot,
-                          void *copy_stream, void *stream, double *stats) {
+// fds: one descriptor per run (runs of several files in one stream of
+// batches), or NULL: every run is in `fd`.
+static int runs_to_device(int fd, const int *fds, int64_t nrun, const int64_t *file_off,
+                          const int64_t *len, void *dev_dst, int64_t dst_bytes,
+                          int64_t slot_bytes, int nslot, void *copy_stream, void *stream,
+                          double *stats) {
   const auto t0 = std::chrono::steady_clock::now();
   if (nrun < 0 || (nrun && (!file_off || !len || !dev_dst)) || slot_bytes < (1 << 20) ||
       nslot < 2 || nslot > 16)
@@ -430,6 +435,8 @@ static int runs_to_device(int fd, int64_t nrun, const int64_t *file_off, const i
   for (int64_t r = 0; r < nrun; ++r) {
     if (len[r] < 0 || file_off[r] < 0)
       return bldp::set_error(BLDP_EINVAL, "runs_to_device: negative offset or size");
+    if (fds && fds[r] < 0 && len[r] > 0)
+      return bldp::set_error(BLDP_EINVAL, "runs_to_device: run %lld has no file", (long long)r);
     total += len[r];
   }
   if (total > dst_bytes)
@@ -450,7 +457,7 @@ static int runs_to_device(int fd, int64_t nrun, const int64_t *file_off, const i
     while (x < len[r]) {
       const int64_t b = (pos + x) / slot_bytes;
       const int64_t n = std::min({piece, len[r] - x, (b + 1) * slot_bytes - (pos + x)});
-      j.pieces.push_back({file_off[r] + x, pos + x, n, (int32_t)b});
+      j.pieces.push_back({file_off[r] + x, pos + x, n, (int32_t)b, fds ? fds[r] : -1});
       j.left[b].fetch_add(1);
       x += n;
     }
@@ -546,7 +553,23 @@ extern "C" BLDP_API int bldp_runs_to_device(int fd, int64_t nrun, const int64_t 
                                             int64_t slot_bytes, int nslot, void *copy_stream,
                                             void *stream, double *stats) {
   try {
-    return runs_to_device(fd, nrun, file_off, len, dev_dst, dst_bytes, slot_bytes, nslot,
+    return runs_to_device(fd, nullptr, nrun, file_off, len, dev_dst, dst_bytes, slot_bytes,
+                          nslot, copy_stream, stream, stats);
+  } catch (const std::bad_alloc &) {
+    return bldp::set_error(BLDP_ENOMEM, "runs_to_device: out of host memory");
+  } catch (...) {
+    return bldp::set_error(BLDP_EINVAL, "runs_to_device: unexpected C++ exception");
+  }
+}
+
+extern "C" BLDP_API int bldp_file_runs_to_device(int64_t nrun, const int *fd,
+                                                 const int64_t *file_off, const int64_t *len,
+                                                 void *dev_dst, int64_t dst_bytes,
+                                                 int64_t slot_bytes, int nslot, void *copy_stream,
+                                                 void *stream, double *stats) {
+  if (nrun > 0 && !fd) return bldp::set_error(BLDP_EINVAL, "runs_to_device: null fd array");
+  try {
+    return runs_to_device(-1, fd, nrun, file_off, len, dev_dst, dst_bytes, slot_bytes, nslot,
                           copy_stream, stream, stats);
   } catch (const std::bad_alloc &) {
     return bldp::set_error(BLDP_ENOMEM, "runs_to_device: out of host memory");

@@ -53,7 +53,7 @@ extern "C" {
 /* 2: bldp_bslz4_decode_dev / _async take out_len (round 2); BLDP_EIO; the
  *    typed (non-Float32) entry points
  * 3: prepared band reduces (bldp_band_reduce_prepare_f32 / bldp_reduce_launch /
- *    bldp_reduce_release) */
+ *    bldp_reduce_release); bldp_plan_option; bldp_file_runs_to_device */
 #define BLDP_ABI_VERSION 3
 
 #if defined(BLDP_BUILD)
@@ -341,6 +341,15 @@ BLDP_API int bldp_runs_to_device(int fd, int64_t nrun, const int64_t *file_off,
                                  const int64_t *len, void *dev_dst, int64_t dst_bytes,
                                  int64_t slot_bytes, int nslot, void *copy_stream, void *stream,
                                  double *stats);
+
+/* bldp_runs_to_device over runs of several files: run r is in the open file
+ * fd[r] (the banks of a band read as one stream of batches into one device
+ * block: GBT.getband, src/gbt.jl:69-79,103).  Same batching, slots, streams
+ * and return as bldp_runs_to_device. */
+BLDP_API int bldp_file_runs_to_device(int64_t nrun, const int *fd, const int64_t *file_off,
+                                      const int64_t *len, void *dev_dst, int64_t dst_bytes,
+                                      int64_t slot_bytes, int nslot, void *copy_stream,
+                                      void *stream, double *stats);
 
 /* Gather a window (Julia order, dense (nc, ni, nt) out) from decoded chunks:
  * packed holds the chunks of a chunk-aligned bounding box back to back in

@@ -521,3 +521,26 @@ def test_file_metadata_cache_follows_rewrites(pkg, tmp_path):
     fb.write(p, dict(foff=-1.0, nfpc=8), np.zeros((128, 1, 4), np.float32, order="F"))
     assert fb.layout(p)["cdims"] == (4, 1, 128)
     assert fb.raw_layout(p) is not None
+
+
+def test_bench_spawns_its_ranks_without_a_launcher():
+    """`python bench.py --gpus N` with no torch.distributed.run: bench.py starts
+    the N rank processes itself (before touching torch or HIP), they meet over
+    127.0.0.1, and rank 0 alone prints the JSON line (the launch and exchange
+    path, no GPU work: --mode rendezvous)."""
+    import json
+    import subprocess
+    import sys
+
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2",
+                        "--dist-backend", "gloo", "--mode", "rendezvous"],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["world_size"] == 2
+    assert d["config"]["gathered_ranks"] == [0, 1] and d["value"] == 2.0
