@@ -514,10 +514,10 @@ int bldp_band_reduce_multi_f32(int nbank, const int *bank_dev, const float *cons
   if (nco * ni * nto == 0) return BLDP_OK;
   if (!out) return fail(BLDP_EINVAL, "null output pointer");
   const int64_t ld_i = (int64_t)nbank * nco, ld_t = ld_i * ni;
-  // BLDP_FORCE_STAGED=1 (tests): every bank takes the staged branch (local
+  // BLDP_FORCE_STAGED=1 or plan option "force_staged" = 1 (tests): every bank takes the staged branch (local
   // reduce + strided copy into the root's slot), even on the root device
   const char *fs = std::getenv("BLDP_FORCE_STAGED");
-  const bool force_staged = fs && fs[0] == '1';
+  const bool force_staged = (fs && fs[0] == '1') || plan_opt(OPT_FORCE_STAGED) == 1;
   int prev = 0;
   HIPCHK(hipGetDevice(&prev));
   std::vector<hipStream_t> streams(ndev, nullptr);

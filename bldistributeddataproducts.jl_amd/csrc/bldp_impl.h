@@ -75,7 +75,7 @@ struct RedArgs {
 // Runtime plan options (bldp_plan_option): process-wide overrides of the
 // planners' choices, for tests that enumerate every form of a plan and for
 // A/B timing in one process.  -1 = the planner's own choice.
-enum PlanOpt { OPT_ROW_SPLIT = 0, OPT_COUNT };
+enum PlanOpt { OPT_ROW_SPLIT = 0, OPT_FORCE_STAGED, OPT_COUNT };
 int64_t plan_opt(int k);
 // name -> option index, or -1
 int plan_opt_index(const char *name);

@@ -1904,17 +1904,22 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
 // ---------------------------------------------------------------------------
 
 namespace {
-std::atomic<int64_t> g_plan_opt[OPT_COUNT] = {{-1}};
-const char *const kPlanOptNames[OPT_COUNT] = {"row_split"};
+struct PlanOpts {
+  std::atomic<int64_t> v[OPT_COUNT];
+  PlanOpts() {
+    for (auto &x : v) x.store(-1);
+  }
+} g_plan_opt;
+const char *const kPlanOptNames[OPT_COUNT] = {"row_split", "force_staged"};
 }  // namespace
 
-int64_t plan_opt(int k) { return g_plan_opt[k].load(std::memory_order_relaxed); }
+int64_t plan_opt(int k) { return g_plan_opt.v[k].load(std::memory_order_relaxed); }
 int plan_opt_index(const char *name) {
   for (int k = 0; k < OPT_COUNT; ++k)
     if (std::strcmp(name, kPlanOptNames[k]) == 0) return k;
   return -1;
 }
-void plan_opt_set(int k, int64_t v) { g_plan_opt[k].store(v, std::memory_order_relaxed); }
+void plan_opt_set(int k, int64_t v) { g_plan_opt.v[k].store(v, std::memory_order_relaxed); }
 
 Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus) {
   Plan p{};
@@ -2060,12 +2065,21 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
       // <= 128 float4 columns: 2 or 4 time groups per workgroup (>= 64 lanes each)
       const int64_t cols = a.nco * (F / 4);
       a.tsub_log2 = BLDP_ROWT_PACK ? (cols <= 64 ? 2 : cols <= 128 ? 1 : 0) : 0;
-      // small launches: 8 rows per lane, twice the workgroups (BLDP_ROWT_SMALL)
+      // small launches: 8 rows per lane, twice the workgroups (BLDP_ROWT_SMALL);
+      // at T = 8 that is one time block per workgroup, i.e. k_reduce_row, whose
+      // 3-D grid must then hold (IF, time block) in y
       if (bc * cdiv(cdiv(a.nto, tpb), (int64_t)1 << a.tsub_log2) * a.ni * a.nbank <
-          (int64_t)BLDP_ROWT_SMALL * num_cus)
+              (int64_t)BLDP_ROWT_SMALL * num_cus &&
+          (8 / T > 1 || (bc <= INT32_MAX && a.ni * a.nto <= 65535)))
         tpb = 8 / T;
-      a.tpb = (int32_t)tpb;
-      a.ntiles = bc * cdiv(cdiv(a.nto, tpb), (int64_t)1 << a.tsub_log2) * a.ni * a.nbank;
+      if (tpb == 1) {  // k_reduce_row
+        a.tpb = 1;
+        a.tsub_log2 = 0;
+        a.ntiles = bc * a.ni * a.nto * a.nbank;
+      } else {
+        a.tpb = (int32_t)tpb;
+        a.ntiles = bc * cdiv(cdiv(a.nto, tpb), (int64_t)1 << a.tsub_log2) * a.ni * a.nbank;
+      }
       p.grid = a.ntiles;
     } else if (bc <= INT32_MAX && a.ni * a.nto <= 65535) {
       p.path = PATH_VEC_ROW;

@@ -339,9 +339,11 @@ class PreparedBandReduce:
         self.close()
 
 
-def band_reduce_multi(banks, fqavby=1, tavby=1, op="sum", win=None, root=0):
+def band_reduce_multi(banks, fqavby=1, tavby=1, op="sum", win=None, root=0, out=None):
     """One process, banks on several GPUs (bldp_band_reduce_multi_f32): each
-    GPU reduces its banks straight into the stitched product on `root`."""
+    GPU reduces its banks straight into the stitched product on `root` (into
+    ``out`` when given: a dense Julia-order (nbank*nco, ni, nto) Float32 tensor
+    there)."""
     torch = _torch()
     L = _lib.lib()
     banks = list(banks)
@@ -352,7 +354,14 @@ def band_reduce_multi(banks, fqavby=1, tavby=1, op="sum", win=None, root=0):
             raise ValueError("all banks of a band must have the same shape and layout")
     _check_bounds(win, shape)
     nco, ni, nto = out_shape(shape, win, fqavby, tavby)
-    out = fb_empty(len(banks) * nco, ni, nto, device=torch.device("cuda", root))
+    if out is None:
+        out = fb_empty(len(banks) * nco, ni, nto, device=torch.device("cuda", root))
+    elif (_dtype_code(out.dtype) != 0 or tuple(out.shape) != (len(banks) * nco, ni, nto)
+          or out.device != torch.device("cuda", root)
+          or (out.numel() and ni * nto > 1 and out.stride() != (1, len(banks) * nco,
+                                                                 len(banks) * nco * ni))):
+        raise ValueError("out must be a dense Julia-order (nbank*nco, ni, nto) Float32 tensor "
+                         "on the root device")
     devs = (ctypes.c_int * len(banks))(*[b.device.index for b in banks])
     ptrs = (ctypes.c_void_p * len(banks))(*[b.data_ptr() for b in banks])
     keep, wp = _lib.win_arg(_full_win(win, shape))

@@ -303,3 +303,55 @@ def window_to_device(path, base, jshape, win, device, timings=None):
     buf = read_runs_to_device(path, runs, device, timings)
     x = buf.view(dtype=__import__("torch").float32).view(dshape[2], dshape[1], dshape[0])
     return x.permute(2, 1, 0), dshape, rwin
+
+
+def files_to_device(paths, bases, runs0, dshape, device, timings=None):
+    """The same window of several raw files (a band's banks: identical
+    geometry, data block at ``bases[k]`` of ``paths[k]``) as one stream of
+    batches into one device buffer (bldp_file_runs_to_device): bank k's dense
+    block (``runs0`` of :func:`plan_window` relative to base 0, Julia shape
+    ``dshape``) at byte k * block.  Returns the banks' Julia-order Float32
+    views, in order.  The caller's current stream waits for the last copy."""
+    import ctypes
+    import time
+
+    import torch
+
+    from . import _lib
+
+    dev = torch.device(device)
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    runs0 = np.ascontiguousarray(runs0, np.int64)
+    per = int(runs0[:, 1].sum()) if len(runs0) else 0
+    n = len(paths)
+    out = torch.empty(n * per, dtype=torch.uint8, device=dev)
+    if per:
+        cs = _native_streams.get(dev.index)
+        if cs is None:
+            cs = _native_streams[dev.index] = torch.cuda.Stream(dev, priority=-1)
+        fds = []
+        try:
+            for pth in paths:
+                fds.append(os.open(pth, os.O_RDONLY))
+            nr = len(runs0)
+            fo = np.concatenate([runs0[:, 0] + int(b) for b in bases])
+            ln = np.tile(runs0[:, 1], n)
+            fd = np.repeat(np.asarray(fds, np.int32), nr)
+            stats = (ctypes.c_double * 4)()
+            t0 = time.perf_counter()
+            with torch.cuda.device(dev):
+                rc = _lib.lib().bldp_file_runs_to_device(
+                    len(ln), fd.ctypes.data, fo.ctypes.data, ln.ctypes.data, out.data_ptr(),
+                    out.numel(), BATCH_BYTES, NSLOTS, cs.cuda_stream, _lib.stream_ptr(), stats)
+        finally:
+            for f in fds:
+                os.close(f)
+        _lib.check(rc, "bldp_file_runs_to_device")
+        if timings is not None:
+            timings.update(read_call_ms=(time.perf_counter() - t0) * 1e3,
+                           first_copy_ms=stats[0], reads_ms=stats[1], bytes=n * per,
+                           pieces=int(stats[2]), threads=int(stats[3]))
+    nc, ni, nt = dshape
+    return [out[k * per:(k + 1) * per].view(torch.float32).view(nt, ni, nc).permute(2, 1, 0)
+            for k in range(n)]

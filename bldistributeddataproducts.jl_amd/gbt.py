@@ -132,35 +132,117 @@ def bandaxis(headers, idxs=(COLON, COLON, COLON), fqavby=1):
     return np.concatenate([p.values() for p in parts])
 
 
-def _bank_shape(f):
-    """(nchan, nif, ntime) of a bank: an in-memory array / tensor, or a file's
-    header (src/gbtworkerfunctions.jl:131-159)."""
+def _bank_geometry(f):
+    """(kind, Julia shape, data offset) of a bank, from the per-file layout
+    the read itself uses (cached per file version: one libhdf5 open per file,
+    not one for the header and another for the data):
+    "raw" = an uncompressed contiguous FBH5 ``data`` block or a 32-bit SIGPROC
+    data block at that offset (read by preads); "h5" = another FBH5 layout;
+    "other" = anything else, shape from the header
+    (src/gbtworkerfunctions.jl:131-159); "array" = an in-memory array/tensor."""
     if not isinstance(f, (str, bytes)) and not hasattr(f, "__fspath__"):
-        return tuple(int(n) for n in f.shape)
+        return "array", tuple(int(n) for n in f.shape), None
+    from . import fbh5
+
+    if readers.ishdf5(f):
+        raw = fbh5.raw_layout(f)
+        if raw is not None:
+            return "raw", tuple(int(n) for n in raw[1]), int(raw[0])
+        cd = fbh5.layout(f)["cdims"]
+        if len(cd) == 3:
+            return "h5", tuple(int(n) for n in cd[::-1]), None
+    else:
+        raw = readers.fil_raw_layout(f)
+        if raw is not None:
+            return "raw", tuple(int(n) for n in raw[1]), int(raw[0])
     h = readers.getheader(f)
-    return int(h["nchans"]), int(h.get("nifs", 1)), int(h["nsamps"])
+    return "other", (int(h["nchans"]), int(h.get("nifs", 1)), int(h["nsamps"])), None
 
 
-def _band_on_device(ws, fs, idxs, fqavby, op, tavby, nfpc):
+def _bank_shape(f):
+    """(nchan, nif, ntime) of a bank (see _bank_geometry)."""
+    return _bank_geometry(f)[1]
+
+
+def _band_raw(ws, fs, geo, idxs, fqavby, op, tavby, band, root, force_copy, tm):
+    """Every bank a raw file of one geometry: each GPU reads its banks' windows
+    as ONE stream of batches (bldp_file_runs_to_device: preads of every file
+    into the pinned slot ring, H2D copies overlapping the reads) into one
+    buffer, then the band is reduced straight into its vcat slots: one launch
+    on the root (bldp_band_reduce_f32), or, with banks on several GPUs, each
+    GPU's kernels writing the root's slots over xGMI
+    (bldp_band_reduce_multi_f32)."""
+    import time
+
+    import torch
+
+    from . import engine, filestream
+    from .idxs import to_window
+
+    jshape = geo[0][1]
+    win = to_window(idxs, jshape) or [0, jshape[0], 1, 0, jshape[1], 1, 0, jshape[2], 1]
+    runs0, dshape, rwin = filestream.plan_window(jshape, win, 0)
+    groups = {}
+    for b, w in enumerate(ws):
+        groups.setdefault(int(w), []).append(b)
+    views = [None] * len(fs)
+
+    def read(item):
+        dev, bl = item
+        t = {}
+        t0 = time.perf_counter()
+        with torch.cuda.device(dev):
+            vs = filestream.files_to_device([fs[b] for b in bl], [geo[b][2] for b in bl], runs0,
+                                            dshape, f"cuda:{dev}", timings=t)
+        for b, v in zip(bl, vs):
+            views[b] = v
+        t["group_ms"] = (time.perf_counter() - t0) * 1e3
+        return dev, t
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(max_workers=len(groups)) as ex:  # one reader per GPU
+        tread = dict(ex.map(read, groups.items()))
+    tm["read"] = {str(d): t for d, t in tread.items()}
+    tm["read_ms"] = (time.perf_counter() - t0) * 1e3
+    t1 = time.perf_counter()
+    if list(groups) == [root] and not force_copy:
+        with torch.cuda.device(root):
+            engine.band_reduce(views, fqavby, tavby, op, rwin, out=band)
+        tm["reduce"] = "bldp_band_reduce_f32 (one launch)"
+    else:
+        from . import _lib
+
+        with _lib.plan_option("force_staged", 1 if force_copy else -1):
+            engine.band_reduce_multi(views, fqavby, tavby, op, rwin, root=root, out=band)
+        tm["reduce"] = "bldp_band_reduce_multi_f32" + (" (staged)" if force_copy else "")
+    tm["reduce_queue_ms"] = (time.perf_counter() - t1) * 1e3
+
+
+def _band_on_device(ws, fs, idxs, fqavby, op, tavby, nfpc, timings=None):
     """One band stitched on the GPU (src/gbt.jl:103): every
     bank is read and reduced on its worker's GPU straight into its vcat slot
-    of the band product on the first worker's GPU (a bank on another GPU is
-    reduced there and its result copied into the slot), the DC-spike patch
-    runs on the stitched product in place (src/gbt.jl:101-102,111), and the
-    band crosses PCIe once.  None when the banks' products differ in shape or
-    are not Float32: the caller then concatenates on the host."""
+    of the band product on the first worker's GPU, the DC-spike patch runs on
+    the stitched product in place (src/gbt.jl:101-102,111), and the band
+    crosses PCIe once.  Banks that are all raw files of one geometry take
+    _band_raw (one read stream per GPU, one reduce); others go bank by bank
+    (a bank on another GPU is reduced there and its result copied into the
+    slot).  None when the banks' products differ in shape or are not Float32:
+    the caller then concatenates on the host.  ``timings``: a dict that
+    receives the host timeline (ms)."""
     import os
+    import time
 
     import torch
 
     from . import engine
     from .idxs import sanitizeidxs, to_window
 
+    tm = timings if timings is not None else {}
+    t0 = time.perf_counter()
     idxs = sanitizeidxs(idxs)
-    shapes = []
-    for f in fs:
-        shape = _bank_shape(f)
-        shapes.append(engine.out_shape(shape, to_window(idxs, shape), fqavby, tavby))
+    geo = [_bank_geometry(f) for f in fs]
+    shapes = [engine.out_shape(g[1], to_window(idxs, g[1]), fqavby, tavby) for g in geo]
+    tm["geometry_ms"] = (time.perf_counter() - t0) * 1e3
     if len(set(shapes)) != 1 or 0 in shapes[0]:
         return None
     nco, ni, nto = shapes[0]
@@ -169,30 +251,61 @@ def _band_on_device(ws, fs, idxs, fqavby, op, tavby, nfpc):
     # BLDP_BAND_FORCE_COPY=1 takes the other-GPU branch (reduce, then copy into
     # the slot) for every bank: how a one-GPU box tests it
     force_copy = os.environ.get("BLDP_BAND_FORCE_COPY", "0") == "1"
+    raw = (all(g[0] == "raw" for g in geo) and len({g[1] for g in geo}) == 1
+           and os.environ.get("BLDP_NATIVE_READ", "1") != "0")
+    if raw:
+        _band_raw(ws, fs, geo, idxs, fqavby, op, tavby, band, root, force_copy, tm)
+    else:
+        def bank(b):
+            slot = band[b * nco:(b + 1) * nco]
+            dev = int(ws[b])
+            if dev == root and not force_copy:
+                return W.getdata_device(fs[b], idxs, fqavby, op, tavby, device=dev, out=slot)
+            r = W.getdata_device(fs[b], idxs, fqavby, op, tavby, device=dev)
+            if r is not None:
+                with torch.cuda.device(dev):
+                    torch.cuda.current_stream().synchronize()
+                with torch.cuda.device(root):
+                    slot.copy_(r)
+            return r
 
-    def bank(b):
-        slot = band[b * nco:(b + 1) * nco]
-        dev = int(ws[b])
-        if dev == root and not force_copy:
-            return W.getdata_device(fs[b], idxs, fqavby, op, tavby, device=dev, out=slot)
-        r = W.getdata_device(fs[b], idxs, fqavby, op, tavby, device=dev)
-        if r is not None:
-            with torch.cuda.device(dev):
-                torch.cuda.current_stream().synchronize()
-            with torch.cuda.device(root):
-                slot.copy_(r)
-        return r
-
-    with ThreadPoolExecutor(max_workers=max(1, nb)) as ex:  # @spawnat per bank
-        got = list(ex.map(bank, range(nb)))
+        t1 = time.perf_counter()
+        with ThreadPoolExecutor(max_workers=max(1, nb)) as ex:  # @spawnat per bank
+            got = list(ex.map(bank, range(nb)))
+        tm["banks_ms"] = (time.perf_counter() - t1) * 1e3
+        if any(r is None for r in got):
+            return None
+    t2 = time.perf_counter()
     for d in sorted({int(w) for w in ws}):
         torch.cuda.synchronize(d)
-    if any(r is None for r in got):
-        return None
+    tm["sync_ms"] = (time.perf_counter() - t2) * 1e3
     with torch.cuda.device(root):
+        t3 = time.perf_counter()
         if nfpc:
             engine.despike(band, nco // 64 if nfpc is True else int(nfpc))
-        return engine.fb_to_numpy(band)  # the one device -> host copy
+        out = engine.fb_to_numpy(band)  # the one device -> host copy
+        tm["despike_d2h_ms"] = (time.perf_counter() - t3) * 1e3
+    tm["path"] = "raw band" if raw else "bank by bank"
+    tm["total_ms"] = (time.perf_counter() - t0) * 1e3
+    return out
+
+
+def _despike_host(d: np.ndarray, nfpc: int) -> np.ndarray:
+    """d[spike:nfpc:end, :, :] .= d[spike-1:nfpc:end, :, :] with
+    spike = nfpc÷2 + 1 (src/gbt.jl:101-102,111) on a host array of any element
+    type, in place; the errors of bldp_despike_f32."""
+    from . import _lib
+
+    if nfpc < 2:
+        raise _lib.BoundsError(_lib.BLDP_EBOUNDS, f"BoundsError: nfpc={nfpc} < 2")
+    sp = nfpc // 2  # 0-based spike bin
+    dst, src = d[sp::nfpc], d[sp - 1::nfpc]
+    if dst.shape[0] != src.shape[0]:
+        raise _lib.DimensionMismatch(_lib.BLDP_EDIM,
+                                     f"DimensionMismatch: {dst.shape[0]} spike bins vs "
+                                     f"{src.shape[0]} source bins (nchan={d.shape[0]}, nfpc={nfpc})")
+    d[sp::nfpc] = src.copy()
+    return d
 
 
 def getband(workers, fnames, idxs=(COLON, COLON, COLON), fqavby=1, fqavfunc="sum", tavby=1,
@@ -234,10 +347,13 @@ def getband(workers, fnames, idxs=(COLON, COLON, COLON), fqavby=1, fqavfunc="sum
             nfpc = parts[0].shape[0] // 64  # size(ds[1], 1) ÷ 64
         band = np.asfortranarray(np.concatenate(parts, axis=0))
         if nfpc:
-            from . import engine
+            if band.dtype == np.float32:
+                from . import engine
 
-            x = engine.fb_from_numpy(band, device=f"cuda:{int(ws[0])}")
-            band = engine.fb_to_numpy(engine.despike(x, nfpc))
+                x = engine.fb_from_numpy(band, device=f"cuda:{int(ws[0])}")
+                band = engine.fb_to_numpy(engine.despike(x, nfpc))
+            else:  # other result types (integer sums, Float64) keep their type
+                band = _despike_host(band, int(nfpc))
         bands[j] = band
     if freqs:
         axes = [bandaxis(getheaders(ws, fs), idxs, fqavby) for ws, fs in zip(wcol, fcol)]

@@ -116,8 +116,11 @@ BLDP_API int bldp_reduce_plan_f32(const float *in, int64_t nchan, int64_t nif, i
 /* Process-wide plan options (tests and tuning): force one form of a plan the
  * planner would otherwise choose by shape.  value -1 = the planner's choice
  * (the default); *previous (may be NULL) receives the old value.  Options:
- *   "row_split"  k_reduce_row's time block over 1, 2 or 4 slices of a
- *                workgroup (whole 16-row batches only; bit-identical forms).
+ *   "row_split"     k_reduce_row's time block over 1, 2 or 4 slices of a
+ *                   workgroup (whole 16-row batches only; bit-identical forms).
+ *   "force_staged"  1: bldp_band_reduce_multi_f32 takes its staged branch
+ *                   (reduce on the bank's device, then a strided copy into
+ *                   the slot) for every bank, the root's included.
  * Unknown names: BLDP_EINVAL. */
 BLDP_API int bldp_plan_option(const char *name, int64_t value, int64_t *previous);
 

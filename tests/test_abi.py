@@ -105,9 +105,27 @@ def test_launch_plans_host_only(pkg, L):
     assert plan(pkg, L, A, 1 << 26, 1, 16, 4096, 16)[0] == 4
     assert plan(pkg, L, A, 1 << 26, 1, 16, 8192, 16)[0] == 0
     assert plan(pkg, L, A, 4096, 1, 4096, 1024, 4096)[0] == 0
-    # cfg1: F=64 -> 16 lanes per group, one float4 each: the row kernel
-    p = plan(pkg, L, A, 65536, 1, 279, 64, 16, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
-    assert p[0] == 5 and p[1] == 16 and p[3] == 1 and p[5] == 64 * 17
+    # cfg1: F=64 -> 16 lanes per group, one float4 each: the row kernel; one
+    # file is a small launch, so each 16-row block is split over 2 workgroup
+    # slices (k_reduce_rows: 512 channels per workgroup); forced forms
+    w272 = [0, 65536, 1, 0, 1, 1, 0, 272, 1]
+    p = plan(pkg, L, A, 65536, 1, 279, 64, 16, w272)
+    assert p[0] == 5 and p[1] == 16 and p[2] == 2 and p[3] == 1 and p[5] == 128 * 17
+    for S, wg in ((1, 64 * 17), (2, 128 * 17), (4, 256 * 17)):
+        with pkg._lib.plan_option("row_split", S):
+            p = plan(pkg, L, A, 65536, 1, 279, 64, 16, w272)
+            assert p[0] == 5 and p[2] == S and p[5] == wg, (S, p)
+    # tavby = 9 (no whole 16-row batch): k_reduce_row, whatever the option says
+    with pkg._lib.plan_option("row_split", 4):
+        p = plan(pkg, L, A, 65536, 1, 279, 64, 9, [0, 65536, 1, 0, 1, 1, 0, 270, 1])
+        assert p[0] == 5 and p[2] == 1
+    with pytest.raises(pkg._lib.ArgumentError):
+        pkg._lib.check(L.bldp_plan_option(b"no_such_option", 1, None))
+    # a small launch at tavby = 8: one 8-row block per workgroup (k_reduce_row)
+    # where its grid holds the time blocks, else k_reduce_rowt
+    assert plan(pkg, L, A, 65536, 1, 279, 64, 8, w272)[5] == 64 * 34
+    p = plan(pkg, L, A, 256, 1, 8 * 70000, 4, 8)
+    assert p[0] == 5 and p[5] == -(-70000 // 2 // 4)
     # too few tiles for one wave per tile: waves split time, generic kernel
     assert plan(pkg, L, A, 4096, 1, 64, 64, 16)[0] == 0
     # cfg4: narrow channel, long time -> time split waves and/or chunks

@@ -1126,3 +1126,22 @@ def test_row_split_forms_bit_identical(pkg, eng, orc, F):
     # the planner's own choice on one 0002 file at fqavby = 64, tavby = 16
     x = dev(eng, np.zeros((65536, 1, 16), np.float32))
     assert eng.plan(x, 64, 16)["time_split_waves"] in (2, 4)
+
+
+def test_rowt_small_launch_tavby8_long_narrow_window(eng, orc):
+    """A small launch at tavby = 8 on a narrow window (256 channels) with more
+    than 65535 time blocks: the 8-rows-per-lane downgrade would be
+    k_reduce_row, whose grid y (IF x time block) cannot hold them, so the
+    plan keeps k_reduce_rowt; the result matches the oracle."""
+    rng = np.random.default_rng(8)
+    nto = 70000
+    a = np.asfortranarray(rng.integers(0, 256, (256, 1, 8 * nto)).astype(np.float32))
+    x = dev(eng, a)
+    for F in (4, 64):
+        got = host(eng, eng.reduce(x, F, 8))
+        assert same_bits(got, orc.reduce(a, F, 8)), F
+    # and where the grid does hold them, T = 8 on a small launch is k_reduce_row
+    b = np.asfortranarray(rng.integers(0, 256, (65536, 1, 272)).astype(np.float32))
+    y = dev(eng, b)
+    assert eng.plan(y, 64, 8)["path"] == "row"
+    assert same_bits(host(eng, eng.reduce(y, 64, 8)), orc.reduce(b, 64, 8))

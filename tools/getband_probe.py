@@ -47,16 +47,19 @@ def main():
     workers = [0] * 8
     C = pkg.COLON
     cases = [("F64 T1", dict(fqavby=64)), ("F64 T1 despike", dict(fqavby=64, despike_nfpc=16)),
-             ("F1 T1 despike", dict(despike_nfpc=1024)), ("F64 T9", dict(fqavby=64, tavby=9))]
+             ("F1 T1 despike", dict(despike_nfpc=1024)), ("F64 T9", dict(fqavby=64, tavby=9)),
+             ("F64 T16 (cfg2 window 1:272)", dict(fqavby=64, tavby=16, idxs=(C, C, pkg.JRange(1, 272))))]
     res = {}
     for label, kw in cases:
         out = {}
+        kw = dict(kw)
+        idxs = kw.pop("idxs", (C, C, C))
         for mode in ("host", "device"):
-            G.getband(workers, names, (C, C, C), stitch=mode, **kw)  # warm (page cache, plans)
+            G.getband(workers, names, idxs, stitch=mode, **kw)  # warm (page cache, plans)
             ts = []
             for _ in range(a.reps):
                 t0 = time.perf_counter()
-                band = G.getband(workers, names, (C, C, C), stitch=mode, **kw)
+                band = G.getband(workers, names, idxs, stitch=mode, **kw)
                 ts.append((time.perf_counter() - t0) * 1e3)
             ts.sort()
             out[mode] = {"median_ms": round(ts[len(ts) // 2], 3), "min_ms": round(ts[0], 3),
@@ -64,8 +67,15 @@ def main():
             out[mode + "_band"] = band
         same = bool(np.array_equal(out["host_band"].view(np.uint32),
                                    out["device_band"].view(np.uint32)))
+        # the device path's host timeline of one more call (ms per stage)
+        tm = {}
+        G._band_on_device(workers, names, idxs, kw.get("fqavby", 1), "sum", kw.get("tavby", 1),
+                          kw.get("despike_nfpc"), timings=tm)
+        nbytes = 8 * 4 * a.nchan * a.ntime
         res[label] = {"host": out["host"], "device": out["device"], "bit_identical": same,
-                      "speedup": round(out["host"]["median_ms"] / out["device"]["median_ms"], 3)}
+                      "speedup": round(out["host"]["median_ms"] / out["device"]["median_ms"], 3),
+                      "device_GBps_of_files": round(nbytes / out["device"]["median_ms"] / 1e6, 2),
+                      "device_timeline_ms": tm}
         print(label, json.dumps(res[label]), flush=True)
         assert same, label
     for p in names:
