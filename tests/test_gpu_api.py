@@ -126,6 +126,53 @@ def test_getband_device_stitch_matches_host_concat(pkg, orc, files, monkeypatch,
     assert same_bits(got, orc.stitch([orc.reduce(a, 4, 1) for a in banks[:2]]))
 
 
+@pytest.mark.parametrize("force_copy", ["0", "1"])
+def test_getband_raw_band_one_stream(pkg, orc, tmp_path, monkeypatch, force_copy):
+    """Banks that are all raw files of one geometry (uncompressed contiguous
+    FBH5 and 32-bit SIGPROC, data at different file offsets) take the band
+    read: one stream of preads / H2D batches for every bank
+    (bldp_file_runs_to_device) and one reduce into the vcat slots
+    (bldp_band_reduce_f32; with BLDP_BAND_FORCE_COPY=1 the multi-GPU form,
+    bldp_band_reduce_multi_f32, on its staged branch).  Bit-exact against the
+    host concatenation and the oracle, with and without despike, whole rows
+    and channel sub-spans (zoom windows read span by span)."""
+    monkeypatch.setenv("BLDP_BAND_FORCE_COPY", force_copy)
+    rng = np.random.default_rng(77)
+    J, C = pkg.JRange, pkg.COLON
+    nc = 1 << 18
+    banks, names = [], []
+    for b in range(6):
+        a = np.asfortranarray(rng.integers(0, 256, (nc, 1, 24)).astype(np.float32))
+        hdr = dict(fch1=8400.0 - b * 187.5, foff=-187.5 / nc, nchans=nc, nifs=1, tsamp=1.07)
+        if b % 2 == 0:
+            p = tmp_path / f"raw{b}.h5"
+            pkg.fbh5.write(p, dict(hdr, nfpc=1024), a)
+        else:
+            p = tmp_path / f"raw{b}.fil"
+            pkg.readers.write_fil(p, dict(hdr, telescope_id=6, machine_id=10, data_type=1,
+                                          tstart=59000.5, nbits=32, source_name="X"), a)
+        banks.append(a)
+        names.append(str(p))
+    workers = [0] * len(names)
+    for idxs, F, T, op, nfpc in (((C, C, C), 64, 8, "sum", None),
+                                 ((C, C, J(3, 18)), 16, 4, "max", 1024),
+                                 ((J(4097, 4096 + 65536), C, J(1, 24)), 1024, 24, "mean", None),
+                                 ((C, C, J(1, 2)), 1, 1, "sum", True)):
+        tm = {}
+        dev = pkg.GBT._band_on_device(workers, names, idxs, F, op, T, nfpc, timings=tm)
+        assert tm["path"] == "raw band", tm
+        host = pkg.GBT.getband(workers, names, idxs, fqavby=F, tavby=T, fqavfunc=op,
+                               despike_nfpc=nfpc, stitch="host")
+        assert same_bits(dev, host), (idxs, F, T, op, nfpc)
+        win = pkg.idxs.to_window(pkg.sanitizeidxs(idxs), banks[0].shape)
+        want = orc.stitch([orc.reduce(a, F, T, op, win) for a in banks])
+        if nfpc:
+            want = orc.despike(want, want.shape[0] // len(banks) // 64 if nfpc is True else nfpc)
+        assert same_bits(dev, want), (idxs, F, T, op, nfpc)
+        assert same_bits(pkg.GBT.getband(workers, names, idxs, fqavby=F, tavby=T, fqavfunc=op,
+                                         despike_nfpc=nfpc), want)
+
+
 def test_gbt_getkurtosis_fanout_long_windows(pkg, orc, tmp_path):
     """GBT.getkurtosis over 6 files on one device with > 512 spectra: one
     thread per (worker, file) on the same stream and scratch (the leaf
