@@ -244,30 +244,24 @@ bool pitch_ok(const Geo &g) {
   return (g.ni <= 1 || g.ld_i % 4 == 0) && (g.nt <= 1 || g.ld_t % 4 == 0);
 }
 bool vec_ok(const Geo &g) { return g.cs == 1 && g.off % 4 == 0 && pitch_ok(g); }
-//   BLDP_UNALIGNED_VEC  unit-step windows that start off a 16-byte boundary
-//                  (or have row pitches that are not multiples of 4 floats)
-//                  on the vector paths: gfx950 executes global_load_dwordx4 at
-//                  any dword alignment (LLVM: unaligned-buffer-access), so the
-//                  lanes load the window's own float4 columns and no
-//                  realignment is needed.  A/B on MI355X
-//                  (profiles/r02/ab_unaligned_vec.json, 8 banks):
-//                    c0=3 F=64 cfg3 5.42 -> 5.08 ms, c0=1 F=8 T=1024 cfg4
-//                    3.30 -> 2.19 ms, c0=1 F=1 5.92 -> 5.78 ms; but c0=1/3
-//                    F=1024 4.92 -> 5.12 ms and c0=2 F=2 5.83 -> 6.03 ms (the
-//                    tile / realigning kernels keep those); kurtosis c0=1 cfg4
-//                    5.79 -> 2.45 ms, cfg3 11.85 -> 6.64 ms (leaf / register
-//                    paths instead of the two-pass / mid ones)
-//                  0 = off; 1 = reduce windows where it pays (below); 2 (default)
-//                  = 1 + kurtosis; 3 = every unit-step reduce window + kurtosis
-#ifndef BLDP_UNALIGNED_VEC
-#define BLDP_UNALIGNED_VEC 2
-#endif
+// Unit-step windows that start off a 16-byte boundary (or have row pitches
+// that are not multiples of 4 floats) on the vector paths (plan option
+// "unaligned_vec"): gfx950 executes global_load_dwordx4 at any dword alignment
+// (LLVM: unaligned-buffer-access), so the lanes load the window's own float4
+// columns and no realignment is needed.  A/B on MI355X
+// (profiles/r02/ab_unaligned_vec.json, 8 banks): c0=3 F=64 cfg3 5.42 -> 5.08
+// ms, c0=1 F=8 T=1024 cfg4 3.30 -> 2.19 ms, c0=1 F=1 5.92 -> 5.78 ms; but
+// c0=1/3 F=1024 4.92 -> 5.12 ms and c0=2 F=2 5.83 -> 6.03 ms (the tile /
+// realigning kernels keep those); kurtosis c0=1 cfg4 5.79 -> 2.45 ms, cfg3
+// 11.85 -> 6.64 ms (leaf / register paths instead of the two-pass / mid
+// ones).  0 = off; 1 = reduce windows where it pays (below); 2 (default) =
+// 1 + kurtosis; 3 = every unit-step reduce window + kurtosis.
 // A dword-aligned unit-step reduce window that is not 16-byte aligned goes to
 // the vector / narrow paths when that measured faster than the realigning
 // kernels, or when the alternative is the scalar path (pitches that are not
 // multiples of 4 floats).
 bool unaligned_vec_pays(int64_t F, bool rows16) {
-  if (BLDP_UNALIGNED_VEC >= 3 || !rows16) return true;
+  if (opt(OPT_UNALIGNED_VEC) >= 3 || !rows16) return true;
   return F == 1 || (F % 4 == 0 && F <= 256);
 }
 
@@ -319,7 +313,7 @@ int prepare_reduce(int nbank, const float *const *in, int64_t nchan, int64_t nif
     words = words && aligned4(a.in[b]);
   }
   const bool aligned = (rows16 && vec_ok(g)) ||
-                       (BLDP_UNALIGNED_VEC >= 1 && words && g.cs == 1 &&
+                       (opt(OPT_UNALIGNED_VEC) >= 1 && words && g.cs == 1 &&
                         unaligned_vec_pays(F, rows16));
   *pp = plan_reduce(a, aligned, rows16, words && g.cs == 1, num_cus_current());
   if (!query) {
@@ -390,7 +384,7 @@ int bldp_plan_option(const char *name, int64_t value, int64_t *previous) {
   if (!name) return fail(BLDP_EINVAL, "null option name");
   const int k = plan_opt_index(name);
   if (k < 0) return fail(BLDP_EINVAL, "unknown plan option '%s'", name);
-  if (previous) *previous = plan_opt(k);
+  if (previous) *previous = plan_opt_override(k);
   plan_opt_set(k, value < 0 ? -1 : value);
   return BLDP_OK;
 }
@@ -645,7 +639,7 @@ static int kurt_setup(int nbank, const float *const *in, int64_t nchan, int64_t 
   k->nt = g.nt;
   k->nrow = (int64_t)nbank * g.ni;
   k->rows16 = vec_ok(g) && g.nc % 4 == 0 && aligned;
-  k->vec = BLDP_UNALIGNED_VEC >= 2 ? (g.cs == 1 && g.nc % 4 == 0 && words) : k->rows16;
+  k->vec = opt(OPT_UNALIGNED_VEC) >= 2 ? (g.cs == 1 && g.nc % 4 == 0 && words) : k->rows16;
   plan_kurtosis(*k, num_cus_current());
   return BLDP_OK;
 }

@@ -74,11 +74,22 @@ struct RedArgs {
 
 // Runtime plan options (bldp_plan_option): process-wide overrides of the
 // planners' choices, for tests that enumerate every form of a plan and for
-// A/B timing in one process.  -1 = the planner's own choice.
-enum PlanOpt { OPT_ROW_SPLIT = 0, OPT_FORCE_STAGED, OPT_COUNT };
+// A/B timing in one process.  plan_opt returns the override, or the option's
+// default (the measured choice) when there is none; -1 = "the planner
+// decides by shape" where an option has that setting (row_split).
+// Names and defaults: kernels.hip kPlanOpts.
+enum PlanOpt {
+  OPT_ROW_SPLIT = 0, OPT_FORCE_STAGED, OPT_MAX_WG_PER_CU, OPT_TS_FILL, OPT_NARROW_MIS, OPT_T38,
+  OPT_WIDE_SPLIT, OPT_NARROW_TPB, OPT_LANE, OPT_LANE3, OPT_LANET, OPT_LANET_PACK, OPT_VEC_IL,
+  OPT_VEC_ROW, OPT_ROW_TPB, OPT_ROWT_PACK, OPT_ROWT_SMALL, OPT_WAVET, OPT_UNALIGNED_VEC,
+  OPT_KURT_EXACT, OPT_KURT_MID_CPL, OPT_KURT_MID_SMALL, OPT_KURT_LEAF_NARROW, OPT_KURT_LEAF_TILE,
+  OPT_COUNT
+};
 int64_t plan_opt(int k);
+inline int64_t opt(int k) { return plan_opt(k); }
 // name -> option index, or -1
 int plan_opt_index(const char *name);
+int64_t plan_opt_override(int k);  // -1 = none
 void plan_opt_set(int k, int64_t v);
 
 enum Path { PATH_VEC = 0, PATH_NARROW = 1, PATH_SCALAR = 2, PATH_TILE = 3, PATH_VEC_IL = 4,

@@ -31,7 +31,7 @@ namespace {
 constexpr int kBlock = 256;  // 4 waves of 64
 typedef float f4v __attribute__((ext_vector_type(4)));
 // What the streaming loads point at: a float4 that may sit on any dword
-// boundary (BLDP_UNALIGNED_VEC windows start off a 16-byte boundary).  gfx950
+// boundary (plan option unaligned_vec: windows off a 16-byte boundary).  gfx950
 // executes global_load_dwordx4 at dword alignment, so the code is unchanged.
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
 
@@ -62,12 +62,9 @@ __device__ __forceinline__ float fold4(float4 v) {
   return R<OP>::f(R<OP>::f(v.x, v.y), R<OP>::f(v.z, v.w));
 }
 
-//   BLDP_DPP  1 (default) = the lane folds of the reduce kernels run on DPP row
-//             permutes and gfx950's v_permlane16/32_swap (VALU only); 0 =
-//             __shfl_xor, which is a ds_bpermute (an LDS round trip) per step
-#ifndef BLDP_DPP
-#define BLDP_DPP 1
-#endif
+// The lane folds of the reduce kernels run on DPP row permutes and gfx950's
+// v_permlane16/32_swap (VALU only), not __shfl_xor (a ds_bpermute, an LDS round
+// trip per step): profiles/r03/ab_t1v_r03a_dpp.json.
 template <int CTRL>
 __device__ __forceinline__ float dpp(float x) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL,
@@ -83,7 +80,6 @@ __device__ __forceinline__ float dpp(float x) {
 // lanes, so the result is the same on every lane of the group.
 template <int OP, int W>
 __device__ __forceinline__ float lanes_fold(float s) {
-#if BLDP_DPP
   if constexpr (W >= 2) s = R<OP>::f(s, dpp<0xB1>(s));   // quad_perm [1,0,3,2]
   if constexpr (W >= 4) s = R<OP>::f(s, dpp<0x4E>(s));   // quad_perm [2,3,0,1]
   if constexpr (W >= 8) s = R<OP>::f(s, dpp<0x141>(s));  // row_half_mirror
@@ -98,100 +94,47 @@ __device__ __forceinline__ float lanes_fold(float s) {
     const auto p = __builtin_amdgcn_permlane32_swap(u, u, false, false);
     s = R<OP>::f(__builtin_bit_cast(float, (unsigned)p[0]), __builtin_bit_cast(float, (unsigned)p[1]));
   }
-#else
-#pragma unroll
-  for (int off = W / 2; off > 0; off >>= 1) s = R<OP>::f(s, __shfl_xor(s, off, 64));
-#endif
   return s;
 }
-// Build-time variants (A/B tested with tools/ab_variants.py):
-//   BLDP_NT_LOADS  1 (default) = streaming loads carry the non-temporal hint:
-//                  the window is read once; measured +10% on cfg3 (6.35 -> 6.98 TB/s)
-//   BLDP_BATCH     independent 16-byte loads a lane issues before the first use
-#ifndef BLDP_NT_LOADS
-#define BLDP_NT_LOADS 1
-#endif
-#ifndef BLDP_BATCH
-#define BLDP_BATCH 8
-#endif
-//   BLDP_MAX_WG_PER_CU  0 (default) = one workgroup per tile; N > 0 caps the
-//                  grid at N workgroups per CU looping over tiles; -1 = that cap
-//                  (4) only for plans whose waves split the time rows.  With
-//                  BLDP_TS_FILL the uncapped grid is as fast or faster on every
-//                  measured shape (0001 band F=64 T=16: 6.80 vs 6.05 TB/s)
-#ifndef BLDP_MAX_WG_PER_CU
-#define BLDP_MAX_WG_PER_CU 0
-#endif
-//   BLDP_NT_STORES 1 (default) = the narrow path's 16-byte output stores carry
-//                  the nt hint; measured +5% on cfg3 F=1 (5.90 -> 6.21 TB/s)
-//   BLDP_TS_FILL   1 (default) = vector-path plans with fewer than 4 column
-//                  tiles raise ts until no wave of a workgroup idles (0001
-//                  band, 512 channels, F=8 T=1024: 7.05 vs 6.84 TB/s)
-#ifndef BLDP_TS_FILL
-#define BLDP_TS_FILL 1
-#endif
-#ifndef BLDP_NT_STORES
-#define BLDP_NT_STORES 1
-#endif
-//   BLDP_NARROW_MIS 1 (default) = misaligned F = 1 windows take the
-//                  realigning narrow kernel instead of the tile path; 2 = F = 2
-//                  too; 0 = neither
-#ifndef BLDP_NARROW_MIS
-#define BLDP_NARROW_MIS 1
-#endif
+// Code-shape constants (each measured against its alternatives with
+// tools/ab_variants.py, whose text-patch variants rebuild the others):
+//   streaming loads carry the non-temporal hint (the window is read once):
+//     +10% on cfg3 (6.35 -> 6.98 TB/s);
+//   kBatch  independent 16-byte loads a lane issues before the first use
+//     (4: neutral, 16: -1 .. -19%).
+constexpr int kBatch = 8;
+// 16-byte output stores carry the nt hint (+5% on cfg3 F=1, 5.90 -> 6.21 TB/s).
 __device__ __forceinline__ void st4(float *p, float4 r) {
   const f4v v = {r.x, r.y, r.z, r.w};
-#if BLDP_NT_STORES
   __builtin_nontemporal_store(v, reinterpret_cast<f4v *>(p));
-#else
-  *reinterpret_cast<f4v *>(p) = v;
-#endif
 }
-//   BLDP_NT_SCALAR_STORES  one-float-per-lane output stores with the nt hint
-//                  (written once, never re-read here): 1 (default) = the row and
-//                  interleaved kernels (A/B, profiles/r02/ab_nt_scalar_stores.json:
-//                  c0=2 F=8 +3.9%, c0=3 F=64 +2.7%, cfg3 F=64 +1.8%, cfg2 +1.6%,
-//                  cfg3 F=1024 +0.5%); 2 = every path (the tile path lost up to
-//                  1.9% with it); 0 = none
-#ifndef BLDP_NT_SCALAR_STORES
-#define BLDP_NT_SCALAR_STORES 1
-#endif
-template <int MIN_LEVEL = 2>
+// One-float-per-lane output stores: st1<1> (the row, interleaved and
+// short-time-block kernels) carries the nt hint (written once, never re-read
+// here; profiles/r02/ab_nt_scalar_stores.json: c0=2 F=8 +3.9%, c0=3 F=64
+// +2.7%, cfg3 F=64 +1.8%, cfg2 +1.6%, cfg3 F=1024 +0.5%); st1<> (the tile,
+// lane and scalar paths, which lost up to 1.9% with it) is a plain store.
+template <int NT = 0>
 __device__ __forceinline__ void st1(float *p, float v) {
-  if constexpr (BLDP_NT_SCALAR_STORES >= MIN_LEVEL)
+  if constexpr (NT)
     __builtin_nontemporal_store(v, p);
   else
     *p = v;
 }
-//   BLDP_NACC      independent float4 accumulators per lane (power of two <= 8)
-#ifndef BLDP_NACC
-#define BLDP_NACC 8
-#endif
-constexpr int kNacc = BLDP_NACC;
-//   BLDP_T38  1 (default) = the short-time-block kernels (k_reduce_rowt,
-//             k_reduce_narrowt, k_reduce_lanet) also take tavby = 3 and 8, not
-//             only 1, 2, 4 (the 512-channel 0001 product at tavby = 3 ran one
-//             3-row block per wave with half the waves idle: 2.4-2.7 TB/s).
-//             narrowt: fqavby = 2 at tavby = 3 only (fqavby = 1 lost 7% on the
-//             0002 band; at tavby = 8 narrow_tile's one full batch sums in
-//             another order).  profiles/r03/ab_t38_r03t.json
-#ifndef BLDP_T38
-#define BLDP_T38 1
-#endif
-#if BLDP_T38
+// independent float4 accumulators per lane
+constexpr int kNacc = 8;
+// Resident-wave caps (amdgpu_waves_per_eu) per SIMD: fewer concurrent row
+// streams per CU are faster on these kernels (profiles/r01_ab_row.json,
+// r02/ab_row_tpb.json, r01_ab_tilecap.json); k_reduce_row / k_reduce_rows,
+// k_reduce_rowt, k_reduce_tile.
+constexpr int kRowMaxWaves = 4, kRowtMaxWaves = 6, kTileMaxWaves = 3;
+// The short-time-block kernels (k_reduce_rowt, k_reduce_narrowt,
+// k_reduce_lanet) also take tavby = 3 and 8, not only 1, 2, 4 (plan option
+// "t38"; the 512-channel 0001 product at tavby = 3 ran one 3-row block per
+// wave with half the waves idle: 2.4-2.7 TB/s).  narrowt: fqavby = 2 at
+// tavby = 3 only (fqavby = 1 lost 7% on the 0002 band; at tavby = 8
+// narrow_tile's one full batch sums in another order).
+// profiles/r03/ab_t38_r03t.json
 #define BLDP_T38_CASES(M, X) case 3: M(X, 3) case 8: M(X, 8)
-#else
-#define BLDP_T38_CASES(M, X)
-#endif
-//   BLDP_TAIL_BATCH  1 (default) = the rows of a block left after the last full
-//                  batch (all of them when T is below the batch size: tavby = 3,
-//                  8, 9, ...) are loaded together and then chained into the first
-//                  accumulator in row order -- the same sums as one row at a
-//                  time, with up to batch - 1 loads in flight per lane instead of
-//                  one; 0 = one row at a time
-#ifndef BLDP_TAIL_BATCH
-#define BLDP_TAIL_BATCH 1
-#endif
 
 // Pairwise fold of the per-lane accumulators into acc[0].
 template <int OP>
@@ -203,27 +146,14 @@ __device__ __forceinline__ float4 fold_acc(float4 (&acc)[kNacc]) {
   return acc[0];
 }
 __device__ __forceinline__ float4 ld4(const float *p) {
-#if BLDP_NT_LOADS
   const f4u v = __builtin_nontemporal_load(reinterpret_cast<const f4u *>(p));
-#else
-  const f4u v = *reinterpret_cast<const f4u *>(p);
-#endif
   return make_float4(v.x, v.y, v.z, v.w);
 }
-//   BLDP_WIDE_SPLIT  1 (default) = groups wider than 4096 channels split their
-//               time rows over waves (ts) and workgroups (time chunks) by the
-//               work in a row, not only by the row count; 0 = by rows only
-#ifndef BLDP_WIDE_SPLIT
-#define BLDP_WIDE_SPLIT 1
-#endif
-//   BLDP_VEC_K3  groups of 3 float4 per lane on the vector path (fqavby = 12,
-//               24, 48, ..., 768): 0 = the generic K4 loop (one load at a time), 1 = a
-//               compiled K4 = 3 form with nt loads, 2 (default) = the same with
-//               plain loads (an nt load covers a third of each line at the
-//               48-byte lane pitch; the next instruction re-reads it from HBM)
-#ifndef BLDP_VEC_K3
-#define BLDP_VEC_K3 2
-#endif
+// Groups of 3 float4 per lane on the vector path (fqavby = 12, 24, 48, ...,
+// 768) have a compiled K4 = 3 form with plain loads: an nt load covers a third
+// of each line at the 48-byte lane pitch and the next instruction re-reads it
+// from HBM (profiles/r03/ab_k3_r03n.json: generic loop 10.97, nt 7.43, plain
+// 5.55 ms on the 0000 band at F = 12).
 template <bool PLAIN>
 __device__ __forceinline__ float4 ld4x(const float *p) {
   if constexpr (PLAIN) {
@@ -233,10 +163,14 @@ __device__ __forceinline__ float4 ld4x(const float *p) {
     return ld4(p);
   }
 }
+// The rows of a block left after the last full batch (all of them when T is
+// below the batch size: tavby = 3, 8, 9, ...), loaded together and then
+// chained into the first accumulator in row order: the same sums as one row
+// at a time, with up to N - 1 loads in flight per lane instead of one
+// (profiles/r03/ab_row_tail_r03l.json: +11 .. +48%).
 template <int OP, int N, bool PLAIN = false>
 __device__ __forceinline__ float4 tail_rows(float4 acc, const float *p, int64_t st, int64_t nrows) {
   static_assert(N <= 16, "tail_rows: at most 15 rows");
-#if BLDP_TAIL_BATCH
   // nrows (< N, wave-uniform) as 8 + 4 + 2 + 1 rows: every load issued before
   // the first add, no predicated array elements
   float4 v8[8], v4[4], v2[2], v1;
@@ -272,9 +206,6 @@ __device__ __forceinline__ float4 tail_rows(float4 acc, const float *p, int64_t 
     for (int u = 0; u < 2; ++u) acc = f4<OP>(acc, v2[u]);
   }
   if (b1) acc = f4<OP>(acc, v1);
-#else
-  for (; nrows > 0; --nrows, p += st) acc = f4<OP>(acc, ld4x<PLAIN>(p));
-#endif
   return acc;
 }
 
@@ -338,9 +269,9 @@ __device__ __forceinline__ void vec_tile(const RedArgs &a, int64_t tile) {
     nrows = nrows > 0 ? (nrows + ts - 1) / ts : 0;
     const int64_t rstep = (int64_t)ts * a.in_ld_t;
     if constexpr (K4C > 0) {
-      constexpr int RB = (K4C >= BLDP_BATCH) ? 1 : BLDP_BATCH / K4C;
+      constexpr int RB = (K4C >= kBatch) ? 1 : kBatch / K4C;
       constexpr int NV = RB * K4C;
-      constexpr bool PL = K4C == 3 && BLDP_VEC_K3 == 2;
+      constexpr bool PL = K4C == 3;
       for (; nrows >= RB; nrows -= RB) {
         float4 v[NV];
 #pragma unroll
@@ -422,15 +353,15 @@ __device__ __forceinline__ void narrow_tile(const RedArgs &a, int64_t tile) {
       a.in[c.bank] + a.in_off + c.i * a.in_ld_i + (c.to * a.T + r0) * a.in_ld_t + 4 * q4;
   const int64_t st = a.in_ld_t;
   int64_t nrows = r1 - r0;
-  for (; nrows >= BLDP_BATCH; nrows -= BLDP_BATCH) {
-    float4 v[BLDP_BATCH];
+  for (; nrows >= kBatch; nrows -= kBatch) {
+    float4 v[kBatch];
 #pragma unroll
-    for (int u = 0; u < BLDP_BATCH; ++u) v[u] = ld4(p + u * st);
-    p += BLDP_BATCH * st;
+    for (int u = 0; u < kBatch; ++u) v[u] = ld4(p + u * st);
+    p += kBatch * st;
 #pragma unroll
-    for (int u = 0; u < BLDP_BATCH; ++u) acc[u % kNacc] = f4<OP>(acc[u % kNacc], v[u]);
+    for (int u = 0; u < kBatch; ++u) acc[u % kNacc] = f4<OP>(acc[u % kNacc], v[u]);
   }
-  acc[0] = tail_rows<OP, BLDP_BATCH>(acc[0], p, st, nrows);
+  acc[0] = tail_rows<OP, kBatch>(acc[0], p, st, nrows);
   float4 r = fold_acc<OP>(acc);
   const int64_t co = q4 * (4 / F);
   if (a.nchunk == 1) {
@@ -465,19 +396,12 @@ __device__ __forceinline__ void narrow_tile(const RedArgs &a, int64_t tile) {
 // the reference's own fqav, no time integration), organised like
 // k_reduce_rowt: 16 / T time blocks per workgroup, 2 or 4 time groups per
 // workgroup for windows of <= 128 float4 columns.  Each block is summed and
-// stored exactly as narrow_tile does it (bit-identical).
-//   BLDP_NARROW_TPB  2 (default) = use it for T in {1, 2, 4}, the copy
-//                  (fqavby = tavby = 1) included; 1 = not for the copy;
-//                  0 = k_reduce_narrow
-#ifndef BLDP_NARROW_TPB
-#define BLDP_NARROW_TPB 2
-#endif
+// stored exactly as narrow_tile does it (bit-identical).  No resident-wave cap
+// (the narrow kernels run uncapped: a cap of 4 cost k_reduce_narrow 1.2%).
+// Plan option "narrow_tpb": 2 (default) = use it for T in {1, 2, 4}, the copy
+// (fqavby = tavby = 1) included; 1 = not for the copy; 0 = k_reduce_narrow.
 template <int OP, int F, int T>
-__global__ __launch_bounds__(kBlock)
-#if BLDP_ROWT_MAXWAVES > 0
-__attribute__((amdgpu_waves_per_eu(1, BLDP_ROWT_MAXWAVES)))
-#endif
-void k_reduce_narrowt(const RedArgs a) {
+__global__ __launch_bounds__(kBlock) void k_reduce_narrowt(const RedArgs a) {
   constexpr int TPB = 16 / T, NR = TPB * T;
   const int tid = threadIdx.x;
   const uint32_t bx = blockIdx.x, bc = (uint32_t)a.blocks_c;
@@ -501,7 +425,7 @@ void k_reduce_narrowt(const RedArgs a) {
 #pragma unroll
   for (int b = 0; b < TPB; ++b) {
     if (b < nb) {
-      // narrow_tile's accumulators for T < BLDP_BATCH rows: chained into the
+      // narrow_tile's accumulators for T < kBatch rows: chained into the
       // first, then its fold with the identities = one op with the identity
       float4 r = id4;
 #pragma unroll
@@ -531,7 +455,7 @@ void k_reduce_narrowt(const RedArgs a) {
 // ---------------------------------------------------------------------------
 // Narrow path for windows that start off a 16-byte boundary (unit channel
 // step, F = 1, e.g. idxs = (2:n, :, :) with time integration; F = 2 with
-// BLDP_NARROW_MIS=2).  Each wave owns 256 window channels = 64 output float4
+// plan option narrow_mis = 2).  Each wave owns 256 window channels = 64 output float4
 // (1 KiB of output, aligned like the output row).  Lane L streams the ALIGNED
 // input float4 column L (lane 63 also column 64) and sums its T rows in
 // registers exactly like narrow_tile; output float4 L is then elements
@@ -561,22 +485,22 @@ __device__ __forceinline__ void narrow_mis_tile(const RedArgs &a, int64_t tile) 
     const float *p = a.in[c.bank] + (abs0 - mis) + (c.to * a.T + r0) * a.in_ld_t + 4 * lane;
     const int64_t st = a.in_ld_t;
     int64_t nrows = r1 - r0;
-    for (; nrows >= BLDP_BATCH; nrows -= BLDP_BATCH) {
-      float4 v[BLDP_BATCH], w[BLDP_BATCH];
+    for (; nrows >= kBatch; nrows -= kBatch) {
+      float4 v[kBatch], w[kBatch];
 #pragma unroll
-      for (int u = 0; u < BLDP_BATCH; ++u) v[u] = ld4(p + u * st);
+      for (int u = 0; u < kBatch; ++u) v[u] = ld4(p + u * st);
       if (extra) {
 #pragma unroll
-        for (int u = 0; u < BLDP_BATCH; ++u) w[u] = ld4(p + 4 + u * st);
+        for (int u = 0; u < kBatch; ++u) w[u] = ld4(p + 4 + u * st);
 #pragma unroll
-        for (int u = 0; u < BLDP_BATCH; ++u) ax = f4<OP>(ax, w[u]);
+        for (int u = 0; u < kBatch; ++u) ax = f4<OP>(ax, w[u]);
       }
-      p += BLDP_BATCH * st;
+      p += kBatch * st;
 #pragma unroll
-      for (int u = 0; u < BLDP_BATCH; ++u) acc[u % kNacc] = f4<OP>(acc[u % kNacc], v[u]);
+      for (int u = 0; u < kBatch; ++u) acc[u % kNacc] = f4<OP>(acc[u % kNacc], v[u]);
     }
-    acc[0] = tail_rows<OP, BLDP_BATCH>(acc[0], p, st, nrows);
-    if (extra) ax = tail_rows<OP, BLDP_BATCH>(ax, p + 4, st, nrows);
+    acc[0] = tail_rows<OP, kBatch>(acc[0], p, st, nrows);
+    if (extra) ax = tail_rows<OP, kBatch>(ax, p + 4, st, nrows);
   }
   const float4 lo = fold_acc<OP>(acc);
   float4 hi = make_float4(__shfl_down(lo.x, 1, 64), __shfl_down(lo.y, 1, 64),
@@ -632,21 +556,15 @@ __device__ __forceinline__ void narrow_mis_tile(const RedArgs &a, int64_t tile) 
 // pair per lane at a 20- / 28-byte lane pitch splits every wave-instruction
 // into many partial lines).  A third form, float4 columns in clusters of F
 // lanes gathered by shuffles, lost to both (F = 3 6.18, F = 7 5.77 ms: its
-// one-float stores are scattered over 4 instructions).  So:
-//   BLDP_LANE  1 (default) = F in {2, 3, 5, 6, 7} only where the tile path
-//              cannot run (row pitches that are not multiples of 4 floats; the
-//              alternative is the scalar path); 2 = always; 0 = off
-//   BLDP_LANE3  1 (default) = F = 3 on the lane kernel everywhere: one dwordx3
-//              per lane covers whole lines, and on narrow windows (the
-//              512-channel 0001 product, 170 groups a row) the tile path ran at
-//              2.8-4.3 TB/s against the lane kernel's 1.6x more
-//              (profiles/r03/ab_grid1_lane2_r03v.json)
-#ifndef BLDP_LANE3
-#define BLDP_LANE3 1
-#endif
-#ifndef BLDP_LANE
-#define BLDP_LANE 1
-#endif
+// one-float stores are scattered over 4 instructions).  So (plan options):
+//   lane   1 (default) = F in {2, 3, 5, 6, 7} only where the tile path cannot
+//          run (row pitches that are not multiples of 4 floats; the
+//          alternative is the scalar path); 2 = always; 0 = off
+//   lane3  1 (default) = F = 3 on the lane kernel everywhere: one dwordx3 per
+//          lane covers whole lines, and on narrow windows (the 512-channel
+//          0001 product, 170 groups a row) the tile path ran at 2.8-4.3 TB/s
+//          against the lane kernel's 1.6x more
+//          (profiles/r03/ab_grid1_lane2_r03v.json)
 template <int OP, int F>
 __device__ __forceinline__ void lane_tile(const RedArgs &a, int64_t tile) {
   const Coord c = decompose(a, tile);
@@ -664,15 +582,15 @@ __device__ __forceinline__ void lane_tile(const RedArgs &a, int64_t tile) {
       a.in[c.bank] + a.in_off + c.i * a.in_ld_i + (c.to * a.T + r0) * a.in_ld_t + co * F;
   const int64_t st = a.in_ld_t;
   int64_t nrows = r1 - r0;
-  for (; nrows >= BLDP_BATCH; nrows -= BLDP_BATCH) {
-    float v[BLDP_BATCH][F];
+  for (; nrows >= kBatch; nrows -= kBatch) {
+    float v[kBatch][F];
 #pragma unroll
-    for (int u = 0; u < BLDP_BATCH; ++u)
+    for (int u = 0; u < kBatch; ++u)
 #pragma unroll
       for (int f = 0; f < F; ++f) v[u][f] = __builtin_nontemporal_load(p + u * st + f);
-    p += BLDP_BATCH * st;
+    p += kBatch * st;
 #pragma unroll
-    for (int u = 0; u < BLDP_BATCH; ++u)
+    for (int u = 0; u < kBatch; ++u)
 #pragma unroll
       for (int f = 0; f < F; ++f) acc[u & 1][f] = R<OP>::f(acc[u & 1][f], v[u][f]);
   }
@@ -709,57 +627,26 @@ __device__ __forceinline__ void lane_tile(const RedArgs &a, int64_t tile) {
 // coalesced float4 loads and every lane reading its group back, F = 12 0.144
 // vs 0.125 ms, F = 3 0.171 vs 0.162 ms on the 0002 band (the LDS round trip
 // and the workgroup barrier cost more than the partial-line loads).
-//   BLDP_LANET  1 (default) = use it for T in {1, 2, 4}; 0 = the lane / tile / vector paths
-#ifndef BLDP_LANET
-#define BLDP_LANET 1
-#endif
-//   BLDP_LANET_NT3 1 (default) = F = 3 rows as non-temporal dwordx3 loads; 0 = plain
-//   BLDP_LANET_ROWS_S / _M / _L  rows per lane for F <= 3 / F <= 6 / F > 6
-//                 (8 / 8 / 8 by default; 16 for F <= 3 and 4 for F > 6 were the
-//                 defaults until the aligned output segments below, with which 8
-//                 is 10% (F = 3) and 3% (F = 12) faster, profiles/r03/ab_t1v_r03h.json)
-//   BLDP_LANET_NTL 1 = F > 4 pieces as non-temporal loads; 0 (default) = plain
-// (G consecutive groups per lane with whole float4 loads and float4 / float2
-// stores was measured too, profiles/r03/ab_t1v_r03e.json: F = 3 with 4 groups
-// per lane 0.297 vs 0.164 ms, not taken.)
-#ifndef BLDP_LANET_NT3
-#define BLDP_LANET_NT3 1
-#endif
-#ifndef BLDP_LANET_ROWS_S
-#define BLDP_LANET_ROWS_S 8
-#endif
-#ifndef BLDP_LANET_ROWS_M
-#define BLDP_LANET_ROWS_M 8
-#endif
-#ifndef BLDP_LANET_ROWS_L
-#define BLDP_LANET_ROWS_L 8
-#endif
-#ifndef BLDP_LANET_NTL
-#define BLDP_LANET_NTL 0
-#endif
-//   BLDP_LANET_CS_S  column sets per lane for F <= 3 (1 default)
-#ifndef BLDP_LANET_CS_S
-#define BLDP_LANET_CS_S 1
-#endif
-//   BLDP_LANET_OALIGN 1 = each output row's 256-group segments start on a
-//                 64-byte boundary of the product (the segment grid shifted by
-//                 that row's misalignment), so no two workgroups share a line
-//                 and only row ends are partial writes; 0 = segments at k x 256.
-//                 A product row of nco groups starts on a line only when nco is a
-//                 multiple of 16; otherwise every workgroup boundary fell inside a
-//                 line and each of those lines went out as two partial writes from
-//                 two workgroups.  0002 band, fqavby = 3 (21845 groups a row):
-//                 0.169 -> 0.134 ms with 8 rows per lane; fqavby = 12 0.125 -> 0.122
-//                 (profiles/r03/ab_t1v_r03g_oalign.json, bit-identical)
-#ifndef BLDP_LANET_OALIGN
-#define BLDP_LANET_OALIGN 1
-#endif
-constexpr int lanet_oalign_pad() { return BLDP_LANET_OALIGN ? 15 : 0; }
-//   BLDP_LANET_PACK  1 (default) = windows of <= 113 groups share a workgroup
-//                 between 2 or 4 time groups (with BLDP_LANET_OALIGN)
-#ifndef BLDP_LANET_PACK
-#define BLDP_LANET_PACK 1
-#endif
+// Plan option "lanet": 1 (default) = use it for T in {1, 2, 3, 4, 8}; 0 = the
+// lane / tile / vector paths.  Measured forms (tools/ab_variants.py text
+// patches rebuild them): F = 3 rows as one non-temporal dwordx3 (plain: slower);
+// 8 rows per lane for every F (16 for F <= 3 and 4 for F > 6 were the defaults
+// until the aligned output segments below, with which 8 is 10% (F = 3) and 3%
+// (F = 12) faster, profiles/r03/ab_t1v_r03h.json); F > 4 pieces as plain
+// loads (nt: slower); one column set per lane.  (G consecutive groups per lane
+// with whole float4 loads and float4 / float2 stores was measured too,
+// profiles/r03/ab_t1v_r03e.json: F = 3 with 4 groups per lane 0.297 vs 0.164
+// ms, not taken.)  Each output row's 256-group segments start on a 64-byte
+// boundary of the product (the segment grid shifted by that row's
+// misalignment), so no two workgroups share a line and only row ends are
+// partial writes.  A product row of nco groups starts on a line only when nco
+// is a multiple of 16; otherwise every workgroup boundary fell inside a line
+// and each of those lines went out as two partial writes from two workgroups.
+// 0002 band, fqavby = 3 (21845 groups a row): 0.169 -> 0.134 ms with 8 rows
+// per lane; fqavby = 12 0.125 -> 0.122 (profiles/r03/ab_t1v_r03g_oalign.json,
+// bit-identical).  Plan option "lanet_pack": 1 (default) = windows of <= 113
+// groups share a workgroup between 2 or 4 time groups.
+constexpr int lanet_oalign_pad() { return 15; }  // output segments on 64-byte lines
 typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
@@ -771,123 +658,76 @@ __device__ __forceinline__ V ldv(const float *p, bool nt) {
 template <int F>
 __device__ __forceinline__ void ldF(const float *p, float (&x)[F]) {
   if constexpr (F == 3) {
-    const f3u v = ldv<f3u>(p, BLDP_LANET_NT3);
+    const f3u v = ldv<f3u>(p, true);  // one nt dwordx3: whole lines per wave
     x[0] = v.x; x[1] = v.y; x[2] = v.z;
   } else {
     int f = 0;
 #pragma unroll
     for (; f + 4 <= F; f += 4) {
-      const f4u v = ldv<f4u>(p + f, BLDP_LANET_NTL);
+      const f4u v = ldv<f4u>(p + f, false);
       x[f] = v.x; x[f + 1] = v.y; x[f + 2] = v.z; x[f + 3] = v.w;
     }
     if constexpr (F % 4 == 3) {
-      const f3u v = ldv<f3u>(p + f, BLDP_LANET_NTL);
+      const f3u v = ldv<f3u>(p + f, false);
       x[f] = v.x; x[f + 1] = v.y; x[f + 2] = v.z;
     } else if constexpr (F % 4 == 2) {
-      const f2u v = ldv<f2u>(p + f, BLDP_LANET_NTL);
+      const f2u v = ldv<f2u>(p + f, false);
       x[f] = v.x; x[f + 1] = v.y;
     } else if constexpr (F % 4 == 1) {
       x[f] = p[f];
     }
   }
 }
-constexpr int lanet_rows(int F) {
-  return F <= 3 ? BLDP_LANET_ROWS_S : F <= 6 ? BLDP_LANET_ROWS_M : BLDP_LANET_ROWS_L;
-}
-// column sets per lane: a workgroup's groups are CS x 256 consecutive ones
-// (lane t: t, t + 256, ...), so every row it reads is CS x 256 x F floats long
-constexpr int lanet_cs(int F) { return F <= 3 ? BLDP_LANET_CS_S : 1; }
+constexpr int kLanetRows = 8;  // rows per lane (every F)
 template <int OP, int F, int T>
 __global__ __launch_bounds__(kBlock) void k_reduce_lanet(const RedArgs a) {
-  constexpr int TPB = lanet_rows(F) / T, NRW = TPB * T, CS = lanet_cs(F);  // (T = 3: 6 rows)
+  constexpr int TPB = kLanetRows / T, NRW = TPB * T;  // (T = 3: 6 rows)
   static_assert(TPB >= 1, "k_reduce_lanet: rows per lane");
   const int tid = threadIdx.x;
   const uint32_t bx = blockIdx.x, bc = (uint32_t)a.blocks_c;
   const uint32_t tq = bx / bc, i = blockIdx.y;
   const int bank = blockIdx.z;
-  const int64_t co = (int64_t)(bx - tq * bc) * (kBlock * CS) + tid;  // this lane's first group
-  const int64_t to0 = (int64_t)tq * TPB;
-  const int nb = (int)min((int64_t)TPB, a.nto - to0);
   const float id = R<OP>::id();
   const int64_t ld = a.in_ld_t;
-  if constexpr (BLDP_LANET_OALIGN && CS == 1) {
-    // narrow windows (nco + 15 <= 128 / 64 groups): 2 / 4 time groups share the
-    // workgroup, 256 >> sh lanes each (a.tsub_log2 = sh; 0 otherwise)
-    const int sh = a.tsub_log2, cw = kBlock >> sh, lt = tid & (cw - 1);
-    const int64_t tp0 = (((int64_t)tq << sh) + (tid >> (8 - sh))) * TPB;  // first time block
-    const int nbp = (int)max((int64_t)0, min((int64_t)TPB, a.nto - tp0));
-    // per output row b: this lane's group, shifted so the workgroup's outputs
-    // of that row start on a 64-byte line of the product
-    float *orow[TPB];
-    int64_t g[TPB];
-    bool ok[TPB];
-    const int64_t cb = (int64_t)(bx - tq * bc) * cw;
-#pragma unroll
-    for (int b = 0; b < TPB; ++b) {
-      orow[b] = a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + (tp0 + b) * a.out_ld_t;
-      const int64_t s = (int64_t)((reinterpret_cast<uintptr_t>(orow[b]) >> 2) & 15);
-      g[b] = cb - s + lt;
-      ok[b] = b < nbp && g[b] >= 0 && g[b] < a.nco;
-    }
-    float v[NRW][F];
-    const float *p = a.in[bank] + a.in_off + (int64_t)i * a.in_ld_i + tp0 * T * ld;
-#pragma unroll
-    for (int u = 0; u < NRW; ++u) {
-      if (ok[u / T]) {
-        ldF<F>(p + u * ld + g[u / T] * F, v[u]);
-      } else {
-#pragma unroll
-        for (int f = 0; f < F; ++f) v[u][f] = id;
-      }
-    }
-#pragma unroll
-    for (int b = 0; b < TPB; ++b) {
-      float acc = id;
-#pragma unroll
-      for (int r = 0; r < T; ++r)
-#pragma unroll
-        for (int f = 0; f < F; ++f) acc = R<OP>::f(acc, v[b * T + r][f]);
-      if (ok[b]) st1<1>(orow[b] + g[b], finish<OP>(acc, a));
-    }
-    return;
-  }
-  if (co >= a.nco) return;  // (no barrier below)
-  float v[CS][NRW][F];
-  const float *p = a.in[bank] + a.in_off + (int64_t)i * a.in_ld_i + to0 * T * ld + co * F;
-#pragma unroll
-  for (int j = 0; j < CS; ++j) {
-    const bool cj = j == 0 || co + j * kBlock < a.nco;
-    const float *pj = p + j * kBlock * F;
-    if (nb == TPB && cj) {
-#pragma unroll
-      for (int u = 0; u < NRW; ++u) ldF<F>(pj + u * ld, v[j][u]);
-    } else {
-#pragma unroll
-      for (int u = 0; u < NRW; ++u) {
-        if (cj && u < nb * T) {
-          ldF<F>(pj + u * ld, v[j][u]);
-        } else {
-#pragma unroll
-          for (int f = 0; f < F; ++f) v[j][u][f] = id;
-        }
-      }
-    }
-  }
-  float *o = a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + co;
+  // narrow windows (nco + 15 <= 128 / 64 groups): 2 / 4 time groups share the
+  // workgroup, 256 >> sh lanes each (a.tsub_log2 = sh; 0 otherwise)
+  const int sh = a.tsub_log2, cw = kBlock >> sh, lt = tid & (cw - 1);
+  const int64_t tp0 = (((int64_t)tq << sh) + (tid >> (8 - sh))) * TPB;  // first time block
+  const int nbp = (int)max((int64_t)0, min((int64_t)TPB, a.nto - tp0));
+  // per output row b: this lane's group, shifted so the workgroup's outputs
+  // of that row start on a 64-byte line of the product
+  float *orow[TPB];
+  int64_t g[TPB];
+  bool ok[TPB];
+  const int64_t cb = (int64_t)(bx - tq * bc) * cw;
 #pragma unroll
   for (int b = 0; b < TPB; ++b) {
+    orow[b] = a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + (tp0 + b) * a.out_ld_t;
+    const int64_t s = (int64_t)((reinterpret_cast<uintptr_t>(orow[b]) >> 2) & 15);
+    g[b] = cb - s + lt;
+    ok[b] = b < nbp && g[b] >= 0 && g[b] < a.nco;
+  }
+  float v[NRW][F];
+  const float *p = a.in[bank] + a.in_off + (int64_t)i * a.in_ld_i + tp0 * T * ld;
 #pragma unroll
-    for (int j = 0; j < CS; ++j) {
-      // a block's F x T values in the reference's order: the F channels of a
-      // spectrum in sequence (fqav's sum over dims = 1), spectrum after spectrum
-      float acc = id;
+  for (int u = 0; u < NRW; ++u) {
+    if (ok[u / T]) {
+      ldF<F>(p + u * ld + g[u / T] * F, v[u]);
+    } else {
 #pragma unroll
-      for (int r = 0; r < T; ++r)
-#pragma unroll
-        for (int f = 0; f < F; ++f) acc = R<OP>::f(acc, v[j][b * T + r][f]);
-      if (b < nb && (j == 0 || co + j * kBlock < a.nco))
-        st1<1>(o + (to0 + b) * a.out_ld_t + j * kBlock, finish<OP>(acc, a));
+      for (int f = 0; f < F; ++f) v[u][f] = id;
     }
+  }
+#pragma unroll
+  for (int b = 0; b < TPB; ++b) {
+    // a block's F x T values in the reference's order: the F channels of a
+    // spectrum in sequence (fqav's sum over dims = 1), spectrum after spectrum
+    float acc = id;
+#pragma unroll
+    for (int r = 0; r < T; ++r)
+#pragma unroll
+      for (int f = 0; f < F; ++f) acc = R<OP>::f(acc, v[b * T + r][f]);
+    if (ok[b]) st1<1>(orow[b] + g[b], finish<OP>(acc, a));
   }
 }
 
@@ -932,17 +772,11 @@ __device__ __forceinline__ void scalar_tile(const RedArgs &a, int64_t tile) {
 // every channel in registers, then drops the selected channels into LDS and
 // folds each group of F there: 16-channel segments first, then the segments
 // of a group.  HBM traffic is the window plus <= 3 floats per tile row edge.
-//   BLDP_TILE_K    float4 columns per thread (tile row span = 1024 * K floats)
-//   BLDP_TILE_ACC  accumulator sets per column (1 or 2)
-#ifndef BLDP_TILE_K
-#define BLDP_TILE_K 4
-#endif
-#ifndef BLDP_TILE_ACC
-#define BLDP_TILE_ACC 2
-#endif
-constexpr int kTK = BLDP_TILE_K;         // float4 columns per thread
-constexpr int kTA = BLDP_TILE_ACC;
-constexpr int kTRB = BLDP_BATCH / kTK > 0 ? BLDP_BATCH / kTK : 1;  // rows per load batch
+// (A/B of 2 columns per thread and of one accumulator set: +-4%,
+// profiles/r01_ab_tile.json)
+constexpr int kTK = 4;                   // float4 columns per thread (a tile row: 1024 * kTK floats)
+constexpr int kTA = 2;                   // accumulator sets per column
+constexpr int kTRB = kBatch / kTK > 0 ? kBatch / kTK : 1;  // rows per load batch
 constexpr int kSpan = kBlock * 4 * kTK;  // floats of one row one tile may read
 constexpr int kSeg = 16;                 // channels folded per thread in stage 1
 __device__ __forceinline__ int lpad(int x) { return x + (x >> 4); }  // LDS bank spread
@@ -1050,7 +884,8 @@ __device__ __forceinline__ void tile_tile(const RedArgs &a, int64_t tile) {
 }
 
 // Grid-stride wrappers: one tile per workgroup when the grid covers every
-// tile (the default), several when plan_reduce caps the grid (BLDP_MAX_WG_PER_CU).
+// tile (the default), several when plan_reduce caps the grid (plan option
+// max_wg_per_cu).
 template <int OP, int LPG, int K4C>
 __global__ __launch_bounds__(kBlock) void k_reduce_vec(const RedArgs a) {
   for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) vec_tile<OP, LPG, K4C>(a, t);
@@ -1067,26 +902,18 @@ __global__ __launch_bounds__(kBlock) void k_reduce_vec(const RedArgs a) {
 // (xor butterfly), then over waves through LDS in wave order (deterministic).
 // Grid: x = GPW-group segment, y = (IF, time block), z = bank: no 64-bit
 // division on the way to the first load.
-//   BLDP_VEC_IL  1 (default) = use it where it applies; 0 = k_reduce_vec
-#ifndef BLDP_VEC_IL
-#define BLDP_VEC_IL 1
-#endif
-//   BLDP_IL_GPW  groups per workgroup: 2 (default; +0.4% on the 0000 band, +1.3% on one
-//                bank, i.e. one rank at N=8) or 4
-#ifndef BLDP_IL_GPW
-#define BLDP_IL_GPW 2
-#endif
-//   BLDP_IL_INFLIGHT  16-byte loads a lane issues per batch (power of two); 4
-//                  measured +0.1..0.7% against 8 on 1-, 2- and 8-bank launches
-#ifndef BLDP_IL_INFLIGHT
-#define BLDP_IL_INFLIGHT 4
-#endif
+// Plan option "vec_il": 1 (default) = use it where it applies; 0 = k_reduce_vec.
+//   kIlGpw       groups per workgroup: 2 (+0.4% on the 0000 band, +1.3% on one
+//                bank, i.e. one rank at N=8, against 4)
+//   kIlInflight  16-byte loads a lane issues per batch (power of two); 4
+//                measured +0.1..0.7% against 8 on 1-, 2- and 8-bank launches
+constexpr int kIlGpw = 2, kIlInflight = 4;
 template <int OP, int K4, int GPW>
 __global__ __launch_bounds__(kBlock) void k_reduce_il(const RedArgs a) {
   constexpr int NI = GPW * K4 / 4;           // loads per lane per row
   constexpr int PER = K4 < 4 ? 1 : K4 / 4;   // consecutive loads of one group slot
   constexpr int NS = NI / PER;               // group slots per lane
-  constexpr int IF = BLDP_IL_INFLIGHT;       // loads in flight per lane
+  constexpr int IF = kIlInflight;       // loads in flight per lane
   constexpr int RB = NI < IF ? IF / NI : 1;  // rows in flight
   constexpr int JB = NI < IF ? NI : IF;      // loads per batch within a row
   static_assert(NI >= 1 && NI % PER == 0, "k_reduce_il: GPW * K4 must be a multiple of 4");
@@ -1167,28 +994,16 @@ __global__ __launch_bounds__(kBlock) void k_reduce_il(const RedArgs a) {
 // per lane, and each group folds over its G4 lanes with an xor butterfly
 // (groups never straddle a wave).  The lean sibling of k_reduce_vec for
 // these plans: 3-D grid, no 64-bit division, no time split.
-//   BLDP_VEC_ROW 1 (default) = use it where it applies; 0 = k_reduce_vec
-#ifndef BLDP_VEC_ROW
-#define BLDP_VEC_ROW 1
-#endif
-//   BLDP_ROW_BATCH rows in flight per lane in k_reduce_row.  16 (default):
-//                  +2.6% / +3.2% on the 0002 band / bank against 8, -0.4% on
-//                  0000 F=64, -1.7% on 0001 F=64
-#ifndef BLDP_ROW_BATCH
-#define BLDP_ROW_BATCH 16
-#endif
-//   BLDP_ROW_MAXWAVES  cap on resident waves per SIMD for k_reduce_row (0 = none).
-//                  Default 4: fewer 4 KiB row streams per CU in flight is faster
-//                  on the 0002 shapes (A/B against uncapped / k_reduce_vec:
-//                  cfg1 5.85 vs 5.59 / 5.43 TB/s, cfg2 6.18 vs 5.78 / 6.10)
-#ifndef BLDP_ROW_MAXWAVES
-#define BLDP_ROW_MAXWAVES 4
-#endif
+// Plan option "vec_row": 1 (default) = use it where it applies; 0 =
+// k_reduce_vec.  kRowBatch rows in flight per lane: 16 (+2.6% / +3.2% on the
+// 0002 band / bank against 8, -0.4% on 0000 F=64, -1.7% on 0001 F=64).  At
+// most kRowMaxWaves = 4 resident waves per SIMD: fewer 4 KiB row streams per
+// CU in flight is faster on the 0002 shapes (A/B against uncapped /
+// k_reduce_vec: cfg1 5.85 vs 5.59 / 5.43 TB/s, cfg2 6.18 vs 5.78 / 6.10).
+constexpr int kRowBatch = 16;
 template <int OP, int G4>
 __global__ __launch_bounds__(kBlock)
-#if BLDP_ROW_MAXWAVES > 0
-__attribute__((amdgpu_waves_per_eu(1, BLDP_ROW_MAXWAVES)))
-#endif
+__attribute__((amdgpu_waves_per_eu(1, kRowMaxWaves)))
 void k_reduce_row(const RedArgs a) {
   const int tid = threadIdx.x;
   const uint32_t it = blockIdx.y, ni = (uint32_t)a.ni;
@@ -1205,15 +1020,15 @@ void k_reduce_row(const RedArgs a) {
                      (int64_t)to * a.T * a.in_ld_t + 4 * col;
     const int64_t ld = a.in_ld_t;
     int64_t nrows = a.T;
-    for (; nrows >= BLDP_ROW_BATCH; nrows -= BLDP_ROW_BATCH) {
-      float4 v[BLDP_ROW_BATCH];
+    for (; nrows >= kRowBatch; nrows -= kRowBatch) {
+      float4 v[kRowBatch];
 #pragma unroll
-      for (int u = 0; u < BLDP_ROW_BATCH; ++u) v[u] = ld4(p + u * ld);
-      p += BLDP_ROW_BATCH * ld;
+      for (int u = 0; u < kRowBatch; ++u) v[u] = ld4(p + u * ld);
+      p += kRowBatch * ld;
 #pragma unroll
-      for (int u = 0; u < BLDP_ROW_BATCH; ++u) acc[u % kNacc] = f4<OP>(acc[u % kNacc], v[u]);
+      for (int u = 0; u < kRowBatch; ++u) acc[u % kNacc] = f4<OP>(acc[u % kNacc], v[u]);
     }
-    acc[0] = tail_rows<OP, BLDP_ROW_BATCH>(acc[0], p, ld, nrows);
+    acc[0] = tail_rows<OP, kRowBatch>(acc[0], p, ld, nrows);
   }
   const float s = lanes_fold<OP, G4>(fold4<OP>(fold_acc<OP>(acc)));
   if (valid && (tid & (G4 - 1)) == 0)
@@ -1232,14 +1047,12 @@ void k_reduce_row(const RedArgs a) {
 // k_reduce_row's folds, so the results are bit-identical to it.
 template <int OP, int G4, int S>
 __global__ __launch_bounds__(kBlock)
-#if BLDP_ROW_MAXWAVES > 0
-__attribute__((amdgpu_waves_per_eu(1, BLDP_ROW_MAXWAVES)))
-#endif
+__attribute__((amdgpu_waves_per_eu(1, kRowMaxWaves)))
 void k_reduce_rows(const RedArgs a) {
   constexpr int CW = kBlock / S;      // float4 columns per workgroup
   constexpr int NA = kNacc / S;       // accumulators per slice
   constexpr int RPB = 16 / S;         // rows per 16-row batch per slice
-  static_assert(kNacc == 8 && BLDP_ROW_BATCH == 16, "k_reduce_rows mirrors k_reduce_row's 16 x 8");
+  static_assert(kNacc == 8 && kRowBatch == 16, "k_reduce_rows mirrors k_reduce_row's 16 x 8");
   static_assert(CW >= 64 && G4 <= 64, "groups never straddle a wave");
   const int tid = threadIdx.x;
   const int sl = tid / CW, c = tid - sl * CW;  // slice (wave-uniform), column within the workgroup
@@ -1298,41 +1111,21 @@ void k_reduce_rows(const RedArgs a) {
 // flight per lane, as k_reduce_row at T = 16.  Each block is summed exactly as
 // k_reduce_row sums it (rows chained into the first accumulator, the same
 // folds), so the results are bit-identical to it.
-//   BLDP_ROW_TPB  1 (default) = use it for T in {1, 2, 4}; 0 = k_reduce_row
-#ifndef BLDP_ROW_TPB
-#define BLDP_ROW_TPB 1
-#endif
-//   BLDP_ROWT_PACK  1 (default) = windows of <= 128 float4 columns share a
-//                  workgroup between 2 or 4 time groups (no idle lanes)
-#ifndef BLDP_ROWT_PACK
-#define BLDP_ROWT_PACK 1
-#endif
-//   BLDP_ROWT_LDS_OUT  1 (default) = k_reduce_rowt stages its output tile in LDS
-//                  and stores whole row segments (16-byte stores where legal);
-//                  0 = each wave stores its own groups' outputs
-#ifndef BLDP_ROWT_LDS_OUT
-#define BLDP_ROWT_LDS_OUT 1
-#endif
-//   BLDP_ROWT_MAXWAVES  cap on resident waves per SIMD for k_reduce_rowt (0 = none)
-//                      6 (default): A/B against 4 and none, profiles/r02/ab_row_tpb.json
-#ifndef BLDP_ROWT_MAXWAVES
-#define BLDP_ROWT_MAXWAVES 6
-#endif
-//   BLDP_ROWT_SMALL  launches that would have fewer than this many workgroups
-//                  per CU with 16 rows per lane take 8 rows per lane (TPB = 8 / T,
-//                  twice the workgroups; 0 = always 16).  A/B, profiles/r03/
-//                  ab_rowt_r03i.json (bit-identical): 8 rows win on one 0002 file
-//                  (1152 workgroups, 4.5 per CU: +10-18% at F = 16..256, T = 1, 2, 4)
-//                  and on the 0002 band (9216: +1.5-3.5%), and lose on the 0000 and
-//                  0001 bands (>= 200k workgroups: -1.5-3.5%)
-#ifndef BLDP_ROWT_SMALL
-#define BLDP_ROWT_SMALL 64
-#endif
+// Plan options: "row_tpb" 1 (default) = use it for T in {1, 2, 3, 4, 8}; 0 =
+// k_reduce_row.  "rowt_pack" 1 (default) = windows of <= 128 float4 columns
+// share a workgroup between 2 or 4 time groups (no idle lanes).  "rowt_small"
+// (64): launches that would have fewer than this many workgroups per CU with
+// 16 rows per lane take 8 rows per lane (TPB = 8 / T, twice the workgroups;
+// 0 = always 16).  A/B, profiles/r03/ab_rowt_r03i.json (bit-identical): 8 rows
+// win on one 0002 file (1152 workgroups, 4.5 per CU: +10-18% at F = 16..256,
+// T = 1, 2, 4) and on the 0002 band (9216: +1.5-3.5%), and lose on the 0000
+// and 0001 bands (>= 200k workgroups: -1.5-3.5%).  The output tile is staged
+// in LDS and stored as whole row segments (16-byte stores where legal; each
+// wave storing its own groups' outputs was slower).  At most kRowtMaxWaves = 6
+// resident waves per SIMD (A/B against 4 and none, profiles/r02/ab_row_tpb.json).
 template <int OP, int G4, int T, int NRW>
 __global__ __launch_bounds__(kBlock)
-#if BLDP_ROWT_MAXWAVES > 0
-__attribute__((amdgpu_waves_per_eu(1, BLDP_ROWT_MAXWAVES)))
-#endif
+__attribute__((amdgpu_waves_per_eu(1, kRowtMaxWaves)))
 void k_reduce_rowt(const RedArgs a) {
   constexpr int TPB = NRW / T, NR = TPB * T;
   const int tid = threadIdx.x;
@@ -1375,7 +1168,6 @@ void k_reduce_rowt(const RedArgs a) {
     if constexpr (kNacc > 1) acc = f4<OP>(acc, id4);
     sv[b] = lanes_fold<OP, G4>(fold4<OP>(acc));
   }
-#if BLDP_ROWT_LDS_OUT
   // Output tile through LDS: the workgroup's outputs are (time groups x TPB)
   // rows of 256/G4 >> tsub_log2 consecutive groups.  Lane j of a group
   // deposits block j (j + G4, ...); then each row segment is stored by
@@ -1429,24 +1221,6 @@ void k_reduce_rowt(const RedArgs a) {
     }
   }
   (void)valid;
-#else
-  // Stores: lane j of a group writes block j (j + G4, ... when the group has
-  // fewer lanes than blocks), so a store instruction has every lane busy
-  // (k_reduce_row's one-lane-per-group store would take TPB instructions).
-  const int j = tid & (G4 - 1);
-  constexpr int NS = TPB > G4 ? (TPB + G4 - 1) / G4 : 1;  // store instructions
-  constexpr int NSEL = TPB < G4 ? TPB : G4;                // blocks a lane chooses from
-  float *o = a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + col / G4;
-#pragma unroll
-  for (int m = 0; m < NS; ++m) {
-    const int b = m * G4 + j;
-    float val = sv[m * G4];
-#pragma unroll
-    for (int q = 1; q < NSEL; ++q)
-      if (m * G4 + q < TPB) val = (j == q) ? sv[m * G4 + q] : val;
-    if (valid && b < nb) st1<1>(o + (to0 + b) * a.out_ld_t, finish<OP>(val, a));
-  }
-#endif
 }
 
 // Large groups (F = 512..4096: 64 lanes x K4 float4 per row, one output per
@@ -1458,11 +1232,9 @@ void k_reduce_rowt(const RedArgs a) {
 // time blocks, TB of them per batch (>= 16 loads per lane in flight); a time
 // block is summed exactly as k_reduce_vec sums it (its batched and remainder
 // accumulator patterns, the same folds), so the results are bit-identical.
-//   BLDP_WAVET  1 (default) = use it where the interleaved kernel cannot run or a
-//               row holds fewer than 4 groups; 2 = for every such shape; 0 = never
-#ifndef BLDP_WAVET
-#define BLDP_WAVET 1
-#endif
+// Plan option "wavet": 1 (default) = use it where the interleaved kernel
+// cannot run or a row holds fewer than 4 groups; 2 = for every such shape;
+// 0 = never.
 template <int OP, int K4, int T>
 __global__ __launch_bounds__(kBlock) void k_reduce_wavet(const RedArgs a) {
   constexpr int TB = (16 / (T * K4)) > 0 ? 16 / (T * K4) : 1;  // time blocks per batch
@@ -1470,7 +1242,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce_wavet(const RedArgs a) {
   // k_reduce_vec's accumulation of one time block: K4 in {2, 4} take RB-row
   // batches (accumulator (u * K4 + k) % kNacc) then single rows (k % kNacc);
   // K4 >= 8 always the latter
-  constexpr int RB = (K4 == 2 || K4 == 4) ? (K4 >= BLDP_BATCH ? 1 : BLDP_BATCH / K4) : 0;
+  constexpr int RB = (K4 == 2 || K4 == 4) ? (K4 >= kBatch ? 1 : kBatch / K4) : 0;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t bx = blockIdx.x, g = bx % a.nco, chunk = bx / a.nco;
   const int64_t i = blockIdx.y;
@@ -1538,18 +1310,12 @@ template <int OP>
 __global__ __launch_bounds__(kBlock) void k_reduce_scalar(const RedArgs a) {
   for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) scalar_tile<OP>(a, t);
 }
-//   BLDP_TILE_MAXWAVES  cap on resident waves per SIMD for k_reduce_tile (0 = none).
-//                  Default 3 (A/B against uncapped, 5 waves: +0.6 to +4.6% on the
-//                  misaligned / odd-F windows; 2 is better on 0000-sized windows
-//                  but 2.6% worse on a misaligned 0002 band)
-#ifndef BLDP_TILE_MAXWAVES
-#define BLDP_TILE_MAXWAVES 3
-#endif
+// At most kTileMaxWaves = 3 resident waves per SIMD for k_reduce_tile (A/B
+// against uncapped, 5 waves: +0.6 to +4.6% on the misaligned / odd-F windows;
+// 2 is better on 0000-sized windows but 2.6% worse on a misaligned 0002 band).
 template <int OP, bool CS1>
 __global__ __launch_bounds__(kBlock)
-#if BLDP_TILE_MAXWAVES > 0
-__attribute__((amdgpu_waves_per_eu(1, BLDP_TILE_MAXWAVES)))
-#endif
+__attribute__((amdgpu_waves_per_eu(1, kTileMaxWaves)))
 void k_reduce_tile(const RedArgs a) {
   for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) tile_tile<OP, CS1>(a, t);
 }
@@ -1681,7 +1447,7 @@ int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 template <int OP>
 hipError_t launch_vec(const RedArgs &a, const Plan &p, hipStream_t s) {
   const dim3 grid((unsigned)p.grid), block(kBlock);
-  const int k4c = (a.k4 == 1 || a.k4 == 2 || a.k4 == 4 || (BLDP_VEC_K3 && a.k4 == 3)) ? a.k4 : 0;
+  const int k4c = (a.k4 == 1 || a.k4 == 2 || a.k4 == 4 || a.k4 == 3) ? a.k4 : 0;
 #define BLDP_VEC(L, K)                                                 \
   if (p.lpg == L && k4c == K) {                                        \
     hipLaunchKernelGGL((k_reduce_vec<OP, L, K>), grid, block, 0, s, a); \
@@ -1691,10 +1457,8 @@ hipError_t launch_vec(const RedArgs &a, const Plan &p, hipStream_t s) {
   BLDP_VEC(32, 1) BLDP_VEC(32, 0) BLDP_VEC(16, 1) BLDP_VEC(16, 0)
   BLDP_VEC(8, 1) BLDP_VEC(8, 0) BLDP_VEC(4, 1) BLDP_VEC(4, 0)
   BLDP_VEC(2, 1) BLDP_VEC(2, 0) BLDP_VEC(1, 1) BLDP_VEC(1, 0)
-#if BLDP_VEC_K3
   BLDP_VEC(1, 3) BLDP_VEC(2, 3) BLDP_VEC(4, 3) BLDP_VEC(8, 3) BLDP_VEC(16, 3) BLDP_VEC(32, 3)
   BLDP_VEC(64, 3)
-#endif
 #undef BLDP_VEC
   return hipErrorInvalidValue;
 }
@@ -1713,9 +1477,7 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
     else if (a.F == 2 && a.T == 1) { BLDP_NARROWT(2, 1) }
     else if (a.F == 2 && a.T == 2) { BLDP_NARROWT(2, 2) }
     else if (a.F == 2 && a.T == 4) { BLDP_NARROWT(2, 4) }
-#if BLDP_T38
     else if (a.F == 2 && a.T == 3) { BLDP_NARROWT(2, 3) }
-#endif
     else return hipErrorInvalidValue;
 #undef BLDP_NARROWT
     return hipGetLastError();
@@ -1846,10 +1608,10 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
   if (p.path == PATH_VEC_IL) {
     const dim3 g3((unsigned)a.blocks_c, (unsigned)(a.ni * a.nto), (unsigned)a.nbank);
     switch (a.k4) {
-      case 2: hipLaunchKernelGGL((k_reduce_il<OP, 2, BLDP_IL_GPW>), g3, block, 0, s, a); break;
-      case 4: hipLaunchKernelGGL((k_reduce_il<OP, 4, BLDP_IL_GPW>), g3, block, 0, s, a); break;
-      case 8: hipLaunchKernelGGL((k_reduce_il<OP, 8, BLDP_IL_GPW>), g3, block, 0, s, a); break;
-      case 16: hipLaunchKernelGGL((k_reduce_il<OP, 16, BLDP_IL_GPW>), g3, block, 0, s, a); break;
+      case 2: hipLaunchKernelGGL((k_reduce_il<OP, 2, kIlGpw>), g3, block, 0, s, a); break;
+      case 4: hipLaunchKernelGGL((k_reduce_il<OP, 4, kIlGpw>), g3, block, 0, s, a); break;
+      case 8: hipLaunchKernelGGL((k_reduce_il<OP, 8, kIlGpw>), g3, block, 0, s, a); break;
+      case 16: hipLaunchKernelGGL((k_reduce_il<OP, 16, kIlGpw>), g3, block, 0, s, a); break;
       default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -1904,21 +1666,56 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
 // ---------------------------------------------------------------------------
 
 namespace {
+// name, default, and what it selects (the defaults are the measured choices;
+// each of them cites its A/B where the planner uses it)
+struct PlanOptDef {
+  const char *name;
+  int64_t def;
+};
+const PlanOptDef kPlanOpts[OPT_COUNT] = {
+    {"row_split", -1},        // k_reduce_row's block over 1 / 2 / 4 workgroup slices; -1 by launch size
+    {"force_staged", 0},      // 1: bldp_band_reduce_multi_f32 stages every bank
+    {"max_wg_per_cu", 0},     // N > 0: grid capped at N workgroups per CU (grid-stride loops)
+    {"ts_fill", 1},           // narrow vector-path windows split time over idle waves
+    {"narrow_mis", 1},        // misaligned F = 1 (2: and F = 2) on k_reduce_narrow_mis
+    {"t38", 1},               // tavby = 3, 8 on the short-time-block kernels
+    {"wide_split", 1},        // groups > 4096 channels split time by work, not rows
+    {"narrow_tpb", 2},        // k_reduce_narrowt: 2 = incl. the copy, 1 = not it, 0 = off
+    {"lane", 1},              // k_reduce_lane: 1 = where the tile path cannot run, 2 = always
+    {"lane3", 1},             // fqavby = 3 on the lane kernel everywhere
+    {"lanet", 1},             // k_reduce_lanet for small odd groups, short time blocks
+    {"lanet_pack", 1},        // narrow lanet windows: 2 / 4 time groups per workgroup
+    {"vec_il", 1},            // k_reduce_il for F = 512 .. 4096
+    {"vec_row", 1},           // k_reduce_row for F = 4 .. 256
+    {"row_tpb", 1},           // k_reduce_rowt for short time blocks
+    {"rowt_pack", 1},         // narrow rowt windows: 2 / 4 time groups per workgroup
+    {"rowt_small", 64},       // rowt: launches below this many workgroups per CU take 8 rows
+    {"wavet", 1},             // k_reduce_wavet: 1 = where il is a poor fit, 2 = always, 0 = never
+    {"unaligned_vec", 2},     // dword-aligned 16-byte loads: 1 = reduce, 2 = + kurtosis, 3 = all
+    {"kurt_exact", 1},        // k_kurt_regs exact-count forms for 16 / 32 spectra
+    {"kurt_mid_cpl", 2},      // 2: k_kurt_mid2 (two channels per lane) where it applies
+    {"kurt_mid_small", 1},    // k_kurt_mid2 on 4 waves for <= 64 spectra
+    {"kurt_leaf_narrow", 4},  // leaf plans below this many waves per CU: one channel per lane
+    {"kurt_leaf_tile", 1},    // k_kurt_tile: 1 = narrow short leaves, 2 = every leaf plan
+};
 struct PlanOpts {
-  std::atomic<int64_t> v[OPT_COUNT];
+  std::atomic<int64_t> v[OPT_COUNT];  // -1 = no override
   PlanOpts() {
     for (auto &x : v) x.store(-1);
   }
 } g_plan_opt;
-const char *const kPlanOptNames[OPT_COUNT] = {"row_split", "force_staged"};
 }  // namespace
 
-int64_t plan_opt(int k) { return g_plan_opt.v[k].load(std::memory_order_relaxed); }
+int64_t plan_opt(int k) {
+  const int64_t v = g_plan_opt.v[k].load(std::memory_order_relaxed);
+  return v >= 0 ? v : kPlanOpts[k].def;
+}
 int plan_opt_index(const char *name) {
   for (int k = 0; k < OPT_COUNT; ++k)
-    if (std::strcmp(name, kPlanOptNames[k]) == 0) return k;
+    if (std::strcmp(name, kPlanOpts[k].name) == 0) return k;
   return -1;
 }
+int64_t plan_opt_override(int k) { return g_plan_opt.v[k].load(std::memory_order_relaxed); }
 void plan_opt_set(int k, int64_t v) { g_plan_opt.v[k].store(v, std::memory_order_relaxed); }
 
 Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus) {
@@ -1932,20 +1729,19 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
   a.tpb = 1;
   a.tsub_log2 = 0;
   a.rsplit = 1;
-  if (BLDP_LANET && words && a.in_cs == 1 && (T == 1 || T == 2 || T == 4 || (BLDP_T38 && (T == 3 || T == 8))) &&
+  const bool t38 = opt(OPT_T38) != 0;
+  if (opt(OPT_LANET) && words && a.in_cs == 1 && (T == 1 || T == 2 || T == 4 || (t38 && (T == 3 || T == 8))) &&
       (F == 3 || F == 5 || F == 6 || F == 7 || F == 12) && a.ni <= 65535 && a.nbank <= 65535 &&
-      cdiv(a.nco + lanet_oalign_pad(), (int64_t)kBlock * lanet_cs((int)F)) *
-              cdiv(a.nto, lanet_rows((int)F) / T) <=
+      cdiv(a.nco + lanet_oalign_pad(), (int64_t)kBlock) * cdiv(a.nto, kLanetRows / T) <=
           INT32_MAX) {
     // small odd groups, short time blocks: one lane per group, NRW rows per lane
     p.path = PATH_LANE;
     p.lanet = true;
-    a.tpb = (int32_t)(lanet_rows((int)F) / T);
-    a.blocks_c = cdiv(a.nco + (lanet_cs((int)F) == 1 ? lanet_oalign_pad() : 0),
-                      (int64_t)kBlock * lanet_cs((int)F));
+    a.tpb = (int32_t)(kLanetRows / T);
+    a.blocks_c = cdiv(a.nco + lanet_oalign_pad(), (int64_t)kBlock);
     // narrow windows: 2 or 4 time groups per workgroup (the 0001 product at
     // fqavby = 12: 42 groups a row kept 42 of 256 lanes busy)
-    if (BLDP_LANET_OALIGN && BLDP_LANET_PACK && lanet_cs((int)F) == 1)
+    if (opt(OPT_LANET_PACK))
       a.tsub_log2 = a.nco + 15 <= 64 ? 2 : a.nco + 15 <= 128 ? 1 : 0;
     a.nchunk = 1;
     a.rows_per_chunk = T;
@@ -1967,12 +1763,12 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
     // rows a time-split wave needs at least: groups wider than the interleaved
     // kernel's (G4 > 1024: one wave reads K4 > 16 float4 per lane per row) have
     // enough work in one row (fqavby = 65536 at tavby = 8 was 272 waves)
-    const int64_t tsrows = (BLDP_WIDE_SPLIT && a.k4 > 16) ? 1 : 8;
+    const int64_t tsrows = (opt(OPT_WIDE_SPLIT) && a.k4 > 16) ? 1 : 8;
     while (a.ts < 4 && tiles * a.ts < target_waves && T >= 2 * a.ts * tsrows) a.ts *= 2;
     // no idle waves: a workgroup holds 4/ts column tiles, so narrow windows
     // (fewer than 4 column tiles, e.g. the 512-channel 0001 product) split
     // their time rows over the spare waves instead
-    if (BLDP_TS_FILL)
+    if (opt(OPT_TS_FILL))
       while (a.ts < 4 && ctiles < 4 / a.ts && T >= 2 * a.ts * 8) a.ts *= 2;
     a.blocks_c = cdiv(ctiles, 4 / a.ts);
     tiles *= a.ts;
@@ -1981,15 +1777,15 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
     const int64_t nc4 = a.nco * F / 4;
     a.blocks_c = cdiv(nc4, kBlock);
     tiles = cdiv(nc4, 64) * a.ni * a.nto * a.nbank;
-  } else if (words && a.in_cs == 1 && BLDP_LANE >= 1 &&
+  } else if (words && a.in_cs == 1 && opt(OPT_LANE) >= 1 &&
              (F == 2 || F == 3 || F == 5 || F == 6 || F == 7) &&
-             (BLDP_LANE >= 2 || !rows16 || (BLDP_LANE3 && F == 3))) {
+             (opt(OPT_LANE) >= 2 || !rows16 || (opt(OPT_LANE3) && F == 3))) {
     // small odd / not-multiple-of-4 groups: one lane per output
     p.path = PATH_LANE;
     a.blocks_c = cdiv(a.nco, kBlock);
     tiles = cdiv(a.nco, 64) * a.ni * a.nto * a.nbank;
-  } else if (rows16 && a.in_cs == 1 && ((BLDP_NARROW_MIS >= 1 && F == 1) ||
-                                         (BLDP_NARROW_MIS >= 2 && F == 2))) {
+  } else if (rows16 && a.in_cs == 1 && ((opt(OPT_NARROW_MIS) >= 1 && F == 1) ||
+                                         (opt(OPT_NARROW_MIS) >= 2 && F == 2))) {
     // misaligned start, time integration (+ pairs): aligned columns realigned by shuffle
     p.path = PATH_NARROW_MIS;
     a.blocks_c = cdiv(a.nco * F, kMisSpan);
@@ -2008,7 +1804,7 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
   const int64_t rows_per_wave = cdiv(T, a.ts);
   // float4 per lane in a wave's rows (wide groups: K4 of them per row)
   const int64_t wave_work =
-      rows_per_wave * ((BLDP_WIDE_SPLIT && p.path == PATH_VEC && a.k4 > 16) ? a.k4 : 1);
+      rows_per_wave * ((opt(OPT_WIDE_SPLIT) && p.path == PATH_VEC && a.k4 > 16) ? a.k4 : 1);
   int64_t nchunk = 1;
   if (tiles > 0 && tiles < target_waves && wave_work >= 128) {  // (empty windows: no split)
     nchunk = std::min<int64_t>(cdiv(target_waves, tiles), wave_work / 64);
@@ -2021,17 +1817,17 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
   p.ws_bytes = a.nchunk > 1 ? (size_t)a.nchunk * a.nbank * p.nout * sizeof(float) : 0;
   a.ntiles = a.blocks_c * a.ni * a.nchunk * a.nto * a.nbank;
   p.grid = a.ntiles;
-  const int cap = BLDP_MAX_WG_PER_CU >= 0 ? BLDP_MAX_WG_PER_CU : (a.ts > 1 ? 4 : 0);
+  const int64_t cap = opt(OPT_MAX_WG_PER_CU);  // 0: one workgroup per tile
   if (cap > 0) p.grid = std::min<int64_t>(p.grid, (int64_t)cap * num_cus);
   p.grid = std::min<int64_t>(p.grid, INT32_MAX);  // tiles beyond: grid-stride loop
   // large groups with short time blocks where the interleaved kernel is a
   // poor fit (few groups per row, or its 3-D grid too small): k_reduce_wavet
   // (path "vector", a.tpb = time blocks per wave)
-  if (BLDP_WAVET && p.path == PATH_VEC && p.lpg == 64 &&
+  if (opt(OPT_WAVET) && p.path == PATH_VEC && p.lpg == 64 &&
       (a.k4 == 2 || a.k4 == 4 || a.k4 == 8 || a.k4 == 16) &&
-      (T == 1 || T == 2 || T == 4 || (BLDP_T38 && T == 3)) &&  // (T = 8: -8%, ab_t38_r03w)
+      (T == 1 || T == 2 || T == 4 || (t38 && T == 3)) &&  // (T = 8: -8%, ab_t38_r03w)
       a.ts == 1 && a.nchunk == 1 &&
-      (BLDP_WAVET >= 2 || a.nco < 4 || a.ni * a.nto > 65535) && a.ni <= 65535 &&
+      (opt(OPT_WAVET) >= 2 || a.nco < 4 || a.ni * a.nto > 65535) && a.ni <= 65535 &&
       a.nbank <= 65535) {
     const int64_t tb = std::max<int64_t>(1, 16 / (T * a.k4)), rw = tb * 4;
     if (a.nco * cdiv(a.nto, 4 * rw) <= INT32_MAX) {
@@ -2042,34 +1838,34 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
   }
   // whole-time-block tiles of 512..4096-channel groups: interleaved kernel
   // (3-D grid, so every dimension must fit)
-  if (BLDP_VEC_IL && p.path == PATH_VEC && p.lpg == 64 && a.tpb == 1 &&
+  if (opt(OPT_VEC_IL) && p.path == PATH_VEC && p.lpg == 64 && a.tpb == 1 &&
       (a.k4 == 2 || a.k4 == 4 || a.k4 == 8 || a.k4 == 16) && a.ts == 1 && a.nchunk == 1 &&
-      cdiv(a.nco, BLDP_IL_GPW) <= INT32_MAX && a.ni * a.nto <= 65535 && a.nbank <= 65535) {
+      cdiv(a.nco, kIlGpw) <= INT32_MAX && a.ni * a.nto <= 65535 && a.nbank <= 65535) {
     p.path = PATH_VEC_IL;
-    a.blocks_c = cdiv(a.nco, BLDP_IL_GPW);
+    a.blocks_c = cdiv(a.nco, kIlGpw);
     a.ntiles = a.blocks_c * a.ni * a.nto * a.nbank;
     p.grid = a.ntiles;
   }
   // small power-of-two groups, whole time block per tile, no time split:
   // the lean row kernel (3-D grid, so every dimension must fit)
-  if (BLDP_VEC_ROW && p.path == PATH_VEC && a.k4 == 1 && a.ts == 1 && a.nchunk == 1 &&
+  if (opt(OPT_VEC_ROW) && p.path == PATH_VEC && a.k4 == 1 && a.ts == 1 && a.nchunk == 1 &&
       F >= 4 && F <= 256 && (F & (F - 1)) == 0 && a.nbank <= 65535) {
     const int64_t bc = cdiv(a.nco * (F / 4), kBlock);
     // short time blocks: 16 / T of them per workgroup (k_reduce_rowt; grid x =
     // column blocks x time groups, so long 0001-product windows fit too)
-    int64_t tpb = (T == 1 || T == 2 || T == 4 || (BLDP_T38 && (T == 3 || T == 8))) ? 16 / T : 1;
-    if (BLDP_ROW_TPB && tpb > 1 && a.nto > 1 && bc * cdiv(a.nto, tpb) <= INT32_MAX &&
+    int64_t tpb = (T == 1 || T == 2 || T == 4 || (t38 && (T == 3 || T == 8))) ? 16 / T : 1;
+    if (opt(OPT_ROW_TPB) && tpb > 1 && a.nto > 1 && bc * cdiv(a.nto, tpb) <= INT32_MAX &&
         a.ni <= 65535) {
       p.path = PATH_VEC_ROW;
       a.blocks_c = bc;
       // <= 128 float4 columns: 2 or 4 time groups per workgroup (>= 64 lanes each)
       const int64_t cols = a.nco * (F / 4);
-      a.tsub_log2 = BLDP_ROWT_PACK ? (cols <= 64 ? 2 : cols <= 128 ? 1 : 0) : 0;
-      // small launches: 8 rows per lane, twice the workgroups (BLDP_ROWT_SMALL);
+      a.tsub_log2 = opt(OPT_ROWT_PACK) ? (cols <= 64 ? 2 : cols <= 128 ? 1 : 0) : 0;
+      // small launches: 8 rows per lane, twice the workgroups (option rowt_small);
       // at T = 8 that is one time block per workgroup, i.e. k_reduce_row, whose
       // 3-D grid must then hold (IF, time block) in y
       if (bc * cdiv(cdiv(a.nto, tpb), (int64_t)1 << a.tsub_log2) * a.ni * a.nbank <
-              (int64_t)BLDP_ROWT_SMALL * num_cus &&
+              opt(OPT_ROWT_SMALL) * num_cus &&
           (8 / T > 1 || (bc <= INT32_MAX && a.ni * a.nto <= 65535)))
         tpb = 8 / T;
       if (tpb == 1) {  // k_reduce_row
@@ -2104,9 +1900,9 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
     }
   }
   // narrow path, short time blocks: k_reduce_narrowt (grid as k_reduce_rowt's)
-  if (BLDP_NARROW_TPB && p.path == PATH_NARROW && a.nchunk == 1 &&
-      (T == 1 || T == 2 || T == 4 || (BLDP_T38 && T == 3 && F == 2)) &&
-      (BLDP_NARROW_TPB >= 1 + (F == 1 && T == 1)) && a.nto > 1 && a.ni <= 65535 && a.nbank <= 65535) {
+  if (opt(OPT_NARROW_TPB) && p.path == PATH_NARROW && a.nchunk == 1 &&
+      (T == 1 || T == 2 || T == 4 || (t38 && T == 3 && F == 2)) &&
+      (opt(OPT_NARROW_TPB) >= 1 + (F == 1 && T == 1)) && a.nto > 1 && a.ni <= 65535 && a.nbank <= 65535) {
     const int64_t cols = a.nco * F / 4, tpb = 16 / T;
     const int sh = cols <= 64 ? 2 : cols <= 128 ? 1 : 0;
     const int64_t x = a.blocks_c * cdiv(cdiv(a.nto, tpb), (int64_t)1 << sh);

@@ -103,7 +103,7 @@ constexpr int kB = 256;  // 4 waves of 64
 typedef float f4v __attribute__((ext_vector_type(4)));
 typedef float f2v __attribute__((ext_vector_type(2)));
 // streamed input: dword alignment is all gfx950's global_load_dwordx4 needs
-// (BLDP_UNALIGNED_VEC >= 2 windows start off a 16-byte boundary)
+// (plan option unaligned_vec >= 2: windows that start off a 16-byte boundary)
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
 typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
 typedef double d2v __attribute__((ext_vector_type(2)));
@@ -163,17 +163,10 @@ __device__ __forceinline__ double kurt_ratio(int64_t nt, float S, double ma, dou
 // registers and runs the recipe in the recipe's own order, so the result is
 // bit-identical to it.  EXACT (nt == NTMAX, e.g. the 16-spectrum 0000
 // product) is straight-line code: all NTMAX loads issue back to back.
-//   BLDP_KURT_EXACT 1 (default) = use the exact-count instantiation
-#ifndef BLDP_KURT_EXACT
-#define BLDP_KURT_EXACT 1
-#endif
-//   BLDP_KURT_STORE 3 (default) = the wave's 256 Float64 results go through
-//                   LDS so every nt store instruction writes 1 KiB contiguous
-//                   (+2.5% on the 0000 band against 1); 1 = each lane's 32 B as
-//                   two nt 16-byte stores
-#ifndef BLDP_KURT_STORE
-#define BLDP_KURT_STORE 3
-#endif
+// (plan option "kurt_exact": 1 = use the exact-count instantiation).  The
+// wave's 256 Float64 results go through LDS so every nt store instruction
+// writes 1 KiB contiguous (+2.5% on the 0000 band against each lane's 32 B as
+// two nt 16-byte stores).
 template <int NTMAX, bool EXACT>
 __global__ __launch_bounds__(kB) void k_kurt_regs(const KurtArgs k) {
   const int64_t ncols = k.nc / 4;
@@ -219,7 +212,7 @@ __global__ __launch_bounds__(kB) void k_kurt_regs(const KurtArgs k) {
     r[w] = (cm4 / (cm2 * cm2)) - 3.0;
   }
   d2v *o = reinterpret_cast<d2v *>(k.out + ib * k.nc + 4 * col);
-  if (BLDP_KURT_STORE == 3 && ncols % 64 == 0 &&
+  if (ncols % 64 == 0 &&
       (reinterpret_cast<uintptr_t>(k.out + ib * k.nc) & 15) == 0) {
     // whole wave in range: transpose through this wave's 2 KiB of LDS so each
     // store instruction writes 1 KiB contiguous (lane L: doubles 2L, 2L+1 of
@@ -317,20 +310,12 @@ __global__ __launch_bounds__(kB) void k_kurt_mid(const KurtArgs k) {
 // (279 spectra) +4%, one 0002 bank +17%, a window 16 bytes off a 256-byte
 // boundary +27%, 100 spectra +6%; at 512 spectra (3 waves/SIMD, one workgroup
 // per CU) -18%, so longer windows stay on k_kurt_mid.
-//   BLDP_KURT_MID_CPL  2 (default) = this kernel where it applies; 1 = k_kurt_mid only
-//   BLDP_KURT_MID_NW   its waves per workgroup (8 default, 4 or 16)
-#ifndef BLDP_KURT_MID_CPL
-#define BLDP_KURT_MID_CPL 2
-#endif
-#ifndef BLDP_KURT_MID_NW
-#define BLDP_KURT_MID_NW 8
-#endif
-//   BLDP_KURT_MID_SMALL  1 (default) = windows of <= 64 spectra take 4 waves (A/B,
-//                        profiles/r03/ab_kfile_r03ad.json: 0002 band nt = 33 / 48 /
-//                        64 1.34 / 1.22 / 1.04x; nt >= 100 and one file no gain)
-#ifndef BLDP_KURT_MID_SMALL
-#define BLDP_KURT_MID_SMALL 1
-#endif
+// Plan options: "kurt_mid_cpl" (2 = this kernel where it applies, 1 =
+// k_kurt_mid only), "kurt_mid_small" (1 = windows of <= 64 spectra take 4
+// waves; A/B, profiles/r03/ab_kfile_r03ad.json: 0002 band nt = 33 / 48 / 64
+// 1.34 / 1.22 / 1.04x; nt >= 100 and one file no gain).  kMidNW waves per
+// workgroup otherwise (4 and 16 measured and lost).
+constexpr int kMidNW = 8;
 template <int NR, int NW>
 __global__ __launch_bounds__(64 * NW) void k_kurt_mid2(const KurtArgs k) {
   constexpr int TW = 128;  // channels per tile
@@ -424,43 +409,17 @@ __global__ __launch_bounds__(64 * NW) void k_kurt_mid2(const KurtArgs k) {
 //     below, so moving the sums to the leaf's mean loses at most ~len ulps.
 // Writes the leaf's (mean, M2, M3, M4) and (sum, max, min), W contiguous
 // values per lane per quantity.
-//   BLDP_KURT_LEAF_B      spectra per batch
-//   BLDP_KURT_LEAF_W      channels per lane (4: 16-byte loads, 1 KiB per
-//                         wave-instruction; 2: 8-byte loads, twice the waves)
-//   BLDP_KURT_LEAF_PIPE   1 = the next batch's loads issue before this batch
-//                         is processed
-//   BLDP_KURT_LEAF_WAVES  cap on resident waves per SIMD (0 = the register budget's)
-#ifndef BLDP_KURT_LEAF_B
-#define BLDP_KURT_LEAF_B 4
-#endif
-#ifndef BLDP_KURT_LEAF_W
-#define BLDP_KURT_LEAF_W 4
-#endif
-#ifndef BLDP_KURT_LEAF_PIPE
-#define BLDP_KURT_LEAF_PIPE 0
-#endif
-#ifndef BLDP_KURT_LEAF_WAVES
-#define BLDP_KURT_LEAF_WAVES 0
-#endif
-//   BLDP_KURT_LEAF_MINWAVES  resident waves per SIMD the register allocation must
-//                         allow (0 = the compiler's choice)
-#ifndef BLDP_KURT_LEAF_MINWAVES
-#define BLDP_KURT_LEAF_MINWAVES 0
-#endif
-//   BLDP_KURT_LEAF_NARROW  plans whose leaves would give fewer than this many
-//                         waves per CU at W channels per lane take one channel
-//                         per lane (4x the waves) and BLDP_KURT_LEAF_NB spectra per
-//                         batch: short windows of narrow products (0001: 512
-//                         channels, nt = 513..8192 had 32-128 waves on the chip);
-//                         0 = never.  Each channel's arithmetic is unchanged.
-#ifndef BLDP_KURT_LEAF_NARROW
-#define BLDP_KURT_LEAF_NARROW 4
-#endif
-#ifndef BLDP_KURT_LEAF_NB
-#define BLDP_KURT_LEAF_NB 16
-#endif
-constexpr int kLeafW = BLDP_KURT_LEAF_W;
-static_assert(kLeafW == 1 || kLeafW == 2 || kLeafW == 4, "BLDP_KURT_LEAF_W: 1, 2 or 4");
+//   kLeafB  spectra per batch (4: +1% on the band, +3% on one bank against 8;
+//           the next batch's loads issued before this batch is processed lost
+//           2%, wave caps of 2 or 3 per SIMD 1%: profiles/r02/ab_kurt_leaf_variants.json)
+//   kLeafW  channels per lane (4: 16-byte loads, 1 KiB per wave-instruction;
+//           2 or 1: -4 .. -5% on the band)
+// Plan option "kurt_leaf_narrow": plans whose leaves would give fewer than
+// this many waves per CU at kLeafW channels per lane take one channel per
+// lane (4x the waves) and kLeafNB spectra per batch: short windows of narrow
+// products (0001: 512 channels, nt = 513..8192 had 32-128 waves on the chip);
+// 0 = never.  Each channel's arithmetic is unchanged.
+constexpr int kLeafB = 4, kLeafW = 4, kLeafNB = 16;
 
 template <int W>
 __device__ __forceinline__ void ldw(const float *p, float (&x)[W]) {
@@ -533,15 +492,7 @@ __device__ __forceinline__ void leaf_store(const KurtArgs &k, const LeafAcc<W> &
 }
 
 template <int W, int B>
-__global__ __launch_bounds__(kB)
-#if BLDP_KURT_LEAF_MINWAVES > 0 && BLDP_KURT_LEAF_WAVES > 0
-__attribute__((amdgpu_waves_per_eu(BLDP_KURT_LEAF_MINWAVES, BLDP_KURT_LEAF_WAVES)))
-#elif BLDP_KURT_LEAF_MINWAVES > 0
-__attribute__((amdgpu_waves_per_eu(BLDP_KURT_LEAF_MINWAVES)))
-#elif BLDP_KURT_LEAF_WAVES > 0
-__attribute__((amdgpu_waves_per_eu(1, BLDP_KURT_LEAF_WAVES)))
-#endif
-void k_kurt_leaf(const KurtArgs k) {
+__global__ __launch_bounds__(kB) void k_kurt_leaf(const KurtArgs k) {
   const int lane = threadIdx.x & 63;
   const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t seg = u % k.nseg, r = u / k.nseg;
@@ -575,26 +526,12 @@ void k_kurt_leaf(const KurtArgs k) {
   }
   for (int64_t bt = 0; bt < nb; ++bt) {
     p += B * ld;
-#if BLDP_KURT_LEAF_PIPE
-    float nxt[B][W];
-    if (bt + 1 < nb) {
-#pragma unroll
-      for (int q = 0; q < B; ++q) ldw<W>(p + q * ld, nxt[q]);
-    }
-#pragma unroll
-    for (int q = 0; q < B; ++q) leaf_step<W>(A, cur[q]);
-#pragma unroll
-    for (int q = 0; q < B; ++q)
-#pragma unroll
-      for (int w = 0; w < W; ++w) cur[q][w] = nxt[q][w];
-#else
 #pragma unroll
     for (int q = 0; q < B; ++q) leaf_step<W>(A, cur[q]);
     if (bt + 1 < nb) {
 #pragma unroll
       for (int q = 0; q < B; ++q) ldw<W>(p + q * ld, cur[q]);
     }
-#endif
   }
   const int tail = (int)(rem - nb * B);
   if (tail > 0) {
@@ -627,17 +564,12 @@ void k_kurt_leaf(const KurtArgs k) {
 //   !RECIPE the leaf's partials for the tree: (sum, max, min) and (mean,
 //           M2, M3, M4) about the leaf's own Float64 mean, both passes over
 //           the registers.
-//   BLDP_KURT_LEAF_TILE  1 (default) = this kernel for the plans that would
-//                        take one channel per lane on k_kurt_leaf
-//                        (BLDP_KURT_LEAF_NARROW) and fit one workgroup per CU:
-//                        Q = 2 if that many fit, else Q = 1, else the streamed
-//                        leaf (A/B, profiles/r03/ab_ktile_r03ab.json: at 2-4
-//                        workgroups per CU the streamed lanes win, and Q = 4
-//                        lost to Q = 2 everywhere); 2 = every leaf plan (Q = 2);
-//                        0 = never
-#ifndef BLDP_KURT_LEAF_TILE
-#define BLDP_KURT_LEAF_TILE 1
-#endif
+// Plan option "kurt_leaf_tile": 1 (default) = this kernel for the plans that
+// would take one channel per lane on k_kurt_leaf ("kurt_leaf_narrow") and fit
+// one workgroup per CU: Q = 2 if that many fit, else Q = 1, else the streamed
+// leaf (A/B, profiles/r03/ab_ktile_r03ab.json: at 2-4 workgroups per CU the
+// streamed lanes win, and Q = 4 lost to Q = 2 everywhere); 2 = every leaf plan
+// (Q = 2); 0 = never.
 constexpr int kTileW = 16;
 
 template <int Q, bool RECIPE>
@@ -987,14 +919,8 @@ __global__ __launch_bounds__(kB) void k_kurt_final_w(const KurtArgs k, const Tre
 // tiles per workgroup), 8 loads in flight, Float64 partials combined through
 // LDS in wave order.  With one time chunk the ratio is written here;
 // otherwise chunks are folded in a fixed order by k_kurt_fold.
-//   BLDP_KURT_PASS_MAXWAVES  cap on resident waves per SIMD (0 = none)
-#ifndef BLDP_KURT_PASS_MAXWAVES
-#define BLDP_KURT_PASS_MAXWAVES 4
-#endif
-__global__ __launch_bounds__(kB)
-#if BLDP_KURT_PASS_MAXWAVES > 0
-__attribute__((amdgpu_waves_per_eu(1, BLDP_KURT_PASS_MAXWAVES)))
-#endif
+// At most 4 resident waves per SIMD.
+__global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(1, 4)))
 void k_kurt_pass(const KurtArgs k) {
   constexpr int B = 8;  // spectra in flight per lane
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1076,17 +1002,15 @@ __global__ __launch_bounds__(kB) void k_fill_nan(double *out, int64_t n) {
 }
 
 // ---- host side -------------------------------------------------------------
-//   BLDP_KURT_MID_NR spectra per wave of the largest k_kurt_mid instantiation
-//                   (windows up to 4 x this many spectra use it, <= 128)
-#ifndef BLDP_KURT_MID_NR
-#define BLDP_KURT_MID_NR 128
-#endif
+// spectra per wave of the largest k_kurt_mid instantiation (windows up to 4 x
+// this many spectra use it)
+constexpr int kMidNR = 128;
 
 enum KPath { KP_REGS = 0, KP_MID = 1, KP_LEAF = 2, KP_TWOPASS = 3 };
 
 int path_of(const KurtArgs &k) {
   if (k.vec && k.nt <= 32) return KP_REGS;
-  if (k.nt <= 4 * BLDP_KURT_MID_NR) return KP_MID;  // any channel alignment and step
+  if (k.nt <= 4 * kMidNR) return KP_MID;  // any channel alignment and step
   if (k.vec) return KP_LEAF;
   return KP_TWOPASS;
 }
@@ -1207,13 +1131,14 @@ void plan_kurtosis(KurtArgs &k, int num_cus) {
   k.K = pw_level(std::max<int64_t>(k.nt, 1));
   k.nslot = (int64_t)2 << k.K;
   k.leafw = kLeafW;
-  if (BLDP_KURT_LEAF_NARROW > 0 && kLeafW > 1 &&
-      k.nrow * k.nslot * cdivk(k.nc / kLeafW, 64) < (int64_t)num_cus * BLDP_KURT_LEAF_NARROW)
+  const int64_t narrow = opt(OPT_KURT_LEAF_NARROW);
+  if (narrow > 0 && kLeafW > 1 && k.nrow * k.nslot * cdivk(k.nc / kLeafW, 64) < num_cus * narrow)
     k.leafw = 1;
   k.leaftile = 0;  // lane groups per channel of k_kurt_tile; 0 = streamed leaves
-  if (BLDP_KURT_LEAF_TILE == 2) {
+  const int64_t ltile = opt(OPT_KURT_LEAF_TILE);
+  if (ltile == 2) {
     k.leaftile = 2;
-  } else if (BLDP_KURT_LEAF_TILE == 1 && k.leafw == 1) {
+  } else if (ltile == 1 && k.leafw == 1) {
     const int64_t units = k.nrow * (k.nt <= 1024 ? 1 : k.nslot);  // leaves x rows
     if (units * cdivk(k.nc, 32) <= num_cus)
       k.leaftile = 2;
@@ -1251,9 +1176,10 @@ hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s) {
   const int64_t ncols = k.nc / 4;
   if (p == KP_REGS) {
     const dim3 g1((unsigned)(cdivk(ncols, kB) * k.nrow));
-    if (BLDP_KURT_EXACT && k.nt == 16)
+    const bool exact = opt(OPT_KURT_EXACT) != 0;
+    if (exact && k.nt == 16)
       hipLaunchKernelGGL((k_kurt_regs<16, true>), g1, block, 0, s, k);
-    else if (BLDP_KURT_EXACT && k.nt == 32)
+    else if (exact && k.nt == 32)
       hipLaunchKernelGGL((k_kurt_regs<32, true>), g1, block, 0, s, k);
     else if (k.nt <= 16)
       hipLaunchKernelGGL((k_kurt_regs<16, false>), g1, block, 0, s, k);
@@ -1261,11 +1187,10 @@ hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s) {
       hipLaunchKernelGGL((k_kurt_regs<32, false>), g1, block, 0, s, k);
     return hipGetLastError();
   }
-  if (p == KP_MID && BLDP_KURT_MID_CPL == 2 && k.vec && cdivk(k.nt, 8) <= 48) {
-    constexpr int NW = BLDP_KURT_MID_NW;
-    static_assert(NW == 4 || NW == 8 || NW == 16, "BLDP_KURT_MID_NW: 4, 8 or 16");
+  if (p == KP_MID && opt(OPT_KURT_MID_CPL) == 2 && k.vec && cdivk(k.nt, 8) <= 48) {
+    constexpr int NW = kMidNW;
     const dim3 g1((unsigned)(cdivk(k.nc, 128) * k.nrow)), b2(64 * NW);
-    if (BLDP_KURT_MID_SMALL && NW > 4 && k.nt <= 64) {  // (33..64 here) 4 waves of <= 16 spectra
+    if (opt(OPT_KURT_MID_SMALL) && k.nt <= 64) {  // (33..64 here) 4 waves of <= 16 spectra
       hipLaunchKernelGGL((k_kurt_mid2<16, 4>), g1, dim3(256), 0, s, k);
       return hipGetLastError();
     }
@@ -1279,14 +1204,6 @@ hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s) {
       case 4: BLDP_MID2(32)
       case 5: BLDP_MID2(40)
       case 6: BLDP_MID2(48)
-#if BLDP_KURT_MID_NW < 8
-      case 7: BLDP_MID2(56)
-      case 8: BLDP_MID2(64)
-      case 9: BLDP_MID2(72)
-      case 10: BLDP_MID2(80)
-      case 11: BLDP_MID2(88)
-      case 12: BLDP_MID2(96)
-#endif
 #undef BLDP_MID2
       default: return hipErrorInvalidValue;
     }
@@ -1331,9 +1248,9 @@ hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s) {
     }
     const dim3 g1((unsigned)cdivk(k.nrow * k.nslot * k.nseg, 4));
     if (k.leafw == 1)
-      hipLaunchKernelGGL((k_kurt_leaf<1, BLDP_KURT_LEAF_NB>), g1, block, 0, s, k);
+      hipLaunchKernelGGL((k_kurt_leaf<1, kLeafNB>), g1, block, 0, s, k);
     else
-      hipLaunchKernelGGL((k_kurt_leaf<kLeafW, BLDP_KURT_LEAF_B>), g1, block, 0, s, k);
+      hipLaunchKernelGGL((k_kurt_leaf<kLeafW, kLeafB>), g1, block, 0, s, k);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return launch_tree<true>(k, ws, L, s);

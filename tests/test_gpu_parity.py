@@ -1145,3 +1145,71 @@ def test_rowt_small_launch_tavby8_long_narrow_window(eng, orc):
     y = dev(eng, b)
     assert eng.plan(y, 64, 8)["path"] == "row"
     assert same_bits(host(eng, eng.reduce(y, 64, 8)), orc.reduce(b, 64, 8))
+
+
+# Every runtime plan option (bldp_plan_option) at every value: each form of a
+# plan the planner can take must give the oracle's results (integer data:
+# exact in any summation order), so a plan choice is a pure speed choice.
+PLAN_OPTION_VALUES = {
+    "row_split": (1, 2, 4), "max_wg_per_cu": (0, 4), "ts_fill": (0, 1), "narrow_mis": (0, 1, 2),
+    "t38": (0, 1), "wide_split": (0, 1), "narrow_tpb": (0, 1, 2), "lane": (0, 1, 2),
+    "lane3": (0, 1), "lanet": (0, 1), "lanet_pack": (0, 1), "vec_il": (0, 1), "vec_row": (0, 1),
+    "row_tpb": (0, 1), "rowt_pack": (0, 1), "rowt_small": (0, 64, 100000), "wavet": (0, 1, 2),
+    "unaligned_vec": (0, 1, 2, 3),
+}
+# (nchan, nif, ntime, window, F, T): shapes where the options above change the plan
+PLAN_OPTION_SHAPES = [
+    (65536, 1, 64, None, 64, 16), (65536, 1, 64, None, 64, 1), (65536, 1, 48, None, 64, 3),
+    (65536, 1, 64, None, 64, 8), (512, 1, 4096, None, 8, 1), (512, 1, 4096, None, 64, 4),
+    (512, 1, 2048, None, 8, 512), (512, 1, 4096, None, 512, 1), (65536, 1, 16, None, 1024, 16),
+    (65536, 1, 16, None, 1024, 1), (65535, 1, 24, None, 3, 1), (65532, 1, 24, None, 12, 2),
+    (4096, 2, 40, [1, 4092, 1, 0, 2, 1, 0, 40, 1], 1, 4),
+    (4096, 2, 40, [2, 4092, 1, 0, 2, 1, 0, 40, 1], 2, 5),
+    (4096, 1, 40, [3, 4032, 1, 0, 1, 1, 0, 40, 1], 64, 8), (4095, 1, 40, None, 3, 10),
+    (4095, 1, 40, None, 5, 1), (65536, 1, 24, None, 65536, 8), (4096, 1, 64, None, 2, 1),
+    (4096, 1, 64, None, 1, 1), (4096, 1, 64, None, 2, 3), (131072, 1, 8, None, 4, 8),
+]
+
+
+@pytest.mark.parametrize("name", sorted(PLAN_OPTION_VALUES))
+def test_plan_options_every_form(pkg, eng, orc, name):
+    rng = np.random.default_rng(len(name))
+    cases = []
+    for nc, ni, nt, win, F, T in PLAN_OPTION_SHAPES:
+        a = np.asfortranarray(rng.integers(0, 256, (nc, ni, nt)).astype(np.float32))
+        cases.append((a, dev(eng, a), win, F, T))
+    paths = set()
+    for val in PLAN_OPTION_VALUES[name]:
+        with pkg._lib.plan_option(name, val):
+            for a, x, win, F, T in cases:
+                for op in ("sum", "max"):
+                    paths.add(eng.plan(x, F, T, op, win)["path"])
+                    got = host(eng, eng.reduce(x, F, T, op, win))
+                    assert same_bits(got, orc.reduce(a, F, T, op, win)), \
+                        (name, val, a.shape, win, F, T, op)
+                # two banks stitched
+                got = host(eng, eng.band_reduce([x, x], F, T, "sum", win))
+                want = orc.reduce(a, F, T, "sum", win)
+                assert same_bits(got, orc.stitch([want, want])), (name, val, a.shape, F, T)
+    assert paths
+
+
+KURT_OPTION_VALUES = {"kurt_exact": (0, 1), "kurt_mid_cpl": (1, 2), "kurt_mid_small": (0, 1),
+                      "kurt_leaf_narrow": (0, 4), "kurt_leaf_tile": (0, 1, 2),
+                      "unaligned_vec": (0, 2)}
+
+
+@pytest.mark.parametrize("name", sorted(KURT_OPTION_VALUES))
+def test_kurtosis_plan_options_every_form(pkg, eng, orc, name):
+    """The kurtosis plan options at every value against the oracle, each at
+    the tolerance of the path the plan took."""
+    rng = np.random.default_rng(7 + len(name))
+    shapes = [(4096, 1, 16, None), (4096, 1, 32, None), (8192, 1, 48, None), (8192, 1, 279, None),
+              (512, 1, 3000, None), (512, 2, 1500, None), (4096, 1, 40, [1, 4092, 1, 0, 1, 1, 0, 40, 1])]
+    for nc, ni, nt, win in shapes:
+        a = np.asfortranarray(rng.gamma(20.0, 1e6, (nc, ni, nt)).astype(np.float32))
+        x = dev(eng, a)
+        want = orc.kurtosis(a, win)
+        for val in KURT_OPTION_VALUES[name]:
+            with pkg._lib.plan_option(name, val):
+                kurt_ok(eng, x, win, host(eng, eng.kurtosis(x, win)), want, (name, val, nc, nt))

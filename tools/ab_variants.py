@@ -25,156 +25,130 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 VDIR = os.path.join(REPO, "build", "variants")
 CSRC = os.path.join(REPO, "bldistributeddataproducts.jl_amd", "csrc")
 
-# Variants that only exist in an earlier source tree (experiments measured
-# and then taken out of the product sources) are built from that revision:
-# {"rev": commit, "extra": flags}.  R02 is the last round-2 commit.
-R02 = "5f5c135"
+# Variant kinds:
+#   {"opts": {name: value}}  runtime plan options (bldp_plan_option) on the base
+#                            build: no rebuild, set around every call;
+#   {"patch": [(file, old, new), ...]}  the current sources with text
+#                            substitutions (code-shape constants, timing-only
+#                            experiments), built under build/variants/src_NAME;
+#   {"rev": commit, "extra": flags}  an earlier source tree: experiments taken
+#                            out of the product sources, and the compile-time
+#                            -D knobs of the sources before round 4 (PRE), when
+#                            every code-shape choice was a #ifndef BLDP_* switch.
+R02 = "5f5c135"   # the last round-2 commit
+PRE = "c44cb7c"   # the last commit with the -D knobs in kernels.hip / kurtosis.hip
+
+
+def _pre(flags):
+    return {"rev": PRE, "extra": flags}
+
+
+K = "kernels.hip"
+KU = "kurtosis.hip"
 VARIANTS = {
-    "base": "",  # nt loads+stores, batch 8, no grid cap
-    "nodpp": "-DBLDP_DPP=0",  # lane folds on __shfl_xor (ds_bpermute) instead of DPP / permlane swaps
+    "base": "",  # the product build
+    "pre": _pre(""),  # the product build before the knobs left the sources (same kernels)
     "r02": {"rev": R02, "extra": ""},  # the round-2 product build
     "r03x": {"rev": "ae8255c", "extra": ""},  # the r03x product build (before the r03z..ab kurtosis changes)
-    "nolanet": "-DBLDP_LANET=0",  # small odd F, short time blocks: the lane / tile / vector paths
-    "rowtst": "-DBLDP_ROWT_LDS_OUT=0",  # k_reduce_rowt: each wave stores its own outputs
-    "lanetg": {"rev": "bbf0328", "extra": "-DBLDP_LANET_G=1"},  # F = 3 / 6: 4 / 2 groups per lane (removed)
-    "lanetp3": "-DBLDP_LANET_NT3=0",  # k_reduce_lanet: F = 3 rows as plain dwordx3 loads
-    "lanetntl": "-DBLDP_LANET_NTL=1",  # k_reduce_lanet: F > 4 pieces as nt loads
-    "lanets8": "-DBLDP_LANET_ROWS_S=8",  # rows per lane for F <= 3
-    "lanets32": "-DBLDP_LANET_ROWS_S=32",
-    "lanetl8": "-DBLDP_LANET_ROWS_L=8",  # rows per lane for F > 6
-    "lanets4": "-DBLDP_LANET_ROWS_S=4",
-    "lanets12": "-DBLDP_LANET_ROWS_S=12",
-    "lanets8c2": "-DBLDP_LANET_ROWS_S=8 -DBLDP_LANET_CS_S=2",  # F <= 3: 512 groups per workgroup
-    "lanets4c4": "-DBLDP_LANET_ROWS_S=4 -DBLDP_LANET_CS_S=4",
-    "lanetoa": "-DBLDP_LANET_OALIGN=1",  # output segments on 64-byte lines of each product row
-    "lanetoas8": "-DBLDP_LANET_OALIGN=1 -DBLDP_LANET_ROWS_S=8",
-    "lanetoap3": "-DBLDP_LANET_OALIGN=1 -DBLDP_LANET_NT3=0",
-    "lanetold": "-DBLDP_LANET_OALIGN=0 -DBLDP_LANET_ROWS_S=16",  # the r03f defaults
-    "nolanetpack": "-DBLDP_LANET_PACK=0",  # lanet: one time group per workgroup on narrow windows
-    "kleafwide": "-DBLDP_KURT_LEAF_NARROW=0",  # k_kurt_leaf always 4 channels per lane
-    "ktile0": "-DBLDP_KURT_LEAF_TILE=0",  # short narrow windows on the streamed leaf lanes
-    "ktile2": "-DBLDP_KURT_LEAF_TILE=2",  # every leaf plan read whole into registers
-    "knb32": "-DBLDP_KURT_LEAF_NB=32",  # one-channel leaf lanes: spectra per batch
-    "knb64": "-DBLDP_KURT_LEAF_NB=64",
-    "knb32p": "-DBLDP_KURT_LEAF_NB=32 -DBLDP_KURT_LEAF_PIPE=1",  # + next batch in flight
-    "knb16p": "-DBLDP_KURT_LEAF_PIPE=1",
-    "lane3off": "-DBLDP_LANE3=0",  # fqavby = 3 with long time blocks on the tile path
-    "not38": "-DBLDP_T38=0",  # tavby = 3, 8 off the short-time-block kernels
-    "nowide": "-DBLDP_WIDE_SPLIT=0",  # fqavby > 4096: time split by row count only
-    "nocopyt": "-DBLDP_NARROW_TPB=1",  # fqavby = tavby = 1 on k_reduce_narrow (one row per WG)
-    "veck3off": "-DBLDP_VEC_K3=0",  # fqavby = 12 / 24: the generic K4 loop
-    "veck3nt": "-DBLDP_VEC_K3=1",  # the K4 = 3 form with nt loads
-    "tail1": "-DBLDP_TAIL_BATCH=0",  # the rows after the last full batch one at a time
-    "rowt16": "-DBLDP_ROWT_SMALL=0",  # k_reduce_rowt: always 16 rows per lane (r03h default)
-    "kmidnr16": {"rev": "7474fea", "extra": ""},  # k_kurt_mid2 registers in steps of 16 spectra
-    "kmid2w16": "-DBLDP_KURT_MID_NW=16",  # k_kurt_mid2 with 16 waves (<= 24 spectra each)
-    "kmid2w4": "-DBLDP_KURT_MID_NW=4",  # k_kurt_mid2 with 4 waves
-    "kmidsmall0": "-DBLDP_KURT_MID_SMALL=0",  # windows of <= 64 spectra on 8 waves too
-    "kmid1": "-DBLDP_KURT_MID_CPL=1",  # k_kurt_mid only (64 channels per workgroup, 4 waves)
-    # TIMING-ONLY patch variants (wrong numerics, never in the product sources):
-    # the current sources with a text substitution, built under build/variants/
-    "kmid2f32": {"patch": [("kurtosis.hip", "double a2 = 0.0, a4 = 0.0, b2 = 0.0, b4 = 0.0;",
-                            "float a2 = 0.f, a4 = 0.f, b2 = 0.f, b4 = 0.f;"),
-                           ("kurtosis.hip", "      a2 += (double)q.x;\n      a4 += (double)q2.x;\n"
-                            "      b2 += (double)q.y;\n      b4 += (double)q2.y;",
-                            "      a2 += q.x;\n      a4 += q2.x;\n      b2 += q.y;\n      b4 += q2.y;")]},
-    "kmid2nochain": {"patch": [("kurtosis.hip",
-                                "    if (wave == w) {\n      if (w > 0) s = carry[lane];",
-                                "    if (wave == w) {\n      if (false) s = carry[lane];")]},
-}
-VARIANTS["kmid2min"] = {"patch": VARIANTS["kmid2f32"]["patch"] + VARIANTS["kmid2nochain"]["patch"]}
-# Runtime plan options (bldp_plan_option) on the base build: no rebuild, the
-# option is set around every call of the variant.
-VARIANTS.update({
+    # ---- runtime plan options
     "rows1": {"opts": {"row_split": 1}},  # k_reduce_row: one workgroup per time block
     "rows2": {"opts": {"row_split": 2}},  # k_reduce_rows: block rows over 2 slices
     "rows4": {"opts": {"row_split": 4}},
-})
-VARIANTS.update({
-    "cap4ts": "-DBLDP_MAX_WG_PER_CU=-1",  # 4 WG/CU grid cap for time-split plans
-    "plain": "-DBLDP_NT_LOADS=0 -DBLDP_NT_STORES=0 -DBLDP_MAX_WG_PER_CU=0",  # round-1 start
-    # tile path (misaligned / odd-F windows): columns per thread, accumulator sets
-    "tk4a1": "-DBLDP_TILE_ACC=1",
-    "tk2a1": "-DBLDP_TILE_K=2 -DBLDP_TILE_ACC=1",
-    "tk2a2": "-DBLDP_TILE_K=2",
-    # k_reduce_vec instead of the interleaved k_reduce_il for F = 512..4096
-    "noil": "-DBLDP_VEC_IL=0",
-    "gpw4": "-DBLDP_IL_GPW=4",
-    "ilb8": "-DBLDP_IL_INFLIGHT=8",
-    "batch4": "-DBLDP_BATCH=4",
-    "batch16": "-DBLDP_BATCH=16",
-    "rowb8": "-DBLDP_ROW_BATCH=8",
-    "norow": "-DBLDP_VEC_ROW=0",
-    "tilenocap": "-DBLDP_TILE_MAXWAVES=0",
-    "nomis": "-DBLDP_NARROW_MIS=0",  # misaligned F = 1, 2 windows on the tile path
-    "misf2": "-DBLDP_NARROW_MIS=2",  # F = 2 on the realigning narrow kernel too
-    "kpnocap": "-DBLDP_KURT_PASS_MAXWAVES=0",
-    "rownocap": "-DBLDP_ROW_MAXWAVES=0",
-    "rowmw3": "-DBLDP_ROW_MAXWAVES=3",
-    "rowmw5": "-DBLDP_ROW_MAXWAVES=5",
-    "rowmw6": "-DBLDP_ROW_MAXWAVES=6",
-    "norowt": "-DBLDP_ROW_TPB=0",  # k_reduce_row for short time blocks too (one block per WG)
-    "rowtmw6": "-DBLDP_ROWT_MAXWAVES=6",
-    "rowtmw4": "-DBLDP_ROWT_MAXWAVES=4",
-    "rowtnopack": "-DBLDP_ROWT_PACK=0",
-    "nowavet": "-DBLDP_WAVET=0",
-    "wavet2": "-DBLDP_WAVET=2",
+    "nolanet": {"opts": {"lanet": 0}},  # small odd F, short time blocks: the lane / tile / vector paths
+    "nolanetpack": {"opts": {"lanet_pack": 0}},  # lanet: one time group per workgroup on narrow windows
+    "kleafwide": {"opts": {"kurt_leaf_narrow": 0}},  # k_kurt_leaf always 4 channels per lane
+    "ktile0": {"opts": {"kurt_leaf_tile": 0}},  # short narrow windows on the streamed leaf lanes
+    "ktile2": {"opts": {"kurt_leaf_tile": 2}},  # every leaf plan read whole into registers
+    "lane3off": {"opts": {"lane3": 0}},  # fqavby = 3 with long time blocks on the tile path
+    "not38": {"opts": {"t38": 0}},  # tavby = 3, 8 off the short-time-block kernels
+    "nowide": {"opts": {"wide_split": 0}},  # fqavby > 4096: time split by row count only
+    "nocopyt": {"opts": {"narrow_tpb": 1}},  # fqavby = tavby = 1 on k_reduce_narrow (one row per WG)
+    "nonarrowt": {"opts": {"narrow_tpb": 0}},
+    "rowt16": {"opts": {"rowt_small": 0}},  # k_reduce_rowt: always 16 rows per lane
+    "kmidsmall0": {"opts": {"kurt_mid_small": 0}},  # windows of <= 64 spectra on 8 waves too
+    "kmid1": {"opts": {"kurt_mid_cpl": 1}},  # k_kurt_mid only (64 channels per workgroup, 4 waves)
+    "kold": {"opts": {"kurt_exact": 0}},  # no exact-count k_kurt_regs forms
+    "cap4": {"opts": {"max_wg_per_cu": 4}},  # grid capped at 4 workgroups per CU
+    "noil": {"opts": {"vec_il": 0}},  # k_reduce_vec instead of the interleaved k_reduce_il
+    "norow": {"opts": {"vec_row": 0}},
+    "norowt": {"opts": {"row_tpb": 0}},  # k_reduce_row for short time blocks too
+    "rowtnopack": {"opts": {"rowt_pack": 0}},
+    "nowavet": {"opts": {"wavet": 0}},
+    "wavet2": {"opts": {"wavet": 2}},
+    "notsfill": {"opts": {"ts_fill": 0}},
+    "nomis": {"opts": {"narrow_mis": 0}},  # misaligned F = 1, 2 windows on the tile path
+    "misf2": {"opts": {"narrow_mis": 2}},  # F = 2 on the realigning narrow kernel too
+    "unal0": {"opts": {"unaligned_vec": 0}},  # misaligned unit-step windows: no dword-aligned 16-byte loads
+    "unal": {"opts": {"unaligned_vec": 1}},
+    "unal3": {"opts": {"unaligned_vec": 3}},
+    "nolane": {"opts": {"lane": 0}},
+    "lane2": {"opts": {"lane": 2}},  # F in {2, 3, 5, 6, 7} on one lane per output everywhere
+    # ---- code-shape constants, text patches of the current sources
+    "lanets4": {"patch": [(K, "constexpr int kLanetRows = 8;", "constexpr int kLanetRows = 4;")]},
+    "lanets16": {"patch": [(K, "constexpr int kLanetRows = 8;", "constexpr int kLanetRows = 16;")]},
+    "batch4": {"patch": [(K, "constexpr int kBatch = 8;", "constexpr int kBatch = 4;")]},
+    "batch16": {"patch": [(K, "constexpr int kBatch = 8;", "constexpr int kBatch = 16;")]},
+    "rowb8": {"patch": [(K, "constexpr int kRowBatch = 16;", "constexpr int kRowBatch = 8;"),
+                        (K, "static_assert(kNacc == 8 && kRowBatch == 16,",
+                         "static_assert(kNacc == 8 && kRowBatch == 8,")]},
+    "gpw4": {"patch": [(K, "constexpr int kIlGpw = 2, kIlInflight = 4;",
+                        "constexpr int kIlGpw = 4, kIlInflight = 4;")]},
+    "ilb8": {"patch": [(K, "constexpr int kIlGpw = 2, kIlInflight = 4;",
+                        "constexpr int kIlGpw = 2, kIlInflight = 8;")]},
+    "rowmw6": {"patch": [(K, "constexpr int kRowMaxWaves = 4,", "constexpr int kRowMaxWaves = 6,")]},
+    "rownocap": {"patch": [(K, "constexpr int kRowMaxWaves = 4,", "constexpr int kRowMaxWaves = 8,")]},
+    "rowtmw4": {"patch": [(K, "kRowtMaxWaves = 6,", "kRowtMaxWaves = 4,")]},
+    "rowtmw8": {"patch": [(K, "kRowtMaxWaves = 6,", "kRowtMaxWaves = 8,")]},
+    "tilenocap": {"patch": [(K, "kTileMaxWaves = 3;", "kTileMaxWaves = 8;")]},
+    "tk4a1": {"patch": [(K, "constexpr int kTA = 2;", "constexpr int kTA = 1;")]},
+    "kleaf8": {"patch": [(KU, "constexpr int kLeafB = 4,", "constexpr int kLeafB = 8,")]},
+    "knb32": {"patch": [(KU, "kLeafNB = 16;", "kLeafNB = 32;")]},
+    "kmid2w4": {"patch": [(KU, "constexpr int kMidNW = 8;", "constexpr int kMidNW = 4;")]},
+    # ---- code paths no longer in the sources: the pre-round-4 tree and its -D knobs
+    "nodpp": _pre("-DBLDP_DPP=0"),  # lane folds on __shfl_xor (ds_bpermute) instead of DPP / permlane swaps
+    "plain": _pre("-DBLDP_NT_LOADS=0 -DBLDP_NT_STORES=0"),  # no nt hints (round-1 start)
+    "nts0": _pre("-DBLDP_NT_SCALAR_STORES=0"),
+    "nts2": _pre("-DBLDP_NT_SCALAR_STORES=2"),
+    "veck3off": _pre("-DBLDP_VEC_K3=0"),  # fqavby = 12 / 24: the generic K4 loop
+    "veck3nt": _pre("-DBLDP_VEC_K3=1"),  # the K4 = 3 form with nt loads
+    "tail1": _pre("-DBLDP_TAIL_BATCH=0"),  # the rows after the last full batch one at a time
+    "rowtst": _pre("-DBLDP_ROWT_LDS_OUT=0"),  # k_reduce_rowt: each wave stores its own outputs
+    "lanetp3": _pre("-DBLDP_LANET_NT3=0"),  # k_reduce_lanet: F = 3 rows as plain dwordx3 loads
+    "lanetntl": _pre("-DBLDP_LANET_NTL=1"),  # k_reduce_lanet: F > 4 pieces as nt loads
+    "lanetold": _pre("-DBLDP_LANET_OALIGN=0 -DBLDP_LANET_ROWS_S=16"),  # the r03f defaults
+    "lanets8c2": _pre("-DBLDP_LANET_ROWS_S=8 -DBLDP_LANET_CS_S=2"),  # F <= 3: 512 groups per workgroup
+    "kst1": _pre("-DBLDP_KURT_STORE=1"),
+    "kleafpipe": _pre("-DBLDP_KURT_LEAF_PIPE=1"),
+    "kleafw2ch": _pre("-DBLDP_KURT_LEAF_W=2"),
+    "kleafw2": _pre("-DBLDP_KURT_LEAF_WAVES=2"),
+    "kpnocap": _pre("-DBLDP_KURT_PASS_MAXWAVES=0"),
+    "lanetg": {"rev": "bbf0328", "extra": "-DBLDP_LANET_G=1"},  # F = 3 / 6: 4 / 2 groups per lane (removed)
+    "kmidnr16": {"rev": "7474fea", "extra": ""},  # k_kurt_mid2 registers in steps of 16 spectra
     "ilt": {"rev": R02, "extra": "-DBLDP_IL_TPB=1"},  # k_reduce_ilt (removed in round 3)
     "rowtnobfly": {"rev": R02, "extra": "-DBLDP_ROWT_TIMING_NOBFLY=1"},  # timing only: wrong numerics
     "rowthalv": {"rev": R02, "extra": "-DBLDP_ROWT_HALVING=1"},
-    "nonarrowt": "-DBLDP_NARROW_TPB=0",
-    "rowtmw8": "-DBLDP_ROWT_MAXWAVES=0",
-    # narrow windows: time split over otherwise idle waves, with / without grid cap
-    "notsfill": "-DBLDP_TS_FILL=0",
-
-    # kurtosis: exact-count register kernel, LDS-transposed stores
-    "kold": "-DBLDP_KURT_EXACT=0",
-    "kst1": "-DBLDP_KURT_STORE=1",
-    # kurtosis, streamed leaves: spectra in flight per lane, waves/SIMD caps
-    "kleaf8": "-DBLDP_KURT_LEAF_B=8",
-    "kleafpipe": "-DBLDP_KURT_LEAF_PIPE=1",
-    "kleafpipe8": "-DBLDP_KURT_LEAF_PIPE=1 -DBLDP_KURT_LEAF_B=8",
-    "kleafw2ch": "-DBLDP_KURT_LEAF_W=2",
-    "kleafw2chpipe": "-DBLDP_KURT_LEAF_W=2 -DBLDP_KURT_LEAF_PIPE=1",
-    "kleafw1ch": "-DBLDP_KURT_LEAF_W=1 -DBLDP_KURT_LEAF_B=8",
-    "kleafw2": "-DBLDP_KURT_LEAF_WAVES=2",
-    "kleafw3": "-DBLDP_KURT_LEAF_WAVES=3",
-    "kleafb2": "-DBLDP_KURT_LEAF_B=2",
     "kleaft32": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_TIMING_F32=1"},  # timing only: wrong numerics
-    "kleaft32b8": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_TIMING_F32=1 -DBLDP_KURT_LEAF_B=8"},
     "kleaflo": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_TIMING_LOADONLY=1"},  # timing only: loads + sum
-    "kleaflow4": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_TIMING_LOADONLY=1 -DBLDP_KURT_LEAF_WAVES=4"},
-    "kleaflob8w4": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_TIMING_LOADONLY=1 -DBLDP_KURT_LEAF_B=8 -DBLDP_KURT_LEAF_WAVES=4"},
-    "kleaflob8": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_TIMING_LOADONLY=1 -DBLDP_KURT_LEAF_B=8"},
     "kleafilv": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_TIMING_ILV=1"},  # timing only: reduce-like leaf streams
-    "kleafilvb8": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_TIMING_ILV=1 -DBLDP_KURT_LEAF_B=8"},
-    "kleafilvw4": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_TIMING_ILV=1 -DBLDP_KURT_LEAF_WAVES=4"},
     "kilv": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_ILV=1"},  # k_kurt_leaf_ilv (bit-identical to base)
-    "kilvb2": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_ILV=1 -DBLDP_KURT_ILV_B=2"},
-    "kilvb8": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_ILV=1 -DBLDP_KURT_ILV_B=8"},
-    "kleafilvw2": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_TIMING_ILV=1 -DBLDP_KURT_LEAF_WAVES=2"},
-    # k_kurt_mid with two channels per lane (512-byte wave loads), 8 or 4 waves
-    "kmid2w8": "-DBLDP_KURT_MID_CPL=2 -DBLDP_KURT_MID_NW=8",
-    "kmid2w4": "-DBLDP_KURT_MID_CPL=2 -DBLDP_KURT_MID_NW=4",
-    "kleafpipe2": "-DBLDP_KURT_LEAF_PIPE=1 -DBLDP_KURT_LEAF_B=2",
-    "kleafpipe2w5": "-DBLDP_KURT_LEAF_PIPE=1 -DBLDP_KURT_LEAF_B=2 -DBLDP_KURT_LEAF_MINWAVES=5",
-    "kmidnochain": {"rev": R02, "extra": "-DBLDP_KURT_MID_TIMING_NOCHAIN=1"},  # timing only: wrong numerics
-    # misaligned unit-step windows on the vector paths (dword-aligned 16-byte loads);
-    # 2 = the kurtosis register / leaf paths too
-    "unal": "-DBLDP_UNALIGNED_VEC=1",
-    "unal2": "-DBLDP_UNALIGNED_VEC=2",
-    "unal0": "-DBLDP_UNALIGNED_VEC=0",
-    "unal3": "-DBLDP_UNALIGNED_VEC=3",
-    # small odd F on one lane per output (dwordx3 etc.) vs the tile path's LDS fold
-    "nolane": "-DBLDP_LANE=0",
-    "lane2": "-DBLDP_LANE=2",  # F in {2, 3, 5, 6, 7} on one lane per output everywhere
-    # streamed kurtosis leaves through a per-wave LDS ring filled by global_load_lds
-    "nts0": "-DBLDP_NT_SCALAR_STORES=0",
-    "nts2": "-DBLDP_NT_SCALAR_STORES=2",
-    "klds8": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_LDS=8"},
-    "klds16": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_LDS=16"},
-    "klds8b2": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_LDS=8 -DBLDP_KURT_LEAF_LB=2"},
-    "klds16b8": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_LDS=16 -DBLDP_KURT_LEAF_LB=8"},
+    "kmidnochain": {"rev": R02, "extra": "-DBLDP_KURT_MID_TIMING_NOCHAIN=1"},  # timing only
+    "klds8": {"rev": R02, "extra": "-DBLDP_KURT_LEAF_LDS=8"},  # streamed leaves through an LDS ring
+    # TIMING-ONLY patch variants (wrong numerics, never in the product sources)
+    "kmid2f32": {"patch": [(KU, "double a2 = 0.0, a4 = 0.0, b2 = 0.0, b4 = 0.0;",
+                            "float a2 = 0.f, a4 = 0.f, b2 = 0.f, b4 = 0.f;"),
+                           (KU, "      a2 += (double)q.x;\n      a4 += (double)q2.x;\n"
+                            "      b2 += (double)q.y;\n      b4 += (double)q2.y;",
+                            "      a2 += q.x;\n      a4 += q2.x;\n      b2 += q.y;\n      b4 += q2.y;")]},
+    "kmid2nochain": {"patch": [(KU, "    if (wave == w) {\n      if (w > 0) s = carry[lane];",
+                                "    if (wave == w) {\n      if (false) s = carry[lane];")]},
+}
+VARIANTS["kmid2min"] = {"patch": VARIANTS["kmid2f32"]["patch"] + VARIANTS["kmid2nochain"]["patch"]}
+# the round-3 A/B of the reference's own fqav shapes (profiles/r03/ab_t1v_r03h.json:
+# base, lanetold, lanets4, lanets12, lanetl8, rowt8) in the pre-round-4 tree
+VARIANTS.update({
+    "lanets12": _pre("-DBLDP_LANET_ROWS_S=12"),
+    "lanetl8": _pre("-DBLDP_LANET_ROWS_L=8"),
+    "rowt8": _pre("-DBLDP_ROWT_SMALL=100000"),
 })
 
 
