@@ -550,6 +550,44 @@ def rendezvous_check(args, dist, rank, world):
     return r
 
 
+def bench_typed(args, eng, torch, pkg):
+    """fqav on 8-bit SIGPROC data (the reference's UInt8 arrays, Blio nbits 8;
+    src/gbtworkerfunctions.jl:173-174) at the 0002 geometry: one file (65536
+    ch x 1 IF x 279 spectra) and the 8-file band, fqavby=64, sum (UInt64
+    results).  GB/s of input bytes; kernel time from HIP events over
+    back-to-back launches (rocprofv3 gives the per-launch figure)."""
+    import numpy as np
+
+    rng = np.random.default_rng(0)
+    out = {}
+    for label, nb in (("0002 file", 1), ("0002 band", 8)):
+        a = rng.integers(0, 256, (279, 1, 65536 * nb), dtype=np.uint8)  # C order [t][i][c]
+        x = torch.from_numpy(a).cuda().permute(2, 1, 0)  # Julia-order (65536*nb, 1, 279)
+        for _ in range(args.warmup):
+            eng.reduce(x, 64, 1, "sum")
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.steps):
+            eng.reduce(x, 64, 1, "sum")
+        e1.record()
+        e1.synchronize()
+        ms = e0.elapsed_time(e1) / args.steps
+        nbytes = a.nbytes + 8 * (65536 * nb // 64) * 279
+        out[label] = {"ms_per_call": round(ms, 4), "GBps_in_plus_out": round(nbytes / ms / 1e6, 1),
+                      "input_bytes": int(a.nbytes)}
+    f = out["0002 file"]
+    return {"metric": "fqav GB/s on UInt8 SIGPROC data (0002 geometry, fqavby=64, sum)",
+            "value": f["GBps_in_plus_out"], "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": f["ms_per_call"], "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "u8->u64",
+            "data": "synthetic uniform 0..255", "config": {"workload": "typed reduce", **out},
+            "roofline": {"bound": "hbm", "achieved": f["GBps_in_plus_out"], "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(f["GBps_in_plus_out"] / HBM_PEAK_GBS, 4),
+                         "traffic": None, "kernel": "k_reduce_typed_vec (one call per step; "
+                                                    "host-call bound below ~20 us)"}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -560,7 +598,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", default="reduce",
                     choices=["reduce", "kurtosis", "host", "decode", "file", "rawfile",
-                             "rendezvous"])
+                             "rendezvous", "typed"])
     ap.add_argument("--local-banks", type=int, default=None,
                     help="N=1 only: reduce just this many banks per launch, i.e. one rank's "
                          "share of an N-GPU run (for per-launch PMC profiles)")
@@ -629,8 +667,9 @@ def main():
         return r
     if args.mode != "reduce":
         if world != 1:
-            raise SystemExit("--mode kurtosis/decode/file/rawfile are single-GPU measurements")
+            raise SystemExit("--mode kurtosis/typed/decode/file/rawfile are single-GPU measurements")
         r = (bench_kurtosis(args, cfg, eng, torch) if args.mode == "kurtosis"
+             else bench_typed(args, eng, torch, pkg) if args.mode == "typed"
              else bench_decode(args, eng, torch, pkg) if args.mode == "decode"
              else bench_file(args, eng, torch, pkg) if args.mode == "file"
              else bench_rawfile(args, eng, torch, pkg))

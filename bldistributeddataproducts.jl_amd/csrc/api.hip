@@ -746,6 +746,7 @@ int bldp_reduce_strided(int dtype, const void *in, int64_t nchan, int64_t nif, i
   a.nto = g.nt / T;
   a.F = F;
   a.T = T;
+  a.num_cus = num_cus_current();
   if (a.nco * a.ni * a.nto == 0) return BLDP_OK;
   if (!in || !out) return fail(BLDP_EINVAL, "null pointer");
   hipError_t e = launch_reduce_typed(a, op, (hipStream_t)stream);

@@ -33,6 +33,9 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <limits>
+#include <type_traits>
+
 #include "bldp_impl.h"
 
 // StatsBase rounds z*z before adding it (Julia contracts nothing without
@@ -171,6 +174,166 @@ __global__ __launch_bounds__(256) void k_reduce_typed(const TypedArgs a) {
   }
 }
 
+int64_t cdivt(int64_t x, int64_t y) { return (x + y - 1) / y; }
+unsigned grid_for(int64_t n) { return (unsigned)std::min<int64_t>(cdivt(n, 256), 65536); }
+
+// ---------------------------------------------------------------------------
+// Coalesced form for the order-free reductions: integer sums (exact, wrapping:
+// (U)Int64 addition is associative), max / min of integers and Float64 (NaN
+// propagates and -0.0 < +0.0 whatever the order), and means of <= 32-bit
+// integers whose partial sums stay below 2^53 (every order then gives the
+// exact sum, which is what Julia's Float64 sum of the converted values is).
+// The one-lane-per-group kernel above reads a group's F elements one at a
+// time at a lane pitch of F elements; here each lane loads 16 contiguous bytes
+// of a row (16 UInt8 SIGPROC samples, 8 UInt16, ...), so a wave-instruction
+// reads 1 KiB contiguous, and the LPG lanes of a group combine by shuffle.
+// A workgroup takes TPB consecutive time blocks of its 256 / LPG groups.
+__device__ __forceinline__ uint32_t sad_u8(uint32_t x, uint32_t acc) {
+  return __builtin_amdgcn_sad_u8(x, 0u, acc);  // acc + the 4 bytes of x
+}
+__device__ __forceinline__ uint32_t sad_u16(uint32_t x, uint32_t acc) {
+  return __builtin_amdgcn_sad_u16(x, 0u, acc);  // acc + the 2 halfwords of x
+}
+
+template <typename TI, int OP>
+struct Vec16 {
+  // accumulator: exact integer sums in 64 bits (signed types biased to
+  // unsigned and corrected at the end), max / min in the element type
+  static constexpr bool SUM = OP == BLDP_OP_SUM || OP == BLDP_OP_MEAN;
+  static constexpr int N = 16 / (int)sizeof(TI);  // elements per 16-byte load
+  typedef typename std::conditional<SUM, uint64_t, TI>::type A;
+  __device__ static A init() {
+    // the identities of max / min (Float64: -Inf / +Inf, so an all -Inf group stays -Inf)
+    typedef std::numeric_limits<TI> L;
+    if constexpr (SUM) return 0;
+    else if constexpr (OP == BLDP_OP_MAX) return L::has_infinity ? -L::infinity() : L::lowest();
+    else return L::has_infinity ? L::infinity() : L::max();
+  }
+  __device__ static A add(A acc, uint4 q) {
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+    if constexpr (SUM && sizeof(TI) == 1) {
+      const uint32_t b = std::is_signed<TI>::value ? 0x80808080u : 0u;
+      uint32_t s = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s = sad_u8(w[k] ^ b, s);
+      return acc + s;
+    } else if constexpr (SUM && sizeof(TI) == 2) {
+      const uint32_t b = std::is_signed<TI>::value ? 0x80008000u : 0u;
+      uint32_t s = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s = sad_u16(w[k] ^ b, s);
+      return acc + s;
+    } else if constexpr (SUM && sizeof(TI) == 4) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc += (uint64_t)(int64_t)(TI)w[k];  // (sign-extended)
+      return acc;
+    } else if constexpr (SUM) {  // 64-bit: wrapping adds
+      return acc + (((uint64_t)w[1] << 32) | w[0]) + (((uint64_t)w[3] << 32) | w[2]);
+    } else {
+      TI e[N];
+      __builtin_memcpy(e, w, 16);
+#pragma unroll
+      for (int k = 0; k < N; ++k) acc = OP == BLDP_OP_MAX ? jmax<TI>(acc, e[k]) : jmin<TI>(acc, e[k]);
+      return acc;
+    }
+  }
+  __device__ static A combine(A x, A y) {
+    if constexpr (SUM) return x + y;
+    else return OP == BLDP_OP_MAX ? jmax<TI>(x, y) : jmin<TI>(x, y);
+  }
+  // the lanes' accumulators of a group -> the group's exact value
+  __device__ static A shfl_xor(A x, int m) {
+    if constexpr (sizeof(A) == 8) {
+      uint64_t u;
+      __builtin_memcpy(&u, &x, 8);
+      const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)u, m, 64);
+      const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(u >> 32), m, 64);
+      u = ((uint64_t)hi << 32) | lo;
+      __builtin_memcpy(&x, &u, 8);
+      return x;
+    } else {
+      return (A)__shfl_xor((int)x, m, 64);
+    }
+  }
+};
+
+typedef unsigned u4u __attribute__((ext_vector_type(4), aligned(4)));
+__device__ __forceinline__ uint4 ld16(const char *p) {  // (dword-aligned: gfx950 dwordx4)
+  const u4u v = __builtin_nontemporal_load(reinterpret_cast<const u4u *>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// Grid: x = (column tile, time group) column tile fastest, y = IF, z = bank;
+// a column tile is 256 / lpg groups (lpg lanes per group, k16 16-byte loads
+// per lane per row), a time group tpb time blocks.
+template <typename TI, int OP>
+__global__ __launch_bounds__(256) void k_reduce_typed_vec(const TypedArgs a, int lpg, int k16,
+                                                          int tpb, int64_t nct) {
+  typedef Vec16<TI, OP> V;
+  typedef typename V::A A;
+  typedef typename SumT<TI>::type TS;
+  constexpr int NB = 8;  // 16-byte loads in flight per lane
+  const int tid = threadIdx.x;
+  const int64_t bx = blockIdx.x, ct = bx % nct, tg = bx / nct;
+  const int64_t co = ct * (256 / lpg) + tid / lpg;  // this lane's group (lanes of a group: one wave)
+  const int j = tid % lpg;
+  const int64_t i = blockIdx.y;
+  const int bank = blockIdx.z;
+  const bool valid = co < a.nco;
+  const int64_t T = a.T, ldb = a.in_ld_t * (int64_t)sizeof(TI), kb = 16 * (int64_t)lpg;
+  const char *base = static_cast<const char *>(a.in[bank]) +
+                     (a.in_off + i * a.in_ld_i + co * a.F) * (int64_t)sizeof(TI) + 16 * j;
+  for (int b = 0; b < tpb; ++b) {
+    const int64_t to = tg * tpb + b;
+    if (to >= a.nto) break;  // (uniform over the workgroup)
+    A acc = V::init();
+    if (valid) {
+      const char *p = base + to * T * ldb;
+      if (k16 == 1) {
+        int64_t r = 0;
+        for (; r + NB <= T; r += NB) {
+          uint4 q[NB];
+#pragma unroll
+          for (int m = 0; m < NB; ++m) q[m] = ld16(p + (r + m) * ldb);
+#pragma unroll
+          for (int m = 0; m < NB; ++m) acc = V::add(acc, q[m]);
+        }
+        for (; r < T; ++r) acc = V::add(acc, ld16(p + r * ldb));
+      } else {
+        for (int64_t r = 0; r < T; ++r, p += ldb) {
+          int k = 0;
+          for (; k + NB <= k16; k += NB) {
+            uint4 q[NB];
+#pragma unroll
+            for (int m = 0; m < NB; ++m) q[m] = ld16(p + (k + m) * kb);
+#pragma unroll
+            for (int m = 0; m < NB; ++m) acc = V::add(acc, q[m]);
+          }
+          for (; k < k16; ++k) acc = V::add(acc, ld16(p + k * kb));
+        }
+      }
+    }
+    for (int m = 1; m < lpg; m <<= 1) acc = V::combine(acc, V::shfl_xor(acc, m));
+    if (valid && j == 0) {
+      const int64_t oe = bank * a.out_bank + i * a.out_ld_i + to * a.out_ld_t + co;
+      if constexpr (V::SUM) {
+        // undo the bias of signed 8- / 16-bit elements (x + 2^(bits-1) was summed)
+        uint64_t u = acc;
+        if constexpr (std::is_signed<TI>::value && sizeof(TI) <= 2)
+          u -= (uint64_t)(a.F * T) << (8 * sizeof(TI) - 1);
+        if constexpr (OP == BLDP_OP_MEAN) {
+          const double sum = std::is_signed<TI>::value ? (double)(int64_t)u : (double)u;
+          static_cast<double *>(a.out)[oe] = sum / (double)(a.F * T);
+        } else {
+          static_cast<TS *>(a.out)[oe] = (TS)u;
+        }
+      } else {
+        static_cast<TI *>(a.out)[oe] = acc;
+      }
+    }
+  }
+}
+
 template <typename TI>
 __global__ __launch_bounds__(256) void k_kurt_typed(const TypedArgs a, double *out) {
   const int64_t nrow = a.nco * a.ni * a.nbank;
@@ -197,11 +360,69 @@ __global__ __launch_bounds__(256) void k_kurt_typed(const TypedArgs a, double *o
   }
 }
 
-int64_t cdivt(int64_t x, int64_t y) { return (x + y - 1) / y; }
-unsigned grid_for(int64_t n) { return (unsigned)std::min<int64_t>(cdivt(n, 256), 65536); }
+
+// The coalesced kernel's geometry for this window, or false when it does not
+// apply (Float64 sums, 64-bit means and inexact 32-bit means keep the
+// reference's order on k_reduce_typed; windows without dword-aligned 16-byte
+// rows of whole groups, too).
+struct TVec {
+  int lpg, k16, tpb;
+  int64_t nct, grid_x;
+};
+bool typed_vec_plan(const TypedArgs &a, int op, int num_cus, TVec *v) {
+  const int64_t sz = (int64_t)dtype_size(a.dtype);
+  const bool f64 = a.dtype == BLDP_DT_F64;
+  if (f64 && (op == BLDP_OP_SUM || op == BLDP_OP_MEAN)) return false;
+  if (op == BLDP_OP_MEAN && (sz == 8 || (sz == 4 && a.F * a.T > (1 << 21)))) return false;
+  if (a.in_cs != 1 || (a.F * sz) % 16 != 0 || a.ni > 65535 || a.nbank > 65535) return false;
+  // every 16-byte load on a dword boundary
+  auto al = [](int64_t bytes) { return bytes % 4 == 0; };
+  for (int b = 0; b < a.nbank; ++b)
+    if ((uintptr_t)a.in[b] % 4) return false;
+  if (!al(a.in_off * sz) || (a.ni > 1 && !al(a.in_ld_i * sz)) ||
+      (a.nto * a.T > 1 && !al(a.in_ld_t * sz)))
+    return false;
+  const int64_t g16 = a.F * sz / 16;
+  int lpg = 1;
+  while (lpg < 64 && g16 % (2 * lpg) == 0) lpg *= 2;
+  v->lpg = lpg;
+  v->k16 = (int)(g16 / lpg);
+  v->nct = cdivt(a.nco, 256 / lpg);
+  // time blocks per workgroup: >= 16 rows each where the blocks are short,
+  // halved while the grid holds fewer than 8 workgroups per CU
+  int64_t tpb = std::max<int64_t>(1, std::min<int64_t>(a.nto, 16 / std::max<int64_t>(1, a.T)));
+  while (tpb > 1 && v->nct * cdivt(a.nto, tpb) * a.ni * a.nbank < (int64_t)8 * num_cus) tpb /= 2;
+  v->tpb = (int)tpb;
+  v->grid_x = v->nct * cdivt(a.nto, tpb);
+  return v->grid_x <= INT32_MAX;
+}
+
+template <typename TI>
+hipError_t launch_typed_vec(const TypedArgs &a, int op, const TVec &v, hipStream_t s) {
+  const dim3 g((unsigned)v.grid_x, (unsigned)a.ni, (unsigned)a.nbank), b(256);
+  switch (op) {
+#define BLDP_TV(O)                                                                          \
+  hipLaunchKernelGGL((k_reduce_typed_vec<TI, O>), g, b, 0, s, a, v.lpg, v.k16, v.tpb, v.nct); \
+  break;
+    case BLDP_OP_SUM:
+      if constexpr (!std::is_floating_point<TI>::value) { BLDP_TV(BLDP_OP_SUM) }
+      return hipErrorInvalidValue;
+    case BLDP_OP_MEAN:
+      if constexpr (!std::is_floating_point<TI>::value && sizeof(TI) <= 4) { BLDP_TV(BLDP_OP_MEAN) }
+      return hipErrorInvalidValue;
+    case BLDP_OP_MAX: BLDP_TV(BLDP_OP_MAX)
+    case BLDP_OP_MIN: BLDP_TV(BLDP_OP_MIN)
+#undef BLDP_TV
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
 
 template <typename TI>
 hipError_t launch_typed_op(const TypedArgs &a, int op, hipStream_t s) {
+  TVec v;
+  if (opt(OPT_TYPED_VEC) && typed_vec_plan(a, op, a.num_cus, &v))
+    return launch_typed_vec<TI>(a, op, v, s);
   const int64_t n = a.nco * a.ni * a.nto * a.nbank;
   const dim3 g(grid_for(n)), b(256);
   switch (op) {

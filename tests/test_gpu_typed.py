@@ -197,3 +197,37 @@ def test_worker_api_keeps_reference_types(pkg, eng, orc, tmp_path):
     assert W.fqav(b.astype(np.int16), 4).dtype == np.int64
     with pytest.raises(TypeError):
         W.fqav(b.astype(np.float16), 4)
+
+
+@pytest.mark.parametrize("dt", ALL_TYPES, ids=lambda d: np.dtype(d).name)
+def test_typed_vec_kernel_matches_oracle(pkg, eng, orc, dt):
+    """The coalesced typed kernel (16-byte row loads, groups folded over
+    lanes: integer sums, max / min of every type, means of <= 32-bit
+    integers) against the restatement, and bit-identical to the
+    one-lane-per-group kernel (plan option typed_vec = 0): the SIGPROC 8-bit
+    0002 geometry at fqavby 64, windows, several IFs, extremes of the type."""
+    rng = np.random.default_rng(np.dtype(dt).num)
+    sz = np.dtype(dt).itemsize
+    shapes = [(65536, 1, 40, 64, 1), (4096, 2, 24, 16 // sz * 4, 3), (2048, 1, 17, 1024 // sz, 17),
+              (768, 3, 10, 48, 2), (16384, 1, 9, 4096 // sz, 1)]
+    for nc, ni, nt, F, T in shapes:
+        if nc % F:
+            continue
+        a = rand(dt, (nc, ni, nt), seed=nc + F)
+        if np.dtype(dt).kind != "f":  # the type's extremes too
+            info = np.iinfo(dt)
+            a[0, 0, 0], a[1, 0, 0] = info.min, info.max
+        else:
+            a[0, 0, 0], a[3, 0, 0], a[5, 0, min(1, nt - 1)] = np.nan, -np.inf, -0.0
+        x = to_dev(eng, a)
+        for op in ("sum", "mean", "max", "min"):
+            want = orc.np_reduce_typed(a, F, T, op)
+            got = eng.fb_to_numpy(eng.reduce(x, F, T, op))
+            assert same(got, want), (dt, (nc, ni, nt, F, T), op)
+            with pkg._lib.plan_option("typed_vec", 0):
+                assert same(eng.fb_to_numpy(eng.reduce(x, F, T, op)), got), (dt, op, "typed_vec 0")
+        # a window: channels from group 2 on, spectra 2.. (a misaligned row start)
+        w = [2 * F, nc - 2 * F, 1, 0, ni, 1, 1, (nt - 1) // T * T, 1]
+        for op in ("sum", "max"):
+            want = orc.np_reduce_typed(a, F, T, op, w)
+            assert same(eng.fb_to_numpy(eng.reduce(x, F, T, op, w)), want), (dt, op, w)

@@ -244,11 +244,17 @@ int main(int argc, char **argv) {
     int64_t bytes;
   };
   // one 0002 file (65536 x 279 floats), the 0002 band (8 of them), the 0000 band
-  const Size sizes[] = {{"0002 file 73 MB", 65536ll * 279 * 4},
-                        {"0002 band 585 MB", 8ll * 65536 * 279 * 4},
-                        {"0000 band 32 GiB", big}};
+  const Size all_sizes[] = {{"0002 file 73 MB", 65536ll * 279 * 4},
+                            {"0002 band 585 MB", 8ll * 65536 * 279 * 4},
+                            {"0001 band 14.4 GB", 8ll * 512 * 879616 * 4},
+                            {"0000 band 32 GiB", big}};
+  // argv[2] = "0001": only the 0001 band (its read:write-mix ceilings)
+  const bool only1 = argc > 2 && std::string(argv[2]) == "0001";
+  std::vector<Size> sizes;
+  for (const Size &z : all_sizes)
+    if (!only1 || std::string(z.label).rfind("0001", 0) == 0) sizes.push_back(z);
   for (const Size &s : sizes) {
-    const bool grids = s.bytes < big;
+    const bool grids = s.bytes < (1ll << 30);
     run_r<1>(in, out, s.bytes, reps, s.label, ncu, grids);
     run_r<2>(in, out, s.bytes, reps, s.label, ncu, grids);
     run_r<3>(in, out, s.bytes, reps, s.label, ncu, grids);

@@ -52,7 +52,11 @@ for s in $STEPS; do
         -- python bench.py $(bench_args "$C") ;;
     ab_*) run "$s" 900 python tools/ab_variants.py --run --suite "${s#ab_}" --rounds 5 \
           --variants "${AB_VARIANTS:-base}" --json "$OUT/$s.json" ;;
-    mix1) run mix1 300 ./build/mix_ceiling 10 ;;
+    mix1) run mix1 300 ./build/mix_ceiling 10 0001 ;;
+    typed) run typed 300 python bench.py --mode typed ;;
+    prof_typed) run prof_typed 300 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d "$OUT/prof_typed" -o run -- python bench.py --mode typed --steps 20 --warmup 5 ;;
+    getband) run getband 600 python tools/getband_probe.py --json "$OUT/getband.json" ;;
   esac
 done
 echo "== session done"
