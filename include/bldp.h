@@ -113,14 +113,23 @@ BLDP_API int bldp_reduce_plan_f32(const float *in, int64_t nchan, int64_t nif, i
                          const int64_t *win, int64_t fqavby, int64_t tavby, int op,
                          const float *out, int64_t info[8]);
 
-/* Process-wide plan options (tests and tuning): force one form of a plan the
- * planner would otherwise choose by shape.  value -1 = the planner's choice
- * (the default); *previous (may be NULL) receives the old value.  Options:
- *   "row_split"     k_reduce_row's time block over 1, 2 or 4 slices of a
- *                   workgroup (whole 16-row batches only; bit-identical forms).
- *   "force_staged"  1: bldp_band_reduce_multi_f32 takes its staged branch
- *                   (reduce on the bank's device, then a strided copy into
- *                   the slot) for every bank, the root's included.
+/* Process-wide plan options (tests and tuning): override one of the
+ * planners' measured choices.  value -1 restores the default; *previous (may
+ * be NULL) receives the old override (-1 = none).  Every form is
+ * parity-tested (tests/test_gpu_parity.py::test_plan_options_every_form).
+ *   "row_split"      k_reduce_row's time block over 1, 2 or 4 slices of a
+ *                    workgroup (whole 16-row batches only; bit-identical
+ *                    forms); default -1 = chosen by launch size
+ *   "force_staged"   1: bldp_band_reduce_multi_f32 takes its staged branch
+ *                    (reduce on the bank's device, then a strided copy into
+ *                    the slot) for every bank, the root's included
+ *   "max_wg_per_cu", "ts_fill", "narrow_mis", "t38", "wide_split",
+ *   "narrow_tpb", "lane", "lane3", "lanet", "lanet_pack", "vec_il",
+ *   "vec_row", "row_tpb", "rowt_pack", "rowt_small", "wavet",
+ *   "unaligned_vec", "kurt_exact", "kurt_mid_cpl", "kurt_mid_small",
+ *   "kurt_leaf_narrow", "kurt_leaf_tile", "typed_vec"
+ *                    which kernel a reduce / kurtosis / typed shape takes
+ *                    (csrc/kernels.hip kPlanOpts: defaults and meanings).
  * Unknown names: BLDP_EINVAL. */
 BLDP_API int bldp_plan_option(const char *name, int64_t value, int64_t *previous);
 

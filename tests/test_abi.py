@@ -512,3 +512,26 @@ def test_typed_entry_points_host_checks(pkg, L):
     assert L.bldp_kurtosis(D["u16"], None, 64, 1, 4, w, None, None) == pkg._lib.BLDP_EBOUNDS
     assert pkg.engine.out_dtype(np.dtype(np.uint8), "sum") == np.uint64
     assert pkg.engine.out_dtype(np.dtype(np.int16), "mean") == np.float64
+
+
+def test_plan_options_documented_and_accepted(pkg, L):
+    """Every plan option named in include/bldp.h is accepted by
+    bldp_plan_option, reads back what was set, and resets with -1; the
+    planner's defaults come back after the reset."""
+    src = open(os.path.join(REPO, "include", "bldp.h")).read()
+    block = src[src.index("Process-wide plan options"):src.index("BLDP_API int bldp_plan_option")]
+    names = re.findall(r'"([a-z0-9_]+)"', block)
+    assert len(names) >= 20, names
+    A = 1 << 20
+    base = plan(pkg, L, A, 65536, 1, 279, 64, 16, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
+    for n in names:
+        prev = ctypes.c_int64(99)
+        assert L.bldp_plan_option(n.encode(), 1, ctypes.byref(prev)) == 0, n
+        assert prev.value == -1, (n, prev.value)
+        assert L.bldp_plan_option(n.encode(), -1, ctypes.byref(prev)) == 0, n
+        assert prev.value == 1, (n, prev.value)
+    assert plan(pkg, L, A, 65536, 1, 279, 64, 16, [0, 65536, 1, 0, 1, 1, 0, 272, 1]) == base
+    # an option changes the plan it names, and the reset restores it
+    with pkg._lib.plan_option("vec_row", 0):
+        assert plan(pkg, L, A, 65536, 1, 279, 64, 16, [0, 65536, 1, 0, 1, 1, 0, 272, 1])[0] == 0
+    assert plan(pkg, L, A, 65536, 1, 279, 64, 16, [0, 65536, 1, 0, 1, 1, 0, 272, 1]) == base

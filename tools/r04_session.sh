@@ -54,8 +54,8 @@ for s in $STEPS; do
           --variants "${AB_VARIANTS:-base}" --json "$OUT/$s.json" ;;
     mix1) run mix1 300 ./build/mix_ceiling 10 0001 ;;
     typed) run typed 300 python bench.py --mode typed ;;
-    prof_typed) run prof_typed 300 rocprofv3 --kernel-trace --stats --output-format csv \
-        -d "$OUT/prof_typed" -o run -- python bench.py --mode typed --steps 20 --warmup 5 ;;
+    typedprof) run typedprof 300 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d "$OUT/typedprof" -o run -- python bench.py --mode typed --steps 20 --warmup 5 ;;
     getband) run getband 600 python tools/getband_probe.py --json "$OUT/getband.json" ;;
   esac
 done
