@@ -1178,7 +1178,8 @@ def test_plan_options_every_form(pkg, eng, orc, name):
     rng = np.random.default_rng(len(name))
     cases = []
     for nc, ni, nt, win, F, T in PLAN_OPTION_SHAPES:
-        a = np.asfortranarray(rng.integers(0, 256, (nc, ni, nt)).astype(np.float32))
+        top = min(255, (2 ** 24 - 1) // (F * T))  # every Float32 group sum exact (< 2^24)
+        a = np.asfortranarray(rng.integers(0, top + 1, (nc, ni, nt)).astype(np.float32))
         cases.append((a, dev(eng, a), win, F, T))
     paths = set()
     for val in PLAN_OPTION_VALUES[name]:

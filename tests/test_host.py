@@ -544,3 +544,25 @@ def test_bench_spawns_its_ranks_without_a_launcher():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["world_size"] == 2
     assert d["config"]["gathered_ranks"] == [0, 1] and d["value"] == 2.0
+
+
+def test_despike_host_keeps_the_result_type(pkg):
+    """getband's host despike for non-Float32 bands (integer sums, Float64):
+    d[spike:nfpc:end, :, :] .= d[spike-1:nfpc:end, :, :] with spike = nfpc÷2+1
+    (src/gbt.jl:101-102,111) in the band's own element type (the
+    Float32 device despike cast a UInt64 / Float64 band to Float32)."""
+    nfpc = 8
+    d = np.asfortranarray((np.arange(32 * 2 * 3, dtype=np.uint64) * (2 ** 40 + 3)).reshape(
+        (32, 2, 3), order="F"))
+    want = d.copy(order="F")
+    for c in range(nfpc // 2, 32, nfpc):  # 0-based spike bin nfpc/2 takes its left neighbour
+        want[c] = want[c - 1]
+    got = pkg.GBT._despike_host(d.copy(order="F"), nfpc)
+    assert got.dtype == np.uint64 and np.array_equal(got, want)
+    f = np.asfortranarray(np.random.default_rng(1).standard_normal((16, 1, 2)))
+    g = pkg.GBT._despike_host(f.copy(order="F"), 4)
+    assert g.dtype == np.float64 and np.array_equal(g[2::4], f[1::4])
+    with pytest.raises(pkg.BoundsError):
+        pkg.GBT._despike_host(f.copy(order="F"), 1)
+    with pytest.raises(pkg.DimensionMismatch):  # 3 spike bins vs 4 source bins
+        pkg.GBT._despike_host(np.zeros((14, 1, 1)), 4)
