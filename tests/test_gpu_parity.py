@@ -1169,7 +1169,7 @@ PLAN_OPTION_SHAPES = [
     (4096, 2, 40, [2, 4092, 1, 0, 2, 1, 0, 40, 1], 2, 5),
     (4096, 1, 40, [3, 4032, 1, 0, 1, 1, 0, 40, 1], 64, 8), (4095, 1, 40, None, 3, 10),
     (4095, 1, 40, None, 5, 1), (65536, 1, 24, None, 65536, 8), (4096, 1, 64, None, 2, 1),
-    (4096, 1, 64, None, 1, 1), (4096, 1, 64, None, 2, 3), (131072, 1, 8, None, 4, 8),
+    (4096, 1, 64, None, 1, 1), (4096, 1, 63, None, 2, 3), (131072, 1, 8, None, 4, 8),
 ]
 
 

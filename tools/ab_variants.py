@@ -545,6 +545,13 @@ def run(names, rounds, iters, suite="main"):
         band_case("0000 1 bank F64 T16", b3[:1], 64, 16)
         band_case("0000 band F256 T16", b3, 256, 16)
         cases_done = True
+    elif suite == "t1_0001":  # the 0001 band without time integration
+        del b3
+        b4 = [eng.synth(512, 1, 880000, 8, seed=10 * b + 1, kind=0) for b in range(8)]
+        for F in (1, 2, 3, 4, 8, 12, 16, 64, 512):
+            w = [0, 512 // F * F, 1, 0, 1, 1, 0, 879616, 1]
+            band_case(f"0001 band F{F} T1 {eng.plan(b4[0], F, 1, 'sum', w)['path']}", b4, F, 1, w)
+        cases_done = True
     elif suite == "kmid":  # the register-tile kurtosis path (0002 products)
         del b3
         b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
@@ -662,7 +669,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--suite", default="main", choices=["main", "rows", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy", "wide", "grid0", "grid1", "t38", "lane3", "kgrid", "lanetpack", "kshort", "kfile"])
+    ap.add_argument("--suite", default="main", choices=["main", "rows", "t1_0001", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy", "wide", "grid0", "grid1", "t38", "lane3", "kgrid", "lanetpack", "kshort", "kfile"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:
