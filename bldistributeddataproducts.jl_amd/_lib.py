@@ -71,6 +71,7 @@ SIGNATURES = {
     "bldp_band_reduce_f32": ([I, P, I64, I64, I64, P, I64, I64, I, P, P], I),
     "bldp_band_reduce_prepare_f32": ([I, P, I64, I64, I64, P, I64, I64, I, P, P], I),
     "bldp_reduce_launch": ([P, P], I),
+    "bldp_reduce_launch_timed": ([P, P, P, P], I),
     "bldp_reduce_release": ([P], I),
     "bldp_band_reduce_multi_f32": ([I, P, P, I64, I64, I64, P, I64, I64, I, I, P], I),
     "bldp_stitch_f32": ([I, P, I64, I64, I64, P, P], I),

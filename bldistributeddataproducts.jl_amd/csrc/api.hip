@@ -485,6 +485,20 @@ int bldp_reduce_launch(bldp_reduce_op_t h, void *stream) {
   return run_reduce(h->a, h->p, h->op, (hipStream_t)stream);
 }
 
+int bldp_reduce_launch_timed(bldp_reduce_op_t h, void *stream, void *ev_start, void *ev_stop) {
+  if (!h) return fail(BLDP_EINVAL, "null reduce handle");
+  if (!ev_start || !ev_stop) return fail(BLDP_EINVAL, "null timing event");
+  if (h->empty) return BLDP_OK;
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess || dev != h->dev)
+    return fail(BLDP_EINVAL, "reduce handle prepared on device %d, current device %d", h->dev,
+                dev);
+  set_launch_events((hipEvent_t)ev_start, (hipEvent_t)ev_stop);
+  const int rc = run_reduce(h->a, h->p, h->op, (hipStream_t)stream);
+  set_launch_events(nullptr, nullptr);
+  return rc;
+}
+
 int bldp_reduce_release(bldp_reduce_op_t h) {
   delete h;
   return BLDP_OK;

@@ -113,6 +113,8 @@ struct Plan {
 Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus);
 
 hipError_t launch_reduce(const RedArgs &a, const Plan &p, int op, hipStream_t s);
+// events the next launch_reduce's dispatches carry (null, null: none)
+void set_launch_events(hipEvent_t start, hipEvent_t stop);
 
 hipError_t launch_stitch(int nbank, const float *g, int64_t nc, int64_t nrows, float *out,
                          hipStream_t s);

@@ -16,6 +16,7 @@
 //     gfx950) for max/min, which is exactly Julia's max/min: NaN propagates
 //     and -0.0 < +0.0.
 // No MFMA: nothing here is matmul shaped.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -1444,13 +1445,30 @@ __global__ __launch_bounds__(kBlock) void k_synth(float *out, int64_t n, int64_t
 
 int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// Timing events carried by the reduce's own dispatches (hipExtLaunchKernel,
+// bldp_reduce_launch_timed): the start event takes the first dispatch's start
+// and the stop event the last dispatch's end, with no marker packets queued
+// between one launch and the next (a hipEventRecord pair costs a short launch
+// a few microseconds of command-processor time).
+thread_local hipEvent_t t_ev_start = nullptr, t_ev_stop = nullptr;
+
+#define BLDP_LAUNCH(KN, GR, BL, SH, ST, ...)                                          \
+  do {                                                                                \
+    if (t_ev_stop) {                                                                  \
+      hipExtLaunchKernelGGL(KN, GR, BL, SH, ST, t_ev_start, t_ev_stop, 0, __VA_ARGS__); \
+      t_ev_start = nullptr;                                                           \
+    } else {                                                                          \
+      hipLaunchKernelGGL(KN, GR, BL, SH, ST, __VA_ARGS__);                            \
+    }                                                                                 \
+  } while (0)
+
 template <int OP>
 hipError_t launch_vec(const RedArgs &a, const Plan &p, hipStream_t s) {
   const dim3 grid((unsigned)p.grid), block(kBlock);
   const int k4c = (a.k4 == 1 || a.k4 == 2 || a.k4 == 4 || a.k4 == 3) ? a.k4 : 0;
 #define BLDP_VEC(L, K)                                                 \
   if (p.lpg == L && k4c == K) {                                        \
-    hipLaunchKernelGGL((k_reduce_vec<OP, L, K>), grid, block, 0, s, a); \
+    BLDP_LAUNCH((k_reduce_vec<OP, L, K>), grid, block, 0, s, a); \
     return hipGetLastError();                                          \
   }
   BLDP_VEC(64, 1) BLDP_VEC(64, 2) BLDP_VEC(64, 4) BLDP_VEC(64, 0)
@@ -1470,7 +1488,7 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
   if (p.path == PATH_NARROW && a.tpb > 1) {  // short time blocks, several per workgroup
     const dim3 g3((unsigned)(a.blocks_c * cdiv(cdiv(a.nto, a.tpb), 1 << a.tsub_log2)),
                   (unsigned)a.ni, (unsigned)a.nbank);
-#define BLDP_NARROWT(FF, TT) hipLaunchKernelGGL((k_reduce_narrowt<OP, FF, TT>), g3, block, 0, s, a);
+#define BLDP_NARROWT(FF, TT) BLDP_LAUNCH((k_reduce_narrowt<OP, FF, TT>), g3, block, 0, s, a);
     if (a.F == 1 && a.T == 1) { BLDP_NARROWT(1, 1) }
     else if (a.F == 1 && a.T == 2) { BLDP_NARROWT(1, 2) }
     else if (a.F == 1 && a.T == 4) { BLDP_NARROWT(1, 4) }
@@ -1487,7 +1505,7 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
     (void)NW;
     const int64_t rw = (int64_t)a.tpb;  // time blocks per wave
     const dim3 g3((unsigned)(a.nco * cdiv(a.nto, 4 * rw)), (unsigned)a.ni, (unsigned)a.nbank);
-#define BLDP_WAVETL(K, T) hipLaunchKernelGGL((k_reduce_wavet<OP, K, T>), g3, block, 0, s, a); break;
+#define BLDP_WAVETL(K, T) BLDP_LAUNCH((k_reduce_wavet<OP, K, T>), g3, block, 0, s, a); break;
 #define BLDP_WAVET_T(K)                      \
   switch (a.T) {                             \
     case 1: BLDP_WAVETL(K, 1)                \
@@ -1511,7 +1529,7 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
   if (p.path == PATH_LANE && p.lanet) {  // short time blocks, small odd groups: k_reduce_lanet
     const dim3 g3((unsigned)(a.blocks_c * cdiv(cdiv(a.nto, a.tpb), 1 << a.tsub_log2)),
                   (unsigned)a.ni, (unsigned)a.nbank);
-#define BLDP_LANETL(FF, TT) hipLaunchKernelGGL((k_reduce_lanet<OP, FF, TT>), g3, block, 0, s, a); break;
+#define BLDP_LANETL(FF, TT) BLDP_LAUNCH((k_reduce_lanet<OP, FF, TT>), g3, block, 0, s, a); break;
 #define BLDP_LANET_T(FF)                   \
   switch (a.T) {                           \
     case 1: BLDP_LANETL(FF, 1)             \
@@ -1538,13 +1556,13 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
                   (unsigned)a.ni, (unsigned)a.nbank);
 #define BLDP_ROWTN(T, N)                                                                    \
   switch (a.F / 4) {                                                                        \
-    case 1: hipLaunchKernelGGL((k_reduce_rowt<OP, 1, T, N>), g3, block, 0, s, a); break;    \
-    case 2: hipLaunchKernelGGL((k_reduce_rowt<OP, 2, T, N>), g3, block, 0, s, a); break;    \
-    case 4: hipLaunchKernelGGL((k_reduce_rowt<OP, 4, T, N>), g3, block, 0, s, a); break;    \
-    case 8: hipLaunchKernelGGL((k_reduce_rowt<OP, 8, T, N>), g3, block, 0, s, a); break;    \
-    case 16: hipLaunchKernelGGL((k_reduce_rowt<OP, 16, T, N>), g3, block, 0, s, a); break;  \
-    case 32: hipLaunchKernelGGL((k_reduce_rowt<OP, 32, T, N>), g3, block, 0, s, a); break;  \
-    case 64: hipLaunchKernelGGL((k_reduce_rowt<OP, 64, T, N>), g3, block, 0, s, a); break;  \
+    case 1: BLDP_LAUNCH((k_reduce_rowt<OP, 1, T, N>), g3, block, 0, s, a); break;    \
+    case 2: BLDP_LAUNCH((k_reduce_rowt<OP, 2, T, N>), g3, block, 0, s, a); break;    \
+    case 4: BLDP_LAUNCH((k_reduce_rowt<OP, 4, T, N>), g3, block, 0, s, a); break;    \
+    case 8: BLDP_LAUNCH((k_reduce_rowt<OP, 8, T, N>), g3, block, 0, s, a); break;    \
+    case 16: BLDP_LAUNCH((k_reduce_rowt<OP, 16, T, N>), g3, block, 0, s, a); break;  \
+    case 32: BLDP_LAUNCH((k_reduce_rowt<OP, 32, T, N>), g3, block, 0, s, a); break;  \
+    case 64: BLDP_LAUNCH((k_reduce_rowt<OP, 64, T, N>), g3, block, 0, s, a); break;  \
     default: return hipErrorInvalidValue;                                                   \
   }
 #define BLDP_ROWT(T)                 \
@@ -1572,13 +1590,13 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
     const dim3 g3((unsigned)a.blocks_c, (unsigned)(a.ni * a.nto), (unsigned)a.nbank);
 #define BLDP_ROWS(S)                                                                          \
   switch (a.F / 4) {                                                                          \
-    case 1: hipLaunchKernelGGL((k_reduce_rows<OP, 1, S>), g3, block, 0, s, a); break;         \
-    case 2: hipLaunchKernelGGL((k_reduce_rows<OP, 2, S>), g3, block, 0, s, a); break;         \
-    case 4: hipLaunchKernelGGL((k_reduce_rows<OP, 4, S>), g3, block, 0, s, a); break;         \
-    case 8: hipLaunchKernelGGL((k_reduce_rows<OP, 8, S>), g3, block, 0, s, a); break;         \
-    case 16: hipLaunchKernelGGL((k_reduce_rows<OP, 16, S>), g3, block, 0, s, a); break;       \
-    case 32: hipLaunchKernelGGL((k_reduce_rows<OP, 32, S>), g3, block, 0, s, a); break;       \
-    case 64: hipLaunchKernelGGL((k_reduce_rows<OP, 64, S>), g3, block, 0, s, a); break;       \
+    case 1: BLDP_LAUNCH((k_reduce_rows<OP, 1, S>), g3, block, 0, s, a); break;         \
+    case 2: BLDP_LAUNCH((k_reduce_rows<OP, 2, S>), g3, block, 0, s, a); break;         \
+    case 4: BLDP_LAUNCH((k_reduce_rows<OP, 4, S>), g3, block, 0, s, a); break;         \
+    case 8: BLDP_LAUNCH((k_reduce_rows<OP, 8, S>), g3, block, 0, s, a); break;         \
+    case 16: BLDP_LAUNCH((k_reduce_rows<OP, 16, S>), g3, block, 0, s, a); break;       \
+    case 32: BLDP_LAUNCH((k_reduce_rows<OP, 32, S>), g3, block, 0, s, a); break;       \
+    case 64: BLDP_LAUNCH((k_reduce_rows<OP, 64, S>), g3, block, 0, s, a); break;       \
     default: return hipErrorInvalidValue;                                                     \
   }
     if (a.rsplit == 2) {
@@ -1594,13 +1612,13 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
   if (p.path == PATH_VEC_ROW) {
     const dim3 g3((unsigned)a.blocks_c, (unsigned)(a.ni * a.nto), (unsigned)a.nbank);
     switch (a.F / 4) {
-      case 1: hipLaunchKernelGGL((k_reduce_row<OP, 1>), g3, block, 0, s, a); break;
-      case 2: hipLaunchKernelGGL((k_reduce_row<OP, 2>), g3, block, 0, s, a); break;
-      case 4: hipLaunchKernelGGL((k_reduce_row<OP, 4>), g3, block, 0, s, a); break;
-      case 8: hipLaunchKernelGGL((k_reduce_row<OP, 8>), g3, block, 0, s, a); break;
-      case 16: hipLaunchKernelGGL((k_reduce_row<OP, 16>), g3, block, 0, s, a); break;
-      case 32: hipLaunchKernelGGL((k_reduce_row<OP, 32>), g3, block, 0, s, a); break;
-      case 64: hipLaunchKernelGGL((k_reduce_row<OP, 64>), g3, block, 0, s, a); break;
+      case 1: BLDP_LAUNCH((k_reduce_row<OP, 1>), g3, block, 0, s, a); break;
+      case 2: BLDP_LAUNCH((k_reduce_row<OP, 2>), g3, block, 0, s, a); break;
+      case 4: BLDP_LAUNCH((k_reduce_row<OP, 4>), g3, block, 0, s, a); break;
+      case 8: BLDP_LAUNCH((k_reduce_row<OP, 8>), g3, block, 0, s, a); break;
+      case 16: BLDP_LAUNCH((k_reduce_row<OP, 16>), g3, block, 0, s, a); break;
+      case 32: BLDP_LAUNCH((k_reduce_row<OP, 32>), g3, block, 0, s, a); break;
+      case 64: BLDP_LAUNCH((k_reduce_row<OP, 64>), g3, block, 0, s, a); break;
       default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -1608,10 +1626,10 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
   if (p.path == PATH_VEC_IL) {
     const dim3 g3((unsigned)a.blocks_c, (unsigned)(a.ni * a.nto), (unsigned)a.nbank);
     switch (a.k4) {
-      case 2: hipLaunchKernelGGL((k_reduce_il<OP, 2, kIlGpw>), g3, block, 0, s, a); break;
-      case 4: hipLaunchKernelGGL((k_reduce_il<OP, 4, kIlGpw>), g3, block, 0, s, a); break;
-      case 8: hipLaunchKernelGGL((k_reduce_il<OP, 8, kIlGpw>), g3, block, 0, s, a); break;
-      case 16: hipLaunchKernelGGL((k_reduce_il<OP, 16, kIlGpw>), g3, block, 0, s, a); break;
+      case 2: BLDP_LAUNCH((k_reduce_il<OP, 2, kIlGpw>), g3, block, 0, s, a); break;
+      case 4: BLDP_LAUNCH((k_reduce_il<OP, 4, kIlGpw>), g3, block, 0, s, a); break;
+      case 8: BLDP_LAUNCH((k_reduce_il<OP, 8, kIlGpw>), g3, block, 0, s, a); break;
+      case 16: BLDP_LAUNCH((k_reduce_il<OP, 16, kIlGpw>), g3, block, 0, s, a); break;
       default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -1619,44 +1637,44 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
     e = launch_vec<OP>(a, p, s);
   } else if (p.path == PATH_NARROW) {
     if (a.F == 1)
-      hipLaunchKernelGGL((k_reduce_narrow<OP, 1>), grid, block, 0, s, a);
+      BLDP_LAUNCH((k_reduce_narrow<OP, 1>), grid, block, 0, s, a);
     else
-      hipLaunchKernelGGL((k_reduce_narrow<OP, 2>), grid, block, 0, s, a);
+      BLDP_LAUNCH((k_reduce_narrow<OP, 2>), grid, block, 0, s, a);
     e = hipGetLastError();
   } else if (p.path == PATH_NARROW_MIS) {
     if (a.F == 1)
-      hipLaunchKernelGGL((k_reduce_narrow_mis<OP, 1>), grid, block, 0, s, a);
+      BLDP_LAUNCH((k_reduce_narrow_mis<OP, 1>), grid, block, 0, s, a);
     else
-      hipLaunchKernelGGL((k_reduce_narrow_mis<OP, 2>), grid, block, 0, s, a);
+      BLDP_LAUNCH((k_reduce_narrow_mis<OP, 2>), grid, block, 0, s, a);
     e = hipGetLastError();
   } else if (p.path == PATH_LANE) {
     switch (a.F) {
-      case 2: hipLaunchKernelGGL((k_reduce_lane<OP, 2>), grid, block, 0, s, a); break;
-      case 3: hipLaunchKernelGGL((k_reduce_lane<OP, 3>), grid, block, 0, s, a); break;
-      case 5: hipLaunchKernelGGL((k_reduce_lane<OP, 5>), grid, block, 0, s, a); break;
-      case 6: hipLaunchKernelGGL((k_reduce_lane<OP, 6>), grid, block, 0, s, a); break;
-      case 7: hipLaunchKernelGGL((k_reduce_lane<OP, 7>), grid, block, 0, s, a); break;
+      case 2: BLDP_LAUNCH((k_reduce_lane<OP, 2>), grid, block, 0, s, a); break;
+      case 3: BLDP_LAUNCH((k_reduce_lane<OP, 3>), grid, block, 0, s, a); break;
+      case 5: BLDP_LAUNCH((k_reduce_lane<OP, 5>), grid, block, 0, s, a); break;
+      case 6: BLDP_LAUNCH((k_reduce_lane<OP, 6>), grid, block, 0, s, a); break;
+      case 7: BLDP_LAUNCH((k_reduce_lane<OP, 7>), grid, block, 0, s, a); break;
       default: return hipErrorInvalidValue;
     }
     e = hipGetLastError();
   } else if (p.path == PATH_TILE) {
     if (a.in_cs == 1)
-      hipLaunchKernelGGL((k_reduce_tile<OP, true>), grid, block, 0, s, a);
+      BLDP_LAUNCH((k_reduce_tile<OP, true>), grid, block, 0, s, a);
     else
-      hipLaunchKernelGGL((k_reduce_tile<OP, false>), grid, block, 0, s, a);
+      BLDP_LAUNCH((k_reduce_tile<OP, false>), grid, block, 0, s, a);
     e = hipGetLastError();
   } else {
-    hipLaunchKernelGGL((k_reduce_scalar<OP>), grid, block, 0, s, a);
+    BLDP_LAUNCH((k_reduce_scalar<OP>), grid, block, 0, s, a);
     e = hipGetLastError();
   }
   if (e != hipSuccess || a.nchunk == 1) return e;
   const int64_t nout = (int64_t)a.nbank * a.nto * a.ni * a.nco;
   if (a.nchunk > 16) {
     const unsigned fg = (unsigned)std::min<int64_t>(cdiv(nout, 4), 16384);
-    hipLaunchKernelGGL((k_reduce_finalize_w<OP>), dim3(fg), block, 0, s, a);
+    BLDP_LAUNCH((k_reduce_finalize_w<OP>), dim3(fg), block, 0, s, a);
   } else {
     const unsigned fg = (unsigned)std::min<int64_t>(cdiv(nout, kBlock), 8192);
-    hipLaunchKernelGGL((k_reduce_finalize<OP>), dim3(fg), block, 0, s, a);
+    BLDP_LAUNCH((k_reduce_finalize<OP>), dim3(fg), block, 0, s, a);
   }
   return hipGetLastError();
 }
@@ -1882,16 +1900,17 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
       p.path = PATH_VEC_ROW;
       a.blocks_c = bc;
       a.ntiles = a.blocks_c * a.ni * a.nto * a.nbank;
-      // small launches of whole 16-row batches: the block's rows split over
-      // 2 or 4 slices of the workgroup (k_reduce_rows), so that the launch
-      // does not end on a partial round of 64 KiB tiles
+      // launches of whole 16-row batches with < 64 tiles per CU: the block's
+      // rows split over 4 slices of the workgroup (2 for F = 256, whose
+      // slices each fold 64 columns), so that the launch does not end on a
+      // partial round of 64 KiB tiles (profiles/r04/ab_rows_r04c.json: one to
+      // eight 0002 files 5-11% faster; 0000 bands, 256+ tiles per CU, 9-27%
+      // slower split)
       int64_t S = plan_opt(OPT_ROW_SPLIT);
-      if (T % 16 != 0) {
+      if (T % 16 != 0)
         S = 1;
-      } else if (S < 0) {
-        S = 1;
-        while (S < 4 && a.ntiles * S < (int64_t)8 * num_cus) S *= 2;
-      }
+      else if (S < 0)
+        S = a.ntiles < (int64_t)64 * num_cus ? (F >= 256 ? 2 : 4) : 1;
       if (S == 2 || S == 4) {
         a.rsplit = (int32_t)S;
         a.blocks_c = cdiv(a.nco * (F / 4), kBlock / S);
@@ -1935,6 +1954,11 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
   }
   a.div = (float)(F * T);
   return p;
+}
+
+void set_launch_events(hipEvent_t start, hipEvent_t stop) {
+  t_ev_start = start;
+  t_ev_stop = stop;
 }
 
 hipError_t launch_reduce(const RedArgs &a, const Plan &p, int op, hipStream_t s) {

@@ -263,6 +263,33 @@ __device__ __forceinline__ uint4 ld16(const char *p) {  // (dword-aligned: gfx95
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// One time block's result: the lanes' accumulators of a group folded, then
+// stored by the group's first lane (signed 8- / 16-bit sums unbiased).
+template <typename TI, int OP>
+__device__ __forceinline__ void typed_vec_store(const TypedArgs &a, typename Vec16<TI, OP>::A acc,
+                                                int lpg, bool st, int64_t bank, int64_t i,
+                                                int64_t to, int64_t co) {
+  typedef Vec16<TI, OP> V;
+  typedef typename SumT<TI>::type TS;
+  for (int m = 1; m < lpg; m <<= 1) acc = V::combine(acc, V::shfl_xor(acc, m));
+  if (!st) return;
+  const int64_t oe = bank * a.out_bank + i * a.out_ld_i + to * a.out_ld_t + co;
+  if constexpr (V::SUM) {
+    // undo the bias of signed 8- / 16-bit elements (x + 2^(bits-1) was summed)
+    uint64_t u = acc;
+    if constexpr (std::is_signed<TI>::value && sizeof(TI) <= 2)
+      u -= (uint64_t)(a.F * a.T) << (8 * sizeof(TI) - 1);
+    if constexpr (OP == BLDP_OP_MEAN) {
+      const double sum = std::is_signed<TI>::value ? (double)(int64_t)u : (double)u;
+      static_cast<double *>(a.out)[oe] = sum / (double)(a.F * a.T);
+    } else {
+      static_cast<TS *>(a.out)[oe] = (TS)u;
+    }
+  } else {
+    static_cast<TI *>(a.out)[oe] = acc;
+  }
+}
+
 // Grid: x = (column tile, time group) column tile fastest, y = IF, z = bank;
 // a column tile is 256 / lpg groups (lpg lanes per group, k16 16-byte loads
 // per lane per row), a time group tpb time blocks.
@@ -271,8 +298,7 @@ __global__ __launch_bounds__(256) void k_reduce_typed_vec(const TypedArgs a, int
                                                           int tpb, int64_t nct) {
   typedef Vec16<TI, OP> V;
   typedef typename V::A A;
-  typedef typename SumT<TI>::type TS;
-  constexpr int NB = 8;  // 16-byte loads in flight per lane
+  constexpr int NB = 16;  // 16-byte loads in flight per lane
   const int tid = threadIdx.x;
   const int64_t bx = blockIdx.x, ct = bx % nct, tg = bx / nct;
   const int64_t co = ct * (256 / lpg) + tid / lpg;  // this lane's group (lanes of a group: one wave)
@@ -313,25 +339,55 @@ __global__ __launch_bounds__(256) void k_reduce_typed_vec(const TypedArgs a, int
         }
       }
     }
-    for (int m = 1; m < lpg; m <<= 1) acc = V::combine(acc, V::shfl_xor(acc, m));
-    if (valid && j == 0) {
-      const int64_t oe = bank * a.out_bank + i * a.out_ld_i + to * a.out_ld_t + co;
-      if constexpr (V::SUM) {
-        // undo the bias of signed 8- / 16-bit elements (x + 2^(bits-1) was summed)
-        uint64_t u = acc;
-        if constexpr (std::is_signed<TI>::value && sizeof(TI) <= 2)
-          u -= (uint64_t)(a.F * T) << (8 * sizeof(TI) - 1);
-        if constexpr (OP == BLDP_OP_MEAN) {
-          const double sum = std::is_signed<TI>::value ? (double)(int64_t)u : (double)u;
-          static_cast<double *>(a.out)[oe] = sum / (double)(a.F * T);
-        } else {
-          static_cast<TS *>(a.out)[oe] = (TS)u;
-        }
-      } else {
-        static_cast<TI *>(a.out)[oe] = acc;
-      }
-    }
+    typed_vec_store<TI, OP>(a, acc, lpg, valid && j == 0, bank, i, to, co);
   }
+}
+
+// Short time blocks (T a power of two <= 16, one 16-byte load per lane per
+// row): the rows of the workgroup's tpb blocks (tpb * T <= 16) are loaded in
+// one batch, then folded into blocks, so a lane waits for memory once per
+// workgroup instead of once per block.
+template <typename TI, int OP>
+__global__ __launch_bounds__(256) void k_reduce_typed_vec16(const TypedArgs a, int lpg, int tpb,
+                                                            int64_t nct) {
+  typedef Vec16<TI, OP> V;
+  typedef typename V::A A;
+  const int tid = threadIdx.x;
+  const int64_t bx = blockIdx.x, ct = bx % nct, tg = bx / nct;
+  const int64_t co = ct * (256 / lpg) + tid / lpg;
+  const int j = tid % lpg;
+  const int64_t i = blockIdx.y;
+  const int bank = blockIdx.z;
+  const bool valid = co < a.nco;
+  const int T = (int)a.T, tsh = __builtin_ctz((unsigned)T);
+  const int64_t ldb = a.in_ld_t * (int64_t)sizeof(TI), to0 = tg * tpb;
+  const int nb = (int)std::min<int64_t>(tpb, a.nto - to0), nrow = nb * T;
+  A r[16];
+  if (valid) {
+    const char *p = static_cast<const char *>(a.in[bank]) +
+                    (a.in_off + i * a.in_ld_i + co * a.F) * (int64_t)sizeof(TI) + 16 * j +
+                    to0 * T * ldb;
+    uint4 q[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m)
+      if (m < nrow) q[m] = ld16(p + m * ldb);
+#pragma unroll
+    for (int m = 0; m < 16; ++m) r[m] = m < nrow ? V::add(V::init(), q[m]) : V::init();
+  } else {
+#pragma unroll
+    for (int m = 0; m < 16; ++m) r[m] = V::init();
+  }
+  // rows -> time blocks: block b's value ends in r[b * T]
+#pragma unroll
+  for (int h = 1; h < 16; h *= 2)
+    if (h < T) {
+#pragma unroll
+      for (int m = 0; m < 16; m += 2 * h) r[m] = V::combine(r[m], r[m + h]);
+    }
+#pragma unroll
+  for (int m = 0; m < 16; ++m)
+    if ((m & (T - 1)) == 0 && (m >> tsh) < nb)  // (uniform)
+      typed_vec_store<TI, OP>(a, r[m], lpg, valid && j == 0, bank, i, to0 + (m >> tsh), co);
 }
 
 template <typename TI>
@@ -367,6 +423,7 @@ __global__ __launch_bounds__(256) void k_kurt_typed(const TypedArgs a, double *o
 // rows of whole groups, too).
 struct TVec {
   int lpg, k16, tpb;
+  bool rows16;  // k_reduce_typed_vec16
   int64_t nct, grid_x;
 };
 bool typed_vec_plan(const TypedArgs &a, int op, int num_cus, TVec *v) {
@@ -388,8 +445,9 @@ bool typed_vec_plan(const TypedArgs &a, int op, int num_cus, TVec *v) {
   v->lpg = lpg;
   v->k16 = (int)(g16 / lpg);
   v->nct = cdivt(a.nco, 256 / lpg);
-  // time blocks per workgroup: >= 16 rows each where the blocks are short,
-  // halved while the grid holds fewer than 8 workgroups per CU
+  // time blocks per workgroup: 16 rows where the blocks are short, halved
+  // while the grid holds fewer than 8 workgroups per CU
+  v->rows16 = v->k16 == 1 && a.T <= 16 && (a.T & (a.T - 1)) == 0;
   int64_t tpb = std::max<int64_t>(1, std::min<int64_t>(a.nto, 16 / std::max<int64_t>(1, a.T)));
   while (tpb > 1 && v->nct * cdivt(a.nto, tpb) * a.ni * a.nbank < (int64_t)8 * num_cus) tpb /= 2;
   v->tpb = (int)tpb;
@@ -401,8 +459,11 @@ template <typename TI>
 hipError_t launch_typed_vec(const TypedArgs &a, int op, const TVec &v, hipStream_t s) {
   const dim3 g((unsigned)v.grid_x, (unsigned)a.ni, (unsigned)a.nbank), b(256);
   switch (op) {
-#define BLDP_TV(O)                                                                          \
-  hipLaunchKernelGGL((k_reduce_typed_vec<TI, O>), g, b, 0, s, a, v.lpg, v.k16, v.tpb, v.nct); \
+#define BLDP_TV(O)                                                                            \
+  if (v.rows16)                                                                               \
+    hipLaunchKernelGGL((k_reduce_typed_vec16<TI, O>), g, b, 0, s, a, v.lpg, v.tpb, v.nct);    \
+  else                                                                                        \
+    hipLaunchKernelGGL((k_reduce_typed_vec<TI, O>), g, b, 0, s, a, v.lpg, v.k16, v.tpb, v.nct); \
   break;
     case BLDP_OP_SUM:
       if constexpr (!std::is_floating_point<TI>::value) { BLDP_TV(BLDP_OP_SUM) }

@@ -320,6 +320,7 @@ class PreparedBandReduce:
         _lib.check(rc, "bldp_band_reduce_prepare_f32")
         self._L, self._h = L, h
         self._fn = L.bldp_reduce_launch
+        self._timed = L.bldp_reduce_launch_timed
         self.banks, self.out = banks, out
 
     def launch(self, stream=None) -> None:
@@ -329,6 +330,15 @@ class PreparedBandReduce:
         rc = self._fn(self._h, sp)
         if rc:
             _lib.check(rc, "bldp_reduce_launch")
+
+    def launch_timed(self, stream, ev_start, ev_stop) -> None:
+        """``launch`` with the reduce's own dispatches carrying two timing
+        ``_lib.HipEvent`` s (bldp_reduce_launch_timed): nothing is queued
+        between this launch and the next."""
+        sp = stream if isinstance(stream, int) else _lib.stream_ptr(stream)
+        rc = self._timed(self._h, sp, ev_start.ev, ev_stop.ev)
+        if rc:
+            _lib.check(rc, "bldp_reduce_launch_timed")
 
     def close(self) -> None:
         if getattr(self, "_h", None):

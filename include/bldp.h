@@ -53,7 +53,7 @@ extern "C" {
 /* 2: bldp_bslz4_decode_dev / _async take out_len (round 2); BLDP_EIO; the
  *    typed (non-Float32) entry points
  * 3: prepared band reduces (bldp_band_reduce_prepare_f32 / bldp_reduce_launch /
- *    bldp_reduce_release); bldp_plan_option; bldp_file_runs_to_device */
+ *    bldp_reduce_launch_timed / bldp_reduce_release); bldp_plan_option; bldp_file_runs_to_device */
 #define BLDP_ABI_VERSION 3
 
 #if defined(BLDP_BUILD)
@@ -174,6 +174,13 @@ BLDP_API int bldp_band_reduce_prepare_f32(int nbank, const float *const *in, int
                                           int64_t fqavby, int64_t tavby, int op, float *out,
                                           bldp_reduce_op_t *handle);
 BLDP_API int bldp_reduce_launch(bldp_reduce_op_t handle, void *stream);
+/* bldp_reduce_launch with timing: the reduce's own kernel dispatches carry
+ * the events (hipExtLaunchKernel), `ev_start` taking the first dispatch's
+ * start and `ev_stop` the last one's end, so timing a launch queues nothing
+ * between it and the next.  Both are hipEvent_t created with timing enabled;
+ * read them with hipEventElapsedTime.  An empty reduce records neither. */
+BLDP_API int bldp_reduce_launch_timed(bldp_reduce_op_t handle, void *stream, void *ev_start,
+                                      void *ev_stop);
 BLDP_API int bldp_reduce_release(bldp_reduce_op_t handle);
 
 /* One process, one or more banks per GPU: bank b lives on

@@ -106,11 +106,16 @@ def test_launch_plans_host_only(pkg, L):
     assert plan(pkg, L, A, 1 << 26, 1, 16, 8192, 16)[0] == 0
     assert plan(pkg, L, A, 4096, 1, 4096, 1024, 4096)[0] == 0
     # cfg1: F=64 -> 16 lanes per group, one float4 each: the row kernel; one
-    # file is a small launch, so each 16-row block is split over 2 workgroup
-    # slices (k_reduce_rows: 512 channels per workgroup); forced forms
+    # file is a small launch (< 64 tiles per CU), so each 16-row block is
+    # split over 4 workgroup slices (k_reduce_rows: 256 channels per
+    # workgroup), 2 at F = 256; a 0000 bank is not split; forced forms
     w272 = [0, 65536, 1, 0, 1, 1, 0, 272, 1]
     p = plan(pkg, L, A, 65536, 1, 279, 64, 16, w272)
-    assert p[0] == 5 and p[1] == 16 and p[2] == 2 and p[3] == 1 and p[5] == 128 * 17
+    assert p[0] == 5 and p[1] == 16 and p[2] == 4 and p[3] == 1 and p[5] == 256 * 17
+    p = plan(pkg, L, A, 65536, 1, 279, 256, 16, w272)
+    assert p[0] == 5 and p[2] == 2 and p[5] == 128 * 17
+    p = plan(pkg, L, A, 1 << 26, 1, 16, 64, 16)
+    assert p[0] == 5 and p[2] == 1 and p[5] == 65536
     for S, wg in ((1, 64 * 17), (2, 128 * 17), (4, 256 * 17)):
         with pkg._lib.plan_option("row_split", S):
             p = plan(pkg, L, A, 65536, 1, 279, 64, 16, w272)

@@ -616,6 +616,41 @@ def test_native_band_gather_world1(pkg, orc):
         nb.close()
 
 
+@pytest.mark.parametrize("F,T,nbank", [(64, 16, 1), (64, 16, 3), (256, 16, 2), (4, 1, 2),
+                                        (1024, 16, 1), (8, 2048, 1)])
+def test_prepared_reduce_and_timed_launch(pkg, orc, F, T, nbank):
+    """bldp_band_reduce_prepare_f32 + bldp_reduce_launch / _launch_timed give
+    band_reduce's bits on every path (row split, rowt, interleaved, chunked +
+    finalize: the timed form's events span both dispatches), launched again
+    on the same buffers; the dispatch-carried events time the launch."""
+    import torch
+
+    eng, HipEvent = pkg.engine, pkg._lib.HipEvent
+    nt = 64 if T < 2048 else 4096
+    banks = [eng.synth(16384, 1, nt + 3, 1024, seed=7 * b + F, kind=1) for b in range(nbank)]
+    win = [0, 16384, 1, 0, 1, 1, 0, nt, 1]
+    want = eng.fb_to_numpy(eng.band_reduce(banks, F, T, "sum", win))
+    prep = eng.PreparedBandReduce(banks, F, T, "sum", win)
+    try:
+        sp = int(torch.cuda.current_stream().cuda_stream)
+        e0, e1 = HipEvent(timing=True, fence=False), HipEvent(timing=True, fence=False)
+        for k in range(3):
+            prep.out.fill_(float("nan"))
+            if k == 1:
+                prep.launch(sp)
+            else:
+                prep.launch_timed(sp, e0, e1)
+            torch.cuda.synchronize()
+            assert same_bits(eng.fb_to_numpy(prep.out), want), k
+        assert 0 < e0.elapsed_time(e1) < 1000
+        b0 = orc.reduce(eng.fb_to_numpy(banks[0]), F, T, "sum", win)
+        assert same_bits(want[:16384 // F], b0)
+    finally:
+        prep.close()
+    L = pkg._lib.lib()
+    assert L.bldp_reduce_launch_timed(None, None, None, None) == pkg._lib.BLDP_EINVAL
+
+
 def test_bench_json_contract():
     """bench.py prints one JSON line with the keys the driver reads (a short
     cfg1 run; the default cfg3 run is the round-end bench)."""

@@ -201,15 +201,19 @@ def test_worker_api_keeps_reference_types(pkg, eng, orc, tmp_path):
 
 @pytest.mark.parametrize("dt", ALL_TYPES, ids=lambda d: np.dtype(d).name)
 def test_typed_vec_kernel_matches_oracle(pkg, eng, orc, dt):
-    """The coalesced typed kernel (16-byte row loads, groups folded over
-    lanes: integer sums, max / min of every type, means of <= 32-bit
+    """The coalesced typed kernels (16-byte row loads, groups folded over
+    lanes; blocks of <= 16 rows loaded in one batch: integer sums, max / min of every type, means of <= 32-bit
     integers) against the restatement, and bit-identical to the
     one-lane-per-group kernel (plan option typed_vec = 0): the SIGPROC 8-bit
     0002 geometry at fqavby 64, windows, several IFs, extremes of the type."""
     rng = np.random.default_rng(np.dtype(dt).num)
     sz = np.dtype(dt).itemsize
     shapes = [(65536, 1, 40, 64, 1), (4096, 2, 24, 16 // sz * 4, 3), (2048, 1, 17, 1024 // sz, 17),
-              (768, 3, 10, 48, 2), (16384, 1, 9, 4096 // sz, 1)]
+              (768, 3, 10, 48, 2), (16384, 1, 9, 4096 // sz, 1),
+              # short power-of-two blocks in one batch of <= 16 rows
+              # (k_reduce_typed_vec16), a partial last batch of blocks
+              (4096, 1, 70, 64, 4), (2048, 2, 45, 32, 8), (8192, 1, 50, 64, 16),
+              (1024, 1, 300, 16, 1)]
     for nc, ni, nt, F, T in shapes:
         if nc % F:
             continue

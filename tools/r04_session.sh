@@ -2,7 +2,7 @@
 # Round 4 GPU sessions: per-config kernel stats and PMC passes (one counter
 # group per run, MI355X_MICROARCH.md §rocprofv3), A/B suites, tests, bench.
 #   usage: tools/r04_session.sh TAG [steps...]
-#   steps: smoke tests tests_K bench bench_CFG prof_CFG pmc_CFG sq_CFG ab_SUITE mix1
+#   steps: smoke tests tests_K bench bench_CFG prof_CFG pmc_CFG sq_CFG ab_SUITE mix1 typed typedprof gap getband
 # Every GPU step has its own time limit; after any failure nothing more runs.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -56,6 +56,7 @@ for s in $STEPS; do
     typed) run typed 300 python bench.py --mode typed ;;
     typedprof) run typedprof 300 rocprofv3 --kernel-trace --stats --output-format csv \
         -d "$OUT/typedprof" -o run -- python bench.py --mode typed --steps 20 --warmup 5 ;;
+    gap) run gap 300 python tools/gap_probe.py --json "$OUT/gap.json" ;;
     getband) run getband 600 python tools/getband_probe.py --json "$OUT/getband.json" ;;
   esac
 done
