@@ -212,7 +212,7 @@ def test_typed_vec_kernel_matches_oracle(pkg, eng, orc, dt):
               (768, 3, 10, 48, 2), (16384, 1, 9, 4096 // sz, 1),
               # short power-of-two blocks in one batch of <= 16 rows
               # (k_reduce_typed_vec16), a partial last batch of blocks
-              (4096, 1, 70, 64, 4), (2048, 2, 45, 32, 8), (8192, 1, 50, 64, 16),
+              (4096, 1, 68, 64, 4), (2048, 2, 40, 32, 8), (8192, 1, 48, 64, 16),
               (1024, 1, 300, 16, 1)]
     for nc, ni, nt, F, T in shapes:
         if nc % F:
