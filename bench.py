@@ -613,6 +613,8 @@ def main():
     ap.add_argument("--pipeline", action="store_true",
                     help="N=1: run the N>1 exchange anyway (a one-rank process group, "
                          "RCCL gather + stitch of every step) to exercise it on one GPU")
+    ap.add_argument("--plan-option", action="append", default=[], metavar="NAME=VALUE",
+                    help="override a planner choice (bldp_plan_option; A/B runs only)")
     args = ap.parse_args()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # no launcher: this process only starts the N ranks (no torch, no HIP here)
@@ -638,6 +640,10 @@ def main():
 
     pkg = entry.load_package()
     eng = pkg.engine
+    for o in args.plan_option:
+        name, _, val = o.partition("=")
+        pkg._lib.check(pkg._lib.lib().bldp_plan_option(name.encode(), int(val), None),
+                       "bldp_plan_option")
     local = local % max(1, torch.cuda.device_count())  # gloo rehearsal: ranks share GPUs
     torch.cuda.set_device(local)
     use_pg = world > 1 or args.pipeline
@@ -740,29 +746,50 @@ def main():
         pipe.drain()
     torch.cuda.synchronize()
     # timing-only events without the system-scope fence, carried by the
-    # reduce's own dispatches (bldp_reduce_launch_timed): no marker packets
-    # between one step's kernel and the next (tools/gap_probe.py)
-    evs = [(pkg._lib.HipEvent(timing=True, fence=False),
-            pkg._lib.HipEvent(timing=True, fence=False)) for _ in range(args.steps)]
+    # reduce's own dispatches (bldp_reduce_launch_timed).  Even so, an event
+    # pair costs a launch ~4 us of command-processor time (tools/gap_probe.py:
+    # cfg1 11.4 us a step bare, 15.0 with events on every launch), so the
+    # timed steps carry only the two that span them: the first launch's start
+    # and the last one's end.  The per-launch kernel time comes from K more
+    # launches right after, each carrying its own pair (what rocprofv3's
+    # kernel trace reports).
+    HipEvent = pkg._lib.HipEvent
+    evs = [(HipEvent(timing=True, fence=False), HipEvent(timing=True, fence=False))
+           for _ in range(args.steps)]
+    sp0, sp1, sx0, sx1 = (HipEvent(timing=True, fence=False) for _ in range(4))
+    K = args.steps
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(*evs[k])
-    host_ms = (time.perf_counter() - t0) * 1e3 / args.steps  # enqueue cost per step
+    for k in range(K):
+        if K == 1:
+            step(sp0, sp1)
+        elif k == 0:
+            step(sp0, sx1)
+        elif k == K - 1:
+            step(sx0, sp1)
+        else:
+            step()
+    host_ms = (time.perf_counter() - t0) * 1e3 / K  # enqueue cost per step
     if pipe:
         pipe.drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    span_ms = sp0.elapsed_time(sp1) / K  # first kernel's start to last one's end, per launch
+    for k in range(K):  # the kernel pass
+        step(*evs[k])
+    if pipe:
+        pipe.drain()
+    torch.cuda.synchronize()
+    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / K
     if world > 1:
-        t = torch.tensor([el, kern_ms], dtype=torch.float64,
+        t = torch.tensor([el, kern_ms, span_ms], dtype=torch.float64,
                          device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el, kern_ms = float(t[0]), float(t[1])
+        el, kern_ms, span_ms = float(t[0]), float(t[1]), float(t[2])
     ms_step = el * 1e3 / args.steps
     path = eng.plan(banks[0], cfg["F"], cfg["T"], "sum", win)["path"] if banks else None
     kernel_name = {"interleaved": "k_reduce_il", "vector": "k_reduce_vec",
@@ -810,7 +837,11 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": kernel_name,
-                         "kernel_ms": round(kern_ms, 4), "bytes_per_launch": bytes_launch},
+                         "kernel_ms": round(kern_ms, 4),
+                         "kernel_ms_source": "per-launch dispatch events over K launches after "
+                                             "the timed region",
+                         "span_ms_per_launch": round(span_ms, 4),
+                         "bytes_per_launch": bytes_launch},
             "host_enqueue_ms_per_step": round(host_ms, 4),
             "cpu_baseline": cpu,
         }

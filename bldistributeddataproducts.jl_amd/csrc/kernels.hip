@@ -1716,6 +1716,7 @@ const PlanOptDef kPlanOpts[OPT_COUNT] = {
     {"kurt_leaf_narrow", 4},  // leaf plans below this many waves per CU: one channel per lane
     {"kurt_leaf_tile", 1},    // k_kurt_tile: 1 = narrow short leaves, 2 = every leaf plan
     {"typed_vec", 1},         // order-free typed reductions on k_reduce_typed_vec
+    {"typed_rows", 16},       // k_reduce_typed_vec16: most rows a workgroup loads in one batch (4-16)
 };
 struct PlanOpts {
   std::atomic<int64_t> v[OPT_COUNT];  // -1 = no override

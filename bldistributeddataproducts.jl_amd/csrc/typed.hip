@@ -241,6 +241,17 @@ struct Vec16 {
     if constexpr (SUM) return x + y;
     else return OP == BLDP_OP_MAX ? jmax<TI>(x, y) : jmin<TI>(x, y);
   }
+  // one row's 16 bytes as a row accumulator R: 32 bits for 8- / 16-bit sums
+  // (<= 16 rows of one lane stay below 2^24), else A
+  typedef typename std::conditional<SUM && sizeof(TI) <= 2, uint32_t, A>::type R;
+  __device__ static R row(uint4 q) {
+    if constexpr (SUM && sizeof(TI) <= 2) return (R)add(0, q);
+    else return add(init(), q);
+  }
+  __device__ static R rcombine(R x, R y) {
+    if constexpr (SUM) return x + y;
+    else return combine(x, y);
+  }
   // the lanes' accumulators of a group -> the group's exact value
   __device__ static A shfl_xor(A x, int m) {
     if constexpr (sizeof(A) == 8) {
@@ -347,11 +358,11 @@ __global__ __launch_bounds__(256) void k_reduce_typed_vec(const TypedArgs a, int
 // row): the rows of the workgroup's tpb blocks (tpb * T <= 16) are loaded in
 // one batch, then folded into blocks, so a lane waits for memory once per
 // workgroup instead of once per block.
-template <typename TI, int OP>
+template <typename TI, int OP, int NR>
 __global__ __launch_bounds__(256) void k_reduce_typed_vec16(const TypedArgs a, int lpg, int tpb,
                                                             int64_t nct) {
   typedef Vec16<TI, OP> V;
-  typedef typename V::A A;
+  typedef typename V::R R;
   const int tid = threadIdx.x;
   const int64_t bx = blockIdx.x, ct = bx % nct, tg = bx / nct;
   const int64_t co = ct * (256 / lpg) + tid / lpg;
@@ -362,32 +373,34 @@ __global__ __launch_bounds__(256) void k_reduce_typed_vec16(const TypedArgs a, i
   const int T = (int)a.T, tsh = __builtin_ctz((unsigned)T);
   const int64_t ldb = a.in_ld_t * (int64_t)sizeof(TI), to0 = tg * tpb;
   const int nb = (int)std::min<int64_t>(tpb, a.nto - to0), nrow = nb * T;
-  A r[16];
+  R r[NR];
   if (valid) {
     const char *p = static_cast<const char *>(a.in[bank]) +
                     (a.in_off + i * a.in_ld_i + co * a.F) * (int64_t)sizeof(TI) + 16 * j +
                     to0 * T * ldb;
-    uint4 q[16];
+    uint4 q[NR];
 #pragma unroll
-    for (int m = 0; m < 16; ++m)
+    for (int m = 0; m < NR; ++m)
       if (m < nrow) q[m] = ld16(p + m * ldb);
 #pragma unroll
-    for (int m = 0; m < 16; ++m) r[m] = m < nrow ? V::add(V::init(), q[m]) : V::init();
+    for (int m = 0; m < NR; ++m) r[m] = m < nrow ? V::row(q[m]) : V::row(make_uint4(0, 0, 0, 0));
   } else {
 #pragma unroll
-    for (int m = 0; m < 16; ++m) r[m] = V::init();
+    for (int m = 0; m < NR; ++m) r[m] = R();
   }
-  // rows -> time blocks: block b's value ends in r[b * T]
+  // rows -> time blocks: block b's value ends in r[b * T] (rows past nrow
+  // are never folded into a stored block)
 #pragma unroll
-  for (int h = 1; h < 16; h *= 2)
+  for (int h = 1; h < NR; h *= 2)
     if (h < T) {
 #pragma unroll
-      for (int m = 0; m < 16; m += 2 * h) r[m] = V::combine(r[m], r[m + h]);
+      for (int m = 0; m < NR; m += 2 * h) r[m] = V::rcombine(r[m], r[m + h]);
     }
 #pragma unroll
-  for (int m = 0; m < 16; ++m)
+  for (int m = 0; m < NR; ++m)
     if ((m & (T - 1)) == 0 && (m >> tsh) < nb)  // (uniform)
-      typed_vec_store<TI, OP>(a, r[m], lpg, valid && j == 0, bank, i, to0 + (m >> tsh), co);
+      typed_vec_store<TI, OP>(a, (typename V::A)r[m], lpg, valid && j == 0, bank, i,
+                              to0 + (m >> tsh), co);
 }
 
 template <typename TI>
@@ -423,7 +436,7 @@ __global__ __launch_bounds__(256) void k_kurt_typed(const TypedArgs a, double *o
 // rows of whole groups, too).
 struct TVec {
   int lpg, k16, tpb;
-  bool rows16;  // k_reduce_typed_vec16
+  int nr;  // k_reduce_typed_vec16's rows per batch (4, 8, 16), 0: k_reduce_typed_vec
   int64_t nct, grid_x;
 };
 bool typed_vec_plan(const TypedArgs &a, int op, int num_cus, TVec *v) {
@@ -445,12 +458,21 @@ bool typed_vec_plan(const TypedArgs &a, int op, int num_cus, TVec *v) {
   v->lpg = lpg;
   v->k16 = (int)(g16 / lpg);
   v->nct = cdivt(a.nco, 256 / lpg);
-  // time blocks per workgroup: 16 rows where the blocks are short, halved
-  // while the grid holds fewer than 8 workgroups per CU
-  v->rows16 = v->k16 == 1 && a.T <= 16 && (a.T & (a.T - 1)) == 0;
-  int64_t tpb = std::max<int64_t>(1, std::min<int64_t>(a.nto, 16 / std::max<int64_t>(1, a.T)));
+  // time blocks per workgroup: up to typed_rows (16) rows where the blocks
+  // are short, halved while the grid holds fewer than 8 workgroups per CU;
+  // one batch of the next power of two >= 4 rows (fewer registers, more
+  // waves resident, for the smaller batches)
+  const int64_t rows = std::max<int64_t>(4, std::min<int64_t>(16, opt(OPT_TYPED_ROWS)));
+  const bool batch = v->k16 == 1 && a.T <= rows && (a.T & (a.T - 1)) == 0;
+  int64_t tpb = std::max<int64_t>(1, std::min<int64_t>(a.nto, (batch ? rows : 16) /
+                                                                  std::max<int64_t>(1, a.T)));
   while (tpb > 1 && v->nct * cdivt(a.nto, tpb) * a.ni * a.nbank < (int64_t)8 * num_cus) tpb /= 2;
   v->tpb = (int)tpb;
+  v->nr = 0;
+  if (batch) {
+    const int64_t n = tpb * a.T;
+    v->nr = n <= 4 ? 4 : n <= 8 ? 8 : 16;
+  }
   v->grid_x = v->nct * cdivt(a.nto, tpb);
   return v->grid_x <= INT32_MAX;
 }
@@ -460,8 +482,12 @@ hipError_t launch_typed_vec(const TypedArgs &a, int op, const TVec &v, hipStream
   const dim3 g((unsigned)v.grid_x, (unsigned)a.ni, (unsigned)a.nbank), b(256);
   switch (op) {
 #define BLDP_TV(O)                                                                            \
-  if (v.rows16)                                                                               \
-    hipLaunchKernelGGL((k_reduce_typed_vec16<TI, O>), g, b, 0, s, a, v.lpg, v.tpb, v.nct);    \
+  if (v.nr == 4)                                                                              \
+    hipLaunchKernelGGL((k_reduce_typed_vec16<TI, O, 4>), g, b, 0, s, a, v.lpg, v.tpb, v.nct); \
+  else if (v.nr == 8)                                                                         \
+    hipLaunchKernelGGL((k_reduce_typed_vec16<TI, O, 8>), g, b, 0, s, a, v.lpg, v.tpb, v.nct); \
+  else if (v.nr == 16)                                                                        \
+    hipLaunchKernelGGL((k_reduce_typed_vec16<TI, O, 16>), g, b, 0, s, a, v.lpg, v.tpb, v.nct); \
   else                                                                                        \
     hipLaunchKernelGGL((k_reduce_typed_vec<TI, O>), g, b, 0, s, a, v.lpg, v.k16, v.tpb, v.nct); \
   break;

@@ -25,7 +25,7 @@ run() {  # name seconds cmd...
 pmc() {  # name counters...
   local name=$1; shift
   run "pmc_$name" 180 rocprofv3 --pmc "$@" --output-format csv -d "$OUT/pmc_$name" -o run \
-    -- python tools/t1_probe.py --pmc --json "$OUT/cases.json"
+    -- python tools/t1_probe.py --pmc --which "${T1_WHICH:-all}" --json "$OUT/cases.json"
 }
 
 for s in $STEPS; do
@@ -44,7 +44,8 @@ for s in $STEPS; do
     ab_*) run "$s" 900 python tools/ab_variants.py --run --suite "${s#ab_}" --rounds 5 \
           --variants "${AB_VARIANTS:-base,r02}" --json "$OUT/$s.json" ;;
     stats) run stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run \
-          -- python tools/t1_probe.py --rounds 3 --iters 10 --json "$OUT/t1_probe.json" ;;
+          -- python tools/t1_probe.py --rounds 3 --iters 10 --which "${T1_WHICH:-all}" \
+          --json "$OUT/t1_probe.json" ;;
     pmc)
       pmc fetch FETCH_SIZE
       pmc write WRITE_SIZE

@@ -35,6 +35,7 @@ for s in $STEPS; do
           --timeout-method thread -k "${s#tests_}" ;;
     bench) run bench 600 python bench.py ;;
     bench_*) run "$s" 600 python bench.py --config "${s#bench_}" ;;
+    benchw_*) run "$s" 600 python bench.py --config "${s#benchw_}" --warmup 300 --no-cpu-baseline ;;
     prof_*) C=${s#prof_}
       run "$s" 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$s" -o run \
         -- python bench.py $(bench_args "$C") ;;
@@ -54,6 +55,7 @@ for s in $STEPS; do
           --variants "${AB_VARIANTS:-base}" --json "$OUT/$s.json" ;;
     mix1) run mix1 300 ./build/mix_ceiling 10 0001 ;;
     typed) run typed 300 python bench.py --mode typed ;;
+    typed_*) run "$s" 300 python bench.py --mode typed --plan-option typed_rows="${s#typed_}" ;;
     typedprof) run typedprof 300 rocprofv3 --kernel-trace --stats --output-format csv \
         -d "$OUT/typedprof" -o run -- python bench.py --mode typed --steps 20 --warmup 5 ;;
     gap) run gap 300 python tools/gap_probe.py --json "$OUT/gap.json" ;;

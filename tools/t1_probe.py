@@ -15,6 +15,7 @@ Shapes (reference: src/gbtworkerfunctions.jl:16-20, 188):
   0002 band   8 x (65536, 1, 279), F = 2, 3 (65535-channel window),
               8, 12 (65532-channel window), 64, 256
   0002 file   1 x (65536, 1, 279), F = 64 (exactly getdata(f; fqavby=64))
+  0001 band   8 x (512, 1, 880000), F = 1, 2, 3, 4, 8, 12, 16, 64, 512 (--which 0001)
 """
 from __future__ import annotations
 
@@ -59,6 +60,11 @@ def build_cases(pkg, which="all"):
         for F, nc in ((2, 65536), (3, 65535), (8, 65536), (12, 65532), (64, 65536), (256, 65536)):
             band_case(f"0002 band F{F} T1", b2, F, 1, nc)
         band_case("0002 file F64 T1", b2[:1], 64, 1)
+    if which == "0001":  # 8 x (512, 1, 880000): VERDICT r03 next #5
+        b4 = [eng.synth(512, 1, 880000, 8, seed=10 * b + 1, kind=0, out=o)
+              for b, o in enumerate(eng.band_empty(8, 512, 1, 880000))]
+        for F in (1, 2, 3, 4, 8, 12, 16, 64, 512):
+            band_case(f"0001 band F{F} T1", b4, F, 1, 512 // F * F)
     return cases
 
 
@@ -68,7 +74,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--pmc", action="store_true")
     ap.add_argument("--pmc-calls", type=int, default=5)
-    ap.add_argument("--which", default="all", choices=["all", "0000", "0002"])
+    ap.add_argument("--which", default="all", choices=["all", "0000", "0002", "0001"])
     ap.add_argument("--lib", default=None, help="a variant libbldp .so (tools/ab_variants.py)")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
