@@ -56,6 +56,7 @@ VARIANTS = {
     "rows4": {"opts": {"row_split": 4}},
     "nolanet": {"opts": {"lanet": 0}},  # small odd F, short time blocks: the lane / tile / vector paths
     "nolanetpack": {"opts": {"lanet_pack": 0}},  # lanet: one time group per workgroup on narrow windows
+    "nodense": {"opts": {"lanet_dense": 0}},  # lanet's power-of-two lane sets on narrow windows
     "kleafwide": {"opts": {"kurt_leaf_narrow": 0}},  # k_kurt_leaf always 4 channels per lane
     "ktile0": {"opts": {"kurt_leaf_tile": 0}},  # short narrow windows on the streamed leaf lanes
     "ktile2": {"opts": {"kurt_leaf_tile": 2}},  # every leaf plan read whole into registers
