@@ -24,6 +24,7 @@ sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 VDIR = os.path.join(REPO, "build", "variants")
 CSRC = os.path.join(REPO, "bldistributeddataproducts.jl_amd", "csrc")
+PRODUCT_LIB = os.path.join(REPO, "bldistributeddataproducts.jl_amd", "libbldp_hip.so")
 
 # Variant kinds:
 #   {"opts": {name: value}}  runtime plan options (bldp_plan_option) on the base
@@ -190,8 +191,8 @@ def build(names):
     for n in names:
         out = os.path.join(VDIR, f"libbldp_{n}.so")
         v = VARIANTS[n]
-        if isinstance(v, dict) and "opts" in v:
-            continue  # runtime plan option on the base build
+        if n == "base" or (isinstance(v, dict) and "opts" in v):
+            continue  # the product build itself (runtime plan options)
         if isinstance(v, str):
             csrc, extra = CSRC, v
         elif "patch" in v:
@@ -227,8 +228,8 @@ def run(names, rounds, iters, suite="main"):
     eng = pkg.engine
     def lib_path(n):
         v = VARIANTS.get(n)
-        if isinstance(v, dict) and "opts" in v:
-            return os.path.join(VDIR, "libbldp_base.so")
+        if n == "base" or (isinstance(v, dict) and "opts" in v):
+            return PRODUCT_LIB  # the in-tree product build (options set at run time)
         return os.path.join(VDIR, f"libbldp_{n}.so")
 
     libs = {n: load(lib_path(n)) for n in names}
