@@ -32,6 +32,12 @@ SUBSPAN_MAX_FRACTION = 0.5
 PIECE_BYTES = 4 << 20    # largest single pread
 BATCH_BYTES = 64 << 20   # one pinned slot = one H2D copy
 NSLOTS = 4               # up to NSLOTS - 1 batches being read while one is copied
+# the native reader's ring (bldp_runs_to_device / bldp_file_runs_to_device):
+# the same 256 MiB of pinned slots as 8 x 32 MiB, so the first H2D copy
+# starts after 32 MiB of reads and the last one is half as long
+# (BLDP_NATIVE_BATCH_MB overrides the slot size, for probes)
+NATIVE_BATCH_BYTES = int(os.environ.get("BLDP_NATIVE_BATCH_MB", "32")) << 20
+NATIVE_NSLOTS = max(2, min(16, (256 << 20) // NATIVE_BATCH_BYTES))
 
 
 def _check(win, jshape):
@@ -281,7 +287,8 @@ def _runs_native(path, runs, device, total, timings):
     try:
         with torch.cuda.device(dev):
             rc = _lib.lib().bldp_runs_to_device(fd, len(ln), fo.ctypes.data, ln.ctypes.data,
-                                                out.data_ptr(), out.numel(), BATCH_BYTES, NSLOTS,
+                                                out.data_ptr(), out.numel(),
+                                                NATIVE_BATCH_BYTES, NATIVE_NSLOTS,
                                                 cs.cuda_stream, _lib.stream_ptr(), stats)
     finally:
         os.close(fd)
@@ -343,7 +350,8 @@ def files_to_device(paths, bases, runs0, dshape, device, timings=None):
             with torch.cuda.device(dev):
                 rc = _lib.lib().bldp_file_runs_to_device(
                     len(ln), fd.ctypes.data, fo.ctypes.data, ln.ctypes.data, out.data_ptr(),
-                    out.numel(), BATCH_BYTES, NSLOTS, cs.cuda_stream, _lib.stream_ptr(), stats)
+                    out.numel(), NATIVE_BATCH_BYTES, NATIVE_NSLOTS, cs.cuda_stream,
+                    _lib.stream_ptr(), stats)
         finally:
             for f in fds:
                 os.close(f)

@@ -283,7 +283,7 @@ def _band_on_device(ws, fs, idxs, fqavby, op, tavby, nfpc, timings=None):
         t3 = time.perf_counter()
         if nfpc:
             engine.despike(band, nco // 64 if nfpc is True else int(nfpc))
-        out = engine.fb_to_numpy(band)  # the one device -> host copy
+        out = engine.fb_to_numpy(band, pinned=True)  # the one device -> host copy
         tm["despike_d2h_ms"] = (time.perf_counter() - t3) * 1e3
     tm["path"] = "raw band" if raw else "bank by bank"
     tm["total_ms"] = (time.perf_counter() - t0) * 1e3

@@ -59,6 +59,8 @@ for s in $STEPS; do
     typedprof) run typedprof 300 rocprofv3 --kernel-trace --stats --output-format csv \
         -d "$OUT/typedprof" -o run -- python bench.py --mode typed --steps 20 --warmup 5 ;;
     gap) run gap 300 python tools/gap_probe.py --json "$OUT/gap.json" ;;
+    getband64) run getband64 600 env BLDP_NATIVE_BATCH_MB=64 python tools/getband_probe.py \
+        --json "$OUT/getband64.json" ;;
     getband) run getband 600 python tools/getband_probe.py --json "$OUT/getband.json" ;;
   esac
 done
