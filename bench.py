@@ -613,6 +613,8 @@ def main():
     ap.add_argument("--pipeline", action="store_true",
                     help="N=1: run the N>1 exchange anyway (a one-rank process group, "
                          "RCCL gather + stitch of every step) to exercise it on one GPU")
+    ap.add_argument("--settle-ms", type=float, default=100.0,
+                    help="untimed launches for this long before the warmup steps (GPU clocks)")
     ap.add_argument("--plan-option", action="append", default=[], metavar="NAME=VALUE",
                     help="override a planner choice (bldp_plan_option; A/B runs only)")
     args = ap.parse_args()
@@ -740,6 +742,23 @@ def main():
             prep.launch(sp)
         return pipe.exchange(slot) if pipe else prep.out  # root: the stitched band
 
+    # clock settle: the GPU's clocks ramp under sustained load, so the W
+    # warmup steps are preceded by untimed launches until --settle-ms of GPU
+    # time has passed (the 0002 band's 86 us kernel: 85.8 us after 5 warmup
+    # launches, 83.9 us after 300, profiles/r04/bench_cfg2_warmup_r04e.json)
+    # (the reduce alone, into an output of its own: ranks may settle for
+    # different counts without unbalancing the exchange's collectives)
+    settle = 0
+    if args.settle_ms > 0:
+        sprep = eng.PreparedBandReduce(banks, cfg["F"], cfg["T"], "sum", win)
+        t_settle = time.perf_counter()
+        while (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:
+            for _ in range(8):
+                sprep.launch(sp)
+            settle += 8
+            torch.cuda.synchronize()
+        sprep.close()
+        del sprep
     for _ in range(args.warmup):
         step()
     if pipe:
@@ -843,6 +862,7 @@ def main():
                          "span_ms_per_launch": round(span_ms, 4),
                          "bytes_per_launch": bytes_launch},
             "host_enqueue_ms_per_step": round(host_ms, 4),
+            "settle_launches": settle,
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)

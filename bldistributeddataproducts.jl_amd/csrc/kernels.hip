@@ -732,47 +732,6 @@ __global__ __launch_bounds__(kBlock) void k_reduce_lanet(const RedArgs a) {
   }
 }
 
-// k_reduce_lanet with the lanes laid densely over (time group, group) pairs:
-// lane k of the launch takes group k % nco of time group k / nco, so a window
-// of a few hundred groups or less (the 512-channel 0001 product: 170 groups a
-// row at fqavby = 3, 42 at 12) keeps every lane busy where k_reduce_lanet's
-// power-of-two lane sets per time group left a third of them idle.  Rows and
-// blocks are summed exactly as k_reduce_lanet sums them (bit-identical); its
-// 64-byte output alignment is dropped (a row of a few hundred outputs is one
-// or two workgroups' stores either way).  Plan option "lanet_dense".
-template <int OP, int F, int T>
-__global__ __launch_bounds__(kBlock) void k_reduce_laned(const RedArgs a) {
-  constexpr int TPB = kLanetRows / T, NRW = TPB * T;
-  const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  const int64_t tgp = k / a.nco, g = k - tgp * a.nco;
-  const uint32_t i = blockIdx.y;
-  const int bank = blockIdx.z;
-  const float id = R<OP>::id();
-  const int64_t ld = a.in_ld_t, tp0 = tgp * TPB;
-  const int nbp = (int)max((int64_t)0, min((int64_t)TPB, a.nto - tp0));
-  float v[NRW][F];
-  const float *p = a.in[bank] + a.in_off + (int64_t)i * a.in_ld_i + tp0 * T * ld + g * F;
-#pragma unroll
-  for (int u = 0; u < NRW; ++u) {
-    if (u / T < nbp) {
-      ldF<F>(p + u * ld, v[u]);
-    } else {
-#pragma unroll
-      for (int f = 0; f < F; ++f) v[u][f] = id;
-    }
-  }
-  float *o = a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + tp0 * a.out_ld_t + g;
-#pragma unroll
-  for (int b = 0; b < TPB; ++b) {
-    float acc = id;
-#pragma unroll
-    for (int r = 0; r < T; ++r)
-#pragma unroll
-      for (int f = 0; f < F; ++f) acc = R<OP>::f(acc, v[b * T + r][f]);
-    if (b < nbp) st1<1>(o + b * a.out_ld_t, finish<OP>(acc, a));
-  }
-}
-
 // ---------------------------------------------------------------------------
 // Scalar path: any F, any channel step, any alignment.  One lane per output.
 template <int OP>
@@ -1568,15 +1527,9 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
     return hipGetLastError();
   }
   if (p.path == PATH_LANE && p.lanet) {  // short time blocks, small odd groups: k_reduce_lanet
-    const dim3 g3(p.laned ? (unsigned)p.grid / (unsigned)(a.ni * a.nbank)
-                          : (unsigned)(a.blocks_c * cdiv(cdiv(a.nto, a.tpb), 1 << a.tsub_log2)),
+    const dim3 g3((unsigned)(a.blocks_c * cdiv(cdiv(a.nto, a.tpb), 1 << a.tsub_log2)),
                   (unsigned)a.ni, (unsigned)a.nbank);
-#define BLDP_LANETL(FF, TT)                                                 \
-  if (p.laned)                                                              \
-    BLDP_LAUNCH((k_reduce_laned<OP, FF, TT>), g3, block, 0, s, a);          \
-  else                                                                      \
-    BLDP_LAUNCH((k_reduce_lanet<OP, FF, TT>), g3, block, 0, s, a);          \
-  break;
+#define BLDP_LANETL(FF, TT) BLDP_LAUNCH((k_reduce_lanet<OP, FF, TT>), g3, block, 0, s, a); break;
 #define BLDP_LANET_T(FF)                   \
   switch (a.T) {                           \
     case 1: BLDP_LANETL(FF, 1)             \
@@ -1763,8 +1716,7 @@ const PlanOptDef kPlanOpts[OPT_COUNT] = {
     {"kurt_leaf_narrow", 4},  // leaf plans below this many waves per CU: one channel per lane
     {"kurt_leaf_tile", 1},    // k_kurt_tile: 1 = narrow short leaves, 2 = every leaf plan
     {"typed_vec", 1},         // order-free typed reductions on k_reduce_typed_vec
-    {"typed_rows", 16},       // k_reduce_typed_vec16: most rows a workgroup loads in one batch (4-16)
-    {"lanet_dense", 1},       // lanet lanes dense over (time group, group): 1 below 7/8 busy, 2 always
+    {"typed_rows", 4},        // k_reduce_typed_vec16: most rows a workgroup loads in one batch (4-16)
 };
 struct PlanOpts {
   std::atomic<int64_t> v[OPT_COUNT];  // -1 = no override
@@ -1814,17 +1766,6 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
     a.nchunk = 1;
     a.rows_per_chunk = T;
     a.ntiles = a.blocks_c * cdiv(cdiv(a.nto, a.tpb), (int64_t)1 << a.tsub_log2) * a.ni * a.nbank;
-    // lanes busy in k_reduce_lanet: nco of every (256 >> sh)-lane time group's
-    // blocks_c * (256 >> sh); below 7/8 the dense layout (k_reduce_laned)
-    const int64_t lanes = a.blocks_c * (kBlock >> a.tsub_log2);
-    const int64_t dense = cdiv(a.nco * cdiv(a.nto, a.tpb), (int64_t)kBlock);
-    const int64_t ld_opt = opt(OPT_LANET_DENSE);
-    if ((ld_opt == 2 || (ld_opt == 1 && 8 * a.nco < 7 * lanes)) && dense <= INT32_MAX) {
-      p.laned = true;
-      a.tsub_log2 = 0;
-      a.blocks_c = 1;
-      a.ntiles = dense * a.ni * a.nbank;
-    }
     p.grid = a.ntiles;
     p.ws_bytes = 0;
     a.div = (float)(F * T);

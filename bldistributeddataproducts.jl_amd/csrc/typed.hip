@@ -327,15 +327,16 @@ __global__ __launch_bounds__(256) void k_reduce_typed_vec(const TypedArgs a, int
     if (valid) {
       const char *p = base + to * T * ldb;
       if (k16 == 1) {
-        int64_t r = 0;
-        for (; r + NB <= T; r += NB) {
+        for (int64_t r = 0; r < T; r += NB) {  // up to NB rows per batch, one wait each
+          const int64_t n = T - r < NB ? T - r : NB;
           uint4 q[NB];
 #pragma unroll
-          for (int m = 0; m < NB; ++m) q[m] = ld16(p + (r + m) * ldb);
+          for (int m = 0; m < NB; ++m)
+            if (m < n) q[m] = ld16(p + (r + m) * ldb);
 #pragma unroll
-          for (int m = 0; m < NB; ++m) acc = V::add(acc, q[m]);
+          for (int m = 0; m < NB; ++m)
+            if (m < n) acc = V::add(acc, q[m]);
         }
-        for (; r < T; ++r) acc = V::add(acc, ld16(p + r * ldb));
       } else {
         for (int64_t r = 0; r < T; ++r, p += ldb) {
           int k = 0;
@@ -458,10 +459,11 @@ bool typed_vec_plan(const TypedArgs &a, int op, int num_cus, TVec *v) {
   v->lpg = lpg;
   v->k16 = (int)(g16 / lpg);
   v->nct = cdivt(a.nco, 256 / lpg);
-  // time blocks per workgroup: up to typed_rows (16) rows where the blocks
+  // time blocks per workgroup: up to typed_rows (4) rows where the blocks
   // are short, halved while the grid holds fewer than 8 workgroups per CU;
-  // one batch of the next power of two >= 4 rows (fewer registers, more
-  // waves resident, for the smaller batches)
+  // one batch of the next power of two >= 4 rows.  4 rows (20 VGPRs, every
+  // wave resident) beat 8 and 16 (37 / 68 VGPRs) on the 8-bit 0002 file and
+  // band (profiles/r04/typed_rows_r04e.json)
   const int64_t rows = std::max<int64_t>(4, std::min<int64_t>(16, opt(OPT_TYPED_ROWS)));
   const bool batch = v->k16 == 1 && a.T <= rows && (a.T & (a.T - 1)) == 0;
   int64_t tpb = std::max<int64_t>(1, std::min<int64_t>(a.nto, (batch ? rows : 16) /

@@ -1157,7 +1157,7 @@ PLAN_OPTION_VALUES = {
     "t38": (0, 1), "wide_split": (0, 1), "narrow_tpb": (0, 1, 2), "lane": (0, 1, 2),
     "lane3": (0, 1), "lanet": (0, 1), "lanet_pack": (0, 1), "vec_il": (0, 1), "vec_row": (0, 1),
     "row_tpb": (0, 1), "rowt_pack": (0, 1), "rowt_small": (0, 64, 100000), "wavet": (0, 1, 2),
-    "unaligned_vec": (0, 1, 2, 3), "lanet_dense": (0, 1, 2),
+    "unaligned_vec": (0, 1, 2, 3),
 }
 # (nchan, nif, ntime, window, F, T): shapes where the options above change the plan
 PLAN_OPTION_SHAPES = [
@@ -1170,7 +1170,7 @@ PLAN_OPTION_SHAPES = [
     (4096, 1, 40, [3, 4032, 1, 0, 1, 1, 0, 40, 1], 64, 8), (4095, 1, 40, None, 3, 10),
     (4095, 1, 40, None, 5, 1), (65536, 1, 24, None, 65536, 8), (4096, 1, 64, None, 2, 1),
     (4096, 1, 64, None, 1, 1), (4096, 1, 63, None, 2, 3), (131072, 1, 8, None, 4, 8),
-    # 0001-like narrow rows on the lane path (k_reduce_laned: dense lanes)
+    # 0001-like narrow rows on the lane path (k_reduce_lanet)
     (512, 1, 4096, [0, 510, 1, 0, 1, 1, 0, 4096, 1], 3, 1),
     (512, 1, 4000, [0, 504, 1, 0, 1, 1, 0, 4000, 1], 12, 1),
     (512, 2, 100, [0, 510, 1, 0, 2, 1, 0, 100, 1], 3, 2),

@@ -230,7 +230,7 @@ def test_typed_vec_kernel_matches_oracle(pkg, eng, orc, dt):
             assert same(got, want), (dt, (nc, ni, nt, F, T), op)
             with pkg._lib.plan_option("typed_vec", 0):
                 assert same(eng.fb_to_numpy(eng.reduce(x, F, T, op)), got), (dt, op, "typed_vec 0")
-            for rows in (4, 8):  # smaller one-batch row counts
+            for rows in (8, 16):  # larger one-batch row counts
                 with pkg._lib.plan_option("typed_rows", rows):
                     assert same(eng.fb_to_numpy(eng.reduce(x, F, T, op)), got), (dt, op, rows)
         # a window: channels from group 2 on, spectra 2.. (a misaligned row start)

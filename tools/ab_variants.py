@@ -57,7 +57,17 @@ VARIANTS = {
     "rows4": {"opts": {"row_split": 4}},
     "nolanet": {"opts": {"lanet": 0}},  # small odd F, short time blocks: the lane / tile / vector paths
     "nolanetpack": {"opts": {"lanet_pack": 0}},  # lanet: one time group per workgroup on narrow windows
-    "nodense": {"opts": {"lanet_dense": 0}},  # lanet's power-of-two lane sets on narrow windows
+    # ---- code-shape patches of the 0001 short-time-block kernels (round 4)
+    "lanet16": {"patch": [("kernels.hip", "constexpr int kLanetRows = 8;",
+                           "constexpr int kLanetRows = 16;")]},
+    "rowt6": {"patch": [("kernels.hip", "__attribute__((amdgpu_waves_per_eu(1, kRowtMaxWaves)))",
+                         "__attribute__((amdgpu_waves_per_eu(kRowtMaxWaves, kRowtMaxWaves)))")]},
+    "wavetnb1": {"patch": [("kernels.hip", "constexpr int NBAT = 4, RW = TB * NBAT;",
+                            "constexpr int NBAT = 1, RW = TB * NBAT;"),
+                           ("kernels.hip", "rw = tb * 4;", "rw = tb * 1;")]},
+    "wavetnb2": {"patch": [("kernels.hip", "constexpr int NBAT = 4, RW = TB * NBAT;",
+                            "constexpr int NBAT = 2, RW = TB * NBAT;"),
+                           ("kernels.hip", "rw = tb * 4;", "rw = tb * 2;")]},
     "kleafwide": {"opts": {"kurt_leaf_narrow": 0}},  # k_kurt_leaf always 4 channels per lane
     "ktile0": {"opts": {"kurt_leaf_tile": 0}},  # short narrow windows on the streamed leaf lanes
     "ktile2": {"opts": {"kurt_leaf_tile": 2}},  # every leaf plan read whole into registers
