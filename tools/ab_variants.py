@@ -563,6 +563,24 @@ def run(names, rounds, iters, suite="main"):
         for F in (1, 2, 3, 4, 8, 12, 16, 64, 512):
             w = [0, 512 // F * F, 1, 0, 1, 1, 0, 879616, 1]
             band_case(f"0001 band F{F} T1 {eng.plan(b4[0], F, 1, 'sum', w)['path']}", b4, F, 1, w)
+        # one bank: its product rows are contiguous (no 8-bank stitch), so
+        # every output row segment is whole lines
+        for F in (3, 12, 16, 64, 512):
+            w = [0, 512 // F * F, 1, 0, 1, 1, 0, 879616, 1]
+            band_case(f"0001 1 bank F{F} T1", b4[:1], F, 1, w)
+        cases_done = True
+    elif suite == "wavet":  # k_reduce_wavet's shapes: 0001 at fqavby 512, long windows
+        del b3
+        b4 = [eng.synth(512, 1, 880000, 8, seed=10 * b + 1, kind=0) for b in range(8)]
+        for T in (1, 2, 3, 4):
+            nt = 879616 // T * T
+            band_case(f"0001 band F512 T{T}", b4, 512, T, [0, 512, 1, 0, 1, 1, 0, nt, 1])
+        band_case("0001 1 bank F512 T1", b4[:1], 512, 1, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
+        del b4
+        bl = [eng.synth(4096, 1, 70000, 1024, seed=5, kind=0)]
+        for F in (1024, 2048, 4096):
+            for T in (1, 2):
+                band_case(f"4096 x 70000 F{F} T{T}", bl, F, T, [0, 4096, 1, 0, 1, 1, 0, 70000, 1])
         cases_done = True
     elif suite == "kmid":  # the register-tile kurtosis path (0002 products)
         del b3
@@ -681,7 +699,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--suite", default="main", choices=["main", "rows", "t1_0001", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy", "wide", "grid0", "grid1", "t38", "lane3", "kgrid", "lanetpack", "kshort", "kfile"])
+    ap.add_argument("--suite", default="main", choices=["main", "rows", "t1_0001", "wavet", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy", "wide", "grid0", "grid1", "t38", "lane3", "kgrid", "lanetpack", "kshort", "kfile"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:
