@@ -1133,11 +1133,15 @@ void k_reduce_rowt(const RedArgs a) {
   // grid: x = (column block, time group) column block fastest, y = IF, z = bank.
   // Windows of <= 128 float4 columns (the 512-channel 0001 product) share a
   // workgroup between 2^tsub_log2 time groups, 256 >> tsub_log2 lanes each.
+  // With a.bpack the 2^tsub_log2 lane sets take 2^tsub_log2 consecutive banks
+  // of one time group instead (grid z = bank sets): a stitched product's rows
+  // then get whole segments of 2^tsub_log2 banks' outputs (below).
   const uint32_t bx = blockIdx.x, bc = (uint32_t)a.blocks_c;
-  const int sh = a.tsub_log2, cw = kBlock >> sh;
+  const int sh = a.tsub_log2, cw = kBlock >> sh, sub = threadIdx.x >> (8 - sh);  // (kBlock = 256)
+  const bool bp = a.bpack != 0;
   const uint32_t tq = bx / bc, i = blockIdx.y;
-  const int64_t tg = ((int64_t)tq << sh) + (tid >> (8 - sh));  // (kBlock = 256)
-  const int bank = blockIdx.z;
+  const int64_t tg = bp ? (int64_t)tq : ((int64_t)tq << sh) + sub;
+  const int bank = bp ? (int)(blockIdx.z << sh) + sub : (int)blockIdx.z;
   const int64_t col = (int64_t)(bx - tq * bc) * kBlock + (tid & (cw - 1));  // float4 column
   const int64_t to0 = tg * TPB;
   const bool valid = col < a.nco * G4 && to0 < a.nto;
@@ -1183,7 +1187,7 @@ void k_reduce_rowt(const RedArgs a) {
   constexpr int NSEL = TPB < G4 ? TPB : G4;
   constexpr int LG4 = G4 >= 64 ? 6 : G4 >= 32 ? 5 : G4 >= 16 ? 4 : G4 >= 8 ? 3 : G4 >= 4 ? 2 : G4 >= 2 ? 1 : 0;
   const int lng = 8 - sh - LG4;  // log2 of the groups per row segment (>= 0: cw >= G4)
-  const int tgl = tid >> (8 - sh), gl = (tid & (cw - 1)) >> LG4;
+  const int gl = (tid & (cw - 1)) >> LG4;
 #pragma unroll
   for (int m = 0; m < NS; ++m) {
     const int b = m * G4 + j;
@@ -1191,33 +1195,39 @@ void k_reduce_rowt(const RedArgs a) {
 #pragma unroll
     for (int q = 1; q < NSEL; ++q)
       if (m * G4 + q < TPB) val = (j == q) ? sv[m * G4 + q] : val;
-    if (b < TPB) tile[((tgl * TPB + b) << lng) + gl] = finish<OP>(val, a);
+    // tile rows: (time group, block) pairs, or with bpack one row per block
+    // holding the bank sets' segments side by side (nco = 2^lng: contiguous
+    // in the stitched product, whose banks are nco outputs apart)
+    if (b < TPB) tile[((bp ? (b << sh) + sub : sub * TPB + b) << lng) + gl] = finish<OP>(val, a);
   }
   __syncthreads();
   const int64_t gcol0 = (int64_t)(bx - tq * bc) * (kBlock / G4);
-  float *ob = a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + gcol0;
-  const int nrow = TPB << sh;
-  if (a.vec_out && lng >= 2) {
-    const int lq = lng - 2;  // log2 of the float4 per row segment
+  float *ob = a.out + (int64_t)(bp ? (int)(blockIdx.z << sh) : bank) * a.out_bank +
+              (int64_t)i * a.out_ld_i + gcol0;
+  const int nrow = bp ? TPB : TPB << sh;
+  const int lw = bp ? lng + sh : lng;  // log2 of a tile row's outputs
+  const int64_t lim = bp ? a.nco << sh : a.nco, tob = bp ? (int64_t)tq * TPB : ((int64_t)tq << sh) * TPB;
+  if (a.vec_out && lw >= 2) {
+    const int lq = lw - 2;  // log2 of the float4 per row segment
     for (int e = tid; e < (nrow << lq); e += kBlock) {
       const int r = e >> lq, q = e & ((1 << lq) - 1);
-      const int64_t to = ((int64_t)tq << sh) * TPB + r;  // r = tgl * TPB + b
+      const int64_t to = tob + r;  // r = sub * TPB + b (bpack: r = b)
       const int64_t g = gcol0 + 4 * q;
-      if (to >= a.nto || g >= a.nco) continue;
-      const float *src = &tile[(r << lng) + 4 * q];
+      if (to >= a.nto || g >= lim) continue;
+      const float *src = &tile[(r << lw) + 4 * q];
       float *dst = ob + to * a.out_ld_t + 4 * q;
-      if (g + 3 < a.nco) {
+      if (g + 3 < lim) {
         st4(dst, make_float4(src[0], src[1], src[2], src[3]));
       } else {
         for (int k = 0; k < 4; ++k)
-          if (g + k < a.nco) st1<1>(dst + k, src[k]);
+          if (g + k < lim) st1<1>(dst + k, src[k]);
       }
     }
   } else {
-    for (int e = tid; e < (nrow << lng); e += kBlock) {
-      const int r = e >> lng, q = e & ((1 << lng) - 1);
-      const int64_t to = ((int64_t)tq << sh) * TPB + r;
-      if (to >= a.nto || gcol0 + q >= a.nco) continue;
+    for (int e = tid; e < (nrow << lw); e += kBlock) {
+      const int r = e >> lw, q = e & ((1 << lw) - 1);
+      const int64_t to = tob + r;
+      if (to >= a.nto || gcol0 + q >= lim) continue;
       st1<1>(ob + to * a.out_ld_t + q, tile[e]);
     }
   }
@@ -1239,7 +1249,11 @@ void k_reduce_rowt(const RedArgs a) {
 template <int OP, int K4, int T>
 __global__ __launch_bounds__(kBlock) void k_reduce_wavet(const RedArgs a) {
   constexpr int TB = (16 / (T * K4)) > 0 ? 16 / (T * K4) : 1;  // time blocks per batch
-  constexpr int NBAT = 4, RW = TB * NBAT;                        // per wave
+  // batches per wave: one where a batch holds >= 2 time blocks (the 0001
+  // band at fqavby = 512: 2.75 -> 2.31 ms at T = 1, +3..19% at T = 2..4 and
+  // on long windows at F = 1024, 2048; profiles/r04/ab_wavet_r04g.json), else
+  // 4 (one block per batch: 4 batches measured faster than 2 at F = 4096)
+  constexpr int NBAT = TB >= 2 ? 1 : 4, RW = TB * NBAT;
   // k_reduce_vec's accumulation of one time block: K4 in {2, 4} take RB-row
   // batches (accumulator (u * K4 + k) % kNacc) then single rows (k % kNacc);
   // K4 >= 8 always the latter
@@ -1552,8 +1566,9 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
     return hipGetLastError();
   }
   if (p.path == PATH_VEC_ROW && a.tpb > 1) {  // short time blocks, several per workgroup
-    const dim3 g3((unsigned)(a.blocks_c * cdiv(cdiv(a.nto, a.tpb), 1 << a.tsub_log2)),
-                  (unsigned)a.ni, (unsigned)a.nbank);
+    const dim3 g3(a.bpack ? (unsigned)(a.blocks_c * cdiv(a.nto, a.tpb))
+                          : (unsigned)(a.blocks_c * cdiv(cdiv(a.nto, a.tpb), 1 << a.tsub_log2)),
+                  (unsigned)a.ni, (unsigned)(a.bpack ? a.nbank >> a.tsub_log2 : a.nbank));
 #define BLDP_ROWTN(T, N)                                                                    \
   switch (a.F / 4) {                                                                        \
     case 1: BLDP_LAUNCH((k_reduce_rowt<OP, 1, T, N>), g3, block, 0, s, a); break;    \
@@ -1717,6 +1732,7 @@ const PlanOptDef kPlanOpts[OPT_COUNT] = {
     {"kurt_leaf_tile", 1},    // k_kurt_tile: 1 = narrow short leaves, 2 = every leaf plan
     {"typed_vec", 1},         // order-free typed reductions on k_reduce_typed_vec
     {"typed_rows", 4},        // k_reduce_typed_vec16: most rows a workgroup loads in one batch (4-16)
+    {"row_bpack", 1},         // k_reduce_rowt: lane sets over consecutive banks on narrow stitched rows
 };
 struct PlanOpts {
   std::atomic<int64_t> v[OPT_COUNT];  // -1 = no override
@@ -1749,6 +1765,7 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
   a.tpb = 1;
   a.tsub_log2 = 0;
   a.rsplit = 1;
+  a.bpack = 0;
   const bool t38 = opt(OPT_T38) != 0;
   if (opt(OPT_LANET) && words && a.in_cs == 1 && (T == 1 || T == 2 || T == 4 || (t38 && (T == 3 || T == 8))) &&
       (F == 3 || F == 5 || F == 6 || F == 7 || F == 12) && a.ni <= 65535 && a.nbank <= 65535 &&
@@ -1849,7 +1866,7 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
       a.ts == 1 && a.nchunk == 1 &&
       (opt(OPT_WAVET) >= 2 || a.nco < 4 || a.ni * a.nto > 65535) && a.ni <= 65535 &&
       a.nbank <= 65535) {
-    const int64_t tb = std::max<int64_t>(1, 16 / (T * a.k4)), rw = tb * 4;
+    const int64_t tb = std::max<int64_t>(1, 16 / (T * a.k4)), rw = tb * (tb >= 2 ? 1 : 4);
     if (a.nco * cdiv(a.nto, 4 * rw) <= INT32_MAX) {
       a.tpb = (int32_t)rw;
       a.ntiles = a.nco * cdiv(a.nto, 4 * rw) * a.ni * a.nbank;
@@ -1895,6 +1912,17 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
       } else {
         a.tpb = (int32_t)tpb;
         a.ntiles = bc * cdiv(cdiv(a.nto, tpb), (int64_t)1 << a.tsub_log2) * a.ni * a.nbank;
+        // a stitched band of narrow banks whose row segments are < 128 bytes
+        // (the 0001 band at fqavby = 64: 32 bytes a bank): the lane sets take
+        // consecutive banks instead of time groups, so each product row gets
+        // whole segments of 2^tsub_log2 banks (option row_bpack)
+        const int64_t sets = (int64_t)1 << a.tsub_log2;
+        if (opt(OPT_ROW_BPACK) && a.tsub_log2 > 0 && cols == (kBlock >> a.tsub_log2) &&
+            a.nbank % sets == 0 && a.out_bank == a.nco && 4 * a.nco < 128 &&
+            bc * cdiv(a.nto, tpb) <= INT32_MAX) {
+          a.bpack = 1;
+          a.ntiles = bc * cdiv(a.nto, tpb) * a.ni * (a.nbank / sets);
+        }
       }
       p.grid = a.ntiles;
     } else if (bc <= INT32_MAX && a.ni * a.nto <= 65535) {

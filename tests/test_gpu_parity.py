@@ -1095,6 +1095,30 @@ def test_reduce_wide_groups_time_split(eng, orc, F, T):
     np.testing.assert_allclose(got, orc.reduce(g, F, T, "mean"), rtol=RTOL)
 
 
+@pytest.mark.parametrize("F", [64, 128, 16])
+def test_rowt_bank_pack_stitched(pkg, eng, orc, F):
+    """k_reduce_rowt with its lane sets over consecutive banks (plan option
+    row_bpack: a stitched band of narrow banks, the 0001 band at fqavby = 64,
+    so each product row gets whole segments of two banks) against the time-
+    group form and the oracle: 2, 3 (odd: no packing), 4 and 8 banks, T = 1,
+    2, 4, partial last time groups, every op; F = 16 (128-byte segments) is
+    never packed."""
+    rng = np.random.default_rng(F + 1)
+    for nb in (2, 3, 4, 8):
+        for T, nt in ((1, 4001), (2, 1000), (4, 968)):
+            data = [np.asfortranarray(rng.integers(0, 256, (512, 1, nt)).astype(np.float32))
+                    for _ in range(nb)]
+            xs = [dev(eng, a) for a in data]
+            for op in ("sum", "mean", "max", "min"):
+                got = host(eng, eng.band_reduce(xs, F, T, op))
+                with pkg._lib.plan_option("row_bpack", 0):
+                    ref = host(eng, eng.band_reduce(xs, F, T, op))
+                assert same_bits(got, ref), (F, nb, T, op)
+                want = orc.stitch([orc.reduce(a, F, T, op) for a in data])
+                assert same_bits(got, want), (F, nb, T, op)
+
+
+
 @pytest.mark.parametrize("F", [4, 16, 64, 256])
 def test_row_split_forms_bit_identical(pkg, eng, orc, F):
     """k_reduce_row and its row-split forms (k_reduce_rows, a time block's
@@ -1157,7 +1181,7 @@ PLAN_OPTION_VALUES = {
     "t38": (0, 1), "wide_split": (0, 1), "narrow_tpb": (0, 1, 2), "lane": (0, 1, 2),
     "lane3": (0, 1), "lanet": (0, 1), "lanet_pack": (0, 1), "vec_il": (0, 1), "vec_row": (0, 1),
     "row_tpb": (0, 1), "rowt_pack": (0, 1), "rowt_small": (0, 64, 100000), "wavet": (0, 1, 2),
-    "unaligned_vec": (0, 1, 2, 3),
+    "unaligned_vec": (0, 1, 2, 3), "row_bpack": (0, 1),
 }
 # (nchan, nif, ntime, window, F, T): shapes where the options above change the plan
 PLAN_OPTION_SHAPES = [
@@ -1177,6 +1201,8 @@ PLAN_OPTION_SHAPES = [
     (512, 1, 1000, [1, 507, 1, 0, 1, 1, 0, 1000, 1], 3, 4),
     (512, 1, 300, [0, 510, 1, 0, 1, 1, 0, 300, 1], 6, 1),
     (512, 1, 300, [0, 504, 1, 0, 1, 1, 0, 300, 1], 7, 1),
+    # narrow rows at fqavby 64 / 128 (row_bpack on the two-bank stitch)
+    (512, 1, 4001, None, 64, 1), (512, 1, 1000, None, 128, 2),
 ]
 
 

@@ -57,17 +57,16 @@ VARIANTS = {
     "rows4": {"opts": {"row_split": 4}},
     "nolanet": {"opts": {"lanet": 0}},  # small odd F, short time blocks: the lane / tile / vector paths
     "nolanetpack": {"opts": {"lanet_pack": 0}},  # lanet: one time group per workgroup on narrow windows
+    "nobpack": {"opts": {"row_bpack": 0}},  # rowt: time groups, not banks, share a workgroup
     # ---- code-shape patches of the 0001 short-time-block kernels (round 4)
     "lanet16": {"patch": [("kernels.hip", "constexpr int kLanetRows = 8;",
                            "constexpr int kLanetRows = 16;")]},
     "rowt6": {"patch": [("kernels.hip", "__attribute__((amdgpu_waves_per_eu(1, kRowtMaxWaves)))",
                          "__attribute__((amdgpu_waves_per_eu(kRowtMaxWaves, kRowtMaxWaves)))")]},
-    "wavetnb1": {"patch": [("kernels.hip", "constexpr int NBAT = 4, RW = TB * NBAT;",
-                            "constexpr int NBAT = 1, RW = TB * NBAT;"),
-                           ("kernels.hip", "rw = tb * 4;", "rw = tb * 1;")]},
-    "wavetnb2": {"patch": [("kernels.hip", "constexpr int NBAT = 4, RW = TB * NBAT;",
-                            "constexpr int NBAT = 2, RW = TB * NBAT;"),
-                           ("kernels.hip", "rw = tb * 4;", "rw = tb * 2;")]},
+    # k_reduce_wavet with 4 batches of TB time blocks per wave (before round 4)
+    "wavet4": {"patch": [("kernels.hip", "constexpr int NBAT = TB >= 2 ? 1 : 4,",
+                          "constexpr int NBAT = 4,"),
+                         ("kernels.hip", "rw = tb * (tb >= 2 ? 1 : 4);", "rw = tb * 4;")]},
     "kleafwide": {"opts": {"kurt_leaf_narrow": 0}},  # k_kurt_leaf always 4 channels per lane
     "ktile0": {"opts": {"kurt_leaf_tile": 0}},  # short narrow windows on the streamed leaf lanes
     "ktile2": {"opts": {"kurt_leaf_tile": 2}},  # every leaf plan read whole into registers
@@ -658,6 +657,8 @@ def run(names, rounds, iters, suite="main"):
                         call()
                     e1.record(stream)
                     e1.synchronize()
+                if r == 0:  # a sentinel, so an output a variant leaves unwritten shows
+                    out.fill_(-1.0e30)
                 with_opts(n, L, timed)
                 ms = e0.elapsed_time(e1) / iters
                 res[label][n].append(ms)
