@@ -732,6 +732,49 @@ __global__ __launch_bounds__(kBlock) void k_reduce_lanet(const RedArgs a) {
   }
 }
 
+// k_reduce_lanet over a stitched band of narrow banks (the 0001 band at
+// fqavby = 3 / 12: 170 / 42 groups a bank row): the lanes run along the
+// stitched product row, lane k of a time group taking group k % nco of bank
+// k / nco, so a workgroup's outputs of each of its rows are 256 consecutive
+// floats of the product (1 KiB, whole 64-byte lines where the row is
+// line-aligned) instead of one bank's short segment with a partial line at
+// each end, and every lane is busy (lanet left 86 of 256 idle at 170 groups).
+// Rows and blocks are summed exactly as k_reduce_lanet sums them
+// (bit-identical).  Plan option "lane_bpack".
+template <int OP, int F, int T>
+__global__ __launch_bounds__(kBlock) void k_reduce_lanes(const RedArgs a) {
+  constexpr int TPB = kLanetRows / T, NRW = TPB * T;
+  const uint32_t nbx = (uint32_t)a.blocks_c, bx = blockIdx.x, tq = bx / nbx, i = blockIdx.y;
+  const uint32_t k = (bx - tq * nbx) * kBlock + threadIdx.x;  // position in the stitched row
+  const uint32_t nco = (uint32_t)a.nco, bank = k / nco, g = k - bank * nco;
+  const bool in = bank < (uint32_t)a.nbank;
+  const float id = R<OP>::id();
+  const int64_t ld = a.in_ld_t, tp0 = (int64_t)tq * TPB;
+  const int nbp = (int)min((int64_t)TPB, a.nto - tp0);
+  float v[NRW][F];
+  const float *p = a.in[in ? bank : 0] + a.in_off + (int64_t)i * a.in_ld_i + tp0 * T * ld +
+                   (int64_t)g * F;
+#pragma unroll
+  for (int u = 0; u < NRW; ++u) {
+    if (in && u / T < nbp) {
+      ldF<F>(p + u * ld, v[u]);
+    } else {
+#pragma unroll
+      for (int f = 0; f < F; ++f) v[u][f] = id;
+    }
+  }
+  float *o = a.out + (int64_t)i * a.out_ld_i + tp0 * a.out_ld_t + k;  // (out_bank == nco)
+#pragma unroll
+  for (int b = 0; b < TPB; ++b) {
+    float acc = id;
+#pragma unroll
+    for (int r = 0; r < T; ++r)
+#pragma unroll
+      for (int f = 0; f < F; ++f) acc = R<OP>::f(acc, v[b * T + r][f]);
+    if (in && b < nbp) st1<1>(o + b * a.out_ld_t, finish<OP>(acc, a));
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Scalar path: any F, any channel step, any alignment.  One lane per output.
 template <int OP>
@@ -1541,9 +1584,15 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
     return hipGetLastError();
   }
   if (p.path == PATH_LANE && p.lanet) {  // short time blocks, small odd groups: k_reduce_lanet
-    const dim3 g3((unsigned)(a.blocks_c * cdiv(cdiv(a.nto, a.tpb), 1 << a.tsub_log2)),
-                  (unsigned)a.ni, (unsigned)a.nbank);
-#define BLDP_LANETL(FF, TT) BLDP_LAUNCH((k_reduce_lanet<OP, FF, TT>), g3, block, 0, s, a); break;
+    const dim3 g3(a.bpack ? (unsigned)(a.blocks_c * cdiv(a.nto, a.tpb))
+                          : (unsigned)(a.blocks_c * cdiv(cdiv(a.nto, a.tpb), 1 << a.tsub_log2)),
+                  (unsigned)a.ni, a.bpack ? 1u : (unsigned)a.nbank);
+#define BLDP_LANETL(FF, TT)                                        \
+  if (a.bpack)                                                     \
+    BLDP_LAUNCH((k_reduce_lanes<OP, FF, TT>), g3, block, 0, s, a); \
+  else                                                             \
+    BLDP_LAUNCH((k_reduce_lanet<OP, FF, TT>), g3, block, 0, s, a); \
+  break;
 #define BLDP_LANET_T(FF)                   \
   switch (a.T) {                           \
     case 1: BLDP_LANETL(FF, 1)             \
@@ -1733,6 +1782,7 @@ const PlanOptDef kPlanOpts[OPT_COUNT] = {
     {"typed_vec", 1},         // order-free typed reductions on k_reduce_typed_vec
     {"typed_rows", 4},        // k_reduce_typed_vec16: most rows a workgroup loads in one batch (4-16)
     {"row_bpack", 1},         // k_reduce_rowt: lane sets over consecutive banks on narrow stitched rows
+    {"lane_bpack", 1},        // k_reduce_lanes: lanet's lanes along narrow stitched band rows
 };
 struct PlanOpts {
   std::atomic<int64_t> v[OPT_COUNT];  // -1 = no override
@@ -1783,6 +1833,16 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
     a.nchunk = 1;
     a.rows_per_chunk = T;
     a.ntiles = a.blocks_c * cdiv(cdiv(a.nto, a.tpb), (int64_t)1 << a.tsub_log2) * a.ni * a.nbank;
+    // a stitched band of banks narrower than a workgroup: lanes along the
+    // product row (k_reduce_lanes, option lane_bpack)
+    const int64_t row = a.nbank * a.nco;
+    if (opt(OPT_LANE_BPACK) && a.nbank > 1 && a.out_bank == a.nco && a.nco + 15 < kBlock &&
+        row <= UINT32_MAX - kBlock && cdiv(row, (int64_t)kBlock) * cdiv(a.nto, a.tpb) <= INT32_MAX) {
+      a.bpack = 1;
+      a.tsub_log2 = 0;
+      a.blocks_c = cdiv(row, (int64_t)kBlock);
+      a.ntiles = a.blocks_c * cdiv(a.nto, a.tpb) * a.ni;
+    }
     p.grid = a.ntiles;
     p.ws_bytes = 0;
     a.div = (float)(F * T);

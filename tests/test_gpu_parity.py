@@ -1095,6 +1095,29 @@ def test_reduce_wide_groups_time_split(eng, orc, F, T):
     np.testing.assert_allclose(got, orc.reduce(g, F, T, "mean"), rtol=RTOL)
 
 
+@pytest.mark.parametrize("F", [3, 5, 6, 7, 12])
+def test_lanes_along_stitched_rows(pkg, eng, orc, F):
+    """k_reduce_lanes (plan option lane_bpack: k_reduce_lanet's lanes along
+    the stitched product row of a band of narrow banks, the 0001 band at
+    fqavby = 3 / 12) against k_reduce_lanet and the oracle: 2, 3 and 8 banks,
+    T = 1, 2, 3, 4, 8, partial last time groups, a channel window, every op."""
+    rng = np.random.default_rng(F + 7)
+    nc = 512 // F * F
+    for nb in (2, 3, 8):
+        for T, nt in ((1, 1001), (2, 300), (3, 297), (4, 100), (8, 200)):
+            data = [np.asfortranarray(rng.integers(0, 256, (512, 1, nt)).astype(np.float32))
+                    for _ in range(nb)]
+            xs = [dev(eng, a) for a in data]
+            for win in ([0, nc, 1, 0, 1, 1, 0, nt, 1], [F, nc - F, 1, 0, 1, 1, 0, nt, 1]):
+                for op in ("sum", "mean", "max", "min"):
+                    got = host(eng, eng.band_reduce(xs, F, T, op, win))
+                    with pkg._lib.plan_option("lane_bpack", 0):
+                        ref = host(eng, eng.band_reduce(xs, F, T, op, win))
+                    assert same_bits(got, ref), (F, nb, T, op, win)
+                    want = orc.stitch([orc.reduce(a, F, T, op, win) for a in data])
+                    assert same_bits(got, want), (F, nb, T, op, win)
+
+
 @pytest.mark.parametrize("F", [64, 128, 16])
 def test_rowt_bank_pack_stitched(pkg, eng, orc, F):
     """k_reduce_rowt with its lane sets over consecutive banks (plan option
@@ -1181,7 +1204,7 @@ PLAN_OPTION_VALUES = {
     "t38": (0, 1), "wide_split": (0, 1), "narrow_tpb": (0, 1, 2), "lane": (0, 1, 2),
     "lane3": (0, 1), "lanet": (0, 1), "lanet_pack": (0, 1), "vec_il": (0, 1), "vec_row": (0, 1),
     "row_tpb": (0, 1), "rowt_pack": (0, 1), "rowt_small": (0, 64, 100000), "wavet": (0, 1, 2),
-    "unaligned_vec": (0, 1, 2, 3), "row_bpack": (0, 1),
+    "unaligned_vec": (0, 1, 2, 3), "row_bpack": (0, 1), "lane_bpack": (0, 1),
 }
 # (nchan, nif, ntime, window, F, T): shapes where the options above change the plan
 PLAN_OPTION_SHAPES = [

@@ -58,6 +58,7 @@ VARIANTS = {
     "nolanet": {"opts": {"lanet": 0}},  # small odd F, short time blocks: the lane / tile / vector paths
     "nolanetpack": {"opts": {"lanet_pack": 0}},  # lanet: one time group per workgroup on narrow windows
     "nobpack": {"opts": {"row_bpack": 0}},  # rowt: time groups, not banks, share a workgroup
+    "nolanes": {"opts": {"lane_bpack": 0}},  # lanet per bank, not along the stitched row
     # ---- code-shape patches of the 0001 short-time-block kernels (round 4)
     "lanet16": {"patch": [("kernels.hip", "constexpr int kLanetRows = 8;",
                            "constexpr int kLanetRows = 16;")]},
