@@ -60,8 +60,6 @@ VARIANTS = {
     "nobpack": {"opts": {"row_bpack": 0}},  # rowt: time groups, not banks, share a workgroup
     "nolanes": {"opts": {"lane_bpack": 0}},  # lanet per bank, not along the stitched row
     # ---- code-shape patches of the 0001 short-time-block kernels (round 4)
-    "lanet16": {"patch": [("kernels.hip", "constexpr int kLanetRows = 8;",
-                           "constexpr int kLanetRows = 16;")]},
     "rowt6": {"patch": [("kernels.hip", "__attribute__((amdgpu_waves_per_eu(1, kRowtMaxWaves)))",
                          "__attribute__((amdgpu_waves_per_eu(kRowtMaxWaves, kRowtMaxWaves)))")]},
     # k_reduce_wavet with 4 batches of TB time blocks per wave (before round 4)
