@@ -94,7 +94,6 @@ VARIANTS = {
     "nolane": {"opts": {"lane": 0}},
     "lane2": {"opts": {"lane": 2}},  # F in {2, 3, 5, 6, 7} on one lane per output everywhere
     # ---- code-shape constants, text patches of the current sources
-    "lanets4": {"patch": [(K, "constexpr int kLanetRows = 8;", "constexpr int kLanetRows = 4;")]},
     "lanets16": {"patch": [(K, "constexpr int kLanetRows = 8;", "constexpr int kLanetRows = 16;")]},
     "batch4": {"patch": [(K, "constexpr int kBatch = 8;", "constexpr int kBatch = 4;")]},
     "batch16": {"patch": [(K, "constexpr int kBatch = 8;", "constexpr int kBatch = 16;")]},
@@ -125,7 +124,6 @@ VARIANTS = {
     "rowtst": _pre("-DBLDP_ROWT_LDS_OUT=0"),  # k_reduce_rowt: each wave stores its own outputs
     "lanetp3": _pre("-DBLDP_LANET_NT3=0"),  # k_reduce_lanet: F = 3 rows as plain dwordx3 loads
     "lanetntl": _pre("-DBLDP_LANET_NTL=1"),  # k_reduce_lanet: F > 4 pieces as nt loads
-    "lanetold": _pre("-DBLDP_LANET_OALIGN=0 -DBLDP_LANET_ROWS_S=16"),  # the r03f defaults
     "lanets8c2": _pre("-DBLDP_LANET_ROWS_S=8 -DBLDP_LANET_CS_S=2"),  # F <= 3: 512 groups per workgroup
     "kst1": _pre("-DBLDP_KURT_STORE=1"),
     "kleafpipe": _pre("-DBLDP_KURT_LEAF_PIPE=1"),
@@ -154,11 +152,16 @@ VARIANTS = {
 }
 VARIANTS["kmid2min"] = {"patch": VARIANTS["kmid2f32"]["patch"] + VARIANTS["kmid2nochain"]["patch"]}
 # the round-3 A/B of the reference's own fqav shapes (profiles/r03/ab_t1v_r03h.json:
-# base, lanetold, lanets4, lanets12, lanetl8, rowt8) in the pre-round-4 tree
+# base, lanetold, lanets4, lanets12, lanetl8, rowt8), rebuilt from the tree it
+# was measured on (d8a509b) with the same -D flags: "r03h" is that run's base
+R03H = "d8a509b"
 VARIANTS.update({
-    "lanets12": _pre("-DBLDP_LANET_ROWS_S=12"),
-    "lanetl8": _pre("-DBLDP_LANET_ROWS_L=8"),
-    "rowt8": _pre("-DBLDP_ROWT_SMALL=100000"),
+    "r03h": {"rev": R03H, "extra": ""},
+    "lanetold": {"rev": R03H, "extra": "-DBLDP_LANET_OALIGN=0 -DBLDP_LANET_ROWS_S=16"},
+    "lanets4": {"rev": R03H, "extra": "-DBLDP_LANET_ROWS_S=4"},
+    "lanets12": {"rev": R03H, "extra": "-DBLDP_LANET_ROWS_S=12"},
+    "lanetl8": {"rev": R03H, "extra": "-DBLDP_LANET_ROWS_L=8"},
+    "rowt8": {"rev": R03H, "extra": "-DBLDP_ROWT_ROWS=8"},
 })
 
 
