@@ -1289,8 +1289,14 @@ void k_reduce_rowt(const RedArgs a) {
 // Plan option "wavet": 1 (default) = use it where the interleaved kernel
 // cannot run or a row holds fewer than 4 groups; 2 = for every such shape;
 // 0 = never.
-template <int OP, int K4, int T>
-__global__ __launch_bounds__(kBlock) void k_reduce_wavet(const RedArgs a) {
+// BP (plan option "wave_bpack"): a stitched band whose product row is <= 16
+// groups (the 0001 band at fqavby = 512: one output per bank per spectrum) is
+// reduced by workgroups of one wave per (bank, group) of the row, all on the
+// same time blocks; their outputs go through LDS and leave as whole product
+// rows, contiguous over the workgroup's RW spectra, where each wave storing
+// its own put 4 bytes into every 32-byte row.
+template <int OP, int K4, int T, bool BP>
+__global__ __launch_bounds__(BP ? 1024 : kBlock) void k_reduce_wavet(const RedArgs a) {
   constexpr int TB = (16 / (T * K4)) > 0 ? 16 / (T * K4) : 1;  // time blocks per batch
   // batches per wave: one where a batch holds >= 2 time blocks (the 0001
   // band at fqavby = 512: 2.75 -> 2.31 ms at T = 1, +3..19% at T = 2..4 and
@@ -1302,10 +1308,13 @@ __global__ __launch_bounds__(kBlock) void k_reduce_wavet(const RedArgs a) {
   // K4 >= 8 always the latter
   constexpr int RB = (K4 == 2 || K4 == 4) ? (K4 >= kBatch ? 1 : kBatch / K4) : 0;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t bx = blockIdx.x, g = bx % a.nco, chunk = bx / a.nco;
+  const int64_t bx = blockIdx.x;
+  const int64_t g = BP ? wave % a.nco : bx % a.nco, chunk = BP ? bx : bx / a.nco;
   const int64_t i = blockIdx.y;
-  const int bank = blockIdx.z;
-  const int64_t tb0 = (chunk * 4 + wave) * RW;
+  const int bank = BP ? (int)(wave / a.nco) : (int)blockIdx.z;
+  const int64_t tb0 = BP ? chunk * RW : (chunk * 4 + wave) * RW;
+  __shared__ float tile[BP ? RW * 16 : 1];  // (BP: RW rows of <= 16 outputs)
+  const int W = BP ? (int)(blockDim.x >> 6) : 0;
   const float id = R<OP>::id();
   const float *base = a.in[bank] + a.in_off + i * a.in_ld_i + g * a.F + 4 * lane;
   const int64_t ld = a.in_ld_t;
@@ -1344,10 +1353,22 @@ __global__ __launch_bounds__(kBlock) void k_reduce_wavet(const RedArgs a) {
           for (int k = 0; k < K4; ++k)
             acc[k % kNacc] = f4<OP>(acc[k % kNacc], v[(b * T + r) * K4 + k]);
         const float s = lanes_fold<OP, 64>(fold4<OP>(fold_acc<OP>(acc)));
-        if (lane == 0)
-          st1<1>(a.out + bank * a.out_bank + i * a.out_ld_i + (t0 + b) * a.out_ld_t + g,
-                 finish<OP>(s, a));
+        if (lane == 0) {
+          if constexpr (BP)
+            tile[(bt * TB + b) * W + wave] = finish<OP>(s, a);
+          else
+            st1<1>(a.out + bank * a.out_bank + i * a.out_ld_i + (t0 + b) * a.out_ld_t + g,
+                   finish<OP>(s, a));
+        }
       }
+    }
+  }
+  if constexpr (BP) {  // the RW product rows, W = nbank * nco outputs each (out_bank = nco)
+    __syncthreads();
+    const int64_t nr = min((int64_t)RW, a.nto - tb0);
+    for (int e = threadIdx.x; e < nr * W; e += blockDim.x) {
+      const int r = e / W, w = e - r * W;
+      st1<1>(a.out + i * a.out_ld_i + (tb0 + r) * a.out_ld_t + w, tile[e]);
     }
   }
 }
@@ -1562,7 +1583,14 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
     (void)NW;
     const int64_t rw = (int64_t)a.tpb;  // time blocks per wave
     const dim3 g3((unsigned)(a.nco * cdiv(a.nto, 4 * rw)), (unsigned)a.ni, (unsigned)a.nbank);
-#define BLDP_WAVETL(K, T) BLDP_LAUNCH((k_reduce_wavet<OP, K, T>), g3, block, 0, s, a); break;
+    const unsigned wb = (unsigned)(a.nbank * a.nco);  // bpack: one wave per (bank, group)
+    const dim3 g3b((unsigned)cdiv(a.nto, rw), (unsigned)a.ni, 1u);
+#define BLDP_WAVETL(K, T)                                                        \
+  if (a.bpack)                                                                   \
+    BLDP_LAUNCH((k_reduce_wavet<OP, K, T, true>), g3b, dim3(64 * wb), 0, s, a);  \
+  else                                                                           \
+    BLDP_LAUNCH((k_reduce_wavet<OP, K, T, false>), g3, block, 0, s, a);          \
+  break;
 #define BLDP_WAVET_T(K)                      \
   switch (a.T) {                             \
     case 1: BLDP_WAVETL(K, 1)                \
@@ -1783,6 +1811,7 @@ const PlanOptDef kPlanOpts[OPT_COUNT] = {
     {"typed_rows", 4},        // k_reduce_typed_vec16: most rows a workgroup loads in one batch (4-16)
     {"row_bpack", 1},         // k_reduce_rowt: lane sets over consecutive banks on narrow stitched rows
     {"lane_bpack", 1},        // k_reduce_lanes: lanet's lanes along narrow stitched band rows
+    {"wave_bpack", 1},        // k_reduce_wavet: a wave per (bank, group) of <= 16-group stitched rows
 };
 struct PlanOpts {
   std::atomic<int64_t> v[OPT_COUNT];  // -1 = no override
@@ -1930,6 +1959,12 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
     if (a.nco * cdiv(a.nto, 4 * rw) <= INT32_MAX) {
       a.tpb = (int32_t)rw;
       a.ntiles = a.nco * cdiv(a.nto, 4 * rw) * a.ni * a.nbank;
+      // a stitched band whose product row is <= 16 groups: one workgroup per
+      // RW spectra with a wave per (bank, group), whole rows stored (wave_bpack)
+      if (opt(OPT_WAVE_BPACK) && a.nbank > 1 && a.nbank * a.nco <= 16 && a.out_bank == a.nco) {
+        a.bpack = 1;
+        a.ntiles = cdiv(a.nto, rw) * a.ni;
+      }
       p.grid = a.ntiles;
     }
   }

@@ -1095,6 +1095,28 @@ def test_reduce_wide_groups_time_split(eng, orc, F, T):
     np.testing.assert_allclose(got, orc.reduce(g, F, T, "mean"), rtol=RTOL)
 
 
+@pytest.mark.parametrize("nc", [512, 1024])
+def test_wavet_bank_pack_stitched(pkg, eng, orc, nc):
+    """k_reduce_wavet with one wave per (bank, group) of a <= 16-group
+    stitched row (plan option wave_bpack: the 0001 band at fqavby = 512)
+    against the per-wave form and the oracle: 2, 3, 8 (and 16 at one group a
+    bank) banks, T = 1, 2, 3, 4, partial last workgroups, every op."""
+    rng = np.random.default_rng(nc)
+    for nb in ((2, 3, 8, 16) if nc == 512 else (2, 3, 8)):
+        for T, nt in ((1, 1001), (2, 402), (3, 303), (4, 100)):
+            data = [np.asfortranarray(rng.integers(0, 256, (nc, 1, nt)).astype(np.float32))
+                    for _ in range(nb)]
+            xs = [dev(eng, a) for a in data]
+            assert eng.plan(xs[0], 512, T, "sum")["path"] == "vector"
+            for op in ("sum", "mean", "max", "min"):
+                got = host(eng, eng.band_reduce(xs, 512, T, op))
+                with pkg._lib.plan_option("wave_bpack", 0):
+                    ref = host(eng, eng.band_reduce(xs, 512, T, op))
+                assert same_bits(got, ref), (nc, nb, T, op)
+                want = orc.stitch([orc.reduce(a, 512, T, op) for a in data])
+                assert same_bits(got, want), (nc, nb, T, op)
+
+
 @pytest.mark.parametrize("F", [3, 5, 6, 7, 12])
 def test_lanes_along_stitched_rows(pkg, eng, orc, F):
     """k_reduce_lanes (plan option lane_bpack: k_reduce_lanet's lanes along
@@ -1205,6 +1227,7 @@ PLAN_OPTION_VALUES = {
     "lane3": (0, 1), "lanet": (0, 1), "lanet_pack": (0, 1), "vec_il": (0, 1), "vec_row": (0, 1),
     "row_tpb": (0, 1), "rowt_pack": (0, 1), "rowt_small": (0, 64, 100000), "wavet": (0, 1, 2),
     "unaligned_vec": (0, 1, 2, 3), "row_bpack": (0, 1), "lane_bpack": (0, 1),
+    "wave_bpack": (0, 1),
 }
 # (nchan, nif, ntime, window, F, T): shapes where the options above change the plan
 PLAN_OPTION_SHAPES = [

@@ -59,6 +59,7 @@ VARIANTS = {
     "nolanetpack": {"opts": {"lanet_pack": 0}},  # lanet: one time group per workgroup on narrow windows
     "nobpack": {"opts": {"row_bpack": 0}},  # rowt: time groups, not banks, share a workgroup
     "nolanes": {"opts": {"lane_bpack": 0}},  # lanet per bank, not along the stitched row
+    "nowaveb": {"opts": {"wave_bpack": 0}},  # wavet: a wave per (group, bank, time chunk)
     # ---- code-shape patches of the 0001 short-time-block kernels (round 4)
     "rowt6": {"patch": [("kernels.hip", "__attribute__((amdgpu_waves_per_eu(1, kRowtMaxWaves)))",
                          "__attribute__((amdgpu_waves_per_eu(kRowtMaxWaves, kRowtMaxWaves)))")]},
