@@ -1865,7 +1865,9 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
     // a stitched band of banks narrower than a workgroup: lanes along the
     // product row (k_reduce_lanes, option lane_bpack)
     const int64_t row = a.nbank * a.nco;
-    if (opt(OPT_LANE_BPACK) && a.nbank > 1 && a.out_bank == a.nco && a.nco + 15 < kBlock &&
+    // (F = 12: 2.94 vs 2.90 ms on the 0001 band, not taken; F = 3 3.53 vs
+    // 4.21, profiles/r04/ab_t1_0001_r04h.json)
+    if (opt(OPT_LANE_BPACK) && F <= 7 && a.nbank > 1 && a.out_bank == a.nco && a.nco + 15 < kBlock &&
         row <= UINT32_MAX - kBlock && cdiv(row, (int64_t)kBlock) * cdiv(a.nto, a.tpb) <= INT32_MAX) {
       a.bpack = 1;
       a.tsub_log2 = 0;

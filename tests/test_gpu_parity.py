@@ -1117,11 +1117,11 @@ def test_wavet_bank_pack_stitched(pkg, eng, orc, nc):
                 assert same_bits(got, want), (nc, nb, T, op)
 
 
-@pytest.mark.parametrize("F", [3, 5, 6, 7, 12])
+@pytest.mark.parametrize("F", [3, 5, 6, 7])
 def test_lanes_along_stitched_rows(pkg, eng, orc, F):
     """k_reduce_lanes (plan option lane_bpack: k_reduce_lanet's lanes along
     the stitched product row of a band of narrow banks, the 0001 band at
-    fqavby = 3 / 12) against k_reduce_lanet and the oracle: 2, 3 and 8 banks,
+    fqavby = 3) against k_reduce_lanet and the oracle: 2, 3 and 8 banks,
     T = 1, 2, 3, 4, 8, partial last time groups, a channel window, every op."""
     rng = np.random.default_rng(F + 7)
     nc = 512 // F * F

@@ -312,7 +312,7 @@ def run(names, rounds, iters, suite="main"):
         import t1_probe
 
         for c in t1_probe.build_cases(pkg):
-            cases.append((c["label"], lambda L, c=c: c["go"](L, sp), c["bytes"], c["out"],
+            cases.append((c["label"], lambda L, n=None, c=c: c["go"](L, sp), c["bytes"], c["out"],
                           (c["keep"], c["banks"])))
         cases_done = True
     elif suite == "kurt":
