@@ -775,6 +775,62 @@ __global__ __launch_bounds__(kBlock) void k_reduce_lanes(const RedArgs a) {
   }
 }
 
+// fqavby = 12 with short time blocks (T = 1, 2, 3, 4, 8; e.g. the 0001 band
+// without time integration, 42 groups a bank row): lanes on float4 columns,
+// three to a group, so every wave-instruction reads 1 KiB contiguous, where
+// k_reduce_lanet's one lane per group read three 16-byte pieces at a 48-byte
+// lane pitch (three instructions touching every line).  A workgroup of three
+// waves takes 64 consecutive groups of the stitched product row (bank-major:
+// several narrow banks per workgroup) and TPB = 16 / T time blocks; each
+// lane sums its column over a block's T rows and folds the float4, the three
+// partials of a group meet in LDS, and the workgroup stores 64 consecutive
+// outputs (256 bytes) per product row.  Summation order: per lane the T rows
+// in sequence, then (x + y) + (z + w); the group's three lane sums left to
+// right (integer data: the oracle's bits; Float32 data within the stated
+// tolerance, as every path).  Plan option "col3".
+constexpr int kCol3Threads = 192;
+template <int OP, int T>
+__global__ __launch_bounds__(kCol3Threads) void k_reduce_col3(const RedArgs a) {
+  constexpr int TPB = 16 / T > 0 ? 16 / T : 1, NR = TPB * T;
+  const uint32_t nbx = (uint32_t)a.blocks_c, bx = blockIdx.x, tq = bx / nbx, i = blockIdx.y;
+  const uint32_t gb = bx - tq * nbx;                    // this workgroup's 64 groups
+  const uint32_t k = gb * kCol3Threads + threadIdx.x;   // float4 column of the stitched row
+  const uint32_t cols = 3 * (uint32_t)a.nco, bank = k / cols, c = k - bank * cols;
+  const bool in = bank < (uint32_t)a.nbank;
+  const float id = R<OP>::id();
+  const float4 id4 = make_float4(id, id, id, id);
+  const int64_t ld = a.in_ld_t, tp0 = (int64_t)tq * TPB;
+  const int nbp = (int)min((int64_t)TPB, a.nto - tp0);
+  const float *p = a.in[in ? bank : 0] + a.in_off + (int64_t)i * a.in_ld_i + tp0 * T * ld + 4 * c;
+  float4 v[NR];
+  if (in && nbp == TPB) {
+#pragma unroll
+    for (int u = 0; u < NR; ++u) v[u] = ld4(p + u * ld);
+  } else {
+#pragma unroll
+    for (int u = 0; u < NR; ++u) v[u] = (in && u < nbp * T) ? ld4(p + u * ld) : id4;
+  }
+  __shared__ float part[TPB][kCol3Threads];
+#pragma unroll
+  for (int b = 0; b < TPB; ++b) {
+    float4 acc = id4;
+#pragma unroll
+    for (int r = 0; r < T; ++r) acc = f4<OP>(acc, v[b * T + r]);
+    part[b][threadIdx.x] = fold4<OP>(acc);
+  }
+  __syncthreads();
+  const int64_t ng = (int64_t)a.nbank * a.nco;  // groups of the stitched row
+  for (int e = threadIdx.x; e < TPB * 64; e += kCol3Threads) {
+    const int b = e >> 6, q = e & 63;
+    const int64_t G = (int64_t)gb * 64 + q;
+    if (b >= nbp || G >= ng) continue;
+    const float s = R<OP>::f(R<OP>::f(part[b][3 * q], part[b][3 * q + 1]), part[b][3 * q + 2]);
+    const int64_t bk = G / a.nco, g = G - bk * a.nco;
+    st1<1>(a.out + bk * a.out_bank + (int64_t)i * a.out_ld_i + (tp0 + b) * a.out_ld_t + g,
+           finish<OP>(s, a));
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Scalar path: any F, any channel step, any alignment.  One lane per output.
 template <int OP>
@@ -1611,6 +1667,19 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
 #undef BLDP_WAVETL
     return hipGetLastError();
   }
+  if (p.path == PATH_LANE && p.col3) {  // fqavby = 12, short time blocks: k_reduce_col3
+    const dim3 g3((unsigned)(a.blocks_c * cdiv(a.nto, a.tpb)), (unsigned)a.ni, 1u);
+    const dim3 b3(kCol3Threads);
+    switch (a.T) {
+      case 1: BLDP_LAUNCH((k_reduce_col3<OP, 1>), g3, b3, 0, s, a); break;
+      case 2: BLDP_LAUNCH((k_reduce_col3<OP, 2>), g3, b3, 0, s, a); break;
+      case 3: BLDP_LAUNCH((k_reduce_col3<OP, 3>), g3, b3, 0, s, a); break;
+      case 4: BLDP_LAUNCH((k_reduce_col3<OP, 4>), g3, b3, 0, s, a); break;
+      case 8: BLDP_LAUNCH((k_reduce_col3<OP, 8>), g3, b3, 0, s, a); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   if (p.path == PATH_LANE && p.lanet) {  // short time blocks, small odd groups: k_reduce_lanet
     const dim3 g3(a.bpack ? (unsigned)(a.blocks_c * cdiv(a.nto, a.tpb))
                           : (unsigned)(a.blocks_c * cdiv(cdiv(a.nto, a.tpb), 1 << a.tsub_log2)),
@@ -1812,6 +1881,7 @@ const PlanOptDef kPlanOpts[OPT_COUNT] = {
     {"row_bpack", 1},         // k_reduce_rowt: lane sets over consecutive banks on narrow stitched rows
     {"lane_bpack", 1},        // k_reduce_lanes: lanet's lanes along narrow stitched band rows
     {"wave_bpack", 1},        // k_reduce_wavet: a wave per (bank, group) of <= 16-group stitched rows
+    {"col3", 1},              // fqavby = 12, short time blocks: k_reduce_col3 (float4 columns)
 };
 struct PlanOpts {
   std::atomic<int64_t> v[OPT_COUNT];  // -1 = no override
@@ -1873,6 +1943,18 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
       a.tsub_log2 = 0;
       a.blocks_c = cdiv(row, (int64_t)kBlock);
       a.ntiles = a.blocks_c * cdiv(a.nto, a.tpb) * a.ni;
+    }
+    // fqavby = 12: float4 columns, three lanes a group (k_reduce_col3, option
+    // col3); any output layout, several banks per workgroup
+    if (opt(OPT_COL3) && F == 12 && (T == 1 || T == 2 || T == 3 || T == 4 || T == 8) &&
+        3 * a.nco * a.nbank <= UINT32_MAX - kCol3Threads &&
+        cdiv(a.nbank * a.nco, (int64_t)64) * cdiv(a.nto, (int64_t)(16 / T)) <= INT32_MAX) {
+      p.col3 = true;
+      a.bpack = 0;
+      a.tsub_log2 = 0;
+      a.tpb = (int32_t)(16 / T);
+      a.blocks_c = cdiv(a.nbank * a.nco, (int64_t)64);
+      a.ntiles = a.blocks_c * cdiv(a.nto, (int64_t)a.tpb) * a.ni;
     }
     p.grid = a.ntiles;
     p.ws_bytes = 0;

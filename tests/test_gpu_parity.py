@@ -1117,6 +1117,37 @@ def test_wavet_bank_pack_stitched(pkg, eng, orc, nc):
                 assert same_bits(got, want), (nc, nb, T, op)
 
 
+@pytest.mark.parametrize("T", [1, 2, 3, 4, 8])
+def test_col3_fqavby12_short_blocks(pkg, eng, orc, T):
+    """k_reduce_col3 (fqavby = 12 with short time blocks: float4 columns,
+    three lanes a group, 64 groups of the stitched row per workgroup) against
+    the oracle: integer data bit for bit (and equal to k_reduce_lanet, plan
+    option col3 = 0), Float32 data within RTOL; 1, 2, 3 and 8 banks, the 0001
+    row width and a wide row, a misaligned channel window, two IFs, partial
+    last time groups."""
+    rng = np.random.default_rng(T)
+    for nc, ni, nt, nbs in ((512, 1, 16 * T * 7 + T, (1, 2, 3, 8)), (8192, 2, 24 * T, (1, 3))):
+        for nb in nbs:
+            ints = [np.asfortranarray(rng.integers(0, 256, (nc, ni, nt)).astype(np.float32))
+                    for _ in range(nb)]
+            xs = [dev(eng, a) for a in ints]
+            for win in (None, [1, nc // 12 * 12 - 12, 1, 0, ni, 1, 0, nt, 1]):
+                w = win or [0, nc // 12 * 12, 1, 0, ni, 1, 0, nt, 1]
+                for op in ("sum", "mean", "max", "min"):
+                    got = host(eng, eng.band_reduce(xs, 12, T, op, w))
+                    want = orc.stitch([orc.reduce(a, 12, T, op, w) for a in ints])
+                    assert same_bits(got, want), (nc, nb, T, op, w)
+                    with pkg._lib.plan_option("col3", 0):
+                        ref = host(eng, eng.band_reduce(xs, 12, T, op, w))
+                    assert same_bits(got, ref), (nc, nb, T, op, w)
+            gam = [orc.gamma_bandpass(nc, ni, nt, 64, 31 * T + k) for k in range(nb)]
+            xs = [dev(eng, a) for a in gam]
+            w = [0, nc // 12 * 12, 1, 0, ni, 1, 0, nt, 1]
+            got = host(eng, eng.band_reduce(xs, 12, T, "sum", w))
+            want = orc.stitch([orc.reduce(a, 12, T, "sum", w) for a in gam])
+            np.testing.assert_allclose(got, want, rtol=RTOL)
+
+
 @pytest.mark.parametrize("F", [3, 5, 6, 7])
 def test_lanes_along_stitched_rows(pkg, eng, orc, F):
     """k_reduce_lanes (plan option lane_bpack: k_reduce_lanet's lanes along
@@ -1227,7 +1258,7 @@ PLAN_OPTION_VALUES = {
     "lane3": (0, 1), "lanet": (0, 1), "lanet_pack": (0, 1), "vec_il": (0, 1), "vec_row": (0, 1),
     "row_tpb": (0, 1), "rowt_pack": (0, 1), "rowt_small": (0, 64, 100000), "wavet": (0, 1, 2),
     "unaligned_vec": (0, 1, 2, 3), "row_bpack": (0, 1), "lane_bpack": (0, 1),
-    "wave_bpack": (0, 1),
+    "wave_bpack": (0, 1), "col3": (0, 1),
 }
 # (nchan, nif, ntime, window, F, T): shapes where the options above change the plan
 PLAN_OPTION_SHAPES = [

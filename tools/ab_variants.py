@@ -60,6 +60,7 @@ VARIANTS = {
     "nobpack": {"opts": {"row_bpack": 0}},  # rowt: time groups, not banks, share a workgroup
     "nolanes": {"opts": {"lane_bpack": 0}},  # lanet per bank, not along the stitched row
     "nowaveb": {"opts": {"wave_bpack": 0}},  # wavet: a wave per (group, bank, time chunk)
+    "nocol3": {"opts": {"col3": 0}},  # fqavby = 12 short blocks on k_reduce_lanet
     # ---- code-shape patches of the 0001 short-time-block kernels (round 4)
     "rowt6": {"patch": [("kernels.hip", "__attribute__((amdgpu_waves_per_eu(1, kRowtMaxWaves)))",
                          "__attribute__((amdgpu_waves_per_eu(kRowtMaxWaves, kRowtMaxWaves)))")]},
