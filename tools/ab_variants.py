@@ -61,6 +61,7 @@ VARIANTS = {
     "nolanes": {"opts": {"lane_bpack": 0}},  # lanet per bank, not along the stitched row
     "nowaveb": {"opts": {"wave_bpack": 0}},  # wavet: a wave per (group, bank, time chunk)
     "nocol3": {"opts": {"col3": 0}},  # fqavby = 12 short blocks on k_reduce_lanet
+    "rowt8o": {"opts": {"rowt_small": 100000}},  # k_reduce_rowt: always 8 rows per lane
     # ---- code-shape patches of the 0001 short-time-block kernels (round 4)
     "rowt6": {"patch": [("kernels.hip", "__attribute__((amdgpu_waves_per_eu(1, kRowtMaxWaves)))",
                          "__attribute__((amdgpu_waves_per_eu(kRowtMaxWaves, kRowtMaxWaves)))")]},
