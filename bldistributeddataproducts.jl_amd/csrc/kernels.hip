@@ -1882,6 +1882,7 @@ const PlanOptDef kPlanOpts[OPT_COUNT] = {
     {"lane_bpack", 1},        // k_reduce_lanes: lanet's lanes along narrow stitched band rows
     {"wave_bpack", 1},        // k_reduce_wavet: a wave per (bank, group) of <= 16-group stitched rows
     {"col3", 1},              // fqavby = 12, short time blocks: k_reduce_col3 (float4 columns)
+    {"rowt_narrow8", 1},      // k_reduce_rowt: 8 rows per lane on <= 128-column windows too
 };
 struct PlanOpts {
   std::atomic<int64_t> v[OPT_COUNT];  // -1 = no override
@@ -2080,8 +2081,12 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
       // small launches: 8 rows per lane, twice the workgroups (option rowt_small);
       // at T = 8 that is one time block per workgroup, i.e. k_reduce_row, whose
       // 3-D grid must then hold (IF, time block) in y
-      if (bc * cdiv(cdiv(a.nto, tpb), (int64_t)1 << a.tsub_log2) * a.ni * a.nbank <
-              opt(OPT_ROWT_SMALL) * num_cus &&
+      // windows of <= 128 float4 columns (the 0001 product) take 8 rows too
+      // (option rowt_narrow8: 0001 band at T = 1, F = 4 / 8 / 16 / 64 +1.7..4.7%,
+      // profiles/r04/ab_t1_0001_r04j.json)
+      if ((bc * cdiv(cdiv(a.nto, tpb), (int64_t)1 << a.tsub_log2) * a.ni * a.nbank <
+               opt(OPT_ROWT_SMALL) * num_cus ||
+           (opt(OPT_ROWT_NARROW8) && cols <= 128)) &&
           (8 / T > 1 || (bc <= INT32_MAX && a.ni * a.nto <= 65535)))
         tpb = 8 / T;
       if (tpb == 1) {  // k_reduce_row

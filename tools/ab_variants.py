@@ -62,6 +62,7 @@ VARIANTS = {
     "nowaveb": {"opts": {"wave_bpack": 0}},  # wavet: a wave per (group, bank, time chunk)
     "nocol3": {"opts": {"col3": 0}},  # fqavby = 12 short blocks on k_reduce_lanet
     "rowt8o": {"opts": {"rowt_small": 100000}},  # k_reduce_rowt: always 8 rows per lane
+    "rowtn16": {"opts": {"rowt_narrow8": 0}},  # narrow windows back on 16 rows per lane
     # ---- code-shape patches of the 0001 short-time-block kernels (round 4)
     "rowt6": {"patch": [("kernels.hip", "__attribute__((amdgpu_waves_per_eu(1, kRowtMaxWaves)))",
                          "__attribute__((amdgpu_waves_per_eu(kRowtMaxWaves, kRowtMaxWaves)))")]},
