@@ -178,8 +178,8 @@ def test_reduce_short_time_blocks_integer_exact(eng, orc, shape):
     tsub = 1 if tpb == 1 else 4 if cols <= 64 else 2 if cols <= 128 else 1
     blocks_c = -(-cols // 256)
     ncu = torch.cuda.get_device_properties(0).multi_processor_count
-    if tpb > 1 and blocks_c * ni * -(-(-(-nto // tpb)) // tsub) < 64 * ncu:
-        tpb = 8 // T  # small launch: 8 rows per lane
+    if tpb > 1 and (blocks_c * ni * -(-(-(-nto // tpb)) // tsub) < 64 * ncu or cols <= 128):
+        tpb = 8 // T  # small launch or narrow window: 8 rows per lane
         if tpb == 1:  # (tavby = 8: one block per workgroup, k_reduce_row's grid)
             tsub = 1
     for op in ("sum", "max", "min", "mean"):
@@ -232,8 +232,11 @@ def test_reduce_small_odd_groups_short_time_blocks_integer_exact(eng, orc, shape
         # (nco + 15): each row's segments start on a 64-byte line of the product;
         # windows of nco + 15 <= 128 / 64 pack 2 / 4 time groups per workgroup
         tsub = 4 if nco + 15 <= 64 else 2 if nco + 15 <= 128 else 1
-        assert plan["workgroups"] == -(-(nco + 15) // 256) * ni * -(-(-(-nto // tpb)) // tsub), \
-            (shape, plan)
+        if F == 12:  # k_reduce_col3: 64 groups x 16 / T time blocks per workgroup
+            assert plan["workgroups"] == -(-nco // 64) * ni * -(-nto // (16 // T)), (shape, plan)
+        else:
+            assert plan["workgroups"] == \
+                -(-(nco + 15) // 256) * ni * -(-(-(-nto // tpb)) // tsub), (shape, plan)
         got = host(eng, eng.reduce(x, F, T, op))
         want = orc.reduce(a, F, T, op)
         if op == "mean" and (F * T) & (F * T - 1):
@@ -281,7 +284,8 @@ def test_reduce_large_groups_short_time_blocks_integer_exact(eng, orc, shape):
     x = eng.synth(nco * F, ni, nt, 1024, seed=3 * nco + F + nt, kind=1)
     a = host(eng, x)
     nto, k4 = nt // T, F // 256
-    rw = 4 * max(1, 16 // (T * k4))  # time blocks per wave
+    tb = max(1, 16 // (T * k4))  # time blocks per batch
+    rw = tb * (1 if tb >= 2 else 4)  # per wave: one batch, or 4 of one block
     for op in ("sum", "max", "min", "mean"):
         plan = eng.plan(x, F, T, op)
         assert plan["path"] == "vector", (shape, plan)

@@ -573,6 +573,10 @@ def run(names, rounds, iters, suite="main"):
         for F in (3, 12, 16, 64, 512):
             w = [0, 512 // F * F, 1, 0, 1, 1, 0, 879616, 1]
             band_case(f"0001 1 bank F{F} T1", b4[:1], F, 1, w)
+        # short time blocks above 1 on the narrow rows (rowt_narrow8 covers them too)
+        for F, T in ((8, 2), (64, 2), (16, 4), (64, 4), (4, 3)):
+            w = [0, 512, 1, 0, 1, 1, 0, 879616 // T * T, 1]
+            band_case(f"0001 band F{F} T{T}", b4, F, T, w)
         cases_done = True
     elif suite == "wavet":  # k_reduce_wavet's shapes: 0001 at fqavby 512, long windows
         del b3
