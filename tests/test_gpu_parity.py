@@ -178,7 +178,8 @@ def test_reduce_short_time_blocks_integer_exact(eng, orc, shape):
     tsub = 1 if tpb == 1 else 4 if cols <= 64 else 2 if cols <= 128 else 1
     blocks_c = -(-cols // 256)
     ncu = torch.cuda.get_device_properties(0).multi_processor_count
-    if tpb > 1 and (blocks_c * ni * -(-(-(-nto // tpb)) // tsub) < 64 * ncu or cols <= 128):
+    if tpb > 1 and (blocks_c * ni * -(-(-(-nto // tpb)) // tsub) < 64 * ncu or
+                    (cols <= 128 and (T == 1 or F >= 16))):
         tpb = 8 // T  # small launch or narrow window: 8 rows per lane
         if tpb == 1:  # (tavby = 8: one block per workgroup, k_reduce_row's grid)
             tsub = 1
