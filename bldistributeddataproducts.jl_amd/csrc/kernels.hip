@@ -1223,7 +1223,7 @@ void k_reduce_rows(const RedArgs a) {
 // in LDS and stored as whole row segments (16-byte stores where legal; each
 // wave storing its own groups' outputs was slower).  At most kRowtMaxWaves = 6
 // resident waves per SIMD (A/B against 4 and none, profiles/r02/ab_row_tpb.json).
-template <int OP, int G4, int T, int NRW>
+template <int OP, int G4, int T, int NRW, bool BP>
 __global__ __launch_bounds__(kBlock)
 __attribute__((amdgpu_waves_per_eu(1, kRowtMaxWaves)))
 void k_reduce_rowt(const RedArgs a) {
@@ -1237,7 +1237,7 @@ void k_reduce_rowt(const RedArgs a) {
   // then get whole segments of 2^tsub_log2 banks' outputs (below).
   const uint32_t bx = blockIdx.x, bc = (uint32_t)a.blocks_c;
   const int sh = a.tsub_log2, cw = kBlock >> sh, sub = threadIdx.x >> (8 - sh);  // (kBlock = 256)
-  const bool bp = a.bpack != 0;
+  constexpr bool bp = BP;  // (a.bpack: a template form, so the time-group form pays nothing)
   const uint32_t tq = bx / bc, i = blockIdx.y;
   const int64_t tg = bp ? (int64_t)tq : ((int64_t)tq << sh) + sub;
   const int bank = bp ? (int)(blockIdx.z << sh) + sub : (int)blockIdx.z;
@@ -1715,15 +1715,21 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
     const dim3 g3(a.bpack ? (unsigned)(a.blocks_c * cdiv(a.nto, a.tpb))
                           : (unsigned)(a.blocks_c * cdiv(cdiv(a.nto, a.tpb), 1 << a.tsub_log2)),
                   (unsigned)a.ni, (unsigned)(a.bpack ? a.nbank >> a.tsub_log2 : a.nbank));
+#define BLDP_ROWTK(G, T, N)                                                \
+  if (a.bpack)                                                             \
+    BLDP_LAUNCH((k_reduce_rowt<OP, G, T, N, true>), g3, block, 0, s, a);   \
+  else                                                                     \
+    BLDP_LAUNCH((k_reduce_rowt<OP, G, T, N, false>), g3, block, 0, s, a);  \
+  break;
 #define BLDP_ROWTN(T, N)                                                                    \
   switch (a.F / 4) {                                                                        \
-    case 1: BLDP_LAUNCH((k_reduce_rowt<OP, 1, T, N>), g3, block, 0, s, a); break;    \
-    case 2: BLDP_LAUNCH((k_reduce_rowt<OP, 2, T, N>), g3, block, 0, s, a); break;    \
-    case 4: BLDP_LAUNCH((k_reduce_rowt<OP, 4, T, N>), g3, block, 0, s, a); break;    \
-    case 8: BLDP_LAUNCH((k_reduce_rowt<OP, 8, T, N>), g3, block, 0, s, a); break;    \
-    case 16: BLDP_LAUNCH((k_reduce_rowt<OP, 16, T, N>), g3, block, 0, s, a); break;  \
-    case 32: BLDP_LAUNCH((k_reduce_rowt<OP, 32, T, N>), g3, block, 0, s, a); break;  \
-    case 64: BLDP_LAUNCH((k_reduce_rowt<OP, 64, T, N>), g3, block, 0, s, a); break;  \
+    case 1: BLDP_ROWTK(1, T, N)    \
+    case 2: BLDP_ROWTK(2, T, N)    \
+    case 4: BLDP_ROWTK(4, T, N)    \
+    case 8: BLDP_ROWTK(8, T, N)    \
+    case 16: BLDP_ROWTK(16, T, N)  \
+    case 32: BLDP_ROWTK(32, T, N)  \
+    case 64: BLDP_ROWTK(64, T, N)  \
     default: return hipErrorInvalidValue;                                                   \
   }
 #define BLDP_ROWT(T)                 \
@@ -1745,6 +1751,7 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
 #undef BLDP_ROWTC
 #undef BLDP_ROWT
 #undef BLDP_ROWTN
+#undef BLDP_ROWTK
     return hipGetLastError();
   }
   if (p.path == PATH_VEC_ROW && a.rsplit > 1) {  // a block's rows over 2 / 4 slices
@@ -1938,7 +1945,9 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
     const int64_t row = a.nbank * a.nco;
     // (F = 12: 2.94 vs 2.90 ms on the 0001 band, not taken; F = 3 3.53 vs
     // 4.21, profiles/r04/ab_t1_0001_r04h.json)
-    if (opt(OPT_LANE_BPACK) && F <= 7 && a.nbank > 1 && a.out_bank == a.nco && a.nco + 15 < kBlock &&
+    // (T <= 4: at T = 8, 2% slower on the 0001 band)
+    if (opt(OPT_LANE_BPACK) && F <= 7 && T <= 4 && a.nbank > 1 && a.out_bank == a.nco &&
+        a.nco + 15 < kBlock &&
         row <= UINT32_MAX - kBlock && cdiv(row, (int64_t)kBlock) * cdiv(a.nto, a.tpb) <= INT32_MAX) {
       a.bpack = 1;
       a.tsub_log2 = 0;
@@ -1947,7 +1956,10 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
     }
     // fqavby = 12: float4 columns, three lanes a group (k_reduce_col3, option
     // col3); any output layout, several banks per workgroup
+    // (rows of < 65536 groups: the 0000 product's 5.6M-group rows lost 3-5% at
+    // T = 2..4, profiles/r04/ab_grid0_r04l.json)
     if (opt(OPT_COL3) && F == 12 && (T == 1 || T == 2 || T == 3 || T == 4 || T == 8) &&
+        a.nco < 65536 &&
         3 * a.nco * a.nbank <= UINT32_MAX - kCol3Threads &&
         cdiv(a.nbank * a.nco, (int64_t)64) * cdiv(a.nto, (int64_t)(16 / T)) <= INT32_MAX) {
       p.col3 = true;
@@ -2121,11 +2133,15 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
       // partial round of 64 KiB tiles (profiles/r04/ab_rows_r04c.json: one to
       // eight 0002 files 5-11% faster; 0000 bands, 256+ tiles per CU, 9-27%
       // slower split)
+      // (F >= 128: only below 16 tiles per CU, in 2 slices; the 0002 band at
+      // F = 128 / 256, 34 tiles per CU, lost 3-5% split, profiles/r04/
+      // ab_grid_r04l.json)
       int64_t S = plan_opt(OPT_ROW_SPLIT);
       if (T % 16 != 0)
         S = 1;
       else if (S < 0)
-        S = a.ntiles < (int64_t)64 * num_cus ? (F >= 256 ? 2 : 4) : 1;
+        S = F >= 128 ? (a.ntiles < (int64_t)16 * num_cus ? 2 : 1)
+                     : (a.ntiles < (int64_t)64 * num_cus ? 4 : 1);
       if (S == 2 || S == 4) {
         a.rsplit = (int32_t)S;
         a.blocks_c = cdiv(a.nco * (F / 4), kBlock / S);
