@@ -63,6 +63,12 @@ VARIANTS = {
     "nocol3": {"opts": {"col3": 0}},  # fqavby = 12 short blocks on k_reduce_lanet
     "rowt8o": {"opts": {"rowt_small": 100000}},  # k_reduce_rowt: always 8 rows per lane
     "rowtn16": {"opts": {"rowt_narrow8": 0}},  # narrow windows back on 16 rows per lane
+    # k_reduce_col3 with 8 rows per lane (twice the workgroups)
+    "col3r8": {"patch": [("kernels.hip", "constexpr int TPB = 16 / T > 0 ? 16 / T : 1, NR = TPB * T;\n"
+                          "  const uint32_t nbx", "constexpr int TPB = 8 / T > 0 ? 8 / T : 1, NR = TPB * T;\n"
+                          "  const uint32_t nbx"),
+                         ("kernels.hip", "a.tpb = (int32_t)(16 / T);\n      a.blocks_c = cdiv(a.nbank * a.nco, (int64_t)64);",
+                          "a.tpb = (int32_t)(8 / T > 0 ? 8 / T : 1);\n      a.blocks_c = cdiv(a.nbank * a.nco, (int64_t)64);")]},
     # ---- code-shape patches of the 0001 short-time-block kernels (round 4)
     "rowt6": {"patch": [("kernels.hip", "__attribute__((amdgpu_waves_per_eu(1, kRowtMaxWaves)))",
                          "__attribute__((amdgpu_waves_per_eu(kRowtMaxWaves, kRowtMaxWaves)))")]},

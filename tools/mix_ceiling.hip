@@ -248,11 +248,11 @@ int main(int argc, char **argv) {
                             {"0002 band 585 MB", 8ll * 65536 * 279 * 4},
                             {"0001 band 14.4 GB", 8ll * 512 * 879616 * 4},
                             {"0000 band 32 GiB", big}};
-  // argv[2] = "0001": only the 0001 band (its read:write-mix ceilings)
-  const bool only1 = argc > 2 && std::string(argv[2]) == "0001";
+  // argv[2] = "0001" / "0002": only that product's sizes
+  const std::string only = argc > 2 ? std::string(argv[2]) : std::string();
   std::vector<Size> sizes;
   for (const Size &z : all_sizes)
-    if (!only1 || std::string(z.label).rfind("0001", 0) == 0) sizes.push_back(z);
+    if (only.empty() || std::string(z.label).rfind(only, 0) == 0) sizes.push_back(z);
   for (const Size &s : sizes) {
     const bool grids = s.bytes < (1ll << 30);
     run_r<1>(in, out, s.bytes, reps, s.label, ncu, grids);

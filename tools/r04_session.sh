@@ -54,6 +54,7 @@ for s in $STEPS; do
     ab_*) run "$s" 900 python tools/ab_variants.py --run --suite "${s#ab_}" --rounds 5 \
           --variants "${AB_VARIANTS:-base}" --json "$OUT/$s.json" ;;
     mix1) run mix1 300 ./build/mix_ceiling 10 0001 ;;
+    mix2) run mix2 300 ./build/mix_ceiling 10 0002 ;;
     typed) run typed 300 python bench.py --mode typed ;;
     typed_*) run "$s" 300 python bench.py --mode typed --plan-option typed_rows="${s#typed_}" ;;
     typedprof) run typedprof 300 rocprofv3 --kernel-trace --stats --output-format csv \
