@@ -63,6 +63,11 @@ VARIANTS = {
     "nocol3": {"opts": {"col3": 0}},  # fqavby = 12 short blocks on k_reduce_lanet
     "rowt8o": {"opts": {"rowt_small": 100000}},  # k_reduce_rowt: always 8 rows per lane
     "rowtn16": {"opts": {"rowt_narrow8": 0}},  # narrow windows back on 16 rows per lane
+    # k_reduce_narrowt with 8 rows per lane (twice the workgroups)
+    "narrowt8": {"patch": [("kernels.hip", "constexpr int TPB = 16 / T, NR = TPB * T;\n  const int tid",
+                            "constexpr int TPB = 8 / T, NR = TPB * T;\n  const int tid"),
+                           ("kernels.hip", "const int64_t cols = a.nco * F / 4, tpb = 16 / T;",
+                            "const int64_t cols = a.nco * F / 4, tpb = 8 / T;")]},
     # k_reduce_col3 with 8 rows per lane (twice the workgroups)
     "col3r8": {"patch": [("kernels.hip", "constexpr int TPB = 16 / T > 0 ? 16 / T : 1, NR = TPB * T;\n"
                           "  const uint32_t nbx", "constexpr int TPB = 8 / T > 0 ? 8 / T : 1, NR = TPB * T;\n"
