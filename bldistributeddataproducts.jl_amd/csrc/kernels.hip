@@ -401,9 +401,9 @@ __device__ __forceinline__ void narrow_tile(const RedArgs &a, int64_t tile) {
 // (the narrow kernels run uncapped: a cap of 4 cost k_reduce_narrow 1.2%).
 // Plan option "narrow_tpb": 2 (default) = use it for T in {1, 2, 4}, the copy
 // (fqavby = tavby = 1) included; 1 = not for the copy; 0 = k_reduce_narrow.
-template <int OP, int F, int T>
+template <int OP, int F, int T, int NRW>
 __global__ __launch_bounds__(kBlock) void k_reduce_narrowt(const RedArgs a) {
-  constexpr int TPB = 16 / T, NR = TPB * T;
+  constexpr int TPB = NRW / T, NR = TPB * T;
   const int tid = threadIdx.x;
   const uint32_t bx = blockIdx.x, bc = (uint32_t)a.blocks_c;
   const int sh = a.tsub_log2, cw = kBlock >> sh;
@@ -791,7 +791,9 @@ __global__ __launch_bounds__(kBlock) void k_reduce_lanes(const RedArgs a) {
 constexpr int kCol3Threads = 192;
 template <int OP, int T>
 __global__ __launch_bounds__(kCol3Threads) void k_reduce_col3(const RedArgs a) {
-  constexpr int TPB = 16 / T > 0 ? 16 / T : 1, NR = TPB * T;
+  // 8 rows per lane: 2-8% faster than 16 on the 0001 and 0002 bands at T = 1..8
+  // (profiles/r04/ab_t1_0001_r04o.json, ab_grid_r04o.json)
+  constexpr int TPB = 8 / T > 0 ? 8 / T : 1, NR = TPB * T;
   const uint32_t nbx = (uint32_t)a.blocks_c, bx = blockIdx.x, tq = bx / nbx, i = blockIdx.y;
   const uint32_t gb = bx - tq * nbx;                    // this workgroup's 64 groups
   const uint32_t k = gb * kCol3Threads + threadIdx.x;   // float4 column of the stitched row
@@ -1622,7 +1624,11 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
   if (p.path == PATH_NARROW && a.tpb > 1) {  // short time blocks, several per workgroup
     const dim3 g3((unsigned)(a.blocks_c * cdiv(cdiv(a.nto, a.tpb), 1 << a.tsub_log2)),
                   (unsigned)a.ni, (unsigned)a.nbank);
-#define BLDP_NARROWT(FF, TT) BLDP_LAUNCH((k_reduce_narrowt<OP, FF, TT>), g3, block, 0, s, a);
+#define BLDP_NARROWT(FF, TT)                                                  \
+  if (a.tpb == 8 / (TT))                                                      \
+    BLDP_LAUNCH((k_reduce_narrowt<OP, FF, TT, 8>), g3, block, 0, s, a);       \
+  else                                                                        \
+    BLDP_LAUNCH((k_reduce_narrowt<OP, FF, TT, 16>), g3, block, 0, s, a);
     if (a.F == 1 && a.T == 1) { BLDP_NARROWT(1, 1) }
     else if (a.F == 1 && a.T == 2) { BLDP_NARROWT(1, 2) }
     else if (a.F == 1 && a.T == 4) { BLDP_NARROWT(1, 4) }
@@ -1961,11 +1967,12 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
     if (opt(OPT_COL3) && F == 12 && (T == 1 || T == 2 || T == 3 || T == 4 || T == 8) &&
         a.nco < 65536 &&
         3 * a.nco * a.nbank <= UINT32_MAX - kCol3Threads &&
-        cdiv(a.nbank * a.nco, (int64_t)64) * cdiv(a.nto, (int64_t)(16 / T)) <= INT32_MAX) {
+        cdiv(a.nbank * a.nco, (int64_t)64) * cdiv(a.nto, (int64_t)(8 / T > 0 ? 8 / T : 1)) <=
+            INT32_MAX) {
       p.col3 = true;
       a.bpack = 0;
       a.tsub_log2 = 0;
-      a.tpb = (int32_t)(16 / T);
+      a.tpb = (int32_t)(8 / T > 0 ? 8 / T : 1);
       a.blocks_c = cdiv(a.nbank * a.nco, (int64_t)64);
       a.ntiles = a.blocks_c * cdiv(a.nto, (int64_t)a.tpb) * a.ni;
     }
@@ -2154,8 +2161,18 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
   if (opt(OPT_NARROW_TPB) && p.path == PATH_NARROW && a.nchunk == 1 &&
       (T == 1 || T == 2 || T == 4 || (t38 && T == 3 && F == 2)) &&
       (opt(OPT_NARROW_TPB) >= 1 + (F == 1 && T == 1)) && a.nto > 1 && a.ni <= 65535 && a.nbank <= 65535) {
-    const int64_t cols = a.nco * F / 4, tpb = 16 / T;
+    const int64_t cols = a.nco * F / 4;
     const int sh = cols <= 64 ? 2 : cols <= 128 ? 1 : 0;
+    // 8 rows per lane (instead of 16) on launches under rowt_small (64)
+    // workgroups per CU and, at T = 1, on windows of <= 128 float4 columns:
+    // the 0002 band at F = 1 / 2, T = 1..4 +5..12%, the 0001 band F = 1 / 2
+    // T = 1 +7 / 3%; the 0000 band (1.8% slower) keeps 16
+    // (profiles/r04/ab_grid_r04o.json, ab_t1_0001_r04o.json)
+    int64_t tpb = 16 / T;
+    if ((a.blocks_c * cdiv(cdiv(a.nto, tpb), (int64_t)1 << sh) * a.ni * a.nbank <
+             opt(OPT_ROWT_SMALL) * num_cus ||
+         (opt(OPT_ROWT_NARROW8) && cols <= 128 && T == 1)) && 8 / T >= 1)
+      tpb = 8 / T;
     const int64_t x = a.blocks_c * cdiv(cdiv(a.nto, tpb), (int64_t)1 << sh);
     if (x <= INT32_MAX) {
       a.tpb = (int32_t)tpb;

@@ -234,7 +234,8 @@ def test_reduce_small_odd_groups_short_time_blocks_integer_exact(eng, orc, shape
         # windows of nco + 15 <= 128 / 64 pack 2 / 4 time groups per workgroup
         tsub = 4 if nco + 15 <= 64 else 2 if nco + 15 <= 128 else 1
         if F == 12:  # k_reduce_col3: 64 groups x 16 / T time blocks per workgroup
-            assert plan["workgroups"] == -(-nco // 64) * ni * -(-nto // (16 // T)), (shape, plan)
+            assert plan["workgroups"] == -(-nco // 64) * ni * -(-nto // max(1, 8 // T)), \
+                (shape, plan)
         else:
             assert plan["workgroups"] == \
                 -(-(nco + 15) // 256) * ni * -(-(-(-nto // tpb)) // tsub), (shape, plan)
@@ -314,10 +315,14 @@ def test_reduce_narrow_short_time_blocks_integer_exact(eng, orc, shape):
     a = host(eng, x)
     nto, cols = nt // T, nco * F // 4
     tsub = 4 if cols <= 64 else 2 if cols <= 128 else 1
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    tpb = 16 // T  # 8 rows per lane on small launches and, at T = 1, narrow windows
+    if -(-cols // 256) * ni * -(-(-(-nto // tpb)) // tsub) < 64 * ncu or (cols <= 128 and T == 1):
+        tpb = 8 // T
     for op in ("sum", "max", "min", "mean"):
         plan = eng.plan(x, F, T, op)
         assert plan["path"] == "narrow", (shape, plan)
-        assert plan["workgroups"] == -(-cols // 256) * ni * -(-(-(-nto // (16 // T))) // tsub), \
+        assert plan["workgroups"] == -(-cols // 256) * ni * -(-(-(-nto // tpb)) // tsub), \
             (shape, plan)
         got = host(eng, eng.reduce(x, F, T, op))
         assert same_bits(got, orc.reduce(a, F, T, op)), (shape, op)
