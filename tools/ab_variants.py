@@ -63,17 +63,9 @@ VARIANTS = {
     "nocol3": {"opts": {"col3": 0}},  # fqavby = 12 short blocks on k_reduce_lanet
     "rowt8o": {"opts": {"rowt_small": 100000}},  # k_reduce_rowt: always 8 rows per lane
     "rowtn16": {"opts": {"rowt_narrow8": 0}},  # narrow windows back on 16 rows per lane
-    # k_reduce_narrowt with 8 rows per lane (twice the workgroups)
-    "narrowt8": {"patch": [("kernels.hip", "constexpr int TPB = 16 / T, NR = TPB * T;\n  const int tid",
-                            "constexpr int TPB = 8 / T, NR = TPB * T;\n  const int tid"),
-                           ("kernels.hip", "const int64_t cols = a.nco * F / 4, tpb = 16 / T;",
-                            "const int64_t cols = a.nco * F / 4, tpb = 8 / T;")]},
-    # k_reduce_col3 with 8 rows per lane (twice the workgroups)
-    "col3r8": {"patch": [("kernels.hip", "constexpr int TPB = 16 / T > 0 ? 16 / T : 1, NR = TPB * T;\n"
-                          "  const uint32_t nbx", "constexpr int TPB = 8 / T > 0 ? 8 / T : 1, NR = TPB * T;\n"
-                          "  const uint32_t nbx"),
-                         ("kernels.hip", "a.tpb = (int32_t)(16 / T);\n      a.blocks_c = cdiv(a.nbank * a.nco, (int64_t)64);",
-                          "a.tpb = (int32_t)(8 / T > 0 ? 8 / T : 1);\n      a.blocks_c = cdiv(a.nbank * a.nco, (int64_t)64);")]},
+    # (round 4: 8 rows per lane for k_reduce_narrowt on small / narrow launches and
+    # for k_reduce_col3 were measured as text patches, profiles/r04/ab_*_r04o.json;
+    # "rowt16" / "rowtn16" put the narrowt and rowt kernels back on 16 rows)
     # ---- code-shape patches of the 0001 short-time-block kernels (round 4)
     "rowt6": {"patch": [("kernels.hip", "__attribute__((amdgpu_waves_per_eu(1, kRowtMaxWaves)))",
                          "__attribute__((amdgpu_waves_per_eu(kRowtMaxWaves, kRowtMaxWaves)))")]},
