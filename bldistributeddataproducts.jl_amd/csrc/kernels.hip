@@ -2101,13 +2101,13 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
       // at T = 8 that is one time block per workgroup, i.e. k_reduce_row, whose
       // 3-D grid must then hold (IF, time block) in y
       // windows of <= 128 float4 columns (the 0001 product) take 8 rows too at
-      // T = 1 and at F >= 16 (option rowt_narrow8: 0001 band at T = 1, F = 4 / 8
-      // / 16 / 64 +1.2..6%, F = 64 T = 2 / 4 +4.5 / 1.8%, F = 16 T = 4 +1.5%; F = 8
-      // T = 2 and F = 4 T = 3 -1.7 / 2.6%: not taken; profiles/r04/
-      // ab_t1_0001_r04{j,k}.json)
+      // T = 1 and at F >= 64 (option rowt_narrow8: 0001 band at T = 1, F = 4 / 8
+      // / 16 / 64 +1.2..6%, F = 64 T = 2 / 4 +4.5 / 1.8%; F = 16 T = 2, F = 8 T = 2
+      // and F = 4 T = 3 -1.7..4%: not taken; profiles/r04/ab_t1_0001_r04{j,k}.json,
+      // ab_grid1_r04p.json)
       if ((bc * cdiv(cdiv(a.nto, tpb), (int64_t)1 << a.tsub_log2) * a.ni * a.nbank <
                opt(OPT_ROWT_SMALL) * num_cus ||
-           (opt(OPT_ROWT_NARROW8) && cols <= 128 && (T == 1 || F >= 16))) &&
+           (opt(OPT_ROWT_NARROW8) && cols <= 128 && (T == 1 || F >= 64))) &&
           (8 / T > 1 || (bc <= INT32_MAX && a.ni * a.nto <= 65535)))
         tpb = 8 / T;
       if (tpb == 1) {  // k_reduce_row

@@ -179,7 +179,7 @@ def test_reduce_short_time_blocks_integer_exact(eng, orc, shape):
     blocks_c = -(-cols // 256)
     ncu = torch.cuda.get_device_properties(0).multi_processor_count
     if tpb > 1 and (blocks_c * ni * -(-(-(-nto // tpb)) // tsub) < 64 * ncu or
-                    (cols <= 128 and (T == 1 or F >= 16))):
+                    (cols <= 128 and (T == 1 or F >= 64))):
         tpb = 8 // T  # small launch or narrow window: 8 rows per lane
         if tpb == 1:  # (tavby = 8: one block per workgroup, k_reduce_row's grid)
             tsub = 1
