@@ -63,6 +63,15 @@ VARIANTS = {
     "nocol3": {"opts": {"col3": 0}},  # fqavby = 12 short blocks on k_reduce_lanet
     "rowt8o": {"opts": {"rowt_small": 100000}},  # k_reduce_rowt: always 8 rows per lane
     "rowtn16": {"opts": {"rowt_narrow8": 0}},  # narrow windows back on 16 rows per lane
+    # k_reduce_rows with a register budget for 6 / 8 resident waves per SIMD
+    "rowsw6": {"patch": [("kernels.hip", "template <int OP, int G4, int S>\n__global__ __launch_bounds__(kBlock)\n"
+                          "__attribute__((amdgpu_waves_per_eu(1, kRowMaxWaves)))",
+                          "template <int OP, int G4, int S>\n__global__ __launch_bounds__(kBlock)\n"
+                          "__attribute__((amdgpu_waves_per_eu(6, 8)))")]},
+    "rowsw8": {"patch": [("kernels.hip", "template <int OP, int G4, int S>\n__global__ __launch_bounds__(kBlock)\n"
+                          "__attribute__((amdgpu_waves_per_eu(1, kRowMaxWaves)))",
+                          "template <int OP, int G4, int S>\n__global__ __launch_bounds__(kBlock)\n"
+                          "__attribute__((amdgpu_waves_per_eu(8, 8)))")]},
     # (round 4: 8 rows per lane for k_reduce_narrowt on small / narrow launches and
     # for k_reduce_col3 were measured as text patches, profiles/r04/ab_*_r04o.json;
     # "rowt16" / "rowtn16" put the narrowt and rowt kernels back on 16 rows)
