@@ -576,6 +576,18 @@ def bench_typed(args, eng, torch, pkg):
         nbytes = a.nbytes + 8 * (65536 * nb // 64) * 279
         out[label] = {"ms_per_call": round(ms, 4), "GBps_in_plus_out": round(nbytes / ms / 1e6, 1),
                       "input_bytes": int(a.nbytes)}
+        # getkurtosis on the same UInt8 data (Float64 StatsBase per channel row)
+        for _ in range(2):
+            eng.kurtosis(x)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(args.steps):
+            eng.kurtosis(x)
+        e1.record()
+        e1.synchronize()
+        km = e0.elapsed_time(e1) / args.steps
+        out[label]["kurtosis_ms_per_call"] = round(km, 4)
+        out[label]["kurtosis_GBps_of_input"] = round(a.nbytes / km / 1e6, 1)
     f = out["0002 band"]  # (one file is host-call bound: ~20 us a call, 7 us of kernel)
     return {"metric": "fqav GB/s on UInt8 SIGPROC data (0002 band geometry, fqavby=64, sum)",
             "value": f["GBps_in_plus_out"], "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
