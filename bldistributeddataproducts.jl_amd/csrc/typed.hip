@@ -431,6 +431,90 @@ __global__ __launch_bounds__(256) void k_kurt_typed(const TypedArgs a, double *o
 }
 
 
+// getkurtosis of 8- and 16-bit rows (SIGPROC nbits 8 / 16): k_kurt_typed's
+// arithmetic with every lane on the 4 / 2 consecutive channels of one 32-bit
+// word, so a wave-instruction reads 256 contiguous bytes instead of 64 / 128,
+// and 16 spectra of loads in flight.  The mean's Float64 sum is exact for
+// these types (|sum| < 2^53 for any n below 2^37), so the integer sum
+// converted once is the value of Julia's pairwise Float64 sum; the moment
+// loop runs in spectrum order per channel as StatsBase's does: bit-identical
+// to k_kurt_typed (tests/test_gpu_typed.py).
+template <typename TI>
+__device__ __forceinline__ int32_t word_elem(uint32_t w, int k) {
+  if constexpr (sizeof(TI) == 1)
+    return std::is_signed<TI>::value ? (int32_t)(int8_t)(w >> (8 * k)) : (int32_t)((w >> (8 * k)) & 0xffu);
+  else
+    return std::is_signed<TI>::value ? (int32_t)(int16_t)(w >> (16 * k))
+                                     : (int32_t)((w >> (16 * k)) & 0xffffu);
+}
+template <typename TI>
+__global__ __launch_bounds__(256) void k_kurt_typed_w(const TypedArgs a, double *out) {
+  constexpr int CPL = 4 / (int)sizeof(TI), U = 16;
+  const int64_t ngl = a.nco / CPL, nrow = ngl * a.ni * a.nbank, n = a.nto;
+  const int64_t ldb = a.in_ld_t * (int64_t)sizeof(TI);
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < nrow;
+       e += (int64_t)gridDim.x * 256) {
+    const int64_t q = e % ngl, r = e / ngl, i = r % a.ni, bank = r / a.ni;
+    const char *p = static_cast<const char *>(a.in[bank]) +
+                    (a.in_off + i * a.in_ld_i + q * CPL) * (int64_t)sizeof(TI);
+    int64_t s[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) s[k] = 0;
+    int64_t t = 0;
+    for (; t + U <= n; t += U) {
+      uint32_t w[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) w[u] = *reinterpret_cast<const uint32_t *>(p + (t + u) * ldb);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) s[k] += word_elem<TI>(w[u], k);
+    }
+    for (; t < n; ++t) {
+      const uint32_t w = *reinterpret_cast<const uint32_t *>(p + t * ldb);
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) s[k] += word_elem<TI>(w, k);
+    }
+    double m[CPL], cm2[CPL], cm4[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+      m[k] = (double)s[k] / (double)n;
+      cm2[k] = 0.0;
+      cm4[k] = 0.0;
+    }
+    t = 0;
+    for (; t + U <= n; t += U) {
+      uint32_t w[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) w[u] = *reinterpret_cast<const uint32_t *>(p + (t + u) * ldb);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+          const double z = (double)word_elem<TI>(w[u], k) - m[k];
+          const double z2 = z * z;
+          cm2[k] += z2;
+          cm4[k] += z2 * z2;
+        }
+    }
+    for (; t < n; ++t) {
+      const uint32_t w = *reinterpret_cast<const uint32_t *>(p + t * ldb);
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) {
+        const double z = (double)word_elem<TI>(w, k) - m[k];
+        const double z2 = z * z;
+        cm2[k] += z2;
+        cm4[k] += z2 * z2;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+      const double c4 = cm4[k] / (double)n, c2 = cm2[k] / (double)n;
+      out[q * CPL + k + a.nco * r] = (c4 / (c2 * c2)) - 3.0;
+    }
+  }
+}
+
 // The coalesced kernel's geometry for this window, or false when it does not
 // apply (Float64 sums, 64-bit means and inexact 32-bit means keep the
 // reference's order on k_reduce_typed; windows without dword-aligned 16-byte
@@ -527,6 +611,18 @@ hipError_t launch_typed_op(const TypedArgs &a, int op, hipStream_t s) {
 template <typename TI>
 hipError_t launch_kurt_t(const TypedArgs &a, double *out, hipStream_t s) {
   const int64_t n = a.nco * a.ni * a.nbank;
+  if constexpr (sizeof(TI) <= 2) {  // 32-bit words of 4 / 2 channels (k_kurt_typed_w)
+    constexpr int64_t cpl = 4 / (int64_t)sizeof(TI);
+    bool ok = opt(OPT_TYPED_VEC) && a.in_cs == 1 && a.nco % cpl == 0 && a.nto > 0 &&
+              (a.in_off * (int64_t)sizeof(TI)) % 4 == 0 &&
+              (a.ni == 1 || (a.in_ld_i * (int64_t)sizeof(TI)) % 4 == 0) &&
+              (a.in_ld_t * (int64_t)sizeof(TI)) % 4 == 0;
+    for (int b = 0; ok && b < a.nbank; ++b) ok = (uintptr_t)a.in[b] % 4 == 0;
+    if (ok) {
+      hipLaunchKernelGGL((k_kurt_typed_w<TI>), dim3(grid_for(n / cpl)), dim3(256), 0, s, a, out);
+      return hipGetLastError();
+    }
+  }
   hipLaunchKernelGGL((k_kurt_typed<TI>), dim3(grid_for(n)), dim3(256), 0, s, a, out);
   return hipGetLastError();
 }

@@ -168,6 +168,29 @@ def test_kurtosis_typed(pkg, eng, orc, dt):
     assert e.shape == (40, 1) and np.isnan(e).all()
 
 
+@pytest.mark.parametrize("dt", [np.uint8, np.int8, np.uint16, np.int16],
+                         ids=lambda d: np.dtype(d).name)
+def test_kurtosis_typed_words(pkg, eng, orc, dt):
+    """8- and 16-bit getkurtosis with a lane on each 32-bit word of 4 / 2
+    channels (k_kurt_typed_w): bit-identical to the one-lane-per-channel
+    kernel (plan option typed_vec = 0) and to the oracle; the type's full
+    range, spectrum counts around the 16-spectrum batches, two IFs, a
+    channel window on a word boundary and one off it (the fallback)."""
+    info = np.iinfo(dt)
+    for k, (nc, ni, nt) in enumerate([(256, 2, 1000), (1024, 1, 77), (64, 1, 16), (128, 3, 15)]):
+        rng = np.random.default_rng(k + np.dtype(dt).num)
+        a = np.asfortranarray(rng.integers(info.min, info.max, (nc, ni, nt), endpoint=True)
+                              .astype(dt))
+        x = to_dev(eng, a)
+        got = eng.fb_to_numpy(eng.kurtosis(x))
+        assert same(got, orc.np_kurtosis_typed(a)), (dt, (nc, ni, nt))
+        with pkg._lib.plan_option("typed_vec", 0):
+            assert same(eng.fb_to_numpy(eng.kurtosis(x)), got), (dt, (nc, ni, nt))
+        for w in ([4, nc - 8, 1, 0, ni, 1, 3, nt - 3, 1], [1, nc - 4, 1, 0, ni, 1, 0, nt, 1]):
+            assert same(eng.fb_to_numpy(eng.kurtosis(x, w)), orc.np_kurtosis_typed(a, w)), \
+                (dt, (nc, ni, nt), w)
+
+
 def test_worker_api_keeps_reference_types(pkg, eng, orc, tmp_path):
     """getdata / getkurtosis / fqav on 8- and 16-bit SIGPROC files and on a
     Float64 array: Julia's result types and values (no Float32 detour)."""
