@@ -57,6 +57,7 @@ for s in $STEPS; do
     mix2) run mix2 300 ./build/mix_ceiling 10 0002 ;;
     typed) run typed 300 python bench.py --mode typed ;;
     typed_*) run "$s" 300 python bench.py --mode typed --plan-option typed_rows="${s#typed_}" ;;
+    typedoff) run typedoff 300 python bench.py --mode typed --plan-option typed_vec=0 ;;
     typedprof) run typedprof 300 rocprofv3 --kernel-trace --stats --output-format csv \
         -d "$OUT/typedprof" -o run -- python bench.py --mode typed --steps 20 --warmup 5 ;;
     gap) run gap 300 python tools/gap_probe.py --json "$OUT/gap.json" ;;
