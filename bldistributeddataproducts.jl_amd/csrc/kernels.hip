@@ -791,9 +791,11 @@ __global__ __launch_bounds__(kBlock) void k_reduce_lanes(const RedArgs a) {
 constexpr int kCol3Threads = 192;
 template <int OP, int T>
 __global__ __launch_bounds__(kCol3Threads) void k_reduce_col3(const RedArgs a) {
-  // 8 rows per lane: 2-8% faster than 16 on the 0001 and 0002 bands at T = 1..8
-  // (profiles/r04/ab_t1_0001_r04o.json, ab_grid_r04o.json)
-  constexpr int TPB = 8 / T > 0 ? 8 / T : 1, NR = TPB * T;
+  // 4 rows per lane at T <= 4: 8 rows were 2-8% faster than 16 on the 0001
+  // and 0002 bands at T = 1..8 (profiles/r04/ab_t1_0001_r04o.json,
+  // ab_grid_r04o.json), 4 another 6% at T = 1 and 2% at T = 3 (ab_t1v_r04v.json,
+  // ab_k3_r04v.json)
+  constexpr int TPB = 4 / T > 0 ? 4 / T : 1, NR = TPB * T;
   const uint32_t nbx = (uint32_t)a.blocks_c, bx = blockIdx.x, tq = bx / nbx, i = blockIdx.y;
   const uint32_t gb = bx - tq * nbx;                    // this workgroup's 64 groups
   const uint32_t k = gb * kCol3Threads + threadIdx.x;   // float4 column of the stitched row
@@ -1967,12 +1969,12 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
     if (opt(OPT_COL3) && F == 12 && (T == 1 || T == 2 || T == 3 || T == 4 || T == 8) &&
         a.nco < 65536 &&
         3 * a.nco * a.nbank <= UINT32_MAX - kCol3Threads &&
-        cdiv(a.nbank * a.nco, (int64_t)64) * cdiv(a.nto, (int64_t)(8 / T > 0 ? 8 / T : 1)) <=
+        cdiv(a.nbank * a.nco, (int64_t)64) * cdiv(a.nto, (int64_t)(4 / T > 0 ? 4 / T : 1)) <=
             INT32_MAX) {
       p.col3 = true;
       a.bpack = 0;
       a.tsub_log2 = 0;
-      a.tpb = (int32_t)(8 / T > 0 ? 8 / T : 1);
+      a.tpb = (int32_t)(4 / T > 0 ? 4 / T : 1);
       a.blocks_c = cdiv(a.nbank * a.nco, (int64_t)64);
       a.ntiles = a.blocks_c * cdiv(a.nto, (int64_t)a.tpb) * a.ni;
     }

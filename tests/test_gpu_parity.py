@@ -234,7 +234,7 @@ def test_reduce_small_odd_groups_short_time_blocks_integer_exact(eng, orc, shape
         # windows of nco + 15 <= 128 / 64 pack 2 / 4 time groups per workgroup
         tsub = 4 if nco + 15 <= 64 else 2 if nco + 15 <= 128 else 1
         if F == 12:  # k_reduce_col3: 64 groups x 16 / T time blocks per workgroup
-            assert plan["workgroups"] == -(-nco // 64) * ni * -(-nto // max(1, 8 // T)), \
+            assert plan["workgroups"] == -(-nco // 64) * ni * -(-nto // max(1, 4 // T)), \
                 (shape, plan)
         else:
             assert plan["workgroups"] == \

@@ -63,13 +63,6 @@ VARIANTS = {
     "nocol3": {"opts": {"col3": 0}},  # fqavby = 12 short blocks on k_reduce_lanet
     "rowt8o": {"opts": {"rowt_small": 100000}},  # k_reduce_rowt: always 8 rows per lane
     "rowtn16": {"opts": {"rowt_narrow8": 0}},  # narrow windows back on 16 rows per lane
-    # k_reduce_col3 with 4 rows per lane
-    "col3r4": {"patch": [("kernels.hip", "constexpr int TPB = 8 / T > 0 ? 8 / T : 1, NR = TPB * T;",
-                          "constexpr int TPB = 4 / T > 0 ? 4 / T : 1, NR = TPB * T;"),
-                         ("kernels.hip", "a.tpb = (int32_t)(8 / T > 0 ? 8 / T : 1);",
-                          "a.tpb = (int32_t)(4 / T > 0 ? 4 / T : 1);"),
-                         ("kernels.hip", "cdiv(a.nto, (int64_t)(8 / T > 0 ? 8 / T : 1))",
-                          "cdiv(a.nto, (int64_t)(4 / T > 0 ? 4 / T : 1))")]},
     # k_reduce_rows with a register budget for 6 / 8 resident waves per SIMD
     "rowsw6": {"patch": [("kernels.hip", "template <int OP, int G4, int S>\n__global__ __launch_bounds__(kBlock)\n"
                           "__attribute__((amdgpu_waves_per_eu(1, kRowMaxWaves)))",
