@@ -1627,7 +1627,9 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
     const dim3 g3((unsigned)(a.blocks_c * cdiv(cdiv(a.nto, a.tpb), 1 << a.tsub_log2)),
                   (unsigned)a.ni, (unsigned)a.nbank);
 #define BLDP_NARROWT(FF, TT)                                                  \
-  if (a.tpb == 8 / (TT))                                                      \
+  if ((TT) <= 2 && a.tpb == 4 / (TT))                                         \
+    BLDP_LAUNCH((k_reduce_narrowt<OP, FF, TT, ((TT) <= 2 ? 4 : 16)>), g3, block, 0, s, a); \
+  else if (a.tpb == 8 / (TT))                                                 \
     BLDP_LAUNCH((k_reduce_narrowt<OP, FF, TT, 8>), g3, block, 0, s, a);       \
   else                                                                        \
     BLDP_LAUNCH((k_reduce_narrowt<OP, FF, TT, 16>), g3, block, 0, s, a);
@@ -2165,16 +2167,17 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
       (opt(OPT_NARROW_TPB) >= 1 + (F == 1 && T == 1)) && a.nto > 1 && a.ni <= 65535 && a.nbank <= 65535) {
     const int64_t cols = a.nco * F / 4;
     const int sh = cols <= 64 ? 2 : cols <= 128 ? 1 : 0;
-    // 8 rows per lane (instead of 16) on launches under rowt_small (64)
-    // workgroups per CU and, at T = 1, on windows of <= 128 float4 columns:
-    // the 0002 band at F = 1 / 2, T = 1..4 +5..12%, the 0001 band F = 1 / 2
-    // T = 1 +7 / 3%; the 0000 band (1.8% slower) keeps 16
-    // (profiles/r04/ab_grid_r04o.json, ab_t1_0001_r04o.json)
+    // fewer rows per lane (instead of 16) on launches under rowt_small (64)
+    // workgroups per CU and, at T = 1, on windows of <= 128 float4 columns: 8
+    // (T = 3, 4) or 4 (T = 1, 2). 8 against 16: the 0002 band at F = 1 / 2,
+    // T = 1..4 +5..12%, the 0001 band F = 1 / 2 T = 1 +7 / 3%; 4 against 8 at
+    // T = 1, 2 another 2..8% (0002 / 0001 bands); the 0000 band keeps 16
+    // (profiles/r04/ab_grid_r04{o,w}.json, ab_t1_0001_r04{o,w}.json)
     int64_t tpb = 16 / T;
     if ((a.blocks_c * cdiv(cdiv(a.nto, tpb), (int64_t)1 << sh) * a.ni * a.nbank <
              opt(OPT_ROWT_SMALL) * num_cus ||
          (opt(OPT_ROWT_NARROW8) && cols <= 128 && T == 1)) && 8 / T >= 1)
-      tpb = 8 / T;
+      tpb = T <= 2 ? 4 / T : 8 / T;
     const int64_t x = a.blocks_c * cdiv(cdiv(a.nto, tpb), (int64_t)1 << sh);
     if (x <= INT32_MAX) {
       a.tpb = (int32_t)tpb;

@@ -316,9 +316,9 @@ def test_reduce_narrow_short_time_blocks_integer_exact(eng, orc, shape):
     nto, cols = nt // T, nco * F // 4
     tsub = 4 if cols <= 64 else 2 if cols <= 128 else 1
     ncu = torch.cuda.get_device_properties(0).multi_processor_count
-    tpb = 16 // T  # 8 rows per lane on small launches and, at T = 1, narrow windows
+    tpb = 16 // T  # 8 / 4 rows per lane on small launches and, at T = 1, narrow windows
     if -(-cols // 256) * ni * -(-(-(-nto // tpb)) // tsub) < 64 * ncu or (cols <= 128 and T == 1):
-        tpb = 8 // T
+        tpb = 4 // T if T <= 2 else 8 // T
     for op in ("sum", "max", "min", "mean"):
         plan = eng.plan(x, F, T, op)
         assert plan["path"] == "narrow", (shape, plan)
