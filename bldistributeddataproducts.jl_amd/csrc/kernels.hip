@@ -1743,7 +1743,9 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
     default: return hipErrorInvalidValue;                                                   \
   }
 #define BLDP_ROWT(T)                 \
-  if (a.tpb == 8 / (T)) {            \
+  if ((T) <= 2 && a.tpb == 4 / (T)) { \
+    BLDP_ROWTN(T, ((T) <= 2 ? 4 : 8))  \
+  } else if (a.tpb == 8 / (T)) {     \
     BLDP_ROWTN(T, 8)                 \
   } else if (a.tpb == 16 / (T)) {    \
     BLDP_ROWTN(T, 16)                \
@@ -2109,11 +2111,14 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
       // / 16 / 64 +1.2..6%, F = 64 T = 2 / 4 +4.5 / 1.8%; F = 16 T = 2, F = 8 T = 2
       // and F = 4 T = 3 -1.7..4%: not taken; profiles/r04/ab_t1_0001_r04{j,k}.json,
       // ab_grid1_r04p.json)
-      if ((bc * cdiv(cdiv(a.nto, tpb), (int64_t)1 << a.tsub_log2) * a.ni * a.nbank <
-               opt(OPT_ROWT_SMALL) * num_cus ||
-           (opt(OPT_ROWT_NARROW8) && cols <= 128 && (T == 1 || F >= 64))) &&
+      // Small launches at T <= 2 take 4 rows (0002 band T = 1 / 2, F = 4..256
+      // +2..6%, profiles/r04/ab_grid_r04x.json; the narrow 0001 windows stay on
+      // 8: 4 lost 2-5% there, ab_t1_0001_r04x.json)
+      const bool small = bc * cdiv(cdiv(a.nto, tpb), (int64_t)1 << a.tsub_log2) * a.ni *
+                             a.nbank < opt(OPT_ROWT_SMALL) * num_cus;
+      if ((small || (opt(OPT_ROWT_NARROW8) && cols <= 128 && (T == 1 || F >= 64))) &&
           (8 / T > 1 || (bc <= INT32_MAX && a.ni * a.nto <= 65535)))
-        tpb = 8 / T;
+        tpb = small && T <= 2 ? 4 / T : 8 / T;
       if (tpb == 1) {  // k_reduce_row
         a.tpb = 1;
         a.tsub_log2 = 0;

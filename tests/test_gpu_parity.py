@@ -178,9 +178,10 @@ def test_reduce_short_time_blocks_integer_exact(eng, orc, shape):
     tsub = 1 if tpb == 1 else 4 if cols <= 64 else 2 if cols <= 128 else 1
     blocks_c = -(-cols // 256)
     ncu = torch.cuda.get_device_properties(0).multi_processor_count
-    if tpb > 1 and (blocks_c * ni * -(-(-(-nto // tpb)) // tsub) < 64 * ncu or
-                    (cols <= 128 and (T == 1 or F >= 64))):
-        tpb = 8 // T  # small launch or narrow window: 8 rows per lane
+    small = blocks_c * ni * -(-(-(-nto // tpb)) // tsub) < 64 * ncu
+    if tpb > 1 and (small or (cols <= 128 and (T == 1 or F >= 64))):
+        # small launch (4 rows per lane at T <= 2) or narrow window: 8 rows
+        tpb = 4 // T if small and T <= 2 else 8 // T
         if tpb == 1:  # (tavby = 8: one block per workgroup, k_reduce_row's grid)
             tsub = 1
     for op in ("sum", "max", "min", "mean"):

@@ -63,11 +63,6 @@ VARIANTS = {
     "nocol3": {"opts": {"col3": 0}},  # fqavby = 12 short blocks on k_reduce_lanet
     "rowt8o": {"opts": {"rowt_small": 100000}},  # k_reduce_rowt: always 8 rows per lane
     "rowtn16": {"opts": {"rowt_narrow8": 0}},  # narrow windows back on 16 rows per lane
-    # k_reduce_rowt with 4 rows per lane at T <= 2 where it takes 8
-    "rowt4": {"patch": [("kernels.hip", "  if (a.tpb == 8 / (T)) {            \\\n",
-                         "  if ((T) <= 2 && a.tpb == 4 / (T)) {  \\\n    BLDP_ROWTN(T, ((T) <= 2 ? 4 : 8)) \\\n"
-                         "  } else if (a.tpb == 8 / (T)) {            \\\n"),
-                        ("kernels.hip", "\n        tpb = 8 / T;\n", "\n        tpb = T <= 2 ? 4 / T : 8 / T;\n")]},
     # k_reduce_rows with a register budget for 6 / 8 resident waves per SIMD
     "rowsw6": {"patch": [("kernels.hip", "template <int OP, int G4, int S>\n__global__ __launch_bounds__(kBlock)\n"
                           "__attribute__((amdgpu_waves_per_eu(1, kRowMaxWaves)))",
