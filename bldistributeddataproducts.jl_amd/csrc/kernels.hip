@@ -1219,11 +1219,15 @@ void k_reduce_rows(const RedArgs a) {
 // k_reduce_row.  "rowt_pack" 1 (default) = windows of <= 128 float4 columns
 // share a workgroup between 2 or 4 time groups (no idle lanes).  "rowt_small"
 // (64): launches that would have fewer than this many workgroups per CU with
-// 16 rows per lane take 8 rows per lane (TPB = 8 / T, twice the workgroups;
-// 0 = always 16).  A/B, profiles/r03/ab_rowt_r03i.json (bit-identical): 8 rows
-// win on one 0002 file (1152 workgroups, 4.5 per CU: +10-18% at F = 16..256,
-// T = 1, 2, 4) and on the 0002 band (9216: +1.5-3.5%), and lose on the 0000
-// and 0001 bands (>= 200k workgroups: -1.5-3.5%).  The output tile is staged
+// 16 rows per lane take 8 rows per lane (TPB = 8 / T, twice the workgroups),
+// 4 at T <= 2 (round 4; 0 = always 16).  A/B, profiles/r03/ab_rowt_r03i.json
+// (bit-identical): 8 rows win on one 0002 file (1152 workgroups, 4.5 per CU:
+// +10-18% at F = 16..256, T = 1, 2, 4) and on the 0002 band (9216: +1.5-3.5%),
+// and lose on the 0000 band (>= 200k workgroups: -1.5-3.5%); 4 rows another
+// 2-6% on the 0002 band at T = 1, 2 (profiles/r04/ab_grid_r04x.json).
+// "rowt_narrow8": the 0001 product's <= 128-column windows take 8 rows too at
+// T = 1 and F >= 64; "row_bpack": on a stitched band of such windows the two
+// lane sets take two banks (template form BP).  The output tile is staged
 // in LDS and stored as whole row segments (16-byte stores where legal; each
 // wave storing its own groups' outputs was slower).  At most kRowtMaxWaves = 6
 // resident waves per SIMD (A/B against 4 and none, profiles/r02/ab_row_tpb.json).
@@ -1887,7 +1891,7 @@ const PlanOptDef kPlanOpts[OPT_COUNT] = {
     {"vec_row", 1},           // k_reduce_row for F = 4 .. 256
     {"row_tpb", 1},           // k_reduce_rowt for short time blocks
     {"rowt_pack", 1},         // narrow rowt windows: 2 / 4 time groups per workgroup
-    {"rowt_small", 64},       // rowt: launches below this many workgroups per CU take 8 rows
+    {"rowt_small", 64},       // rowt/narrowt: launches below this many workgroups per CU take 8 (4 at T <= 2) rows
     {"wavet", 1},             // k_reduce_wavet: 1 = where il is a poor fit, 2 = always, 0 = never
     {"unaligned_vec", 2},     // dword-aligned 16-byte loads: 1 = reduce, 2 = + kurtosis, 3 = all
     {"kurt_exact", 1},        // k_kurt_regs exact-count forms for 16 / 32 spectra
@@ -2103,7 +2107,7 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
       // <= 128 float4 columns: 2 or 4 time groups per workgroup (>= 64 lanes each)
       const int64_t cols = a.nco * (F / 4);
       a.tsub_log2 = opt(OPT_ROWT_PACK) ? (cols <= 64 ? 2 : cols <= 128 ? 1 : 0) : 0;
-      // small launches: 8 rows per lane, twice the workgroups (option rowt_small);
+      // small launches: 8 rows per lane (4 at T <= 2), more workgroups (option rowt_small);
       // at T = 8 that is one time block per workgroup, i.e. k_reduce_row, whose
       // 3-D grid must then hold (IF, time block) in y
       // windows of <= 128 float4 columns (the 0001 product) take 8 rows too at
