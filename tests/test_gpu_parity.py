@@ -1114,8 +1114,8 @@ def test_wavet_bank_pack_stitched(pkg, eng, orc, nc):
     bank) banks, T = 1, 2, 3, 4, partial last workgroups, every op."""
     rng = np.random.default_rng(nc)
     for nb in ((2, 3, 8, 16) if nc == 512 else (2, 3, 8)):
-        for T, nt in ((1, 1001), (2, 402), (3, 303), (4, 100)):
-            data = [np.asfortranarray(rng.integers(0, 256, (nc, 1, nt)).astype(np.float32))
+        for T, nt, ni in ((1, 1001, 1), (2, 402, 1), (3, 303, 1), (4, 100, 1), (1, 64, 3)):
+            data = [np.asfortranarray(rng.integers(0, 256, (nc, ni, nt)).astype(np.float32))
                     for _ in range(nb)]
             xs = [dev(eng, a) for a in data]
             assert eng.plan(xs[0], 512, T, "sum")["path"] == "vector"
@@ -1168,11 +1168,12 @@ def test_lanes_along_stitched_rows(pkg, eng, orc, F):
     rng = np.random.default_rng(F + 7)
     nc = 512 // F * F
     for nb in (2, 3, 8):
-        for T, nt in ((1, 1001), (2, 300), (3, 297), (4, 100), (8, 200)):
-            data = [np.asfortranarray(rng.integers(0, 256, (512, 1, nt)).astype(np.float32))
+        for T, nt, ni in ((1, 1001, 1), (2, 300, 1), (3, 297, 1), (4, 100, 1), (8, 200, 1),
+                          (1, 120, 2)):
+            data = [np.asfortranarray(rng.integers(0, 256, (512, ni, nt)).astype(np.float32))
                     for _ in range(nb)]
             xs = [dev(eng, a) for a in data]
-            for win in ([0, nc, 1, 0, 1, 1, 0, nt, 1], [F, nc - F, 1, 0, 1, 1, 0, nt, 1]):
+            for win in ([0, nc, 1, 0, ni, 1, 0, nt, 1], [F, nc - F, 1, 0, ni, 1, 0, nt, 1]):
                 for op in ("sum", "mean", "max", "min"):
                     got = host(eng, eng.band_reduce(xs, F, T, op, win))
                     with pkg._lib.plan_option("lane_bpack", 0):
@@ -1192,8 +1193,8 @@ def test_rowt_bank_pack_stitched(pkg, eng, orc, F):
     never packed."""
     rng = np.random.default_rng(F + 1)
     for nb in (2, 3, 4, 8):
-        for T, nt in ((1, 4001), (2, 1000), (4, 968)):
-            data = [np.asfortranarray(rng.integers(0, 256, (512, 1, nt)).astype(np.float32))
+        for T, nt, ni in ((1, 4001, 1), (2, 1000, 1), (4, 968, 1), (1, 300, 2)):
+            data = [np.asfortranarray(rng.integers(0, 256, (512, ni, nt)).astype(np.float32))
                     for _ in range(nb)]
             xs = [dev(eng, a) for a in data]
             for op in ("sum", "mean", "max", "min"):
