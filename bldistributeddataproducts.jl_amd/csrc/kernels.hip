@@ -121,6 +121,27 @@ __device__ __forceinline__ void st1(float *p, float v) {
   else
     *p = v;
 }
+// The row, interleaved and short-time-block row kernels choose per launch
+// (a.st_plain, plan option "st_plain"): launches of < 2 GB keep their output
+// stores plain, larger ones non-temporal.  On the 0002 products plain stores
+// were 4-9% faster (cfg1 -6%, cfg2 -6%, fqavby 4..16 without time
+// integration -4..6%, fqavby 512..4096 at T <= 3 -3..9%), on the 0001 (14.4 GB)
+// and 0000 (32 GiB) bands nt stores 1-10% faster (profiles/r04/
+// ab_*_stores_r04ad.json).  (The lane kernels keep theirs non-temporal: plain
+// lost 2-8% there at every size.)
+__device__ __forceinline__ void st1o(float *p, float v, int32_t plain) {
+  if (plain)
+    *p = v;
+  else
+    __builtin_nontemporal_store(v, p);
+}
+__device__ __forceinline__ void st4o(float *p, float4 r, int32_t plain) {
+  const f4v v = {r.x, r.y, r.z, r.w};
+  if (plain)
+    *reinterpret_cast<f4v *>(p) = v;
+  else
+    __builtin_nontemporal_store(v, reinterpret_cast<f4v *>(p));
+}
 // independent float4 accumulators per lane
 constexpr int kNacc = 8;
 // Resident-wave caps (amdgpu_waves_per_eu) per SIMD: fewer concurrent row
@@ -1085,8 +1106,8 @@ __global__ __launch_bounds__(kBlock) void k_reduce_il(const RedArgs a) {
 #pragma unroll
       for (int q = 0; q < NS; ++q)
         if ((4 * q * PER + w) / K4 == tid) s = R<OP>::f(s, red[w][q]);
-    st1<1>(a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + (int64_t)to * a.out_ld_t + g0 + tid,
-           finish<OP>(s, a));
+    st1o(a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + (int64_t)to * a.out_ld_t + g0 + tid,
+         finish<OP>(s, a), a.st_plain);
   }
 }
 
@@ -1136,8 +1157,8 @@ void k_reduce_row(const RedArgs a) {
   }
   const float s = lanes_fold<OP, G4>(fold4<OP>(fold_acc<OP>(acc)));
   if (valid && (tid & (G4 - 1)) == 0)
-    st1<1>(a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + (int64_t)to * a.out_ld_t + col / G4,
-           finish<OP>(s, a));
+    st1o(a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + (int64_t)to * a.out_ld_t + col / G4,
+         finish<OP>(s, a), a.st_plain);
 }
 
 // k_reduce_row with a time block's rows split over S slices of the
@@ -1200,9 +1221,9 @@ void k_reduce_rows(const RedArgs a) {
       for (int q = 0; q < NA; ++q) all[s2 * NA + q] = xs[s2 - 1][q][c];
     const float s = lanes_fold<OP, G4>(fold4<OP>(fold_acc<OP>(all)));
     if (valid && (c & (G4 - 1)) == 0)
-      st1<1>(a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + (int64_t)to * a.out_ld_t +
-                 col / G4,
-             finish<OP>(s, a));
+      st1o(a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + (int64_t)to * a.out_ld_t +
+               col / G4,
+           finish<OP>(s, a), a.st_plain);
   }
 }
 
@@ -1324,10 +1345,10 @@ void k_reduce_rowt(const RedArgs a) {
       const float *src = &tile[(r << lw) + 4 * q];
       float *dst = ob + to * a.out_ld_t + 4 * q;
       if (g + 3 < lim) {
-        st4(dst, make_float4(src[0], src[1], src[2], src[3]));
+        st4o(dst, make_float4(src[0], src[1], src[2], src[3]), a.st_plain);
       } else {
         for (int k = 0; k < 4; ++k)
-          if (g + k < lim) st1<1>(dst + k, src[k]);
+          if (g + k < lim) st1o(dst + k, src[k], a.st_plain);
       }
     }
   } else {
@@ -1335,7 +1356,7 @@ void k_reduce_rowt(const RedArgs a) {
       const int r = e >> lw, q = e & ((1 << lw) - 1);
       const int64_t to = tob + r;
       if (to >= a.nto || gcol0 + q >= lim) continue;
-      st1<1>(ob + to * a.out_ld_t + q, tile[e]);
+      st1o(ob + to * a.out_ld_t + q, tile[e], a.st_plain);
     }
   }
   (void)valid;
@@ -1906,6 +1927,7 @@ const PlanOptDef kPlanOpts[OPT_COUNT] = {
     {"wave_bpack", 1},        // k_reduce_wavet: a wave per (bank, group) of <= 16-group stitched rows
     {"col3", 1},              // fqavby = 12, short time blocks: k_reduce_col3 (float4 columns)
     {"rowt_narrow8", 1},      // k_reduce_rowt: 8 rows per lane on <= 128-column windows too
+    {"st_plain", 1},          // row / il stores: 1 plain below 2 GB of traffic, 0 always nt, 2 always plain
 };
 struct PlanOpts {
   std::atomic<int64_t> v[OPT_COUNT];  // -1 = no override
@@ -1939,6 +1961,7 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
   a.tsub_log2 = 0;
   a.rsplit = 1;
   a.bpack = 0;
+  a.st_plain = 0;
   const bool t38 = opt(OPT_T38) != 0;
   if (opt(OPT_LANET) && words && a.in_cs == 1 && (T == 1 || T == 2 || T == 4 || (t38 && (T == 3 || T == 8))) &&
       (F == 3 || F == 5 || F == 6 || F == 7 || F == 12) && a.ni <= 65535 && a.nbank <= 65535 &&
@@ -2213,6 +2236,13 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
     const uintptr_t op = (uintptr_t)a.out;
     a.vec_out = (op % (4 * w) == 0) && a.out_bank % w == 0 && a.out_ld_i % w == 0 &&
                 a.out_ld_t % w == 0;
+  }
+  // output stores of the row / interleaved kernels: plain below 2 GB of
+  // launch traffic, non-temporal above (option st_plain: -1 by size, 0 nt, 1 plain)
+  {
+    const int64_t bytes = 4 * a.nbank * a.ni * (a.nco * F * a.nto * T + a.nco * a.nto);
+    const int64_t o = opt(OPT_ST_PLAIN);
+    a.st_plain = o == 2 ? 1 : o == 0 ? 0 : (bytes < ((int64_t)2 << 30) ? 1 : 0);
   }
   a.div = (float)(F * T);
   return p;

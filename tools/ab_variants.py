@@ -63,13 +63,7 @@ VARIANTS = {
     "nocol3": {"opts": {"col3": 0}},  # fqavby = 12 short blocks on k_reduce_lanet
     "rowt8o": {"opts": {"rowt_small": 100000}},  # k_reduce_rowt: always 8 rows per lane
     "rowtn16": {"opts": {"rowt_narrow8": 0}},  # narrow windows back on 16 rows per lane
-    # 16-byte output stores without the nt hint (and st1<1> plain too)
-    "stplain": {"patch": [("kernels.hip", "  __builtin_nontemporal_store(v, reinterpret_cast<f4v *>(p));",
-                           "  *reinterpret_cast<f4v *>(p) = v;"),
-                          ("kernels.hip", "  if constexpr (NT)\n    __builtin_nontemporal_store(v, p);",
-                           "  if constexpr (false)\n    __builtin_nontemporal_store(v, p);")]},
-    "st4plain": {"patch": [("kernels.hip", "  __builtin_nontemporal_store(v, reinterpret_cast<f4v *>(p));",
-                            "  *reinterpret_cast<f4v *>(p) = v;")]},
+    "stnt": {"opts": {"st_plain": 0}},  # row / il output stores always non-temporal
     # k_reduce_rows with a register budget for 6 / 8 resident waves per SIMD
     "rowsw6": {"patch": [("kernels.hip", "template <int OP, int G4, int S>\n__global__ __launch_bounds__(kBlock)\n"
                           "__attribute__((amdgpu_waves_per_eu(1, kRowMaxWaves)))",
