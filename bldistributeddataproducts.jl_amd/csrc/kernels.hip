@@ -123,12 +123,13 @@ __device__ __forceinline__ void st1(float *p, float v) {
 }
 // The row, interleaved and short-time-block row kernels choose per launch
 // (a.st_plain, plan option "st_plain"): launches of < 2 GB keep their output
-// stores plain, larger ones non-temporal.  On the 0002 products plain stores
-// were 4-9% faster (cfg1 -6%, cfg2 -6%, fqavby 4..16 without time
-// integration -4..6%, fqavby 512..4096 at T <= 3 -3..9%), on the 0001 (14.4 GB)
-// and 0000 (32 GiB) bands nt stores 1-10% faster (profiles/r04/
-// ab_*_stores_r04ad.json).  (The lane kernels keep theirs non-temporal: plain
-// lost 2-8% there at every size.)
+// stores plain, larger ones non-temporal.  On one box plain stores were 4-9%
+// faster on the 0002 products (cfg1 -6%, cfg2 -6%, fqavby 4..16 without time
+// integration -4..6%, fqavby 512..4096 at T <= 3 -3..9%) and nt stores 1-10%
+// faster on the 0001 (14.4 GB) and 0000 (32 GiB) bands (profiles/r04/
+// ab_*_stores_r04ad.json); on another the size rule and nt everywhere were
+// even (geomean 0.994-1.002, ab_*_stplain_r04ae.json).  (The lane kernels keep
+// theirs non-temporal: plain lost 2-8% there at every size.)
 __device__ __forceinline__ void st1o(float *p, float v, int32_t plain) {
   if (plain)
     *p = v;
