@@ -1831,15 +1831,6 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
   }
   if (p.path == PATH_VEC_IL) {
     const dim3 g3((unsigned)a.blocks_c, (unsigned)(a.ni * a.nto), (unsigned)a.nbank);
-    if (a.il_gpw == 1) {  // (small launches, K4 >= 4: one group per workgroup)
-      switch (a.k4) {
-        case 4: BLDP_LAUNCH((k_reduce_il<OP, 4, 1>), g3, block, 0, s, a); break;
-        case 8: BLDP_LAUNCH((k_reduce_il<OP, 8, 1>), g3, block, 0, s, a); break;
-        case 16: BLDP_LAUNCH((k_reduce_il<OP, 16, 1>), g3, block, 0, s, a); break;
-        default: return hipErrorInvalidValue;
-      }
-      return hipGetLastError();
-    }
     switch (a.k4) {
       case 2: BLDP_LAUNCH((k_reduce_il<OP, 2, kIlGpw>), g3, block, 0, s, a); break;
       case 4: BLDP_LAUNCH((k_reduce_il<OP, 4, kIlGpw>), g3, block, 0, s, a); break;
@@ -1938,7 +1929,6 @@ const PlanOptDef kPlanOpts[OPT_COUNT] = {
     {"col3", 1},              // fqavby = 12, short time blocks: k_reduce_col3 (float4 columns)
     {"rowt_narrow8", 1},      // k_reduce_rowt: 8 rows per lane on <= 128-column windows too
     {"st_plain", 1},          // row / il stores: 1 plain below 2 GB of traffic, 0 always nt, 2 always plain
-    {"il_gpw1", 1},           // k_reduce_il: one group per workgroup on small launches (K4 >= 4)
 };
 struct PlanOpts {
   std::atomic<int64_t> v[OPT_COUNT];  // -1 = no override
@@ -1973,7 +1963,6 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
   a.rsplit = 1;
   a.bpack = 0;
   a.st_plain = 0;
-  a.il_gpw = kIlGpw;
   const bool t38 = opt(OPT_T38) != 0;
   if (opt(OPT_LANET) && words && a.in_cs == 1 && (T == 1 || T == 2 || T == 4 || (t38 && (T == 3 || T == 8))) &&
       (F == 3 || F == 5 || F == 6 || F == 7 || F == 12) && a.ni <= 65535 && a.nbank <= 65535 &&
@@ -2123,16 +2112,8 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
       (a.k4 == 2 || a.k4 == 4 || a.k4 == 8 || a.k4 == 16) && a.ts == 1 && a.nchunk == 1 &&
       cdiv(a.nco, kIlGpw) <= INT32_MAX && a.ni * a.nto <= 65535 && a.nbank <= 65535) {
     p.path = PATH_VEC_IL;
-    a.il_gpw = kIlGpw;
     a.blocks_c = cdiv(a.nco, kIlGpw);
     a.ntiles = a.blocks_c * a.ni * a.nto * a.nbank;
-    // launches of fewer than 64 workgroups per CU at K4 >= 4: one group per
-    // workgroup, twice the workgroups (option il_gpw1)
-    if (opt(OPT_IL_GPW1) && a.k4 >= 4 && a.ntiles < (int64_t)64 * num_cus) {
-      a.il_gpw = 1;
-      a.blocks_c = a.nco;
-      a.ntiles = a.blocks_c * a.ni * a.nto * a.nbank;
-    }
     p.grid = a.ntiles;
   }
   // small power-of-two groups, whole time block per tile, no time split:

@@ -1271,7 +1271,7 @@ PLAN_OPTION_VALUES = {
     "row_tpb": (0, 1), "rowt_pack": (0, 1), "rowt_small": (0, 64, 100000), "wavet": (0, 1, 2),
     "unaligned_vec": (0, 1, 2, 3), "row_bpack": (0, 1), "lane_bpack": (0, 1),
     "wave_bpack": (0, 1), "col3": (0, 1), "rowt_narrow8": (0, 1),
-    "st_plain": (0, 2), "il_gpw1": (0, 1),
+    "st_plain": (0, 2),
 }
 # (nchan, nif, ntime, window, F, T): shapes where the options above change the plan
 PLAN_OPTION_SHAPES = [

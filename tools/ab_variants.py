@@ -64,7 +64,6 @@ VARIANTS = {
     "rowt8o": {"opts": {"rowt_small": 100000}},  # k_reduce_rowt: always 8 rows per lane
     "rowtn16": {"opts": {"rowt_narrow8": 0}},  # narrow windows back on 16 rows per lane
     "stnt": {"opts": {"st_plain": 0}},  # row / il output stores always non-temporal
-    "ilgpw2": {"opts": {"il_gpw1": 0}},  # k_reduce_il: two groups per workgroup on small launches too
     # k_reduce_rows with a register budget for 6 / 8 resident waves per SIMD
     "rowsw6": {"patch": [("kernels.hip", "template <int OP, int G4, int S>\n__global__ __launch_bounds__(kBlock)\n"
                           "__attribute__((amdgpu_waves_per_eu(1, kRowMaxWaves)))",
