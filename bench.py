@@ -608,6 +608,8 @@ def main():
     ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-read-probe", action="store_true",
+                    help="skip the box pure-read reference (roofline.box_read_probe)")
     ap.add_argument("--mode", default="reduce",
                     choices=["reduce", "kurtosis", "host", "decode", "file", "rawfile",
                              "rendezvous", "typed"])
@@ -845,6 +847,15 @@ def main():
                        f"backend (CPU transport) gather + stitch, {len(mine)} bank(s)/rank")
     result = None
     if rank == 0:
+        # this box's pure-read rate for a buffer of the launch's bytes
+        # (bldp_read_probe, the pure read of tools/mix_ceiling.hip): HBM rates
+        # differ box to box by several percent, so the reduce is also set
+        # beside what a kernel that only reads reaches on the same GPU
+        probe = None
+        if not args.no_read_probe:
+            preps.clear()
+            torch.cuda.empty_cache()
+            probe = eng.read_probe(bytes_launch, stream=stream)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             preps.clear()  # (they hold the banks)
@@ -872,7 +883,9 @@ def main():
                          "kernel_ms_source": "per-launch dispatch events over K launches after "
                                              "the timed region",
                          "span_ms_per_launch": round(span_ms, 4),
-                         "bytes_per_launch": bytes_launch},
+                         "bytes_per_launch": bytes_launch,
+                         "box_read_probe": probe,
+                         "frac_of_box_read": probe and round(achieved / probe["GBps"], 4)},
             "host_enqueue_ms_per_step": round(host_ms, 4),
             "settle_launches": settle,
             "cpu_baseline": cpu,

@@ -83,6 +83,7 @@ SIGNATURES = {
     "bldp_band_kurtosis_f32": ([I, P, I64, I64, I64, P, P, P], I),
     "bldp_fqav_range": ([D, D, I64, I64, P, P, P], I),
     "bldp_synth_f32": ([P, I64, I64, I64, I64, U64, I, P], I),
+    "bldp_read_probe": ([P, I64, I, P, P, P], I),
     "bldp_reduce_out_dtype": ([I, I], I),
     "bldp_reduce_strided": ([I, P, I64, I64, I64, P, I64, I64, I, P, I64, I64, P], I),
     "bldp_kurtosis": ([I, P, I64, I64, I64, P, P, P], I),

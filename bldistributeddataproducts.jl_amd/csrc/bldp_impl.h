@@ -188,6 +188,8 @@ int typed_out_dtype(int dtype, int op);    // -1 = invalid
 hipError_t launch_reduce_typed(const TypedArgs &a, int op, hipStream_t s);
 hipError_t launch_kurtosis_typed(const TypedArgs &a, double *out, hipStream_t s);
 
+hipError_t launch_read_probe(const float *in, int64_t bytes, int form, int num_cus,
+                             hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
 hipError_t launch_synth(float *out, int64_t nchan, int64_t nif, int64_t ntime, int64_t nfpc,
                         uint64_t seed, int kind, hipStream_t s);
 

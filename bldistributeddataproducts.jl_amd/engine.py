@@ -500,6 +500,44 @@ def synth(nchan, nif, ntime, nfpc=1024, seed=0, kind=0, device=None, stream=None
     return out
 
 
+def read_probe(nbytes, launches=20, forms=(0, 2, 4), buf=None, stream=None,
+               every=False) -> dict:
+    """The pure-read rate of this GPU for an ``nbytes`` buffer
+    (bldp_read_probe): ``launches`` back-to-back launches per form (include/
+    bldp.h: workgroups per CU | plain loads << 8 | 8 loads in flight << 9),
+    each timed by events carried on its dispatch; the best form's median.  The
+    measurement reference bench.py sets a reduce's bandwidth beside (boxes
+    differ by several percent)."""
+    import statistics
+    torch = _torch()
+    L = _lib.lib()
+    nbytes = int(nbytes) // 16 * 16
+    if buf is None:
+        buf = torch.zeros(max(nbytes // 4, 4), dtype=torch.float32, device="cuda")
+    elif buf.numel() * buf.element_size() < nbytes:
+        raise ValueError("probe buffer smaller than nbytes")
+    sp = _lib.stream_ptr(stream)
+    evs = [(_lib.HipEvent(timing=True, fence=False), _lib.HipEvent(timing=True, fence=False))
+           for _ in range(launches)]
+    best, seen = None, []
+    for g in forms:
+        for _ in range(3):
+            _lib.check(L.bldp_read_probe(buf.data_ptr(), nbytes, g, sp, None, None),
+                       "bldp_read_probe")
+        for e0, e1 in evs:
+            _lib.check(L.bldp_read_probe(buf.data_ptr(), nbytes, g, sp, e0.ev, e1.ev),
+                       "bldp_read_probe")
+        torch.cuda.synchronize()
+        ms = statistics.median(e0.elapsed_time(e1) for e0, e1 in evs)
+        r = {"GBps": round(nbytes / (ms * 1e-3) / 1e9, 1), "ms": round(ms, 5),
+             "form": g, "wg_per_cu": g & 255, "loads": "plain" if g & 256 else "nt",
+             "in_flight": 8 if g & 512 else 16, "bytes": nbytes}
+        seen.append(r)
+        if best is None or r["GBps"] > best["GBps"]:
+            best = r
+    return dict(best, forms=seen) if every else best
+
+
 def reduce_host(a: np.ndarray, fqavby=1, tavby=1, op="sum", win=None, device=0) -> np.ndarray:
     """Host array in, host array out (bldp_reduce_host_f32): the window is
     streamed through the GPU and reduced there."""

@@ -388,6 +388,16 @@ BLDP_API int bldp_fqav_range(double first, double step, int64_t len, int64_t n, 
 /* Synthetic BL-like filterbank (nchan, nif, ntime) on the device:
  * kind 0 = gamma(2, 5e8) x bandpass scallop x DC spike (nfpc bins per coarse
  * channel); kind 1 = integer-valued 0..255 (order-independent exact sums). */
+/* Measurement support (bench.py): stream `bytes` of a 16-byte-aligned device
+ * buffer once and store nothing.  form: bits 0-7 workgroups per CU (0: one
+ * workgroup per chunk, else that many persistent ones per CU), bit 8 plain
+ * loads instead of non-temporal ones, bit 9 8 loads in flight per thread
+ * instead of 16.  ev_start/ev_stop (hipEvent_t or NULL) ride on the dispatch
+ * as in bldp_reduce_launch_timed: the pure-read rate of this box for that
+ * buffer, the reference a reduce's bandwidth is set beside. */
+BLDP_API int bldp_read_probe(const void *dev, int64_t bytes, int form, void *stream,
+                             void *ev_start, void *ev_stop);
+
 BLDP_API int bldp_synth_f32(float *out, int64_t nchan, int64_t nif, int64_t ntime, int64_t nfpc,
                    uint64_t seed, int kind, void *stream);
 

@@ -679,6 +679,10 @@ def test_bench_json_contract():
     assert rf["kernel_ms"] > 0 and rf["span_ms_per_launch"] > 0
     assert rf["span_ms_per_launch"] <= d["ms_per_step"] * 1.05
     assert d["settle_launches"] > 0
+    # the box's pure-read rate for the launch's bytes, and the reduce beside it
+    pr = rf["box_read_probe"]
+    assert pr["bytes"] == rf["bytes_per_launch"] // 16 * 16 and 0 < pr["GBps"] < 20000.0
+    assert rf["frac_of_box_read"] == pytest.approx(rf["achieved"] / pr["GBps"], rel=1e-3)
     cb = d["cpu_baseline"]
     assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1
     assert "workload" in d["config"]
@@ -916,3 +920,26 @@ def test_cfg5_share_full_size_host_path(pkg, orc):
             del t
         del h
         torch.cuda.empty_cache()
+
+
+def test_read_probe(pkg):
+    """bldp_read_probe: the pure-read reference bench.py reports (timed by
+    dispatch-carried events), its grid forms, and its argument checks."""
+    import torch
+
+    r = pkg.engine.read_probe(64 << 20, launches=5)
+    # (a 64 MiB buffer read over and over partly stays in the 256 MB
+    # Infinity Cache: 8.7 TB/s measured, above the HBM peak)
+    assert r["bytes"] == 64 << 20 and r["form"] in (0, 2, 4) and 500 < r["GBps"] < 20000
+    L = pkg._lib.lib()
+    buf = torch.zeros(1 << 20, dtype=torch.float32, device="cuda")
+    for g in (0, 1, 2, 4):  # ragged tail (a partial chunk) in every form
+        for m in range(4):
+            assert L.bldp_read_probe(buf.data_ptr(), (4 << 20) - 48, m << 8 | g, None, None,
+                                     None) == 0
+    assert L.bldp_read_probe(None, 0, 0, None, None, None) == 0
+    assert L.bldp_read_probe(buf.data_ptr() + 4, 1024, 0, None, None, None) != 0
+    assert L.bldp_read_probe(buf.data_ptr(), -16, 0, None, None, None) != 0
+    assert L.bldp_read_probe(buf.data_ptr(), 1024, -1, None, None, None) != 0
+    assert L.bldp_read_probe(buf.data_ptr(), 1024, 1024, None, None, None) != 0
+    torch.cuda.synchronize()

@@ -63,6 +63,7 @@ for s in $STEPS; do
     gap) run gap 300 python tools/gap_probe.py --json "$OUT/gap.json" ;;
     getband64) run getband64 600 env BLDP_NATIVE_BATCH_MB=64 python tools/getband_probe.py \
         --json "$OUT/getband64.json" ;;
+    probesweep) run probesweep 300 python tools/read_probe_sweep.py --json "$OUT/probesweep.json" ;;
     getband) run getband 600 python tools/getband_probe.py --json "$OUT/getband.json" ;;
   esac
 done

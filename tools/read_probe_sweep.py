@@ -1,0 +1,40 @@
+#!/usr/bin/env python3
+"""The pure-read probe (bldp_read_probe) over grid forms and buffer sizes:
+which form bench.py's box reference should try.
+
+    python tools/read_probe_sweep.py [--json out.json]
+"""
+import argparse
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sizes-mb", default="68,272,545,1090,4096,32768")
+    ap.add_argument("--wg", default="0,1,2,3,4,8")
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    import __graft_entry__ as entry
+
+    eng = entry.load_package().engine
+    forms = tuple(m << 8 | int(g) for m in range(4) for g in a.wg.split(","))
+    res = {}
+    for mb in (int(m) for m in a.sizes_mb.split(",")):
+        r = eng.read_probe(mb << 20, launches=20, forms=forms, every=True)
+        res[mb] = r
+        print(mb, "MiB best", r["GBps"], "at form", r["form"], flush=True)
+        for f in r["forms"]:
+            print(f"   wg/cu {f['wg_per_cu']:2d} {f['loads']:5s} {f['in_flight']:2d} in flight: "
+                  f"{f['GBps']}", flush=True)
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
