@@ -842,7 +842,7 @@ int bldp_unchunk_f32(const float *packed, const int64_t chunk[3], const int64_t 
 
 int bldp_read_probe(const void *dev, int64_t bytes, int form, void *stream, void *ev_start,
                     void *ev_stop) {
-  if (bytes < 0 || form < 0 || form >= 1024) return fail(BLDP_EINVAL, "bad size or form");
+  if (bytes < 0 || form < 0 || form >= 2048) return fail(BLDP_EINVAL, "bad size or form");
   if (bytes >= 16 && (!dev || (uintptr_t)dev % 16)) return fail(BLDP_EINVAL, "null or unaligned buffer");
   hipError_t e = launch_read_probe(static_cast<const float *>(dev), bytes, form,
                                    num_cus_current(), (hipStream_t)stream, (hipEvent_t)ev_start,

@@ -2292,51 +2292,63 @@ hipError_t launch_despike(float *d, int64_t nchan, int64_t nrows, int64_t nfpc, 
 // the pure read of tools/mix_ceiling.hip): chunks of NL*kBlock 16-byte words,
 // each thread NL 16-byte loads (non-temporal unless PLAIN) at a kBlock-word
 // stride, nothing stored (a store that never happens keeps the loads); one
-// workgroup per chunk or wg_per_cu persistent workgroups per CU.
-template <bool PLAIN, int NL>
+// workgroup per chunk or wg_per_cu persistent workgroups per CU.  SLABS: the
+// buffer is cut into NL equal slabs and chunk c reads kBlock words of each
+// (NL streams far apart at once, as a reduce reads a block's time rows).
+template <bool PLAIN, int NL, bool SLABS>
 __global__ __launch_bounds__(kBlock) void k_read_probe(const float *in, int64_t nchunk, int64_t n4,
-                                                        float *sink) {
+                                                        int64_t slab, float *sink) {
   const int t = threadIdx.x;
   f4v acc = {0, 0, 0, 0};
   const f4v *p = reinterpret_cast<const f4v *>(in);
   for (int64_t c = blockIdx.x; c < nchunk; c += gridDim.x) {
-    const int64_t b = c * NL * kBlock + t;
+    const int64_t b = SLABS ? c * kBlock + t : c * NL * kBlock + t;
     f4v v[NL];
 #pragma unroll
-    for (int k = 0; k < NL; ++k)
-      v[k] = b + kBlock * k >= n4 ? f4v{0, 0, 0, 0}
-             : PLAIN              ? p[b + kBlock * k]
-                                  : __builtin_nontemporal_load(p + b + kBlock * k);
+    for (int k = 0; k < NL; ++k) {
+      const int64_t i = b + (SLABS ? slab : kBlock) * k;
+      v[k] = i >= n4 ? f4v{0, 0, 0, 0} : PLAIN ? p[i] : __builtin_nontemporal_load(p + i);
+    }
 #pragma unroll
     for (int k = 0; k < NL; ++k) acc += v[k];
   }
   if (acc.x == 1234.5f && sink) sink[t] = acc.y;
 }
 
-template <bool PLAIN, int NL>
+template <bool PLAIN, int NL, bool SLABS>
 static void read_probe_go(const float *in, int64_t bytes, int wg_per_cu, int num_cus,
                           hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
-  const int64_t n4 = bytes / 16, nchunk = cdiv(n4, (int64_t)NL * kBlock);
+  const int64_t n4 = bytes / 16, slab = cdiv(cdiv(n4, NL), kBlock) * kBlock;
+  const int64_t nchunk = SLABS ? slab / kBlock : cdiv(n4, (int64_t)NL * kBlock);
   if (nchunk == 0) return;
   const int64_t grid = wg_per_cu > 0 ? std::min<int64_t>(nchunk, (int64_t)wg_per_cu * num_cus)
                                      : std::min<int64_t>(nchunk, INT32_MAX);
   if (ev1)  // timed like bldp_reduce_launch_timed: events carried by the dispatch
-    hipExtLaunchKernelGGL((k_read_probe<PLAIN, NL>), dim3((unsigned)grid), dim3(kBlock), 0, s,
-                          ev0, ev1, 0, in, nchunk, n4, (float *)nullptr);
+    hipExtLaunchKernelGGL((k_read_probe<PLAIN, NL, SLABS>), dim3((unsigned)grid), dim3(kBlock), 0,
+                          s, ev0, ev1, 0, in, nchunk, n4, slab, (float *)nullptr);
   else
-    hipLaunchKernelGGL((k_read_probe<PLAIN, NL>), dim3((unsigned)grid), dim3(kBlock), 0, s, in,
-                       nchunk, n4, (float *)nullptr);
+    hipLaunchKernelGGL((k_read_probe<PLAIN, NL, SLABS>), dim3((unsigned)grid), dim3(kBlock), 0, s,
+                       in, nchunk, n4, slab, (float *)nullptr);
+}
+
+template <bool SLABS>
+static void read_probe_form(const float *in, int64_t bytes, int form, int num_cus, hipStream_t s,
+                            hipEvent_t ev0, hipEvent_t ev1) {
+  const int g = form & 255;
+  switch (form >> 8 & 3) {
+    case 0: read_probe_go<false, 16, SLABS>(in, bytes, g, num_cus, s, ev0, ev1); break;
+    case 1: read_probe_go<true, 16, SLABS>(in, bytes, g, num_cus, s, ev0, ev1); break;
+    case 2: read_probe_go<false, 8, SLABS>(in, bytes, g, num_cus, s, ev0, ev1); break;
+    default: read_probe_go<true, 8, SLABS>(in, bytes, g, num_cus, s, ev0, ev1); break;
+  }
 }
 
 hipError_t launch_read_probe(const float *in, int64_t bytes, int form, int num_cus, hipStream_t s,
                              hipEvent_t ev0, hipEvent_t ev1) {
-  const int g = form & 255;
-  switch (form >> 8 & 3) {
-    case 0: read_probe_go<false, 16>(in, bytes, g, num_cus, s, ev0, ev1); break;
-    case 1: read_probe_go<true, 16>(in, bytes, g, num_cus, s, ev0, ev1); break;
-    case 2: read_probe_go<false, 8>(in, bytes, g, num_cus, s, ev0, ev1); break;
-    default: read_probe_go<true, 8>(in, bytes, g, num_cus, s, ev0, ev1); break;
-  }
+  if (form & 1024)
+    read_probe_form<true>(in, bytes, form, num_cus, s, ev0, ev1);
+  else
+    read_probe_form<false>(in, bytes, form, num_cus, s, ev0, ev1);
   return hipGetLastError();
 }
 

@@ -504,7 +504,8 @@ def read_probe(nbytes, launches=20, forms=(0, 2, 4), buf=None, stream=None,
                every=False) -> dict:
     """The pure-read rate of this GPU for an ``nbytes`` buffer
     (bldp_read_probe): ``launches`` back-to-back launches per form (include/
-    bldp.h: workgroups per CU | plain loads << 8 | 8 loads in flight << 9),
+    bldp.h: workgroups per CU | plain loads << 8 | 8 loads in flight << 9 |
+    slabs << 10),
     each timed by events carried on its dispatch; the best form's median.  The
     measurement reference bench.py sets a reduce's bandwidth beside (boxes
     differ by several percent)."""
@@ -531,7 +532,7 @@ def read_probe(nbytes, launches=20, forms=(0, 2, 4), buf=None, stream=None,
         ms = statistics.median(e0.elapsed_time(e1) for e0, e1 in evs)
         r = {"GBps": round(nbytes / (ms * 1e-3) / 1e9, 1), "ms": round(ms, 5),
              "form": g, "wg_per_cu": g & 255, "loads": "plain" if g & 256 else "nt",
-             "in_flight": 8 if g & 512 else 16, "bytes": nbytes}
+             "in_flight": 8 if g & 512 else 16, "slabs": bool(g & 1024), "bytes": nbytes}
         seen.append(r)
         if best is None or r["GBps"] > best["GBps"]:
             best = r

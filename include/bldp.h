@@ -392,7 +392,9 @@ BLDP_API int bldp_fqav_range(double first, double step, int64_t len, int64_t n, 
  * buffer once and store nothing.  form: bits 0-7 workgroups per CU (0: one
  * workgroup per chunk, else that many persistent ones per CU), bit 8 plain
  * loads instead of non-temporal ones, bit 9 8 loads in flight per thread
- * instead of 16.  ev_start/ev_stop (hipEvent_t or NULL) ride on the dispatch
+ * instead of 16, bit 10 the loads of one chunk spread over as many equal
+ * slabs of the buffer (that many streams far apart, as a reduce reads a
+ * block's time rows) instead of one contiguous piece.  ev_start/ev_stop (hipEvent_t or NULL) ride on the dispatch
  * as in bldp_reduce_launch_timed: the pure-read rate of this box for that
  * buffer, the reference a reduce's bandwidth is set beside. */
 BLDP_API int bldp_read_probe(const void *dev, int64_t bytes, int form, void *stream,

@@ -934,12 +934,12 @@ def test_read_probe(pkg):
     L = pkg._lib.lib()
     buf = torch.zeros(1 << 20, dtype=torch.float32, device="cuda")
     for g in (0, 1, 2, 4):  # ragged tail (a partial chunk) in every form
-        for m in range(4):
+        for m in range(8):
             assert L.bldp_read_probe(buf.data_ptr(), (4 << 20) - 48, m << 8 | g, None, None,
                                      None) == 0
     assert L.bldp_read_probe(None, 0, 0, None, None, None) == 0
     assert L.bldp_read_probe(buf.data_ptr() + 4, 1024, 0, None, None, None) != 0
     assert L.bldp_read_probe(buf.data_ptr(), -16, 0, None, None, None) != 0
     assert L.bldp_read_probe(buf.data_ptr(), 1024, -1, None, None, None) != 0
-    assert L.bldp_read_probe(buf.data_ptr(), 1024, 1024, None, None, None) != 0
+    assert L.bldp_read_probe(buf.data_ptr(), 1024, 2048, None, None, None) != 0
     torch.cuda.synchronize()

@@ -22,14 +22,15 @@ def main():
     import __graft_entry__ as entry
 
     eng = entry.load_package().engine
-    forms = tuple(m << 8 | int(g) for m in range(4) for g in a.wg.split(","))
+    forms = tuple(m << 8 | int(g) for m in (0, 1, 2, 3, 4, 5, 6, 7) for g in a.wg.split(","))
     res = {}
     for mb in (int(m) for m in a.sizes_mb.split(",")):
         r = eng.read_probe(mb << 20, launches=20, forms=forms, every=True)
         res[mb] = r
         print(mb, "MiB best", r["GBps"], "at form", r["form"], flush=True)
         for f in r["forms"]:
-            print(f"   wg/cu {f['wg_per_cu']:2d} {f['loads']:5s} {f['in_flight']:2d} in flight: "
+            print(f"   wg/cu {f['wg_per_cu']:2d} {f['loads']:5s} {f['in_flight']:2d} in flight "
+                  f"{'slabs' if f['slabs'] else 'contig'}: "
                   f"{f['GBps']}", flush=True)
     if a.json:
         with open(a.json, "w") as f:
