@@ -500,7 +500,12 @@ def synth(nchan, nif, ntime, nfpc=1024, seed=0, kind=0, device=None, stream=None
     return out
 
 
-def read_probe(nbytes, launches=20, forms=(0, 2, 4), buf=None, stream=None,
+# nt loads, 16 or 8 in flight, contiguous or slab-spread: the forms that led
+# some size of tools/read_probe_sweep.py (profiles/r04/read_probe_sweep_r04probe_b.json)
+PROBE_FORMS = (0, 3, 513, 514, 520, 1537, 1544)
+
+
+def read_probe(nbytes, launches=20, forms=PROBE_FORMS, buf=None, stream=None,
                every=False) -> dict:
     """The pure-read rate of this GPU for an ``nbytes`` buffer
     (bldp_read_probe): ``launches`` back-to-back launches per form (include/
