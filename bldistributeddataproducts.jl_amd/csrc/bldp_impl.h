@@ -72,6 +72,7 @@ struct RedArgs {
                            // lane path: k_reduce_lanes (lanes along the stitched row)
   int32_t rsplit;          // k_reduce_rows: slices of a workgroup splitting a block's rows (1 = k_reduce_row)
   int32_t st_plain;        // row / il / rowt output stores plain (1) or non-temporal (0)
+  int32_t il_pgrid;        // k_reduce_ilp: persistent grid of the interleaved path (0 = k_reduce_il)
   float div;               // F*T, the mean divisor
 };
 
@@ -86,7 +87,7 @@ enum PlanOpt {
   OPT_WIDE_SPLIT, OPT_NARROW_TPB, OPT_LANE, OPT_LANE3, OPT_LANET, OPT_LANET_PACK, OPT_VEC_IL,
   OPT_VEC_ROW, OPT_ROW_TPB, OPT_ROWT_PACK, OPT_ROWT_SMALL, OPT_WAVET, OPT_UNALIGNED_VEC,
   OPT_KURT_EXACT, OPT_KURT_MID_CPL, OPT_KURT_MID_SMALL, OPT_KURT_LEAF_NARROW, OPT_KURT_LEAF_TILE,
-  OPT_TYPED_VEC, OPT_TYPED_ROWS, OPT_ROW_BPACK, OPT_LANE_BPACK, OPT_WAVE_BPACK, OPT_COL3, OPT_ROWT_NARROW8, OPT_ST_PLAIN, OPT_COUNT
+  OPT_TYPED_VEC, OPT_TYPED_ROWS, OPT_ROW_BPACK, OPT_LANE_BPACK, OPT_WAVE_BPACK, OPT_COL3, OPT_ROWT_NARROW8, OPT_ST_PLAIN, OPT_IL_PERSIST, OPT_COUNT
 };
 int64_t plan_opt(int k);
 inline int64_t opt(int k) { return plan_opt(k); }

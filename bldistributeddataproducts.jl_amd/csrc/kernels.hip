@@ -1034,20 +1034,21 @@ __global__ __launch_bounds__(kBlock) void k_reduce_vec(const RedArgs a) {
 //   kIlInflight  16-byte loads a lane issues per batch (power of two); 4
 //                measured +0.1..0.7% against 8 on 1-, 2- and 8-bank launches
 constexpr int kIlGpw = 2, kIlInflight = 4;
-template <int OP, int K4, int GPW>
-__global__ __launch_bounds__(kBlock) void k_reduce_il(const RedArgs a) {
+// One tile (GPW groups x one (IF, time block) x one bank) of the interleaved
+// path; PERS: called in a loop by k_reduce_ilp, so the LDS is released by a
+// barrier before the next tile.
+template <int OP, int K4, int GPW, int IF, bool PERS>
+__device__ __forceinline__ void il_tile(const RedArgs &a, int64_t bx, uint32_t it, int bank) {
   constexpr int NI = GPW * K4 / 4;           // loads per lane per row
   constexpr int PER = K4 < 4 ? 1 : K4 / 4;   // consecutive loads of one group slot
   constexpr int NS = NI / PER;               // group slots per lane
-  constexpr int IF = kIlInflight;       // loads in flight per lane
   constexpr int RB = NI < IF ? IF / NI : 1;  // rows in flight
   constexpr int JB = NI < IF ? NI : IF;      // loads per batch within a row
   static_assert(NI >= 1 && NI % PER == 0, "k_reduce_il: GPW * K4 must be a multiple of 4");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t it = blockIdx.y, ni = (uint32_t)a.ni;
+  const uint32_t ni = (uint32_t)a.ni;
   const uint32_t to = it / ni, i = it - to * ni;
-  const int bank = blockIdx.z;
-  const int64_t g0 = (int64_t)blockIdx.x * GPW;
+  const int64_t g0 = bx * GPW;
   const int ng = (int)min((int64_t)GPW, a.nco - g0);
   const float id = R<OP>::id();
   float4 acc[NS];
@@ -1109,6 +1110,25 @@ __global__ __launch_bounds__(kBlock) void k_reduce_il(const RedArgs a) {
         if ((4 * q * PER + w) / K4 == tid) s = R<OP>::f(s, red[w][q]);
     st1o(a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + (int64_t)to * a.out_ld_t + g0 + tid,
          finish<OP>(s, a), a.st_plain);
+  }
+  if constexpr (PERS) __syncthreads();
+}
+
+template <int OP, int K4, int GPW>
+__global__ __launch_bounds__(kBlock) void k_reduce_il(const RedArgs a) {
+  il_tile<OP, K4, GPW, kIlInflight, false>(a, blockIdx.x, blockIdx.y, blockIdx.z);
+}
+
+// Plan option "il_persist": N > 0 = the interleaved path as a persistent grid
+// of N workgroups per CU walking the tiles in k_reduce_il's dispatch order,
+// 8 loads in flight per lane (the pure read's best shape: one workgroup per
+// CU, 8 nt loads in flight, 7.35 TB/s on 32 GiB).
+template <int OP, int K4, int GPW>
+__global__ __launch_bounds__(kBlock) void k_reduce_ilp(const RedArgs a) {
+  const int64_t nx = a.blocks_c, ny = a.ni * a.nto, n = a.ntiles;
+  for (int64_t t = blockIdx.x; t < n; t += gridDim.x) {
+    const int64_t r = t / nx;
+    il_tile<OP, K4, GPW, 8, true>(a, t - r * nx, (uint32_t)(r % ny), (int)(r / ny));
   }
 }
 
@@ -1829,6 +1849,17 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
     }
     return hipGetLastError();
   }
+  if (p.path == PATH_VEC_IL && a.il_pgrid > 0) {
+    const dim3 g1((unsigned)a.il_pgrid);
+    switch (a.k4) {
+      case 2: BLDP_LAUNCH((k_reduce_ilp<OP, 2, kIlGpw>), g1, block, 0, s, a); break;
+      case 4: BLDP_LAUNCH((k_reduce_ilp<OP, 4, kIlGpw>), g1, block, 0, s, a); break;
+      case 8: BLDP_LAUNCH((k_reduce_ilp<OP, 8, kIlGpw>), g1, block, 0, s, a); break;
+      case 16: BLDP_LAUNCH((k_reduce_ilp<OP, 16, kIlGpw>), g1, block, 0, s, a); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   if (p.path == PATH_VEC_IL) {
     const dim3 g3((unsigned)a.blocks_c, (unsigned)(a.ni * a.nto), (unsigned)a.nbank);
     switch (a.k4) {
@@ -1929,6 +1960,7 @@ const PlanOptDef kPlanOpts[OPT_COUNT] = {
     {"col3", 1},              // fqavby = 12, short time blocks: k_reduce_col3 (float4 columns)
     {"rowt_narrow8", 1},      // k_reduce_rowt: 8 rows per lane on <= 128-column windows too
     {"st_plain", 1},          // row / il stores: 1 plain below 2 GB of traffic, 0 always nt, 2 always plain
+    {"il_persist", 0},        // N > 0: interleaved path as k_reduce_ilp, N workgroups per CU
 };
 struct PlanOpts {
   std::atomic<int64_t> v[OPT_COUNT];  // -1 = no override
@@ -1963,6 +1995,7 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
   a.rsplit = 1;
   a.bpack = 0;
   a.st_plain = 0;
+  a.il_pgrid = 0;
   const bool t38 = opt(OPT_T38) != 0;
   if (opt(OPT_LANET) && words && a.in_cs == 1 && (T == 1 || T == 2 || T == 4 || (t38 && (T == 3 || T == 8))) &&
       (F == 3 || F == 5 || F == 6 || F == 7 || F == 12) && a.ni <= 65535 && a.nbank <= 65535 &&
@@ -2115,6 +2148,9 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
     a.blocks_c = cdiv(a.nco, kIlGpw);
     a.ntiles = a.blocks_c * a.ni * a.nto * a.nbank;
     p.grid = a.ntiles;
+    const int64_t pers = opt(OPT_IL_PERSIST);
+    if (pers > 0) p.grid = std::min<int64_t>(p.grid, pers * num_cus);
+    a.il_pgrid = pers > 0 ? (int32_t)p.grid : 0;
   }
   // small power-of-two groups, whole time block per tile, no time split:
   // the lean row kernel (3-D grid, so every dimension must fit)

@@ -128,7 +128,8 @@ BLDP_API int bldp_reduce_plan_f32(const float *in, int64_t nchan, int64_t nif, i
  *   "vec_row", "row_tpb", "rowt_pack", "rowt_small", "wavet",
  *   "unaligned_vec", "kurt_exact", "kurt_mid_cpl", "kurt_mid_small",
  *   "kurt_leaf_narrow", "kurt_leaf_tile", "typed_vec", "typed_rows",
- *   "row_bpack", "lane_bpack", "wave_bpack", "col3", "rowt_narrow8", "st_plain"
+ *   "row_bpack", "lane_bpack", "wave_bpack", "col3", "rowt_narrow8", "st_plain",
+ *   "il_persist"
  *                    which kernel a reduce / kurtosis / typed shape takes
  *                    (csrc/kernels.hip kPlanOpts: defaults and meanings).
  * Unknown names: BLDP_EINVAL. */

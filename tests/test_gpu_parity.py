@@ -1271,7 +1271,7 @@ PLAN_OPTION_VALUES = {
     "row_tpb": (0, 1), "rowt_pack": (0, 1), "rowt_small": (0, 64, 100000), "wavet": (0, 1, 2),
     "unaligned_vec": (0, 1, 2, 3), "row_bpack": (0, 1), "lane_bpack": (0, 1),
     "wave_bpack": (0, 1), "col3": (0, 1), "rowt_narrow8": (0, 1),
-    "st_plain": (0, 2),
+    "st_plain": (0, 2), "il_persist": (0, 1, 2),
 }
 # (nchan, nif, ntime, window, F, T): shapes where the options above change the plan
 PLAN_OPTION_SHAPES = [
@@ -1293,6 +1293,9 @@ PLAN_OPTION_SHAPES = [
     (512, 1, 300, [0, 504, 1, 0, 1, 1, 0, 300, 1], 7, 1),
     # narrow rows at fqavby 64 / 128 (row_bpack on the two-bank stitch)
     (512, 1, 4001, None, 64, 1), (512, 1, 1000, None, 128, 2),
+    # interleaved groups with two IFs, a window, an odd group count (the last
+    # segment half full) and time blocks shorter than the rows in flight
+    (8192, 2, 40, [256, 7680, 1, 0, 2, 1, 0, 40, 1], 512, 5),
 ]
 
 

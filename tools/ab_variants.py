@@ -64,6 +64,8 @@ VARIANTS = {
     "rowt8o": {"opts": {"rowt_small": 100000}},  # k_reduce_rowt: always 8 rows per lane
     "rowtn16": {"opts": {"rowt_narrow8": 0}},  # narrow windows back on 16 rows per lane
     "stnt": {"opts": {"st_plain": 0}},  # row / il output stores always non-temporal
+    "ilp1": {"opts": {"il_persist": 1}},  # interleaved path persistent, 1 workgroup per CU
+    "ilp2": {"opts": {"il_persist": 2}},
     # k_reduce_rows with a register budget for 6 / 8 resident waves per SIMD
     "rowsw6": {"patch": [("kernels.hip", "template <int OP, int G4, int S>\n__global__ __launch_bounds__(kBlock)\n"
                           "__attribute__((amdgpu_waves_per_eu(1, kRowMaxWaves)))",
