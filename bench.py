@@ -62,6 +62,26 @@ def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
+COLD_BYTES = 1 << 30  # > 4x the 256 MB Infinity Cache (MI355X_MICROARCH.md)
+
+
+def cold_copies(mode, launch_bytes):
+    """Distinct copies of a launch's input the steps rotate over: 1 (warm, or
+    a launch too big for any cache), else enough for >= COLD_BYTES."""
+    if mode == "warm" or (mode == "auto" and launch_bytes >= COLD_BYTES) or launch_bytes <= 0:
+        return 1
+    return max(2, min(64, -(-COLD_BYTES // launch_bytes)))
+
+
+def cache_note(ncopy, launch_bytes):
+    if ncopy == 1:
+        return ("one copy: every launch re-reads the same buffer" +
+                (" (larger than any cache: HBM-bound)" if launch_bytes >= COLD_BYTES else
+                 " (warm: the Infinity Cache may hold part of it)"))
+    return (f"cold: launches rotate over {ncopy} copies of the input "
+            f"({ncopy * launch_bytes / 2**20:.0f} MiB), none in cache from the launch before")
+
+
 def traffic_from_profile(cfg_name, n_local_banks, with_source=False):
     """HBM bytes per launch from the committed PMC profile (profiles/), or None.
     with_source: (bytes, where they come from) — a committed counter session,
@@ -169,24 +189,33 @@ def bench_kurtosis(args, cfg, eng, torch):
     win = None
     if cfg["tw"] != cfg["ntime"]:
         win = [0, cfg["nchan"], 1, 0, cfg["nif"], 1, 0, cfg["tw"], 1]
-    dst = eng.band_empty(cfg["nbank"], cfg["nchan"], cfg["nif"], cfg["ntime"])
-    banks = [eng.synth(cfg["nchan"], cfg["nif"], cfg["ntime"], cfg["nfpc"],
-                       seed=10 * b + cfg["product"], kind=0, out=o) for b, o in enumerate(dst)]
+    n = cfg["nbank"] * cfg["nchan"] * cfg["nif"] * cfg["tw"]
+    ncopy = cold_copies(args.cache, 4 * n)  # (cold: calls rotate over copies, >= 1 GiB)
+    copies = []
+    for _ in range(ncopy):
+        dst = eng.band_empty(cfg["nbank"], cfg["nchan"], cfg["nif"], cfg["ntime"])
+        copies.append([eng.synth(cfg["nchan"], cfg["nif"], cfg["ntime"], cfg["nfpc"],
+                                 seed=10 * b + cfg["product"], kind=0, out=o)
+                       for b, o in enumerate(dst)])
+    banks = copies[0]
     plan = eng.kurtosis_plan(banks[0], win)
     stream = torch.cuda.current_stream()
-    for _ in range(args.warmup):
-        eng.band_kurtosis(banks, win)
+    for w in range(max(args.warmup, ncopy)):
+        eng.band_kurtosis(copies[w % ncopy], win)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    e0.record(stream)
-    for _ in range(args.steps):
-        eng.band_kurtosis(banks, win)  # every bank in one set of launches
-    e1.record(stream)
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    ms = e0.elapsed_time(e1) / args.steps
-    n = cfg["nbank"] * cfg["nchan"] * cfg["nif"] * cfg["tw"]
+
+    def timed(rot):
+        t0 = time.perf_counter()
+        e0.record(stream)
+        for k in range(args.steps):
+            eng.band_kurtosis(copies[k % rot], win)  # every bank in one set of launches
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, e0.elapsed_time(e1) / args.steps
+
+    el, ms = timed(ncopy)
+    warm_ms = timed(1)[1] if ncopy > 1 else ms
     nout = cfg["nbank"] * cfg["nchan"] * cfg["nif"]
     path = plan["path"]
     reads = 2 if path == "twopass" else 1
@@ -213,7 +242,11 @@ def bench_kurtosis(args, cfg, eng, torch):
                          "traffic": traffic_from_profile("kurt_" + args.config, cfg["nbank"]),
                          "traffic_source": traffic_from_profile("kurt_" + args.config,
                                                                 cfg["nbank"], True)[1],
-                         "kernel": kern, "call_ms": round(ms, 4), "bytes_per_call": algo}}
+                         "kernel": kern, "call_ms": round(ms, 4), "bytes_per_call": algo,
+                         "cache": cache_note(ncopy, 4 * n),
+                         "warm": None if ncopy == 1 else {
+                             "call_ms": round(warm_ms, 4),
+                             "frac": round(algo / warm_ms / 1e6 / HBM_PEAK_GBS, 4)}}}
 
 
 CFG5_PRODUCTS = ["cfg3", "cfg4", "cfg1"]  # 0000, 0001, 0002 single-bank geometry
@@ -509,7 +542,12 @@ def spawn_ranks(n: int) -> int:
     this same command (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, one GPU
     each) and wait for them.  Runs before anything imports torch or touches
     HIP in this process, and starts children instead of re-exec'ing; rank 0
-    prints the JSON line.  Returns the exit status (the first failing rank's)."""
+    prints the JSON line.  Returns the exit status: 0, or the first failing
+    rank's.  The ranks are polled, not waited on in order: when one exits
+    non-zero (e.g. before the rendezvous or the RCCL communicator, where its
+    peers would block until the process-group timeout) the others are sent
+    SIGTERM, then SIGKILL after a grace period, and its status is returned."""
+    import signal
     import subprocess
 
     port = str(free_port())
@@ -519,8 +557,30 @@ def spawn_ranks(n: int) -> int:
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
                                       env=env))
-    rcs = [p.wait() for p in procs]
-    return next((rc for rc in rcs if rc), 0)
+    failed = 0
+    try:
+        while True:
+            rcs = [p.poll() for p in procs]
+            failed = next((rc for rc in rcs if rc), 0)
+            if failed or all(rc is not None for rc in rcs):
+                break
+            time.sleep(0.05)
+    except KeyboardInterrupt:
+        failed = 128 + signal.SIGINT
+    if failed:
+        log(f"a rank exited with status {failed}: stopping the others")
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        deadline = time.time() + 10.0
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, deadline - time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    # a signal-killed rank reports -SIG: exit with 128 + SIG like a shell
+    return failed if failed >= 0 else 128 - failed
 
 
 def rendezvous_check(args, dist, rank, world):
@@ -562,20 +622,31 @@ def bench_typed(args, eng, torch, pkg):
     out = {}
     for label, nb in (("0002 file", 1), ("0002 band", 8)):
         a = rng.integers(0, 256, (279, 1, 65536 * nb), dtype=np.uint8)  # C order [t][i][c]
-        x = torch.from_numpy(a).cuda().permute(2, 1, 0)  # Julia-order (65536*nb, 1, 279)
-        for _ in range(args.warmup):
-            eng.reduce(x, 64, 1, "sum")
+        ncopy = cold_copies(args.cache, a.nbytes)  # cold: calls rotate over >= 1 GiB of copies
+        xs = [torch.from_numpy(a).cuda().permute(2, 1, 0)  # Julia-order (65536*nb, 1, 279)
+              for _ in range(ncopy)]
+        outs = [eng.fb_empty(65536 * nb // 64, 1, 279, dtype=torch.uint64) for _ in range(ncopy)]
+        x = xs[0]
+        for w in range(max(args.warmup, ncopy)):
+            eng.reduce(xs[w % ncopy], 64, 1, "sum", out=outs[w % ncopy])
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(args.steps):
-            eng.reduce(x, 64, 1, "sum")
-        e1.record()
-        e1.synchronize()
-        ms = e0.elapsed_time(e1) / args.steps
+
+        def timed(rot):
+            e0.record()
+            for k in range(args.steps):
+                eng.reduce(xs[k % rot], 64, 1, "sum", out=outs[k % rot])
+            e1.record()
+            e1.synchronize()
+            return e0.elapsed_time(e1) / args.steps
+
+        ms = timed(ncopy)
+        warm_ms = timed(1) if ncopy > 1 else ms
         nbytes = a.nbytes + 8 * (65536 * nb // 64) * 279
         out[label] = {"ms_per_call": round(ms, 4), "GBps_in_plus_out": round(nbytes / ms / 1e6, 1),
-                      "input_bytes": int(a.nbytes)}
+                      "input_bytes": int(a.nbytes), "cache": cache_note(ncopy, a.nbytes),
+                      "warm_ms_per_call": round(warm_ms, 4),
+                      "warm_GBps_in_plus_out": round(nbytes / warm_ms / 1e6, 1)}
         # getkurtosis on the same UInt8 data (Float64 StatsBase per channel row)
         for _ in range(2):
             eng.kurtosis(x)
@@ -629,6 +700,10 @@ def main():
                          "RCCL gather + stitch of every step) to exercise it on one GPU")
     ap.add_argument("--settle-ms", type=float, default=100.0,
                     help="untimed launches for this long before the warmup steps (GPU clocks)")
+    ap.add_argument("--cache", default="auto", choices=["auto", "cold", "warm"],
+                    help="cold: rotate launches over copies of the input totalling >= 1 GiB "
+                         "(auto: when a launch reads < 1 GiB); warm figures are reported "
+                         "beside the cold ones")
     ap.add_argument("--plan-option", action="append", default=[], metavar="NAME=VALUE",
                     help="override a planner choice (bldp_plan_option; A/B runs only)")
     args = ap.parse_args()
@@ -645,6 +720,12 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     if args.mode == "rendezvous":
+        # BENCH_RENDEZVOUS_FAIL_RANK=r: rank r exits with status 3 before the
+        # rendezvous, as a rank that dies before init_process_group does (the
+        # fail-fast test of spawn_ranks; rendezvous mode only)
+        if os.environ.get("BENCH_RENDEZVOUS_FAIL_RANK") == str(rank):
+            log(f"rank {rank}: injected failure before the rendezvous")
+            sys.exit(3)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", str(free_port()))
         os.environ.setdefault("RANK", "0")
@@ -711,20 +792,32 @@ def main():
     if cfg["tw"] != cfg["ntime"]:
         win = [0, cfg["nchan"], 1, 0, cfg["nif"], 1, 0, cfg["tw"], 1]  # idxs=(:, :, 1:tw)
 
-    log(f"rank {rank}/{world}: generating banks {mine} of {args.config} on device")
-    # the rank's banks: views of one HBM slab (engine.band_empty), or separate
-    # allocations (--band-alloc per-bank, 2.4% slower on MI355X)
-    dst = eng.band_empty(len(mine), cfg["nchan"], cfg["nif"], cfg["ntime"]) \
-        if args.band_alloc == "slab" else [None] * len(mine)
-    banks = [eng.synth(cfg["nchan"], cfg["nif"], cfg["ntime"], cfg["nfpc"],
-                       seed=10 * b + cfg["product"], kind=0, out=o) for b, o in zip(mine, dst)]
-    del dst  # the banks keep the slab alive (freed before the CPU baseline)
-    torch.cuda.synchronize()
     nco, ni, nto = cfg["nchan"] // cfg["F"], cfg["nif"], cfg["tw"] // cfg["T"]
     read_b = 4 * cfg["nchan"] * cfg["nif"] * cfg["tw"]
     write_b = 4 * nco * ni * nto
     bytes_step = nb * (read_b + write_b)          # whole band (all ranks)
     bytes_launch = len(mine) * (read_b + write_b)  # this rank's single reduce launch
+    # --cache cold (auto: launches below 1 GiB): the steps rotate over `ncopy`
+    # distinct copies of the rank's banks, >= 1 GiB in all, so no launch finds
+    # its input in the 256 MB Infinity Cache the previous launches filled (a
+    # 71 MB cfg1 window re-read launch after launch mostly would: its pure
+    # read passes 8 TB/s); warm figures beside them
+    ncopy = cold_copies(args.cache, bytes_launch)
+
+    log(f"rank {rank}/{world}: generating banks {mine} of {args.config} on device"
+        + (f" ({ncopy} copies, cold cache)" if ncopy > 1 else ""))
+    # the rank's banks: views of one HBM slab (engine.band_empty), or separate
+    # allocations (--band-alloc per-bank, 2.4% slower on MI355X)
+    copies = []
+    for _ in range(ncopy):
+        dst = eng.band_empty(len(mine), cfg["nchan"], cfg["nif"], cfg["ntime"]) \
+            if args.band_alloc == "slab" else [None] * len(mine)
+        copies.append([eng.synth(cfg["nchan"], cfg["nif"], cfg["ntime"], cfg["nfpc"],
+                                 seed=10 * b + cfg["product"], kind=0, out=o)
+                       for b, o in zip(mine, dst)])
+        del dst  # the banks keep the slab alive (freed before the CPU baseline)
+    banks = copies[0]
+    torch.cuda.synchronize()
     stream = torch.cuda.current_stream()
     # this rank's slice of the band; N > 1: two slots, the RCCL gather of step
     # k (to rank 0, over xGMI) overlaps the reduce of step k+1
@@ -743,13 +836,13 @@ def main():
     sp = int(stream.cuda_stream)
     preps = {}
 
-    def step(ev0=None, ev1=None):
+    def step(ev0=None, ev1=None, copy=0):
         slot = pipe.begin() if pipe else 0
-        prep = preps.get(slot)
+        prep = preps.get((copy, slot))
         if prep is None:
             dst = pipe.local(slot) if pipe else out
-            prep = preps[slot] = eng.PreparedBandReduce(banks, cfg["F"], cfg["T"], "sum", win,
-                                                        out=dst)
+            prep = preps[copy, slot] = eng.PreparedBandReduce(copies[copy], cfg["F"], cfg["T"],
+                                                              "sum", win, out=dst)
         if ev0 is not None:  # the events ride on the kernel dispatch itself
             prep.launch_timed(sp, ev0, ev1)
         else:
@@ -773,8 +866,8 @@ def main():
             torch.cuda.synchronize()
         sprep.close()
         del sprep
-    for _ in range(args.warmup):
-        step()
+    for w in range(max(args.warmup, ncopy)):
+        step(copy=w % ncopy)
     if pipe:
         pipe.drain()
     torch.cuda.synchronize()
@@ -796,14 +889,15 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(K):
+        c = k % ncopy
         if K == 1:
-            step(sp0, sp1)
+            step(sp0, sp1, copy=c)
         elif k == 0:
-            step(sp0, sx1)
+            step(sp0, sx1, copy=c)
         elif k == K - 1:
-            step(sx0, sp1)
+            step(sx0, sp1, copy=c)
         else:
-            step()
+            step(copy=c)
     host_ms = (time.perf_counter() - t0) * 1e3 / K  # enqueue cost per step
     if pipe:
         pipe.drain()
@@ -813,16 +907,24 @@ def main():
     el = time.perf_counter() - t0
     span_ms = sp0.elapsed_time(sp1) / K  # first kernel's start to last one's end, per launch
     for k in range(K):  # the kernel pass
-        step(*evs[k])
+        step(*evs[k], copy=(K + k) % ncopy)
     if pipe:
         pipe.drain()
     torch.cuda.synchronize()
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / K
+    warm_ms = kern_ms
+    if ncopy > 1:  # the same K launches on one copy: the warm (cache-resident) figure
+        for k in range(K):
+            step(*evs[k], copy=0)
+        if pipe:
+            pipe.drain()
+        torch.cuda.synchronize()
+        warm_ms = sum(a.elapsed_time(b) for a, b in evs) / K
     if world > 1:
-        t = torch.tensor([el, kern_ms, span_ms], dtype=torch.float64,
+        t = torch.tensor([el, kern_ms, span_ms, warm_ms], dtype=torch.float64,
                          device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el, kern_ms, span_ms = float(t[0]), float(t[1]), float(t[2])
+        el, kern_ms, span_ms, warm_ms = float(t[0]), float(t[1]), float(t[2]), float(t[3])
     ms_step = el * 1e3 / args.steps
     path = eng.plan(banks[0], cfg["F"], cfg["T"], "sum", win)["path"] if banks else None
     kernel_name = {"interleaved": "k_reduce_il", "vector": "k_reduce_vec",
@@ -848,18 +950,21 @@ def main():
     result = None
     if rank == 0:
         # this box's pure-read rate for a buffer of the launch's bytes
-        # (bldp_read_probe, the pure read of tools/mix_ceiling.hip): HBM rates
+        # (tools/hbm_probe.hip, the pure read of tools/mix_ceiling.hip): HBM rates
         # differ box to box by several percent, so the reduce is also set
         # beside what a kernel that only reads reaches on the same GPU
         probe = None
         if not args.no_read_probe:
             preps.clear()
             torch.cuda.empty_cache()
-            probe = eng.read_probe(bytes_launch, stream=stream)
+            sys.path.insert(0, os.path.join(REPO, "tools"))
+            import hbm_probe
+
+            probe = hbm_probe.read_probe(bytes_launch, stream=stream, pkg=pkg, copies=ncopy)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             preps.clear()  # (they hold the banks)
-            del banks
+            del banks, copies
             torch.cuda.empty_cache()
             log("cpu baseline (oracle port) ...")
             cpu = cpu_baseline(cfg, args.cpu_seconds, eng, torch)
@@ -885,7 +990,15 @@ def main():
                          "span_ms_per_launch": round(span_ms, 4),
                          "bytes_per_launch": bytes_launch,
                          "box_read_probe": probe,
-                         "frac_of_box_read": probe and round(achieved / probe["GBps"], 4)},
+                         "frac_of_box_read": probe and round(achieved / probe["GBps"], 4),
+                         "cache": cache_note(ncopy, bytes_launch),
+                         "warm": None if ncopy == 1 else {
+                             "kernel_ms": round(warm_ms, 4),
+                             "achieved": round(bytes_launch / (warm_ms * 1e-3) / 1e9, 1),
+                             "frac": round(bytes_launch / (warm_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                           4),
+                             "note": "the same launches on one copy, its input left in the "
+                                     "Infinity Cache by the launch before"}},
             "host_enqueue_ms_per_step": round(host_ms, 4),
             "settle_launches": settle,
             "cpu_baseline": cpu,

@@ -21,7 +21,8 @@ KURT_PATHS = {0: "regs", 1: "mid", 2: "leaf", 3: "twopass"}
 
 BLDP_OK, BLDP_EINVAL, BLDP_EDIM, BLDP_EHIP, BLDP_ENOMEM, BLDP_EBOUNDS = 0, -1, -2, -3, -5, -6
 BLDP_ECOMM, BLDP_EIO = -7, -8
-ABI_VERSION = 3
+ABI_VERSION = 4
+BLDP_BAND_STAGED = 1
 BLDP_COMM_ID_BYTES = 128
 
 
@@ -73,7 +74,10 @@ SIGNATURES = {
     "bldp_reduce_launch": ([P, P], I),
     "bldp_reduce_launch_timed": ([P, P, P, P], I),
     "bldp_reduce_release": ([P], I),
-    "bldp_band_reduce_multi_f32": ([I, P, P, I64, I64, I64, P, I64, I64, I, I, P], I),
+    "bldp_band_reduce_multi_f32": ([I, P, P, I64, I64, I64, P, I64, I64, I, I, P, ctypes.c_uint],
+                                   I),
+    "bldp_peer_access": ([I, I, P], I),
+    "bldp_device_to_host": ([P, P, I64, P, P, P], I),
     "bldp_stitch_f32": ([I, P, I64, I64, I64, P, P], I),
     "bldp_despike_f32": ([P, I64, I64, I64, I64, P], I),
     "bldp_kurtosis_workspace_size": ([I64, I64, I64, P], SZ),
@@ -83,7 +87,6 @@ SIGNATURES = {
     "bldp_band_kurtosis_f32": ([I, P, I64, I64, I64, P, P, P], I),
     "bldp_fqav_range": ([D, D, I64, I64, P, P, P], I),
     "bldp_synth_f32": ([P, I64, I64, I64, I64, U64, I, P], I),
-    "bldp_read_probe": ([P, I64, I, P, P, P], I),
     "bldp_reduce_out_dtype": ([I, I], I),
     "bldp_reduce_strided": ([I, P, I64, I64, I64, P, I64, I64, I, P, I64, I64, P], I),
     "bldp_kurtosis": ([I, P, I64, I64, I64, P, P, P], I),
@@ -140,7 +143,8 @@ def lib():
 class plan_option:
     """Context manager forcing a plan option (bldp_plan_option) and restoring
     it: ``with plan_option("row_split", 4): ...``; value -1 = the planner's
-    choice."""
+    choice.  A/B and TEST facility only: the option is process-wide (every
+    thread's plans see it), so no product code path uses this."""
 
     def __init__(self, name: str, value: int):
         self.name, self.value = name, int(value)

@@ -384,6 +384,13 @@ int bldp_plan_option(const char *name, int64_t value, int64_t *previous) {
   if (!name) return fail(BLDP_EINVAL, "null option name");
   const int k = plan_opt_index(name);
   if (k < 0) return fail(BLDP_EINVAL, "unknown plan option '%s'", name);
+  if (!plan_opt_valid(k, value)) {
+    int64_t lo, hi;
+    plan_opt_domain(k, &lo, &hi);
+    return fail(BLDP_EINVAL, "plan option '%s' takes %s%lld..%lld or -1 (the default), not %lld",
+                name, k == OPT_ROW_SPLIT ? "1, 2 or 4 in " : "", (long long)lo, (long long)hi,
+                (long long)value);
+  }
   if (previous) *previous = plan_opt_override(k);
   plan_opt_set(k, value < 0 ? -1 : value);
   return BLDP_OK;
@@ -504,11 +511,39 @@ int bldp_reduce_release(bldp_reduce_op_t h) {
   return BLDP_OK;
 }
 
+int bldp_peer_access(int dev, int peer, int *direct) {
+  if (!direct) return fail(BLDP_EINVAL, "null pointer");
+  *direct = 0;
+  int ndev = 0;
+  HIPCHK(hipGetDeviceCount(&ndev));
+  if (dev < 0 || dev >= ndev || peer < 0 || peer >= ndev)
+    return fail(BLDP_EINVAL, "device %d / peer %d not available (%d visible)", dev, peer, ndev);
+  if (dev == peer) {
+    *direct = 1;
+    return BLDP_OK;
+  }
+  int can = 0;
+  if (hipDeviceCanAccessPeer(&can, dev, peer) != hipSuccess || !can) {
+    (void)hipGetLastError();
+    return BLDP_OK;
+  }
+  int prev = 0;
+  HIPCHK(hipGetDevice(&prev));
+  HIPCHK(hipSetDevice(dev));
+  const hipError_t pe = hipDeviceEnablePeerAccess(peer, 0);
+  (void)hipGetLastError();
+  (void)hipSetDevice(prev);
+  *direct = pe == hipSuccess || pe == hipErrorPeerAccessAlreadyEnabled;
+  return BLDP_OK;
+}
+
 int bldp_band_reduce_multi_f32(int nbank, const int *bank_dev, const float *const *in,
                                int64_t nchan, int64_t nif, int64_t ntime, const int64_t *win,
-                               int64_t fqavby, int64_t tavby, int op, int root, float *out) {
+                               int64_t fqavby, int64_t tavby, int op, int root, float *out,
+                               unsigned flags) {
   if (nbank < 1 || nbank > BLDP_MAX_BANKS || !bank_dev || !in)
     return fail(BLDP_EINVAL, "bad bank arguments");
+  if (flags & ~BLDP_BAND_STAGED) return fail(BLDP_EINVAL, "unknown flags 0x%x", flags);
   int ndev = 0;
   HIPCHK(hipGetDeviceCount(&ndev));
   if (root < 0 || root >= ndev) return fail(BLDP_EINVAL, "root device %d not available", root);
@@ -522,10 +557,9 @@ int bldp_band_reduce_multi_f32(int nbank, const int *bank_dev, const float *cons
   if (nco * ni * nto == 0) return BLDP_OK;
   if (!out) return fail(BLDP_EINVAL, "null output pointer");
   const int64_t ld_i = (int64_t)nbank * nco, ld_t = ld_i * ni;
-  // BLDP_FORCE_STAGED=1 or plan option "force_staged" = 1 (tests): every bank takes the staged branch (local
-  // reduce + strided copy into the root's slot), even on the root device
-  const char *fs = std::getenv("BLDP_FORCE_STAGED");
-  const bool force_staged = (fs && fs[0] == '1') || plan_opt(OPT_FORCE_STAGED) == 1;
+  // BLDP_BAND_STAGED: every bank takes the staged branch (local reduce +
+  // strided copy into the root's slot), even on the root device
+  const bool force_staged = (flags & BLDP_BAND_STAGED) != 0;
   int prev = 0;
   HIPCHK(hipGetDevice(&prev));
   std::vector<hipStream_t> streams(ndev, nullptr);
@@ -837,17 +871,6 @@ int bldp_unchunk_f32(const float *packed, const int64_t chunk[3], const int64_t 
   if (!packed || !out) return fail(BLDP_EINVAL, "null pointer");
   hipError_t e = launch_unchunk(packed, u, out, (hipStream_t)stream);
   if (e != hipSuccess) return fail(BLDP_EHIP, "unchunk launch: %s", hipGetErrorString(e));
-  return BLDP_OK;
-}
-
-int bldp_read_probe(const void *dev, int64_t bytes, int form, void *stream, void *ev_start,
-                    void *ev_stop) {
-  if (bytes < 0 || form < 0 || form >= 2048) return fail(BLDP_EINVAL, "bad size or form");
-  if (bytes >= 16 && (!dev || (uintptr_t)dev % 16)) return fail(BLDP_EINVAL, "null or unaligned buffer");
-  hipError_t e = launch_read_probe(static_cast<const float *>(dev), bytes, form,
-                                   num_cus_current(), (hipStream_t)stream, (hipEvent_t)ev_start,
-                                   (hipEvent_t)ev_stop);
-  if (e != hipSuccess) return fail(BLDP_EHIP, "read probe launch: %s", hipGetErrorString(e));
   return BLDP_OK;
 }
 

@@ -72,7 +72,6 @@ struct RedArgs {
                            // lane path: k_reduce_lanes (lanes along the stitched row)
   int32_t rsplit;          // k_reduce_rows: slices of a workgroup splitting a block's rows (1 = k_reduce_row)
   int32_t st_plain;        // row / il / rowt output stores plain (1) or non-temporal (0)
-  int32_t il_pgrid;        // k_reduce_ilp: persistent grid of the interleaved path (0 = k_reduce_il)
   float div;               // F*T, the mean divisor
 };
 
@@ -83,17 +82,19 @@ struct RedArgs {
 // decides by shape" where an option has that setting (row_split).
 // Names and defaults: kernels.hip kPlanOpts.
 enum PlanOpt {
-  OPT_ROW_SPLIT = 0, OPT_FORCE_STAGED, OPT_MAX_WG_PER_CU, OPT_TS_FILL, OPT_NARROW_MIS, OPT_T38,
+  OPT_ROW_SPLIT = 0, OPT_TS_FILL, OPT_NARROW_MIS, OPT_T38,
   OPT_WIDE_SPLIT, OPT_NARROW_TPB, OPT_LANE, OPT_LANE3, OPT_LANET, OPT_LANET_PACK, OPT_VEC_IL,
   OPT_VEC_ROW, OPT_ROW_TPB, OPT_ROWT_PACK, OPT_ROWT_SMALL, OPT_WAVET, OPT_UNALIGNED_VEC,
   OPT_KURT_EXACT, OPT_KURT_MID_CPL, OPT_KURT_MID_SMALL, OPT_KURT_LEAF_NARROW, OPT_KURT_LEAF_TILE,
-  OPT_TYPED_VEC, OPT_TYPED_ROWS, OPT_ROW_BPACK, OPT_LANE_BPACK, OPT_WAVE_BPACK, OPT_COL3, OPT_ROWT_NARROW8, OPT_ST_PLAIN, OPT_IL_PERSIST, OPT_COUNT
+  OPT_TYPED_VEC, OPT_TYPED_ROWS, OPT_ROW_BPACK, OPT_LANE_BPACK, OPT_WAVE_BPACK, OPT_COL3, OPT_ROWT_NARROW8, OPT_ST_PLAIN, OPT_COUNT
 };
 int64_t plan_opt(int k);
 inline int64_t opt(int k) { return plan_opt(k); }
 // name -> option index, or -1
 int plan_opt_index(const char *name);
 int64_t plan_opt_override(int k);  // -1 = none
+bool plan_opt_valid(int k, int64_t v);  // v in the option's domain (or < 0: the default)
+void plan_opt_domain(int k, int64_t *lo, int64_t *hi);
 void plan_opt_set(int k, int64_t v);
 
 enum Path { PATH_VEC = 0, PATH_NARROW = 1, PATH_SCALAR = 2, PATH_TILE = 3, PATH_VEC_IL = 4,
@@ -189,8 +190,6 @@ int typed_out_dtype(int dtype, int op);    // -1 = invalid
 hipError_t launch_reduce_typed(const TypedArgs &a, int op, hipStream_t s);
 hipError_t launch_kurtosis_typed(const TypedArgs &a, double *out, hipStream_t s);
 
-hipError_t launch_read_probe(const float *in, int64_t bytes, int form, int num_cus,
-                             hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
 hipError_t launch_synth(float *out, int64_t nchan, int64_t nif, int64_t ntime, int64_t nfpc,
                         uint64_t seed, int kind, hipStream_t s);
 

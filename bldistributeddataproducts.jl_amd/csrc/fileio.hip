@@ -43,10 +43,16 @@ struct Piece {
 // Pieces land at host + hoff, or, with a slot ring, in slot (batch % nslot)
 // at hoff - batch * slot_bytes; then only batches below `open` may be read
 // (their slot's previous copy is done).
+//
+// Copy-out jobs (bldp_device_to_host) use the same pieces the other way
+// round: `copy_src` is the slot ring, a piece of batch b is a memcpy from
+// slot b % nslot to host + hoff, and `open` counts the batches whose DMA into
+// their slot has landed.
 struct Job {
   int fd = -1;
   uint8_t *host = nullptr;
   const std::vector<void *> *slot_base = nullptr;
+  const std::vector<void *> *copy_src = nullptr;
   int64_t slot_bytes = 0;
   std::vector<Piece> pieces;
   std::unique_ptr<std::atomic<int64_t>[]> left;
@@ -116,6 +122,23 @@ class ReadPool {
       const int64_t i = j->next.fetch_add(1);
       if (i >= n) return;
       const Piece &p = j->pieces[i];
+      if (j->copy_src) {  // copy-out: slot -> caller memory once the batch's DMA landed
+        if (p.batch >= j->open.load()) {
+          std::unique_lock<std::mutex> lk(j->mu);
+          j->gate.wait(lk, [&] { return p.batch < j->open.load() || j->err.load(); });
+        }
+        if (!j->err.load(std::memory_order_relaxed)) {
+          const std::vector<void *> &sl = *j->copy_src;
+          std::memcpy(j->host + p.hoff,
+                      (const uint8_t *)sl[p.batch % sl.size()] + (p.hoff - p.batch * j->slot_bytes),
+                      (size_t)p.len);
+        }
+        if (j->left[p.batch].fetch_sub(1) == 1 || j->err.load()) {
+          std::lock_guard<std::mutex> lk(j->mu);
+          j->cv.notify_all();
+        }
+        continue;
+      }
       uint8_t *dst = j->host + p.hoff;
       if (j->slot_base) {
         if (p.batch >= j->open.load()) {  // wait for the slot
@@ -575,6 +598,123 @@ extern "C" BLDP_API int bldp_file_runs_to_device(int64_t nrun, const int *fd,
     return bldp::set_error(BLDP_ENOMEM, "runs_to_device: out of host memory");
   } catch (...) {
     return bldp::set_error(BLDP_EINVAL, "runs_to_device: unexpected C++ exception");
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Device -> pageable host memory through the same pinned slot ring: the DMA
+// of batch b + 1 runs while the reader threads copy batch b out of its slot.
+// (GBT.getband's one device -> host copy of the stitched band, src/gbt.jl:103:
+// the product lands in ordinary memory the caller owns, and no pinned memory
+// is allocated or held per call.)
+namespace {
+constexpr int64_t kD2hSlotBytes = 32ll << 20;
+constexpr int kD2hSlots = 8;
+}  // namespace
+
+static int device_to_host(const void *src, void *dst, int64_t bytes, void *copy_stream,
+                          void *stream, double *stats) {
+  const auto t0 = std::chrono::steady_clock::now();
+  if (bytes < 0 || (bytes > 0 && (!src || !dst)))
+    return bldp::set_error(BLDP_EINVAL, "device_to_host: bad argument");
+  if (bytes == 0) return BLDP_OK;
+  std::unique_lock<std::mutex> call;
+  const std::shared_ptr<DevIO> io = dev_io(call);
+  // the ring the file readers left (any slot size), else the default one
+  int rc = io->slots.p.size() >= 2 ? BLDP_OK : ensure_slots(io->slots, kD2hSlotBytes, kD2hSlots);
+  if (rc) return rc;
+  const int64_t sb = io->slots.bytes, nslot = (int64_t)io->slots.p.size();
+  const int64_t nbatch = (bytes + sb - 1) / sb;
+  const int64_t piece = std::max<int64_t>(256 << 10, sb / 8);
+  Job j;
+  j.host = (uint8_t *)dst;
+  j.copy_src = &io->slots.p;
+  j.slot_bytes = sb;
+  j.open.store(0);
+  j.left.reset(new std::atomic<int64_t>[nbatch]);
+  for (int64_t b = 0; b < nbatch; ++b) {
+    const int64_t lo = b * sb, n = std::min(sb, bytes - lo);
+    int64_t cnt = 0;
+    for (int64_t x = 0; x < n; x += piece, ++cnt)
+      j.pieces.push_back({0, lo + x, std::min(piece, n - x), (int32_t)b, -1});
+    j.left[b].store(cnt);
+  }
+  hipStream_t cs = (hipStream_t)copy_stream, s = (hipStream_t)stream;
+  hipEvent_t after = nullptr;  // the producer's work queued so far on `stream`
+  std::vector<hipEvent_t> evs(nbatch, nullptr);
+  if (hipEventCreateWithFlags(&after, hipEventDisableTiming) != hipSuccess ||
+      hipEventRecord(after, s) != hipSuccess || hipStreamWaitEvent(cs, after, 0) != hipSuccess) {
+    if (after) (void)hipEventDestroy(after);
+    return bldp::set_error(BLDP_EHIP, "device_to_host: stream ordering failed");
+  }
+  ReadPool *rp = io->pool.get();
+  double t_first = -1.0;
+  {
+    PostedJob posted(rp, &j);
+    auto land = [&](int64_t b) -> bool {  // batch b's DMA done: open it for copy-out
+      if (hipEventSynchronize(evs[b]) != hipSuccess) return false;
+      {
+        std::lock_guard<std::mutex> lk(j.mu);
+        j.open.store(b + 1);
+      }
+      j.gate.notify_all();
+      return true;
+    };
+    for (int64_t b = 0; b < nbatch && rc == BLDP_OK; ++b) {
+      if (b >= nslot) {  // slot b % nslot: batch b - nslot copied out of it
+        std::unique_lock<std::mutex> lk(j.mu);
+        j.cv.wait(lk, [&] { return j.left[b - nslot].load() == 0 || j.err.load(); });
+      }
+      const int64_t lo = b * sb, n = std::min(sb, bytes - lo);
+      if (hipEventCreateWithFlags(&evs[b], hipEventDisableTiming) != hipSuccess ||
+          hipMemcpyAsync(io->slots.p[b % nslot], (const uint8_t *)src + lo, (size_t)n,
+                         hipMemcpyDeviceToHost, cs) != hipSuccess ||
+          hipEventRecord(evs[b], cs) != hipSuccess) {
+        rc = bldp::set_error(BLDP_EHIP, "device_to_host: copy of batch %lld failed", (long long)b);
+        break;
+      }
+      if (t_first < 0) t_first = ms_since(t0);
+      if (b >= 1 && !land(b - 1))
+        rc = bldp::set_error(BLDP_EHIP, "device_to_host: copy of batch %lld failed",
+                             (long long)(b - 1));
+    }
+    if (rc == BLDP_OK && !land(nbatch - 1))
+      rc = bldp::set_error(BLDP_EHIP, "device_to_host: copy of the last batch failed");
+    if (rc == BLDP_OK) {
+      ReadPool::run(&j);  // help with the last pieces, then wait for every one
+      std::unique_lock<std::mutex> lk(j.mu);
+      j.cv.wait(lk, [&] {
+        for (int64_t b = 0; b < nbatch; ++b)
+          if (j.left[b].load()) return false;
+        return true;
+      });
+    }
+    posted.finish(rc != BLDP_OK);
+  }
+  // no DMA into the slots may outlive the call (the next call reuses them)
+  for (hipEvent_t ev : evs)
+    if (ev) {
+      (void)hipEventSynchronize(ev);
+      (void)hipEventDestroy(ev);
+    }
+  (void)hipEventDestroy(after);
+  if (stats) {
+    stats[0] = t_first;
+    stats[1] = ms_since(t0);
+    stats[2] = (double)nbatch;
+    stats[3] = (double)rp->threads();
+  }
+  return rc;
+}
+
+extern "C" BLDP_API int bldp_device_to_host(const void *src, void *dst, int64_t bytes,
+                                            void *copy_stream, void *stream, double *stats) {
+  try {
+    return device_to_host(src, dst, bytes, copy_stream, stream, stats);
+  } catch (const std::bad_alloc &) {
+    return bldp::set_error(BLDP_ENOMEM, "device_to_host: out of host memory");
+  } catch (...) {
+    return bldp::set_error(BLDP_EINVAL, "device_to_host: unexpected C++ exception");
   }
 }
 

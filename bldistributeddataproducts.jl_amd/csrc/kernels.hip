@@ -1010,8 +1010,7 @@ __device__ __forceinline__ void tile_tile(const RedArgs &a, int64_t tile) {
 }
 
 // Grid-stride wrappers: one tile per workgroup when the grid covers every
-// tile (the default), several when plan_reduce caps the grid (plan option
-// max_wg_per_cu).
+// tile, several when a launch has more tiles than INT32_MAX workgroups.
 template <int OP, int LPG, int K4C>
 __global__ __launch_bounds__(kBlock) void k_reduce_vec(const RedArgs a) {
   for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) vec_tile<OP, LPG, K4C>(a, t);
@@ -1035,9 +1034,8 @@ __global__ __launch_bounds__(kBlock) void k_reduce_vec(const RedArgs a) {
 //                measured +0.1..0.7% against 8 on 1-, 2- and 8-bank launches
 constexpr int kIlGpw = 2, kIlInflight = 4;
 // One tile (GPW groups x one (IF, time block) x one bank) of the interleaved
-// path; PERS: called in a loop by k_reduce_ilp, so the LDS is released by a
-// barrier before the next tile.
-template <int OP, int K4, int GPW, int IF, bool PERS>
+// path.
+template <int OP, int K4, int GPW, int IF>
 __device__ __forceinline__ void il_tile(const RedArgs &a, int64_t bx, uint32_t it, int bank) {
   constexpr int NI = GPW * K4 / 4;           // loads per lane per row
   constexpr int PER = K4 < 4 ? 1 : K4 / 4;   // consecutive loads of one group slot
@@ -1111,25 +1109,11 @@ __device__ __forceinline__ void il_tile(const RedArgs &a, int64_t bx, uint32_t i
     st1o(a.out + bank * a.out_bank + (int64_t)i * a.out_ld_i + (int64_t)to * a.out_ld_t + g0 + tid,
          finish<OP>(s, a), a.st_plain);
   }
-  if constexpr (PERS) __syncthreads();
 }
 
 template <int OP, int K4, int GPW>
 __global__ __launch_bounds__(kBlock) void k_reduce_il(const RedArgs a) {
-  il_tile<OP, K4, GPW, kIlInflight, false>(a, blockIdx.x, blockIdx.y, blockIdx.z);
-}
-
-// Plan option "il_persist": N > 0 = the interleaved path as a persistent grid
-// of N workgroups per CU walking the tiles in k_reduce_il's dispatch order,
-// 8 loads in flight per lane (the pure read's best shape: one workgroup per
-// CU, 8 nt loads in flight, 7.35 TB/s on 32 GiB).
-template <int OP, int K4, int GPW>
-__global__ __launch_bounds__(kBlock) void k_reduce_ilp(const RedArgs a) {
-  const int64_t nx = a.blocks_c, ny = a.ni * a.nto, n = a.ntiles;
-  for (int64_t t = blockIdx.x; t < n; t += gridDim.x) {
-    const int64_t r = t / nx;
-    il_tile<OP, K4, GPW, 8, true>(a, t - r * nx, (uint32_t)(r % ny), (int)(r / ny));
-  }
+  il_tile<OP, K4, GPW, kIlInflight>(a, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
 // Vector path, small groups (PATH_VEC_ROW): F = 4*G4 channels with G4 = 1..64
@@ -1849,17 +1833,6 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
     }
     return hipGetLastError();
   }
-  if (p.path == PATH_VEC_IL && a.il_pgrid > 0) {
-    const dim3 g1((unsigned)a.il_pgrid);
-    switch (a.k4) {
-      case 2: BLDP_LAUNCH((k_reduce_ilp<OP, 2, kIlGpw>), g1, block, 0, s, a); break;
-      case 4: BLDP_LAUNCH((k_reduce_ilp<OP, 4, kIlGpw>), g1, block, 0, s, a); break;
-      case 8: BLDP_LAUNCH((k_reduce_ilp<OP, 8, kIlGpw>), g1, block, 0, s, a); break;
-      case 16: BLDP_LAUNCH((k_reduce_ilp<OP, 16, kIlGpw>), g1, block, 0, s, a); break;
-      default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-  }
   if (p.path == PATH_VEC_IL) {
     const dim3 g3((unsigned)a.blocks_c, (unsigned)(a.ni * a.nto), (unsigned)a.nbank);
     switch (a.k4) {
@@ -1926,41 +1899,41 @@ namespace {
 struct PlanOptDef {
   const char *name;
   int64_t def;
+  int64_t lo, hi;  // the values bldp_plan_option accepts (and -1: the default)
 };
 const PlanOptDef kPlanOpts[OPT_COUNT] = {
-    {"row_split", -1},        // k_reduce_row's block over 1 / 2 / 4 workgroup slices; -1 by launch size
-    {"force_staged", 0},      // 1: bldp_band_reduce_multi_f32 stages every bank
-    {"max_wg_per_cu", 0},     // N > 0: grid capped at N workgroups per CU (grid-stride loops)
-    {"ts_fill", 1},           // narrow vector-path windows split time over idle waves
-    {"narrow_mis", 1},        // misaligned F = 1 (2: and F = 2) on k_reduce_narrow_mis
-    {"t38", 1},               // tavby = 3, 8 on the short-time-block kernels
-    {"wide_split", 1},        // groups > 4096 channels split time by work, not rows
-    {"narrow_tpb", 2},        // k_reduce_narrowt: 2 = incl. the copy, 1 = not it, 0 = off
-    {"lane", 1},              // k_reduce_lane: 1 = where the tile path cannot run, 2 = always
-    {"lane3", 1},             // fqavby = 3 on the lane kernel everywhere
-    {"lanet", 1},             // k_reduce_lanet for small odd groups, short time blocks
-    {"lanet_pack", 1},        // narrow lanet windows: 2 / 4 time groups per workgroup
-    {"vec_il", 1},            // k_reduce_il for F = 512 .. 4096
-    {"vec_row", 1},           // k_reduce_row for F = 4 .. 256
-    {"row_tpb", 1},           // k_reduce_rowt for short time blocks
-    {"rowt_pack", 1},         // narrow rowt windows: 2 / 4 time groups per workgroup
-    {"rowt_small", 64},       // rowt/narrowt: launches below this many workgroups per CU take 8 (4 at T <= 2) rows
-    {"wavet", 1},             // k_reduce_wavet: 1 = where il is a poor fit, 2 = always, 0 = never
-    {"unaligned_vec", 2},     // dword-aligned 16-byte loads: 1 = reduce, 2 = + kurtosis, 3 = all
-    {"kurt_exact", 1},        // k_kurt_regs exact-count forms for 16 / 32 spectra
-    {"kurt_mid_cpl", 2},      // 2: k_kurt_mid2 (two channels per lane) where it applies
-    {"kurt_mid_small", 1},    // k_kurt_mid2 on 4 waves for <= 64 spectra
-    {"kurt_leaf_narrow", 4},  // leaf plans below this many waves per CU: one channel per lane
-    {"kurt_leaf_tile", 1},    // k_kurt_tile: 1 = narrow short leaves, 2 = every leaf plan
-    {"typed_vec", 1},         // order-free typed reductions on k_reduce_typed_vec
-    {"typed_rows", 4},        // k_reduce_typed_vec16: most rows a workgroup loads in one batch (4-16)
-    {"row_bpack", 1},         // k_reduce_rowt: lane sets over consecutive banks on narrow stitched rows
-    {"lane_bpack", 1},        // k_reduce_lanes: lanet's lanes along narrow stitched band rows
-    {"wave_bpack", 1},        // k_reduce_wavet: a wave per (bank, group) of <= 16-group stitched rows
-    {"col3", 1},              // fqavby = 12, short time blocks: k_reduce_col3 (float4 columns)
-    {"rowt_narrow8", 1},      // k_reduce_rowt: 8 rows per lane on <= 128-column windows too
-    {"st_plain", 1},          // row / il stores: 1 plain below 2 GB of traffic, 0 always nt, 2 always plain
-    {"il_persist", 0},        // N > 0: interleaved path as k_reduce_ilp, N workgroups per CU
+    {"row_split", -1, 1, 4},      // k_reduce_row's block over 1 / 2 / 4 workgroup slices; -1 by launch size
+    {"ts_fill", 1, 0, 1},         // narrow vector-path windows split time over idle waves
+    {"narrow_mis", 1, 0, 2},      // misaligned F = 1 (2: and F = 2) on k_reduce_narrow_mis
+    {"t38", 1, 0, 1},             // tavby = 3, 8 on the short-time-block kernels
+    {"wide_split", 1, 0, 1},      // groups > 4096 channels split time by work, not rows
+    {"narrow_tpb", 2, 0, 2},      // k_reduce_narrowt: 2 = incl. the copy, 1 = not it, 0 = off
+    {"lane", 1, 0, 2},            // k_reduce_lane: 1 = where the tile path cannot run, 2 = always
+    {"lane3", 1, 0, 1},           // fqavby = 3 on the lane kernel everywhere
+    {"lanet", 1, 0, 1},           // k_reduce_lanet for small odd groups, short time blocks
+    {"lanet_pack", 1, 0, 1},      // narrow lanet windows: 2 / 4 time groups per workgroup
+    {"vec_il", 1, 0, 1},          // k_reduce_il for F = 512 .. 4096
+    {"vec_row", 1, 0, 1},         // k_reduce_row for F = 4 .. 256
+    {"row_tpb", 1, 0, 1},         // k_reduce_rowt for short time blocks
+    {"rowt_pack", 1, 0, 1},       // narrow rowt windows: 2 / 4 time groups per workgroup
+    // rowt/narrowt: launches below this many workgroups per CU take 8 (4 at T <= 2) rows
+    {"rowt_small", 64, 0, 1 << 20},
+    {"wavet", 1, 0, 2},           // k_reduce_wavet: 1 = where il is a poor fit, 2 = always, 0 = never
+    {"unaligned_vec", 2, 0, 3},   // dword-aligned 16-byte loads: 1 = reduce, 2 = + kurtosis, 3 = all
+    {"kurt_exact", 1, 0, 1},      // k_kurt_regs exact-count forms for 16 / 32 spectra
+    {"kurt_mid_cpl", 2, 1, 2},    // 2: k_kurt_mid2 (two channels per lane) where it applies
+    {"kurt_mid_small", 1, 0, 1},  // k_kurt_mid2 on 4 waves for <= 64 spectra
+    // leaf plans below this many waves per CU: one channel per lane
+    {"kurt_leaf_narrow", 4, 0, 1 << 20},
+    {"kurt_leaf_tile", 1, 0, 2},  // k_kurt_tile: 1 = narrow short leaves, 2 = every leaf plan
+    {"typed_vec", 1, 0, 1},       // order-free typed reductions on k_reduce_typed_vec
+    {"typed_rows", 4, 4, 16},     // k_reduce_typed_vec16: most rows a workgroup loads in one batch
+    {"row_bpack", 1, 0, 1},       // k_reduce_rowt: lane sets over consecutive banks on narrow stitched rows
+    {"lane_bpack", 1, 0, 1},      // k_reduce_lanes: lanet's lanes along narrow stitched band rows
+    {"wave_bpack", 1, 0, 1},      // k_reduce_wavet: a wave per (bank, group) of <= 16-group stitched rows
+    {"col3", 1, 0, 1},            // fqavby = 12, short time blocks: k_reduce_col3 (float4 columns)
+    {"rowt_narrow8", 1, 0, 1},    // k_reduce_rowt: 8 rows per lane on <= 128-column windows too
+    {"st_plain", 1, 0, 2},        // row / il stores: 0 always nt, 1 plain below 2 GB of traffic, 2 always plain
 };
 struct PlanOpts {
   std::atomic<int64_t> v[OPT_COUNT];  // -1 = no override
@@ -1980,6 +1953,15 @@ int plan_opt_index(const char *name) {
   return -1;
 }
 int64_t plan_opt_override(int k) { return g_plan_opt.v[k].load(std::memory_order_relaxed); }
+bool plan_opt_valid(int k, int64_t v) {
+  if (v < 0) return true;
+  if (v < kPlanOpts[k].lo || v > kPlanOpts[k].hi) return false;
+  return k != OPT_ROW_SPLIT || v == 1 || v == 2 || v == 4;
+}
+void plan_opt_domain(int k, int64_t *lo, int64_t *hi) {
+  *lo = kPlanOpts[k].lo;
+  *hi = kPlanOpts[k].hi;
+}
 void plan_opt_set(int k, int64_t v) { g_plan_opt.v[k].store(v, std::memory_order_relaxed); }
 
 Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus) {
@@ -1995,7 +1977,6 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
   a.rsplit = 1;
   a.bpack = 0;
   a.st_plain = 0;
-  a.il_pgrid = 0;
   const bool t38 = opt(OPT_T38) != 0;
   if (opt(OPT_LANET) && words && a.in_cs == 1 && (T == 1 || T == 2 || T == 4 || (t38 && (T == 3 || T == 8))) &&
       (F == 3 || F == 5 || F == 6 || F == 7 || F == 12) && a.ni <= 65535 && a.nbank <= 65535 &&
@@ -2113,10 +2094,7 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
   a.nchunk = (int32_t)std::max<int64_t>(1, cdiv(T, a.rows_per_chunk));
   p.ws_bytes = a.nchunk > 1 ? (size_t)a.nchunk * a.nbank * p.nout * sizeof(float) : 0;
   a.ntiles = a.blocks_c * a.ni * a.nchunk * a.nto * a.nbank;
-  p.grid = a.ntiles;
-  const int64_t cap = opt(OPT_MAX_WG_PER_CU);  // 0: one workgroup per tile
-  if (cap > 0) p.grid = std::min<int64_t>(p.grid, (int64_t)cap * num_cus);
-  p.grid = std::min<int64_t>(p.grid, INT32_MAX);  // tiles beyond: grid-stride loop
+  p.grid = std::min<int64_t>(a.ntiles, INT32_MAX);  // tiles beyond: grid-stride loop
   // large groups with short time blocks where the interleaved kernel is a
   // poor fit (few groups per row, or its 3-D grid too small): k_reduce_wavet
   // (path "vector", a.tpb = time blocks per wave)
@@ -2148,9 +2126,6 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
     a.blocks_c = cdiv(a.nco, kIlGpw);
     a.ntiles = a.blocks_c * a.ni * a.nto * a.nbank;
     p.grid = a.ntiles;
-    const int64_t pers = opt(OPT_IL_PERSIST);
-    if (pers > 0) p.grid = std::min<int64_t>(p.grid, pers * num_cus);
-    a.il_pgrid = pers > 0 ? (int32_t)p.grid : 0;
   }
   // small power-of-two groups, whole time block per tile, no time split:
   // the lean row kernel (3-D grid, so every dimension must fit)
@@ -2275,7 +2250,8 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
                 a.out_ld_t % w == 0;
   }
   // output stores of the row / interleaved kernels: plain below 2 GB of
-  // launch traffic, non-temporal above (option st_plain: -1 by size, 0 nt, 1 plain)
+  // launch traffic, non-temporal above (option st_plain: 0 always nt, 1 (the
+  // default) by that size rule, 2 always plain)
   {
     const int64_t bytes = 4 * a.nbank * a.ni * (a.nco * F * a.nto * T + a.nco * a.nto);
     const int64_t o = opt(OPT_ST_PLAIN);
@@ -2321,70 +2297,6 @@ hipError_t launch_despike(float *d, int64_t nchan, int64_t nrows, int64_t nfpc, 
   if (n == 0) return hipSuccess;
   const unsigned grid = (unsigned)std::min<int64_t>(cdiv(n, kBlock), 16384);
   hipLaunchKernelGGL(k_despike, dim3(grid), dim3(kBlock), 0, s, d, nchan, nrows, nfpc, nspike);
-  return hipGetLastError();
-}
-
-// The pure-read rate of a buffer on this box (bench.py's per-box reference,
-// the pure read of tools/mix_ceiling.hip): chunks of NL*kBlock 16-byte words,
-// each thread NL 16-byte loads (non-temporal unless PLAIN) at a kBlock-word
-// stride, nothing stored (a store that never happens keeps the loads); one
-// workgroup per chunk or wg_per_cu persistent workgroups per CU.  SLABS: the
-// buffer is cut into NL equal slabs and chunk c reads kBlock words of each
-// (NL streams far apart at once, as a reduce reads a block's time rows).
-template <bool PLAIN, int NL, bool SLABS>
-__global__ __launch_bounds__(kBlock) void k_read_probe(const float *in, int64_t nchunk, int64_t n4,
-                                                        int64_t slab, float *sink) {
-  const int t = threadIdx.x;
-  f4v acc = {0, 0, 0, 0};
-  const f4v *p = reinterpret_cast<const f4v *>(in);
-  for (int64_t c = blockIdx.x; c < nchunk; c += gridDim.x) {
-    const int64_t b = SLABS ? c * kBlock + t : c * NL * kBlock + t;
-    f4v v[NL];
-#pragma unroll
-    for (int k = 0; k < NL; ++k) {
-      const int64_t i = b + (SLABS ? slab : kBlock) * k;
-      v[k] = i >= n4 ? f4v{0, 0, 0, 0} : PLAIN ? p[i] : __builtin_nontemporal_load(p + i);
-    }
-#pragma unroll
-    for (int k = 0; k < NL; ++k) acc += v[k];
-  }
-  if (acc.x == 1234.5f && sink) sink[t] = acc.y;
-}
-
-template <bool PLAIN, int NL, bool SLABS>
-static void read_probe_go(const float *in, int64_t bytes, int wg_per_cu, int num_cus,
-                          hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
-  const int64_t n4 = bytes / 16, slab = cdiv(cdiv(n4, NL), kBlock) * kBlock;
-  const int64_t nchunk = SLABS ? slab / kBlock : cdiv(n4, (int64_t)NL * kBlock);
-  if (nchunk == 0) return;
-  const int64_t grid = wg_per_cu > 0 ? std::min<int64_t>(nchunk, (int64_t)wg_per_cu * num_cus)
-                                     : std::min<int64_t>(nchunk, INT32_MAX);
-  if (ev1)  // timed like bldp_reduce_launch_timed: events carried by the dispatch
-    hipExtLaunchKernelGGL((k_read_probe<PLAIN, NL, SLABS>), dim3((unsigned)grid), dim3(kBlock), 0,
-                          s, ev0, ev1, 0, in, nchunk, n4, slab, (float *)nullptr);
-  else
-    hipLaunchKernelGGL((k_read_probe<PLAIN, NL, SLABS>), dim3((unsigned)grid), dim3(kBlock), 0, s,
-                       in, nchunk, n4, slab, (float *)nullptr);
-}
-
-template <bool SLABS>
-static void read_probe_form(const float *in, int64_t bytes, int form, int num_cus, hipStream_t s,
-                            hipEvent_t ev0, hipEvent_t ev1) {
-  const int g = form & 255;
-  switch (form >> 8 & 3) {
-    case 0: read_probe_go<false, 16, SLABS>(in, bytes, g, num_cus, s, ev0, ev1); break;
-    case 1: read_probe_go<true, 16, SLABS>(in, bytes, g, num_cus, s, ev0, ev1); break;
-    case 2: read_probe_go<false, 8, SLABS>(in, bytes, g, num_cus, s, ev0, ev1); break;
-    default: read_probe_go<true, 8, SLABS>(in, bytes, g, num_cus, s, ev0, ev1); break;
-  }
-}
-
-hipError_t launch_read_probe(const float *in, int64_t bytes, int form, int num_cus, hipStream_t s,
-                             hipEvent_t ev0, hipEvent_t ev1) {
-  if (form & 1024)
-    read_probe_form<true>(in, bytes, form, num_cus, s, ev0, ev1);
-  else
-    read_probe_form<false>(in, bytes, form, num_cus, s, ev0, ev1);
   return hipGetLastError();
 }
 

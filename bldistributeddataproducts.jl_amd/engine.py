@@ -102,19 +102,58 @@ def fb_from_numpy(a: np.ndarray, device=None):
     return t.to(device or "cuda").permute(2, 1, 0)
 
 
+_d2h_streams: dict = {}
+
+
+def device_to_host(c, stats=None) -> np.ndarray:
+    """A contiguous device tensor into a new ordinary (pageable) numpy array
+    of the same shape through the library's pinned slot ring
+    (bldp_device_to_host: slot-sized DMAs overlapped with the slots' copy-out
+    by the reader threads).  Ordered after the work queued on torch's current
+    stream of the tensor's device.  No pinned memory is allocated or held: the
+    result is the caller's ordinary memory (what torch's pinned caching
+    allocator would have kept page-locked, rounded up to a power of two, for as
+    long as the array lives and after)."""
+    torch = _torch()
+    if not c.is_contiguous():
+        raise ValueError("device_to_host needs a contiguous tensor")
+    h = np.empty(tuple(c.shape), dtype=np.dtype(str(c.dtype).replace("torch.", "")))
+    if h.nbytes == 0:
+        return h
+    dev = c.device
+    with torch.cuda.device(dev):
+        cs = _d2h_streams.get(dev.index)
+        if cs is None:
+            cs = _d2h_streams[dev.index] = torch.cuda.Stream(dev, priority=-1)
+        st = (ctypes.c_double * 4)()
+        rc = _lib.lib().bldp_device_to_host(c.data_ptr(), h.ctypes.data, h.nbytes, cs.cuda_stream,
+                                            _lib.stream_ptr(), st)
+    _lib.check(rc, "bldp_device_to_host")
+    if stats is not None:
+        stats.update(first_dma_ms=st[0], total_ms=st[1], slots=int(st[2]), threads=int(st[3]))
+    return h
+
+
 def fb_to_numpy(t, pinned=False) -> np.ndarray:
     """Device tensor (Julia order) -> Fortran-ordered numpy array.  With
-    ``pinned`` the copy lands in page-locked memory from torch's caching host
-    allocator (one DMA at PCIe speed instead of the staged copy into pageable
-    memory, ~7 GB/s); the array keeps that block until it is dropped."""
+    ``pinned`` the copy goes through the library's pinned slot ring
+    (device_to_host: DMA at PCIe speed instead of torch's staged copy into
+    pageable memory, ~7 GB/s) into ordinary memory the array owns."""
     torch = _torch()
     c = t.permute(2, 1, 0).contiguous() if t.dim() == 3 else t.t().contiguous()
     if pinned and c.is_cuda:
-        h = torch.empty(c.shape, dtype=c.dtype, pin_memory=True)
-        h.copy_(c)
+        h = device_to_host(c)
     else:
-        h = c.cpu()
-    return np.asfortranarray(h.numpy().transpose(2, 1, 0) if t.dim() == 3 else h.numpy().T)
+        h = c.cpu().numpy()
+    return np.asfortranarray(h.transpose(2, 1, 0) if t.dim() == 3 else h.T)
+
+
+def peer_access(dev, peer) -> bool:
+    """bldp_peer_access: may kernels on ``dev`` store straight into memory of
+    ``peer`` (same device, or xGMI peer access, enabled here)?"""
+    d = ctypes.c_int()
+    _lib.check(_lib.lib().bldp_peer_access(int(dev), int(peer), ctypes.byref(d)), "bldp_peer_access")
+    return bool(d.value)
 
 
 def _abi_dims(t, allow_typed=False):
@@ -357,11 +396,14 @@ class PreparedBandReduce:
         self.close()
 
 
-def band_reduce_multi(banks, fqavby=1, tavby=1, op="sum", win=None, root=0, out=None):
+def band_reduce_multi(banks, fqavby=1, tavby=1, op="sum", win=None, root=0, out=None,
+                      staged=False):
     """One process, banks on several GPUs (bldp_band_reduce_multi_f32): each
     GPU reduces its banks straight into the stitched product on `root` (into
     ``out`` when given: a dense Julia-order (nbank*nco, ni, nto) Float32 tensor
-    there)."""
+    there).  ``staged``: every bank takes the staged branch (BLDP_BAND_STAGED:
+    reduce on its device, then one strided copy into its slot), the root's
+    included -- a per-call argument, not process state."""
     torch = _torch()
     L = _lib.lib()
     banks = list(banks)
@@ -388,7 +430,8 @@ def band_reduce_multi(banks, fqavby=1, tavby=1, op="sum", win=None, root=0, out=
     rc = L.bldp_band_reduce_multi_f32(len(banks), ctypes.cast(devs, ctypes.c_void_p),
                                       ctypes.cast(ptrs, ctypes.c_void_p), *geo, wp,
                                       int(fqavby), int(tavby), _lib.OPS[op], int(root),
-                                      out.data_ptr() if out.numel() else None)
+                                      out.data_ptr() if out.numel() else None,
+                                      _lib.BLDP_BAND_STAGED if staged else 0)
     _lib.check(rc, "bldp_band_reduce_multi_f32")
     return out
 
@@ -498,50 +541,6 @@ def synth(nchan, nif, ntime, nfpc=1024, seed=0, kind=0, device=None, stream=None
                           seed, kind, _lib.stream_ptr(stream))
     _lib.check(rc, "bldp_synth_f32")
     return out
-
-
-# nt loads, 16 or 8 in flight, contiguous or slab-spread: the forms that led
-# some size of tools/read_probe_sweep.py (profiles/r04/read_probe_sweep_r04probe_b.json)
-PROBE_FORMS = (0, 3, 513, 514, 520, 1537, 1544)
-
-
-def read_probe(nbytes, launches=20, forms=PROBE_FORMS, buf=None, stream=None,
-               every=False) -> dict:
-    """The pure-read rate of this GPU for an ``nbytes`` buffer
-    (bldp_read_probe): ``launches`` back-to-back launches per form (include/
-    bldp.h: workgroups per CU | plain loads << 8 | 8 loads in flight << 9 |
-    slabs << 10),
-    each timed by events carried on its dispatch; the best form's median.  The
-    measurement reference bench.py sets a reduce's bandwidth beside (boxes
-    differ by several percent)."""
-    import statistics
-    torch = _torch()
-    L = _lib.lib()
-    nbytes = int(nbytes) // 16 * 16
-    if buf is None:
-        buf = torch.zeros(max(nbytes // 4, 4), dtype=torch.float32, device="cuda")
-    elif buf.numel() * buf.element_size() < nbytes:
-        raise ValueError("probe buffer smaller than nbytes")
-    sp = _lib.stream_ptr(stream)
-    evs = [(_lib.HipEvent(timing=True, fence=False), _lib.HipEvent(timing=True, fence=False))
-           for _ in range(launches)]
-    best, seen = None, []
-    for g in forms:
-        for _ in range(3):
-            _lib.check(L.bldp_read_probe(buf.data_ptr(), nbytes, g, sp, None, None),
-                       "bldp_read_probe")
-        for e0, e1 in evs:
-            _lib.check(L.bldp_read_probe(buf.data_ptr(), nbytes, g, sp, e0.ev, e1.ev),
-                       "bldp_read_probe")
-        torch.cuda.synchronize()
-        ms = statistics.median(e0.elapsed_time(e1) for e0, e1 in evs)
-        r = {"GBps": round(nbytes / (ms * 1e-3) / 1e9, 1), "ms": round(ms, 5),
-             "form": g, "wg_per_cu": g & 255, "loads": "plain" if g & 256 else "nt",
-             "in_flight": 8 if g & 512 else 16, "slabs": bool(g & 1024), "bytes": nbytes}
-        seen.append(r)
-        if best is None or r["GBps"] > best["GBps"]:
-            best = r
-    return dict(best, forms=seen) if every else best
 
 
 def reduce_host(a: np.ndarray, fqavby=1, tavby=1, op="sum", win=None, device=0) -> np.ndarray:

@@ -186,12 +186,18 @@ def _band_raw(ws, fs, geo, idxs, fqavby, op, tavby, band, root, force_copy, tm):
     for b, w in enumerate(ws):
         groups.setdefault(int(w), []).append(b)
     views = [None] * len(fs)
+    # the caller's current stream on every device: each reader thread queues
+    # its copies' completion (and allocates its buffer) on it, so the reduce
+    # queued below on the same stream is ordered after the copies even when
+    # the caller runs under `with torch.cuda.stream(s)` (torch's current
+    # stream is per thread: a reader thread's own would be the default one)
+    cur = {d: torch.cuda.current_stream(d) for d in set(groups) | {root}}
 
     def read(item):
         dev, bl = item
         t = {}
         t0 = time.perf_counter()
-        with torch.cuda.device(dev):
+        with torch.cuda.device(dev), torch.cuda.stream(cur[dev]):
             vs = filestream.files_to_device([fs[b] for b in bl], [geo[b][2] for b in bl], runs0,
                                             dshape, f"cuda:{dev}", timings=t)
         for b, v in zip(bl, vs):
@@ -210,15 +216,13 @@ def _band_raw(ws, fs, geo, idxs, fqavby, op, tavby, band, root, force_copy, tm):
             engine.band_reduce(views, fqavby, tavby, op, rwin, out=band)
         tm["reduce"] = "bldp_band_reduce_f32 (one launch)"
     else:
-        from . import _lib
-
-        with _lib.plan_option("force_staged", 1 if force_copy else -1):
-            engine.band_reduce_multi(views, fqavby, tavby, op, rwin, root=root, out=band)
+        engine.band_reduce_multi(views, fqavby, tavby, op, rwin, root=root, out=band,
+                                 staged=force_copy)
         tm["reduce"] = "bldp_band_reduce_multi_f32" + (" (staged)" if force_copy else "")
     tm["reduce_queue_ms"] = (time.perf_counter() - t1) * 1e3
 
 
-def _band_on_device(ws, fs, idxs, fqavby, op, tavby, nfpc, timings=None):
+def _band_on_device(ws, fs, idxs, fqavby, op, tavby, nfpc, timings=None, staged=None):
     """One band stitched on the GPU (src/gbt.jl:103): every
     bank is read and reduced on its worker's GPU straight into its vcat slot
     of the band product on the first worker's GPU, the DC-spike patch runs on
@@ -248,26 +252,38 @@ def _band_on_device(ws, fs, idxs, fqavby, op, tavby, nfpc, timings=None):
     nco, ni, nto = shapes[0]
     nb, root = len(fs), int(ws[0])
     band = engine.fb_empty(nb * nco, ni, nto, device=f"cuda:{root}")
-    # BLDP_BAND_FORCE_COPY=1 takes the other-GPU branch (reduce, then copy into
-    # the slot) for every bank: how a one-GPU box tests it
-    force_copy = os.environ.get("BLDP_BAND_FORCE_COPY", "0") == "1"
+    # staged (or BLDP_BAND_FORCE_COPY=1 when not given) takes the other-GPU
+    # branch (reduce, then copy into the slot) for every bank: how a one-GPU
+    # box runs it.  An argument of this call: no process state is touched
+    force_copy = (os.environ.get("BLDP_BAND_FORCE_COPY", "0") == "1" if staged is None
+                  else bool(staged))
     raw = (all(g[0] == "raw" for g in geo) and len({g[1] for g in geo}) == 1
            and os.environ.get("BLDP_NATIVE_READ", "1") != "0")
     if raw:
         _band_raw(ws, fs, geo, idxs, fqavby, op, tavby, band, root, force_copy, tm)
     else:
+        # every bank is read (compressed chunks decoded) on its own GPU and
+        # reduced there straight into its vcat slot on the root: a kernel
+        # store over xGMI where the bank's GPU may write the root's memory
+        # (bldp_peer_access), else reduced locally and copied into the slot
+        # by one stream-ordered device-to-device copy.  No host wait per bank:
+        # every reader queues on the caller's current stream of its device
+        # (ordered with the root's despike and D2H below by the device
+        # synchronize), and the band is complete when those streams drain.
+        devs = sorted({int(w) for w in ws} | {root})
+        cur = {d: torch.cuda.current_stream(d) for d in devs}
+        direct = {d: (not force_copy) and engine.peer_access(d, root) for d in devs}
+
         def bank(b):
             slot = band[b * nco:(b + 1) * nco]
             dev = int(ws[b])
-            if dev == root and not force_copy:
-                return W.getdata_device(fs[b], idxs, fqavby, op, tavby, device=dev, out=slot)
-            r = W.getdata_device(fs[b], idxs, fqavby, op, tavby, device=dev)
-            if r is not None:
-                with torch.cuda.device(dev):
-                    torch.cuda.current_stream().synchronize()
-                with torch.cuda.device(root):
-                    slot.copy_(r)
-            return r
+            with torch.cuda.device(dev), torch.cuda.stream(cur[dev]):
+                if direct[dev]:
+                    return W.getdata_device(fs[b], idxs, fqavby, op, tavby, device=dev, out=slot)
+                r = W.getdata_device(fs[b], idxs, fqavby, op, tavby, device=dev)
+                if r is not None:  # (torch orders a cross-device copy on both devices' streams)
+                    slot.copy_(r, non_blocking=True)
+                return r
 
         t1 = time.perf_counter()
         with ThreadPoolExecutor(max_workers=max(1, nb)) as ex:  # @spawnat per bank
@@ -285,7 +301,7 @@ def _band_on_device(ws, fs, idxs, fqavby, op, tavby, nfpc, timings=None):
             engine.despike(band, nco // 64 if nfpc is True else int(nfpc))
         out = engine.fb_to_numpy(band, pinned=True)  # the one device -> host copy
         tm["despike_d2h_ms"] = (time.perf_counter() - t3) * 1e3
-    tm["path"] = "raw band" if raw else "bank by bank"
+    tm["path"] = "raw band" if raw else ("bank by bank" + (" (staged)" if force_copy else ""))
     tm["total_ms"] = (time.perf_counter() - t0) * 1e3
     return out
 
@@ -309,7 +325,7 @@ def _despike_host(d: np.ndarray, nfpc: int) -> np.ndarray:
 
 
 def getband(workers, fnames, idxs=(COLON, COLON, COLON), fqavby=1, fqavfunc="sum", tavby=1,
-            despike_nfpc=None, freqs=False, stitch="device"):
+            despike_nfpc=None, freqs=False, stitch="device", staged=None):
     """The stitched band product: reduce(vcat, getdata(...)) in the given
     bank order (src/gbt.jl:103).  ``workers``/``fnames`` are one band's banks
     (1-D), or a (nbank, nband) matrix like loadscan's ``ds``, whose columns are
@@ -323,7 +339,11 @@ def getband(workers, fnames, idxs=(COLON, COLON, COLON), fqavby=1, fqavfunc="sum
     ``stitch="device"`` (default) stitches each band on the GPU
     (:func:`_band_on_device`); ``stitch="host"`` reduces every bank on its GPU,
     copies each bank's product to the host and concatenates there (also what
-    bands of unequal bank products or non-Float32 data get)."""
+    bands of unequal bank products or non-Float32 data get).  ``staged=True``
+    sends every bank of the device stitch through the staged branch (reduced
+    on its own GPU, then copied into its slot) even where its GPU could write
+    the root's memory directly: how a one-GPU box runs that branch (default:
+    the environment's BLDP_BAND_FORCE_COPY, else off)."""
     w = np.asarray(workers, dtype=object)
     f = np.asarray(fnames, dtype=object)
     if w.ndim not in (1, 2):
@@ -337,7 +357,8 @@ def getband(workers, fnames, idxs=(COLON, COLON, COLON), fqavby=1, fqavfunc="sum
     bands = [None] * len(wcol)
     if stitch == "device" and op is not None:
         for j, (ws, fs) in enumerate(zip(wcol, fcol)):
-            bands[j] = _band_on_device(ws, fs, idxs, fqavby, op, tavby, despike_nfpc)
+            bands[j] = _band_on_device(ws, fs, idxs, fqavby, op, tavby, despike_nfpc,
+                                       staged=staged)
     for j, (ws, fs) in enumerate(zip(wcol, fcol)):
         if bands[j] is not None:
             continue

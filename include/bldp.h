@@ -39,6 +39,23 @@
  *     and never synchronize; buffers are owned by the caller.
  *   - Return value 0 = ok, negative = error; bldp_last_error() returns the
  *     thread-local message of the last failing call.
+ *
+ * Threading ("reentrant per device handle")
+ *   - Every entry point may be called from several host threads at once, for
+ *     the same or different devices (GBT.getdata's per-worker fan-out,
+ *     src/gbt.jl:75-77).  Library state shared between calls (per-(device,
+ *     stream) scratch, staging pipelines, pinned slot rings, reader threads)
+ *     is leased per call under its own lock; results never depend on what
+ *     another thread is doing.
+ *   - The only process-wide mutable setting is bldp_plan_option, an A/B and
+ *     test facility: the product path never sets it, and a caller that sets
+ *     it changes the kernel choice (never the results: every form is
+ *     bit-identical or held to the same tolerance) of every thread's later
+ *     plans.  Choices that are part of a call (e.g. the staged branch of
+ *     bldp_band_reduce_multi_f32) are arguments of that call.
+ *   - Asynchronous entry points order their work on the caller's stream only;
+ *     a caller that hands data between streams or threads does the ordering
+ *     (events) itself.
  */
 #ifndef BLDP_H
 #define BLDP_H
@@ -53,8 +70,14 @@ extern "C" {
 /* 2: bldp_bslz4_decode_dev / _async take out_len (round 2); BLDP_EIO; the
  *    typed (non-Float32) entry points
  * 3: prepared band reduces (bldp_band_reduce_prepare_f32 / bldp_reduce_launch /
- *    bldp_reduce_launch_timed / bldp_reduce_release); bldp_plan_option; bldp_file_runs_to_device */
-#define BLDP_ABI_VERSION 3
+ *    bldp_reduce_launch_timed / bldp_reduce_release); bldp_plan_option; bldp_file_runs_to_device
+ * 4: bldp_band_reduce_multi_f32 takes a flags word (BLDP_BAND_STAGED replaces
+ *    the process-wide "force_staged" option and BLDP_FORCE_STAGED);
+ *    bldp_peer_access; bldp_device_to_host; bldp_plan_option checks each
+ *    option's domain; bldp_read_probe moved out of the product library
+ *    (tools/read_probe.hip, build/libbldp_probe.so); plan options
+ *    "force_staged", "il_persist", "max_wg_per_cu" removed */
+#define BLDP_ABI_VERSION 4
 
 #if defined(BLDP_BUILD)
 #define BLDP_API __attribute__((visibility("default")))
@@ -113,26 +136,24 @@ BLDP_API int bldp_reduce_plan_f32(const float *in, int64_t nchan, int64_t nif, i
                          const int64_t *win, int64_t fqavby, int64_t tavby, int op,
                          const float *out, int64_t info[8]);
 
-/* Process-wide plan options (tests and tuning): override one of the
- * planners' measured choices.  value -1 restores the default; *previous (may
- * be NULL) receives the old override (-1 = none).  Every form is
- * parity-tested (tests/test_gpu_parity.py::test_plan_options_every_form).
+/* Process-wide plan options, an A/B and TEST facility only (see Threading
+ * above: the product path never sets one): override one of the planners'
+ * measured choices.  value -1 restores the default; *previous (may be NULL)
+ * receives the old override (-1 = none).  Every form is parity-tested
+ * (tests/test_gpu_parity.py::test_plan_options_every_form).
  *   "row_split"      k_reduce_row's time block over 1, 2 or 4 slices of a
  *                    workgroup (whole 16-row batches only; bit-identical
  *                    forms); default -1 = chosen by launch size
- *   "force_staged"   1: bldp_band_reduce_multi_f32 takes its staged branch
- *                    (reduce on the bank's device, then a strided copy into
- *                    the slot) for every bank, the root's included
- *   "max_wg_per_cu", "ts_fill", "narrow_mis", "t38", "wide_split",
+ *   "ts_fill", "narrow_mis", "t38", "wide_split",
  *   "narrow_tpb", "lane", "lane3", "lanet", "lanet_pack", "vec_il",
  *   "vec_row", "row_tpb", "rowt_pack", "rowt_small", "wavet",
  *   "unaligned_vec", "kurt_exact", "kurt_mid_cpl", "kurt_mid_small",
  *   "kurt_leaf_narrow", "kurt_leaf_tile", "typed_vec", "typed_rows",
- *   "row_bpack", "lane_bpack", "wave_bpack", "col3", "rowt_narrow8", "st_plain",
- *   "il_persist"
+ *   "row_bpack", "lane_bpack", "wave_bpack", "col3", "rowt_narrow8", "st_plain"
  *                    which kernel a reduce / kurtosis / typed shape takes
- *                    (csrc/kernels.hip kPlanOpts: defaults and meanings).
- * Unknown names: BLDP_EINVAL. */
+ *                    (csrc/kernels.hip kPlanOpts: defaults, meanings and the
+ *                    values each option accepts).
+ * Unknown names, and values outside an option's domain: BLDP_EINVAL. */
 BLDP_API int bldp_plan_option(const char *name, int64_t value, int64_t *previous);
 
 /* out[c', i, t'] = op over the F x T block of the window (device pointers).
@@ -190,11 +211,34 @@ BLDP_API int bldp_reduce_release(bldp_reduce_op_t handle);
  * its banks and writes each result straight into its vcat slot of `out`, the
  * stitched (nbank*nco, ni, nto) product on device `root` — over xGMI with peer
  * access, else through a staged peer copy.  Synchronous; all banks share the
- * same (nchan, nif, ntime) and window. */
+ * same (nchan, nif, ntime) and window.
+ * flags: 0, or BLDP_BAND_STAGED: every bank takes the staged branch (reduce on
+ * its device into library staging, then one strided copy into its slot), the
+ * root's banks included (how a one-GPU box runs that branch). */
+#define BLDP_BAND_STAGED 1u
 BLDP_API int bldp_band_reduce_multi_f32(int nbank, const int *bank_dev, const float *const *in,
                                         int64_t nchan, int64_t nif, int64_t ntime,
                                         const int64_t *win, int64_t fqavby, int64_t tavby,
-                                        int op, int root, float *out);
+                                        int op, int root, float *out, unsigned flags);
+
+/* Whether kernels running on device `dev` may store straight into memory of
+ * device `peer` (the same device, or peer access over xGMI, which this call
+ * enables when the hardware allows it): *direct = 1, else 0 (the caller stages
+ * and copies).  What GBT.getband's bank-by-bank branch asks before a bank's
+ * reduce on its own GPU writes the root's vcat slot (src/gbt.jl:103). */
+BLDP_API int bldp_peer_access(int dev, int peer, int *direct);
+
+/* Device -> host copy of `bytes` from src (memory of the current device) into
+ * ordinary (pageable) host memory dst through the library's ring of pinned
+ * slots (the current device's, shared with the file readers): slot-sized DMA
+ * copies on copy_stream, each landed slot copied out to dst by the reader
+ * threads while the next DMA runs.  The copies start after the work queued so
+ * far on `stream` (the producer's stream).  Synchronous: returns when dst is
+ * filled.  No pinned memory is allocated per call, and dst is never
+ * page-locked.  stats (NULL or 4 doubles): ms to the first DMA, total ms,
+ * slots, copy-out threads. */
+BLDP_API int bldp_device_to_host(const void *src, void *dst, int64_t bytes, void *copy_stream,
+                                 void *stream, double *stats);
 
 /* Band stitch across processes, one GPU each (the reference's one
  * Distributed.jl worker per bank, src/gbt.jl:75-77): an RCCL communicator
@@ -389,18 +433,6 @@ BLDP_API int bldp_fqav_range(double first, double step, int64_t len, int64_t n, 
 /* Synthetic BL-like filterbank (nchan, nif, ntime) on the device:
  * kind 0 = gamma(2, 5e8) x bandpass scallop x DC spike (nfpc bins per coarse
  * channel); kind 1 = integer-valued 0..255 (order-independent exact sums). */
-/* Measurement support (bench.py): stream `bytes` of a 16-byte-aligned device
- * buffer once and store nothing.  form: bits 0-7 workgroups per CU (0: one
- * workgroup per chunk, else that many persistent ones per CU), bit 8 plain
- * loads instead of non-temporal ones, bit 9 8 loads in flight per thread
- * instead of 16, bit 10 the loads of one chunk spread over as many equal
- * slabs of the buffer (that many streams far apart, as a reduce reads a
- * block's time rows) instead of one contiguous piece.  ev_start/ev_stop (hipEvent_t or NULL) ride on the dispatch
- * as in bldp_reduce_launch_timed: the pure-read rate of this box for that
- * buffer, the reference a reduce's bandwidth is set beside. */
-BLDP_API int bldp_read_probe(const void *dev, int64_t bytes, int form, void *stream,
-                             void *ev_start, void *ev_stop);
-
 BLDP_API int bldp_synth_f32(float *out, int64_t nchan, int64_t nif, int64_t ntime, int64_t nfpc,
                    uint64_t seed, int kind, void *stream);
 

@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol(pkg, L):
     assert not missing, missing
     for s in declared_symbols():
         assert getattr(L, s) is not None
-    assert L.bldp_abi_version() == pkg._lib.ABI_VERSION == 3
+    assert L.bldp_abi_version() == pkg._lib.ABI_VERSION == 4
 
 
 def test_library_is_gfx950_code(pkg):
@@ -425,7 +425,8 @@ def test_runs_to_device_validates_before_any_read(pkg, L):
 # with the same return type and the same argument types, position by position.
 _C_TO_JL = {"int": "Cint", "int64_t": "Int64", "size_t": "Csize_t", "uint64_t": "UInt64",
             "uint32_t": "UInt32", "uint8_t": "UInt8", "char": "UInt8", "float": "Float32",
-            "double": "Float64", "void": "Cvoid", "bldp_reduce_op_t": "Ptr{Cvoid}"}
+            "double": "Float64", "void": "Cvoid", "bldp_reduce_op_t": "Ptr{Cvoid}",
+            "unsigned": "Cuint"}
 
 
 def _c_param_to_jl(p):
@@ -530,13 +531,38 @@ def test_plan_options_documented_and_accepted(pkg, L):
     A = 1 << 20
     base = plan(pkg, L, A, 65536, 1, 279, 64, 16, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
     for n in names:
+        v = 4 if n == "typed_rows" else 1  # (typed_rows takes 4..16)
         prev = ctypes.c_int64(99)
-        assert L.bldp_plan_option(n.encode(), 1, ctypes.byref(prev)) == 0, n
+        assert L.bldp_plan_option(n.encode(), v, ctypes.byref(prev)) == 0, n
         assert prev.value == -1, (n, prev.value)
         assert L.bldp_plan_option(n.encode(), -1, ctypes.byref(prev)) == 0, n
-        assert prev.value == 1, (n, prev.value)
+        assert prev.value == v, (n, prev.value)
     assert plan(pkg, L, A, 65536, 1, 279, 64, 16, [0, 65536, 1, 0, 1, 1, 0, 272, 1]) == base
     # an option changes the plan it names, and the reset restores it
     with pkg._lib.plan_option("vec_row", 0):
         assert plan(pkg, L, A, 65536, 1, 279, 64, 16, [0, 65536, 1, 0, 1, 1, 0, 272, 1])[0] == 0
     assert plan(pkg, L, A, 65536, 1, 279, 64, 16, [0, 65536, 1, 0, 1, 1, 0, 272, 1]) == base
+
+
+def test_plan_option_domains_checked(pkg, L):
+    """bldp_plan_option rejects values outside an option's domain (ADVICE r04:
+    huge values multiplied by the CU count, out-of-domain forms silently
+    coerced) with BLDP_EINVAL and leaves the option unchanged; the removed
+    options (force_staged, il_persist, max_wg_per_cu: ABI 4) are unknown."""
+    cases = {"row_split": ((1, 2, 4), (0, 3, 5, 8)), "st_plain": ((0, 1, 2), (3, 100)),
+             "typed_rows": ((4, 8, 16), (0, 3, 17)), "unaligned_vec": ((0, 3), (4,)),
+             "kurt_mid_cpl": ((1, 2), (0, 3)), "vec_il": ((0, 1), (2, 1 << 40)),
+             "rowt_small": ((0, 64, 100000), (1 << 21, 1 << 62))}
+    for n, (good, bad) in cases.items():
+        for v in good:
+            assert L.bldp_plan_option(n.encode(), v, None) == 0, (n, v)
+        for v in bad:
+            prev = ctypes.c_int64(99)
+            assert L.bldp_plan_option(n.encode(), v, ctypes.byref(prev)) == pkg._lib.BLDP_EINVAL, \
+                (n, v)
+            assert prev.value == 99  # not written on error
+            assert n in pkg._lib.last_error()
+        assert L.bldp_plan_option(n.encode(), -1, None) == 0
+        assert L.bldp_plan_option(n.encode(), -7, None) == 0  # any negative: the default
+    for n in ("force_staged", "il_persist", "max_wg_per_cu"):
+        assert L.bldp_plan_option(n.encode(), 1, None) == pkg._lib.BLDP_EINVAL, n

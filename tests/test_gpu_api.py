@@ -173,6 +173,178 @@ def test_getband_raw_band_one_stream(pkg, orc, tmp_path, monkeypatch, force_copy
                                          despike_nfpc=nfpc), want)
 
 
+@pytest.mark.parametrize("staged", [False, True])
+def test_getband_compressed_banks_device_stitch(pkg, orc, tmp_path, staged):
+    """A band of compressed (HDF5 filter 32008) banks takes the bank-by-bank
+    branch of the device stitch: each bank's chunks are decoded on its GPU and
+    the reduce there writes the root's vcat slot directly (bldp_peer_access;
+    one GPU: the same device), or, staged, reduces locally and one
+    stream-ordered device copy fills the slot; no host wait per bank.
+    Bit-exact against the host concatenation and the oracle, with and without
+    despike (src/gbt.jl:75-78,101-103; src/gbtworkerfunctions.jl:181-187)."""
+    rng = np.random.default_rng(4242)
+    J, C = pkg.JRange, pkg.COLON
+    banks, names = [], []
+    for b in range(8):
+        a = np.asfortranarray(rng.integers(0, 200, (4096, 1, 48)).astype(np.float32))
+        f = str(tmp_path / f"z{b}.rawspec.0002.h5")
+        pkg.fbh5.write_bslz4(f, dict(foff=-187.5 / 4096, fch1=8400.0 - 187.5 * b, nfpc=64), a,
+                             (16, 1, 4096),
+                             lambda blk: orc.np_bslz4_encode(blk, 512, lz4=orc.lz4_compress))
+        banks.append(a)
+        names.append(f)
+    workers = [0] * len(names)
+    for idxs, F, T, op, nfpc in (((C, C, C), 64, 16, "sum", None),
+                                 ((C, C, J(1, 32)), 1, 8, "mean", 64),
+                                 ((J(1, 2048), C, J(2, 47)), 4, 1, "max", True)):
+        tm = {}
+        dev = pkg.GBT._band_on_device(workers, names, idxs, F, op, T, nfpc, timings=tm,
+                                      staged=staged)
+        assert tm["path"] == "bank by bank" + (" (staged)" if staged else ""), tm
+        host = pkg.GBT.getband(workers, names, idxs, fqavby=F, tavby=T, fqavfunc=op,
+                               despike_nfpc=nfpc, stitch="host")
+        assert same_bits(dev, host), (idxs, F, T, op, nfpc)
+        win = pkg.idxs.to_window(pkg.sanitizeidxs(idxs), banks[0].shape)
+        want = orc.stitch([orc.reduce(a, F, T, op, win) for a in banks])
+        if nfpc:
+            want = orc.despike(want, want.shape[0] // 8 // 64 if nfpc is True else nfpc)
+        assert same_bits(dev, want), (idxs, F, T, op, nfpc)
+        assert same_bits(pkg.GBT.getband(workers, names, idxs, fqavby=F, tavby=T, fqavfunc=op,
+                                         despike_nfpc=nfpc, staged=staged), want)
+
+
+@pytest.mark.parametrize("kind", ["raw", "compressed"])
+def test_getband_under_a_caller_stream(pkg, orc, tmp_path, kind):
+    """getband called inside `with torch.cuda.stream(s)`: the
+    reader threads queue their copies' completion on the caller's stream, so
+    the reduce the caller's thread queues on s reads landed bank data.  The
+    caller's stream is kept busy first, so a reduce not ordered after the
+    copies would read the buffer before they land."""
+    import torch
+
+    rng = np.random.default_rng(31)
+    C = pkg.COLON
+    nc = 1 << 18 if kind == "raw" else 4096
+    banks, names = [], []
+    for b in range(4):
+        a = np.asfortranarray(rng.integers(0, 256, (nc, 1, 16)).astype(np.float32))
+        f = str(tmp_path / f"s{b}.h5")
+        if kind == "raw":
+            pkg.fbh5.write(f, dict(foff=-1.0, nfpc=1024), a)
+        else:
+            pkg.fbh5.write_bslz4(f, dict(foff=-1.0, nfpc=64), a, (16, 1, 4096),
+                                 lambda blk: orc.np_bslz4_encode(blk, 512, lz4=orc.lz4_compress))
+        banks.append(a)
+        names.append(f)
+    want = orc.stitch([orc.reduce(a, 64, 8) for a in banks])
+    s = torch.cuda.Stream()
+    junk = torch.empty(1 << 28, dtype=torch.float32, device="cuda")
+    for _ in range(3):
+        with torch.cuda.stream(s):
+            for _ in range(20):  # ~0.1 s of queued work ahead of the band on s
+                junk.mul_(1.0)
+            tm = {}
+            got = pkg.GBT._band_on_device([0] * 4, names, (C, C, C), 64, "sum", 8, None,
+                                          timings=tm)
+        assert tm["path"] == ("raw band" if kind == "raw" else "bank by bank"), tm
+        assert same_bits(got, want)
+    torch.cuda.synchronize()
+
+
+def test_getband_staged_leaves_other_threads_plans_alone(pkg, orc, tmp_path):
+    """The staged/direct choice of the band reduce is an argument of the call
+    (BLDP_BAND_STAGED), not process state: while one
+    thread runs getband(staged=True) over raw banks, another thread's
+    plan-sensitive reduces keep their plans and their bits."""
+    import threading
+
+    import torch
+
+    eng = pkg.engine
+    rng = np.random.default_rng(9)
+    C = pkg.COLON
+    names, banks = [], []
+    for b in range(4):
+        a = np.asfortranarray(rng.integers(0, 256, (1 << 16, 1, 16)).astype(np.float32))
+        f = str(tmp_path / f"t{b}.h5")
+        pkg.fbh5.write(f, dict(foff=-1.0, nfpc=1024), a)
+        names.append(f)
+        banks.append(a)
+    want_band = orc.stitch([orc.reduce(a, 64, 16) for a in banks])
+    shapes = [((65536, 1, 279), 64, 16, [0, 65536, 1, 0, 1, 1, 0, 272, 1]),
+              ((4096, 1, 64), 1024, 64, None), ((512, 1, 4096), 8, 1, None)]
+    xs = []
+    for shape, F, T, w in shapes:
+        a = np.asfortranarray(rng.integers(0, 256, shape).astype(np.float32))
+        x = eng.fb_from_numpy(a)
+        xs.append((a, x, F, T, w, eng.plan(x, F, T, "sum", w), orc.reduce(a, F, T, "sum", w)))
+    stop, errs = threading.Event(), []
+
+    def bander():
+        try:
+            while not stop.is_set():
+                got = pkg.GBT.getband([0] * 4, names, (C, C, C), fqavby=64, tavby=16, staged=True)
+                assert same_bits(got, want_band)
+        except Exception as e:  # noqa: BLE001 (reported below)
+            errs.append(e)
+
+    th = threading.Thread(target=bander)
+    th.start()
+    try:
+        for _ in range(30):
+            for a, x, F, T, w, plan0, want in xs:
+                assert eng.plan(x, F, T, "sum", w) == plan0
+                s = torch.cuda.Stream()
+                with torch.cuda.stream(s):
+                    got = eng.fb_to_numpy(eng.reduce(x, F, T, "sum", w))
+                assert same_bits(got, want)
+    finally:
+        stop.set()
+        th.join()
+    assert not errs, errs
+
+
+def test_device_to_host_through_the_slot_ring(pkg):
+    """bldp_device_to_host (fb_to_numpy(pinned=True), getband's one D2H): the
+    band lands in ordinary numpy memory through the library's pinned slots,
+    bit-exact, for sizes below one slot, a ragged multiple, and more than the
+    whole ring (slot reuse); ordered after the producer's stream; nothing
+    pinned is handed out."""
+    import ctypes
+
+    import torch
+
+    eng = pkg.engine
+    for n in (1, 1000, (32 << 20) // 4 + 3, (300 << 20) // 4 + 5):
+        x = torch.arange(n, dtype=torch.int32, device="cuda")
+        st = {}
+        h = eng.device_to_host(x, stats=st)
+        assert h.dtype == np.int32 and h.shape == (n,)
+        assert np.array_equal(h, np.arange(n, dtype=np.int32)), n
+        assert st["slots"] >= 1 and st["threads"] >= 1
+        assert h.base is None or not isinstance(h.base, torch.Tensor)
+    # ordered after the work queued on the caller's (producer's) stream
+    s = torch.cuda.Stream()
+    y = torch.zeros(1 << 26, dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s):
+        for _ in range(10):
+            y.add_(1.0)
+        h = eng.device_to_host(y)
+    assert (h == 10.0).all()
+    # the Julia-order product copy getband makes
+    z = eng.fb_empty(4096, 2, 7)
+    z.copy_(torch.arange(4096 * 2 * 7, dtype=torch.float32, device="cuda").view(7, 2, 4096)
+            .permute(2, 1, 0))
+    got = eng.fb_to_numpy(z, pinned=True)
+    assert got.flags.f_contiguous and same_bits(got, eng.fb_to_numpy(z))
+    L = pkg._lib.lib()
+    assert L.bldp_device_to_host(None, None, 0, None, None, None) == 0
+    assert L.bldp_device_to_host(None, None, 16, None, None, None) == pkg._lib.BLDP_EINVAL
+    assert L.bldp_device_to_host(ctypes.c_void_p(16), None, -1, None, None, None) == \
+        pkg._lib.BLDP_EINVAL
+
+
 def test_gbt_getkurtosis_fanout_long_windows(pkg, orc, tmp_path):
     """GBT.getkurtosis over 6 files on one device with > 512 spectra: one
     thread per (worker, file) on the same stream and scratch (the leaf
@@ -923,23 +1095,30 @@ def test_cfg5_share_full_size_host_path(pkg, orc):
 
 
 def test_read_probe(pkg):
-    """bldp_read_probe: the pure-read reference bench.py reports (timed by
+    """tools/hbm_probe (build/libbldp_probe.so, a measurement tool outside the
+    product library): the pure-read reference bench.py reports (timed by
     dispatch-carried events), its grid forms, and its argument checks."""
+    import sys
+
     import torch
 
-    r = pkg.engine.read_probe(64 << 20, launches=5)
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "tools"))
+    import hbm_probe
+
+    r = hbm_probe.read_probe(64 << 20, launches=5, pkg=pkg)
     # (a 64 MiB buffer read over and over partly stays in the 256 MB
     # Infinity Cache: 8.7 TB/s measured, above the HBM peak)
-    assert r["bytes"] == 64 << 20 and r["form"] in pkg.engine.PROBE_FORMS and 500 < r["GBps"] < 20000
-    L = pkg._lib.lib()
+    assert r["bytes"] == 64 << 20 and r["form"] in hbm_probe.PROBE_FORMS and 500 < r["GBps"] < 20000
+    L = hbm_probe.lib()
     buf = torch.zeros(1 << 20, dtype=torch.float32, device="cuda")
     for g in (0, 1, 2, 4):  # ragged tail (a partial chunk) in every form
         for m in range(8):
-            assert L.bldp_read_probe(buf.data_ptr(), (4 << 20) - 48, m << 8 | g, None, None,
+            assert L.bldp_probe_read(buf.data_ptr(), (4 << 20) - 48, m << 8 | g, None, None,
                                      None) == 0
-    assert L.bldp_read_probe(None, 0, 0, None, None, None) == 0
-    assert L.bldp_read_probe(buf.data_ptr() + 4, 1024, 0, None, None, None) != 0
-    assert L.bldp_read_probe(buf.data_ptr(), -16, 0, None, None, None) != 0
-    assert L.bldp_read_probe(buf.data_ptr(), 1024, -1, None, None, None) != 0
-    assert L.bldp_read_probe(buf.data_ptr(), 1024, 2048, None, None, None) != 0
+    assert L.bldp_probe_read(None, 0, 0, None, None, None) == 0
+    assert L.bldp_probe_read(buf.data_ptr() + 4, 1024, 0, None, None, None) != 0
+    assert L.bldp_probe_read(buf.data_ptr(), -16, 0, None, None, None) != 0
+    assert L.bldp_probe_read(buf.data_ptr(), 1024, -1, None, None, None) != 0
+    assert L.bldp_probe_read(buf.data_ptr(), 1024, 2048, None, None, None) != 0
     torch.cuda.synchronize()

@@ -717,17 +717,25 @@ def test_band_reduce_multi_device_api(eng, orc, pkg):
 
     devs = (ctypes.c_int * 2)(0, torch.cuda.device_count())  # no such device
     ptrs = (ctypes.c_void_p * 2)(xs[0].data_ptr(), xs[1].data_ptr())
-    rc = L.bldp_band_reduce_multi_f32(2, devs, ptrs, 8192, 2, 48, None, 64, 16, 0, 0, None)
+    rc = L.bldp_band_reduce_multi_f32(2, devs, ptrs, 8192, 2, 48, None, 64, 16, 0, 0, None, 0)
     assert rc == pkg._lib.BLDP_EINVAL
+    devs = (ctypes.c_int * 2)(0, 0)
+    rc = L.bldp_band_reduce_multi_f32(2, devs, ptrs, 8192, 2, 48, None, 64, 16, 0, 0, None, 6)
+    assert rc == pkg._lib.BLDP_EINVAL  # unknown flag bits
+    d = ctypes.c_int(-1)
+    assert L.bldp_peer_access(0, 0, ctypes.byref(d)) == 0 and d.value == 1
+    assert L.bldp_peer_access(0, torch.cuda.device_count(), ctypes.byref(d)) == \
+        pkg._lib.BLDP_EINVAL
+    assert eng.peer_access(0, 0)
 
 
-def test_band_reduce_multi_staged_branch(eng, orc, monkeypatch):
-    """BLDP_FORCE_STAGED=1 sends every bank of bldp_band_reduce_multi_f32
-    through the staged branch a bank off the root takes without peer access
-    (local reduce into a staging buffer, then one strided hipMemcpy2DAsync
-    into the bank's slot of the root's product): bit-exact against the
-    single-launch band reduce, for a one-row and a many-row product."""
-    monkeypatch.setenv("BLDP_FORCE_STAGED", "1")
+def test_band_reduce_multi_staged_branch(eng, orc):
+    """BLDP_BAND_STAGED (staged=True) sends every bank of
+    bldp_band_reduce_multi_f32 through the staged branch a bank off the root
+    takes without peer access (local reduce into a staging buffer, then one
+    strided hipMemcpy2DAsync into the bank's slot of the root's product):
+    bit-exact against the single-launch band reduce, for a one-row and a
+    many-row product."""
     rng = np.random.default_rng(88)
     for shape, F, T, w in (((8192, 2, 48), 64, 16, [0, 8192, 1, 0, 2, 1, 0, 48, 1]),
                            ((4096, 1, 64), 1024, 64, None),
@@ -735,7 +743,7 @@ def test_band_reduce_multi_staged_branch(eng, orc, monkeypatch):
         banks = [np.asfortranarray(rng.integers(0, 256, shape).astype(np.float32))
                  for _ in range(5)]
         xs = [dev(eng, b) for b in banks]
-        got = host(eng, eng.band_reduce_multi(xs, F, T, "sum", w))
+        got = host(eng, eng.band_reduce_multi(xs, F, T, "sum", w, staged=True))
         assert same_bits(got, host(eng, eng.band_reduce(xs, F, T, "sum", w))), shape
         assert same_bits(got, orc.stitch([orc.reduce(b, F, T, "sum", w) for b in banks]))
 
@@ -1265,13 +1273,13 @@ def test_rowt_small_launch_tavby8_long_narrow_window(eng, orc):
 # plan the planner can take must give the oracle's results (integer data:
 # exact in any summation order), so a plan choice is a pure speed choice.
 PLAN_OPTION_VALUES = {
-    "row_split": (1, 2, 4), "max_wg_per_cu": (0, 4), "ts_fill": (0, 1), "narrow_mis": (0, 1, 2),
+    "row_split": (1, 2, 4), "ts_fill": (0, 1), "narrow_mis": (0, 1, 2),
     "t38": (0, 1), "wide_split": (0, 1), "narrow_tpb": (0, 1, 2), "lane": (0, 1, 2),
     "lane3": (0, 1), "lanet": (0, 1), "lanet_pack": (0, 1), "vec_il": (0, 1), "vec_row": (0, 1),
     "row_tpb": (0, 1), "rowt_pack": (0, 1), "rowt_small": (0, 64, 100000), "wavet": (0, 1, 2),
     "unaligned_vec": (0, 1, 2, 3), "row_bpack": (0, 1), "lane_bpack": (0, 1),
     "wave_bpack": (0, 1), "col3": (0, 1), "rowt_narrow8": (0, 1),
-    "st_plain": (0, 2), "il_persist": (0, 1, 2),
+    "st_plain": (0, 1, 2),
 }
 # (nchan, nif, ntime, window, F, T): shapes where the options above change the plan
 PLAN_OPTION_SHAPES = [

@@ -546,6 +546,29 @@ def test_bench_spawns_its_ranks_without_a_launcher():
     assert d["config"]["gathered_ranks"] == [0, 1] and d["value"] == 2.0
 
 
+def test_bench_spawned_ranks_fail_fast():
+    """One self-spawned rank dies before the rendezvous: bench.py stops the
+    others (blocked in init_process_group, whose own timeout is 30 min) and
+    returns that rank's status within seconds (spawn_ranks polls its ranks)."""
+    import subprocess
+    import sys
+    import time
+
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for bad in ("1", "0"):
+        env["BENCH_RENDEZVOUS_FAIL_RANK"] = bad
+        t0 = time.time()
+        r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2",
+                            "--dist-backend", "gloo", "--mode", "rendezvous"],
+                           capture_output=True, text=True, timeout=120, env=env)
+        el = time.time() - t0
+        assert r.returncode == 3, (bad, r.returncode, r.stderr[-2000:])
+        assert el < 60, el
+        assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
 def test_despike_host_keeps_the_result_type(pkg):
     """getband's host despike for non-Float32 bands (integer sums, Float64):
     d[spike:nfpc:end, :, :] .= d[spike-1:nfpc:end, :, :] with spike = nfpc÷2+1

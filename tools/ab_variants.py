@@ -64,8 +64,10 @@ VARIANTS = {
     "rowt8o": {"opts": {"rowt_small": 100000}},  # k_reduce_rowt: always 8 rows per lane
     "rowtn16": {"opts": {"rowt_narrow8": 0}},  # narrow windows back on 16 rows per lane
     "stnt": {"opts": {"st_plain": 0}},  # row / il output stores always non-temporal
-    "ilp1": {"opts": {"il_persist": 1}},  # interleaved path persistent, 1 workgroup per CU
-    "ilp2": {"opts": {"il_persist": 2}},
+    # ("ilp1" / "ilp2", il_persist = 1 / 2: the interleaved path as a persistent
+    # grid, and "cap4", max_wg_per_cu = 4: measured slower in round 4,
+    # profiles/r04/ab_il_persist_r04j.json; removed from the product in round 5,
+    # their sources are at commit 66a9b63)
     # k_reduce_rows with a register budget for 6 / 8 resident waves per SIMD
     "rowsw6": {"patch": [("kernels.hip", "template <int OP, int G4, int S>\n__global__ __launch_bounds__(kBlock)\n"
                           "__attribute__((amdgpu_waves_per_eu(1, kRowMaxWaves)))",
@@ -97,7 +99,6 @@ VARIANTS = {
     "kmidsmall0": {"opts": {"kurt_mid_small": 0}},  # windows of <= 64 spectra on 8 waves too
     "kmid1": {"opts": {"kurt_mid_cpl": 1}},  # k_kurt_mid only (64 channels per workgroup, 4 waves)
     "kold": {"opts": {"kurt_exact": 0}},  # no exact-count k_kurt_regs forms
-    "cap4": {"opts": {"max_wg_per_cu": 4}},  # grid capped at 4 workgroups per CU
     "noil": {"opts": {"vec_il": 0}},  # k_reduce_vec instead of the interleaved k_reduce_il
     "norow": {"opts": {"vec_row": 0}},
     "norowt": {"opts": {"row_tpb": 0}},  # k_reduce_row for short time blocks too

@@ -5,7 +5,13 @@ spectra, integer-valued Float32, uncompressed FBH5 in the page cache), all
 workers on GPU 0; each mode timed over --reps calls after one warm call, and
 checked bit for bit against the other.
 
-    python tools/getband_probe.py [--reps 5] [--json out.json]
+    python tools/getband_probe.py [--reps 5] [--json out.json] [--compressed]
+
+--compressed: the 8 files are rawspec-style compressed FBH5 (HDF5 filter
+32008, chunks (16, 1, 4096) produced by the bitshuffle library: the committed
+fixture chunk tests/golden/bslz4_v1.npz replicated), 272 spectra; the device
+stitch then takes the bank-by-bank branch (chunks decoded on the GPU, each
+bank's reduce writing its slot).
 """
 from __future__ import annotations
 
@@ -26,7 +32,10 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--nchan", type=int, default=65536)
     ap.add_argument("--ntime", type=int, default=279)
+    ap.add_argument("--compressed", action="store_true")
     a = ap.parse_args()
+    if a.compressed:
+        a.ntime -= a.ntime % 16
 
     import numpy as np
     import torch
@@ -37,17 +46,27 @@ def main():
     eng, G = pkg.engine, pkg.GBT
     d = tempfile.mkdtemp(prefix="bldp_band_")
     names = []
+    if a.compressed:
+        z = np.load(os.path.join(REPO, "tests", "golden", "bslz4_v1.npz"), allow_pickle=False)
+        chunk = z["chunk_gamma_chunk_b2048"].tobytes()
+        nchunk = (a.nchan // 4096) * (a.ntime // 16)
     for b in range(8):
-        x = eng.synth(a.nchan, 1, a.ntime, 1024, seed=10 * b + 2, kind=1)  # integers 0..255
         p = os.path.join(d, f"blc0{b}_guppi_59000_12345_X_0011.rawspec.0002.h5")
-        pkg.fbh5.write(p, dict(fch1=8400.0 - 187.5 * b, foff=-187.5 / a.nchan, nchans=a.nchan,
-                               nifs=1, tsamp=1.07, nfpc=1024), eng.fb_to_numpy(x))
+        attrs = dict(fch1=8400.0 - 187.5 * b, foff=-187.5 / a.nchan, nchans=a.nchan, nifs=1,
+                     tsamp=1.07, nfpc=1024)
+        if a.compressed:
+            pkg.fbh5.write_bslz4_chunks(p, attrs, (a.nchan, 1, a.ntime), (16, 1, 4096),
+                                        (chunk for _ in range(nchunk)))
+        else:
+            x = eng.synth(a.nchan, 1, a.ntime, 1024, seed=10 * b + 2, kind=1)  # integers 0..255
+            pkg.fbh5.write(p, attrs, eng.fb_to_numpy(x))
         names.append(p)
     torch.cuda.synchronize()
     workers = [0] * 8
     C = pkg.COLON
     cases = [("F64 T1", dict(fqavby=64)), ("F64 T1 despike", dict(fqavby=64, despike_nfpc=16)),
-             ("F1 T1 despike", dict(despike_nfpc=1024)), ("F64 T9", dict(fqavby=64, tavby=9)),
+             ("F1 T1 despike", dict(despike_nfpc=1024)), ("F64 T9", dict(fqavby=64, tavby=9)) if not a.compressed else
+             ("F64 T8", dict(fqavby=64, tavby=8)),
              ("F64 T16 (cfg2 window 1:272)", dict(fqavby=64, tavby=16, idxs=(C, C, pkg.JRange(1, 272))))]
     res = {}
     for label, kw in cases:
@@ -81,11 +100,13 @@ def main():
     for p in names:
         os.remove(p)
     os.rmdir(d)
-    res["what"] = ("GBT.getband on 8 uncompressed FBH5 files of (%d ch x 1 IF x %d spectra) "
+    res["what"] = ("GBT.getband on 8 %s FBH5 files of (%d ch x 1 IF x %d spectra) "
                    "Float32, every worker on GPU 0, files in the page cache; 'host' = each bank "
                    "reduced on the GPU, copied to the host and concatenated there (round 2), "
                    "despike H2D + kernel + D2H; 'device' = each bank reduced into its slot of the "
-                   "band on the GPU, despike in place, one D2H" % (a.nchan, a.ntime))
+                   "band on the GPU, despike in place, one D2H" %
+                   ("compressed (filter 32008)" if a.compressed else "uncompressed", a.nchan,
+                    a.ntime))
     if a.json:
         with open(a.json, "w") as f:
             json.dump(res, f, indent=1)

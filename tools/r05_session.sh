@@ -1,0 +1,77 @@
+#!/bin/bash
+# Round 5 GPU sessions: per-rank launches of an N-GPU cfg3 run (--local-banks),
+# kernel stats and PMC passes (one counter group per run, MI355X_MICROARCH.md
+# §rocprofv3), SQ counters beside the pure-read probe, tests, bench.
+#   usage: tools/r05_session.sh TAG [steps...]
+#   steps: smoke tests tests_K bench bench_CFG list
+#          prof_CFG[_lbN] pmc_CFG[_lbN] sq_CFG[_lbN] cold_CFG typed typedprof typedpmc typedsq
+#          ab_SUITE getband getbandz
+# CFG[_lbN]: a config, optionally with --local-banks N (one rank's launch of an
+# (8/N)-GPU run).  Every GPU step has its own time limit; after any failure
+# nothing more runs.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=${1:-r05a}; shift || true
+STEPS=${*:-"smoke tests"}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+
+run() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -n 4 "$OUT/$name.log"
+  if [ $rc -ne 0 ]; then echo "== $name failed (rc=$rc): stopping GPU work"; exit $rc; fi
+}
+
+bench_args() {  # CFG[_lbN] -> bench.py arguments for a short profiled run
+  local c=${1%%_lb*} lb=""
+  [ "$c" != "$1" ] && lb="--local-banks ${1##*_lb}"
+  echo "--config $c $lb --steps 20 --warmup 5 --no-cpu-baseline"
+}
+
+SQ="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE GRBM_COUNT"
+
+for s in $STEPS; do
+  case $s in
+    smoke) run smoke 300 python -c "import __graft_entry__ as e; e.smoke()" ;;
+    list) run list 120 rocprofv3 -L ;;
+    tests) run tests 1100 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 \
+          --timeout-method thread ;;
+    tests_*) run "$s" 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 \
+          --timeout-method thread -k "${s#tests_}" ;;
+    bench) run bench 600 python bench.py ;;
+    bench_*) run "$s" 600 python bench.py $(bench_args "${s#bench_}" | sed 's/--no-cpu-baseline//') ;;
+    benchn_*) run "$s" 600 python bench.py $(bench_args "${s#benchn_}") ;;
+    cold_*) run "$s" 600 python bench.py --config "${s#cold_}" --cache cold --no-cpu-baseline ;;
+    prof_*) C=${s#prof_}
+      run "$s" 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$s" -o run \
+        -- python bench.py $(bench_args "$C") ;;
+    pmc_*) C=${s#pmc_}
+      run "pmc_fetch_$C" 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_$C" \
+        -o run -- python bench.py $(bench_args "$C")
+      run "pmc_write_$C" 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$C" \
+        -o run -- python bench.py $(bench_args "$C") ;;
+    sq_*) C=${s#sq_}
+      run "$s" 180 rocprofv3 --pmc $SQ --output-format csv -d "$OUT/$s" -o run \
+        -- python bench.py $(bench_args "$C") ;;
+    ab_*) run "$s" 900 python tools/ab_variants.py --run --suite "${s#ab_}" --rounds 5 \
+          --variants "${AB_VARIANTS:-base}" --json "$OUT/$s.json" ;;
+    typed) run typed 300 python bench.py --mode typed ;;
+    typedprof) run typedprof 300 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d "$OUT/typedprof" -o run -- python bench.py --mode typed --steps 20 --warmup 5 ;;
+    typedpmc)
+      run typedpmc_fetch 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/typedpmc_fetch" \
+        -o run -- python bench.py --mode typed --steps 20 --warmup 5
+      run typedpmc_write 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/typedpmc_write" \
+        -o run -- python bench.py --mode typed --steps 20 --warmup 5 ;;
+    typedsq) run typedsq 180 rocprofv3 --pmc $SQ --output-format csv -d "$OUT/typedsq" -o run \
+        -- python bench.py --mode typed --steps 20 --warmup 5 ;;
+    getband) run getband 600 python tools/getband_probe.py --json "$OUT/getband.json" ;;
+    getbandz) run getbandz 600 python tools/getband_probe.py --compressed --json "$OUT/getbandz.json" ;;
+  esac
+done
+echo "== session done"

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""The pure-read probe (bldp_read_probe) over grid forms and buffer sizes:
+"""The pure-read probe (tools/hbm_probe.hip) over grid forms and buffer sizes:
 which form bench.py's box reference should try.
 
     python tools/read_probe_sweep.py [--json out.json]
@@ -19,13 +19,12 @@ def main():
     ap.add_argument("--wg", default="0,1,2,3,4,8")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
-    import __graft_entry__ as entry
-
-    eng = entry.load_package().engine
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import hbm_probe
     forms = tuple(m << 8 | int(g) for m in (0, 1, 2, 3, 4, 5, 6, 7) for g in a.wg.split(","))
     res = {}
     for mb in (int(m) for m in a.sizes_mb.split(",")):
-        r = eng.read_probe(mb << 20, launches=20, forms=forms, every=True)
+        r = hbm_probe.read_probe(mb << 20, launches=20, forms=forms, every=True)
         res[mb] = r
         print(mb, "MiB best", r["GBps"], "at form", r["form"], flush=True)
         for f in r["forms"]:
