@@ -667,8 +667,12 @@ def bench_typed(args, eng, torch, pkg):
             "data": "synthetic uniform 0..255", "config": {"workload": "typed reduce", **out},
             "roofline": {"bound": "hbm", "achieved": f["GBps_in_plus_out"], "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(f["GBps_in_plus_out"] / HBM_PEAK_GBS, 4),
-                         "traffic": None, "kernel": "k_reduce_typed_vec16 (8-file band, one call "
-                                                    "per step)"}}
+                         "traffic": traffic_from_profile("typed_band", 1),
+                         "traffic_source": traffic_from_profile("typed_band", 1, True)[1],
+                         "kernel": "k_reduce_typed_vec16 (8-file band, one call per step)",
+                         "cache": f["cache"],
+                         "warm": {"ms_per_call": f["warm_ms_per_call"],
+                                  "frac": round(f["warm_GBps_in_plus_out"] / HBM_PEAK_GBS, 4)}}}
 
 
 def main():

@@ -150,6 +150,10 @@ constexpr int kNacc = 8;
 // r02/ab_row_tpb.json, r01_ab_tilecap.json); k_reduce_row / k_reduce_rows,
 // k_reduce_rowt, k_reduce_tile.
 constexpr int kRowMaxWaves = 4, kRowtMaxWaves = 6, kTileMaxWaves = 3;
+// Dynamic LDS per workgroup as a cap on the workgroups resident per CU (160
+// KiB of LDS per CU): the bytes in flight per CU, not the waves, set a
+// stream's HBM rate (round 5, profiles/r05/).  0 = no cap.
+constexpr unsigned kRowShm = 0, kRowtShm = 0, kVecShm = 0;
 // The short-time-block kernels (k_reduce_rowt, k_reduce_narrowt,
 // k_reduce_lanet) also take tavby = 3 and 8, not only 1, 2, 4 (plan option
 // "t38"; the 512-channel 0001 product at tavby = 3 ran one 3-row block per
@@ -1033,6 +1037,18 @@ __global__ __launch_bounds__(kBlock) void k_reduce_vec(const RedArgs a) {
 //   kIlInflight  16-byte loads a lane issues per batch (power of two); 4
 //                measured +0.1..0.7% against 8 on 1-, 2- and 8-bank launches
 constexpr int kIlGpw = 2, kIlInflight = 4;
+//   kIlShm       dynamic LDS bytes per workgroup, an allocation that caps the
+//                workgroups resident per CU at 2 (160 KiB of LDS per CU):
+//                32 KiB of loads in flight per CU instead of ~128 KiB (8
+//                workgroups).  cfg3 4.886 -> 4.629 ms (+5.3%), one bank
+//                +5.5%, tavby 8 +7.1%, the 0002 band at fqavby 1024 +3%; 3 per
+//                CU +1%, 4 per CU +0%, 8 loads in flight per lane at 2 per CU
+//                +1% (profiles/r05/ab_il_r05b.json).  Uncapped, SQ counters
+//                showed 27.5 waves per CU with 53% of their cycles stalled on
+//                issue (VMEM queues full), where the pure read's best form
+//                runs 4 waves per CU 81% parked on s_waitcnt
+//                (profiles/r05/cfg3_sq_summary_r05a.json).
+constexpr unsigned kIlShm = 65536;
 // One tile (GPW groups x one (IF, time block) x one bank) of the interleaved
 // path.
 template <int OP, int K4, int GPW, int IF>
@@ -1620,8 +1636,13 @@ int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 // a few microseconds of command-processor time).
 thread_local hipEvent_t t_ev_start = nullptr, t_ev_stop = nullptr;
 
+// SH: dynamic LDS bytes, here an occupancy cap (kIlShm, kRowShm, ...): a
+// workgroup's allocation above 64 KiB needs the kernel's attribute raised.
 #define BLDP_LAUNCH(KN, GR, BL, SH, ST, ...)                                          \
   do {                                                                                \
+    if ((SH) > 65536u)                                                                \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(KN),                   \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)(SH)); \
     if (t_ev_stop) {                                                                  \
       hipExtLaunchKernelGGL(KN, GR, BL, SH, ST, t_ev_start, t_ev_stop, 0, __VA_ARGS__); \
       t_ev_start = nullptr;                                                           \
@@ -1636,7 +1657,7 @@ hipError_t launch_vec(const RedArgs &a, const Plan &p, hipStream_t s) {
   const int k4c = (a.k4 == 1 || a.k4 == 2 || a.k4 == 4 || a.k4 == 3) ? a.k4 : 0;
 #define BLDP_VEC(L, K)                                                 \
   if (p.lpg == L && k4c == K) {                                        \
-    BLDP_LAUNCH((k_reduce_vec<OP, L, K>), grid, block, 0, s, a); \
+    BLDP_LAUNCH((k_reduce_vec<OP, L, K>), grid, block, kVecShm, s, a); \
     return hipGetLastError();                                          \
   }
   BLDP_VEC(64, 1) BLDP_VEC(64, 2) BLDP_VEC(64, 4) BLDP_VEC(64, 0)
@@ -1757,9 +1778,9 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
                   (unsigned)a.ni, (unsigned)(a.bpack ? a.nbank >> a.tsub_log2 : a.nbank));
 #define BLDP_ROWTK(G, T, N)                                                \
   if (a.bpack)                                                             \
-    BLDP_LAUNCH((k_reduce_rowt<OP, G, T, N, true>), g3, block, 0, s, a);   \
+    BLDP_LAUNCH((k_reduce_rowt<OP, G, T, N, true>), g3, block, kRowtShm, s, a);   \
   else                                                                     \
-    BLDP_LAUNCH((k_reduce_rowt<OP, G, T, N, false>), g3, block, 0, s, a);  \
+    BLDP_LAUNCH((k_reduce_rowt<OP, G, T, N, false>), g3, block, kRowtShm, s, a);  \
   break;
 #define BLDP_ROWTN(T, N)                                                                    \
   switch (a.F / 4) {                                                                        \
@@ -1800,13 +1821,13 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
     const dim3 g3((unsigned)a.blocks_c, (unsigned)(a.ni * a.nto), (unsigned)a.nbank);
 #define BLDP_ROWS(S)                                                                          \
   switch (a.F / 4) {                                                                          \
-    case 1: BLDP_LAUNCH((k_reduce_rows<OP, 1, S>), g3, block, 0, s, a); break;         \
-    case 2: BLDP_LAUNCH((k_reduce_rows<OP, 2, S>), g3, block, 0, s, a); break;         \
-    case 4: BLDP_LAUNCH((k_reduce_rows<OP, 4, S>), g3, block, 0, s, a); break;         \
-    case 8: BLDP_LAUNCH((k_reduce_rows<OP, 8, S>), g3, block, 0, s, a); break;         \
-    case 16: BLDP_LAUNCH((k_reduce_rows<OP, 16, S>), g3, block, 0, s, a); break;       \
-    case 32: BLDP_LAUNCH((k_reduce_rows<OP, 32, S>), g3, block, 0, s, a); break;       \
-    case 64: BLDP_LAUNCH((k_reduce_rows<OP, 64, S>), g3, block, 0, s, a); break;       \
+    case 1: BLDP_LAUNCH((k_reduce_rows<OP, 1, S>), g3, block, kRowShm, s, a); break;         \
+    case 2: BLDP_LAUNCH((k_reduce_rows<OP, 2, S>), g3, block, kRowShm, s, a); break;         \
+    case 4: BLDP_LAUNCH((k_reduce_rows<OP, 4, S>), g3, block, kRowShm, s, a); break;         \
+    case 8: BLDP_LAUNCH((k_reduce_rows<OP, 8, S>), g3, block, kRowShm, s, a); break;         \
+    case 16: BLDP_LAUNCH((k_reduce_rows<OP, 16, S>), g3, block, kRowShm, s, a); break;       \
+    case 32: BLDP_LAUNCH((k_reduce_rows<OP, 32, S>), g3, block, kRowShm, s, a); break;       \
+    case 64: BLDP_LAUNCH((k_reduce_rows<OP, 64, S>), g3, block, kRowShm, s, a); break;       \
     default: return hipErrorInvalidValue;                                                     \
   }
     if (a.rsplit == 2) {
@@ -1822,13 +1843,13 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
   if (p.path == PATH_VEC_ROW) {
     const dim3 g3((unsigned)a.blocks_c, (unsigned)(a.ni * a.nto), (unsigned)a.nbank);
     switch (a.F / 4) {
-      case 1: BLDP_LAUNCH((k_reduce_row<OP, 1>), g3, block, 0, s, a); break;
-      case 2: BLDP_LAUNCH((k_reduce_row<OP, 2>), g3, block, 0, s, a); break;
-      case 4: BLDP_LAUNCH((k_reduce_row<OP, 4>), g3, block, 0, s, a); break;
-      case 8: BLDP_LAUNCH((k_reduce_row<OP, 8>), g3, block, 0, s, a); break;
-      case 16: BLDP_LAUNCH((k_reduce_row<OP, 16>), g3, block, 0, s, a); break;
-      case 32: BLDP_LAUNCH((k_reduce_row<OP, 32>), g3, block, 0, s, a); break;
-      case 64: BLDP_LAUNCH((k_reduce_row<OP, 64>), g3, block, 0, s, a); break;
+      case 1: BLDP_LAUNCH((k_reduce_row<OP, 1>), g3, block, kRowShm, s, a); break;
+      case 2: BLDP_LAUNCH((k_reduce_row<OP, 2>), g3, block, kRowShm, s, a); break;
+      case 4: BLDP_LAUNCH((k_reduce_row<OP, 4>), g3, block, kRowShm, s, a); break;
+      case 8: BLDP_LAUNCH((k_reduce_row<OP, 8>), g3, block, kRowShm, s, a); break;
+      case 16: BLDP_LAUNCH((k_reduce_row<OP, 16>), g3, block, kRowShm, s, a); break;
+      case 32: BLDP_LAUNCH((k_reduce_row<OP, 32>), g3, block, kRowShm, s, a); break;
+      case 64: BLDP_LAUNCH((k_reduce_row<OP, 64>), g3, block, kRowShm, s, a); break;
       default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -1836,10 +1857,10 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
   if (p.path == PATH_VEC_IL) {
     const dim3 g3((unsigned)a.blocks_c, (unsigned)(a.ni * a.nto), (unsigned)a.nbank);
     switch (a.k4) {
-      case 2: BLDP_LAUNCH((k_reduce_il<OP, 2, kIlGpw>), g3, block, 0, s, a); break;
-      case 4: BLDP_LAUNCH((k_reduce_il<OP, 4, kIlGpw>), g3, block, 0, s, a); break;
-      case 8: BLDP_LAUNCH((k_reduce_il<OP, 8, kIlGpw>), g3, block, 0, s, a); break;
-      case 16: BLDP_LAUNCH((k_reduce_il<OP, 16, kIlGpw>), g3, block, 0, s, a); break;
+      case 2: BLDP_LAUNCH((k_reduce_il<OP, 2, kIlGpw>), g3, block, kIlShm, s, a); break;
+      case 4: BLDP_LAUNCH((k_reduce_il<OP, 4, kIlGpw>), g3, block, kIlShm, s, a); break;
+      case 8: BLDP_LAUNCH((k_reduce_il<OP, 8, kIlGpw>), g3, block, kIlShm, s, a); break;
+      case 16: BLDP_LAUNCH((k_reduce_il<OP, 16, kIlGpw>), g3, block, kIlShm, s, a); break;
       default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -1934,6 +1955,7 @@ const PlanOptDef kPlanOpts[OPT_COUNT] = {
     {"col3", 1, 0, 1},            // fqavby = 12, short time blocks: k_reduce_col3 (float4 columns)
     {"rowt_narrow8", 1, 0, 1},    // k_reduce_rowt: 8 rows per lane on <= 128-column windows too
     {"st_plain", 1, 0, 2},        // row / il stores: 0 always nt, 1 plain below 2 GB of traffic, 2 always plain
+    {"typed_pipe", 0, 0, 8},      // k_reduce_typed_vec16p: N persistent workgroups per CU (0: off)
 };
 struct PlanOpts {
   std::atomic<int64_t> v[OPT_COUNT];  // -1 = no override

@@ -75,7 +75,7 @@ extern "C" {
  *    the process-wide "force_staged" option and BLDP_FORCE_STAGED);
  *    bldp_peer_access; bldp_device_to_host; bldp_plan_option checks each
  *    option's domain; bldp_read_probe moved out of the product library
- *    (tools/read_probe.hip, build/libbldp_probe.so); plan options
+ *    (tools/hbm_probe.hip, build/libbldp_probe.so); plan options
  *    "force_staged", "il_persist", "max_wg_per_cu" removed */
 #define BLDP_ABI_VERSION 4
 
@@ -149,7 +149,8 @@ BLDP_API int bldp_reduce_plan_f32(const float *in, int64_t nchan, int64_t nif, i
  *   "vec_row", "row_tpb", "rowt_pack", "rowt_small", "wavet",
  *   "unaligned_vec", "kurt_exact", "kurt_mid_cpl", "kurt_mid_small",
  *   "kurt_leaf_narrow", "kurt_leaf_tile", "typed_vec", "typed_rows",
- *   "row_bpack", "lane_bpack", "wave_bpack", "col3", "rowt_narrow8", "st_plain"
+ *   "row_bpack", "lane_bpack", "wave_bpack", "col3", "rowt_narrow8", "st_plain",
+ *   "typed_pipe"
  *                    which kernel a reduce / kurtosis / typed shape takes
  *                    (csrc/kernels.hip kPlanOpts: defaults, meanings and the
  *                    values each option accepts).

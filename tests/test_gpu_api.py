@@ -855,6 +855,10 @@ def test_bench_json_contract():
     pr = rf["box_read_probe"]
     assert pr["bytes"] == rf["bytes_per_launch"] // 16 * 16 and 0 < pr["GBps"] < 20000.0
     assert rf["frac_of_box_read"] == pytest.approx(rf["achieved"] / pr["GBps"], rel=1e-3)
+    # cfg1 (71 MB a launch) runs cold by default: the launches rotate over
+    # >= 1 GiB of copies, the probe too, and the warm figure is beside it
+    assert rf["cache"].startswith("cold") and pr["copies"] >= 15
+    assert rf["warm"]["kernel_ms"] > 0 and rf["warm"]["frac"] > 0
     cb = d["cpu_baseline"]
     assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1
     assert "workload" in d["config"]

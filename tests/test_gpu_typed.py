@@ -256,6 +256,12 @@ def test_typed_vec_kernel_matches_oracle(pkg, eng, orc, dt):
             for rows in (8, 16):  # larger one-batch row counts
                 with pkg._lib.plan_option("typed_rows", rows):
                     assert same(eng.fb_to_numpy(eng.reduce(x, F, T, op)), got), (dt, op, rows)
+                    with pkg._lib.plan_option("typed_pipe", 1):
+                        assert same(eng.fb_to_numpy(eng.reduce(x, F, T, op)), got), \
+                            (dt, op, rows, "typed_pipe 1")
+            for pipe in (1, 2, 8):  # the persistent pipelined form (k_reduce_typed_vec16p)
+                with pkg._lib.plan_option("typed_pipe", pipe):
+                    assert same(eng.fb_to_numpy(eng.reduce(x, F, T, op)), got), (dt, op, pipe)
         # a window: channels from group 2 on, spectra 2.. (a misaligned row start)
         w = [2 * F, nc - 2 * F, 1, 0, ni, 1, 1, (nt - 1) // T * T, 1]
         for op in ("sum", "max"):

@@ -46,6 +46,12 @@ def _pre(flags):
 
 K = "kernels.hip"
 KU = "kurtosis.hip"
+_S0 = "constexpr unsigned kRowShm = 0, kRowtShm = 0, kVecShm = 0;"
+
+
+def RS(row=0, rowt=0, vec=0):
+    """Patch of the row / rowt / vector kernels' LDS occupancy caps."""
+    return (K, _S0, f"constexpr unsigned kRowShm = {row}, kRowtShm = {rowt}, kVecShm = {vec};")
 VARIANTS = {
     "base": "",  # the product build
     "pre": _pre(""),  # the product build before the knobs left the sources (same kernels)
@@ -124,6 +130,26 @@ VARIANTS = {
                         "constexpr int kIlGpw = 4, kIlInflight = 4;")]},
     "ilb8": {"patch": [(K, "constexpr int kIlGpw = 2, kIlInflight = 4;",
                         "constexpr int kIlGpw = 2, kIlInflight = 8;")]},
+    # round 5: bytes in flight per CU.  Workgroups resident per CU capped by an
+    # LDS allocation (kIlShm, kRowShm, kRowtShm, kVecShm: 96 / 64 / 48 / 36 KiB
+    # = 1 / 2 / 3 / 4 workgroups of 160 KiB) x loads in flight per lane.
+    # (round 5 first pass, profiles/r05/ab_il_r05b.json: ilo2 = 2 per CU won
+    # and is the product default; ilo3 / ilo4 / ilo2b8 / ilo4b8 / ilb8 lost)
+    "ilnocap": {"patch": [(K, "constexpr unsigned kIlShm = 65536;", "constexpr unsigned kIlShm = 0;")]},
+    "il1b8": {"patch": [(K, "constexpr unsigned kIlShm = 65536;", "constexpr unsigned kIlShm = 98304;"),
+                        (K, "constexpr int kIlGpw = 2, kIlInflight = 4;",
+                         "constexpr int kIlGpw = 2, kIlInflight = 8;")]},
+    "il2b2": {"patch": [(K, "constexpr int kIlGpw = 2, kIlInflight = 4;",
+                         "constexpr int kIlGpw = 2, kIlInflight = 2;")]},
+    "il2g4": {"patch": [(K, "constexpr int kIlGpw = 2, kIlInflight = 4;",
+                         "constexpr int kIlGpw = 4, kIlInflight = 4;")]},
+    "rowo1": {"patch": [RS(row=98304)]},
+    "rowo2": {"patch": [RS(row=65536)]},
+    "rowo4": {"patch": [RS(row=36864)]},
+    "rowto2": {"patch": [RS(rowt=65536)]},
+    "rowto4": {"patch": [RS(rowt=36864)]},
+    "veco2": {"patch": [RS(vec=65536)]},
+    "veco4": {"patch": [RS(vec=36864)]},
     "rowmw6": {"patch": [(K, "constexpr int kRowMaxWaves = 4,", "constexpr int kRowMaxWaves = 6,")]},
     "rownocap": {"patch": [(K, "constexpr int kRowMaxWaves = 4,", "constexpr int kRowMaxWaves = 8,")]},
     "rowtmw4": {"patch": [(K, "kRowtMaxWaves = 6,", "kRowtMaxWaves = 4,")]},
@@ -376,6 +402,40 @@ def run(names, rounds, iters, suite="main"):
             band_case(f"0001 F{F} T1", b4, F, 1, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
         band_case("0001 F1 T2", b4, 1, 2, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
         band_case("0001 F1 T4", b4, 1, 4, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
+        cases_done = True
+    elif suite == "il":  # the interleaved kernel: the north-star band and one rank's share
+        band_case("cfg3 8 banks F1024 T16", b3, 1024, 16)
+        band_case("cfg3 4 banks F1024 T16", b3[:4], 1024, 16)
+        band_case("cfg3 2 banks F1024 T16", b3[:2], 1024, 16)
+        band_case("cfg3 1 bank F1024 T16", b3[:1], 1024, 16)
+        band_case("cfg3 8 banks F512 T16", b3, 512, 16)
+        band_case("cfg3 8 banks F4096 T16", b3, 4096, 16)
+        band_case("cfg3 8 banks F1024 T8", b3, 1024, 8, [0, 1 << 26, 1, 0, 1, 1, 0, 8, 1])
+        del b3
+        b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
+        band_case("0002 band F1024 T16", b2, 1024, 16, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
+        band_case("0002 band F512 T16", b2, 512, 16, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
+        cases_done = True
+    elif suite == "occ":  # round 5: occupancy caps over the reduce kernels' main shapes
+        band_case("cfg3 8 banks F1024 T16", b3, 1024, 16)
+        band_case("cfg3 1 bank F1024 T16", b3[:1], 1024, 16)
+        band_case("0000 band F64 T16", b3, 64, 16)
+        band_case("0000 band F64 T1", b3, 64, 1)
+        band_case("0000 band F8 T16", b3, 8, 16)
+        del b3
+        b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
+        w272 = [0, 65536, 1, 0, 1, 1, 0, 272, 1]
+        band_case("cfg2 F64 T16", b2, 64, 16, w272)
+        band_case("cfg1 F64 T16", b2[:1], 64, 16, w272)
+        band_case("0002 band F64 T1", b2, 64, 1)
+        band_case("0002 band F16 T1", b2, 16, 1)
+        band_case("0002 band F256 T16", b2, 256, 16, w272)
+        band_case("0002 band F8 T9", b2, 8, 9)
+        del b2
+        b4 = [eng.synth(512, 1, 880000, 8, seed=10 * b + 1, kind=0) for b in range(8)]
+        band_case("cfg4 F8 T1024", b4, 8, 1024, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
+        band_case("0001 band F8 T1", b4, 8, 1, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
+        band_case("0001 band F64 T16", b4, 64, 16, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
         cases_done = True
     elif suite == "il1":  # large groups with short time blocks: interleaved vs wave kernel
         for F, T in ((1024, 1), (512, 1), (2048, 1), (4096, 1), (1024, 2), (1024, 4)):
@@ -726,7 +786,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--suite", default="main", choices=["main", "rows", "t1_0001", "wavet", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy", "wide", "grid0", "grid1", "t38", "lane3", "kgrid", "lanetpack", "kshort", "kfile"])
+    ap.add_argument("--suite", default="main", choices=["main", "il", "occ", "rows", "t1_0001", "wavet", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy", "wide", "grid0", "grid1", "t38", "lane3", "kgrid", "lanetpack", "kshort", "kfile"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:

@@ -33,7 +33,17 @@ def main():
     ap.add_argument("--nchan", type=int, default=65536)
     ap.add_argument("--ntime", type=int, default=279)
     ap.add_argument("--compressed", action="store_true")
+    ap.add_argument("--threads", type=int, default=0,
+                    help="reader threads (BLDP_READ_THREADS; 0: the library's default, 16)")
+    ap.add_argument("--batch-mb", type=int, default=0,
+                    help="pinned slot size (BLDP_NATIVE_BATCH_MB; 0: the default, 32)")
+    ap.add_argument("--cases", default="",
+                    help="comma-separated case labels to run (default: all)")
     a = ap.parse_args()
+    if a.threads:
+        os.environ["BLDP_READ_THREADS"] = str(a.threads)
+    if a.batch_mb:
+        os.environ["BLDP_NATIVE_BATCH_MB"] = str(a.batch_mb)
     if a.compressed:
         a.ntime -= a.ntime % 16
 
@@ -68,7 +78,10 @@ def main():
              ("F1 T1 despike", dict(despike_nfpc=1024)), ("F64 T9", dict(fqavby=64, tavby=9)) if not a.compressed else
              ("F64 T8", dict(fqavby=64, tavby=8)),
              ("F64 T16 (cfg2 window 1:272)", dict(fqavby=64, tavby=16, idxs=(C, C, pkg.JRange(1, 272))))]
-    res = {}
+    if a.cases:
+        want = set(a.cases.split(","))
+        cases = [c for c in cases if c[0] in want]
+    res = {"reader_threads": a.threads or "default", "batch_mb": a.batch_mb or "default"}
     for label, kw in cases:
         out = {}
         kw = dict(kw)

@@ -60,7 +60,10 @@ for s in $STEPS; do
         -- python bench.py $(bench_args "$C") ;;
     ab_*) run "$s" 900 python tools/ab_variants.py --run --suite "${s#ab_}" --rounds 5 \
           --variants "${AB_VARIANTS:-base}" --json "$OUT/$s.json" ;;
+    kurt_*) run "$s" 300 python bench.py --mode kurtosis --config "${s#kurt_}" ;;
     typed) run typed 300 python bench.py --mode typed ;;
+    typedwarm) run typedwarm 300 python bench.py --mode typed --cache warm ;;
+    typedpipe_*) run "$s" 300 python bench.py --mode typed --plan-option typed_pipe="${s#typedpipe_}" ;;
     typedprof) run typedprof 300 rocprofv3 --kernel-trace --stats --output-format csv \
         -d "$OUT/typedprof" -o run -- python bench.py --mode typed --steps 20 --warmup 5 ;;
     typedpmc)
@@ -72,6 +75,8 @@ for s in $STEPS; do
         -- python bench.py --mode typed --steps 20 --warmup 5 ;;
     getband) run getband 600 python tools/getband_probe.py --json "$OUT/getband.json" ;;
     getbandz) run getbandz 600 python tools/getband_probe.py --compressed --json "$OUT/getbandz.json" ;;
+    getband_t*) run "$s" 600 python tools/getband_probe.py --threads "${s#getband_t}" \
+        --cases "F64 T1,F1 T1 despike" --json "$OUT/$s.json" ;;
   esac
 done
 echo "== session done"
