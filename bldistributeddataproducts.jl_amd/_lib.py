@@ -100,6 +100,8 @@ SIGNATURES = {
     "bldp_bslz4_error": ([P, P], I),
     "bldp_chunks_to_device": ([I, I64, P, P, P, P, I64, P, P, P, I64, P, I64, I64, P, P, P, P],
                               I),
+    "bldp_file_chunks_to_device": ([I64, P, P, P, P, P, I64, P, P, P, I64, P, I64, I64, P, P, P,
+                                    P], I),
     "bldp_runs_to_device": ([I, I64, P, P, P, I64, I64, I, P, P, P], I),
     "bldp_file_runs_to_device": ([I64, P, P, P, P, I64, I64, I, P, P, P], I),
     "bldp_comm_id": ([P], I),

@@ -255,13 +255,14 @@ bool vec_ok(const Geo &g) { return g.cs == 1 && g.off % 4 == 0 && pitch_ok(g); }
 // realigning kernels keep those); kurtosis c0=1 cfg4 5.79 -> 2.45 ms, cfg3
 // 11.85 -> 6.64 ms (leaf / register paths instead of the two-pass / mid
 // ones).  0 = off; 1 = reduce windows where it pays (below); 2 (default) =
-// 1 + kurtosis; 3 = every unit-step reduce window + kurtosis.
+// 1 + kurtosis.  (3, every unit-step reduce window: never won; removed in
+// round 5.)
 // A dword-aligned unit-step reduce window that is not 16-byte aligned goes to
 // the vector / narrow paths when that measured faster than the realigning
 // kernels, or when the alternative is the scalar path (pitches that are not
 // multiples of 4 floats).
 bool unaligned_vec_pays(int64_t F, bool rows16) {
-  if (opt(OPT_UNALIGNED_VEC) >= 3 || !rows16) return true;
+  if (!rows16) return true;
   return F == 1 || (F % 4 == 0 && F <= 256);
 }
 

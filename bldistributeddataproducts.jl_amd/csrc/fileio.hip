@@ -257,8 +257,10 @@ struct PostedJob {
 
 }  // namespace
 
+// fds: one descriptor per chunk (the chunks of several files -- a band's banks
+// -- in one stream of batches), or NULL: every chunk is in `fd`.
 static int chunks_to_device(
-    int fd, int64_t nchunk, const int64_t *file_off, const int64_t *stored_len,
+    int fd, const int *fds, int64_t nchunk, const int64_t *file_off, const int64_t *stored_len,
     const int64_t *stage_off, const uint32_t *filter_mask, int64_t nbatch, const int64_t *batch_end,
     void *host_pinned, void *dev_stage, int64_t stage_bytes, void *dev_out, int64_t out_chunk_bytes,
     int64_t out_bytes, int *err_dev, void *copy_stream, void *stream, double *stats) {
@@ -279,6 +281,8 @@ static int chunks_to_device(
   for (int64_t k = 0; k < nchunk; ++k) {
     if (stored_len[k] < 0 || stage_off[k] < 0 || file_off[k] < 0)
       return bldp::set_error(BLDP_EINVAL, "chunks_to_device: negative offset or size");
+    if (fds && stored_len[k] && fds[k] < 0)
+      return bldp::set_error(BLDP_EINVAL, "chunks_to_device: chunk %lld has no file", (long long)k);
     if (stored_len[k] > stage_bytes - stage_off[k])
       return bldp::set_error(BLDP_EINVAL, "chunks_to_device: chunk %lld overruns the %lld-byte "
                              "staging buffers", (long long)k, (long long)stage_bytes);
@@ -321,13 +325,15 @@ static int chunks_to_device(
         continue;
       }
       int64_t f = file_off[k], h = stage_off[k], n = stored_len[k];
+      const int kfd = fds ? fds[k] : -1;
       int64_t q = k + 1;
-      while (q < k1 && stored_len[q] && file_off[q] == f + n && stage_off[q] == h + n) {
+      while (q < k1 && stored_len[q] && file_off[q] == f + n && stage_off[q] == h + n &&
+             (!fds || fds[q] == kfd)) {
         n += stored_len[q];
         ++q;
       }
       for (int64_t x = 0; x < n; x += piece)
-        j.pieces.push_back({f + x, h + x, std::min(piece, n - x), (int32_t)b, -1});
+        j.pieces.push_back({f + x, h + x, std::min(piece, n - x), (int32_t)b, kfd});
       k = q;
     }
     j.left[b].store((int64_t)(j.pieces.size() - first));
@@ -561,7 +567,24 @@ extern "C" BLDP_API int bldp_chunks_to_device(
     void *host_pinned, void *dev_stage, int64_t stage_bytes, void *dev_out, int64_t out_chunk_bytes,
     int64_t out_bytes, int *err_dev, void *copy_stream, void *stream, double *stats) {
   try {
-    return chunks_to_device(fd, nchunk, file_off, stored_len, stage_off, filter_mask, nbatch,
+    return chunks_to_device(fd, nullptr, nchunk, file_off, stored_len, stage_off, filter_mask,
+                            nbatch, batch_end, host_pinned, dev_stage, stage_bytes, dev_out,
+                            out_chunk_bytes, out_bytes, err_dev, copy_stream, stream, stats);
+  } catch (const std::bad_alloc &) {
+    return bldp::set_error(BLDP_ENOMEM, "chunks_to_device: out of host memory");
+  } catch (...) {
+    return bldp::set_error(BLDP_EINVAL, "chunks_to_device: unexpected C++ exception");
+  }
+}
+
+extern "C" BLDP_API int bldp_file_chunks_to_device(
+    int64_t nchunk, const int *fd, const int64_t *file_off, const int64_t *stored_len,
+    const int64_t *stage_off, const uint32_t *filter_mask, int64_t nbatch, const int64_t *batch_end,
+    void *host_pinned, void *dev_stage, int64_t stage_bytes, void *dev_out, int64_t out_chunk_bytes,
+    int64_t out_bytes, int *err_dev, void *copy_stream, void *stream, double *stats) {
+  if (nchunk > 0 && !fd) return bldp::set_error(BLDP_EINVAL, "chunks_to_device: null fd array");
+  try {
+    return chunks_to_device(-1, fd, nchunk, file_off, stored_len, stage_off, filter_mask, nbatch,
                             batch_end, host_pinned, dev_stage, stage_bytes, dev_out,
                             out_chunk_bytes, out_bytes, err_dev, copy_stream, stream, stats);
   } catch (const std::bad_alloc &) {

@@ -1873,10 +1873,7 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
       BLDP_LAUNCH((k_reduce_narrow<OP, 2>), grid, block, 0, s, a);
     e = hipGetLastError();
   } else if (p.path == PATH_NARROW_MIS) {
-    if (a.F == 1)
-      BLDP_LAUNCH((k_reduce_narrow_mis<OP, 1>), grid, block, 0, s, a);
-    else
-      BLDP_LAUNCH((k_reduce_narrow_mis<OP, 2>), grid, block, 0, s, a);
+    BLDP_LAUNCH((k_reduce_narrow_mis<OP, 1>), grid, block, 0, s, a);
     e = hipGetLastError();
   } else if (p.path == PATH_LANE) {
     switch (a.F) {
@@ -1925,11 +1922,11 @@ struct PlanOptDef {
 const PlanOptDef kPlanOpts[OPT_COUNT] = {
     {"row_split", -1, 1, 4},      // k_reduce_row's block over 1 / 2 / 4 workgroup slices; -1 by launch size
     {"ts_fill", 1, 0, 1},         // narrow vector-path windows split time over idle waves
-    {"narrow_mis", 1, 0, 2},      // misaligned F = 1 (2: and F = 2) on k_reduce_narrow_mis
+    {"narrow_mis", 1, 0, 1},      // misaligned F = 1 on k_reduce_narrow_mis
     {"t38", 1, 0, 1},             // tavby = 3, 8 on the short-time-block kernels
     {"wide_split", 1, 0, 1},      // groups > 4096 channels split time by work, not rows
     {"narrow_tpb", 2, 0, 2},      // k_reduce_narrowt: 2 = incl. the copy, 1 = not it, 0 = off
-    {"lane", 1, 0, 2},            // k_reduce_lane: 1 = where the tile path cannot run, 2 = always
+    {"lane", 1, 0, 1},            // k_reduce_lane where the tile path cannot run
     {"lane3", 1, 0, 1},           // fqavby = 3 on the lane kernel everywhere
     {"lanet", 1, 0, 1},           // k_reduce_lanet for small odd groups, short time blocks
     {"lanet_pack", 1, 0, 1},      // narrow lanet windows: 2 / 4 time groups per workgroup
@@ -1939,16 +1936,15 @@ const PlanOptDef kPlanOpts[OPT_COUNT] = {
     {"rowt_pack", 1, 0, 1},       // narrow rowt windows: 2 / 4 time groups per workgroup
     // rowt/narrowt: launches below this many workgroups per CU take 8 (4 at T <= 2) rows
     {"rowt_small", 64, 0, 1 << 20},
-    {"wavet", 1, 0, 2},           // k_reduce_wavet: 1 = where il is a poor fit, 2 = always, 0 = never
-    {"unaligned_vec", 2, 0, 3},   // dword-aligned 16-byte loads: 1 = reduce, 2 = + kurtosis, 3 = all
+    {"wavet", 1, 0, 1},           // k_reduce_wavet where il is a poor fit
+    {"unaligned_vec", 2, 0, 2},   // dword-aligned 16-byte loads: 1 = reduce, 2 = + kurtosis
     {"kurt_exact", 1, 0, 1},      // k_kurt_regs exact-count forms for 16 / 32 spectra
     {"kurt_mid_cpl", 2, 1, 2},    // 2: k_kurt_mid2 (two channels per lane) where it applies
     {"kurt_mid_small", 1, 0, 1},  // k_kurt_mid2 on 4 waves for <= 64 spectra
     // leaf plans below this many waves per CU: one channel per lane
     {"kurt_leaf_narrow", 4, 0, 1 << 20},
-    {"kurt_leaf_tile", 1, 0, 2},  // k_kurt_tile: 1 = narrow short leaves, 2 = every leaf plan
+    {"kurt_leaf_tile", 1, 0, 1},  // k_kurt_tile for narrow short leaves
     {"typed_vec", 1, 0, 1},       // order-free typed reductions on k_reduce_typed_vec
-    {"typed_rows", 4, 4, 16},     // k_reduce_typed_vec16: most rows a workgroup loads in one batch
     {"row_bpack", 1, 0, 1},       // k_reduce_rowt: lane sets over consecutive banks on narrow stitched rows
     {"lane_bpack", 1, 0, 1},      // k_reduce_lanes: lanet's lanes along narrow stitched band rows
     {"wave_bpack", 1, 0, 1},      // k_reduce_wavet: a wave per (bank, group) of <= 16-group stitched rows
@@ -2079,14 +2075,16 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
     tiles = cdiv(nc4, 64) * a.ni * a.nto * a.nbank;
   } else if (words && a.in_cs == 1 && opt(OPT_LANE) >= 1 &&
              (F == 2 || F == 3 || F == 5 || F == 6 || F == 7) &&
-             (opt(OPT_LANE) >= 2 || !rows16 || (opt(OPT_LANE3) && F == 3))) {
+             (!rows16 || (opt(OPT_LANE3) && F == 3))) {
     // small odd / not-multiple-of-4 groups: one lane per output
     p.path = PATH_LANE;
     a.blocks_c = cdiv(a.nco, kBlock);
     tiles = cdiv(a.nco, 64) * a.ni * a.nto * a.nbank;
-  } else if (rows16 && a.in_cs == 1 && ((opt(OPT_NARROW_MIS) >= 1 && F == 1) ||
-                                         (opt(OPT_NARROW_MIS) >= 2 && F == 2))) {
-    // misaligned start, time integration (+ pairs): aligned columns realigned by shuffle
+  } else if (rows16 && a.in_cs == 1 && opt(OPT_NARROW_MIS) >= 1 && F == 1) {
+    // misaligned start, time integration: aligned columns realigned by shuffle
+    // (F = 2 on the same kernel lost to the tile path: 6.06 vs 5.83 ms on the
+    // 0000 band at c0 = 2, profiles/r02/ab_tile_narrow_mis.json; removed in
+    // round 5)
     p.path = PATH_NARROW_MIS;
     a.blocks_c = cdiv(a.nco * F, kMisSpan);
     tiles = a.blocks_c * 4 * a.ni * a.nto * a.nbank;
@@ -2124,7 +2122,7 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
       (a.k4 == 2 || a.k4 == 4 || a.k4 == 8 || a.k4 == 16) &&
       (T == 1 || T == 2 || T == 4 || (t38 && T == 3)) &&  // (T = 8: -8%, ab_t38_r03w)
       a.ts == 1 && a.nchunk == 1 &&
-      (opt(OPT_WAVET) >= 2 || a.nco < 4 || a.ni * a.nto > 65535) && a.ni <= 65535 &&
+      (a.nco < 4 || a.ni * a.nto > 65535) && a.ni <= 65535 &&
       a.nbank <= 65535) {
     const int64_t tb = std::max<int64_t>(1, 16 / (T * a.k4)), rw = tb * (tb >= 2 ? 1 : 4);
     if (a.nco * cdiv(a.nto, 4 * rw) <= INT32_MAX) {

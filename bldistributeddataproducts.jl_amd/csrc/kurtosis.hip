@@ -1135,10 +1135,7 @@ void plan_kurtosis(KurtArgs &k, int num_cus) {
   if (narrow > 0 && kLeafW > 1 && k.nrow * k.nslot * cdivk(k.nc / kLeafW, 64) < num_cus * narrow)
     k.leafw = 1;
   k.leaftile = 0;  // lane groups per channel of k_kurt_tile; 0 = streamed leaves
-  const int64_t ltile = opt(OPT_KURT_LEAF_TILE);
-  if (ltile == 2) {
-    k.leaftile = 2;
-  } else if (ltile == 1 && k.leafw == 1) {
+  if (opt(OPT_KURT_LEAF_TILE) == 1 && k.leafw == 1) {
     const int64_t units = k.nrow * (k.nt <= 1024 ? 1 : k.nslot);  // leaves x rows
     if (units * cdivk(k.nc, 32) <= num_cus)
       k.leaftile = 2;

@@ -604,7 +604,7 @@ __global__ __launch_bounds__(256) void k_kurt_typed_w(const TypedArgs a, double 
 // rows of whole groups, too).
 struct TVec {
   int lpg, k16, tpb;
-  int nr;  // k_reduce_typed_vec16's rows per batch (4, 8, 16), 0: k_reduce_typed_vec
+  int nr;  // k_reduce_typed_vec16's rows per batch (4), 0: k_reduce_typed_vec
   int64_t nct, grid_x;
   int64_t pgrid;  // > 0: k_reduce_typed_vec16p, this many persistent workgroups
 };
@@ -627,12 +627,12 @@ bool typed_vec_plan(const TypedArgs &a, int op, int num_cus, TVec *v) {
   v->lpg = lpg;
   v->k16 = (int)(g16 / lpg);
   v->nct = cdivt(a.nco, 256 / lpg);
-  // time blocks per workgroup: up to typed_rows (4) rows where the blocks
-  // are short, halved while the grid holds fewer than 8 workgroups per CU;
-  // one batch of the next power of two >= 4 rows.  4 rows (20 VGPRs, every
-  // wave resident) beat 8 and 16 (37 / 68 VGPRs) on the 8-bit 0002 file and
-  // band (profiles/r04/typed_rows_r04e.json)
-  const int64_t rows = std::max<int64_t>(4, std::min<int64_t>(16, opt(OPT_TYPED_ROWS)));
+  // time blocks per workgroup: up to 4 rows where the blocks are short,
+  // halved while the grid holds fewer than 8 workgroups per CU; one batch of
+  // 4 rows.  4 rows (20 VGPRs, every wave resident) beat 8 and 16 (37 / 68
+  // VGPRs) on the 8-bit 0002 file and band (profiles/r04/typed_rows_r04e.json;
+  // the 8- and 16-row forms and their option typed_rows removed in round 5)
+  constexpr int64_t rows = 4;
   const bool batch = v->k16 == 1 && a.T <= rows && (a.T & (a.T - 1)) == 0;
   int64_t tpb = std::max<int64_t>(1, std::min<int64_t>(a.nto, (batch ? rows : 16) /
                                                                   std::max<int64_t>(1, a.T)));
@@ -640,8 +640,7 @@ bool typed_vec_plan(const TypedArgs &a, int op, int num_cus, TVec *v) {
   v->tpb = (int)tpb;
   v->nr = 0;
   if (batch) {
-    const int64_t n = tpb * a.T;
-    v->nr = n <= 4 ? 4 : n <= 8 ? 8 : 16;
+    v->nr = 4;  // (tpb * T <= 4)
   }
   v->grid_x = v->nct * cdivt(a.nto, tpb);
   v->pgrid = 0;
@@ -660,21 +659,11 @@ hipError_t launch_typed_vec(const TypedArgs &a, int op, const TVec &v, hipStream
   const dim3 gp((unsigned)std::max<int64_t>(1, v.pgrid));
   switch (op) {
 #define BLDP_TV(O)                                                                            \
-  if (v.pgrid > 0 && v.nr == 4)                                                               \
+  if (v.pgrid > 0)                                                                            \
     hipLaunchKernelGGL((k_reduce_typed_vec16p<TI, O, 4>), gp, b, 0, s, a, v.lpg, v.tpb, v.nct, \
                        ntg, ntiles);                                                          \
-  else if (v.pgrid > 0 && v.nr == 8)                                                          \
-    hipLaunchKernelGGL((k_reduce_typed_vec16p<TI, O, 8>), gp, b, 0, s, a, v.lpg, v.tpb, v.nct, \
-                       ntg, ntiles);                                                          \
-  else if (v.pgrid > 0)                                                                       \
-    hipLaunchKernelGGL((k_reduce_typed_vec16p<TI, O, 16>), gp, b, 0, s, a, v.lpg, v.tpb,      \
-                       v.nct, ntg, ntiles);                                                   \
   else if (v.nr == 4)                                                                         \
     hipLaunchKernelGGL((k_reduce_typed_vec16<TI, O, 4>), g, b, 0, s, a, v.lpg, v.tpb, v.nct); \
-  else if (v.nr == 8)                                                                         \
-    hipLaunchKernelGGL((k_reduce_typed_vec16<TI, O, 8>), g, b, 0, s, a, v.lpg, v.tpb, v.nct); \
-  else if (v.nr == 16)                                                                        \
-    hipLaunchKernelGGL((k_reduce_typed_vec16<TI, O, 16>), g, b, 0, s, a, v.lpg, v.tpb, v.nct); \
   else                                                                                        \
     hipLaunchKernelGGL((k_reduce_typed_vec<TI, O>), g, b, 0, s, a, v.lpg, v.k16, v.tpb, v.nct); \
   break;

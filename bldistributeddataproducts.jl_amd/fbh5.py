@@ -1045,6 +1045,115 @@ def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 
                        packed, timings, t0, t_io, t_dec, batches, total, tab is not None)
 
 
+def band_window_chunked_dev(fnames, idxs, device, timings=None, batch_bytes=64 << 20,
+                            first_batch_bytes=16 << 20):
+    """The same window of several chunked FBH5 files (a band's banks: one
+    dataset shape and chunk shape, compressed with filter 32008 or stored
+    without a filter) on GPU ``device`` as ONE stream of batches
+    (bldp_file_chunks_to_device: the stored chunks of every file read by the
+    native reader threads, copied to the device and decoded there into one
+    chunk grid per bank), instead of one read call per bank
+    (src/gbtworkerfunctions.jl:181-187 for each file, fanned out by
+    GBT.getdata, src/gbt.jl:69-79).  Returns ``(views, rwin)``: each bank's
+    decoded chunk grid as a Julia-order (cc, ci, gt*ct) tensor holding the
+    window, and the window relative to it (the same for every bank), or None
+    when the banks do not qualify (different layouts, a chunk box more than
+    one chunk wide in IF or channel, a chunk index the parser cannot read):
+    the caller then reads bank by bank.  The caller's current stream on the
+    device is ordered after the decode."""
+    import time
+
+    import torch
+
+    from . import _lib
+
+    if not fnames:
+        return None
+    t0 = time.perf_counter()
+    lays = [layout(f) for f in fnames]
+    cdims, chunk = lays[0]["cdims"], lays[0]["chunk"]
+    if chunk is None or len(cdims) != 3 or any(
+            tuple(lay["cdims"]) != tuple(cdims) or tuple(lay["chunk"] or ()) != tuple(chunk)
+            for lay in lays):
+        return None
+    comp = [needs_bslz4(f) for f in fnames]
+    if not all(c or raw_chunked(f) for c, f in zip(comp, fnames)):
+        return None
+    jshape = cdims[::-1]
+    win = to_window(idxs, jshape) or [0, jshape[0], 1, 0, jshape[1], 1, 0, jshape[2], 1]
+    for ax in range(3):
+        st, ct, sp = win[3 * ax: 3 * ax + 3]
+        if ct > 0:
+            last = st + (ct - 1) * sp
+            if min(st, last) < 0 or max(st, last) >= jshape[ax]:
+                raise BoundsError(-6, f"BoundsError: axis {ax + 1} window {st + 1}:{sp}:"
+                                      f"{last + 1} of {jshape[ax]}")
+    nc, ni, nt = win[1], win[4], win[7]
+    kt0, gt = _box(win[6:9], chunk[0])
+    ki0, gi = _box(win[3:6], chunk[1])
+    kc0, gc = _box(win[0:3], chunk[2])
+    if gi != 1 or gc != 1 or nc * ni * nt == 0:
+        return None
+    chunk = tuple(int(c) for c in chunk)
+    cvol = int(np.prod(chunk))
+    tabs = [chunk_index(f) for f in fnames]
+    if any(t is None for t in tabs):
+        return None
+    sl = (slice(kt0, kt0 + gt), slice(ki0, ki0 + gi), slice(kc0, kc0 + gc))
+    faddr = np.concatenate([t["addr"][sl].ravel() for t in tabs]).astype(np.int64)
+    sizes = np.concatenate([t["size"][sl].ravel() for t in tabs]).astype(np.int64)
+    masks = np.concatenate([t["mask"][sl].ravel() if c else np.ones(gt, np.int64)
+                            for t, c in zip(tabs, comp)]).astype(np.uint32)
+    nper = gt * gi * gc
+    bank_of = np.repeat(np.arange(len(fnames), dtype=np.int32), nper)
+    offsets = np.zeros(len(sizes), np.int64)
+    if len(sizes) > 1:
+        offsets[1:] = np.cumsum(sizes[:-1])
+    total = int(sizes.sum())
+    batches = _batches_of(sizes, first_batch_bytes, batch_bytes, True)
+    bend = np.array([k1 for _, k1 in batches], np.int64)
+    dev = torch.device(device)
+    t_setup = time.perf_counter() - t0
+    pinned = torch.empty(total + 16, dtype=torch.uint8, pin_memory=True)
+    with torch.cuda.device(dev):
+        cdev = torch.empty(total + 16, dtype=torch.uint8, device=dev)
+        # chunks never written read as the fill value 0
+        packed = (torch.empty if bool(np.all(sizes > 0)) else torch.zeros)(
+            len(fnames) * nper * cvol, dtype=torch.float32, device=dev)
+        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        stats = (ctypes.c_double * 4)()
+        L = _lib.lib()
+        fds = []
+        try:
+            for f in fnames:
+                fds.append(os.open(f, os.O_RDONLY))
+            fdk = np.asarray(fds, np.int32)[bank_of]
+            sp = _lib.stream_ptr()
+            rc = L.bldp_file_chunks_to_device(
+                len(sizes), fdk.ctypes.data, faddr.ctypes.data, sizes.ctypes.data,
+                offsets.ctypes.data, masks.ctypes.data, len(bend), bend.ctypes.data,
+                pinned.data_ptr(), cdev.data_ptr(), total + 16, packed.data_ptr(), 4 * cvol,
+                4 * packed.numel(), err.data_ptr(), _copy_stream(dev, -1).cuda_stream, sp, stats)
+            # (waits for every queued copy and decode, also after a failed call)
+            rc2 = L.bldp_bslz4_error(err.data_ptr(), sp)
+        finally:
+            for fd in fds:
+                os.close(fd)
+        _lib.check(rc, "bldp_file_chunks_to_device")
+        _lib.check(rc2, "bslz4 decode")
+    ct, ci, cc = chunk
+    views = [packed[b * nper * cvol:(b + 1) * nper * cvol].view(gt * ct, ci, cc).permute(2, 1, 0)
+             for b in range(len(fnames))]
+    rwin = [win[0] - kc0 * cc, nc, win[2], win[3] - ki0 * ci, ni, win[5], win[6] - kt0 * ct, nt,
+            win[8]]
+    if timings is not None:
+        timings.update(setup_ms=t_setup * 1e3, read_decode_ms=(time.perf_counter() - t0) * 1e3,
+                       first_copy_ms=stats[0], reads_ms=stats[1], pieces=int(stats[2]),
+                       threads=int(stats[3]), stored_bytes=total, batches=len(batches),
+                       chunks=len(sizes))
+    return views, rwin
+
+
 def _native_chunks(fname, faddr, sizes, offsets, masks, batches, pinned, cdev, packed, cvol,
                    copy_stream, _lib, torch):
     """bldp_chunks_to_device for the chunks of the box, then the decoder's

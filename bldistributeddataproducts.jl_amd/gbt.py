@@ -222,6 +222,61 @@ def _band_raw(ws, fs, geo, idxs, fqavby, op, tavby, band, root, force_copy, tm):
     tm["reduce_queue_ms"] = (time.perf_counter() - t1) * 1e3
 
 
+def _band_chunked(ws, fs, geo, idxs, fqavby, op, tavby, band, root, force_copy, tm):
+    """Every bank a chunked FBH5 file (filter 32008 or no filter) of one
+    geometry: each GPU reads and decodes its banks' chunks as ONE stream of
+    batches (fbh5.band_window_chunked_dev: bldp_file_chunks_to_device) into
+    one chunk grid per bank, then the band is reduced straight into its vcat
+    slots, as _band_raw does for raw files (one launch on the root, or each
+    GPU writing the root's slots over xGMI).  False when the banks do not
+    qualify (the caller reads bank by bank)."""
+    import time
+
+    import torch
+
+    from . import engine, fbh5
+
+    groups = {}
+    for b, w in enumerate(ws):
+        groups.setdefault(int(w), []).append(b)
+    # the caller's current stream on every device (as in _band_raw)
+    cur = {d: torch.cuda.current_stream(d) for d in set(groups) | {root}}
+    views, rwins = [None] * len(fs), {}
+
+    def read(item):
+        dev, bl = item
+        t = {}
+        with torch.cuda.device(dev), torch.cuda.stream(cur[dev]):
+            got = fbh5.band_window_chunked_dev([fs[b] for b in bl], idxs, f"cuda:{dev}",
+                                               timings=t)
+        if got is None:
+            return dev, None
+        for b, v in zip(bl, got[0]):
+            views[b] = v
+        rwins[dev] = got[1]
+        return dev, t
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(max_workers=len(groups)) as ex:  # one reader per GPU
+        tread = dict(ex.map(read, groups.items()))
+    if any(t is None for t in tread.values()) or len({tuple(w) for w in rwins.values()}) != 1:
+        return False
+    rwin = next(iter(rwins.values()))
+    tm["read"] = {str(d): t for d, t in tread.items()}
+    tm["read_ms"] = (time.perf_counter() - t0) * 1e3
+    t1 = time.perf_counter()
+    if list(groups) == [root] and not force_copy:
+        with torch.cuda.device(root):
+            engine.band_reduce(views, fqavby, tavby, op, rwin, out=band)
+        tm["reduce"] = "bldp_band_reduce_f32 (one launch)"
+    else:
+        engine.band_reduce_multi(views, fqavby, tavby, op, rwin, root=root, out=band,
+                                 staged=force_copy)
+        tm["reduce"] = "bldp_band_reduce_multi_f32" + (" (staged)" if force_copy else "")
+    tm["reduce_queue_ms"] = (time.perf_counter() - t1) * 1e3
+    return True
+
+
 def _band_on_device(ws, fs, idxs, fqavby, op, tavby, nfpc, timings=None, staged=None):
     """One band stitched on the GPU (src/gbt.jl:103): every
     bank is read and reduced on its worker's GPU straight into its vcat slot
@@ -259,9 +314,15 @@ def _band_on_device(ws, fs, idxs, fqavby, op, tavby, nfpc, timings=None, staged=
                   else bool(staged))
     raw = (all(g[0] == "raw" for g in geo) and len({g[1] for g in geo}) == 1
            and os.environ.get("BLDP_NATIVE_READ", "1") != "0")
+    # every bank a chunked FBH5 file of one geometry (the rawspec products:
+    # filter 32008): the band's chunks read and decoded as one stream per GPU
+    chunked = (not raw and all(g[0] == "h5" for g in geo) and len({g[1] for g in geo}) == 1
+               and os.environ.get("BLDP_NATIVE_READ", "1") != "0")
+    if chunked:
+        chunked = _band_chunked(ws, fs, geo, idxs, fqavby, op, tavby, band, root, force_copy, tm)
     if raw:
         _band_raw(ws, fs, geo, idxs, fqavby, op, tavby, band, root, force_copy, tm)
-    else:
+    elif not chunked:
         # every bank is read (compressed chunks decoded) on its own GPU and
         # reduced there straight into its vcat slot on the root: a kernel
         # store over xGMI where the bank's GPU may write the root's memory
@@ -301,7 +362,8 @@ def _band_on_device(ws, fs, idxs, fqavby, op, tavby, nfpc, timings=None, staged=
             engine.despike(band, nco // 64 if nfpc is True else int(nfpc))
         out = engine.fb_to_numpy(band, pinned=True)  # the one device -> host copy
         tm["despike_d2h_ms"] = (time.perf_counter() - t3) * 1e3
-    tm["path"] = "raw band" if raw else ("bank by bank" + (" (staged)" if force_copy else ""))
+    tm["path"] = ("raw band" if raw else "chunked band" if chunked else "bank by bank") + \
+        (" (staged)" if force_copy and not raw else "")
     tm["total_ms"] = (time.perf_counter() - t0) * 1e3
     return out
 

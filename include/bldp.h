@@ -73,10 +73,13 @@ extern "C" {
  *    bldp_reduce_launch_timed / bldp_reduce_release); bldp_plan_option; bldp_file_runs_to_device
  * 4: bldp_band_reduce_multi_f32 takes a flags word (BLDP_BAND_STAGED replaces
  *    the process-wide "force_staged" option and BLDP_FORCE_STAGED);
- *    bldp_peer_access; bldp_device_to_host; bldp_plan_option checks each
+ *    bldp_peer_access; bldp_device_to_host; bldp_file_chunks_to_device;
+ *    bldp_plan_option checks each
  *    option's domain; bldp_read_probe moved out of the product library
  *    (tools/hbm_probe.hip, build/libbldp_probe.so); plan options
- *    "force_staged", "il_persist", "max_wg_per_cu" removed */
+ *    "force_staged", "il_persist", "max_wg_per_cu", "typed_rows" removed, and
+ *    the values that only ever forced a losing form (narrow_mis 2, lane 2,
+ *    wavet 2, unaligned_vec 3, kurt_leaf_tile 2); "typed_pipe" added */
 #define BLDP_ABI_VERSION 4
 
 #if defined(BLDP_BUILD)
@@ -148,7 +151,7 @@ BLDP_API int bldp_reduce_plan_f32(const float *in, int64_t nchan, int64_t nif, i
  *   "narrow_tpb", "lane", "lane3", "lanet", "lanet_pack", "vec_il",
  *   "vec_row", "row_tpb", "rowt_pack", "rowt_small", "wavet",
  *   "unaligned_vec", "kurt_exact", "kurt_mid_cpl", "kurt_mid_small",
- *   "kurt_leaf_narrow", "kurt_leaf_tile", "typed_vec", "typed_rows",
+ *   "kurt_leaf_narrow", "kurt_leaf_tile", "typed_vec",
  *   "row_bpack", "lane_bpack", "wave_bpack", "col3", "rowt_narrow8", "st_plain",
  *   "typed_pipe"
  *                    which kernel a reduce / kurtosis / typed shape takes
@@ -393,6 +396,19 @@ BLDP_API int bldp_chunks_to_device(int fd, int64_t nchunk, const int64_t *file_o
                                    int64_t stage_bytes, void *dev_out, int64_t out_chunk_bytes,
                                    int64_t out_bytes, int *err_dev, void *copy_stream,
                                    void *stream, double *stats);
+
+/* bldp_chunks_to_device over the chunks of several files: chunk k is in the
+ * open file fd[k] (the banks of a band of compressed FBH5 files read as one
+ * stream of batches and decoded into one chunk grid per bank: GBT.getband,
+ * src/gbt.jl:69-79,103; src/gbtworkerfunctions.jl:181-187).  Same staging,
+ * batches, decode, streams, errors and return as bldp_chunks_to_device (ABI 4). */
+BLDP_API int bldp_file_chunks_to_device(int64_t nchunk, const int *fd, const int64_t *file_off,
+                                        const int64_t *stored_len, const int64_t *stage_off,
+                                        const uint32_t *filter_mask, int64_t nbatch,
+                                        const int64_t *batch_end, void *host_pinned,
+                                        void *dev_stage, int64_t stage_bytes, void *dev_out,
+                                        int64_t out_chunk_bytes, int64_t out_bytes, int *err_dev,
+                                        void *copy_stream, void *stream, double *stats);
 
 /* Raw byte runs of a file (an uncompressed contiguous FBH5 `data` dataset or
  * a SIGPROC data block: src/gbtworkerfunctions.jl:171-189) into a dense device

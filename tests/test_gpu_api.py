@@ -174,14 +174,21 @@ def test_getband_raw_band_one_stream(pkg, orc, tmp_path, monkeypatch, force_copy
 
 
 @pytest.mark.parametrize("staged", [False, True])
-def test_getband_compressed_banks_device_stitch(pkg, orc, tmp_path, staged):
-    """A band of compressed (HDF5 filter 32008) banks takes the bank-by-bank
-    branch of the device stitch: each bank's chunks are decoded on its GPU and
-    the reduce there writes the root's vcat slot directly (bldp_peer_access;
-    one GPU: the same device), or, staged, reduces locally and one
-    stream-ordered device copy fills the slot; no host wait per bank.
-    Bit-exact against the host concatenation and the oracle, with and without
-    despike (src/gbt.jl:75-78,101-103; src/gbtworkerfunctions.jl:181-187)."""
+@pytest.mark.parametrize("branch", ["chunked band", "bank by bank"])
+def test_getband_compressed_banks_device_stitch(pkg, orc, tmp_path, monkeypatch, staged, branch):
+    """A band of compressed (HDF5 filter 32008) banks.  "chunked band": every
+    bank's chunks read and decoded as one stream of batches per GPU
+    (bldp_file_chunks_to_device) into one chunk grid per bank, then one band
+    reduce into the vcat slots (staged: bldp_band_reduce_multi_f32's staged
+    branch).  "bank by bank" (the fallback for banks that do not share a
+    layout): each bank's chunks are decoded on its GPU and the reduce there
+    writes the root's vcat slot directly (bldp_peer_access; one GPU: the same
+    device), or, staged, reduces locally and one stream-ordered device copy
+    fills the slot; no host wait per bank.  Bit-exact against the host
+    concatenation and the oracle, with and without despike (src/gbt.jl:75-78,
+    101-103; src/gbtworkerfunctions.jl:181-187)."""
+    if branch == "bank by bank":
+        monkeypatch.setattr(pkg.GBT, "_band_chunked", lambda *a, **k: False)
     rng = np.random.default_rng(4242)
     J, C = pkg.JRange, pkg.COLON
     banks, names = [], []
@@ -200,7 +207,7 @@ def test_getband_compressed_banks_device_stitch(pkg, orc, tmp_path, staged):
         tm = {}
         dev = pkg.GBT._band_on_device(workers, names, idxs, F, op, T, nfpc, timings=tm,
                                       staged=staged)
-        assert tm["path"] == "bank by bank" + (" (staged)" if staged else ""), tm
+        assert tm["path"] == branch + (" (staged)" if staged else ""), tm
         host = pkg.GBT.getband(workers, names, idxs, fqavby=F, tavby=T, fqavfunc=op,
                                despike_nfpc=nfpc, stitch="host")
         assert same_bits(dev, host), (idxs, F, T, op, nfpc)
@@ -211,6 +218,54 @@ def test_getband_compressed_banks_device_stitch(pkg, orc, tmp_path, staged):
         assert same_bits(dev, want), (idxs, F, T, op, nfpc)
         assert same_bits(pkg.GBT.getband(workers, names, idxs, fqavby=F, tavby=T, fqavfunc=op,
                                          despike_nfpc=nfpc, staged=staged), want)
+
+
+def test_getband_chunked_band_mixed_filters_and_fallback(pkg, orc, tmp_path):
+    """The chunked-band read takes compressed and unfiltered chunked banks of
+    one geometry together (unfiltered chunks copied raw, a chunk never written
+    read as 0), and hands banks whose chunk box is several chunks wide in
+    channel back to the bank-by-bank branch; both bit-exact against the
+    oracle."""
+    rng = np.random.default_rng(515)
+    J, C = pkg.JRange, pkg.COLON
+    enc = lambda blk: orc.np_bslz4_encode(blk, 512, lz4=orc.lz4_compress)  # noqa: E731
+    for chunk, want_path in (((8, 1, 2048), "chunked band"), ((8, 1, 512), "bank by bank")):
+        banks, names = [], []
+        for b in range(4):
+            a = np.asfortranarray(rng.integers(0, 200, (2048, 1, 40)).astype(np.float32))
+            f = str(tmp_path / f"m{b}_{chunk[2]}.h5")
+            if b % 2:
+                pkg.fbh5.write(f, dict(foff=-1.0, nfpc=64), a, chunks=chunk)
+            else:
+                pkg.fbh5.write_bslz4(f, dict(foff=-1.0, nfpc=64), a, chunk, enc)
+            banks.append(a)
+            names.append(f)
+        for idxs, F, T, op in (((C, C, C), 64, 8, "sum"), ((J(129, 2048), C, J(3, 34)), 8, 4, "max")):
+            tm = {}
+            got = pkg.GBT._band_on_device([0] * 4, names, idxs, F, op, T, None, timings=tm)
+            assert tm["path"] == want_path, (chunk, tm)
+            win = pkg.idxs.to_window(pkg.sanitizeidxs(idxs), banks[0].shape)
+            want = orc.stitch([orc.reduce(a, F, T, op, win) for a in banks])
+            assert same_bits(got, want), (chunk, idxs, F, T, op)
+    # a compressed band with a chunk never written (fill value 0)
+    a = np.asfortranarray(rng.integers(0, 200, (2048, 1, 32)).astype(np.float32))
+    c = np.ascontiguousarray(a.transpose(2, 1, 0))
+    items, want_a = [], a.copy(order="F")
+    for k in range(4):
+        if k == 2:
+            items.append(None)
+            want_a[:, :, 8 * k:8 * k + 8] = 0.0
+        else:
+            items.append(enc(np.ascontiguousarray(c[8 * k:8 * k + 8])))
+    names = []
+    for b in range(3):
+        f = str(tmp_path / f"hole{b}.h5")
+        pkg.fbh5.write_bslz4_chunks(f, dict(foff=-1.0, nfpc=64), (2048, 1, 32), (8, 1, 2048), items)
+        names.append(f)
+    tm = {}
+    got = pkg.GBT._band_on_device([0] * 3, names, (C, C, C), 16, "sum", 4, None, timings=tm)
+    assert tm["path"] == "chunked band", tm
+    assert same_bits(got, orc.stitch([orc.reduce(want_a, 16, 4)] * 3))
 
 
 @pytest.mark.parametrize("kind", ["raw", "compressed"])
@@ -246,7 +301,7 @@ def test_getband_under_a_caller_stream(pkg, orc, tmp_path, kind):
             tm = {}
             got = pkg.GBT._band_on_device([0] * 4, names, (C, C, C), 64, "sum", 8, None,
                                           timings=tm)
-        assert tm["path"] == ("raw band" if kind == "raw" else "bank by bank"), tm
+        assert tm["path"] == ("raw band" if kind == "raw" else "chunked band"), tm
         assert same_bits(got, want)
     torch.cuda.synchronize()
 

@@ -1273,11 +1273,11 @@ def test_rowt_small_launch_tavby8_long_narrow_window(eng, orc):
 # plan the planner can take must give the oracle's results (integer data:
 # exact in any summation order), so a plan choice is a pure speed choice.
 PLAN_OPTION_VALUES = {
-    "row_split": (1, 2, 4), "ts_fill": (0, 1), "narrow_mis": (0, 1, 2),
-    "t38": (0, 1), "wide_split": (0, 1), "narrow_tpb": (0, 1, 2), "lane": (0, 1, 2),
+    "row_split": (1, 2, 4), "ts_fill": (0, 1), "narrow_mis": (0, 1),
+    "t38": (0, 1), "wide_split": (0, 1), "narrow_tpb": (0, 1, 2), "lane": (0, 1),
     "lane3": (0, 1), "lanet": (0, 1), "lanet_pack": (0, 1), "vec_il": (0, 1), "vec_row": (0, 1),
-    "row_tpb": (0, 1), "rowt_pack": (0, 1), "rowt_small": (0, 64, 100000), "wavet": (0, 1, 2),
-    "unaligned_vec": (0, 1, 2, 3), "row_bpack": (0, 1), "lane_bpack": (0, 1),
+    "row_tpb": (0, 1), "rowt_pack": (0, 1), "rowt_small": (0, 64, 100000), "wavet": (0, 1),
+    "unaligned_vec": (0, 1, 2), "row_bpack": (0, 1), "lane_bpack": (0, 1),
     "wave_bpack": (0, 1), "col3": (0, 1), "rowt_narrow8": (0, 1),
     "st_plain": (0, 1, 2),
 }
@@ -1332,7 +1332,7 @@ def test_plan_options_every_form(pkg, eng, orc, name):
 
 
 KURT_OPTION_VALUES = {"kurt_exact": (0, 1), "kurt_mid_cpl": (1, 2), "kurt_mid_small": (0, 1),
-                      "kurt_leaf_narrow": (0, 4), "kurt_leaf_tile": (0, 1, 2),
+                      "kurt_leaf_narrow": (0, 4), "kurt_leaf_tile": (0, 1),
                       "unaligned_vec": (0, 2)}
 
 

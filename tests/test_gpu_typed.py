@@ -253,12 +253,6 @@ def test_typed_vec_kernel_matches_oracle(pkg, eng, orc, dt):
             assert same(got, want), (dt, (nc, ni, nt, F, T), op)
             with pkg._lib.plan_option("typed_vec", 0):
                 assert same(eng.fb_to_numpy(eng.reduce(x, F, T, op)), got), (dt, op, "typed_vec 0")
-            for rows in (8, 16):  # larger one-batch row counts
-                with pkg._lib.plan_option("typed_rows", rows):
-                    assert same(eng.fb_to_numpy(eng.reduce(x, F, T, op)), got), (dt, op, rows)
-                    with pkg._lib.plan_option("typed_pipe", 1):
-                        assert same(eng.fb_to_numpy(eng.reduce(x, F, T, op)), got), \
-                            (dt, op, rows, "typed_pipe 1")
             for pipe in (1, 2, 8):  # the persistent pipelined form (k_reduce_typed_vec16p)
                 with pkg._lib.plan_option("typed_pipe", pipe):
                     assert same(eng.fb_to_numpy(eng.reduce(x, F, T, op)), got), (dt, op, pipe)

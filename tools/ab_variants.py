@@ -93,9 +93,11 @@ VARIANTS = {
     "wavet4": {"patch": [("kernels.hip", "constexpr int NBAT = TB >= 2 ? 1 : 4,",
                           "constexpr int NBAT = 4,"),
                          ("kernels.hip", "rw = tb * (tb >= 2 ? 1 : 4);", "rw = tb * 4;")]},
+    # (round 5: option values that only forced a losing form were removed from
+    # the product, and their variants with them: wavet2, misf2, unal3, lane2,
+    # ktile2; their last measurements are in profiles/r02..r04)
     "kleafwide": {"opts": {"kurt_leaf_narrow": 0}},  # k_kurt_leaf always 4 channels per lane
     "ktile0": {"opts": {"kurt_leaf_tile": 0}},  # short narrow windows on the streamed leaf lanes
-    "ktile2": {"opts": {"kurt_leaf_tile": 2}},  # every leaf plan read whole into registers
     "lane3off": {"opts": {"lane3": 0}},  # fqavby = 3 with long time blocks on the tile path
     "not38": {"opts": {"t38": 0}},  # tavby = 3, 8 off the short-time-block kernels
     "nowide": {"opts": {"wide_split": 0}},  # fqavby > 4096: time split by row count only
@@ -110,15 +112,11 @@ VARIANTS = {
     "norowt": {"opts": {"row_tpb": 0}},  # k_reduce_row for short time blocks too
     "rowtnopack": {"opts": {"rowt_pack": 0}},
     "nowavet": {"opts": {"wavet": 0}},
-    "wavet2": {"opts": {"wavet": 2}},
     "notsfill": {"opts": {"ts_fill": 0}},
     "nomis": {"opts": {"narrow_mis": 0}},  # misaligned F = 1, 2 windows on the tile path
-    "misf2": {"opts": {"narrow_mis": 2}},  # F = 2 on the realigning narrow kernel too
     "unal0": {"opts": {"unaligned_vec": 0}},  # misaligned unit-step windows: no dword-aligned 16-byte loads
     "unal": {"opts": {"unaligned_vec": 1}},
-    "unal3": {"opts": {"unaligned_vec": 3}},
     "nolane": {"opts": {"lane": 0}},
-    "lane2": {"opts": {"lane": 2}},  # F in {2, 3, 5, 6, 7} on one lane per output everywhere
     # ---- code-shape constants, text patches of the current sources
     "lanets16": {"patch": [(K, "constexpr int kLanetRows = 8;", "constexpr int kLanetRows = 16;")]},
     "batch4": {"patch": [(K, "constexpr int kBatch = 8;", "constexpr int kBatch = 4;")]},

@@ -3,7 +3,7 @@
 # kernel stats and PMC passes (one counter group per run, MI355X_MICROARCH.md
 # §rocprofv3), SQ counters beside the pure-read probe, tests, bench.
 #   usage: tools/r05_session.sh TAG [steps...]
-#   steps: smoke tests tests_K bench bench_CFG list
+#   steps: smoke tests tests_K bench bench_CFG list ab_SUITE[:v1,v2,...]
 #          prof_CFG[_lbN] pmc_CFG[_lbN] sq_CFG[_lbN] cold_CFG typed typedprof typedpmc typedsq
 #          ab_SUITE getband getbandz
 # CFG[_lbN]: a config, optionally with --local-banks N (one rank's launch of an
@@ -58,8 +58,9 @@ for s in $STEPS; do
     sq_*) C=${s#sq_}
       run "$s" 180 rocprofv3 --pmc $SQ --output-format csv -d "$OUT/$s" -o run \
         -- python bench.py $(bench_args "$C") ;;
-    ab_*) run "$s" 900 python tools/ab_variants.py --run --suite "${s#ab_}" --rounds 5 \
-          --variants "${AB_VARIANTS:-base}" --json "$OUT/$s.json" ;;
+    ab_*) A=${s#ab_}; SUITE=${A%%:*}; V=${AB_VARIANTS:-base}; [ "$SUITE" != "$A" ] && V=${A#*:}
+      run "ab_$SUITE" 900 python tools/ab_variants.py --run --suite "$SUITE" --rounds 5 \
+          --variants "$V" --json "$OUT/ab_$SUITE.json" ;;
     kurt_*) run "$s" 300 python bench.py --mode kurtosis --config "${s#kurt_}" ;;
     typed) run typed 300 python bench.py --mode typed ;;
     typedwarm) run typedwarm 300 python bench.py --mode typed --cache warm ;;
