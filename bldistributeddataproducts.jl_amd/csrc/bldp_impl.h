@@ -86,7 +86,7 @@ enum PlanOpt {
   OPT_WIDE_SPLIT, OPT_NARROW_TPB, OPT_LANE, OPT_LANE3, OPT_LANET, OPT_LANET_PACK, OPT_VEC_IL,
   OPT_VEC_ROW, OPT_ROW_TPB, OPT_ROWT_PACK, OPT_ROWT_SMALL, OPT_WAVET, OPT_UNALIGNED_VEC,
   OPT_KURT_EXACT, OPT_KURT_MID_CPL, OPT_KURT_MID_SMALL, OPT_KURT_LEAF_NARROW, OPT_KURT_LEAF_TILE,
-  OPT_TYPED_VEC, OPT_ROW_BPACK, OPT_LANE_BPACK, OPT_WAVE_BPACK, OPT_COL3, OPT_ROWT_NARROW8, OPT_ST_PLAIN, OPT_TYPED_PIPE, OPT_COUNT
+  OPT_TYPED_VEC, OPT_ROW_BPACK, OPT_LANE_BPACK, OPT_WAVE_BPACK, OPT_COL3, OPT_ROWT_NARROW8, OPT_ST_PLAIN, OPT_COUNT
 };
 int64_t plan_opt(int k);
 inline int64_t opt(int k) { return plan_opt(k); }

@@ -1036,7 +1036,9 @@ __global__ __launch_bounds__(kBlock) void k_reduce_vec(const RedArgs a) {
 //                bank, i.e. one rank at N=8, against 4)
 //   kIlInflight  16-byte loads a lane issues per batch (power of two); 4
 //                measured +0.1..0.7% against 8 on 1-, 2- and 8-bank launches
-constexpr int kIlGpw = 2, kIlInflight = 4;
+constexpr int kIlGpw = 2, kIlInflight = 4, kIlGpwK2 = 2;
+// groups per workgroup for K4 float4 per lane per row (kIlGpwK2 at K4 = 2)
+constexpr int il_gpw(int k4) { return k4 == 2 ? kIlGpwK2 : kIlGpw; }
 //   kIlShm       dynamic LDS bytes per workgroup, an allocation that caps the
 //                workgroups resident per CU at 2 (160 KiB of LDS per CU):
 //                32 KiB of loads in flight per CU instead of ~128 KiB (8
@@ -1857,7 +1859,7 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
   if (p.path == PATH_VEC_IL) {
     const dim3 g3((unsigned)a.blocks_c, (unsigned)(a.ni * a.nto), (unsigned)a.nbank);
     switch (a.k4) {
-      case 2: BLDP_LAUNCH((k_reduce_il<OP, 2, kIlGpw>), g3, block, kIlShm, s, a); break;
+      case 2: BLDP_LAUNCH((k_reduce_il<OP, 2, il_gpw(2)>), g3, block, kIlShm, s, a); break;
       case 4: BLDP_LAUNCH((k_reduce_il<OP, 4, kIlGpw>), g3, block, kIlShm, s, a); break;
       case 8: BLDP_LAUNCH((k_reduce_il<OP, 8, kIlGpw>), g3, block, kIlShm, s, a); break;
       case 16: BLDP_LAUNCH((k_reduce_il<OP, 16, kIlGpw>), g3, block, kIlShm, s, a); break;
@@ -1951,7 +1953,6 @@ const PlanOptDef kPlanOpts[OPT_COUNT] = {
     {"col3", 1, 0, 1},            // fqavby = 12, short time blocks: k_reduce_col3 (float4 columns)
     {"rowt_narrow8", 1, 0, 1},    // k_reduce_rowt: 8 rows per lane on <= 128-column windows too
     {"st_plain", 1, 0, 2},        // row / il stores: 0 always nt, 1 plain below 2 GB of traffic, 2 always plain
-    {"typed_pipe", 0, 0, 8},      // k_reduce_typed_vec16p: N persistent workgroups per CU (0: off)
 };
 struct PlanOpts {
   std::atomic<int64_t> v[OPT_COUNT];  // -1 = no override
@@ -2141,9 +2142,9 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
   // (3-D grid, so every dimension must fit)
   if (opt(OPT_VEC_IL) && p.path == PATH_VEC && p.lpg == 64 && a.tpb == 1 &&
       (a.k4 == 2 || a.k4 == 4 || a.k4 == 8 || a.k4 == 16) && a.ts == 1 && a.nchunk == 1 &&
-      cdiv(a.nco, kIlGpw) <= INT32_MAX && a.ni * a.nto <= 65535 && a.nbank <= 65535) {
+      cdiv(a.nco, il_gpw(a.k4)) <= INT32_MAX && a.ni * a.nto <= 65535 && a.nbank <= 65535) {
     p.path = PATH_VEC_IL;
-    a.blocks_c = cdiv(a.nco, kIlGpw);
+    a.blocks_c = cdiv(a.nco, il_gpw(a.k4));
     a.ntiles = a.blocks_c * a.ni * a.nto * a.nbank;
     p.grid = a.ntiles;
   }

@@ -1127,6 +1127,10 @@ hipError_t launch_tree(const KurtArgs &k, char *ws, const KLayout &L, hipStream_
 
 }  // namespace
 
+// Dynamic LDS per workgroup of k_kurt_leaf / k_kurt_mid2 as a cap on the
+// workgroups resident per CU (as kIlShm in kernels.hip); 0 = no cap.
+constexpr unsigned kKurtLeafShm = 0, kKurtMidShm = 0;
+
 void plan_kurtosis(KurtArgs &k, int num_cus) {
   k.K = pw_level(std::max<int64_t>(k.nt, 1));
   k.nslot = (int64_t)2 << k.K;
@@ -1194,7 +1198,7 @@ hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s) {
     // registers sized to a wave's spectra, 8 at a time (occupancy: 113 VGPRs
     // at 48 spectra = 4 waves/SIMD, 80 at 32 = 6, 48 at 16 = 8)
     switch (cdivk(cdivk(k.nt, NW), 8)) {
-#define BLDP_MID2(NR) hipLaunchKernelGGL((k_kurt_mid2<NR, NW>), g1, b2, 0, s, k); break;
+#define BLDP_MID2(NR) hipLaunchKernelGGL((k_kurt_mid2<NR, NW>), g1, b2, kKurtMidShm, s, k); break;
       case 1: BLDP_MID2(8)
       case 2: BLDP_MID2(16)
       case 3: BLDP_MID2(24)
@@ -1245,9 +1249,9 @@ hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s) {
     }
     const dim3 g1((unsigned)cdivk(k.nrow * k.nslot * k.nseg, 4));
     if (k.leafw == 1)
-      hipLaunchKernelGGL((k_kurt_leaf<1, kLeafNB>), g1, block, 0, s, k);
+      hipLaunchKernelGGL((k_kurt_leaf<1, kLeafNB>), g1, block, kKurtLeafShm, s, k);
     else
-      hipLaunchKernelGGL((k_kurt_leaf<kLeafW, kLeafB>), g1, block, 0, s, k);
+      hipLaunchKernelGGL((k_kurt_leaf<kLeafW, kLeafB>), g1, block, kKurtLeafShm, s, k);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return launch_tree<true>(k, ws, L, s);

@@ -404,89 +404,6 @@ __global__ __launch_bounds__(256) void k_reduce_typed_vec16(const TypedArgs a, i
                               to0 + (m >> tsh), co);
 }
 
-// Persistent, software-pipelined form of k_reduce_typed_vec16 (plan option
-// "typed_pipe" = W > 0: W workgroups per CU).  A 0002 band of UInt8 data at
-// fqavby = 64 is 146 MB in ~9000 workgroups of 16 KiB each: every workgroup
-// issues one batch of loads, waits for it once, folds and stores, so the
-// launch is a few rounds of full memory latency.  Here each workgroup walks
-// the tiles t = blockIdx.x + k * gridDim.x (column tile fastest, then time
-// group, IF, bank: the workgroups in flight sweep adjacent bytes of the same
-// rows) and issues tile t + gridDim.x's loads before folding and storing tile
-// t, so a lane always has a batch in flight.  Same folds, same stores: the
-// results are bit-identical to k_reduce_typed_vec16.
-template <typename TI, int OP, int NR>
-__global__ __launch_bounds__(256) void k_reduce_typed_vec16p(const TypedArgs a, int lpg, int tpb,
-                                                             int64_t nct, int64_t ntg,
-                                                             int64_t ntiles) {
-  typedef Vec16<TI, OP> V;
-  typedef typename V::R R;
-  const int tid = threadIdx.x, j = tid % lpg, gl = tid / lpg;
-  const int T = (int)a.T, tsh = __builtin_ctz((unsigned)T);
-  const int64_t ldb = a.in_ld_t * (int64_t)sizeof(TI);
-  struct Tile {
-    const char *p;
-    int64_t co, to0, i, bank;
-    int nb;
-    bool valid;
-  };
-  auto tile = [&](int64_t t) {
-    Tile x;
-    const int64_t ct = t % nct;
-    int64_t r = t / nct;
-    const int64_t tg = r % ntg;
-    r /= ntg;
-    x.i = r % a.ni;
-    x.bank = r / a.ni;
-    x.co = ct * (256 / lpg) + gl;
-    x.to0 = tg * tpb;
-    x.nb = (int)min((int64_t)tpb, a.nto - x.to0);
-    x.valid = x.co < a.nco;
-    x.p = static_cast<const char *>(a.in[x.bank]) +
-          (a.in_off + x.i * a.in_ld_i + x.co * a.F) * (int64_t)sizeof(TI) + 16 * j +
-          x.to0 * T * ldb;
-    return x;
-  };
-  auto load = [&](const Tile &x, uint4 (&q)[NR]) {
-    const int nrow = x.nb * T;
-#pragma unroll
-    for (int m = 0; m < NR; ++m)
-      if (x.valid && m < nrow) q[m] = ld16(x.p + m * ldb);
-  };
-  int64_t t = blockIdx.x;
-  if (t >= ntiles) return;
-  Tile cur = tile(t);
-  uint4 qa[NR];
-  load(cur, qa);
-  for (; t < ntiles; t += gridDim.x) {
-    const int64_t tn = t + gridDim.x;
-    Tile nxt = cur;
-    uint4 qb[NR];
-    if (tn < ntiles) {  // (uniform over the workgroup) the next tile's batch in flight
-      nxt = tile(tn);
-      load(nxt, qb);
-    }
-    const int nrow = cur.nb * T;
-    R r[NR];
-#pragma unroll
-    for (int m = 0; m < NR; ++m)
-      r[m] = (cur.valid && m < nrow) ? V::row(qa[m]) : V::row(make_uint4(0, 0, 0, 0));
-#pragma unroll
-    for (int h = 1; h < NR; h *= 2)
-      if (h < T) {
-#pragma unroll
-        for (int m = 0; m < NR; m += 2 * h) r[m] = V::rcombine(r[m], r[m + h]);
-      }
-#pragma unroll
-    for (int m = 0; m < NR; ++m)
-      if ((m & (T - 1)) == 0 && (m >> tsh) < cur.nb)  // (uniform)
-        typed_vec_store<TI, OP>(a, (typename V::A)r[m], lpg, cur.valid && j == 0, cur.bank,
-                                cur.i, cur.to0 + (m >> tsh), cur.co);
-    cur = nxt;
-#pragma unroll
-    for (int m = 0; m < NR; ++m) qa[m] = qb[m];
-  }
-}
-
 template <typename TI>
 __global__ __launch_bounds__(256) void k_kurt_typed(const TypedArgs a, double *out) {
   const int64_t nrow = a.nco * a.ni * a.nbank;
@@ -602,11 +519,18 @@ __global__ __launch_bounds__(256) void k_kurt_typed_w(const TypedArgs a, double 
 // apply (Float64 sums, 64-bit means and inexact 32-bit means keep the
 // reference's order on k_reduce_typed; windows without dword-aligned 16-byte
 // rows of whole groups, too).
+// Dynamic LDS per k_reduce_typed_vec16 workgroup as a cap on the workgroups
+// resident per CU (as kIlShm in kernels.hip); 0 = no cap.  (Round 5: a
+// persistent, software-pipelined form -- tiles walked by 1..4 workgroups per
+// CU, the next tile's loads issued before the current one's folds -- was
+// slower on the UInt8 0002 band at every width: 72 / 43 / 32 vs 29 us,
+// profiles/r05/typed_pipe_r05d.json; removed.)
+constexpr unsigned kTypedShm = 0;
+
 struct TVec {
   int lpg, k16, tpb;
   int nr;  // k_reduce_typed_vec16's rows per batch (4), 0: k_reduce_typed_vec
   int64_t nct, grid_x;
-  int64_t pgrid;  // > 0: k_reduce_typed_vec16p, this many persistent workgroups
 };
 bool typed_vec_plan(const TypedArgs &a, int op, int num_cus, TVec *v) {
   const int64_t sz = (int64_t)dtype_size(a.dtype);
@@ -643,27 +567,17 @@ bool typed_vec_plan(const TypedArgs &a, int op, int num_cus, TVec *v) {
     v->nr = 4;  // (tpb * T <= 4)
   }
   v->grid_x = v->nct * cdivt(a.nto, tpb);
-  v->pgrid = 0;
-  const int64_t pipe = opt(OPT_TYPED_PIPE);  // persistent workgroups per CU (0: off)
-  if (batch && pipe > 0) {
-    const int64_t ntiles = v->grid_x * a.ni * a.nbank;
-    v->pgrid = std::min<int64_t>(ntiles, pipe * num_cus);
-  }
   return v->grid_x <= INT32_MAX;
 }
 
 template <typename TI>
 hipError_t launch_typed_vec(const TypedArgs &a, int op, const TVec &v, hipStream_t s) {
   const dim3 g((unsigned)v.grid_x, (unsigned)a.ni, (unsigned)a.nbank), b(256);
-  const int64_t ntg = cdivt(a.nto, v.tpb), ntiles = v.grid_x * a.ni * a.nbank;
-  const dim3 gp((unsigned)std::max<int64_t>(1, v.pgrid));
   switch (op) {
 #define BLDP_TV(O)                                                                            \
-  if (v.pgrid > 0)                                                                            \
-    hipLaunchKernelGGL((k_reduce_typed_vec16p<TI, O, 4>), gp, b, 0, s, a, v.lpg, v.tpb, v.nct, \
-                       ntg, ntiles);                                                          \
-  else if (v.nr == 4)                                                                         \
-    hipLaunchKernelGGL((k_reduce_typed_vec16<TI, O, 4>), g, b, 0, s, a, v.lpg, v.tpb, v.nct); \
+  if (v.nr == 4)                                                                              \
+    hipLaunchKernelGGL((k_reduce_typed_vec16<TI, O, 4>), g, b, kTypedShm, s, a, v.lpg, v.tpb,  \
+                       v.nct);                                                                \
   else                                                                                        \
     hipLaunchKernelGGL((k_reduce_typed_vec<TI, O>), g, b, 0, s, a, v.lpg, v.k16, v.tpb, v.nct); \
   break;

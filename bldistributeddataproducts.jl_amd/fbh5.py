@@ -1054,13 +1054,15 @@ def band_window_chunked_dev(fnames, idxs, device, timings=None, batch_bytes=64 <
     native reader threads, copied to the device and decoded there into one
     chunk grid per bank), instead of one read call per bank
     (src/gbtworkerfunctions.jl:181-187 for each file, fanned out by
-    GBT.getdata, src/gbt.jl:69-79).  Returns ``(views, rwin)``: each bank's
-    decoded chunk grid as a Julia-order (cc, ci, gt*ct) tensor holding the
-    window, and the window relative to it (the same for every bank), or None
-    when the banks do not qualify (different layouts, a chunk box more than
-    one chunk wide in IF or channel, a chunk index the parser cannot read):
-    the caller then reads bank by bank.  The caller's current stream on the
-    device is ordered after the decode."""
+    GBT.getdata, src/gbt.jl:69-79).  Returns ``(views, rwin)``: when the
+    chunk box is one chunk wide in IF and channel, each bank's decoded chunk
+    grid as a Julia-order (cc, ci, gt*ct) tensor holding the window, and the
+    window relative to it (the same for every bank); otherwise each bank's
+    window gathered from its chunk grid (bldp_unchunk_f32) into a dense
+    Julia-order tensor, and None.  None when the banks do not qualify
+    (different layouts, a chunk index the parser cannot read): the caller then
+    reads bank by bank.  The caller's current stream on the device is ordered
+    after the decode."""
     import time
 
     import torch
@@ -1092,7 +1094,7 @@ def band_window_chunked_dev(fnames, idxs, device, timings=None, batch_bytes=64 <
     kt0, gt = _box(win[6:9], chunk[0])
     ki0, gi = _box(win[3:6], chunk[1])
     kc0, gc = _box(win[0:3], chunk[2])
-    if gi != 1 or gc != 1 or nc * ni * nt == 0:
+    if nc * ni * nt == 0:
         return None
     chunk = tuple(int(c) for c in chunk)
     cvol = int(np.prod(chunk))
@@ -1102,9 +1104,10 @@ def band_window_chunked_dev(fnames, idxs, device, timings=None, batch_bytes=64 <
     sl = (slice(kt0, kt0 + gt), slice(ki0, ki0 + gi), slice(kc0, kc0 + gc))
     faddr = np.concatenate([t["addr"][sl].ravel() for t in tabs]).astype(np.int64)
     sizes = np.concatenate([t["size"][sl].ravel() for t in tabs]).astype(np.int64)
-    masks = np.concatenate([t["mask"][sl].ravel() if c else np.ones(gt, np.int64)
-                            for t, c in zip(tabs, comp)]).astype(np.uint32)
     nper = gt * gi * gc
+    # unfiltered files: every stored chunk holds raw elements (filter mask bit 0)
+    masks = np.concatenate([t["mask"][sl].ravel() if c else np.ones(nper, np.int64)
+                            for t, c in zip(tabs, comp)]).astype(np.uint32)
     bank_of = np.repeat(np.arange(len(fnames), dtype=np.int32), nper)
     offsets = np.zeros(len(sizes), np.int64)
     if len(sizes) > 1:
@@ -1142,10 +1145,27 @@ def band_window_chunked_dev(fnames, idxs, device, timings=None, batch_bytes=64 <
         _lib.check(rc, "bldp_file_chunks_to_device")
         _lib.check(rc2, "bslz4 decode")
     ct, ci, cc = chunk
-    views = [packed[b * nper * cvol:(b + 1) * nper * cvol].view(gt * ct, ci, cc).permute(2, 1, 0)
-             for b in range(len(fnames))]
-    rwin = [win[0] - kc0 * cc, nc, win[2], win[3] - ki0 * ci, ni, win[5], win[6] - kt0 * ct, nt,
-            win[8]]
+    if gi == 1 and gc == 1:  # the chunk grid itself holds each bank's window
+        views = [packed[b * nper * cvol:(b + 1) * nper * cvol].view(gt * ct, ci, cc)
+                 .permute(2, 1, 0) for b in range(len(fnames))]
+        rwin = [win[0] - kc0 * cc, nc, win[2], win[3] - ki0 * ci, ni, win[5], win[6] - kt0 * ct,
+                nt, win[8]]
+    else:  # several chunks across: each bank's window gathered dense on the device
+        from . import engine
+
+        keep = [(ctypes.c_int64 * 3)(*v) for v in (chunk, (kt0 * ct, ki0 * ci, kc0 * cc),
+                                                   (gt, gi, gc))]
+        w9 = (ctypes.c_int64 * 9)(*win)
+        views = []
+        with torch.cuda.device(dev):
+            for b in range(len(fnames)):
+                out = engine.fb_empty(nc, ni, nt, device=dev)
+                rc = _lib.lib().bldp_unchunk_f32(packed.data_ptr() + 4 * b * nper * cvol,
+                                                 keep[0], keep[1], keep[2], w9, out.data_ptr(),
+                                                 _lib.stream_ptr())
+                _lib.check(rc, "bldp_unchunk_f32")
+                views.append(out)
+        rwin = None
     if timings is not None:
         timings.update(setup_ms=t_setup * 1e3, read_decode_ms=(time.perf_counter() - t0) * 1e3,
                        first_copy_ms=stats[0], reads_ms=stats[1], pieces=int(stats[2]),

@@ -259,7 +259,8 @@ def _band_chunked(ws, fs, geo, idxs, fqavby, op, tavby, band, root, force_copy, 
     t0 = time.perf_counter()
     with ThreadPoolExecutor(max_workers=len(groups)) as ex:  # one reader per GPU
         tread = dict(ex.map(read, groups.items()))
-    if any(t is None for t in tread.values()) or len({tuple(w) for w in rwins.values()}) != 1:
+    if any(t is None for t in tread.values()) or \
+            len({None if w is None else tuple(w) for w in rwins.values()}) != 1:
         return False
     rwin = next(iter(rwins.values()))
     tm["read"] = {str(d): t for d, t in tread.items()}

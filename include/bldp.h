@@ -79,7 +79,7 @@ extern "C" {
  *    (tools/hbm_probe.hip, build/libbldp_probe.so); plan options
  *    "force_staged", "il_persist", "max_wg_per_cu", "typed_rows" removed, and
  *    the values that only ever forced a losing form (narrow_mis 2, lane 2,
- *    wavet 2, unaligned_vec 3, kurt_leaf_tile 2); "typed_pipe" added */
+ *    wavet 2, unaligned_vec 3, kurt_leaf_tile 2) */
 #define BLDP_ABI_VERSION 4
 
 #if defined(BLDP_BUILD)
@@ -152,8 +152,7 @@ BLDP_API int bldp_reduce_plan_f32(const float *in, int64_t nchan, int64_t nif, i
  *   "vec_row", "row_tpb", "rowt_pack", "rowt_small", "wavet",
  *   "unaligned_vec", "kurt_exact", "kurt_mid_cpl", "kurt_mid_small",
  *   "kurt_leaf_narrow", "kurt_leaf_tile", "typed_vec",
- *   "row_bpack", "lane_bpack", "wave_bpack", "col3", "rowt_narrow8", "st_plain",
- *   "typed_pipe"
+ *   "row_bpack", "lane_bpack", "wave_bpack", "col3", "rowt_narrow8", "st_plain"
  *                    which kernel a reduce / kurtosis / typed shape takes
  *                    (csrc/kernels.hip kPlanOpts: defaults, meanings and the
  *                    values each option accepts).

@@ -550,7 +550,7 @@ def test_plan_option_domains_checked(pkg, L):
     coerced) with BLDP_EINVAL and leaves the option unchanged; the removed
     options (force_staged, il_persist, max_wg_per_cu: ABI 4) are unknown."""
     cases = {"row_split": ((1, 2, 4), (0, 3, 5, 8)), "st_plain": ((0, 1, 2), (3, 100)),
-             "typed_pipe": ((0, 1, 8), (9,)), "unaligned_vec": ((0, 2), (3,)),
+             "unaligned_vec": ((0, 2), (3,)),
              "lane": ((0, 1), (2,)), "wavet": ((0, 1), (2,)), "narrow_mis": ((0, 1), (2,)),
              "kurt_leaf_tile": ((0, 1), (2,)),
              "kurt_mid_cpl": ((1, 2), (0, 3)), "vec_il": ((0, 1), (2, 1 << 40)),
@@ -566,5 +566,5 @@ def test_plan_option_domains_checked(pkg, L):
             assert n in pkg._lib.last_error()
         assert L.bldp_plan_option(n.encode(), -1, None) == 0
         assert L.bldp_plan_option(n.encode(), -7, None) == 0  # any negative: the default
-    for n in ("force_staged", "il_persist", "max_wg_per_cu", "typed_rows"):
+    for n in ("force_staged", "il_persist", "max_wg_per_cu", "typed_rows", "typed_pipe"):
         assert L.bldp_plan_option(n.encode(), 1, None) == pkg._lib.BLDP_EINVAL, n

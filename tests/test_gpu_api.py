@@ -223,21 +223,24 @@ def test_getband_compressed_banks_device_stitch(pkg, orc, tmp_path, monkeypatch,
 def test_getband_chunked_band_mixed_filters_and_fallback(pkg, orc, tmp_path):
     """The chunked-band read takes compressed and unfiltered chunked banks of
     one geometry together (unfiltered chunks copied raw, a chunk never written
-    read as 0), and hands banks whose chunk box is several chunks wide in
-    channel back to the bank-by-bank branch; both bit-exact against the
-    oracle."""
+    read as 0), with the window inside one chunk column (the chunk grid is the
+    window's array) or across several (each bank's window gathered from its
+    grid, bldp_unchunk_f32), and hands banks of different chunk layouts back
+    to the bank-by-bank branch; all bit-exact against the oracle."""
     rng = np.random.default_rng(515)
     J, C = pkg.JRange, pkg.COLON
     enc = lambda blk: orc.np_bslz4_encode(blk, 512, lz4=orc.lz4_compress)  # noqa: E731
-    for chunk, want_path in (((8, 1, 2048), "chunked band"), ((8, 1, 512), "bank by bank")):
+    for chunk, want_path in (((8, 1, 2048), "chunked band"), ((8, 1, 512), "chunked band"),
+                             (None, "bank by bank")):
         banks, names = [], []
         for b in range(4):
             a = np.asfortranarray(rng.integers(0, 200, (2048, 1, 40)).astype(np.float32))
-            f = str(tmp_path / f"m{b}_{chunk[2]}.h5")
+            ck = chunk or ((8, 1, 2048) if b < 2 else (8, 1, 1024))  # None: two layouts
+            f = str(tmp_path / f"m{b}_{chunk[2] if chunk else 0}.h5")
             if b % 2:
-                pkg.fbh5.write(f, dict(foff=-1.0, nfpc=64), a, chunks=chunk)
+                pkg.fbh5.write(f, dict(foff=-1.0, nfpc=64), a, chunks=ck)
             else:
-                pkg.fbh5.write_bslz4(f, dict(foff=-1.0, nfpc=64), a, chunk, enc)
+                pkg.fbh5.write_bslz4(f, dict(foff=-1.0, nfpc=64), a, ck, enc)
             banks.append(a)
             names.append(f)
         for idxs, F, T, op in (((C, C, C), 64, 8, "sum"), ((J(129, 2048), C, J(3, 34)), 8, 4, "max")):

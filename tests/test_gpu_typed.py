@@ -253,9 +253,6 @@ def test_typed_vec_kernel_matches_oracle(pkg, eng, orc, dt):
             assert same(got, want), (dt, (nc, ni, nt, F, T), op)
             with pkg._lib.plan_option("typed_vec", 0):
                 assert same(eng.fb_to_numpy(eng.reduce(x, F, T, op)), got), (dt, op, "typed_vec 0")
-            for pipe in (1, 2, 8):  # the persistent pipelined form (k_reduce_typed_vec16p)
-                with pkg._lib.plan_option("typed_pipe", pipe):
-                    assert same(eng.fb_to_numpy(eng.reduce(x, F, T, op)), got), (dt, op, pipe)
         # a window: channels from group 2 on, spectra 2.. (a misaligned row start)
         w = [2 * F, nc - 2 * F, 1, 0, ni, 1, 1, (nt - 1) // T * T, 1]
         for op in ("sum", "max"):

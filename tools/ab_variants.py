@@ -124,10 +124,10 @@ VARIANTS = {
     "rowb8": {"patch": [(K, "constexpr int kRowBatch = 16;", "constexpr int kRowBatch = 8;"),
                         (K, "static_assert(kNacc == 8 && kRowBatch == 16,",
                          "static_assert(kNacc == 8 && kRowBatch == 8,")]},
-    "gpw4": {"patch": [(K, "constexpr int kIlGpw = 2, kIlInflight = 4;",
-                        "constexpr int kIlGpw = 4, kIlInflight = 4;")]},
-    "ilb8": {"patch": [(K, "constexpr int kIlGpw = 2, kIlInflight = 4;",
-                        "constexpr int kIlGpw = 2, kIlInflight = 8;")]},
+    "gpw4": {"patch": [(K, "constexpr int kIlGpw = 2, kIlInflight = 4, kIlGpwK2 = 2;",
+                        "constexpr int kIlGpw = 4, kIlInflight = 4, kIlGpwK2 = 2;")]},
+    "ilb8": {"patch": [(K, "constexpr int kIlGpw = 2, kIlInflight = 4, kIlGpwK2 = 2;",
+                        "constexpr int kIlGpw = 2, kIlInflight = 8, kIlGpwK2 = 2;")]},
     # round 5: bytes in flight per CU.  Workgroups resident per CU capped by an
     # LDS allocation (kIlShm, kRowShm, kRowtShm, kVecShm: 96 / 64 / 48 / 36 KiB
     # = 1 / 2 / 3 / 4 workgroups of 160 KiB) x loads in flight per lane.
@@ -135,12 +135,28 @@ VARIANTS = {
     # and is the product default; ilo3 / ilo4 / ilo2b8 / ilo4b8 / ilb8 lost)
     "ilnocap": {"patch": [(K, "constexpr unsigned kIlShm = 65536;", "constexpr unsigned kIlShm = 0;")]},
     "il1b8": {"patch": [(K, "constexpr unsigned kIlShm = 65536;", "constexpr unsigned kIlShm = 98304;"),
-                        (K, "constexpr int kIlGpw = 2, kIlInflight = 4;",
-                         "constexpr int kIlGpw = 2, kIlInflight = 8;")]},
-    "il2b2": {"patch": [(K, "constexpr int kIlGpw = 2, kIlInflight = 4;",
-                         "constexpr int kIlGpw = 2, kIlInflight = 2;")]},
-    "il2g4": {"patch": [(K, "constexpr int kIlGpw = 2, kIlInflight = 4;",
-                         "constexpr int kIlGpw = 4, kIlInflight = 4;")]},
+                        (K, "constexpr int kIlGpw = 2, kIlInflight = 4, kIlGpwK2 = 2;",
+                         "constexpr int kIlGpw = 2, kIlInflight = 8, kIlGpwK2 = 2;")]},
+    "il2b2": {"patch": [(K, "constexpr int kIlGpw = 2, kIlInflight = 4, kIlGpwK2 = 2;",
+                         "constexpr int kIlGpw = 2, kIlInflight = 2, kIlGpwK2 = 2;")]},
+    "il2g4": {"patch": [(K, "constexpr int kIlGpw = 2, kIlInflight = 4, kIlGpwK2 = 2;",
+                         "constexpr int kIlGpw = 4, kIlInflight = 4, kIlGpwK2 = 2;")]},
+    # round 5 second pass (profiles/r05/ab_il_r05d.json, ab_occ_r05d.json): the
+    # interleaved kernel at 1 workgroup per CU with 8 in flight, 2 loads in
+    # flight, 4 groups per workgroup all lost on F = 1024 (il2g4 won F = 512:
+    # ilk2g4 takes 4 groups there only); capping the row kernels lost
+    # (cfg1 / cfg2 1.14-2.5x), the rowt cap at 4 per CU won the 0002 band at
+    # F = 64 T = 1 by 5%
+    "ilk2g4": {"patch": [(K, "kIlInflight = 4, kIlGpwK2 = 2;", "kIlInflight = 4, kIlGpwK2 = 4;")]},
+    "typo2": {"patch": [("typed.hip", "constexpr unsigned kTypedShm = 0;",
+                         "constexpr unsigned kTypedShm = 65536;")]},
+    "typo3": {"patch": [("typed.hip", "constexpr unsigned kTypedShm = 0;",
+                         "constexpr unsigned kTypedShm = 49152;")]},
+    "typo4": {"patch": [("typed.hip", "constexpr unsigned kTypedShm = 0;",
+                         "constexpr unsigned kTypedShm = 36864;")]},
+    "kleafo2": {"patch": [(KU, "constexpr unsigned kKurtLeafShm = 0,", "constexpr unsigned kKurtLeafShm = 65536,")]},
+    "kleafo4": {"patch": [(KU, "constexpr unsigned kKurtLeafShm = 0,", "constexpr unsigned kKurtLeafShm = 36864,")]},
+    "kmido2": {"patch": [(KU, "kKurtMidShm = 0;", "kKurtMidShm = 65536;")]},
     "rowo1": {"patch": [RS(row=98304)]},
     "rowo2": {"patch": [RS(row=65536)]},
     "rowo4": {"patch": [RS(row=36864)]},
@@ -434,6 +450,31 @@ def run(names, rounds, iters, suite="main"):
         band_case("cfg4 F8 T1024", b4, 8, 1024, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
         band_case("0001 band F8 T1", b4, 8, 1, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
         band_case("0001 band F64 T16", b4, 64, 16, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
+        cases_done = True
+    elif suite == "typed":  # UInt8 / UInt16 SIGPROC-style data (bldp_reduce_strided)
+        del b3
+        import numpy as np
+
+        def typed_case(label, a, dcode, F, T):
+            x = torch.from_numpy(a).cuda().permute(2, 1, 0)  # Julia order
+            nchan, nif, ntime = x.shape
+            nco, nto = nchan // F, ntime // T
+            out = torch.empty((nto, nif, nco), dtype=torch.int64, device="cuda")
+            nbytes = a.nbytes + 8 * nco * nif * nto
+
+            def go(L):
+                rc = L.bldp_reduce_strided(dcode, x.data_ptr(), nchan, nif, ntime, None, F, T, 0,
+                                           out.data_ptr(), nco, nco * nif, sp)
+                assert rc == 0
+            cases.append((label, go, nbytes, out, x))
+        rng = np.random.default_rng(0)
+        a8 = rng.integers(0, 256, (279, 1, 65536 * 8), dtype=np.uint8)
+        typed_case("u8 0002 band F64 T1", a8, 2, 64, 1)
+        typed_case("u8 0002 band F16 T1", a8, 2, 16, 1)
+        typed_case("u8 0002 band F64 T4", a8[:276], 2, 64, 4)
+        typed_case("u8 0002 file F64 T1", np.ascontiguousarray(a8[:, :, :65536]), 2, 64, 1)
+        a16 = rng.integers(0, 65536, (279, 1, 65536 * 8), dtype=np.uint16)
+        typed_case("u16 0002 band F64 T1", a16, 3, 64, 1)
         cases_done = True
     elif suite == "il1":  # large groups with short time blocks: interleaved vs wave kernel
         for F, T in ((1024, 1), (512, 1), (2048, 1), (4096, 1), (1024, 2), (1024, 4)):
@@ -784,7 +825,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--suite", default="main", choices=["main", "il", "occ", "rows", "t1_0001", "wavet", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy", "wide", "grid0", "grid1", "t38", "lane3", "kgrid", "lanetpack", "kshort", "kfile"])
+    ap.add_argument("--suite", default="main", choices=["main", "il", "occ", "typed", "rows", "t1_0001", "wavet", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy", "wide", "grid0", "grid1", "t38", "lane3", "kgrid", "lanetpack", "kshort", "kfile"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:

@@ -7,7 +7,7 @@ percent, so a reduce is also compared with what a kernel that only reads
 reaches on the same GPU.  It is a reference, not a ceiling: a reduce can beat
 a probe form that under-reads some shapes.
 
-    python tools/hbm_probe.py [MiB ...]   (prints one JSON line per size)
+    python tools/hbm_probe.py [MiB ...] [--cold]   (prints one JSON line per size)
 """
 from __future__ import annotations
 
@@ -91,5 +91,14 @@ def read_probe(nbytes, launches=20, forms=PROBE_FORMS, buf=None, stream=None, ev
 
 
 if __name__ == "__main__":
-    for mb in [int(x) for x in sys.argv[1:]] or [64, 4096]:
-        print(json.dumps(read_probe(mb << 20, every=True)), flush=True)
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("mib", nargs="*", type=float, default=[64, 4096])
+    ap.add_argument("--cold", action="store_true",
+                    help="rotate over copies totalling >= 1 GiB (bench.py --cache cold)")
+    a = ap.parse_args()
+    for mb in a.mib:
+        n = int(mb * (1 << 20))
+        k = max(2, -(-(1 << 30) // n)) if a.cold and n < (1 << 30) else 1
+        print(json.dumps(read_probe(n, every=True, copies=k)), flush=True)

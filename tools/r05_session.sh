@@ -75,6 +75,7 @@ for s in $STEPS; do
     typedsq) run typedsq 180 rocprofv3 --pmc $SQ --output-format csv -d "$OUT/typedsq" -o run \
         -- python bench.py --mode typed --steps 20 --warmup 5 ;;
     getband) run getband 600 python tools/getband_probe.py --json "$OUT/getband.json" ;;
+    probe_cold) run probe_cold 300 python tools/hbm_probe.py 68.07 156.99 557.5 --cold ;;
     getbandz) run getbandz 600 python tools/getband_probe.py --compressed --json "$OUT/getbandz.json" ;;
     getband_t*) run "$s" 600 python tools/getband_probe.py --threads "${s#getband_t}" \
         --cases "F64 T1,F1 T1 despike" --json "$OUT/$s.json" ;;
