@@ -151,8 +151,13 @@ constexpr int kNacc = 8;
 // k_reduce_rowt, k_reduce_tile.
 constexpr int kRowMaxWaves = 4, kRowtMaxWaves = 6, kTileMaxWaves = 3;
 // Dynamic LDS per workgroup as a cap on the workgroups resident per CU (160
-// KiB of LDS per CU): the bytes in flight per CU, not the waves, set a
-// stream's HBM rate (round 5, profiles/r05/).  0 = no cap.
+// KiB of LDS per CU), as kIlShm does for the interleaved kernel.  Measured
+// for these kernels in round 5 and not taken (0 = no cap): the row kernels
+// at 1 / 2 / 4 per CU lost 14-150% on the 0002 file and band
+// (profiles/r05/ab_occ_r05d.json); the rowt kernel at 4 per CU gained 3-4%
+// on the 0002 band at T <= 2 but lost 8-11% on one 0002 file and up to 3% on
+// the 0001 band (ab_rowt_r05g2.json, ab_t1_0001_r05g2.json); the vector
+// kernel at 2 per CU lost 60% on the 0001 band at F = 64.
 constexpr unsigned kRowShm = 0, kRowtShm = 0, kVecShm = 0;
 // The short-time-block kernels (k_reduce_rowt, k_reduce_narrowt,
 // k_reduce_lanet) also take tavby = 3 and 8, not only 1, 2, 4 (plan option
@@ -1036,8 +1041,12 @@ __global__ __launch_bounds__(kBlock) void k_reduce_vec(const RedArgs a) {
 //                bank, i.e. one rank at N=8, against 4)
 //   kIlInflight  16-byte loads a lane issues per batch (power of two); 4
 //                measured +0.1..0.7% against 8 on 1-, 2- and 8-bank launches
-constexpr int kIlGpw = 2, kIlInflight = 4, kIlGpwK2 = 2;
-// groups per workgroup for K4 float4 per lane per row (kIlGpwK2 at K4 = 2)
+constexpr int kIlGpw = 2, kIlInflight = 4, kIlGpwK2 = 4;
+// groups per workgroup for K4 float4 per lane per row: kIlGpwK2 = 4 at K4 = 2
+// (fqavby = 512: two loads per lane per row, as fqavby = 1024 has with 2),
+// +7% on the 0000 band and +6% on the 0002 band at fqavby 512, F = 1024
+// unchanged (round 5, capped at 2 workgroups per CU, profiles/r05/
+// ab_il_r05g.json)
 constexpr int il_gpw(int k4) { return k4 == 2 ? kIlGpwK2 : kIlGpw; }
 //   kIlShm       dynamic LDS bytes per workgroup, an allocation that caps the
 //                workgroups resident per CU at 2 (160 KiB of LDS per CU):

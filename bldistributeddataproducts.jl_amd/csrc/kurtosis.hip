@@ -1128,7 +1128,9 @@ hipError_t launch_tree(const KurtArgs &k, char *ws, const KLayout &L, hipStream_
 }  // namespace
 
 // Dynamic LDS per workgroup of k_kurt_leaf / k_kurt_mid2 as a cap on the
-// workgroups resident per CU (as kIlShm in kernels.hip); 0 = no cap.
+// workgroups resident per CU (as kIlShm in kernels.hip); 0 = no cap: the leaf
+// at 2 / 4 per CU within +-1% on every kurtosis shape but one, k_kurt_mid2 at
+// 2 per CU 62% slower on cfg2 (round 5, profiles/r05/ab_kurt_r05g2.json).
 constexpr unsigned kKurtLeafShm = 0, kKurtMidShm = 0;
 
 void plan_kurtosis(KurtArgs &k, int num_cus) {

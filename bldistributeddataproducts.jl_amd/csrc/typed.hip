@@ -520,7 +520,9 @@ __global__ __launch_bounds__(256) void k_kurt_typed_w(const TypedArgs a, double 
 // reference's order on k_reduce_typed; windows without dword-aligned 16-byte
 // rows of whole groups, too).
 // Dynamic LDS per k_reduce_typed_vec16 workgroup as a cap on the workgroups
-// resident per CU (as kIlShm in kernels.hip); 0 = no cap.  (Round 5: a
+// resident per CU (as kIlShm in kernels.hip); 0 = no cap: 2 / 3 / 4 per CU
+// lost 8-85% on the UInt8 / UInt16 0002 band and file (round 5,
+// profiles/r05/ab_typed_r05g2.json).  (Round 5: a
 // persistent, software-pipelined form -- tiles walked by 1..4 workgroups per
 // CU, the next tile's loads issued before the current one's folds -- was
 // slower on the UInt8 0002 band at every width: 72 / 43 / 32 vs 29 us,
