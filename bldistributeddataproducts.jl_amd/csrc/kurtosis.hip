@@ -1132,6 +1132,9 @@ hipError_t launch_tree(const KurtArgs &k, char *ws, const KLayout &L, hipStream_
 // at 2 / 4 per CU within +-1% on every kurtosis shape but one, k_kurt_mid2 at
 // 2 per CU 62% slower on cfg2 (round 5, profiles/r05/ab_kurt_r05g2.json).
 constexpr unsigned kKurtLeafShm = 0, kKurtMidShm = 0;
+// k_kurt_regs (<= 32 spectra: a lane's whole float4 column in flight at once,
+// 16-32 x 16 B per lane)
+constexpr unsigned kKurtRegsShm = 0;
 
 void plan_kurtosis(KurtArgs &k, int num_cus) {
   k.K = pw_level(std::max<int64_t>(k.nt, 1));
@@ -1181,13 +1184,13 @@ hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s) {
     const dim3 g1((unsigned)(cdivk(ncols, kB) * k.nrow));
     const bool exact = opt(OPT_KURT_EXACT) != 0;
     if (exact && k.nt == 16)
-      hipLaunchKernelGGL((k_kurt_regs<16, true>), g1, block, 0, s, k);
+      hipLaunchKernelGGL((k_kurt_regs<16, true>), g1, block, kKurtRegsShm, s, k);
     else if (exact && k.nt == 32)
-      hipLaunchKernelGGL((k_kurt_regs<32, true>), g1, block, 0, s, k);
+      hipLaunchKernelGGL((k_kurt_regs<32, true>), g1, block, kKurtRegsShm, s, k);
     else if (k.nt <= 16)
-      hipLaunchKernelGGL((k_kurt_regs<16, false>), g1, block, 0, s, k);
+      hipLaunchKernelGGL((k_kurt_regs<16, false>), g1, block, kKurtRegsShm, s, k);
     else
-      hipLaunchKernelGGL((k_kurt_regs<32, false>), g1, block, 0, s, k);
+      hipLaunchKernelGGL((k_kurt_regs<32, false>), g1, block, kKurtRegsShm, s, k);
     return hipGetLastError();
   }
   if (p == KP_MID && opt(OPT_KURT_MID_CPL) == 2 && k.vec && cdivk(k.nt, 8) <= 48) {

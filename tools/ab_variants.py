@@ -157,6 +157,9 @@ VARIANTS = {
     "kleafo2": {"patch": [(KU, "constexpr unsigned kKurtLeafShm = 0,", "constexpr unsigned kKurtLeafShm = 65536,")]},
     "kleafo4": {"patch": [(KU, "constexpr unsigned kKurtLeafShm = 0,", "constexpr unsigned kKurtLeafShm = 36864,")]},
     "kmido2": {"patch": [(KU, "kKurtMidShm = 0;", "kKurtMidShm = 65536;")]},
+    "kregso3": {"patch": [(KU, "constexpr unsigned kKurtRegsShm = 0;", "constexpr unsigned kKurtRegsShm = 49152;")]},
+    "kregso2": {"patch": [(KU, "constexpr unsigned kKurtRegsShm = 0;", "constexpr unsigned kKurtRegsShm = 65536;")]},
+    "kregso4": {"patch": [(KU, "constexpr unsigned kKurtRegsShm = 0;", "constexpr unsigned kKurtRegsShm = 36864;")]},
     "rowo1": {"patch": [RS(row=98304)]},
     "rowo2": {"patch": [RS(row=65536)]},
     "rowo4": {"patch": [RS(row=36864)]},
@@ -717,6 +720,17 @@ def run(names, rounds, iters, suite="main"):
         b6 = [eng.synth(32768, 1, 512, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
         kurt_case("kurt 32768ch nt512", b6)
         cases_done = True
+    elif suite == "kregs":  # getkurtosis of <= 32-spectrum windows (k_kurt_regs)
+        for nt in (4, 8, 12, 16):
+            kurt_case(f"kurt 0000 band nt{nt}", b3, [0, 1 << 26, 1, 0, 1, 1, 0, nt, 1])
+        kurt_case("kurt 0000 1 bank nt16", b3[:1])
+        kurt_case("kurt 0000 c0=1 nt16", b3, [1, (1 << 26) - 4, 1, 0, 1, 1, 0, 16, 1])
+        del b3
+        b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
+        for nt in (16, 32):
+            kurt_case(f"kurt 0002 band nt{nt}", b2, [0, 65536, 1, 0, 1, 1, 0, nt, 1])
+        kurt_case("kurt 0002 file nt32", b2[:1], [0, 65536, 1, 0, 1, 1, 0, 32, 1])
+        cases_done = True
     elif suite == "kleaf":  # the streamed-leaf kurtosis path only
         del b3
         b4 = [eng.synth(512, 1, 880000, 8, seed=10 * b + 1, kind=0) for b in range(8)]
@@ -825,7 +839,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--suite", default="main", choices=["main", "il", "occ", "typed", "rows", "t1_0001", "wavet", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy", "wide", "grid0", "grid1", "t38", "lane3", "kgrid", "lanetpack", "kshort", "kfile"])
+    ap.add_argument("--suite", default="main", choices=["main", "il", "occ", "typed", "kregs", "rows", "t1_0001", "wavet", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy", "wide", "grid0", "grid1", "t38", "lane3", "kgrid", "lanetpack", "kshort", "kfile"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:

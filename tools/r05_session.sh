@@ -58,6 +58,9 @@ for s in $STEPS; do
     sq_*) C=${s#sq_}
       run "$s" 180 rocprofv3 --pmc $SQ --output-format csv -d "$OUT/$s" -o run \
         -- python bench.py $(bench_args "$C") ;;
+    kurtsq_*) C=${s#kurtsq_}
+      run "$s" 180 rocprofv3 --pmc $SQ --output-format csv -d "$OUT/$s" -o run \
+        -- python bench.py --mode kurtosis --config "$C" --steps 20 --warmup 5 ;;
     ab_*) A=${s#ab_}; SUITE=${A%%:*}; V=${AB_VARIANTS:-base}; [ "$SUITE" != "$A" ] && V=${A#*:}
       run "ab_$SUITE" 900 python tools/ab_variants.py --run --suite "$SUITE" --rounds 5 \
           --variants "$V" --json "$OUT/ab_$SUITE.json" ;;
@@ -75,6 +78,8 @@ for s in $STEPS; do
     typedsq) run typedsq 180 rocprofv3 --pmc $SQ --output-format csv -d "$OUT/typedsq" -o run \
         -- python bench.py --mode typed --steps 20 --warmup 5 ;;
     getband) run getband 600 python tools/getband_probe.py --json "$OUT/getband.json" ;;
+    dist*) N=${s#dist}; run "$s" 400 python bench.py --gpus "$N" --dist-backend gloo --steps 5 \
+        --warmup 2 --no-cpu-baseline ;;
     probe_cold) run probe_cold 300 python tools/hbm_probe.py 68.07 156.99 557.5 --cold ;;
     getbandz) run getbandz 600 python tools/getband_probe.py --compressed --json "$OUT/getbandz.json" ;;
     getband_t*) run "$s" 600 python tools/getband_probe.py --threads "${s#getband_t}" \
