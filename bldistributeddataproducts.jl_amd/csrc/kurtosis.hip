@@ -1133,8 +1133,15 @@ hipError_t launch_tree(const KurtArgs &k, char *ws, const KLayout &L, hipStream_
 // 2 per CU 62% slower on cfg2 (round 5, profiles/r05/ab_kurt_r05g2.json).
 constexpr unsigned kKurtLeafShm = 0, kKurtMidShm = 0;
 // k_kurt_regs (<= 32 spectra: a lane's whole float4 column in flight at once,
-// 16-32 x 16 B per lane)
-constexpr unsigned kKurtRegsShm = 0;
+// 16-32 x 16 B per lane): 2 workgroups per CU for windows of 12-16 spectra
+// (48-64 KiB of loads a workgroup), uncapped otherwise.  Round 5 A/B
+// (profiles/r05/ab_kregs_r05h.json, one process, one box), time relative to
+// uncapped: the 0000 band nt = 12 / 16 0.946 / 0.969, one 0000 bank nt = 16
+// 0.920, c0 = 1 0.974, the 0002 band nt = 16 0.965; but nt = 4 / 8 1.21 /
+// 1.09 (there the Float64 outputs are 1/2 - 1/4 of the traffic) and nt = 32
+// 1.02 (3 / 4 per CU: within +-3% either way).
+constexpr unsigned kKurtRegsShm = 65536;
+constexpr int64_t kKurtRegsCapLo = 12, kKurtRegsCapHi = 16;
 
 void plan_kurtosis(KurtArgs &k, int num_cus) {
   k.K = pw_level(std::max<int64_t>(k.nt, 1));
@@ -1183,14 +1190,15 @@ hipError_t launch_kurtosis(KurtArgs &k, char *ws, hipStream_t s) {
   if (p == KP_REGS) {
     const dim3 g1((unsigned)(cdivk(ncols, kB) * k.nrow));
     const bool exact = opt(OPT_KURT_EXACT) != 0;
+    const unsigned shm = k.nt >= kKurtRegsCapLo && k.nt <= kKurtRegsCapHi ? kKurtRegsShm : 0;
     if (exact && k.nt == 16)
-      hipLaunchKernelGGL((k_kurt_regs<16, true>), g1, block, kKurtRegsShm, s, k);
+      hipLaunchKernelGGL((k_kurt_regs<16, true>), g1, block, shm, s, k);
     else if (exact && k.nt == 32)
-      hipLaunchKernelGGL((k_kurt_regs<32, true>), g1, block, kKurtRegsShm, s, k);
+      hipLaunchKernelGGL((k_kurt_regs<32, true>), g1, block, shm, s, k);
     else if (k.nt <= 16)
-      hipLaunchKernelGGL((k_kurt_regs<16, false>), g1, block, kKurtRegsShm, s, k);
+      hipLaunchKernelGGL((k_kurt_regs<16, false>), g1, block, shm, s, k);
     else
-      hipLaunchKernelGGL((k_kurt_regs<32, false>), g1, block, kKurtRegsShm, s, k);
+      hipLaunchKernelGGL((k_kurt_regs<32, false>), g1, block, shm, s, k);
     return hipGetLastError();
   }
   if (p == KP_MID && opt(OPT_KURT_MID_CPL) == 2 && k.vec && cdivk(k.nt, 8) <= 48) {
