@@ -35,9 +35,11 @@ NSLOTS = 4               # up to NSLOTS - 1 batches being read while one is copi
 # the native reader's ring (bldp_runs_to_device / bldp_file_runs_to_device):
 # the same 256 MiB of pinned slots as 8 x 32 MiB, so the first H2D copy
 # starts after 32 MiB of reads and the last one is half as long
-# (BLDP_NATIVE_BATCH_MB overrides the slot size, for probes)
+# (BLDP_NATIVE_BATCH_MB / BLDP_NATIVE_RING_MB override the slot size and the
+# ring's total, for probes)
 NATIVE_BATCH_BYTES = int(os.environ.get("BLDP_NATIVE_BATCH_MB", "32")) << 20
-NATIVE_NSLOTS = max(2, min(16, (256 << 20) // NATIVE_BATCH_BYTES))
+NATIVE_RING_BYTES = int(os.environ.get("BLDP_NATIVE_RING_MB", "256")) << 20
+NATIVE_NSLOTS = max(2, min(16, NATIVE_RING_BYTES // NATIVE_BATCH_BYTES))
 
 
 def _check(win, jshape):

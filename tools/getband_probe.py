@@ -37,6 +37,8 @@ def main():
                     help="reader threads (BLDP_READ_THREADS; 0: the library's default, 16)")
     ap.add_argument("--batch-mb", type=int, default=0,
                     help="pinned slot size (BLDP_NATIVE_BATCH_MB; 0: the default, 32)")
+    ap.add_argument("--ring-mb", type=int, default=0,
+                    help="pinned ring total (BLDP_NATIVE_RING_MB; 0: the default, 256)")
     ap.add_argument("--cases", default="",
                     help="comma-separated case labels to run (default: all)")
     a = ap.parse_args()
@@ -44,6 +46,8 @@ def main():
         os.environ["BLDP_READ_THREADS"] = str(a.threads)
     if a.batch_mb:
         os.environ["BLDP_NATIVE_BATCH_MB"] = str(a.batch_mb)
+    if a.ring_mb:
+        os.environ["BLDP_NATIVE_RING_MB"] = str(a.ring_mb)
     if a.compressed:
         a.ntime -= a.ntime % 16
 
@@ -81,7 +85,8 @@ def main():
     if a.cases:
         want = set(a.cases.split(","))
         cases = [c for c in cases if c[0] in want]
-    res = {"reader_threads": a.threads or "default", "batch_mb": a.batch_mb or "default"}
+    res = {"reader_threads": a.threads or "default", "batch_mb": a.batch_mb or "default",
+           "ring_mb": a.ring_mb or "default"}
     for label, kw in cases:
         out = {}
         kw = dict(kw)
