@@ -84,9 +84,11 @@ for s in $STEPS; do
     getbandz) run getbandz 600 python tools/getband_probe.py --compressed --json "$OUT/getbandz.json" ;;
     getband_t*) run "$s" 600 python tools/getband_probe.py --threads "${s#getband_t}" \
         --cases "F64 T1,F1 T1 despike" --json "$OUT/$s.json" ;;
-    getbandb_*) IFS=_ read -r B R T <<< "${s#getbandb_}"  # getbandb_BATCHMB_RINGMB_THREADS
+    getbandb_*) IFS=_ read -r B R T X <<< "${s#getbandb_}"  # getbandb_BATCHMB_RINGMB_THREADS[_rep]
       run "$s" 300 python tools/getband_probe.py --threads "$T" --batch-mb "$B" --ring-mb "$R" \
         --cases "F64 T1" --json "$OUT/$s.json" ;;
+    getbandzp) run getbandzp 600 python tools/getband_probe.py --compressed \
+        --cases "F64 T1" --json "$OUT/getbandzp.json" ;;
   esac
 done
 echo "== session done"
