@@ -23,6 +23,13 @@ struct ScratchLease {
   std::unique_lock<std::mutex> hold;
 };
 int scratch_lease(hipStream_t s, size_t bytes, ScratchLease *lease);
+// bldp_bslz4_decode_dev_async with chunk k's host header at comp_host +
+// (chunk_off[k] - host_base) (bslz4.hip; the chunk reader's slot ring)
+int bslz4_decode_async_at(int nchunk, const uint8_t *comp_host, uint64_t host_base,
+                          const uint8_t *comp_dev, const uint64_t *chunk_off,
+                          const uint64_t *chunk_len, int elem_size, uint8_t *out_dev,
+                          const uint64_t *out_off, const uint64_t *out_len, int *err_dev,
+                          hipStream_t s);
 std::vector<int> scratch_devices();  // devices holding scratch
 void scratch_release_all();          // frees it (callers drained the devices)
 // The native file readers (fileio.hip): stop the reader threads and free the

@@ -349,11 +349,14 @@ BLDP_API int bldp_bslz4_decode_host(const void *chunk, size_t nbytes, int elem_s
 // Shared by the synchronous and asynchronous entry points: describe the
 // chunks on the host, then queue the planner and the decoder on `s`; error
 // bits are OR-ed into *derr (device memory).
+// The host copy of chunk k's header is at comp_host + (chunk_off[k] - host_base)
+// (host_base 0: the host and device staging buffers share offsets; the chunk
+// reader's slot ring passes the batch's first staged offset).
 static int decode_launch(int nchunk, const uint8_t *comp_host, const uint8_t *comp_dev,
                          const uint64_t *chunk_off, const uint64_t *chunk_len, int elem_size,
                          uint8_t *out_dev, const uint64_t *out_off, const uint64_t *out_len,
                          int *derr_user, hipStream_t s, int **derr_used,
-                         bldp::ScratchLease &lease) {
+                         bldp::ScratchLease &lease, uint64_t host_base = 0) {
   if (nchunk < 0 || (nchunk && (!comp_host || !comp_dev || !chunk_off || !chunk_len ||
                                 !out_dev || !out_off || !out_len)) ||
       elem_size <= 0 || elem_size > 64)
@@ -365,7 +368,10 @@ static int decode_launch(int nchunk, const uint8_t *comp_host, const uint8_t *co
   uint64_t ntask = 0;
   uint32_t maxbb = 0;
   for (int k = 0; k < nchunk; ++k) {
-    int rc = describe_chunk(comp_host + chunk_off[k], chunk_len[k], chunk_off[k], out_off[k],
+    if (chunk_off[k] < host_base)
+      return bldp::set_error(BLDP_EINVAL, "bslz4: chunk %d below the host staging base", k);
+    int rc = describe_chunk(comp_host + (chunk_off[k] - host_base), chunk_len[k], chunk_off[k],
+                            out_off[k],
                             elem_size, &descs[k]);
     if (rc) return rc;
     // the header's byte count decides how much the kernels write: it must be
@@ -457,3 +463,17 @@ BLDP_API int bldp_bslz4_error(const int *err_dev, void *stream) {
 }
 
 }  // extern "C"
+
+// bldp_bslz4_decode_dev_async with the host headers at comp_host +
+// (chunk_off[k] - host_base): the chunk reader's slot ring (fileio.hip).
+int bldp::bslz4_decode_async_at(int nchunk, const uint8_t *comp_host, uint64_t host_base,
+                                const uint8_t *comp_dev, const uint64_t *chunk_off,
+                                const uint64_t *chunk_len, int elem_size, uint8_t *out_dev,
+                                const uint64_t *out_off, const uint64_t *out_len, int *err_dev,
+                                hipStream_t s) {
+  if (!err_dev) return bldp::set_error(BLDP_EINVAL, "bslz4: null error word");
+  int *derr = nullptr;
+  bldp::ScratchLease lease;  // until the planner and decoder are queued
+  return decode_launch(nchunk, comp_host, comp_dev, chunk_off, chunk_len, elem_size, out_dev,
+                       out_off, out_len, err_dev, s, &derr, lease, host_base);
+}

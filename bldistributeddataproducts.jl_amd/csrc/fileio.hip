@@ -54,6 +54,10 @@ struct Job {
   const std::vector<void *> *slot_base = nullptr;
   const std::vector<void *> *copy_src = nullptr;
   int64_t slot_bytes = 0;
+  // slot ring with batches of any size (the chunk reader): batch b starts at
+  // staged offset batch_lo[b], i.e. at the start of its slot; empty: batch b
+  // starts at b * slot_bytes
+  std::vector<int64_t> batch_lo;
   std::vector<Piece> pieces;
   std::unique_ptr<std::atomic<int64_t>[]> left;
   std::atomic<int64_t> next{0};
@@ -146,7 +150,8 @@ class ReadPool {
           j->gate.wait(lk, [&] { return p.batch < j->open.load() || j->err.load(); });
         }
         const std::vector<void *> &sl = *j->slot_base;
-        dst = (uint8_t *)sl[p.batch % sl.size()] + (p.hoff - p.batch * j->slot_bytes);
+        const int64_t lo = j->batch_lo.empty() ? p.batch * j->slot_bytes : j->batch_lo[p.batch];
+        dst = (uint8_t *)sl[p.batch % sl.size()] + (p.hoff - lo);
       }
       int64_t got = 0;
       while (got < p.len && !j->err.load(std::memory_order_relaxed)) {
@@ -178,6 +183,10 @@ class ReadPool {
 };
 
 // nslot pinned host slots of `bytes` each (bldp_runs_to_device's ring).
+// The chunk reader's default ring: 8 x 32 MiB, the geometry filestream.py
+// gives bldp_runs_to_device, so the two readers share one ring per device.
+constexpr int64_t kRingSlotBytes = 32ll << 20;
+constexpr int kRingSlots = 8;
 struct Slots {
   int64_t bytes = 0;
   std::vector<void *> p;
@@ -255,6 +264,28 @@ struct PostedJob {
   ~PostedJob() { finish(true); }
 };
 
+// The ring reused across calls of one device (under its call lock).
+void free_slots(Slots &sl) {
+  for (void *q : sl.p) (void)hipHostFree(q);
+  sl.p.clear();
+  sl.bytes = 0;
+}
+int ensure_slots(Slots &sl, int64_t bytes, int nslot) {
+  if (sl.bytes == bytes && (int)sl.p.size() == nslot) return BLDP_OK;
+  free_slots(sl);
+  for (int i = 0; i < nslot; ++i) {
+    void *q = nullptr;
+    if (hipHostMalloc(&q, (size_t)bytes, hipHostMallocDefault) != hipSuccess) {
+      free_slots(sl);
+      return bldp::set_error(BLDP_ENOMEM, "%lld bytes of pinned slots",
+                             (long long)bytes);
+    }
+    sl.p.push_back(q);
+  }
+  sl.bytes = bytes;
+  return BLDP_OK;
+}
+
 }  // namespace
 
 // fds: one descriptor per chunk (the chunks of several files -- a band's banks
@@ -266,8 +297,8 @@ static int chunks_to_device(
     int64_t out_bytes, int *err_dev, void *copy_stream, void *stream, double *stats) {
   const auto t0 = std::chrono::steady_clock::now();
   if (nchunk < 0 || nbatch < 0 || (nchunk && (!file_off || !stored_len || !stage_off ||
-                                               !filter_mask || !batch_end || !host_pinned ||
-                                               !dev_stage || nbatch < 1)))
+                                               !filter_mask || !batch_end || !dev_stage ||
+                                               nbatch < 1)))
     return bldp::set_error(BLDP_EINVAL, "chunks_to_device: bad argument");
   if (nchunk == 0) return BLDP_OK;
   if (batch_end[nbatch - 1] != nchunk)
@@ -344,13 +375,35 @@ static int chunks_to_device(
   int64_t maxb = 0;
   for (int64_t b = 0, q = 0; b < nbatch; q = batch_end[b], ++b)
     maxb = std::max(maxb, batch_end[b] - q);
-  std::vector<hipEvent_t> evs;
+  std::vector<hipEvent_t> evs(nbatch, nullptr);  // batch b's H2D copy done
   std::vector<uint64_t> offs, lens, ooff, olen;
-  evs.reserve(nbatch);
   for (auto *v : {&offs, &lens, &ooff, &olen}) v->reserve(maxb);
   std::unique_lock<std::mutex> call;
   const std::shared_ptr<DevIO> io = dev_io(call);
   ReadPool *rp = io->pool.get();
+  // host_pinned NULL: batch b is read into slot b % nslot of the device's
+  // pinned ring (the one bldp_runs_to_device uses, kept when its slots hold
+  // the largest batch), reopened once the slot's previous H2D copy is done
+  const bool ring = host_pinned == nullptr;
+  int64_t nslot = 0;
+  if (ring) {
+    int64_t span = 0;
+    for (const auto &r : brange) span = std::max(span, r.second - r.first);
+    if (io->slots.p.size() < 2 || io->slots.bytes < span) {
+      int nring = kRingSlots;  // (BLDP_RING_SLOTS: a probe knob, 2..16)
+      if (const char *e = getenv("BLDP_RING_SLOTS")) nring = std::min(16, std::max(2, atoi(e)));
+      const int rc = ensure_slots(io->slots, std::max(kRingSlotBytes, (span + (1 << 20) - 1) &
+                                                                          ~(int64_t)((1 << 20) - 1)),
+                                  nring);
+      if (rc) return rc;
+    }
+    nslot = (int64_t)io->slots.p.size();
+    j.slot_base = &io->slots.p;
+    j.slot_bytes = io->slots.bytes;
+    j.batch_lo.resize(nbatch);
+    for (int64_t b = 0; b < nbatch; ++b) j.batch_lo[b] = brange[b].first;
+    j.open.store(std::min<int64_t>(nbatch, nslot));
+  }
   PostedJob posted(rp, &j);
   hipStream_t cs = (hipStream_t)copy_stream, s = (hipStream_t)stream;
   int rc = BLDP_OK;
@@ -368,14 +421,15 @@ static int chunks_to_device(
       break;
     }
     const int64_t lo = brange[b].first, hi = brange[b].second;
+    // the batch's staged bytes on the host, and the offset they start at
+    const uint8_t *hsrc = ring ? (const uint8_t *)io->slots.p[b % nslot] : (const uint8_t *)host_pinned + lo;
     if (hi > lo) {
-      hipEvent_t ev;
-      if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+      if (hipEventCreateWithFlags(&evs[b], hipEventDisableTiming) != hipSuccess) {
         rc = bldp::set_error(BLDP_EHIP, "chunks_to_device: event create failed");
         break;
       }
-      evs.push_back(ev);
-      if (hipMemcpyAsync((uint8_t *)dev_stage + lo, (uint8_t *)host_pinned + lo, (size_t)(hi - lo),
+      hipEvent_t ev = evs[b];
+      if (hipMemcpyAsync((uint8_t *)dev_stage + lo, hsrc, (size_t)(hi - lo),
                          hipMemcpyHostToDevice, cs) != hipSuccess ||
           hipEventRecord(ev, cs) != hipSuccess || hipStreamWaitEvent(s, ev, 0) != hipSuccess) {
         rc = bldp::set_error(BLDP_EHIP, "chunks_to_device: H2D copy of batch %lld failed",
@@ -403,15 +457,36 @@ static int chunks_to_device(
       ooff.push_back((uint64_t)(k * out_chunk_bytes));
       olen.push_back((uint64_t)out_chunk_bytes);
     }
+    // (the decoder reads each chunk's 12-byte header on the host, here: before
+    // the batch's slot can be reopened below)
     if (rc == BLDP_OK && !offs.empty())
-      rc = bldp_bslz4_decode_dev_async((int)offs.size(), (const uint8_t *)host_pinned,
+      rc = bldp::bslz4_decode_async_at((int)offs.size(), hsrc, (uint64_t)lo,
                                        (const uint8_t *)dev_stage, offs.data(), lens.data(), 4,
                                        (uint8_t *)dev_out, ooff.data(), olen.data(), err_dev, s);
+    if (rc == BLDP_OK && ring && b >= 1) {  // slot of batch b - 1: free once its copy is done
+      if (evs[b - 1] && hipEventSynchronize(evs[b - 1]) != hipSuccess) {
+        rc = bldp::set_error(BLDP_EHIP, "chunks_to_device: copy of batch %lld failed",
+                             (long long)(b - 1));
+        break;
+      }
+      {
+        std::lock_guard<std::mutex> lk(j.mu);
+        j.open.store(std::min<int64_t>(nbatch, b - 1 + nslot + 1));
+      }
+      j.gate.notify_all();
+    }
     k0 = k1;
   }
   const double t_reads = ms_since(t0);
   posted.finish(rc != BLDP_OK);  // (an error: cancel the readers first)
-  for (hipEvent_t ev : evs) (void)hipEventDestroy(ev);
+  // the ring's slots are reused by the next call: no copy out of them may
+  // outlive this one (the caller's buffer: bldp_bslz4_error waits instead)
+  for (hipEvent_t ev : evs)
+    if (ev) {
+      if (ring && hipEventSynchronize(ev) != hipSuccess && rc == BLDP_OK)
+        rc = bldp::set_error(BLDP_EHIP, "chunks_to_device: copy failed");
+      (void)hipEventDestroy(ev);
+    }
   if (stats) {
     stats[0] = t_first;
     stats[1] = t_reads;
@@ -424,32 +499,6 @@ static int chunks_to_device(
 // ---------------------------------------------------------------------------
 // Raw runs (uncompressed contiguous FBH5 `data`, SIGPROC data blocks) into a
 // dense device block through a ring of library-owned pinned slots.
-namespace {
-
-// The ring reused across calls of one device (under its call lock).
-void free_slots(Slots &sl) {
-  for (void *q : sl.p) (void)hipHostFree(q);
-  sl.p.clear();
-  sl.bytes = 0;
-}
-int ensure_slots(Slots &sl, int64_t bytes, int nslot) {
-  if (sl.bytes == bytes && (int)sl.p.size() == nslot) return BLDP_OK;
-  free_slots(sl);
-  for (int i = 0; i < nslot; ++i) {
-    void *q = nullptr;
-    if (hipHostMalloc(&q, (size_t)bytes, hipHostMallocDefault) != hipSuccess) {
-      free_slots(sl);
-      return bldp::set_error(BLDP_ENOMEM, "runs_to_device: %lld bytes of pinned slots",
-                             (long long)bytes);
-    }
-    sl.p.push_back(q);
-  }
-  sl.bytes = bytes;
-  return BLDP_OK;
-}
-
-}  // namespace
-
 // fds: one descriptor per run (runs of several files in one stream of
 // batches), or NULL: every run is in `fd`.
 static int runs_to_device(int fd, const int *fds, int64_t nrun, const int64_t *file_off,

@@ -898,9 +898,17 @@ def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 
         if len(sizes) > 1:
             offsets[1:] = np.cumsum(sizes[:-1])
         total = int(sizes.sum())
+        native = tab is not None and os.environ.get("BLDP_NATIVE_READ", "1") != "0"
         t_pin = time.perf_counter()
-        pinned = torch.empty(total + 16, dtype=torch.uint8, pin_memory=True)
-        host = pinned.numpy()
+        if native:
+            # the library's pinned slot ring stages the reads (batches no
+            # larger than its slots): no pinned buffer the size of the window
+            pinned = host = None
+            batch_bytes = min(batch_bytes, filestream.NATIVE_BATCH_BYTES)
+            first_batch_bytes = min(first_batch_bytes, batch_bytes)
+        else:
+            pinned = torch.empty(total + 16, dtype=torch.uint8, pin_memory=True)
+            host = pinned.numpy()
         t_pin = time.perf_counter() - t_pin
         batches = _batches_of(sizes, first_batch_bytes, batch_bytes, ramp)
         with torch.cuda.device(dev):
@@ -913,9 +921,10 @@ def _read_window_bslz4_dev(fname, idxs, device, timings=None, batch_bytes=64 << 
                     len(sizes) * cvol, dtype=torch.float32, device=dev)
             # the H2D copies (the critical path) on a cached high-priority stream
             copy_streams = [_copy_stream(dev, -1)]
-            if tab is not None and os.environ.get("BLDP_NATIVE_READ", "1") != "0":
+            if native:
                 # parsed chunk index: reads, copies and decodes queued natively
-                # (bldp_chunks_to_device: C++ reader threads, no interpreter lock)
+                # (bldp_chunks_to_device: C++ reader threads, no interpreter lock,
+                # through the device's pinned slot ring)
                 t_setup = time.perf_counter() - t0
                 if raw_chunks:  # no filter: stored chunks are raw elements
                     masks[:] = 1
@@ -1067,7 +1076,7 @@ def band_window_chunked_dev(fnames, idxs, device, timings=None, batch_bytes=64 <
 
     import torch
 
-    from . import _lib
+    from . import _lib, filestream
 
     if not fnames:
         return None
@@ -1113,11 +1122,13 @@ def band_window_chunked_dev(fnames, idxs, device, timings=None, batch_bytes=64 <
     if len(sizes) > 1:
         offsets[1:] = np.cumsum(sizes[:-1])
     total = int(sizes.sum())
-    batches = _batches_of(sizes, first_batch_bytes, batch_bytes, True)
+    # reads staged through the library's pinned slot ring: batches no larger
+    # than its slots, no pinned buffer the size of the band
+    batch_bytes = min(batch_bytes, filestream.NATIVE_BATCH_BYTES)
+    batches = _batches_of(sizes, min(first_batch_bytes, batch_bytes), batch_bytes, True)
     bend = np.array([k1 for _, k1 in batches], np.int64)
     dev = torch.device(device)
     t_setup = time.perf_counter() - t0
-    pinned = torch.empty(total + 16, dtype=torch.uint8, pin_memory=True)
     with torch.cuda.device(dev):
         cdev = torch.empty(total + 16, dtype=torch.uint8, device=dev)
         # chunks never written read as the fill value 0
@@ -1135,7 +1146,7 @@ def band_window_chunked_dev(fnames, idxs, device, timings=None, batch_bytes=64 <
             rc = L.bldp_file_chunks_to_device(
                 len(sizes), fdk.ctypes.data, faddr.ctypes.data, sizes.ctypes.data,
                 offsets.ctypes.data, masks.ctypes.data, len(bend), bend.ctypes.data,
-                pinned.data_ptr(), cdev.data_ptr(), total + 16, packed.data_ptr(), 4 * cvol,
+                None, cdev.data_ptr(), total + 16, packed.data_ptr(), 4 * cvol,
                 4 * packed.numel(), err.data_ptr(), _copy_stream(dev, -1).cuda_stream, sp, stats)
             # (waits for every queued copy and decode, also after a failed call)
             rc2 = L.bldp_bslz4_error(err.data_ptr(), sp)
@@ -1177,8 +1188,10 @@ def band_window_chunked_dev(fnames, idxs, device, timings=None, batch_bytes=64 <
 def _native_chunks(fname, faddr, sizes, offsets, masks, batches, pinned, cdev, packed, cvol,
                    copy_stream, _lib, torch):
     """bldp_chunks_to_device for the chunks of the box, then the decoder's
-    error check (which also waits for the copies: the pinned buffer is free
-    once this returns).  Returns the call's stats (4 doubles)."""
+    error check (which also waits for the copies: a pinned buffer is free
+    once this returns).  ``pinned`` None: the reads are staged through the
+    library's pinned slot ring (every batch no larger than a slot).  Returns
+    the call's stats (4 doubles)."""
     import ctypes as ct
 
     fa = np.ascontiguousarray(faddr, np.int64)
@@ -1193,8 +1206,8 @@ def _native_chunks(fname, faddr, sizes, offsets, masks, batches, pinned, cdev, p
     try:
         rc = L.bldp_chunks_to_device(
             fd, len(sz), fa.ctypes.data, sz.ctypes.data, of.ctypes.data, mk.ctypes.data,
-            len(bend), bend.ctypes.data, pinned.data_ptr(), cdev.data_ptr(),
-            min(pinned.numel(), cdev.numel()),
+            len(bend), bend.ctypes.data, None if pinned is None else pinned.data_ptr(),
+            cdev.data_ptr(), cdev.numel() if pinned is None else min(pinned.numel(), cdev.numel()),
             packed.data_ptr() if packed is not None else None, 4 * cvol,
             4 * packed.numel() if packed is not None else 0, err.data_ptr(),
             copy_stream.cuda_stream, _lib.stream_ptr(), stats)

@@ -74,6 +74,8 @@ extern "C" {
  * 4: bldp_band_reduce_multi_f32 takes a flags word (BLDP_BAND_STAGED replaces
  *    the process-wide "force_staged" option and BLDP_FORCE_STAGED);
  *    bldp_peer_access; bldp_device_to_host; bldp_file_chunks_to_device;
+ *    bldp_chunks_to_device stages through the pinned slot ring when
+ *    host_pinned is NULL;
  *    bldp_plan_option checks each
  *    option's domain; bldp_read_probe moved out of the product library
  *    (tools/hbm_probe.hip, build/libbldp_probe.so); plan options
@@ -376,7 +378,13 @@ BLDP_API int bldp_bslz4_error(const int *err_dev, void *stream);
  * parallel preads (a persistent pool of reader threads, BLDP_READ_THREADS)
  * into host_pinned + stage_off[k] (both staging buffers hold stage_bytes;
  * dev_out holds out_bytes: every table entry is checked against them before
- * anything is read).  Chunks [batch_end[b-1], batch_end[b]) form
+ * anything is read).  host_pinned NULL (since ABI 4): the reads are staged
+ * through the device's library-owned pinned slot ring instead (the one
+ * bldp_runs_to_device uses, 8 x 32 MiB unless a batch's staged range needs
+ * larger slots), batch b in slot b % nslot once that slot's previous copy is
+ * done, so pinned host memory stays bounded whatever the window's size; the
+ * call then also waits for its last copy before returning.
+ * Chunks [batch_end[b-1], batch_end[b]) form
  * batch b: once its reads land, its staged byte range is copied to dev_stage
  * (same offsets) on copy_stream, `stream` waits for that copy, and the batch's
  * chunks are decoded on `stream` into dev_out + k * out_chunk_bytes

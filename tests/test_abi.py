@@ -400,6 +400,16 @@ def test_chunks_to_device_validates_before_any_read(pkg, L):
     assert call(obytes=799) == pkg._lib.BLDP_EINVAL and "exceed" in pkg._lib.last_error()
     assert L.bldp_chunks_to_device(-1, 0, None, None, None, None, 0, None, None, None, 0, None, 0,
                                    0, None, None, None, None) == 0  # nothing to do
+    # host_pinned NULL (the library's slot ring): the same checks, before any
+    # ring is allocated or a device is touched
+    be = np.array([1], np.int64)
+    assert L.bldp_chunks_to_device(-1, len(sz), fa.ctypes.data, sz.ctypes.data, of.ctypes.data,
+                                   mk.ctypes.data, 1, be.ctypes.data, None, fake, 200, fake, 400,
+                                   800, fake, None, None, None) == pkg._lib.BLDP_EINVAL
+    assert "end at chunk" in pkg._lib.last_error()
+    assert L.bldp_chunks_to_device(-1, len(sz), fa.ctypes.data, sz.ctypes.data, of.ctypes.data,
+                                   mk.ctypes.data, 1, be.ctypes.data, None, None, 200, fake, 400,
+                                   800, fake, None, None, None) == pkg._lib.BLDP_EINVAL
 
 
 def test_runs_to_device_validates_before_any_read(pkg, L):

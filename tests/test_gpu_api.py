@@ -1116,6 +1116,60 @@ def test_compressed_and_raw_files_random_windows(pkg, orc, tmp_path, seed):
             assert same_bits(got, want), (f, idxs, F, T, op, chunk)
 
 
+def test_chunk_reader_stages_through_the_slot_ring(pkg, tmp_path):
+    """The native chunk reader stages compressed reads through the device's
+    pinned slot ring (bldp_chunks_to_device with host_pinned NULL), the ring
+    bldp_runs_to_device uses, so no pinned buffer the size of the window is
+    allocated.  Cases, each bit-exact against the data written:
+    - a 260 MB window of mixed chunks (bitshuffle/LZ4, stored unfiltered with
+      per-chunk values, never written): more batches than the ring has
+      slots, so slots are reused;
+    - unfiltered chunks of 40 MiB, larger than a 32 MiB slot: the ring grows;
+    - raw-file reads in between, which take the ring back to 8 x 32 MiB."""
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "bslz4_v1.npz"))
+    comp, dec = z["chunk_gamma_chunk_b2048"].tobytes(), z["raw_gamma_chunk_b2048"]
+    C = pkg.COLON
+    ct, cc = 16, 4096
+    gt, gc = 80, 16
+    want = np.empty((gt * ct, 1, gc * cc), np.float32)  # C order (time, IF, chan)
+    chunks = []
+    for t in range(gt):
+        for c in range(gc):
+            k = t * gc + c
+            blk = want[t * ct:(t + 1) * ct, :, c * cc:(c + 1) * cc]
+            if k % 7 == 3:  # stored without the filter: values unique to the chunk
+                v = (np.arange(ct * cc, dtype=np.float32).reshape(ct, 1, cc) + 65536.0 * k)
+                blk[...] = v
+                chunks.append((1, v.tobytes()))
+            elif k % 11 == 5:  # never written: the fill value
+                blk[...] = 0.0
+                chunks.append(None)
+            else:
+                blk[...] = dec
+                chunks.append(comp)
+    big = str(tmp_path / "mixed.h5")
+    pkg.fbh5.write_bslz4_chunks(big, dict(foff=-1.0), (gc * cc, 1, gt * ct), (ct, 1, cc), chunks)
+    wide = np.asfortranarray(
+        np.arange(2 * 160 * 65536, dtype=np.float32).reshape(65536, 1, 320, order="F"))
+    wide_f = str(tmp_path / "wide.h5")
+    pkg.fbh5.write_bslz4_chunks(
+        wide_f, dict(foff=-1.0), (65536, 1, 320), (160, 1, 65536),
+        [(1, np.ascontiguousarray(wide[:, :, 160 * i:160 * (i + 1)].transpose(2, 1, 0)).tobytes())
+         for i in range(2)])
+    raw = np.asfortranarray(np.random.default_rng(3).integers(0, 256, (8192, 1, 64))
+                            .astype(np.float32))
+    raw_f = str(tmp_path / "raw.h5")
+    pkg.fbh5.write(raw_f, dict(foff=-1.0), raw)
+    want_j = np.asfortranarray(want.transpose(2, 1, 0))
+    for f, w in ((big, want_j), (raw_f, raw), (wide_f, wide), (raw_f, raw), (big, want_j),
+                 (wide_f, wide)):
+        got = pkg.WorkerFunctions.getdata(f, (C, C, C))
+        assert same_bits(got, w), f
+    J = pkg.JRange
+    got = pkg.WorkerFunctions.getdata(big, (J(4000, 40000), C, J(17, 1000)), fqavby=1)
+    assert same_bits(got, want_j[3999:40000, :, 16:1000])
+
+
 def test_cfg5_share_full_size_host_path(pkg, orc):
     """One GPU's share of cfg5 (bank b of 4 bands x {0000, 0001, 0002}) at the
     full per-array sizes (4 GiB, 1.8 GB, 73 MB) through bldp_reduce_host_f32

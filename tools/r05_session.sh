@@ -65,6 +65,8 @@ for s in $STEPS; do
       run "ab_$SUITE" 900 python tools/ab_variants.py --run --suite "$SUITE" --rounds 5 \
           --variants "$V" --json "$OUT/ab_$SUITE.json" ;;
     kurt_*) run "$s" 300 python bench.py --mode kurtosis --config "${s#kurt_}" ;;
+    file) run file 300 python bench.py --mode file ;;
+    rawfile) run rawfile 300 python bench.py --mode rawfile ;;
     typed) run typed 300 python bench.py --mode typed ;;
     typedwarm) run typedwarm 300 python bench.py --mode typed --cache warm ;;
     typedpipe_*) run "$s" 300 python bench.py --mode typed --plan-option typed_pipe="${s#typedpipe_}" ;;
