@@ -159,6 +159,12 @@ constexpr int kRowMaxWaves = 4, kRowtMaxWaves = 6, kTileMaxWaves = 3;
 // the 0001 band (ab_rowt_r05g2.json, ab_t1_0001_r05g2.json); the vector
 // kernel at 2 per CU lost 60% on the 0001 band at F = 64.
 constexpr unsigned kRowShm = 0, kRowtShm = 0, kVecShm = 0;
+// k_reduce_narrow (F = 1, 2: a lane's float4 column down the time block,
+// 16 rows in flight), 0 = no cap: at 2 / 3 / 4 workgroups per CU it was
+// +2.5-7% / +-0.5% / +-0.8% on the 0000 band at F = 1, 2 and T = 8, 16
+// (round 5, profiles/r05/ab_narrow_r05q.json; 14 waves per CU, half the
+// cycles parked on loads: cfg3f1_sq_summary_r05p.json).
+constexpr unsigned kNarrowShm = 0;
 // The short-time-block kernels (k_reduce_rowt, k_reduce_narrowt,
 // k_reduce_lanet) also take tavby = 3 and 8, not only 1, 2, 4 (plan option
 // "t38"; the 512-channel 0001 product at tavby = 3 ran one 3-row block per
@@ -1879,9 +1885,9 @@ hipError_t launch_op(const RedArgs &a, const Plan &p, hipStream_t s) {
     e = launch_vec<OP>(a, p, s);
   } else if (p.path == PATH_NARROW) {
     if (a.F == 1)
-      BLDP_LAUNCH((k_reduce_narrow<OP, 1>), grid, block, 0, s, a);
+      BLDP_LAUNCH((k_reduce_narrow<OP, 1>), grid, block, kNarrowShm, s, a);
     else
-      BLDP_LAUNCH((k_reduce_narrow<OP, 2>), grid, block, 0, s, a);
+      BLDP_LAUNCH((k_reduce_narrow<OP, 2>), grid, block, kNarrowShm, s, a);
     e = hipGetLastError();
   } else if (p.path == PATH_NARROW_MIS) {
     BLDP_LAUNCH((k_reduce_narrow_mis<OP, 1>), grid, block, 0, s, a);

@@ -165,6 +165,9 @@ VARIANTS = {
     "rowo4": {"patch": [RS(row=36864)]},
     "rowto2": {"patch": [RS(rowt=65536)]},
     "rowto4": {"patch": [RS(rowt=36864)]},
+    "narrowo2": {"patch": [(K, "constexpr unsigned kNarrowShm = 0;", "constexpr unsigned kNarrowShm = 65536;")]},
+    "narrowo3": {"patch": [(K, "constexpr unsigned kNarrowShm = 0;", "constexpr unsigned kNarrowShm = 49152;")]},
+    "narrowo4": {"patch": [(K, "constexpr unsigned kNarrowShm = 0;", "constexpr unsigned kNarrowShm = 36864;")]},
     "veco2": {"patch": [RS(vec=65536)]},
     "veco4": {"patch": [RS(vec=36864)]},
     "rowmw6": {"patch": [(K, "constexpr int kRowMaxWaves = 4,", "constexpr int kRowMaxWaves = 6,")]},
@@ -731,6 +734,19 @@ def run(names, rounds, iters, suite="main"):
             kurt_case(f"kurt 0002 band nt{nt}", b2, [0, 65536, 1, 0, 1, 1, 0, nt, 1])
         kurt_case("kurt 0002 file nt32", b2[:1], [0, 65536, 1, 0, 1, 1, 0, 32, 1])
         cases_done = True
+    elif suite == "narrow":  # k_reduce_narrow: F = 1, 2 over long enough time blocks
+        n = 1 << 26
+        band_case("cfg3 F1 T16", b3, 1, 16)
+        band_case("cfg3 1 bank F1 T16", b3[:1], 1, 16)
+        band_case("cfg3 F2 T16", b3, 2, 16)
+        band_case("cfg3 F1 T8", b3, 1, 8)
+        band_case("cfg3 F1 T16 c0=4", b3, 1, 16, [4, n - 4, 1, 0, 1, 1, 0, 16, 1])
+        del b3
+        b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
+        band_case("cfg2 F1 T16", b2, 1, 16, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
+        band_case("cfg1 F1 T16", b2[:1], 1, 16, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
+        band_case("cfg2 F2 T8", b2, 2, 8, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
+        cases_done = True
     elif suite == "kleaf":  # the streamed-leaf kurtosis path only
         del b3
         b4 = [eng.synth(512, 1, 880000, 8, seed=10 * b + 1, kind=0) for b in range(8)]
@@ -839,7 +855,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--suite", default="main", choices=["main", "il", "occ", "typed", "kregs", "rows", "t1_0001", "wavet", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy", "wide", "grid0", "grid1", "t38", "lane3", "kgrid", "lanetpack", "kshort", "kfile"])
+    ap.add_argument("--suite", default="main", choices=["main", "il", "occ", "typed", "kregs", "narrow", "rows", "t1_0001", "wavet", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy", "wide", "grid0", "grid1", "t38", "lane3", "kgrid", "lanetpack", "kshort", "kfile"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:
