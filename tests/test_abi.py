@@ -502,6 +502,18 @@ def test_julia_binding_ccalls_match_the_header():
         assert n in named, n
 
 
+def test_julia_binding_abi_version_is_the_headers():
+    """BLDPHip.__init__ refuses a library whose bldp_abi_version differs from
+    the ABI_VERSION it was written against: that constant must be the
+    header's BLDP_ABI_VERSION (the ccall signatures above are checked against
+    the same header), or every Julia worker fails at load."""
+    hdr = open(os.path.join(REPO, "include", "bldp.h")).read()
+    jl = open(os.path.join(REPO, "bldistributeddataproducts.jl_amd", "julia", "BLDPHip.jl")).read()
+    want = int(re.search(r"#define BLDP_ABI_VERSION (\d+)", hdr).group(1))
+    got = int(re.search(r"^const ABI_VERSION = (\d+)$", jl, re.M).group(1))
+    assert got == want, (got, want)
+
+
 def test_typed_entry_points_host_checks(pkg, L):
     """Julia's fqav result element types (bldp_reduce_out_dtype, host only) and
     the typed entry points' argument checks (nothing is launched)."""
