@@ -3,6 +3,9 @@
 # MiB) against the round-5 build that staged each window in one pinned buffer
 # (build/prevtree), alternating on one box: bench.py --mode file (one 1 GiB
 # file) and tools/getband_probe.py --compressed (8 files, 476 MB stored).
+# build/prevtree: `git archive <rev> bench.py __graft_entry__.py
+# bldistributeddataproducts.jl_amd tools/getband_probe.py tests/golden | tar -x
+# -C build/prevtree`, plus oracle/ and that revision's built libbldp_hip.so.
 set -u
 O=gpurun_out/${1:-r05m}; mkdir -p $O
 R=$PWD
