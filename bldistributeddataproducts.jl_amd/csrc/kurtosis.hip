@@ -1139,7 +1139,9 @@ constexpr unsigned kKurtLeafShm = 0, kKurtMidShm = 0;
 // uncapped: the 0000 band nt = 12 / 16 0.946 / 0.969, one 0000 bank nt = 16
 // 0.920, c0 = 1 0.974, the 0002 band nt = 16 0.965; but nt = 4 / 8 1.21 /
 // 1.09 (there the Float64 outputs are 1/2 - 1/4 of the traffic) and nt = 32
-// 1.02 (3 / 4 per CU: within +-3% either way).
+// 1.02 (3 / 4 per CU: within +-3% either way).  Re-run on another box
+// (ab_kregs_r05s.json, against this cap): uncapped 1.004 on the band, 1.038 on
+// one bank; 1 per CU 1.15-1.53; 3 per CU within +-1%.
 constexpr unsigned kKurtRegsShm = 65536;
 constexpr int64_t kKurtRegsCapLo = 12, kKurtRegsCapHi = 16;
 

@@ -157,9 +157,11 @@ VARIANTS = {
     "kleafo2": {"patch": [(KU, "constexpr unsigned kKurtLeafShm = 0,", "constexpr unsigned kKurtLeafShm = 65536,")]},
     "kleafo4": {"patch": [(KU, "constexpr unsigned kKurtLeafShm = 0,", "constexpr unsigned kKurtLeafShm = 36864,")]},
     "kmido2": {"patch": [(KU, "kKurtMidShm = 0;", "kKurtMidShm = 65536;")]},
-    "kregso3": {"patch": [(KU, "constexpr unsigned kKurtRegsShm = 0;", "constexpr unsigned kKurtRegsShm = 49152;")]},
-    "kregso2": {"patch": [(KU, "constexpr unsigned kKurtRegsShm = 0;", "constexpr unsigned kKurtRegsShm = 65536;")]},
-    "kregso4": {"patch": [(KU, "constexpr unsigned kKurtRegsShm = 0;", "constexpr unsigned kKurtRegsShm = 36864;")]},
+    # k_kurt_regs at 12-16 spectra runs at 2 per CU since round 5 (kregso2 of
+    # profiles/r05/ab_kregs_r05h.json); these move that cap
+    "kregsnocap": {"patch": [(KU, "constexpr unsigned kKurtRegsShm = 65536;", "constexpr unsigned kKurtRegsShm = 0;")]},
+    "kregso1": {"patch": [(KU, "constexpr unsigned kKurtRegsShm = 65536;", "constexpr unsigned kKurtRegsShm = 98304;")]},
+    "kregso3": {"patch": [(KU, "constexpr unsigned kKurtRegsShm = 65536;", "constexpr unsigned kKurtRegsShm = 49152;")]},
     "rowo1": {"patch": [RS(row=98304)]},
     "rowo2": {"patch": [RS(row=65536)]},
     "rowo4": {"patch": [RS(row=36864)]},
