@@ -16,11 +16,16 @@
 //     (bldp_bslz4_decode_dev_async) or raw-chunk copies on `stream`.
 // Batch b+1 is being read while batch b is copied and decoded.
 #include <errno.h>
+#include <pthread.h>
+#include <sched.h>
+#include <sys/syscall.h>
 #include <unistd.h>
 
 #include <atomic>
 #include <chrono>
+#include <cctype>
 #include <condition_variable>
+#include <cstdio>
 #include <cstring>
 #include <cstdlib>
 #include <map>
@@ -67,10 +72,79 @@ struct Job {
   std::condition_variable cv, gate;
 };
 
+// The CPUs of device `dev`'s NUMA node that this process may run on (the
+// node of the GPU's PCIe root, where the pinned slots the readers fill should
+// be copied from and to); false when the node or its CPU list is unknown.
+int device_numa_node(int dev) {
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, (int)sizeof(bus), dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  for (char *c = bus; *c; ++c) *c = (char)tolower((unsigned char)*c);
+  char path[160];
+  snprintf(path, sizeof(path), "/sys/bus/pci/devices/%s/numa_node", bus);
+  FILE *f = fopen(path, "r");
+  if (!f) return -1;
+  int node = -1;
+  if (fscanf(f, "%d", &node) != 1) node = -1;
+  fclose(f);
+  return node;
+}
+
+bool device_node_cpus(int dev, cpu_set_t *set) {
+  const int node = device_numa_node(dev);
+  if (node < 0) return false;
+  char path[160];
+  snprintf(path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", node);
+  FILE *f = fopen(path, "r");
+  if (!f) return false;
+  cpu_set_t want;
+  CPU_ZERO(&want);
+  int lo = 0, hi = 0;
+  char sep = 0;
+  while (fscanf(f, "%d", &lo) == 1) {  // "0-63,128-191"
+    hi = lo;
+    if (fscanf(f, "%c", &sep) == 1 && sep == '-') {
+      if (fscanf(f, "%d", &hi) != 1) break;
+      if (fscanf(f, "%c", &sep) != 1) sep = 0;
+    }
+    for (int c = lo; c <= hi && c < CPU_SETSIZE; ++c) CPU_SET(c, &want);
+    if (sep != ',') break;
+  }
+  fclose(f);
+  cpu_set_t allowed;
+  if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return false;
+  CPU_AND(set, &want, &allowed);
+  return CPU_COUNT(set) > 0;
+}
+
+// Reader threads: 16, or 4 fewer than the CPUs the process may use when that
+// is less (the cgroup's CPU quota, else the affinity mask), so the readers do
+// not starve the calling thread and the HIP runtime's threads of their quota:
+// on a 16-CPU quota 12 readers read a band 10-25% faster than 16 (round 5,
+// profiles/r05/reads/).
+int default_reader_threads() {
+  int cpus = (int)std::thread::hardware_concurrency();
+  cpu_set_t allowed;
+  if (sched_getaffinity(0, sizeof(allowed), &allowed) == 0) cpus = CPU_COUNT(&allowed);
+  if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {  // cgroup v2: "quota period" or "max ..."
+    long long quota = 0, period = 0;
+    if (fscanf(f, "%lld %lld", &quota, &period) == 2 && quota > 0 && period > 0)
+      cpus = std::min<long long>(cpus, std::max<long long>(1, quota / period));
+    fclose(f);
+  }
+  return std::min(16, std::max(2, cpus >= 16 + 4 ? 16 : cpus - 4));
+}
+
 class ReadPool {
  public:
-  explicit ReadPool(int n) {
-    for (int i = 0; i < n; ++i) th_.emplace_back([this] { work(); });
+  // n reader threads, each confined to `cpus` when given
+  explicit ReadPool(int n, const cpu_set_t *cpus = nullptr) {
+    for (int i = 0; i < n; ++i) {
+      th_.emplace_back([this] { work(); });
+      if (cpus) (void)pthread_setaffinity_np(th_.back().native_handle(), sizeof(*cpus), cpus);
+    }
   }
   ~ReadPool() {
     {
@@ -200,6 +274,8 @@ struct DevIO {
   std::mutex call;
   std::unique_ptr<ReadPool> pool;
   Slots slots;
+  bool node_pinned = false;  // readers confined to the GPU's NUMA node
+  int node = -1;             // the GPU's NUMA node (-1: unknown)
   bool retired = false;  // released by bldp_finalize (under `call`)
 };
 std::mutex g_io_mu;
@@ -220,9 +296,17 @@ std::shared_ptr<DevIO> dev_io(std::unique_lock<std::mutex> &call) {
       if (!slot) {
         int n = 0;
         if (const char *e = getenv("BLDP_READ_THREADS")) n = atoi(e);
-        if (n <= 0) n = std::min(16, std::max(2, (int)std::thread::hardware_concurrency()));
+        if (n <= 0) n = default_reader_threads();
         slot = std::make_shared<DevIO>();
-        slot->pool.reset(new ReadPool(n));
+        // the readers run on the CPUs of the GPU's NUMA node (BLDP_READ_AFFINITY=0:
+        // anywhere), so the page-cache copies into the pinned slots, which sit
+        // on that node too (ensure_slots), stay on the GPU's socket
+        cpu_set_t cpus;
+        const char *aff = getenv("BLDP_READ_AFFINITY");
+        const bool pin = !(aff && atoi(aff) == 0) && device_node_cpus(dev, &cpus);
+        slot->pool.reset(new ReadPool(n, pin ? &cpus : nullptr));
+        slot->node_pinned = pin;
+        slot->node = device_numa_node(dev);
       }
       io = slot;
     }
@@ -270,12 +354,28 @@ void free_slots(Slots &sl) {
   sl.p.clear();
   sl.bytes = 0;
 }
-int ensure_slots(Slots &sl, int64_t bytes, int nslot) {
+// node >= 0: the slots' pages are placed on that NUMA node, the GPU's (the
+// calling thread's memory policy set to prefer it while the runtime pins
+// them, hipHostMallocNumaUser); BLDP_SLOT_NUMA=0: wherever the runtime puts
+// them.
+int ensure_slots(Slots &sl, int64_t bytes, int nslot, int node = -1) {
   if (sl.bytes == bytes && (int)sl.p.size() == nslot) return BLDP_OK;
   free_slots(sl);
+  const char *e = getenv("BLDP_SLOT_NUMA");
+  const bool numa = node >= 0 && node < 64 && !(e && atoi(e) == 0);
+  constexpr int kMpolDefault = 0, kMpolPreferred = 1;  // <numaif.h>, no libnuma
+  unsigned long mask = 1ul << (node >= 0 && node < 64 ? node : 0);
+  if (numa && syscall(SYS_set_mempolicy, kMpolPreferred, &mask, 64) != 0) mask = 0;
+  struct Restore {
+    bool on;
+    ~Restore() {
+      if (on) (void)syscall(SYS_set_mempolicy, kMpolDefault, nullptr, 0);
+    }
+  } restore{numa && mask};
+  const unsigned flags = restore.on ? hipHostMallocNumaUser : hipHostMallocDefault;
   for (int i = 0; i < nslot; ++i) {
     void *q = nullptr;
-    if (hipHostMalloc(&q, (size_t)bytes, hipHostMallocDefault) != hipSuccess) {
+    if (hipHostMalloc(&q, (size_t)bytes, flags) != hipSuccess) {
       free_slots(sl);
       return bldp::set_error(BLDP_ENOMEM, "%lld bytes of pinned slots",
                              (long long)bytes);
@@ -394,7 +494,7 @@ static int chunks_to_device(
       if (const char *e = getenv("BLDP_RING_SLOTS")) nring = std::min(16, std::max(2, atoi(e)));
       const int rc = ensure_slots(io->slots, std::max(kRingSlotBytes, (span + (1 << 20) - 1) &
                                                                           ~(int64_t)((1 << 20) - 1)),
-                                  nring);
+                                  nring, io->node);
       if (rc) return rc;
     }
     nslot = (int64_t)io->slots.p.size();
@@ -543,7 +643,7 @@ static int runs_to_device(int fd, const int *fds, int64_t nrun, const int64_t *f
   }
   std::unique_lock<std::mutex> call;
   const std::shared_ptr<DevIO> io = dev_io(call);
-  int rc = ensure_slots(io->slots, slot_bytes, nslot);
+  int rc = ensure_slots(io->slots, slot_bytes, nslot, io->node);
   if (rc) return rc;
   // reads of batch b go to slot b % nslot at (hoff - b * slot_bytes); a batch
   // may be read once the copy out of its slot two rounds back is done
@@ -693,7 +793,7 @@ static int device_to_host(const void *src, void *dst, int64_t bytes, void *copy_
   std::unique_lock<std::mutex> call;
   const std::shared_ptr<DevIO> io = dev_io(call);
   // the ring the file readers left (any slot size), else the default one
-  int rc = io->slots.p.size() >= 2 ? BLDP_OK : ensure_slots(io->slots, kD2hSlotBytes, kD2hSlots);
+  int rc = io->slots.p.size() >= 2 ? BLDP_OK : ensure_slots(io->slots, kD2hSlotBytes, kD2hSlots, io->node);
   if (rc) return rc;
   const int64_t sb = io->slots.bytes, nslot = (int64_t)io->slots.p.size();
   const int64_t nbatch = (bytes + sb - 1) / sb;

@@ -375,7 +375,10 @@ BLDP_API int bldp_bslz4_error(const int *err_dev, void *stream);
  * chunk reads and filter 32008 of h5["data"][idxs...],
  * src/gbtworkerfunctions.jl:181-187).  Chunk k (stored_len[k] bytes at
  * file_off[k] of the open file `fd`; 0 bytes = never written) is read with
- * parallel preads (a persistent pool of reader threads, BLDP_READ_THREADS)
+ * parallel preads (a persistent pool of reader threads per device: 16, or 4
+ * fewer than the process's CPU quota when that is less, BLDP_READ_THREADS
+ * overrides; they run on the CPUs of the GPU's NUMA node and the pinned slots
+ * are placed on that node, BLDP_READ_AFFINITY=0 / BLDP_SLOT_NUMA=0 undo that)
  * into host_pinned + stage_off[k] (both staging buffers hold stage_bytes;
  * dev_out holds out_bytes: every table entry is checked against them before
  * anything is read).  host_pinned NULL (since ABI 4): the reads are staged
