@@ -3,7 +3,7 @@
 # kernel stats and PMC passes (one counter group per run, MI355X_MICROARCH.md
 # §rocprofv3), SQ counters beside the pure-read probe, tests, bench.
 #   usage: tools/r05_session.sh TAG [steps...]
-#   steps: smoke tests tests_K bench bench_CFG list ab_SUITE[:v1,v2,...]
+#   steps: smoke tests tests_K[+K2...] bench bench_CFG list ab_SUITE[:v1,v2,...]
 #          prof_CFG[_lbN] pmc_CFG[_lbN] sq_CFG[_lbN] cold_CFG typed typedprof typedpmc typedsq
 #          ab_SUITE getband getbandz
 # CFG[_lbN]: a config, optionally with --local-banks N (one rank's launch of an
@@ -41,8 +41,9 @@ for s in $STEPS; do
     list) run list 120 rocprofv3 -L ;;
     tests) run tests 1100 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 \
           --timeout-method thread ;;
-    tests_*) run "$s" 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 \
-          --timeout-method thread -k "${s#tests_}" ;;
+    tests_*) K=${s#tests_}  # tests_a+b: -k "a or b"
+      run "$s" 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 \
+          --timeout-method thread -k "${K//+/ or }" ;;
     bench) run bench 600 python bench.py ;;
     bench_*) run "$s" 600 python bench.py $(bench_args "${s#bench_}" | sed 's/--no-cpu-baseline//') ;;
     benchn_*) run "$s" 600 python bench.py $(bench_args "${s#benchn_}") ;;
