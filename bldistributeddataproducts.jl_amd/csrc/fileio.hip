@@ -621,20 +621,43 @@ static int runs_to_device(int fd, const int *fds, int64_t nrun, const int64_t *f
     return bldp::set_error(BLDP_EINVAL, "runs_to_device: %lld bytes exceed the %lld-byte "
                            "destination", (long long)total, (long long)dst_bytes);
   if (total == 0) return BLDP_OK;
-  const int64_t nbatch = (total + slot_bytes - 1) / slot_bytes;
-  // pieces: runs cut at batch (slot) boundaries and into ~8 pieces per slot;
+  // batches: slot-sized, but (blocks of more than 4 slots) the first two and
+  // the last two ramp (slot/4, slot/2 ... slot/2, slot/4), so the first copy
+  // starts after a quarter slot of reads and the copy left after the last
+  // read is a quarter slot (BLDP_RUNS_RAMP=0: uniform, a probe knob)
+  std::vector<int64_t> blo;  // batch b = [blo[b], blo[b + 1])
+  {
+    const char *e = getenv("BLDP_RUNS_RAMP");
+    const bool ramp = !(e && atoi(e) == 0) && total > 4 * slot_bytes;
+    const int64_t q = std::max<int64_t>(1 << 20, slot_bytes / 4);
+    const int64_t h = std::max<int64_t>(1 << 20, slot_bytes / 2);
+    int64_t at = 0, mid_end = total;
+    blo.push_back(0);
+    if (ramp) {
+      blo.push_back(at += q);
+      blo.push_back(at += h);
+      mid_end = total - h - q;
+    }
+    while (at < mid_end) blo.push_back(at = std::min(at + slot_bytes, mid_end));
+    if (ramp) {
+      blo.push_back(at += h);
+      blo.push_back(at += q);
+    }
+  }
+  const int64_t nbatch = (int64_t)blo.size() - 1;
+  // pieces: runs cut at batch boundaries and into ~8 pieces per batch;
   // piece.hoff is the offset in the whole block (the slot is batch % nslot)
-  const int64_t piece = std::max<int64_t>(256 << 10, slot_bytes / 8);
   Job j;
   j.fd = fd;
   j.left.reset(new std::atomic<int64_t>[nbatch]);
   for (int64_t b = 0; b < nbatch; ++b) j.left[b].store(0);
-  int64_t pos = 0;
+  int64_t pos = 0, b = 0;
   for (int64_t r = 0; r < nrun; ++r) {
     int64_t x = 0;
     while (x < len[r]) {
-      const int64_t b = (pos + x) / slot_bytes;
-      const int64_t n = std::min({piece, len[r] - x, (b + 1) * slot_bytes - (pos + x)});
+      while (pos + x >= blo[b + 1]) ++b;
+      const int64_t piece = std::max<int64_t>(256 << 10, (blo[b + 1] - blo[b]) / 8);
+      const int64_t n = std::min({piece, len[r] - x, blo[b + 1] - (pos + x)});
       j.pieces.push_back({file_off[r] + x, pos + x, n, (int32_t)b, fds ? fds[r] : -1});
       j.left[b].fetch_add(1);
       x += n;
@@ -645,10 +668,11 @@ static int runs_to_device(int fd, const int *fds, int64_t nrun, const int64_t *f
   const std::shared_ptr<DevIO> io = dev_io(call);
   int rc = ensure_slots(io->slots, slot_bytes, nslot, io->node);
   if (rc) return rc;
-  // reads of batch b go to slot b % nslot at (hoff - b * slot_bytes); a batch
-  // may be read once the copy out of its slot two rounds back is done
+  // reads of batch b go to slot b % nslot at (hoff - blo[b]); a batch may be
+  // read once the copy out of its slot one round back is done
   j.slot_base = &io->slots.p;
   j.slot_bytes = slot_bytes;
+  j.batch_lo.assign(blo.begin(), blo.end() - 1);
   j.open.store(std::min<int64_t>(nbatch, nslot));
   std::vector<hipEvent_t> evs(nbatch, nullptr);
   ReadPool *rp = io->pool.get();
@@ -665,7 +689,7 @@ static int runs_to_device(int fd, const int *fds, int64_t nrun, const int64_t *f
                            strerror(e));
       break;
     }
-    const int64_t lo = b * slot_bytes, n = std::min(slot_bytes, total - lo);
+    const int64_t lo = blo[b], n = blo[b + 1] - lo;
     if (hipEventCreateWithFlags(&evs[b], hipEventDisableTiming) != hipSuccess ||
         hipMemcpyAsync((uint8_t *)dev_dst + lo, io->slots.p[b % nslot], (size_t)n,
                        hipMemcpyHostToDevice, cs) != hipSuccess ||

@@ -787,6 +787,36 @@ def test_raw_files_stream_to_gpu(pkg, orc, tmp_path, monkeypatch, native):
                                             .permute(2, 1, 0)), a)
 
 
+@pytest.mark.parametrize("ramp", ["1", "0"])
+def test_raw_reader_ramped_batches(pkg, orc, tmp_path, monkeypatch, ramp):
+    """bldp_runs_to_device / bldp_file_runs_to_device cut blocks of more than
+    4 slots into batches of slot/4, slot/2, slots..., slot/2, slot/4
+    (BLDP_RUNS_RAMP=0: slot-sized).  With 4 MiB slots: one 20 MB raw file
+    (whole, and a channel span per row: many runs crossing batch boundaries)
+    and a band of three raw files through the band read, bit-exact."""
+    monkeypatch.setenv("BLDP_RUNS_RAMP", ramp)
+    monkeypatch.setenv("BLDP_NATIVE_READ", "1")
+    monkeypatch.setattr(pkg.filestream, "NATIVE_BATCH_BYTES", 4 << 20)
+    rng = np.random.default_rng(13)
+    J, C = pkg.JRange, pkg.COLON
+    banks, names = [], []
+    for b in range(3):
+        a = np.asfortranarray(rng.integers(0, 256, (4096, 2, 600)).astype(np.float32))
+        p = str(tmp_path / f"r{b}.h5")
+        pkg.fbh5.write(p, dict(foff=-187.5 / 4096, nfpc=64), a)
+        banks.append(a)
+        names.append(p)
+    W = pkg.WorkerFunctions
+    for idxs, F, T in (((C, C, C), 1, 1), ((J(1025, 2048), C, J(3, 598)), 4, 2)):
+        win = pkg.idxs.to_window(pkg.sanitizeidxs(idxs), banks[0].shape)
+        got = W.getdata(names[0], idxs, fqavby=F, tavby=T)
+        assert same_bits(got, orc.reduce(banks[0], F, T, "sum", win)), idxs
+    tm = {}
+    got = pkg.GBT._band_on_device([0] * 3, names, (C, C, C), 64, "sum", 8, None, timings=tm)
+    assert tm["path"] == "raw band", tm
+    assert same_bits(got, orc.stitch([orc.reduce(a, 64, 8) for a in banks]))
+
+
 def test_truncated_file_raises_read_error(pkg, tmp_path, monkeypatch):
     """A read past the end of a file (truncated after its layout was taken, or
     a stale index) is an I/O error (BLDP_EIO -> ReadError, an OSError), not an
