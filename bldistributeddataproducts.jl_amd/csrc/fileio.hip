@@ -128,12 +128,19 @@ int default_reader_threads() {
   int cpus = (int)std::thread::hardware_concurrency();
   cpu_set_t allowed;
   if (sched_getaffinity(0, sizeof(allowed), &allowed) == 0) cpus = CPU_COUNT(&allowed);
+  long long quota = 0, period = 0;
   if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {  // cgroup v2: "quota period" or "max ..."
-    long long quota = 0, period = 0;
-    if (fscanf(f, "%lld %lld", &quota, &period) == 2 && quota > 0 && period > 0)
-      cpus = std::min<long long>(cpus, std::max<long long>(1, quota / period));
+    if (fscanf(f, "%lld %lld", &quota, &period) != 2) quota = 0;
     fclose(f);
+  } else if (FILE *q = fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {  // cgroup v1
+    if (fscanf(q, "%lld", &quota) != 1) quota = 0;
+    fclose(q);
+    if (FILE *p = fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+      if (fscanf(p, "%lld", &period) != 1) period = 0;
+      fclose(p);
+    }
   }
+  if (quota > 0 && period > 0) cpus = std::min<long long>(cpus, std::max<long long>(1, quota / period));
   return std::min(16, std::max(2, cpus >= 16 + 4 ? 16 : cpus - 4));
 }
 
