@@ -1,6 +1,7 @@
-// fileio.hip — native reader for chunked FBH5 windows: the stored chunks of
-// the window's chunk box are read with parallel preads into the caller's
-// pinned host buffer, copied to the device in batches and decoded there.
+// fileio.hip — native file readers: the stored chunks of a chunked FBH5
+// window (or the byte runs of a raw file) are read with parallel preads into
+// pinned host memory (the device's library-owned slot ring, or a caller's
+// buffer), copied to the device in batches and decoded there.
 //
 // The reference reads the window with h5["data"][idxs...]
 // (src/gbtworkerfunctions.jl:181-187): libhdf5 reads each chunk, H5Zbitshuffle
@@ -14,7 +15,10 @@
 //   * the calling thread waits for each batch's pieces, queues its H2D copy on
 //     `copy_stream`, makes `stream` wait for it and queues the batch's decode
 //     (bldp_bslz4_decode_dev_async) or raw-chunk copies on `stream`.
-// Batch b+1 is being read while batch b is copied and decoded.
+// Batch b+1 is being read while batch b is copied and decoded.  The reader
+// threads run on the CPUs of the GPU's NUMA node and the slots sit on that
+// node (round 5: the page-cache copies stay on the GPU's socket and leave
+// CPU quota to the caller; profiles/r05/reads/).
 #include <errno.h>
 #include <pthread.h>
 #include <sched.h>
