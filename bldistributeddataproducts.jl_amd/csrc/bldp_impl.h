@@ -79,6 +79,7 @@ struct RedArgs {
                            // lane path: k_reduce_lanes (lanes along the stitched row)
   int32_t rsplit;          // k_reduce_rows: slices of a workgroup splitting a block's rows (1 = k_reduce_row)
   int32_t st_plain;        // row / il / rowt output stores plain (1) or non-temporal (0)
+  int32_t il_xcd;          // k_reduce_il: contiguous segments per XCD (small launches)
   float div;               // F*T, the mean divisor
 };
 

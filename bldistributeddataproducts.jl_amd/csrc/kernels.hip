@@ -165,6 +165,18 @@ constexpr unsigned kRowShm = 0, kRowtShm = 0, kVecShm = 0;
 // (round 5, profiles/r05/ab_narrow_r05q.json; 14 waves per CU, half the
 // cycles parked on loads: cfg3f1_sq_summary_r05p.json).
 constexpr unsigned kNarrowShm = 0;
+// Interleaved launches whose tiles are at least kIlXcdMinT rows deep and whose
+// rows are at most kIlXcdMaxPitch bytes apart give each XCD a contiguous run
+// of segments (RedArgs::il_xcd).  Round 5 A/B, one box, against the
+// dispatcher's round-robin order (profiles/r05/ab_ilxcd_r05ae.json,
+// ab_ilsmall_r05ad.json; a rebuilt identical library within +-1%):
+//   T = 16: 0002 band (256 KiB rows) 0.90-0.91, one 0002 file 0.93-0.95,
+//   16 / 32 / 128 MiB rows 0.93 / 0.91-0.95 / 0.97, but the 0000 product's
+//   256 MiB rows (cfg3) 1.005-1.022; T = 8: 16 MiB rows 0.95, the 0002 band
+//   1.00; T = 1 / 2 / 4: 1.08 / 1.00 / 1.00 (16 MiB rows), 1.05 / 1.01 / 1.01
+//   (0002 band).
+constexpr int kIlXcdMinT = 8;
+constexpr int64_t kIlXcdMaxPitch = (int64_t)128 << 20;
 // The short-time-block kernels (k_reduce_rowt, k_reduce_narrowt,
 // k_reduce_lanet) also take tavby = 3 and 8, not only 1, 2, 4 (plan option
 // "t38"; the 512-channel 0001 product at tavby = 3 ran one 3-row block per
@@ -1144,9 +1156,18 @@ __device__ __forceinline__ void il_tile(const RedArgs &a, int64_t bx, uint32_t i
   }
 }
 
+// a.il_xcd (deep tiles of rows up to 128 MiB apart, see kIlXcdMinT): workgroup x, which the
+// dispatcher sends to XCD x % 8, takes segment (x % 8) * X/8 + x / 8, so each
+// XCD streams one contiguous eighth of a row of segments instead of every
+// eighth segment.
 template <int OP, int K4, int GPW>
 __global__ __launch_bounds__(kBlock) void k_reduce_il(const RedArgs a) {
-  il_tile<OP, K4, GPW, kIlInflight>(a, blockIdx.x, blockIdx.y, blockIdx.z);
+  uint32_t x = blockIdx.x;
+  if (a.il_xcd) {
+    const uint32_t X = gridDim.x;
+    if ((X & 7) == 0) x = (x & 7) * (X >> 3) + (x >> 3);
+  }
+  il_tile<OP, K4, GPW, kIlInflight>(a, x, blockIdx.y, blockIdx.z);
 }
 
 // Vector path, small groups (PATH_VEC_ROW): F = 4*G4 channels with G4 = 1..64
@@ -2292,6 +2313,7 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
     const int64_t bytes = 4 * a.nbank * a.ni * (a.nco * F * a.nto * T + a.nco * a.nto);
     const int64_t o = opt(OPT_ST_PLAIN);
     a.st_plain = o == 2 ? 1 : o == 0 ? 0 : (bytes < ((int64_t)2 << 30) ? 1 : 0);
+    a.il_xcd = p.path == PATH_VEC_IL && T >= kIlXcdMinT && 4 * a.in_ld_t <= kIlXcdMaxPitch;
   }
   a.div = (float)(F * T);
   return p;

@@ -167,6 +167,12 @@ VARIANTS = {
     "rowo4": {"patch": [RS(row=36864)]},
     "rowto2": {"patch": [RS(rowt=65536)]},
     "rowto4": {"patch": [RS(rowt=36864)]},
+    "ctl": {"patch": []},  # the base sources rebuilt: the harness's own spread
+    # per-XCD segment order of k_reduce_il (round 5): off, or on everywhere
+    "ilxcdoff": {"patch": [(K, "constexpr int kIlXcdMinT = 8;", "constexpr int kIlXcdMinT = 1 << 30;")]},
+    "ilxcdall": {"patch": [(K, "constexpr int kIlXcdMinT = 8;", "constexpr int kIlXcdMinT = 1;"),
+                           (K, "constexpr int64_t kIlXcdMaxPitch = (int64_t)128 << 20;",
+                            "constexpr int64_t kIlXcdMaxPitch = INT64_MAX;")]},
     "narrowo2": {"patch": [(K, "constexpr unsigned kNarrowShm = 0;", "constexpr unsigned kNarrowShm = 65536;")]},
     "narrowo3": {"patch": [(K, "constexpr unsigned kNarrowShm = 0;", "constexpr unsigned kNarrowShm = 49152;")]},
     "narrowo4": {"patch": [(K, "constexpr unsigned kNarrowShm = 0;", "constexpr unsigned kNarrowShm = 36864;")]},
@@ -437,6 +443,41 @@ def run(names, rounds, iters, suite="main"):
         b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
         band_case("0002 band F1024 T16", b2, 1024, 16, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
         band_case("0002 band F512 T16", b2, 512, 16, [0, 65536, 1, 0, 1, 1, 0, 272, 1])
+        cases_done = True
+    elif suite == "ilsmall":  # round 5: the interleaved kernel on launches under 1 GiB
+        del b3
+        b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
+        w = [0, 65536, 1, 0, 1, 1, 0, 272, 1]
+        for F in (512, 1024, 2048, 4096):
+            band_case(f"0002 band F{F} T16", b2, F, 16, w)
+        band_case("0002 band F1024 T1", b2, 1024, 1, w)
+        band_case("0002 band F1024 T4", b2, 1024, 4, w)
+        band_case("0002 file F1024 T16", b2[:1], 1024, 16, w)
+        band_case("0002 file F512 T16", b2[:1], 512, 16, w)
+        b7 = [eng.synth(1 << 22, 1, 16, 1 << 20, seed=7 + b, kind=0) for b in range(8)]
+        band_case("16 MiB x 8 F1024 T16", b7, 1024, 16)
+        band_case("16 MiB x 8 F512 T16", b7, 512, 16)
+        b8 = [eng.synth(1 << 24, 1, 16, 1 << 20, seed=7 + b, kind=0) for b in range(8)]
+        band_case("64 MiB x 8 F1024 T16", b8, 1024, 16)
+        band_case("64 MiB x 1 F1024 T16", b8[:1], 1024, 16)
+        cases_done = True
+    elif suite == "ilxcd":  # round 5: where the per-XCD segment order pays (time block, row pitch)
+        band_case("cfg3 1 bank F1024 T16", b3[:1], 1024, 16)
+        band_case("cfg3 2 banks F1024 T16", b3[:2], 1024, 16)
+        del b3
+        b9 = [eng.synth(1 << 22, 1, 16, 1 << 20, seed=7 + b, kind=0) for b in range(8)]
+        for T in (1, 2, 4, 8, 16):
+            band_case(f"16 MiB rows x 8 F1024 T{T}", b9, 1024, T)
+        del b9
+        for lg in (23, 25):
+            bb = [eng.synth(1 << lg, 1, 16, 1 << 20, seed=7 + b, kind=0) for b in range(4)]
+            band_case(f"{4 << (lg - 20)} MiB rows x 4 F1024 T16", bb, 1024, 16)
+            band_case(f"{4 << (lg - 20)} MiB rows x 1 F1024 T16", bb[:1], 1024, 16)
+            del bb
+        b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
+        w = [0, 65536, 1, 0, 1, 1, 0, 272, 1]
+        for T in (2, 8, 16):
+            band_case(f"0002 band F1024 T{T}", b2, 1024, T, w)
         cases_done = True
     elif suite == "occ":  # round 5: occupancy caps over the reduce kernels' main shapes
         band_case("cfg3 8 banks F1024 T16", b3, 1024, 16)
@@ -857,7 +898,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--suite", default="main", choices=["main", "il", "occ", "typed", "kregs", "narrow", "rows", "t1_0001", "wavet", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy", "wide", "grid0", "grid1", "t38", "lane3", "kgrid", "lanetpack", "kshort", "kfile"])
+    ap.add_argument("--suite", default="main", choices=["main", "il", "ilsmall", "ilxcd", "occ", "typed", "kregs", "narrow", "rows", "t1_0001", "wavet", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy", "wide", "grid0", "grid1", "t38", "lane3", "kgrid", "lanetpack", "kshort", "kfile"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:
