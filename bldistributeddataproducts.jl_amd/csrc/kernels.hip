@@ -176,6 +176,11 @@ constexpr unsigned kNarrowShm = 0;
 //   1.00; T = 1 / 2 / 4: 1.08 / 1.00 / 1.00 (16 MiB rows), 1.05 / 1.01 / 1.01
 //   (0002 band).
 constexpr int kIlXcdMinT = 8;
+// The same order for k_reduce_row / k_reduce_rows, only for rows at least
+// kRowXcdMinPitch apart (round 5 A/B, profiles/r05/ab_rowxcd_r05ag.json:
+// 16 MiB rows at F = 64 / 256, T = 16 0.77 / 0.76; but the 0002 band (256 KiB
+// rows) 1.03, one 0002 file 1.12, the 0001 band (2 KiB rows) 1.02).
+constexpr int64_t kRowXcdMinPitch = (int64_t)4 << 20;
 constexpr int64_t kIlXcdMaxPitch = (int64_t)128 << 20;
 // The short-time-block kernels (k_reduce_rowt, k_reduce_narrowt,
 // k_reduce_lanet) also take tavby = 3 and 8, not only 1, 2, 4 (plan option
@@ -1185,6 +1190,16 @@ __global__ __launch_bounds__(kBlock) void k_reduce_il(const RedArgs a) {
 // CU in flight is faster on the 0002 shapes (A/B against uncapped /
 // k_reduce_vec: cfg1 5.85 vs 5.59 / 5.43 TB/s, cfg2 6.18 vs 5.78 / 6.10).
 constexpr int kRowBatch = 16;
+// The column block of a workgroup: blockIdx.x, or with a.il_xcd the per-XCD
+// contiguous order k_reduce_il uses (workgroup x runs on XCD x % 8).
+__device__ __forceinline__ uint32_t xcd_block(const RedArgs &a) {
+  uint32_t x = blockIdx.x;
+  if (a.il_xcd) {
+    const uint32_t X = gridDim.x;
+    if ((X & 7) == 0) x = (x & 7) * (X >> 3) + (x >> 3);
+  }
+  return x;
+}
 template <int OP, int G4>
 __global__ __launch_bounds__(kBlock)
 __attribute__((amdgpu_waves_per_eu(1, kRowMaxWaves)))
@@ -1193,7 +1208,7 @@ void k_reduce_row(const RedArgs a) {
   const uint32_t it = blockIdx.y, ni = (uint32_t)a.ni;
   const uint32_t to = it / ni, i = it - to * ni;
   const int bank = blockIdx.z;
-  const int64_t col = (int64_t)blockIdx.x * kBlock + tid;  // float4 column of the window
+  const int64_t col = (int64_t)xcd_block(a) * kBlock + tid;  // float4 column of the window
   const bool valid = col < a.nco * G4;
   const float id = R<OP>::id();
   float4 acc[kNacc];
@@ -1243,7 +1258,7 @@ void k_reduce_rows(const RedArgs a) {
   const uint32_t it = blockIdx.y, ni = (uint32_t)a.ni;
   const uint32_t to = it / ni, i = it - to * ni;
   const int bank = blockIdx.z;
-  const int64_t col = (int64_t)blockIdx.x * CW + c;  // float4 column of the window
+  const int64_t col = (int64_t)xcd_block(a) * CW + c;  // float4 column of the window
   const bool valid = col < a.nco * G4;
   const float id = R<OP>::id();
   float4 acc[NA];
@@ -2313,7 +2328,9 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
     const int64_t bytes = 4 * a.nbank * a.ni * (a.nco * F * a.nto * T + a.nco * a.nto);
     const int64_t o = opt(OPT_ST_PLAIN);
     a.st_plain = o == 2 ? 1 : o == 0 ? 0 : (bytes < ((int64_t)2 << 30) ? 1 : 0);
-    a.il_xcd = p.path == PATH_VEC_IL && T >= kIlXcdMinT && 4 * a.in_ld_t <= kIlXcdMaxPitch;
+    const bool row_xcd = p.path == PATH_VEC_ROW && a.tpb == 1 && 4 * a.in_ld_t >= kRowXcdMinPitch;
+    a.il_xcd = (p.path == PATH_VEC_IL || row_xcd) && T >= kIlXcdMinT &&
+               4 * a.in_ld_t <= kIlXcdMaxPitch;
   }
   a.div = (float)(F * T);
   return p;

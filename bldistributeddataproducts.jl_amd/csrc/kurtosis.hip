@@ -316,6 +316,10 @@ __global__ __launch_bounds__(kB) void k_kurt_mid(const KurtArgs k) {
 // 1.34 / 1.22 / 1.04x; nt >= 100 and one file no gain).  kMidNW waves per
 // workgroup otherwise (4 and 16 measured and lost).
 constexpr int kMidNW = 8;
+// k_kurt_mid2 in the per-XCD contiguous tile order of k_reduce_il: off
+// (round 5 A/B, profiles/r05/ab_kmidxcd_r05ah.json: the 0002 band 1.01-1.02,
+// one file 1.006, a window 4 channels in 0.87)
+constexpr bool kMidXcd = false;
 template <int NR, int NW>
 __global__ __launch_bounds__(64 * NW) void k_kurt_mid2(const KurtArgs k) {
   constexpr int TW = 128;  // channels per tile
@@ -324,7 +328,11 @@ __global__ __launch_bounds__(64 * NW) void k_kurt_mid2(const KurtArgs k) {
   // an exec-mask save/restore per spectrum
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t ctiles = (k.nc + TW - 1) / TW;
-  const int64_t b = blockIdx.x;
+  int64_t b = blockIdx.x;
+  if constexpr (kMidXcd) {  // workgroup b runs on XCD b % 8: give each XCD a contiguous run
+    const int64_t G = gridDim.x;
+    if ((G & 7) == 0) b = (b & 7) * (G >> 3) + (b >> 3);
+  }
   const int64_t ib = b / ctiles, c = (b % ctiles) * TW + 2 * lane;
   const bool valid = c < k.nc;  // (nc even: c + 1 < nc too)
   const int bank = (int)(ib / k.ni);

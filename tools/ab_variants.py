@@ -169,6 +169,9 @@ VARIANTS = {
     "rowto4": {"patch": [RS(rowt=36864)]},
     "ctl": {"patch": []},  # the base sources rebuilt: the harness's own spread
     # per-XCD segment order of k_reduce_il (round 5): off, or on everywhere
+    "kmidxcd": {"patch": [(KU, "constexpr bool kMidXcd = false;", "constexpr bool kMidXcd = true;")]},
+    "rowxcdoff": {"patch": [(K, "constexpr int64_t kRowXcdMinPitch = (int64_t)4 << 20;",
+                             "constexpr int64_t kRowXcdMinPitch = INT64_MAX;")]},
     "ilxcdoff": {"patch": [(K, "constexpr int kIlXcdMinT = 8;", "constexpr int kIlXcdMinT = 1 << 30;")]},
     "ilxcdall": {"patch": [(K, "constexpr int kIlXcdMinT = 8;", "constexpr int kIlXcdMinT = 1;"),
                            (K, "constexpr int64_t kIlXcdMaxPitch = (int64_t)128 << 20;",
@@ -478,6 +481,21 @@ def run(names, rounds, iters, suite="main"):
         w = [0, 65536, 1, 0, 1, 1, 0, 272, 1]
         for T in (2, 8, 16):
             band_case(f"0002 band F1024 T{T}", b2, 1024, T, w)
+        cases_done = True
+    elif suite == "rowxcd":  # round 5: the per-XCD order on the row kernels (T >= 8)
+        del b3
+        b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
+        w = [0, 65536, 1, 0, 1, 1, 0, 272, 1]
+        for F, T in ((64, 16), (16, 16), (256, 16), (4, 16), (64, 8), (64, 1)):
+            band_case(f"0002 band F{F} T{T}", b2, F, T, w)
+        band_case("cfg1 F64 T16", b2[:1], 64, 16, w)
+        del b2
+        b9 = [eng.synth(1 << 22, 1, 16, 1 << 20, seed=7 + b, kind=0) for b in range(8)]
+        band_case("16 MiB rows x 8 F64 T16", b9, 64, 16)
+        band_case("16 MiB rows x 8 F256 T16", b9, 256, 16)
+        del b9
+        b4 = [eng.synth(512, 1, 880000, 8, seed=10 * b + 1, kind=0) for b in range(8)]
+        band_case("0001 band F64 T16", b4, 64, 16, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
         cases_done = True
     elif suite == "occ":  # round 5: occupancy caps over the reduce kernels' main shapes
         band_case("cfg3 8 banks F1024 T16", b3, 1024, 16)
@@ -898,7 +916,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--suite", default="main", choices=["main", "il", "ilsmall", "ilxcd", "occ", "typed", "kregs", "narrow", "rows", "t1_0001", "wavet", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy", "wide", "grid0", "grid1", "t38", "lane3", "kgrid", "lanetpack", "kshort", "kfile"])
+    ap.add_argument("--suite", default="main", choices=["main", "il", "ilsmall", "ilxcd", "rowxcd", "occ", "typed", "kregs", "narrow", "rows", "t1_0001", "wavet", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy", "wide", "grid0", "grid1", "t38", "lane3", "kgrid", "lanetpack", "kshort", "kfile"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:
