@@ -167,11 +167,19 @@ __device__ __forceinline__ double kurt_ratio(int64_t nt, float S, double ma, dou
 // wave's 256 Float64 results go through LDS so every nt store instruction
 // writes 1 KiB contiguous (+2.5% on the 0000 band against each lane's 32 B as
 // two nt 16-byte stores).
+// k_kurt_regs in the per-XCD contiguous tile order of k_reduce_il: off
+// (round 5 A/B, profiles/r05/ab_kregsxcd_r05ai.json: the 0000 band 0.98-1.005,
+// one bank 0.97, inside the control's +-1.5% but one shape)
+constexpr bool kRegsXcd = false;
 template <int NTMAX, bool EXACT>
 __global__ __launch_bounds__(kB) void k_kurt_regs(const KurtArgs k) {
   const int64_t ncols = k.nc / 4;
   const int64_t ctiles = (ncols + kB - 1) / kB;
-  const int64_t b = blockIdx.x;
+  int64_t b = blockIdx.x;
+  if constexpr (kRegsXcd) {  // workgroup b runs on XCD b % 8: a contiguous run per XCD
+    const int64_t G = gridDim.x;
+    if ((G & 7) == 0) b = (b & 7) * (G >> 3) + (b >> 3);
+  }
   const int64_t ib = b / ctiles, col = (b % ctiles) * kB + threadIdx.x;
   if (col >= ncols) return;
   const int bank = (int)(ib / k.ni);
