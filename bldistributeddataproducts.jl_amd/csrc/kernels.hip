@@ -1043,9 +1043,17 @@ __device__ __forceinline__ void tile_tile(const RedArgs &a, int64_t tile) {
 
 // Grid-stride wrappers: one tile per workgroup when the grid covers every
 // tile, several when a launch has more tiles than INT32_MAX workgroups.
+// kVecXcd (A/B knob, round 5): the first tile of workgroup x in the per-XCD
+// contiguous order of k_reduce_il.
+constexpr bool kVecXcd = false;
 template <int OP, int LPG, int K4C>
 __global__ __launch_bounds__(kBlock) void k_reduce_vec(const RedArgs a) {
-  for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) vec_tile<OP, LPG, K4C>(a, t);
+  int64_t t0 = blockIdx.x;
+  if constexpr (kVecXcd) {
+    const int64_t G = gridDim.x;
+    if ((G & 7) == 0) t0 = (t0 & 7) * (G >> 3) + (t0 >> 3);
+  }
+  for (int64_t t = t0; t < a.ntiles; t += gridDim.x) vec_tile<OP, LPG, K4C>(a, t);
 }
 
 // Vector path, interleaved (PATH_VEC_IL): groups of F = 256*K4 channels
