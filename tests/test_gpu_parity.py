@@ -114,7 +114,10 @@ IL_SHAPES = [(4098, 1, 16, 1024, 16), (8194, 2, 8, 512, 4), (4097, 1, 8, 2048, 8
              # short time blocks, one per workgroup: T = 1 is the reference's
              # fqav, no integration
              (4098, 1, 16, 1024, 1), (4097, 2, 20, 512, 1), (4096, 1, 5, 2048, 1),
-             (4099, 1, 36, 1024, 4)]
+             (4099, 1, 36, 1024, 4),
+             # tiles >= 8 rows deep, grid x a multiple of 8: the per-XCD segment
+             # order (RedArgs::il_xcd)
+             (4096, 1, 32, 1024, 16), (4096, 2, 16, 512, 8), (2048, 1, 16, 2048, 8)]
 
 
 @pytest.mark.parametrize("shape", IL_SHAPES, ids=lambda s: "x".join(map(str, s)))
@@ -150,6 +153,20 @@ def test_reduce_row_integer_exact(eng, orc, shape):
     banks = [x] + [eng.synth(nco * F, ni, nt, 1024, seed=b, kind=1) for b in (1, 2)]
     got = host(eng, eng.band_reduce(banks, F, T))
     assert same_bits(got, orc.stitch([orc.reduce(host(eng, b), F, T) for b in banks]))
+
+
+@pytest.mark.parametrize("F,T", [(64, 16), (16, 8), (256, 16)])
+def test_reduce_row_xcd_order_integer_exact(eng, orc, F, T):
+    """Rows 4 MiB apart and tiles >= 8 rows deep: the row kernels take the
+    per-XCD segment order (RedArgs::il_xcd); a permutation of the tiles, so
+    bit-exact against the oracle like the default order."""
+    nc, nt = 1 << 20, 2 * T
+    x = eng.synth(nc, 1, nt, 1024, seed=F + T, kind=1)  # integers 0..255
+    a = host(eng, x)
+    assert eng.plan(x, F, T, "sum")["path"] == "row"
+    for op in ("sum", "max"):
+        got = host(eng, eng.reduce(x, F, T, op))
+        assert same_bits(got, orc.reduce(a, F, T, op)), (F, T, op)
 
 
 # Short time blocks (T in {1, 2, 4}; T = 1 is the reference's fqav with no
