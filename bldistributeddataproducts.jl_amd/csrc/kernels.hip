@@ -1043,9 +1043,10 @@ __device__ __forceinline__ void tile_tile(const RedArgs &a, int64_t tile) {
 
 // Grid-stride wrappers: one tile per workgroup when the grid covers every
 // tile, several when a launch has more tiles than INT32_MAX workgroups.
-// kVecXcd (A/B knob, round 5): the first tile of workgroup x in the per-XCD
-// contiguous order of k_reduce_il.
-constexpr bool kVecXcd = false;
+// kVecXcd: the first tile of workgroup x in the per-XCD contiguous order of
+// k_reduce_il (round 5 A/B, profiles/r05/ab_vecxcd_r05ak.json: the 0001 band
+// at F = 64 T = 16 0.963, cfg4 0.992, every other main shape within +-1%).
+constexpr bool kVecXcd = true;
 template <int OP, int LPG, int K4C>
 __global__ __launch_bounds__(kBlock) void k_reduce_vec(const RedArgs a) {
   int64_t t0 = blockIdx.x;

@@ -169,7 +169,7 @@ VARIANTS = {
     "rowto4": {"patch": [RS(rowt=36864)]},
     "ctl": {"patch": []},  # the base sources rebuilt: the harness's own spread
     # per-XCD segment order of k_reduce_il (round 5): off, or on everywhere
-    "vecxcd": {"patch": [(K, "constexpr bool kVecXcd = false;", "constexpr bool kVecXcd = true;")]},
+    "vecxcdoff": {"patch": [(K, "constexpr bool kVecXcd = true;", "constexpr bool kVecXcd = false;")]},
     "kregsxcd": {"patch": [(KU, "constexpr bool kRegsXcd = false;", "constexpr bool kRegsXcd = true;")]},
     "kmidxcd": {"patch": [(KU, "constexpr bool kMidXcd = false;", "constexpr bool kMidXcd = true;")]},
     "rowxcdoff": {"patch": [(K, "constexpr int64_t kRowXcdMinPitch = (int64_t)4 << 20;",
