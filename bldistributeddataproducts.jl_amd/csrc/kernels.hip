@@ -165,6 +165,10 @@ constexpr unsigned kRowShm = 0, kRowtShm = 0, kVecShm = 0;
 // (round 5, profiles/r05/ab_narrow_r05q.json; 14 waves per CU, half the
 // cycles parked on loads: cfg3f1_sq_summary_r05p.json).
 constexpr unsigned kNarrowShm = 0;
+// k_reduce_narrow in the per-XCD tile order (round 5 A/B,
+// profiles/r05/ab_narrowxcd_r05am.json: the 0000 band at F = 1, 2 0.975-0.987,
+// one bank 0.979, the 0002 band at F = 1 T = 16 0.93, F = 2 T = 8 0.98)
+constexpr bool kNarrowXcd = true;
 // Interleaved launches whose tiles are at least kIlXcdMinT rows deep and whose
 // rows are at most kIlXcdMaxPitch bytes apart give each XCD a contiguous run
 // of segments (RedArgs::il_xcd).  Round 5 A/B, one box, against the
@@ -1543,7 +1547,12 @@ __global__ __launch_bounds__(BP ? 1024 : kBlock) void k_reduce_wavet(const RedAr
 
 template <int OP, int F>
 __global__ __launch_bounds__(kBlock) void k_reduce_narrow(const RedArgs a) {
-  for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) narrow_tile<OP, F>(a, t);
+  int64_t t0 = blockIdx.x;
+  if constexpr (kNarrowXcd) {  // the per-XCD contiguous order of k_reduce_il
+    const int64_t G = gridDim.x;
+    if ((G & 7) == 0) t0 = (t0 & 7) * (G >> 3) + (t0 >> 3);
+  }
+  for (int64_t t = t0; t < a.ntiles; t += gridDim.x) narrow_tile<OP, F>(a, t);
 }
 template <int OP, int F>
 __global__ __launch_bounds__(kBlock) void k_reduce_narrow_mis(const RedArgs a) {

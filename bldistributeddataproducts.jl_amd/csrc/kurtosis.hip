@@ -436,6 +436,9 @@ __global__ __launch_bounds__(64 * NW) void k_kurt_mid2(const KurtArgs k) {
 // products (0001: 512 channels, nt = 513..8192 had 32-128 waves on the chip);
 // 0 = never.  Each channel's arithmetic is unchanged.
 constexpr int kLeafB = 4, kLeafW = 4, kLeafNB = 16;
+// k_kurt_leaf in the per-XCD workgroup order: off (round 5 A/B,
+// profiles/r05/ab_kleafxcd_r05am.json: cfg4 1.006, 2048 spectra 0.987)
+constexpr bool kLeafXcd = false;
 
 template <int W>
 __device__ __forceinline__ void ldw(const float *p, float (&x)[W]) {
@@ -510,7 +513,12 @@ __device__ __forceinline__ void leaf_store(const KurtArgs &k, const LeafAcc<W> &
 template <int W, int B>
 __global__ __launch_bounds__(kB) void k_kurt_leaf(const KurtArgs k) {
   const int lane = threadIdx.x & 63;
-  const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  int64_t bx = blockIdx.x;
+  if constexpr (kLeafXcd) {  // the per-XCD contiguous order of k_reduce_il
+    const int64_t G = gridDim.x;
+    if ((G & 7) == 0) bx = (bx & 7) * (G >> 3) + (bx >> 3);
+  }
+  const int64_t u = bx * 4 + (threadIdx.x >> 6);
   const int64_t seg = u % k.nseg, r = u / k.nseg;
   const int64_t slot = r % k.nslot, row = r / k.nslot;
   const int64_t col = seg * 64 + lane;

@@ -169,6 +169,8 @@ VARIANTS = {
     "rowto4": {"patch": [RS(rowt=36864)]},
     "ctl": {"patch": []},  # the base sources rebuilt: the harness's own spread
     # per-XCD segment order of k_reduce_il (round 5): off, or on everywhere
+    "narrowxcdoff": {"patch": [(K, "constexpr bool kNarrowXcd = true;", "constexpr bool kNarrowXcd = false;")]},
+    "kleafxcd": {"patch": [(KU, "constexpr bool kLeafXcd = false;", "constexpr bool kLeafXcd = true;")]},
     "vecxcdoff": {"patch": [(K, "constexpr bool kVecXcd = true;", "constexpr bool kVecXcd = false;")]},
     "kregsxcd": {"patch": [(KU, "constexpr bool kRegsXcd = false;", "constexpr bool kRegsXcd = true;")]},
     "kmidxcd": {"patch": [(KU, "constexpr bool kMidXcd = false;", "constexpr bool kMidXcd = true;")]},
