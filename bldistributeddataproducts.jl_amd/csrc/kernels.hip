@@ -165,6 +165,8 @@ constexpr unsigned kRowShm = 0, kRowtShm = 0, kVecShm = 0;
 // (round 5, profiles/r05/ab_narrow_r05q.json; 14 waves per CU, half the
 // cycles parked on loads: cfg3f1_sq_summary_r05p.json).
 constexpr unsigned kNarrowShm = 0;
+// k_reduce_rowt in the per-XCD order (A/B knob, round 5)
+constexpr bool kRowtXcd = false;
 // k_reduce_narrow in the per-XCD tile order (round 5 A/B,
 // profiles/r05/ab_narrowxcd_r05am.json: the 0000 band at F = 1, 2 0.975-0.987,
 // one bank 0.979, the 0002 band at F = 1 T = 16 0.93, F = 2 T = 8 0.98)
@@ -1351,7 +1353,12 @@ void k_reduce_rowt(const RedArgs a) {
   // With a.bpack the 2^tsub_log2 lane sets take 2^tsub_log2 consecutive banks
   // of one time group instead (grid z = bank sets): a stitched product's rows
   // then get whole segments of 2^tsub_log2 banks' outputs (below).
-  const uint32_t bx = blockIdx.x, bc = (uint32_t)a.blocks_c;
+  uint32_t bx = blockIdx.x;
+  const uint32_t bc = (uint32_t)a.blocks_c;
+  if constexpr (kRowtXcd) {  // the per-XCD contiguous order of k_reduce_il
+    const uint32_t X = gridDim.x;
+    if ((X & 7) == 0) bx = (bx & 7) * (X >> 3) + (bx >> 3);
+  }
   const int sh = a.tsub_log2, cw = kBlock >> sh, sub = threadIdx.x >> (8 - sh);  // (kBlock = 256)
   constexpr bool bp = BP;  // (a.bpack: a template form, so the time-group form pays nothing)
   const uint32_t tq = bx / bc, i = blockIdx.y;

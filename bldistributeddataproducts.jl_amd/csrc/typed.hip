@@ -359,13 +359,20 @@ __global__ __launch_bounds__(256) void k_reduce_typed_vec(const TypedArgs a, int
 // row): the rows of the workgroup's tpb blocks (tpb * T <= 16) are loaded in
 // one batch, then folded into blocks, so a lane waits for memory once per
 // workgroup instead of once per block.
+// k_reduce_typed_vec16 in the per-XCD workgroup order (A/B knob, round 5)
+constexpr bool kTypedXcd = false;
 template <typename TI, int OP, int NR>
 __global__ __launch_bounds__(256) void k_reduce_typed_vec16(const TypedArgs a, int lpg, int tpb,
                                                             int64_t nct) {
   typedef Vec16<TI, OP> V;
   typedef typename V::R R;
   const int tid = threadIdx.x;
-  const int64_t bx = blockIdx.x, ct = bx % nct, tg = bx / nct;
+  int64_t bx = blockIdx.x;
+  if constexpr (kTypedXcd) {  // the per-XCD contiguous order of k_reduce_il
+    const int64_t X = gridDim.x;
+    if ((X & 7) == 0) bx = (bx & 7) * (X >> 3) + (bx >> 3);
+  }
+  const int64_t ct = bx % nct, tg = bx / nct;
   const int64_t co = ct * (256 / lpg) + tid / lpg;
   const int j = tid % lpg;
   const int64_t i = blockIdx.y;
