@@ -165,8 +165,13 @@ constexpr unsigned kRowShm = 0, kRowtShm = 0, kVecShm = 0;
 // (round 5, profiles/r05/ab_narrow_r05q.json; 14 waves per CU, half the
 // cycles parked on loads: cfg3f1_sq_summary_r05p.json).
 constexpr unsigned kNarrowShm = 0;
-// k_reduce_rowt in the per-XCD order (A/B knob, round 5)
-constexpr bool kRowtXcd = false;
+// k_reduce_rowt in the per-XCD order for launches of at least kRowtXcdBytes
+// whose rows are at least kRowXcdMinPitch apart (round 5 A/B on two boxes,
+// profiles/r05/ab_rowtxcd_r05an.json, ab_rowtxcd_gate_r05ao.json: the 0000
+// band at T = 1, 2 0.95-0.97; the 0001 band (2 KiB rows) mixed, F = 8 T = 1
+// 0.94-0.96 but F = 64 T = 1 1.01-1.05; one 0002 file 1.07-1.13, the 0002
+// band 0.95-1.02)
+constexpr int64_t kRowtXcdBytes = (int64_t)1 << 30;
 // k_reduce_narrow in the per-XCD tile order (round 5 A/B,
 // profiles/r05/ab_narrowxcd_r05am.json: the 0000 band at F = 1, 2 0.975-0.987,
 // one bank 0.979, the 0002 band at F = 1 T = 16 0.93, F = 2 T = 8 0.98)
@@ -1355,7 +1360,7 @@ void k_reduce_rowt(const RedArgs a) {
   // then get whole segments of 2^tsub_log2 banks' outputs (below).
   uint32_t bx = blockIdx.x;
   const uint32_t bc = (uint32_t)a.blocks_c;
-  if constexpr (kRowtXcd) {  // the per-XCD contiguous order of k_reduce_il
+  if (a.il_xcd) {  // the per-XCD contiguous order of k_reduce_il (launches >= kRowtXcdBytes)
     const uint32_t X = gridDim.x;
     if ((X & 7) == 0) bx = (bx & 7) * (X >> 3) + (bx >> 3);
   }
@@ -2354,8 +2359,10 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
     const int64_t o = opt(OPT_ST_PLAIN);
     a.st_plain = o == 2 ? 1 : o == 0 ? 0 : (bytes < ((int64_t)2 << 30) ? 1 : 0);
     const bool row_xcd = p.path == PATH_VEC_ROW && a.tpb == 1 && 4 * a.in_ld_t >= kRowXcdMinPitch;
-    a.il_xcd = (p.path == PATH_VEC_IL || row_xcd) && T >= kIlXcdMinT &&
-               4 * a.in_ld_t <= kIlXcdMaxPitch;
+    a.il_xcd = ((p.path == PATH_VEC_IL || row_xcd) && T >= kIlXcdMinT &&
+                4 * a.in_ld_t <= kIlXcdMaxPitch) ||
+               (p.path == PATH_VEC_ROW && a.tpb > 1 && bytes >= kRowtXcdBytes &&
+                4 * a.in_ld_t >= kRowXcdMinPitch);
   }
   a.div = (float)(F * T);
   return p;

@@ -359,7 +359,8 @@ __global__ __launch_bounds__(256) void k_reduce_typed_vec(const TypedArgs a, int
 // row): the rows of the workgroup's tpb blocks (tpb * T <= 16) are loaded in
 // one batch, then folded into blocks, so a lane waits for memory once per
 // workgroup instead of once per block.
-// k_reduce_typed_vec16 in the per-XCD workgroup order (A/B knob, round 5)
+// k_reduce_typed_vec16 in the per-XCD workgroup order: off (round 5 A/B,
+// profiles/r05/ab_typedxcd_r05an.json: 1.02-1.08 on every typed shape)
 constexpr bool kTypedXcd = false;
 template <typename TI, int OP, int NR>
 __global__ __launch_bounds__(256) void k_reduce_typed_vec16(const TypedArgs a, int lpg, int tpb,

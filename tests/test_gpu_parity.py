@@ -169,6 +169,17 @@ def test_reduce_row_xcd_order_integer_exact(eng, orc, F, T):
         assert same_bits(got, orc.reduce(a, F, T, op)), (F, T, op)
 
 
+@pytest.mark.parametrize("F,T", [(64, 1), (16, 2)])
+def test_reduce_rowt_xcd_order_integer_exact(eng, orc, F, T):
+    """A short-time-block launch of >= 1 GiB: k_reduce_rowt in the per-XCD
+    segment order (RedArgs::il_xcd); bit-exact against the oracle."""
+    nc, nt = 1 << 20, 256
+    x = eng.synth(nc, 1, nt, 1024, seed=F + T, kind=1)  # integers 0..255, 1 GiB
+    assert eng.plan(x, F, T, "sum")["path"] == "row"
+    got = host(eng, eng.reduce(x, F, T, "sum"))
+    assert same_bits(got, orc.reduce(host(eng, x), F, T, "sum")), (F, T)
+
+
 # Short time blocks (T in {1, 2, 4}; T = 1 is the reference's fqav with no
 # time integration): k_reduce_rowt takes 16 / T time blocks per workgroup,
 # the last group partial, and windows of <= 128 float4 columns (the 512-channel

@@ -169,7 +169,8 @@ VARIANTS = {
     "rowto4": {"patch": [RS(rowt=36864)]},
     "ctl": {"patch": []},  # the base sources rebuilt: the harness's own spread
     # per-XCD segment order of k_reduce_il (round 5): off, or on everywhere
-    "rowtxcd": {"patch": [(K, "constexpr bool kRowtXcd = false;", "constexpr bool kRowtXcd = true;")]},
+    "rowtxcdoff": {"patch": [(K, "constexpr int64_t kRowtXcdBytes = (int64_t)1 << 30;",
+                              "constexpr int64_t kRowtXcdBytes = INT64_MAX;")]},
     "typedxcd": {"patch": [("typed.hip", "constexpr bool kTypedXcd = false;", "constexpr bool kTypedXcd = true;")]},
     "narrowxcdoff": {"patch": [(K, "constexpr bool kNarrowXcd = true;", "constexpr bool kNarrowXcd = false;")]},
     "kleafxcd": {"patch": [(KU, "constexpr bool kLeafXcd = false;", "constexpr bool kLeafXcd = true;")]},
