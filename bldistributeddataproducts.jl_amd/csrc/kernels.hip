@@ -165,6 +165,13 @@ constexpr unsigned kRowShm = 0, kRowtShm = 0, kVecShm = 0;
 // (round 5, profiles/r05/ab_narrow_r05q.json; 14 waves per CU, half the
 // cycles parked on loads: cfg3f1_sq_summary_r05p.json).
 constexpr unsigned kNarrowShm = 0;
+// k_reduce_tile in the per-XCD order: off (round 5 A/B,
+// profiles/r05/ab_tilexcd_r05ar.json: 0.94-1.035 by shape).  k_reduce_narrowt
+// at F = 2 in that order (ab_narrowtxcd_r05ar.json, ab_narrowtxcd_r05as.json:
+// the 0000 band at T = 1 / 2 / 4 0.93 / 0.96 / 0.94, the 0001 band T = 1 0.92,
+// the 0002 shapes within +-1.4%; F = 1 mixed, 1.05 on the 0000 band at T = 2,
+// so F = 1 keeps the dispatcher's order).
+constexpr bool kTileXcd = false, kNarrowtXcd = true;
 // k_reduce_rowt in the per-XCD order for launches of at least kRowtXcdBytes
 // whose rows are at least kRowXcdMinPitch apart (round 5 A/B on two boxes,
 // profiles/r05/ab_rowtxcd_r05an.json, ab_rowtxcd_gate_r05ao.json: the 0000
@@ -470,7 +477,12 @@ template <int OP, int F, int T, int NRW>
 __global__ __launch_bounds__(kBlock) void k_reduce_narrowt(const RedArgs a) {
   constexpr int TPB = NRW / T, NR = TPB * T;
   const int tid = threadIdx.x;
-  const uint32_t bx = blockIdx.x, bc = (uint32_t)a.blocks_c;
+  uint32_t bx = blockIdx.x;
+  const uint32_t bc = (uint32_t)a.blocks_c;
+  if constexpr (kNarrowtXcd && F == 2) {  // the per-XCD contiguous order of k_reduce_il
+    const uint32_t X = gridDim.x;
+    if ((X & 7) == 0) bx = (bx & 7) * (X >> 3) + (bx >> 3);
+  }
   const int sh = a.tsub_log2, cw = kBlock >> sh;
   const uint32_t tq = bx / bc, i = blockIdx.y;
   const int64_t tg = ((int64_t)tq << sh) + (tid >> (8 - sh));
@@ -1585,7 +1597,12 @@ template <int OP, bool CS1>
 __global__ __launch_bounds__(kBlock)
 __attribute__((amdgpu_waves_per_eu(1, kTileMaxWaves)))
 void k_reduce_tile(const RedArgs a) {
-  for (int64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) tile_tile<OP, CS1>(a, t);
+  int64_t t0 = blockIdx.x;
+  if constexpr (kTileXcd) {  // the per-XCD contiguous order of k_reduce_il
+    const int64_t G = gridDim.x;
+    if ((G & 7) == 0) t0 = (t0 & 7) * (G >> 3) + (t0 >> 3);
+  }
+  for (int64_t t = t0; t < a.ntiles; t += gridDim.x) tile_tile<OP, CS1>(a, t);
 }
 
 // Second stage of a time-chunked reduction: fold the nchunk partials of every

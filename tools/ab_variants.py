@@ -169,6 +169,8 @@ VARIANTS = {
     "rowto4": {"patch": [RS(rowt=36864)]},
     "ctl": {"patch": []},  # the base sources rebuilt: the harness's own spread
     # per-XCD segment order of k_reduce_il (round 5): off, or on everywhere
+    "tilexcd": {"patch": [(K, "constexpr bool kTileXcd = false,", "constexpr bool kTileXcd = true,")]},
+    "narrowtxcdoff": {"patch": [(K, "kNarrowtXcd = true;", "kNarrowtXcd = false;")]},
     "rowtxcdoff": {"patch": [(K, "constexpr int64_t kRowtXcdBytes = (int64_t)1 << 30;",
                               "constexpr int64_t kRowtXcdBytes = INT64_MAX;")]},
     "typedxcd": {"patch": [("typed.hip", "constexpr bool kTypedXcd = false;", "constexpr bool kTypedXcd = true;")]},
@@ -503,6 +505,22 @@ def run(names, rounds, iters, suite="main"):
         del b9
         b4 = [eng.synth(512, 1, 880000, 8, seed=10 * b + 1, kind=0) for b in range(8)]
         band_case("0001 band F64 T16", b4, 64, 16, [0, 512, 1, 0, 1, 1, 0, 879616, 1])
+        cases_done = True
+    elif suite == "narrowt":  # round 5: k_reduce_narrowt (F = 1, 2 with T = 1, 2, 4)
+        for F, T in ((2, 1), (2, 2), (1, 2), (1, 4), (2, 4)):
+            band_case(f"0000 band F{F} T{T}", b3, F, T)
+        band_case("0000 1 bank F2 T1", b3[:1], 2, 1)
+        del b3
+        b2 = [eng.synth(65536, 1, 279, 1024, seed=10 * b + 2, kind=0) for b in range(8)]
+        w = [0, 65536, 1, 0, 1, 1, 0, 272, 1]
+        for F, T in ((2, 1), (1, 2), (2, 4)):
+            band_case(f"0002 band F{F} T{T}", b2, F, T, w)
+        band_case("0002 file F2 T1", b2[:1], 2, 1, w)
+        del b2
+        b4 = [eng.synth(512, 1, 880000, 8, seed=10 * b + 1, kind=0) for b in range(8)]
+        w4 = [0, 512, 1, 0, 1, 1, 0, 879616, 1]
+        band_case("0001 band F2 T1", b4, 2, 1, w4)
+        band_case("0001 band F1 T2", b4, 1, 2, w4)
         cases_done = True
     elif suite == "occ":  # round 5: occupancy caps over the reduce kernels' main shapes
         band_case("cfg3 8 banks F1024 T16", b3, 1024, 16)
@@ -923,7 +941,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--suite", default="main", choices=["main", "il", "ilsmall", "ilxcd", "rowxcd", "occ", "typed", "kregs", "narrow", "rows", "t1_0001", "wavet", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy", "wide", "grid0", "grid1", "t38", "lane3", "kgrid", "lanetpack", "kshort", "kfile"])
+    ap.add_argument("--suite", default="main", choices=["main", "il", "ilsmall", "ilxcd", "rowxcd", "narrowt", "occ", "typed", "kregs", "narrow", "rows", "t1_0001", "wavet", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy", "wide", "grid0", "grid1", "t38", "lane3", "kgrid", "lanetpack", "kshort", "kfile"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:
