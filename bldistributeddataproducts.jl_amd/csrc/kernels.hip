@@ -170,7 +170,9 @@ constexpr unsigned kNarrowShm = 0;
 // at F = 2 in that order (ab_narrowtxcd_r05ar.json, ab_narrowtxcd_r05as.json:
 // the 0000 band at T = 1 / 2 / 4 0.93 / 0.96 / 0.94, the 0001 band T = 1 0.92,
 // the 0002 shapes within +-1.4%; F = 1 mixed, 1.05 on the 0000 band at T = 2,
-// so F = 1 keeps the dispatcher's order).
+// so F = 1 keeps the dispatcher's order; on a second box the 0002 band at
+// F = 2 T = 1 lost 4%, so launches under kRowtXcdBytes keep it too:
+// ab_narrowtxcd_confirm_r05at.json).
 constexpr bool kTileXcd = false, kNarrowtXcd = true;
 // k_reduce_rowt in the per-XCD order for launches of at least kRowtXcdBytes
 // whose rows are at least kRowXcdMinPitch apart (round 5 A/B on two boxes,
@@ -479,7 +481,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce_narrowt(const RedArgs a) {
   const int tid = threadIdx.x;
   uint32_t bx = blockIdx.x;
   const uint32_t bc = (uint32_t)a.blocks_c;
-  if constexpr (kNarrowtXcd && F == 2) {  // the per-XCD contiguous order of k_reduce_il
+  if (F == 2 && a.il_xcd) {  // the per-XCD contiguous order of k_reduce_il (>= 1 GiB launches)
     const uint32_t X = gridDim.x;
     if ((X & 7) == 0) bx = (bx & 7) * (X >> 3) + (bx >> 3);
   }
@@ -2379,7 +2381,9 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
     a.il_xcd = ((p.path == PATH_VEC_IL || row_xcd) && T >= kIlXcdMinT &&
                 4 * a.in_ld_t <= kIlXcdMaxPitch) ||
                (p.path == PATH_VEC_ROW && a.tpb > 1 && bytes >= kRowtXcdBytes &&
-                4 * a.in_ld_t >= kRowXcdMinPitch);
+                4 * a.in_ld_t >= kRowXcdMinPitch) ||
+               (kNarrowtXcd && p.path == PATH_NARROW && a.tpb > 1 && F == 2 &&
+                bytes >= kRowtXcdBytes);
   }
   a.div = (float)(F * T);
   return p;

@@ -169,6 +169,18 @@ def test_reduce_row_xcd_order_integer_exact(eng, orc, F, T):
         assert same_bits(got, orc.reduce(a, F, T, op)), (F, T, op)
 
 
+@pytest.mark.parametrize("T", [1, 2, 4])
+def test_reduce_narrowt_xcd_order_integer_exact(eng, orc, T):
+    """F = 2 with short time blocks on a >= 1 GiB launch: k_reduce_narrowt in
+    the per-XCD segment order (RedArgs::il_xcd); bit-exact against the
+    oracle."""
+    nc, nt = 1 << 20, 256
+    x = eng.synth(nc, 1, nt, 1024, seed=T, kind=1)  # integers 0..255, 1 GiB
+    assert eng.plan(x, 2, T, "sum")["path"] == "narrow"
+    got = host(eng, eng.reduce(x, 2, T, "sum"))
+    assert same_bits(got, orc.reduce(host(eng, x), 2, T, "sum")), T
+
+
 @pytest.mark.parametrize("F,T", [(64, 1), (16, 2)])
 def test_reduce_rowt_xcd_order_integer_exact(eng, orc, F, T):
     """A short-time-block launch of >= 1 GiB: k_reduce_rowt in the per-XCD
