@@ -174,6 +174,9 @@ constexpr unsigned kNarrowShm = 0;
 // F = 2 T = 1 lost 4%, so launches under kRowtXcdBytes keep it too:
 // ab_narrowtxcd_confirm_r05at.json).
 constexpr bool kTileXcd = false, kNarrowtXcd = true;
+// k_reduce_wavet in the per-XCD order: off (round 5 A/B,
+// profiles/r05/ab_wavetxcd_r05aw.json: the 0001 band at F = 512 1.03-1.045)
+constexpr bool kWavetXcd = false;
 // k_reduce_rowt in the per-XCD order for launches of at least kRowtXcdBytes
 // whose rows are at least kRowXcdMinPitch apart (round 5 A/B on two boxes,
 // profiles/r05/ab_rowtxcd_r05an.json, ab_rowtxcd_gate_r05ao.json: the 0000
@@ -1506,7 +1509,11 @@ __global__ __launch_bounds__(BP ? 1024 : kBlock) void k_reduce_wavet(const RedAr
   // K4 >= 8 always the latter
   constexpr int RB = (K4 == 2 || K4 == 4) ? (K4 >= kBatch ? 1 : kBatch / K4) : 0;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t bx = blockIdx.x;
+  int64_t bx = blockIdx.x;
+  if constexpr (kWavetXcd) {  // the per-XCD contiguous order of k_reduce_il
+    const int64_t X = gridDim.x;
+    if ((X & 7) == 0) bx = (bx & 7) * (X >> 3) + (bx >> 3);
+  }
   const int64_t g = BP ? wave % a.nco : bx % a.nco, chunk = BP ? bx : bx / a.nco;
   const int64_t i = blockIdx.y;
   const int bank = BP ? (int)(wave / a.nco) : (int)blockIdx.z;

@@ -170,6 +170,7 @@ VARIANTS = {
     "ctl": {"patch": []},  # the base sources rebuilt: the harness's own spread
     # per-XCD segment order of k_reduce_il (round 5): off, or on everywhere
     "tilexcd": {"patch": [(K, "constexpr bool kTileXcd = false,", "constexpr bool kTileXcd = true,")]},
+    "wavetxcd": {"patch": [(K, "constexpr bool kWavetXcd = false;", "constexpr bool kWavetXcd = true;")]},
     "narrowtxcdoff": {"patch": [(K, "kNarrowtXcd = true;", "kNarrowtXcd = false;")]},
     "rowtxcdoff": {"patch": [(K, "constexpr int64_t kRowtXcdBytes = (int64_t)1 << 30;",
                               "constexpr int64_t kRowtXcdBytes = INT64_MAX;")]},
