@@ -537,7 +537,7 @@ def free_port() -> int:
         return so.getsockname()[1]
 
 
-def spawn_ranks(n: int) -> int:
+def spawn_ranks(n: int, deadline_s: float) -> int:
     """`python bench.py --gpus N` without a launcher: start N rank processes of
     this same command (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, one GPU
     each) and wait for them.  Runs before anything imports torch or touches
@@ -546,7 +546,10 @@ def spawn_ranks(n: int) -> int:
     rank's.  The ranks are polled, not waited on in order: when one exits
     non-zero (e.g. before the rendezvous or the RCCL communicator, where its
     peers would block until the process-group timeout) the others are sent
-    SIGTERM, then SIGKILL after a grace period, and its status is returned."""
+    SIGTERM, then SIGKILL after a grace period, and its status is returned.
+    Ranks still running ``deadline_s`` after the start (a rank hung in a
+    collective, which no exit status would ever report) are stopped the same
+    way and the status is 124, as timeout(1) reports."""
     import signal
     import subprocess
 
@@ -558,24 +561,30 @@ def spawn_ranks(n: int) -> int:
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
                                       env=env))
     failed = 0
+    t_end = time.monotonic() + deadline_s
     try:
         while True:
             rcs = [p.poll() for p in procs]
             failed = next((rc for rc in rcs if rc), 0)
             if failed or all(rc is not None for rc in rcs):
                 break
+            if time.monotonic() > t_end:
+                hung = [r for r, rc in enumerate(rcs) if rc is None]
+                log(f"rank(s) {hung} still running after the {deadline_s:.0f} s deadline")
+                failed = 124
+                break
             time.sleep(0.05)
     except KeyboardInterrupt:
         failed = 128 + signal.SIGINT
     if failed:
-        log(f"a rank exited with status {failed}: stopping the others")
+        log(f"stopping the ranks (status {failed})")
         for p in procs:
             if p.poll() is None:
                 p.terminate()
-        deadline = time.time() + 10.0
+        grace = time.monotonic() + 10.0
         for p in procs:
             try:
-                p.wait(timeout=max(0.1, deadline - time.time()))
+                p.wait(timeout=max(0.1, grace - time.monotonic()))
             except subprocess.TimeoutExpired:
                 p.kill()
                 p.wait()
@@ -675,6 +684,56 @@ def bench_typed(args, eng, torch, pkg):
                                   "frac": round(f["warm_GBps_in_plus_out"] / HBM_PEAK_GBS, 4)}}}
 
 
+def verify_band(cfg, eng, torch, dist, banks, mine, nb, run_step, rank, world, use_pg):
+    """The timed path checked on its own result, after the timed region: this
+    rank's banks are regenerated in place as integer data (bldp_synth_f32
+    kind 1, values 0..255, so every Float32 sum of F*T <= 65536 of them is
+    exact in any order), ``run_step()`` runs one step exactly as timed
+    (prepared reduce into the rank's slice; N > 1: the exchange to the root and
+    its stitch) and returns the root's stitched band.  Every rank computes, from
+    its own inputs, each bank's window total and a few spot groups (Float64,
+    exact); the root gathers them and compares every bank's vcat slot of the
+    product bit for bit (src/gbt.jl:75-78,103: reduce(vcat, fetch.(futures))).
+    Returns (ok, detail) on the root, (None, None) elsewhere."""
+    F, T = cfg["F"], cfg["T"]
+    nco, ni, nto = cfg["nchan"] // F, cfg["nif"], cfg["tw"] // T
+    for b, v in zip(mine, banks):
+        eng.synth(cfg["nchan"], cfg["nif"], cfg["ntime"], cfg["nfpc"],
+                  seed=7919 + 10 * b + cfg["product"], kind=1, out=v)
+    spots = [(0, 0, 0), (nco // 2, ni - 1, nto // 2), (nco - 1, ni - 1, nto - 1)]
+    expect = []
+    for b, v in zip(mine, banks):
+        row = [v[:, :, :nto * T].sum(dtype=torch.float64)]
+        for k, i, t in spots:
+            row.append(v[k * F:(k + 1) * F, i, t * T:(t + 1) * T].sum(dtype=torch.float64))
+        expect.append(torch.stack(row))
+    expect = torch.stack(expect)  # (banks of this rank, 1 + spots)
+    torch.cuda.synchronize()
+    product = run_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        nccl = dist.get_backend() == "nccl"
+        mine_t = expect if nccl else expect.cpu()
+        allx = [torch.empty_like(mine_t) for _ in range(world)] if rank == 0 else None
+        dist.gather(mine_t, allx, dst=0)
+        if rank != 0:
+            return None, None
+        expect = torch.cat([x.to(product.device) for x in allx])
+    if tuple(product.shape) != (nb * nco, ni, nto):
+        return False, f"product shape {tuple(product.shape)} != {(nb * nco, ni, nto)}"
+    bad = []
+    for b in range(nb):
+        slot = product[b * nco:(b + 1) * nco]
+        got = [slot.sum(dtype=torch.float64)] + [slot[k, i, t].double() for k, i, t in spots]
+        got = torch.stack(got).cpu()
+        want = expect[b].cpu()
+        if not torch.equal(got, want):
+            bad.append({"bank": b, "got": got.tolist(), "want": want.tolist()})
+    detail = (f"integer data (bldp_synth_f32 kind 1), one step of the timed path; {nb} banks' "
+              f"vcat slots: window total + {len(spots)} spot groups each, bit-exact")
+    return not bad, (detail if not bad else {"mismatch": bad[:4], "check": detail})
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -710,10 +769,15 @@ def main():
                          "beside the cold ones")
     ap.add_argument("--plan-option", action="append", default=[], metavar="NAME=VALUE",
                     help="override a planner choice (bldp_plan_option; A/B runs only)")
+    ap.add_argument("--rank-deadline", type=float, default=900.0,
+                    help="N>1 without a launcher: seconds after which ranks still running "
+                         "(e.g. hung in a collective) are stopped and bench.py exits 124")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="skip the integer-data check of one step after the timed region")
     args = ap.parse_args()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # no launcher: this process only starts the N ranks (no torch, no HIP here)
-        sys.exit(spawn_ranks(args.gpus))
+        sys.exit(spawn_ranks(args.gpus, args.rank_deadline))
 
     import torch
     import torch.distributed as dist
@@ -730,6 +794,12 @@ def main():
         if os.environ.get("BENCH_RENDEZVOUS_FAIL_RANK") == str(rank):
             log(f"rank {rank}: injected failure before the rendezvous")
             sys.exit(3)
+        # BENCH_RENDEZVOUS_HANG_RANK=r: rank r never reaches the rendezvous (a
+        # rank hung in a collective; the deadline test of spawn_ranks)
+        if os.environ.get("BENCH_RENDEZVOUS_HANG_RANK") == str(rank):
+            log(f"rank {rank}: injected hang before the rendezvous")
+            while True:
+                time.sleep(60)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", str(free_port()))
         os.environ.setdefault("RANK", "0")
@@ -929,6 +999,15 @@ def main():
                          device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el, kern_ms, span_ms, warm_ms = float(t[0]), float(t[1]), float(t[2]), float(t[3])
+    verified, verify_detail = None, None
+    if not args.no_verify:
+        def one_step():
+            res = step(copy=0)
+            if pipe:
+                pipe.drain()
+            return res
+        verified, verify_detail = verify_band(cfg, eng, torch, dist, banks, mine, nb, one_step,
+                                              rank, world, use_pg)
     ms_step = el * 1e3 / args.steps
     path = eng.plan(banks[0], cfg["F"], cfg["T"], "sum", win)["path"] if banks else None
     kernel_name = {"interleaved": "k_reduce_il", "vector": "k_reduce_vec",
@@ -1005,6 +1084,8 @@ def main():
                                      "Infinity Cache by the launch before"}},
             "host_enqueue_ms_per_step": round(host_ms, 4),
             "settle_launches": settle,
+            "verified": verified,
+            "verify": verify_detail,
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)
@@ -1013,6 +1094,9 @@ def main():
         if native_x:
             pipe.close()
         dist.destroy_process_group()
+    if verified is False:
+        log(f"VERIFY FAILED: {verify_detail}")
+        sys.exit(5)
     return result
 
 

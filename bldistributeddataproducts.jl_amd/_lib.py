@@ -23,6 +23,7 @@ BLDP_OK, BLDP_EINVAL, BLDP_EDIM, BLDP_EHIP, BLDP_ENOMEM, BLDP_EBOUNDS = 0, -1, -
 BLDP_ECOMM, BLDP_EIO = -7, -8
 ABI_VERSION = 4
 BLDP_BAND_STAGED = 1
+BLDP_BAND_PEER_STORE = 2
 BLDP_COMM_ID_BYTES = 128
 
 

@@ -544,7 +544,10 @@ int bldp_band_reduce_multi_f32(int nbank, const int *bank_dev, const float *cons
                                unsigned flags) {
   if (nbank < 1 || nbank > BLDP_MAX_BANKS || !bank_dev || !in)
     return fail(BLDP_EINVAL, "bad bank arguments");
-  if (flags & ~BLDP_BAND_STAGED) return fail(BLDP_EINVAL, "unknown flags 0x%x", flags);
+  if (flags & ~(BLDP_BAND_STAGED | BLDP_BAND_PEER_STORE))
+    return fail(BLDP_EINVAL, "unknown flags 0x%x", flags);
+  if ((flags & BLDP_BAND_STAGED) && (flags & BLDP_BAND_PEER_STORE))
+    return fail(BLDP_EINVAL, "BLDP_BAND_STAGED and BLDP_BAND_PEER_STORE exclude each other");
   int ndev = 0;
   HIPCHK(hipGetDeviceCount(&ndev));
   if (root < 0 || root >= ndev) return fail(BLDP_EINVAL, "root device %d not available", root);
@@ -561,37 +564,67 @@ int bldp_band_reduce_multi_f32(int nbank, const int *bank_dev, const float *cons
   // BLDP_BAND_STAGED: every bank takes the staged branch (local reduce +
   // strided copy into the root's slot), even on the root device
   const bool force_staged = (flags & BLDP_BAND_STAGED) != 0;
+  const bool peer_store = (flags & BLDP_BAND_PEER_STORE) != 0;
   int prev = 0;
   HIPCHK(hipGetDevice(&prev));
+  // A device's banks, in bank order, cut into runs whose bank indices step
+  // evenly (b0, b0 + s, b0 + 2s, ...): one reduce launch per run, its banks'
+  // vcat slots nco * s floats apart.  Contiguous bank-per-device shards (GBT's
+  // workers, bench.py's ranks) are one run, i.e. one launch per device.
+  struct Run {
+    int dev, nb, step;
+    int bank[BLDP_MAX_BANKS];
+    bool direct;
+    size_t stage_off;  // staged runs: floats into the device's staging buffer
+  };
+  std::vector<Run> runs;
+  std::vector<size_t> nstaged(ndev, 0);  // floats of staging per device
   std::vector<hipStream_t> streams(ndev, nullptr);
-  // which banks write the root's product directly (same device, or peer
-  // access over xGMI) and which are reduced into staging on their own device
-  std::vector<char> direct(nbank, 0);
-  std::vector<int> nstaged(ndev, 0), slot(nbank, -1);
-  rc = BLDP_OK;
-  for (int b = 0; b < nbank && rc == BLDP_OK; ++b) {
-    const int d = bank_dev[b];
-    if (!streams[d] && (rc = device_stream(d, &streams[d])) != BLDP_OK) break;
-    if (hipSetDevice(d) != hipSuccess) {
-      rc = fail(BLDP_EHIP, "hipSetDevice(%d) failed", d);
-      break;
-    }
+  const size_t per = (size_t)(nco * ni * nto);
+  for (int d = 0; d < ndev && rc == BLDP_OK; ++d) {
+    std::vector<int> mine;
+    for (int b = 0; b < nbank; ++b)
+      if (bank_dev[b] == d) mine.push_back(b);
+    if (mine.empty()) continue;
+    if ((rc = device_stream(d, &streams[d])) != BLDP_OK) break;
+    // the root stores its own slots; another device only with
+    // BLDP_BAND_PEER_STORE and peer access (kernel stores over xGMI), else
+    // its runs are reduced into staging on the device and DMA-copied
     bool dir = d == root && !force_staged;
-    if (!dir && !force_staged) {
+    if (!dir && peer_store) {
       int can = 0;
       if (hipDeviceCanAccessPeer(&can, d, root) == hipSuccess && can) {
-        hipError_t pe = hipDeviceEnablePeerAccess(root, 0);
+        if (hipSetDevice(d) != hipSuccess) {
+          rc = fail(BLDP_EHIP, "hipSetDevice(%d) failed", d);
+          break;
+        }
+        const hipError_t pe = hipDeviceEnablePeerAccess(root, 0);
         dir = pe == hipSuccess || pe == hipErrorPeerAccessAlreadyEnabled;
-        (void)hipGetLastError();
       }
+      (void)hipGetLastError();
     }
-    direct[b] = dir;
-    if (!dir) slot[b] = nstaged[d]++;
+    for (size_t i = 0; i < mine.size();) {
+      Run r{};
+      r.dev = d;
+      r.direct = dir;
+      r.bank[0] = mine[i];
+      r.nb = 1;
+      r.step = i + 1 < mine.size() ? mine[i + 1] - mine[i] : 1;
+      while (i + r.nb < mine.size() && mine[i + r.nb] - mine[i + r.nb - 1] == r.step) {
+        r.bank[r.nb] = mine[i + r.nb];
+        ++r.nb;
+      }
+      i += r.nb;
+      if (!dir) {
+        r.stage_off = nstaged[d];
+        nstaged[d] += per * r.nb;
+      }
+      runs.push_back(r);
+    }
   }
   // staging: a library-owned buffer per device (no allocation per call once
-  // it has grown), one slot per staged bank, held until every launch and copy
-  // of this call is done (the call synchronizes before it returns)
-  const size_t per = (size_t)(nco * ni * nto) * sizeof(float);
+  // it has grown), held until every launch and copy of this call is done
+  // (the call synchronizes before it returns)
   std::vector<std::unique_lock<std::mutex>> hold;
   std::vector<void *> stage(ndev, nullptr);
   for (int d = 0; d < ndev && rc == BLDP_OK; ++d)
@@ -600,28 +633,36 @@ int bldp_band_reduce_multi_f32(int nbank, const int *bank_dev, const float *cons
         rc = fail(BLDP_EHIP, "hipSetDevice(%d) failed", d);
         break;
       }
-      rc = staging_buffer(d, per * nstaged[d], &stage[d], &hold);
+      rc = staging_buffer(d, nstaged[d] * sizeof(float), &stage[d], &hold);
     }
-  for (int b = 0; b < nbank && rc == BLDP_OK; ++b) {
-    const int d = bank_dev[b];
-    if (hipSetDevice(d) != hipSuccess) {
-      rc = fail(BLDP_EHIP, "hipSetDevice(%d) failed", d);
+  for (const Run &r : runs) {
+    if (rc != BLDP_OK) break;
+    if (hipSetDevice(r.dev) != hipSuccess) {
+      rc = fail(BLDP_EHIP, "hipSetDevice(%d) failed", r.dev);
       break;
     }
-    const float *ins[1] = {in[b]};
-    if (direct[b]) {
-      rc = reduce_impl(1, ins, nchan, nif, ntime, win, fqavby, tavby, op, out + b * nco, 0,
-                       ld_i, ld_t, false, streams[d], nullptr);
-    } else {  // reduce locally, then one strided peer copy into the bank's slot
-      float *st = (float *)((char *)stage[d] + per * slot[b]);
-      rc = reduce_impl(1, ins, nchan, nif, ntime, win, fqavby, tavby, op, st, 0, nco, nco * ni,
-                       false, streams[d], nullptr);
-      if (rc == BLDP_OK &&
-          hipMemcpy2DAsync(out + b * nco, ld_i * sizeof(float), st, nco * sizeof(float),
-                           nco * sizeof(float), (size_t)(ni * nto), hipMemcpyDeviceToDevice,
-                           streams[d]) != hipSuccess)
-        rc = fail(BLDP_EHIP, "peer copy of bank %d failed", b);
+    const float *ins[BLDP_MAX_BANKS];
+    for (int j = 0; j < r.nb; ++j) ins[j] = in[r.bank[j]];
+    if (r.direct) {  // one launch: the run's banks into their slots of the root's product
+      rc = reduce_impl(r.nb, ins, nchan, nif, ntime, win, fqavby, tavby, op,
+                       out + (int64_t)r.bank[0] * nco, (int64_t)r.step * nco, ld_i, ld_t, false,
+                       streams[r.dev], nullptr);
+      continue;
     }
+    // one launch into staging (the run's banks stitched among themselves),
+    // then strided copies into the root's slots: one 2-D copy for a run of
+    // neighbouring banks, one per bank otherwise
+    float *st = (float *)stage[r.dev] + r.stage_off;
+    const int64_t sld_i = (int64_t)r.nb * nco;
+    rc = reduce_impl(r.nb, ins, nchan, nif, ntime, win, fqavby, tavby, op, st, nco, sld_i,
+                     sld_i * ni, false, streams[r.dev], nullptr);
+    const int ncopy = r.step == 1 ? 1 : r.nb;
+    const int64_t width = r.step == 1 ? sld_i : nco;
+    for (int j = 0; j < ncopy && rc == BLDP_OK; ++j)
+      if (hipMemcpy2DAsync(out + (int64_t)r.bank[j] * nco, ld_i * sizeof(float), st + j * nco,
+                           sld_i * sizeof(float), width * sizeof(float), (size_t)(ni * nto),
+                           hipMemcpyDeviceToDevice, streams[r.dev]) != hipSuccess)
+        rc = fail(BLDP_EHIP, "peer copy of bank %d failed", r.bank[j]);
   }
   for (int d = 0; d < ndev; ++d)
     if (streams[d]) {

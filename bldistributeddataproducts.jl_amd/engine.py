@@ -397,13 +397,17 @@ class PreparedBandReduce:
 
 
 def band_reduce_multi(banks, fqavby=1, tavby=1, op="sum", win=None, root=0, out=None,
-                      staged=False):
+                      staged=False, peer_store=False):
     """One process, banks on several GPUs (bldp_band_reduce_multi_f32): each
-    GPU reduces its banks straight into the stitched product on `root` (into
-    ``out`` when given: a dense Julia-order (nbank*nco, ni, nto) Float32 tensor
-    there).  ``staged``: every bank takes the staged branch (BLDP_BAND_STAGED:
-    reduce on its device, then one strided copy into its slot), the root's
-    included -- a per-call argument, not process state."""
+    GPU reduces its banks (one launch per device for contiguous shards) into
+    their vcat slots of the stitched product on `root` (into ``out`` when
+    given: a dense Julia-order (nbank*nco, ni, nto) Float32 tensor there); a
+    device other than the root reduces into staging and one peer copy moves
+    its slots.  ``staged``: every bank takes the staged branch
+    (BLDP_BAND_STAGED), the root's included; ``peer_store``: devices with peer
+    access store their slots over xGMI from the kernels (BLDP_BAND_PEER_STORE,
+    opt-in until a multi-GPU node has run it) -- per-call arguments, not
+    process state."""
     torch = _torch()
     L = _lib.lib()
     banks = list(banks)
@@ -431,7 +435,8 @@ def band_reduce_multi(banks, fqavby=1, tavby=1, op="sum", win=None, root=0, out=
                                       ctypes.cast(ptrs, ctypes.c_void_p), *geo, wp,
                                       int(fqavby), int(tavby), _lib.OPS[op], int(root),
                                       out.data_ptr() if out.numel() else None,
-                                      _lib.BLDP_BAND_STAGED if staged else 0)
+                                      (_lib.BLDP_BAND_STAGED if staged else 0)
+                                      | (_lib.BLDP_BAND_PEER_STORE if peer_store else 0))
     _lib.check(rc, "bldp_band_reduce_multi_f32")
     return out
 

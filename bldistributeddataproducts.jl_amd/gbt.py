@@ -164,14 +164,15 @@ def _bank_shape(f):
     return _bank_geometry(f)[1]
 
 
-def _band_raw(ws, fs, geo, idxs, fqavby, op, tavby, band, root, force_copy, tm):
+def _band_raw(ws, fs, geo, idxs, fqavby, op, tavby, band, root, force_copy, tm,
+              peer_store=False):
     """Every bank a raw file of one geometry: each GPU reads its banks' windows
     as ONE stream of batches (bldp_file_runs_to_device: preads of every file
     into the pinned slot ring, H2D copies overlapping the reads) into one
     buffer, then the band is reduced straight into its vcat slots: one launch
-    on the root (bldp_band_reduce_f32), or, with banks on several GPUs, each
-    GPU's kernels writing the root's slots over xGMI
-    (bldp_band_reduce_multi_f32)."""
+    on the root (bldp_band_reduce_f32), or, with banks on several GPUs, one
+    launch per GPU whose slots reach the root by a peer copy (or, peer_store,
+    by the kernels' own stores over xGMI): bldp_band_reduce_multi_f32."""
     import time
 
     import torch
@@ -217,18 +218,19 @@ def _band_raw(ws, fs, geo, idxs, fqavby, op, tavby, band, root, force_copy, tm):
         tm["reduce"] = "bldp_band_reduce_f32 (one launch)"
     else:
         engine.band_reduce_multi(views, fqavby, tavby, op, rwin, root=root, out=band,
-                                 staged=force_copy)
+                                 staged=force_copy, peer_store=peer_store and not force_copy)
         tm["reduce"] = "bldp_band_reduce_multi_f32" + (" (staged)" if force_copy else "")
     tm["reduce_queue_ms"] = (time.perf_counter() - t1) * 1e3
 
 
-def _band_chunked(ws, fs, geo, idxs, fqavby, op, tavby, band, root, force_copy, tm):
+def _band_chunked(ws, fs, geo, idxs, fqavby, op, tavby, band, root, force_copy, tm,
+                  peer_store=False):
     """Every bank a chunked FBH5 file (filter 32008 or no filter) of one
     geometry: each GPU reads and decodes its banks' chunks as ONE stream of
     batches (fbh5.band_window_chunked_dev: bldp_file_chunks_to_device) into
     one chunk grid per bank, then the band is reduced straight into its vcat
-    slots, as _band_raw does for raw files (one launch on the root, or each
-    GPU writing the root's slots over xGMI).  False when the banks do not
+    slots, as _band_raw does for raw files (one launch on the root, or one
+    launch per GPU and a peer copy of its slots).  False when the banks do not
     qualify (the caller reads bank by bank)."""
     import time
 
@@ -272,13 +274,14 @@ def _band_chunked(ws, fs, geo, idxs, fqavby, op, tavby, band, root, force_copy, 
         tm["reduce"] = "bldp_band_reduce_f32 (one launch)"
     else:
         engine.band_reduce_multi(views, fqavby, tavby, op, rwin, root=root, out=band,
-                                 staged=force_copy)
+                                 staged=force_copy, peer_store=peer_store and not force_copy)
         tm["reduce"] = "bldp_band_reduce_multi_f32" + (" (staged)" if force_copy else "")
     tm["reduce_queue_ms"] = (time.perf_counter() - t1) * 1e3
     return True
 
 
-def _band_on_device(ws, fs, idxs, fqavby, op, tavby, nfpc, timings=None, staged=None):
+def _band_on_device(ws, fs, idxs, fqavby, op, tavby, nfpc, timings=None, staged=None,
+                    peer_store=None):
     """One band stitched on the GPU (src/gbt.jl:103): every
     bank is read and reduced on its worker's GPU straight into its vcat slot
     of the band product on the first worker's GPU, the DC-spike patch runs on
@@ -313,6 +316,12 @@ def _band_on_device(ws, fs, idxs, fqavby, op, tavby, nfpc, timings=None, staged=
     # box runs it.  An argument of this call: no process state is touched
     force_copy = (os.environ.get("BLDP_BAND_FORCE_COPY", "0") == "1" if staged is None
                   else bool(staged))
+    # peer_store (or BLDP_BAND_PEER_STORE=1 when not given): a bank's GPU
+    # other than the root stores its slot over xGMI from the reduce kernel
+    # instead of reducing locally and copying (opt-in: that branch has not yet
+    # run on a multi-GPU node)
+    peer_store = (os.environ.get("BLDP_BAND_PEER_STORE", "0") == "1" if peer_store is None
+                  else bool(peer_store))
     raw = (all(g[0] == "raw" for g in geo) and len({g[1] for g in geo}) == 1
            and os.environ.get("BLDP_NATIVE_READ", "1") != "0")
     # every bank a chunked FBH5 file of one geometry (the rawspec products:
@@ -320,21 +329,24 @@ def _band_on_device(ws, fs, idxs, fqavby, op, tavby, nfpc, timings=None, staged=
     chunked = (not raw and all(g[0] == "h5" for g in geo) and len({g[1] for g in geo}) == 1
                and os.environ.get("BLDP_NATIVE_READ", "1") != "0")
     if chunked:
-        chunked = _band_chunked(ws, fs, geo, idxs, fqavby, op, tavby, band, root, force_copy, tm)
+        chunked = _band_chunked(ws, fs, geo, idxs, fqavby, op, tavby, band, root, force_copy, tm,
+                                peer_store)
     if raw:
-        _band_raw(ws, fs, geo, idxs, fqavby, op, tavby, band, root, force_copy, tm)
+        _band_raw(ws, fs, geo, idxs, fqavby, op, tavby, band, root, force_copy, tm, peer_store)
     elif not chunked:
         # every bank is read (compressed chunks decoded) on its own GPU and
         # reduced there straight into its vcat slot on the root: a kernel
-        # store over xGMI where the bank's GPU may write the root's memory
-        # (bldp_peer_access), else reduced locally and copied into the slot
-        # by one stream-ordered device-to-device copy.  No host wait per bank:
+        # store where the bank's GPU is the root (or, with peer_store, may
+        # write the root's memory over xGMI: bldp_peer_access), else reduced
+        # locally and copied into the slot by one stream-ordered
+        # device-to-device copy.  No host wait per bank:
         # every reader queues on the caller's current stream of its device
         # (ordered with the root's despike and D2H below by the device
         # synchronize), and the band is complete when those streams drain.
         devs = sorted({int(w) for w in ws} | {root})
         cur = {d: torch.cuda.current_stream(d) for d in devs}
-        direct = {d: (not force_copy) and engine.peer_access(d, root) for d in devs}
+        direct = {d: (not force_copy)
+                  and (d == root or (peer_store and engine.peer_access(d, root))) for d in devs}
 
         def bank(b):
             slot = band[b * nco:(b + 1) * nco]
@@ -388,7 +400,7 @@ def _despike_host(d: np.ndarray, nfpc: int) -> np.ndarray:
 
 
 def getband(workers, fnames, idxs=(COLON, COLON, COLON), fqavby=1, fqavfunc="sum", tavby=1,
-            despike_nfpc=None, freqs=False, stitch="device", staged=None):
+            despike_nfpc=None, freqs=False, stitch="device", staged=None, peer_store=None):
     """The stitched band product: reduce(vcat, getdata(...)) in the given
     bank order (src/gbt.jl:103).  ``workers``/``fnames`` are one band's banks
     (1-D), or a (nbank, nband) matrix like loadscan's ``ds``, whose columns are
@@ -406,7 +418,10 @@ def getband(workers, fnames, idxs=(COLON, COLON, COLON), fqavby=1, fqavfunc="sum
     sends every bank of the device stitch through the staged branch (reduced
     on its own GPU, then copied into its slot) even where its GPU could write
     the root's memory directly: how a one-GPU box runs that branch (default:
-    the environment's BLDP_BAND_FORCE_COPY, else off)."""
+    the environment's BLDP_BAND_FORCE_COPY, else off).  ``peer_store=True``
+    lets a bank's GPU other than the root store its slot over xGMI straight
+    from the reduce kernel (default: the environment's BLDP_BAND_PEER_STORE,
+    else off: such banks are reduced on their GPU and copied into the slot)."""
     w = np.asarray(workers, dtype=object)
     f = np.asarray(fnames, dtype=object)
     if w.ndim not in (1, 2):
@@ -421,7 +436,7 @@ def getband(workers, fnames, idxs=(COLON, COLON, COLON), fqavby=1, fqavfunc="sum
     if stitch == "device" and op is not None:
         for j, (ws, fs) in enumerate(zip(wcol, fcol)):
             bands[j] = _band_on_device(ws, fs, idxs, fqavby, op, tavby, despike_nfpc,
-                                       staged=staged)
+                                       staged=staged, peer_store=peer_store)
     for j, (ws, fs) in enumerate(zip(wcol, fcol)):
         if bands[j] is not None:
             continue

@@ -213,14 +213,23 @@ BLDP_API int bldp_reduce_release(bldp_reduce_op_t handle);
 
 /* One process, one or more banks per GPU: bank b lives on
  * device bank_dev[b] (in[b] is a device pointer there).  Every device reduces
- * its banks and writes each result straight into its vcat slot of `out`, the
- * stitched (nbank*nco, ni, nto) product on device `root` — over xGMI with peer
- * access, else through a staged peer copy.  Synchronous; all banks share the
- * same (nchan, nif, ntime) and window.
- * flags: 0, or BLDP_BAND_STAGED: every bank takes the staged branch (reduce on
- * its device into library staging, then one strided copy into its slot), the
- * root's banks included (how a one-GPU box runs that branch). */
+ * its banks into their vcat slots of `out`, the stitched (nbank*nco, ni, nto)
+ * product on device `root`.  A device's banks are reduced by one launch per
+ * run of evenly spaced bank indices (one launch per device for contiguous
+ * shards).  The root's kernels store their slots directly; another device's
+ * banks are reduced into library staging on that device and moved by one
+ * strided peer copy per run (DMA over xGMI).  Synchronous; all banks share the
+ * same (nchan, nif, ntime) and window.  Replaces the per-worker getdata +
+ * reduce(vcat, ...) of GBT.getdata / loadscan (src/gbt.jl:75-78,103).
+ * flags: 0, or one of
+ *   BLDP_BAND_STAGED      every bank takes the staged branch, the root's banks
+ *                         included (how a one-GPU box runs that branch);
+ *   BLDP_BAND_PEER_STORE  devices with peer access to `root` store their
+ *                         slots directly from the reduce kernels (xGMI
+ *                         stores, no staging copy).  Opt-in: this branch has
+ *                         not yet run on a multi-GPU node. */
 #define BLDP_BAND_STAGED 1u
+#define BLDP_BAND_PEER_STORE 2u
 BLDP_API int bldp_band_reduce_multi_f32(int nbank, const int *bank_dev, const float *const *in,
                                         int64_t nchan, int64_t nif, int64_t ntime,
                                         const int64_t *win, int64_t fqavby, int64_t tavby,

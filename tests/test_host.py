@@ -569,6 +569,30 @@ def test_bench_spawned_ranks_fail_fast():
         assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
 
 
+def test_bench_spawned_ranks_deadline():
+    """A self-spawned rank that hangs (here: before the rendezvous, where its
+    peer blocks in init_process_group; on a GPU node, in an RCCL collective)
+    never exits, so no exit status reports it: spawn_ranks stops every rank
+    at --rank-deadline and bench.py returns 124."""
+    import subprocess
+    import sys
+    import time
+
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["BENCH_RENDEZVOUS_HANG_RANK"] = "1"
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    t0 = time.time()
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2",
+                        "--dist-backend", "gloo", "--mode", "rendezvous", "--rank-deadline", "20"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    el = time.time() - t0
+    assert r.returncode == 124, (r.returncode, r.stderr[-2000:])
+    assert 20 <= el < 60, el
+    assert "deadline" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
 def test_despike_host_keeps_the_result_type(pkg):
     """getband's host despike for non-Float32 bands (integer sums, Float64):
     d[spike:nfpc:end, :, :] .= d[spike-1:nfpc:end, :, :] with spike = nfpc÷2+1

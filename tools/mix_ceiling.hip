@@ -33,11 +33,12 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 
 // ST: 1 = nt store, 2 = plain store, 0 = no store (pure read; the store is
 // kept behind an impossible condition so the loads are not dead)
-template <int R, int ST>
+// LIF: float4 loads in flight per lane (16; 8 = the kurtosis kernels' batch)
+template <int R, int ST, int LIF = 16>
 __global__ __launch_bounds__(256) void k_mix(const f4v *__restrict__ in, f4v *__restrict__ out,
                                              int64_t nunits) {
-  constexpr int UB = R >= 16 ? 1 : 16 / R;  // units per chunk
-  constexpr int KB = R >= 16 ? 16 : R;      // loads per batch per unit
+  constexpr int UB = R >= LIF ? 1 : LIF / R;  // units per chunk
+  constexpr int KB = R >= LIF ? LIF : R;      // loads per batch per unit
   const int t = threadIdx.x;
   const int64_t nchunks = (nunits + UB - 1) / UB;
   for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
@@ -80,6 +81,11 @@ __global__ __launch_bounds__(256) void k_mix(const f4v *__restrict__ in, f4v *__
     }
   }
 }
+
+struct Size {
+  const char *label;
+  int64_t bytes;
+};
 
 static float median(std::vector<float> v) {
   std::sort(v.begin(), v.end());
@@ -157,12 +163,12 @@ __global__ void k_fill(f4v *p, int64_t n4) {
     p[i] = f4v{1.f, 2.f, 3.f, 4.f};
 }
 
-template <int R, int ST>
+template <int R, int ST, int LIF = 16>
 static void run(const f4v *in, f4v *out, int64_t read_bytes, int grid_mode, int reps,
                 const char *label, int ncu) {
   const int64_t nunits = read_bytes / ((int64_t)R * 4096);
   if (nunits <= 0) return;
-  constexpr int UB = R >= 16 ? 1 : 16 / R;
+  constexpr int UB = R >= LIF ? 1 : LIF / R;
   const int64_t nchunks = (nunits + UB - 1) / UB;
   // grid_mode 0: one workgroup per chunk; k > 0: k workgroups per CU (persistent)
   const int64_t grid = grid_mode == 0 ? nchunks : std::min<int64_t>(nchunks, (int64_t)grid_mode * ncu);
@@ -173,7 +179,7 @@ static void run(const f4v *in, f4v *out, int64_t read_bytes, int grid_mode, int 
   for (int r = 0; r < reps + 2; ++r) {
     CK(hipEventRecord(e0, 0));
     for (int i = 0; i < 5; ++i)  // back to back, as the library's timings are taken
-      hipLaunchKernelGGL((k_mix<R, ST>), dim3((unsigned)grid), dim3(256), 0, 0, in, out, nunits);
+      hipLaunchKernelGGL((k_mix<R, ST, LIF>), dim3((unsigned)grid), dim3(256), 0, 0, in, out, nunits);
     CK(hipEventRecord(e1, 0));
     CK(hipEventSynchronize(e1));
     float m;
@@ -182,9 +188,10 @@ static void run(const f4v *in, f4v *out, int64_t read_bytes, int grid_mode, int 
   }
   const double rb = (double)nunits * R * 4096, wb = ST ? (double)nunits * 4096 : 0.0;
   const float med = median(ms);
-  printf("{\"size\": \"%s\", \"read_bytes\": %.0f, \"write_bytes\": %.0f, \"R\": %d, \"store\": \"%s\", "
+  printf("{\"size\": \"%s\", \"read_bytes\": %.0f, \"write_bytes\": %.0f, \"R\": %d, "
+         "\"loads_in_flight\": %d, \"store\": \"%s\", "
          "\"grid\": \"%s\", \"ms_median\": %.4f, \"ms_min\": %.4f, \"GBps_median\": %.1f}\n",
-         label, rb, wb, R, ST == 1 ? "nt" : ST == 2 ? "plain" : ST == 3 ? "nt dword" : "none",
+         label, rb, wb, R, LIF, ST == 1 ? "nt" : ST == 2 ? "plain" : ST == 3 ? "nt dword" : "none",
          grid_mode == 0 ? "chunk" : (grid_mode == 1 ? "1/CU" : grid_mode == 2 ? "2/CU" : "4/CU"),
          med, *std::min_element(ms.begin(), ms.end()), (rb + wb) / med / 1e6);
   fflush(stdout);
@@ -226,6 +233,27 @@ int main(int argc, char **argv) {
     }
     return 0;
   }
+  if (argc > 2 && std::string(argv[2]) == "kurt") {
+    // the Float32 kurtosis bands' mixes: cfg3 reads 32 GiB
+    // and writes 4 GiB of Float64 (R = 8), cfg4 reads 14.4 GB (pure read), cfg2
+    // 585 MB (pure read); every grid form, 16 and 8 float4 loads in flight
+    const Size ks[] = {{"0000 band 32 GiB", big}, {"0001 band 14.4 GB", 8ll * 512 * 879616 * 4},
+                       {"0002 band 585 MB", 8ll * 65536 * 279 * 4}};
+    for (const Size &s : ks) {
+      if (s.bytes == big) {
+        for (int g : {0, 1, 2, 4}) {
+          run<8, 1, 16>(in, out, s.bytes, g, reps, s.label, ncu);
+          run<8, 1, 8>(in, out, s.bytes, g, reps, s.label, ncu);
+        }
+        run<8, 2, 16>(in, out, s.bytes, 0, reps, s.label, ncu);
+      }
+      for (int g : {0, 1, 2, 4}) {
+        run<16, 0, 16>(in, out, s.bytes, g, reps, s.label, ncu);
+        run<8, 0, 8>(in, out, s.bytes, g, reps, s.label, ncu);
+      }
+    }
+    return 0;
+  }
   if (argc > 2 && std::string(argv[2]) == "coltile") {  // the 0002 band as the kurtosis reads it
     const float *fi = reinterpret_cast<const float *>(in);
     double *fo = reinterpret_cast<double *>(out);
@@ -239,10 +267,6 @@ int main(int argc, char **argv) {
     }
     return 0;
   }
-  struct Size {
-    const char *label;
-    int64_t bytes;
-  };
   // one 0002 file (65536 x 279 floats), the 0002 band (8 of them), the 0000 band
   const Size all_sizes[] = {{"0002 file 73 MB", 65536ll * 279 * 4},
                             {"0002 band 585 MB", 8ll * 65536 * 279 * 4},
