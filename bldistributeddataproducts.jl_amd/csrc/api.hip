@@ -866,8 +866,15 @@ int bldp_kurtosis(int dtype, const void *in, int64_t nchan, int64_t nif, int64_t
   a.ni = g.ni;
   a.nto = g.nt;
   a.F = a.T = 1;
+  a.num_cus = num_cus_current();
   if (a.nco * a.ni == 0) return BLDP_OK;
   if (!out || (!in && g.nt > 0)) return fail(BLDP_EINVAL, "null pointer");
+  ScratchLease lease;  // time-chunk partial sums (k_kurt_i8), held until queued
+  if (const size_t wsb = kurtosis_typed_ws_bytes(a)) {
+    rc = scratch_lease((hipStream_t)stream, wsb, &lease);
+    if (rc) return rc;
+    a.ws = lease.ptr;
+  }
   hipError_t e = launch_kurtosis_typed(a, out, (hipStream_t)stream);
   if (e != hipSuccess) return fail(BLDP_EHIP, "typed kurtosis launch: %s", hipGetErrorString(e));
   return BLDP_OK;

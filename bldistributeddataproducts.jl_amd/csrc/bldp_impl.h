@@ -94,7 +94,7 @@ enum PlanOpt {
   OPT_WIDE_SPLIT, OPT_NARROW_TPB, OPT_LANE, OPT_LANE3, OPT_LANET, OPT_LANET_PACK, OPT_VEC_IL,
   OPT_VEC_ROW, OPT_ROW_TPB, OPT_ROWT_PACK, OPT_ROWT_SMALL, OPT_WAVET, OPT_UNALIGNED_VEC,
   OPT_KURT_EXACT, OPT_KURT_MID_CPL, OPT_KURT_MID_SMALL, OPT_KURT_LEAF_NARROW, OPT_KURT_LEAF_TILE,
-  OPT_TYPED_VEC, OPT_ROW_BPACK, OPT_LANE_BPACK, OPT_WAVE_BPACK, OPT_COL3, OPT_ROWT_NARROW8, OPT_ST_PLAIN, OPT_COUNT
+  OPT_TYPED_VEC, OPT_TYPED_KURT, OPT_ROW_BPACK, OPT_LANE_BPACK, OPT_WAVE_BPACK, OPT_COL3, OPT_ROWT_NARROW8, OPT_ST_PLAIN, OPT_COUNT
 };
 int64_t plan_opt(int k);
 inline int64_t opt(int k) { return plan_opt(k); }
@@ -192,11 +192,13 @@ struct TypedArgs {
   int64_t in_off, in_cs, in_ld_i, in_ld_t;
   int64_t nco, ni, nto, F, T;
   int32_t num_cus;  // of the launch's device (the coalesced kernel's grid)
+  void *ws;         // typed kurtosis: kurtosis_typed_ws_bytes of scratch (or null)
 };
 size_t dtype_size(int dtype);              // 0 = unknown
 int typed_out_dtype(int dtype, int op);    // -1 = invalid
 hipError_t launch_reduce_typed(const TypedArgs &a, int op, hipStream_t s);
 hipError_t launch_kurtosis_typed(const TypedArgs &a, double *out, hipStream_t s);
+size_t kurtosis_typed_ws_bytes(const TypedArgs &a);  // scratch launch_kurtosis_typed wants
 
 hipError_t launch_synth(float *out, int64_t nchan, int64_t nif, int64_t ntime, int64_t nfpc,
                         uint64_t seed, int kind, hipStream_t s);

@@ -523,6 +523,203 @@ __global__ __launch_bounds__(256) void k_kurt_typed_w(const TypedArgs a, double 
   }
 }
 
+// getkurtosis of 8-bit rows (SIGPROC nbits 8, the UInt8 products) from exact
+// integer power sums.  For each channel the row's S1..S4 = sum of d^1..d^4,
+// d = x - 128 (UInt8) or x (Int8), are integers that Int64 / UInt64 hold
+// exactly (|d| <= 128, n <= 2^23), so any split of the time axis adds them
+// back exactly: the window is read once by NW waves per 64-word tile (4
+// channels a lane, one 32-bit word of each spectrum; 256 contiguous bytes per
+// wave-instruction), each wave summing a time slab, the slabs added in LDS
+// (ds_add_u64), and, for long rows, time chunks of several workgroups added by
+// k_kurt_i8_final.  From the exact sums, with n the window's length:
+//   Y = n S2 - S1^2                                  = n^2 cm2
+//   X = n^3 S4 - 4 n^2 S1 S3 + 6 n S1^2 S2 - 3 S1^4   = n^4 cm4
+// (cm2, cm4: the central moments sum((x - mu)^k) / n, which the shift leaves
+// alone) in Int128 (exact for n <= 2^23), and kurtosis = X / Y^2 - 3 in
+// Float64: StatsBase's (cm4 / n) / (cm2 / n)^2 - 3 with exact central moments.
+// The recipe (src/gbtworkerfunctions.jl:197-202; Float64 m, z, z^2, z^4 and
+// sequential Float64 sums) differs from it by its own rounding, at most
+// (3 nt + 10) 2^-53 relative on k + 3 (tests hold it to
+// conftest.kurt_int_tol).  A row of one value: X = Y = 0 -> NaN, as the recipe.
+// Plan option "typed_kurt": 1 (default) = this path for 8-bit rows of
+// dword-aligned words, 0 = k_kurt_typed_w (the recipe's order, bit-exact).
+struct KTM {
+  int nw;           // waves per workgroup (time slabs)
+  int64_t ntile;    // 64-word tiles per row
+  int64_t nchunk;   // time chunks (workgroups along time); 1: fused finish
+  int64_t crow;     // spectra per chunk
+  int64_t srow;     // spectra per wave slab (<= 65536: the UInt32 lane sums)
+};
+constexpr int64_t kI8MaxN = (int64_t)1 << 23;
+
+__device__ __forceinline__ double i128_to_f64(__int128 x) {
+  const int64_t hi = (int64_t)(x >> 64);
+  const uint64_t lo = (uint64_t)x;
+  return (double)hi * 18446744073709551616.0 + (double)lo;
+}
+
+__device__ __forceinline__ double kurt_from_sums(int64_t n, int64_t S1, uint64_t S2, int64_t S3,
+                                                 uint64_t S4) {
+  const __int128 N = n, A = S1, B = (__int128)S2, C = S3, D = (__int128)S4;
+  const __int128 Y = N * B - A * A;
+  const __int128 X = N * N * N * D - 4 * N * N * A * C + 6 * N * A * A * B - 3 * A * A * A * A;
+  const double y = i128_to_f64(Y);
+  return i128_to_f64(X) / (y * y) - 3.0;
+}
+
+typedef short s2v __attribute__((ext_vector_type(2)));
+typedef unsigned short u2v __attribute__((ext_vector_type(2)));
+
+// 4 spectra x 4 channels of bytes (one word per spectrum) -> one word per
+// channel holding its 4 spectra (v_perm_b32: 8 per 16 bytes)
+__device__ __forceinline__ void transpose4(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3,
+                                           uint32_t (&T)[4]) {
+  const uint32_t A = __builtin_amdgcn_perm(w1, w0, 0x05010400u);  // w0.b0 w1.b0 w0.b1 w1.b1
+  const uint32_t B = __builtin_amdgcn_perm(w1, w0, 0x07030602u);  // w0.b2 w1.b2 w0.b3 w1.b3
+  const uint32_t C = __builtin_amdgcn_perm(w3, w2, 0x05010400u);
+  const uint32_t D = __builtin_amdgcn_perm(w3, w2, 0x07030602u);
+  T[0] = __builtin_amdgcn_perm(C, A, 0x05040100u);
+  T[1] = __builtin_amdgcn_perm(C, A, 0x07060302u);
+  T[2] = __builtin_amdgcn_perm(D, B, 0x05040100u);
+  T[3] = __builtin_amdgcn_perm(D, B, 0x07060302u);
+}
+
+template <bool SIGNED>
+__global__ __launch_bounds__(1024) void k_kurt_i8(const TypedArgs a, const KTM m, double *out,
+                                                  uint64_t *ws) {
+  constexpr int U = 16;  // spectra of loads in flight per lane
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t ngl = a.nco / 4, tile = blockIdx.x, r = blockIdx.y, chunk = blockIdx.z;
+  const int64_t q = tile * 64 + lane;  // this lane's word
+  const int64_t i = r % a.ni, bank = r / a.ni;
+  const int64_t ct0 = chunk * m.crow, ct1 = min(a.nto, ct0 + m.crow);
+  const int64_t t0 = min(ct1, ct0 + (int64_t)wave * m.srow), t1 = min(ct1, t0 + m.srow);
+  // sums of d = x - 128 (UInt8: the byte's top bit flipped, read as Int8) or
+  // x (Int8), |d| <= 128, per channel over 4 spectra at a time: the batch's
+  // words transposed so a word holds one channel's 4 spectra, then
+  //   S1 += sdot4(T, 1), S2 += sdot4(T, T)                (<= 2^30 in 65536)
+  //   S3 += sdot2(d^2, d) over the Int16 halves           (<= 2^25 a batch)
+  //   S4 += udot2(d^2, d^2)                               (<= 2^31 per 8)
+  // (d^2 by v_pk_mul_lo_u16: <= 2^14), S3 and S4 moved to 64-bit sums per
+  // batch / per 8 spectra: ~4 VALU operations per byte
+  int32_t s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
+  int64_t s3[4] = {0, 0, 0, 0};
+  uint64_t s4[4] = {0, 0, 0, 0};
+  if (q < ngl) {
+    const int64_t ldb = a.in_ld_t;  // bytes (1-byte elements)
+    const char *p = static_cast<const char *>(a.in[bank]) + a.in_off + i * a.in_ld_i + 4 * q;
+    for (int64_t t = t0; t < t1; t += U) {
+      const int cnt = (int)min((int64_t)U, t1 - t);
+      uint32_t w[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        w[u] = u < cnt ? __builtin_nontemporal_load(
+                             reinterpret_cast<const uint32_t *>(p + (t + u) * ldb))
+                       : (SIGNED ? 0u : 0x80808080u);  // (d = 0: adds nothing)
+      int32_t b3[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int h = 0; h < U; h += 8) {
+        uint32_t b4[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int g = h; g < h + 8; g += 4) {
+          if (g >= cnt) break;  // (uniform: a short last batch)
+          uint32_t T[4];
+          if (SIGNED)
+            transpose4(w[g], w[g + 1], w[g + 2], w[g + 3], T);
+          else
+            transpose4(w[g] ^ 0x80808080u, w[g + 1] ^ 0x80808080u, w[g + 2] ^ 0x80808080u,
+                       w[g + 3] ^ 0x80808080u, T);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int tk = (int)T[k];
+            s1[k] = __builtin_amdgcn_sdot4(tk, 0x01010101, s1[k], false);
+            s2[k] = __builtin_amdgcn_sdot4(tk, tk, s2[k], false);
+            // Int16 halves: spectra (0, 2) and (1, 3), sign-extended
+            const s2v e = __builtin_bit_cast(s2v, T[k] << 8) >> (short)8;
+            const s2v o = __builtin_bit_cast(s2v, T[k]) >> (short)8;
+            const u2v ue = __builtin_bit_cast(u2v, e), uo = __builtin_bit_cast(u2v, o);
+            const u2v qe = ue * ue, qo = uo * uo;  // d^2 (mod 2^16: exact, <= 2^14)
+            b3[k] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2v, qe), e, b3[k], false);
+            b3[k] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2v, qo), o, b3[k], false);
+            b4[k] = __builtin_amdgcn_udot2(qe, qe, b4[k], false);
+            b4[k] = __builtin_amdgcn_udot2(qo, qo, b4[k], false);
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s4[k] += b4[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s3[k] += b3[k];
+    }
+  }
+  // the slabs' sums added in LDS (two's complement: the signed sums too)
+  __shared__ unsigned long long acc[4][256];
+  for (int e = threadIdx.x; e < 4 * 256; e += blockDim.x) (&acc[0][0])[e] = 0ull;
+  __syncthreads();
+  if (q < ngl && t1 > t0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int ch = 4 * lane + k;
+      atomicAdd(&acc[0][ch], (unsigned long long)(int64_t)s1[k]);
+      atomicAdd(&acc[1][ch], (unsigned long long)s2[k]);
+      atomicAdd(&acc[2][ch], (unsigned long long)s3[k]);
+      atomicAdd(&acc[3][ch], (unsigned long long)s4[k]);
+    }
+  }
+  __syncthreads();
+  for (int ch = threadIdx.x; ch < 256; ch += blockDim.x) {
+    const int64_t c = tile * 256 + ch;  // this workgroup's 256 channels, coalesced
+    if (c < a.nco) {
+      if (m.nchunk == 1) {
+        out[c + a.nco * r] = kurt_from_sums(a.nto, (int64_t)acc[0][ch], acc[1][ch],
+                                            (int64_t)acc[2][ch], acc[3][ch]);
+      } else {
+        const int64_t rows = a.ni * a.nbank;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) ws[((chunk * 4 + s) * rows + r) * a.nco + c] = acc[s][ch];
+      }
+    }
+  }
+}
+
+// The chunks' sums of every channel added in chunk order (exact), then the
+// kurtosis (nchunk > 1).
+__global__ __launch_bounds__(256) void k_kurt_i8_final(const TypedArgs a, const KTM m,
+                                                       double *out, const uint64_t *ws) {
+  const int64_t rows = a.ni * a.nbank, n = a.nco * rows;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n) return;
+  uint64_t S[4] = {0, 0, 0, 0};
+  for (int64_t c = 0; c < m.nchunk; ++c)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) S[s] += ws[(c * 4 + s) * n + e];
+  out[e] = kurt_from_sums(a.nto, (int64_t)S[0], S[1], (int64_t)S[2], S[3]);
+}
+
+// The k_kurt_i8 geometry, or false when the path does not apply.
+bool kurt_i8_plan(const TypedArgs &a, KTM *m) {
+  if (dtype_size(a.dtype) != 1 || !opt(OPT_TYPED_KURT)) return false;
+  if (a.in_cs != 1 || a.nco % 4 || a.nto < 1 || a.nto > kI8MaxN) return false;
+  if (a.in_off % 4 || (a.ni > 1 && a.in_ld_i % 4) || (a.nto > 1 && a.in_ld_t % 4)) return false;
+  for (int b = 0; b < a.nbank; ++b)
+    if ((uintptr_t)a.in[b] % 4) return false;
+  const int64_t rows = a.ni * a.nbank;
+  m->ntile = cdivt(a.nco / 4, 64);
+  m->nw = (int)std::min<int64_t>(16, cdivt(a.nto, 16));
+  // time chunks only while the tiles' waves leave the CUs short of 16 each
+  // (0001: 512 channels = 2 tiles a row, ~10^6 spectra), never slabs under 16
+  // spectra, and never over 65536 (the lanes' UInt32 sums)
+  const int64_t waves = m->ntile * rows * m->nw, want = 16 * (int64_t)std::max(1, a.num_cus);
+  int64_t nchunk = std::max<int64_t>(1, std::min(cdivt(want, waves),
+                                                 a.nto / (16 * (int64_t)m->nw)));
+  nchunk = std::max(nchunk, cdivt(a.nto, (int64_t)m->nw * 65536));
+  m->crow = cdivt(a.nto, nchunk);
+  m->srow = cdivt(m->crow, m->nw);
+  m->crow = m->srow * m->nw;
+  m->nchunk = cdivt(a.nto, m->crow);
+  return m->ntile <= INT32_MAX && rows <= 65535 && m->nchunk <= 65535;
+}
+
 // The coalesced kernel's geometry for this window, or false when it does not
 // apply (Float64 sums, 64-bit means and inexact 32-bit means keep the
 // reference's order on k_reduce_typed; windows without dword-aligned 16-byte
@@ -625,6 +822,19 @@ hipError_t launch_typed_op(const TypedArgs &a, int op, hipStream_t s) {
 template <typename TI>
 hipError_t launch_kurt_t(const TypedArgs &a, double *out, hipStream_t s) {
   const int64_t n = a.nco * a.ni * a.nbank;
+  if constexpr (sizeof(TI) == 1) {  // exact integer moments (k_kurt_i8)
+    KTM m;
+    if (kurt_i8_plan(a, &m) && (m.nchunk == 1 || a.ws)) {
+      const dim3 g((unsigned)m.ntile, (unsigned)(a.ni * a.nbank), (unsigned)m.nchunk);
+      uint64_t *ws = static_cast<uint64_t *>(a.ws);
+      hipLaunchKernelGGL((k_kurt_i8<std::is_signed<TI>::value>), g, dim3(64 * m.nw), 0, s, a, m,
+                         out, ws);
+      if (m.nchunk > 1)
+        hipLaunchKernelGGL(k_kurt_i8_final, dim3((unsigned)cdivt(n, 256)), dim3(256), 0, s, a, m,
+                           out, ws);
+      return hipGetLastError();
+    }
+  }
   if constexpr (sizeof(TI) <= 2) {  // 32-bit words of 4 / 2 channels (k_kurt_typed_w)
     constexpr int64_t cpl = 4 / (int64_t)sizeof(TI);
     bool ok = opt(OPT_TYPED_VEC) && a.in_cs == 1 && a.nco % cpl == 0 && a.nto > 0 &&
@@ -642,6 +852,12 @@ hipError_t launch_kurt_t(const TypedArgs &a, double *out, hipStream_t s) {
 }
 
 }  // namespace
+
+size_t kurtosis_typed_ws_bytes(const TypedArgs &a) {
+  KTM m;
+  if (!kurt_i8_plan(a, &m) || m.nchunk == 1) return 0;
+  return (size_t)m.nchunk * 4 * (size_t)(a.ni * a.nbank * a.nco) * sizeof(uint64_t);
+}
 
 size_t dtype_size(int dtype) {
   switch (dtype) {

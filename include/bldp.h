@@ -153,7 +153,7 @@ BLDP_API int bldp_reduce_plan_f32(const float *in, int64_t nchan, int64_t nif, i
  *   "narrow_tpb", "lane", "lane3", "lanet", "lanet_pack", "vec_il",
  *   "vec_row", "row_tpb", "rowt_pack", "rowt_small", "wavet",
  *   "unaligned_vec", "kurt_exact", "kurt_mid_cpl", "kurt_mid_small",
- *   "kurt_leaf_narrow", "kurt_leaf_tile", "typed_vec",
+ *   "kurt_leaf_narrow", "kurt_leaf_tile", "typed_vec", "typed_kurt",
  *   "row_bpack", "lane_bpack", "wave_bpack", "col3", "rowt_narrow8", "st_plain"
  *                    which kernel a reduce / kurtosis / typed shape takes
  *                    (csrc/kernels.hip kPlanOpts: defaults, meanings and the

@@ -19,6 +19,8 @@ from __future__ import annotations
 import numpy as np
 import pytest
 
+from conftest import assert_kurtosis
+
 pytestmark = pytest.mark.gpu
 
 INT_TYPES = [np.uint8, np.uint16, np.uint32, np.uint64, np.int8, np.int16, np.int32, np.int64]
@@ -59,6 +61,36 @@ def same(got, want):
         return np.array_equal(got.view(np.uint64), want.view(np.uint64)) or \
             np.array_equal(got, want, equal_nan=True)
     return np.array_equal(got, want)
+
+
+def kurt_same(got, want, dt, nt, msg=""):
+    """Typed getkurtosis against the recipe: 8-bit rows take k_kurt_i8 (exact
+    integer moments), within conftest.kurt_int_tol(nt) of it; every other type
+    follows the recipe's sequence, bit for bit."""
+    if np.dtype(dt).itemsize == 1:
+        assert np.asarray(got).dtype == np.asarray(want).dtype
+        assert_kurtosis(got, want, "int", nt, msg)
+    else:
+        assert same(got, want), msg
+
+
+def exact_kurtosis(a):
+    """The exact excess kurtosis of every (channel, IF) row of an 8-bit
+    array, rounded once: power sums in Int64 (exact for these types), then
+    Python integers, X / Y^2 - 3 with Y = n S2 - S1^2,
+    X = n^3 S4 - 4 n^2 S1 S3 + 6 n S1^2 S2 - 3 S1^4 (typed.hip k_kurt_i8)."""
+    from fractions import Fraction
+
+    v = a.astype(np.int64)
+    n = a.shape[2]
+    S = [(v ** k).sum(axis=2) for k in (1, 2, 3, 4)]
+    out = np.empty(a.shape[:2])
+    for idx in np.ndindex(*a.shape[:2]):
+        s1, s2, s3, s4 = (int(x[idx]) for x in S)
+        y = n * s2 - s1 * s1
+        x = n ** 3 * s4 - 4 * n * n * s1 * s3 + 6 * n * s1 * s1 * s2 - 3 * s1 ** 4
+        out[idx] = np.nan if y == 0 else float(Fraction(x, y * y) - 3)
+    return out
 
 
 JULIA_OUT = {("sum", np.uint8): np.uint64, ("sum", np.uint16): np.uint64,
@@ -158,12 +190,12 @@ def test_kurtosis_typed(pkg, eng, orc, dt):
             a = np.asfortranarray((a.astype(np.int64) % 1000).astype(dt))
         want = orc.np_kurtosis_typed(a)
         got = eng.fb_to_numpy(eng.kurtosis(to_dev(eng, a)))
-        assert same(got, want), (dt, (nc, ni, nt))
-        assert same(eng.kurtosis_host_typed(a), want), (dt, (nc, ni, nt), "host")
+        kurt_same(got, want, dt, nt, (dt, (nc, ni, nt)))
+        kurt_same(eng.kurtosis_host_typed(a), want, dt, nt, (dt, (nc, ni, nt), "host"))
     # windows: a spectrum range of every other channel; an empty time window -> NaN
     a = rand(dt, (40, 1, 300), seed=3)
     w = [1, 19, 2, 0, 1, 1, 10, 250, 1]
-    assert same(eng.kurtosis_host_typed(a, w), orc.np_kurtosis_typed(a, w))
+    kurt_same(eng.kurtosis_host_typed(a, w), orc.np_kurtosis_typed(a, w), dt, 250)
     e = eng.kurtosis_host_typed(a, [0, 40, 1, 0, 1, 1, 0, 0, 1])
     assert e.shape == (40, 1) and np.isnan(e).all()
 
@@ -172,23 +204,67 @@ def test_kurtosis_typed(pkg, eng, orc, dt):
                          ids=lambda d: np.dtype(d).name)
 def test_kurtosis_typed_words(pkg, eng, orc, dt):
     """8- and 16-bit getkurtosis with a lane on each 32-bit word of 4 / 2
-    channels (k_kurt_typed_w): bit-identical to the one-lane-per-channel
-    kernel (plan option typed_vec = 0) and to the oracle; the type's full
-    range, spectrum counts around the 16-spectrum batches, two IFs, a
-    channel window on a word boundary and one off it (the fallback)."""
+    channels (k_kurt_typed_w, the recipe's order; for 8-bit rows with plan
+    option typed_kurt = 0): bit-identical to the one-lane-per-channel kernel
+    (plan option typed_vec = 0) and to the oracle; the type's full range,
+    spectrum counts around the 16-spectrum batches, two IFs, a channel window
+    on a word boundary and one off it (the fallback).  8-bit rows by default
+    take k_kurt_i8, held to kurt_int_tol."""
     info = np.iinfo(dt)
+    one = np.dtype(dt).itemsize == 1
     for k, (nc, ni, nt) in enumerate([(256, 2, 1000), (1024, 1, 77), (64, 1, 16), (128, 3, 15)]):
         rng = np.random.default_rng(k + np.dtype(dt).num)
         a = np.asfortranarray(rng.integers(info.min, info.max, (nc, ni, nt), endpoint=True)
                               .astype(dt))
         x = to_dev(eng, a)
+        want = orc.np_kurtosis_typed(a)
         got = eng.fb_to_numpy(eng.kurtosis(x))
-        assert same(got, orc.np_kurtosis_typed(a)), (dt, (nc, ni, nt))
-        with pkg._lib.plan_option("typed_vec", 0):
-            assert same(eng.fb_to_numpy(eng.kurtosis(x)), got), (dt, (nc, ni, nt))
+        kurt_same(got, want, dt, nt, (dt, (nc, ni, nt)))
+        with pkg._lib.plan_option("typed_kurt", 0):
+            rec = eng.fb_to_numpy(eng.kurtosis(x))
+            assert same(rec, want), (dt, (nc, ni, nt))
+            with pkg._lib.plan_option("typed_vec", 0):
+                assert same(eng.fb_to_numpy(eng.kurtosis(x)), rec), (dt, (nc, ni, nt))
+        if not one:
+            assert same(got, rec)
         for w in ([4, nc - 8, 1, 0, ni, 1, 3, nt - 3, 1], [1, nc - 4, 1, 0, ni, 1, 0, nt, 1]):
-            assert same(eng.fb_to_numpy(eng.kurtosis(x, w)), orc.np_kurtosis_typed(a, w)), \
-                (dt, (nc, ni, nt), w)
+            kurt_same(eng.fb_to_numpy(eng.kurtosis(x, w)), orc.np_kurtosis_typed(a, w), dt,
+                      w[7], (dt, (nc, ni, nt), w))
+
+
+@pytest.mark.parametrize("dt", [np.uint8, np.int8], ids=lambda d: np.dtype(d).name)
+def test_kurtosis_8bit_exact_moments(pkg, eng, orc, dt):
+    """k_kurt_i8 (8-bit getkurtosis from exact integer power sums, time split
+    over waves and, for long rows, over workgroups whose sums a second kernel
+    adds): within 8 roundings (8 x 2^-53 relative on k + 3) of the exactly
+    rounded kurtosis (Python integers), and within kurt_int_tol(nt) of the
+    recipe (oracle).  The 0002 file geometry, one and several time chunks
+    (the 0001 shape: few channels, long rows), the type's extremes (rows of
+    only min / max: NaN as the recipe; two values), two IFs and a window."""
+    info = np.iinfo(dt)
+    rng = np.random.default_rng(99 + np.dtype(dt).num)
+    for nc, ni, nt in ((65536, 1, 279), (512, 1, 200000), (256, 2, 4099), (8, 1, 17)):
+        a = np.asfortranarray(rng.integers(info.min, info.max, (nc, ni, nt), endpoint=True)
+                              .astype(dt))
+        a[0, 0, :] = info.max  # constant rows: NaN
+        a[1, 0, :] = info.min
+        a[2, 0, :] = np.where(np.arange(nt) % 3 == 0, info.min, info.max)  # two values
+        a[3, 0, :nt // 2] = info.min  # a long run then noise
+        x = to_dev(eng, a)
+        got = eng.fb_to_numpy(eng.kurtosis(x))
+        sub = (slice(None), slice(None)) if nc * ni <= 4096 else (slice(0, 1024), slice(None))
+        ex = exact_kurtosis(a[sub[0]])
+        assert_kurtosis(got[sub], ex, "int", 1, (dt, nc, nt, "exact"))
+        fin = np.isfinite(ex)
+        assert np.all(np.abs(got[sub][fin] - ex[fin]) <= 8 * 2.0 ** -53 * np.abs(ex[fin] + 3)), \
+            (dt, nc, nt)
+        if nc * ni * nt <= 5e6:
+            assert_kurtosis(got, orc.np_kurtosis_typed(a), "int", nt, (dt, nc, nt))
+    a = np.asfortranarray(rng.integers(info.min, info.max, (1000, 1, 300), endpoint=True)
+                          .astype(dt))
+    w = [8, 960, 1, 0, 1, 1, 5, 290, 1]  # word-aligned channel span, a time window
+    got = eng.fb_to_numpy(eng.kurtosis(to_dev(eng, a), w))
+    assert_kurtosis(got, orc.np_kurtosis_typed(a, w), "int", 290, (dt, "window"))
 
 
 def test_worker_api_keeps_reference_types(pkg, eng, orc, tmp_path):
@@ -213,7 +289,7 @@ def test_worker_api_keeps_reference_types(pkg, eng, orc, tmp_path):
         w = [0, 128, 1, 1, 1, 1, 4, 40, 1]
         assert same(got, orc.np_reduce_typed(a, 8, 4, "sum", w))
         k = W.getkurtosis(f)
-        assert same(k, orc.np_kurtosis_typed(a)), nbits
+        kurt_same(k, orc.np_kurtosis_typed(a), dt, 50, nbits)
     b = np.asfortranarray(rng.standard_normal((512, 1, 30)))
     assert same(W.fqav(b, 8), orc.np_reduce_typed(b, 8, 1, "sum"))
     assert same(W.fqav(b, 8, "mean"), orc.np_reduce_typed(b, 8, 1, "mean"))
