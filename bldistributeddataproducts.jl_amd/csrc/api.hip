@@ -120,6 +120,26 @@ int num_cus_current() {
   return n;
 }
 
+// log2 of the current device's XCD count for the per-XCD tile order
+// (hipDeviceAttributeNumberOfXccs: 8 on an MI355X in SPX mode, fewer in the
+// compute partitions), 0 when it is 1 or not a power of two.
+int xcd_log2_current() {
+  static std::mutex mu;
+  static std::map<int, int> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(dev);
+  if (it != cache.end()) return it->second;
+  int n = 1, lg = 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeNumberOfXccs, dev) != hipSuccess) n = 1;
+  (void)hipGetLastError();
+  if (n > 1 && (n & (n - 1)) == 0)
+    while ((1 << lg) < n) ++lg;
+  cache[dev] = lg;
+  return lg;
+}
+
 // Library-owned scratch, cached per (device, stream) so that concurrent
 // streams never share a buffer.  Host threads sharing one stream (the GBT
 // fan-out runs a thread per (worker, file) on torch's current stream) take
@@ -316,7 +336,8 @@ int prepare_reduce(int nbank, const float *const *in, int64_t nchan, int64_t nif
   const bool aligned = (rows16 && vec_ok(g)) ||
                        (opt(OPT_UNALIGNED_VEC) >= 1 && words && g.cs == 1 &&
                         unaligned_vec_pays(F, rows16));
-  *pp = plan_reduce(a, aligned, rows16, words && g.cs == 1, num_cus_current());
+  *pp = plan_reduce(a, aligned, rows16, words && g.cs == 1, num_cus_current(),
+                    xcd_log2_current());
   if (!query) {
     for (int b = 0; b < nbank; ++b)
       if (!in[b] && !*empty) return fail(BLDP_EINVAL, "null input pointer (bank %d)", b);

@@ -79,7 +79,7 @@ struct RedArgs {
                            // lane path: k_reduce_lanes (lanes along the stitched row)
   int32_t rsplit;          // k_reduce_rows: slices of a workgroup splitting a block's rows (1 = k_reduce_row)
   int32_t st_plain;        // row / il / rowt output stores plain (1) or non-temporal (0)
-  int32_t il_xcd;          // k_reduce_il: contiguous segments per XCD (small launches)
+  int32_t xcd_lg;          // log2 XCDs of the per-XCD tile order (xcd_order), 0 = off
   float div;               // F*T, the mean divisor
 };
 
@@ -124,7 +124,8 @@ struct Plan {
 // `rows16` whether every bank pointer is 16-byte aligned and the IF/time
 // pitches are multiples of 4 floats (any channel offset and step); `words`
 // whether the channel step is 1 and every bank pointer is dword-aligned.
-Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus);
+// xcd_lg: log2 of the device's XCD count (0: one XCD, or not a power of two)
+Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus, int xcd_lg);
 
 hipError_t launch_reduce(const RedArgs &a, const Plan &p, int op, hipStream_t s);
 // events the next launch_reduce's dispatches carry (null, null: none)

@@ -165,46 +165,54 @@ constexpr unsigned kRowShm = 0, kRowtShm = 0, kVecShm = 0;
 // (round 5, profiles/r05/ab_narrow_r05q.json; 14 waves per CU, half the
 // cycles parked on loads: cfg3f1_sq_summary_r05p.json).
 constexpr unsigned kNarrowShm = 0;
-// k_reduce_tile in the per-XCD order: off (round 5 A/B,
-// profiles/r05/ab_tilexcd_r05ar.json: 0.94-1.035 by shape).  k_reduce_narrowt
-// at F = 2 in that order (ab_narrowtxcd_r05ar.json, ab_narrowtxcd_r05as.json:
-// the 0000 band at T = 1 / 2 / 4 0.93 / 0.96 / 0.94, the 0001 band T = 1 0.92,
-// the 0002 shapes within +-1.4%; F = 1 mixed, 1.05 on the 0000 band at T = 2,
-// so F = 1 keeps the dispatcher's order; on a second box the 0002 band at
-// F = 2 T = 1 lost 4%, so launches under kRowtXcdBytes keep it too:
-// ab_narrowtxcd_confirm_r05at.json).
-constexpr bool kTileXcd = false, kNarrowtXcd = true;
-// k_reduce_wavet in the per-XCD order: off (round 5 A/B,
-// profiles/r05/ab_wavetxcd_r05aw.json: the 0001 band at F = 512 1.03-1.045)
-constexpr bool kWavetXcd = false;
-// k_reduce_rowt in the per-XCD order for launches of at least kRowtXcdBytes
-// whose rows are at least kRowXcdMinPitch apart (round 5 A/B on two boxes,
-// profiles/r05/ab_rowtxcd_r05an.json, ab_rowtxcd_gate_r05ao.json: the 0000
-// band at T = 1, 2 0.95-0.97; the 0001 band (2 KiB rows) mixed, F = 8 T = 1
-// 0.94-0.96 but F = 64 T = 1 1.01-1.05; one 0002 file 1.07-1.13, the 0002
-// band 0.95-1.02)
-constexpr int64_t kRowtXcdBytes = (int64_t)1 << 30;
-// k_reduce_narrow in the per-XCD tile order (round 5 A/B,
-// profiles/r05/ab_narrowxcd_r05am.json: the 0000 band at F = 1, 2 0.975-0.987,
-// one bank 0.979, the 0002 band at F = 1 T = 16 0.93, F = 2 T = 8 0.98)
-constexpr bool kNarrowXcd = true;
-// Interleaved launches whose tiles are at least kIlXcdMinT rows deep and whose
-// rows are at most kIlXcdMaxPitch bytes apart give each XCD a contiguous run
-// of segments (RedArgs::il_xcd).  Round 5 A/B, one box, against the
-// dispatcher's round-robin order (profiles/r05/ab_ilxcd_r05ae.json,
-// ab_ilsmall_r05ad.json; a rebuilt identical library within +-1%):
-//   T = 16: 0002 band (256 KiB rows) 0.90-0.91, one 0002 file 0.93-0.95,
-//   16 / 32 / 128 MiB rows 0.93 / 0.91-0.95 / 0.97, but the 0000 product's
-//   256 MiB rows (cfg3) 1.005-1.022; T = 8: 16 MiB rows 0.95, the 0002 band
-//   1.00; T = 1 / 2 / 4: 1.08 / 1.00 / 1.00 (16 MiB rows), 1.05 / 1.01 / 1.01
-//   (0002 band).
+// The per-XCD contiguous tile order (xcd_order below; RedArgs::xcd_lg): the
+// dispatcher sends workgroup x of a launch to XCD x % 8 on an MI355X in SPX
+// mode, so in launch order every XCD streams every eighth tile, from 8
+// places in each row; in the per-XCD order XCD k takes the k-th contiguous
+// eighth of the tiles.  One rule, xcd_order_pays (plan_reduce), says where it
+// pays; the round 5 A/B on MI355X it rests on (ratios of time, order on /
+// dispatcher order; profiles/r05/ab_*xcd*.json, boxes within +-1.5% of a
+// rebuilt identical library):
+//   k_reduce_il, tiles of >= kIlXcdMinT rows at most kIlXcdMaxPitch apart:
+//     T = 8, 16 on 16-128 MiB rows 0.91-0.97 (ab_ilxcd_r05ae.json,
+//     ab_ilsmall_r05ad.json); the 0000 product's 256 MiB rows (cfg3)
+//     1.005-1.022, so the pitch bound; T = 1, 2, 4 1.00-1.08, so the depth
+//     bound;
+//   k_reduce_row / rows (tpb = 1), rows at least kRowXcdMinPitch apart, T >= 8:
+//     16 MiB rows at F = 64 / 256 0.77 / 0.76, but 256 KiB rows (the 0002 band)
+//     1.03 and 2 KiB rows (the 0001 band) 1.02 (ab_rowxcd_r05ag.json);
+//   k_reduce_rowt (tpb > 1), launches >= kRowtXcdBytes, rows >= kRowXcdMinPitch
+//     apart: the 0000 band at T = 1, 2 0.95-0.97; smaller launches mixed, one
+//     0002 file 1.07-1.13 (ab_rowtxcd_r05an.json, ab_rowtxcd_gate_r05ao.json);
+//   k_reduce_narrowt at F = 2 on launches >= kRowtXcdBytes: the 0000 band at
+//     T = 1 / 2 / 4 0.93 / 0.96 / 0.94; F = 1 mixed, and the 0002 band at F = 2
+//     T = 1 lost 4% on a second box (ab_narrowtxcd_r05ar.json, _r05as.json,
+//     ab_narrowtxcd_confirm_r05at.json);
+//   k_reduce_narrow, k_reduce_vec: always (the 0000 band at F = 1, 2
+//     0.975-0.987, ab_narrowxcd_r05am.json; the 0001 band at F = 64 T = 16
+//     0.963, cfg4 0.992, ab_vecxcd_r05ak.json);
+//   k_reduce_tile 0.94-1.035 by shape, k_reduce_wavet 1.03-1.045
+//     (ab_tilexcd_r05ar.json, ab_wavetxcd_r05aw.json), and the kurtosis and
+//     typed kernels (ab_kregsxcd_r05ai, ab_kmidxcd_r05ah, ab_kleafxcd_r05am,
+//     ab_typedxcd_r05an: 0.97-1.08): never (round 6: their branches removed;
+//     tools/ab_variants.py re-creates the reduce ones by patching the rule).
+// Only on a device whose XCD count is a power of two (hipDeviceAttribute-
+// NumberOfXccs: 8 in SPX mode, 4 / 2 / 1 in the DPX / QPX / CPX partitions,
+// where the order spreads over that many XCDs; the bounds were measured in SPX).
 constexpr int kIlXcdMinT = 8;
-// The same order for k_reduce_row / k_reduce_rows, only for rows at least
-// kRowXcdMinPitch apart (round 5 A/B, profiles/r05/ab_rowxcd_r05ag.json:
-// 16 MiB rows at F = 64 / 256, T = 16 0.77 / 0.76; but the 0002 band (256 KiB
-// rows) 1.03, one 0002 file 1.12, the 0001 band (2 KiB rows) 1.02).
 constexpr int64_t kRowXcdMinPitch = (int64_t)4 << 20;
 constexpr int64_t kIlXcdMaxPitch = (int64_t)128 << 20;
+constexpr int64_t kRowtXcdBytes = (int64_t)1 << 30;
+
+// Workgroup x of a launch of X in the per-XCD contiguous order over 2^lg
+// XCDs: x runs on XCD x % 2^lg and takes tile (x % 2^lg) * (X / 2^lg) +
+// x / 2^lg.  lg = 0 (the plan's "no"), or a grid 2^lg does not divide: x.
+__device__ __forceinline__ uint32_t xcd_order(uint32_t x, uint32_t X, int lg) {
+  const uint32_t m = (1u << lg) - 1u;
+  if (lg == 0 || (X & m)) return x;
+  return (x & m) * (X >> lg) + (x >> lg);
+}
+
 // The short-time-block kernels (k_reduce_rowt, k_reduce_narrowt,
 // k_reduce_lanet) also take tavby = 3 and 8, not only 1, 2, 4 (plan option
 // "t38"; the 512-channel 0001 product at tavby = 3 ran one 3-row block per
@@ -482,12 +490,8 @@ template <int OP, int F, int T, int NRW>
 __global__ __launch_bounds__(kBlock) void k_reduce_narrowt(const RedArgs a) {
   constexpr int TPB = NRW / T, NR = TPB * T;
   const int tid = threadIdx.x;
-  uint32_t bx = blockIdx.x;
+  const uint32_t bx = xcd_order(blockIdx.x, gridDim.x, a.xcd_lg);
   const uint32_t bc = (uint32_t)a.blocks_c;
-  if (F == 2 && a.il_xcd) {  // the per-XCD contiguous order of k_reduce_il (>= 1 GiB launches)
-    const uint32_t X = gridDim.x;
-    if ((X & 7) == 0) bx = (bx & 7) * (X >> 3) + (bx >> 3);
-  }
   const int sh = a.tsub_log2, cw = kBlock >> sh;
   const uint32_t tq = bx / bc, i = blockIdx.y;
   const int64_t tg = ((int64_t)tq << sh) + (tid >> (8 - sh));
@@ -1070,18 +1074,11 @@ __device__ __forceinline__ void tile_tile(const RedArgs &a, int64_t tile) {
 }
 
 // Grid-stride wrappers: one tile per workgroup when the grid covers every
-// tile, several when a launch has more tiles than INT32_MAX workgroups.
-// kVecXcd: the first tile of workgroup x in the per-XCD contiguous order of
-// k_reduce_il (round 5 A/B, profiles/r05/ab_vecxcd_r05ak.json: the 0001 band
-// at F = 64 T = 16 0.963, cfg4 0.992, every other main shape within +-1%).
-constexpr bool kVecXcd = true;
+// tile, several when a launch has more tiles than INT32_MAX workgroups; the
+// first tile of a workgroup in the per-XCD order where the plan chose it.
 template <int OP, int LPG, int K4C>
 __global__ __launch_bounds__(kBlock) void k_reduce_vec(const RedArgs a) {
-  int64_t t0 = blockIdx.x;
-  if constexpr (kVecXcd) {
-    const int64_t G = gridDim.x;
-    if ((G & 7) == 0) t0 = (t0 & 7) * (G >> 3) + (t0 >> 3);
-  }
+  const int64_t t0 = xcd_order(blockIdx.x, gridDim.x, a.xcd_lg);
   for (int64_t t = t0; t < a.ntiles; t += gridDim.x) vec_tile<OP, LPG, K4C>(a, t);
 }
 
@@ -1198,18 +1195,10 @@ __device__ __forceinline__ void il_tile(const RedArgs &a, int64_t bx, uint32_t i
   }
 }
 
-// a.il_xcd (deep tiles of rows up to 128 MiB apart, see kIlXcdMinT): workgroup x, which the
-// dispatcher sends to XCD x % 8, takes segment (x % 8) * X/8 + x / 8, so each
-// XCD streams one contiguous eighth of a row of segments instead of every
-// eighth segment.
 template <int OP, int K4, int GPW>
 __global__ __launch_bounds__(kBlock) void k_reduce_il(const RedArgs a) {
-  uint32_t x = blockIdx.x;
-  if (a.il_xcd) {
-    const uint32_t X = gridDim.x;
-    if ((X & 7) == 0) x = (x & 7) * (X >> 3) + (x >> 3);
-  }
-  il_tile<OP, K4, GPW, kIlInflight>(a, x, blockIdx.y, blockIdx.z);
+  il_tile<OP, K4, GPW, kIlInflight>(a, xcd_order(blockIdx.x, gridDim.x, a.xcd_lg), blockIdx.y,
+                                    blockIdx.z);
 }
 
 // Vector path, small groups (PATH_VEC_ROW): F = 4*G4 channels with G4 = 1..64
@@ -1227,16 +1216,6 @@ __global__ __launch_bounds__(kBlock) void k_reduce_il(const RedArgs a) {
 // CU in flight is faster on the 0002 shapes (A/B against uncapped /
 // k_reduce_vec: cfg1 5.85 vs 5.59 / 5.43 TB/s, cfg2 6.18 vs 5.78 / 6.10).
 constexpr int kRowBatch = 16;
-// The column block of a workgroup: blockIdx.x, or with a.il_xcd the per-XCD
-// contiguous order k_reduce_il uses (workgroup x runs on XCD x % 8).
-__device__ __forceinline__ uint32_t xcd_block(const RedArgs &a) {
-  uint32_t x = blockIdx.x;
-  if (a.il_xcd) {
-    const uint32_t X = gridDim.x;
-    if ((X & 7) == 0) x = (x & 7) * (X >> 3) + (x >> 3);
-  }
-  return x;
-}
 template <int OP, int G4>
 __global__ __launch_bounds__(kBlock)
 __attribute__((amdgpu_waves_per_eu(1, kRowMaxWaves)))
@@ -1245,7 +1224,7 @@ void k_reduce_row(const RedArgs a) {
   const uint32_t it = blockIdx.y, ni = (uint32_t)a.ni;
   const uint32_t to = it / ni, i = it - to * ni;
   const int bank = blockIdx.z;
-  const int64_t col = (int64_t)xcd_block(a) * kBlock + tid;  // float4 column of the window
+  const int64_t col = (int64_t)xcd_order(blockIdx.x, gridDim.x, a.xcd_lg) * kBlock + tid;  // float4 column of the window
   const bool valid = col < a.nco * G4;
   const float id = R<OP>::id();
   float4 acc[kNacc];
@@ -1295,7 +1274,7 @@ void k_reduce_rows(const RedArgs a) {
   const uint32_t it = blockIdx.y, ni = (uint32_t)a.ni;
   const uint32_t to = it / ni, i = it - to * ni;
   const int bank = blockIdx.z;
-  const int64_t col = (int64_t)xcd_block(a) * CW + c;  // float4 column of the window
+  const int64_t col = (int64_t)xcd_order(blockIdx.x, gridDim.x, a.xcd_lg) * CW + c;  // float4 column of the window
   const bool valid = col < a.nco * G4;
   const float id = R<OP>::id();
   float4 acc[NA];
@@ -1375,12 +1354,8 @@ void k_reduce_rowt(const RedArgs a) {
   // With a.bpack the 2^tsub_log2 lane sets take 2^tsub_log2 consecutive banks
   // of one time group instead (grid z = bank sets): a stitched product's rows
   // then get whole segments of 2^tsub_log2 banks' outputs (below).
-  uint32_t bx = blockIdx.x;
+  const uint32_t bx = xcd_order(blockIdx.x, gridDim.x, a.xcd_lg);
   const uint32_t bc = (uint32_t)a.blocks_c;
-  if (a.il_xcd) {  // the per-XCD contiguous order of k_reduce_il (launches >= kRowtXcdBytes)
-    const uint32_t X = gridDim.x;
-    if ((X & 7) == 0) bx = (bx & 7) * (X >> 3) + (bx >> 3);
-  }
   const int sh = a.tsub_log2, cw = kBlock >> sh, sub = threadIdx.x >> (8 - sh);  // (kBlock = 256)
   constexpr bool bp = BP;  // (a.bpack: a template form, so the time-group form pays nothing)
   const uint32_t tq = bx / bc, i = blockIdx.y;
@@ -1509,11 +1484,7 @@ __global__ __launch_bounds__(BP ? 1024 : kBlock) void k_reduce_wavet(const RedAr
   // K4 >= 8 always the latter
   constexpr int RB = (K4 == 2 || K4 == 4) ? (K4 >= kBatch ? 1 : kBatch / K4) : 0;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int64_t bx = blockIdx.x;
-  if constexpr (kWavetXcd) {  // the per-XCD contiguous order of k_reduce_il
-    const int64_t X = gridDim.x;
-    if ((X & 7) == 0) bx = (bx & 7) * (X >> 3) + (bx >> 3);
-  }
+  const int64_t bx = xcd_order(blockIdx.x, gridDim.x, a.xcd_lg);
   const int64_t g = BP ? wave % a.nco : bx % a.nco, chunk = BP ? bx : bx / a.nco;
   const int64_t i = blockIdx.y;
   const int bank = BP ? (int)(wave / a.nco) : (int)blockIdx.z;
@@ -1580,11 +1551,7 @@ __global__ __launch_bounds__(BP ? 1024 : kBlock) void k_reduce_wavet(const RedAr
 
 template <int OP, int F>
 __global__ __launch_bounds__(kBlock) void k_reduce_narrow(const RedArgs a) {
-  int64_t t0 = blockIdx.x;
-  if constexpr (kNarrowXcd) {  // the per-XCD contiguous order of k_reduce_il
-    const int64_t G = gridDim.x;
-    if ((G & 7) == 0) t0 = (t0 & 7) * (G >> 3) + (t0 >> 3);
-  }
+  const int64_t t0 = xcd_order(blockIdx.x, gridDim.x, a.xcd_lg);
   for (int64_t t = t0; t < a.ntiles; t += gridDim.x) narrow_tile<OP, F>(a, t);
 }
 template <int OP, int F>
@@ -1606,11 +1573,7 @@ template <int OP, bool CS1>
 __global__ __launch_bounds__(kBlock)
 __attribute__((amdgpu_waves_per_eu(1, kTileMaxWaves)))
 void k_reduce_tile(const RedArgs a) {
-  int64_t t0 = blockIdx.x;
-  if constexpr (kTileXcd) {  // the per-XCD contiguous order of k_reduce_il
-    const int64_t G = gridDim.x;
-    if ((G & 7) == 0) t0 = (t0 & 7) * (G >> 3) + (t0 >> 3);
-  }
+  const int64_t t0 = xcd_order(blockIdx.x, gridDim.x, a.xcd_lg);
   for (int64_t t = t0; t < a.ntiles; t += gridDim.x) tile_tile<OP, CS1>(a, t);
 }
 
@@ -2091,7 +2054,27 @@ void plan_opt_domain(int k, int64_t *lo, int64_t *hi) {
 }
 void plan_opt_set(int k, int64_t v) { g_plan_opt.v[k].store(v, std::memory_order_relaxed); }
 
-Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus) {
+// Where the per-XCD tile order pays (the rule and its measurements: the
+// comment above kIlXcdMinT).  `bytes`: the launch's algorithmic traffic.
+bool xcd_order_pays(int path, const RedArgs &a, int64_t F, int64_t T, int64_t bytes) {
+  const int64_t pitch = 4 * a.in_ld_t;  // bytes between a column's rows
+  switch (path) {
+    case PATH_VEC_IL: return T >= kIlXcdMinT && pitch <= kIlXcdMaxPitch;
+    case PATH_VEC_ROW:
+      if (a.tpb > 1) return bytes >= kRowtXcdBytes && pitch >= kRowXcdMinPitch;  // rowt
+      return T >= kIlXcdMinT && pitch >= kRowXcdMinPitch && pitch <= kIlXcdMaxPitch;  // row(s)
+    case PATH_NARROW:
+      if (a.tpb > 1) return F == 2 && bytes >= kRowtXcdBytes;  // narrowt
+      return true;  // narrow
+    case PATH_VEC:
+      if (a.tpb > 1) return false;  // wavet
+      return true;  // vec
+    case PATH_TILE: return false;
+    default: return false;
+  }
+}
+
+Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus, int xcd_lg) {
   Plan p{};
   const int64_t F = a.F, T = a.T;
   p.nout = a.nco * a.ni * a.nto;
@@ -2385,13 +2368,7 @@ Plan plan_reduce(RedArgs &a, bool aligned, bool rows16, bool words, int num_cus)
     const int64_t bytes = 4 * a.nbank * a.ni * (a.nco * F * a.nto * T + a.nco * a.nto);
     const int64_t o = opt(OPT_ST_PLAIN);
     a.st_plain = o == 2 ? 1 : o == 0 ? 0 : (bytes < ((int64_t)2 << 30) ? 1 : 0);
-    const bool row_xcd = p.path == PATH_VEC_ROW && a.tpb == 1 && 4 * a.in_ld_t >= kRowXcdMinPitch;
-    a.il_xcd = ((p.path == PATH_VEC_IL || row_xcd) && T >= kIlXcdMinT &&
-                4 * a.in_ld_t <= kIlXcdMaxPitch) ||
-               (p.path == PATH_VEC_ROW && a.tpb > 1 && bytes >= kRowtXcdBytes &&
-                4 * a.in_ld_t >= kRowXcdMinPitch) ||
-               (kNarrowtXcd && p.path == PATH_NARROW && a.tpb > 1 && F == 2 &&
-                bytes >= kRowtXcdBytes);
+    a.xcd_lg = xcd_order_pays(p.path, a, F, T, bytes) ? xcd_lg : 0;
   }
   a.div = (float)(F * T);
   return p;

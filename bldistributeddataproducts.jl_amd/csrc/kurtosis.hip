@@ -167,19 +167,11 @@ __device__ __forceinline__ double kurt_ratio(int64_t nt, float S, double ma, dou
 // wave's 256 Float64 results go through LDS so every nt store instruction
 // writes 1 KiB contiguous (+2.5% on the 0000 band against each lane's 32 B as
 // two nt 16-byte stores).
-// k_kurt_regs in the per-XCD contiguous tile order of k_reduce_il: off
-// (round 5 A/B, profiles/r05/ab_kregsxcd_r05ai.json: the 0000 band 0.98-1.005,
-// one bank 0.97, inside the control's +-1.5% but one shape)
-constexpr bool kRegsXcd = false;
 template <int NTMAX, bool EXACT>
 __global__ __launch_bounds__(kB) void k_kurt_regs(const KurtArgs k) {
   const int64_t ncols = k.nc / 4;
   const int64_t ctiles = (ncols + kB - 1) / kB;
-  int64_t b = blockIdx.x;
-  if constexpr (kRegsXcd) {  // workgroup b runs on XCD b % 8: a contiguous run per XCD
-    const int64_t G = gridDim.x;
-    if ((G & 7) == 0) b = (b & 7) * (G >> 3) + (b >> 3);
-  }
+  const int64_t b = blockIdx.x;
   const int64_t ib = b / ctiles, col = (b % ctiles) * kB + threadIdx.x;
   if (col >= ncols) return;
   const int bank = (int)(ib / k.ni);
@@ -324,10 +316,6 @@ __global__ __launch_bounds__(kB) void k_kurt_mid(const KurtArgs k) {
 // 1.34 / 1.22 / 1.04x; nt >= 100 and one file no gain).  kMidNW waves per
 // workgroup otherwise (4 and 16 measured and lost).
 constexpr int kMidNW = 8;
-// k_kurt_mid2 in the per-XCD contiguous tile order of k_reduce_il: off
-// (round 5 A/B, profiles/r05/ab_kmidxcd_r05ah.json: the 0002 band 1.01-1.02,
-// one file 1.006, a window 4 channels in 0.87)
-constexpr bool kMidXcd = false;
 template <int NR, int NW>
 __global__ __launch_bounds__(64 * NW) void k_kurt_mid2(const KurtArgs k) {
   constexpr int TW = 128;  // channels per tile
@@ -336,11 +324,7 @@ __global__ __launch_bounds__(64 * NW) void k_kurt_mid2(const KurtArgs k) {
   // an exec-mask save/restore per spectrum
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t ctiles = (k.nc + TW - 1) / TW;
-  int64_t b = blockIdx.x;
-  if constexpr (kMidXcd) {  // workgroup b runs on XCD b % 8: give each XCD a contiguous run
-    const int64_t G = gridDim.x;
-    if ((G & 7) == 0) b = (b & 7) * (G >> 3) + (b >> 3);
-  }
+  const int64_t b = blockIdx.x;
   const int64_t ib = b / ctiles, c = (b % ctiles) * TW + 2 * lane;
   const bool valid = c < k.nc;  // (nc even: c + 1 < nc too)
   const int bank = (int)(ib / k.ni);
@@ -436,9 +420,6 @@ __global__ __launch_bounds__(64 * NW) void k_kurt_mid2(const KurtArgs k) {
 // products (0001: 512 channels, nt = 513..8192 had 32-128 waves on the chip);
 // 0 = never.  Each channel's arithmetic is unchanged.
 constexpr int kLeafB = 4, kLeafW = 4, kLeafNB = 16;
-// k_kurt_leaf in the per-XCD workgroup order: off (round 5 A/B,
-// profiles/r05/ab_kleafxcd_r05am.json: cfg4 1.006, 2048 spectra 0.987)
-constexpr bool kLeafXcd = false;
 
 template <int W>
 __device__ __forceinline__ void ldw(const float *p, float (&x)[W]) {
@@ -513,12 +494,7 @@ __device__ __forceinline__ void leaf_store(const KurtArgs &k, const LeafAcc<W> &
 template <int W, int B>
 __global__ __launch_bounds__(kB) void k_kurt_leaf(const KurtArgs k) {
   const int lane = threadIdx.x & 63;
-  int64_t bx = blockIdx.x;
-  if constexpr (kLeafXcd) {  // the per-XCD contiguous order of k_reduce_il
-    const int64_t G = gridDim.x;
-    if ((G & 7) == 0) bx = (bx & 7) * (G >> 3) + (bx >> 3);
-  }
-  const int64_t u = bx * 4 + (threadIdx.x >> 6);
+  const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t seg = u % k.nseg, r = u / k.nseg;
   const int64_t slot = r % k.nslot, row = r / k.nslot;
   const int64_t col = seg * 64 + lane;

@@ -359,20 +359,13 @@ __global__ __launch_bounds__(256) void k_reduce_typed_vec(const TypedArgs a, int
 // row): the rows of the workgroup's tpb blocks (tpb * T <= 16) are loaded in
 // one batch, then folded into blocks, so a lane waits for memory once per
 // workgroup instead of once per block.
-// k_reduce_typed_vec16 in the per-XCD workgroup order: off (round 5 A/B,
-// profiles/r05/ab_typedxcd_r05an.json: 1.02-1.08 on every typed shape)
-constexpr bool kTypedXcd = false;
 template <typename TI, int OP, int NR>
 __global__ __launch_bounds__(256) void k_reduce_typed_vec16(const TypedArgs a, int lpg, int tpb,
                                                             int64_t nct) {
   typedef Vec16<TI, OP> V;
   typedef typename V::R R;
   const int tid = threadIdx.x;
-  int64_t bx = blockIdx.x;
-  if constexpr (kTypedXcd) {  // the per-XCD contiguous order of k_reduce_il
-    const int64_t X = gridDim.x;
-    if ((X & 7) == 0) bx = (bx & 7) * (X >> 3) + (bx >> 3);
-  }
+  const int64_t bx = blockIdx.x;
   const int64_t ct = bx % nct, tg = bx / nct;
   const int64_t co = ct * (256 / lpg) + tid / lpg;
   const int j = tid % lpg;
@@ -610,12 +603,17 @@ __global__ __launch_bounds__(1024) void k_kurt_i8(const TypedArgs a, const KTM m
     const char *p = static_cast<const char *>(a.in[bank]) + a.in_off + i * a.in_ld_i + 4 * q;
     for (int64_t t = t0; t < t1; t += U) {
       const int cnt = (int)min((int64_t)U, t1 - t);
+      // every load issued before the first is waited on: a short batch
+      // re-reads its last spectrum (in bounds) and replaces the extra words
+      // by d = 0 with a select, not a branch around each load
       uint32_t w[U];
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        w[u] = u < cnt ? __builtin_nontemporal_load(
-                             reinterpret_cast<const uint32_t *>(p + (t + u) * ldb))
-                       : (SIGNED ? 0u : 0x80808080u);  // (d = 0: adds nothing)
+        w[u] = __builtin_nontemporal_load(
+            reinterpret_cast<const uint32_t *>(p + (t + min(u, cnt - 1)) * ldb));
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (u >= cnt) w[u] = SIGNED ? 0u : 0x80808080u;  // (d = 0: adds nothing)
       int32_t b3[4] = {0, 0, 0, 0};
 #pragma unroll
       for (int h = 0; h < U; h += 8) {

@@ -168,18 +168,18 @@ VARIANTS = {
     "rowto2": {"patch": [RS(rowt=65536)]},
     "rowto4": {"patch": [RS(rowt=36864)]},
     "ctl": {"patch": []},  # the base sources rebuilt: the harness's own spread
-    # per-XCD segment order of k_reduce_il (round 5): off, or on everywhere
-    "tilexcd": {"patch": [(K, "constexpr bool kTileXcd = false,", "constexpr bool kTileXcd = true,")]},
-    "wavetxcd": {"patch": [(K, "constexpr bool kWavetXcd = false;", "constexpr bool kWavetXcd = true;")]},
-    "narrowtxcdoff": {"patch": [(K, "kNarrowtXcd = true;", "kNarrowtXcd = false;")]},
+    # the per-XCD tile order (round 5 measurements; round 6: one rule,
+    # kernels.hip xcd_order_pays, which these patch; the kurtosis / typed
+    # forms, measured losers, were removed from the sources)
+    "tilexcd": {"patch": [(K, "    case PATH_TILE: return false;", "    case PATH_TILE: return true;")]},
+    "wavetxcd": {"patch": [(K, "      if (a.tpb > 1) return false;  // wavet",
+                            "      if (a.tpb > 1) return true;  // wavet")]},
+    "narrowtxcdoff": {"patch": [(K, "      if (a.tpb > 1) return F == 2 && bytes >= kRowtXcdBytes;  // narrowt",
+                                 "      if (a.tpb > 1) return false;  // narrowt")]},
     "rowtxcdoff": {"patch": [(K, "constexpr int64_t kRowtXcdBytes = (int64_t)1 << 30;",
                               "constexpr int64_t kRowtXcdBytes = INT64_MAX;")]},
-    "typedxcd": {"patch": [("typed.hip", "constexpr bool kTypedXcd = false;", "constexpr bool kTypedXcd = true;")]},
-    "narrowxcdoff": {"patch": [(K, "constexpr bool kNarrowXcd = true;", "constexpr bool kNarrowXcd = false;")]},
-    "kleafxcd": {"patch": [(KU, "constexpr bool kLeafXcd = false;", "constexpr bool kLeafXcd = true;")]},
-    "vecxcdoff": {"patch": [(K, "constexpr bool kVecXcd = true;", "constexpr bool kVecXcd = false;")]},
-    "kregsxcd": {"patch": [(KU, "constexpr bool kRegsXcd = false;", "constexpr bool kRegsXcd = true;")]},
-    "kmidxcd": {"patch": [(KU, "constexpr bool kMidXcd = false;", "constexpr bool kMidXcd = true;")]},
+    "narrowxcdoff": {"patch": [(K, "      return true;  // narrow", "      return false;  // narrow")]},
+    "vecxcdoff": {"patch": [(K, "      return true;  // vec", "      return false;  // vec")]},
     "rowxcdoff": {"patch": [(K, "constexpr int64_t kRowXcdMinPitch = (int64_t)4 << 20;",
                              "constexpr int64_t kRowXcdMinPitch = INT64_MAX;")]},
     "ilxcdoff": {"patch": [(K, "constexpr int kIlXcdMinT = 8;", "constexpr int kIlXcdMinT = 1 << 30;")]},
