@@ -314,7 +314,11 @@ std::shared_ptr<DevIO> dev_io(std::unique_lock<std::mutex> &call) {
         // on that node too (ensure_slots), stay on the GPU's socket
         cpu_set_t cpus;
         const char *aff = getenv("BLDP_READ_AFFINITY");
-        const bool pin = !(aff && atoi(aff) == 0) && device_node_cpus(dev, &cpus);
+        // (only where that node has at least half as many allowed CPUs as
+        // there are readers: 16 readers on the 1-2 node CPUs of a cpuset that
+        // spans sockets would crowd them)
+        const bool pin = !(aff && atoi(aff) == 0) && device_node_cpus(dev, &cpus) &&
+                         2 * CPU_COUNT(&cpus) >= n;
         slot->pool.reset(new ReadPool(n, pin ? &cpus : nullptr));
         slot->node_pinned = pin;
         slot->node = device_numa_node(dev);
@@ -373,14 +377,22 @@ int ensure_slots(Slots &sl, int64_t bytes, int nslot, int node = -1) {
   if (sl.bytes == bytes && (int)sl.p.size() == nslot) return BLDP_OK;
   free_slots(sl);
   const char *e = getenv("BLDP_SLOT_NUMA");
-  const bool numa = node >= 0 && node < 64 && !(e && atoi(e) == 0);
+  bool numa = node >= 0 && node < 64 && !(e && atoi(e) == 0);
   constexpr int kMpolDefault = 0, kMpolPreferred = 1;  // <numaif.h>, no libnuma
+  // only a thread on the default policy is switched (and switched back to
+  // it): a caller's own policy (numactl --membind / --interleave, or one it
+  // set) stays in force and places the slots itself
+  int prev_mode = -1;
+  unsigned long prev_mask[16] = {0};
+  if (numa && (syscall(SYS_get_mempolicy, &prev_mode, prev_mask, 16 * 64, nullptr, 0) != 0 ||
+               prev_mode != kMpolDefault))
+    numa = false;
   unsigned long mask = 1ul << (node >= 0 && node < 64 ? node : 0);
   if (numa && syscall(SYS_set_mempolicy, kMpolPreferred, &mask, 64) != 0) mask = 0;
   struct Restore {
     bool on;
     ~Restore() {
-      if (on) (void)syscall(SYS_set_mempolicy, kMpolDefault, nullptr, 0);
+      if (on) (void)syscall(SYS_set_mempolicy, kMpolDefault, nullptr, 0);  // (was default)
     }
   } restore{numa && mask};
   const unsigned flags = restore.on ? hipHostMallocNumaUser : hipHostMallocDefault;
@@ -503,6 +515,10 @@ static int chunks_to_device(
     if (io->slots.p.size() < 2 || io->slots.bytes < span) {
       int nring = kRingSlots;  // (BLDP_RING_SLOTS: a probe knob, 2..16)
       if (const char *e = getenv("BLDP_RING_SLOTS")) nring = std::min(16, std::max(2, atoi(e)));
+      // a batch larger than a ring slot (one big unfiltered chunk): two slots
+      // of its size, released when the call returns (the ring
+      // stays bounded between calls whatever the chunk size)
+      if (span > kRingSlotBytes) nring = 2;
       const int rc = ensure_slots(io->slots, std::max(kRingSlotBytes, (span + (1 << 20) - 1) &
                                                                           ~(int64_t)((1 << 20) - 1)),
                                   nring, io->node);
@@ -598,6 +614,7 @@ static int chunks_to_device(
         rc = bldp::set_error(BLDP_EHIP, "chunks_to_device: copy failed");
       (void)hipEventDestroy(ev);
     }
+  if (ring && io->slots.bytes > kRingSlotBytes) free_slots(io->slots);  // (oversized batches)
   if (stats) {
     stats[0] = t_first;
     stats[1] = t_reads;

@@ -386,16 +386,20 @@ BLDP_API int bldp_bslz4_error(const int *err_dev, void *stream);
  * file_off[k] of the open file `fd`; 0 bytes = never written) is read with
  * parallel preads (a persistent pool of reader threads per device: 16, or 4
  * fewer than the process's CPU quota when that is less, BLDP_READ_THREADS
- * overrides; they run on the CPUs of the GPU's NUMA node and the pinned slots
- * are placed on that node, BLDP_READ_AFFINITY=0 / BLDP_SLOT_NUMA=0 undo that)
+ * overrides; they run on the CPUs of the GPU's NUMA node when the caller may
+ * use at least half as many CPUs there, and the pinned slots are placed on
+ * that node unless the calling thread has a memory policy of its own,
+ * BLDP_READ_AFFINITY=0 / BLDP_SLOT_NUMA=0 undo that)
  * into host_pinned + stage_off[k] (both staging buffers hold stage_bytes;
  * dev_out holds out_bytes: every table entry is checked against them before
  * anything is read).  host_pinned NULL (since ABI 4): the reads are staged
  * through the device's library-owned pinned slot ring instead (the one
- * bldp_runs_to_device uses, 8 x 32 MiB unless a batch's staged range needs
- * larger slots), batch b in slot b % nslot once that slot's previous copy is
- * done, so pinned host memory stays bounded whatever the window's size; the
- * call then also waits for its last copy before returning.
+ * bldp_runs_to_device uses, 8 x 32 MiB; a batch whose staged range is larger
+ * takes 2 slots of that size, released when the call returns), batch b in
+ * slot b % nslot once that slot's previous copy is done, so pinned host memory
+ * stays bounded whatever the window's size: 256 MiB between calls, at most
+ * 2 x the largest batch during one; the call then also waits for its last
+ * copy before returning.
  * Chunks [batch_end[b-1], batch_end[b]) form
  * batch b: once its reads land, its staged byte range is copied to dev_stage
  * (same offsets) on copy_stream, `stream` waits for that copy, and the batch's
