@@ -620,68 +620,84 @@ def rendezvous_check(args, dist, rank, world):
 
 
 def bench_typed(args, eng, torch, pkg):
-    """fqav on 8-bit SIGPROC data (the reference's UInt8 arrays, Blio nbits 8;
-    src/gbtworkerfunctions.jl:173-174) at the 0002 geometry: one file (65536
-    ch x 1 IF x 279 spectra) and the 8-file band, fqavby=64, sum (UInt64
-    results).  GB/s of input bytes; kernel time from HIP events over
-    back-to-back launches (rocprofv3 gives the per-launch figure)."""
+    """fqav and getkurtosis on 8-bit SIGPROC data (the reference's UInt8
+    arrays, Blio nbits 8; src/gbtworkerfunctions.jl:173-174,197-202) at the
+    0002 geometry: one file (65536 ch x 1 IF x 279 spectra) and the 8-file
+    band, fqavby=64, sum (UInt64 results), and the kurtosis of the same data.
+    Each call is prepared once per buffer (bldp_reduce_prepare /
+    bldp_kurtosis_prepare: one ctypes call and the launch, as a worker
+    re-reducing resident buffers pays) and the calls rotate over copies of
+    the input (>= 1 GiB, cold: none in cache from the call before).  Per call:
+    the GPU time of K back-to-back calls (HIP events), the kernel time alone
+    (events on each launch), and the unprepared Python call (engine.reduce /
+    engine.kurtosis) for comparison."""
     import numpy as np
 
     rng = np.random.default_rng(0)
     out = {}
+    HipEvent = pkg._lib.HipEvent
+    sp = int(torch.cuda.current_stream().cuda_stream)
     for label, nb in (("0002 file", 1), ("0002 band", 8)):
         a = rng.integers(0, 256, (279, 1, 65536 * nb), dtype=np.uint8)  # C order [t][i][c]
         ncopy = cold_copies(args.cache, a.nbytes)  # cold: calls rotate over >= 1 GiB of copies
         xs = [torch.from_numpy(a).cuda().permute(2, 1, 0)  # Julia-order (65536*nb, 1, 279)
               for _ in range(ncopy)]
-        outs = [eng.fb_empty(65536 * nb // 64, 1, 279, dtype=torch.uint64) for _ in range(ncopy)]
-        x = xs[0]
-        for w in range(max(args.warmup, ncopy)):
-            eng.reduce(xs[w % ncopy], 64, 1, "sum", out=outs[w % ncopy])
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        preps = {"reduce": [eng.PreparedReduce(x, 64, 1, "sum") for x in xs],
+                 "kurtosis": [eng.PreparedKurtosis(x) for x in xs]}
+        calls = {"reduce": lambda x: eng.reduce(x, 64, 1, "sum"),
+                 "kurtosis": lambda x: eng.kurtosis(x)}
+        rec = out[label] = {"input_bytes": int(a.nbytes), "cache": cache_note(ncopy, a.nbytes)}
+        for what, pl in preps.items():
+            for w in range(max(args.warmup, ncopy)):
+                pl[w % ncopy].launch(sp)
+            torch.cuda.synchronize()
+            e0, e1 = HipEvent(timing=True, fence=False), HipEvent(timing=True, fence=False)
+            evs = [(HipEvent(timing=True, fence=False), HipEvent(timing=True, fence=False))
+                   for _ in range(args.steps)]
 
-        def timed(rot):
-            e0.record()
-            for k in range(args.steps):
-                eng.reduce(xs[k % rot], 64, 1, "sum", out=outs[k % rot])
-            e1.record()
-            e1.synchronize()
-            return e0.elapsed_time(e1) / args.steps
+            def timed(rot, fn):
+                e0.record(sp)
+                t0 = time.perf_counter()
+                for k in range(args.steps):
+                    fn(k % rot)
+                host = (time.perf_counter() - t0) / args.steps
+                e1.record(sp)
+                torch.cuda.synchronize()
+                return e0.elapsed_time(e1) / args.steps, host * 1e3
 
-        ms = timed(ncopy)
-        warm_ms = timed(1) if ncopy > 1 else ms
-        nbytes = a.nbytes + 8 * (65536 * nb // 64) * 279
-        out[label] = {"ms_per_call": round(ms, 4), "GBps_in_plus_out": round(nbytes / ms / 1e6, 1),
-                      "input_bytes": int(a.nbytes), "cache": cache_note(ncopy, a.nbytes),
-                      "warm_ms_per_call": round(warm_ms, 4),
-                      "warm_GBps_in_plus_out": round(nbytes / warm_ms / 1e6, 1)}
-        # getkurtosis on the same UInt8 data (Float64 StatsBase per channel row)
-        for _ in range(2):
-            eng.kurtosis(x)
-        torch.cuda.synchronize()
-        e0.record()
-        for _ in range(args.steps):
-            eng.kurtosis(x)
-        e1.record()
-        e1.synchronize()
-        km = e0.elapsed_time(e1) / args.steps
-        out[label]["kurtosis_ms_per_call"] = round(km, 4)
-        out[label]["kurtosis_GBps_of_input"] = round(a.nbytes / km / 1e6, 1)
-    f = out["0002 band"]  # (one file is host-call bound: ~20 us a call, 7 us of kernel)
+            ms, host_ms = timed(ncopy, lambda c: pl[c].launch(sp))
+            warm_ms = timed(1, lambda c: pl[0].launch(sp))[0] if ncopy > 1 else ms
+            for k in range(args.steps):  # the kernel alone: events on each launch
+                pl[k % ncopy].launch_timed(sp, *evs[k])
+            torch.cuda.synchronize()
+            kern = sorted(x.elapsed_time(y) for x, y in evs)[args.steps // 2]
+            py_ms = timed(ncopy, lambda c: calls[what](xs[c]))[0]  # the unprepared Python call
+            nbytes = a.nbytes + (8 * (65536 * nb // 64) * 279 if what == "reduce"
+                                 else 8 * 65536 * nb)
+            rec[what] = {"ms_per_call": round(ms, 4), "kernel_ms": round(kern, 4),
+                         "host_enqueue_ms_per_call": round(host_ms, 4),
+                         "GBps_in_plus_out": round(nbytes / ms / 1e6, 1),
+                         "GBps_of_input": round(a.nbytes / ms / 1e6, 1),
+                         "frac": round(nbytes / ms / 1e6 / HBM_PEAK_GBS, 4),
+                         "warm_ms_per_call": round(warm_ms, 4),
+                         "unprepared_python_ms_per_call": round(py_ms, 4)}
+            for p_ in pl:
+                p_.close()
+    f = out["0002 band"]["reduce"]
     return {"metric": "fqav GB/s on UInt8 SIGPROC data (0002 band geometry, fqavby=64, sum)",
             "value": f["GBps_in_plus_out"], "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": f["ms_per_call"], "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "u8->u64",
             "data": "synthetic uniform 0..255", "config": {"workload": "typed reduce", **out},
             "roofline": {"bound": "hbm", "achieved": f["GBps_in_plus_out"], "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(f["GBps_in_plus_out"] / HBM_PEAK_GBS, 4),
+                         "unit": "GB/s", "frac": f["frac"],
                          "traffic": traffic_from_profile("typed_band", 1),
                          "traffic_source": traffic_from_profile("typed_band", 1, True)[1],
                          "kernel": "k_reduce_typed_vec16 (8-file band, one call per step)",
-                         "cache": f["cache"],
+                         "cache": out["0002 band"]["cache"],
                          "warm": {"ms_per_call": f["warm_ms_per_call"],
-                                  "frac": round(f["warm_GBps_in_plus_out"] / HBM_PEAK_GBS, 4)}}}
+                                  "frac": round(f["GBps_in_plus_out"] * f["ms_per_call"]
+                                                / f["warm_ms_per_call"] / HBM_PEAK_GBS, 4)}}}
 
 
 def verify_band(cfg, eng, torch, dist, banks, mine, nb, run_step, rank, world, use_pg):

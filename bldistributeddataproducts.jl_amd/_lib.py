@@ -21,7 +21,7 @@ KURT_PATHS = {0: "regs", 1: "mid", 2: "leaf", 3: "twopass"}
 
 BLDP_OK, BLDP_EINVAL, BLDP_EDIM, BLDP_EHIP, BLDP_ENOMEM, BLDP_EBOUNDS = 0, -1, -2, -3, -5, -6
 BLDP_ECOMM, BLDP_EIO = -7, -8
-ABI_VERSION = 4
+ABI_VERSION = 5
 BLDP_BAND_STAGED = 1
 BLDP_BAND_PEER_STORE = 2
 BLDP_COMM_ID_BYTES = 128
@@ -73,6 +73,8 @@ SIGNATURES = {
     "bldp_band_reduce_f32": ([I, P, I64, I64, I64, P, I64, I64, I, P, P], I),
     "bldp_band_reduce_prepare_f32": ([I, P, I64, I64, I64, P, I64, I64, I, P, P], I),
     "bldp_reduce_launch": ([P, P], I),
+    "bldp_reduce_prepare": ([I, P, I64, I64, I64, P, I64, I64, I, P, I64, I64, P], I),
+    "bldp_kurtosis_prepare": ([I, P, I64, I64, I64, P, P, P], I),
     "bldp_reduce_launch_timed": ([P, P, P, P], I),
     "bldp_reduce_release": ([P], I),
     "bldp_band_reduce_multi_f32": ([I, P, P, I64, I64, I64, P, I64, I64, I, I, P, ctypes.c_uint],

@@ -477,8 +477,15 @@ int bldp_band_reduce_f32(int nbank, const float *const *in, int64_t nchan, int64
 // but the kernel launch itself (a worker re-reducing the same buffers, bench
 // loops).
 struct bldp_reduce_op {
+  // what a launch runs: a Float32 (band) reduce, a typed reduce, a typed
+  // getkurtosis, a Float32 getkurtosis (bldp_reduce_prepare /
+  // bldp_kurtosis_prepare prepare the last three)
+  enum Kind { F32_REDUCE = 0, TYPED_REDUCE, TYPED_KURT, F32_KURT } kind = F32_REDUCE;
   RedArgs a;
   Plan p;
+  bldp::TypedArgs t;
+  bldp::KurtArgs k;
+  double *kout = nullptr;
   int op;
   int dev;
   bool empty;
@@ -504,6 +511,36 @@ int bldp_band_reduce_prepare_f32(int nbank, const float *const *in, int64_t ncha
   return BLDP_OK;
 }
 
+static int kurt_run(KurtArgs &k, double *out, void *workspace, void *stream);
+
+namespace {
+// Queue a prepared operation of any kind on s.
+int run_prepared(bldp_reduce_op_t h, hipStream_t s) {
+  switch (h->kind) {
+    case bldp_reduce_op::F32_REDUCE: return run_reduce(h->a, h->p, h->op, s);
+    case bldp_reduce_op::TYPED_REDUCE: {
+      const hipError_t e = launch_reduce_typed(h->t, h->op, s);
+      return e == hipSuccess ? BLDP_OK
+                             : fail(BLDP_EHIP, "typed reduce launch: %s", hipGetErrorString(e));
+    }
+    case bldp_reduce_op::TYPED_KURT: {
+      ScratchLease lease;  // time-chunk partial sums (k_kurt_i8), held until queued
+      bldp::TypedArgs t = h->t;
+      if (const size_t wsb = kurtosis_typed_ws_bytes(t)) {
+        const int rc = scratch_lease(s, wsb, &lease);
+        if (rc) return rc;
+        t.ws = lease.ptr;
+      }
+      const hipError_t e = launch_kurtosis_typed(t, h->kout, s);
+      return e == hipSuccess ? BLDP_OK
+                             : fail(BLDP_EHIP, "typed kurtosis launch: %s", hipGetErrorString(e));
+    }
+    case bldp_reduce_op::F32_KURT: return kurt_run(h->k, h->kout, nullptr, s);
+  }
+  return fail(BLDP_EINVAL, "bad prepared operation");
+}
+}  // namespace
+
 int bldp_reduce_launch(bldp_reduce_op_t h, void *stream) {
   if (!h) return fail(BLDP_EINVAL, "null reduce handle");
   if (h->empty) return BLDP_OK;
@@ -511,7 +548,7 @@ int bldp_reduce_launch(bldp_reduce_op_t h, void *stream) {
   if (hipGetDevice(&dev) != hipSuccess || dev != h->dev)
     return fail(BLDP_EINVAL, "reduce handle prepared on device %d, current device %d", h->dev,
                 dev);
-  return run_reduce(h->a, h->p, h->op, (hipStream_t)stream);
+  return run_prepared(h, (hipStream_t)stream);
 }
 
 int bldp_reduce_launch_timed(bldp_reduce_op_t h, void *stream, void *ev_start, void *ev_stop) {
@@ -522,8 +559,16 @@ int bldp_reduce_launch_timed(bldp_reduce_op_t h, void *stream, void *ev_start, v
   if (hipGetDevice(&dev) != hipSuccess || dev != h->dev)
     return fail(BLDP_EINVAL, "reduce handle prepared on device %d, current device %d", h->dev,
                 dev);
+  if (h->kind != bldp_reduce_op::F32_REDUCE) {  // events recorded around the launch
+    if (hipEventRecord((hipEvent_t)ev_start, (hipStream_t)stream) != hipSuccess)
+      return fail(BLDP_EHIP, "hipEventRecord failed");
+    const int rc = run_prepared(h, (hipStream_t)stream);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord((hipEvent_t)ev_stop, (hipStream_t)stream));
+    return BLDP_OK;
+  }
   set_launch_events((hipEvent_t)ev_start, (hipEvent_t)ev_stop);
-  const int rc = run_reduce(h->a, h->p, h->op, (hipStream_t)stream);
+  const int rc = run_prepared(h, (hipStream_t)stream);
   set_launch_events(nullptr, nullptr);
   return rc;
 }
@@ -826,13 +871,14 @@ int bldp_reduce_out_dtype(int dtype, int op) {
   return d;
 }
 
-int bldp_reduce_strided(int dtype, const void *in, int64_t nchan, int64_t nif, int64_t ntime,
-                        const int64_t *win, int64_t fqavby, int64_t tavby, int op, void *out,
-                        int64_t out_ld_i, int64_t out_ld_t, void *stream) {
-  if (dtype == BLDP_DT_F32)
-    return bldp_reduce_strided_f32(static_cast<const float *>(in), nchan, nif, ntime, win, fqavby,
-                                   tavby, op, static_cast<float *>(out), out_ld_i, out_ld_t,
-                                   stream);
+}  // extern "C"
+
+namespace {
+// The TypedArgs of a typed reduce (bldp_reduce_strided's checks); *empty when
+// there is nothing to do.
+int typed_reduce_args(int dtype, const void *in, int64_t nchan, int64_t nif, int64_t ntime,
+                      const int64_t *win, int64_t fqavby, int64_t tavby, int op, void *out,
+                      int64_t out_ld_i, int64_t out_ld_t, TypedArgs *ap, bool *empty) {
   if (!dtype_size(dtype)) return fail(BLDP_EINVAL, "unknown element type %d", dtype);
   if (!valid_op(op)) return fail(BLDP_EINVAL, "unknown op %d (0=sum 1=mean 2=max 3=min)", op);
   Geo g;
@@ -841,7 +887,8 @@ int bldp_reduce_strided(int dtype, const void *in, int64_t nchan, int64_t nif, i
   int64_t F, T;
   rc = resolve_factors(g, fqavby, tavby, &F, &T);
   if (rc) return rc;
-  TypedArgs a{};
+  TypedArgs &a = *ap;
+  a = TypedArgs{};
   a.dtype = dtype;
   a.nbank = 1;
   a.in[0] = in;
@@ -858,23 +905,21 @@ int bldp_reduce_strided(int dtype, const void *in, int64_t nchan, int64_t nif, i
   a.F = F;
   a.T = T;
   a.num_cus = num_cus_current();
-  if (a.nco * a.ni * a.nto == 0) return BLDP_OK;
+  *empty = a.nco * a.ni * a.nto == 0;
+  if (*empty) return BLDP_OK;
   if (!in || !out) return fail(BLDP_EINVAL, "null pointer");
-  hipError_t e = launch_reduce_typed(a, op, (hipStream_t)stream);
-  if (e != hipSuccess) return fail(BLDP_EHIP, "typed reduce launch: %s", hipGetErrorString(e));
   return BLDP_OK;
 }
 
-int bldp_kurtosis(int dtype, const void *in, int64_t nchan, int64_t nif, int64_t ntime,
-                  const int64_t *win, double *out, void *stream) {
-  if (dtype == BLDP_DT_F32)
-    return bldp_kurtosis_f32(static_cast<const float *>(in), nchan, nif, ntime, win, out, nullptr,
-                             stream);
+// The TypedArgs of a typed getkurtosis (bldp_kurtosis's checks).
+int typed_kurt_args(int dtype, const void *in, int64_t nchan, int64_t nif, int64_t ntime,
+                    const int64_t *win, double *out, TypedArgs *ap, bool *empty) {
   if (!dtype_size(dtype)) return fail(BLDP_EINVAL, "unknown element type %d", dtype);
   Geo g;
   int rc = resolve_window(nchan, nif, ntime, win, &g);
   if (rc) return rc;
-  TypedArgs a{};
+  TypedArgs &a = *ap;
+  a = TypedArgs{};
   a.dtype = dtype;
   a.nbank = 1;
   a.in[0] = in;
@@ -888,8 +933,41 @@ int bldp_kurtosis(int dtype, const void *in, int64_t nchan, int64_t nif, int64_t
   a.nto = g.nt;
   a.F = a.T = 1;
   a.num_cus = num_cus_current();
-  if (a.nco * a.ni == 0) return BLDP_OK;
+  *empty = a.nco * a.ni == 0;
+  if (*empty) return BLDP_OK;
   if (!out || (!in && g.nt > 0)) return fail(BLDP_EINVAL, "null pointer");
+  return BLDP_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int bldp_reduce_strided(int dtype, const void *in, int64_t nchan, int64_t nif, int64_t ntime,
+                        const int64_t *win, int64_t fqavby, int64_t tavby, int op, void *out,
+                        int64_t out_ld_i, int64_t out_ld_t, void *stream) {
+  if (dtype == BLDP_DT_F32)
+    return bldp_reduce_strided_f32(static_cast<const float *>(in), nchan, nif, ntime, win, fqavby,
+                                   tavby, op, static_cast<float *>(out), out_ld_i, out_ld_t,
+                                   stream);
+  TypedArgs a;
+  bool empty = false;
+  int rc = typed_reduce_args(dtype, in, nchan, nif, ntime, win, fqavby, tavby, op, out, out_ld_i,
+                             out_ld_t, &a, &empty);
+  if (rc || empty) return rc;
+  hipError_t e = launch_reduce_typed(a, op, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(BLDP_EHIP, "typed reduce launch: %s", hipGetErrorString(e));
+  return BLDP_OK;
+}
+
+int bldp_kurtosis(int dtype, const void *in, int64_t nchan, int64_t nif, int64_t ntime,
+                  const int64_t *win, double *out, void *stream) {
+  if (dtype == BLDP_DT_F32)
+    return bldp_kurtosis_f32(static_cast<const float *>(in), nchan, nif, ntime, win, out, nullptr,
+                             stream);
+  TypedArgs a;
+  bool empty = false;
+  int rc = typed_kurt_args(dtype, in, nchan, nif, ntime, win, out, &a, &empty);
+  if (rc || empty) return rc;
   ScratchLease lease;  // time-chunk partial sums (k_kurt_i8), held until queued
   if (const size_t wsb = kurtosis_typed_ws_bytes(a)) {
     rc = scratch_lease((hipStream_t)stream, wsb, &lease);
@@ -898,6 +976,67 @@ int bldp_kurtosis(int dtype, const void *in, int64_t nchan, int64_t nif, int64_t
   }
   hipError_t e = launch_kurtosis_typed(a, out, (hipStream_t)stream);
   if (e != hipSuccess) return fail(BLDP_EHIP, "typed kurtosis launch: %s", hipGetErrorString(e));
+  return BLDP_OK;
+}
+
+// bldp_reduce_strided / bldp_kurtosis prepared once (any element type): a
+// launch through bldp_reduce_launch is one kernel launch (two for the typed
+// getkurtosis of long rows), no argument handling.
+int bldp_reduce_prepare(int dtype, const void *in, int64_t nchan, int64_t nif, int64_t ntime,
+                        const int64_t *win, int64_t fqavby, int64_t tavby, int op, void *out,
+                        int64_t out_ld_i, int64_t out_ld_t, bldp_reduce_op_t *handle) {
+  if (!handle) return fail(BLDP_EINVAL, "null handle pointer");
+  *handle = nullptr;
+  auto *h = new (std::nothrow) bldp_reduce_op{};
+  if (!h) return fail(BLDP_ENOMEM, "out of host memory");
+  int rc;
+  if (dtype == BLDP_DT_F32) {
+    h->kind = bldp_reduce_op::F32_REDUCE;
+    const float *ins[1] = {static_cast<const float *>(in)};
+    rc = prepare_reduce(1, ins, nchan, nif, ntime, win, fqavby, tavby, op,
+                        static_cast<float *>(out), 0, out_ld_i, out_ld_t, false, false, &h->a,
+                        &h->p, &h->empty);
+  } else {
+    h->kind = bldp_reduce_op::TYPED_REDUCE;
+    rc = typed_reduce_args(dtype, in, nchan, nif, ntime, win, fqavby, tavby, op, out, out_ld_i,
+                           out_ld_t, &h->t, &h->empty);
+  }
+  if (rc == BLDP_OK && hipGetDevice(&h->dev) != hipSuccess)
+    rc = fail(BLDP_EHIP, "hipGetDevice failed");
+  if (rc) {
+    delete h;
+    return rc;
+  }
+  h->op = op;
+  *handle = h;
+  return BLDP_OK;
+}
+
+int bldp_kurtosis_prepare(int dtype, const void *in, int64_t nchan, int64_t nif, int64_t ntime,
+                          const int64_t *win, double *out, bldp_reduce_op_t *handle) {
+  if (!handle) return fail(BLDP_EINVAL, "null handle pointer");
+  *handle = nullptr;
+  auto *h = new (std::nothrow) bldp_reduce_op{};
+  if (!h) return fail(BLDP_ENOMEM, "out of host memory");
+  int rc;
+  if (dtype == BLDP_DT_F32) {
+    h->kind = bldp_reduce_op::F32_KURT;
+    const float *ins[1] = {static_cast<const float *>(in)};
+    rc = kurt_setup(1, ins, nchan, nif, ntime, win, &h->k);
+    h->empty = false;
+  } else {
+    h->kind = bldp_reduce_op::TYPED_KURT;
+    rc = typed_kurt_args(dtype, in, nchan, nif, ntime, win, out, &h->t, &h->empty);
+  }
+  if (rc == BLDP_OK && hipGetDevice(&h->dev) != hipSuccess)
+    rc = fail(BLDP_EHIP, "hipGetDevice failed");
+  if (rc) {
+    delete h;
+    return rc;
+  }
+  h->kout = out;
+  h->op = 0;
+  *handle = h;
   return BLDP_OK;
 }
 

@@ -286,6 +286,92 @@ def reduce(x, fqavby=1, tavby=1, op="sum", win=None, out=None, stream=None):
     return out
 
 
+class _Prepared:
+    """A bldp_reduce_op_t handle: ``launch`` is one ctypes call that queues
+    the kernel(s), ``launch_timed`` the same with two timing HipEvents,
+    ``close`` releases it.  Keeps its tensors alive."""
+
+    def _bind(self, L, h, keep):
+        self._L, self._h, self._keep = L, h, keep
+        self._fn, self._timed = L.bldp_reduce_launch, L.bldp_reduce_launch_timed
+
+    def launch(self, stream=None) -> None:
+        sp = stream if isinstance(stream, int) else _lib.stream_ptr(stream)
+        rc = self._fn(self._h, sp)
+        if rc:
+            _lib.check(rc, "bldp_reduce_launch")
+
+    def launch_timed(self, stream, ev_start, ev_stop) -> None:
+        sp = stream if isinstance(stream, int) else _lib.stream_ptr(stream)
+        rc = self._timed(self._h, sp, ev_start.ev, ev_stop.ev)
+        if rc:
+            _lib.check(rc, "bldp_reduce_launch_timed")
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.bldp_reduce_release(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+
+class PreparedReduce(_Prepared):
+    """``reduce`` prepared once for fixed buffers, any element type
+    (bldp_reduce_prepare): the per-file worker call of
+    src/gbtworkerfunctions.jl:171-177 re-run on resident buffers costs one
+    ctypes call and the kernel launch.  ``out`` as ``reduce`` makes it."""
+
+    def __init__(self, x, fqavby=1, tavby=1, op="sum", win=None, out=None):
+        torch = _torch()
+        L = _lib.lib()
+        shape = tuple(x.shape)
+        _check_bounds(win, shape)
+        nco, ni, nto = out_shape(shape, win, fqavby, tavby)
+        odt = _torch_dtype(out_dtype(x.dtype, op)) if x.dtype != torch.float32 else torch.float32
+        if out is None:
+            out = fb_empty(nco, ni, nto, device=x.device, dtype=odt)
+        elif tuple(out.shape) != (nco, ni, nto) or out.dtype != odt:
+            raise ValueError(f"out is {out.dtype} {tuple(out.shape)}, expected {odt} "
+                             f"{(nco, ni, nto)}")
+        optr, onc, oni, _ = _abi_dims(out, allow_typed=True) if out.numel() else (0, nco, ni, nto)
+        ptr, nchan, nif, ntime = _abi_dims(x, allow_typed=True)
+        keep, wp = _lib.win_arg(_full_win(win, shape))
+        h = ctypes.c_void_p()
+        with torch.cuda.device(x.device):
+            rc = L.bldp_reduce_prepare(_dtype_code(x.dtype), ptr, nchan, nif, ntime, wp,
+                                       int(fqavby), int(tavby), _lib.OPS[op], optr, onc,
+                                       onc * oni, ctypes.byref(h))
+        _lib.check(rc, "bldp_reduce_prepare")
+        self._bind(L, h, (x, keep))
+        self.out = out
+
+
+class PreparedKurtosis(_Prepared):
+    """``kurtosis`` prepared once for fixed buffers, any element type
+    (bldp_kurtosis_prepare): getkurtosis (src/gbtworkerfunctions.jl:197-202)
+    re-run on a resident window for one ctypes call and the kernel launch."""
+
+    def __init__(self, x, win=None, out=None):
+        torch = _torch()
+        L = _lib.lib()
+        shape = tuple(x.shape)
+        _check_bounds(win, shape)
+        nc, ni, _ = window_shape(win, shape)
+        if out is None:
+            out = torch.empty((ni, nc), dtype=torch.float64, device=x.device).t()
+        ptr, nchan, nif, ntime = _abi_dims(x, allow_typed=True)
+        keep, wp = _lib.win_arg(_full_win(win, shape))
+        h = ctypes.c_void_p()
+        with torch.cuda.device(x.device):
+            rc = L.bldp_kurtosis_prepare(_dtype_code(x.dtype), ptr, nchan, nif, ntime, wp,
+                                         out.data_ptr() if out.numel() else None,
+                                         ctypes.byref(h))
+        _lib.check(rc, "bldp_kurtosis_prepare")
+        self._bind(L, h, (x, keep))
+        self.out = out
+
+
 def plan(x, fqavby=1, tavby=1, op="sum", win=None) -> dict:
     """Launch plan the library picks for this call (path, lanes/group, ...)."""
     L = _lib.lib()

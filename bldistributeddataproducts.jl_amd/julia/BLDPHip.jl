@@ -17,7 +17,7 @@ export gpu_init, gpu_finalize, gpu_pin, gpu_unpin, gpu_fqav, gpu_reduce, gpu_kur
 const libbldp = get(ENV, "BLDP_LIB", joinpath(@__DIR__, "..", "libbldp_hip.so"))
 
 # include/bldp.h BLDP_ABI_VERSION this binding is written against
-const ABI_VERSION = 4
+const ABI_VERSION = 5
 function __init__()
     v = ccall((:bldp_abi_version, libbldp), Cint, ())
     v == ABI_VERSION || error("libbldp_hip ABI version $v, BLDPHip expects $ABI_VERSION: rebuild it")

@@ -81,8 +81,12 @@ extern "C" {
  *    (tools/hbm_probe.hip, build/libbldp_probe.so); plan options
  *    "force_staged", "il_persist", "max_wg_per_cu", "typed_rows" removed, and
  *    the values that only ever forced a losing form (narrow_mis 2, lane 2,
- *    wavet 2, unaligned_vec 3, kurt_leaf_tile 2) */
-#define BLDP_ABI_VERSION 4
+ *    wavet 2, unaligned_vec 3, kurt_leaf_tile 2)
+ * 5: bldp_reduce_prepare / bldp_kurtosis_prepare (any element type) launched
+ *    by bldp_reduce_launch; bldp_band_reduce_multi_f32 flag
+ *    BLDP_BAND_PEER_STORE (direct xGMI stores are opt-in); plan option
+ *    "typed_kurt" */
+#define BLDP_ABI_VERSION 5
 
 #if defined(BLDP_BUILD)
 #define BLDP_API __attribute__((visibility("default")))
@@ -333,9 +337,27 @@ BLDP_API int bldp_reduce_strided(int dtype, const void *in, int64_t nchan, int64
                                  void *stream);
 /* getkurtosis for any bldp_dtype (StatsBase's recipe; Float64 arithmetic for
  * integer and Float64 rows: Base.sum's pairwise Float64 mean, sequential
- * moments).  out (nc, ni) float64 on the device.  Asynchronous. */
+ * moments; 8-bit rows from exact integer power sums, within (3 nt + 32)
+ * 2^-53 relative of the recipe on k + 3, plan option "typed_kurt").  out
+ * (nc, ni) float64 on the device.  Asynchronous. */
 BLDP_API int bldp_kurtosis(int dtype, const void *in, int64_t nchan, int64_t nif, int64_t ntime,
                            const int64_t *win, double *out, void *stream);
+/* bldp_reduce_strided / bldp_kurtosis prepared once for fixed buffers (ABI 5;
+ * any bldp_dtype, Float32 included): the checks, window and plan are taken
+ * here, and each bldp_reduce_launch(handle, stream) only queues the kernel(s)
+ * -- what a worker re-reducing the same per-file buffers pays per call
+ * (src/gbtworkerfunctions.jl:171-177,191-195).  Same results and errors as
+ * the unprepared calls; released with bldp_reduce_release.  Bound to the
+ * current device.  bldp_reduce_launch_timed takes these handles too: the
+ * Float32 reduce's own dispatches carry the events, the other kinds record
+ * them on the stream around the launch. */
+BLDP_API int bldp_reduce_prepare(int dtype, const void *in, int64_t nchan, int64_t nif,
+                                 int64_t ntime, const int64_t *win, int64_t fqavby, int64_t tavby,
+                                 int op, void *out, int64_t out_ld_i, int64_t out_ld_t,
+                                 bldp_reduce_op_t *handle);
+BLDP_API int bldp_kurtosis_prepare(int dtype, const void *in, int64_t nchan, int64_t nif,
+                                   int64_t ntime, const int64_t *win, double *out,
+                                   bldp_reduce_op_t *handle);
 /* Host-memory forms (what a Julia worker holding the mmap'ed / read array
  * calls): the window's span is copied to device `dev`, reduced there, and the
  * result copied back into host `out` (dense (nco, ni, nto) of the output type;

@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol(pkg, L):
     assert not missing, missing
     for s in declared_symbols():
         assert getattr(L, s) is not None
-    assert L.bldp_abi_version() == pkg._lib.ABI_VERSION == 4
+    assert L.bldp_abi_version() == pkg._lib.ABI_VERSION == 5
 
 
 def test_library_is_gfx950_code(pkg):

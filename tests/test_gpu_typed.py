@@ -334,3 +334,36 @@ def test_typed_vec_kernel_matches_oracle(pkg, eng, orc, dt):
         for op in ("sum", "max"):
             want = orc.np_reduce_typed(a, F, T, op, w)
             assert same(eng.fb_to_numpy(eng.reduce(x, F, T, op, w)), want), (dt, op, w)
+
+
+@pytest.mark.parametrize("dt", ALL_TYPES + [np.float32], ids=lambda d: np.dtype(d).name)
+def test_prepared_reduce_and_kurtosis(pkg, eng, dt):
+    """bldp_reduce_prepare / bldp_kurtosis_prepare (ABI 5, any element type):
+    each launch gives the unprepared call's result bit for bit, re-launches
+    on new data in the same buffers see the new data, and the timed launch
+    form records its events (the per-file call at one
+    ctypes call and the kernel launch)."""
+    import torch
+
+    for nc, ni, nt, F, T, win in ((4096, 1, 279, 64, 1, None), (1000, 2, 40, 8, 4, None),
+                                  (512, 1, 70, 4, 7, [8, 480, 1, 0, 1, 1, 0, 70, 1])):
+        a = rand(dt, (nc, ni, nt), seed=nc + nt)
+        x = to_dev(eng, a)
+        for op in ("sum", "max"):
+            pr = eng.PreparedReduce(x, F, T, op, win)
+            pr.launch()
+            assert same(eng.fb_to_numpy(pr.out), eng.fb_to_numpy(eng.reduce(x, F, T, op, win)))
+            x.copy_(to_dev(eng, rand(dt, (nc, ni, nt), seed=nc + nt + 1)))
+            e0, e1 = pkg._lib.HipEvent(timing=True), pkg._lib.HipEvent(timing=True)
+            pr.launch_timed(None, e0, e1)
+            torch.cuda.synchronize()
+            assert e0.elapsed_time(e1) >= 0.0
+            assert same(eng.fb_to_numpy(pr.out), eng.fb_to_numpy(eng.reduce(x, F, T, op, win)))
+            pr.close()
+        pk = eng.PreparedKurtosis(x, win)
+        pk.launch()
+        torch.cuda.synchronize()
+        assert same(eng.fb_to_numpy(pk.out), eng.fb_to_numpy(eng.kurtosis(x, win)))
+        pk.close()
+    with pytest.raises(pkg.DimensionMismatch):
+        eng.PreparedReduce(to_dev(eng, rand(dt, (100, 1, 8), seed=1)), 3, 1)
