@@ -577,104 +577,136 @@ __device__ __forceinline__ void transpose4(uint32_t w0, uint32_t w1, uint32_t w2
   T[3] = __builtin_amdgcn_perm(D, B, 0x07060302u);
 }
 
+// One batch of U spectra of a lane's word (4 channels), loaded: words past
+// `cnt` are replaced by d = 0.  Sums of d = x - 128 (UInt8: the byte's top
+// bit flipped, read as Int8) or x (Int8), |d| <= 128, per channel over 4
+// spectra at a time: the words transposed so a word holds one channel's 4
+// spectra, then
+//   S1 += sdot4(T, 1), S2 += sdot4(T, T)                (<= 2^30 in 65536)
+//   S3 += sdot2(d^2, d) over the Int16 halves           (<= 2^25 a batch)
+//   S4 += udot2(d^2, d^2)                               (<= 2^31 per 8)
+// (d^2 by v_pk_mul_lo_u16: <= 2^14), S3 and S4 moved to 64-bit sums per
+// batch / per 8 spectra: ~4 VALU operations per byte.
+template <bool SIGNED, int U>
+__device__ __forceinline__ void i8_batch(uint32_t (&w)[U], int cnt, int32_t (&s1)[4],
+                                         int32_t (&s2)[4], int64_t (&s3)[4], uint64_t (&s4)[4]) {
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (u >= cnt) w[u] = SIGNED ? 0u : 0x80808080u;  // (d = 0: adds nothing)
+  int32_t b3[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int h = 0; h < U; h += 8) {
+    uint32_t b4[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int g = h; g < h + 8; g += 4) {
+      if (g >= cnt) break;  // (uniform: a short last batch)
+      uint32_t T[4];
+      if (SIGNED)
+        transpose4(w[g], w[g + 1], w[g + 2], w[g + 3], T);
+      else
+        transpose4(w[g] ^ 0x80808080u, w[g + 1] ^ 0x80808080u, w[g + 2] ^ 0x80808080u,
+                   w[g + 3] ^ 0x80808080u, T);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int tk = (int)T[k];
+        s1[k] = __builtin_amdgcn_sdot4(tk, 0x01010101, s1[k], false);
+        s2[k] = __builtin_amdgcn_sdot4(tk, tk, s2[k], false);
+        // Int16 halves: spectra (0, 2) and (1, 3), sign-extended
+        const s2v e = __builtin_bit_cast(s2v, T[k] << 8) >> (short)8;
+        const s2v o = __builtin_bit_cast(s2v, T[k]) >> (short)8;
+        const u2v ue = __builtin_bit_cast(u2v, e), uo = __builtin_bit_cast(u2v, o);
+        const u2v qe = ue * ue, qo = uo * uo;  // d^2 (mod 2^16: exact, <= 2^14)
+        b3[k] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2v, qe), e, b3[k], false);
+        b3[k] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2v, qo), o, b3[k], false);
+        b4[k] = __builtin_amdgcn_udot2(qe, qe, b4[k], false);
+        b4[k] = __builtin_amdgcn_udot2(qo, qo, b4[k], false);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s4[k] += b4[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) s3[k] += b3[k];
+}
+
+// Workgroup (tile, row, chunk): 64 words (256 channels) of one (bank x IF)
+// row, NW waves on consecutive slabs of the chunk's spectra.  A wave streams
+// its slab in batches of U spectra, the next batch's loads issued before the
+// current one is summed (every load of a batch issued before the first is
+// waited on: a short batch re-reads its last spectrum, in bounds, and the
+// extra words become d = 0 by a select).
 template <bool SIGNED>
 __global__ __launch_bounds__(1024) void k_kurt_i8(const TypedArgs a, const KTM m, double *out,
                                                   uint64_t *ws) {
-  constexpr int U = 16;  // spectra of loads in flight per lane
+  constexpr int U = 16;  // spectra of loads in flight per lane (and as many prefetched)
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t ngl = a.nco / 4, tile = blockIdx.x, r = blockIdx.y, chunk = blockIdx.z;
   const int64_t q = tile * 64 + lane;  // this lane's word
   const int64_t i = r % a.ni, bank = r / a.ni;
   const int64_t ct0 = chunk * m.crow, ct1 = min(a.nto, ct0 + m.crow);
   const int64_t t0 = min(ct1, ct0 + (int64_t)wave * m.srow), t1 = min(ct1, t0 + m.srow);
-  // sums of d = x - 128 (UInt8: the byte's top bit flipped, read as Int8) or
-  // x (Int8), |d| <= 128, per channel over 4 spectra at a time: the batch's
-  // words transposed so a word holds one channel's 4 spectra, then
-  //   S1 += sdot4(T, 1), S2 += sdot4(T, T)                (<= 2^30 in 65536)
-  //   S3 += sdot2(d^2, d) over the Int16 halves           (<= 2^25 a batch)
-  //   S4 += udot2(d^2, d^2)                               (<= 2^31 per 8)
-  // (d^2 by v_pk_mul_lo_u16: <= 2^14), S3 and S4 moved to 64-bit sums per
-  // batch / per 8 spectra: ~4 VALU operations per byte
   int32_t s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
   int64_t s3[4] = {0, 0, 0, 0};
   uint64_t s4[4] = {0, 0, 0, 0};
-  if (q < ngl) {
+  if (q < ngl && t1 > t0) {
     const int64_t ldb = a.in_ld_t;  // bytes (1-byte elements)
-    const char *p = static_cast<const char *>(a.in[bank]) + a.in_off + i * a.in_ld_i + 4 * q;
-    for (int64_t t = t0; t < t1; t += U) {
-      const int cnt = (int)min((int64_t)U, t1 - t);
-      // every load issued before the first is waited on: a short batch
-      // re-reads its last spectrum (in bounds) and replaces the extra words
-      // by d = 0 with a select, not a branch around each load
-      uint32_t w[U];
+    // the tile's row start is uniform (a scalar base), the lane's word a
+    // 32-bit offset: one address register for every load
+    const char *base = static_cast<const char *>(a.in[bank]) + a.in_off + i * a.in_ld_i +
+                       256 * tile;
+    const uint32_t lofs = 4u * (uint32_t)lane;
+    // spectra past the slab re-read its last one (in bounds; i8_batch drops
+    // them), so no load sits behind a branch
+    auto load = [&](uint32_t (&w)[U], int64_t t) {
 #pragma unroll
       for (int u = 0; u < U; ++u)
         w[u] = __builtin_nontemporal_load(
-            reinterpret_cast<const uint32_t *>(p + (t + min(u, cnt - 1)) * ldb));
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (u >= cnt) w[u] = SIGNED ? 0u : 0x80808080u;  // (d = 0: adds nothing)
-      int32_t b3[4] = {0, 0, 0, 0};
-#pragma unroll
-      for (int h = 0; h < U; h += 8) {
-        uint32_t b4[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int g = h; g < h + 8; g += 4) {
-          if (g >= cnt) break;  // (uniform: a short last batch)
-          uint32_t T[4];
-          if (SIGNED)
-            transpose4(w[g], w[g + 1], w[g + 2], w[g + 3], T);
-          else
-            transpose4(w[g] ^ 0x80808080u, w[g + 1] ^ 0x80808080u, w[g + 2] ^ 0x80808080u,
-                       w[g + 3] ^ 0x80808080u, T);
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int tk = (int)T[k];
-            s1[k] = __builtin_amdgcn_sdot4(tk, 0x01010101, s1[k], false);
-            s2[k] = __builtin_amdgcn_sdot4(tk, tk, s2[k], false);
-            // Int16 halves: spectra (0, 2) and (1, 3), sign-extended
-            const s2v e = __builtin_bit_cast(s2v, T[k] << 8) >> (short)8;
-            const s2v o = __builtin_bit_cast(s2v, T[k]) >> (short)8;
-            const u2v ue = __builtin_bit_cast(u2v, e), uo = __builtin_bit_cast(u2v, o);
-            const u2v qe = ue * ue, qo = uo * uo;  // d^2 (mod 2^16: exact, <= 2^14)
-            b3[k] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2v, qe), e, b3[k], false);
-            b3[k] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2v, qo), o, b3[k], false);
-            b4[k] = __builtin_amdgcn_udot2(qe, qe, b4[k], false);
-            b4[k] = __builtin_amdgcn_udot2(qo, qo, b4[k], false);
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) s4[k] += b4[k];
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) s3[k] += b3[k];
+            reinterpret_cast<const uint32_t *>(base + min(t + u, t1 - 1) * ldb + lofs));
+    };
+    // two register buffers used in turn (no copies between them, so a
+    // batch's sums wait only for its own loads)
+    auto count = [&](int64_t t) { return (int)max((int64_t)0, min((int64_t)U, t1 - t)); };
+    uint32_t wa[U], wb[U];
+    int64_t t = t0;
+    load(wa, t);
+    for (;;) {
+      const int ca = count(t), cb = count(t + U);
+      load(wb, t + U);
+      i8_batch<SIGNED, U>(wa, ca, s1, s2, s3, s4);
+      if (cb == 0) break;
+      load(wa, t + 2 * U);
+      i8_batch<SIGNED, U>(wb, cb, s1, s2, s3, s4);
+      if (count(t + 2 * U) == 0) break;
+      t += 2 * U;
     }
   }
-  // the slabs' sums added in LDS (two's complement: the signed sums too)
-  __shared__ unsigned long long acc[4][256];
-  for (int e = threadIdx.x; e < 4 * 256; e += blockDim.x) (&acc[0][0])[e] = 0ull;
+  // the slabs' sums added in LDS (two's complement: the signed sums too),
+  // laid out [sum][channel of the word][lane]: a wave's ds_add_u64 touches
+  // 512 consecutive bytes
+  __shared__ unsigned long long acc[4][4][64];
+  for (int e = threadIdx.x; e < 4 * 256; e += blockDim.x) (&acc[0][0][0])[e] = 0ull;
   __syncthreads();
   if (q < ngl && t1 > t0) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const int ch = 4 * lane + k;
-      atomicAdd(&acc[0][ch], (unsigned long long)(int64_t)s1[k]);
-      atomicAdd(&acc[1][ch], (unsigned long long)s2[k]);
-      atomicAdd(&acc[2][ch], (unsigned long long)s3[k]);
-      atomicAdd(&acc[3][ch], (unsigned long long)s4[k]);
+      atomicAdd(&acc[0][k][lane], (unsigned long long)(int64_t)s1[k]);
+      atomicAdd(&acc[1][k][lane], (unsigned long long)(int64_t)s2[k]);
+      atomicAdd(&acc[2][k][lane], (unsigned long long)s3[k]);
+      atomicAdd(&acc[3][k][lane], (unsigned long long)s4[k]);
     }
   }
   __syncthreads();
   for (int ch = threadIdx.x; ch < 256; ch += blockDim.x) {
     const int64_t c = tile * 256 + ch;  // this workgroup's 256 channels, coalesced
+    const int l = ch >> 2, k = ch & 3;  // (word, channel in the word)
     if (c < a.nco) {
       if (m.nchunk == 1) {
-        out[c + a.nco * r] = kurt_from_sums(a.nto, (int64_t)acc[0][ch], acc[1][ch],
-                                            (int64_t)acc[2][ch], acc[3][ch]);
+        out[c + a.nco * r] = kurt_from_sums(a.nto, (int64_t)acc[0][k][l], acc[1][k][l],
+                                            (int64_t)acc[2][k][l], acc[3][k][l]);
       } else {
         const int64_t rows = a.ni * a.nbank;
 #pragma unroll
-        for (int s = 0; s < 4; ++s) ws[((chunk * 4 + s) * rows + r) * a.nco + c] = acc[s][ch];
+        for (int s = 0; s < 4; ++s) ws[((chunk * 4 + s) * rows + r) * a.nco + c] = acc[s][k][l];
       }
     }
   }
@@ -703,11 +735,15 @@ bool kurt_i8_plan(const TypedArgs &a, KTM *m) {
     if ((uintptr_t)a.in[b] % 4) return false;
   const int64_t rows = a.ni * a.nbank;
   m->ntile = cdivt(a.nco / 4, 64);
-  m->nw = (int)std::min<int64_t>(16, cdivt(a.nto, 16));
-  // time chunks only while the tiles' waves leave the CUs short of 16 each
-  // (0001: 512 channels = 2 tiles a row, ~10^6 spectra), never slabs under 16
-  // spectra, and never over 65536 (the lanes' UInt32 sums)
-  const int64_t waves = m->ntile * rows * m->nw, want = 16 * (int64_t)std::max(1, a.num_cus);
+  // waves for one round of 8 per SIMD (32 per CU): NW waves a tile (<= 16,
+  // never slabs under 16 spectra), then time chunks while the tiles still
+  // leave the CUs short (0001: 512 channels = 2 tiles a row, ~10^6 spectra),
+  // and never slabs over 65536 (the lanes' 32-bit sums).  The 0002 band: 2048
+  // tiles x 4 waves of 70 spectra; one 0002 file: 256 tiles x 16 waves of 18
+  const int64_t tiles = m->ntile * rows, want = 32 * (int64_t)std::max(1, a.num_cus);
+  m->nw = (int)std::max<int64_t>(1, std::min<int64_t>({16, cdivt(want, tiles),
+                                                       cdivt(a.nto, 16)}));
+  const int64_t waves = tiles * m->nw;
   int64_t nchunk = std::max<int64_t>(1, std::min(cdivt(want, waves),
                                                  a.nto / (16 * (int64_t)m->nw)));
   nchunk = std::max(nchunk, cdivt(a.nto, (int64_t)m->nw * 65536));

@@ -67,6 +67,7 @@ for s in $STEPS; do
           --variants "$V" --json "$OUT/ab_$SUITE.json" ;;
     kurt_*) run "$s" 300 python bench.py --mode kurtosis --config "${s#kurt_}" ;;
     ceil_kurt) run ceil_kurt 600 ./build/mix_ceiling 10 kurt ;;
+    hostbound) run hostbound 600 python tools/host_bound_probe.py --json "$OUT/hostbound.json" ;;
     kurtprof_*) C=${s#kurtprof_}
       run "$s" 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$s" -o run \
         -- python bench.py --mode kurtosis --config "$C" --steps 20 --warmup 5 ;;
