@@ -345,6 +345,11 @@ def test_prepared_reduce_and_kurtosis(pkg, eng, dt):
     ctypes call and the kernel launch)."""
     import torch
 
+    def same(got, want):  # (every element type here: bits, NaN = NaN)
+        got, want = np.asarray(got), np.asarray(want)
+        return got.dtype == want.dtype and got.shape == want.shape and \
+            np.array_equal(got, want, equal_nan=got.dtype.kind == "f")
+
     for nc, ni, nt, F, T, win in ((4096, 1, 279, 64, 1, None), (1000, 2, 40, 8, 4, None),
                                   (512, 1, 70, 4, 7, [8, 480, 1, 0, 1, 1, 0, 70, 1])):
         a = rand(dt, (nc, ni, nt), seed=nc + nt)
