@@ -525,15 +525,14 @@ __global__ __launch_bounds__(256) void k_kurt_typed_w(const TypedArgs a, double 
 // wave-instruction), each wave summing a time slab, the slabs added in LDS
 // (ds_add_u64), and, for long rows, time chunks of several workgroups added by
 // k_kurt_i8_final.  From the exact sums, with n the window's length:
-//   Y = n S2 - S1^2                                  = n^2 cm2
-//   X = n^3 S4 - 4 n^2 S1 S3 + 6 n S1^2 S2 - 3 S1^4   = n^4 cm4
-// (cm2, cm4: the central moments sum((x - mu)^k) / n, which the shift leaves
-// alone) in Int128 (exact for n <= 2^23), and kurtosis = X / Y^2 - 3 in
-// Float64: StatsBase's (cm4 / n) / (cm2 / n)^2 - 3 with exact central moments.
-// The recipe (src/gbtworkerfunctions.jl:197-202; Float64 m, z, z^2, z^4 and
-// sequential Float64 sums) differs from it by its own rounding, at most
-// (3 nt + 10) 2^-53 relative on k + 3 (tests hold it to
-// conftest.kurt_int_tol).  A row of one value: X = Y = 0 -> NaN, as the recipe.
+// the central moments n cm2 = sum((x - mu)^2), n cm4 = sum((x - mu)^4) (which
+// the shift leaves alone) re-centred exactly in Int64 and finished in Float64
+// (kurt_from_sums), and kurtosis = (cm4 / n) / (cm2 / n)^2 - 3 as StatsBase's
+// recipe defines it.  The recipe (src/gbtworkerfunctions.jl:197-202; Float64
+// m, z, z^2, z^4 and sequential Float64 sums) differs from the exact ratio by
+// its own rounding, at most (3 nt + 10) 2^-53 relative on k + 3; this path by
+// at most ~150 2^-53 (tests hold the two to conftest.kurt_int_tol).  A row of
+// one value gives NaN, as the recipe.
 // Plan option "typed_kurt": 1 (default) = this path for 8-bit rows of
 // dword-aligned words, 0 = k_kurt_typed_w (the recipe's order, bit-exact).
 struct KTM {
@@ -543,21 +542,35 @@ struct KTM {
   int64_t crow;     // spectra per chunk
   int64_t srow;     // spectra per wave slab (<= 65536: the UInt32 lane sums)
 };
-constexpr int64_t kI8MaxN = (int64_t)1 << 23;
+constexpr int64_t kI8MaxN = (int64_t)1 << 23;  // (the Int64 re-centring's bound)
 
-__device__ __forceinline__ double i128_to_f64(__int128 x) {
-  const int64_t hi = (int64_t)(x >> 64);
-  const uint64_t lo = (uint64_t)x;
-  return (double)hi * 18446744073709551616.0 + (double)lo;
-}
-
-__device__ __forceinline__ double kurt_from_sums(int64_t n, int64_t S1, uint64_t S2, int64_t S3,
-                                                 uint64_t S4) {
-  const __int128 N = n, A = S1, B = (__int128)S2, C = S3, D = (__int128)S4;
-  const __int128 Y = N * B - A * A;
-  const __int128 X = N * N * N * D - 4 * N * N * A * C + 6 * N * A * A * B - 3 * A * A * A * A;
-  const double y = i128_to_f64(Y);
-  return i128_to_f64(X) / (y * y) - 3.0;
+// The kurtosis of one channel from its exact sums S_k = sum of d^k (|d| <=
+// 128, n <= 2^23).  Re-centred on c = the integer nearest the mean of d, in
+// Int64 exactly (every term below 2^54):
+//   T1 = S1 - n c, T2 = S2 - 2c S1 + n c^2, T3 = ..., T4 = ...  (binomial)
+// then, with e = T1 / n (|e| <= 1/2),
+//   n cm2 = T2 - T1 e,   n cm4 = T4 - 4e T3 + 6e^2 T2 - 3n e^4
+// in Float64, and kurtosis = n (n cm4) / (n cm2)^2 - 3.  For integer data no
+// value is nearer the mean than c is, so n e^4 <= n cm4 and n e^2 <= n cm2:
+// each term above is at most 12 (T4), 20, 12 and 3 times n cm4, so the
+// Float64 evaluation is within ~150 ulps of the exact ratio in the worst case
+// (a few in practice); DESIGN.md §4 "Typed data".  A row of one value:
+// T1 = T2 = T4 = 0 -> 0/0 = NaN, as the recipe.
+__device__ __forceinline__ double kurt_from_sums(int64_t n, int64_t S1, uint64_t S2u, int64_t S3,
+                                                 uint64_t S4u) {
+  const int64_t S2 = (int64_t)S2u, S4 = (int64_t)S4u;
+  const double dn = (double)n;
+  const int32_t c = (int32_t)rint((double)S1 / dn);  // |c| <= 128
+  const int64_t c2 = (int64_t)c * c, c3 = c2 * c, c4 = c2 * c2;
+  const int64_t T1 = S1 - n * c;
+  const int64_t T2 = S2 - 2 * c * S1 + n * c2;
+  const int64_t T3 = S3 - 3 * c * S2 + 3 * c2 * S1 - n * c3;
+  const int64_t T4 = S4 - 4 * c * S3 + 6 * c2 * S2 - 4 * c3 * S1 + n * c4;
+  const double t1 = (double)T1, t2 = (double)T2, t3 = (double)T3, t4 = (double)T4;
+  const double e = t1 / dn;
+  const double m2 = t2 - t1 * e;
+  const double m4 = t4 - e * (4.0 * t3 - e * (6.0 * t2 - 3.0 * t1 * e));
+  return dn * m4 / (m2 * m2) - 3.0;
 }
 
 typedef short s2v __attribute__((ext_vector_type(2)));

@@ -71,12 +71,15 @@ def kurt_sum_tol(nt: int) -> float:
     return 6.0 * max(nt, 1) * 2.0 ** -53
 
 
-# 8-bit rows (k_kurt_i8, typed.hip): exact central moments (integer power
-# sums, Int128), so the difference from StatsBase's recipe is the recipe's own
-# rounding, first order (3 nt + 15) 2^-53 relative on k + 3,
-# plus <= 8 roundings of the final Float64 steps here.
+# 8-bit rows (k_kurt_i8, typed.hip): exact integer power sums, re-centred
+# exactly on the integer nearest the mean and finished in Float64 (within
+# ~150 2^-53 of the exact ratio, typed.hip kurt_from_sums); the recipe's own
+# rounding is first order (3 nt + 15) 2^-53 relative on k + 3.
+KURT_INT_FINISH = 160.0 * 2.0 ** -53
+
+
 def kurt_int_tol(nt: int) -> float:
-    return (3.0 * max(nt, 1) + 32.0) * 2.0 ** -53
+    return (3.0 * max(nt, 1) + 15.0) * 2.0 ** -53 + KURT_INT_FINISH
 
 
 def assert_kurtosis(got, want, path: str, nt: int, msg="") -> None:
