@@ -33,6 +33,7 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <cstdlib>
 #include <limits>
 #include <type_traits>
 
@@ -543,6 +544,9 @@ struct KTM {
   int64_t srow;     // spectra per wave slab (<= 65536: the UInt32 lane sums)
 };
 constexpr int64_t kI8MaxN = (int64_t)1 << 23;  // (the Int64 re-centring's bound)
+// waves per CU one round of k_kurt_i8 should fill (its ~100 VGPRs allow 5 a
+// SIMD, 20 a CU)
+constexpr int64_t kI8WavesPerCu = 32;
 
 // The kurtosis of one channel from its exact sums S_k = sum of d^k (|d| <=
 // 128, n <= 2^23).  Re-centred on c = the integer nearest the mean of d, in
@@ -748,12 +752,15 @@ bool kurt_i8_plan(const TypedArgs &a, KTM *m) {
     if ((uintptr_t)a.in[b] % 4) return false;
   const int64_t rows = a.ni * a.nbank;
   m->ntile = cdivt(a.nco / 4, 64);
-  // waves for one round of 8 per SIMD (32 per CU): NW waves a tile (<= 16,
+  // waves for one round of kI8WavesPerCu: NW waves a tile (<= 16,
   // never slabs under 16 spectra), then time chunks while the tiles still
   // leave the CUs short (0001: 512 channels = 2 tiles a row, ~10^6 spectra),
   // and never slabs over 65536 (the lanes' 32-bit sums).  The 0002 band: 2048
   // tiles x 4 waves of 70 spectra; one 0002 file: 256 tiles x 16 waves of 18
-  const int64_t tiles = m->ntile * rows, want = 32 * (int64_t)std::max(1, a.num_cus);
+  int64_t per_cu = kI8WavesPerCu;  // (BLDP_KURT_I8_WAVES_PER_CU: a probe knob, 4..64)
+  if (const char *e = getenv("BLDP_KURT_I8_WAVES_PER_CU"))
+    per_cu = std::min<int64_t>(64, std::max<int64_t>(4, atoi(e)));
+  const int64_t tiles = m->ntile * rows, want = per_cu * (int64_t)std::max(1, a.num_cus);
   m->nw = (int)std::max<int64_t>(1, std::min<int64_t>({16, cdivt(want, tiles),
                                                        cdivt(a.nto, 16)}));
   const int64_t waves = tiles * m->nw;

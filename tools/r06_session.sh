@@ -81,6 +81,7 @@ for s in $STEPS; do
     file) run file 300 python bench.py --mode file ;;
     rawfile) run rawfile 300 python bench.py --mode rawfile ;;
     typed) run typed 300 python bench.py --mode typed ;;
+    typedw_*) W=${s#typedw_}; BLDP_KURT_I8_WAVES_PER_CU=$W run "$s" 300 python bench.py --mode typed ;;
     typedwarm) run typedwarm 300 python bench.py --mode typed --cache warm ;;
     typedpipe_*) run "$s" 300 python bench.py --mode typed --plan-option typed_pipe="${s#typedpipe_}" ;;
     typedprof) run typedprof 300 rocprofv3 --kernel-trace --stats --output-format csv \
