@@ -545,8 +545,9 @@ struct KTM {
 };
 constexpr int64_t kI8MaxN = (int64_t)1 << 23;  // (the Int64 re-centring's bound)
 // waves per CU one round of k_kurt_i8 should fill (its ~100 VGPRs allow 5 a
-// SIMD, 20 a CU)
-constexpr int64_t kI8WavesPerCu = 32;
+// SIMD, 20 a CU; on the UInt8 0002 band 16 beat 24 and 32 by 5-20%,
+// profiles/r06/typed_r06f.json: fewer, longer slabs per finish)
+constexpr int64_t kI8WavesPerCu = 16;
 
 // The kurtosis of one channel from its exact sums S_k = sum of d^k (|d| <=
 // 128, n <= 2^23).  Re-centred on c = the integer nearest the mean of d, in
@@ -607,9 +608,11 @@ __device__ __forceinline__ void transpose4(uint32_t w0, uint32_t w1, uint32_t w2
 template <bool SIGNED, int U>
 __device__ __forceinline__ void i8_batch(uint32_t (&w)[U], int cnt, int32_t (&s1)[4],
                                          int32_t (&s2)[4], int64_t (&s3)[4], uint64_t (&s4)[4]) {
+  if (cnt < U) {  // (uniform: only a slab's last batch)
 #pragma unroll
-  for (int u = 0; u < U; ++u)
-    if (u >= cnt) w[u] = SIGNED ? 0u : 0x80808080u;  // (d = 0: adds nothing)
+    for (int u = 0; u < U; ++u)
+      if (u >= cnt) w[u] = SIGNED ? 0u : 0x80808080u;  // (d = 0: adds nothing)
+  }
   int32_t b3[4] = {0, 0, 0, 0};
 #pragma unroll
   for (int h = 0; h < U; h += 8) {
@@ -674,11 +677,18 @@ __global__ __launch_bounds__(1024) void k_kurt_i8(const TypedArgs a, const KTM m
     const uint32_t lofs = 4u * (uint32_t)lane;
     // spectra past the slab re-read its last one (in bounds; i8_batch drops
     // them), so no load sits behind a branch
+    const int last = (int)(t1 - 1);  // (spectrum indices < 2^23: 32-bit, uniform)
     auto load = [&](uint32_t (&w)[U], int64_t t) {
+      const int t32 = __builtin_amdgcn_readfirstlane((int)t);
 #pragma unroll
-      for (int u = 0; u < U; ++u)
-        w[u] = __builtin_nontemporal_load(
-            reinterpret_cast<const uint32_t *>(base + min(t + u, t1 - 1) * ldb + lofs));
+      for (int u = 0; u < U; ++u) {
+        // the row's byte offset held in scalar registers, so each load is
+        // global_load_dword v, lofs, s[row] (no vector address arithmetic)
+        const uint64_t ro = (uint64_t)((int64_t)min(t32 + u, last) * ldb);
+        const uint64_t rs = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(ro >> 32)) << 32) |
+                            __builtin_amdgcn_readfirstlane((uint32_t)ro);
+        w[u] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(base + rs + lofs));
+      }
     };
     // two register buffers used in turn (no copies between them, so a
     // batch's sums wait only for its own loads)
