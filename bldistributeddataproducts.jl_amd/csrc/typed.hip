@@ -548,6 +548,7 @@ constexpr int64_t kI8MaxN = (int64_t)1 << 23;  // (the Int64 re-centring's bound
 // SIMD, 20 a CU; on the UInt8 0002 band 16 beat 24 and 32 by 5-20%,
 // profiles/r06/typed_r06f.json: fewer, longer slabs per finish)
 constexpr int64_t kI8WavesPerCu = 16;
+constexpr int64_t kI8MinSlab = 16;  // fewest spectra a wave's slab is cut to
 
 // The kurtosis of one channel from its exact sums S_k = sum of d^k (|d| <=
 // 128, n <= 2^23).  Re-centred on c = the integer nearest the mean of d, in
@@ -658,7 +659,7 @@ __device__ __forceinline__ void i8_batch(uint32_t (&w)[U], int cnt, int32_t (&s1
 template <bool SIGNED>
 __global__ __launch_bounds__(1024) void k_kurt_i8(const TypedArgs a, const KTM m, double *out,
                                                   uint64_t *ws) {
-  constexpr int U = 16;  // spectra of loads in flight per lane (and as many prefetched)
+  constexpr int U = 8;  // spectra of loads in flight per lane (and as many prefetched)
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t ngl = a.nco / 4, tile = blockIdx.x, r = blockIdx.y, chunk = blockIdx.z;
   const int64_t q = tile * 64 + lane;  // this lane's word
@@ -739,18 +740,30 @@ __global__ __launch_bounds__(1024) void k_kurt_i8(const TypedArgs a, const KTM m
   }
 }
 
-// The chunks' sums of every channel added in chunk order (exact), then the
-// kurtosis (nchunk > 1).
-__global__ __launch_bounds__(256) void k_kurt_i8_final(const TypedArgs a, const KTM m,
-                                                       double *out, const uint64_t *ws) {
+// The chunks' sums of every channel added (exact: sums mod 2^64 in any
+// order), then the kurtosis (nchunk > 1).  Workgroup: 64 consecutive
+// channels x 16 waves, wave w adding chunks w, w + 16, ... (the 0001 product:
+// 512 channels of 100+ chunks -- one thread a channel walking the chunks in
+// turn paid a dependent load per chunk, ~0.26 us each).
+__global__ __launch_bounds__(1024) void k_kurt_i8_final(const TypedArgs a, const KTM m,
+                                                        double *out, const uint64_t *ws) {
   const int64_t rows = a.ni * a.nbank, n = a.nco * rows;
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (e >= n) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t e = (int64_t)blockIdx.x * 64 + lane;
   uint64_t S[4] = {0, 0, 0, 0};
-  for (int64_t c = 0; c < m.nchunk; ++c)
+  if (e < n)
+    for (int64_t c = wave; c < m.nchunk; c += 16)
 #pragma unroll
-    for (int s = 0; s < 4; ++s) S[s] += ws[(c * 4 + s) * n + e];
-  out[e] = kurt_from_sums(a.nto, (int64_t)S[0], S[1], (int64_t)S[2], S[3]);
+      for (int s = 0; s < 4; ++s) S[s] += ws[(c * 4 + s) * n + e];
+  __shared__ unsigned long long acc[4][64];
+  if (threadIdx.x < 256) (&acc[0][0])[threadIdx.x] = 0ull;
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < 4; ++s) atomicAdd(&acc[s][lane], (unsigned long long)S[s]);
+  __syncthreads();
+  if (wave == 0 && e < n)
+    out[e] = kurt_from_sums(a.nto, (int64_t)acc[0][lane], acc[1][lane], (int64_t)acc[2][lane],
+                            acc[3][lane]);
 }
 
 // The k_kurt_i8 geometry, or false when the path does not apply.
@@ -770,12 +783,15 @@ bool kurt_i8_plan(const TypedArgs &a, KTM *m) {
   int64_t per_cu = kI8WavesPerCu;  // (BLDP_KURT_I8_WAVES_PER_CU: a probe knob, 4..64)
   if (const char *e = getenv("BLDP_KURT_I8_WAVES_PER_CU"))
     per_cu = std::min<int64_t>(64, std::max<int64_t>(4, atoi(e)));
+  int64_t min_slab = kI8MinSlab;  // (BLDP_KURT_I8_MIN_SLAB: a probe knob, 8..4096)
+  if (const char *e = getenv("BLDP_KURT_I8_MIN_SLAB"))
+    min_slab = std::min<int64_t>(4096, std::max<int64_t>(8, atoi(e)));
   const int64_t tiles = m->ntile * rows, want = per_cu * (int64_t)std::max(1, a.num_cus);
   m->nw = (int)std::max<int64_t>(1, std::min<int64_t>({16, cdivt(want, tiles),
-                                                       cdivt(a.nto, 16)}));
+                                                       cdivt(a.nto, min_slab)}));
   const int64_t waves = tiles * m->nw;
   int64_t nchunk = std::max<int64_t>(1, std::min(cdivt(want, waves),
-                                                 a.nto / (16 * (int64_t)m->nw)));
+                                                 a.nto / (min_slab * (int64_t)m->nw)));
   nchunk = std::max(nchunk, cdivt(a.nto, (int64_t)m->nw * 65536));
   m->crow = cdivt(a.nto, nchunk);
   m->srow = cdivt(m->crow, m->nw);
@@ -894,7 +910,7 @@ hipError_t launch_kurt_t(const TypedArgs &a, double *out, hipStream_t s) {
       hipLaunchKernelGGL((k_kurt_i8<std::is_signed<TI>::value>), g, dim3(64 * m.nw), 0, s, a, m,
                          out, ws);
       if (m.nchunk > 1)
-        hipLaunchKernelGGL(k_kurt_i8_final, dim3((unsigned)cdivt(n, 256)), dim3(256), 0, s, a, m,
+        hipLaunchKernelGGL(k_kurt_i8_final, dim3((unsigned)cdivt(n, 64)), dim3(1024), 0, s, a, m,
                            out, ws);
       return hipGetLastError();
     }

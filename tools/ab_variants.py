@@ -182,6 +182,18 @@ VARIANTS = {
     "vecxcdoff": {"patch": [(K, "      return true;  // vec", "      return false;  // vec")]},
     "rowxcdoff": {"patch": [(K, "constexpr int64_t kRowXcdMinPitch = (int64_t)4 << 20;",
                              "constexpr int64_t kRowXcdMinPitch = INT64_MAX;")]},
+    # k_kurt_i8 (8-bit getkurtosis, round 6): loads per batch, a wave cap
+    "i8u8": {"patch": [("typed.hip", "  constexpr int U = 16;  // spectra of loads in flight per lane",
+                        "  constexpr int U = 8;  // spectra of loads in flight per lane")]},
+    "i8u4": {'patch': [('typed.hip', '  constexpr int U = 16;  // spectra of loads in flight per lane', '  constexpr int U = 4;  // spectra of loads in flight per lane')]},
+    "i8u12": {'patch': [('typed.hip', '  constexpr int U = 16;  // spectra of loads in flight per lane', '  constexpr int U = 12;  // spectra of loads in flight per lane')]},
+    "i8u8w24": {'patch': [('typed.hip', '  constexpr int U = 16;  // spectra of loads in flight per lane', '  constexpr int U = 8;  // spectra of loads in flight per lane'), ('typed.hip', 'constexpr int64_t kI8WavesPerCu = 16;', 'constexpr int64_t kI8WavesPerCu = 24;')]},
+    "i8u8w32": {'patch': [('typed.hip', '  constexpr int U = 16;  // spectra of loads in flight per lane', '  constexpr int U = 8;  // spectra of loads in flight per lane'), ('typed.hip', 'constexpr int64_t kI8WavesPerCu = 16;', 'constexpr int64_t kI8WavesPerCu = 32;')]},
+    "i8u8w12": {'patch': [('typed.hip', '  constexpr int U = 16;  // spectra of loads in flight per lane', '  constexpr int U = 8;  // spectra of loads in flight per lane'), ('typed.hip', 'constexpr int64_t kI8WavesPerCu = 16;', 'constexpr int64_t kI8WavesPerCu = 12;')]},
+    "i8u24": {"patch": [("typed.hip", "  constexpr int U = 16;  // spectra of loads in flight per lane",
+                         "  constexpr int U = 24;  // spectra of loads in flight per lane")]},
+    "i8w6": {"patch": [("typed.hip", "__global__ __launch_bounds__(1024) void k_kurt_i8(",
+                        "__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void k_kurt_i8(")]},
     "ilxcdoff": {"patch": [(K, "constexpr int kIlXcdMinT = 8;", "constexpr int kIlXcdMinT = 1 << 30;")]},
     "ilxcdall": {"patch": [(K, "constexpr int kIlXcdMinT = 8;", "constexpr int kIlXcdMinT = 1;"),
                            (K, "constexpr int64_t kIlXcdMaxPitch = (int64_t)128 << 20;",
@@ -569,6 +581,29 @@ def run(names, rounds, iters, suite="main"):
         a16 = rng.integers(0, 65536, (279, 1, 65536 * 8), dtype=np.uint16)
         typed_case("u16 0002 band F64 T1", a16, 3, 64, 1)
         cases_done = True
+    elif suite == "typedk":  # 8-bit getkurtosis (k_kurt_i8, round 6)
+        del b3
+        import numpy as np
+
+        def typedk_case(label, a, dcode):
+            x = torch.from_numpy(a).cuda().permute(2, 1, 0)  # Julia order
+            nchan, nif, ntime = x.shape
+            out = torch.empty((nif, nchan), dtype=torch.float64, device="cuda")
+            nbytes = a.nbytes + 8 * nchan * nif
+
+            def go(L):
+                rc = L.bldp_kurtosis(dcode, x.data_ptr(), nchan, nif, ntime, None,
+                                     out.data_ptr(), sp)
+                assert rc == 0
+            cases.append((label, go, nbytes, out, x))
+        rng = np.random.default_rng(0)
+        a8 = rng.integers(0, 256, (279, 1, 65536 * 8), dtype=np.uint8)
+        typedk_case("u8 0002 band kurtosis", a8, 2)
+        typedk_case("u8 0002 file kurtosis", np.ascontiguousarray(a8[:, :, :65536]), 2)
+        typedk_case("i8 0002 band kurtosis", a8.view(np.int8), 6)
+        a1 = rng.integers(0, 256, (200000, 1, 512), dtype=np.uint8)
+        typedk_case("u8 0001-like (512 ch x 200000) kurtosis", a1, 2)
+        cases_done = True
     elif suite == "il1":  # large groups with short time blocks: interleaved vs wave kernel
         for F, T in ((1024, 1), (512, 1), (2048, 1), (4096, 1), (1024, 2), (1024, 4)):
             band_case(f"0000 F{F} T{T}", b3, F, T)
@@ -942,7 +977,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--suite", default="main", choices=["main", "il", "ilsmall", "ilxcd", "rowxcd", "narrowt", "occ", "typed", "kregs", "narrow", "rows", "t1_0001", "wavet", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy", "wide", "grid0", "grid1", "t38", "lane3", "kgrid", "lanetpack", "kshort", "kfile"])
+    ap.add_argument("--suite", default="main", choices=["main", "typedk", "il", "ilsmall", "ilxcd", "rowxcd", "narrowt", "occ", "typed", "kregs", "narrow", "rows", "t1_0001", "wavet", "tile", "kurt", "kleaf", "kmid", "row", "t1", "sweep", "il1", "t1v", "rowt", "grid", "k3", "copy", "wide", "grid0", "grid1", "t38", "lane3", "kgrid", "lanetpack", "kshort", "kfile"])
     a = ap.parse_args()
     names = a.variants.split(",")
     if a.build:

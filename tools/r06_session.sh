@@ -5,7 +5,7 @@
 #   usage: tools/r06_session.sh TAG [steps...]
 #   steps: smoke tests tests_K[+K2...] bench bench_CFG list ab_SUITE[:v1,v2,...]
 #          prof_CFG[_lbN] pmc_CFG[_lbN] sq_CFG[_lbN] cold_CFG typed typedprof typedpmc typedsq
-#          ab_SUITE getband getbandz ceil_kurt kurtprof_CFG kurtpmc_CFG
+#          ab_SUITE getband getbandz ceil_kurt kurtprof_CFG kurtpmc_CFG kurtsweep
 # CFG[_lbN]: a config, optionally with --local-banks N (one rank's launch of an
 # (8/N)-GPU run).  Every GPU step has its own time limit; after any failure
 # nothing more runs.
@@ -45,6 +45,7 @@ for s in $STEPS; do
       run "$s" 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 \
           --timeout-method thread -k "${K//+/ or }" ;;
     bench) run bench 600 python bench.py ;;
+    benchpipe_*) run "$s" 600 python bench.py --config "${s#benchpipe_}" --pipeline --no-cpu-baseline ;;
     bench_*) run "$s" 600 python bench.py $(bench_args "${s#bench_}" | sed 's/--no-cpu-baseline//') ;;
     benchn_*) run "$s" 600 python bench.py $(bench_args "${s#benchn_}") ;;
     cold_*) run "$s" 600 python bench.py --config "${s#cold_}" --cache cold --no-cpu-baseline ;;
@@ -62,6 +63,12 @@ for s in $STEPS; do
     kurtsq_*) C=${s#kurtsq_}
       run "$s" 180 rocprofv3 --pmc $SQ --output-format csv -d "$OUT/$s" -o run \
         -- python bench.py --mode kurtosis --config "$C" --steps 20 --warmup 5 ;;
+    kurtsweep)  # k_kurt_i8's grid knobs: waves per CU x shortest slab
+      for W in 12 16 24 32; do for S in 16 32 64; do
+        BLDP_KURT_I8_WAVES_PER_CU=$W BLDP_KURT_I8_MIN_SLAB=$S run "kurtsweep_w${W}_s$S" 300 \
+          python tools/ab_variants.py --run --suite typedk --rounds 3 --variants base \
+          --json "$OUT/kurtsweep_w${W}_s$S.json"
+      done; done ;;
     ab_*) A=${s#ab_}; SUITE=${A%%:*}; V=${AB_VARIANTS:-base}; [ "$SUITE" != "$A" ] && V=${A#*:}
       run "ab_$SUITE" 900 python tools/ab_variants.py --run --suite "$SUITE" --rounds 5 \
           --variants "$V" --json "$OUT/ab_$SUITE.json" ;;
