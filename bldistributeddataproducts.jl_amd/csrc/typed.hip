@@ -521,9 +521,9 @@ __global__ __launch_bounds__(256) void k_kurt_typed_w(const TypedArgs a, double 
 // integer power sums.  For each channel the row's S1..S4 = sum of d^1..d^4,
 // d = x - 128 (UInt8) or x (Int8), are integers that Int64 / UInt64 hold
 // exactly (|d| <= 128, n <= 2^23), so any split of the time axis adds them
-// back exactly: the window is read once by NW waves per 64-word tile (4
-// channels a lane, one 32-bit word of each spectrum; 256 contiguous bytes per
-// wave-instruction), each wave summing a time slab, the slabs added in LDS
+// back exactly: the window is read once by NW waves per tile of 64 lanes x W
+// words (4 W channels a lane, W 32-bit words of each spectrum; 256 W
+// contiguous bytes per wave-instruction), each wave summing a time slab, the slabs added in LDS
 // (ds_add_u64), and, for long rows, time chunks of several workgroups added by
 // k_kurt_i8_final.  From the exact sums, with n the window's length:
 // the central moments n cm2 = sum((x - mu)^2), n cm4 = sum((x - mu)^4) (which
@@ -535,20 +535,25 @@ __global__ __launch_bounds__(256) void k_kurt_typed_w(const TypedArgs a, double 
 // at most ~150 2^-53 (tests hold the two to conftest.kurt_int_tol).  A row of
 // one value gives NaN, as the recipe.
 // Plan option "typed_kurt": 1 (default) = this path for 8-bit rows of
-// dword-aligned words, 0 = k_kurt_typed_w (the recipe's order, bit-exact).
+// dword-aligned words, 4- or 8-byte words a lane by kurt_i8_plan's rule; 2 /
+// 3 = 4- / 8-byte words (8: where the rows are 8-byte aligned); 0 =
+// k_kurt_typed_w (the recipe's order, bit-exact).
 struct KTM {
   int nw;           // waves per workgroup (time slabs)
-  int64_t ntile;    // 64-word tiles per row
+  int wpl;          // words a lane (W: 1 or 2)
+  int64_t ntile;    // tiles (64 lanes x W words) per row
   int64_t nchunk;   // time chunks (workgroups along time); 1: fused finish
   int64_t crow;     // spectra per chunk
-  int64_t srow;     // spectra per wave slab (<= 65536: the UInt32 lane sums)
+  int64_t srow;     // spectra per wave slab (<= 1024: the Int32 lane sums of d^3)
 };
 constexpr int64_t kI8MaxN = (int64_t)1 << 23;  // (the Int64 re-centring's bound)
-// waves per CU one round of k_kurt_i8 should fill (its ~100 VGPRs allow 5 a
-// SIMD, 20 a CU; on the UInt8 0002 band 16 beat 24 and 32 by 5-20%,
-// profiles/r06/typed_r06f.json: fewer, longer slabs per finish)
+// waves per CU one round of k_kurt_i8 should fill (58 VGPRs with 4-byte
+// words, 8 waves a SIMD; 116 with 8-byte, 4 a SIMD); 12..32 are within ~5% of
+// each other on the UInt8 0002 band and file (profiles/r06/kurtsweep_r06j.json,
+// kurtsweep_r06m.json)
 constexpr int64_t kI8WavesPerCu = 16;
 constexpr int64_t kI8MinSlab = 16;  // fewest spectra a wave's slab is cut to
+constexpr int64_t kI8MaxSlab = 1024;  // most: |sum d^3| <= 2^21 x 1024 = 2^31 (Int32)
 
 // The kurtosis of one channel from its exact sums S_k = sum of d^k (|d| <=
 // 128, n <= 2^23).  Re-centred on c = the integer nearest the mean of d, in
@@ -596,137 +601,148 @@ __device__ __forceinline__ void transpose4(uint32_t w0, uint32_t w1, uint32_t w2
   T[3] = __builtin_amdgcn_perm(D, B, 0x07060302u);
 }
 
-// One batch of U spectra of a lane's word (4 channels), loaded: words past
-// `cnt` are replaced by d = 0.  Sums of d = x - 128 (UInt8: the byte's top
-// bit flipped, read as Int8) or x (Int8), |d| <= 128, per channel over 4
+// One batch of U spectra of a lane's W words (4 W channels), loaded: words
+// past `cnt` are replaced by d = 0.  Sums of d = x - 128 (UInt8: the byte's
+// top bit flipped, read as Int8) or x (Int8), |d| <= 128, per channel over 4
 // spectra at a time: the words transposed so a word holds one channel's 4
 // spectra, then
-//   S1 += sdot4(T, 1), S2 += sdot4(T, T)                (<= 2^30 in 65536)
-//   S3 += sdot2(d^2, d) over the Int16 halves           (<= 2^25 a batch)
+//   S1 += sdot4(T, 1), S2 += sdot4(T, T)                (<= 2^24 in 1024)
+//   S3 += sdot2(d^2, d) over the Int16 halves           (|.| <= 2^31 in 1024)
 //   S4 += udot2(d^2, d^2)                               (<= 2^31 per 8)
-// (d^2 by v_pk_mul_lo_u16: <= 2^14), S3 and S4 moved to 64-bit sums per
-// batch / per 8 spectra: ~4 VALU operations per byte.
-template <bool SIGNED, int U>
-__device__ __forceinline__ void i8_batch(uint32_t (&w)[U], int cnt, int32_t (&s1)[4],
-                                         int32_t (&s2)[4], int64_t (&s3)[4], uint64_t (&s4)[4]) {
+// (d^2 by v_pk_mul_lo_u16: <= 2^14), S4 moved to 64-bit sums per 8 spectra:
+// ~4 VALU operations per byte.
+template <bool SIGNED, int U, int W>
+__device__ __forceinline__ void i8_batch(uint32_t (&w)[U][W], int cnt, int32_t (&s1)[4 * W],
+                                         int32_t (&s2)[4 * W], int32_t (&s3)[4 * W],
+                                         uint64_t (&s4)[4 * W]) {
   if (cnt < U) {  // (uniform: only a slab's last batch)
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      if (u >= cnt) w[u] = SIGNED ? 0u : 0x80808080u;  // (d = 0: adds nothing)
+#pragma unroll
+      for (int j = 0; j < W; ++j)
+        if (u >= cnt) w[u][j] = SIGNED ? 0u : 0x80808080u;  // (d = 0: adds nothing)
   }
-  int32_t b3[4] = {0, 0, 0, 0};
 #pragma unroll
   for (int h = 0; h < U; h += 8) {
-    uint32_t b4[4] = {0, 0, 0, 0};
+    uint32_t b4[4 * W];
 #pragma unroll
-    for (int g = h; g < h + 8; g += 4) {
+    for (int k = 0; k < 4 * W; ++k) b4[k] = 0;
+#pragma unroll
+    for (int g = h; g < h + 8 && g < U; g += 4) {
       if (g >= cnt) break;  // (uniform: a short last batch)
-      uint32_t T[4];
-      if (SIGNED)
-        transpose4(w[g], w[g + 1], w[g + 2], w[g + 3], T);
-      else
-        transpose4(w[g] ^ 0x80808080u, w[g + 1] ^ 0x80808080u, w[g + 2] ^ 0x80808080u,
-                   w[g + 3] ^ 0x80808080u, T);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int tk = (int)T[k];
-        s1[k] = __builtin_amdgcn_sdot4(tk, 0x01010101, s1[k], false);
-        s2[k] = __builtin_amdgcn_sdot4(tk, tk, s2[k], false);
-        // Int16 halves: spectra (0, 2) and (1, 3), sign-extended
-        const s2v e = __builtin_bit_cast(s2v, T[k] << 8) >> (short)8;
-        const s2v o = __builtin_bit_cast(s2v, T[k]) >> (short)8;
-        const u2v ue = __builtin_bit_cast(u2v, e), uo = __builtin_bit_cast(u2v, o);
-        const u2v qe = ue * ue, qo = uo * uo;  // d^2 (mod 2^16: exact, <= 2^14)
-        b3[k] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2v, qe), e, b3[k], false);
-        b3[k] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2v, qo), o, b3[k], false);
-        b4[k] = __builtin_amdgcn_udot2(qe, qe, b4[k], false);
-        b4[k] = __builtin_amdgcn_udot2(qo, qo, b4[k], false);
+      for (int j = 0; j < W; ++j) {
+        uint32_t T[4];
+        if (SIGNED)
+          transpose4(w[g][j], w[g + 1][j], w[g + 2][j], w[g + 3][j], T);
+        else
+          transpose4(w[g][j] ^ 0x80808080u, w[g + 1][j] ^ 0x80808080u,
+                     w[g + 2][j] ^ 0x80808080u, w[g + 3][j] ^ 0x80808080u, T);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int x = 4 * j + k;
+          const int tk = (int)T[k];
+          s1[x] = __builtin_amdgcn_sdot4(tk, 0x01010101, s1[x], false);
+          s2[x] = __builtin_amdgcn_sdot4(tk, tk, s2[x], false);
+          // Int16 halves: spectra (0, 2) and (1, 3), sign-extended
+          const s2v e = __builtin_bit_cast(s2v, T[k] << 8) >> (short)8;
+          const s2v o = __builtin_bit_cast(s2v, T[k]) >> (short)8;
+          const u2v ue = __builtin_bit_cast(u2v, e), uo = __builtin_bit_cast(u2v, o);
+          const u2v qe = ue * ue, qo = uo * uo;  // d^2 (mod 2^16: exact, <= 2^14)
+          s3[x] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2v, qe), e, s3[x], false);
+          s3[x] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2v, qo), o, s3[x], false);
+          b4[x] = __builtin_amdgcn_udot2(qe, qe, b4[x], false);
+          b4[x] = __builtin_amdgcn_udot2(qo, qo, b4[x], false);
+        }
       }
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) s4[k] += b4[k];
+    for (int k = 0; k < 4 * W; ++k) s4[k] += b4[k];
   }
-#pragma unroll
-  for (int k = 0; k < 4; ++k) s3[k] += b3[k];
 }
 
-// Workgroup (tile, row, chunk): 64 words (256 channels) of one (bank x IF)
-// row, NW waves on consecutive slabs of the chunk's spectra.  A wave streams
-// its slab in batches of U spectra, the next batch's loads issued before the
-// current one is summed (every load of a batch issued before the first is
-// waited on: a short batch re-reads its last spectrum, in bounds, and the
-// extra words become d = 0 by a select).
-template <bool SIGNED>
+// Workgroup (tile, row, chunk): 64 lanes x W words (256 W channels) of one
+// (bank x IF) row, NW waves on consecutive slabs of the chunk's spectra.  A
+// wave streams its slab in batches of U spectra, the next batch's loads issued
+// before the current one is summed (every load of a batch issued before the
+// first is waited on: a short batch re-reads its last spectrum, in bounds, and
+// the extra words become d = 0 by a select).
+template <bool SIGNED, int W>
 __global__ __launch_bounds__(1024) void k_kurt_i8(const TypedArgs a, const KTM m, double *out,
                                                   uint64_t *ws) {
   constexpr int U = 8;  // spectra of loads in flight per lane (and as many prefetched)
+  constexpr int C = 4 * W;  // channels a lane
+  typedef uint32_t wv_t __attribute__((ext_vector_type(W)));
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t ngl = a.nco / 4, tile = blockIdx.x, r = blockIdx.y, chunk = blockIdx.z;
-  const int64_t q = tile * 64 + lane;  // this lane's word
+  const int64_t ngl = a.nco / C, tile = blockIdx.x, r = blockIdx.y, chunk = blockIdx.z;
+  const int64_t q = tile * 64 + lane;  // this lane's words
   const int64_t i = r % a.ni, bank = r / a.ni;
   const int64_t ct0 = chunk * m.crow, ct1 = min(a.nto, ct0 + m.crow);
   const int64_t t0 = min(ct1, ct0 + (int64_t)wave * m.srow), t1 = min(ct1, t0 + m.srow);
-  int32_t s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
-  int64_t s3[4] = {0, 0, 0, 0};
-  uint64_t s4[4] = {0, 0, 0, 0};
+  int32_t s1[C], s2[C], s3[C];
+  uint64_t s4[C];
+#pragma unroll
+  for (int k = 0; k < C; ++k) s1[k] = s2[k] = s3[k] = 0, s4[k] = 0;
   if (q < ngl && t1 > t0) {
     const int64_t ldb = a.in_ld_t;  // bytes (1-byte elements)
-    // the tile's row start is uniform (a scalar base), the lane's word a
+    // the tile's row start is uniform (a scalar base), the lane's words a
     // 32-bit offset: one address register for every load
     const char *base = static_cast<const char *>(a.in[bank]) + a.in_off + i * a.in_ld_i +
-                       256 * tile;
-    const uint32_t lofs = 4u * (uint32_t)lane;
+                       256 * W * tile;
+    const uint32_t lofs = 4u * W * (uint32_t)lane;
     // spectra past the slab re-read its last one (in bounds; i8_batch drops
     // them), so no load sits behind a branch
     const int last = (int)(t1 - 1);  // (spectrum indices < 2^23: 32-bit, uniform)
-    auto load = [&](uint32_t (&w)[U], int64_t t) {
+    auto load = [&](uint32_t (&w)[U][W], int64_t t) {
       const int t32 = __builtin_amdgcn_readfirstlane((int)t);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         // the row's byte offset held in scalar registers, so each load is
-        // global_load_dword v, lofs, s[row] (no vector address arithmetic)
+        // global_load_dword(x2) v, lofs, s[row] (no vector address arithmetic)
         const uint64_t ro = (uint64_t)((int64_t)min(t32 + u, last) * ldb);
         const uint64_t rs = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(ro >> 32)) << 32) |
                             __builtin_amdgcn_readfirstlane((uint32_t)ro);
-        w[u] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(base + rs + lofs));
+        const wv_t v = __builtin_nontemporal_load(reinterpret_cast<const wv_t *>(base + rs + lofs));
+#pragma unroll
+        for (int j = 0; j < W; ++j) w[u][j] = v[j];
       }
     };
     // two register buffers used in turn (no copies between them, so a
     // batch's sums wait only for its own loads)
     auto count = [&](int64_t t) { return (int)max((int64_t)0, min((int64_t)U, t1 - t)); };
-    uint32_t wa[U], wb[U];
+    uint32_t wa[U][W], wb[U][W];
     int64_t t = t0;
     load(wa, t);
     for (;;) {
       const int ca = count(t), cb = count(t + U);
       load(wb, t + U);
-      i8_batch<SIGNED, U>(wa, ca, s1, s2, s3, s4);
+      i8_batch<SIGNED, U, W>(wa, ca, s1, s2, s3, s4);
       if (cb == 0) break;
       load(wa, t + 2 * U);
-      i8_batch<SIGNED, U>(wb, cb, s1, s2, s3, s4);
+      i8_batch<SIGNED, U, W>(wb, cb, s1, s2, s3, s4);
       if (count(t + 2 * U) == 0) break;
       t += 2 * U;
     }
   }
   // the slabs' sums added in LDS (two's complement: the signed sums too),
-  // laid out [sum][channel of the word][lane]: a wave's ds_add_u64 touches
+  // laid out [sum][channel of the lane][lane]: a wave's ds_add_u64 touches
   // 512 consecutive bytes
-  __shared__ unsigned long long acc[4][4][64];
-  for (int e = threadIdx.x; e < 4 * 256; e += blockDim.x) (&acc[0][0][0])[e] = 0ull;
+  __shared__ unsigned long long acc[4][C][64];
+  for (int e = threadIdx.x; e < 4 * C * 64; e += blockDim.x) (&acc[0][0][0])[e] = 0ull;
   __syncthreads();
   if (q < ngl && t1 > t0) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < C; ++k) {
       atomicAdd(&acc[0][k][lane], (unsigned long long)(int64_t)s1[k]);
       atomicAdd(&acc[1][k][lane], (unsigned long long)(int64_t)s2[k]);
-      atomicAdd(&acc[2][k][lane], (unsigned long long)s3[k]);
+      atomicAdd(&acc[2][k][lane], (unsigned long long)(int64_t)s3[k]);
       atomicAdd(&acc[3][k][lane], (unsigned long long)s4[k]);
     }
   }
   __syncthreads();
-  for (int ch = threadIdx.x; ch < 256; ch += blockDim.x) {
-    const int64_t c = tile * 256 + ch;  // this workgroup's 256 channels, coalesced
-    const int l = ch >> 2, k = ch & 3;  // (word, channel in the word)
+  for (int ch = threadIdx.x; ch < 64 * C; ch += blockDim.x) {
+    const int64_t c = tile * 64 * C + ch;  // this workgroup's channels, coalesced
+    const int l = ch / C, k = ch % C;  // (lane, channel of the lane)
     if (c < a.nco) {
       if (m.nchunk == 1) {
         out[c + a.nco * r] = kurt_from_sums(a.nto, (int64_t)acc[0][k][l], acc[1][k][l],
@@ -774,25 +790,39 @@ bool kurt_i8_plan(const TypedArgs &a, KTM *m) {
   for (int b = 0; b < a.nbank; ++b)
     if ((uintptr_t)a.in[b] % 4) return false;
   const int64_t rows = a.ni * a.nbank;
-  m->ntile = cdivt(a.nco / 4, 64);
-  // waves for one round of kI8WavesPerCu: NW waves a tile (<= 16,
-  // never slabs under 16 spectra), then time chunks while the tiles still
-  // leave the CUs short (0001: 512 channels = 2 tiles a row, ~10^6 spectra),
-  // and never slabs over 65536 (the lanes' 32-bit sums).  The 0002 band: 2048
-  // tiles x 4 waves of 70 spectra; one 0002 file: 256 tiles x 16 waves of 18
   int64_t per_cu = kI8WavesPerCu;  // (BLDP_KURT_I8_WAVES_PER_CU: a probe knob, 4..64)
   if (const char *e = getenv("BLDP_KURT_I8_WAVES_PER_CU"))
     per_cu = std::min<int64_t>(64, std::max<int64_t>(4, atoi(e)));
   int64_t min_slab = kI8MinSlab;  // (BLDP_KURT_I8_MIN_SLAB: a probe knob, 8..4096)
   if (const char *e = getenv("BLDP_KURT_I8_MIN_SLAB"))
     min_slab = std::min<int64_t>(4096, std::max<int64_t>(8, atoi(e)));
-  const int64_t tiles = m->ntile * rows, want = per_cu * (int64_t)std::max(1, a.num_cus);
+  const int64_t want = per_cu * (int64_t)std::max(1, a.num_cus);
+  // 8-byte loads (8 channels a lane: 512 contiguous bytes a wave-load) where
+  // every row start is 8-byte aligned and the tiles alone, cut into slabs,
+  // fill the round (the 0002 band: 1024 tiles, 30.8 vs 33.4 us); 4-byte
+  // loads otherwise (one 0002 file: 128 tiles of 8 channels a lane, 12.1 vs
+  // 8.6 us; profiles/r06/kurtsweep_r06m.json)
+  bool w2a = a.nco % 8 == 0 && a.in_off % 8 == 0 && (a.ni == 1 || a.in_ld_i % 8 == 0) &&
+             (a.nto == 1 || a.in_ld_t % 8 == 0);
+  for (int b = 0; w2a && b < a.nbank; ++b) w2a = (uintptr_t)a.in[b] % 8 == 0;
+  const bool w2 =
+      w2a && cdivt(a.nco / 8, 64) * rows * std::min<int64_t>(16, cdivt(a.nto, min_slab)) >= want;
+  const int64_t form = opt(OPT_TYPED_KURT);  // 1: by the rule, 2: 4-byte, 3: 8-byte words
+  m->wpl = (form == 1 && w2) || (form == 3 && w2a) ? 2 : 1;
+  m->ntile = cdivt(a.nco / (4 * m->wpl), 64);
+  // waves for one round of kI8WavesPerCu: NW waves a tile (<= 16,
+  // never slabs under 16 spectra), then time chunks while the tiles still
+  // leave the CUs short (0001: 512 channels = 2 tiles a row, ~10^6 spectra),
+  // and never slabs over 1024 (the lanes' 32-bit sums of d^3).  The 0002
+  // band: 1024 tiles x 4 waves of 70 spectra; one 0002 file: 256 tiles x 16
+  // waves of 18
+  const int64_t tiles = m->ntile * rows;
   m->nw = (int)std::max<int64_t>(1, std::min<int64_t>({16, cdivt(want, tiles),
                                                        cdivt(a.nto, min_slab)}));
   const int64_t waves = tiles * m->nw;
   int64_t nchunk = std::max<int64_t>(1, std::min(cdivt(want, waves),
                                                  a.nto / (min_slab * (int64_t)m->nw)));
-  nchunk = std::max(nchunk, cdivt(a.nto, (int64_t)m->nw * 65536));
+  nchunk = std::max(nchunk, cdivt(a.nto, (int64_t)m->nw * kI8MaxSlab));
   m->crow = cdivt(a.nto, nchunk);
   m->srow = cdivt(m->crow, m->nw);
   m->crow = m->srow * m->nw;
@@ -907,8 +937,11 @@ hipError_t launch_kurt_t(const TypedArgs &a, double *out, hipStream_t s) {
     if (kurt_i8_plan(a, &m) && (m.nchunk == 1 || a.ws)) {
       const dim3 g((unsigned)m.ntile, (unsigned)(a.ni * a.nbank), (unsigned)m.nchunk);
       uint64_t *ws = static_cast<uint64_t *>(a.ws);
-      hipLaunchKernelGGL((k_kurt_i8<std::is_signed<TI>::value>), g, dim3(64 * m.nw), 0, s, a, m,
-                         out, ws);
+      constexpr bool sg = std::is_signed<TI>::value;
+      if (m.wpl == 2)
+        hipLaunchKernelGGL((k_kurt_i8<sg, 2>), g, dim3(64 * m.nw), 0, s, a, m, out, ws);
+      else
+        hipLaunchKernelGGL((k_kurt_i8<sg, 1>), g, dim3(64 * m.nw), 0, s, a, m, out, ws);
       if (m.nchunk > 1)
         hipLaunchKernelGGL(k_kurt_i8_final, dim3((unsigned)cdivt(n, 64)), dim3(1024), 0, s, a, m,
                            out, ws);

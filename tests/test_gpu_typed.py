@@ -238,7 +238,8 @@ def test_kurtosis_8bit_exact_moments(pkg, eng, orc, dt):
     over waves and, for long rows, over workgroups whose sums a second kernel
     adds): within conftest.KURT_INT_FINISH (relative on k + 3) of the exactly
     rounded kurtosis (Python integers), and within kurt_int_tol(nt) of the
-    recipe (oracle).  The 0002 file geometry, one and several time chunks
+    recipe (oracle); 4- and 8-byte words a lane (plan option typed_kurt 2 / 3)
+    bit-identical.  The 0002 file geometry, one and several time chunks
     (the 0001 shape: few channels, long rows), the type's extremes (rows of
     only min / max: NaN as the recipe; two values), two IFs and a window."""
     info = np.iinfo(dt)
@@ -252,6 +253,9 @@ def test_kurtosis_8bit_exact_moments(pkg, eng, orc, dt):
         a[3, 0, :nt // 2] = info.min  # a long run then noise
         x = to_dev(eng, a)
         got = eng.fb_to_numpy(eng.kurtosis(x))
+        for form in (2, 3):  # 4- and 8-byte words a lane: the same exact sums, the same bits
+            with pkg._lib.plan_option("typed_kurt", form):
+                assert same(eng.fb_to_numpy(eng.kurtosis(x)), got), (dt, nc, nt, form)
         sub = (slice(None), slice(None)) if nc * ni <= 4096 else (slice(0, 1024), slice(None))
         ex = exact_kurtosis(a[sub[0]])
         assert_kurtosis(got[sub], ex, "int", 1, (dt, nc, nt, "exact"))
@@ -265,6 +269,8 @@ def test_kurtosis_8bit_exact_moments(pkg, eng, orc, dt):
     w = [8, 960, 1, 0, 1, 1, 5, 290, 1]  # word-aligned channel span, a time window
     got = eng.fb_to_numpy(eng.kurtosis(to_dev(eng, a), w))
     assert_kurtosis(got, orc.np_kurtosis_typed(a, w), "int", 290, (dt, "window"))
+    with pkg._lib.plan_option("typed_kurt", 3):  # (8-byte aligned rows: 8-byte words)
+        assert same(eng.fb_to_numpy(eng.kurtosis(to_dev(eng, a), w)), got), (dt, "window")
 
 
 def test_worker_api_keeps_reference_types(pkg, eng, orc, tmp_path):

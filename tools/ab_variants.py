@@ -185,6 +185,20 @@ VARIANTS = {
     # k_kurt_i8 (8-bit getkurtosis, round 6): loads per batch, a wave cap
     "i8u8": {"patch": [("typed.hip", "  constexpr int U = 16;  // spectra of loads in flight per lane",
                         "  constexpr int U = 8;  // spectra of loads in flight per lane")]},
+    # probes, not candidates: the loads with a trivial fold (the read's own
+    # rate at this access shape), and S1/S2 only (half the VALU work)
+    "i8read": {"patch": [("typed.hip", "      i8_batch<SIGNED, U>(wa, ca, s1, s2, s3, s4);",
+                          "      for (int u = 0; u < U; ++u) s1[u & 3] += (int)wa[u];"),
+                         ("typed.hip", "      i8_batch<SIGNED, U>(wb, cb, s1, s2, s3, s4);",
+                          "      for (int u = 0; u < U; ++u) s1[u & 3] += (int)wb[u];")]},
+    "i8s12": {"patch": [("typed.hip", "        b3[k] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2v, qe), e, b3[k], false);\n", ""),
+                        ("typed.hip", "        b3[k] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2v, qo), o, b3[k], false);\n", ""),
+                        ("typed.hip", "        b4[k] = __builtin_amdgcn_udot2(qe, qe, b4[k], false);\n", ""),
+                        ("typed.hip", "        b4[k] = __builtin_amdgcn_udot2(qo, qo, b4[k], false);\n", "")]},
+    "i8b4": {"patch": [("typed.hip", "  constexpr int U = 8;  // spectra of loads in flight per lane",
+                        "  constexpr int U = 4;  // spectra of loads in flight per lane")]},
+    "i8b12": {"patch": [("typed.hip", "  constexpr int U = 8;  // spectra of loads in flight per lane",
+                         "  constexpr int U = 12;  // spectra of loads in flight per lane")]},
     "i8u4": {'patch': [('typed.hip', '  constexpr int U = 16;  // spectra of loads in flight per lane', '  constexpr int U = 4;  // spectra of loads in flight per lane')]},
     "i8u12": {'patch': [('typed.hip', '  constexpr int U = 16;  // spectra of loads in flight per lane', '  constexpr int U = 12;  // spectra of loads in flight per lane')]},
     "i8u8w24": {'patch': [('typed.hip', '  constexpr int U = 16;  // spectra of loads in flight per lane', '  constexpr int U = 8;  // spectra of loads in flight per lane'), ('typed.hip', 'constexpr int64_t kI8WavesPerCu = 16;', 'constexpr int64_t kI8WavesPerCu = 24;')]},

@@ -64,7 +64,7 @@ for s in $STEPS; do
       run "$s" 180 rocprofv3 --pmc $SQ --output-format csv -d "$OUT/$s" -o run \
         -- python bench.py --mode kurtosis --config "$C" --steps 20 --warmup 5 ;;
     kurtsweep)  # k_kurt_i8's grid knobs: waves per CU x shortest slab
-      for W in 12 16 24 32; do for S in 16 32 64; do
+      for W in ${KS_W:-12 16 24 32}; do for S in ${KS_S:-16 32 64}; do
         BLDP_KURT_I8_WAVES_PER_CU=$W BLDP_KURT_I8_MIN_SLAB=$S run "kurtsweep_w${W}_s$S" 300 \
           python tools/ab_variants.py --run --suite typedk --rounds 3 --variants base \
           --json "$OUT/kurtsweep_w${W}_s$S.json"
