@@ -187,14 +187,14 @@ VARIANTS = {
                         "  constexpr int U = 8;  // spectra of loads in flight per lane")]},
     # probes, not candidates: the loads with a trivial fold (the read's own
     # rate at this access shape), and S1/S2 only (half the VALU work)
-    "i8read": {"patch": [("typed.hip", "      i8_batch<SIGNED, U>(wa, ca, s1, s2, s3, s4);",
-                          "      for (int u = 0; u < U; ++u) s1[u & 3] += (int)wa[u];"),
-                         ("typed.hip", "      i8_batch<SIGNED, U>(wb, cb, s1, s2, s3, s4);",
-                          "      for (int u = 0; u < U; ++u) s1[u & 3] += (int)wb[u];")]},
-    "i8s12": {"patch": [("typed.hip", "        b3[k] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2v, qe), e, b3[k], false);\n", ""),
-                        ("typed.hip", "        b3[k] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2v, qo), o, b3[k], false);\n", ""),
-                        ("typed.hip", "        b4[k] = __builtin_amdgcn_udot2(qe, qe, b4[k], false);\n", ""),
-                        ("typed.hip", "        b4[k] = __builtin_amdgcn_udot2(qo, qo, b4[k], false);\n", "")]},
+    "i8read": {"patch": [("typed.hip", "      i8_batch<SIGNED, U, W>(wa, ca, s1, s2, s3, s4);",
+                          "      for (int u = 0; u < U; ++u) for (int j = 0; j < W; ++j) s1[(u * W + j) % (4 * W)] += (int)wa[u][j];"),
+                         ("typed.hip", "      i8_batch<SIGNED, U, W>(wb, cb, s1, s2, s3, s4);",
+                          "      for (int u = 0; u < U; ++u) for (int j = 0; j < W; ++j) s1[(u * W + j) % (4 * W)] += (int)wb[u][j];")]},
+    "i8s12": {"patch": [("typed.hip", "          s3[x] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2v, qe), e, s3[x], false);\n", ""),
+                        ("typed.hip", "          s3[x] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2v, qo), o, s3[x], false);\n", ""),
+                        ("typed.hip", "          b4[x] = __builtin_amdgcn_udot2(qe, qe, b4[x], false);\n", ""),
+                        ("typed.hip", "          b4[x] = __builtin_amdgcn_udot2(qo, qo, b4[x], false);\n", "")]},
     "i8b4": {"patch": [("typed.hip", "  constexpr int U = 8;  // spectra of loads in flight per lane",
                         "  constexpr int U = 4;  // spectra of loads in flight per lane")]},
     "i8b12": {"patch": [("typed.hip", "  constexpr int U = 8;  // spectra of loads in flight per lane",

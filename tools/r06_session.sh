@@ -48,7 +48,8 @@ for s in $STEPS; do
     benchpipe_*) run "$s" 600 python bench.py --config "${s#benchpipe_}" --pipeline --no-cpu-baseline ;;
     bench_*) run "$s" 600 python bench.py $(bench_args "${s#bench_}" | sed 's/--no-cpu-baseline//') ;;
     benchn_*) run "$s" 600 python bench.py $(bench_args "${s#benchn_}") ;;
-    cold_*) run "$s" 600 python bench.py --config "${s#cold_}" --cache cold --no-cpu-baseline ;;
+    cold_*) C=${s#cold_}; K=20; [ "${C%_k*}" != "$C" ] && K=${C##*_k} && C=${C%_k*}
+      run "$s" 600 python bench.py --config "$C" --cache cold --steps "$K" --no-cpu-baseline ;;
     prof_*) C=${s#prof_}
       run "$s" 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$s" -o run \
         -- python bench.py $(bench_args "$C") ;;
