@@ -525,7 +525,7 @@ __global__ __launch_bounds__(256) void k_kurt_typed_w(const TypedArgs a, double 
 // words (4 W channels a lane, W 32-bit words of each spectrum; 256 W
 // contiguous bytes per wave-instruction), each wave summing a time slab, the slabs added in LDS
 // (ds_add_u64), and, for long rows, time chunks of several workgroups added by
-// k_kurt_i8_final.  From the exact sums, with n the window's length:
+// k_kurt_int_final.  From the exact sums, with n the window's length:
 // the central moments n cm2 = sum((x - mu)^2), n cm4 = sum((x - mu)^4) (which
 // the shift leaves alone) re-centred exactly in Int64 and finished in Float64
 // (kurt_from_sums), and kurtosis = (cm4 / n) / (cm2 / n)^2 - 3 as StatsBase's
@@ -535,7 +535,7 @@ __global__ __launch_bounds__(256) void k_kurt_typed_w(const TypedArgs a, double 
 // at most ~150 2^-53 (tests hold the two to conftest.kurt_int_tol).  A row of
 // one value gives NaN, as the recipe.
 // Plan option "typed_kurt": 1 (default) = this path for 8-bit rows of
-// dword-aligned words, 4- or 8-byte words a lane by kurt_i8_plan's rule; 2 /
+// dword-aligned words, 4- or 8-byte words a lane by kurt_int_plan's rule; 2 /
 // 3 = 4- / 8-byte words (8: where the rows are 8-byte aligned); 0 =
 // k_kurt_typed_w (the recipe's order, bit-exact).
 struct KTM {
@@ -756,37 +756,234 @@ __global__ __launch_bounds__(1024) void k_kurt_i8(const TypedArgs a, const KTM m
   }
 }
 
+// getkurtosis of 16-bit rows (SIGPROC nbits 16) the same way: d = x - 32768
+// (UInt16) or x (Int16), |d| <= 2^15, and u = d + 32768 (the raw UInt16, or
+// an Int16 with its top bit flipped), 0 <= u < 2^16.  Per channel, a lane's
+// sums over a slab of <= 1024 spectra, every product one v_mad_u64_u32:
+//   U1 += u (UInt32), U2 += u^2, U3 += d^2 u (UInt64; d^2 by v_mul_i32_i24),
+//   S4 += d^2 d^2 (into a UInt64 per batch of 8 spectra, <= 2^63, then into a
+//        96-bit sum: UInt64 + a UInt32 carry count),
+// and at the slab's end, exactly in Int64 (m spectra, padding included: a
+// padded spectrum has d = 0)
+//   S1 = U1 - 2^15 m, S2 = U2 - 2^16 U1 + 2^30 m, S3 = U3 - 2^15 S2.
+// The slabs and chunks add S3 and S4 as two limbs of radix 2^32 (each limb's
+// sum fits 64 bits); kurt_from_limbs re-centres in Int128 (S4 <= 2^83) and
+// finishes in Float64 as kurt_from_sums does, with the same bound.
+__device__ __forceinline__ double i128_to_f64(__int128 v) {
+  // correctly rounded: the top 64 bits with a sticky bit for the rest
+  const bool neg = v < 0;
+  const unsigned __int128 u = neg ? (unsigned __int128)0 - (unsigned __int128)v
+                                  : (unsigned __int128)v;
+  const uint64_t hi = (uint64_t)(u >> 64), lo = (uint64_t)u;
+  double r;
+  if (hi == 0) {
+    r = (double)lo;
+  } else {
+    const int sh = 64 - __clzll((long long)hi);  // 1..64
+    const uint64_t mask = sh >= 64 ? ~0ull : ((1ull << sh) - 1);
+    const uint64_t top = (uint64_t)(u >> sh) | ((lo & mask) != 0);
+    r = ldexp((double)top, sh);
+  }
+  return neg ? -r : r;
+}
+
+__device__ __forceinline__ double kurt_from_limbs(int64_t n, uint64_t L1, uint64_t L2,
+                                                  uint64_t L3lo, uint64_t L3hi, uint64_t L4lo,
+                                                  uint64_t L4hi) {
+  typedef __int128 i128;
+  const int64_t S1 = (int64_t)L1;
+  const i128 S2 = (i128)L2;
+  const i128 S3 = (i128)(int64_t)L3hi * ((i128)1 << 32) + (i128)L3lo;
+  const i128 S4 = (i128)L4hi * ((i128)1 << 32) + (i128)L4lo;
+  const double dn = (double)n;
+  const int64_t c = (int64_t)rint((double)S1 / dn);  // |c| <= 2^15
+  const i128 c1 = c, c2 = c1 * c1, c3 = c2 * c1, c4 = c2 * c2, nn = n;
+  const i128 T1 = (i128)S1 - nn * c1;
+  const i128 T2 = S2 - 2 * c1 * S1 + nn * c2;
+  const i128 T3 = S3 - 3 * c1 * S2 + 3 * c2 * S1 - nn * c3;
+  const i128 T4 = S4 - 4 * c1 * S3 + 6 * c2 * S2 - 4 * c3 * S1 + nn * c4;
+  const double t1 = i128_to_f64(T1), t2 = i128_to_f64(T2), t3 = i128_to_f64(T3),
+               t4 = i128_to_f64(T4);
+  const double e = t1 / dn;
+  const double m2 = t2 - t1 * e;
+  const double m4 = t4 - e * (4.0 * t3 - e * (6.0 * t2 - 3.0 * t1 * e));
+  return dn * m4 / (m2 * m2) - 3.0;
+}
+
+// Workgroup (tile, row, chunk): 64 lanes x W words (128 W channels) of one
+// (bank x IF) row, NW waves on consecutive slabs; loads and batches as
+// k_kurt_i8.
+template <bool SIGNED, int W>
+__global__ __launch_bounds__(1024) void k_kurt_i16(const TypedArgs a, const KTM m, double *out,
+                                                   uint64_t *ws) {
+  constexpr int U = 8;      // spectra of loads in flight per lane (and as many prefetched)
+  constexpr int C = 2 * W;  // channels a lane
+  typedef uint32_t wv_t __attribute__((ext_vector_type(W)));
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t ngl = a.nco / C, tile = blockIdx.x, r = blockIdx.y, chunk = blockIdx.z;
+  const int64_t q = tile * 64 + lane;  // this lane's words
+  const int64_t i = r % a.ni, bank = r / a.ni;
+  const int64_t ct0 = chunk * m.crow, ct1 = min(a.nto, ct0 + m.crow);
+  const int64_t t0 = min(ct1, ct0 + (int64_t)wave * m.srow), t1 = min(ct1, t0 + m.srow);
+  uint32_t u1[C], s4c[C];
+  uint64_t u2[C], u3[C], s4[C];
+#pragma unroll
+  for (int k = 0; k < C; ++k) u1[k] = 0, u2[k] = 0, u3[k] = 0, s4[k] = 0, s4c[k] = 0;
+  int64_t m_rows = 0;  // spectra summed, padding included
+  if (q < ngl && t1 > t0) {
+    const int64_t ldb = 2 * a.in_ld_t;  // bytes
+    const char *base = static_cast<const char *>(a.in[bank]) + 2 * (a.in_off + i * a.in_ld_i) +
+                       256 * W * tile;
+    const uint32_t lofs = 4u * W * (uint32_t)lane;
+    const int last = (int)(t1 - 1);
+    auto load = [&](uint32_t (&w)[U][W], int64_t t) {
+      const int t32 = __builtin_amdgcn_readfirstlane((int)t);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint64_t ro = (uint64_t)((int64_t)min(t32 + u, last) * ldb);
+        const uint64_t rs = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(ro >> 32)) << 32) |
+                            __builtin_amdgcn_readfirstlane((uint32_t)ro);
+        const wv_t v = __builtin_nontemporal_load(reinterpret_cast<const wv_t *>(base + rs + lofs));
+#pragma unroll
+        for (int j = 0; j < W; ++j) w[u][j] = v[j];
+      }
+    };
+    auto batch = [&](uint32_t (&w)[U][W], int cnt) {
+      if (cnt < U) {  // (uniform: only a slab's last batch)
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int j = 0; j < W; ++j)
+            if (u >= cnt) w[u][j] = SIGNED ? 0u : 0x80008000u;  // (d = 0)
+      }
+      m_rows += U;
+      uint64_t p4[C];
+#pragma unroll
+      for (int k = 0; k < C; ++k) p4[k] = 0;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+          const uint32_t x = SIGNED ? w[u][j] ^ 0x80008000u : w[u][j];  // two u
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int k = 2 * j + h;
+            const uint32_t uu = h ? x >> 16 : x & 0xffffu;
+            const int32_t d = (int32_t)uu - 32768;
+            const uint32_t dd = (uint32_t)(d * d);  // <= 2^30 (v_mul_i32_i24)
+            u1[k] += uu;
+            u2[k] += (uint64_t)uu * uu;
+            u3[k] += (uint64_t)dd * uu;
+            p4[k] += (uint64_t)dd * dd;
+          }
+        }
+#pragma unroll
+      for (int k = 0; k < C; ++k) {
+        s4[k] += p4[k];
+        s4c[k] += s4[k] < p4[k];  // (the carry out of the 64-bit sum)
+      }
+    };
+    auto count = [&](int64_t t) { return (int)max((int64_t)0, min((int64_t)U, t1 - t)); };
+    uint32_t wa[U][W], wb[U][W];
+    int64_t t = t0;
+    load(wa, t);
+    for (;;) {
+      const int ca = count(t), cb = count(t + U);
+      load(wb, t + U);
+      batch(wa, ca);
+      if (cb == 0) break;
+      load(wa, t + 2 * U);
+      batch(wb, cb);
+      if (count(t + 2 * U) == 0) break;
+      t += 2 * U;
+    }
+  }
+  // the slab's central sums (exact in Int64), added in LDS as 6 limbs (S1,
+  // S2, S3 low / high 32 bits, S4 low / high 32 bits; the signed limbs in
+  // two's complement)
+  int64_t s1[C], s3[C];
+  uint64_t s2[C];
+#pragma unroll
+  for (int k = 0; k < C; ++k) {
+    s1[k] = (int64_t)u1[k] - ((int64_t)m_rows << 15);
+    s2[k] = u2[k] - ((uint64_t)u1[k] << 16) + ((uint64_t)m_rows << 30);
+    s3[k] = (int64_t)(u3[k] - (s2[k] << 15));
+  }
+  __shared__ unsigned long long acc[6][C][64];
+  for (int e = threadIdx.x; e < 6 * C * 64; e += blockDim.x) (&acc[0][0][0])[e] = 0ull;
+  __syncthreads();
+  if (q < ngl && t1 > t0) {
+#pragma unroll
+    for (int k = 0; k < C; ++k) {
+      atomicAdd(&acc[0][k][lane], (unsigned long long)s1[k]);
+      atomicAdd(&acc[1][k][lane], (unsigned long long)s2[k]);
+      atomicAdd(&acc[2][k][lane], (unsigned long long)(uint32_t)s3[k]);
+      atomicAdd(&acc[3][k][lane], (unsigned long long)(s3[k] >> 32));
+      atomicAdd(&acc[4][k][lane], (unsigned long long)(uint32_t)s4[k]);
+      atomicAdd(&acc[5][k][lane], (unsigned long long)((s4[k] >> 32) + ((uint64_t)s4c[k] << 32)));
+    }
+  }
+  __syncthreads();
+  for (int ch = threadIdx.x; ch < 64 * C; ch += blockDim.x) {
+    const int64_t c = tile * 64 * C + ch;  // this workgroup's channels, coalesced
+    const int l = ch / C, k = ch % C;  // (lane, channel of the lane)
+    if (c < a.nco) {
+      if (m.nchunk == 1) {
+        out[c + a.nco * r] = kurt_from_limbs(a.nto, acc[0][k][l], acc[1][k][l], acc[2][k][l],
+                                             acc[3][k][l], acc[4][k][l], acc[5][k][l]);
+      } else {
+        const int64_t rows = a.ni * a.nbank;
+#pragma unroll
+        for (int s = 0; s < 6; ++s) ws[((chunk * 6 + s) * rows + r) * a.nco + c] = acc[s][k][l];
+      }
+    }
+  }
+}
+
 // The chunks' sums of every channel added (exact: sums mod 2^64 in any
-// order), then the kurtosis (nchunk > 1).  Workgroup: 64 consecutive
-// channels x 16 waves, wave w adding chunks w, w + 16, ... (the 0001 product:
-// 512 channels of 100+ chunks -- one thread a channel walking the chunks in
-// turn paid a dependent load per chunk, ~0.26 us each).
-__global__ __launch_bounds__(1024) void k_kurt_i8_final(const TypedArgs a, const KTM m,
-                                                        double *out, const uint64_t *ws) {
+// order), then the kurtosis (nchunk > 1).  NS = 4 (k_kurt_i8: S1..S4) or 6
+// (k_kurt_i16: S1, S2 and S3, S4 as two 32-bit-radix limbs).  Workgroup: 64
+// consecutive channels x 16 waves, wave w adding chunks w, w + 16, ... (the
+// 0001 product: 512 channels of 100+ chunks -- one thread a channel walking
+// the chunks in turn paid a dependent load per chunk, ~0.26 us each).
+template <int NS>
+__global__ __launch_bounds__(1024) void k_kurt_int_final(const TypedArgs a, const KTM m,
+                                                         double *out, const uint64_t *ws) {
   const int64_t rows = a.ni * a.nbank, n = a.nco * rows;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t e = (int64_t)blockIdx.x * 64 + lane;
-  uint64_t S[4] = {0, 0, 0, 0};
+  uint64_t S[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) S[s] = 0;
   if (e < n)
     for (int64_t c = wave; c < m.nchunk; c += 16)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) S[s] += ws[(c * 4 + s) * n + e];
-  __shared__ unsigned long long acc[4][64];
-  if (threadIdx.x < 256) (&acc[0][0])[threadIdx.x] = 0ull;
+      for (int s = 0; s < NS; ++s) S[s] += ws[(c * NS + s) * n + e];
+  __shared__ unsigned long long acc[NS][64];
+  if (threadIdx.x < NS * 64) (&acc[0][0])[threadIdx.x] = 0ull;
   __syncthreads();
 #pragma unroll
-  for (int s = 0; s < 4; ++s) atomicAdd(&acc[s][lane], (unsigned long long)S[s]);
+  for (int s = 0; s < NS; ++s) atomicAdd(&acc[s][lane], (unsigned long long)S[s]);
   __syncthreads();
-  if (wave == 0 && e < n)
-    out[e] = kurt_from_sums(a.nto, (int64_t)acc[0][lane], acc[1][lane], (int64_t)acc[2][lane],
-                            acc[3][lane]);
+  if (wave == 0 && e < n) {
+    if constexpr (NS == 4)
+      out[e] = kurt_from_sums(a.nto, (int64_t)acc[0][lane], acc[1][lane], (int64_t)acc[2][lane],
+                              acc[3][lane]);
+    else
+      out[e] = kurt_from_limbs(a.nto, acc[0][lane], acc[1][lane], acc[2][lane], acc[3][lane],
+                               acc[4][lane], acc[5][lane]);
+  }
 }
 
-// The k_kurt_i8 geometry, or false when the path does not apply.
-bool kurt_i8_plan(const TypedArgs &a, KTM *m) {
-  if (dtype_size(a.dtype) != 1 || !opt(OPT_TYPED_KURT)) return false;
-  if (a.in_cs != 1 || a.nco % 4 || a.nto < 1 || a.nto > kI8MaxN) return false;
-  if (a.in_off % 4 || (a.ni > 1 && a.in_ld_i % 4) || (a.nto > 1 && a.in_ld_t % 4)) return false;
+// The k_kurt_i8 / k_kurt_i16 geometry, or false when the path does not
+// apply.
+bool kurt_int_plan(const TypedArgs &a, KTM *m) {
+  const int64_t es = (int64_t)dtype_size(a.dtype), cpw = 4 / std::max<int64_t>(1, es);
+  if ((es != 1 && es != 2) || !opt(OPT_TYPED_KURT)) return false;
+  if (a.in_cs != 1 || a.nco % cpw || a.nto < 1 || a.nto > kI8MaxN) return false;
+  // (byte offsets of the window and its rows)
+  const int64_t off = a.in_off * es, ldi = a.in_ld_i * es, ldt = a.in_ld_t * es;
+  if (off % 4 || (a.ni > 1 && ldi % 4) || (a.nto > 1 && ldt % 4)) return false;
   for (int b = 0; b < a.nbank; ++b)
     if ((uintptr_t)a.in[b] % 4) return false;
   const int64_t rows = a.ni * a.nbank;
@@ -797,25 +994,25 @@ bool kurt_i8_plan(const TypedArgs &a, KTM *m) {
   if (const char *e = getenv("BLDP_KURT_I8_MIN_SLAB"))
     min_slab = std::min<int64_t>(4096, std::max<int64_t>(8, atoi(e)));
   const int64_t want = per_cu * (int64_t)std::max(1, a.num_cus);
-  // 8-byte loads (8 channels a lane: 512 contiguous bytes a wave-load) where
+  // 8-byte loads (2 words a lane: 512 contiguous bytes a wave-load) where
   // every row start is 8-byte aligned and the tiles alone, cut into slabs,
-  // fill the round (the 0002 band: 1024 tiles, 30.8 vs 33.4 us); 4-byte
-  // loads otherwise (one 0002 file: 128 tiles of 8 channels a lane, 12.1 vs
-  // 8.6 us; profiles/r06/kurtsweep_r06m.json)
-  bool w2a = a.nco % 8 == 0 && a.in_off % 8 == 0 && (a.ni == 1 || a.in_ld_i % 8 == 0) &&
-             (a.nto == 1 || a.in_ld_t % 8 == 0);
+  // fill the round (the UInt8 0002 band: 1024 tiles, 30.8 vs 33.4 us); 4-byte
+  // loads otherwise (one UInt8 0002 file: 128 tiles of 8 channels a lane,
+  // 12.1 vs 8.6 us; profiles/r06/kurtsweep_r06m.json)
+  bool w2a = a.nco % (2 * cpw) == 0 && off % 8 == 0 && (a.ni == 1 || ldi % 8 == 0) &&
+             (a.nto == 1 || ldt % 8 == 0);
   for (int b = 0; w2a && b < a.nbank; ++b) w2a = (uintptr_t)a.in[b] % 8 == 0;
-  const bool w2 =
-      w2a && cdivt(a.nco / 8, 64) * rows * std::min<int64_t>(16, cdivt(a.nto, min_slab)) >= want;
+  const bool w2 = w2a && cdivt(a.nco / (2 * cpw), 64) * rows *
+                                 std::min<int64_t>(16, cdivt(a.nto, min_slab)) >= want;
   const int64_t form = opt(OPT_TYPED_KURT);  // 1: by the rule, 2: 4-byte, 3: 8-byte words
   m->wpl = (form == 1 && w2) || (form == 3 && w2a) ? 2 : 1;
-  m->ntile = cdivt(a.nco / (4 * m->wpl), 64);
+  m->ntile = cdivt(a.nco / (cpw * m->wpl), 64);
   // waves for one round of kI8WavesPerCu: NW waves a tile (<= 16,
   // never slabs under 16 spectra), then time chunks while the tiles still
   // leave the CUs short (0001: 512 channels = 2 tiles a row, ~10^6 spectra),
-  // and never slabs over 1024 (the lanes' 32-bit sums of d^3).  The 0002
-  // band: 1024 tiles x 4 waves of 70 spectra; one 0002 file: 256 tiles x 16
-  // waves of 18
+  // and never slabs over 1024 (the lanes' 32-bit sums).  The UInt8 0002
+  // band: 1024 tiles x 4 waves of 70 spectra; one UInt8 0002 file: 256 tiles
+  // x 16 waves of 18
   const int64_t tiles = m->ntile * rows;
   m->nw = (int)std::max<int64_t>(1, std::min<int64_t>({16, cdivt(want, tiles),
                                                        cdivt(a.nto, min_slab)}));
@@ -932,19 +1129,28 @@ hipError_t launch_typed_op(const TypedArgs &a, int op, hipStream_t s) {
 template <typename TI>
 hipError_t launch_kurt_t(const TypedArgs &a, double *out, hipStream_t s) {
   const int64_t n = a.nco * a.ni * a.nbank;
-  if constexpr (sizeof(TI) == 1) {  // exact integer moments (k_kurt_i8)
+  if constexpr (sizeof(TI) <= 2 && std::is_integral<TI>::value) {
+    // exact integer moments (k_kurt_i8 / k_kurt_i16)
     KTM m;
-    if (kurt_i8_plan(a, &m) && (m.nchunk == 1 || a.ws)) {
+    if (kurt_int_plan(a, &m) && (m.nchunk == 1 || a.ws)) {
       const dim3 g((unsigned)m.ntile, (unsigned)(a.ni * a.nbank), (unsigned)m.nchunk);
       uint64_t *ws = static_cast<uint64_t *>(a.ws);
       constexpr bool sg = std::is_signed<TI>::value;
-      if (m.wpl == 2)
-        hipLaunchKernelGGL((k_kurt_i8<sg, 2>), g, dim3(64 * m.nw), 0, s, a, m, out, ws);
-      else
-        hipLaunchKernelGGL((k_kurt_i8<sg, 1>), g, dim3(64 * m.nw), 0, s, a, m, out, ws);
+      constexpr int ns = sizeof(TI) == 1 ? 4 : 6;
+      if constexpr (sizeof(TI) == 1) {
+        if (m.wpl == 2)
+          hipLaunchKernelGGL((k_kurt_i8<sg, 2>), g, dim3(64 * m.nw), 0, s, a, m, out, ws);
+        else
+          hipLaunchKernelGGL((k_kurt_i8<sg, 1>), g, dim3(64 * m.nw), 0, s, a, m, out, ws);
+      } else {
+        if (m.wpl == 2)
+          hipLaunchKernelGGL((k_kurt_i16<sg, 2>), g, dim3(64 * m.nw), 0, s, a, m, out, ws);
+        else
+          hipLaunchKernelGGL((k_kurt_i16<sg, 1>), g, dim3(64 * m.nw), 0, s, a, m, out, ws);
+      }
       if (m.nchunk > 1)
-        hipLaunchKernelGGL(k_kurt_i8_final, dim3((unsigned)cdivt(n, 64)), dim3(1024), 0, s, a, m,
-                           out, ws);
+        hipLaunchKernelGGL(k_kurt_int_final<ns>, dim3((unsigned)cdivt(n, 64)), dim3(1024), 0, s,
+                           a, m, out, ws);
       return hipGetLastError();
     }
   }
@@ -968,8 +1174,9 @@ hipError_t launch_kurt_t(const TypedArgs &a, double *out, hipStream_t s) {
 
 size_t kurtosis_typed_ws_bytes(const TypedArgs &a) {
   KTM m;
-  if (!kurt_i8_plan(a, &m) || m.nchunk == 1) return 0;
-  return (size_t)m.nchunk * 4 * (size_t)(a.ni * a.nbank * a.nco) * sizeof(uint64_t);
+  if (!kurt_int_plan(a, &m) || m.nchunk == 1) return 0;
+  const size_t ns = dtype_size(a.dtype) == 1 ? 4 : 6;  // sums a channel
+  return (size_t)m.nchunk * ns * (size_t)(a.ni * a.nbank * a.nco) * sizeof(uint64_t);
 }
 
 size_t dtype_size(int dtype) {

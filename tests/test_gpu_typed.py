@@ -64,10 +64,11 @@ def same(got, want):
 
 
 def kurt_same(got, want, dt, nt, msg=""):
-    """Typed getkurtosis against the recipe: 8-bit rows take k_kurt_i8 (exact
-    integer moments), within conftest.kurt_int_tol(nt) of it; every other type
-    follows the recipe's sequence, bit for bit."""
-    if np.dtype(dt).itemsize == 1:
+    """Typed getkurtosis against the recipe: 8- and 16-bit rows take
+    k_kurt_i8 / k_kurt_i16 (exact integer moments), within
+    conftest.kurt_int_tol(nt) of it; every other type follows the recipe's
+    sequence, bit for bit."""
+    if np.dtype(dt).itemsize <= 2:
         assert np.asarray(got).dtype == np.asarray(want).dtype
         assert_kurtosis(got, want, "int", nt, msg)
     else:
@@ -75,18 +76,27 @@ def kurt_same(got, want, dt, nt, msg=""):
 
 
 def exact_kurtosis(a):
-    """The exact excess kurtosis of every (channel, IF) row of an 8-bit
-    array, rounded once: power sums in Int64 (exact for these types), then
-    Python integers, X / Y^2 - 3 with Y = n S2 - S1^2,
-    X = n^3 S4 - 4 n^2 S1 S3 + 6 n S1^2 S2 - 3 S1^4 (typed.hip k_kurt_i8)."""
+    """The exact excess kurtosis of every (channel, IF) row of an 8- or
+    16-bit array, rounded once: power sums of d = x - centre (|d| <= 2^15),
+    exact (d^2 = a 2^15 + b split so every Int64 sum stays below 2^63, the
+    parts joined as Python integers), then X / Y^2 - 3 with Y = n S2 - S1^2,
+    X = n^3 S4 - 4 n^2 S1 S3 + 6 n S1^2 S2 - 3 S1^4 (typed.hip k_kurt_i8 /
+    k_kurt_i16; the kurtosis does not depend on the centre)."""
     from fractions import Fraction
 
-    v = a.astype(np.int64)
+    info = np.iinfo(a.dtype)
+    d = a.astype(np.int64) - (info.min + info.max + 1) // 2
     n = a.shape[2]
-    S = [(v ** k).sum(axis=2) for k in (1, 2, 3, 4)]
+    q = d * d
+    hi, lo = q >> 15, q & 0x7FFF
+    S1, S2 = d.sum(axis=2), q.sum(axis=2)
+    S3h, S3l = (hi * d).sum(axis=2), (lo * d).sum(axis=2)
+    S4a, S4b, S4c = (hi * hi).sum(axis=2), (2 * hi * lo).sum(axis=2), (lo * lo).sum(axis=2)
     out = np.empty(a.shape[:2])
     for idx in np.ndindex(*a.shape[:2]):
-        s1, s2, s3, s4 = (int(x[idx]) for x in S)
+        s1, s2 = int(S1[idx]), int(S2[idx])
+        s3 = (int(S3h[idx]) << 15) + int(S3l[idx])
+        s4 = (int(S4a[idx]) << 30) + (int(S4b[idx]) << 15) + int(S4c[idx])
         y = n * s2 - s1 * s1
         x = n ** 3 * s4 - 4 * n * n * s1 * s3 + 6 * n * s1 * s1 * s2 - 3 * s1 ** 4
         out[idx] = np.nan if y == 0 else float(Fraction(x, y * y) - 3)
@@ -208,10 +218,9 @@ def test_kurtosis_typed_words(pkg, eng, orc, dt):
     option typed_kurt = 0): bit-identical to the one-lane-per-channel kernel
     (plan option typed_vec = 0) and to the oracle; the type's full range,
     spectrum counts around the 16-spectrum batches, two IFs, a channel window
-    on a word boundary and one off it (the fallback).  8-bit rows by default
-    take k_kurt_i8, held to kurt_int_tol."""
+    on a word boundary and one off it (the fallback).  By default these rows
+    take k_kurt_i8 / k_kurt_i16, held to kurt_int_tol."""
     info = np.iinfo(dt)
-    one = np.dtype(dt).itemsize == 1
     for k, (nc, ni, nt) in enumerate([(256, 2, 1000), (1024, 1, 77), (64, 1, 16), (128, 3, 15)]):
         rng = np.random.default_rng(k + np.dtype(dt).num)
         a = np.asfortranarray(rng.integers(info.min, info.max, (nc, ni, nt), endpoint=True)
@@ -225,18 +234,17 @@ def test_kurtosis_typed_words(pkg, eng, orc, dt):
             assert same(rec, want), (dt, (nc, ni, nt))
             with pkg._lib.plan_option("typed_vec", 0):
                 assert same(eng.fb_to_numpy(eng.kurtosis(x)), rec), (dt, (nc, ni, nt))
-        if not one:
-            assert same(got, rec)
         for w in ([4, nc - 8, 1, 0, ni, 1, 3, nt - 3, 1], [1, nc - 4, 1, 0, ni, 1, 0, nt, 1]):
             kurt_same(eng.fb_to_numpy(eng.kurtosis(x, w)), orc.np_kurtosis_typed(a, w), dt,
                       w[7], (dt, (nc, ni, nt), w))
 
 
-@pytest.mark.parametrize("dt", [np.uint8, np.int8], ids=lambda d: np.dtype(d).name)
-def test_kurtosis_8bit_exact_moments(pkg, eng, orc, dt):
-    """k_kurt_i8 (8-bit getkurtosis from exact integer power sums, time split
-    over waves and, for long rows, over workgroups whose sums a second kernel
-    adds): within conftest.KURT_INT_FINISH (relative on k + 3) of the exactly
+@pytest.mark.parametrize("dt", [np.uint8, np.int8, np.uint16, np.int16],
+                         ids=lambda d: np.dtype(d).name)
+def test_kurtosis_int_exact_moments(pkg, eng, orc, dt):
+    """k_kurt_i8 / k_kurt_i16 (8- and 16-bit getkurtosis from exact integer
+    power sums, time split over waves and, for long rows, over workgroups
+    whose sums a second kernel adds): within conftest.KURT_INT_FINISH (relative on k + 3) of the exactly
     rounded kurtosis (Python integers), and within kurt_int_tol(nt) of the
     recipe (oracle); 4- and 8-byte words a lane (plan option typed_kurt 2 / 3)
     bit-identical.  The 0002 file geometry, one and several time chunks
@@ -256,7 +264,8 @@ def test_kurtosis_8bit_exact_moments(pkg, eng, orc, dt):
         for form in (2, 3):  # 4- and 8-byte words a lane: the same exact sums, the same bits
             with pkg._lib.plan_option("typed_kurt", form):
                 assert same(eng.fb_to_numpy(eng.kurtosis(x)), got), (dt, nc, nt, form)
-        sub = (slice(None), slice(None)) if nc * ni <= 4096 else (slice(0, 1024), slice(None))
+        csub = max(8, min(nc, 1024, 4_000_000 // (nt * ni)))  # (rows the exact check takes)
+        sub = (slice(0, csub), slice(None))
         ex = exact_kurtosis(a[sub[0]])
         assert_kurtosis(got[sub], ex, "int", 1, (dt, nc, nt, "exact"))
         fin = np.isfinite(ex)

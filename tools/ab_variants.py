@@ -617,6 +617,10 @@ def run(names, rounds, iters, suite="main"):
         typedk_case("i8 0002 band kurtosis", a8.view(np.int8), 6)
         a1 = rng.integers(0, 256, (200000, 1, 512), dtype=np.uint8)
         typedk_case("u8 0001-like (512 ch x 200000) kurtosis", a1, 2)
+        del a1, a8
+        a16 = rng.integers(0, 65536, (279, 1, 65536 * 8), dtype=np.uint16)
+        typedk_case("u16 0002 band kurtosis", a16, 3)
+        typedk_case("u16 0002 file kurtosis", np.ascontiguousarray(a16[:, :, :65536]), 3)
         cases_done = True
     elif suite == "il1":  # large groups with short time blocks: interleaved vs wave kernel
         for F, T in ((1024, 1), (512, 1), (2048, 1), (4096, 1), (1024, 2), (1024, 4)):
