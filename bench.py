@@ -621,7 +621,8 @@ def rendezvous_check(args, dist, rank, world):
 
 def bench_typed(args, eng, torch, pkg):
     """fqav and getkurtosis on 8-bit SIGPROC data (the reference's UInt8
-    arrays, Blio nbits 8; src/gbtworkerfunctions.jl:173-174,197-202) at the
+    arrays, Blio nbits 8; src/gbtworkerfunctions.jl:173-174,197-202; and
+    nbits 16, UInt16, beside it) at the
     0002 geometry: one file (65536 ch x 1 IF x 279 spectra) and the 8-file
     band, fqavby=64, sum (UInt64 results), and the kurtosis of the same data.
     Each call is prepared once per buffer (bldp_reduce_prepare /
@@ -637,8 +638,10 @@ def bench_typed(args, eng, torch, pkg):
     out = {}
     HipEvent = pkg._lib.HipEvent
     sp = int(torch.cuda.current_stream().cuda_stream)
-    for label, nb in (("0002 file", 1), ("0002 band", 8)):
-        a = rng.integers(0, 256, (279, 1, 65536 * nb), dtype=np.uint8)  # C order [t][i][c]
+    for label, nb, dt in (("0002 file", 1, np.uint8), ("0002 band", 8, np.uint8),
+                          ("0002 file u16", 1, np.uint16), ("0002 band u16", 8, np.uint16)):
+        # C order [t][i][c]; UInt16: SIGPROC nbits 16
+        a = rng.integers(0, np.iinfo(dt).max, (279, 1, 65536 * nb), dtype=dt, endpoint=True)
         ncopy = cold_copies(args.cache, a.nbytes)  # cold: calls rotate over >= 1 GiB of copies
         xs = [torch.from_numpy(a).cuda().permute(2, 1, 0)  # Julia-order (65536*nb, 1, 279)
               for _ in range(ncopy)]

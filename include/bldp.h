@@ -337,7 +337,7 @@ BLDP_API int bldp_reduce_strided(int dtype, const void *in, int64_t nchan, int64
                                  void *stream);
 /* getkurtosis for any bldp_dtype (StatsBase's recipe; Float64 arithmetic for
  * integer and Float64 rows: Base.sum's pairwise Float64 mean, sequential
- * moments; 8-bit rows from exact integer power sums, within 160 2^-53 of
+ * moments; 8- and 16-bit rows from exact integer power sums, within 160 2^-53 of
  * the exactly rounded kurtosis and (3 nt + 175) 2^-53 relative of the
  * recipe on k + 3, plan option "typed_kurt").  out
  * (nc, ni) float64 on the device.  Asynchronous. */

@@ -199,6 +199,11 @@ VARIANTS = {
                         "  constexpr int U = 4;  // spectra of loads in flight per lane")]},
     "i8b12": {"patch": [("typed.hip", "  constexpr int U = 8;  // spectra of loads in flight per lane",
                          "  constexpr int U = 12;  // spectra of loads in flight per lane")]},
+    # k_kurt_i16 (16-bit getkurtosis, round 6)
+    "i16w1": {"patch": [("typed.hip", "  m->wpl = (form == 1 && w2) || (form == 3 && w2a) ? 2 : 1;",
+                         "  m->wpl = (form == 1 && w2 && es == 1) || (form == 3 && w2a) ? 2 : 1;")]},
+    "i16u8": {"patch": [("typed.hip", '  constexpr int U = 4;  // spectra of loads in flight per lane (and as many prefetched; 8: one', '  constexpr int U = 8;  // spectra of loads in flight per lane (and as many prefetched; 8: one')]},
+    "i16u16": {"patch": [("typed.hip", '  constexpr int U = 4;  // spectra of loads in flight per lane (and as many prefetched; 8: one', '  constexpr int U = 16;  // spectra of loads in flight per lane (and as many prefetched; 8: one')]},
     "i8u4": {'patch': [('typed.hip', '  constexpr int U = 16;  // spectra of loads in flight per lane', '  constexpr int U = 4;  // spectra of loads in flight per lane')]},
     "i8u12": {'patch': [('typed.hip', '  constexpr int U = 16;  // spectra of loads in flight per lane', '  constexpr int U = 12;  // spectra of loads in flight per lane')]},
     "i8u8w24": {'patch': [('typed.hip', '  constexpr int U = 16;  // spectra of loads in flight per lane', '  constexpr int U = 8;  // spectra of loads in flight per lane'), ('typed.hip', 'constexpr int64_t kI8WavesPerCu = 16;', 'constexpr int64_t kI8WavesPerCu = 24;')]},
