@@ -366,7 +366,8 @@ def test_prepared_reduce_and_kurtosis(pkg, eng, dt):
             np.array_equal(got, want, equal_nan=got.dtype.kind == "f")
 
     for nc, ni, nt, F, T, win in ((4096, 1, 279, 64, 1, None), (1000, 2, 40, 8, 4, None),
-                                  (512, 1, 70, 4, 7, [8, 480, 1, 0, 1, 1, 0, 70, 1])):
+                                  (512, 1, 70, 4, 7, [8, 480, 1, 0, 1, 1, 0, 70, 1]),
+                                  (512, 1, 20000, 8, 16, None)):  # (long rows: time chunks)
         a = rand(dt, (nc, ni, nt), seed=nc + nt)
         x = to_dev(eng, a)
         for op in ("sum", "max"):
