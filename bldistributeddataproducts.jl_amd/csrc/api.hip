@@ -530,6 +530,7 @@ int run_prepared(bldp_reduce_op_t h, hipStream_t s) {
         const int rc = scratch_lease(s, wsb, &lease);
         if (rc) return rc;
         t.ws = lease.ptr;
+        t.ws_bytes = wsb;
       }
       const hipError_t e = launch_kurtosis_typed(t, h->kout, s);
       return e == hipSuccess ? BLDP_OK
@@ -973,6 +974,7 @@ int bldp_kurtosis(int dtype, const void *in, int64_t nchan, int64_t nif, int64_t
     rc = scratch_lease((hipStream_t)stream, wsb, &lease);
     if (rc) return rc;
     a.ws = lease.ptr;
+    a.ws_bytes = wsb;
   }
   hipError_t e = launch_kurtosis_typed(a, out, (hipStream_t)stream);
   if (e != hipSuccess) return fail(BLDP_EHIP, "typed kurtosis launch: %s", hipGetErrorString(e));

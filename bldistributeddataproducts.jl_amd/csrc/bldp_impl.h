@@ -194,6 +194,8 @@ struct TypedArgs {
   int64_t nco, ni, nto, F, T;
   int32_t num_cus;  // of the launch's device (the coalesced kernel's grid)
   void *ws;         // typed kurtosis: kurtosis_typed_ws_bytes of scratch (or null)
+  size_t ws_bytes;  // its size (the launch re-plans and checks it: plan options are
+                    // process-wide, so another thread may change them in between)
 };
 size_t dtype_size(int dtype);              // 0 = unknown
 int typed_out_dtype(int dtype, int op);    // -1 = invalid

@@ -988,12 +988,15 @@ bool kurt_int_plan(const TypedArgs &a, KTM *m) {
   for (int b = 0; b < a.nbank; ++b)
     if ((uintptr_t)a.in[b] % 4) return false;
   const int64_t rows = a.ni * a.nbank;
-  int64_t per_cu = kI8WavesPerCu;  // (BLDP_KURT_I8_WAVES_PER_CU: a probe knob, 4..64)
-  if (const char *e = getenv("BLDP_KURT_I8_WAVES_PER_CU"))
-    per_cu = std::min<int64_t>(64, std::max<int64_t>(4, atoi(e)));
-  int64_t min_slab = kI8MinSlab;  // (BLDP_KURT_I8_MIN_SLAB: a probe knob, 8..4096)
-  if (const char *e = getenv("BLDP_KURT_I8_MIN_SLAB"))
-    min_slab = std::min<int64_t>(4096, std::max<int64_t>(8, atoi(e)));
+  // (probe knobs, read once: BLDP_KURT_I8_WAVES_PER_CU 4..64, BLDP_KURT_I8_MIN_SLAB 8..4096)
+  static const int64_t per_cu = [] {
+    const char *e = getenv("BLDP_KURT_I8_WAVES_PER_CU");
+    return e ? std::min<int64_t>(64, std::max<int64_t>(4, atoi(e))) : kI8WavesPerCu;
+  }();
+  static const int64_t min_slab = [] {
+    const char *e = getenv("BLDP_KURT_I8_MIN_SLAB");
+    return e ? std::min<int64_t>(4096, std::max<int64_t>(8, atoi(e))) : kI8MinSlab;
+  }();
   const int64_t want = per_cu * (int64_t)std::max(1, a.num_cus);
   // 8-byte loads (2 words a lane: 512 contiguous bytes a wave-load) where
   // every row start is 8-byte aligned and the tiles alone, cut into slabs,
@@ -1026,6 +1029,12 @@ bool kurt_int_plan(const TypedArgs &a, KTM *m) {
   m->crow = m->srow * m->nw;
   m->nchunk = cdivt(a.nto, m->crow);
   return m->ntile <= INT32_MAX && rows <= 65535 && m->nchunk <= 65535;
+}
+
+// Scratch for a chunked plan's partial sums: NS UInt64 a channel a chunk.
+size_t kurt_int_ws_bytes(const TypedArgs &a, const KTM &m) {
+  const size_t ns = dtype_size(a.dtype) == 1 ? 4 : 6;  // sums a channel
+  return (size_t)m.nchunk * ns * (size_t)(a.ni * a.nbank * a.nco) * sizeof(uint64_t);
 }
 
 // The coalesced kernel's geometry for this window, or false when it does not
@@ -1133,7 +1142,9 @@ hipError_t launch_kurt_t(const TypedArgs &a, double *out, hipStream_t s) {
   if constexpr (sizeof(TI) <= 2 && std::is_integral<TI>::value) {
     // exact integer moments (k_kurt_i8 / k_kurt_i16)
     KTM m;
-    if (kurt_int_plan(a, &m) && (m.nchunk == 1 || a.ws)) {
+    // (chunked: only into scratch the caller sized for this same plan)
+    if (kurt_int_plan(a, &m) &&
+        (m.nchunk == 1 || (a.ws && kurt_int_ws_bytes(a, m) <= a.ws_bytes))) {
       const dim3 g((unsigned)m.ntile, (unsigned)(a.ni * a.nbank), (unsigned)m.nchunk);
       uint64_t *ws = static_cast<uint64_t *>(a.ws);
       constexpr bool sg = std::is_signed<TI>::value;
@@ -1176,8 +1187,7 @@ hipError_t launch_kurt_t(const TypedArgs &a, double *out, hipStream_t s) {
 size_t kurtosis_typed_ws_bytes(const TypedArgs &a) {
   KTM m;
   if (!kurt_int_plan(a, &m) || m.nchunk == 1) return 0;
-  const size_t ns = dtype_size(a.dtype) == 1 ? 4 : 6;  // sums a channel
-  return (size_t)m.nchunk * ns * (size_t)(a.ni * a.nbank * a.nco) * sizeof(uint64_t);
+  return kurt_int_ws_bytes(a, m);
 }
 
 size_t dtype_size(int dtype) {
