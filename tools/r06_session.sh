@@ -64,6 +64,11 @@ for s in $STEPS; do
     kurtsq_*) C=${s#kurtsq_}
       run "$s" 180 rocprofv3 --pmc $SQ --output-format csv -d "$OUT/$s" -o run \
         -- python bench.py --mode kurtosis --config "$C" --steps 20 --warmup 5 ;;
+    gloo_*)  # N ranks sharing the one GPU over gloo (the driver's N-GPU path, exchange and
+             # self-check included; REHEARSAL, not a scaling number): gloo_N_CFG
+      A=${s#gloo_}; N=${A%%_*}; C=${A#*_}
+      run "$s" 600 python bench.py --gpus "$N" --dist-backend gloo --config "$C" --steps 10 \
+        --warmup 3 --no-cpu-baseline ;;
     kurtsweep)  # k_kurt_i8's grid knobs: waves per CU x shortest slab
       for W in ${KS_W:-12 16 24 32}; do for S in ${KS_S:-16 32 64}; do
         BLDP_KURT_I8_WAVES_PER_CU=$W BLDP_KURT_I8_MIN_SLAB=$S run "kurtsweep_w${W}_s$S" 300 \
