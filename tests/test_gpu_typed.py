@@ -252,13 +252,16 @@ def test_kurtosis_int_exact_moments(pkg, eng, orc, dt):
     only min / max: NaN as the recipe; two values), two IFs and a window."""
     info = np.iinfo(dt)
     rng = np.random.default_rng(99 + np.dtype(dt).num)
-    for nc, ni, nt in ((65536, 1, 279), (512, 1, 200000), (256, 2, 4099), (8, 1, 17)):
+    for nc, ni, nt in ((65536, 1, 279), (512, 1, 200000), (256, 2, 4099), (8, 1, 17),
+                       (64, 2, 1), (64, 1, 2), (16, 1, 4)):  # (1 spectrum: NaN, as the recipe)
         a = np.asfortranarray(rng.integers(info.min, info.max, (nc, ni, nt), endpoint=True)
                               .astype(dt))
         a[0, 0, :] = info.max  # constant rows: NaN
         a[1, 0, :] = info.min
         a[2, 0, :] = np.where(np.arange(nt) % 3 == 0, info.min, info.max)  # two values
         a[3, 0, :nt // 2] = info.min  # a long run then noise
+        if nt == 1:
+            assert np.isnan(orc.np_kurtosis_typed(a)).all()
         x = to_dev(eng, a)
         got = eng.fb_to_numpy(eng.kurtosis(x))
         for form in (2, 3):  # 4- and 8-byte words a lane: the same exact sums, the same bits
