@@ -523,8 +523,8 @@ __global__ __launch_bounds__(256) void k_kurt_typed_w(const TypedArgs a, double 
 // exactly (|d| <= 128, n <= 2^23), so any split of the time axis adds them
 // back exactly: the window is read once by NW waves per tile of 64 lanes x W
 // words (4 W channels a lane, W 32-bit words of each spectrum; 256 W
-// contiguous bytes per wave-instruction), each wave summing a time slab, the slabs added in LDS
-// (ds_add_u64), and, for long rows, time chunks of several workgroups added by
+// contiguous bytes per wave-instruction), each wave summing a time slab, the
+// slabs added in LDS (ds_add_u64), and, for long rows, time chunks of several workgroups added by
 // k_kurt_int_final.  From the exact sums, with n the window's length:
 // the central moments n cm2 = sum((x - mu)^2), n cm4 = sum((x - mu)^4) (which
 // the shift leaves alone) re-centred exactly in Int64 and finished in Float64
@@ -534,23 +534,24 @@ __global__ __launch_bounds__(256) void k_kurt_typed_w(const TypedArgs a, double 
 // its own rounding, at most (3 nt + 10) 2^-53 relative on k + 3; this path by
 // at most ~150 2^-53 (tests hold the two to conftest.kurt_int_tol).  A row of
 // one value gives NaN, as the recipe.
-// Plan option "typed_kurt": 1 (default) = this path for 8-bit rows of
-// dword-aligned words, 4- or 8-byte words a lane by kurt_int_plan's rule; 2 /
-// 3 = 4- / 8-byte words (8: where the rows are 8-byte aligned); 0 =
-// k_kurt_typed_w (the recipe's order, bit-exact).
+// 16-bit rows take the same plan and finish with wider sums (k_kurt_i16,
+// below).  Plan option "typed_kurt": 1 (default) = these paths for 8- and
+// 16-bit rows of dword-aligned words, 4- or 8-byte words a lane by
+// kurt_int_plan's rule; 2 / 3 = 4- / 8-byte words (8: where the rows are
+// 8-byte aligned); 0 = k_kurt_typed_w (the recipe's order, bit-exact).
 struct KTM {
   int nw;           // waves per workgroup (time slabs)
   int wpl;          // words a lane (W: 1 or 2)
   int64_t ntile;    // tiles (64 lanes x W words) per row
   int64_t nchunk;   // time chunks (workgroups along time); 1: fused finish
   int64_t crow;     // spectra per chunk
-  int64_t srow;     // spectra per wave slab (<= 1024: the Int32 lane sums of d^3)
+  int64_t srow;     // spectra per wave slab (<= 1024: the lanes' 32-bit sums)
 };
 constexpr int64_t kI8MaxN = (int64_t)1 << 23;  // (the Int64 re-centring's bound)
-// waves per CU one round of k_kurt_i8 should fill (58 VGPRs with 4-byte
-// words, 8 waves a SIMD; 116 with 8-byte, 4 a SIMD); 12..32 are within ~5% of
-// each other on the UInt8 0002 band and file (profiles/r06/kurtsweep_r06j.json,
-// kurtsweep_r06m.json)
+// waves per CU one round of k_kurt_i8 / k_kurt_i16 should fill (k_kurt_i8:
+// 58 VGPRs with 4-byte words, 8 waves a SIMD; 116 with 8-byte, 4 a SIMD;
+// k_kurt_i16: 68 / 86); 12..32 are within ~5% of each other on the UInt8 and
+// UInt16 0002 band and file (profiles/r06/kurtsweep_r06{j,m,w}.json)
 constexpr int64_t kI8WavesPerCu = 16;
 constexpr int64_t kI8MinSlab = 16;  // fewest spectra a wave's slab is cut to
 constexpr int64_t kI8MaxSlab = 1024;  // most: |sum d^3| <= 2^21 x 1024 = 2^31 (Int32)
