@@ -54,6 +54,14 @@ __global__ __launch_bounds__(256) void k_rate(const unsigned *in, unsigned *out)
       if constexpr (OP == 12) asm volatile("v_add_f64 %0, %0, %0" : "+v"(b[c]));
       if constexpr (OP == 13) asm volatile("v_cvt_f64_f32 %0, %1" : "=v"(b[c]) : "v"(a[c]));
       if constexpr (OP == 14) asm volatile("v_fma_f32 %0, %0, %1, %0" : "+v"(a[c]) : "v"(y));
+      if constexpr (OP == 15) asm volatile("v_pk_add_u16 %0, %0, %1" : "+v"(a[c]) : "v"(y));
+      if constexpr (OP == 16) asm volatile("v_and_b32 %0, %0, %1" : "+v"(a[c]) : "v"(y));
+      if constexpr (OP == 17) asm volatile("v_bfe_u32 %0, %0, 8, 8" : "+v"(a[c]));
+      if constexpr (OP == 18) asm volatile("v_mul_i32_i24 %0, %0, %1" : "+v"(a[c]) : "v"(y));
+      if constexpr (OP == 19) asm volatile("v_mad_i64_i32 %0, vcc, %1, %2, %0" : "+v"(b[c]) : "v"(a[c]), "v"(y) : "vcc");
+      if constexpr (OP == 20) asm volatile("v_pk_mad_u16 %0, %0, %1, %0" : "+v"(a[c]) : "v"(y));
+      if constexpr (OP == 21) asm volatile("v_sad_u8 %0, %0, %1, %0" : "+v"(a[c]) : "v"(y));
+      if constexpr (OP == 22) asm volatile("v_lshrrev_b32 %0, 8, %0" : "+v"(a[c]));
     }
   }
   unsigned s = 0;
@@ -65,7 +73,9 @@ __global__ __launch_bounds__(256) void k_rate(const unsigned *in, unsigned *out)
 static const char *kName[] = {"v_dot4c_i32_i8",  "v_dot2c_i32_i16", "v_dot2_u32_u16", "v_pk_mul_lo_u16",
                               "v_perm_b32",      "v_pk_ashrrev_i16", "v_mad_u32_u24", "v_add_u32",
                               "v_lshl_add_u64", "v_mad_u64_u32", "v_mul_lo_u32", "v_fma_f64",
-                              "v_add_f64", "v_cvt_f64_f32", "v_fma_f32"};
+                              "v_add_f64", "v_cvt_f64_f32", "v_fma_f32", "v_pk_add_u16",
+                              "v_and_b32", "v_bfe_u32", "v_mul_i32_i24", "v_mad_i64_i32",
+                              "v_pk_mad_u16", "v_sad_u8", "v_lshrrev_b32"};
 
 template <int OP>
 void run(const unsigned *in, unsigned *out, int ncu, int clock_khz) {
@@ -118,5 +128,13 @@ int main() {
   run<12>(in, out, p.multiProcessorCount, p.clockRate);
   run<13>(in, out, p.multiProcessorCount, p.clockRate);
   run<14>(in, out, p.multiProcessorCount, p.clockRate);
+  run<15>(in, out, p.multiProcessorCount, p.clockRate);
+  run<16>(in, out, p.multiProcessorCount, p.clockRate);
+  run<17>(in, out, p.multiProcessorCount, p.clockRate);
+  run<18>(in, out, p.multiProcessorCount, p.clockRate);
+  run<19>(in, out, p.multiProcessorCount, p.clockRate);
+  run<20>(in, out, p.multiProcessorCount, p.clockRate);
+  run<21>(in, out, p.multiProcessorCount, p.clockRate);
+  run<22>(in, out, p.multiProcessorCount, p.clockRate);
   return 0;
 }
