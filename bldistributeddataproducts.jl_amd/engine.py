@@ -693,7 +693,8 @@ def reduce_host_typed(a: np.ndarray, fqavby=1, tavby=1, op="sum", win=None, devi
 
 def kurtosis_host_typed(a: np.ndarray, win=None, device=0) -> np.ndarray:
     """Host array of any supported element type in, (nc, ni) float64 out
-    (bldp_kurtosis_host; StatsBase's recipe in Float64 for non-Float32 rows)."""
+    (bldp_kurtosis_host; StatsBase's recipe in Float64 for non-Float32 rows,
+    8- and 16-bit integer rows from exact integer power sums)."""
     L = _lib.lib()
     a = np.asarray(a)
     code = _dtype_code(a.dtype)
