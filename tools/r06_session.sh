@@ -6,6 +6,7 @@
 #   steps: smoke tests tests_K[+K2...] bench bench_CFG list ab_SUITE[:v1,v2,...]
 #          prof_CFG[_lbN] pmc_CFG[_lbN] sq_CFG[_lbN] cold_CFG typed typedprof typedpmc typedsq
 #          ab_SUITE getband getbandz ceil_kurt kurtprof_CFG kurtpmc_CFG kurtsweep
+#          gloo_N_CFG hostbound typedw_N benchpipe_CFG cold_CFG[_kSTEPS]
 # CFG[_lbN]: a config, optionally with --local-banks N (one rank's launch of an
 # (8/N)-GPU run).  Every GPU step has its own time limit; after any failure
 # nothing more runs.
