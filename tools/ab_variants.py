@@ -197,6 +197,12 @@ VARIANTS = {
                         ("typed.hip", "          b4[x] = __builtin_amdgcn_udot2(qo, qo, b4[x], false);\n", "")]},
     "i8b4": {"patch": [("typed.hip", "  constexpr int U = 8;  // spectra of loads in flight per lane",
                         "  constexpr int U = 4;  // spectra of loads in flight per lane")]},
+    "i8b4w5": {"patch": [("typed.hip", "  constexpr int U = 8;  // spectra of loads in flight per lane",
+                          "  constexpr int U = 4;  // spectra of loads in flight per lane"),
+                         ("typed.hip", "__global__ __launch_bounds__(1024) void k_kurt_i8(",
+                          "__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(5))) void k_kurt_i8(")]},
+    "i8w5": {"patch": [("typed.hip", "__global__ __launch_bounds__(1024) void k_kurt_i8(",
+                        "__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(5))) void k_kurt_i8(")]},
     "i8b12": {"patch": [("typed.hip", "  constexpr int U = 8;  // spectra of loads in flight per lane",
                          "  constexpr int U = 12;  // spectra of loads in flight per lane")]},
     # k_kurt_i16 (16-bit getkurtosis, round 6)
