@@ -197,6 +197,7 @@ VARIANTS = {
                         ("typed.hip", "          b4[x] = __builtin_amdgcn_udot2(qo, qo, b4[x], false);\n", "")]},
     "i8b4": {"patch": [("typed.hip", "  constexpr int U = 8;  // spectra of loads in flight per lane",
                         "  constexpr int U = 4;  // spectra of loads in flight per lane")]},
+    "i8glds": {"opts": {"typed_kurt": 4}},  # k_kurt_i8g: 1 KiB rows staged through LDS
     "i8b4w5": {"patch": [("typed.hip", "  constexpr int U = 8;  // spectra of loads in flight per lane",
                           "  constexpr int U = 4;  // spectra of loads in flight per lane"),
                          ("typed.hip", "__global__ __launch_bounds__(1024) void k_kurt_i8(",
