@@ -2017,7 +2017,7 @@ const PlanOptDef kPlanOpts[OPT_COUNT] = {
     {"kurt_leaf_narrow", 4, 0, 1 << 20},
     {"kurt_leaf_tile", 1, 0, 1},  // k_kurt_tile for narrow short leaves
     {"typed_vec", 1, 0, 1},       // order-free typed reductions on k_reduce_typed_vec
-    {"typed_kurt", 1, 0, 4},      // 8-bit getkurtosis from exact integer power sums (k_kurt_i8):
+    {"typed_kurt", 1, 0, 3},      // 8-bit getkurtosis from exact integer power sums (k_kurt_i8):
                                   // 1 4- or 8-byte words a lane by the plan's rule, 2 / 3 forced
     {"row_bpack", 1, 0, 1},       // k_reduce_rowt: lane sets over consecutive banks on narrow stitched rows
     {"lane_bpack", 1, 0, 1},      // k_reduce_lanes: lanet's lanes along narrow stitched band rows

@@ -542,7 +542,6 @@ __global__ __launch_bounds__(256) void k_kurt_typed_w(const TypedArgs a, double 
 struct KTM {
   int nw;           // waves per workgroup (time slabs)
   int wpl;          // words a lane (W: 1 or 2)
-  int glds;         // 1: k_kurt_i8g (1 KiB rows staged through LDS; nw = 4 slab groups)
   int64_t ntile;    // tiles (64 lanes x W words) per row
   int64_t nchunk;   // time chunks (workgroups along time); 1: fused finish
   int64_t crow;     // spectra per chunk
@@ -745,108 +744,6 @@ __global__ __launch_bounds__(1024) void k_kurt_i8(const TypedArgs a, const KTM m
   for (int ch = threadIdx.x; ch < 64 * C; ch += blockDim.x) {
     const int64_t c = tile * 64 * C + ch;  // this workgroup's channels, coalesced
     const int l = ch / C, k = ch % C;  // (lane, channel of the lane)
-    if (c < a.nco) {
-      if (m.nchunk == 1) {
-        out[c + a.nco * r] = kurt_from_sums(a.nto, (int64_t)acc[0][k][l], acc[1][k][l],
-                                            (int64_t)acc[2][k][l], acc[3][k][l]);
-      } else {
-        const int64_t rows = a.ni * a.nbank;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) ws[((chunk * 4 + s) * rows + r) * a.nco + c] = acc[s][k][l];
-      }
-    }
-  }
-}
-
-// The same sums with the rows staged through LDS by global_load_lds_dwordx4
-// (no VGPR destination): a workgroup owns a tile of 1024 channels (one 1 KiB
-// piece of each row) and 16 waves, 4 slab groups x the tile's 4 channel
-// quarters.  Per stage of 8 spectra, each wave of a group stages 2 of the
-// group's rows (1 KiB each) into the group's half of a 2-stage ring, then every
-// wave reads its quarter's word of the 8 rows (ds_read_b32, 4 channels a lane)
-// and sums it as k_kurt_i8 does.  Stage s + 1 is in flight while stage s is
-// summed: counted vmcnt, raw s_barrier (never __syncthreads, whose fence would
-// drain the DMA), one __shared__ object (a second one makes hipcc wait for the
-// DMA before every ds_read; cdna_hip_programming.md §5).  ~50 VGPRs: 8 waves a
-// SIMD with the loads in LDS instead of registers.
-template <bool SIGNED>
-__global__ __launch_bounds__(1024) void k_kurt_i8g(const TypedArgs a, const KTM m, double *out,
-                                                   uint64_t *ws) {
-  constexpr int U = 8;  // spectra a stage
-  typedef __attribute__((address_space(3))) void lds_void;
-  typedef __attribute__((address_space(1))) const void gbl_cvoid;
-  // [group][stage][spectrum][word]: 64 KiB; after the loop the slabs' sums
-  __shared__ unsigned long long ringq[4 * 2 * U * 128];
-  uint32_t *ring = reinterpret_cast<uint32_t *>(ringq);
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int q4 = wave & 3, g = wave >> 2;
-  const int64_t tile = blockIdx.x, r = blockIdx.y, chunk = blockIdx.z;
-  const int64_t word = tile * 256 + q4 * 64 + lane;  // this lane's word (4 channels)
-  const bool valid = word < a.nco / 4;
-  const int64_t i = r % a.ni, bank = r / a.ni;
-  const int64_t ct0 = chunk * m.crow, ct1 = min(a.nto, ct0 + m.crow);
-  const int64_t t0 = min(ct1, ct0 + (int64_t)g * m.srow), t1 = min(ct1, t0 + m.srow);
-  const int cnt = (int)(t1 - t0);  // (uniform over the group)
-  const int nstage = (int)((m.srow + U - 1) / U);  // (uniform over the workgroup)
-  const char *base = static_cast<const char *>(a.in[bank]) + a.in_off + i * a.in_ld_i + 1024 * tile;
-  // the lane's 16 bytes of a staged row, kept inside the row (a tail tile's
-  // extra lanes re-read its last 16 bytes; their channels are not stored)
-  const uint32_t gofs = (uint32_t)min<int64_t>(16 * lane, a.nco - 1024 * tile - 16);
-  const int last = cnt > 0 ? (int)(t1 - 1) : 0;
-  auto stage_in = [&](int st) {  // this wave's 2 rows of stage st
-    if (cnt <= 0) return;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int j = 2 * q4 + h;
-      const int t = min((int)t0 + st * U + j, last);
-      const uint64_t ro = (uint64_t)((int64_t)t * a.in_ld_t);
-      __builtin_amdgcn_global_load_lds((gbl_cvoid *)(base + ro + gofs),
-                                       (lds_void *)(ring + ((g * 2 + (st & 1)) * U + j) * 256), 16,
-                                       0, 0);
-    }
-  };
-  int32_t s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0}, s3[4] = {0, 0, 0, 0};
-  uint64_t s4[4] = {0, 0, 0, 0};
-  stage_in(0);
-  for (int st = 0; st < nstage; ++st) {
-    const bool more = st + 1 < nstage;
-    if (more) stage_in(st + 1);
-    if (more && cnt > 0)
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // this wave's stage st landed
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // ... and every other wave's
-    asm volatile("" ::: "memory");
-    const int c = max(0, min(U, cnt - st * U));
-    if (c > 0) {
-      uint32_t w[U][1];
-#pragma unroll
-      for (int j = 0; j < U; ++j) w[j][0] = ring[((g * 2 + (st & 1)) * U + j) * 256 + q4 * 64 + lane];
-      i8_batch<SIGNED, U, 1>(w, c, s1, s2, s3, s4);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (reads of this stage done)
-    __builtin_amdgcn_s_barrier();  // before stage st + 2 overwrites the buffer
-    asm volatile("" ::: "memory");
-  }
-  // the slabs' sums added in the ring's memory: [sum][channel of the word][word]
-  unsigned long long(*acc)[4][256] = reinterpret_cast<unsigned long long(*)[4][256]>(ringq);
-  for (int e = threadIdx.x; e < 4 * 4 * 256; e += blockDim.x) (&acc[0][0][0])[e] = 0ull;
-  __syncthreads();
-  if (valid && cnt > 0) {
-    const int l = q4 * 64 + lane;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      atomicAdd(&acc[0][k][l], (unsigned long long)(int64_t)s1[k]);
-      atomicAdd(&acc[1][k][l], (unsigned long long)(int64_t)s2[k]);
-      atomicAdd(&acc[2][k][l], (unsigned long long)(int64_t)s3[k]);
-      atomicAdd(&acc[3][k][l], (unsigned long long)s4[k]);
-    }
-  }
-  __syncthreads();
-  {
-    const int ch = threadIdx.x;  // the tile's 1024 channels, coalesced
-    const int64_t c = tile * 1024 + ch;
-    const int l = ch >> 2, k = ch & 3;
     if (c < a.nco) {
       if (m.nchunk == 1) {
         out[c + a.nco * r] = kurt_from_sums(a.nto, (int64_t)acc[0][k][l], acc[1][k][l],
@@ -1115,25 +1012,6 @@ bool kurt_int_plan(const TypedArgs &a, KTM *m) {
   const int64_t form = opt(OPT_TYPED_KURT);  // 1: by the rule, 2: 4-byte, 3: 8-byte words
   m->wpl = (form == 1 && w2) || (form == 3 && w2a) ? 2 : 1;
   m->ntile = cdivt(a.nco / (cpw * m->wpl), 64);
-  // k_kurt_i8g (typed_kurt 4: 1 KiB rows through LDS; 8-bit, 16-byte aligned rows)
-  bool g16 = form == 4 && es == 1 && a.nco % 16 == 0 && off % 16 == 0 &&
-             (a.ni == 1 || ldi % 16 == 0) && (a.nto == 1 || ldt % 16 == 0);
-  for (int b = 0; g16 && b < a.nbank; ++b) g16 = (uintptr_t)a.in[b] % 16 == 0;
-  m->glds = g16 ? 1 : 0;
-  if (m->glds) {
-    m->wpl = 1;
-    m->ntile = cdivt(a.nco, 1024);
-    m->nw = 4;
-    const int64_t waves = m->ntile * rows * 16;
-    int64_t nchunk = std::max<int64_t>(1, std::min(cdivt(want, waves),
-                                                   a.nto / (min_slab * 4)));
-    nchunk = std::max(nchunk, cdivt(a.nto, 4 * kI8MaxSlab));
-    m->crow = cdivt(a.nto, nchunk);
-    m->srow = cdivt(m->crow, 4);
-    m->crow = m->srow * 4;
-    m->nchunk = cdivt(a.nto, m->crow);
-    return m->ntile <= INT32_MAX && rows <= 65535 && m->nchunk <= 65535;
-  }
   // waves for one round of kI8WavesPerCu: NW waves a tile (<= 16,
   // never slabs under 16 spectra), then time chunks while the tiles still
   // leave the CUs short (0001: 512 channels = 2 tiles a row, ~10^6 spectra),
@@ -1273,9 +1151,7 @@ hipError_t launch_kurt_t(const TypedArgs &a, double *out, hipStream_t s) {
       constexpr bool sg = std::is_signed<TI>::value;
       constexpr int ns = sizeof(TI) == 1 ? 4 : 6;
       if constexpr (sizeof(TI) == 1) {
-        if (m.glds)
-          hipLaunchKernelGGL((k_kurt_i8g<sg>), g, dim3(1024), 0, s, a, m, out, ws);
-        else if (m.wpl == 2)
+        if (m.wpl == 2)
           hipLaunchKernelGGL((k_kurt_i8<sg, 2>), g, dim3(64 * m.nw), 0, s, a, m, out, ws);
         else
           hipLaunchKernelGGL((k_kurt_i8<sg, 1>), g, dim3(64 * m.nw), 0, s, a, m, out, ws);

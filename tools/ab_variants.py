@@ -197,7 +197,9 @@ VARIANTS = {
                         ("typed.hip", "          b4[x] = __builtin_amdgcn_udot2(qo, qo, b4[x], false);\n", "")]},
     "i8b4": {"patch": [("typed.hip", "  constexpr int U = 8;  // spectra of loads in flight per lane",
                         "  constexpr int U = 4;  // spectra of loads in flight per lane")]},
-    "i8glds": {"opts": {"typed_kurt": 4}},  # k_kurt_i8g: 1 KiB rows staged through LDS
+    # k_kurt_i8g (1 KiB rows staged through LDS, global_load_lds_dwordx4) at the commit
+    # that had it, plan option typed_kurt 4: measured and not taken (r06af)
+    "i8glds": {"rev": "8ebce3d", "extra": ""},
     "i8b4w5": {"patch": [("typed.hip", "  constexpr int U = 8;  // spectra of loads in flight per lane",
                           "  constexpr int U = 4;  // spectra of loads in flight per lane"),
                          ("typed.hip", "__global__ __launch_bounds__(1024) void k_kurt_i8(",
